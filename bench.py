@@ -1,0 +1,125 @@
+#!/usr/bin/env python3
+"""Flagship benchmark: ResNet-50 bf16 training throughput (images/s, whole job).
+
+Metric/config from BASELINE.json ("images/sec (whole node) ResNet-50 bf16
+training at 1/2/4/8 MI355X"), synthetic ImageNet-shaped data (3x224x224,
+1000 classes), random-init weights, full training step timed: forward,
+backward, (N>1) bucketed RCCL all-reduce of every gradient, fused SGD-momentum
+update of every parameter.
+
+    python bench.py --gpus N --steps K --warmup W
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+        --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
+
+Weak scaling: per-GPU batch is fixed (default 256), global batch = N * 256.
+Rank 0 prints ONE JSON line; value = N * batch * K / max-over-ranks(elapsed).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
+    ap.add_argument("--depth", type=int, default=50)
+    ap.add_argument("--image", type=int, default=224)
+    ap.add_argument("--no-graph", action="store_true", help="eager execution instead of HIP-graph replay")
+    ap.add_argument("--lr", type=float, default=0.1)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and world == 1 and args.gpus > 1:
+        print(f"--gpus {args.gpus} requires launching with torch.distributed.run", file=sys.stderr)
+        return 2
+    if not torch.cuda.is_available():
+        print("bench.py needs a GPU", file=sys.stderr)
+        return 2
+    torch.cuda.set_device(local % torch.cuda.device_count())
+
+    from singa_amd import device, opt, tensor
+    from singa_amd.models import resnet
+    from singa_amd.parallel import DistOpt, init_distributed
+
+    dev = device.create_rocm_gpu_on(local % torch.cuda.device_count(), set_default=True)
+    dev.SetRandSeed(1234 + rank)
+    comm = init_distributed(rank=rank, world_size=world, local_rank=local)
+
+    m = resnet.create_model(args.depth, num_classes=1000, compute_dtype=torch.bfloat16)
+    sgd = opt.SGD(lr=args.lr, momentum=0.9, weight_decay=1e-4)
+    optimizer = DistOpt(sgd, comm=comm) if world > 1 else sgd
+    m.set_optimizer(optimizer)
+
+    B = args.batch
+    rng = np.random.RandomState(rank)
+    x = rng.standard_normal((B, 3, args.image, args.image)).astype(np.float32)
+    y = rng.randint(0, 1000, size=(B,)).astype(np.int32)
+    tx = tensor.from_numpy(x, dev)
+    ty = tensor.from_numpy(y, dev)
+
+    use_graph = not args.no_graph
+    m.compile([tx], is_train=True, use_graph=use_graph)
+    m.train()
+
+    for _ in range(args.warmup):
+        out, loss = m(tx, ty)
+    torch.cuda.synchronize()
+    if world > 1:
+        comm.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out, loss = m(tx, ty)
+    torch.cuda.synchronize()
+    if world > 1:
+        comm.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev.torch_device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    final_loss = float(loss.data.float().item())
+    if rank == 0:
+        ips = world * B * args.steps / elapsed
+        rec = {
+            "metric": "images/sec (whole node) ResNet-50 bf16 training",
+            "value": round(ips, 2),
+            "unit": "images/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (random 3x224x224 images, random labels, random-init weights)",
+            "config": {"model": f"ResNet-{args.depth}", "global_batch": world * B, "seq_len": None,
+                       "image": args.image, "parallelism": f"dp{world}",
+                       "exec": "hipgraph" if use_graph else "eager", "optimizer": "SGD momentum 0.9 wd 1e-4",
+                       "final_loss": round(final_loss, 4)},
+        }
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,1344 @@
+"""``singa_amd.autograd`` -- SINGA's operator-tape autograd.
+
+Operators record their inputs when ``autograd.training`` is True; the
+:func:`backward` generator walks the tape in dependency order and yields
+``(param, grad)`` pairs the moment a parameter's gradient is complete -- the
+hook that lets :class:`singa_amd.opt.DistOpt` launch bucketed RCCL
+all-reduces while the rest of the backward pass is still running (the
+reference interleaves ``UpdateParam`` with ``ComputeGradient`` in the same way,
+src/worker/worker.cc:270-302).
+
+Hot operators (convolution, linear, batch-norm(+ReLU, +residual), pooling,
+activations, softmax-cross-entropy, dropout, LRN, layer-norm) call the
+gfx950 kernels through :mod:`singa_amd.ops.functional`.  Parameters that live
+in a flat :class:`singa_amd.opt.ParamStore` carry an fp32 ``grad_view``; the
+conv/linear/BN backward kernels accumulate straight into it (no per-param
+gradient tensors, one fused optimiser launch afterwards).  Non-hot "glue"
+operators (shape manipulation, ONNX odds and ends) are expressed through
+:class:`TorchFn`, which differentiates a small PyTorch function locally.
+"""
+from __future__ import annotations
+
+import builtins as _b
+import math
+from collections import Counter, deque
+from typing import Callable, Dict, Iterator, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from . import tensor as _tensor
+from .ops import functional as F
+from .tensor import Tensor
+
+training = False
+
+ACCUMULATED = object()  # backward() returned: grad already added to the param's grad_view
+
+
+def _as_tuple(x):
+    return x if isinstance(x, tuple) else (x,)
+
+
+class Operator:
+    """Base operator.  Subclasses implement ``forward(*raw)`` and
+    ``backward(*raw_dys)`` on ``torch.Tensor`` storage."""
+
+    op_count = 0
+
+    def __init__(self, name: Optional[str] = None):
+        if name is None:
+            name = f"{type(self).__name__}#{Operator.op_count}"
+            Operator.op_count += 1
+        self.name = name
+        self.src: List = []
+        self.params: List[Optional[Tensor]] = []
+        self.requires_grad = False
+
+    def __call__(self, *xs):
+        return self._do_forward(*xs)
+
+    def _do_forward(self, *xs):
+        xs = tuple(x if isinstance(x, Tensor) else Tensor(data=x, requires_grad=False) for x in xs)
+        self.requires_grad = training and any(x.requires_grad for x in xs)
+        if self.requires_grad:
+            self.src = [(x.creator, x.stores_grad) for x in xs]
+            self.src_idx = [x.creator._yid.get(id(x), 0) if x.creator is not None else 0 for x in xs]
+            self.params = [x if x.stores_grad else None for x in xs]
+            self.input_requires = [x.requires_grad for x in xs]
+        ys = _as_tuple(self.forward(*[x.data for x in xs]))
+        dev = xs[0].device
+        outs = tuple(
+            Tensor(device=dev, data=y, requires_grad=self.requires_grad,
+                   creator=self if self.requires_grad else None) for y in ys)
+        if self.requires_grad:
+            self.n_out = len(outs)
+            self._yid = {id(o): i for i, o in enumerate(outs)}
+        return outs[0] if len(outs) == 1 else outs
+
+    def grad_target(self, i: int) -> Optional[torch.Tensor]:
+        """fp32 flat-buffer gradient view of input i if it is a stored param."""
+        if i < len(self.params) and self.params[i] is not None:
+            return self.params[i].grad_view
+        return None
+
+    def needs_grad(self, i: int) -> bool:
+        return getattr(self, "input_requires", [True] * (i + 1))[i]
+
+    def forward(self, *xs):
+        raise NotImplementedError
+
+    def backward(self, *dys):
+        raise NotImplementedError
+
+    def get_params(self):
+        return {}
+
+
+class Dummy(Operator):
+    """Leaf marker (SINGA compatibility)."""
+
+    def __init__(self, tensor: Tensor, name=None):
+        super().__init__(name)
+        self.tensor = tensor
+
+
+def infer_dependency(op: Operator) -> Dict[Operator, int]:
+    """Number of consumers of each operator reachable from ``op``."""
+    deps: Counter = Counter()
+    seen = {op}
+    q = deque([op])
+    while q:
+        cur = q.popleft()
+        for src_op, _ in cur.src:
+            if src_op is None:
+                continue
+            deps[src_op] += 1
+            if src_op not in seen:
+                seen.add(src_op)
+                q.append(src_op)
+    return deps
+
+
+def _param_uses(op: Operator) -> Counter:
+    uses: Counter = Counter()
+    seen = {op}
+    q = deque([op])
+    while q:
+        cur = q.popleft()
+        for p in cur.params:
+            if p is not None:
+                uses[id(p)] += 1
+        for src_op, _ in cur.src:
+            if src_op is not None and src_op not in seen:
+                seen.add(src_op)
+                q.append(src_op)
+    return uses
+
+
+def _accum(a, b):
+    if a is None:
+        return b
+    if b is None:
+        return a
+    if a.shape != b.shape:
+        b = b.reshape(a.shape)
+    if a.dtype != b.dtype:
+        b = b.to(a.dtype)
+    if a.stride() == b.stride() and a.is_cuda:
+        return F.add_act(a, b)
+    return a + b
+
+
+def is_unit(dy) -> bool:
+    """True if dy is the implicit d(loss)/d(loss) = 1 seed."""
+    return dy is None or getattr(dy, "_sg_unit", False)
+
+
+def backward(y: Tensor, dy: Optional[Tensor] = None) -> Iterator[Tuple[Tensor, Tensor]]:
+    """Generator of (param, grad) in the order gradients complete."""
+    if y.creator is None:
+        return
+    op0 = y.creator
+    deps = infer_dependency(op0)
+    puses = _param_uses(op0)
+    if dy is None:
+        g0 = torch.ones_like(y.data)
+        g0._sg_unit = True
+    else:
+        g0 = dy.data if isinstance(dy, Tensor) else dy
+    pending: Dict[Operator, list] = {op0: [None] * op0.n_out}
+    pending[op0][op0._yid.get(id(y), 0)] = g0
+    pgrad: Dict[int, object] = {}
+    ready = deque([op0])
+    while ready:
+        op = ready.popleft()
+        dys = pending.pop(op)
+        if all(d is None for d in dys):
+            dxs = (None,) * len(op.src)
+        else:
+            dxs = _as_tuple(op.backward(*dys))
+        if len(dxs) != len(op.src):
+            raise RuntimeError(f"{op.name}: backward returned {len(dxs)} grads for {len(op.src)} inputs")
+        for i, ((src_op, stores), dx) in enumerate(zip(op.src, dxs)):
+            p = op.params[i]
+            if p is not None:
+                key = id(p)
+                if dx is ACCUMULATED:
+                    pgrad.setdefault(key, ACCUMULATED)
+                elif dx is not None:
+                    prev = pgrad.get(key)
+                    if p.grad_view is not None:
+                        p.grad_view.add_(dx.reshape(p.grad_view.shape).to(p.grad_view.dtype))
+                        pgrad[key] = ACCUMULATED
+                    else:
+                        pgrad[key] = _accum(prev, dx)
+                puses[key] -= 1
+                if puses[key] == 0:
+                    g = pgrad.pop(key, None)
+                    if g is ACCUMULATED:
+                        g = p.grad_view
+                    if g is not None:
+                        yield p, Tensor(device=p.device, data=g, requires_grad=False)
+                continue
+            if src_op is None:
+                continue
+            if dx is ACCUMULATED:
+                dx = None
+            if src_op not in pending:
+                pending[src_op] = [None] * src_op.n_out
+            j = op.src_idx[i]
+            pending[src_op][j] = _accum(pending[src_op][j], dx)
+            deps[src_op] -= 1
+            if deps[src_op] == 0:
+                ready.append(src_op)
+
+
+def gradients(y: Tensor, dy: Optional[Tensor] = None) -> Dict[Tensor, Tensor]:
+    return {p: g for p, g in backward(y, dy)}
+
+
+# ===========================================================================
+# hot operators (native kernels on GPU)
+# ===========================================================================
+class _Unary(Operator):
+    kind = "identity"
+    needs = "x"  # which saved tensor the backward needs: "x", "y" or "xy"
+
+    def __init__(self, alpha: float = 0.0, name=None):
+        super().__init__(name)
+        self.alpha = alpha
+
+    def forward(self, x):
+        y = F.unary(self.kind, x, self.alpha)
+        if self.requires_grad:
+            self.x = x if "x" in self.needs else None
+            self.y = y if "y" in self.needs else None
+        return y
+
+    def backward(self, dy):
+        dx = F.unary_bwd(self.kind, self.x, self.y, dy, self.alpha)
+        self.x = self.y = None
+        return dx
+
+
+class ReLU(_Unary):
+    kind = "relu"
+    needs = "y"
+
+    def backward(self, dy):
+        dx = F.relu_bwd_from_y(self.y, dy)
+        self.y = None
+        return dx
+
+
+class Sigmoid(_Unary):
+    kind, needs = "sigmoid", "y"
+
+
+class Tanh(_Unary):
+    kind, needs = "tanh", "y"
+
+
+class STanh(_Unary):
+    """LeCun scaled tanh 1.7159*tanh(2/3 x) -- the reference's kTanh layer
+    (include/mshadow/cxxnet_op.h:77-87)."""
+    kind, needs = "stanh", "y"
+
+
+class Gelu(_Unary):
+    kind, needs = "gelu", "x"
+
+
+class SoftPlus(_Unary):
+    kind, needs = "softplus", "x"
+
+
+class Exp(_Unary):
+    kind, needs = "exp", "y"
+
+
+class Log(_Unary):
+    kind, needs = "log", "x"
+
+
+class Abs(_Unary):
+    kind, needs = "abs", "x"
+
+
+class Sqrt(_Unary):
+    kind, needs = "sqrt", "y"
+
+
+class Reciprocal(_Unary):
+    kind, needs = "reciprocal", "y"
+
+
+class Negative(_Unary):
+    kind, needs = "neg", ""
+
+
+class Sign(_Unary):
+    kind, needs = "sign", ""
+
+
+class Square(_Unary):
+    kind, needs = "square", "x"
+
+
+class LeakyRelu(_Unary):
+    kind, needs = "leakyrelu", "x"
+
+    def __init__(self, a: float = 0.01, name=None):
+        super().__init__(a, name)
+
+
+class Elu(_Unary):
+    kind, needs = "elu", "xy"
+
+    def __init__(self, alpha: float = 1.0, name=None):
+        super().__init__(alpha, name)
+
+
+class SeLU(_Unary):
+    kind, needs = "selu", "xy"
+
+    def __init__(self, alpha: float = 1.67326, gamma: float = 1.0507, name=None):
+        super().__init__(0.0, name)
+
+
+class Identity(Operator):
+    def forward(self, x):
+        return x
+
+    def backward(self, dy):
+        return dy
+
+
+def _unbroadcast(g: torch.Tensor, shape) -> torch.Tensor:
+    shape = tuple(shape)
+    if tuple(g.shape) == shape:
+        return g
+    while g.dim() > len(shape):
+        g = g.sum(0)
+    for i, s in enumerate(shape):
+        if s == 1 and g.shape[i] != 1:
+            g = g.sum(i, keepdim=True)
+    return g
+
+
+class Add(Operator):
+    def __init__(self, relu: bool = False, name=None):
+        super().__init__(name)
+        self.relu = relu
+
+    def forward(self, a, b):
+        if a.shape == b.shape:
+            y = F.add_act(a, b, relu=self.relu)
+        else:
+            y = a + b
+            if self.relu:
+                y = torch.relu(y)
+        if self.requires_grad:
+            self.sa, self.sb = a.shape, b.shape
+            self.y = y if self.relu else None
+        return y
+
+    def backward(self, dy):
+        if self.relu:
+            dy = F.relu_bwd_from_y(self.y, dy)
+            self.y = None
+        return _unbroadcast(dy, self.sa), _unbroadcast(dy, self.sb)
+
+
+class Sub(Operator):
+    def forward(self, a, b):
+        if self.requires_grad:
+            self.sa, self.sb = a.shape, b.shape
+        return a - b
+
+    def backward(self, dy):
+        return _unbroadcast(dy, self.sa), _unbroadcast(-dy, self.sb)
+
+
+class Mul(Operator):
+    def forward(self, a, b):
+        if self.requires_grad:
+            self.a, self.b = a, b
+        return a * b
+
+    def backward(self, dy):
+        a, b = self.a, self.b
+        self.a = self.b = None
+        return _unbroadcast(dy * b, a.shape), _unbroadcast(dy * a, b.shape)
+
+
+class Div(Operator):
+    def forward(self, a, b):
+        if self.requires_grad:
+            self.a, self.b = a, b
+        return a / b
+
+    def backward(self, dy):
+        a, b = self.a, self.b
+        self.a = self.b = None
+        return _unbroadcast(dy / b, a.shape), _unbroadcast(-dy * a / (b * b), b.shape)
+
+
+class Pow(Operator):
+    def forward(self, a, b):
+        y = torch.pow(a, b)
+        if self.requires_grad:
+            self.a, self.b, self.y = a, b, y
+        return y
+
+    def backward(self, dy):
+        a, b, y = self.a, self.b, self.y
+        da = dy * b * torch.pow(a, b - 1)
+        db = dy * y * torch.log(torch.clamp(a, min=1e-30))
+        return _unbroadcast(da, a.shape), _unbroadcast(db, b.shape)
+
+
+class Matmul(Operator):
+    """Batched/2-D matrix product; bf16 operands use the MFMA kernel."""
+
+    def forward(self, a, b):
+        if self.requires_grad:
+            self.a, self.b = a, b
+        return F.matmul(a, b) if a.dtype == b.dtype else torch.matmul(a, b.to(a.dtype))
+
+    def backward(self, dy):
+        a, b = self.a, self.b
+        self.a = self.b = None
+        if a.dim() == 2 and b.dim() == 2:
+            da = F.gemm_nt(dy.contiguous(), b.contiguous(), out_dtype=a.dtype) if self.needs_grad(0) else None
+            db = None
+            if self.needs_grad(1):
+                tgt = self.grad_target(1)
+                if tgt is not None:
+                    F.gemm_tn_acc(a, dy, tgt)
+                    db = ACCUMULATED
+                else:
+                    db = torch.matmul(a.t().float(), dy.float()).to(b.dtype)
+            return da, db
+        da = torch.matmul(dy, b.transpose(-1, -2)) if self.needs_grad(0) else None
+        db = torch.matmul(a.transpose(-1, -2), dy) if self.needs_grad(1) else None
+        if db is not None:
+            db = _unbroadcast(db, b.shape)
+        if da is not None:
+            da = _unbroadcast(da, a.shape)
+        return da, db
+
+
+class AddBias(Operator):
+    """y = x + b broadcast along ``axis`` (SINGA AddBias: axis 0 adds a row)."""
+
+    def __init__(self, axis: int = 0, name=None):
+        super().__init__(name)
+        self.axis = axis
+
+    def forward(self, x, b):
+        if self.axis == 0:
+            return x + b.to(x.dtype).reshape(1, -1)
+        return x + b.to(x.dtype).reshape(-1, 1)
+
+    def backward(self, dy):
+        db = dy.float().sum(0) if self.axis == 0 else dy.float().sum(1)
+        tgt = self.grad_target(1)
+        if tgt is not None:
+            tgt.add_(db.reshape(tgt.shape))
+            return dy, ACCUMULATED
+        return dy, db
+
+
+class Linear(Operator):
+    """y = x @ W (+ b) with W [in, out] (SINGA / reference InnerProduct layout,
+    src/worker/layer.cc:193-211).  Mixed precision: when x is bf16 the bf16
+    compute copy ``W.low`` is used and gradients accumulate in fp32."""
+
+    def __init__(self, has_bias=True, name=None):
+        super().__init__(name)
+        self.has_bias = has_bias
+
+    def forward(self, x, W, b=None):
+        w = self._w_compute(x, W)
+        lead = x.shape[:-1]
+        x2 = x.reshape(-1, x.shape[-1])
+        bias = b.float() if b is not None else None
+        y = F.matmul(x2, w, out_dtype=x.dtype, bias=bias) if x2.dtype == torch.bfloat16 else \
+            (torch.addmm(bias.to(x2.dtype), x2, w) if bias is not None else x2 @ w)
+        if self.requires_grad:
+            self.x2, self.w = x2, w
+        return y.reshape(*lead, y.shape[-1])
+
+    def _w_compute(self, x, W):
+        if x.dtype == W.dtype:
+            return W
+        p = self.params[1] if len(self.params) > 1 else None
+        if p is not None and p.low is not None and x.dtype == torch.bfloat16:
+            return p.low
+        return W.to(x.dtype)
+
+    def backward(self, dy):
+        x2, w = self.x2, self.w
+        self.x2 = self.w = None
+        dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
+        dx = None
+        if self.needs_grad(0):
+            dx = F.gemm_nt(dy2, w.contiguous(), out_dtype=x2.dtype) if dy2.dtype == torch.bfloat16 else dy2 @ w.t()
+            dx = dx.reshape(*dy.shape[:-1], x2.shape[-1])
+        tgt = self.grad_target(1)
+        if tgt is not None:
+            F.gemm_tn_acc(x2, dy2, tgt)
+            dw = ACCUMULATED
+        else:
+            dw = (x2.float().t() @ dy2.float())
+        res = [dx, dw]
+        if self.has_bias:
+            tb = self.grad_target(2)
+            db = F.colsum(dy2)[0] if dy2.is_cuda else dy2.float().sum(0)
+            if tb is not None:
+                tb.add_(db)
+                db = ACCUMULATED
+            res.append(db)
+        return tuple(res)
+
+
+class Conv2d(Operator):
+    """2-D convolution; NCHW logical / NHWC physical; implicit-GEMM kernels."""
+
+    def __init__(self, stride=(1, 1), padding=(0, 0), dilation=(1, 1), group=1, has_bias=False,
+                 fuse_relu=False, name=None):
+        super().__init__(name)
+        self.stride, self.padding, self.dilation, self.group = tuple(stride), tuple(padding), tuple(dilation), group
+        self.has_bias = has_bias
+        self.fuse_relu = fuse_relu
+
+    def forward(self, x, W, b=None):
+        p = self.params[1] if len(self.params) > 1 else None
+        w = p.low if (p is not None and p.low is not None and x.dtype == torch.bfloat16) else W
+        y = F.conv2d_fwd(x, w, b, self.stride, self.padding, self.dilation, self.group, out_dtype=x.dtype,
+                         relu=self.fuse_relu)
+        if self.requires_grad:
+            self.x, self.w = x, w
+            self.y = y if self.fuse_relu else None
+        return y
+
+    def backward(self, dy):
+        x, w = self.x, self.w
+        self.x = self.w = None
+        if self.fuse_relu:
+            dy = F.relu_bwd_from_y(self.y, dy)
+            self.y = None
+        tgt = self.grad_target(1)
+        dx, dw, db = F.conv2d_bwd(x, w, dy, self.stride, self.padding, self.dilation, self.group,
+                                  need_dx=self.needs_grad(0), dw_out=tgt, need_db=self.has_bias)
+        res = [dx, ACCUMULATED if tgt is not None else dw]
+        if self.has_bias:
+            tb = self.grad_target(2)
+            if tb is not None:
+                tb.add_(db)
+                db = ACCUMULATED
+            res.append(db)
+        return tuple(res)
+
+
+class BatchNorm2d(Operator):
+    """Batch normalisation (+ optional fused ReLU and residual add).
+    Inputs: x, gamma, beta[, residual].  Running stats are updated in place."""
+
+    def __init__(self, running_mean: torch.Tensor, running_var: torch.Tensor, momentum: float = 0.1,
+                 eps: float = 1e-5, relu: bool = False, has_residual: bool = False, name=None):
+        super().__init__(name)
+        self.rm, self.rv = running_mean, running_var
+        self.momentum, self.eps = momentum, eps
+        self.relu, self.has_residual = relu, has_residual
+
+    def forward(self, x, gamma, beta, res=None):
+        y, st = F.batchnorm_fwd(x, gamma, beta, self.rm, self.rv, training, self.momentum, self.eps, self.relu,
+                                res)
+        if self.requires_grad:
+            self.x, self.gamma, self.st = x, gamma, st
+            self.y = y if (self.relu) else None
+        return y
+
+    def backward(self, dy):
+        dx, dg, db, dres = F.batchnorm_bwd(self.x, dy, self.gamma, self.st, self.y, need_dres=self.has_residual)
+        self.x = self.y = self.st = None
+        out = [dx]
+        for i, g in ((1, dg), (2, db)):
+            t = self.grad_target(i)
+            if t is not None:
+                t.add_(g)
+                out.append(ACCUMULATED)
+            else:
+                out.append(g)
+        if self.has_residual:
+            out.append(dres)
+        return tuple(out)
+
+
+class Pooling2d(Operator):
+    def __init__(self, kernel, stride, padding=(0, 0), is_max=True, count_include_pad=True, ceil_mode=False,
+                 name=None):
+        super().__init__(name)
+        self.kernel, self.stride, self.padding = tuple(kernel), tuple(stride), tuple(padding)
+        self.is_max, self.cip, self.ceil = is_max, count_include_pad, ceil_mode
+
+    def forward(self, x):
+        y, arg = F.pool2d_fwd(x, self.kernel, self.stride, self.padding, self.is_max, self.cip, self.ceil)
+        if self.requires_grad:
+            self.xs, self.xl, self.arg = x.shape, x, arg
+        return y
+
+    def backward(self, dy):
+        dx = F.pool2d_bwd(self.xs, self.xl, dy, self.arg, self.kernel, self.stride, self.padding, self.is_max,
+                          self.cip, self.ceil)
+        self.xl = self.arg = None
+        return dx
+
+
+class GlobalAveragePool(Operator):
+    """[N,C,H,W] -> [N,C] (SINGA's GlobalAveragePool keeps [N,C,1,1]; set keepdims)."""
+
+    def __init__(self, keepdims: bool = False, name=None):
+        super().__init__(name)
+        self.keepdims = keepdims
+
+    def forward(self, x):
+        if self.requires_grad:
+            self.xs = x.shape
+        y = F.global_avgpool_fwd(x)
+        return y.reshape(y.shape[0], y.shape[1], 1, 1) if self.keepdims else y
+
+    def backward(self, dy):
+        return F.global_avgpool_bwd(dy.reshape(dy.shape[0], dy.shape[1]).contiguous(), self.xs)
+
+
+class LRN(Operator):
+    """Across-channel local response normalisation (reference kLRN,
+    src/worker/layer.cc:331-378)."""
+
+    def __init__(self, size=5, alpha=1e-4, beta=0.75, k=1.0, name=None):
+        super().__init__(name)
+        self.size, self.alpha, self.beta, self.k = size, alpha, beta, k
+
+    def forward(self, x):
+        y, norm = F.lrn_fwd(x, self.size, self.alpha, self.beta, self.k)
+        if self.requires_grad:
+            self.x, self.norm = x, norm
+        return y
+
+    def backward(self, dy):
+        dx = F.lrn_bwd(self.x, dy, self.norm, self.size, self.alpha, self.beta)
+        self.x = self.norm = None
+        return dx
+
+
+class Dropout(Operator):
+    """Inverted dropout; identity when not training (fixes reference quirk
+    #9: the kDropout layer masked at test time, src/worker/layer.cc:142-152)."""
+
+    def __init__(self, ratio: float = 0.5, seed_source=None, name=None):
+        super().__init__(name)
+        self.ratio = ratio
+        self.seed_source = seed_source
+
+    def forward(self, x):
+        if not training or self.ratio <= 0.0:
+            self.mask = None
+            return x
+        dev = self.seed_source
+        seed, off = dev.next_rng(x.numel()) if dev is not None else (0, 0)
+        y, self.mask = F.dropout_fwd(x, self.ratio, seed, off)
+        return y
+
+    def backward(self, dy):
+        if self.mask is None:
+            return dy
+        dx = F.dropout_bwd(dy, self.mask, self.ratio)
+        self.mask = None
+        return dx
+
+
+class SoftMax(Operator):
+    def __init__(self, axis: int = 1, name=None):
+        super().__init__(name)
+        self.axis = axis
+
+    def forward(self, x):
+        y = F.softmax(x, self.axis)
+        if self.requires_grad:
+            self.y = y
+        return y
+
+    def backward(self, dy):
+        dx = F.softmax_bwd(self.y, dy, self.axis)
+        self.y = None
+        return dx
+
+
+class SoftMaxCrossEntropy(Operator):
+    """Fused softmax + cross-entropy; loss = mean over the batch.  Target is
+    either class ids or a one-hot / probability matrix.  Also records top-k
+    accuracy in ``self.correct`` (the reference's loss-layer metric)."""
+
+    def __init__(self, t: Optional[torch.Tensor] = None, topk: int = 1, name=None):
+        super().__init__(name)
+        self.t = t
+        self.topk = topk
+
+    def forward(self, x, t=None):
+        t = self.t if t is None else t
+        loss, correct, dx = F.softmax_xent(x, t, self.topk, need_grad=self.requires_grad)
+        self.dx = dx
+        self.correct = correct
+        self.per_row = loss
+        self.nt = 2 if self.t is None and t is not None else 1
+        return loss.mean()
+
+    def backward(self, dy=None):
+        dx = self.dx
+        self.dx = None
+        if not is_unit(dy):
+            dx = (dx.float() * dy.float()).to(dx.dtype)
+        return (dx, None) if len(self.src) == 2 else dx
+
+
+class CrossEntropy(Operator):
+    """Cross entropy over probabilities: -sum(t * log(p)) / B."""
+
+    def forward(self, p, t):
+        if self.requires_grad:
+            self.p, self.t = p, t
+        B = p.shape[0]
+        if t.dim() == 1 or not t.is_floating_point():
+            tt = torch.nn.functional.one_hot(t.long().reshape(-1), p.shape[-1]).to(p.dtype)
+        else:
+            tt = t
+        self.tt = tt
+        return -(tt * torch.log(torch.clamp(p.float(), min=1e-30))).sum() / B
+
+    def backward(self, dy=None):
+        B = self.p.shape[0]
+        g = -self.tt / torch.clamp(self.p.float(), min=1e-30) / B
+        if dy is not None:
+            g = g * dy
+        return g.to(self.p.dtype), None
+
+
+class MeanSquareError(Operator):
+    def forward(self, x, t):
+        if self.requires_grad:
+            self.d = (x.float() - t.float())
+        d = x.float() - t.float()
+        return (d * d).sum() / (2.0 * x.shape[0])
+
+    def backward(self, dy=None):
+        g = self.d / self.d.shape[0]
+        if dy is not None:
+            g = g * dy
+        return g, None
+
+
+class BinaryCrossEntropy(Operator):
+    def forward(self, x, t):
+        p = torch.clamp(x.float(), 1e-7, 1 - 1e-7)
+        if self.requires_grad:
+            self.p, self.t = p, t.float()
+        return -(t.float() * torch.log(p) + (1 - t.float()) * torch.log(1 - p)).mean()
+
+    def backward(self, dy=None):
+        p, t = self.p, self.t
+        g = (p - t) / (p * (1 - p)) / p.numel()
+        if dy is not None:
+            g = g * dy
+        return g, None
+
+
+class LayerNorm(Operator):
+    def __init__(self, eps: float = 1e-5, name=None):
+        super().__init__(name)
+        self.eps = eps
+
+    def forward(self, x, g=None, b=None):
+        y, mean, rstd = F.layernorm_fwd(x, g, b, self.eps)
+        if self.requires_grad:
+            self.x, self.g, self.mean, self.rstd = x, g, mean, rstd
+        return y
+
+    def backward(self, dy):
+        dx, dg, db = F.layernorm_bwd(self.x, dy.contiguous(), self.g, self.mean, self.rstd)
+        self.x = None
+        out = [dx]
+        if len(self.src) > 1:
+            for i, gg in ((1, dg), (2, db)):
+                if i >= len(self.src):
+                    break
+                t = self.grad_target(i)
+                if t is not None and gg is not None:
+                    t.add_(gg)
+                    out.append(ACCUMULATED)
+                else:
+                    out.append(gg)
+        return tuple(out) if len(out) > 1 else out[0]
+
+
+class Cast(Operator):
+    def __init__(self, to, name=None):
+        super().__init__(name)
+        self.to = to
+
+    def forward(self, x):
+        self.from_dtype = x.dtype
+        return F.cast(x, self.to) if x.is_floating_point() else x.to(self.to)
+
+    def backward(self, dy):
+        return F.cast(dy, self.from_dtype) if self.from_dtype.is_floating_point else None
+
+
+class ToChannelsLast(Operator):
+    """Layout change NCHW -> NHWC memory (no logical change); GPU entry op."""
+
+    def __init__(self, dtype=None, name=None):
+        super().__init__(name)
+        self.dtype = dtype
+
+    def forward(self, x):
+        self.from_dtype = x.dtype
+        if x.dim() != 4:
+            return x.to(self.dtype) if self.dtype else x
+        return x.to(dtype=self.dtype or x.dtype, memory_format=torch.channels_last)
+
+    def backward(self, dy):
+        return dy.to(self.from_dtype)
+
+
+class Reshape(Operator):
+    def __init__(self, shape, name=None):
+        super().__init__(name)
+        self.shape = list(shape)
+
+    def forward(self, x):
+        self.in_shape = x.shape
+        shape = [x.shape[i] if s == 0 and i < x.dim() else s for i, s in enumerate(self.shape)]
+        return x.reshape(shape)
+
+    def backward(self, dy):
+        return dy.reshape(self.in_shape)
+
+
+class Flatten(Operator):
+    def __init__(self, axis: int = 1, name=None):
+        super().__init__(name)
+        self.axis = axis
+
+    def forward(self, x):
+        self.in_shape = x.shape
+        a = self.axis % _b.max(x.dim(), 1) if x.dim() else 0
+        lead = int(np.prod(x.shape[:a])) if a > 0 else 1
+        return x.reshape(lead, -1)
+
+    def backward(self, dy):
+        return dy.reshape(self.in_shape)
+
+
+class TorchFn(Operator):
+    """Generic differentiable op defined by a PyTorch function of the raw
+    inputs (used for shape/glue ops that need no hand-written kernel)."""
+
+    def __init__(self, fn: Callable, name=None, nondiff: Sequence[int] = ()):
+        super().__init__(name)
+        self.fn = fn
+        self.nondiff = set(nondiff)
+
+    def forward(self, *xs):
+        if not self.requires_grad:
+            with torch.no_grad():
+                return self.fn(*xs)
+        with torch.enable_grad():
+            self.inp = [x.detach().requires_grad_(True) if (x.is_floating_point() and i not in self.nondiff)
+                        else x.detach() for i, x in enumerate(xs)]
+            out = self.fn(*self.inp)
+        self.out = out
+        outs = out if isinstance(out, tuple) else (out,)
+        return tuple(o.detach() for o in outs) if isinstance(out, tuple) else out.detach()
+
+    def backward(self, *dys):
+        outs = self.out if isinstance(self.out, tuple) else (self.out,)
+        pairs = [(o, d) for o, d in zip(outs, dys) if d is not None and o.requires_grad]
+        req = [x for x in self.inp if x.requires_grad]
+        if not pairs or not req:
+            return tuple(None for _ in self.inp)
+        gs = torch.autograd.grad([o for o, _ in pairs], req, [d.to(o.dtype) for o, d in pairs],
+                                 allow_unused=True)
+        it = iter(gs)
+        res = tuple(next(it) if x.requires_grad else None for x in self.inp)
+        self.inp = self.out = None
+        return res
+
+
+# ===========================================================================
+# functional API (singa.autograd.xxx)
+# ===========================================================================
+def relu(x):
+    return ReLU()(x)
+
+
+def sigmoid(x):
+    return Sigmoid()(x)
+
+
+def tanh(x):
+    return Tanh()(x)
+
+
+def stanh(x):
+    return STanh()(x)
+
+
+def gelu(x):
+    return Gelu()(x)
+
+
+def softplus(x):
+    return SoftPlus()(x)
+
+
+def exp(x):
+    return Exp()(x)
+
+
+def log(x):
+    return Log()(x)
+
+
+def abs(x):  # noqa: A001
+    return Abs()(x)
+
+
+def sqrt(x):
+    return Sqrt()(x)
+
+
+def reciprocal(x):
+    return Reciprocal()(x)
+
+
+def negative(x):
+    return Negative()(x)
+
+
+def sign(x):
+    return Sign()(x)
+
+
+def square(x):
+    return Square()(x)
+
+
+def leakyrelu(x, a=0.01):
+    return LeakyRelu(a)(x)
+
+
+def elu(x, alpha=1.0):
+    return Elu(alpha)(x)
+
+
+def selu(x, alpha=1.67326, gamma=1.0507):
+    return SeLU(alpha, gamma)(x)
+
+
+def identity(x):
+    return Identity()(x)
+
+
+def _t(x, like: Tensor):
+    if isinstance(x, Tensor):
+        return x
+    return Tensor(device=like.device, data=torch.as_tensor(x, dtype=like.dtype, device=like.data.device),
+                  requires_grad=False)
+
+
+def add(a, b):
+    return Add()(a, _t(b, a))
+
+
+def add_relu(a, b):
+    return Add(relu=True)(a, b)
+
+
+def sub(a, b):
+    return Sub()(a, _t(b, a))
+
+
+def mul(a, b):
+    return Mul()(a, _t(b, a))
+
+
+def div(a, b):
+    return Div()(a, _t(b, a))
+
+
+def pow(a, b):  # noqa: A001
+    return Pow()(a, _t(b, a))
+
+
+def matmul(a, b):
+    return Matmul()(a, b)
+
+
+def add_bias(x, b, axis=0):
+    return AddBias(axis)(x, b)
+
+
+def linear(x, W, b=None):
+    return Linear(b is not None)(x, W, b) if b is not None else Linear(False)(x, W)
+
+
+def softmax(x, axis=1):
+    return SoftMax(axis)(x)
+
+
+def softmax_cross_entropy(x, t, topk=1):
+    return SoftMaxCrossEntropy(topk=topk)(x, t)
+
+
+def cross_entropy(y, t):
+    return CrossEntropy()(y, t)
+
+
+def mse_loss(x, t):
+    return MeanSquareError()(x, t)
+
+
+def binary_cross_entropy(x, t):
+    return BinaryCrossEntropy()(x, t)
+
+
+def reshape(x, shape):
+    return Reshape(shape)(x)
+
+
+def flatten(x, axis=1):
+    return Flatten(axis)(x)
+
+
+def dropout(x, ratio=0.5):
+    return Dropout(ratio, x.device)(x)
+
+
+def cast(x, to):
+    return Cast(to)(x)
+
+
+def layer_norm(x, g=None, b=None, eps=1e-5):
+    args = [a for a in (g, b) if a is not None]
+    return LayerNorm(eps)(x, *args)
+
+
+def _fn(fn, *xs, nondiff=()):
+    return TorchFn(fn, nondiff=nondiff)(*xs)
+
+
+def transpose(x, shape=None):
+    perm = tuple(shape) if shape is not None else tuple(reversed(range(x.ndim())))
+    return _fn(lambda a: a.permute(*perm), x)
+
+
+def squeeze(x, axis=None):
+    return _fn(lambda a: a.squeeze() if axis is None else a.squeeze(axis if isinstance(axis, int) else tuple(axis)),
+               x)
+
+
+def unsqueeze(x, axis):
+    ax = [axis] if isinstance(axis, int) else list(axis)
+
+    def f(a):
+        for d in sorted(ax):
+            a = a.unsqueeze(d)
+        return a
+    return _fn(f, x)
+
+
+def cat(xs, axis=0):
+    return TorchFn(lambda *a: torch.cat(a, dim=axis))(*xs)
+
+
+concat = cat
+
+
+def split(x, axis, parts):
+    return TorchFn(lambda a: tuple(torch.split(a, parts, dim=axis)))(x)
+
+
+def slice(x, starts, ends, axes=None, steps=None):  # noqa: A001
+    axes = axes if axes is not None else list(range(len(starts)))
+    steps = steps if steps is not None else [1] * len(starts)
+
+    def f(a):
+        idx = [builtins_slice(None)] * a.dim()
+        for s, e, ax, st in zip(starts, ends, axes, steps):
+            n = a.shape[ax]
+            e = _b.min(e, n) if e >= 0 else e
+            idx[ax] = builtins_slice(s, e, st)
+        return a[tuple(idx)]
+    return _fn(f, x)
+
+
+builtins_slice = _b.slice
+
+
+def gather(x, axis, indices):
+    idx = torch.as_tensor(indices, device=x.data.device).long()
+    return _fn(lambda a: torch.index_select(a, axis, idx.reshape(-1)).reshape(
+        a.shape[:axis] + tuple(idx.shape) + a.shape[axis + 1:]), x)
+
+
+def tile(x, repeats):
+    return _fn(lambda a: a.repeat(*repeats), x)
+
+
+def expand(x, shape):
+    return _fn(lambda a: a.expand(*shape), x)
+
+
+def pad(x, mode="constant", pads=None, constant=0.0):
+    n = x.ndim()
+    half = len(pads) // 2
+    tp = []
+    for i in reversed(range(n)):
+        tp += [pads[i], pads[i + half]]
+    m = {"constant": "constant", "reflect": "reflect", "edge": "replicate"}[mode]
+    return _fn(lambda a: torch.nn.functional.pad(a, tp, mode=m, value=constant) if m == "constant"
+               else torch.nn.functional.pad(a, tp, mode=m), x)
+
+
+def clip(x, min=None, max=None):  # noqa: A002
+    return _fn(lambda a: torch.clamp(a, min=min, max=max), x)
+
+
+def where(x, y, condition):
+    c = condition.data if isinstance(condition, Tensor) else torch.as_tensor(condition)
+    return _fn(lambda a, b: torch.where(c.to(a.device).bool(), a, b), x, y)
+
+
+def reduce_sum(x, axes=None, keepdims=1):
+    return _fn(lambda a: a.sum(dim=tuple(axes), keepdim=bool(keepdims)) if axes is not None else a.sum(), x)
+
+
+def reduce_mean(x, axes=None, keepdims=1):
+    return _fn(lambda a: a.mean(dim=tuple(axes), keepdim=bool(keepdims)) if axes is not None else a.mean(), x)
+
+
+def sum(*xs):  # noqa: A001
+    return TorchFn(lambda *a: _b.sum(a[1:], a[0]))(*xs)
+
+
+def mean(*xs):
+    return TorchFn(lambda *a: _b.sum(a[1:], a[0]) / len(a))(*xs)
+
+
+def max(*xs):  # noqa: A001
+    def f(*a):
+        r = a[0]
+        for t in a[1:]:
+            r = torch.maximum(r, t)
+        return r
+    return TorchFn(f)(*xs)
+
+
+def min(*xs):  # noqa: A001
+    def f(*a):
+        r = a[0]
+        for t in a[1:]:
+            r = torch.minimum(r, t)
+        return r
+    return TorchFn(f)(*xs)
+
+
+def erf(x):
+    return _fn(torch.erf, x)
+
+
+def cos(x):
+    return _fn(torch.cos, x)
+
+
+def sin(x):
+    return _fn(torch.sin, x)
+
+
+def tan(x):
+    return _fn(torch.tan, x)
+
+
+def cosh(x):
+    return _fn(torch.cosh, x)
+
+
+def sinh(x):
+    return _fn(torch.sinh, x)
+
+
+def acos(x):
+    return _fn(torch.acos, x)
+
+
+def asin(x):
+    return _fn(torch.asin, x)
+
+
+def atan(x):
+    return _fn(torch.atan, x)
+
+
+def acosh(x):
+    return _fn(torch.acosh, x)
+
+
+def asinh(x):
+    return _fn(torch.asinh, x)
+
+
+def atanh(x):
+    return _fn(torch.atanh, x)
+
+
+def ceil(x):
+    return _fn(torch.ceil, x)
+
+
+def floor(x):
+    return _fn(torch.floor, x)
+
+
+def round(x):  # noqa: A001
+    return _fn(torch.round, x)
+
+
+def softsign(x):
+    return _fn(lambda a: a / (1 + a.abs()), x)
+
+
+def hardsigmoid(x, alpha=0.2, gamma=0.5):
+    return _fn(lambda a: torch.clamp(alpha * a + gamma, 0, 1), x)
+
+
+def prelu(x, slope):
+    return _fn(lambda a, s: torch.where(a > 0, a, a * s), x, slope)
+
+
+def _cmp_op(fn):
+    def f(x, y):
+        yy = y.data if isinstance(y, Tensor) else torch.as_tensor(y, device=x.data.device)
+        return Tensor(device=x.device, data=fn(x.data, yy).to(x.dtype), requires_grad=False)
+    return f
+
+
+less = _cmp_op(torch.lt)
+greater = _cmp_op(torch.gt)
+equal = _cmp_op(torch.eq)
+_and = _cmp_op(lambda a, b: a.bool() & b.bool())
+_or = _cmp_op(lambda a, b: a.bool() | b.bool())
+_xor = _cmp_op(lambda a, b: a.bool() ^ b.bool())
+
+
+def _not(x):
+    return Tensor(device=x.device, data=(~x.data.bool()).to(x.dtype), requires_grad=False)
+
+
+def shape(x):
+    return Tensor(device=x.device, data=torch.tensor(list(x.shape), dtype=torch.int64), requires_grad=False)
+
+
+def constant_of_shape(x, value=0.0):
+    shp = [int(v) for v in x.data.reshape(-1).tolist()]
+    return Tensor(device=x.device, data=torch.full(shp, value, dtype=torch.float32, device=x.data.device),
+                  requires_grad=False)
+
+
+def onehot(axis, indices, depth, values):
+    idx = indices.data.long()
+    off, on = float(values.data.reshape(-1)[0]), float(values.data.reshape(-1)[1])
+    oh = torch.nn.functional.one_hot(idx % depth, depth).to(torch.float32) * (on - off) + off
+    if axis != -1:
+        oh = oh.movedim(-1, axis)
+    return Tensor(device=indices.device, data=oh, requires_grad=False)
+
+
+def upsample(x, mode, scales):
+    sc = [float(s) for s in scales]
+
+    def f(a):
+        return torch.nn.functional.interpolate(a, scale_factor=sc[2:], mode="nearest")
+    return _fn(f, x)
+
+
+def depth_to_space(x, blocksize, mode="DCR"):
+    return _fn(lambda a: torch.nn.functional.pixel_shuffle(a, blocksize), x)
+
+
+def space_to_depth(x, blocksize, mode="DCR"):
+    return _fn(lambda a: torch.nn.functional.pixel_unshuffle(a, blocksize), x)
+
+
+def embedding(x_idx, W):
+    idx = x_idx.data.long()
+    return TorchFn(lambda w: torch.nn.functional.embedding(idx, w))(W)
+
+
+def globalaveragepool(x, keepdims=True):
+    return GlobalAveragePool(keepdims)(x)
+
+
+def scatter_elements(x, indices, updates, axis=0):
+    idx = indices.data.long()
+    return TorchFn(lambda a, u: a.scatter(axis, idx, u))(x, updates)
+
+
+def gemm(A, B, C=None, alpha=1.0, beta=1.0, transA=0, transB=0):
+    def f(a, b, *c):
+        aa = a.t() if transA else a
+        bb = b.t() if transB else b
+        r = alpha * (aa @ bb)
+        if c:
+            r = r + beta * c[0]
+        return r
+    args = [A, B] + ([C] if C is not None else [])
+    return TorchFn(f)(*args)
+
+
+def conv2d(x, W, b=None, stride=(1, 1), padding=(0, 0), dilation=(1, 1), group=1):
+    op = Conv2d(stride, padding, dilation, group, has_bias=b is not None)
+    return op(x, W, b) if b is not None else op(x, W)
+
+
+def batchnorm_2d(x, gamma, beta, running_mean, running_var, momentum=0.1, eps=1e-5):
+    return BatchNorm2d(running_mean.data if isinstance(running_mean, Tensor) else running_mean,
+                       running_var.data if isinstance(running_var, Tensor) else running_var, momentum, eps)(
+        x, gamma, beta)
+
+
+def pooling_2d(x, kernel, stride, padding=(0, 0), is_max=True):
+    return Pooling2d(kernel, stride, padding, is_max)(x)

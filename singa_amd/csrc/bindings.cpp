@@ -1,0 +1,240 @@
+// pybind11 entry point of the singa_amd gfx950 kernel library (_C).
+//
+// Every launcher takes raw device pointers (uintptr_t from torch's caching
+// allocator) and the hipStream_t of the caller's current stream, so kernels
+// are stream-ordered with everything else and capture into HIP graphs.
+// Shape / dtype validation happens on the Python side (singa_amd/ops/native.py)
+// before anything is launched.
+#include <hip/hip_runtime.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+#include <stdint.h>
+#include <stdexcept>
+#include <string>
+
+namespace py = pybind11;
+typedef uintptr_t P;
+#define V(x) ((void*)(x))
+#define CV(x) ((const void*)(x))
+#define S(x) ((hipStream_t)(x))
+
+extern "C" {
+void sg_unary_fwd(int, const void*, void*, int64_t, int, float, hipStream_t);
+void sg_unary_bwd(int, const void*, const void*, const void*, void*, int64_t, int, float, hipStream_t);
+void sg_add_act(const void*, const void*, void*, int64_t, int, float, float, int, hipStream_t);
+void sg_relu_bwd_from_y(const void*, const void*, void*, int64_t, int, hipStream_t);
+void sg_cast(const void*, int, void*, int, int64_t, hipStream_t);
+void sg_dropout_fwd(const void*, void*, void*, int64_t, int, float, uint64_t, uint64_t, hipStream_t);
+void sg_dropout_bwd(const void*, const void*, void*, int64_t, int, float, hipStream_t);
+void sg_rand_fill(void*, int64_t, int, int, float, float, uint64_t, uint64_t, hipStream_t);
+void sg_nchw_to_nhwc_pad(const void*, void*, int, int, int, int, int, hipStream_t);
+void sg_softmax_fwd(const void*, void*, int64_t, int, int, int, hipStream_t);
+void sg_softmax_bwd(const void*, const void*, void*, int64_t, int, int, hipStream_t);
+void sg_softmax_xent(const void*, const void*, const void*, void*, void*, void*, int64_t, int, int, int, float,
+                     hipStream_t);
+void sg_layernorm_fwd(const void*, const void*, const void*, void*, void*, void*, int64_t, int, int, float,
+                      hipStream_t);
+void sg_layernorm_bwd(const void*, const void*, const void*, const void*, const void*, void*, void*, void*, int64_t,
+                      int, int, hipStream_t);
+void sg_colsum(const void*, void*, void*, int64_t, int, int, hipStream_t);
+void sg_bn_bwd_reduce(const void*, const void*, const void*, const void*, const void*, void*, void*, int64_t, int,
+                      int, hipStream_t);
+void sg_bn_finalize(const void*, const void*, const void*, const void*, void*, void*, void*, void*, void*, void*, int,
+                    float, float, float, hipStream_t);
+void sg_bn_infer_params(const void*, const void*, const void*, const void*, void*, void*, int, float, hipStream_t);
+void sg_bn_apply(const void*, const void*, const void*, const void*, void*, int64_t, int, int, int, hipStream_t);
+void sg_bn_bwd_apply(const void*, const void*, const void*, const void*, const void*, const void*, const void*,
+                     const void*, void*, void*, int64_t, int, int, hipStream_t);
+void sg_pool_fwd(const void*, void*, void*, int, int, int, int, int, int, int, int, int, int, int, int, int, int, int,
+                 hipStream_t);
+void sg_pool_bwd(const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int, int, int,
+                 int, hipStream_t);
+void sg_gap_fwd(const void*, void*, int, int, int, int, hipStream_t);
+void sg_gap_bwd(const void*, void*, int, int, int, int, hipStream_t);
+void sg_lrn_fwd(const void*, void*, void*, int64_t, int, int, float, float, float, int, hipStream_t);
+void sg_lrn_bwd(const void*, const void*, const void*, void*, int64_t, int, int, float, float, int, hipStream_t);
+void sg_opt_update(int, void*, const void*, void*, void*, void*, const void*, const void*, const void*, const void*,
+                   const void*, const void*, int, float, float, float, float, float, float, float, float, int, int,
+                   hipStream_t);
+void sg_sqnorm(const void*, int64_t, void*, hipStream_t);
+void sg_easgd_diff(void*, const void*, void*, int64_t, float, hipStream_t);
+void sg_axpy(void*, const void*, int64_t, float, hipStream_t);
+void sg_rsync_gather(const void*, const void*, void*, int64_t, int64_t, int64_t, int64_t, hipStream_t);
+void sg_rsync_scatter(void*, void*, const void*, int64_t, int64_t, int64_t, int64_t, hipStream_t);
+void sg_gemm(const void*, int64_t, int, const void*, int64_t, int, void*, int64_t, int, int, int, float, float,
+             const void*, int, int, int, int, int64_t, int64_t, int64_t, hipStream_t);
+void sg_conv_fwd(const void*, const void*, void*, const void*, int, int, int, int, int, int, int, int, int, int, int,
+                 int, int, int, int, int, int, hipStream_t);
+void sg_conv_dgrad(const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int, int,
+                   int, int, int, hipStream_t);
+void sg_conv_wgrad(const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int, int,
+                   int, int, int, hipStream_t);
+void sg_wt_transpose(const void*, void*, int, int, int, hipStream_t);
+}
+
+static void check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+#define CHK(name) check_launch(name)
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "singa_amd gfx950 HIP kernel library";
+
+  m.def("device_info", []() {
+    py::dict d;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    d["count"] = n;
+    if (n > 0) {
+      hipDeviceProp_t pr;
+      if (hipGetDeviceProperties(&pr, 0) == hipSuccess) {
+        d["name"] = std::string(pr.name);
+        d["gcnArchName"] = std::string(pr.gcnArchName);
+        d["multiProcessorCount"] = pr.multiProcessorCount;
+        d["sharedMemPerBlock"] = (int64_t)pr.sharedMemPerBlock;
+        d["maxSharedMemoryPerMultiProcessor"] = (int64_t)pr.maxSharedMemoryPerMultiProcessor;
+        d["warpSize"] = pr.warpSize;
+        d["totalGlobalMem"] = (int64_t)pr.totalGlobalMem;
+      }
+    }
+    return d;
+  });
+
+  m.def("unary_fwd", [](int op, P x, P y, int64_t n, int dt, float a, P s) {
+    sg_unary_fwd(op, CV(x), V(y), n, dt, a, S(s)); CHK("unary_fwd");
+  });
+  m.def("unary_bwd", [](int op, P x, P y, P dy, P dx, int64_t n, int dt, float a, P s) {
+    sg_unary_bwd(op, CV(x), CV(y), CV(dy), V(dx), n, dt, a, S(s)); CHK("unary_bwd");
+  });
+  m.def("add_act", [](P a, P b, P y, int64_t n, int dt, float al, float be, int relu, P s) {
+    sg_add_act(CV(a), CV(b), V(y), n, dt, al, be, relu, S(s)); CHK("add_act");
+  });
+  m.def("relu_bwd_from_y", [](P y, P dy, P dx, int64_t n, int dt, P s) {
+    sg_relu_bwd_from_y(CV(y), CV(dy), V(dx), n, dt, S(s)); CHK("relu_bwd_from_y");
+  });
+  m.def("cast", [](P x, int dtx, P y, int dty, int64_t n, P s) {
+    sg_cast(CV(x), dtx, V(y), dty, n, S(s)); CHK("cast");
+  });
+  m.def("dropout_fwd", [](P x, P y, P mask, int64_t n, int dt, float pk, uint64_t seed, uint64_t off, P s) {
+    sg_dropout_fwd(CV(x), V(y), V(mask), n, dt, pk, seed, off, S(s)); CHK("dropout_fwd");
+  });
+  m.def("dropout_bwd", [](P dy, P mask, P dx, int64_t n, int dt, float pk, P s) {
+    sg_dropout_bwd(CV(dy), CV(mask), V(dx), n, dt, pk, S(s)); CHK("dropout_bwd");
+  });
+  m.def("rand_fill", [](P y, int64_t n, int dt, int dist, float a, float b, uint64_t seed, uint64_t off, P s) {
+    sg_rand_fill(V(y), n, dt, dist, a, b, seed, off, S(s)); CHK("rand_fill");
+  });
+  m.def("nchw_to_nhwc_pad", [](P x, P y, int N, int C, int H, int W, int Cp, P s) {
+    sg_nchw_to_nhwc_pad(CV(x), V(y), N, C, H, W, Cp, S(s)); CHK("nchw_to_nhwc_pad");
+  });
+  m.def("softmax_fwd", [](P x, P y, int64_t R, int C, int dt, int out_f32, P s) {
+    sg_softmax_fwd(CV(x), V(y), R, C, dt, out_f32, S(s)); CHK("softmax_fwd");
+  });
+  m.def("softmax_bwd", [](P y, P dy, P dx, int64_t R, int C, int dt, P s) {
+    sg_softmax_bwd(CV(y), CV(dy), V(dx), R, C, dt, S(s)); CHK("softmax_bwd");
+  });
+  m.def("softmax_xent", [](P x, P lab, P soft, P loss, P correct, P dx, int64_t R, int C, int dt, int topk,
+                           float gs, P s) {
+    sg_softmax_xent(CV(x), CV(lab), CV(soft), V(loss), V(correct), V(dx), R, C, dt, topk, gs, S(s));
+    CHK("softmax_xent");
+  });
+  m.def("layernorm_fwd", [](P x, P g, P b, P y, P mean, P rstd, int64_t R, int D, int dt, float eps, P s) {
+    sg_layernorm_fwd(CV(x), CV(g), CV(b), V(y), V(mean), V(rstd), R, D, dt, eps, S(s)); CHK("layernorm_fwd");
+  });
+  m.def("layernorm_bwd", [](P x, P dy, P g, P mean, P rstd, P dx, P dg, P db, int64_t R, int D, int dt, P s) {
+    sg_layernorm_bwd(CV(x), CV(dy), CV(g), CV(mean), CV(rstd), V(dx), V(dg), V(db), R, D, dt, S(s));
+    CHK("layernorm_bwd");
+  });
+  m.def("colsum", [](P x, P o0, P o1, int64_t R, int C, int dt, P s) {
+    sg_colsum(CV(x), V(o0), V(o1), R, C, dt, S(s)); CHK("colsum");
+  });
+  m.def("bn_bwd_reduce", [](P x, P dy, P y, P mean, P invstd, P sdy, P sdyx, int64_t R, int C, int dt, P s) {
+    sg_bn_bwd_reduce(CV(x), CV(dy), CV(y), CV(mean), CV(invstd), V(sdy), V(sdyx), R, C, dt, S(s));
+    CHK("bn_bwd_reduce");
+  });
+  m.def("bn_finalize", [](P sum, P sumsq, P gamma, P beta, P rm, P rv, P mean, P invstd, P scale, P shift, int C,
+                          float count, float mom, float eps, P s) {
+    sg_bn_finalize(CV(sum), CV(sumsq), CV(gamma), CV(beta), V(rm), V(rv), V(mean), V(invstd), V(scale), V(shift), C,
+                   count, mom, eps, S(s));
+    CHK("bn_finalize");
+  });
+  m.def("bn_infer_params", [](P g, P b, P rm, P rv, P scale, P shift, int C, float eps, P s) {
+    sg_bn_infer_params(CV(g), CV(b), CV(rm), CV(rv), V(scale), V(shift), C, eps, S(s)); CHK("bn_infer_params");
+  });
+  m.def("bn_apply", [](P x, P scale, P shift, P res, P y, int64_t R, int C, int relu, int dt, P s) {
+    sg_bn_apply(CV(x), CV(scale), CV(shift), CV(res), V(y), R, C, relu, dt, S(s)); CHK("bn_apply");
+  });
+  m.def("bn_bwd_apply", [](P x, P dy, P y, P mean, P invstd, P gamma, P sdy, P sdyx, P dx, P dres, int64_t R, int C,
+                           int dt, P s) {
+    sg_bn_bwd_apply(CV(x), CV(dy), CV(y), CV(mean), CV(invstd), CV(gamma), CV(sdy), CV(sdyx), V(dx), V(dres), R, C,
+                    dt, S(s));
+    CHK("bn_bwd_apply");
+  });
+  m.def("pool_fwd", [](P x, P y, P arg, int N, int H, int W, int C, int Ho, int Wo, int kh, int kw, int sh, int sw,
+                       int ph, int pw, int is_max, int cp, int dt, P s) {
+    sg_pool_fwd(CV(x), V(y), V(arg), N, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw, is_max, cp, dt, S(s));
+    CHK("pool_fwd");
+  });
+  m.def("pool_bwd", [](P dy, P arg, P dx, int N, int H, int W, int C, int Ho, int Wo, int kh, int kw, int sh, int sw,
+                       int ph, int pw, int is_max, int cp, int dt, P s) {
+    sg_pool_bwd(CV(dy), CV(arg), V(dx), N, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw, is_max, cp, dt, S(s));
+    CHK("pool_bwd");
+  });
+  m.def("gap_fwd", [](P x, P y, int N, int HW, int C, int dt, P s) {
+    sg_gap_fwd(CV(x), V(y), N, HW, C, dt, S(s)); CHK("gap_fwd");
+  });
+  m.def("gap_bwd", [](P dy, P dx, int N, int HW, int C, int dt, P s) {
+    sg_gap_bwd(CV(dy), V(dx), N, HW, C, dt, S(s)); CHK("gap_bwd");
+  });
+  m.def("lrn_fwd", [](P x, P y, P norm, int64_t R, int C, int size, float al, float be, float k, int dt, P s) {
+    sg_lrn_fwd(CV(x), V(y), V(norm), R, C, size, al, be, k, dt, S(s)); CHK("lrn_fwd");
+  });
+  m.def("lrn_bwd", [](P x, P dy, P norm, P dx, int64_t R, int C, int size, float al, float be, int dt, P s) {
+    sg_lrn_bwd(CV(x), CV(dy), CV(norm), V(dx), R, C, size, al, be, dt, S(s)); CHK("lrn_bwd");
+  });
+  m.def("opt_update", [](int kind, P w, P g, P s1, P s2, P wlow, P cstart, P clen, P cseg, P seg_lr, P seg_wd, P hp,
+                         int nchunks, float mom, float damp, float wd, float gs, float b1, float b2, float eps,
+                         float rho, int nesterov, int adamw, P s) {
+    sg_opt_update(kind, V(w), CV(g), V(s1), V(s2), V(wlow), CV(cstart), CV(clen), CV(cseg), CV(seg_lr), CV(seg_wd),
+                  CV(hp), nchunks, mom, damp, wd, gs, b1, b2, eps, rho, nesterov, adamw, S(s));
+    CHK("opt_update");
+  });
+  m.def("sqnorm", [](P x, int64_t n, P out, P s) { sg_sqnorm(CV(x), n, V(out), S(s)); CHK("sqnorm"); });
+  m.def("easgd_diff", [](P w, P c, P d, int64_t n, float alpha, P s) {
+    sg_easgd_diff(V(w), CV(c), V(d), n, alpha, S(s)); CHK("easgd_diff");
+  });
+  m.def("axpy", [](P y, P x, int64_t n, float a, P s) { sg_axpy(V(y), CV(x), n, a, S(s)); CHK("axpy"); });
+  m.def("rsync_gather", [](P w, P snap, P out, int64_t mm, int64_t n, int64_t a, int64_t b, P s) {
+    sg_rsync_gather(CV(w), CV(snap), V(out), mm, n, a, b, S(s)); CHK("rsync_gather");
+  });
+  m.def("rsync_scatter", [](P w, P snap, P dsum, int64_t mm, int64_t n, int64_t a, int64_t b, P s) {
+    sg_rsync_scatter(V(w), V(snap), CV(dsum), mm, n, a, b, S(s)); CHK("rsync_scatter");
+  });
+  m.def("gemm", [](P a, int64_t lda, int ako, P b, int64_t ldb, int bko, P c, int64_t ldc, int M, int N, int K,
+                   float alpha, float beta, P bias, int relu, int out_mode, int splits, int batch, int64_t sa,
+                   int64_t sb, int64_t sc, P s) {
+    sg_gemm(CV(a), lda, ako, CV(b), ldb, bko, V(c), ldc, M, N, K, alpha, beta, CV(bias), relu, out_mode, splits,
+            batch, sa, sb, sc, S(s));
+    CHK("gemm");
+  });
+  m.def("conv_fwd", [](P x, P w, P y, P bias, int N, int H, int W, int C, int K, int R, int Sd, int Ho, int Wo,
+                       int sh, int sw, int ph, int pw, int dh, int dw, int relu, int out_mode, P s) {
+    sg_conv_fwd(CV(x), CV(w), V(y), CV(bias), N, H, W, C, K, R, Sd, Ho, Wo, sh, sw, ph, pw, dh, dw, relu, out_mode,
+                S(s));
+    CHK("conv_fwd");
+  });
+  m.def("conv_dgrad", [](P dy, P wt, P dx, int N, int H, int W, int C, int K, int R, int Sd, int Ho, int Wo, int sh,
+                         int sw, int ph, int pw, int dh, int dw, int out_mode, P s) {
+    sg_conv_dgrad(CV(dy), CV(wt), V(dx), N, H, W, C, K, R, Sd, Ho, Wo, sh, sw, ph, pw, dh, dw, out_mode, S(s));
+    CHK("conv_dgrad");
+  });
+  m.def("conv_wgrad", [](P x, P dy, P dw_out, int N, int H, int W, int C, int K, int R, int Sd, int Ho, int Wo,
+                         int sh, int sw, int ph, int pw, int dh, int dw, int splits, P s) {
+    sg_conv_wgrad(CV(x), CV(dy), V(dw_out), N, H, W, C, K, R, Sd, Ho, Wo, sh, sw, ph, pw, dh, dw, splits, S(s));
+    CHK("conv_wgrad");
+  });
+  m.def("wt_transpose", [](P w, P wt, int K, int RS, int C, P s) {
+    sg_wt_transpose(CV(w), V(wt), K, RS, C, S(s)); CHK("wt_transpose");
+  });
+}

@@ -1,0 +1,117 @@
+// Shared device helpers for the singa_amd gfx950 (CDNA4) kernel library.
+//
+// Everything here is written for wave64 / MI355X only: lane masks are 64-bit,
+// reductions use 64-wide shuffles (the reference's 32-wide warp-synchronous
+// reduction idiom, include/mshadow/cuda/cuda_reduce.cuh:40-112, is deliberately
+// NOT reproduced), and bf16 is handled through clang's native __bf16 type so
+// that hipcc emits v_cvt_pk_bf16_f32 for conversions.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace sg {
+
+constexpr int kWave = 64;
+
+typedef __bf16 bf16;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef short i16x4 __attribute__((ext_vector_type(4)));
+typedef short i16x8 __attribute__((ext_vector_type(8)));
+
+// dtype codes shared with the python side (singa_amd/ops/native.py)
+enum DType : int { kF32 = 0, kBF16 = 1, kF16 = 2, kI32 = 3, kI64 = 4, kU8 = 5 };
+
+__device__ __forceinline__ float to_f32(float x) { return x; }
+__device__ __forceinline__ float to_f32(bf16 x) { return (float)x; }
+template <typename T> __device__ __forceinline__ T from_f32(float x);
+template <> __device__ __forceinline__ float from_f32<float>(float x) { return x; }
+template <> __device__ __forceinline__ bf16 from_f32<bf16>(float x) { return (bf16)x; }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum; `sh` must hold >= blockDim.x/64 floats. Result broadcast.
+__device__ __forceinline__ float block_sum(float v, float* sh) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int nw = (blockDim.x + 63) >> 6;
+  v = wave_sum(v);
+  __syncthreads();
+  if (lane == 0) sh[wid] = v;
+  __syncthreads();
+  float t = 0.f;
+  for (int i = 0; i < nw; ++i) t += sh[i];
+  return t;
+}
+__device__ __forceinline__ float block_max(float v, float* sh) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int nw = (blockDim.x + 63) >> 6;
+  v = wave_max(v);
+  __syncthreads();
+  if (lane == 0) sh[wid] = v;
+  __syncthreads();
+  float t = -INFINITY;
+  for (int i = 0; i < nw; ++i) t = fmaxf(t, sh[i]);
+  return t;
+}
+
+// Philox4x32-10 counter-based RNG (reproducible per (seed, offset)).
+struct Philox {
+  __device__ static inline uint4 round(uint4 c, uint2 k) {
+    const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+    uint32_t hi0 = __umulhi(M0, c.x), lo0 = M0 * c.x;
+    uint32_t hi1 = __umulhi(M1, c.z), lo1 = M1 * c.z;
+    return make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
+  }
+  __device__ static inline uint4 gen(uint64_t seed, uint64_t counter, uint32_t sub) {
+    uint4 c = make_uint4((uint32_t)counter, (uint32_t)(counter >> 32), sub, 0u);
+    uint2 k = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+      c = round(c, k);
+      k.x += 0x9E3779B9u;
+      k.y += 0xBB67AE85u;
+    }
+    return c;
+  }
+  __device__ static inline float u01(uint32_t x) {  // (0,1]
+    return ((float)(x >> 8) + 1.0f) * (1.0f / 16777216.0f);
+  }
+};
+
+// Fast unsigned division by a runtime constant (Granlund-Montgomery style),
+// used by implicit-GEMM loaders to split flat pixel indices without v_div.
+struct FastDiv {
+  uint32_t d, m, s;
+  __host__ __device__ FastDiv() : d(1), m(0), s(0) {}
+  __host__ FastDiv(uint32_t div) : d(div) {
+    s = 0;
+    while ((1u << s) < div) ++s;
+    uint64_t one = 1;
+    m = (uint32_t)(((one << 32) * ((one << s) - div)) / div + 1);
+  }
+  __device__ __forceinline__ uint32_t div(uint32_t n) const {
+    return (uint32_t)(((uint64_t)__umulhi(n, m) + n) >> s);
+  }
+};
+
+}  // namespace sg
+
+#define SG_GRID_STRIDE(i, n) \
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (n); i += (int64_t)gridDim.x * blockDim.x)
+
+static inline int sg_grid(int64_t n, int block = 256, int cap = 4096) {
+  int64_t g = (n + block - 1) / block;
+  if (g < 1) g = 1;
+  return (int)(g > cap ? cap : g);
+}

@@ -1,0 +1,752 @@
+"""Device-dispatching functional ops on raw ``torch.Tensor`` storage.
+
+Every hot op has two implementations:
+
+* GPU (``tensor.is_cuda``): a hand-written gfx950 HIP kernel from
+  ``singa_amd/csrc/kernels`` launched on the current HIP stream.  Activation
+  tensors of 4-D ops are NHWC in memory (``torch.channels_last``) while the
+  logical shape stays NCHW as in SINGA's API.  Convolutions always run the
+  bf16 MFMA implicit-GEMM kernel with fp32 accumulation (fp32 tensors are cast
+  on entry, like TF32 mode on other hardware).
+* CPU: a plain PyTorch fp32/bf16 reference, which doubles as the numerics
+  oracle for the kernel tests (the reference framework's CppCPU device).
+
+Plain GEMMs whose dimensions are not multiples of 8 go to hipBLAS through
+``torch.matmul`` (the "plain library GEMM" path); everything else uses the MFMA
+kernel.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional, Sequence, Tuple
+
+import torch
+import torch.nn.functional as F
+
+from . import native as N
+
+# unary op codes (csrc/kernels/elementwise.hip)
+UNARY = {"relu": 0, "sigmoid": 1, "tanh": 2, "stanh": 3, "gelu": 4, "identity": 5, "softplus": 6, "square": 7,
+         "abs": 8, "exp": 9, "leakyrelu": 10, "elu": 11, "selu": 12, "gelu_tanh": 13, "sqrt": 14, "neg": 15,
+         "reciprocal": 16, "log": 17, "sign": 18}
+
+_CPU_UNARY = {
+    "relu": torch.relu, "sigmoid": torch.sigmoid, "tanh": torch.tanh,
+    "stanh": lambda x: 1.7159047 * torch.tanh(0.66666667 * x),
+    "gelu": lambda x: F.gelu(x), "gelu_tanh": lambda x: F.gelu(x, approximate="tanh"),
+    "identity": lambda x: x.clone(), "softplus": F.softplus, "square": torch.square, "abs": torch.abs,
+    "exp": torch.exp, "sqrt": torch.sqrt, "neg": torch.neg, "reciprocal": torch.reciprocal, "log": torch.log,
+    "sign": torch.sign,
+}
+
+
+def _native_ok(*ts: torch.Tensor) -> bool:
+    return all(t is None or t.is_cuda for t in ts) and N.force_native()
+
+
+def _flat_ok(t: torch.Tensor) -> bool:
+    return t.dtype in (torch.float32, torch.bfloat16) and (t.is_contiguous() or N.is_cl(t))
+
+
+def _like(t: torch.Tensor, dtype=None) -> torch.Tensor:
+    """Empty tensor with the same shape AND memory layout as t."""
+    if t.dim() == 4 and N.is_cl(t) and not t.is_contiguous():
+        return torch.empty(t.shape, dtype=dtype or t.dtype, device=t.device, memory_format=torch.channels_last)
+    return torch.empty(t.shape, dtype=dtype or t.dtype, device=t.device)
+
+
+def _dense(t: torch.Tensor) -> torch.Tensor:
+    return t if (t.is_contiguous() or N.is_cl(t)) else t.contiguous()
+
+
+# ----------------------------------------------------------------------------
+# elementwise
+# ----------------------------------------------------------------------------
+def unary(op: str, x: torch.Tensor, alpha: float = 0.0) -> torch.Tensor:
+    if _native_ok(x) and _flat_ok(x) and op in UNARY:
+        x = _dense(x)
+        y = _like(x)
+        N.lib().unary_fwd(UNARY[op], x.data_ptr(), y.data_ptr(), x.numel(), N.dt(x), alpha, N.stream())
+        return y
+    if op == "leakyrelu":
+        return F.leaky_relu(x, alpha)
+    if op == "elu":
+        return F.elu(x, alpha)
+    if op == "selu":
+        return F.selu(x)
+    return _CPU_UNARY[op](x)
+
+
+def unary_bwd(op: str, x: Optional[torch.Tensor], y: Optional[torch.Tensor], dy: torch.Tensor,
+              alpha: float = 0.0) -> torch.Tensor:
+    if _native_ok(dy) and _flat_ok(dy) and op in UNARY:
+        dy = _dense(dy)
+        xx = _dense(x) if x is not None else None
+        yy = _dense(y) if y is not None else None
+        for t in (xx, yy):
+            if t is not None and t.stride() != dy.stride():
+                raise ValueError("unary_bwd: layout mismatch")
+        dx = _like(dy)
+        N.lib().unary_bwd(UNARY[op], N.ptr(xx), N.ptr(yy), dy.data_ptr(), dx.data_ptr(), dy.numel(), N.dt(dy),
+                          alpha, N.stream())
+        return dx
+    xf = x.float() if x is not None else None
+    yf = y.float() if y is not None else None
+    g = dy.float()
+    if op == "relu":
+        r = g * (xf > 0)
+    elif op == "sigmoid":
+        r = g * yf * (1 - yf)
+    elif op == "tanh":
+        r = g * (1 - yf * yf)
+    elif op == "stanh":
+        r = g * (0.66666667 * 1.7159047 - 0.66666667 / 1.7159047 * yf * yf)
+    elif op in ("gelu", "gelu_tanh"):
+        with torch.enable_grad():
+            xx = xf.detach().requires_grad_(True)
+            out = F.gelu(xx, approximate="tanh" if op == "gelu_tanh" else "none")
+            (r,) = torch.autograd.grad(out, xx, g)
+    elif op == "identity":
+        r = g
+    elif op == "softplus":
+        r = g * torch.sigmoid(xf)
+    elif op == "square":
+        r = g * 2 * xf
+    elif op == "abs":
+        r = g * torch.sign(xf)
+    elif op == "exp":
+        r = g * yf
+    elif op == "leakyrelu":
+        r = torch.where(xf > 0, g, alpha * g)
+    elif op == "elu":
+        r = torch.where(xf > 0, g, g * (yf + alpha))
+    elif op == "selu":
+        l, a = 1.0507009873554805, 1.6732632423543772
+        r = torch.where(xf > 0, l * g, g * (yf + l * a))
+    elif op == "sqrt":
+        r = g * 0.5 / yf
+    elif op == "neg":
+        r = -g
+    elif op == "reciprocal":
+        r = -g * yf * yf
+    elif op == "log":
+        r = g / xf
+    elif op == "sign":
+        r = torch.zeros_like(g)
+    else:
+        raise KeyError(op)
+    return r.to(dy.dtype)
+
+
+def add_act(a: torch.Tensor, b: torch.Tensor, alpha=1.0, beta=1.0, relu=False) -> torch.Tensor:
+    if _native_ok(a, b) and _flat_ok(a) and a.dtype == b.dtype and a.shape == b.shape:
+        a, b = _dense(a), _dense(b)
+        if a.stride() == b.stride():
+            y = _like(a)
+            N.lib().add_act(a.data_ptr(), b.data_ptr(), y.data_ptr(), a.numel(), N.dt(a), alpha, beta, int(relu),
+                            N.stream())
+            return y
+    r = alpha * a + beta * b
+    return torch.relu(r) if relu else r
+
+
+def relu_bwd_from_y(y: torch.Tensor, dy: torch.Tensor) -> torch.Tensor:
+    if _native_ok(y, dy) and _flat_ok(dy) and y.stride() == dy.stride() and y.dtype == dy.dtype:
+        dx = _like(dy)
+        N.lib().relu_bwd_from_y(y.data_ptr(), dy.data_ptr(), dx.data_ptr(), dy.numel(), N.dt(dy), N.stream())
+        return dx
+    return dy * (y > 0)
+
+
+def cast(x: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
+    if x.dtype == dtype:
+        return x
+    if _native_ok(x) and _flat_ok(x) and dtype in (torch.float32, torch.bfloat16):
+        x = _dense(x)
+        y = _like(x, dtype)
+        N.lib().cast(x.data_ptr(), N.dt(x), y.data_ptr(), N.dt(y), x.numel(), N.stream())
+        return y
+    return x.to(dtype)
+
+
+def dropout_fwd(x: torch.Tensor, ratio: float, seed: int, offset: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    pkeep = 1.0 - ratio
+    if _native_ok(x) and _flat_ok(x):
+        x = _dense(x)
+        y = _like(x)
+        mask = _like(x, torch.uint8)
+        N.lib().dropout_fwd(x.data_ptr(), y.data_ptr(), mask.data_ptr(), x.numel(), N.dt(x), pkeep, seed, offset,
+                            N.stream())
+        return y, mask
+    g = torch.Generator(device=x.device).manual_seed(int(seed + offset) & 0x7FFFFFFFFFFFFFFF)
+    mask = (torch.rand(x.shape, generator=g, device=x.device) < pkeep).to(torch.uint8)
+    return x * mask.to(x.dtype) / pkeep, mask
+
+
+def dropout_bwd(dy: torch.Tensor, mask: torch.Tensor, ratio: float) -> torch.Tensor:
+    pkeep = 1.0 - ratio
+    if _native_ok(dy) and _flat_ok(dy) and _dense(dy).stride() == mask.stride():
+        dy = _dense(dy)
+        dx = _like(dy)
+        N.lib().dropout_bwd(dy.data_ptr(), mask.data_ptr(), dx.data_ptr(), dy.numel(), N.dt(dy), pkeep, N.stream())
+        return dx
+    return dy * mask.to(dy.dtype) / pkeep
+
+
+# ----------------------------------------------------------------------------
+# softmax / losses / layernorm
+# ----------------------------------------------------------------------------
+def softmax(x: torch.Tensor, axis: int = -1) -> torch.Tensor:
+    axis = axis % x.dim()
+    if _native_ok(x) and _flat_ok(x) and axis == x.dim() - 1 and x.is_contiguous() and x.shape[-1] <= 16384:
+        C = x.shape[-1]
+        y = torch.empty_like(x)
+        N.lib().softmax_fwd(x.data_ptr(), y.data_ptr(), x.numel() // C, C, N.dt(x), int(x.dtype == torch.float32),
+                            N.stream())
+        return y
+    return torch.softmax(x.float(), dim=axis).to(x.dtype)
+
+
+def softmax_bwd(y: torch.Tensor, dy: torch.Tensor, axis: int = -1) -> torch.Tensor:
+    axis = axis % y.dim()
+    if (_native_ok(y, dy) and _flat_ok(y) and axis == y.dim() - 1 and y.is_contiguous() and dy.is_contiguous()
+            and y.dtype == dy.dtype):
+        C = y.shape[-1]
+        dx = torch.empty_like(dy)
+        N.lib().softmax_bwd(y.data_ptr(), dy.data_ptr(), dx.data_ptr(), y.numel() // C, C, N.dt(y), N.stream())
+        return dx
+    yf, gf = y.float(), dy.float()
+    return (yf * (gf - (gf * yf).sum(dim=axis, keepdim=True))).to(dy.dtype)
+
+
+def softmax_xent(x: torch.Tensor, target: torch.Tensor, topk: int = 1, grad_scale: Optional[float] = None,
+                 need_grad: bool = True):
+    """Fused softmax + cross entropy.  target: int class ids [B] or a [B, C]
+    probability matrix.  Returns (loss_per_row fp32 [B], correct fp32 [B],
+    dx (p - t) * grad_scale or None).  grad_scale defaults to 1/B."""
+    x2 = x.reshape(-1, x.shape[-1])
+    B, C = x2.shape
+    gs = (1.0 / B) if grad_scale is None else grad_scale
+    soft = target.dim() > 1 and target.shape[-1] == C and target.is_floating_point()
+    if _native_ok(x) and _flat_ok(x2) and x2.is_contiguous() and C <= 16384:
+        loss = torch.empty(B, dtype=torch.float32, device=x.device)
+        correct = torch.empty(B, dtype=torch.float32, device=x.device)
+        dx = torch.empty_like(x2) if need_grad else None
+        if soft:
+            t = target.reshape(B, C).float().contiguous()
+            lab = None
+        else:
+            lab = target.reshape(B).to(torch.int32).contiguous()
+            t = None
+        N.lib().softmax_xent(x2.data_ptr(), N.ptr(lab), N.ptr(t), loss.data_ptr(), correct.data_ptr(), N.ptr(dx), B,
+                             C, N.dt(x2), topk, gs, N.stream())
+        return loss, correct, (dx.reshape(x.shape) if dx is not None else None)
+    xf = x2.float()
+    lse = torch.logsumexp(xf, dim=1)
+    if soft:
+        t = target.reshape(B, C).float()
+        loss = (t * (lse[:, None] - xf)).sum(1)
+        correct = torch.zeros(B, dtype=torch.float32, device=x.device)
+        dx = (torch.softmax(xf, 1) * t.sum(1, keepdim=True) - t) * gs if need_grad else None
+    else:
+        lab = target.reshape(B).long()
+        xl = xf.gather(1, lab[:, None])[:, 0]
+        loss = lse - xl
+        rank = (xf > xl[:, None]).sum(1)
+        correct = (rank < topk).float()
+        if need_grad:
+            p = torch.softmax(xf, 1)
+            p[torch.arange(B, device=x.device), lab] -= 1.0
+            dx = p * gs
+        else:
+            dx = None
+    return loss, correct, (dx.to(x.dtype).reshape(x.shape) if dx is not None else None)
+
+
+def layernorm_fwd(x: torch.Tensor, g: Optional[torch.Tensor], b: Optional[torch.Tensor], eps: float = 1e-5):
+    D = x.shape[-1]
+    if _native_ok(x) and _flat_ok(x) and x.is_contiguous():
+        R = x.numel() // D
+        y = torch.empty_like(x)
+        mean = torch.empty(R, dtype=torch.float32, device=x.device)
+        rstd = torch.empty(R, dtype=torch.float32, device=x.device)
+        gg = g.float().contiguous() if g is not None else None
+        bb = b.float().contiguous() if b is not None else None
+        N.lib().layernorm_fwd(x.data_ptr(), N.ptr(gg), N.ptr(bb), y.data_ptr(), mean.data_ptr(), rstd.data_ptr(), R,
+                              D, N.dt(x), eps, N.stream())
+        return y, mean, rstd
+    xf = x.float().reshape(-1, D)
+    mean = xf.mean(1)
+    rstd = torch.rsqrt(xf.var(1, unbiased=False) + eps)
+    y = (xf - mean[:, None]) * rstd[:, None]
+    if g is not None:
+        y = y * g.float()
+    if b is not None:
+        y = y + b.float()
+    return y.to(x.dtype).reshape(x.shape), mean, rstd
+
+
+def layernorm_bwd(x, dy, g, mean, rstd):
+    D = x.shape[-1]
+    R = x.numel() // D
+    if _native_ok(x, dy) and _flat_ok(x) and x.is_contiguous() and dy.is_contiguous():
+        dx = torch.empty_like(x)
+        dg = torch.zeros(D, dtype=torch.float32, device=x.device) if g is not None else None
+        db = torch.zeros(D, dtype=torch.float32, device=x.device) if g is not None else None
+        gg = g.float().contiguous() if g is not None else None
+        N.lib().layernorm_bwd(x.data_ptr(), dy.data_ptr(), N.ptr(gg), mean.data_ptr(), rstd.data_ptr(),
+                              dx.data_ptr(), N.ptr(dg), N.ptr(db), R, D, N.dt(x), N.stream())
+        return dx, dg, db
+    xf = x.float().reshape(R, D)
+    gy = dy.float().reshape(R, D)
+    xh = (xf - mean[:, None]) * rstd[:, None]
+    dg = (gy * xh).sum(0) if g is not None else None
+    db = gy.sum(0) if g is not None else None
+    gg = gy * g.float() if g is not None else gy
+    a = gg.mean(1, keepdim=True)
+    bsum = (gg * xh).mean(1, keepdim=True)
+    dx = rstd[:, None] * (gg - a - xh * bsum)
+    return dx.to(x.dtype).reshape(x.shape), dg, db
+
+
+# ----------------------------------------------------------------------------
+# GEMM
+# ----------------------------------------------------------------------------
+def _gemm_native_ok(*dims) -> bool:
+    return all(d % 8 == 0 for d in dims)
+
+
+def matmul(a: torch.Tensor, b: torch.Tensor, out_dtype: Optional[torch.dtype] = None,
+           bias: Optional[torch.Tensor] = None, relu: bool = False) -> torch.Tensor:
+    """C = a @ b for 2-D (or batched 3-D with equal batch) row-major operands.
+    bf16 operands run on the MFMA kernel with fp32 accumulation."""
+    out_dtype = out_dtype or a.dtype
+    if (_native_ok(a, b) and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and a.dim() in (2, 3)
+            and a.dim() == b.dim() and (a.dim() == 2 or a.shape[0] == b.shape[0])):
+        M, K = a.shape[-2], a.shape[-1]
+        Nn = b.shape[-1]
+        if _gemm_native_ok(K, Nn) and M > 0:
+            a = a.contiguous()
+            b = b.contiguous()
+            batch = a.shape[0] if a.dim() == 3 else 1
+            c = torch.empty(a.shape[:-1] + (Nn,), dtype=out_dtype, device=a.device)
+            bb = bias.float().contiguous() if bias is not None else None
+            # C[m][n] = sum_k A[m][k] * B(n, k) where B(n,k) = b[k][n] -> b is K-outer
+            N.lib().gemm(a.data_ptr(), K, 0, b.data_ptr(), Nn, 1, c.data_ptr(), Nn, M, Nn, K, 1.0, 0.0, N.ptr(bb),
+                         int(relu), 0 if out_dtype == torch.bfloat16 else 1, 1, batch, M * K, K * Nn, M * Nn,
+                         N.stream())
+            return c
+    r = torch.matmul(a, b)
+    if bias is not None:
+        r = r + bias.to(r.dtype)
+    if relu:
+        r = torch.relu(r)
+    return r.to(out_dtype)
+
+
+def gemm_nt(a: torch.Tensor, b: torch.Tensor, out_dtype=None, bias=None, relu=False) -> torch.Tensor:
+    """C = a @ b.T (both operands K-major: a [M,K], b [N,K])."""
+    out_dtype = out_dtype or a.dtype
+    if (_native_ok(a, b) and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and a.dim() == 2
+            and b.dim() == 2):
+        M, K = a.shape
+        Nn = b.shape[0]
+        if _gemm_native_ok(K) and M > 0:
+            a, b = a.contiguous(), b.contiguous()
+            c = torch.empty((M, Nn), dtype=out_dtype, device=a.device)
+            bb = bias.float().contiguous() if bias is not None else None
+            N.lib().gemm(a.data_ptr(), K, 0, b.data_ptr(), K, 0, c.data_ptr(), Nn, M, Nn, K, 1.0, 0.0, N.ptr(bb),
+                         int(relu), 0 if out_dtype == torch.bfloat16 else 1, 1, 1, 0, 0, 0, N.stream())
+            return c
+    r = a @ b.t()
+    if bias is not None:
+        r = r + bias.to(r.dtype)
+    return (torch.relu(r) if relu else r).to(out_dtype)
+
+
+def gemm_tn_acc(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, beta: float = 1.0) -> torch.Tensor:
+    """out (fp32) = beta*out + a.T @ b with a [K,M], b [K,N] (weight-gradient
+    shape: reduction over the batch dim).  Uses split-K atomics on GPU."""
+    if (_native_ok(a, b, out) and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and out.dtype ==
+            torch.float32 and out.is_contiguous()):
+        K, M = a.shape
+        Nn = b.shape[1]
+        if _gemm_native_ok(M, Nn) and K > 0:
+            a, b = a.contiguous(), b.contiguous()
+            if beta == 0.0:
+                out.zero_()
+            elif beta != 1.0:
+                out.mul_(beta)
+            N.lib().gemm(a.data_ptr(), M, 1, b.data_ptr(), Nn, 1, out.data_ptr(), Nn, M, Nn, K, 1.0, 0.0, 0, 0, 2,
+                         0, 1, 0, 0, 0, N.stream())
+            return out
+    r = a.float().t() @ b.float()
+    if beta == 0.0:
+        out.copy_(r)
+    else:
+        out.mul_(beta).add_(r)
+    return out
+
+
+# ----------------------------------------------------------------------------
+# convolution (NCHW logical, NHWC physical on GPU)
+# ----------------------------------------------------------------------------
+def conv_out_size(h, k, s, p, d=1):
+    return (h + 2 * p - d * (k - 1) - 1) // s + 1
+
+
+def _pad8(n: int) -> int:
+    return (n + 7) // 8 * 8
+
+
+def to_nhwc_bf16(x: torch.Tensor, cpad: Optional[int] = None) -> torch.Tensor:
+    """NCHW-logical tensor -> bf16 channels_last, optionally zero-padding C."""
+    Nn, C, H, W = x.shape
+    cp = cpad or C
+    if cp != C:
+        if x.is_cuda and x.dtype == torch.float32 and x.is_contiguous() and cp % 8 == 0:
+            y = torch.empty((Nn, cp, H, W), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+            N.lib().nchw_to_nhwc_pad(x.data_ptr(), y.data_ptr(), Nn, C, H, W, cp, N.stream())
+            return y
+        y = torch.zeros((Nn, cp, H, W), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+        y[:, :C] = x
+        return y
+    return x.to(dtype=torch.bfloat16, memory_format=torch.channels_last)
+
+
+def conv2d_fwd(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], stride, padding, dilation=(1, 1),
+               groups: int = 1, out_dtype: Optional[torch.dtype] = None, relu: bool = False) -> torch.Tensor:
+    """x [N,C,H,W], w [K,C/g,R,S] -> y [N,K,Ho,Wo] (channels_last on GPU)."""
+    out_dtype = out_dtype or x.dtype
+    sh, sw = stride
+    ph, pw = padding
+    dh, dw = dilation
+    if _native_ok(x, w) and groups == 1:
+        Nn, Cx, H, W = x.shape
+        K, C, R, S = w.shape
+        Ho, Wo = conv_out_size(H, R, sh, ph, dh), conv_out_size(W, S, sw, pw, dw)
+        Cp, Kp = _pad8(C), _pad8(K)
+        if Cx not in (C, Cp):
+            raise ValueError(f"conv2d: input has {Cx} channels, weight expects {C}")
+        xb = x if (x.dtype == torch.bfloat16 and N.is_cl(x) and Cx == Cp) else to_nhwc_bf16(x[:, :C], Cp)
+        wb = w
+        if Cp != C or Kp != K:
+            wb = torch.zeros((Kp, Cp, R, S), dtype=torch.bfloat16, device=w.device, memory_format=torch.channels_last)
+            wb[:K, :C] = w
+        elif not (w.dtype == torch.bfloat16 and N.is_cl(w)):
+            wb = w.to(dtype=torch.bfloat16, memory_format=torch.channels_last)
+        bias = None
+        if b is not None:
+            bias = b.float()
+            if Kp != K:
+                bias = torch.cat([bias, bias.new_zeros(Kp - K)])
+            bias = bias.contiguous()
+        od = torch.bfloat16 if out_dtype == torch.bfloat16 else torch.float32
+        y = torch.empty((Nn, Kp, Ho, Wo), dtype=od, device=x.device, memory_format=torch.channels_last)
+        N.lib().conv_fwd(xb.data_ptr(), wb.data_ptr(), y.data_ptr(), N.ptr(bias), Nn, H, W, Cp, Kp, R, S, Ho, Wo, sh,
+                         sw, ph, pw, dh, dw, int(relu), 0 if od == torch.bfloat16 else 1, N.stream())
+        if Kp != K:
+            y = y[:, :K].contiguous(memory_format=torch.channels_last)
+        return y if y.dtype == out_dtype else y.to(out_dtype)
+    xf = x.float() if x.dtype != torch.float32 else x
+    y = F.conv2d(xf, w.float(), b.float() if b is not None else None, (sh, sw), (ph, pw), (dh, dw), groups)
+    if relu:
+        y = torch.relu(y)
+    return y.to(out_dtype)
+
+
+def conv2d_bwd(x: torch.Tensor, w: torch.Tensor, dy: torch.Tensor, stride, padding, dilation=(1, 1), groups=1,
+               need_dx=True, dw_out: Optional[torch.Tensor] = None, need_db=False):
+    """Returns (dx, dw, db).  If dw_out (fp32, same logical shape as w) is given
+    the weight gradient is ACCUMULATED into it (flat grad buffer views)."""
+    sh, sw = stride
+    ph, pw = padding
+    dh, dw_ = dilation
+    if _native_ok(x, w, dy) and groups == 1:
+        Nn, Cx, H, W = x.shape
+        K, C, R, S = w.shape
+        Ho, Wo = dy.shape[2], dy.shape[3]
+        Cp, Kp = _pad8(C), _pad8(K)
+        xb = x if (x.dtype == torch.bfloat16 and N.is_cl(x) and Cx == Cp) else to_nhwc_bf16(x[:, :C], Cp)
+        dyb = dy if (dy.dtype == torch.bfloat16 and N.is_cl(dy) and Kp == K) else to_nhwc_bf16(dy, Kp)
+        padded = Cp != C or Kp != K
+        dx = dwt = db = None
+        if need_dx:
+            if padded:
+                wb = torch.zeros((Kp, Cp, R, S), dtype=torch.bfloat16, device=w.device,
+                                 memory_format=torch.channels_last)
+                wb[:K, :C] = w
+            else:
+                wb = w if (w.dtype == torch.bfloat16 and N.is_cl(w)) else w.to(dtype=torch.bfloat16,
+                                                                                memory_format=torch.channels_last)
+            wt = torch.empty((Cp, R, S, Kp), dtype=torch.bfloat16, device=w.device)
+            N.lib().wt_transpose(wb.data_ptr(), wt.data_ptr(), Kp, R * S, Cp, N.stream())
+            od = torch.bfloat16 if x.dtype == torch.bfloat16 else torch.float32
+            dxp = torch.empty((Nn, Cp, H, W), dtype=od, device=x.device, memory_format=torch.channels_last)
+            N.lib().conv_dgrad(dyb.data_ptr(), wt.data_ptr(), dxp.data_ptr(), Nn, H, W, Cp, Kp, R, S, Ho, Wo, sh, sw,
+                               ph, pw, dh, dw_, 0 if od == torch.bfloat16 else 1, N.stream())
+            dx = dxp[:, :C].contiguous(memory_format=torch.channels_last) if Cx != Cp else dxp
+            if dx.dtype != x.dtype:
+                dx = dx.to(x.dtype)
+        # weight gradient, fp32 [Kp][R][S][Cp]
+        direct = (dw_out is not None and not padded and dw_out.dtype == torch.float32 and N.is_cl(dw_out))
+        target = dw_out if direct else torch.zeros((Kp, Cp, R, S), dtype=torch.float32, device=x.device,
+                                                   memory_format=torch.channels_last)
+        N.lib().conv_wgrad(xb.data_ptr(), dyb.data_ptr(), target.data_ptr(), Nn, H, W, Cp, Kp, R, S, Ho, Wo, sh, sw,
+                           ph, pw, dh, dw_, 0, N.stream())
+        if direct:
+            dwt = dw_out
+        else:
+            g = target[:K, :C]
+            if dw_out is not None:
+                dw_out.add_(g)
+                dwt = dw_out
+            else:
+                dwt = g.contiguous()
+        if need_db:
+            db = colsum(dyb.permute(0, 2, 3, 1).reshape(-1, Kp))[0][:K]
+        return dx, dwt, db
+    # CPU reference via autograd of the functional conv
+    with torch.enable_grad():
+        xx = x.detach().float().requires_grad_(need_dx)
+        ww = w.detach().float().requires_grad_(True)
+        y = F.conv2d(xx, ww, None, (sh, sw), (ph, pw), (dh, dw_), groups)
+        grads = torch.autograd.grad(y, [xx, ww] if need_dx else [ww], dy.float())
+    dx = grads[0].to(x.dtype) if need_dx else None
+    gw = grads[-1]
+    if dw_out is not None:
+        dw_out.add_(gw)
+        gw = dw_out
+    db = dy.float().sum(dim=(0, 2, 3)) if need_db else None
+    return dx, gw, db
+
+
+# ----------------------------------------------------------------------------
+# reductions, batchnorm, pooling, LRN
+# ----------------------------------------------------------------------------
+def _rows_c(x: torch.Tensor) -> Tuple[torch.Tensor, int, int]:
+    """View a channels_last 4-D (or 2-D [R,C]) tensor as [R][C] memory."""
+    if x.dim() == 4:
+        if not N.is_cl(x):
+            raise ValueError("expected channels_last tensor")
+        C = x.shape[1]
+        return x, x.numel() // C, C
+    return x, x.shape[0], x.shape[-1]
+
+
+def colsum(x2: torch.Tensor, with_sq: bool = False):
+    """Per-column sum (and sum of squares) of a [R, C] row-major tensor -> fp32."""
+    if _native_ok(x2) and _flat_ok(x2) and x2.is_contiguous():
+        R, C = x2.shape
+        o0 = torch.zeros(C, dtype=torch.float32, device=x2.device)
+        o1 = torch.zeros(C, dtype=torch.float32, device=x2.device) if with_sq else None
+        N.lib().colsum(x2.data_ptr(), o0.data_ptr(), N.ptr(o1), R, C, N.dt(x2), N.stream())
+        return o0, o1
+    xf = x2.float()
+    return xf.sum(0), ((xf * xf).sum(0) if with_sq else None)
+
+
+class BNState:
+    """Saved tensors of a batch-norm forward needed by the backward."""
+    __slots__ = ("mean", "invstd", "scale", "shift")
+
+    def __init__(self, mean, invstd, scale, shift):
+        self.mean, self.invstd, self.scale, self.shift = mean, invstd, scale, shift
+
+
+def batchnorm_fwd(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, run_mean: torch.Tensor,
+                  run_var: torch.Tensor, training: bool, momentum: float = 0.1, eps: float = 1e-5,
+                  relu: bool = False, residual: Optional[torch.Tensor] = None):
+    """y = act(BN(x) + residual).  4-D x (channels_last on GPU) or 2-D [B, C].
+    momentum follows the PyTorch convention (weight of the new statistic)."""
+    C = x.shape[1]
+    if _native_ok(x) and _flat_ok(x) and (x.dim() == 2 and x.is_contiguous() or N.is_cl(x)):
+        L = N.lib()
+        R = x.numel() // C
+        dev = x.device
+        scale = torch.empty(C, dtype=torch.float32, device=dev)
+        shift = torch.empty(C, dtype=torch.float32, device=dev)
+        if training:
+            s0 = torch.zeros(2 * C, dtype=torch.float32, device=dev)
+            L.colsum(x.data_ptr(), s0.data_ptr(), s0.data_ptr() + 4 * C, R, C, N.dt(x), N.stream())
+            mean = torch.empty(C, dtype=torch.float32, device=dev)
+            invstd = torch.empty(C, dtype=torch.float32, device=dev)
+            L.bn_finalize(s0.data_ptr(), s0.data_ptr() + 4 * C, gamma.data_ptr(), beta.data_ptr(),
+                          run_mean.data_ptr(), run_var.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
+                          scale.data_ptr(), shift.data_ptr(), C, float(R), momentum, eps, N.stream())
+        else:
+            L.bn_infer_params(gamma.data_ptr(), beta.data_ptr(), run_mean.data_ptr(), run_var.data_ptr(),
+                              scale.data_ptr(), shift.data_ptr(), C, eps, N.stream())
+            mean = run_mean
+            invstd = torch.rsqrt(run_var + eps)
+        res = None
+        if residual is not None:
+            res = residual if residual.dtype == x.dtype and residual.stride() == x.stride() else \
+                _dense(residual).to(x.dtype).contiguous(memory_format=torch.channels_last if x.dim() == 4
+                                                        else torch.contiguous_format)
+        y = _like(x)
+        L.bn_apply(x.data_ptr(), scale.data_ptr(), shift.data_ptr(), N.ptr(res), y.data_ptr(), R, C, int(relu),
+                   N.dt(x), N.stream())
+        return y, BNState(mean, invstd, scale, shift)
+    # CPU reference
+    dims = (0,) if x.dim() == 2 else (0, 2, 3)
+    shp = (1, C) if x.dim() == 2 else (1, C, 1, 1)
+    xf = x.float()
+    if training:
+        mean = xf.mean(dims)
+        var = xf.var(dims, unbiased=False)
+        cnt = x.numel() // C
+        with torch.no_grad():
+            run_mean.mul_(1 - momentum).add_(momentum * mean)
+            run_var.mul_(1 - momentum).add_(momentum * var * cnt / max(cnt - 1, 1))
+    else:
+        mean, var = run_mean, run_var
+    invstd = torch.rsqrt(var + eps)
+    scale = gamma.float() * invstd
+    shift = beta.float() - mean * scale
+    y = xf * scale.reshape(shp) + shift.reshape(shp)
+    if residual is not None:
+        y = y + residual.float()
+    if relu:
+        y = torch.relu(y)
+    return y.to(x.dtype), BNState(mean, invstd, scale, shift)
+
+
+def batchnorm_bwd(x: torch.Tensor, dy: torch.Tensor, gamma: torch.Tensor, st: BNState,
+                  y_for_mask: Optional[torch.Tensor] = None, need_dres: bool = False):
+    """Returns dx, dgamma, dbeta, dres (dres = masked dy when a residual was fused)."""
+    C = x.shape[1]
+    if _native_ok(x, dy) and _flat_ok(x) and (x.dim() == 2 and x.is_contiguous() or N.is_cl(x)):
+        L = N.lib()
+        R = x.numel() // C
+        if dy.dtype != x.dtype or dy.stride() != x.stride():
+            dy = dy.to(x.dtype).contiguous(memory_format=torch.channels_last if x.dim() == 4 else
+                                           torch.contiguous_format)
+        ym = y_for_mask
+        if ym is not None and (ym.dtype != x.dtype or ym.stride() != x.stride()):
+            raise ValueError("batchnorm_bwd: mask tensor layout mismatch")
+        s = torch.zeros(2 * C, dtype=torch.float32, device=x.device)
+        L.bn_bwd_reduce(x.data_ptr(), dy.data_ptr(), N.ptr(ym), st.mean.data_ptr(), st.invstd.data_ptr(),
+                        s.data_ptr(), s.data_ptr() + 4 * C, R, C, N.dt(x), N.stream())
+        dx = _like(x)
+        dres = _like(x) if need_dres else None
+        L.bn_bwd_apply(x.data_ptr(), dy.data_ptr(), N.ptr(ym), st.mean.data_ptr(), st.invstd.data_ptr(),
+                       gamma.data_ptr(), s.data_ptr(), s.data_ptr() + 4 * C, dx.data_ptr(), N.ptr(dres), R, C,
+                       N.dt(x), N.stream())
+        return dx, s[C:], s[:C], dres
+    dims = (0,) if x.dim() == 2 else (0, 2, 3)
+    shp = (1, C) if x.dim() == 2 else (1, C, 1, 1)
+    g = dy.float()
+    if y_for_mask is not None:
+        g = g * (y_for_mask > 0)
+    xh = (x.float() - st.mean.reshape(shp)) * st.invstd.reshape(shp)
+    cnt = x.numel() // C
+    sdy = g.sum(dims)
+    sdyx = (g * xh).sum(dims)
+    dx = gamma.float().reshape(shp) * st.invstd.reshape(shp) * (g - sdy.reshape(shp) / cnt -
+                                                                  xh * sdyx.reshape(shp) / cnt)
+    return dx.to(x.dtype), sdyx, sdy, (g.to(x.dtype) if need_dres else None)
+
+
+def pool2d_fwd(x: torch.Tensor, kernel, stride, padding, is_max: bool, count_include_pad: bool = True,
+               ceil_mode: bool = False):
+    kh, kw = kernel
+    sh, sw = stride
+    ph, pw = padding
+    Nn, C, H, W = x.shape
+    if ceil_mode:
+        Ho = -(-(H + 2 * ph - kh) // sh) + 1
+        Wo = -(-(W + 2 * pw - kw) // sw) + 1
+    else:
+        Ho = (H + 2 * ph - kh) // sh + 1
+        Wo = (W + 2 * pw - kw) // sw + 1
+    if _native_ok(x) and _flat_ok(x) and N.is_cl(x):
+        y = torch.empty((Nn, C, Ho, Wo), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+        arg = torch.empty((Nn, Ho, Wo, C), dtype=torch.uint8, device=x.device) if is_max else None
+        N.lib().pool_fwd(x.data_ptr(), y.data_ptr(), N.ptr(arg), Nn, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw,
+                         int(is_max), int(count_include_pad), N.dt(x), N.stream())
+        return y, arg
+    xf = x.float()
+    if is_max:
+        y, idx = F.max_pool2d(xf, (kh, kw), (sh, sw), (ph, pw), ceil_mode=ceil_mode, return_indices=True)
+        return y.to(x.dtype), idx
+    y = F.avg_pool2d(xf, (kh, kw), (sh, sw), (ph, pw), ceil_mode=ceil_mode, count_include_pad=count_include_pad)
+    return y.to(x.dtype), None
+
+
+def pool2d_bwd(x_shape, x_like: torch.Tensor, dy: torch.Tensor, arg, kernel, stride, padding, is_max: bool,
+               count_include_pad: bool = True, ceil_mode: bool = False):
+    kh, kw = kernel
+    sh, sw = stride
+    ph, pw = padding
+    Nn, C, H, W = x_shape
+    Ho, Wo = dy.shape[2], dy.shape[3]
+    if _native_ok(dy) and _flat_ok(dy) and N.is_cl(x_like):
+        if not N.is_cl(dy):
+            dy = dy.contiguous(memory_format=torch.channels_last)
+        dx = torch.empty(x_shape, dtype=dy.dtype, device=dy.device, memory_format=torch.channels_last)
+        N.lib().pool_bwd(dy.data_ptr(), N.ptr(arg), dx.data_ptr(), Nn, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw,
+                         int(is_max), int(count_include_pad), N.dt(dy), N.stream())
+        return dx
+    g = dy.float()
+    if is_max:
+        dx = F.max_unpool2d(g, arg, (kh, kw), (sh, sw), (ph, pw), output_size=(H, W))
+        return dx.to(dy.dtype)
+    with torch.enable_grad():
+        xx = torch.zeros(x_shape, dtype=torch.float32, device=dy.device, requires_grad=True)
+        y = F.avg_pool2d(xx, (kh, kw), (sh, sw), (ph, pw), ceil_mode=ceil_mode, count_include_pad=count_include_pad)
+        (dx,) = torch.autograd.grad(y, xx, g)
+    return dx.to(dy.dtype)
+
+
+def global_avgpool_fwd(x: torch.Tensor) -> torch.Tensor:
+    Nn, C, H, W = x.shape
+    if _native_ok(x) and _flat_ok(x) and N.is_cl(x):
+        y = torch.empty((Nn, C), dtype=x.dtype, device=x.device)
+        N.lib().gap_fwd(x.data_ptr(), y.data_ptr(), Nn, H * W, C, N.dt(x), N.stream())
+        return y
+    return x.float().mean(dim=(2, 3)).to(x.dtype)
+
+
+def global_avgpool_bwd(dy: torch.Tensor, x_shape) -> torch.Tensor:
+    Nn, C, H, W = x_shape
+    if _native_ok(dy) and _flat_ok(dy) and dy.is_contiguous():
+        dx = torch.empty(x_shape, dtype=dy.dtype, device=dy.device, memory_format=torch.channels_last)
+        N.lib().gap_bwd(dy.data_ptr(), dx.data_ptr(), Nn, H * W, C, N.dt(dy), N.stream())
+        return dx
+    return (dy.float()[:, :, None, None] / (H * W)).expand(x_shape).to(dy.dtype)
+
+
+def lrn_fwd(x: torch.Tensor, size: int, alpha: float, beta: float, k: float):
+    if _native_ok(x) and _flat_ok(x) and N.is_cl(x):
+        C = x.shape[1]
+        R = x.numel() // C
+        y = _like(x)
+        norm = torch.empty(x.shape, dtype=torch.float32, device=x.device, memory_format=torch.channels_last)
+        N.lib().lrn_fwd(x.data_ptr(), y.data_ptr(), norm.data_ptr(), R, C, size, alpha, beta, k, N.dt(x),
+                        N.stream())
+        return y, norm
+    xf = x.float()
+    sq = xf * xf
+    half = size // 2
+    pad = F.pad(sq, (0, 0, 0, 0, half, half))
+    s = sum(pad[:, i:i + x.shape[1]] for i in range(size))
+    norm = k + alpha / size * s
+    return (xf * norm.pow(-beta)).to(x.dtype), norm
+
+
+def lrn_bwd(x: torch.Tensor, dy: torch.Tensor, norm: torch.Tensor, size: int, alpha: float, beta: float):
+    if _native_ok(x, dy) and _flat_ok(x) and N.is_cl(x) and N.is_cl(dy) and dy.dtype == x.dtype:
+        C = x.shape[1]
+        R = x.numel() // C
+        dx = _like(x)
+        N.lib().lrn_bwd(x.data_ptr(), dy.data_ptr(), norm.data_ptr(), dx.data_ptr(), R, C, size, alpha, beta,
+                        N.dt(x), N.stream())
+        return dx
+    xf, g = x.float(), dy.float()
+    t = g * xf * norm.pow(-beta - 1)
+    half = size // 2
+    pad = F.pad(t, (0, 0, 0, 0, half, half))
+    s = sum(pad[:, i:i + x.shape[1]] for i in range(size))
+    dx = g * norm.pow(-beta) - 2 * beta * alpha / size * xf * s
+    return dx.to(dy.dtype)

@@ -1,0 +1,81 @@
+"""Loader and thin launch helpers for the gfx950 kernel library (``_C``).
+
+The HIP path is the only GPU compute path for the ops implemented in
+``singa_amd/csrc/kernels``: if the extension cannot be imported on a machine
+with a GPU, :func:`lib` raises instead of silently falling back to PyTorch.
+On CPU-only hosts the CPU reference implementations in
+:mod:`singa_amd.ops.cpu` are used (they are the numerics oracle in tests).
+"""
+from __future__ import annotations
+
+import importlib
+import os
+
+import torch
+
+# dtype codes shared with csrc/kernels/common.h
+F32, BF16, F16, I32, I64, U8 = 0, 1, 2, 3, 4, 5
+_DT = {torch.float32: F32, torch.bfloat16: BF16, torch.float16: F16, torch.int32: I32, torch.int64: I64,
+       torch.uint8: U8}
+
+_lib = None
+_err = None
+
+
+def _load():
+    global _lib, _err
+    if _lib is not None or _err is not None:
+        return _lib
+    try:
+        _lib = importlib.import_module("singa_amd._C")
+    except Exception as e:  # pragma: no cover - reported through lib()
+        _err = e
+    return _lib
+
+
+def lib():
+    """Return the loaded ``_C`` module or raise a descriptive error."""
+    m = _load()
+    if m is None:
+        raise RuntimeError(
+            "singa_amd native kernel library (_C) is not built or failed to load: "
+            f"{_err!r}. Run `python -m singa_amd.build_ext`.")
+    return m
+
+
+def available() -> bool:
+    return _load() is not None
+
+
+def gpu_available() -> bool:
+    return torch.cuda.is_available()
+
+
+def dt(t: torch.Tensor) -> int:
+    try:
+        return _DT[t.dtype]
+    except KeyError:
+        raise TypeError(f"unsupported dtype for native kernel: {t.dtype}")
+
+
+def stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def ptr(t: torch.Tensor | None) -> int:
+    return 0 if t is None else t.data_ptr()
+
+
+def check(cond: bool, msg: str) -> None:
+    if not cond:
+        raise ValueError(msg)
+
+
+def is_cl(t: torch.Tensor) -> bool:
+    """True if a 4-D tensor is dense channels_last (NHWC memory)."""
+    return t.dim() == 4 and t.is_contiguous(memory_format=torch.channels_last)
+
+
+def force_native() -> bool:
+    """SINGA_AMD_NATIVE=0 disables the HIP path (debug only, never default)."""
+    return os.environ.get("SINGA_AMD_NATIVE", "1") != "0"

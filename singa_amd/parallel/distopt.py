@@ -1,0 +1,216 @@
+"""Synchronous data parallelism over RCCL (``torch.distributed`` backend
+"nccl" = RCCL on ROCm) with gradient buckets overlapped with backward.
+
+Reference mapping: the reference ships parameters to a ZeroMQ
+parameter server (Put/Get/kSync, src/utils/param_manager.cc:103-234).  On one
+MI355X node the PS disappears: every GPU owns a full replica in a flat
+:class:`singa_amd.opt.ParamStore`; rank 0's initial weights are broadcast
+(X2/X3 -> ncclBroadcast) and gradients are summed with all-reduce (X4).
+
+Buckets are contiguous slices of the flat fp32 gradient buffer.  Because the
+store is laid out in reverse creation order, gradients complete front to
+back during backward; as soon as every parameter overlapping a bucket is
+done, that bucket's all-reduce is launched asynchronously on RCCL's stream,
+overlapping the remaining backward kernels.  Bucket size defaults to 32 MiB:
+a ring over 8 GPUs moves each bucket in 7 xGMI-link-sized chunks of ~4 MiB,
+large enough to run near link bandwidth (§5.8 link-aware sizing), with a
+smaller first bucket so communication starts early.
+
+When the step is captured into a HIP graph (``Model(use_graph=True)``), the
+collective is NOT captured: forward+backward replay from the graph, then the
+bucketed all-reduce and the fused update run eagerly (:meth:`post_replay`).
+"""
+from __future__ import annotations
+
+import os
+from typing import List, Optional, Sequence
+
+import torch
+import torch.distributed as dist
+
+from .. import autograd
+from ..opt import Optimizer, ParamStore
+from ..tensor import Tensor
+from .communicator import Communicator, init_distributed
+
+
+class DistOpt:
+    def __init__(self, opt: Optimizer, nccl_id=None, local_rank: Optional[int] = None,
+                 world_size: Optional[int] = None, rank: Optional[int] = None, bucket_mb: float = 32.0,
+                 first_bucket_mb: float = 4.0, overlap: bool = True, comm: Optional[Communicator] = None):
+        self.opt = opt
+        self.comm = comm or init_distributed(rank=rank, world_size=world_size, local_rank=local_rank)
+        self.world_size = self.comm.world_size
+        self.global_rank = self.rank = self.comm.rank
+        self.local_rank = self.comm.local_rank
+        self.bucket_bytes = int(bucket_mb * (1 << 20))
+        self.first_bucket_bytes = int(first_bucket_mb * (1 << 20))
+        self.overlap = overlap
+        self.buckets: List[tuple] = []
+        self.graph_mode = False
+        self.defer = False
+        self.comm_ms = 0.0
+
+    # delegate optimiser attributes (lr, step_counter, store, ...)
+    def __getattr__(self, k):
+        return getattr(self.__dict__["opt"], k)
+
+    @property
+    def store(self) -> Optional[ParamStore]:
+        return self.opt.store
+
+    @property
+    def step_counter(self):
+        return self.opt.step_counter
+
+    @step_counter.setter
+    def step_counter(self, v):
+        self.opt.step_counter = v
+
+    def attach(self, params: Sequence[Tensor], mixed_bf16: bool = False) -> ParamStore:
+        st = self.opt.attach(params, mixed_bf16)
+        # rank 0's initial parameters everywhere (reference kPut/kGet bootstrap)
+        self.comm.broadcast(st.w, 0)
+        st.sync_low()
+        self._build_buckets()
+        return st
+
+    def _build_buckets(self):
+        st = self.store
+        self.buckets = []
+        start, limit = 0, self.first_bucket_bytes // 4
+        cur_params: List[int] = []
+        for i, (p, off) in enumerate(zip(st.params, st.offsets)):
+            end = off + ((p.data.numel() + 63) // 64 * 64)
+            cur_params.append(i)
+            if (end - start) >= limit or i == len(st.params) - 1:
+                self.buckets.append((start, end, list(cur_params)))
+                start, cur_params, limit = end, [], self.bucket_bytes // 4
+        self.param_bucket = {}
+        for b, (_, _, ps) in enumerate(self.buckets):
+            for i in ps:
+                self.param_bucket[id(st.params[i])] = b
+
+    def prepare_step(self):
+        self.opt.prepare_step()
+
+    def __call__(self, loss: Tensor) -> None:
+        self.backward_and_update(loss)
+
+    def backward_and_update(self, loss: Tensor, threshold: int = 0) -> None:
+        st = self.store
+        if st is None:
+            raise RuntimeError("DistOpt: parameters not attached (call model.compile first)")
+        st.zero_grad()
+        capturing = torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+        if capturing or not self.overlap or self.world_size == 1:
+            for _ in autograd.backward(loss):
+                pass
+            if capturing:
+                self.defer = True  # collective + update happen in post_replay()
+                return
+            self._allreduce_all()
+            self.opt.update(grad_scale=1.0 / self.world_size)
+            self.opt.step()
+            return
+        remaining = [len(ps) for _, _, ps in self.buckets]
+        works = []
+        for p, _ in autograd.backward(loss):
+            b = self.param_bucket.get(id(p))
+            if b is None:
+                continue
+            remaining[b] -= 1
+            if remaining[b] == 0:
+                s, e, _ = self.buckets[b]
+                works.append(self.comm.all_reduce(st.g[s:e], async_op=True))
+        for b, r in enumerate(remaining):  # params without gradients this step
+            if r > 0:
+                s, e, _ = self.buckets[b]
+                works.append(self.comm.all_reduce(st.g[s:e], async_op=True))
+        for w in works:
+            if w is not None:
+                w.wait()
+        self.opt.update(grad_scale=1.0 / self.world_size)
+        self.opt.step()
+
+    def _allreduce_all(self):
+        st = self.store
+        if self.world_size == 1:
+            return
+        works = [self.comm.all_reduce(st.g[s:e], async_op=True) for s, e, _ in self.buckets]
+        for w in works:
+            if w is not None:
+                w.wait()
+
+    def post_replay(self) -> None:
+        """After a captured forward+backward graph replay: all-reduce + update."""
+        if not self.defer:
+            return
+        self._allreduce_all()
+        self.opt.update(grad_scale=1.0 / self.world_size)
+
+    # ------------------------------------------------ SINGA DistOpt extras
+    def all_reduce(self, tensor: Tensor) -> None:
+        self.comm.all_reduce(tensor.data)
+
+    def fused_all_reduce(self, tensors: Sequence[Tensor], send: bool = True) -> None:
+        flat = torch.cat([t.data.reshape(-1).float() for t in tensors])
+        self.comm.all_reduce(flat)
+        o = 0
+        for t in tensors:
+            n = t.data.numel()
+            t.data.copy_(flat[o:o + n].reshape(t.shape).to(t.dtype))
+            o += n
+
+    def wait(self) -> None:
+        if torch.cuda.is_available():
+            torch.cuda.current_stream().synchronize()
+
+    def backward_and_partial_update(self, loss: Tensor, threshold: int = 2097152) -> None:
+        """SINGA's partial update: all-reduce a rotating window of buckets each
+        step (bounded per-step communication), local SGD for the rest."""
+        st = self.store
+        st.zero_grad()
+        for _ in autograd.backward(loss):
+            pass
+        nb = len(self.buckets)
+        k = self.opt.step_counter % max(nb, 1)
+        s, e, _ = self.buckets[k]
+        self.comm.all_reduce(st.g[s:e])
+        st.g[s:e].mul_(1.0 / self.world_size)
+        self.opt.update(grad_scale=1.0)
+        self.opt.step()
+
+    def backward_and_sparse_update(self, loss: Tensor, threshold: float = 0.01, topK: bool = False,
+                                   corr: bool = True) -> None:
+        """Sparsified gradient exchange: values with |g| >= threshold (or the
+        top threshold-fraction when topK) are summed densely via all-reduce of
+        the masked buffer; residuals are kept locally when ``corr``."""
+        st = self.store
+        st.zero_grad()
+        for _ in autograd.backward(loss):
+            pass
+        g = st.g
+        if corr:
+            if not hasattr(self, "_resid"):
+                self._resid = torch.zeros_like(g)
+            g.add_(self._resid)
+        if topK:
+            k = max(1, int(threshold * g.numel()))
+            thr = g.abs().kthvalue(g.numel() - k + 1).values
+            mask = g.abs() >= thr
+        else:
+            mask = g.abs() >= threshold
+        sparse = torch.where(mask, g, torch.zeros_like(g))
+        if corr:
+            self._resid.copy_(g - sparse)
+        g.copy_(sparse)
+        self.comm.all_reduce(g)
+        self.opt.update(grad_scale=1.0 / self.world_size)
+        self.opt.step()
+
+    def get_states(self):
+        return self.opt.get_states()
+
+    def set_states(self, s):
+        self.opt.set_states(s)

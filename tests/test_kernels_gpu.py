@@ -1,0 +1,350 @@
+"""Numerics of every hand-written gfx950 kernel against a plain PyTorch fp32
+reference of the same op (run on the MI355X box: ``pytest -m gpu``)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as TF
+
+pytestmark = pytest.mark.gpu
+
+
+def rel_err(a, b):
+    a, b = a.float().cpu(), b.float().cpu()
+    return float((a - b).norm() / (b.norm() + 1e-12))
+
+
+def bf(x):
+    return x.to(torch.bfloat16)
+
+
+# --------------------------------------------------------------------- GEMM
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (256, 512, 384), (100, 72, 40), (1000, 2048, 512),
+                                   (7, 8, 16), (333, 256, 1024)])
+@pytest.mark.parametrize("ako,bko", [(0, 0), (0, 1), (1, 0), (1, 1)])
+def test_gemm_orientations(gpu, M, N, K, ako, bko):
+    from singa_amd.ops import native as NT
+    if (ako and M % 8) or (bko and N % 8):
+        pytest.skip("K-outer operands need rows % 8 == 0")
+    g = torch.Generator(device="cpu").manual_seed(0)
+    A = torch.randn(M, K, generator=g)
+    B = torch.randn(N, K, generator=g)
+    a = bf(A.t().contiguous() if ako else A).to(gpu)
+    b = bf(B.t().contiguous() if bko else B).to(gpu)
+    c = torch.empty(M, N, dtype=torch.float32, device=gpu)
+    lda = M if ako else K
+    ldb = N if bko else K
+    NT.lib().gemm(a.data_ptr(), lda, ako, b.data_ptr(), ldb, bko, c.data_ptr(), N, M, N, K, 1.0, 0.0, 0, 0, 1, 1,
+                  1, 0, 0, 0, NT.stream())
+    ref = bf(A).float() @ bf(B).float().t()
+    assert rel_err(c, ref) < 1e-5
+
+
+def test_gemm_asymmetric_identity(gpu):
+    """A = I with an asymmetric B catches transposed epilogue writes."""
+    from singa_amd.ops import functional as F
+    n = 128
+    A = torch.eye(n)
+    B = torch.arange(n * n, dtype=torch.float32).reshape(n, n) % 97 - 48
+    c = F.matmul(bf(A).to(gpu), bf(B).to(gpu), out_dtype=torch.float32)
+    assert torch.equal(c.cpu(), bf(B).float())
+
+
+def test_gemm_bias_relu_bf16_out_batched(gpu):
+    from singa_amd.ops import functional as F
+    g = torch.Generator().manual_seed(1)
+    a = torch.randn(3, 200, 64, generator=g)
+    b = torch.randn(3, 64, 136, generator=g)
+    out = F.matmul(bf(a).to(gpu), bf(b).to(gpu), out_dtype=torch.bfloat16)
+    ref = bf(a).float() @ bf(b).float()
+    assert rel_err(out, ref) < 8e-3
+    a2, b2 = torch.randn(64, 96, generator=g), torch.randn(96, 256, generator=g)
+    bias = torch.randn(256, generator=g)
+    out2 = F.matmul(bf(a2).to(gpu), bf(b2).to(gpu), out_dtype=torch.float32, bias=bias.to(gpu), relu=True)
+    ref2 = torch.relu(bf(a2).float() @ bf(b2).float() + bias)
+    assert rel_err(out2, ref2) < 1e-5
+
+
+def test_gemm_splitk_atomic(gpu):
+    from singa_amd.ops import functional as F
+    g = torch.Generator().manual_seed(2)
+    a = torch.randn(4096, 64, generator=g)  # [K, M]
+    b = torch.randn(4096, 96, generator=g)  # [K, N]
+    out = torch.zeros(64, 96, device=gpu)
+    F.gemm_tn_acc(bf(a).to(gpu), bf(b).to(gpu), out)
+    ref = bf(a).float().t() @ bf(b).float()
+    assert rel_err(out, ref) < 1e-5
+
+
+# --------------------------------------------------------------- convolution
+CONV_CASES = [
+    # N, C, H, W, K, R, S, stride, pad
+    (2, 64, 14, 14, 64, 1, 1, 1, 0),
+    (2, 64, 14, 14, 128, 3, 3, 1, 1),
+    (2, 64, 15, 15, 128, 3, 3, 2, 1),
+    (2, 128, 14, 14, 256, 1, 1, 2, 0),
+    (2, 3, 32, 32, 64, 7, 7, 2, 3),     # stem, C padded to 8
+    (3, 20, 12, 12, 50, 5, 5, 1, 0),    # LeNet conv2: C and K not multiples of 8
+    (2, 32, 9, 11, 40, 3, 3, 1, 2),
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_fwd_bwd(gpu, case):
+    from singa_amd.ops import functional as F
+    N_, C, H, W, K, R, S, st, pd = case
+    g = torch.Generator().manual_seed(3)
+    x = bf(torch.randn(N_, C, H, W, generator=g)).float()
+    w = bf(torch.randn(K, C, R, S, generator=g) * (1.0 / math.sqrt(C * R * S))).float()
+    xr = x.clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    yr = TF.conv2d(xr, wr, None, st, pd)
+    dy = bf(torch.randn(yr.shape, generator=g)).float()
+    yr.backward(dy)
+    xg = x.to(gpu).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    wg = w.to(gpu)
+    y = F.conv2d_fwd(xg, wg, None, (st, st), (pd, pd), out_dtype=torch.float32)
+    assert y.shape == yr.shape
+    assert rel_err(y, yr.detach()) < 1e-5
+    dyg = dy.to(gpu).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    dw_acc = torch.zeros(K, C, R, S, device=gpu)
+    dx, dw, db = F.conv2d_bwd(xg.float().contiguous(memory_format=torch.channels_last), wg, dyg, (st, st),
+                              (pd, pd), need_dx=True, dw_out=dw_acc, need_db=True)
+    assert rel_err(dx, xr.grad) < 1e-5
+    assert rel_err(dw_acc, wr.grad) < 1e-5
+    assert rel_err(db, dy.sum((0, 2, 3))) < 1e-5
+
+
+def test_conv_bias_relu_fused(gpu):
+    from singa_amd.ops import functional as F
+    g = torch.Generator().manual_seed(4)
+    x = bf(torch.randn(2, 16, 10, 10, generator=g)).float()
+    w = bf(torch.randn(24, 16, 3, 3, generator=g) * 0.1).float()
+    b = torch.randn(24, generator=g)
+    y = F.conv2d_fwd(x.to(gpu), w.to(gpu), b.to(gpu), (1, 1), (1, 1), relu=True)
+    ref = torch.relu(TF.conv2d(x, w, b, 1, 1))
+    assert rel_err(y, ref) < 1e-5
+
+
+# --------------------------------------------------------------- batch norm
+@pytest.mark.parametrize("C", [64, 20, 256])
+@pytest.mark.parametrize("relu,residual", [(False, False), (True, False), (True, True)])
+def test_batchnorm(gpu, C, relu, residual):
+    from singa_amd.ops import functional as F
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(4, C, 7, 9, generator=g) * 2 + 0.5
+    gam = torch.rand(C, generator=g) + 0.5
+    bet = torch.randn(C, generator=g)
+    res = torch.randn(4, C, 7, 9, generator=g) if residual else None
+    dy = torch.randn(4, C, 7, 9, generator=g)
+    # reference
+    xr = x.clone().requires_grad_(True)
+    gr, br = gam.clone().requires_grad_(True), bet.clone().requires_grad_(True)
+    rr = res.clone().requires_grad_(True) if residual else None
+    rm, rv = torch.zeros(C), torch.ones(C)
+    yr = TF.batch_norm(xr, rm, rv, gr, br, True, 0.1, 1e-5)
+    if residual:
+        yr = yr + rr
+    if relu:
+        yr = torch.relu(yr)
+    yr.backward(dy)
+    cl = lambda t: t.to(gpu).contiguous(memory_format=torch.channels_last)  # noqa: E731
+    rmg, rvg = torch.zeros(C, device=gpu), torch.ones(C, device=gpu)
+    y, st = F.batchnorm_fwd(cl(x), gam.to(gpu), bet.to(gpu), rmg, rvg, True, 0.1, 1e-5, relu,
+                            cl(res) if residual else None)
+    assert rel_err(y, yr.detach()) < 1e-5
+    assert rel_err(rmg, rm) < 1e-5 and rel_err(rvg, rv) < 1e-5
+    dx, dg, dbt, dres = F.batchnorm_bwd(cl(x), cl(dy), gam.to(gpu), st, y if relu else None, need_dres=residual)
+    assert rel_err(dx, xr.grad) < 1e-4
+    assert rel_err(dg, gr.grad) < 1e-4
+    assert rel_err(dbt, br.grad) < 1e-4
+    if residual:
+        assert rel_err(dres, rr.grad) < 1e-5
+
+
+def test_batchnorm_bf16(gpu):
+    from singa_amd.ops import functional as F
+    g = torch.Generator().manual_seed(6)
+    C = 128
+    x = bf(torch.randn(8, C, 14, 14, generator=g))
+    gam, bet = torch.rand(C, generator=g) + 0.5, torch.randn(C, generator=g)
+    rm, rv = torch.zeros(C), torch.ones(C)
+    yr = torch.relu(TF.batch_norm(x.float(), rm, rv, gam, bet, True, 0.1, 1e-5))
+    y, _ = F.batchnorm_fwd(x.to(gpu).contiguous(memory_format=torch.channels_last), gam.to(gpu), bet.to(gpu),
+                           torch.zeros(C, device=gpu), torch.ones(C, device=gpu), True, relu=True)
+    assert y.dtype == torch.bfloat16
+    assert rel_err(y, yr) < 1e-2
+
+
+# ------------------------------------------------------------------ pooling
+@pytest.mark.parametrize("is_max", [True, False])
+@pytest.mark.parametrize("k,s,p", [(3, 2, 1), (2, 2, 0), (3, 1, 1)])
+def test_pool(gpu, is_max, k, s, p):
+    from singa_amd.ops import functional as F
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(2, 16, 13, 11, generator=g)
+    xr = x.clone().requires_grad_(True)
+    yr = TF.max_pool2d(xr, k, s, p) if is_max else TF.avg_pool2d(xr, k, s, p, count_include_pad=True)
+    dy = torch.randn(yr.shape, generator=g)
+    yr.backward(dy)
+    xg = x.to(gpu).contiguous(memory_format=torch.channels_last)
+    y, arg = F.pool2d_fwd(xg, (k, k), (s, s), (p, p), is_max)
+    assert rel_err(y, yr.detach()) < 1e-6
+    dx = F.pool2d_bwd(xg.shape, xg, dy.to(gpu).contiguous(memory_format=torch.channels_last), arg, (k, k), (s, s),
+                      (p, p), is_max)
+    assert rel_err(dx, xr.grad) < 1e-6
+
+
+def test_global_avgpool(gpu):
+    from singa_amd.ops import functional as F
+    x = torch.randn(4, 64, 7, 7)
+    y = F.global_avgpool_fwd(x.to(gpu).contiguous(memory_format=torch.channels_last))
+    assert rel_err(y, x.mean((2, 3))) < 1e-6
+    dy = torch.randn(4, 64)
+    dx = F.global_avgpool_bwd(dy.to(gpu), x.shape)
+    assert rel_err(dx, (dy[:, :, None, None] / 49).expand_as(x)) < 1e-6
+
+
+def test_lrn(gpu):
+    from singa_amd.ops import functional as F
+    x = torch.randn(2, 16, 5, 5)
+    y_ref, norm_ref = F.lrn_fwd(x, 5, 1e-2, 0.75, 2.0)
+    dy = torch.randn(2, 16, 5, 5)
+    dx_ref = F.lrn_bwd(x, dy, norm_ref, 5, 1e-2, 0.75)
+    # torch oracle for the forward
+    tref = TF.local_response_norm(x, 5, 1e-2, 0.75, 2.0)
+    assert rel_err(y_ref, tref) < 1e-5
+    cl = lambda t: t.to(gpu).contiguous(memory_format=torch.channels_last)  # noqa: E731
+    y, norm = F.lrn_fwd(cl(x), 5, 1e-2, 0.75, 2.0)
+    assert rel_err(y, y_ref) < 1e-5
+    dx = F.lrn_bwd(cl(x), cl(dy), norm, 5, 1e-2, 0.75)
+    assert rel_err(dx, dx_ref) < 1e-5
+
+
+# ------------------------------------------------------- softmax / losses
+@pytest.mark.parametrize("C", [10, 1000, 3000])
+def test_softmax_xent(gpu, C):
+    from singa_amd.ops import functional as F
+    g = torch.Generator().manual_seed(8)
+    x = torch.randn(33, C, generator=g) * 3
+    lab = torch.randint(0, C, (33,), generator=g)
+    loss, correct, dx = F.softmax_xent(x.to(gpu), lab.to(gpu), topk=5)
+    xr = x.clone().requires_grad_(True)
+    l = TF.cross_entropy(xr, lab)
+    l.backward()
+    assert abs(float(loss.mean()) - float(l)) < 1e-5
+    assert rel_err(dx, xr.grad) < 1e-5
+    top5 = (x.topk(5, 1).indices == lab[:, None]).any(1).float()
+    assert torch.equal(correct.cpu(), top5)
+    y = F.softmax(x.to(gpu))
+    assert rel_err(y, torch.softmax(x, 1)) < 1e-6
+    dyy = torch.randn(33, C, generator=g)
+    d = F.softmax_bwd(y, dyy.to(gpu))
+    sr = torch.softmax(x, 1)
+    assert rel_err(d, sr * (dyy - (dyy * sr).sum(1, keepdim=True))) < 1e-5
+
+
+def test_layernorm(gpu):
+    from singa_amd.ops import functional as F
+    g = torch.Generator().manual_seed(9)
+    x = torch.randn(64, 768, generator=g)
+    gm, bt = torch.rand(768, generator=g) + 0.5, torch.randn(768, generator=g)
+    dy = torch.randn(64, 768, generator=g)
+    xr, gr, br = x.clone().requires_grad_(True), gm.clone().requires_grad_(True), bt.clone().requires_grad_(True)
+    yr = TF.layer_norm(xr, (768,), gr, br, 1e-5)
+    yr.backward(dy)
+    y, mu, rs = F.layernorm_fwd(x.to(gpu), gm.to(gpu), bt.to(gpu))
+    assert rel_err(y, yr.detach()) < 1e-5
+    dx, dg, db = F.layernorm_bwd(x.to(gpu), dy.to(gpu), gm.to(gpu), mu, rs)
+    assert rel_err(dx, xr.grad) < 1e-4 and rel_err(dg, gr.grad) < 1e-4 and rel_err(db, br.grad) < 1e-4
+
+
+@pytest.mark.parametrize("op", ["relu", "sigmoid", "tanh", "stanh", "gelu", "softplus", "exp", "abs", "square",
+                                "leakyrelu", "elu", "selu"])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_unary(gpu, op, dtype):
+    from singa_amd.ops import functional as F
+    x = torch.randn(1003) * 2
+    alpha = 0.1 if op in ("leakyrelu",) else (1.0 if op == "elu" else 0.0)
+    y_ref = F.unary(op, x.to(dtype).float(), alpha)
+    y = F.unary(op, x.to(dtype).to(gpu), alpha)
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert rel_err(y, y_ref) < tol
+    dy = torch.randn(1003)
+    d_ref = F.unary_bwd(op, x.to(dtype).float(), y_ref, dy.to(dtype).float(), alpha)
+    d = F.unary_bwd(op, x.to(dtype).to(gpu), y, dy.to(dtype).to(gpu), alpha)
+    assert rel_err(d, d_ref) < (1e-4 if dtype == torch.float32 else 2e-2)
+
+
+def test_add_relu_and_cast(gpu):
+    from singa_amd.ops import functional as F
+    a, b = torch.randn(4, 8, 5, 5), torch.randn(4, 8, 5, 5)
+    cl = lambda t: t.to(gpu).contiguous(memory_format=torch.channels_last)  # noqa: E731
+    y = F.add_act(cl(a), cl(b), relu=True)
+    assert y.is_contiguous(memory_format=torch.channels_last)
+    assert rel_err(y, torch.relu(a + b)) < 1e-7
+    c = F.cast(cl(a), torch.bfloat16)
+    assert c.dtype == torch.bfloat16 and rel_err(c, a) < 1e-2
+
+
+def test_dropout(gpu):
+    from singa_amd.ops import functional as F
+    x = torch.ones(100000, device=gpu)
+    y, mask = F.dropout_fwd(x, 0.3, 42, 0)
+    keep = float(mask.float().mean())
+    assert abs(keep - 0.7) < 0.01
+    assert torch.allclose(y[mask.bool()], torch.full_like(y[mask.bool()], 1 / 0.7))
+    dx = F.dropout_bwd(torch.ones_like(x), mask, 0.3)
+    assert torch.equal(dx, y)
+    y2, m2 = F.dropout_fwd(x, 0.3, 42, 0)
+    assert torch.equal(mask, m2)  # reproducible per (seed, offset)
+
+
+# ----------------------------------------------------------------- optimiser
+@pytest.mark.parametrize("cls,kw", [("SGD", dict(lr=0.1, momentum=0.9, weight_decay=1e-4)),
+                                    ("SGD", dict(lr=0.1, momentum=0.9, nesterov=True)),
+                                    ("Adam", dict(lr=1e-3, weight_decay=1e-2)),
+                                    ("AdamW", dict(lr=1e-3)),
+                                    ("AdaGrad", dict(lr=0.1)), ("RMSProp", dict(lr=0.01)),
+                                    ("AdaDelta", dict(lr=1.0)), ("RefSGD", dict(lr=0.1, momentum=0.9)),
+                                    ("Nesterov", dict(lr=0.1, momentum=0.9))])
+def test_fused_optimizer_matches_cpu(gpu, cls, kw):
+    from singa_amd import opt as O
+    from singa_amd.tensor import Tensor
+    g = torch.Generator().manual_seed(10)
+    shapes = [(64, 3, 3, 3), (64,), (200, 10)]
+    init = [torch.randn(s, generator=g) for s in shapes]
+    grads = [[torch.randn(s, generator=g) for s in shapes] for _ in range(3)]
+    outs = []
+    for dev in ("cpu", gpu):
+        ps = []
+        for i, t in enumerate(init):
+            p = Tensor(data=t.clone().to(dev), stores_grad=True)
+            p.param_meta = {"lr_mult": 1.0 if i != 1 else 2.0, "wd_mult": 1.0 if i != 1 else 0.0}
+            ps.append(p)
+        o = getattr(O, cls)(**kw)
+        o.attach(ps)
+        for step in grads:
+            for p, gg in zip(ps, step):
+                p.grad_view.copy_(gg.to(dev))
+            o.update()
+            o.step()
+        outs.append([p.data.detach().float().cpu().clone() for p in ps])
+    for a, b in zip(*outs):
+        assert rel_err(b, a) < 1e-5
+
+
+def test_easgd_and_rsync_kernels(gpu):
+    from singa_amd.ops import native as NT
+    w = torch.randn(1000, device=gpu)
+    c = torch.randn(1000, device=gpu)
+    w0 = w.clone()
+    d = torch.empty_like(w)
+    NT.lib().easgd_diff(w.data_ptr(), c.data_ptr(), d.data_ptr(), 1000, 0.25, NT.stream())
+    assert rel_err(d, 0.25 * (w0 - c)) < 1e-6 and rel_err(w, w0 - 0.25 * (w0 - c)) < 1e-6
+    snap = torch.randn(1000, device=gpu)
+    out = torch.empty(100, device=gpu)
+    NT.lib().rsync_gather(w.data_ptr(), snap.data_ptr(), out.data_ptr(), 100, 1000, 7, 13, NT.stream())
+    idx = (13 + torch.arange(100) * 7) % 1000
+    assert rel_err(out, (w - snap)[idx.to(gpu)]) < 1e-6
