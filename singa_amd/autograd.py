@@ -516,10 +516,11 @@ class Linear(Operator):
         res = [dx, dw]
         if self.has_bias:
             tb = self.grad_target(2)
-            db = F.colsum(dy2)[0] if dy2.is_cuda else dy2.float().sum(0)
             if tb is not None:
-                tb.add_(db)
+                F.colsum(dy2, out=tb)
                 db = ACCUMULATED
+            else:
+                db = F.colsum(dy2)[0]
             res.append(db)
         return tuple(res)
 
@@ -565,7 +566,9 @@ class Conv2d(Operator):
 
 class BatchNorm2d(Operator):
     """Batch normalisation (+ optional fused ReLU and residual add).
-    Inputs: x, gamma, beta[, residual].  Running stats are updated in place."""
+    Inputs: x, gamma, beta[, residual].  Running stats are updated in place.
+    dgamma/dbeta are accumulated by the kernel straight into the flat
+    gradient buffer when the params live in a ParamStore."""
 
     def __init__(self, running_mean: torch.Tensor, running_var: torch.Tensor, momentum: float = 0.1,
                  eps: float = 1e-5, relu: bool = False, has_residual: bool = False, name=None):
@@ -579,20 +582,16 @@ class BatchNorm2d(Operator):
                                 res)
         if self.requires_grad:
             self.x, self.gamma, self.st = x, gamma, st
-            self.y = y if (self.relu) else None
+            # the fused output is needed as the ReLU mask only when a residual was added
+            self.y = y if (self.relu and self.has_residual) else None
         return y
 
     def backward(self, dy):
-        dx, dg, db, dres = F.batchnorm_bwd(self.x, dy, self.gamma, self.st, self.y, need_dres=self.has_residual)
+        tg, tb = self.grad_target(1), self.grad_target(2)
+        dx, dg, db, dres = F.batchnorm_bwd(self.x, dy, self.gamma, self.st, self.y, need_dres=self.has_residual,
+                                           relu=self.relu, dg_out=tg, db_out=tb)
         self.x = self.y = self.st = None
-        out = [dx]
-        for i, g in ((1, dg), (2, db)):
-            t = self.grad_target(i)
-            if t is not None:
-                t.add_(g)
-                out.append(ACCUMULATED)
-            else:
-                out.append(g)
+        out = [dx, ACCUMULATED if tg is not None else dg, ACCUMULATED if tb is not None else db]
         if self.has_residual:
             out.append(dres)
         return tuple(out)

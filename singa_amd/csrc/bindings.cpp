@@ -36,15 +36,15 @@ void sg_layernorm_fwd(const void*, const void*, const void*, void*, void*, void*
                       hipStream_t);
 void sg_layernorm_bwd(const void*, const void*, const void*, const void*, const void*, void*, void*, void*, int64_t,
                       int, int, hipStream_t);
-void sg_colsum(const void*, void*, void*, int64_t, int, int, hipStream_t);
-void sg_bn_bwd_reduce(const void*, const void*, const void*, const void*, const void*, void*, void*, int64_t, int,
-                      int, hipStream_t);
-void sg_bn_finalize(const void*, const void*, const void*, const void*, void*, void*, void*, void*, void*, void*, int,
-                    float, float, float, hipStream_t);
-void sg_bn_infer_params(const void*, const void*, const void*, const void*, void*, void*, int, float, hipStream_t);
+int sg_colreduce_bands(int64_t, int);
+void sg_colsum(const void*, void*, void*, void*, int64_t, int, int, int, hipStream_t);
+void sg_bn_fwd_stats(const void*, void*, const void*, const void*, void*, void*, void*, void*, void*, void*, int64_t,
+                     int, float, float, int, hipStream_t);
+void sg_bn_infer_params(const void*, const void*, const void*, const void*, void*, void*, void*, void*, int, float,
+                        hipStream_t);
 void sg_bn_apply(const void*, const void*, const void*, const void*, void*, int64_t, int, int, int, hipStream_t);
-void sg_bn_bwd_apply(const void*, const void*, const void*, const void*, const void*, const void*, const void*,
-                     const void*, void*, void*, int64_t, int, int, hipStream_t);
+void sg_bn_bwd(const void*, const void*, const void*, const void*, const void*, const void*, const void*, const void*,
+               void*, void*, void*, void*, void*, void*, int64_t, int, int, int, hipStream_t);
 void sg_pool_fwd(const void*, void*, void*, int, int, int, int, int, int, int, int, int, int, int, int, int, int, int,
                  hipStream_t);
 void sg_pool_bwd(const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int, int, int,
@@ -69,7 +69,6 @@ void sg_conv_dgrad(const void*, const void*, void*, int, int, int, int, int, int
                    int, int, int, hipStream_t);
 void sg_conv_wgrad(const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int, int,
                    int, int, int, hipStream_t);
-void sg_wt_transpose(const void*, void*, int, int, int, hipStream_t);
 }
 
 static void check_launch(const char* what) {
@@ -146,30 +145,28 @@ PYBIND11_MODULE(_C, m) {
     sg_layernorm_bwd(CV(x), CV(dy), CV(g), CV(mean), CV(rstd), V(dx), V(dg), V(db), R, D, dt, S(s));
     CHK("layernorm_bwd");
   });
-  m.def("colsum", [](P x, P o0, P o1, int64_t R, int C, int dt, P s) {
-    sg_colsum(CV(x), V(o0), V(o1), R, C, dt, S(s)); CHK("colsum");
+  m.def("colreduce_bands", [](int64_t R, int C) { return sg_colreduce_bands(R, C); });
+  m.def("colsum", [](P x, P ws, P o0, P o1, int64_t R, int C, int dt, int acc, P s) {
+    sg_colsum(CV(x), V(ws), V(o0), V(o1), R, C, dt, acc, S(s)); CHK("colsum");
   });
-  m.def("bn_bwd_reduce", [](P x, P dy, P y, P mean, P invstd, P sdy, P sdyx, int64_t R, int C, int dt, P s) {
-    sg_bn_bwd_reduce(CV(x), CV(dy), CV(y), CV(mean), CV(invstd), V(sdy), V(sdyx), R, C, dt, S(s));
-    CHK("bn_bwd_reduce");
+  m.def("bn_fwd_stats", [](P x, P ws, P gamma, P beta, P rm, P rv, P mean, P invstd, P scale, P shift, int64_t R,
+                           int C, float mom, float eps, int dt, P s) {
+    sg_bn_fwd_stats(CV(x), V(ws), CV(gamma), CV(beta), V(rm), V(rv), V(mean), V(invstd), V(scale), V(shift), R, C,
+                    mom, eps, dt, S(s));
+    CHK("bn_fwd_stats");
   });
-  m.def("bn_finalize", [](P sum, P sumsq, P gamma, P beta, P rm, P rv, P mean, P invstd, P scale, P shift, int C,
-                          float count, float mom, float eps, P s) {
-    sg_bn_finalize(CV(sum), CV(sumsq), CV(gamma), CV(beta), V(rm), V(rv), V(mean), V(invstd), V(scale), V(shift), C,
-                   count, mom, eps, S(s));
-    CHK("bn_finalize");
-  });
-  m.def("bn_infer_params", [](P g, P b, P rm, P rv, P scale, P shift, int C, float eps, P s) {
-    sg_bn_infer_params(CV(g), CV(b), CV(rm), CV(rv), V(scale), V(shift), C, eps, S(s)); CHK("bn_infer_params");
+  m.def("bn_infer_params", [](P g, P b, P rm, P rv, P scale, P shift, P mean, P invstd, int C, float eps, P s) {
+    sg_bn_infer_params(CV(g), CV(b), CV(rm), CV(rv), V(scale), V(shift), V(mean), V(invstd), C, eps, S(s));
+    CHK("bn_infer_params");
   });
   m.def("bn_apply", [](P x, P scale, P shift, P res, P y, int64_t R, int C, int relu, int dt, P s) {
     sg_bn_apply(CV(x), CV(scale), CV(shift), CV(res), V(y), R, C, relu, dt, S(s)); CHK("bn_apply");
   });
-  m.def("bn_bwd_apply", [](P x, P dy, P y, P mean, P invstd, P gamma, P sdy, P sdyx, P dx, P dres, int64_t R, int C,
-                           int dt, P s) {
-    sg_bn_bwd_apply(CV(x), CV(dy), CV(y), CV(mean), CV(invstd), CV(gamma), CV(sdy), CV(sdyx), V(dx), V(dres), R, C,
-                    dt, S(s));
-    CHK("bn_bwd_apply");
+  m.def("bn_bwd", [](P x, P dy, P y, P scale, P shift, P mean, P invstd, P gamma, P ws, P coef, P dg, P db, P dx,
+                     P dres, int64_t R, int C, int mask_mode, int dt, P s) {
+    sg_bn_bwd(CV(x), CV(dy), CV(y), CV(scale), CV(shift), CV(mean), CV(invstd), CV(gamma), V(ws), V(coef), V(dg),
+              V(db), V(dx), V(dres), R, C, mask_mode, dt, S(s));
+    CHK("bn_bwd");
   });
   m.def("pool_fwd", [](P x, P y, P arg, int N, int H, int W, int C, int Ho, int Wo, int kh, int kw, int sh, int sw,
                        int ph, int pw, int is_max, int cp, int dt, P s) {
@@ -233,8 +230,5 @@ PYBIND11_MODULE(_C, m) {
                          int sh, int sw, int ph, int pw, int dh, int dw, int splits, P s) {
     sg_conv_wgrad(CV(x), CV(dy), V(dw_out), N, H, W, C, K, R, Sd, Ho, Wo, sh, sw, ph, pw, dh, dw, splits, S(s));
     CHK("conv_wgrad");
-  });
-  m.def("wt_transpose", [](P w, P wt, int K, int RS, int C, P s) {
-    sg_wt_transpose(CV(w), V(wt), K, RS, C, S(s)); CHK("wt_transpose");
   });
 }

@@ -1,0 +1,438 @@
+// BatchNorm2d (NHWC / [R][C] rows) and per-channel column reductions.
+//
+// Design for MI355X (HBM-bound ops, every byte counts):
+//  * Reductions are two-stage: each workgroup reduces a band of rows for its
+//    channel slice in registers + LDS and writes ONE partial per channel to a
+//    slab ws[band][2][C] with plain stores; a per-channel finalize kernel sums
+//    the bands.  (A first version ended every workgroup with float atomics on
+//    the same 64..2048 channel addresses: thousands of contended adds per
+//    line serialised at the memory side and ran 20x below HBM bandwidth.)
+//  * Thread mapping is 2-D: a thread owns a fixed 8-channel (16-byte) slice
+//    and walks rows, so per-channel coefficients are loaded once into
+//    registers and no per-element channel index math (64-bit modulo) is done.
+//  * The backward finalize turns (sum dy, sum dy*xhat) into three per-channel
+//    coefficients so the apply pass is dx = k*g + b*x + a, and accumulates
+//    dgamma/dbeta straight into the flat fp32 gradient buffer.
+//  * With fused BN+ReLU (no residual) the ReLU mask is recomputed from
+//    x*scale+shift instead of re-reading the output (one HBM pass fewer).
+//
+// Reference: per-channel bias-gradient reduction K4 (include/mshadow/cuda/
+// tensor_gpu-inl.cuh:135-168) and F2 (src/worker/layer.cc:107); BatchNorm
+// itself is a north-star addition (not in the reference).
+#include "common.h"
+
+namespace sg {
+
+enum MaskMode : int { MASK_NONE = 0, MASK_Y = 1, MASK_AFFINE = 2 };
+
+struct Tile2D {
+  int CT, RT, tx, ty, c0;
+  bool cok;
+};
+template <int V>
+__device__ __forceinline__ Tile2D tile2d(int C) {
+  Tile2D t;
+  const int chunks = C / V;
+  t.CT = chunks < 64 ? chunks : 64;
+  t.RT = blockDim.x / t.CT;
+  t.tx = threadIdx.x % t.CT;
+  t.ty = threadIdx.x / t.CT;
+  t.c0 = (blockIdx.y * t.CT + t.tx) * V;
+  t.cok = t.ty < t.RT && t.c0 < C;
+  return t;
+}
+
+// ---------------------------------------------------------------------------
+// Stage 1: per-band partial column sums.
+//   MODE 0: p0 = sum x, p1 = sum x^2
+//   MODE 1: g = dy (masked), xh = (x-mean)*invstd: p0 = sum g, p1 = sum g*xh
+// ws layout: [band][2][C] fp32
+// ---------------------------------------------------------------------------
+template <typename T, int MODE, int V>
+__global__ void __launch_bounds__(256) colpart_k(const T* __restrict__ x, const T* __restrict__ dy,
+                                                 const T* __restrict__ y, const float* __restrict__ scale,
+                                                 const float* __restrict__ shift, const float* __restrict__ mean,
+                                                 const float* __restrict__ invstd, float* __restrict__ ws, int64_t R,
+                                                 int C, int rows_per_band, int mask_mode) {
+  __shared__ float red[256 * V];
+  const Tile2D t = tile2d<V>(C);
+  float a0[V], a1[V];
+#pragma unroll
+  for (int i = 0; i < V; ++i) { a0[i] = 0.f; a1[i] = 0.f; }
+  float mu[V], is[V], sc[V], sf[V];
+  if (MODE == 1 && t.cok) {
+    ldc<V>(mean + t.c0, mu);
+    ldc<V>(invstd + t.c0, is);
+    if (mask_mode == MASK_AFFINE) {
+      ldc<V>(scale + t.c0, sc);
+      ldc<V>(shift + t.c0, sf);
+    }
+  }
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_band;
+  const int64_t r1 = min(R, r0 + rows_per_band);
+  if (t.cok) {
+    int64_t r = r0 + t.ty;
+    // two rows per iteration keeps two independent 16-B loads per stream in flight
+    for (; r + t.RT < r1; r += 2 * t.RT) {
+      float v0[V], v1[V];
+      ldv<T, V>(x + r * C + t.c0, v0);
+      ldv<T, V>(x + (r + t.RT) * C + t.c0, v1);
+      if (MODE == 0) {
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+          a0[i] += v0[i] + v1[i];
+          a1[i] += v0[i] * v0[i] + v1[i] * v1[i];
+        }
+      } else {
+        float g0[V], g1[V];
+        ldv<T, V>(dy + r * C + t.c0, g0);
+        ldv<T, V>(dy + (r + t.RT) * C + t.c0, g1);
+        if (mask_mode == MASK_Y) {
+          float y0[V], y1[V];
+          ldv<T, V>(y + r * C + t.c0, y0);
+          ldv<T, V>(y + (r + t.RT) * C + t.c0, y1);
+#pragma unroll
+          for (int i = 0; i < V; ++i) {
+            g0[i] = y0[i] > 0.f ? g0[i] : 0.f;
+            g1[i] = y1[i] > 0.f ? g1[i] : 0.f;
+          }
+        } else if (mask_mode == MASK_AFFINE) {
+#pragma unroll
+          for (int i = 0; i < V; ++i) {
+            g0[i] = v0[i] * sc[i] + sf[i] > 0.f ? g0[i] : 0.f;
+            g1[i] = v1[i] * sc[i] + sf[i] > 0.f ? g1[i] : 0.f;
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+          a0[i] += g0[i] + g1[i];
+          a1[i] += g0[i] * (v0[i] - mu[i]) * is[i] + g1[i] * (v1[i] - mu[i]) * is[i];
+        }
+      }
+    }
+    for (; r < r1; r += t.RT) {
+      float v0[V];
+      ldv<T, V>(x + r * C + t.c0, v0);
+      if (MODE == 0) {
+#pragma unroll
+        for (int i = 0; i < V; ++i) { a0[i] += v0[i]; a1[i] += v0[i] * v0[i]; }
+      } else {
+        float g0[V];
+        ldv<T, V>(dy + r * C + t.c0, g0);
+        if (mask_mode == MASK_Y) {
+          float y0[V];
+          ldv<T, V>(y + r * C + t.c0, y0);
+#pragma unroll
+          for (int i = 0; i < V; ++i) g0[i] = y0[i] > 0.f ? g0[i] : 0.f;
+        } else if (mask_mode == MASK_AFFINE) {
+#pragma unroll
+          for (int i = 0; i < V; ++i) g0[i] = v0[i] * sc[i] + sf[i] > 0.f ? g0[i] : 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < V; ++i) { a0[i] += g0[i]; a1[i] += g0[i] * (v0[i] - mu[i]) * is[i]; }
+      }
+    }
+  }
+  // reduce over ty in LDS, then one plain store per channel per band
+  float* out = ws + (int64_t)blockIdx.x * 2 * C;
+  for (int pass = 0; pass < 2; ++pass) {
+    const float* acc = pass == 0 ? a0 : a1;
+    __syncthreads();
+    if (t.ty < t.RT) {
+#pragma unroll
+      for (int i = 0; i < V; ++i) red[threadIdx.x * V + i] = acc[i];
+    }
+    __syncthreads();
+    if (t.ty == 0 && t.c0 < C) {
+      float s[V];
+#pragma unroll
+      for (int i = 0; i < V; ++i) s[i] = red[t.tx * V + i];
+      for (int k = 1; k < t.RT; ++k) {
+#pragma unroll
+        for (int i = 0; i < V; ++i) s[i] += red[(k * t.CT + t.tx) * V + i];
+      }
+#pragma unroll
+      for (int i = 0; i < V; ++i) out[pass * C + t.c0 + i] = s[i];
+    }
+  }
+}
+
+__device__ __forceinline__ void band_sum(const float* __restrict__ ws, int nb, int C, int c, float* s0, float* s1) {
+  float a = 0.f, b = 0.f;
+  for (int k = 0; k < nb; ++k) {
+    a += ws[(int64_t)k * 2 * C + c];
+    b += ws[(int64_t)k * 2 * C + C + c];
+  }
+  *s0 = a;
+  *s1 = b;
+}
+
+// colsum finalize: out0[c] (+)= sum, out1[c] (+)= sumsq
+__global__ void colsum_finalize_k(const float* __restrict__ ws, int nb, int C, float* __restrict__ out0,
+                                  float* __restrict__ out1, int accumulate) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s0, s1;
+  band_sum(ws, nb, C, c, &s0, &s1);
+  if (out0) out0[c] = accumulate ? out0[c] + s0 : s0;
+  if (out1) out1[c] = accumulate ? out1[c] + s1 : s1;
+}
+
+// forward finalize: mean/var -> invstd, scale/shift, running stats
+__global__ void bn_fwd_finalize_k(const float* __restrict__ ws, int nb, int C, const float* __restrict__ gamma,
+                                  const float* __restrict__ beta, float* __restrict__ run_mean,
+                                  float* __restrict__ run_var, float* __restrict__ mean, float* __restrict__ invstd,
+                                  float* __restrict__ scale, float* __restrict__ shift, float count, float momentum,
+                                  float eps) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s0, s1;
+  band_sum(ws, nb, C, c, &s0, &s1);
+  float mu = s0 / count;
+  float var = fmaxf(s1 / count - mu * mu, 0.f);
+  float is = rsqrtf(var + eps);
+  mean[c] = mu;
+  invstd[c] = is;
+  float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
+  scale[c] = g * is;
+  shift[c] = b - mu * g * is;
+  if (run_mean) {
+    float unbiased = count > 1.f ? var * count / (count - 1.f) : var;
+    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mu;
+    run_var[c] = (1.f - momentum) * run_var[c] + momentum * unbiased;
+  }
+}
+
+// backward finalize: coefficients for dx = k*g + b*x + a; dgamma/dbeta
+// accumulated into dg/db (the flat fp32 gradient buffer views).
+__global__ void bn_bwd_finalize_k(const float* __restrict__ ws, int nb, int C, const float* __restrict__ gamma,
+                                  const float* __restrict__ mean, const float* __restrict__ invstd,
+                                  float* __restrict__ coef, float* __restrict__ dg, float* __restrict__ db,
+                                  float count) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float sdy, sdyx;
+  band_sum(ws, nb, C, c, &sdy, &sdyx);
+  float is = invstd[c];
+  float k = (gamma ? gamma[c] : 1.f) * is;
+  float bcoef = -k * is * sdyx / count;
+  float acoef = -k * sdy / count - bcoef * mean[c];
+  coef[c] = k;
+  coef[C + c] = bcoef;
+  coef[2 * C + c] = acoef;
+  if (dg) dg[c] += sdyx;
+  if (db) db[c] += sdy;
+}
+
+// inference: scale/shift from running stats
+__global__ void bn_infer_params_k(const float* __restrict__ gamma, const float* __restrict__ beta,
+                                  const float* __restrict__ run_mean, const float* __restrict__ run_var,
+                                  float* __restrict__ scale, float* __restrict__ shift, float* __restrict__ mean,
+                                  float* __restrict__ invstd, int C, float eps) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float is = rsqrtf(run_var[c] + eps);
+  float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
+  scale[c] = g * is;
+  shift[c] = b - run_mean[c] * g * is;
+  if (mean) mean[c] = run_mean[c];
+  if (invstd) invstd[c] = is;
+}
+
+// y = act(x*scale + shift + res)
+template <typename T, int V>
+__global__ void __launch_bounds__(256) bn_apply_k(const T* __restrict__ x, const float* __restrict__ scale,
+                                                  const float* __restrict__ shift, const T* __restrict__ res,
+                                                  T* __restrict__ y, int64_t R, int C, int relu) {
+  const Tile2D t = tile2d<V>(C);
+  if (!t.cok) return;
+  float sc[V], sf[V];
+  ldc<V>(scale + t.c0, sc);
+  ldc<V>(shift + t.c0, sf);
+  const int64_t step = (int64_t)t.RT * gridDim.x;
+  for (int64_t r = (int64_t)blockIdx.x * t.RT + t.ty; r < R; r += step) {
+    float v[V];
+    const int64_t o = r * C + t.c0;
+    ldv<T, V>(x + o, v);
+#pragma unroll
+    for (int k = 0; k < V; ++k) v[k] = v[k] * sc[k] + sf[k];
+    if (res) {
+      float rv[V];
+      ldv<T, V>(res + o, rv);
+#pragma unroll
+      for (int k = 0; k < V; ++k) v[k] += rv[k];
+    }
+    if (relu) {
+#pragma unroll
+      for (int k = 0; k < V; ++k) v[k] = fmaxf(v[k], 0.f);
+    }
+    stv<T, V>(y + o, v);
+  }
+}
+
+// g = mask(dy); dx = k*g + b*x + a; dres = g (residual branch)
+template <typename T, int V>
+__global__ void __launch_bounds__(256) bn_bwd_apply_k(const T* __restrict__ x, const T* __restrict__ dy,
+                                                      const T* __restrict__ y, const float* __restrict__ scale,
+                                                      const float* __restrict__ shift,
+                                                      const float* __restrict__ coef, T* __restrict__ dx,
+                                                      T* __restrict__ dres, int64_t R, int C, int mask_mode) {
+  const Tile2D t = tile2d<V>(C);
+  if (!t.cok) return;
+  float kk[V], bb[V], aa[V], sc[V], sf[V];
+  ldc<V>(coef + t.c0, kk);
+  ldc<V>(coef + C + t.c0, bb);
+  ldc<V>(coef + 2 * C + t.c0, aa);
+  if (mask_mode == MASK_AFFINE) {
+    ldc<V>(scale + t.c0, sc);
+    ldc<V>(shift + t.c0, sf);
+  }
+  const int64_t step = (int64_t)t.RT * gridDim.x;
+  for (int64_t r = (int64_t)blockIdx.x * t.RT + t.ty; r < R; r += step) {
+    const int64_t o = r * C + t.c0;
+    float v[V], g[V];
+    ldv<T, V>(x + o, v);
+    ldv<T, V>(dy + o, g);
+    if (mask_mode == MASK_Y) {
+      float yy[V];
+      ldv<T, V>(y + o, yy);
+#pragma unroll
+      for (int k = 0; k < V; ++k) g[k] = yy[k] > 0.f ? g[k] : 0.f;
+    } else if (mask_mode == MASK_AFFINE) {
+#pragma unroll
+      for (int k = 0; k < V; ++k) g[k] = v[k] * sc[k] + sf[k] > 0.f ? g[k] : 0.f;
+    }
+    if (dres) stv<T, V>(dres + o, g);
+    float o8[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) o8[k] = kk[k] * g[k] + bb[k] * v[k] + aa[k];
+    stv<T, V>(dx + o, o8);
+  }
+}
+
+}  // namespace sg
+
+using namespace sg;
+
+// number of row bands for a [R][C] column reduction (slab ws = bands*2*C floats)
+extern "C" int sg_colreduce_bands(int64_t R, int C) {
+  const int V = (C % 8 == 0) ? 8 : 1;
+  const int chunks = C / V;
+  const int CT = chunks < 64 ? chunks : 64;
+  const int cblocks = (chunks + CT - 1) / CT;
+  int64_t want = 1024 / cblocks;  // ~4 workgroups per CU in total
+  if (want < 1) want = 1;
+  int64_t minrows = 64;
+  int64_t bands = (R + minrows - 1) / minrows;
+  if (bands > want) bands = want;
+  return (int)(bands < 1 ? 1 : bands);
+}
+
+static inline void colgrid(int64_t R, int C, dim3& grid, int& rpb, int& V) {
+  V = (C % 8 == 0) ? 8 : 1;
+  const int chunks = C / V;
+  const int CT = chunks < 64 ? chunks : 64;
+  const int cblocks = (chunks + CT - 1) / CT;
+  const int bands = sg_colreduce_bands(R, C);
+  rpb = (int)((R + bands - 1) / bands);
+  grid = dim3(bands, cblocks);
+}
+
+static inline dim3 apply_grid(int64_t R, int C, int V) {
+  const int chunks = C / V;
+  const int CT = chunks < 64 ? chunks : 64;
+  const int cblocks = (chunks + CT - 1) / CT;
+  const int RT = 256 / CT;
+  int64_t rb = (R + RT - 1) / RT;
+  int64_t cap = 2048 / cblocks;
+  if (cap < 1) cap = 1;
+  if (rb > cap) rb = cap;
+  return dim3((unsigned)(rb < 1 ? 1 : rb), cblocks);
+}
+
+#define DISPATCH_FT(dtype, ...) \
+  if ((dtype) == kF32) {        \
+    typedef float T;            \
+    __VA_ARGS__;                \
+  } else {                      \
+    typedef bf16 T;             \
+    __VA_ARGS__;                \
+  }
+
+#define DISPATCH_V(Vv, ...)       \
+  if ((Vv) == 8) {                \
+    constexpr int VV = 8;         \
+    __VA_ARGS__;                  \
+  } else {                        \
+    constexpr int VV = 1;         \
+    __VA_ARGS__;                  \
+  }
+
+extern "C" {
+
+// out0/out1 (fp32 [C]) = column sums (accumulate != 0: added to existing)
+void sg_colsum(const void* x, void* ws, void* out0, void* out1, int64_t R, int C, int dtype, int accumulate,
+               hipStream_t s) {
+  dim3 grid;
+  int rpb, V;
+  colgrid(R, C, grid, rpb, V);
+  DISPATCH_FT(dtype, DISPATCH_V(V, hipLaunchKernelGGL((colpart_k<T, 0, VV>), grid, dim3(256), 0, s, (const T*)x,
+                                                      nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                                                      (float*)ws, R, C, rpb, 0)));
+  hipLaunchKernelGGL(colsum_finalize_k, dim3((C + 255) / 256), dim3(256), 0, s, (const float*)ws, (int)grid.x, C,
+                     (float*)out0, (float*)out1, accumulate);
+}
+
+void sg_bn_fwd_stats(const void* x, void* ws, const void* gamma, const void* beta, void* run_mean, void* run_var,
+                     void* mean, void* invstd, void* scale, void* shift, int64_t R, int C, float momentum, float eps,
+                     int dtype, hipStream_t s) {
+  dim3 grid;
+  int rpb, V;
+  colgrid(R, C, grid, rpb, V);
+  DISPATCH_FT(dtype, DISPATCH_V(V, hipLaunchKernelGGL((colpart_k<T, 0, VV>), grid, dim3(256), 0, s, (const T*)x,
+                                                      nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                                                      (float*)ws, R, C, rpb, 0)));
+  hipLaunchKernelGGL(bn_fwd_finalize_k, dim3((C + 255) / 256), dim3(256), 0, s, (const float*)ws, (int)grid.x, C,
+                     (const float*)gamma, (const float*)beta, (float*)run_mean, (float*)run_var, (float*)mean,
+                     (float*)invstd, (float*)scale, (float*)shift, (float)R, momentum, eps);
+}
+
+void sg_bn_infer_params(const void* gamma, const void* beta, const void* run_mean, const void* run_var, void* scale,
+                        void* shift, void* mean, void* invstd, int C, float eps, hipStream_t s) {
+  hipLaunchKernelGGL(bn_infer_params_k, dim3((C + 255) / 256), dim3(256), 0, s, (const float*)gamma,
+                     (const float*)beta, (const float*)run_mean, (const float*)run_var, (float*)scale,
+                     (float*)shift, (float*)mean, (float*)invstd, C, eps);
+}
+
+void sg_bn_apply(const void* x, const void* scale, const void* shift, const void* res, void* y, int64_t R, int C,
+                 int relu, int dtype, hipStream_t s) {
+  const int V = (C % 8 == 0) ? 8 : 1;
+  dim3 grid = apply_grid(R, C, V);
+  DISPATCH_FT(dtype, DISPATCH_V(V, hipLaunchKernelGGL((bn_apply_k<T, VV>), grid, dim3(256), 0, s, (const T*)x,
+                                                      (const float*)scale, (const float*)shift, (const T*)res, (T*)y,
+                                                      R, C, relu)));
+}
+
+// Full BN backward: reduce + finalize (coef, dgamma/dbeta accumulation) + apply.
+// mask_mode: 0 none, 1 mask from y (y>0), 2 mask from x*scale+shift>0.
+void sg_bn_bwd(const void* x, const void* dy, const void* y, const void* scale, const void* shift, const void* mean,
+               const void* invstd, const void* gamma, void* ws, void* coef, void* dg, void* db, void* dx, void* dres,
+               int64_t R, int C, int mask_mode, int dtype, hipStream_t s) {
+  dim3 grid;
+  int rpb, V;
+  colgrid(R, C, grid, rpb, V);
+  DISPATCH_FT(dtype, DISPATCH_V(V, hipLaunchKernelGGL((colpart_k<T, 1, VV>), grid, dim3(256), 0, s, (const T*)x,
+                                                      (const T*)dy, (const T*)y, (const float*)scale,
+                                                      (const float*)shift, (const float*)mean, (const float*)invstd,
+                                                      (float*)ws, R, C, rpb, mask_mode)));
+  hipLaunchKernelGGL(bn_bwd_finalize_k, dim3((C + 255) / 256), dim3(256), 0, s, (const float*)ws, (int)grid.x, C,
+                     (const float*)gamma, (const float*)mean, (const float*)invstd, (float*)coef, (float*)dg,
+                     (float*)db, (float)R);
+  dim3 ag = apply_grid(R, C, V);
+  DISPATCH_FT(dtype, DISPATCH_V(V, hipLaunchKernelGGL((bn_bwd_apply_k<T, VV>), ag, dim3(256), 0, s, (const T*)x,
+                                                      (const T*)dy, (const T*)y, (const float*)scale,
+                                                      (const float*)shift, (const float*)coef, (T*)dx, (T*)dres, R,
+                                                      C, mask_mode)));
+}
+
+}  // extern "C"

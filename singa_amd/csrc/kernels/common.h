@@ -105,6 +105,51 @@ struct FastDiv {
   }
 };
 
+// V-wide (8 x 16-bit or 8 x fp32, or scalar) vector loads/stores to fp32 regs
+template <typename T, int V>
+__device__ __forceinline__ void ldv(const T* p, float* v) {
+  if constexpr (V == 8) {
+    if constexpr (sizeof(T) == 2) {
+      bf16x8 t = *(const bf16x8*)p;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = (float)t[i];
+    } else {
+      float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < V; ++i) v[i] = to_f32(p[i]);
+  }
+}
+template <typename T, int V>
+__device__ __forceinline__ void stv(T* p, const float* v) {
+  if constexpr (V == 8) {
+    if constexpr (sizeof(T) == 2) {
+      bf16x8 t;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) t[i] = (bf16)v[i];
+      *(bf16x8*)p = t;
+    } else {
+      *(float4*)p = make_float4(v[0], v[1], v[2], v[3]);
+      *(float4*)(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < V; ++i) p[i] = from_f32<T>(v[i]);
+  }
+}
+template <int V>
+__device__ __forceinline__ void ldc(const float* p, float* v) {
+  if constexpr (V == 8) {
+    float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  } else {
+#pragma unroll
+    for (int i = 0; i < V; ++i) v[i] = p[i];
+  }
+}
+
 }  // namespace sg
 
 #define SG_GRID_STRIDE(i, n) \

@@ -55,6 +55,10 @@ def _like(t: torch.Tensor, dtype=None) -> torch.Tensor:
     return torch.empty(t.shape, dtype=dtype or t.dtype, device=t.device)
 
 
+def _zeros_cl(shape, dtype, device) -> torch.Tensor:
+    return torch.empty(shape, dtype=dtype, device=device, memory_format=torch.channels_last).zero_()
+
+
 def _dense(t: torch.Tensor) -> torch.Tensor:
     return t if (t.is_contiguous() or N.is_cl(t)) else t.contiguous()
 
@@ -408,7 +412,7 @@ def to_nhwc_bf16(x: torch.Tensor, cpad: Optional[int] = None) -> torch.Tensor:
             y = torch.empty((Nn, cp, H, W), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
             N.lib().nchw_to_nhwc_pad(x.data_ptr(), y.data_ptr(), Nn, C, H, W, cp, N.stream())
             return y
-        y = torch.zeros((Nn, cp, H, W), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+        y = _zeros_cl((Nn, cp, H, W), torch.bfloat16, x.device)
         y[:, :C] = x
         return y
     return x.to(dtype=torch.bfloat16, memory_format=torch.channels_last)
@@ -431,7 +435,7 @@ def conv2d_fwd(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], stri
         xb = x if (x.dtype == torch.bfloat16 and N.is_cl(x) and Cx == Cp) else to_nhwc_bf16(x[:, :C], Cp)
         wb = w
         if Cp != C or Kp != K:
-            wb = torch.zeros((Kp, Cp, R, S), dtype=torch.bfloat16, device=w.device, memory_format=torch.channels_last)
+            wb = _zeros_cl((Kp, Cp, R, S), torch.bfloat16, w.device)
             wb[:K, :C] = w
         elif not (w.dtype == torch.bfloat16 and N.is_cl(w)):
             wb = w.to(dtype=torch.bfloat16, memory_format=torch.channels_last)
@@ -472,26 +476,26 @@ def conv2d_bwd(x: torch.Tensor, w: torch.Tensor, dy: torch.Tensor, stride, paddi
         padded = Cp != C or Kp != K
         dx = dwt = db = None
         if need_dx:
+            if dh != 1 or dw_ != 1:
+                raise NotImplementedError("GPU conv data-gradient with dilation > 1")
+            if sh * sw > 16:
+                raise NotImplementedError("GPU conv data-gradient with stride_h*stride_w > 16")
             if padded:
-                wb = torch.zeros((Kp, Cp, R, S), dtype=torch.bfloat16, device=w.device,
-                                 memory_format=torch.channels_last)
+                wb = _zeros_cl((Kp, Cp, R, S), torch.bfloat16, w.device)
                 wb[:K, :C] = w
             else:
                 wb = w if (w.dtype == torch.bfloat16 and N.is_cl(w)) else w.to(dtype=torch.bfloat16,
                                                                                 memory_format=torch.channels_last)
-            wt = torch.empty((Cp, R, S, Kp), dtype=torch.bfloat16, device=w.device)
-            N.lib().wt_transpose(wb.data_ptr(), wt.data_ptr(), Kp, R * S, Cp, N.stream())
             od = torch.bfloat16 if x.dtype == torch.bfloat16 else torch.float32
             dxp = torch.empty((Nn, Cp, H, W), dtype=od, device=x.device, memory_format=torch.channels_last)
-            N.lib().conv_dgrad(dyb.data_ptr(), wt.data_ptr(), dxp.data_ptr(), Nn, H, W, Cp, Kp, R, S, Ho, Wo, sh, sw,
+            N.lib().conv_dgrad(dyb.data_ptr(), wb.data_ptr(), dxp.data_ptr(), Nn, H, W, Cp, Kp, R, S, Ho, Wo, sh, sw,
                                ph, pw, dh, dw_, 0 if od == torch.bfloat16 else 1, N.stream())
             dx = dxp[:, :C].contiguous(memory_format=torch.channels_last) if Cx != Cp else dxp
             if dx.dtype != x.dtype:
                 dx = dx.to(x.dtype)
         # weight gradient, fp32 [Kp][R][S][Cp]
         direct = (dw_out is not None and not padded and dw_out.dtype == torch.float32 and N.is_cl(dw_out))
-        target = dw_out if direct else torch.zeros((Kp, Cp, R, S), dtype=torch.float32, device=x.device,
-                                                   memory_format=torch.channels_last)
+        target = dw_out if direct else _zeros_cl((Kp, Cp, R, S), torch.float32, x.device)
         N.lib().conv_wgrad(xb.data_ptr(), dyb.data_ptr(), target.data_ptr(), Nn, H, W, Cp, Kp, R, S, Ho, Wo, sh, sw,
                            ph, pw, dh, dw_, 0, N.stream())
         if direct:
@@ -534,16 +538,33 @@ def _rows_c(x: torch.Tensor) -> Tuple[torch.Tensor, int, int]:
     return x, x.shape[0], x.shape[-1]
 
 
-def colsum(x2: torch.Tensor, with_sq: bool = False):
-    """Per-column sum (and sum of squares) of a [R, C] row-major tensor -> fp32."""
+_BANDS: dict = {}
+
+
+def _ws(R: int, C: int, device) -> torch.Tensor:
+    key = (R, C)
+    nb = _BANDS.get(key)
+    if nb is None:
+        nb = _BANDS[key] = N.lib().colreduce_bands(R, C)
+    return torch.empty(nb * 2 * C, dtype=torch.float32, device=device)
+
+
+def colsum(x2: torch.Tensor, with_sq: bool = False, out: Optional[torch.Tensor] = None):
+    """Per-column sum (and sum of squares) of a [R, C] row-major tensor -> fp32.
+    If ``out`` is given the column sums are ACCUMULATED into it."""
     if _native_ok(x2) and _flat_ok(x2) and x2.is_contiguous():
         R, C = x2.shape
-        o0 = torch.zeros(C, dtype=torch.float32, device=x2.device)
-        o1 = torch.zeros(C, dtype=torch.float32, device=x2.device) if with_sq else None
-        N.lib().colsum(x2.data_ptr(), o0.data_ptr(), N.ptr(o1), R, C, N.dt(x2), N.stream())
+        o0 = out if out is not None else torch.empty(C, dtype=torch.float32, device=x2.device)
+        o1 = torch.empty(C, dtype=torch.float32, device=x2.device) if with_sq else None
+        N.lib().colsum(x2.data_ptr(), _ws(R, C, x2.device).data_ptr(), o0.data_ptr(), N.ptr(o1), R, C, N.dt(x2),
+                       int(out is not None), N.stream())
         return o0, o1
     xf = x2.float()
-    return xf.sum(0), ((xf * xf).sum(0) if with_sq else None)
+    s0 = xf.sum(0)
+    if out is not None:
+        out.add_(s0)
+        s0 = out
+    return s0, ((xf * xf).sum(0) if with_sq else None)
 
 
 class BNState:
@@ -554,36 +575,36 @@ class BNState:
         self.mean, self.invstd, self.scale, self.shift = mean, invstd, scale, shift
 
 
+def _bn_native(x: torch.Tensor) -> bool:
+    return _native_ok(x) and _flat_ok(x) and ((x.dim() == 2 and x.is_contiguous()) or N.is_cl(x))
+
+
 def batchnorm_fwd(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, run_mean: torch.Tensor,
                   run_var: torch.Tensor, training: bool, momentum: float = 0.1, eps: float = 1e-5,
                   relu: bool = False, residual: Optional[torch.Tensor] = None):
     """y = act(BN(x) + residual).  4-D x (channels_last on GPU) or 2-D [B, C].
     momentum follows the PyTorch convention (weight of the new statistic)."""
     C = x.shape[1]
-    if _native_ok(x) and _flat_ok(x) and (x.dim() == 2 and x.is_contiguous() or N.is_cl(x)):
+    if _bn_native(x):
         L = N.lib()
         R = x.numel() // C
         dev = x.device
-        scale = torch.empty(C, dtype=torch.float32, device=dev)
-        shift = torch.empty(C, dtype=torch.float32, device=dev)
+        p = torch.empty(4 * C, dtype=torch.float32, device=dev)
+        mean, invstd, scale, shift = p[:C], p[C:2 * C], p[2 * C:3 * C], p[3 * C:]
         if training:
-            s0 = torch.zeros(2 * C, dtype=torch.float32, device=dev)
-            L.colsum(x.data_ptr(), s0.data_ptr(), s0.data_ptr() + 4 * C, R, C, N.dt(x), N.stream())
-            mean = torch.empty(C, dtype=torch.float32, device=dev)
-            invstd = torch.empty(C, dtype=torch.float32, device=dev)
-            L.bn_finalize(s0.data_ptr(), s0.data_ptr() + 4 * C, gamma.data_ptr(), beta.data_ptr(),
-                          run_mean.data_ptr(), run_var.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
-                          scale.data_ptr(), shift.data_ptr(), C, float(R), momentum, eps, N.stream())
+            L.bn_fwd_stats(x.data_ptr(), _ws(R, C, dev).data_ptr(), gamma.data_ptr(), beta.data_ptr(),
+                           run_mean.data_ptr(), run_var.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
+                           scale.data_ptr(), shift.data_ptr(), R, C, momentum, eps, N.dt(x), N.stream())
         else:
             L.bn_infer_params(gamma.data_ptr(), beta.data_ptr(), run_mean.data_ptr(), run_var.data_ptr(),
-                              scale.data_ptr(), shift.data_ptr(), C, eps, N.stream())
-            mean = run_mean
-            invstd = torch.rsqrt(run_var + eps)
+                              scale.data_ptr(), shift.data_ptr(), mean.data_ptr(), invstd.data_ptr(), C, eps,
+                              N.stream())
         res = None
         if residual is not None:
-            res = residual if residual.dtype == x.dtype and residual.stride() == x.stride() else \
-                _dense(residual).to(x.dtype).contiguous(memory_format=torch.channels_last if x.dim() == 4
-                                                        else torch.contiguous_format)
+            res = residual
+            if res.dtype != x.dtype or res.stride() != x.stride():
+                res = _dense(res).to(x.dtype).contiguous(
+                    memory_format=torch.channels_last if x.dim() == 4 else torch.contiguous_format)
         y = _like(x)
         L.bn_apply(x.data_ptr(), scale.data_ptr(), shift.data_ptr(), N.ptr(res), y.data_ptr(), R, C, int(relu),
                    N.dt(x), N.stream())
@@ -613,38 +634,55 @@ def batchnorm_fwd(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, run_
 
 
 def batchnorm_bwd(x: torch.Tensor, dy: torch.Tensor, gamma: torch.Tensor, st: BNState,
-                  y_for_mask: Optional[torch.Tensor] = None, need_dres: bool = False):
-    """Returns dx, dgamma, dbeta, dres (dres = masked dy when a residual was fused)."""
+                  y_for_mask: Optional[torch.Tensor] = None, need_dres: bool = False, relu: bool = False,
+                  dg_out: Optional[torch.Tensor] = None, db_out: Optional[torch.Tensor] = None):
+    """Returns dx, dgamma, dbeta, dres.  ReLU mask: from ``y_for_mask`` (the
+    fused output, required when a residual was added) or, with ``relu`` and no
+    residual, recomputed from x*scale+shift.  dgamma/dbeta are accumulated
+    into dg_out/db_out when given (and those are returned)."""
     C = x.shape[1]
-    if _native_ok(x, dy) and _flat_ok(x) and (x.dim() == 2 and x.is_contiguous() or N.is_cl(x)):
+    if _bn_native(x):
         L = N.lib()
         R = x.numel() // C
         if dy.dtype != x.dtype or dy.stride() != x.stride():
             dy = dy.to(x.dtype).contiguous(memory_format=torch.channels_last if x.dim() == 4 else
                                            torch.contiguous_format)
         ym = y_for_mask
-        if ym is not None and (ym.dtype != x.dtype or ym.stride() != x.stride()):
-            raise ValueError("batchnorm_bwd: mask tensor layout mismatch")
-        s = torch.zeros(2 * C, dtype=torch.float32, device=x.device)
-        L.bn_bwd_reduce(x.data_ptr(), dy.data_ptr(), N.ptr(ym), st.mean.data_ptr(), st.invstd.data_ptr(),
-                        s.data_ptr(), s.data_ptr() + 4 * C, R, C, N.dt(x), N.stream())
+        if ym is not None:
+            if ym.dtype != x.dtype or ym.stride() != x.stride():
+                raise ValueError("batchnorm_bwd: mask tensor layout mismatch")
+            mode = 1
+        else:
+            mode = 2 if relu else 0
+        dg = dg_out if dg_out is not None else torch.zeros(C, dtype=torch.float32, device=x.device)
+        db = db_out if db_out is not None else torch.zeros(C, dtype=torch.float32, device=x.device)
+        coef = torch.empty(3 * C, dtype=torch.float32, device=x.device)
         dx = _like(x)
         dres = _like(x) if need_dres else None
-        L.bn_bwd_apply(x.data_ptr(), dy.data_ptr(), N.ptr(ym), st.mean.data_ptr(), st.invstd.data_ptr(),
-                       gamma.data_ptr(), s.data_ptr(), s.data_ptr() + 4 * C, dx.data_ptr(), N.ptr(dres), R, C,
-                       N.dt(x), N.stream())
-        return dx, s[C:], s[:C], dres
+        L.bn_bwd(x.data_ptr(), dy.data_ptr(), N.ptr(ym), st.scale.data_ptr(), st.shift.data_ptr(),
+                 st.mean.data_ptr(), st.invstd.data_ptr(), gamma.data_ptr(), _ws(R, C, x.device).data_ptr(),
+                 coef.data_ptr(), dg.data_ptr(), db.data_ptr(), dx.data_ptr(), N.ptr(dres), R, C, mode, N.dt(x),
+                 N.stream())
+        return dx, dg, db, dres
     dims = (0,) if x.dim() == 2 else (0, 2, 3)
     shp = (1, C) if x.dim() == 2 else (1, C, 1, 1)
     g = dy.float()
     if y_for_mask is not None:
         g = g * (y_for_mask > 0)
+    elif relu:
+        g = g * ((x.float() * st.scale.reshape(shp) + st.shift.reshape(shp)) > 0)
     xh = (x.float() - st.mean.reshape(shp)) * st.invstd.reshape(shp)
     cnt = x.numel() // C
     sdy = g.sum(dims)
     sdyx = (g * xh).sum(dims)
     dx = gamma.float().reshape(shp) * st.invstd.reshape(shp) * (g - sdy.reshape(shp) / cnt -
                                                                   xh * sdyx.reshape(shp) / cnt)
+    if dg_out is not None:
+        dg_out.add_(sdyx)
+        sdyx = dg_out
+    if db_out is not None:
+        db_out.add_(sdy)
+        sdy = db_out
     return dx.to(x.dtype), sdyx, sdy, (g.to(x.dtype) if need_dres else None)
 
 

@@ -155,7 +155,8 @@ def test_batchnorm(gpu, C, relu, residual):
                             cl(res) if residual else None)
     assert rel_err(y, yr.detach()) < 1e-5
     assert rel_err(rmg, rm) < 1e-5 and rel_err(rvg, rv) < 1e-5
-    dx, dg, dbt, dres = F.batchnorm_bwd(cl(x), cl(dy), gam.to(gpu), st, y if relu else None, need_dres=residual)
+    dx, dg, dbt, dres = F.batchnorm_bwd(cl(x), cl(dy), gam.to(gpu), st, y if (relu and residual) else None,
+                                        need_dres=residual, relu=relu)
     assert rel_err(dx, xr.grad) < 1e-4
     assert rel_err(dg, gr.grad) < 1e-4
     assert rel_err(dbt, br.grad) < 1e-4
