@@ -37,6 +37,7 @@ void sg_layernorm_fwd(const void*, const void*, const void*, void*, void*, void*
 void sg_layernorm_bwd(const void*, const void*, const void*, const void*, const void*, void*, void*, void*, int64_t,
                       int, int, hipStream_t);
 int sg_colreduce_bands(int64_t, int);
+int sg_colreduce_ws(int);
 void sg_colsum(const void*, void*, void*, void*, int64_t, int, int, int, hipStream_t);
 void sg_bn_fwd_stats(const void*, void*, const void*, const void*, void*, void*, void*, void*, void*, void*, int64_t,
                      int, float, float, int, hipStream_t);
@@ -146,6 +147,7 @@ PYBIND11_MODULE(_C, m) {
     CHK("layernorm_bwd");
   });
   m.def("colreduce_bands", [](int64_t R, int C) { return sg_colreduce_bands(R, C); });
+  m.def("colreduce_ws", [](int C) { return sg_colreduce_ws(C); });
   m.def("colsum", [](P x, P ws, P o0, P o1, int64_t R, int C, int dt, int acc, P s) {
     sg_colsum(CV(x), V(ws), V(o0), V(o1), R, C, dt, acc, S(s)); CHK("colsum");
   });

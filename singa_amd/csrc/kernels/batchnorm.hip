@@ -2,11 +2,13 @@
 //
 // Design for MI355X (HBM-bound ops, every byte counts):
 //  * Reductions are two-stage: each workgroup reduces a band of rows for its
-//    channel slice in registers + LDS and writes ONE partial per channel to a
-//    slab ws[band][2][C] with plain stores; a per-channel finalize kernel sums
-//    the bands.  (A first version ended every workgroup with float atomics on
-//    the same 64..2048 channel addresses: thousands of contended adds per
-//    line serialised at the memory side and ran 20x below HBM bandwidth.)
+//    channel slice in registers + LDS and adds ONE partial per channel into
+//    one of 32 slot rows ws[band % 32][2][C] (32 adders per address), and a
+//    per-channel finalize kernel sums the 32 slots.  (v1 ended every
+//    workgroup with atomics on the same channel addresses -- 2048 contended
+//    adds on two cache lines ran 20x below HBM bandwidth; v2 stored one
+//    partial per band with plain stores, but then the per-channel finalize
+//    summed up to 1024 partials serially: 150 us per BN layer.)
 //  * Thread mapping is 2-D: a thread owns a fixed 8-channel (16-byte) slice
 //    and walks rows, so per-channel coefficients are loaded once into
 //    registers and no per-element channel index math (64-bit modulo) is done.
@@ -24,6 +26,7 @@
 namespace sg {
 
 enum MaskMode : int { MASK_NONE = 0, MASK_Y = 1, MASK_AFFINE = 2 };
+constexpr int NSLOT = 32;  // partial-sum slot rows (ws = NSLOT*2*C floats, zeroed per call)
 
 struct Tile2D {
   int CT, RT, tx, ty, c0;
@@ -133,8 +136,8 @@ __global__ void __launch_bounds__(256) colpart_k(const T* __restrict__ x, const 
       }
     }
   }
-  // reduce over ty in LDS, then one plain store per channel per band
-  float* out = ws + (int64_t)blockIdx.x * 2 * C;
+  // reduce over ty in LDS, then one atomic add per channel into slot band%32
+  float* out = ws + (int64_t)(blockIdx.x & (NSLOT - 1)) * 2 * C;
   for (int pass = 0; pass < 2; ++pass) {
     const float* acc = pass == 0 ? a0 : a1;
     __syncthreads();
@@ -152,7 +155,7 @@ __global__ void __launch_bounds__(256) colpart_k(const T* __restrict__ x, const 
         for (int i = 0; i < V; ++i) s[i] += red[(k * t.CT + t.tx) * V + i];
       }
 #pragma unroll
-      for (int i = 0; i < V; ++i) out[pass * C + t.c0 + i] = s[i];
+      for (int i = 0; i < V; ++i) atomicAdd(out + pass * C + t.c0 + i, s[i]);
     }
   }
 }
@@ -314,7 +317,10 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_k(const T* __restrict__ x, c
 
 using namespace sg;
 
-// number of row bands for a [R][C] column reduction (slab ws = bands*2*C floats)
+// workspace floats needed by the column reductions: NSLOT*2*C (see NSLOT)
+extern "C" int sg_colreduce_ws(int C) { return NSLOT * 2 * C; }
+
+// number of row bands for a [R][C] column reduction
 extern "C" int sg_colreduce_bands(int64_t R, int C) {
   const int V = (C % 8 == 0) ? 8 : 1;
   const int chunks = C / V;
@@ -376,10 +382,11 @@ void sg_colsum(const void* x, void* ws, void* out0, void* out1, int64_t R, int C
   dim3 grid;
   int rpb, V;
   colgrid(R, C, grid, rpb, V);
+  hipMemsetAsync(ws, 0, sizeof(float) * NSLOT * 2 * C, s);
   DISPATCH_FT(dtype, DISPATCH_V(V, hipLaunchKernelGGL((colpart_k<T, 0, VV>), grid, dim3(256), 0, s, (const T*)x,
                                                       nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
                                                       (float*)ws, R, C, rpb, 0)));
-  hipLaunchKernelGGL(colsum_finalize_k, dim3((C + 255) / 256), dim3(256), 0, s, (const float*)ws, (int)grid.x, C,
+  hipLaunchKernelGGL(colsum_finalize_k, dim3((C + 255) / 256), dim3(256), 0, s, (const float*)ws, NSLOT, C,
                      (float*)out0, (float*)out1, accumulate);
 }
 
@@ -389,10 +396,11 @@ void sg_bn_fwd_stats(const void* x, void* ws, const void* gamma, const void* bet
   dim3 grid;
   int rpb, V;
   colgrid(R, C, grid, rpb, V);
+  hipMemsetAsync(ws, 0, sizeof(float) * NSLOT * 2 * C, s);
   DISPATCH_FT(dtype, DISPATCH_V(V, hipLaunchKernelGGL((colpart_k<T, 0, VV>), grid, dim3(256), 0, s, (const T*)x,
                                                       nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
                                                       (float*)ws, R, C, rpb, 0)));
-  hipLaunchKernelGGL(bn_fwd_finalize_k, dim3((C + 255) / 256), dim3(256), 0, s, (const float*)ws, (int)grid.x, C,
+  hipLaunchKernelGGL(bn_fwd_finalize_k, dim3((C + 255) / 256), dim3(256), 0, s, (const float*)ws, NSLOT, C,
                      (const float*)gamma, (const float*)beta, (float*)run_mean, (float*)run_var, (float*)mean,
                      (float*)invstd, (float*)scale, (float*)shift, (float)R, momentum, eps);
 }
@@ -421,11 +429,12 @@ void sg_bn_bwd(const void* x, const void* dy, const void* y, const void* scale, 
   dim3 grid;
   int rpb, V;
   colgrid(R, C, grid, rpb, V);
+  hipMemsetAsync(ws, 0, sizeof(float) * NSLOT * 2 * C, s);
   DISPATCH_FT(dtype, DISPATCH_V(V, hipLaunchKernelGGL((colpart_k<T, 1, VV>), grid, dim3(256), 0, s, (const T*)x,
                                                       (const T*)dy, (const T*)y, (const float*)scale,
                                                       (const float*)shift, (const float*)mean, (const float*)invstd,
                                                       (float*)ws, R, C, rpb, mask_mode)));
-  hipLaunchKernelGGL(bn_bwd_finalize_k, dim3((C + 255) / 256), dim3(256), 0, s, (const float*)ws, (int)grid.x, C,
+  hipLaunchKernelGGL(bn_bwd_finalize_k, dim3((C + 255) / 256), dim3(256), 0, s, (const float*)ws, NSLOT, C,
                      (const float*)gamma, (const float*)mean, (const float*)invstd, (float*)coef, (float*)dg,
                      (float*)db, (float)R);
   dim3 ag = apply_grid(R, C, V);

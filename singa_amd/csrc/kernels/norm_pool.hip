@@ -17,119 +17,151 @@ struct PoolGeom {
   int N, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw;
 };
 
-template <typename T>
+// thread = (output pixel, V channels); V = 8 when C % 8 == 0
+template <typename T, int V>
 __global__ void maxpool_fwd_k(const T* __restrict__ x, T* __restrict__ y, uint8_t* __restrict__ arg, PoolGeom g) {
-  const int64_t total = (int64_t)g.N * g.Ho * g.Wo * g.C;
+  const int CV = g.C / V;
+  const int64_t total = (int64_t)g.N * g.Ho * g.Wo * CV;
   SG_GRID_STRIDE(i, total) {
-    int c = (int)(i % g.C);
-    int64_t p = i / g.C;
-    int ow = (int)(p % g.Wo);
-    p /= g.Wo;
-    int oh = (int)(p % g.Ho);
-    int n = (int)(p / g.Ho);
-    float m = -INFINITY;
-    int best = 0;
+    const int cv = (int)(i % CV);
+    const int p = (int)(i / CV);
+    const int ow = p % g.Wo;
+    const int t2 = p / g.Wo;
+    const int oh = t2 % g.Ho;
+    const int n = t2 / g.Ho;
+    float m[V];
+    uint8_t best[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) { m[k] = -INFINITY; best[k] = 0; }
     for (int r = 0; r < g.kh; ++r) {
-      int ih = oh * g.sh - g.ph + r;
+      const int ih = oh * g.sh - g.ph + r;
       if (ih < 0 || ih >= g.H) continue;
       for (int s = 0; s < g.kw; ++s) {
-        int iw = ow * g.sw - g.pw + s;
+        const int iw = ow * g.sw - g.pw + s;
         if (iw < 0 || iw >= g.W) continue;
-        float v = to_f32(x[(((int64_t)n * g.H + ih) * g.W + iw) * g.C + c]);
-        if (v > m) { m = v; best = r * g.kw + s; }
+        float v[V];
+        ldv<T, V>(x + (((int64_t)n * g.H + ih) * g.W + iw) * g.C + cv * V, v);
+#pragma unroll
+        for (int k = 0; k < V; ++k)
+          if (v[k] > m[k]) { m[k] = v[k]; best[k] = (uint8_t)(r * g.kw + s); }
       }
     }
-    y[i] = from_f32<T>(m);
-    if (arg) arg[i] = (uint8_t)best;
+    const int64_t o = (int64_t)p * g.C + cv * V;
+    stv<T, V>(y + o, m);
+    if (arg) {
+#pragma unroll
+      for (int k = 0; k < V; ++k) arg[o + k] = best[k];
+    }
   }
 }
 
-template <typename T>
+template <typename T, int V>
 __global__ void maxpool_bwd_k(const T* __restrict__ dy, const uint8_t* __restrict__ arg, T* __restrict__ dx,
                               PoolGeom g) {
-  const int64_t total = (int64_t)g.N * g.H * g.W * g.C;
+  const int CV = g.C / V;
+  const int64_t total = (int64_t)g.N * g.H * g.W * CV;
   SG_GRID_STRIDE(i, total) {
-    int c = (int)(i % g.C);
-    int64_t p = i / g.C;
-    int iw = (int)(p % g.W);
-    p /= g.W;
-    int ih = (int)(p % g.H);
-    int n = (int)(p / g.H);
-    // output windows that contain (ih, iw)
-    int oh0 = max(0, (ih + g.ph - g.kh + g.sh) / g.sh), oh1 = min(g.Ho - 1, (ih + g.ph) / g.sh);
-    int ow0 = max(0, (iw + g.pw - g.kw + g.sw) / g.sw), ow1 = min(g.Wo - 1, (iw + g.pw) / g.sw);
-    float acc = 0.f;
+    const int cv = (int)(i % CV);
+    const int p = (int)(i / CV);
+    const int iw = p % g.W;
+    const int t2 = p / g.W;
+    const int ih = t2 % g.H;
+    const int n = t2 / g.H;
+    const int oh0 = max(0, (ih + g.ph - g.kh + g.sh) / g.sh), oh1 = min(g.Ho - 1, (ih + g.ph) / g.sh);
+    const int ow0 = max(0, (iw + g.pw - g.kw + g.sw) / g.sw), ow1 = min(g.Wo - 1, (iw + g.pw) / g.sw);
+    float acc[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) acc[k] = 0.f;
     for (int oh = oh0; oh <= oh1; ++oh) {
-      int r = ih + g.ph - oh * g.sh;
+      const int r = ih + g.ph - oh * g.sh;
       if (r < 0 || r >= g.kh) continue;
       for (int ow = ow0; ow <= ow1; ++ow) {
-        int s = iw + g.pw - ow * g.sw;
+        const int s = iw + g.pw - ow * g.sw;
         if (s < 0 || s >= g.kw) continue;
-        int64_t o = (((int64_t)n * g.Ho + oh) * g.Wo + ow) * g.C + c;
-        if (arg[o] == r * g.kw + s) acc += to_f32(dy[o]);
+        const int64_t o = (((int64_t)n * g.Ho + oh) * g.Wo + ow) * g.C + cv * V;
+        float d[V];
+        ldv<T, V>(dy + o, d);
+        const uint8_t want = (uint8_t)(r * g.kw + s);
+#pragma unroll
+        for (int k = 0; k < V; ++k) acc[k] += arg[o + k] == want ? d[k] : 0.f;
       }
     }
-    dx[i] = from_f32<T>(acc);
+    stv<T, V>(dx + (int64_t)p * g.C + cv * V, acc);
   }
 }
 
-template <typename T>
+template <typename T, int V>
 __global__ void avgpool_fwd_k(const T* __restrict__ x, T* __restrict__ y, PoolGeom g, int count_pad) {
-  const int64_t total = (int64_t)g.N * g.Ho * g.Wo * g.C;
+  const int CV = g.C / V;
+  const int64_t total = (int64_t)g.N * g.Ho * g.Wo * CV;
   SG_GRID_STRIDE(i, total) {
-    int c = (int)(i % g.C);
-    int64_t p = i / g.C;
-    int ow = (int)(p % g.Wo);
-    p /= g.Wo;
-    int oh = (int)(p % g.Ho);
-    int n = (int)(p / g.Ho);
-    float acc = 0.f;
+    const int cv = (int)(i % CV);
+    const int p = (int)(i / CV);
+    const int ow = p % g.Wo;
+    const int t2 = p / g.Wo;
+    const int oh = t2 % g.Ho;
+    const int n = t2 / g.Ho;
+    float acc[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) acc[k] = 0.f;
     int cnt = 0;
     for (int r = 0; r < g.kh; ++r) {
-      int ih = oh * g.sh - g.ph + r;
+      const int ih = oh * g.sh - g.ph + r;
       if (ih < 0 || ih >= g.H) continue;
       for (int s = 0; s < g.kw; ++s) {
-        int iw = ow * g.sw - g.pw + s;
+        const int iw = ow * g.sw - g.pw + s;
         if (iw < 0 || iw >= g.W) continue;
-        acc += to_f32(x[(((int64_t)n * g.H + ih) * g.W + iw) * g.C + c]);
+        float v[V];
+        ldv<T, V>(x + (((int64_t)n * g.H + ih) * g.W + iw) * g.C + cv * V, v);
+#pragma unroll
+        for (int k = 0; k < V; ++k) acc[k] += v[k];
         ++cnt;
       }
     }
-    float d = count_pad ? (float)(g.kh * g.kw) : (float)max(cnt, 1);
-    y[i] = from_f32<T>(acc / d);
+    const float d = 1.f / (count_pad ? (float)(g.kh * g.kw) : (float)max(cnt, 1));
+#pragma unroll
+    for (int k = 0; k < V; ++k) acc[k] *= d;
+    stv<T, V>(y + (int64_t)p * g.C + cv * V, acc);
   }
 }
 
-template <typename T>
+template <typename T, int V>
 __global__ void avgpool_bwd_k(const T* __restrict__ dy, T* __restrict__ dx, PoolGeom g, int count_pad) {
-  const int64_t total = (int64_t)g.N * g.H * g.W * g.C;
+  const int CV = g.C / V;
+  const int64_t total = (int64_t)g.N * g.H * g.W * CV;
   SG_GRID_STRIDE(i, total) {
-    int c = (int)(i % g.C);
-    int64_t p = i / g.C;
-    int iw = (int)(p % g.W);
-    p /= g.W;
-    int ih = (int)(p % g.H);
-    int n = (int)(p / g.H);
-    int oh0 = max(0, (ih + g.ph - g.kh + g.sh) / g.sh), oh1 = min(g.Ho - 1, (ih + g.ph) / g.sh);
-    int ow0 = max(0, (iw + g.pw - g.kw + g.sw) / g.sw), ow1 = min(g.Wo - 1, (iw + g.pw) / g.sw);
-    float acc = 0.f;
+    const int cv = (int)(i % CV);
+    const int p = (int)(i / CV);
+    const int iw = p % g.W;
+    const int t2 = p / g.W;
+    const int ih = t2 % g.H;
+    const int n = t2 / g.H;
+    const int oh0 = max(0, (ih + g.ph - g.kh + g.sh) / g.sh), oh1 = min(g.Ho - 1, (ih + g.ph) / g.sh);
+    const int ow0 = max(0, (iw + g.pw - g.kw + g.sw) / g.sw), ow1 = min(g.Wo - 1, (iw + g.pw) / g.sw);
+    float acc[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) acc[k] = 0.f;
     for (int oh = oh0; oh <= oh1; ++oh) {
-      int r = ih + g.ph - oh * g.sh;
+      const int r = ih + g.ph - oh * g.sh;
       if (r < 0 || r >= g.kh) continue;
       for (int ow = ow0; ow <= ow1; ++ow) {
-        int s = iw + g.pw - ow * g.sw;
+        const int s = iw + g.pw - ow * g.sw;
         if (s < 0 || s >= g.kw) continue;
         float d;
         if (count_pad) d = (float)(g.kh * g.kw);
         else {
-          int h0 = max(oh * g.sh - g.ph, 0), h1 = min(oh * g.sh - g.ph + g.kh, g.H);
-          int w0 = max(ow * g.sw - g.pw, 0), w1 = min(ow * g.sw - g.pw + g.kw, g.W);
+          const int h0 = max(oh * g.sh - g.ph, 0), h1 = min(oh * g.sh - g.ph + g.kh, g.H);
+          const int w0 = max(ow * g.sw - g.pw, 0), w1 = min(ow * g.sw - g.pw + g.kw, g.W);
           d = (float)max((h1 - h0) * (w1 - w0), 1);
         }
-        acc += to_f32(dy[(((int64_t)n * g.Ho + oh) * g.Wo + ow) * g.C + c]) / d;
+        float v[V];
+        ldv<T, V>(dy + (((int64_t)n * g.Ho + oh) * g.Wo + ow) * g.C + cv * V, v);
+        const float inv = 1.f / d;
+#pragma unroll
+        for (int k = 0; k < V; ++k) acc[k] += v[k] * inv;
       }
     }
-    dx[i] = from_f32<T>(acc);
+    stv<T, V>(dx + (int64_t)p * g.C + cv * V, acc);
   }
 }
 
@@ -229,28 +261,40 @@ using namespace sg;
 
 extern "C" {
 
+#define DISPATCH_V(Vv, ...)       \
+  if ((Vv) == 8) {                \
+    constexpr int VV = 8;         \
+    __VA_ARGS__;                  \
+  } else {                        \
+    constexpr int VV = 1;         \
+    __VA_ARGS__;                  \
+  }
+
 void sg_pool_fwd(const void* x, void* y, void* arg, int N, int H, int W, int C, int Ho, int Wo, int kh, int kw,
                  int sh, int sw, int ph, int pw, int is_max, int count_pad, int dtype, hipStream_t s) {
   PoolGeom g{N, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw};
-  int64_t total = (int64_t)N * Ho * Wo * C;
+  const int V = (C % 8 == 0) ? 8 : 1;
+  const int64_t total = (int64_t)N * Ho * Wo * (C / V);
   if (is_max) {
-    DISPATCH_FT(dtype, hipLaunchKernelGGL(maxpool_fwd_k<T>, dim3(sg_grid(total, 256, 16384)), dim3(256), 0, s,
-                                          (const T*)x, (T*)y, (uint8_t*)arg, g));
+    DISPATCH_FT(dtype, DISPATCH_V(V, hipLaunchKernelGGL((maxpool_fwd_k<T, VV>), dim3(sg_grid(total, 256, 16384)),
+                                                        dim3(256), 0, s, (const T*)x, (T*)y, (uint8_t*)arg, g)));
   } else {
-    DISPATCH_FT(dtype, hipLaunchKernelGGL(avgpool_fwd_k<T>, dim3(sg_grid(total, 256, 16384)), dim3(256), 0, s,
-                                          (const T*)x, (T*)y, g, count_pad));
+    DISPATCH_FT(dtype, DISPATCH_V(V, hipLaunchKernelGGL((avgpool_fwd_k<T, VV>), dim3(sg_grid(total, 256, 16384)),
+                                                        dim3(256), 0, s, (const T*)x, (T*)y, g, count_pad)));
   }
 }
 void sg_pool_bwd(const void* dy, const void* arg, void* dx, int N, int H, int W, int C, int Ho, int Wo, int kh,
                  int kw, int sh, int sw, int ph, int pw, int is_max, int count_pad, int dtype, hipStream_t s) {
   PoolGeom g{N, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw};
-  int64_t total = (int64_t)N * H * W * C;
+  const int V = (C % 8 == 0) ? 8 : 1;
+  const int64_t total = (int64_t)N * H * W * (C / V);
   if (is_max) {
-    DISPATCH_FT(dtype, hipLaunchKernelGGL(maxpool_bwd_k<T>, dim3(sg_grid(total, 256, 16384)), dim3(256), 0, s,
-                                          (const T*)dy, (const uint8_t*)arg, (T*)dx, g));
+    DISPATCH_FT(dtype, DISPATCH_V(V, hipLaunchKernelGGL((maxpool_bwd_k<T, VV>), dim3(sg_grid(total, 256, 16384)),
+                                                        dim3(256), 0, s, (const T*)dy, (const uint8_t*)arg, (T*)dx,
+                                                        g)));
   } else {
-    DISPATCH_FT(dtype, hipLaunchKernelGGL(avgpool_bwd_k<T>, dim3(sg_grid(total, 256, 16384)), dim3(256), 0, s,
-                                          (const T*)dy, (T*)dx, g, count_pad));
+    DISPATCH_FT(dtype, DISPATCH_V(V, hipLaunchKernelGGL((avgpool_bwd_k<T, VV>), dim3(sg_grid(total, 256, 16384)),
+                                                        dim3(256), 0, s, (const T*)dy, (T*)dx, g, count_pad)));
   }
 }
 void sg_gap_fwd(const void* x, void* y, int N, int HW, int C, int dtype, hipStream_t s) {

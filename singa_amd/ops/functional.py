@@ -542,11 +542,10 @@ _BANDS: dict = {}
 
 
 def _ws(R: int, C: int, device) -> torch.Tensor:
-    key = (R, C)
-    nb = _BANDS.get(key)
-    if nb is None:
-        nb = _BANDS[key] = N.lib().colreduce_bands(R, C)
-    return torch.empty(nb * 2 * C, dtype=torch.float32, device=device)
+    n = _BANDS.get(C)
+    if n is None:
+        n = _BANDS[C] = N.lib().colreduce_ws(C)
+    return torch.empty(n, dtype=torch.float32, device=device)
 
 
 def colsum(x2: torch.Tensor, with_sq: bool = False, out: Optional[torch.Tensor] = None):
