@@ -1,0 +1,417 @@
+"""NeuralNet (reference C23, src/worker/neuralnet.cc): builds the layer DAG
+from a ``NetProto``, topologically sorts it (native ``_core.Graph``), infers
+shapes, optionally partitions it across a worker group, shares weights
+between train/test/validation nets, and exports a node-link JSON graph.
+
+Partitioning (P4 data partition on dim 0, P5 layer partition on dim 1, P6
+placement by ``locationid``) follows the reference's graph-rewrite rules
+(CreatePartitonedGraph, neuralnet.cc:198-323): partitioned layers become
+``name-00..name-(g-1)`` nodes; Slice / Concate / Split nodes are inserted on
+mixed edges; fan-out gets a Split; edges that cross locations get a
+BridgeSrc -> BridgeDst pair.  Unlike the reference (where the partitioned net
+was never executed and the connection layers were stubs), the partitioned
+net here runs: data-partition replicas share their parameters (and loss
+replicas are scaled by 1/g, the reference ParamManager's grad_scale=1/k
+aggregation), layer-partition replicas own their slice of the parameters,
+and the result equals the unpartitioned net (tests/test_neuralnet.py).
+"""
+from __future__ import annotations
+
+import json
+from collections import OrderedDict
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from .. import autograd
+from ..config import schema
+from ..tensor import Tensor
+from .layers import RefLayer, create_layer
+
+
+class _Node:
+    def __init__(self, name, origin, loc, pid, slice_dim=-1, concate_dim=-1):
+        self.name, self.origin, self.loc, self.pid = name, origin, loc, pid
+        self.slice_dim, self.concate_dim = slice_dim, concate_dim
+        self.srcs: List["_Node"] = []
+        self.dsts: List["_Node"] = []
+
+
+class _PGraph:
+    def __init__(self):
+        self.nodes: "OrderedDict[str, _Node]" = OrderedDict()
+
+    def add(self, name, *a, **k) -> _Node:
+        base, i = name, 1
+        while name in self.nodes:
+            name = f"{base}#{i}"
+            i += 1
+        n = _Node(name, *a, **k)
+        self.nodes[name] = n
+        return n
+
+    @staticmethod
+    def edge(a: _Node, b: _Node):
+        if b not in a.dsts:
+            a.dsts.append(b)
+            b.srcs.append(a)
+
+    @staticmethod
+    def remove(a: _Node, b: _Node):
+        a.dsts.remove(b)
+        b.srcs.remove(a)
+
+    def slice_node(self, src, dsts, slice_dim, connect=True):
+        n = self.add("slice-" + src.name, "kSlice", src.loc, src.pid, slice_dim=slice_dim)
+        self.edge(src, n)
+        if connect:
+            for d in dsts:
+                self.edge(n, d)
+        return n
+
+    def concate_node(self, srcs, dst, concate_dim):
+        n = self.add("concate-" + dst.name, "kConcate", dst.loc, dst.pid, concate_dim=concate_dim)
+        self.edge(n, dst)
+        for s in srcs:
+            self.edge(s, n)
+        return n
+
+    def split_node(self, src, dsts):
+        n = self.add("split-" + src.name, "kSplit", src.loc, src.pid)
+        self.edge(src, n)
+        for d in dsts:
+            self.edge(n, d)
+        return n
+
+    def bridge(self, src, dst):
+        """Replace edge src->dst by src->BridgeSrc->BridgeDst->dst, keeping
+        the positions in src.dsts / dst.srcs (concate order = partition id)."""
+        a = self.add(f"s-{src.name}-{dst.name}", "kBridgeSrc", src.loc, src.pid)
+        b = self.add(f"d-{src.name}-{dst.name}", "kBridgeDst", dst.loc, dst.pid)
+        src.dsts[src.dsts.index(dst)] = a
+        a.srcs.append(src)
+        self.edge(a, b)
+        b.dsts.append(dst)
+        dst.srcs[dst.srcs.index(src)] = b
+
+    def sort(self) -> List[_Node]:
+        from .. import _core
+
+        g = _core.Graph()
+        for n in self.nodes.values():
+            g.add_node(n.name)
+        for n in self.nodes.values():
+            for d in n.dsts:
+                g.add_edge(n.name, d.name)
+        order = g.sort()
+        self.nodes = OrderedDict((k, self.nodes[k]) for k in order)
+        return list(self.nodes.values())
+
+
+class NeuralNet:
+    def __init__(self, net_proto, group_size: int = 1, phase: str = "kTrain", dev=None,
+                 data_override: Optional[dict] = None, seed: int = 0, devices: Optional[List] = None):
+        from ..device import get_default_device
+
+        self.dev = dev or get_default_device()
+        self.devices = devices  # per-location device list (placement, P6)
+        self.group_size = group_size
+        self.phase = phase
+        default_pt = schema.enum_name(net_proto, "partition_type")
+        protos = []
+        for lp in net_proto.layer:
+            excl = [schema.message_class("LayerProto").DESCRIPTOR.fields_by_name["exclude"].enum_type
+                    .values_by_number[e].name for e in lp.exclude]
+            if phase in excl:
+                continue
+            protos.append(lp)
+        self.layers: List[RefLayer] = []
+        self.name2layer: Dict[str, RefLayer] = {}
+        for lp in protos:
+            pt = schema.enum_name(lp, "partition_type") if lp.HasField("partition_type") else default_pt
+            layer = create_layer(lp, partition_type=pt)
+            self.layers.append(layer)
+            self.name2layer[layer.name] = layer
+        self.gen = torch.Generator().manual_seed(seed)
+        data_override = data_override or {}
+        for l in self.layers:
+            if l.is_data:
+                ov = data_override.get(l.name, data_override.get("*", {}))
+                l.configure(synthetic_shape=ov.get("shape", (28, 28)), nclass=ov.get("nclass", 10),
+                            seed=ov.get("seed", seed), prefetch=ov.get("prefetch", True))
+                if "batch" in ov:
+                    l.batch = int(ov["batch"])
+                    l.source.batch = l.batch
+                    if l.source.prefetcher is not None:
+                        raise ValueError("batch override is not supported for shard-backed data layers")
+        self._construct()
+        self.partitioned = group_size > 1 and any(l.partition_type != "kNone" for l in self.layers)
+        if self.partitioned:
+            self._partition()
+        self._assign_param_ids()
+
+    # ------------------------------------------------------------- construct
+    def _construct(self):
+        from .. import _core
+
+        g = _core.Graph()
+        for l in self.layers:
+            g.add_node(l.name)
+        for l in self.layers:
+            for s in l.srcs:
+                if s not in self.name2layer:
+                    raise KeyError(f"layer {l.name}: unknown src layer {s}")
+                g.add_edge(s, l.name)
+        order = g.sort()
+        self.layers = [self.name2layer[n] for n in order]
+        self.order = order
+        self.dsts: Dict[str, List[str]] = {l.name: [] for l in self.layers}
+        for l in self.layers:
+            for s in l.srcs:
+                self.dsts[s].append(l.name)
+        shapes: Dict[str, tuple] = {}
+        for l in self.layers:
+            src_shapes = []
+            for s in l.srcs:
+                src_shapes.append(shapes[s])
+            shapes[l.name] = l.setup(src_shapes, self._dev_of(l.locationid), self.gen)
+        self.shapes = shapes
+
+    def _dev_of(self, loc: int):
+        if self.devices:
+            return self.devices[loc % len(self.devices)]
+        return self.dev
+
+    # ------------------------------------------------------------- partition
+    def _partition(self):
+        g = self.group_size
+        pg = _PGraph()
+        l2n: Dict[str, List[_Node]] = {}
+        for l in self.layers:
+            if l.partition_type in ("kDataPartition", "kLayerPartition"):
+                l2n[l.name] = [pg.add(f"{l.name}-{i:02d}", l.name, i, i) for i in range(g)]
+            else:
+                l2n[l.name] = [pg.add(l.name, l.name, l.locationid, 0)]
+        for l in self.layers:
+            nodes = l2n[l.name]
+            tt = l.partition_type
+            for si, sname in enumerate(l.srcs):
+                src = self.name2layer[sname]
+                snodes = l2n[sname]
+                st = src.partition_type
+                conn = l.connection_type(si)
+                part = ("kDataPartition", "kLayerPartition")
+                if st == "kNone":
+                    if tt == "kDataPartition" or (tt == "kLayerPartition" and conn == "kOneToOne"):
+                        pg.slice_node(snodes[0], nodes, l.partition_dimension())
+                    elif tt == "kNone":
+                        pg.edge(snodes[0], nodes[0])
+                    else:
+                        pg.split_node(snodes[0], nodes)
+                elif (tt == "kNone" and st in part) or (tt == "kLayerPartition" and conn == "kOneToAll"
+                                                        and st in part):
+                    for n in nodes:
+                        pg.concate_node(snodes, n, src.partition_dimension())
+                elif (st == "kLayerPartition" and tt == "kDataPartition") or (
+                        st == "kDataPartition" and tt == "kLayerPartition"):
+                    slices = [pg.slice_node(sn, nodes, l.partition_dimension(), connect=False) for sn in snodes]
+                    for n in nodes:
+                        pg.concate_node(slices, n, src.partition_dimension())
+                else:  # same partitioning, one-to-one
+                    for a, b in zip(snodes, nodes):
+                        pg.edge(a, b)
+        order = pg.sort()
+        for i, n in enumerate(order):
+            if i > 0 and len(n.dsts) > 1 and n.origin not in ("kSlice", "kSplit"):
+                sp = pg.add("split-" + n.name, "kSplit", n.loc, n.pid)
+                for d in n.dsts:  # keep each consumer's input position
+                    d.srcs[d.srcs.index(n)] = sp
+                sp.dsts, n.dsts = list(n.dsts), [sp]
+                sp.srcs.append(n)
+        for n in list(pg.sort()):
+            for d in list(n.dsts):
+                if n.loc != d.loc:
+                    pg.bridge(n, d)
+        order = pg.sort()
+        self.graph_nodes = order
+        self._instantiate_partitioned(order)
+
+    def _instantiate_partitioned(self, order: List[_Node]):
+        from .layers import create_layer as mk
+
+        g = self.group_size
+        orig = self.name2layer
+        new_layers: List[RefLayer] = []
+        by_name: Dict[str, RefLayer] = {}
+        shapes: Dict[str, tuple] = {}
+        self.slice_route: Dict[str, Dict[str, int]] = {}
+        for n in order:
+            if n.origin in ("kSlice", "kConcate", "kSplit", "kBridgeSrc", "kBridgeDst"):
+                lp = schema.new("LayerProto")
+                lp.name, lp.type, lp.locationid, lp.partitionid = n.name, n.origin, n.loc, n.pid
+                if n.origin == "kSlice":
+                    lp.slice_param.slice_dimension = n.slice_dim
+                    lp.slice_param.slice_num = len(n.dsts)
+                elif n.origin == "kConcate":
+                    lp.concate_param.concate_dimension = n.concate_dim
+                    lp.concate_param.concate_num = len(n.srcs)
+                elif n.origin == "kSplit":
+                    lp.split_param.num_splits = len(n.dsts)
+                layer = mk(lp)
+            else:
+                base = orig[n.origin]
+                if base.partition_type == "kNone":
+                    layer = base
+                else:
+                    lp = schema.new("LayerProto")
+                    lp.CopyFrom(base.proto)
+                    lp.name, lp.locationid, lp.partitionid = n.name, n.loc, n.pid
+                    layer = mk(lp, partition_type=base.partition_type)
+                    pdim = base.partition_dimension()
+                    full = base.shape[pdim]
+                    share = full // g + (full % g if n.pid == g - 1 else 0)
+                    if base.partition_type == "kLayerPartition" and pdim == 1:
+                        layer.nf_override = share
+                        layer.part_offset = (full // g) * n.pid
+                    if base.partition_type == "kDataPartition":
+                        layer.params = base.params  # replicas share the parameters
+                        if base.is_loss:
+                            layer.loss_scale = 1.0 / g
+                    layer.origin = base
+            layer.srcs = [s.name for s in n.srcs]
+            layer.graph_dsts = [d.name for d in n.dsts]
+            new_layers.append(layer)
+            by_name[n.name] = layer
+        # shapes / params for the new layers
+        for layer in new_layers:
+            src_shapes = []
+            for s in layer.srcs:
+                sl = by_name[s]
+                if sl.type_name == "kSlice":
+                    src_shapes.append(sl.shapes[sl.graph_dsts.index(layer.name)])
+                else:
+                    src_shapes.append(shapes[s])
+            if layer.partition_type == "kLayerPartition" and getattr(layer, "origin", None) is not None \
+                    and not layer.params:
+                base = layer.origin
+                shapes[layer.name] = layer.setup(src_shapes, self._dev_of(layer.locationid), self.gen)
+                # take this partition's slice of the unpartitioned params
+                off = getattr(layer, "part_offset", None)
+                if not base.params or off is None:
+                    continue
+                w = base.params[0].data
+                if base.type_name == "kConvolution":
+                    layer.params[0].data.copy_(w[off:off + layer.nf])
+                else:
+                    layer.params[0].data.copy_(w[:, off:off + layer.hdim])
+                if len(base.params) > 1:
+                    nb = layer.params[1].shape[0]
+                    layer.params[1].data.copy_(base.params[1].data[off:off + nb])
+            else:
+                shapes[layer.name] = layer.setup(src_shapes, self._dev_of(layer.locationid), self.gen)
+        self.layers = new_layers
+        self.name2layer = by_name
+        self.shapes = shapes
+        self.order = [l.name for l in new_layers]
+
+    def _assign_param_ids(self):
+        seen, pid = set(), 0
+        for l in self.layers:
+            for p in l.params:
+                if id(p) not in seen:
+                    seen.add(id(p))
+                    if p.param_meta is None:
+                        p.param_meta = {}
+                    p.param_meta["id"] = pid
+                    pid += 1
+        self.num_params = pid
+
+    # -------------------------------------------------------------- execute
+    def params(self) -> List[Tensor]:
+        out, seen = [], set()
+        for l in self.layers:
+            for p in l.params:
+                if id(p) not in seen:
+                    seen.add(id(p))
+                    out.append(p)
+        return out
+
+    def loss_layers(self) -> List[RefLayer]:
+        return [l for l in self.layers if l.is_loss]
+
+    def forward(self, training: bool = True) -> Dict[str, object]:
+        """Run every layer in topological order; returns name -> output."""
+        autograd.training = training
+        outs: Dict[str, object] = {}
+        for l in self.layers:
+            xs = []
+            for s in l.srcs:
+                o = outs[s]
+                if isinstance(o, list):  # slice: pick this consumer's part
+                    src = self.name2layer[s]
+                    dsts = getattr(src, "graph_dsts", None) or self.dsts.get(s, [])
+                    o = o[dsts.index(l.name)]
+                xs.append(o)
+            outs[l.name] = l.forward(xs, training)
+        self.outputs = outs
+        return outs
+
+    def total_loss(self, outs) -> Optional[Tensor]:
+        losses = [outs[l.name] for l in self.loss_layers()]
+        if not losses:
+            return None
+        tot = losses[0]
+        for t in losses[1:]:
+            tot = autograd.add(tot, t)
+        return tot
+
+    def metrics(self) -> np.ndarray:
+        """[loss, precision] summed over loss layers (reference metric blob)."""
+        m = np.zeros(2, np.float64)
+        for l in self.loss_layers():
+            if hasattr(l, "metric"):
+                m += np.array([float(l.metric[0]), float(l.metric[1])]) * (l.loss_scale if l.loss_scale else 1)
+        return m
+
+    def share_weights(self, other: "NeuralNet") -> None:
+        """Share parameter storage with ``other`` (test/validation nets)."""
+        src = {}
+        for l in other.layers:
+            src.setdefault(getattr(l, "origin", l).name, l.params)
+        for l in self.layers:
+            key = getattr(l, "origin", l).name
+            if key in src and len(src[key]) == len(l.params):
+                for a, b in zip(l.params, src[key]):
+                    a.data = b.data
+                    a.low = b.low
+                l.params = src[key]
+
+    def to_json(self) -> str:
+        """Node-link JSON (colour by locationid), script/graph.py compatible."""
+        from .. import _core
+
+        g = _core.Graph()
+        for l in self.layers:
+            g.add_node(l.name)
+        for l in self.layers:
+            for s in l.srcs:
+                g.add_edge(s, l.name)
+        return g.to_json([l.locationid for l in self.layers])
+
+    def debug_info(self) -> str:
+        """norm1 (mean |x|) of every layer output and parameter (reference
+        NeuralNet::DebugInfo; Blob::asum_data is a mean, Appendix A #14)."""
+        lines = []
+        for l in self.layers:
+            o = getattr(self, "outputs", {}).get(l.name)
+            if isinstance(o, Tensor):
+                lines.append(f"layer {l.name} data norm1 {o.data.float().abs().mean().item():.6f}")
+            for p in l.params:
+                g = p.grad_view
+                gs = f" grad norm1 {g.float().abs().mean().item():.6f}" if g is not None else ""
+                lines.append(f"param {p.name} data norm1 {p.data.float().abs().mean().item():.6f}{gs}")
+        return "\n".join(lines)
+
+    def __repr__(self):
+        return "NeuralNet(" + ", ".join(f"{l.name}:{self.shapes.get(l.name)}" for l in self.layers) + ")"

@@ -1,0 +1,207 @@
+"""Worker runtime (reference C24, src/worker/worker.cc): trains a
+``ModelProto`` net with the reference cadence semantics.
+
+* nets: train / test / validation built from the same NetProto with phase
+  exclusion (worker.cc:69-95); test & validation share the train weights;
+* updater from ``UpdaterProto`` (type + the six LR change methods,
+  updater.cc:11-182) as a fused flat-buffer optimiser;
+* loop: ``warmup_steps`` local steps, bandwidth-model configuration
+  (SyncConfig), bootstrap broadcast of group 0's weights, then
+  ``train_steps`` with test / validation / display at the configured
+  frequencies (include/worker/worker.h:118-158), and EASGD / RandomSync
+  exchange every ``sync_frequency`` steps when more than one group runs;
+* ``Performance`` accumulates the loss layers' [loss, precision] metric and
+  prints averages; ``TimerInfo`` reports ms/step split into forward,
+  backward+update and sync (HIP-event timed on a RocmGPU).
+
+One process = one worker group (GPU); ``ClusterProto`` roles map onto
+torch.distributed ranks (servers are replaced by collectives).
+"""
+from __future__ import annotations
+
+import time
+from typing import Callable, Dict, Optional
+
+import numpy as np
+import torch
+
+from .. import autograd, opt
+from ..config import schema
+from ..device import Timer, get_default_device
+from ..parallel.communicator import Communicator, init_distributed
+from ..parallel.easgd import ElasticSync, RandomSync
+from .neuralnet import NeuralNet
+
+
+def make_updater(up) -> opt.Optimizer:
+    """Updater factory (reference param_manager.cc:19-37)."""
+    kind = schema.enum_name(up, "type")
+    method = schema.enum_name(up, "learning_rate_change_method")
+    base = up.base_learning_rate if up.HasField("base_learning_rate") else 0.01
+    sched = opt.RefSchedule(method, base, up.final_learning_rate, up.learning_rate_change_frequency, up.gamma,
+                            up.pow)
+    if kind == "kSGD":
+        return opt.RefSGD(sched, up.momentum, up.weight_decay)
+    if kind == "kNesterov":
+        return opt.Nesterov(sched, up.momentum, up.weight_decay)
+    if kind == "kAdaGrad":
+        return opt.AdaGrad(sched, up.delta, up.weight_decay)
+    if kind == "kRMSProp":
+        return opt.RMSProp(sched, up.rho, up.delta, up.weight_decay)
+    if kind == "kAdaDelta":
+        return opt.AdaDelta(1.0, up.rho, up.delta, up.weight_decay)
+    raise ValueError(kind)
+
+
+class Performance:
+    def __init__(self, name: str = "train"):
+        self.name = name
+        self.reset()
+
+    def reset(self):
+        self.sum = np.zeros(2)
+        self.n = 0
+
+    def update(self, metric: np.ndarray):
+        self.sum += metric
+        self.n += 1
+
+    def avg(self) -> np.ndarray:
+        return self.sum / max(1, self.n)
+
+    def to_string(self) -> str:
+        a = self.avg()
+        return f"{self.name}: loss : {a[0]:.6f}, precision : {a[1]:.6f}"
+
+
+class Worker:
+    def __init__(self, model_proto, cluster_proto=None, dev=None, comm: Optional[Communicator] = None,
+                 data_override: Optional[dict] = None, log: Callable[[str], None] = print, group_size: int = 1,
+                 seed: int = 0):
+        self.model = model_proto
+        self.cluster = cluster_proto
+        self.dev = dev or get_default_device()
+        self.comm = comm or init_distributed()
+        self.log = log
+        self.group_size = group_size
+        self.data_override = data_override or {}
+        self.seed = seed
+        self.timers = {"forward": 0.0, "backward": 0.0, "sync": 0.0}
+        self.history = []
+        self._setup()
+
+    # ------------------------------------------------------------------ setup
+    def _phase_has_layers(self, phase: str) -> bool:
+        return True
+
+    def _setup(self):
+        net = self.model.neuralnet
+        self.train_net = NeuralNet(net, self.group_size, "kTrain", self.dev, self.data_override,
+                                   seed=self.seed + self.comm.rank)
+        self.test_net = None
+        self.val_net = None
+        if self.model.test_steps and self.model.test_frequency:
+            self.test_net = NeuralNet(net, 1, "kTest", self.dev, self.data_override, seed=self.seed + 1)
+            self.test_net.share_weights(self.train_net)
+        if self.model.validation_steps and self.model.validation_frequency:
+            self.val_net = NeuralNet(net, 1, "kValidation", self.dev, self.data_override, seed=self.seed + 2)
+            self.val_net.share_weights(self.train_net)
+        self.updater = make_updater(self.model.updater)
+        self.store = self.updater.attach(self.train_net.params())
+        for n in (self.test_net, self.val_net):
+            if n is not None:
+                n.share_weights(self.train_net)
+        up = self.model.updater
+        self.sync = None
+        if self.comm.world_size > 1:
+            if up.param_type == "RandomSync":
+                self.sync = RandomSync(self.store, self.comm, 1.0, up.sync_frequency, up.warmup_steps)
+            else:
+                self.sync = ElasticSync(self.store, self.comm, up.moving_rate or 0.9, up.sync_frequency,
+                                        up.warmup_steps)
+        self.perf = Performance("train")
+
+    # ------------------------------------------------------------- cadence
+    @staticmethod
+    def _due(step: int, after: int, freq: int) -> bool:
+        return freq > 0 and step >= after and (step - after) % freq == 0
+
+    def display_now(self, step):
+        return self._due(step, self.model.display_after_steps, self.model.display_frequency)
+
+    def test_now(self, step):
+        return self.test_net is not None and step > 0 and self._due(step, self.model.test_after_steps,
+                                                                   self.model.test_frequency)
+
+    def validate_now(self, step):
+        return self.val_net is not None and step > 0 and self._due(step, self.model.validation_after_steps,
+                                                                  self.model.validation_frequency)
+
+    # ---------------------------------------------------------------- steps
+    def train_one_batch(self, step: int) -> np.ndarray:
+        net = self.train_net
+        with Timer(self.dev) as tf:
+            outs = net.forward(training=True)
+            loss = net.total_loss(outs)
+        with Timer(self.dev) as tb:
+            self.store.zero_grad()
+            for _ in autograd.backward(loss):
+                pass
+            self.updater.update()
+            self.updater.step()
+        self.timers["forward"] += tf.ms
+        self.timers["backward"] += tb.ms
+        if self.sync is not None and self.sync.sync_now(step + 1):
+            with Timer(self.dev) as ts:
+                if isinstance(self.sync, RandomSync):
+                    self.sync.sync(step)
+                else:
+                    self.sync.sync()
+            self.timers["sync"] += ts.ms
+        autograd.training = False
+        return net.metrics()
+
+    def test(self, net: NeuralNet, nsteps: int, name: str) -> np.ndarray:
+        perf = Performance(name)
+        for _ in range(nsteps):
+            net.forward(training=False)
+            perf.update(net.metrics())
+        self.log(f"{perf.to_string()}")
+        return perf.avg()
+
+    def timer_info(self, nsteps: int) -> str:
+        n = max(1, nsteps)
+        return ("time per step: forward {:.2f} ms, backward+update {:.2f} ms, sync {:.2f} ms".format(
+            self.timers["forward"] / n, self.timers["backward"] / n, self.timers["sync"] / n))
+
+    def run(self, train_steps: Optional[int] = None) -> Dict[str, list]:
+        steps = train_steps if train_steps is not None else (self.model.train_steps or 0)
+        warm = min(self.model.updater.warmup_steps if self.sync is not None else 0, steps)
+        t0 = time.perf_counter()
+        for s in range(warm):  # local warm-up (no sync)
+            self.perf.update(self.train_one_batch(s))
+        if warm and isinstance(self.sync, RandomSync):
+            dt = (time.perf_counter() - t0) / warm
+            bw = self.cluster.bandwidth if self.cluster is not None and self.cluster.HasField("bandwidth") else None
+            self.sync.configure_bandwidth(dt, bw)
+        if self.sync is not None:
+            self.sync.bootstrap()
+        last = 0
+        for step in range(warm, steps):
+            if self.validate_now(step):
+                self.history.append(("validation", step, self.test(self.val_net, self.model.validation_steps,
+                                                                   "validation")))
+            if self.test_now(step):
+                self.history.append(("test", step, self.test(self.test_net, self.model.test_steps, "test")))
+            self.perf.update(self.train_one_batch(step))
+            if self.display_now(step):
+                self.log(f"step-{step} {self.perf.to_string()}")
+                self.log(self.timer_info(step - last + 1))
+                if self.model.debug:
+                    self.log(self.train_net.debug_info())
+                self.history.append(("train", step, self.perf.avg()))
+                self.perf.reset()
+                for k in self.timers:
+                    self.timers[k] = 0.0
+                last = step + 1
+        return {"history": self.history}

@@ -1,0 +1,144 @@
+"""Config-driven path: reference .conf parsing, NeuralNet construction and
+partitioning (reference src/test/test_neuralnet.cc expectations), Worker."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from singa_amd import autograd
+from singa_amd.config import schema
+from singa_amd.runtime import NeuralNet, Worker
+
+REF = "/root/reference/examples/mnist"
+
+
+def conv_test_net(partition=None):
+    """The 8-layer conv net of the reference NeuralNet tests."""
+    txt = """
+    layer { name: "data" type: "kShardData" data_param { batchsize: 8 path: "/nonexistent" } }
+    layer { name: "mnist" type: "kMnistImage" srclayers: "data" }
+    layer { name: "label" type: "kLabel" srclayers: "data" }
+    layer { name: "conv1" type: "kConvolution" srclayers: "mnist" param {} param {}
+            convolution_param { num_filters: 8 kernel: 2 } }
+    layer { name: "relu1" type: "kReLU" srclayers: "conv1" }
+    layer { name: "pool1" type: "kPooling" srclayers: "relu1" pooling_param { kernel: 4 stride: 2 } }
+    layer { name: "fc1" type: "kInnerProduct" srclayers: "pool1" param {} param {}
+            inner_product_param { num_output: 10 } }
+    layer { name: "loss" type: "kSoftmaxLoss" srclayers: "fc1" srclayers: "label" }
+    """
+    net = schema.parse_text("NetProto", txt)
+    for l in net.layer:
+        for p in l.param:
+            p.init_method = p.kUniform
+            p.low, p.high = -0.1, 0.1
+    if partition:
+        net.partition_type = partition
+    return net
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason="reference examples not mounted")
+@pytest.mark.parametrize("f,msg", [("mlp.conf", "ModelProto"), ("conv.conf", "ModelProto"),
+                                   ("cluster.conf", "ClusterProto"), ("topology.conf", "Topology")])
+def test_reference_confs_parse_unchanged(f, msg):
+    m = schema.read_text_file(msg, os.path.join(REF, f))
+    assert m.IsInitialized()
+    if msg == "ModelProto":
+        assert len(m.neuralnet.layer) > 0
+        assert schema.enum_name(m.updater, "type") == "kSGD"
+
+
+def test_proto2_defaults():
+    up = schema.new("UpdaterProto")
+    assert schema.enum_name(up, "type") == "kAdaGrad" and up.param_type == "Elastic" and up.warmup_steps == 10
+    assert schema.new("ClusterProto").start_port == 6723
+
+
+def test_neuralnet_no_partition():
+    net = NeuralNet(conv_test_net())
+    assert len(net.layers) == 8
+    assert net.layers[0].name == "data" and net.layers[-1].name == "loss"
+    assert net.shapes["conv1"] == (8, 8, 27, 27)
+    assert net.shapes["pool1"] == (8, 8, 12, 12)
+
+
+def test_neuralnet_data_partition_count():
+    net = NeuralNet(conv_test_net("kDataPartition"), group_size=3)
+    assert len(net.layers) == 28  # reference test_neuralnet.cc DataPartition
+    assert net.layers[0].name == "data"
+
+
+def _run(net, seed=0):
+    torch.manual_seed(seed)
+    for l in net.layers:
+        if l.is_data:
+            l.source.rng = np.random.RandomState(7)
+    autograd.training = True
+    outs = net.forward(True)
+    loss = net.total_loss(outs)
+    grads = {}
+    for p, g in autograd.backward(loss):
+        grads.setdefault(p.name, []).append(g.data.clone())
+    autograd.training = False
+    return float(loss.data), grads
+
+
+@pytest.mark.parametrize("ptype,g", [("kDataPartition", 2), ("kDataPartition", 4), ("kLayerPartition", 2)])
+def test_partitioned_equals_unpartitioned(ptype, g):
+    base = NeuralNet(conv_test_net(), seed=3)
+    part = NeuralNet(conv_test_net(ptype), group_size=g, seed=3)
+    # copy unpartitioned weights into the partitioned net's original layers
+    for l in base.layers:
+        if l.params and ptype == "kDataPartition":
+            for pl in part.layers:
+                if getattr(pl, "origin", None) is not None and pl.origin.name == l.name:
+                    for a, b in zip(pl.params, l.params):
+                        a.data.copy_(b.data)
+    if ptype == "kLayerPartition":
+        # partition slices were copied from the (seed-identical) original params at build
+        pass
+    lb, gb = _run(base)
+    lp, gp = _run(part)
+    assert abs(lb - lp) < 1e-4, (lb, lp)
+    if ptype == "kDataPartition":
+        for k, v in gb.items():
+            assert torch.allclose(v[0], sum(gp[k]), atol=1e-5), k
+
+
+def test_hybrid_partition_builds():
+    net = conv_test_net("kLayerPartition")
+    net.layer[-2].partition_type = "kDataPartition"
+    net.layer[-1].partition_type = "kDataPartition"
+    nn = NeuralNet(net, group_size=2)
+    types = [l.type_name for l in nn.layers]
+    assert "kSlice" in types and "kConcate" in types
+    loss, _ = _run(nn)
+    assert np.isfinite(loss)
+
+
+def test_worker_trains_lenet_style():
+    txt = """
+    name: "lenet-test" train_steps: 40 test_steps: 2 test_frequency: 20 display_frequency: 20
+    updater { base_learning_rate: 0.05 type: kSGD momentum: 0.9 learning_rate_change_method: kFixed }
+    neuralnet {
+      layer { name: "data" type: "kShardData" data_param { batchsize: 16 path: "/nonexistent" } }
+      layer { name: "mnist" type: "kMnistImage" srclayers: "data" mnist_param { norm_a: 255 norm_b: 0 } }
+      layer { name: "label" type: "kLabel" srclayers: "data" }
+      layer { name: "conv1" type: "kConvolution" srclayers: "mnist" convolution_param { num_filters: 8 kernel: 5 }
+              param { init_method: kUniformSqrtFanIn low: -1 high: 1 } param { init_method: kConstant value: 0 } }
+      layer { name: "pool1" type: "kPooling" srclayers: "conv1" pooling_param { pool: MAX kernel: 2 stride: 2 } }
+      layer { name: "ip1" type: "kInnerProduct" srclayers: "pool1" inner_product_param { num_output: 10 }
+              param { init_method: kUniformSqrtFanIn low: -1 high: 1 } param { init_method: kConstant value: 0 } }
+      layer { name: "loss" type: "kSoftmaxLoss" srclayers: "ip1" srclayers: "label" }
+    }"""
+    m = schema.parse_text("ModelProto", txt)
+    logs = []
+    w = Worker(m, data_override={"*": {"shape": (28, 28), "nclass": 10}}, log=logs.append)
+    # fixed batch so the net can memorise it
+    src = w.train_net.layers[0].source
+    img, lab = src.next()
+    src.next = lambda: (img, lab)
+    w.run()
+    train_hist = [h for h in w.history if h[0] == "train"]
+    assert train_hist[-1][2][0] < train_hist[0][2][0]
+    assert any(l.startswith("test:") for l in logs)
