@@ -82,11 +82,7 @@ class Communicator:
         if self.backend == "gloo":
             ins = list(inp.chunk(self.world_size))
             outs = list(out.chunk(self.world_size))
-            reqs = []
-            for r in range(self.world_size):
-                if r == self.rank:
-                    outs[r].copy_(ins[r])
-                    continue
+            outs[self.rank].copy_(ins[self.rank])
             # pairwise exchange through send/recv (gloo lacks all_to_all)
             for k in range(1, self.world_size):
                 dst = (self.rank + k) % self.world_size

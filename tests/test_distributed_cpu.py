@@ -1,0 +1,259 @@
+"""Multi-process (gloo, world_size 2) tests of the communication layer,
+synchronous data parallelism (DistOpt), EASGD and RandomSync.  The oracle is
+the reference's "rank 0 recomputes with gathered data" pattern
+(src/test/test_da.cc:38-61) or a single-process run on the global batch."""
+import numpy as np
+import pytest
+import torch
+
+from dist_util import run_ranks
+
+pytestmark = pytest.mark.timeout(600)
+
+
+# ----------------------------------------------------------------- collectives
+def _collectives(rank, world, comm):
+    out = {}
+    t = torch.arange(8, dtype=torch.float32) + 100 * rank
+    comm.all_reduce(t)
+    out["all_reduce"] = t.tolist()
+    b = torch.full((4,), float(rank + 1))
+    comm.broadcast(b, 1)
+    out["broadcast"] = b.tolist()
+    inp = torch.arange(world * 3, dtype=torch.float32) * (rank + 1)
+    rs = torch.empty(3)
+    comm.reduce_scatter(rs, inp)
+    out["reduce_scatter"] = rs.tolist()
+    ag = torch.empty(world * 2)
+    comm.all_gather(ag, torch.full((2,), float(rank)))
+    out["all_gather"] = ag.tolist()
+    a2a_in = torch.tensor([10.0 * rank + j for j in range(world)])
+    a2a_out = torch.empty(world)
+    comm.all_to_all(a2a_out, a2a_in)
+    out["all_to_all"] = a2a_out.tolist()
+    if rank == 0:
+        comm.send(torch.tensor([42.0, 43.0]), 1)
+    else:
+        r = torch.empty(2)
+        comm.recv(r, 0)
+        out["recv"] = r.tolist()
+    comm.barrier()
+    return out
+
+
+def test_collectives_gloo():
+    res = run_ranks(_collectives, 2)
+    exp_ar = [(2 * i + 100) for i in range(8)]
+    for r, o in enumerate(res):
+        assert o["all_reduce"] == exp_ar
+        assert o["broadcast"] == [2.0] * 4
+        full = [3 * i for i in range(6)]  # sum over ranks of i*(rank+1)
+        assert o["reduce_scatter"] == full[r * 3:(r + 1) * 3]
+        assert o["all_gather"] == [0.0, 0.0, 1.0, 1.0]
+        assert o["all_to_all"] == [10.0 * s + r for s in range(2)]
+    assert res[1]["recv"] == [42.0, 43.0]
+
+
+# ---------------------------------------------------------------- DistOpt DP
+def _mlp_model():
+    from singa_amd import layer, model
+
+    class MLP(model.Model):
+        def __init__(self):
+            super().__init__()
+            self.l1 = layer.Linear(32)
+            self.act = layer.ReLU()
+            self.l2 = layer.Linear(10)
+            self.loss = layer.SoftMaxCrossEntropy()
+
+        def forward(self, x):
+            return self.l2(self.act(self.l1(x)))
+
+        def train_one_batch(self, x, y):
+            out = self.forward(x)
+            l = self.loss(out, y)
+            self.optimizer(l)
+            return out, l
+
+    return MLP()
+
+
+def _data(n=16):
+    rng = np.random.RandomState(7)
+    return rng.randn(n, 20).astype(np.float32), rng.randint(0, 10, n).astype(np.int32)
+
+
+def _train(m, X, Y, steps, optim, seed=0):
+    from singa_amd import device, tensor
+
+    device.get_default_device().SetRandSeed(seed)
+    m.set_optimizer(optim)
+    tx, ty = tensor.from_numpy(X), tensor.from_numpy(Y)
+    m.compile([tx], is_train=True)
+    losses = []
+    for _ in range(steps):
+        _, l = m(tx, ty)
+        losses.append(float(l.data))
+    return {k: v.data.clone().numpy() for k, v in m.get_params().items()}, losses
+
+
+def _dp_rank(rank, world, comm, mode, bucket_mb):
+    from singa_amd import opt
+    from singa_amd.parallel import DistOpt
+
+    X, Y = _data()
+    n = X.shape[0] // world
+    m = _mlp_model()
+    d = DistOpt(opt.SGD(0.1, 0.9, weight_decay=1e-4), comm=comm, bucket_mb=bucket_mb, first_bucket_mb=bucket_mb,
+                overlap=(mode == "overlap"))
+    # different init per rank: attach() must broadcast rank 0's weights
+    params, losses = _train(m, X[rank * n:(rank + 1) * n], Y[rank * n:(rank + 1) * n], 4, d, seed=rank * 1234)
+    return params
+
+
+@pytest.mark.parametrize("mode,bucket_mb", [("overlap", 0.001), ("overlap", 32.0), ("sync", 0.001)])
+def test_distopt_equals_single_process(mode, bucket_mb):
+    from singa_amd import opt
+
+    X, Y = _data()
+    ref, _ = _train(_mlp_model(), X, Y, 4, opt.SGD(0.1, 0.9, weight_decay=1e-4))
+    res = run_ranks(_dp_rank, 2, mode, bucket_mb)
+    for r in range(2):
+        for k, v in ref.items():
+            np.testing.assert_allclose(res[r][k], v, rtol=1e-4, atol=1e-5, err_msg=f"rank {r} {k}")
+
+
+# ---------------------------------------------------------------- EASGD / RSync
+def _easgd_rank(rank, world, comm, sharded):
+    from singa_amd.opt import SGD
+    from singa_amd.parallel.easgd import ElasticSync
+    from singa_amd.tensor import Tensor
+
+    torch.manual_seed(0)
+    p = Tensor(data=torch.randn(64), requires_grad=True, stores_grad=True)
+    q = Tensor(data=torch.randn(10, 6), requires_grad=True, stores_grad=True)
+    o = SGD(0.1)
+    st = o.attach([p, q])
+    es = ElasticSync(st, comm, moving_rate=0.5, sharded=sharded)
+    es.bootstrap()
+    c0 = st.w.clone()
+    st.w.add_(float(rank + 1))  # diverge the workers
+    w_before = st.w.clone()
+    es.sync()
+    full_c = torch.empty_like(st.w)
+    if es.sharded:
+        comm.all_gather(full_c, es.centre)
+    else:
+        full_c.copy_(es.centre)
+    return c0.numpy(), w_before.numpy(), st.w.clone().numpy(), full_c.numpy(), es.alpha
+
+
+@pytest.mark.parametrize("sharded", [False, True])
+def test_easgd_matches_closed_form(sharded):
+    res = run_ranks(_easgd_rank, 2, sharded)
+    c0 = res[0][0]
+    alpha = res[0][4]
+    assert alpha == pytest.approx(0.25)
+    ds = [alpha * (wb - c0) for _, wb, _, _, _ in res]
+    for r, (_, wb, wa, c, _) in enumerate(res):
+        np.testing.assert_allclose(wa, wb - ds[r], rtol=1e-6, atol=1e-6)
+        np.testing.assert_allclose(c, c0 + ds[0] + ds[1], rtol=1e-6, atol=1e-6)
+
+
+def _rsync_rank(rank, world, comm, ratio):
+    from singa_amd.opt import SGD
+    from singa_amd.parallel.easgd import RandomSync
+    from singa_amd.tensor import Tensor
+
+    torch.manual_seed(0)
+    p = Tensor(data=torch.randn(101), requires_grad=True, stores_grad=True)
+    st = SGD(0.1).attach([p])
+    rs = RandomSync(st, comm, sample_ratio=ratio)
+    rs.bootstrap()
+    snap0 = st.w.clone()
+    st.w.add_(torch.arange(st.w.numel(), dtype=torch.float32) * (rank + 1) * 1e-3)
+    wb = st.w.clone()
+    rs.sync(step=5)
+    m, a, b = rs._progression(st.w.numel(), 5)
+    return snap0.numpy(), wb.numpy(), st.w.clone().numpy(), rs.snapshot.clone().numpy(), (m, a, b)
+
+
+@pytest.mark.parametrize("ratio", [0.3, 1.0])
+def test_random_sync(ratio):
+    res = run_ranks(_rsync_rank, 2, ratio)
+    snap0 = res[0][0]
+    n = snap0.size
+    m, a, b = res[0][4]
+    assert res[1][4] == (m, a, b)  # same sample on every rank, no index traffic
+    idx = (b + np.arange(m, dtype=np.int64) * a) % n
+    assert len(set(idx.tolist())) == m  # arithmetic progression with gcd(a,n)=1 has no duplicates
+    delta = sum(r[1] - snap0 for r in res)
+    for _, wb, wa, snap, _ in res:
+        exp = wb.copy()
+        exp[idx] = snap0[idx] + delta[idx]
+        np.testing.assert_allclose(wa, exp, rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(snap[idx], exp[idx], rtol=1e-5, atol=1e-6)
+
+
+# -------------------------------------------------- Worker with 2 EASGD groups
+MLP_CONF = """
+train_steps: 30
+display_frequency: 10
+updater { base_learning_rate: 0.05 type: kSGD momentum: 0.9 sync_frequency: 2 warmup_steps: 2 moving_rate: 0.5
+          param_type: "%s" }
+neuralnet {
+  layer { name: "data" type: "kSyntheticData" data_param { batchsize: 16 } }
+  layer { name: "mnist" type: "kMnistImage" srclayers: "data" mnist_param { norm_a: 255 norm_b: 0 } }
+  layer { name: "label" type: "kLabel" srclayers: "data" }
+  layer { name: "fc1" type: "kInnerProduct" srclayers: "mnist" inner_product_param { num_output: 32 }
+          param { name: "w1" init_method: kUniform low: -0.05 high: 0.05 }
+          param { name: "b1" init_method: kConstant value: 0 } }
+  layer { name: "tanh1" type: "kTanh" srclayers: "fc1" }
+  layer { name: "fc2" type: "kInnerProduct" srclayers: "tanh1" inner_product_param { num_output: 10 }
+          param { name: "w2" init_method: kUniform low: -0.05 high: 0.05 }
+          param { name: "b2" init_method: kConstant value: 0 } }
+  layer { name: "loss" type: "kSoftmaxLoss" srclayers: "fc2" srclayers: "label" softmaxloss_param { topk: 1 } }
+}
+"""
+
+
+def _worker_rank(rank, world, comm, ptype):
+    from singa_amd.config import schema
+    from singa_amd.runtime import Worker
+
+    mp_ = schema.parse_text("ModelProto", MLP_CONF % ptype)
+    w = Worker(mp_, comm=comm, log=lambda s: None, seed=rank,
+               data_override={"*": {"shape": (8, 8), "nclass": 10, "seed": 3}})
+    hist = w.run()
+    losses = [float(m[0]) for kind, _, m in hist["history"] if kind == "train"]
+    return losses, w.sync.nsync, w.store.w.clone().numpy()
+
+
+@pytest.mark.parametrize("ptype", ["Elastic", "RandomSync"])
+def test_worker_two_groups(ptype):
+    res = run_ranks(_worker_rank, 2, ptype)
+    for losses, nsync, _ in res:
+        assert nsync >= 10
+        assert losses[-1] < losses[0]
+    if ptype == "Elastic":  # elastic force keeps the groups close to each other
+        spread = np.abs(res[0][2] - res[1][2]).mean()
+        assert spread < 0.05
+
+
+# ------------------------------------------------------------- liveness
+def _hb_rank(rank, world, comm):
+    import time
+
+    import torch.distributed as dist
+
+    store = dist.distributed_c10d._get_default_store()
+    comm.start_heartbeat(store, period_s=0.1)
+    time.sleep(0.3)
+    comm.barrier()
+    alive = comm.dead_ranks(timeout_s=5.0, store=store)
+    comm.stop_heartbeat()
+    return alive
+
+
+def test_heartbeat_all_alive():
+    assert run_ranks(_hb_rank, 2) == [[], []]
