@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import builtins as _b
 import math
+import heapq
 from collections import Counter, deque
 from typing import Callable, Dict, Iterator, List, Optional, Sequence, Tuple
 
@@ -38,6 +39,14 @@ ACCUMULATED = object()  # backward() returned: grad already added to the param's
 
 def _as_tuple(x):
     return x if isinstance(x, tuple) else (x,)
+
+
+_SEQ = [0]
+
+
+def _next_seq() -> int:
+    _SEQ[0] += 1
+    return _SEQ[0]
 
 
 class Operator:
@@ -74,6 +83,7 @@ class Operator:
         if self.requires_grad:
             self.n_out = len(outs)
             self._yid = {id(o): i for i, o in enumerate(outs)}
+            self._seq = _next_seq()
         return outs[0] if len(outs) == 1 else outs
 
     def grad_target(self, i: int) -> Optional[torch.Tensor]:
@@ -155,29 +165,63 @@ def is_unit(dy) -> bool:
     return dy is None or getattr(dy, "_sg_unit", False)
 
 
-def backward(y: Tensor, dy: Optional[Tensor] = None) -> Iterator[Tuple[Tensor, Tensor]]:
-    """Generator of (param, grad) in the order gradients complete."""
-    if y.creator is None:
+def backward(y, dy=None) -> Iterator[Tuple[Tensor, Tensor]]:
+    """Generator of (param, grad) in the order gradients complete.
+
+    ``y`` may be one tensor or a list of roots (with a matching list ``dy``;
+    ``None`` seeds a loss with ones).  Ready operators run in decreasing
+    forward order (a max-heap on the forward sequence number): gradients
+    complete from the last layer backwards, which is what bucketed
+    all-reduce overlap wants, and it gives every process the same global
+    order, which the cross-process bridge operators rely on (see
+    :mod:`singa_amd.runtime.neuralnet`)."""
+    roots = list(y) if isinstance(y, (list, tuple)) else [y]
+    dys = list(dy) if isinstance(dy, (list, tuple)) else [dy] * len(roots)
+    heap: List = []
+    pending: Dict[Operator, list] = {}
+    puses: Counter = Counter()
+    for r, d in zip(roots, dys):
+        if r is None or r.creator is None:
+            continue
+        op0 = r.creator
+        if op0 not in pending:
+            pending[op0] = [None] * op0.n_out
+        if d is None:
+            g0 = torch.ones_like(r.data)
+            g0._sg_unit = True
+        else:
+            g0 = d.data if isinstance(d, Tensor) else d
+        j = op0._yid.get(id(r), 0)
+        pending[op0][j] = _accum(pending[op0][j], g0)
+    if not pending:
         return
-    op0 = y.creator
-    deps = infer_dependency(op0)
-    puses = _param_uses(op0)
-    if dy is None:
-        g0 = torch.ones_like(y.data)
-        g0._sg_unit = True
-    else:
-        g0 = dy.data if isinstance(dy, Tensor) else dy
-    pending: Dict[Operator, list] = {op0: [None] * op0.n_out}
-    pending[op0][op0._yid.get(id(y), 0)] = g0
+    # dependency counts / param uses over the union of the root subgraphs
+    deps = Counter()
+    seen = set(pending)
+    q = deque(pending)
+    while q:
+        cur = q.popleft()
+        for p in cur.params:
+            if p is not None:
+                puses[id(p)] += 1
+        for src_op, _ in cur.src:
+            if src_op is None:
+                continue
+            deps[src_op] += 1
+            if src_op not in seen:
+                seen.add(src_op)
+                q.append(src_op)
+    for op0 in pending:
+        if deps[op0] == 0:
+            heapq.heappush(heap, (-getattr(op0, "_seq", 0), id(op0), op0))
     pgrad: Dict[int, object] = {}
-    ready = deque([op0])
-    while ready:
-        op = ready.popleft()
-        dys = pending.pop(op)
-        if all(d is None for d in dys):
+    while heap:
+        op = heapq.heappop(heap)[2]
+        dys_ = pending.pop(op)
+        if all(d is None for d in dys_) and not getattr(op, "always_run", False):
             dxs = (None,) * len(op.src)
         else:
-            dxs = _as_tuple(op.backward(*dys))
+            dxs = _as_tuple(op.backward(*dys_))
         if len(dxs) != len(op.src):
             raise RuntimeError(f"{op.name}: backward returned {len(dxs)} grads for {len(op.src)} inputs")
         for i, ((src_op, stores), dx) in enumerate(zip(op.src, dxs)):
@@ -211,7 +255,7 @@ def backward(y: Tensor, dy: Optional[Tensor] = None) -> Iterator[Tuple[Tensor, T
             pending[src_op][j] = _accum(pending[src_op][j], dx)
             deps[src_op] -= 1
             if deps[src_op] == 0:
-                ready.append(src_op)
+                heapq.heappush(heap, (-getattr(src_op, "_seq", 0), id(src_op), src_op))
 
 
 def gradients(y: Tensor, dy: Optional[Tensor] = None) -> Dict[Tensor, Tensor]:

@@ -29,11 +29,30 @@ import torch.distributed as dist
 
 
 class Communicator:
-    def __init__(self, world_size: int, rank: int, local_rank: int, backend: str, group=None):
+    def __init__(self, world_size: int, rank: int, local_rank: int, backend: str, group=None,
+                 ranks: Optional[List[int]] = None):
         self.world_size, self.rank, self.local_rank, self.backend = world_size, rank, local_rank, backend
         self.group = group
+        self.ranks = list(ranks) if ranks is not None else list(range(world_size))  # local -> global rank
         self._hb_thread = None
         self._hb_stop = threading.Event()
+
+    def split(self, ranks: List[int]) -> Optional["Communicator"]:
+        """Sub-communicator over ``ranks`` (global ranks, ascending); every
+        rank must call this collectively with the same list.  Returns None
+        on non-members.  Ranks inside the sub-communicator are 0..len-1."""
+        ranks = sorted(int(r) for r in ranks)
+        if self.world_size == 1:
+            return Communicator(1, 0, self.local_rank, self.backend) if self.rank in ranks else None
+        grp = dist.new_group(ranks=ranks, backend=self.backend) if len(ranks) > 1 else None
+        if self.rank not in ranks:
+            return None
+        if len(ranks) == 1:
+            return Communicator(1, 0, self.local_rank, self.backend, None, ranks)
+        return Communicator(len(ranks), ranks.index(self.rank), self.local_rank, self.backend, grp, ranks)
+
+    def _g(self, r: int) -> int:
+        return self.ranks[r]
 
     # ---------------------------------------------------------- collectives
     def all_reduce(self, t: torch.Tensor, op: str = "sum", async_op: bool = False):
@@ -49,7 +68,7 @@ class Communicator:
     def broadcast(self, t: torch.Tensor, src: int = 0, async_op: bool = False):
         if self.world_size == 1:
             return None
-        return dist.broadcast(t, src, group=self.group, async_op=async_op)
+        return dist.broadcast(t, self._g(src), group=self.group, async_op=async_op)
 
     def reduce_scatter(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = False):
         """inp: flat [world*n] -> out [n] (sum)."""
@@ -87,25 +106,25 @@ class Communicator:
             for k in range(1, self.world_size):
                 dst = (self.rank + k) % self.world_size
                 src = (self.rank - k) % self.world_size
-                s = dist.isend(ins[dst].contiguous(), dst, group=self.group)
+                s = dist.isend(ins[dst].contiguous(), self._g(dst), group=self.group)
                 buf = torch.empty_like(outs[src])
-                dist.recv(buf, src, group=self.group)
+                dist.recv(buf, self._g(src), group=self.group)
                 outs[src].copy_(buf)
                 s.wait()
             return None
         return dist.all_to_all_single(out, inp, group=self.group)
 
     def send(self, t: torch.Tensor, dst: int):
-        return dist.send(t, dst, group=self.group)
+        return dist.send(t, self._g(dst), group=self.group)
 
     def recv(self, t: torch.Tensor, src: int):
-        return dist.recv(t, src, group=self.group)
+        return dist.recv(t, self._g(src), group=self.group)
 
     def isend(self, t: torch.Tensor, dst: int):
-        return dist.isend(t, dst, group=self.group)
+        return dist.isend(t, self._g(dst), group=self.group)
 
     def irecv(self, t: torch.Tensor, src: int):
-        return dist.irecv(t, src, group=self.group)
+        return dist.irecv(t, self._g(src), group=self.group)
 
     def barrier(self):
         if self.world_size > 1:

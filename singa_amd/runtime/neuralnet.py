@@ -111,11 +111,18 @@ class _PGraph:
 
 class NeuralNet:
     def __init__(self, net_proto, group_size: int = 1, phase: str = "kTrain", dev=None,
-                 data_override: Optional[dict] = None, seed: int = 0, devices: Optional[List] = None):
+                 data_override: Optional[dict] = None, seed: int = 0, devices: Optional[List] = None,
+                 comm=None):
         from ..device import get_default_device
 
         self.dev = dev or get_default_device()
-        self.devices = devices  # per-location device list (placement, P6)
+        self.devices = devices  # per-location device list (placement, P6, one process)
+        # group communicator: locations are owned by the group's processes
+        # (location l -> group rank l % size), bridges become p2p send/recv
+        self.comm = comm if comm is not None and comm.world_size > 1 else None
+        self.dist = self.comm is not None
+        if self.dist:
+            group_size = max(group_size, self.comm.world_size)
         self.group_size = group_size
         self.phase = phase
         default_pt = schema.enum_name(net_proto, "partition_type")
@@ -147,6 +154,8 @@ class NeuralNet:
                         raise ValueError("batch override is not supported for shard-backed data layers")
         self._construct()
         self.partitioned = group_size > 1 and any(l.partition_type != "kNone" for l in self.layers)
+        self.placed = len({l.locationid for l in self.layers}) > 1
+        self.partitioned = self.partitioned or self.placed  # placement alone still needs bridges
         if self.partitioned:
             self._partition()
         self._assign_param_ids()
@@ -328,9 +337,18 @@ class NeuralNet:
         self.num_params = pid
 
     # -------------------------------------------------------------- execute
+    def _rank_of(self, loc: int) -> int:
+        return loc % self.comm.world_size
+
+    def is_local(self, l: RefLayer) -> bool:
+        return not self.dist or self._rank_of(l.locationid) == self.comm.rank
+
     def params(self) -> List[Tensor]:
+        """Parameters of the layers this process executes."""
         out, seen = [], set()
         for l in self.layers:
+            if not self.is_local(l):
+                continue
             for p in l.params:
                 if id(p) not in seen:
                     seen.add(id(p))
@@ -338,13 +356,30 @@ class NeuralNet:
         return out
 
     def loss_layers(self) -> List[RefLayer]:
-        return [l for l in self.layers if l.is_loss]
+        return [l for l in self.layers if l.is_loss and self.is_local(l)]
 
     def forward(self, training: bool = True) -> Dict[str, object]:
-        """Run every layer in topological order; returns name -> output."""
+        """Run every (local) layer in the global topological order; returns
+        name -> output.  Cross-process bridges send/receive (see
+        :mod:`singa_amd.parallel.bridge`); cross-device inputs are moved."""
+        from ..parallel import bridge as B
+
         autograd.training = training
         outs: Dict[str, object] = {}
+        self._extra_roots = []
+        self._pending = getattr(self, "_pending", [])
         for l in self.layers:
+            if not self.is_local(l):
+                continue
+            ldev = self._dev_of(l.locationid)
+            if self.dist and l.type_name == "kBridgeDst":
+                src = self.name2layer[l.srcs[0]]
+                if not self.is_local(src):
+                    y = B.BridgeRecv(self.comm, self._rank_of(src.locationid), self._pending)(ldev)
+                    if y.requires_grad:
+                        self._extra_roots.append((y, torch.zeros_like(y.data)))
+                    outs[l.name] = y
+                    continue
             xs = []
             for s in l.srcs:
                 o = outs[s]
@@ -352,10 +387,79 @@ class NeuralNet:
                     src = self.name2layer[s]
                     dsts = getattr(src, "graph_dsts", None) or self.dsts.get(s, [])
                     o = o[dsts.index(l.name)]
+                if isinstance(o, Tensor) and o.data.device != ldev.torch_device:
+                    o = B.to_device(o, ldev)
                 xs.append(o)
+            if self.dist and l.type_name == "kBridgeSrc":
+                dst = self.name2layer[l.graph_dsts[0]]
+                if not self.is_local(dst):
+                    r = B.bridge_send(xs[0], self.comm, self._rank_of(dst.locationid), self._pending)
+                    if r is not None:
+                        self._extra_roots.append((r, None))
+                    outs[l.name] = xs[0]
+                    continue
             outs[l.name] = l.forward(xs, training)
         self.outputs = outs
         return outs
+
+    def backward_roots(self, outs) -> tuple:
+        """(roots, seeds) for :func:`autograd.backward`: the local loss plus,
+        in a distributed group, every bridge endpoint."""
+        roots, seeds = [], []
+        loss = self.total_loss(outs)
+        if loss is not None:
+            roots.append(loss)
+            seeds.append(None)
+        for t, d in getattr(self, "_extra_roots", []):
+            roots.append(t)
+            seeds.append(d)
+        return roots, seeds
+
+    def finish_step(self) -> None:
+        """Complete outstanding bridge sends."""
+        from ..parallel import bridge as B
+
+        B.wait_all(getattr(self, "_pending", []))
+
+    def replica_keys(self) -> List[tuple]:
+        """(base layer, param index, numel) of every data-partition-replicated
+        parameter, in the same order on every process of the group."""
+        keys = []
+        for l in self.layers:
+            base = getattr(l, "origin", None)
+            if base is None or base.partition_type != "kDataPartition" or not base.params:
+                continue
+            if any(k[0] is base for k in keys):
+                continue
+            for i, p in enumerate(base.params):
+                keys.append((base, i, p.data.numel()))
+        return keys
+
+    def sync_replica_grads(self) -> None:
+        """Sum the gradients of data-partition replicas held by different
+        processes of the group (the reference ParamManager aggregated
+        shared-param gradients in-process, param_manager.cc:169-187)."""
+        if not self.dist:
+            return
+        keys = getattr(self, "_rkeys", None)
+        if keys is None:
+            keys = self._rkeys = self.replica_keys()
+        if not keys:
+            return
+        held = {id(p) for p in self.params()}
+        total = sum(k[2] for k in keys)
+        buf = torch.zeros(total, dtype=torch.float32, device=self.dev.torch_device)
+        o = 0
+        spans = []
+        for base, i, n in keys:
+            p = base.params[i]
+            if id(p) in held and p.grad_view is not None:
+                buf[o:o + n].copy_(p.grad_view.reshape(-1))
+                spans.append((p, o, n))
+            o += n
+        self.comm.all_reduce(buf)
+        for p, o, n in spans:
+            p.grad_view.copy_(buf[o:o + n].reshape(p.grad_view.shape))
 
     def total_loss(self, outs) -> Optional[Tensor]:
         losses = [outs[l.name] for l in self.loss_layers()]
@@ -367,20 +471,26 @@ class NeuralNet:
         return tot
 
     def metrics(self) -> np.ndarray:
-        """[loss, precision] summed over loss layers (reference metric blob)."""
+        """[loss, precision] summed over loss layers (reference metric blob);
+        summed over the processes of a distributed group."""
         m = np.zeros(2, np.float64)
         for l in self.loss_layers():
             if hasattr(l, "metric"):
                 m += np.array([float(l.metric[0]), float(l.metric[1])]) * (l.loss_scale if l.loss_scale else 1)
+        if self.dist:
+            t = torch.tensor(m, dtype=torch.float32, device=self.dev.torch_device)
+            self.comm.all_reduce(t)
+            m = t.cpu().double().numpy()
         return m
 
     def share_weights(self, other: "NeuralNet") -> None:
         """Share parameter storage with ``other`` (test/validation nets)."""
         src = {}
-        for l in other.layers:
+        for l in other.layers:  # exact layer (incl. partition replicas) first, then its origin
+            src.setdefault(l.name, l.params)
             src.setdefault(getattr(l, "origin", l).name, l.params)
         for l in self.layers:
-            key = getattr(l, "origin", l).name
+            key = l.name if l.name in src else getattr(l, "origin", l).name
             if key in src and len(src[key]) == len(l.params):
                 for a, b in zip(l.params, src[key]):
                     a.data = b.data

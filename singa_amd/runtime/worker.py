@@ -78,10 +78,15 @@ class Worker:
     def __init__(self, model_proto, cluster_proto=None, dev=None, comm: Optional[Communicator] = None,
                  data_override: Optional[dict] = None, log: Callable[[str], None] = print, group_size: int = 1,
                  seed: int = 0):
+        from .cluster import Cluster
+
         self.model = model_proto
-        self.cluster = cluster_proto
+        self.cluster_proto = cluster_proto
         self.dev = dev or get_default_device()
         self.comm = comm or init_distributed()
+        self.cluster = Cluster(cluster_proto, self.comm, make_folders=cluster_proto is not None)
+        if self.cluster.nprocs_per_group() > 1:
+            group_size = max(group_size, self.cluster.nprocs_per_group())
         self.log = log
         self.group_size = group_size
         self.data_override = data_override or {}
@@ -96,16 +101,24 @@ class Worker:
 
     def _setup(self):
         net = self.model.neuralnet
+        cl = self.cluster
+        self.group_comm = cl.group_comm if cl.nprocs_per_group() > 1 else None
+        self.peer_comm = cl.peer_comm if cl.world > 1 else None
+        if self.peer_comm is None and cl.world > 1 and cl.nprocs_per_group() == 1:
+            self.peer_comm = self.comm
+        # same weights-init seed inside a group (replicas/slices must agree),
+        # a different data seed per group
         self.train_net = NeuralNet(net, self.group_size, "kTrain", self.dev, self.data_override,
-                                   seed=self.seed + self.comm.rank)
+                                   seed=self.seed + cl.groupid(), comm=self.group_comm)
         self.test_net = None
         self.val_net = None
-        if self.model.test_steps and self.model.test_frequency:
-            self.test_net = NeuralNet(net, 1, "kTest", self.dev, self.data_override, seed=self.seed + 1)
-            self.test_net.share_weights(self.train_net)
-        if self.model.validation_steps and self.model.validation_frequency:
-            self.val_net = NeuralNet(net, 1, "kValidation", self.dev, self.data_override, seed=self.seed + 2)
-            self.val_net.share_weights(self.train_net)
+        eval_group = cl.groupid() == 0  # group 0 tests / validates (worker.h:141-158)
+        if self.model.test_steps and self.model.test_frequency and eval_group:
+            self.test_net = NeuralNet(net, self.group_size, "kTest", self.dev, self.data_override,
+                                      seed=self.seed + 1, comm=self.group_comm)
+        if self.model.validation_steps and self.model.validation_frequency and eval_group:
+            self.val_net = NeuralNet(net, self.group_size, "kValidation", self.dev, self.data_override,
+                                     seed=self.seed + 2, comm=self.group_comm)
         self.updater = make_updater(self.model.updater)
         self.store = self.updater.attach(self.train_net.params())
         for n in (self.test_net, self.val_net):
@@ -113,12 +126,18 @@ class Worker:
                 n.share_weights(self.train_net)
         up = self.model.updater
         self.sync = None
-        if self.comm.world_size > 1:
-            if up.param_type == "RandomSync":
-                self.sync = RandomSync(self.store, self.comm, 1.0, up.sync_frequency, up.warmup_steps)
+        self.sync_dp = False
+        pc = self.peer_comm
+        if pc is not None and pc.world_size > 1:
+            if cl.synchronous():  # P10: gradient all-reduce across groups every step
+                self.sync_dp = True
+                pc.broadcast(self.store.w, 0)
+                self.store.sync_low()
+            elif up.param_type == "RandomSync":
+                self.sync = RandomSync(self.store, pc, 1.0, up.sync_frequency, up.warmup_steps)
             else:
-                self.sync = ElasticSync(self.store, self.comm, up.moving_rate or 0.9, up.sync_frequency,
-                                        up.warmup_steps)
+                self.sync = ElasticSync(self.store, pc, up.moving_rate or 0.9, up.sync_frequency,
+                                        up.warmup_steps, sharded=cl.sharded_centre())
         self.perf = Performance("train")
 
     # ------------------------------------------------------------- cadence
@@ -142,12 +161,19 @@ class Worker:
         net = self.train_net
         with Timer(self.dev) as tf:
             outs = net.forward(training=True)
-            loss = net.total_loss(outs)
+            roots, seeds = net.backward_roots(outs)
         with Timer(self.dev) as tb:
             self.store.zero_grad()
-            for _ in autograd.backward(loss):
-                pass
-            self.updater.update()
+            if roots:
+                for _ in autograd.backward(roots, seeds):
+                    pass
+            net.finish_step()
+            net.sync_replica_grads()
+            scale = 1.0
+            if self.sync_dp:
+                self.peer_comm.all_reduce(self.store.g)
+                scale = 1.0 / self.peer_comm.world_size
+            self.updater.update(grad_scale=scale)
             self.updater.step()
         self.timers["forward"] += tf.ms
         self.timers["backward"] += tb.ms
@@ -182,7 +208,8 @@ class Worker:
             self.perf.update(self.train_one_batch(s))
         if warm and isinstance(self.sync, RandomSync):
             dt = (time.perf_counter() - t0) / warm
-            bw = self.cluster.bandwidth if self.cluster is not None and self.cluster.HasField("bandwidth") else None
+            cp = self.cluster_proto
+            bw = cp.bandwidth if cp is not None and cp.HasField("bandwidth") else None
             self.sync.configure_bandwidth(dt, bw)
         if self.sync is not None:
             self.sync.bootstrap()

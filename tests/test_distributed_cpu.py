@@ -257,3 +257,83 @@ def _hb_rank(rank, world, comm):
 
 def test_heartbeat_all_alive():
     assert run_ranks(_hb_rank, 2) == [[], []]
+
+
+# ------------------------------- a partitioned / placed net across processes
+PART_CONF = """
+train_steps: 6
+display_frequency: 1
+updater { base_learning_rate: 0.1 type: kSGD momentum: 0.9 weight_decay: 0.0001 warmup_steps: 1 sync_frequency: 2 }
+neuralnet {
+  %s
+  layer { name: "data" type: "kSyntheticData" data_param { batchsize: 8 } }
+  layer { name: "mnist" type: "kMnistImage" srclayers: "data" mnist_param { norm_a: 255 norm_b: 0 } }
+  layer { name: "label" type: "kLabel" srclayers: "data" }
+  layer { name: "fc1" type: "kInnerProduct" srclayers: "mnist" inner_product_param { num_output: 12 }
+          param { name: "w1" init_method: kUniform low: -0.2 high: 0.2 }
+          param { name: "b1" init_method: kUniform low: -0.1 high: 0.1 } }
+  layer { name: "tanh1" type: "kTanh" srclayers: "fc1" }
+  layer { name: "fc2" type: "kInnerProduct" srclayers: "tanh1" inner_product_param { num_output: 10 } %s
+          param { name: "w2" init_method: kUniform low: -0.2 high: 0.2 }
+          param { name: "b2" init_method: kUniform low: -0.1 high: 0.1 } }
+  layer { name: "loss" type: "kSoftmaxLoss" srclayers: "fc2" srclayers: "label" %s }
+}
+"""
+
+
+def _part_conf(kind):
+    if kind == "none":
+        return PART_CONF % ("", "", "")
+    if kind == "placement":  # P6: fc2 + loss on location 1
+        return PART_CONF % ("", "locationid: 1", "locationid: 1")
+    return PART_CONF % (f"partition_type: {kind}", "", "")
+
+
+def _part_worker(rank, world, comm, kind, nppg):
+    from singa_amd.config import schema
+    from singa_amd.runtime import Worker
+
+    m = schema.parse_text("ModelProto", _part_conf(kind))
+    cp = schema.new("ClusterProto")
+    cp.nworkers, cp.nprocs_per_group, cp.workspace = world, nppg, ""
+    w = Worker(m, cp, comm=comm, log=lambda s: None, seed=0,
+               data_override={"*": {"shape": (6, 6), "nclass": 10, "seed": 5}})
+    src = [l for l in w.train_net.layers if l.is_data and w.train_net.is_local(l)]
+    if src:  # a fixed batch
+        s = src[0].source
+        img, lab = s.next()
+        s.next = lambda: (img, lab)
+    w.run()
+    return [float(h[2][0]) for h in w.history if h[0] == "train"]
+
+
+def _single_losses(kind):
+    from singa_amd.config import schema
+    from singa_amd.parallel import communicator
+    from singa_amd.runtime import Worker
+
+    communicator.reset()
+    m = schema.parse_text("ModelProto", _part_conf("none"))
+    w = Worker(m, log=lambda s: None, seed=0, data_override={"*": {"shape": (6, 6), "nclass": 10, "seed": 5}})
+    s = w.train_net.layers[0].source
+    img, lab = s.next()
+    s.next = lambda: (img, lab)
+    w.run()
+    return [float(h[2][0]) for h in w.history if h[0] == "train"]
+
+
+@pytest.mark.parametrize("kind", ["kDataPartition", "kLayerPartition", "placement"])
+def test_partitioned_net_across_processes(kind):
+    ref = _single_losses(kind)
+    res = run_ranks(_part_worker, 2, kind, 2)
+    assert ref[-1] < ref[0]
+    for r in range(2):
+        np.testing.assert_allclose(res[r], ref, rtol=2e-4, atol=2e-5, err_msg=f"rank {r}")
+
+
+def test_two_groups_of_two_procs_easgd():
+    """4 processes: 2 worker groups x 2 processes (data partition inside a
+    group, EASGD between groups)."""
+    res = run_ranks(_part_worker, 4, "kDataPartition", 2)
+    assert res[0] == res[1] and res[2] == res[3]  # one loss per group
+    assert res[0][-1] < res[0][0] and res[2][-1] < res[2][0]
