@@ -61,6 +61,12 @@ PYBIND11_MODULE(_core, m) {
         return n;
       });
 
+  m.def("load_mnist", &LoadMnist, py::arg("imagefile"), py::arg("labelfile"), py::arg("folder"),
+        py::arg("limit") = 0, py::call_guard<py::gil_scoped_release>());
+  m.def("split_shard", &SplitShard, py::arg("num"), py::arg("input"), py::arg("prefix"),
+        py::call_guard<py::gil_scoped_release>());
+  m.def("split_shard_n", &SplitShardN, py::arg("n"), py::arg("input"), py::arg("prefix"),
+        py::call_guard<py::gil_scoped_release>());
   py::class_<Graph>(m, "Graph")
       .def(py::init<>())
       .def("add_node", &Graph::AddNode)

@@ -63,6 +63,12 @@ bool DecodeRecord(const std::string& bytes, ImageRecord* r);
 // Decode one record into a float buffer of `dim` values: pixel bytes are read
 // as UNSIGNED (fixes reference quirk: RGBImageLayer casts through signed char,
 // src/worker/layer.cc:599); `data` floats are used if present.
+// Loader (C28): MNIST idx -> shard; Split / SplitN of a shard folder.
+int64_t LoadMnist(const std::string& imagefile, const std::string& labelfile, const std::string& folder,
+                  int64_t limit = 0);
+std::vector<int64_t> SplitShard(int64_t num, const std::string& input, const std::string& prefix);
+std::vector<int64_t> SplitShardN(int nshards, const std::string& input, const std::string& prefix);
+
 bool DecodeRecordToFloat(const std::string& bytes, float* out, int64_t dim, float scale, float bias, int32_t* label);
 
 class Prefetcher {

@@ -190,6 +190,7 @@ class _DataLayerBase(RefLayer):
 
     def forward(self, xs, training):
         img, lab = self.source.next()
+        self.draws = getattr(self, "draws", 0) + 1  # batches consumed (checkpoint fast-forward)
         return {"image": Tensor(device=self.dev, data=torch.from_numpy(np.ascontiguousarray(img)),
                                 requires_grad=False),
                 "label": Tensor(device=self.dev, data=torch.from_numpy(lab), requires_grad=False)}

@@ -19,6 +19,7 @@ torch.distributed ranks (servers are replaced by collectives).
 """
 from __future__ import annotations
 
+import os
 import time
 from typing import Callable, Dict, Optional
 
@@ -93,6 +94,8 @@ class Worker:
         self.seed = seed
         self.timers = {"forward": 0.0, "backward": 0.0, "sync": 0.0}
         self.history = []
+        self.checkpoint_path = ""
+        self.checkpoint_every = 0
         self._setup()
 
     # ------------------------------------------------------------------ setup
@@ -200,27 +203,45 @@ class Worker:
         return ("time per step: forward {:.2f} ms, backward+update {:.2f} ms, sync {:.2f} ms".format(
             self.timers["forward"] / n, self.timers["backward"] / n, self.timers["sync"] / n))
 
+    def _after_step(self, step: int) -> None:
+        """Periodic checkpoint + fault injection (tests of the recovery path:
+        SINGA_AMD_FAULT_STEP / SINGA_AMD_FAULT_RANK make that rank die at
+        that step unless the run was resumed)."""
+        if self.checkpoint_path and self.checkpoint_every and (step + 1) % self.checkpoint_every == 0:
+            from .checkpoint import save_worker
+
+            self.step = step + 1
+            save_worker(self, self.checkpoint_path.replace("{rank}", str(self.comm.rank)))
+        fs = os.environ.get("SINGA_AMD_FAULT_STEP")
+        if fs is not None and int(fs) == step and not getattr(self, "start_step", 0):
+            if int(os.environ.get("SINGA_AMD_FAULT_RANK", "0")) == self.comm.rank:
+                os._exit(17)
+
     def run(self, train_steps: Optional[int] = None) -> Dict[str, list]:
         steps = train_steps if train_steps is not None else (self.model.train_steps or 0)
+        start = int(getattr(self, "start_step", 0))
         warm = min(self.model.updater.warmup_steps if self.sync is not None else 0, steps)
         t0 = time.perf_counter()
-        for s in range(warm):  # local warm-up (no sync)
+        for s in range(start, warm):  # local warm-up (no sync)
+            self.step = s
             self.perf.update(self.train_one_batch(s))
-        if warm and isinstance(self.sync, RandomSync):
-            dt = (time.perf_counter() - t0) / warm
+        if warm > start and isinstance(self.sync, RandomSync):
+            dt = (time.perf_counter() - t0) / (warm - start)
             cp = self.cluster_proto
             bw = cp.bandwidth if cp is not None and cp.HasField("bandwidth") else None
             self.sync.configure_bandwidth(dt, bw)
-        if self.sync is not None:
+        if self.sync is not None and not getattr(self.sync, "resumed", False):
             self.sync.bootstrap()
-        last = 0
-        for step in range(warm, steps):
+        last = max(warm, start)
+        for step in range(max(warm, start), steps):
+            self.step = step
             if self.validate_now(step):
                 self.history.append(("validation", step, self.test(self.val_net, self.model.validation_steps,
                                                                    "validation")))
             if self.test_now(step):
                 self.history.append(("test", step, self.test(self.test_net, self.model.test_steps, "test")))
             self.perf.update(self.train_one_batch(step))
+            self._after_step(step)
             if self.display_now(step):
                 self.log(f"step-{step} {self.perf.to_string()}")
                 self.log(self.timer_info(step - last + 1))
@@ -231,4 +252,5 @@ class Worker:
                 for k in self.timers:
                     self.timers[k] = 0.0
                 last = step + 1
+        self.step = steps
         return {"history": self.history}
