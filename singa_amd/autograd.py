@@ -906,6 +906,32 @@ class Flatten(Operator):
         return dy.reshape(self.in_shape)
 
 
+class Attention(Operator):
+    """Scaled dot-product attention softmax(q k^T * scale + mask) v over
+    [..., S, D] heads (mask: additive, non-differentiable).  bf16 on the GPU
+    runs batched MFMA GEMMs + the softmax kernels (functional.attention_*)."""
+
+    def __init__(self, scale: Optional[float] = None, name=None):
+        super().__init__(name)
+        self.scale = scale
+
+    def forward(self, q, k, v, mask=None):
+        o, p = F.attention_fwd(q, k, v, mask, self.scale)
+        if self.requires_grad:
+            self.saved = (q, k, v, p)
+        return o
+
+    def backward(self, do):
+        q, k, v, p = self.saved
+        self.saved = None
+        dq, dk, dv = F.attention_bwd(q, k, v, p, do.contiguous(), self.scale)
+        return (dq, dk, dv) + ((None,) if len(self.src) == 4 else ())
+
+
+def attention(q, k, v, mask=None, scale=None):
+    return Attention(scale)(q, k, v, mask) if mask is not None else Attention(scale)(q, k, v)
+
+
 class TorchFn(Operator):
     """Generic differentiable op defined by a PyTorch function of the raw
     inputs (used for shape/glue ops that need no hand-written kernel)."""

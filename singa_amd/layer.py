@@ -44,9 +44,12 @@ class Layer:
             self.__dict__.setdefault("_layers", OrderedDict())[key] = value
             if value.name is None:
                 value.name = key
-        elif isinstance(value, (list, tuple)) and value and all(isinstance(v, Layer) for v in value):
+        elif (isinstance(value, (list, tuple)) and any(isinstance(v, Layer) for v in value)
+              and all(isinstance(v, Layer) or v is None for v in value)):
             d = self.__dict__.setdefault("_layers", OrderedDict())
             for i, v in enumerate(value):
+                if v is None:
+                    continue
                 d[f"{key}.{i}"] = v
                 if v.name is None:
                     v.name = f"{key}.{i}"

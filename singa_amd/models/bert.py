@@ -1,0 +1,169 @@
+"""BERT encoder (Devlin et al. 2019) -- the north-star ``sonnx`` model
+family (SURVEY §7.2 phase 10: MatMul, Softmax, LayerNorm, GELU, Add,
+Reshape/Transpose, Gather).  BERT-base: 12 layers, hidden 768, 12 heads,
+FFN 3072, vocab 30522, 512 positions.
+
+GPU bf16 path: every projection is the MFMA GEMM with a fused bias epilogue,
+attention is batched MFMA GEMMs + the softmax kernels (autograd.Attention),
+LayerNorm / GELU / dropout are the hand-written kernels; fp32 master weights
+in the flat ParamStore.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+
+from .. import autograd, layer, model
+from ..tensor import Tensor
+
+
+class SplitHeads(autograd.Operator):
+    """[B, S, 3*H*D] -> q, k, v each [B, H, S, D] (contiguous)."""
+
+    def __init__(self, heads: int, name=None):
+        super().__init__(name)
+        self.h = heads
+
+    def forward(self, x):
+        B, S, E3 = x.shape
+        D = E3 // (3 * self.h)
+        t = x.view(B, S, 3, self.h, D).permute(2, 0, 3, 1, 4)
+        return t[0].contiguous(), t[1].contiguous(), t[2].contiguous()
+
+    def backward(self, dq, dk, dv):
+        ref = next(d for d in (dq, dk, dv) if d is not None)
+        B, H, S, D = ref.shape
+        parts = [d if d is not None else torch.zeros_like(ref) for d in (dq, dk, dv)]
+        return torch.stack(parts, 0).permute(1, 3, 0, 2, 4).reshape(B, S, 3 * H * D)
+
+
+class MergeHeads(autograd.Operator):
+    """[B, H, S, D] -> [B, S, H*D]."""
+
+    def forward(self, x):
+        B, H, S, D = x.shape
+        return x.permute(0, 2, 1, 3).reshape(B, S, H * D)
+
+    def backward(self, dy):
+        B, S, E = dy.shape
+        H = self.h
+        return dy.view(B, S, H, E // H).permute(0, 2, 1, 3).contiguous()
+
+    def __call__(self, x):
+        self.h = x.shape[1]
+        return super().__call__(x)
+
+
+class EncoderLayer(layer.Layer):
+    def __init__(self, hidden: int, heads: int, ffn: int, dropout: float = 0.1):
+        super().__init__()
+        self.heads = heads
+        self.qkv = layer.Linear(3 * hidden)
+        self.proj = layer.Linear(hidden)
+        self.ln1 = layer.LayerNorm(1e-12)
+        self.fc1 = layer.Linear(ffn)
+        self.act = layer.Gelu()
+        self.fc2 = layer.Linear(hidden)
+        self.ln2 = layer.LayerNorm(1e-12)
+        self.drop1 = layer.Dropout(dropout)
+        self.drop2 = layer.Dropout(dropout)
+
+    def forward(self, x, mask: Optional[Tensor] = None):
+        q, k, v = SplitHeads(self.heads)(self.qkv(x))
+        a = autograd.attention(q, k, v, mask)
+        a = self.drop1(self.proj(MergeHeads()(a)))
+        x = self.ln1(autograd.add(x, a))
+        f = self.drop2(self.fc2(self.act(self.fc1(x))))
+        return self.ln2(autograd.add(x, f))
+
+
+class Embeddings(layer.Layer):
+    def __init__(self, vocab: int, hidden: int, max_pos: int, type_vocab: int, dropout: float):
+        super().__init__()
+        self.vocab, self.hidden, self.max_pos, self.type_vocab = vocab, hidden, max_pos, type_vocab
+        self.ln = layer.LayerNorm(1e-12)
+        self.drop = layer.Dropout(dropout)
+
+    def initialize(self, ids, types=None):
+        dev = ids.device
+        for name, n in (("word", self.vocab), ("position", self.max_pos), ("token_type", self.type_vocab)):
+            W = Tensor((n, self.hidden), dev, requires_grad=True, stores_grad=True)
+            W.gaussian(0.0, 0.02)
+            self._param(name, W, wd_mult=0.0)
+
+    def forward(self, ids, types=None):
+        B, S = ids.shape
+        pos = Tensor(data=torch.arange(S, device=ids.data.device).unsqueeze(0).expand(B, S), device=ids.device,
+                     requires_grad=False)
+        e = autograd.add(autograd.embedding(ids, self.word), autograd.embedding(pos, self.position))
+        if types is None:
+            types = Tensor(data=torch.zeros((B, S), dtype=torch.int64, device=ids.data.device), device=ids.device,
+                           requires_grad=False)
+        e = autograd.add(e, autograd.embedding(types, self.token_type))
+        return self.drop(self.ln(e))
+
+
+class Bert(model.Model):
+    def __init__(self, vocab: int = 30522, hidden: int = 768, layers: int = 12, heads: int = 12, ffn: int = 3072,
+                 max_pos: int = 512, type_vocab: int = 2, num_labels: int = 2, dropout: float = 0.1,
+                 compute_dtype=torch.bfloat16):
+        super().__init__()
+        self.compute_dtype = compute_dtype
+        self.embeddings = Embeddings(vocab, hidden, max_pos, type_vocab, dropout)
+        self.encoder = [EncoderLayer(hidden, heads, ffn, dropout) for _ in range(layers)]
+        self.pooler = layer.Linear(hidden)
+        self.pool_act = layer.Tanh()
+        self.classifier = layer.Linear(num_labels)
+        self.loss_fn = layer.SoftMaxCrossEntropy()
+
+    def encode(self, ids, mask=None, types=None):
+        x = self.embeddings(ids, types)
+        if x.data.is_cuda and x.dtype != self.compute_dtype:
+            x = autograd.cast(x, self.compute_dtype)
+        m = None
+        if mask is not None:  # [B, S] of 1/0 -> additive [B, 1, 1, S]
+            md = mask.data if isinstance(mask, Tensor) else mask
+            m = Tensor(data=((1.0 - md.float()) * -10000.0).view(md.shape[0], 1, 1, md.shape[1]), device=ids.device,
+                       requires_grad=False)
+        for blk in self.encoder:
+            x = blk(x, m)
+        return x
+
+    def forward(self, ids, mask=None, types=None):
+        x = self.encode(ids, mask, types)
+        cls = TorchCLS()(x)
+        return self.classifier(self.pool_act(self.pooler(cls)))
+
+    def train_one_batch(self, ids, y, mask=None):
+        out = self.forward(ids, mask)
+        loss = self.loss_fn(out, y)
+        self.optimizer(loss)
+        return out, loss
+
+
+class TorchCLS(autograd.Operator):
+    """x[:, 0] (the [CLS] token)."""
+
+    def forward(self, x):
+        self.shape = x.shape
+        return x[:, 0].contiguous()
+
+    def backward(self, dy):
+        dx = torch.zeros(self.shape, dtype=dy.dtype, device=dy.device)
+        dx[:, 0] = dy
+        return dx
+
+
+def bert_base(**kw) -> Bert:
+    return Bert(**kw)
+
+
+def bert_tiny(**kw) -> Bert:
+    kw = {**dict(vocab=1000, hidden=128, layers=2, heads=2, ffn=512, max_pos=128), **kw}
+    return Bert(**kw)
+
+
+def create_model(size: str = "base", **kw) -> Bert:
+    return bert_base(**kw) if size == "base" else bert_tiny(**kw)

@@ -787,3 +787,75 @@ def lrn_bwd(x: torch.Tensor, dy: torch.Tensor, norm: torch.Tensor, size: int, al
     s = sum(pad[:, i:i + x.shape[1]] for i in range(size))
     dx = g * norm.pow(-beta) - 2 * beta * alpha / size * xf * s
     return dx.to(dy.dtype)
+
+
+# ---------------------------------------------------------------- attention
+def _bgemm(a, b, M, Nn, K, batch, ako, bko, lda, ldb, sa, sb, alpha=1.0, out_dtype=torch.bfloat16, out=None,
+           beta=0.0):
+    """Batched C[i] = alpha * A[i] B[i] (+ beta C) on the MFMA kernel (bf16 operands)."""
+    c = out if out is not None else torch.empty((batch, M, Nn), dtype=out_dtype, device=a.device)
+    mode = 0 if c.dtype == torch.bfloat16 else 1
+    N.lib().gemm(a.data_ptr(), lda, ako, b.data_ptr(), ldb, bko, c.data_ptr(), Nn, M, Nn, K, alpha, beta, 0, 0,
+                 mode, 1, batch, sa, sb, M * Nn, N.stream())
+    return c
+
+
+def _attn_native_ok(q, k, v):
+    return (_native_ok(q, k, v) and q.dtype == torch.bfloat16 and k.dtype == q.dtype and v.dtype == q.dtype
+            and q.shape[-1] % 8 == 0 and q.shape[-2] % 8 == 0 and k.shape[-2] % 8 == 0)
+
+
+def attention_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, mask: Optional[torch.Tensor] = None,
+                  scale: Optional[float] = None):
+    """softmax(q k^T * scale + mask) v for q [..., Sq, D], k/v [..., Sk, D];
+    mask broadcastable to [..., Sq, Sk] (additive).  Returns (o, p) with the
+    probabilities p kept for backward."""
+    D = q.shape[-1]
+    scale = (1.0 / math.sqrt(D)) if scale is None else scale
+    lead = q.shape[:-2]
+    Sq, Sk = q.shape[-2], k.shape[-2]
+    if _attn_native_ok(q, k, v):
+        q3 = q.reshape(-1, Sq, D).contiguous()
+        k3 = k.reshape(-1, Sk, D).contiguous()
+        v3 = v.reshape(-1, Sk, D).contiguous()
+        B = q3.shape[0]
+        s = _bgemm(q3, k3, Sq, Sk, D, B, 0, 0, D, D, Sq * D, Sk * D, alpha=scale, out_dtype=torch.float32)
+        if mask is not None:
+            s = (s.view(*lead, Sq, Sk) + mask.to(torch.float32)).reshape(B, Sq, Sk)
+        p = softmax(s).to(torch.bfloat16)
+        o = _bgemm(p, v3, Sq, D, Sk, B, 0, 1, Sk, D, Sq * Sk, Sk * D)
+        return o.view(*lead, Sq, D), p.view(*lead, Sq, Sk)
+    s = torch.matmul(q.float(), k.float().transpose(-1, -2)) * scale
+    if mask is not None:
+        s = s + mask.float()
+    p = torch.softmax(s, dim=-1)
+    o = torch.matmul(p, v.float())
+    return o.to(q.dtype), p.to(q.dtype)
+
+
+def attention_bwd(q, k, v, p, do, scale: Optional[float] = None):
+    """Gradients (dq, dk, dv) of attention_fwd given the saved probabilities."""
+    D = q.shape[-1]
+    scale = (1.0 / math.sqrt(D)) if scale is None else scale
+    Sq, Sk = q.shape[-2], k.shape[-2]
+    if _attn_native_ok(q, k, v) and p.dtype == torch.bfloat16 and do.dtype == torch.bfloat16:
+        q3 = q.reshape(-1, Sq, D).contiguous()
+        k3 = k.reshape(-1, Sk, D).contiguous()
+        v3 = v.reshape(-1, Sk, D).contiguous()
+        p3 = p.reshape(-1, Sq, Sk).contiguous()
+        do3 = do.reshape(-1, Sq, D).contiguous()
+        B = q3.shape[0]
+        # dV = P^T dO ; dP = dO V^T
+        dv = _bgemm(p3, do3, Sk, D, Sq, B, 1, 1, Sk, D, Sq * Sk, Sq * D)
+        dp = _bgemm(do3, v3, Sq, Sk, D, B, 0, 0, D, D, Sq * D, Sk * D)
+        ds = softmax_bwd(p3, dp)  # P * (dP - rowsum(dP * P)), bf16
+        dq = _bgemm(ds, k3, Sq, D, Sk, B, 0, 1, Sk, D, Sq * Sk, Sk * D, alpha=scale)
+        dk = _bgemm(ds, q3, Sk, D, Sq, B, 1, 1, Sk, D, Sq * Sk, Sq * D, alpha=scale)
+        return dq.view(q.shape), dk.view(k.shape), dv.view(v.shape)
+    pf, dof = p.float(), do.float()
+    dv = torch.matmul(pf.transpose(-1, -2), dof)
+    dp = torch.matmul(dof, v.float().transpose(-1, -2))
+    ds = pf * (dp - (dp * pf).sum(-1, keepdim=True))
+    dq = torch.matmul(ds, k.float()) * scale
+    dk = torch.matmul(ds.transpose(-1, -2), q.float()) * scale
+    return dq.to(q.dtype), dk.to(k.dtype), dv.to(v.dtype)
