@@ -42,6 +42,7 @@ def _as_tuple(x):
 
 
 _SEQ = [0]
+_TRACE: list = []  # stack of op-record lists (sonnx.to_onnx tracing)
 
 
 def _next_seq() -> int:
@@ -84,6 +85,8 @@ class Operator:
             self.n_out = len(outs)
             self._yid = {id(o): i for i, o in enumerate(outs)}
             self._seq = _next_seq()
+        if _TRACE:  # sonnx export: record (op, inputs, outputs)
+            _TRACE[-1].append((self, xs, outs))
         return outs[0] if len(outs) == 1 else outs
 
     def grad_target(self, i: int) -> Optional[torch.Tensor]:
@@ -936,10 +939,12 @@ class TorchFn(Operator):
     """Generic differentiable op defined by a PyTorch function of the raw
     inputs (used for shape/glue ops that need no hand-written kernel)."""
 
-    def __init__(self, fn: Callable, name=None, nondiff: Sequence[int] = ()):
+    def __init__(self, fn: Callable, name=None, nondiff: Sequence[int] = (), onnx: Optional[dict] = None):
         super().__init__(name)
         self.fn = fn
         self.nondiff = set(nondiff)
+        # export spec for sonnx: {"op": type, "attrs": {...}, "inputs": [("in", i) | ("const", array)]}
+        self.onnx = onnx
 
     def forward(self, *xs):
         if not self.requires_grad:
@@ -1126,18 +1131,26 @@ def layer_norm(x, g=None, b=None, eps=1e-5):
     return LayerNorm(eps)(x, *args)
 
 
-def _fn(fn, *xs, nondiff=()):
-    return TorchFn(fn, nondiff=nondiff)(*xs)
+def _fn(fn, *xs, nondiff=(), onnx=None):
+    return TorchFn(fn, nondiff=nondiff, onnx=onnx)(*xs)
+
+
+def _ox(op, attrs=None, inputs=None, n_in=1):
+    """sonnx export spec; default inputs: the op's tensor inputs in order."""
+    return {"op": op, "attrs": attrs or {}, "inputs": inputs if inputs is not None else
+            [("in", i) for i in range(n_in)]}
 
 
 def transpose(x, shape=None):
     perm = tuple(shape) if shape is not None else tuple(reversed(range(x.ndim())))
-    return _fn(lambda a: a.permute(*perm), x)
+    return _fn(lambda a: a.permute(*perm), x, onnx=_ox("Transpose", {"perm": list(perm)}))
 
 
 def squeeze(x, axis=None):
+    ax = None if axis is None else ([axis] if isinstance(axis, int) else list(axis))
+    spec = _ox("Squeeze") if ax is None else _ox("Squeeze", inputs=[("in", 0), ("const", np.asarray(ax, np.int64))])
     return _fn(lambda a: a.squeeze() if axis is None else a.squeeze(axis if isinstance(axis, int) else tuple(axis)),
-               x)
+               x, onnx=spec)
 
 
 def unsqueeze(x, axis):
@@ -1147,18 +1160,19 @@ def unsqueeze(x, axis):
         for d in sorted(ax):
             a = a.unsqueeze(d)
         return a
-    return _fn(f, x)
+    return _fn(f, x, onnx=_ox("Unsqueeze", inputs=[("in", 0), ("const", np.asarray(ax, np.int64))]))
 
 
 def cat(xs, axis=0):
-    return TorchFn(lambda *a: torch.cat(a, dim=axis))(*xs)
+    return TorchFn(lambda *a: torch.cat(a, dim=axis), onnx=_ox("Concat", {"axis": axis}, n_in=len(xs)))(*xs)
 
 
 concat = cat
 
 
 def split(x, axis, parts):
-    return TorchFn(lambda a: tuple(torch.split(a, parts, dim=axis)))(x)
+    return TorchFn(lambda a: tuple(torch.split(a, parts, dim=axis)),
+                   onnx=_ox("Split", {"axis": axis}, [("in", 0), ("const", np.asarray(parts, np.int64))]))(x)
 
 
 def slice(x, starts, ends, axes=None, steps=None):  # noqa: A001
@@ -1172,7 +1186,11 @@ def slice(x, starts, ends, axes=None, steps=None):  # noqa: A001
             e = _b.min(e, n) if e >= 0 else e
             idx[ax] = builtins_slice(s, e, st)
         return a[tuple(idx)]
-    return _fn(f, x)
+    big = 2 ** 62
+    spec = _ox("Slice", inputs=[("in", 0), ("const", np.asarray(starts, np.int64)),
+                                ("const", np.asarray([e if e < big else big for e in ends], np.int64)),
+                                ("const", np.asarray(axes, np.int64)), ("const", np.asarray(steps, np.int64))])
+    return _fn(f, x, onnx=spec)
 
 
 builtins_slice = _b.slice
@@ -1181,15 +1199,18 @@ builtins_slice = _b.slice
 def gather(x, axis, indices):
     idx = torch.as_tensor(indices, device=x.data.device).long()
     return _fn(lambda a: torch.index_select(a, axis, idx.reshape(-1)).reshape(
-        a.shape[:axis] + tuple(idx.shape) + a.shape[axis + 1:]), x)
+        a.shape[:axis] + tuple(idx.shape) + a.shape[axis + 1:]), x,
+        onnx=_ox("Gather", {"axis": axis}, [("in", 0), ("const", idx.cpu().numpy())]))
 
 
 def tile(x, repeats):
-    return _fn(lambda a: a.repeat(*repeats), x)
+    return _fn(lambda a: a.repeat(*repeats), x,
+               onnx=_ox("Tile", inputs=[("in", 0), ("const", np.asarray(repeats, np.int64))]))
 
 
 def expand(x, shape):
-    return _fn(lambda a: a.expand(*shape), x)
+    return _fn(lambda a: a.expand(*shape), x,
+               onnx=_ox("Expand", inputs=[("in", 0), ("const", np.asarray(shape, np.int64))]))
 
 
 def pad(x, mode="constant", pads=None, constant=0.0):
@@ -1199,33 +1220,44 @@ def pad(x, mode="constant", pads=None, constant=0.0):
     for i in reversed(range(n)):
         tp += [pads[i], pads[i + half]]
     m = {"constant": "constant", "reflect": "reflect", "edge": "replicate"}[mode]
+    spec = _ox("Pad", {"mode": mode}, [("in", 0), ("const", np.asarray(pads, np.int64)),
+                                        ("const", np.asarray(constant, np.float32))])
     return _fn(lambda a: torch.nn.functional.pad(a, tp, mode=m, value=constant) if m == "constant"
-               else torch.nn.functional.pad(a, tp, mode=m), x)
+               else torch.nn.functional.pad(a, tp, mode=m), x, onnx=spec)
 
 
 def clip(x, min=None, max=None):  # noqa: A002
-    return _fn(lambda a: torch.clamp(a, min=min, max=max), x)
+    ins = [("in", 0), ("const", np.asarray(-3.4e38 if min is None else min, np.float32)),
+           ("const", np.asarray(3.4e38 if max is None else max, np.float32))]
+    return _fn(lambda a: torch.clamp(a, min=min, max=max), x, onnx=_ox("Clip", inputs=ins))
 
 
 def where(x, y, condition):
     c = condition.data if isinstance(condition, Tensor) else torch.as_tensor(condition)
-    return _fn(lambda a, b: torch.where(c.to(a.device).bool(), a, b), x, y)
+    spec = _ox("Where", inputs=[("const", c.bool().cpu().numpy()), ("in", 0), ("in", 1)])
+    return _fn(lambda a, b: torch.where(c.to(a.device).bool(), a, b), x, y, onnx=spec)
 
 
 def reduce_sum(x, axes=None, keepdims=1):
-    return _fn(lambda a: a.sum(dim=tuple(axes), keepdim=bool(keepdims)) if axes is not None else a.sum(), x)
+    ins = [("in", 0)] + ([("const", np.asarray(axes, np.int64))] if axes is not None else [])
+    return _fn(lambda a: a.sum(dim=tuple(axes), keepdim=bool(keepdims)) if axes is not None else a.sum(), x,
+               onnx=_ox("ReduceSum", {"keepdims": int(keepdims) if axes is not None else 0}, ins))
 
 
 def reduce_mean(x, axes=None, keepdims=1):
-    return _fn(lambda a: a.mean(dim=tuple(axes), keepdim=bool(keepdims)) if axes is not None else a.mean(), x)
+    at = {"keepdims": int(keepdims) if axes is not None else 0}
+    if axes is not None:
+        at["axes"] = list(axes)
+    return _fn(lambda a: a.mean(dim=tuple(axes), keepdim=bool(keepdims)) if axes is not None else a.mean(), x,
+               onnx=_ox("ReduceMean", at))
 
 
 def sum(*xs):  # noqa: A001
-    return TorchFn(lambda *a: _b.sum(a[1:], a[0]))(*xs)
+    return TorchFn(lambda *a: _b.sum(a[1:], a[0]), onnx=_ox("Sum", n_in=len(xs)))(*xs)
 
 
 def mean(*xs):
-    return TorchFn(lambda *a: _b.sum(a[1:], a[0]) / len(a))(*xs)
+    return TorchFn(lambda *a: _b.sum(a[1:], a[0]) / len(a), onnx=_ox("Mean", n_in=len(xs)))(*xs)
 
 
 def max(*xs):  # noqa: A001
@@ -1234,7 +1266,7 @@ def max(*xs):  # noqa: A001
         for t in a[1:]:
             r = torch.maximum(r, t)
         return r
-    return TorchFn(f)(*xs)
+    return TorchFn(f, onnx=_ox("Max", n_in=len(xs)))(*xs)
 
 
 def min(*xs):  # noqa: A001
@@ -1243,79 +1275,80 @@ def min(*xs):  # noqa: A001
         for t in a[1:]:
             r = torch.minimum(r, t)
         return r
-    return TorchFn(f)(*xs)
+    return TorchFn(f, onnx=_ox("Min", n_in=len(xs)))(*xs)
 
 
 def erf(x):
-    return _fn(torch.erf, x)
+    return _fn(torch.erf, x, onnx=_ox("Erf"))
 
 
 def cos(x):
-    return _fn(torch.cos, x)
+    return _fn(torch.cos, x, onnx=_ox("Cos"))
 
 
 def sin(x):
-    return _fn(torch.sin, x)
+    return _fn(torch.sin, x, onnx=_ox("Sin"))
 
 
 def tan(x):
-    return _fn(torch.tan, x)
+    return _fn(torch.tan, x, onnx=_ox("Tan"))
 
 
 def cosh(x):
-    return _fn(torch.cosh, x)
+    return _fn(torch.cosh, x, onnx=_ox("Cosh"))
 
 
 def sinh(x):
-    return _fn(torch.sinh, x)
+    return _fn(torch.sinh, x, onnx=_ox("Sinh"))
 
 
 def acos(x):
-    return _fn(torch.acos, x)
+    return _fn(torch.acos, x, onnx=_ox("Acos"))
 
 
 def asin(x):
-    return _fn(torch.asin, x)
+    return _fn(torch.asin, x, onnx=_ox("Asin"))
 
 
 def atan(x):
-    return _fn(torch.atan, x)
+    return _fn(torch.atan, x, onnx=_ox("Atan"))
 
 
 def acosh(x):
-    return _fn(torch.acosh, x)
+    return _fn(torch.acosh, x, onnx=_ox("Acosh"))
 
 
 def asinh(x):
-    return _fn(torch.asinh, x)
+    return _fn(torch.asinh, x, onnx=_ox("Asinh"))
 
 
 def atanh(x):
-    return _fn(torch.atanh, x)
+    return _fn(torch.atanh, x, onnx=_ox("Atanh"))
 
 
 def ceil(x):
-    return _fn(torch.ceil, x)
+    return _fn(torch.ceil, x, onnx=_ox("Ceil"))
 
 
 def floor(x):
-    return _fn(torch.floor, x)
+    return _fn(torch.floor, x, onnx=_ox("Floor"))
 
 
 def round(x):  # noqa: A001
-    return _fn(torch.round, x)
+    return _fn(torch.round, x, onnx=_ox("Round"))
 
 
 def softsign(x):
-    return _fn(lambda a: a / (1 + a.abs()), x)
+    return _fn(lambda a: a / (1 + a.abs()), x, onnx=_ox("Softsign"))
 
 
 def hardsigmoid(x, alpha=0.2, gamma=0.5):
-    return _fn(lambda a: torch.clamp(alpha * a + gamma, 0, 1), x)
+    return _fn(lambda a: torch.clamp(alpha * a + gamma, 0, 1), x,
+               onnx=_ox("HardSigmoid", {"alpha": float(alpha), "beta": float(gamma)}))
 
 
 def prelu(x, slope):
-    return _fn(lambda a, s: torch.where(a > 0, a, a * s), x, slope)
+    return _fn(lambda a, s: torch.where(a > 0, a, a * s), x, slope, onnx=_ox("PRelu", n_in=2))
 
 
 def _cmp_op(fn):
@@ -1361,20 +1394,23 @@ def upsample(x, mode, scales):
 
     def f(a):
         return torch.nn.functional.interpolate(a, scale_factor=sc[2:], mode="nearest")
-    return _fn(f, x)
+    return _fn(f, x, onnx=_ox("Resize", {"mode": "nearest"}, [("in", 0), ("const", np.zeros(0, np.float32)),
+                                                              ("const", np.asarray(sc, np.float32))]))
 
 
 def depth_to_space(x, blocksize, mode="DCR"):
-    return _fn(lambda a: torch.nn.functional.pixel_shuffle(a, blocksize), x)
+    return _fn(lambda a: torch.nn.functional.pixel_shuffle(a, blocksize), x,
+               onnx=_ox("DepthToSpace", {"blocksize": blocksize, "mode": "CRD"}))
 
 
 def space_to_depth(x, blocksize, mode="DCR"):
-    return _fn(lambda a: torch.nn.functional.pixel_unshuffle(a, blocksize), x)
+    return _fn(lambda a: torch.nn.functional.pixel_unshuffle(a, blocksize), x,
+               onnx=_ox("SpaceToDepth", {"blocksize": blocksize}))
 
 
 def embedding(x_idx, W):
-    idx = x_idx.data.long()
-    return TorchFn(lambda w: torch.nn.functional.embedding(idx, w))(W)
+    return TorchFn(lambda w, i: torch.nn.functional.embedding(i.long(), w), nondiff=(1,),
+                   onnx=_ox("Gather", {"axis": 0}, n_in=2))(W, x_idx)
 
 
 def globalaveragepool(x, keepdims=True):
@@ -1383,7 +1419,9 @@ def globalaveragepool(x, keepdims=True):
 
 def scatter_elements(x, indices, updates, axis=0):
     idx = indices.data.long()
-    return TorchFn(lambda a, u: a.scatter(axis, idx, u))(x, updates)
+    return TorchFn(lambda a, u: a.scatter(axis, idx, u),
+                   onnx=_ox("ScatterElements", {"axis": axis}, [("in", 0), ("const", idx.cpu().numpy()),
+                                                                ("in", 1)]))(x, updates)
 
 
 def gemm(A, B, C=None, alpha=1.0, beta=1.0, transA=0, transB=0):

@@ -70,6 +70,7 @@ def test_bert_tiny_gpu_matches_cpu_loss(gpu):
     ids_np = rng.randint(0, 1000, (4, 64)).astype(np.int64)
     y_np = rng.randint(0, 2, 4).astype(np.int32)
     losses = []
+    init = None
     for dev in (device.get_default_device(), device.create_rocm_gpu()):
         dev.SetRandSeed(3)
         m = bert.bert_tiny(dropout=0.0, compute_dtype=torch.bfloat16)
@@ -77,6 +78,10 @@ def test_bert_tiny_gpu_matches_cpu_loss(gpu):
         y = tensor.from_numpy(y_np).to_device(dev)
         m.set_optimizer(opt.SGD(0.01, 0.9))
         m.compile([ids], is_train=True)
+        if init is None:  # CPU and GPU generators differ: start the GPU model from the CPU weights
+            init = {k: v.data.clone() for k, v in m.get_states().items()}
+        else:
+            m.set_states(init)
         ls = []
         for _ in range(6):
             _, l = m(ids, y)
