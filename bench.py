@@ -33,7 +33,10 @@ def main() -> int:
     ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
     ap.add_argument("--depth", type=int, default=50)
     ap.add_argument("--image", type=int, default=224)
-    ap.add_argument("--no-graph", action="store_true", help="eager execution instead of HIP-graph replay")
+    ap.add_argument("--graph", dest="graph", action="store_true", default=None,
+                    help="HIP-graph replay of forward+backward (default for 1 GPU)")
+    ap.add_argument("--no-graph", dest="graph", action="store_false",
+                    help="eager execution; the default for N>1, where bucketed all-reduces overlap the backward")
     ap.add_argument("--lr", type=float, default=0.1)
     args = ap.parse_args()
 
@@ -71,7 +74,10 @@ def main() -> int:
     tx = tensor.from_numpy(x, dev)
     ty = tensor.from_numpy(y, dev)
 
-    use_graph = not args.no_graph
+    # 1 GPU: graph replay (no launch overhead).  N>1: eager, so each gradient
+    # bucket's RCCL all-reduce starts as soon as backward has produced it and
+    # overlaps the rest of the backward (a captured graph would defer it).
+    use_graph = args.graph if args.graph is not None else world == 1
     m.compile([tx], is_train=True, use_graph=use_graph)
     m.train()
 

@@ -89,3 +89,25 @@ def test_bert_tiny_gpu_matches_cpu_loss(gpu):
         losses.append(ls)
     assert abs(losses[0][0] - losses[1][0]) < 5e-2 * max(1, abs(losses[0][0])), losses
     assert losses[1][-1] < losses[1][0]
+
+
+def test_sonnx_import_runs_on_gpu(gpu):
+    """ResNet-18 exported on the CPU, imported on the MI355X: same logits
+    (the GPU conv runs bf16 MFMA internally)."""
+    from singa_amd import autograd, sonnx
+    from singa_amd.models import resnet
+    from singa_amd.sonnx import onnx_proto as P
+
+    cpu = device.get_default_device()
+    cpu.SetRandSeed(0)
+    x = tensor.from_numpy(np.random.RandomState(0).randn(4, 3, 32, 32).astype(np.float32))
+    m = resnet.resnet18(num_classes=10)
+    m.compile([x], is_train=False)
+    autograd.training = False
+    ref = m.forward(x).data.float().numpy()
+    blob = sonnx.to_onnx(m, [x]).SerializeToString()
+    rep = sonnx.prepare(P.load_model(blob), device.create_rocm_gpu())
+    out = rep.run([x.data.numpy()])[0]
+    assert out.data.is_cuda
+    err = np.abs(out.data.float().cpu().numpy() - ref).max() / (np.abs(ref).max() + 1e-6)
+    assert err < 5e-2, err
