@@ -70,6 +70,7 @@ void sg_conv_dgrad(const void*, const void*, void*, int, int, int, int, int, int
                    int, int, int, hipStream_t);
 void sg_conv_wgrad(const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int, int,
                    int, int, int, hipStream_t);
+void sg_set_tuning(int key, int value);
 }
 
 static void check_launch(const char* what) {
@@ -233,4 +234,5 @@ PYBIND11_MODULE(_C, m) {
     sg_conv_wgrad(CV(x), CV(dy), V(dw_out), N, H, W, C, K, R, Sd, Ho, Wo, sh, sw, ph, pw, dh, dw, splits, S(s));
     CHK("conv_wgrad");
   });
+  m.def("set_tuning", [](int key, int value) { sg_set_tuning(key, value); });
 }

@@ -96,10 +96,28 @@ __device__ __forceinline__ int kouter_swz(int krow, int chunk) {
 __device__ __forceinline__ uint4 sel(bool ok, uint4 v) { return ok ? v : make_uint4(0, 0, 0, 0); }
 
 // ------------------------------------------------------------------------------
-// Operand loader: ROWS = tile rows of this operand, VPT 16-byte vectors/thread.
-// KMAJOR kinds: thread t owns rows (t>>3)+32v, k-chunk t&7.
-// KOUTER kinds: thread t owns k-rows t/CPR + (256/CPR)v, col chunk t%CPR.
+// Operand loader: ROWS = tile rows of this operand, VPT 16-byte vectors/thread,
+// staged global -> LDS directly with global_load_lds_dwordx4 (no registers,
+// no ds_write, no zero-select: out-of-range / padding vectors read a zero
+// page).  One wave-instruction fills 1 KB of LDS at (wave-uniform base +
+// lane*16), so each operand image is laid out lane-linearly and the XOR
+// swizzle is applied to the SOURCE chunk each lane fetches:
+//   KMAJOR kinds: thread t owns rows (t>>3)+32v, LDS slot t&7 holds k-chunk
+//                 (t&7) ^ swz(row)           (a wave = 8 rows x 128 B)
+//   KOUTER kinds: thread t owns k-rows t/CPR + (256/CPR)v, LDS slot t%CPR
+//                 holds column chunk (t%CPR) ^ swz(k-row)
+// Conv gathers cache each vector's row pointer for the current filter tap and
+// recompute it only when the (wave-uniform) tap changes.
 // ------------------------------------------------------------------------------
+__device__ __attribute__((aligned(16))) uint4 sg_zero_page[4];
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef const __attribute__((address_space(1))) void* gbl_ptr_t;
+
+__device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)lds_wave_base, 16, 0, 0);
+}
+
 template <int ROWS, int MODE>
 struct Loader {
   static constexpr int VPT = ROWS / 32;
@@ -110,16 +128,22 @@ struct Loader {
   int i0[VPT], j0[VPT];
   bool ok[VPT];
   int64_t ld;
-  int cr, cs, cc;  // WGRAD_B: fixed column decomposition
+  int lchunk;                 // KMAJOR: the k-chunk this lane fetches (swizzled)
+  int cr, cs, cc;             // WGRAD_B: fixed column decomposition
   bool cok;
+  int tap_cached;             // conv gathers: tap of the cached row pointers
+  const bf16* rp[VPT];        // conv gathers: row pointer at the cached tap (nullptr = zero)
 
   __device__ __forceinline__ void init(const GemmArgs& p, int row0, int nrows, const Phase& P, int64_t ld_) {
     const int t = threadIdx.x;
     ld = ld_;
+    tap_cached = -1;
     if constexpr (!KOUT) {
+      const int row_l = t >> 3;  // (row >> 1) & 7 is the same for every v (32v keeps bits 1-3)
+      lchunk = (t & 7) ^ ((row_l >> 1) & 7);
 #pragma unroll
       for (int v = 0; v < VPT; ++v) {
-        const int row = row0 + (t >> 3) + 32 * v;
+        const int row = row0 + row_l + 32 * v;
         ok[v] = row < nrows;
         const int rr = ok[v] ? row : 0;
         if constexpr (MODE == LM_KMAJOR) {
@@ -146,7 +170,8 @@ struct Loader {
       }
     } else if constexpr (MODE == LM_WGRAD_B) {
       const ConvGeom& g = p.g;
-      const int col = row0 + (t % CPR) * 8;  // gemm column n = (r, s, c)
+      const int kr = t / CPR;
+      const int col = row0 + (((t % CPR) ^ kouter_swz<ROWS>(kr, 0)) * 8);  // swz(kr) same for every v
       cok = col < nrows;
       const int c2 = cok ? col : 0;
       const int rs = g.dC.div(c2);
@@ -156,81 +181,99 @@ struct Loader {
     }
   }
 
-  // Fetch the K-tile starting at k0 (absolute) into registers.
-  __device__ __forceinline__ void fetch(uint4 (&rg)[VPT], const GemmArgs& p, const bf16* __restrict__ src,
-                                        int row0, int nrows, int k0, int kend, const Phase& P) const {
+  // Issue the K-tile starting at k0 (absolute) into the LDS stage `lds`.
+  __device__ __forceinline__ void issue(const GemmArgs& p, const bf16* __restrict__ src, int row0, int nrows, int k0,
+                                        int kend, const Phase& P, char* lds) {
     const int t = threadIdx.x;
+    const int w = t >> 6;
+    const void* zero = (const void*)sg_zero_page;
     if constexpr (MODE == LM_KMAJOR) {
-      const int kk = k0 + (t & 7) * 8;
+      const int kk = k0 + lchunk * 8;
       const bool kin = kk < kend;
 #pragma unroll
       for (int v = 0; v < VPT; ++v) {
         const bool o = ok[v] && kin;
-        rg[v] = sel(o, *(const uint4*)(src + (o ? base[v] + kk : 0)));
+        glds16(o ? (const void*)(src + base[v] + kk) : zero, lds + (8 * w + 32 * v) * 128);
       }
-    } else if constexpr (MODE == LM_CONV_FWD) {
+    } else if constexpr (MODE == LM_CONV_FWD || MODE == LM_DGRAD_A) {
       const ConvGeom& g = p.g;
-      int kk = k0 + (t & 7) * 8;
+      const int CH = MODE == LM_CONV_FWD ? g.C : g.K;
+      const FastDiv& dch = MODE == LM_CONV_FWD ? g.dC : g.dK;
+      int kk = k0 + lchunk * 8;
       const bool kin = kk < kend;
       kk = kin ? kk : 0;
-      int tap, c0;
-      if ((g.C & 63) == 0) {  // wave-uniform tap
-        tap = g.dC.div(k0);
-        c0 = kk - tap * g.C;
-      } else {
-        tap = g.dC.div(kk);
-        c0 = kk - tap * g.C;
-      }
-      const int r = g.dS.div(tap), s = tap - r * g.S;
-      const int dr = r * g.dh, ds = s * g.dw;
+      if ((CH & 63) == 0) {  // the whole K-tile is one tap: cache row pointers per tap
+        const int tap = dch.div(k0);
+        const int c0 = kk - tap * CH;
+        if (tap != tap_cached) {
+          tap_cached = tap;
+          int dr, ds;
+          if constexpr (MODE == LM_CONV_FWD) {
+            const int r = g.dS.div(tap), s = tap - r * g.S;
+            dr = r * g.dh;
+            ds = s * g.dw;
+          } else {
+            const int j = P.dns.div(tap), i = tap - j * P.ns;
+            dr = -j;
+            ds = -i;
+          }
+          const int HH = MODE == LM_CONV_FWD ? g.H : g.Ho, WW = MODE == LM_CONV_FWD ? g.W : g.Wo;
 #pragma unroll
-      for (int v = 0; v < VPT; ++v) {
-        const int ih = i0[v] + dr, iw = j0[v] + ds;
-        const bool o = ok[v] && kin && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
-        const int64_t off = base[v] + ((int64_t)ih * g.W + iw) * g.C + c0;
-        rg[v] = sel(o, *(const uint4*)(src + (o ? off : 0)));
-      }
-    } else if constexpr (MODE == LM_DGRAD_A) {
-      const ConvGeom& g = p.g;
-      int kk = k0 + (t & 7) * 8;
-      const bool kin = kk < kend;
-      kk = kin ? kk : 0;
-      int tap, k;
-      if ((g.K & 63) == 0) {
-        tap = g.dK.div(k0);
-        k = kk - tap * g.K;
-      } else {
-        tap = g.dK.div(kk);
-        k = kk - tap * g.K;
-      }
-      const int j = P.dns.div(tap), i = tap - j * P.ns;
+          for (int v = 0; v < VPT; ++v) {
+            const int ih = i0[v] + dr, iw = j0[v] + ds;
+            const bool o = ok[v] && (unsigned)ih < (unsigned)HH && (unsigned)iw < (unsigned)WW;
+            rp[v] = o ? src + base[v] + ((int64_t)ih * WW + iw) * CH : nullptr;
+          }
+        }
 #pragma unroll
-      for (int v = 0; v < VPT; ++v) {
-        const int oh = i0[v] - j, ow = j0[v] - i;
-        const bool o = ok[v] && kin && (unsigned)oh < (unsigned)g.Ho && (unsigned)ow < (unsigned)g.Wo;
-        const int64_t off = base[v] + ((int64_t)oh * g.Wo + ow) * g.K + k;
-        rg[v] = sel(o, *(const uint4*)(src + (o ? off : 0)));
+        for (int v = 0; v < VPT; ++v) {
+          const bool o = rp[v] != nullptr && kin;
+          glds16(o ? (const void*)(rp[v] + c0) : zero, lds + (8 * w + 32 * v) * 128);
+        }
+      } else {  // per-lane tap (channel counts not a multiple of 64, e.g. the padded stem)
+        const int tap = dch.div(kk);
+        const int c0 = kk - tap * CH;
+        int dr, ds;
+        if constexpr (MODE == LM_CONV_FWD) {
+          const int r = g.dS.div(tap), s = tap - r * g.S;
+          dr = r * g.dh;
+          ds = s * g.dw;
+        } else {
+          const int j = P.dns.div(tap), i = tap - j * P.ns;
+          dr = -j;
+          ds = -i;
+        }
+        const int HH = MODE == LM_CONV_FWD ? g.H : g.Ho, WW = MODE == LM_CONV_FWD ? g.W : g.Wo;
+#pragma unroll
+        for (int v = 0; v < VPT; ++v) {
+          const int ih = i0[v] + dr, iw = j0[v] + ds;
+          const bool o = ok[v] && kin && (unsigned)ih < (unsigned)HH && (unsigned)iw < (unsigned)WW;
+          const int64_t off = base[v] + ((int64_t)ih * WW + iw) * CH + c0;
+          glds16(o ? (const void*)(src + off) : zero, lds + (8 * w + 32 * v) * 128);
+        }
       }
     } else if constexpr (MODE == LM_KOUTER) {
-      const int col = row0 + (t % CPR) * 8;
+      const int kr0 = t / CPR;
+      const int col = row0 + (((t % CPR) ^ kouter_swz<ROWS>(kr0, 0)) * 8);
       const bool cin = col < nrows;
 #pragma unroll
       for (int v = 0; v < VPT; ++v) {
-        const int kr = k0 + t / CPR + KRP * v;
+        const int kr = k0 + kr0 + KRP * v;
         const bool o = cin && kr < kend;
-        rg[v] = sel(o, *(const uint4*)(src + (o ? (int64_t)kr * ld + col : 0)));
+        glds16(o ? (const void*)(src + (int64_t)kr * ld + col) : zero, lds + (w * (64 / CPR) + KRP * v) * (ROWS * 2));
       }
     } else if constexpr (MODE == LM_DGRAD_B) {
       // B(n = c, kk = (tap, k)) = W[k][r][s][c]; rows c contiguous per (k, tap)
       const ConvGeom& g = p.g;
-      const int col = row0 + (t % CPR) * 8;
+      const int kr0 = t / CPR;
+      const int col = row0 + (((t % CPR) ^ kouter_swz<ROWS>(kr0, 0)) * 8);
       const bool cin = col < nrows;
       const int RSC = g.R * g.S * g.C;
       const bool uni = (g.K & 63) == 0;
       const int tapu = g.dK.div(k0);
 #pragma unroll
       for (int v = 0; v < VPT; ++v) {
-        int kk = k0 + t / CPR + KRP * v;
+        int kk = k0 + kr0 + KRP * v;
         const bool kin = kk < kend;
         kk = kin ? kk : 0;
         const int tap = uni ? tapu : (int)g.dK.div(kk);
@@ -239,13 +282,14 @@ struct Loader {
         const int r = P.r0 + g.sh * j, s = P.s0 + g.sw * i;
         const bool o = cin && kin;
         const int64_t off = (int64_t)k * RSC + (r * g.S + s) * g.C + col;
-        rg[v] = sel(o, *(const uint4*)(src + (o ? off : 0)));
+        glds16(o ? (const void*)(src + off) : zero, lds + (w * (64 / CPR) + KRP * v) * (ROWS * 2));
       }
     } else if constexpr (MODE == LM_WGRAD_B) {
       const ConvGeom& g = p.g;
+      const int kr0 = t / CPR;
 #pragma unroll
       for (int v = 0; v < VPT; ++v) {
-        const int pix = k0 + t / CPR + KRP * v;  // output pixel (n, oh, ow)
+        const int pix = k0 + kr0 + KRP * v;  // output pixel (n, oh, ow)
         bool o = cok && pix < kend;
         const int pp = o ? pix : 0;
         const int n = g.dHoWo.div(pp);
@@ -256,24 +300,7 @@ struct Loader {
         const int iw = ow * g.sw - g.pw + cs * g.dw;
         o = o && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
         const int64_t off = (((int64_t)n * g.H + ih) * g.W + iw) * g.C + cc;
-        rg[v] = sel(o, *(const uint4*)(src + (o ? off : 0)));
-      }
-    }
-  }
-
-  __device__ __forceinline__ void store(const uint4 (&rg)[VPT], char* lds) const {
-    const int t = threadIdx.x;
-    if constexpr (KOUT) {
-#pragma unroll
-      for (int v = 0; v < VPT; ++v) {
-        const int kr = t / CPR + KRP * v, ch = t % CPR;
-        *(uint4*)(lds + kr * (ROWS * 2) + kouter_swz<ROWS>(kr, ch) * 16) = rg[v];
-      }
-    } else {
-#pragma unroll
-      for (int v = 0; v < VPT; ++v) {
-        const int row = (t >> 3) + 32 * v, ch = t & 7;
-        *(uint4*)(lds + row * 128 + kmajor_swz(row, ch) * 16) = rg[v];
+        glds16(o ? (const void*)(src + off) : zero, lds + (w * (64 / CPR) + KRP * v) * (ROWS * 2));
       }
     }
   }
@@ -356,18 +383,17 @@ __global__ void __launch_bounds__(NT, 2) igemm_k(const GemmArgs p) {
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   if (nk > 0) {
-    uint4 ra[Loader<BM, AM>::VPT], rb[Loader<BN, BMODE>::VPT];
-    la.fetch(ra, p, pa, m0, M, kbeg, kend, P);
-    lb.fetch(rb, p, pb, n0, p.N, kbeg, kend, P);
-    la.store(ra, smem);
-    lb.store(rb, smem + A_BYTES);
-    __syncthreads();
+    la.issue(p, pa, m0, M, kbeg, kend, P, smem);
+    lb.issue(p, pb, n0, p.N, kbeg, kend, P, smem + A_BYTES);
     for (int kt = 0; kt < nk; ++kt) {
       const int cur = kt & 1;
-      const bool more = kt + 1 < nk;
-      if (more) {
-        la.fetch(ra, p, pa, m0, M, kbeg + (kt + 1) * BK, kend, P);
-        lb.fetch(rb, p, pb, n0, p.N, kbeg + (kt + 1) * BK, kend, P);
+      // this wave's DMA for tile kt retired (vmcnt(0)), then every wave's has,
+      // and every wave finished reading the other stage (tile kt-1)
+      __syncthreads();
+      if (kt + 1 < nk) {
+        char* nxt = smem + (cur ^ 1) * STAGE;
+        la.issue(p, pa, m0, M, kbeg + (kt + 1) * BK, kend, P, nxt);
+        lb.issue(p, pb, n0, p.N, kbeg + (kt + 1) * BK, kend, P, nxt + A_BYTES);
       }
       const char* sa = smem + cur * STAGE;
       const char* sb = sa + A_BYTES;
@@ -384,17 +410,75 @@ __global__ void __launch_bounds__(NT, 2) igemm_k(const GemmArgs p) {
           for (int j = 0; j < TN; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
       }
-      if (more) {
-        char* nxt = smem + (cur ^ 1) * STAGE;
-        la.store(ra, nxt);
-        lb.store(rb, nxt + A_BYTES);
-      }
-      __syncthreads();
     }
   }
 
   // Epilogue.  acc[i][j] = D[n][m]: lane col m = l&15, rows n = (l>>4)*4+r.
   const int l = threadIdx.x & 63;
+  if constexpr (OUT == OUT_BF16) {
+    // Staged through LDS so every store is a full 16-byte vector of 8
+    // consecutive channels (the MFMA layout alone gives 8-byte pieces of 16
+    // different rows per wave-instruction).  The tile is kept in fp32 so
+    // beta*C + ReLU round to bf16 once.
+    if ((p.N & 7) == 0 && (p.ldc & 7) == 0) {
+      constexpr int LDT = BN + 4;  // fp32 row stride (+16 B against bank conflicts)
+      float* tile = (float*)smem;
+      __syncthreads();  // all waves are done reading the last operand stage
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int ml = wm * (BM / 2) + i * 16 + (l & 15);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int nl = wn * (BN / 2) + j * 16 + (l >> 4) * 4;
+          const int n = n0 + nl;
+          float4 v = make_float4(acc[i][j][0] * p.alpha, acc[i][j][1] * p.alpha, acc[i][j][2] * p.alpha,
+                                 acc[i][j][3] * p.alpha);
+          if (p.bias && n < p.N) {
+            v.x += p.bias[n]; v.y += p.bias[n + 1]; v.z += p.bias[n + 2]; v.w += p.bias[n + 3];
+          }
+          *(float4*)(tile + ml * LDT + nl) = v;
+        }
+      }
+      __syncthreads();
+      constexpr int CPRW = BN / 8;            // 16-byte output chunks per row
+      constexpr int RPP = NT / CPRW;           // rows per pass
+      const int ch = threadIdx.x % CPRW, r0 = threadIdx.x / CPRW;
+      const int n = n0 + ch * 8;
+      if (n < p.N) {
+#pragma unroll
+        for (int pass = 0; pass < BM / RPP; ++pass) {
+          const int ml = r0 + pass * RPP;
+          const int m = m0 + ml;
+          if (m >= M) continue;
+          int64_t rowoff;
+          if (p.out_phase) {
+            const ConvGeom& g = p.g;
+            const int nn = P.dHpWp.div(m);
+            const int rem = m - nn * P.Hp * P.Wp;
+            const int hh = P.dWp.div(rem);
+            const int ww = rem - hh * P.Wp;
+            rowoff = (((int64_t)nn * g.H + P.a + g.sh * hh) * g.W + P.b + g.sw * ww) * p.ldc;
+          } else {
+            rowoff = (int64_t)m * p.ldc;
+          }
+          const float4 a = *(const float4*)(tile + ml * LDT + ch * 8);
+          const float4 b = *(const float4*)(tile + ml * LDT + ch * 8 + 4);
+          float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+          bf16* c = (bf16*)pc + rowoff + n;
+          if (p.beta != 0.f) {
+            const bf16x8 old = *(const bf16x8*)c;
+#pragma unroll
+            for (int r = 0; r < 8; ++r) v[r] += p.beta * (float)old[r];
+          }
+          bf16x8 o;
+#pragma unroll
+          for (int r = 0; r < 8; ++r) o[r] = (bf16)(p.relu ? fmaxf(v[r], 0.f) : v[r]);
+          *(bf16x8*)c = o;
+        }
+      }
+      return;
+    }
+  }
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int m = m0 + wm * (BM / 2) + i * 16 + (l & 15);
@@ -517,7 +601,16 @@ static int make_phases(ConvGeom& g) {
 template <int BM, int BN, int AM, int BMODE, int OUT>
 static void launch_t(const GemmArgs& p, int tiles, int ydim, int zdim, hipStream_t s) {
   dim3 grid(tiles, ydim, zdim), block(NT);
-  constexpr int lds = 2 * (BM + BN) * BK * 2;
+  constexpr int stages = 2 * (BM + BN) * BK * 2;
+  constexpr int etile = OUT == OUT_BF16 ? BM * (BN + 4) * 4 : 0;  // fp32 epilogue tile
+  constexpr int lds = stages > etile ? stages : etile;
+  if constexpr (lds > 65536) {
+    static bool attr = [] {
+      return hipFuncSetAttribute((const void*)igemm_k<BM, BN, AM, BMODE, OUT>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
+    }();
+    (void)attr;
+  }
   hipLaunchKernelGGL((igemm_k<BM, BN, AM, BMODE, OUT>), grid, block, lds, s, p);
 }
 
@@ -530,6 +623,41 @@ static void pick_tile(int M, int N, int& BM, int& BN) {
   if (BN == 128 && (N % 128) != 0 && (N % 128) <= 64) BN = 64;
   if (wg(BM, BN) < 256 && M > 64) BM = 64;
   if (wg(BM, BN) < 256 && BN == 128) BN = 64;
+}
+
+template <int AM, int BMODE, int OUT>
+static void launch_tile(const GemmArgs& p, int M, int BM, int BN, int splits, hipStream_t s, int batch, int zdim) {
+  const int tiles = ((M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
+  const int z = zdim > 0 ? zdim : splits;
+  if (BM == 128 && BN == 128) launch_t<128, 128, AM, BMODE, OUT>(p, tiles, batch, z, s);
+  else if (BM == 128 && BN == 64) launch_t<128, 64, AM, BMODE, OUT>(p, tiles, batch, z, s);
+  else if (BM == 64 && BN == 128) launch_t<64, 128, AM, BMODE, OUT>(p, tiles, batch, z, s);
+  else launch_t<64, 64, AM, BMODE, OUT>(p, tiles, batch, z, s);
+}
+
+// Tuning knobs (sg_set_tuning): 0 = wgrad tile/split policy
+static int g_tune[8] = {1, 0, 0, 0, 0, 0, 0, 0};
+
+// wgrad: the reduction (output pixels) is huge and M x N small, so
+// parallelism comes from split-K; use the largest tile that fits (operand
+// reuse -> arithmetic intensity) and only as many splits as fill the chip.
+static void pick_wgrad(int M, int N, int K, int mode, int& BM, int& BN, int& splits) {
+  const int nkt = (K + BK - 1) / BK;
+  if (mode == 0) {
+    pick_tile(M, N, BM, BN);
+    const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+    splits = 1;
+    while (tiles * splits < 768 && splits * 2 <= nkt / 4) splits *= 2;
+    return;
+  }
+  auto fit = [](int d) { return (d >= 128 && !((d % 128) != 0 && (d % 128) <= 64)) ? 128 : 64; };
+  BM = fit(M);
+  BN = fit(N);
+  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  const int target = mode == 1 ? 512 : mode == 2 ? 1024 : 768;
+  const int min_kt = mode == 2 ? 4 : 8;
+  splits = 1;
+  while (tiles * splits < target && (splits * 2) * min_kt <= nkt) splits *= 2;
 }
 
 template <int AM, int BMODE, int OUT>
@@ -630,9 +758,15 @@ void sg_conv_wgrad(const void* x, const void* dy, void* dw_out, int N, int H, in
   p.M = K; p.N = R * S * C; p.K = N * Ho * Wo;
   p.a = (const bf16*)dy; p.lda = K; p.b = (const bf16*)x; p.ldb = 0;
   p.c = dw_out; p.ldc = R * S * C; p.alpha = 1.f; p.beta = 0.f; p.bias = nullptr; p.relu = 0;
-  splits = pick_splits(p.M, p.N, p.K, splits);
-  p.k_per_split = kps(p.K, splits);
-  launch<LM_KOUTER, LM_WGRAD_B, OUT_F32_ATOMIC>(p, p.M, splits, s, 1, 0);
+  int BM, BN, sp;
+  pick_wgrad(p.M, p.N, p.K, g_tune[0], BM, BN, sp);
+  if (splits > 0) sp = splits;
+  p.k_per_split = kps(p.K, sp);
+  launch_tile<LM_KOUTER, LM_WGRAD_B, OUT_F32_ATOMIC>(p, p.M, BM, BN, sp, s, 1, 0);
+}
+
+void sg_set_tuning(int key, int value) {
+  if (key >= 0 && key < 8) g_tune[key] = value;
 }
 
 }  // extern "C"

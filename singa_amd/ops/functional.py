@@ -48,6 +48,18 @@ def _flat_ok(t: torch.Tensor) -> bool:
     return t.dtype in (torch.float32, torch.bfloat16) and (t.is_contiguous() or N.is_cl(t))
 
 
+def _same_layout(a: torch.Tensor, b: torch.Tensor) -> bool:
+    """Same shape and the same dense element order (strides of size-1 dims
+    do not matter: [N,C,1,1] is both NCHW- and NHWC-dense)."""
+    if a.shape != b.shape:
+        return False
+    if a.stride() == b.stride():
+        return True
+    if a.is_contiguous() and b.is_contiguous():
+        return True
+    return a.dim() == 4 and N.is_cl(a) and N.is_cl(b)
+
+
 def _like(t: torch.Tensor, dtype=None) -> torch.Tensor:
     """Empty tensor with the same shape AND memory layout as t."""
     if t.dim() == 4 and N.is_cl(t) and not t.is_contiguous():
@@ -88,7 +100,7 @@ def unary_bwd(op: str, x: Optional[torch.Tensor], y: Optional[torch.Tensor], dy:
         xx = _dense(x) if x is not None else None
         yy = _dense(y) if y is not None else None
         for t in (xx, yy):
-            if t is not None and t.stride() != dy.stride():
+            if t is not None and not _same_layout(t, dy):
                 raise ValueError("unary_bwd: layout mismatch")
         dx = _like(dy)
         N.lib().unary_bwd(UNARY[op], N.ptr(xx), N.ptr(yy), dy.data_ptr(), dx.data_ptr(), dy.numel(), N.dt(dy),
@@ -145,7 +157,7 @@ def unary_bwd(op: str, x: Optional[torch.Tensor], y: Optional[torch.Tensor], dy:
 def add_act(a: torch.Tensor, b: torch.Tensor, alpha=1.0, beta=1.0, relu=False) -> torch.Tensor:
     if _native_ok(a, b) and _flat_ok(a) and a.dtype == b.dtype and a.shape == b.shape:
         a, b = _dense(a), _dense(b)
-        if a.stride() == b.stride():
+        if _same_layout(a, b):
             y = _like(a)
             N.lib().add_act(a.data_ptr(), b.data_ptr(), y.data_ptr(), a.numel(), N.dt(a), alpha, beta, int(relu),
                             N.stream())
@@ -155,7 +167,7 @@ def add_act(a: torch.Tensor, b: torch.Tensor, alpha=1.0, beta=1.0, relu=False) -
 
 
 def relu_bwd_from_y(y: torch.Tensor, dy: torch.Tensor) -> torch.Tensor:
-    if _native_ok(y, dy) and _flat_ok(dy) and y.stride() == dy.stride() and y.dtype == dy.dtype:
+    if _native_ok(y, dy) and _flat_ok(dy) and _same_layout(y, dy) and y.dtype == dy.dtype:
         dx = _like(dy)
         N.lib().relu_bwd_from_y(y.data_ptr(), dy.data_ptr(), dx.data_ptr(), dy.numel(), N.dt(dy), N.stream())
         return dx
@@ -189,7 +201,7 @@ def dropout_fwd(x: torch.Tensor, ratio: float, seed: int, offset: int) -> Tuple[
 
 def dropout_bwd(dy: torch.Tensor, mask: torch.Tensor, ratio: float) -> torch.Tensor:
     pkeep = 1.0 - ratio
-    if _native_ok(dy) and _flat_ok(dy) and _dense(dy).stride() == mask.stride():
+    if _native_ok(dy) and _flat_ok(dy) and _same_layout(_dense(dy), mask):
         dy = _dense(dy)
         dx = _like(dy)
         N.lib().dropout_bwd(dy.data_ptr(), mask.data_ptr(), dx.data_ptr(), dy.numel(), N.dt(dy), pkeep, N.stream())
@@ -601,7 +613,7 @@ def batchnorm_fwd(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, run_
         res = None
         if residual is not None:
             res = residual
-            if res.dtype != x.dtype or res.stride() != x.stride():
+            if res.dtype != x.dtype or not _same_layout(res, x):
                 res = _dense(res).to(x.dtype).contiguous(
                     memory_format=torch.channels_last if x.dim() == 4 else torch.contiguous_format)
         y = _like(x)
@@ -643,12 +655,12 @@ def batchnorm_bwd(x: torch.Tensor, dy: torch.Tensor, gamma: torch.Tensor, st: BN
     if _bn_native(x):
         L = N.lib()
         R = x.numel() // C
-        if dy.dtype != x.dtype or dy.stride() != x.stride():
+        if dy.dtype != x.dtype or not _same_layout(dy, x):
             dy = dy.to(x.dtype).contiguous(memory_format=torch.channels_last if x.dim() == 4 else
                                            torch.contiguous_format)
         ym = y_for_mask
         if ym is not None:
-            if ym.dtype != x.dtype or ym.stride() != x.stride():
+            if ym.dtype != x.dtype or not _same_layout(ym, x):
                 raise ValueError("batchnorm_bwd: mask tensor layout mismatch")
             mode = 1
         else:
