@@ -83,6 +83,7 @@ struct GemmArgs {
   int k_per_split;     // multiple of BK
   int64_t sa, sb, sc;  // batch strides (elements), blockIdx.y = batch
   int out_phase;       // dgrad: output rows map through the phase grid
+  int lds_epilogue;    // stage bf16 output tiles through LDS (16-byte stores)
   ConvGeom g;
 };
 
@@ -287,20 +288,47 @@ struct Loader {
     } else if constexpr (MODE == LM_WGRAD_B) {
       const ConvGeom& g = p.g;
       const int kr0 = t / CPR;
+      if (g.R == 1 && g.S == 1 && g.sh == 1 && g.sw == 1 && g.ph == 0 && g.pw == 0) {
+        // 1x1 stride-1 conv: input pixel == output pixel, no bounds
 #pragma unroll
-      for (int v = 0; v < VPT; ++v) {
-        const int pix = k0 + kr0 + KRP * v;  // output pixel (n, oh, ow)
-        bool o = cok && pix < kend;
-        const int pp = o ? pix : 0;
-        const int n = g.dHoWo.div(pp);
-        const int rem = pp - n * g.Ho * g.Wo;
-        const int oh = g.dWo.div(rem);
-        const int ow = rem - oh * g.Wo;
-        const int ih = oh * g.sh - g.ph + cr * g.dh;
-        const int iw = ow * g.sw - g.pw + cs * g.dw;
-        o = o && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
-        const int64_t off = (((int64_t)n * g.H + ih) * g.W + iw) * g.C + cc;
-        glds16(o ? (const void*)(src + off) : zero, lds + (w * (64 / CPR) + KRP * v) * (ROWS * 2));
+        for (int v = 0; v < VPT; ++v) {
+          const int pix = k0 + kr0 + KRP * v;
+          const bool o = cok && pix < kend;
+          glds16(o ? (const void*)(src + (int64_t)pix * g.C + cc) : zero,
+                 lds + (w * (64 / CPR) + KRP * v) * (ROWS * 2));
+        }
+      } else {
+        // decompose the first pixel once; later vectors step by KRP with
+        // carries when a row is at least KRP wide (else divide again)
+        const int pix0 = k0 + kr0;
+        const int pp0 = pix0 < kend ? pix0 : 0;
+        int n = g.dHoWo.div(pp0);
+        int rem = pp0 - n * g.Ho * g.Wo;
+        int oh = g.dWo.div(rem);
+        int ow = rem - oh * g.Wo;
+        const bool step = g.Wo >= KRP;
+#pragma unroll
+        for (int v = 0; v < VPT; ++v) {
+          const int pix = pix0 + KRP * v;
+          if (v > 0) {
+            if (step) {
+              ow += KRP;
+              if (ow >= g.Wo) { ow -= g.Wo; ++oh; }
+              if (oh >= g.Ho) { oh -= g.Ho; ++n; }
+            } else {
+              const int pp = pix < kend ? pix : 0;
+              n = g.dHoWo.div(pp);
+              rem = pp - n * g.Ho * g.Wo;
+              oh = g.dWo.div(rem);
+              ow = rem - oh * g.Wo;
+            }
+          }
+          const int ih = oh * g.sh - g.ph + cr * g.dh;
+          const int iw = ow * g.sw - g.pw + cs * g.dw;
+          const bool o = cok && pix < kend && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+          const int64_t off = (((int64_t)n * g.H + ih) * g.W + iw) * g.C + cc;
+          glds16(o ? (const void*)(src + off) : zero, lds + (w * (64 / CPR) + KRP * v) * (ROWS * 2));
+        }
       }
     }
   }
@@ -420,7 +448,7 @@ __global__ void __launch_bounds__(NT, 2) igemm_k(const GemmArgs p) {
     // consecutive channels (the MFMA layout alone gives 8-byte pieces of 16
     // different rows per wave-instruction).  The tile is kept in fp32 so
     // beta*C + ReLU round to bf16 once.
-    if ((p.N & 7) == 0 && (p.ldc & 7) == 0) {
+    if ((p.N & 7) == 0 && (p.ldc & 7) == 0 && p.lds_epilogue) {
       constexpr int LDT = BN + 4;  // fp32 row stride (+16 B against bank conflicts)
       float* tile = (float*)smem;
       __syncthreads();  // all waves are done reading the last operand stage
@@ -598,8 +626,12 @@ static int make_phases(ConvGeom& g) {
   return np;
 }
 
+static int g_tune[8] = {4, 1, 0, 0, 0, 0, 0, 0};
+
 template <int BM, int BN, int AM, int BMODE, int OUT>
-static void launch_t(const GemmArgs& p, int tiles, int ydim, int zdim, hipStream_t s) {
+static void launch_t(const GemmArgs& p_in, int tiles, int ydim, int zdim, hipStream_t s) {
+  GemmArgs p = p_in;
+  p.lds_epilogue = g_tune[1];
   dim3 grid(tiles, ydim, zdim), block(NT);
   constexpr int stages = 2 * (BM + BN) * BK * 2;
   constexpr int etile = OUT == OUT_BF16 ? BM * (BN + 4) * 4 : 0;  // fp32 epilogue tile
@@ -635,14 +667,18 @@ static void launch_tile(const GemmArgs& p, int M, int BM, int BN, int splits, hi
   else launch_t<64, 64, AM, BMODE, OUT>(p, tiles, batch, z, s);
 }
 
-// Tuning knobs (sg_set_tuning): 0 = wgrad tile/split policy
-static int g_tune[8] = {1, 0, 0, 0, 0, 0, 0, 0};
+// Tuning knobs (sg_set_tuning): 0 = wgrad tile/split policy, 1 = LDS-staged
+// bf16 epilogue (g_tune is defined above launch_t)
 
 // wgrad: the reduction (output pixels) is huge and M x N small, so
 // parallelism comes from split-K; use the largest tile that fits (operand
 // reuse -> arithmetic intensity) and only as many splits as fill the chip.
 static void pick_wgrad(int M, int N, int K, int mode, int& BM, int& BN, int& splits) {
   const int nkt = (K + BK - 1) / BK;
+  // measured (tools/tune_conv.py, b256): bigger tiles win when the pixel
+  // reduction dwarfs the output (early, narrow layers); 64x64 + many splits
+  // elsewhere
+  if (mode == 4) mode = ((long)K >= 8L * M * N) ? 1 : 0;
   if (mode == 0) {
     pick_tile(M, N, BM, BN);
     const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);

@@ -30,6 +30,12 @@ def _load():
         _lib = importlib.import_module("singa_amd._C")
     except Exception as e:  # pragma: no cover - reported through lib()
         _err = e
+        return _lib
+    # kernel tuning knobs from the environment: SG_TUNE="0=4,1=1" (key=value)
+    for kv in os.environ.get("SG_TUNE", "").split(","):
+        if "=" in kv and hasattr(_lib, "set_tuning"):
+            k, v = kv.split("=")
+            _lib.set_tuning(int(k), int(v))
     return _lib
 
 

@@ -87,12 +87,22 @@ CONV_CASES = [
     (2, 3, 32, 32, 64, 7, 7, 2, 3),     # stem, C padded to 8
     (3, 20, 12, 12, 50, 5, 5, 1, 0),    # LeNet conv2: C and K not multiples of 8
     (2, 32, 9, 11, 40, 3, 3, 1, 2),
+    # ResNet-sized spatial extents: wgrad's stepping pixel decomposition
+    # (output rows >= 16 / 32 pixels) and the 128-row tiles
+    (2, 64, 56, 56, 64, 3, 3, 1, 1),
+    (2, 64, 56, 56, 256, 1, 1, 1, 0),
+    (2, 256, 56, 56, 128, 1, 1, 2, 0),
+    (2, 128, 56, 56, 128, 3, 3, 2, 1),
+    (1, 32, 70, 70, 64, 3, 3, 1, 1),
 ]
 
 
+@pytest.mark.parametrize("wmode", [0, 1])
 @pytest.mark.parametrize("case", CONV_CASES)
-def test_conv_fwd_bwd(gpu, case):
+def test_conv_fwd_bwd(gpu, case, wmode):
     from singa_amd.ops import functional as F
+    from singa_amd.ops import native as NN
+    NN.lib().set_tuning(0, wmode)  # wgrad tile policy: 64-tiles + splits / largest tiles
     N_, C, H, W, K, R, S, st, pd = case
     g = torch.Generator().manual_seed(3)
     x = bf(torch.randn(N_, C, H, W, generator=g)).float()
@@ -111,6 +121,12 @@ def test_conv_fwd_bwd(gpu, case):
     dw_acc = torch.zeros(K, C, R, S, device=gpu)
     dx, dw, db = F.conv2d_bwd(xg.float().contiguous(memory_format=torch.channels_last), wg, dyg, (st, st),
                               (pd, pd), need_dx=True, dw_out=dw_acc, need_db=True)
+    NN.lib().set_tuning(0, 4)
+    # bf16 outputs (the LDS-staged epilogue): fwd and dgrad
+    yb = F.conv2d_fwd(xg, wg, None, (st, st), (pd, pd), out_dtype=torch.bfloat16)
+    assert yb.dtype == torch.bfloat16 and rel_err(yb.float(), yr.detach()) < 1e-2
+    dxb = F.conv2d_bwd(xg, wg, dyg, (st, st), (pd, pd), need_dx=True)[0]
+    assert dxb.dtype == torch.bfloat16 and rel_err(dxb.float(), xr.grad) < 1e-2
     assert rel_err(dx, xr.grad) < 1e-5
     assert rel_err(dw_acc, wr.grad) < 1e-5
     assert rel_err(db, dy.sum((0, 2, 3))) < 1e-5
