@@ -37,7 +37,7 @@ def main() -> int:
                     help="HIP-graph replay of forward+backward (default for 1 GPU)")
     ap.add_argument("--no-graph", dest="graph", action="store_false",
                     help="eager execution; the default for N>1, where bucketed all-reduces overlap the backward")
-    ap.add_argument("--lr", type=float, default=0.02,
+    ap.add_argument("--lr", type=float, default=0.01,
                     help="SGD lr (random labels + no warmup: 0.1 occasionally diverges; throughput is lr-independent)")
     args = ap.parse_args()
 

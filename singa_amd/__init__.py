@@ -14,3 +14,15 @@ __version__ = "0.1.0"
 
 def native_loaded() -> bool:
     return _native.available()
+
+
+def set_deterministic(on: bool = True) -> None:
+    """Deterministic mode: ordered (atomic-free) BatchNorm and
+    fused-statistics reductions and single-split weight gradients, so a
+    training step is bitwise reproducible run to run (slower).  Philox
+    dropout streams are already reproducible for a given device seed."""
+    if _native.available():
+        _native.lib().set_deterministic(int(bool(on)))
+    import os
+
+    os.environ["SINGA_AMD_DETERMINISTIC"] = "1" if on else "0"

@@ -576,17 +576,18 @@ class Conv2d(Operator):
     """2-D convolution; NCHW logical / NHWC physical; implicit-GEMM kernels."""
 
     def __init__(self, stride=(1, 1), padding=(0, 0), dilation=(1, 1), group=1, has_bias=False,
-                 fuse_relu=False, name=None):
+                 fuse_relu=False, bn_stats=False, name=None):
         super().__init__(name)
         self.stride, self.padding, self.dilation, self.group = tuple(stride), tuple(padding), tuple(dilation), group
         self.has_bias = has_bias
         self.fuse_relu = fuse_relu
+        self.bn_stats = bn_stats  # a training-mode BatchNorm consumes the output: sum its statistics in the epilogue
 
     def forward(self, x, W, b=None):
         p = self.params[1] if len(self.params) > 1 else None
         w = p.low if (p is not None and p.low is not None and x.dtype == torch.bfloat16) else W
         y = F.conv2d_fwd(x, w, b, self.stride, self.padding, self.dilation, self.group, out_dtype=x.dtype,
-                         relu=self.fuse_relu)
+                         relu=self.fuse_relu, bn_stats=self.bn_stats and training)
         if self.requires_grad:
             self.x, self.w = x, w
             self.y = y if self.fuse_relu else None

@@ -37,7 +37,10 @@ void sg_layernorm_fwd(const void*, const void*, const void*, void*, void*, void*
 void sg_layernorm_bwd(const void*, const void*, const void*, const void*, const void*, void*, void*, void*, int64_t,
                       int, int, hipStream_t);
 int sg_colreduce_bands(int64_t, int);
-int sg_colreduce_ws(int);
+int64_t sg_colreduce_ws(int64_t, int);
+int sg_conv_stats_rows(int, int);
+void sg_bn_set_deterministic(int);
+int sg_bn_deterministic();
 void sg_colsum(const void*, void*, void*, void*, int64_t, int, int, int, hipStream_t);
 void sg_bn_fwd_stats(const void*, void*, const void*, const void*, void*, void*, void*, void*, void*, void*, int64_t,
                      int, float, float, int, hipStream_t);
@@ -65,7 +68,9 @@ void sg_rsync_scatter(void*, void*, const void*, int64_t, int64_t, int64_t, int6
 void sg_gemm(const void*, int64_t, int, const void*, int64_t, int, void*, int64_t, int, int, int, float, float,
              const void*, int, int, int, int, int64_t, int64_t, int64_t, hipStream_t);
 void sg_conv_fwd(const void*, const void*, void*, const void*, int, int, int, int, int, int, int, int, int, int, int,
-                 int, int, int, int, int, int, hipStream_t);
+                 int, int, int, int, int, int, void*, hipStream_t);
+void sg_bn_fwd_from_ws(const void*, int, const void*, const void*, void*, void*, void*, void*, void*, void*, int64_t,
+                       int, float, float, hipStream_t);
 void sg_conv_dgrad(const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int, int,
                    int, int, int, hipStream_t);
 void sg_conv_wgrad(const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int, int,
@@ -148,7 +153,10 @@ PYBIND11_MODULE(_C, m) {
     CHK("layernorm_bwd");
   });
   m.def("colreduce_bands", [](int64_t R, int C) { return sg_colreduce_bands(R, C); });
-  m.def("colreduce_ws", [](int C) { return sg_colreduce_ws(C); });
+  m.def("colreduce_ws", [](int64_t R, int C) { return sg_colreduce_ws(R, C); });
+  m.def("conv_stats_rows", [](int M, int N) { return sg_conv_stats_rows(M, N); });
+  m.def("set_deterministic", [](int on) { sg_bn_set_deterministic(on); });
+  m.def("deterministic", []() { return sg_bn_deterministic(); });
   m.def("colsum", [](P x, P ws, P o0, P o1, int64_t R, int C, int dt, int acc, P s) {
     sg_colsum(CV(x), V(ws), V(o0), V(o1), R, C, dt, acc, S(s)); CHK("colsum");
   });
@@ -219,10 +227,19 @@ PYBIND11_MODULE(_C, m) {
     CHK("gemm");
   });
   m.def("conv_fwd", [](P x, P w, P y, P bias, int N, int H, int W, int C, int K, int R, int Sd, int Ho, int Wo,
-                       int sh, int sw, int ph, int pw, int dh, int dw, int relu, int out_mode, P s) {
+                       int sh, int sw, int ph, int pw, int dh, int dw, int relu, int out_mode, P s, P stats) {
     sg_conv_fwd(CV(x), CV(w), V(y), CV(bias), N, H, W, C, K, R, Sd, Ho, Wo, sh, sw, ph, pw, dh, dw, relu, out_mode,
-                S(s));
+                V(stats), S(s));
     CHK("conv_fwd");
+  }, py::arg("x"), py::arg("w"), py::arg("y"), py::arg("bias"), py::arg("N"), py::arg("H"), py::arg("W"), py::arg("C"),
+     py::arg("K"), py::arg("R"), py::arg("S"), py::arg("Ho"), py::arg("Wo"), py::arg("sh"), py::arg("sw"),
+     py::arg("ph"), py::arg("pw"), py::arg("dh"), py::arg("dw"), py::arg("relu"), py::arg("out_mode"),
+     py::arg("stream"), py::arg("stats") = 0);
+  m.def("bn_fwd_from_ws", [](P ws, int nb, P gamma, P beta, P rm, P rv, P mean, P invstd, P scale, P shift, int64_t R,
+                             int C, float mom, float eps, P s) {
+    sg_bn_fwd_from_ws(CV(ws), nb, CV(gamma), CV(beta), V(rm), V(rv), V(mean), V(invstd), V(scale), V(shift), R, C, mom,
+                      eps, S(s));
+    CHK("bn_fwd_from_ws");
   });
   m.def("conv_dgrad", [](P dy, P wt, P dx, int N, int H, int W, int C, int K, int R, int Sd, int Ho, int Wo, int sh,
                          int sw, int ph, int pw, int dh, int dw, int out_mode, P s) {

@@ -2,13 +2,19 @@
 //
 // Design for MI355X (HBM-bound ops, every byte counts):
 //  * Reductions are two-stage: each workgroup reduces a band of rows for its
-//    channel slice in registers + LDS and adds ONE partial per channel into
-//    one of 32 slot rows ws[band % 32][2][C] (32 adders per address), and a
-//    per-channel finalize kernel sums the 32 slots.  (v1 ended every
-//    workgroup with atomics on the same channel addresses -- 2048 contended
-//    adds on two cache lines ran 20x below HBM bandwidth; v2 stored one
-//    partial per band with plain stores, but then the per-channel finalize
-//    summed up to 1024 partials serially: 150 us per BN layer.)
+//    channel slice in registers + LDS and emits ONE partial per channel.
+//    Default (fast): the partial is atomically added into one of 32 slot
+//    rows ws[band % 32][2][C] (32 adders per address; ws zeroed per call) and
+//    the finalize sums 32 rows.  Deterministic mode (sg_set_deterministic):
+//    every band stores its partial into its own row ws[band][2][C] with plain
+//    stores and the finalize sums the rows in a fixed order -- bitwise
+//    reproducible, at the cost of a longer finalize.  (History: v1 ended every
+//    workgroup with atomics on the same addresses, 20x below HBM bandwidth;
+//    v2 summed up to 1024 partials with one thread per channel, 150 us per
+//    BN layer.)  Atomic-order noise is amplified by 50 BN layers into visibly
+//    different training runs, hence the mode.
+//  * The conv epilogue can produce the same [tiles][2][C] partials for the
+//    BN that consumes its output (igemm.hip, GemmArgs::stats).
 //  * Thread mapping is 2-D: a thread owns a fixed 8-channel (16-byte) slice
 //    and walks rows, so per-channel coefficients are loaded once into
 //    registers and no per-element channel index math (64-bit modulo) is done.
@@ -26,7 +32,9 @@
 namespace sg {
 
 enum MaskMode : int { MASK_NONE = 0, MASK_Y = 1, MASK_AFFINE = 2 };
-constexpr int NSLOT = 32;  // partial-sum slot rows (ws = NSLOT*2*C floats, zeroed per call)
+constexpr int NSLOT = 32;      // atomic partial-sum slot rows of the fast mode
+constexpr int FIN_GROUPS = 4;  // band groups per finalize workgroup (256 threads = 64 channels x 4)
+static int g_bn_det = 0;       // deterministic reductions (set by sg_set_deterministic)
 
 struct Tile2D {
   int CT, RT, tx, ty, c0;
@@ -56,7 +64,7 @@ __global__ void __launch_bounds__(256) colpart_k(const T* __restrict__ x, const 
                                                  const T* __restrict__ y, const float* __restrict__ scale,
                                                  const float* __restrict__ shift, const float* __restrict__ mean,
                                                  const float* __restrict__ invstd, float* __restrict__ ws, int64_t R,
-                                                 int C, int rows_per_band, int mask_mode) {
+                                                 int C, int rows_per_band, int mask_mode, int det) {
   __shared__ float red[256 * V];
   const Tile2D t = tile2d<V>(C);
   float a0[V], a1[V];
@@ -136,8 +144,9 @@ __global__ void __launch_bounds__(256) colpart_k(const T* __restrict__ x, const 
       }
     }
   }
-  // reduce over ty in LDS, then one atomic add per channel into slot band%32
-  float* out = ws + (int64_t)(blockIdx.x & (NSLOT - 1)) * 2 * C;
+  // reduce over ty in LDS, then one partial per channel: plain store into
+  // row `band` (deterministic) or atomic add into slot band % 32
+  float* out = ws + (int64_t)(det ? blockIdx.x : (blockIdx.x & (NSLOT - 1))) * 2 * C;
   for (int pass = 0; pass < 2; ++pass) {
     const float* acc = pass == 0 ? a0 : a1;
     __syncthreads();
@@ -155,28 +164,51 @@ __global__ void __launch_bounds__(256) colpart_k(const T* __restrict__ x, const 
         for (int i = 0; i < V; ++i) s[i] += red[(k * t.CT + t.tx) * V + i];
       }
 #pragma unroll
-      for (int i = 0; i < V; ++i) atomicAdd(out + pass * C + t.c0 + i, s[i]);
+      for (int i = 0; i < V; ++i) {
+        if (det) out[pass * C + t.c0 + i] = s[i];
+        else atomicAdd(out + pass * C + t.c0 + i, s[i]);
+      }
     }
   }
 }
 
-__device__ __forceinline__ void band_sum(const float* __restrict__ ws, int nb, int C, int c, float* s0, float* s1) {
+// Deterministic ordered sum of nb partial rows ws[k][2][C] for the 64
+// channels of this workgroup: thread (c, grp) sums rows grp, grp+4, ... in
+// order, then the 4 group sums are added in fixed order.  Returns true for the
+// thread that owns channel c (grp == 0) with the totals in *s0, *s1.
+__device__ __forceinline__ bool band_sum(const float* __restrict__ ws, int nb, int C, int* cout, float* s0,
+                                         float* s1) {
+  __shared__ float red[2][FIN_GROUPS][64];
+  const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
   float a = 0.f, b = 0.f;
-  for (int k = 0; k < nb; ++k) {
-    a += ws[(int64_t)k * 2 * C + c];
-    b += ws[(int64_t)k * 2 * C + C + c];
+  if (c < C) {
+    for (int k = grp; k < nb; k += FIN_GROUPS) {
+      a += ws[(int64_t)k * 2 * C + c];
+      b += ws[(int64_t)k * 2 * C + C + c];
+    }
   }
+  red[0][grp][cl] = a;
+  red[1][grp][cl] = b;
+  __syncthreads();
+  if (grp != 0 || c >= C) return false;
+#pragma unroll
+  for (int g = 1; g < FIN_GROUPS; ++g) {
+    a += red[0][g][cl];
+    b += red[1][g][cl];
+  }
+  *cout = c;
   *s0 = a;
   *s1 = b;
+  return true;
 }
 
 // colsum finalize: out0[c] (+)= sum, out1[c] (+)= sumsq
 __global__ void colsum_finalize_k(const float* __restrict__ ws, int nb, int C, float* __restrict__ out0,
                                   float* __restrict__ out1, int accumulate) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+  int c;
   float s0, s1;
-  band_sum(ws, nb, C, c, &s0, &s1);
+  if (!band_sum(ws, nb, C, &c, &s0, &s1)) return;
   if (out0) out0[c] = accumulate ? out0[c] + s0 : s0;
   if (out1) out1[c] = accumulate ? out1[c] + s1 : s1;
 }
@@ -187,10 +219,9 @@ __global__ void bn_fwd_finalize_k(const float* __restrict__ ws, int nb, int C, c
                                   float* __restrict__ run_var, float* __restrict__ mean, float* __restrict__ invstd,
                                   float* __restrict__ scale, float* __restrict__ shift, float count, float momentum,
                                   float eps) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+  int c;
   float s0, s1;
-  band_sum(ws, nb, C, c, &s0, &s1);
+  if (!band_sum(ws, nb, C, &c, &s0, &s1)) return;
   float mu = s0 / count;
   float var = fmaxf(s1 / count - mu * mu, 0.f);
   float is = rsqrtf(var + eps);
@@ -212,10 +243,9 @@ __global__ void bn_bwd_finalize_k(const float* __restrict__ ws, int nb, int C, c
                                   const float* __restrict__ mean, const float* __restrict__ invstd,
                                   float* __restrict__ coef, float* __restrict__ dg, float* __restrict__ db,
                                   float count) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+  int c;
   float sdy, sdyx;
-  band_sum(ws, nb, C, c, &sdy, &sdyx);
+  if (!band_sum(ws, nb, C, &c, &sdy, &sdyx)) return;
   float is = invstd[c];
   float k = (gamma ? gamma[c] : 1.f) * is;
   float bcoef = -k * is * sdyx / count;
@@ -317,8 +347,6 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_k(const T* __restrict__ x, c
 
 using namespace sg;
 
-// workspace floats needed by the column reductions: NSLOT*2*C (see NSLOT)
-extern "C" int sg_colreduce_ws(int C) { return NSLOT * 2 * C; }
 
 // number of row bands for a [R][C] column reduction
 extern "C" int sg_colreduce_bands(int64_t R, int C) {
@@ -333,6 +361,21 @@ extern "C" int sg_colreduce_bands(int64_t R, int C) {
   if (bands > want) bands = want;
   return (int)(bands < 1 ? 1 : bands);
 }
+
+// workspace floats needed by a [R][C] column reduction: bands*2*C
+extern "C" int64_t sg_colreduce_ws(int64_t R, int C) {
+  return (int64_t)(g_bn_det ? sg_colreduce_bands(R, C) : NSLOT) * 2 * C;
+}
+extern "C" void sg_bn_set_deterministic(int on) { g_bn_det = on; }
+extern "C" int sg_bn_deterministic() { return g_bn_det; }
+
+// rows the finalize sums for a reduction launched on `grid`
+static inline int fin_rows(const dim3& grid) { return g_bn_det ? (int)grid.x : NSLOT; }
+static inline void zero_ws(void* ws, int C, hipStream_t s) {
+  if (!g_bn_det) hipMemsetAsync(ws, 0, sizeof(float) * NSLOT * 2 * C, s);
+}
+
+static inline dim3 fin_grid(int C) { return dim3((C + 63) / 64); }
 
 static inline void colgrid(int64_t R, int C, dim3& grid, int& rpb, int& V) {
   V = (C % 8 == 0) ? 8 : 1;
@@ -382,11 +425,11 @@ void sg_colsum(const void* x, void* ws, void* out0, void* out1, int64_t R, int C
   dim3 grid;
   int rpb, V;
   colgrid(R, C, grid, rpb, V);
-  hipMemsetAsync(ws, 0, sizeof(float) * NSLOT * 2 * C, s);
+  zero_ws(ws, C, s);
   DISPATCH_FT(dtype, DISPATCH_V(V, hipLaunchKernelGGL((colpart_k<T, 0, VV>), grid, dim3(256), 0, s, (const T*)x,
                                                       nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
-                                                      (float*)ws, R, C, rpb, 0)));
-  hipLaunchKernelGGL(colsum_finalize_k, dim3((C + 255) / 256), dim3(256), 0, s, (const float*)ws, NSLOT, C,
+                                                      (float*)ws, R, C, rpb, 0, g_bn_det)));
+  hipLaunchKernelGGL(colsum_finalize_k, fin_grid(C), dim3(256), 0, s, (const float*)ws, fin_rows(grid), C,
                      (float*)out0, (float*)out1, accumulate);
 }
 
@@ -396,11 +439,21 @@ void sg_bn_fwd_stats(const void* x, void* ws, const void* gamma, const void* bet
   dim3 grid;
   int rpb, V;
   colgrid(R, C, grid, rpb, V);
-  hipMemsetAsync(ws, 0, sizeof(float) * NSLOT * 2 * C, s);
+  zero_ws(ws, C, s);
   DISPATCH_FT(dtype, DISPATCH_V(V, hipLaunchKernelGGL((colpart_k<T, 0, VV>), grid, dim3(256), 0, s, (const T*)x,
                                                       nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
-                                                      (float*)ws, R, C, rpb, 0)));
-  hipLaunchKernelGGL(bn_fwd_finalize_k, dim3((C + 255) / 256), dim3(256), 0, s, (const float*)ws, NSLOT, C,
+                                                      (float*)ws, R, C, rpb, 0, g_bn_det)));
+  hipLaunchKernelGGL(bn_fwd_finalize_k, fin_grid(C), dim3(256), 0, s, (const float*)ws, fin_rows(grid), C,
+                     (const float*)gamma, (const float*)beta, (float*)run_mean, (float*)run_var, (float*)mean,
+                     (float*)invstd, (float*)scale, (float*)shift, (float)R, momentum, eps);
+}
+
+// finalize only: the per-tile column sums were produced by the conv
+// epilogue (igemm stats) into ws [nb][2][C]
+void sg_bn_fwd_from_ws(const void* ws, int nb, const void* gamma, const void* beta, void* run_mean, void* run_var,
+                       void* mean, void* invstd, void* scale, void* shift, int64_t R, int C, float momentum,
+                       float eps, hipStream_t s) {
+  hipLaunchKernelGGL(bn_fwd_finalize_k, fin_grid(C), dim3(256), 0, s, (const float*)ws, nb, C,
                      (const float*)gamma, (const float*)beta, (float*)run_mean, (float*)run_var, (float*)mean,
                      (float*)invstd, (float*)scale, (float*)shift, (float)R, momentum, eps);
 }
@@ -429,12 +482,12 @@ void sg_bn_bwd(const void* x, const void* dy, const void* y, const void* scale, 
   dim3 grid;
   int rpb, V;
   colgrid(R, C, grid, rpb, V);
-  hipMemsetAsync(ws, 0, sizeof(float) * NSLOT * 2 * C, s);
+  zero_ws(ws, C, s);
   DISPATCH_FT(dtype, DISPATCH_V(V, hipLaunchKernelGGL((colpart_k<T, 1, VV>), grid, dim3(256), 0, s, (const T*)x,
                                                       (const T*)dy, (const T*)y, (const float*)scale,
                                                       (const float*)shift, (const float*)mean, (const float*)invstd,
-                                                      (float*)ws, R, C, rpb, mask_mode)));
-  hipLaunchKernelGGL(bn_bwd_finalize_k, dim3((C + 255) / 256), dim3(256), 0, s, (const float*)ws, NSLOT, C,
+                                                      (float*)ws, R, C, rpb, mask_mode, g_bn_det)));
+  hipLaunchKernelGGL(bn_bwd_finalize_k, fin_grid(C), dim3(256), 0, s, (const float*)ws, fin_rows(grid), C,
                      (const float*)gamma, (const float*)mean, (const float*)invstd, (float*)coef, (float*)dg,
                      (float*)db, (float)R);
   dim3 ag = apply_grid(R, C, V);

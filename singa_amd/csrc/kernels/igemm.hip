@@ -84,6 +84,8 @@ struct GemmArgs {
   int64_t sa, sb, sc;  // batch strides (elements), blockIdx.y = batch
   int out_phase;       // dgrad: output rows map through the phase grid
   int lds_epilogue;    // stage bf16 output tiles through LDS (16-byte stores)
+  float* stats;        // optional BN statistics of the bf16 output: ws[row][2][N] (sum, sum of squares)
+  int stats_det;       // 1: row = tile row, plain stores (deterministic); 0: row = tile row % 32, atomics
   ConvGeom g;
 };
 
@@ -472,6 +474,9 @@ __global__ void __launch_bounds__(NT, 2) igemm_k(const GemmArgs p) {
       constexpr int RPP = NT / CPRW;           // rows per pass
       const int ch = threadIdx.x % CPRW, r0 = threadIdx.x / CPRW;
       const int n = n0 + ch * 8;
+      float st_s[8], st_q[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) { st_s[r] = 0.f; st_q[r] = 0.f; }
       if (n < p.N) {
 #pragma unroll
         for (int pass = 0; pass < BM / RPP; ++pass) {
@@ -502,6 +507,50 @@ __global__ void __launch_bounds__(NT, 2) igemm_k(const GemmArgs p) {
 #pragma unroll
           for (int r = 0; r < 8; ++r) o[r] = (bf16)(p.relu ? fmaxf(v[r], 0.f) : v[r]);
           *(bf16x8*)c = o;
+          if (p.stats) {
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+              const float f = (float)o[r];
+              st_s[r] += f;
+              st_q[r] += f * f;
+            }
+          }
+        }
+      }
+      if (p.stats) {
+        // fused BatchNorm statistics: reduce the RPP row-threads of each
+        // 8-channel chunk through LDS, then one plain store per channel into
+        // row tm of the [tiles_m][2][N] workspace (bn_fwd_finalize sums the
+        // rows in a fixed order: deterministic)
+        __syncthreads();
+        float* red = (float*)smem;  // [NT][16]
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          red[threadIdx.x * 16 + r] = st_s[r];
+          red[threadIdx.x * 16 + 8 + r] = st_q[r];
+        }
+        __syncthreads();
+        if (threadIdx.x < CPRW && n < p.N) {
+          float a[16];
+#pragma unroll
+          for (int r = 0; r < 16; ++r) a[r] = red[threadIdx.x * 16 + r];
+          for (int k = 1; k < RPP; ++k)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) a[r] += red[(k * CPRW + threadIdx.x) * 16 + r];
+          if (p.stats_det) {  // own row per tile-row: plain stores, ordered finalize
+            float* ws = p.stats + (int64_t)tm * 2 * p.N;
+            *(float4*)(ws + n) = make_float4(a[0], a[1], a[2], a[3]);
+            *(float4*)(ws + n + 4) = make_float4(a[4], a[5], a[6], a[7]);
+            *(float4*)(ws + p.N + n) = make_float4(a[8], a[9], a[10], a[11]);
+            *(float4*)(ws + p.N + n + 4) = make_float4(a[12], a[13], a[14], a[15]);
+          } else {  // 32 atomic slot rows (zeroed by the caller)
+            float* ws = p.stats + (int64_t)(tm & 31) * 2 * p.N;
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+              atomicAdd(ws + n + r, a[r]);
+              atomicAdd(ws + p.N + n + r, a[8 + r]);
+            }
+          }
         }
       }
       return;
@@ -726,6 +775,8 @@ static inline int kps(int K, int splits) {
 
 extern "C" {
 
+int sg_bn_deterministic();  // batchnorm.hip: deterministic-reduction mode
+
 // Plain GEMM: C[M][N] = alpha * sum_k A(m,k) B(n,k) (+ beta*C) ... with
 //   a_kouter = 0: A stored [M][K] (lda), 1: A stored [K][M]
 //   b_kouter = 0: B stored [N][K] (ldb), 1: B stored [K][N]
@@ -756,8 +807,10 @@ void sg_gemm(const void* a, int64_t lda, int a_kouter, const void* b, int64_t ld
 // conv forward: x NHWC bf16, w [K][R][S][C] bf16 -> y [N*Ho*Wo][K]
 void sg_conv_fwd(const void* x, const void* w, void* y, const void* bias, int N, int H, int W, int C, int K, int R,
                  int S, int Ho, int Wo, int sh, int sw, int ph, int pw, int dh, int dw, int relu, int out_mode,
-                 hipStream_t s) {
+                 void* stats, hipStream_t s) {
   GemmArgs p{};
+  p.stats = (out_mode == OUT_BF16 && (K & 7) == 0 && g_tune[1]) ? (float*)stats : nullptr;
+  p.stats_det = sg_bn_deterministic();
   p.g = make_geom(N, H, W, C, K, R, S, Ho, Wo, sh, sw, ph, pw, dh, dw);
   p.M = N * Ho * Wo; p.N = K; p.K = R * S * C;
   p.a = (const bf16*)x; p.lda = 0; p.b = (const bf16*)w; p.ldb = R * S * C;
@@ -797,8 +850,20 @@ void sg_conv_wgrad(const void* x, const void* dy, void* dw_out, int N, int H, in
   int BM, BN, sp;
   pick_wgrad(p.M, p.N, p.K, g_tune[0], BM, BN, sp);
   if (splits > 0) sp = splits;
+  if (sg_bn_deterministic()) sp = 1;  // one writer per gradient element: reproducible
   p.k_per_split = kps(p.K, sp);
   launch_tile<LM_KOUTER, LM_WGRAD_B, OUT_F32_ATOMIC>(p, p.M, BM, BN, sp, s, 1, 0);
+}
+
+// rows of the fused-BN-statistics workspace a conv forward writes
+// ([rows][2][K]: tiles_m in deterministic mode, else 32 atomic slot rows that
+// the caller zeroes); 0 if that conv cannot produce them
+int sg_conv_stats_rows(int M, int N) {
+  if ((N & 7) != 0 || !g_tune[1]) return 0;
+  if (!sg_bn_deterministic()) return 32;
+  int BM, BN;
+  pick_tile(M, N, BM, BN);
+  return (M + BM - 1) / BM;
 }
 
 void sg_set_tuning(int key, int value) {

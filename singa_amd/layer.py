@@ -118,7 +118,12 @@ class Layer:
 
     @staticmethod
     def _assign(dst: Tensor, v) -> None:
-        src = v.data if isinstance(v, Tensor) else torch.as_tensor(np.asarray(v))
+        if isinstance(v, Tensor):
+            src = v.data
+        elif isinstance(v, torch.Tensor):
+            src = v
+        else:
+            src = torch.as_tensor(np.asarray(v))
         dst.data.copy_(src.reshape(dst.shape).to(device=dst.data.device, dtype=dst.dtype))
         if dst.low is not None:
             dst.low.copy_(dst.data.to(dst.low.dtype))
@@ -228,7 +233,7 @@ class Conv2d(Layer):
 
     def forward(self, x):
         op = autograd.Conv2d(self.stride, self.padding, self.dilation, self.group, has_bias=self.bias,
-                             fuse_relu=(self.activation == "RELU"))
+                             fuse_relu=(self.activation == "RELU"), bn_stats=getattr(self, "bn_stats", False))
         return op(x, self.W, self.b) if self.bias else op(x, self.W)
 
 

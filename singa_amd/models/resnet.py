@@ -52,6 +52,13 @@ class InputPrep(autograd.Operator):
         return None
 
 
+def _feeds_bn(*convs):
+    """Mark convolutions whose output goes straight into a BatchNorm: their
+    epilogue sums the BN statistics (no separate statistics pass)."""
+    for c in convs:
+        c.bn_stats = True
+
+
 class Bottleneck(layer.Layer):
     expansion = 4
 
@@ -67,6 +74,7 @@ class Bottleneck(layer.Layer):
         if downsample:
             self.down_conv = layer.Conv2d(planes * self.expansion, 1, stride=stride, bias=False)
             self.down_bn = layer.BatchNorm2d()
+        _feeds_bn(self.conv1, self.conv2, self.conv3, *([self.down_conv] if downsample else []))
 
     def forward(self, x):
         out = self.bn1(self.conv1(x), relu=True)
@@ -88,6 +96,7 @@ class BasicBlock(layer.Layer):
         if downsample:
             self.down_conv = layer.Conv2d(planes, 1, stride=stride, bias=False)
             self.down_bn = layer.BatchNorm2d()
+        _feeds_bn(self.conv1, self.conv2, *([self.down_conv] if downsample else []))
 
     def forward(self, x):
         out = self.bn1(self.conv1(x), relu=True)
@@ -103,6 +112,7 @@ class ResNet(model.Model):
         self.num_classes = num_classes
         self.conv1 = layer.Conv2d(num_channels, 64, 7, stride=2, padding=3, bias=False)
         self.bn1 = layer.BatchNorm2d()
+        _feeds_bn(self.conv1)
         self.maxpool = layer.MaxPool2d(3, 2, 1)
         blocks: List[layer.Layer] = []
         inplanes = 64

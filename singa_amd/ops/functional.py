@@ -18,6 +18,7 @@ kernel.
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional, Sequence, Tuple
 
 import torch
@@ -46,6 +47,9 @@ def _native_ok(*ts: torch.Tensor) -> bool:
 
 def _flat_ok(t: torch.Tensor) -> bool:
     return t.dtype in (torch.float32, torch.bfloat16) and (t.is_contiguous() or N.is_cl(t))
+
+
+_NO_BN_STATS = os.environ.get("SG_NO_BN_STATS", "0") == "1"
 
 
 def _same_layout(a: torch.Tensor, b: torch.Tensor) -> bool:
@@ -431,8 +435,12 @@ def to_nhwc_bf16(x: torch.Tensor, cpad: Optional[int] = None) -> torch.Tensor:
 
 
 def conv2d_fwd(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], stride, padding, dilation=(1, 1),
-               groups: int = 1, out_dtype: Optional[torch.dtype] = None, relu: bool = False) -> torch.Tensor:
-    """x [N,C,H,W], w [K,C/g,R,S] -> y [N,K,Ho,Wo] (channels_last on GPU)."""
+               groups: int = 1, out_dtype: Optional[torch.dtype] = None, relu: bool = False,
+               bn_stats: bool = False) -> torch.Tensor:
+    """x [N,C,H,W], w [K,C/g,R,S] -> y [N,K,Ho,Wo] (channels_last on GPU).
+    ``bn_stats``: the epilogue also sums per-channel (x, x^2) of the bf16
+    output into a BatchNorm workspace attached as ``y._sg_bn_ws`` (the next
+    BatchNorm skips its statistics pass)."""
     out_dtype = out_dtype or x.dtype
     sh, sw = stride
     ph, pw = padding
@@ -459,8 +467,18 @@ def conv2d_fwd(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], stri
             bias = bias.contiguous()
         od = torch.bfloat16 if out_dtype == torch.bfloat16 else torch.float32
         y = torch.empty((Nn, Kp, Ho, Wo), dtype=od, device=x.device, memory_format=torch.channels_last)
+        ws, rows = None, 0
+        if (bn_stats and od == torch.bfloat16 and Kp == K and out_dtype == torch.bfloat16 and not relu
+                and not _NO_BN_STATS):
+            L = N.lib()
+            rows = L.conv_stats_rows(Nn * Ho * Wo, K)
+            if rows > 0:  # deterministic mode: every row written (plain stores); else 32 atomic slot rows
+                ws = (torch.empty if L.deterministic() else torch.zeros)(rows * 2 * K, dtype=torch.float32,
+                                                                          device=x.device)
         N.lib().conv_fwd(xb.data_ptr(), wb.data_ptr(), y.data_ptr(), N.ptr(bias), Nn, H, W, Cp, Kp, R, S, Ho, Wo, sh,
-                         sw, ph, pw, dh, dw, int(relu), 0 if od == torch.bfloat16 else 1, N.stream())
+                         sw, ph, pw, dh, dw, int(relu), 0 if od == torch.bfloat16 else 1, N.stream(), N.ptr(ws))
+        if ws is not None:
+            y._sg_bn_ws = (ws, rows)
         if Kp != K:
             y = y[:, :K].contiguous(memory_format=torch.channels_last)
         return y if y.dtype == out_dtype else y.to(out_dtype)
@@ -554,9 +572,12 @@ _BANDS: dict = {}
 
 
 def _ws(R: int, C: int, device) -> torch.Tensor:
-    n = _BANDS.get(C)
+    """Partial-sum workspace of a [R][C] column reduction (no zeroing needed:
+    every [band][2][C] slot is written)."""
+    key = (R, C, N.lib().deterministic())
+    n = _BANDS.get(key)
     if n is None:
-        n = _BANDS[C] = N.lib().colreduce_ws(C)
+        n = _BANDS[key] = N.lib().colreduce_ws(R, C)
     return torch.empty(n, dtype=torch.float32, device=device)
 
 
@@ -602,7 +623,12 @@ def batchnorm_fwd(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, run_
         dev = x.device
         p = torch.empty(4 * C, dtype=torch.float32, device=dev)
         mean, invstd, scale, shift = p[:C], p[C:2 * C], p[2 * C:3 * C], p[3 * C:]
-        if training:
+        pre = getattr(x, "_sg_bn_ws", None)  # statistics already summed by the producing conv's epilogue
+        if training and pre is not None and pre[0].numel() == pre[1] * 2 * C:
+            L.bn_fwd_from_ws(pre[0].data_ptr(), pre[1], gamma.data_ptr(), beta.data_ptr(), run_mean.data_ptr(),
+                             run_var.data_ptr(), mean.data_ptr(), invstd.data_ptr(), scale.data_ptr(),
+                             shift.data_ptr(), R, C, momentum, eps, N.stream())
+        elif training:
             L.bn_fwd_stats(x.data_ptr(), _ws(R, C, dev).data_ptr(), gamma.data_ptr(), beta.data_ptr(),
                            run_mean.data_ptr(), run_var.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
                            scale.data_ptr(), shift.data_ptr(), R, C, momentum, eps, N.dt(x), N.stream())

@@ -31,6 +31,8 @@ def _load():
     except Exception as e:  # pragma: no cover - reported through lib()
         _err = e
         return _lib
+    if os.environ.get("SINGA_AMD_DETERMINISTIC", "0") == "1" and hasattr(_lib, "set_deterministic"):
+        _lib.set_deterministic(1)
     # kernel tuning knobs from the environment: SG_TUNE="0=4,1=1" (key=value)
     for kv in os.environ.get("SG_TUNE", "").split(","):
         if "=" in kv and hasattr(_lib, "set_tuning"):

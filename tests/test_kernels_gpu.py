@@ -365,3 +365,75 @@ def test_easgd_and_rsync_kernels(gpu):
     NT.lib().rsync_gather(w.data_ptr(), snap.data_ptr(), out.data_ptr(), 100, 1000, 7, 13, NT.stream())
     idx = (13 + torch.arange(100) * 7) % 1000
     assert rel_err(out, (w - snap)[idx.to(gpu)]) < 1e-6
+
+
+@pytest.mark.parametrize("det", [False, True])
+@pytest.mark.parametrize("C,K,H", [(64, 256, 28), (128, 64, 14), (32, 1024, 7)])
+def test_conv_epilogue_bn_stats(gpu, C, K, H, det):
+    """BN statistics summed by the conv epilogue == the separate stats pass."""
+    import singa_amd
+    from singa_amd.ops import functional as F
+    singa_amd.set_deterministic(det)
+    g = torch.Generator(device=gpu).manual_seed(1)
+    x = torch.randn(8, C, H, H, device=gpu, generator=g).bfloat16().contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(K, C, 3, 3, device=gpu, generator=g) * 0.05).bfloat16().contiguous(
+        memory_format=torch.channels_last)
+    y1 = F.conv2d_fwd(x, w, None, (1, 1), (1, 1), out_dtype=torch.bfloat16, bn_stats=True)
+    assert getattr(y1, "_sg_bn_ws", None) is not None
+    y2 = F.conv2d_fwd(x, w, None, (1, 1), (1, 1), out_dtype=torch.bfloat16)
+    assert torch.equal(y1, y2)
+    gam = torch.rand(K, device=gpu) + 0.5
+    bet = torch.randn(K, device=gpu)
+    outs = []
+    for y in (y1, y2):
+        rm, rv = torch.zeros(K, device=gpu), torch.ones(K, device=gpu)
+        out, st = F.batchnorm_fwd(y, gam, bet, rm, rv, True, 0.1, 1e-5, relu=True)
+        outs.append((out.float(), st.mean.clone(), st.invstd.clone(), rm, rv))
+    singa_amd.set_deterministic(False)
+    for a, b in zip(outs[0], outs[1]):
+        assert rel_err(a, b) < 1e-4
+
+
+@pytest.mark.parametrize("C,K,H,R,st", [(64, 256, 56, 1, 1), (128, 128, 28, 3, 1), (256, 64, 56, 1, 1),
+                                         (512, 512, 7, 3, 1), (256, 512, 56, 1, 2)])
+def test_conv_bitwise_deterministic(gpu, C, K, H, R, st):
+    """Repeated launches with allocator churn in between give bit-identical
+    outputs (fwd with/without fused BN stats, dgrad)."""
+    from singa_amd.ops import functional as F
+    g = torch.Generator(device=gpu).manual_seed(3)
+    x = torch.randn(32, C, H, H, device=gpu, generator=g).bfloat16().contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(K, C, R, R, device=gpu, generator=g) * 0.05).bfloat16().contiguous(
+        memory_format=torch.channels_last)
+    pad = R // 2
+    ref = F.conv2d_fwd(x, w, None, (st, st), (pad, pad), out_dtype=torch.bfloat16)
+    dy = torch.randn(ref.shape, device=gpu, generator=g).bfloat16().contiguous(memory_format=torch.channels_last)
+    dref = F.conv2d_bwd(x, w, dy, (st, st), (pad, pad), need_dx=True)[0]
+    junk = []
+    for i in range(12):
+        junk.append(torch.randn(int(1e6) * (1 + i % 3), device=gpu))
+        if i % 4 == 3:
+            junk.clear()
+        y = F.conv2d_fwd(x, w, None, (st, st), (pad, pad), out_dtype=torch.bfloat16, bn_stats=bool(i % 2))
+        assert torch.equal(y, ref), i
+        d = F.conv2d_bwd(x, w, dy, (st, st), (pad, pad), need_dx=True)[0]
+        assert torch.equal(d, dref), i
+
+
+@pytest.mark.parametrize("C,H", [(64, 56), (256, 14), (2048, 7)])
+def test_batchnorm_bitwise_deterministic(gpu, C, H):
+    import singa_amd
+    from singa_amd.ops import functional as F
+    singa_amd.set_deterministic(True)
+    g = torch.Generator(device=gpu).manual_seed(4)
+    x = (torch.randn(64, C, H, H, device=gpu, generator=g) * 3 + 1).bfloat16().contiguous(
+        memory_format=torch.channels_last)
+    gam, bet = torch.rand(C, device=gpu) + 0.5, torch.randn(C, device=gpu)
+    outs = []
+    for _ in range(6):
+        y, st = F.batchnorm_fwd(x, gam, bet, torch.zeros(C, device=gpu), torch.ones(C, device=gpu), True, 0.1, 1e-5,
+                                relu=True)
+        outs.append((y, st.mean.clone(), st.invstd.clone()))
+    singa_amd.set_deterministic(False)
+    for o in outs[1:]:
+        assert torch.equal(o[1], outs[0][1]) and torch.equal(o[2], outs[0][2])
+        assert torch.equal(o[0], outs[0][0])
