@@ -37,6 +37,9 @@ def main() -> int:
                     help="HIP-graph replay of forward+backward (default for 1 GPU)")
     ap.add_argument("--no-graph", dest="graph", action="store_false",
                     help="eager execution; the default for N>1, where bucketed all-reduces overlap the backward")
+    ap.add_argument("--loss-curve", action="store_true", help="record every step's loss (syncs; diagnostics only)")
+    ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--sync-warmup", action="store_true", help="synchronize after every warmup step (diagnostics)")
     ap.add_argument("--lr", type=float, default=0.01,
                     help="SGD lr (random labels + no warmup: 0.1 occasionally diverges; throughput is lr-independent)")
     args = ap.parse_args()
@@ -60,7 +63,7 @@ def main() -> int:
     from singa_amd.parallel import DistOpt, init_distributed
 
     dev = device.create_rocm_gpu_on(local % torch.cuda.device_count(), set_default=True)
-    dev.SetRandSeed(1234 + rank)
+    dev.SetRandSeed(args.seed + rank)
     comm = init_distributed(rank=rank, world_size=world, local_rank=local)
 
     m = resnet.create_model(args.depth, num_classes=1000, compute_dtype=torch.bfloat16)
@@ -84,13 +87,18 @@ def main() -> int:
 
     for _ in range(args.warmup):
         out, loss = m(tx, ty)
+        if args.sync_warmup:
+            torch.cuda.synchronize()
     torch.cuda.synchronize()
     if world > 1:
         comm.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    curve = []
     for _ in range(args.steps):
         out, loss = m(tx, ty)
+        if args.loss_curve:
+            curve.append(round(float(loss.data.float().item()), 4))
     torch.cuda.synchronize()
     if world > 1:
         comm.barrier()
@@ -121,6 +129,8 @@ def main() -> int:
                        "exec": "hipgraph" if use_graph else "eager", "optimizer": "SGD momentum 0.9 wd 1e-4",
                        "final_loss": round(final_loss, 4)},
         }
+        if curve:
+            rec["config"]["loss_curve"] = curve
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.barrier()

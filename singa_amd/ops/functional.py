@@ -472,9 +472,8 @@ def conv2d_fwd(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], stri
                 and not _NO_BN_STATS):
             L = N.lib()
             rows = L.conv_stats_rows(Nn * Ho * Wo, K)
-            if rows > 0:  # deterministic mode: every row written (plain stores); else 32 atomic slot rows
-                ws = (torch.empty if L.deterministic() else torch.zeros)(rows * 2 * K, dtype=torch.float32,
-                                                                          device=x.device)
+            if rows > 0:  # deterministic: every row written (plain stores); else 32 atomic slot rows zeroed by conv_fwd
+                ws = torch.empty(rows * 2 * K, dtype=torch.float32, device=x.device)
         N.lib().conv_fwd(xb.data_ptr(), wb.data_ptr(), y.data_ptr(), N.ptr(bias), Nn, H, W, Cp, Kp, R, S, Ho, Wo, sh,
                          sw, ph, pw, dh, dw, int(relu), 0 if od == torch.bfloat16 else 1, N.stream(), N.ptr(ws))
         if ws is not None:

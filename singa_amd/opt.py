@@ -232,9 +232,11 @@ class Optimizer:
         outside graph capture; the captured update kernel reads it)."""
         if self._hp_dev is None:
             return
-        self._hp_host[0] = self.current_lr()
-        self._hp_host[1] = float(self.step_counter + 1)
-        self._hp_dev.copy_(self._hp_host, non_blocking=True)
+        # two scalar fill kernels: the values travel as kernel arguments, so
+        # the host can run ahead of the GPU without racing a pinned staging
+        # buffer that an earlier, still-queued async copy would read later
+        self._hp_dev[0].fill_(self.current_lr())
+        self._hp_dev[1].fill_(float(self.step_counter + 1))
 
     # -- SINGA API -----------------------------------------------------------
     def __call__(self, loss: Tensor) -> None:

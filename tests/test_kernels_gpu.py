@@ -437,3 +437,109 @@ def test_batchnorm_bitwise_deterministic(gpu, C, H):
     for o in outs[1:]:
         assert torch.equal(o[1], outs[0][1]) and torch.equal(o[2], outs[0][2])
         assert torch.equal(o[0], outs[0][0])
+
+
+def _guarded(n, dtype, gpu, pad=4096):
+    """A view of n elements inside a buffer with `pad` sentinel elements on
+    both sides; returns (view, check) where check() asserts the guards."""
+    buf = torch.full((n + 2 * pad,), 7.0, dtype=dtype, device=gpu)
+    view = buf[pad:pad + n]
+
+    def check(tag):
+        torch.cuda.synchronize()
+        assert bool((buf[:pad] == 7.0).all()), f"{tag}: write before the buffer"
+        assert bool((buf[pad + n:] == 7.0).all()), f"{tag}: write past the buffer"
+    return view, check
+
+
+@pytest.mark.parametrize("Nb,C,K,H,R,st", [(3, 64, 256, 14, 1, 1), (2, 128, 128, 15, 3, 2), (2, 96, 40, 9, 3, 1),
+                                           (4, 256, 64, 7, 1, 2), (2, 8, 64, 33, 7, 2)])
+def test_conv_kernels_stay_in_bounds(gpu, Nb, C, K, H, R, st):
+    from singa_amd.ops import native as NN
+    L = NN.lib()
+    pad = R // 2
+    Ho = (H + 2 * pad - R) // st + 1
+    g = torch.Generator(device=gpu).manual_seed(9)
+    x = torch.randn(Nb * H * H * C, device=gpu, generator=g).bfloat16()
+    w = (torch.randn(K * R * R * C, device=gpu, generator=g) * 0.05).bfloat16()
+    dy = torch.randn(Nb * Ho * Ho * K, device=gpu, generator=g).bfloat16()
+    s = NN.stream()
+    for stats in (False, True):
+        y, chk = _guarded(Nb * Ho * Ho * K, torch.bfloat16, gpu)
+        ws = None
+        if stats:
+            rows = L.conv_stats_rows(Nb * Ho * Ho, K)
+            ws, wchk = _guarded(max(rows, 1) * 2 * K, torch.float32, gpu)
+            ws.zero_()
+        L.conv_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), 0, Nb, H, H, C, K, R, R, Ho, Ho, st, st, pad, pad, 1, 1,
+                   0, 0, s, ws.data_ptr() if ws is not None else 0)
+        chk("conv_fwd")
+        if ws is not None:
+            wchk("conv_fwd stats")
+    if st * st <= 16:
+        dx, chk = _guarded(Nb * H * H * C, torch.bfloat16, gpu)
+        L.conv_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), Nb, H, H, C, K, R, R, Ho, Ho, st, st, pad, pad, 1, 1, 0,
+                     s)
+        chk("conv_dgrad")
+    dw, chk = _guarded(K * R * R * C, torch.float32, gpu)
+    dw.zero_()
+    L.conv_wgrad(x.data_ptr(), dy.data_ptr(), dw.data_ptr(), Nb, H, H, C, K, R, R, Ho, Ho, st, st, pad, pad, 1, 1, 0, s)
+    chk("conv_wgrad")
+
+
+@pytest.mark.parametrize("R,C", [(1000, 64), (37, 256), (4096, 24)])
+def test_bn_kernels_stay_in_bounds(gpu, R, C):
+    from singa_amd.ops import native as NN
+    L = NN.lib()
+    s = NN.stream()
+    g = torch.Generator(device=gpu).manual_seed(10)
+    x = torch.randn(R * C, device=gpu, generator=g).bfloat16()
+    dy = torch.randn(R * C, device=gpu, generator=g).bfloat16()
+    f = lambda: torch.rand(C, device=gpu) + 0.5  # noqa: E731
+    gam, bet, rm, rv = f(), f(), torch.zeros(C, device=gpu), torch.ones(C, device=gpu)
+    p = [torch.empty(C, device=gpu) for _ in range(4)]
+    ws, wchk = _guarded(L.colreduce_ws(R, C), torch.float32, gpu)
+    L.bn_fwd_stats(x.data_ptr(), ws.data_ptr(), gam.data_ptr(), bet.data_ptr(), rm.data_ptr(), rv.data_ptr(),
+                   *[t.data_ptr() for t in p], R, C, 0.1, 1e-5, NN.BF16, s)
+    wchk("bn_fwd_stats ws")
+    y, chk = _guarded(R * C, torch.bfloat16, gpu)
+    L.bn_apply(x.data_ptr(), p[2].data_ptr(), p[3].data_ptr(), 0, y.data_ptr(), R, C, 1, NN.BF16, s)
+    chk("bn_apply")
+    coef = torch.empty(3 * C, device=gpu)
+    dg, db = torch.zeros(C, device=gpu), torch.zeros(C, device=gpu)
+    dx, chk2 = _guarded(R * C, torch.bfloat16, gpu)
+    dres, chk3 = _guarded(R * C, torch.bfloat16, gpu)
+    L.bn_bwd(x.data_ptr(), dy.data_ptr(), y.data_ptr(), p[2].data_ptr(), p[3].data_ptr(), p[0].data_ptr(),
+             p[1].data_ptr(), gam.data_ptr(), ws.data_ptr(), coef.data_ptr(), dg.data_ptr(), db.data_ptr(),
+             dx.data_ptr(), dres.data_ptr(), R, C, 1, NN.BF16, s)
+    wchk("bn_bwd ws")
+    chk2("bn_bwd dx")
+    chk3("bn_bwd dres")
+
+
+def test_fused_bn_stats_under_graph_replay(gpu):
+    """conv (+epilogue BN statistics) -> BN, captured once and replayed: every
+    replay must see freshly zeroed statistics (identical outputs)."""
+    from singa_amd.ops import functional as F
+    g = torch.Generator(device=gpu).manual_seed(11)
+    x = torch.randn(8, 64, 28, 28, device=gpu, generator=g).bfloat16().contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(128, 64, 3, 3, device=gpu, generator=g) * 0.05).bfloat16().contiguous(
+        memory_format=torch.channels_last)
+    gam, bet = torch.rand(128, device=gpu) + 0.5, torch.randn(128, device=gpu)
+    rm, rv = torch.zeros(128, device=gpu), torch.ones(128, device=gpu)
+
+    def step():
+        y = F.conv2d_fwd(x, w, None, (1, 1), (1, 1), out_dtype=torch.bfloat16, bn_stats=True)
+        out, st = F.batchnorm_fwd(y, gam, bet, rm, rv, True, 0.1, 1e-5, relu=True)
+        return out, st.mean, st.invstd
+
+    ref = [t.clone() for t in step()]
+    torch.cuda.synchronize()
+    gr = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(gr):
+        outs = step()
+    for _ in range(4):
+        gr.replay()
+        torch.cuda.synchronize()
+        for a, b in zip(outs, ref):
+            assert rel_err(a, b) < 1e-5

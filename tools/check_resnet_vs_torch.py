@@ -45,14 +45,19 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--lr", type=float, default=0.02)
+    ap.add_argument("--set-default", action="store_true", help="make the GPU the default device (as bench.py does)")
+    ap.add_argument("--modes", default="eager,graph")
+    ap.add_argument("--no-sync", action="store_true", help="do not read the loss between steps (async replays)")
+    ap.add_argument("--torch", action="store_true", default=True)
+    ap.add_argument("--no-torch", dest="torch", action="store_false")
     a = ap.parse_args()
     rng = np.random.RandomState(0)
     X = rng.standard_normal((a.batch, 3, 224, 224)).astype(np.float32)
     Y = rng.randint(0, 1000, a.batch).astype(np.int32)
     out = {}
     init = None
-    for mode in ("eager", "graph"):
-        dev = device.create_rocm_gpu()
+    for mode in a.modes.split(","):
+        dev = device.create_rocm_gpu(set_default=a.set_default)
         dev.SetRandSeed(7)
         m = resnet.resnet50(num_classes=1000, compute_dtype=torch.bfloat16)
         m.set_optimizer(opt.SGD(a.lr, 0.9, weight_decay=1e-4))
@@ -67,8 +72,11 @@ def main():
         ls = []
         for _ in range(a.steps):
             _, l = m(x, y)
-            ls.append(round(float(l.data.float().cpu()), 4))
-        out[mode] = ls
+            ls.append(l.data.float().clone() if a.no_sync else round(float(l.data.float().cpu()), 4))
+        out[mode] = [round(float(v), 4) for v in ls]
+    if not a.torch:
+        print(json.dumps(out))
+        return
     topt = torch.optim.SGD(tm.parameters(), lr=a.lr, momentum=0.9, weight_decay=1e-4)
     xt, yt = torch.from_numpy(X).cuda(), torch.from_numpy(Y).long().cuda()
     ls = []
