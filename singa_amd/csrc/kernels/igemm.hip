@@ -36,6 +36,8 @@
 //   * wgrad splits the pixel reduction across workgroups (blockIdx.z) and
 //     accumulates fp32 partial tiles atomically into the [K][R][S][C]
 //     gradient (the layout of the flat gradient buffer).
+#include <stdexcept>
+
 #include "common.h"
 
 namespace sg {
@@ -84,6 +86,7 @@ struct GemmArgs {
   int64_t sa, sb, sc;  // batch strides (elements), blockIdx.y = batch
   int out_phase;       // dgrad: output rows map through the phase grid
   int lds_epilogue;    // stage bf16 output tiles through LDS (16-byte stores)
+  unsigned a_bytes, b_bytes;  // operand extents (buffer-resource ranges; per batch slice)
   float* stats;        // optional BN statistics of the bf16 output: ws[row][2][N] (sum, sum of squares)
   int stats_det;       // 1: row = tile row, plain stores (deterministic); 0: row = tile row % 32, atomics
   ConvGeom g;
@@ -112,13 +115,17 @@ __device__ __forceinline__ uint4 sel(bool ok, uint4 v) { return ok ? v : make_ui
 // Conv gathers cache each vector's row pointer for the current filter tap and
 // recompute it only when the (wave-uniform) tap changes.
 // ------------------------------------------------------------------------------
-__device__ __attribute__((aligned(16))) uint4 sg_zero_page[4];
-
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
-typedef const __attribute__((address_space(1))) void* gbl_ptr_t;
 
-__device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)lds_wave_base, 16, 0, 0);
+// 16-byte buffer load straight into LDS (buffer_load_dwordx4 ... offen lds):
+// 32-bit byte offsets against a buffer resource; an offset past num_records
+// returns zeros, which implements padding / out-of-range rows for free.
+constexpr unsigned OOB = 0xFFFFFFF0u;
+__device__ __forceinline__ void bld16(__amdgpu_buffer_rsrc_t rsrc, unsigned off, char* lds_wave_base) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)lds_wave_base, 16, off, 0, 0, 0);
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
 }
 
 template <int ROWS, int MODE>
@@ -127,20 +134,23 @@ struct Loader {
   static constexpr bool KOUT = (MODE == LM_KOUTER || MODE == LM_WGRAD_B || MODE == LM_DGRAD_B);
   static constexpr int CPR = ROWS / 8;  // KOUTER: chunks per k-row
   static constexpr int KRP = NT / CPR;  // KOUTER: k-rows per pass
-  int64_t base[VPT];
+  int base[VPT];  // element offsets (operands are < 2 GiB: checked by the host)
   int i0[VPT], j0[VPT];
+  __amdgpu_buffer_rsrc_t rsrc;
   bool ok[VPT];
   int64_t ld;
   int lchunk;                 // KMAJOR: the k-chunk this lane fetches (swizzled)
   int cr, cs, cc;             // WGRAD_B: fixed column decomposition
   bool cok;
-  int tap_cached;             // conv gathers: tap of the cached row pointers
-  const bf16* rp[VPT];        // conv gathers: row pointer at the cached tap (nullptr = zero)
+  int tap_cached;             // conv gathers: tap of the cached row offsets
+  int ro[VPT];                // conv gathers: row element offset at the cached tap (-1 = zero)
 
-  __device__ __forceinline__ void init(const GemmArgs& p, int row0, int nrows, const Phase& P, int64_t ld_) {
+  __device__ __forceinline__ void init(const GemmArgs& p, int row0, int nrows, const Phase& P, int64_t ld_,
+                                       const bf16* src, unsigned bytes) {
     const int t = threadIdx.x;
     ld = ld_;
     tap_cached = -1;
+    rsrc = make_rsrc(src, bytes);
     if constexpr (!KOUT) {
       const int row_l = t >> 3;  // (row >> 1) & 7 is the same for every v (32v keeps bits 1-3)
       lchunk = (t & 7) ^ ((row_l >> 1) & 7);
@@ -150,14 +160,14 @@ struct Loader {
         ok[v] = row < nrows;
         const int rr = ok[v] ? row : 0;
         if constexpr (MODE == LM_KMAJOR) {
-          base[v] = (int64_t)rr * ld;
+          base[v] = rr * (int)ld;
         } else if constexpr (MODE == LM_CONV_FWD) {
           const ConvGeom& g = p.g;
           const int n = g.dHoWo.div(rr);
           const int rem = rr - n * g.Ho * g.Wo;
           const int oh = g.dWo.div(rem);
           const int ow = rem - oh * g.Wo;
-          base[v] = (int64_t)n * g.H * g.W * g.C;
+          base[v] = n * g.H * g.W * g.C;
           i0[v] = oh * g.sh - g.ph;
           j0[v] = ow * g.sw - g.pw;
         } else {  // LM_DGRAD_A: row = (n, hh, ww) of the phase grid
@@ -166,7 +176,7 @@ struct Loader {
           const int rem = rr - n * P.Hp * P.Wp;
           const int hh = P.dWp.div(rem);
           const int ww = rem - hh * P.Wp;
-          base[v] = (int64_t)n * g.Ho * g.Wo * g.K;
+          base[v] = n * g.Ho * g.Wo * g.K;
           i0[v] = hh + P.offh;
           j0[v] = ww + P.offw;
         }
@@ -189,14 +199,13 @@ struct Loader {
                                         int kend, const Phase& P, char* lds) {
     const int t = threadIdx.x;
     const int w = t >> 6;
-    const void* zero = (const void*)sg_zero_page;
     if constexpr (MODE == LM_KMAJOR) {
       const int kk = k0 + lchunk * 8;
       const bool kin = kk < kend;
 #pragma unroll
       for (int v = 0; v < VPT; ++v) {
         const bool o = ok[v] && kin;
-        glds16(o ? (const void*)(src + base[v] + kk) : zero, lds + (8 * w + 32 * v) * 128);
+        bld16(rsrc, o ? (unsigned)(base[v] + kk) * 2u : OOB, lds + (8 * w + 32 * v) * 128);
       }
     } else if constexpr (MODE == LM_CONV_FWD || MODE == LM_DGRAD_A) {
       const ConvGeom& g = p.g;
@@ -225,13 +234,13 @@ struct Loader {
           for (int v = 0; v < VPT; ++v) {
             const int ih = i0[v] + dr, iw = j0[v] + ds;
             const bool o = ok[v] && (unsigned)ih < (unsigned)HH && (unsigned)iw < (unsigned)WW;
-            rp[v] = o ? src + base[v] + ((int64_t)ih * WW + iw) * CH : nullptr;
+            ro[v] = o ? base[v] + (ih * WW + iw) * CH : -1;
           }
         }
 #pragma unroll
         for (int v = 0; v < VPT; ++v) {
-          const bool o = rp[v] != nullptr && kin;
-          glds16(o ? (const void*)(rp[v] + c0) : zero, lds + (8 * w + 32 * v) * 128);
+          const bool o = ro[v] >= 0 && kin;
+          bld16(rsrc, o ? (unsigned)(ro[v] + c0) * 2u : OOB, lds + (8 * w + 32 * v) * 128);
         }
       } else {  // per-lane tap (channel counts not a multiple of 64, e.g. the padded stem)
         const int tap = dch.div(kk);
@@ -251,8 +260,8 @@ struct Loader {
         for (int v = 0; v < VPT; ++v) {
           const int ih = i0[v] + dr, iw = j0[v] + ds;
           const bool o = ok[v] && kin && (unsigned)ih < (unsigned)HH && (unsigned)iw < (unsigned)WW;
-          const int64_t off = base[v] + ((int64_t)ih * WW + iw) * CH + c0;
-          glds16(o ? (const void*)(src + off) : zero, lds + (8 * w + 32 * v) * 128);
+          const int off = base[v] + (ih * WW + iw) * CH + c0;
+          bld16(rsrc, o ? (unsigned)off * 2u : OOB, lds + (8 * w + 32 * v) * 128);
         }
       }
     } else if constexpr (MODE == LM_KOUTER) {
@@ -263,7 +272,7 @@ struct Loader {
       for (int v = 0; v < VPT; ++v) {
         const int kr = k0 + kr0 + KRP * v;
         const bool o = cin && kr < kend;
-        glds16(o ? (const void*)(src + (int64_t)kr * ld + col) : zero, lds + (w * (64 / CPR) + KRP * v) * (ROWS * 2));
+        bld16(rsrc, o ? (unsigned)(kr * (int)ld + col) * 2u : OOB, lds + (w * (64 / CPR) + KRP * v) * (ROWS * 2));
       }
     } else if constexpr (MODE == LM_DGRAD_B) {
       // B(n = c, kk = (tap, k)) = W[k][r][s][c]; rows c contiguous per (k, tap)
@@ -284,8 +293,8 @@ struct Loader {
         const int j = P.dns.div(tap), i = tap - j * P.ns;
         const int r = P.r0 + g.sh * j, s = P.s0 + g.sw * i;
         const bool o = cin && kin;
-        const int64_t off = (int64_t)k * RSC + (r * g.S + s) * g.C + col;
-        glds16(o ? (const void*)(src + off) : zero, lds + (w * (64 / CPR) + KRP * v) * (ROWS * 2));
+        const int off = k * RSC + (r * g.S + s) * g.C + col;
+        bld16(rsrc, o ? (unsigned)off * 2u : OOB, lds + (w * (64 / CPR) + KRP * v) * (ROWS * 2));
       }
     } else if constexpr (MODE == LM_WGRAD_B) {
       const ConvGeom& g = p.g;
@@ -296,8 +305,7 @@ struct Loader {
         for (int v = 0; v < VPT; ++v) {
           const int pix = k0 + kr0 + KRP * v;
           const bool o = cok && pix < kend;
-          glds16(o ? (const void*)(src + (int64_t)pix * g.C + cc) : zero,
-                 lds + (w * (64 / CPR) + KRP * v) * (ROWS * 2));
+          bld16(rsrc, o ? (unsigned)(pix * g.C + cc) * 2u : OOB, lds + (w * (64 / CPR) + KRP * v) * (ROWS * 2));
         }
       } else {
         // decompose the first pixel once; later vectors step by KRP with
@@ -328,15 +336,18 @@ struct Loader {
           const int ih = oh * g.sh - g.ph + cr * g.dh;
           const int iw = ow * g.sw - g.pw + cs * g.dw;
           const bool o = cok && pix < kend && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
-          const int64_t off = (((int64_t)n * g.H + ih) * g.W + iw) * g.C + cc;
-          glds16(o ? (const void*)(src + off) : zero, lds + (w * (64 / CPR) + KRP * v) * (ROWS * 2));
+          const int off = ((n * g.H + ih) * g.W + iw) * g.C + cc;
+          bld16(rsrc, o ? (unsigned)off * 2u : OOB, lds + (w * (64 / CPR) + KRP * v) * (ROWS * 2));
         }
       }
     }
   }
 
-  // 16x32 fragment (rows r0..r0+15, k = kk*32..+31) for MFMA lane l
-  __device__ __forceinline__ bf16x8 frag(const char* lds, int r0, int kk) const {
+  // 16x32 fragment (rows r0..r0+15, k = kk*32..+31) for MFMA lane l: the
+  // per-lane byte offsets inside a stage image are loop-invariant, so the
+  // kernel computes them once (frag_offsets) and the K loop only adds the
+  // stage base (frag_at) -- the swizzle math used to cost ~10 VALU per MFMA.
+  __device__ __forceinline__ void frag_offsets(int r0, int kk, int& o0, int& o1) const {
     const int l = threadIdx.x & 63;
     if constexpr (KOUT) {
       const int g = l >> 4, i = l & 15;
@@ -344,19 +355,27 @@ struct Loader {
       const int col = r0 + 4 * pp;
       const int ch = col >> 3, within = (col & 7) * 2;
       const int kb0 = kk * 32 + 8 * g + q, kb1 = kb0 + 4;
+      o0 = kb0 * (ROWS * 2) + kouter_swz<ROWS>(kb0, ch) * 16 + within;
+      o1 = kb1 * (ROWS * 2) + kouter_swz<ROWS>(kb1, ch) * 16 + within;
+    } else {
+      const int row = r0 + (l & 15);
+      const int ch = kk * 4 + (l >> 4);
+      o0 = row * 128 + kmajor_swz(row, ch) * 16;
+      o1 = 0;
+    }
+  }
+
+  __device__ __forceinline__ bf16x8 frag_at(const char* lds, int o0, int o1) const {
+    if constexpr (KOUT) {
       typedef short v4s __attribute__((ext_vector_type(4)));
-      const char* a0 = lds + kb0 * (ROWS * 2) + kouter_swz<ROWS>(kb0, ch) * 16 + within;
-      const char* a1 = lds + kb1 * (ROWS * 2) + kouter_swz<ROWS>(kb1, ch) * 16 + within;
-      v4s x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(a0));
-      v4s x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(a1));
+      v4s x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(lds + o0));
+      v4s x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(lds + o1));
       i16x8 r;
       r[0] = x0[0]; r[1] = x0[1]; r[2] = x0[2]; r[3] = x0[3];
       r[4] = x1[0]; r[5] = x1[1]; r[6] = x1[2]; r[7] = x1[3];
       return __builtin_bit_cast(bf16x8, r);
     } else {
-      const int row = r0 + (l & 15);
-      const int ch = kk * 4 + (l >> 4);
-      return *(const bf16x8*)(lds + row * 128 + kmajor_swz(row, ch) * 16);
+      return *(const bf16x8*)(lds + o0);
     }
   }
 };
@@ -401,8 +420,8 @@ __global__ void __launch_bounds__(NT, 2) igemm_k(const GemmArgs p) {
 
   Loader<BM, AM> la;
   Loader<BN, BMODE> lb;
-  la.init(p, m0, M, P, p.lda);
-  lb.init(p, n0, p.N, P, p.ldb);
+  la.init(p, m0, M, P, p.lda, pa, p.a_bytes);
+  lb.init(p, n0, p.N, P, p.ldb, pb, p.b_bytes);
 
   const int wid = threadIdx.x >> 6;
   const int wm = wid >> 1, wn = wid & 1;
@@ -411,6 +430,16 @@ __global__ void __launch_bounds__(NT, 2) igemm_k(const GemmArgs p) {
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // loop-invariant fragment offsets (per lane) for every (tile, k-half)
+  int oa0[TM][BK / 32], oa1[TM][BK / 32], ob0[TN][BK / 32], ob1[TN][BK / 32];
+#pragma unroll
+  for (int kk = 0; kk < BK / 32; ++kk) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) la.frag_offsets(wm * (BM / 2) + i * 16, kk, oa0[i][kk], oa1[i][kk]);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) lb.frag_offsets(wn * (BN / 2) + j * 16, kk, ob0[j][kk], ob1[j][kk]);
+  }
 
   if (nk > 0) {
     la.issue(p, pa, m0, M, kbeg, kend, P, smem);
@@ -431,9 +460,9 @@ __global__ void __launch_bounds__(NT, 2) igemm_k(const GemmArgs p) {
       for (int kk = 0; kk < BK / 32; ++kk) {
         bf16x8 fa[TM], fb[TN];
 #pragma unroll
-        for (int i = 0; i < TM; ++i) fa[i] = la.frag(sa, wm * (BM / 2) + i * 16, kk);
+        for (int i = 0; i < TM; ++i) fa[i] = la.frag_at(sa, oa0[i][kk], oa1[i][kk]);
 #pragma unroll
-        for (int j = 0; j < TN; ++j) fb[j] = lb.frag(sb, wn * (BN / 2) + j * 16, kk);
+        for (int j = 0; j < TN; ++j) fb[j] = lb.frag_at(sb, ob0[j][kk], ob1[j][kk]);
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -773,6 +802,12 @@ static inline int kps(int K, int splits) {
   return ((nkt + splits - 1) / splits) * BK;
 }
 
+static unsigned extent_bytes(int64_t elems) {
+  if (elems * 2 >= (int64_t)1 << 31)
+    throw std::runtime_error("igemm: operand exceeds 2 GiB (32-bit buffer offsets); split the batch");
+  return (unsigned)(elems * 2);
+}
+
 extern "C" {
 
 int sg_bn_deterministic();  // batchnorm.hip: deterministic-reduction mode
@@ -791,6 +826,8 @@ void sg_gemm(const void* a, int64_t lda, int a_kouter, const void* b, int64_t ld
   p.c = c; p.ldc = ldc; p.alpha = alpha; p.beta = beta; p.bias = (const float*)bias; p.relu = relu;
   splits = (out_mode == OUT_F32_ATOMIC) ? pick_splits(M, N, K, splits) : 1;
   p.k_per_split = kps(K, splits);
+  p.a_bytes = extent_bytes(a_kouter ? (int64_t)(K - 1) * lda + M : (int64_t)(M - 1) * lda + K);
+  p.b_bytes = extent_bytes(b_kouter ? (int64_t)(K - 1) * ldb + N : (int64_t)(N - 1) * ldb + K);
 #define GO(AM, BMD)                                                                  \
   {                                                                                  \
     if (out_mode == OUT_BF16) launch<AM, BMD, OUT_BF16>(p, M, splits, s, batch, 0);  \
@@ -817,6 +854,8 @@ void sg_conv_fwd(const void* x, const void* w, void* y, const void* bias, int N,
   p.a = (const bf16*)x; p.lda = 0; p.b = (const bf16*)w; p.ldb = R * S * C;
   p.c = y; p.ldc = K; p.alpha = 1.f; p.beta = 0.f; p.bias = (const float*)bias; p.relu = relu;
   p.k_per_split = kps(p.K, 1);
+  p.a_bytes = extent_bytes((int64_t)N * H * W * C);
+  p.b_bytes = extent_bytes((int64_t)K * R * S * C);
   if (out_mode == OUT_F32) launch<LM_CONV_FWD, LM_KMAJOR, OUT_F32>(p, p.M, 1, s, 1, 0);
   else launch<LM_CONV_FWD, LM_KMAJOR, OUT_BF16>(p, p.M, 1, s, 1, 0);
 }
@@ -835,6 +874,9 @@ void sg_conv_dgrad(const void* dy, const void* w, void* dx, int N, int H, int W,
   p.c = dx; p.ldc = C; p.alpha = 1.f; p.beta = 0.f; p.bias = nullptr; p.relu = 0;
   p.out_phase = 1;
   p.k_per_split = kps(p.K, 1);
+  p.a_bytes = extent_bytes((int64_t)N * Ho * Wo * K);
+  p.b_bytes = extent_bytes((int64_t)K * R * S * C);
+  extent_bytes((int64_t)N * H * W * C);
   if (out_mode == OUT_F32) launch<LM_DGRAD_A, LM_DGRAD_B, OUT_F32>(p, Mmax, 1, s, 1, np);
   else launch<LM_DGRAD_A, LM_DGRAD_B, OUT_BF16>(p, Mmax, 1, s, 1, np);
 }
@@ -848,6 +890,8 @@ void sg_conv_wgrad(const void* x, const void* dy, void* dw_out, int N, int H, in
   p.M = K; p.N = R * S * C; p.K = N * Ho * Wo;
   p.a = (const bf16*)dy; p.lda = K; p.b = (const bf16*)x; p.ldb = 0;
   p.c = dw_out; p.ldc = R * S * C; p.alpha = 1.f; p.beta = 0.f; p.bias = nullptr; p.relu = 0;
+  p.a_bytes = extent_bytes((int64_t)N * Ho * Wo * K);
+  p.b_bytes = extent_bytes((int64_t)N * H * W * C);
   int BM, BN, sp;
   pick_wgrad(p.M, p.N, p.K, g_tune[0], BM, BN, sp);
   if (splits > 0) sp = splits;
