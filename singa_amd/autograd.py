@@ -76,6 +76,7 @@ class Operator:
             self.src_idx = [x.creator._yid.get(id(x), 0) if x.creator is not None else 0 for x in xs]
             self.params = [x if x.stores_grad else None for x in xs]
             self.input_requires = [x.requires_grad for x in xs]
+            self.src_dt = [x.dtype for x in xs]
         ys = _as_tuple(self.forward(*[x.data for x in xs]))
         dev = xs[0].device
         outs = tuple(
@@ -252,6 +253,8 @@ def backward(y, dy=None) -> Iterator[Tuple[Tensor, Tensor]]:
                 continue
             if dx is ACCUMULATED:
                 dx = None
+            elif dx is not None and dx.dtype != op.src_dt[i] and dx.is_floating_point():
+                dx = dx.to(op.src_dt[i])  # mixed-precision edge: grads take the producer's dtype
             if src_op not in pending:
                 pending[src_op] = [None] * src_op.n_out
             j = op.src_idx[i]

@@ -814,10 +814,17 @@ def _i_onehot(rep, n, x, a):
 class SingaRep:
     """An imported ONNX graph bound to a device (SINGA ``SingaRep``)."""
 
-    def __init__(self, mp, device=None, trainable: bool = True):
+    # ops whose float operands run at ``compute_dtype`` (MFMA GEMM / conv);
+    # everything else (softmax, norms, elementwise) sees what they produce
+    _LOWP = {"MatMul": (0, 1), "Gemm": (0, 1), "Conv": (0, 1), "ConvTranspose": (0, 1)}
+
+    def __init__(self, mp, device=None, trainable: bool = True, compute_dtype=None):
         from .. import device as _dev
 
         self.model_proto = mp
+        # autocast-style mixed precision for imported graphs (fp32 master
+        # weights; GEMM-shaped ops cast their operands, grads flow back in fp32)
+        self.compute_dtype = compute_dtype
         self.device = device or _dev.get_default_device()
         g = mp.graph
         self.graph = g
@@ -871,6 +878,10 @@ class SingaRep:
         for nd in self.graph.node:
             attrs = {a.name: attr_value(a) for a in nd.attribute}
             xs = [env.get(i) if i else None for i in nd.input]
+            if self.compute_dtype is not None and nd.op_type in self._LOWP:
+                for k in self._LOWP[nd.op_type]:
+                    if k < len(xs) and xs[k] is not None and xs[k].dtype == torch.float32:
+                        xs[k] = autograd.cast(xs[k], self.compute_dtype)
             ys = _IMPORTERS[nd.op_type](self, nd, xs, attrs)
             for name, y in zip(nd.output, ys):
                 if name:
@@ -902,9 +913,9 @@ class SONNXModel(model.Model):
     ``forward(*inputs)`` runs the graph; initializers in weight positions are
     parameters the optimiser updates (fine-tuning)."""
 
-    def __init__(self, onnx_model, device=None, loss=None):
+    def __init__(self, onnx_model, device=None, loss=None, compute_dtype=None):
         super().__init__()
-        self.rep = prepare(onnx_model, device)
+        self.rep = prepare(onnx_model, device, compute_dtype=compute_dtype)
         self._onnx_params = self.rep.params()
         for k, v in self._onnx_params.items():
             v.param_meta = {"lr_mult": 1.0, "wd_mult": 1.0}

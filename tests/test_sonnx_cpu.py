@@ -176,3 +176,25 @@ def test_tensorproto_roundtrip_dtypes():
     t.data_type = P.FLOAT
     t.float_data.extend([1.5, -2.0])
     np.testing.assert_array_equal(sonnx.tensorproto_to_numpy(t), [1.5, -2.0])
+
+
+def test_sonnx_mixed_precision_import():
+    """compute_dtype=bf16: GEMM operands cast (fp32 master weights), outputs
+    stay close to the fp32 import, and fine-tuning still converges."""
+    from singa_amd.models import bert
+
+    ids = tensor.from_numpy(np.random.RandomState(0).randint(0, 1000, (4, 16)).astype(np.int64))
+    y = tensor.from_numpy(np.array([0, 1, 1, 0], np.int32))
+    device.get_default_device().SetRandSeed(0)
+    m = bert.bert_tiny(dropout=0.0)
+    m.compile([ids], is_train=False)
+    blob = sonnx.to_onnx(m, [ids]).SerializeToString()
+    ref = sonnx.prepare(P.load_model(blob)).run([ids])[0].data.float().numpy()
+    sm = sonnx.SONNXModel(P.load_model(blob), compute_dtype=torch.bfloat16)
+    out = sm.rep.run([ids])[0].data.float().numpy()
+    np.testing.assert_allclose(out, ref, atol=5e-2, rtol=5e-2)
+    assert all(p.dtype == torch.float32 for p in sm.get_params().values())
+    sm.set_optimizer(opt.SGD(0.01))
+    sm.compile([ids], is_train=True)
+    ls = [float(sm(ids, y)[1].data.float()) for _ in range(8)]
+    assert ls[-1] < ls[0], ls

@@ -1,0 +1,163 @@
+"""Benchmarks for the secondary BASELINE.json configs (bench.py covers the
+ResNet-50 headline):
+
+* ``mlp_cpu``     -- MLP 784-512-10 on the CppCPU device, SGD, synthetic MNIST (samples/s);
+* ``mlp_gpu``     -- the reference's deep-big-simple MLP 784-2500-2000-1500-1000-500-10 on one MI355X;
+* ``alexnet``     -- AlexNet (224x224, LRN, dropout) bf16 training, large batch (images/s);
+* ``bert``        -- native BERT-base bf16 fine-tuning step, seq 128 (sequences/s);
+* ``bert_sonnx``  -- BERT-base exported to ONNX, re-imported with sonnx and
+                     fine-tuned through autograd (MatMul/Softmax/LayerNorm) (sequences/s).
+
+Every step is a full training step (forward, backward, optimizer update);
+inputs are synthetic and weights random-init.  One JSON line per benchmark
+on stdout (``--out`` appends them to a file too).
+
+    python tools/bench_suite.py --which mlp_cpu,alexnet,bert,bert_sonnx
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def _time(step, steps, warmup, sync):
+    for _ in range(warmup):
+        step()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        out = step()
+    sync()
+    return (time.perf_counter() - t0) / steps, out
+
+
+def _rec(name, unit, per_step_items, dt, **cfg):
+    return {"bench": name, "value": round(per_step_items / dt, 2), "unit": unit, "ms_per_step": round(dt * 1e3, 3),
+            "dtype": cfg.pop("dtype", "bf16"), "data": "synthetic, random-init weights", "config": cfg}
+
+
+def bench_mlp(a, gpu):
+    from singa_amd import device, opt, tensor
+    from singa_amd.models import mlp
+
+    dev = device.create_rocm_gpu() if gpu else device.get_default_device()
+    dev.SetRandSeed(0)
+    B = a.batch or (1024 if gpu else 64)
+    m = mlp.deep_big_simple() if gpu else mlp.create_model((512,), 10)
+    rng = np.random.RandomState(0)
+    x = tensor.from_numpy(rng.rand(B, 784).astype(np.float32)).to_device(dev)
+    y = tensor.from_numpy(rng.randint(0, 10, B).astype(np.int32)).to_device(dev)
+    m.set_optimizer(opt.SGD(0.01, 0.9))
+    m.compile([x], is_train=True, use_graph=gpu)
+    m.train()
+    sync = torch.cuda.synchronize if gpu else (lambda: None)
+    dt, (_, loss) = _time(lambda: m(x, y), a.steps, a.warmup, sync)
+    name = "mlp_gpu" if gpu else "mlp_cpu"
+    model = "MLP 784-2500-2000-1500-1000-500-10 stanh" if gpu else "MLP 784-512-10 relu"
+    return _rec(name, "samples/s", B, dt, model=model, batch=B, device="RocmGPU" if gpu else "CppCPU",
+                dtype="fp32", optimizer="SGD momentum 0.9", final_loss=round(float(loss.data.float()), 4))
+
+
+def bench_alexnet(a):
+    from singa_amd import device, opt, tensor
+    from singa_amd.models import alexnet
+
+    dev = device.create_rocm_gpu()
+    dev.SetRandSeed(0)
+    B = a.batch or 512
+    m = alexnet.create_model(num_classes=1000, compute_dtype=torch.bfloat16)
+    rng = np.random.RandomState(0)
+    x = tensor.from_numpy(rng.standard_normal((B, 3, 224, 224)).astype(np.float32)).to_device(dev)
+    y = tensor.from_numpy(rng.randint(0, 1000, B).astype(np.int32)).to_device(dev)
+    m.set_optimizer(opt.SGD(0.01, 0.9, weight_decay=5e-4))
+    m.compile([x], is_train=True, use_graph=not a.no_graph)
+    m.train()
+    dt, (_, loss) = _time(lambda: m(x, y), a.steps, a.warmup, torch.cuda.synchronize)
+    return _rec("alexnet", "images/s", B, dt, model="AlexNet-224 (LRN, dropout 0.5)", batch=B,
+                optimizer="SGD momentum 0.9 wd 5e-4", final_loss=round(float(loss.data.float()), 4))
+
+
+def _bert_inputs(dev, B, S, vocab):
+    from singa_amd import tensor
+
+    rng = np.random.RandomState(0)
+    ids = tensor.from_numpy(rng.randint(0, vocab, (B, S)).astype(np.int64)).to_device(dev)
+    y = tensor.from_numpy(rng.randint(0, 2, B).astype(np.int32)).to_device(dev)
+    return ids, y
+
+
+def bench_bert(a):
+    from singa_amd import device, opt
+    from singa_amd.models import bert
+
+    dev = device.create_rocm_gpu()
+    dev.SetRandSeed(0)
+    B, S = a.batch or 32, a.seq
+    m = bert.bert_base(dropout=0.1, compute_dtype=torch.bfloat16)
+    ids, y = _bert_inputs(dev, B, S, 30522)
+    m.set_optimizer(opt.Adam(1e-4))
+    m.compile([ids], is_train=True, use_graph=False)
+    m.train()
+    dt, (_, loss) = _time(lambda: m(ids, y), a.steps, a.warmup, torch.cuda.synchronize)
+    return _rec("bert", "sequences/s", B, dt, model="BERT-base (native)", batch=B, seq_len=S, optimizer="Adam",
+                final_loss=round(float(loss.data.float()), 4))
+
+
+def bench_bert_sonnx(a):
+    from singa_amd import device, opt, sonnx
+    from singa_amd.models import bert
+    from singa_amd.sonnx import onnx_proto as P
+
+    cpu = device.get_default_device()
+    cpu.SetRandSeed(0)
+    B, S = a.batch or 32, a.seq
+    src = bert.bert_base(dropout=0.0, compute_dtype=torch.float32)
+    ids_cpu, _ = _bert_inputs(cpu, 2, S, 30522)
+    src.compile([ids_cpu], is_train=False)
+    blob = sonnx.to_onnx(src, [ids_cpu]).SerializeToString()
+    del src
+    dev = device.create_rocm_gpu()
+    sm = sonnx.SONNXModel(P.load_model(blob), dev, compute_dtype=torch.bfloat16)
+    ids, y = _bert_inputs(dev, B, S, 30522)
+    sm.set_optimizer(opt.Adam(1e-4))
+    sm.compile([ids], is_train=True)
+    sm.train()
+    dt, (_, loss) = _time(lambda: sm(ids, y), a.steps, a.warmup, torch.cuda.synchronize)
+    return _rec("bert_sonnx", "sequences/s", B, dt, model="BERT-base exported -> ONNX -> sonnx import",
+                onnx_bytes=len(blob), batch=B, seq_len=S, optimizer="Adam",
+                final_loss=round(float(loss.data.float()), 4))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--which", default="mlp_cpu,mlp_gpu,alexnet,bert,bert_sonnx")
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=0)
+    ap.add_argument("--seq", type=int, default=128)
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+    fns = {"mlp_cpu": lambda: bench_mlp(a, False), "mlp_gpu": lambda: bench_mlp(a, True),
+           "alexnet": lambda: bench_alexnet(a), "bert": lambda: bench_bert(a), "bert_sonnx": lambda: bench_bert_sonnx(a)}
+    for w in a.which.split(","):
+        rec = fns[w]()
+        line = json.dumps(rec)
+        print(line, flush=True)
+        if a.out:
+            with open(a.out, "a") as f:
+                f.write(line + "\n")
+        if torch.cuda.is_available():
+            torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
