@@ -720,7 +720,8 @@ class Dropout(Operator):
             return x
         dev = self.seed_source
         seed, off = dev.next_rng(x.numel()) if dev is not None else (0, 0)
-        y, self.mask = F.dropout_fwd(x, self.ratio, seed, off)
+        ep = dev.rng_epoch() if dev is not None and x.is_cuda else None
+        y, self.mask = F.dropout_fwd(x, self.ratio, seed, off, ep)
         return y
 
     def backward(self, dy):

@@ -24,7 +24,7 @@ void sg_unary_bwd(int, const void*, const void*, const void*, void*, int64_t, in
 void sg_add_act(const void*, const void*, void*, int64_t, int, float, float, int, hipStream_t);
 void sg_relu_bwd_from_y(const void*, const void*, void*, int64_t, int, hipStream_t);
 void sg_cast(const void*, int, void*, int, int64_t, hipStream_t);
-void sg_dropout_fwd(const void*, void*, void*, int64_t, int, float, uint64_t, uint64_t, hipStream_t);
+void sg_dropout_fwd(const void*, void*, void*, int64_t, int, float, uint64_t, uint64_t, const void*, hipStream_t);
 void sg_dropout_bwd(const void*, const void*, void*, int64_t, int, float, hipStream_t);
 void sg_rand_fill(void*, int64_t, int, int, float, float, uint64_t, uint64_t, hipStream_t);
 void sg_nchw_to_nhwc_pad(const void*, void*, int, int, int, int, int, hipStream_t);
@@ -122,8 +122,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("cast", [](P x, int dtx, P y, int dty, int64_t n, P s) {
     sg_cast(CV(x), dtx, V(y), dty, n, S(s)); CHK("cast");
   });
-  m.def("dropout_fwd", [](P x, P y, P mask, int64_t n, int dt, float pk, uint64_t seed, uint64_t off, P s) {
-    sg_dropout_fwd(CV(x), V(y), V(mask), n, dt, pk, seed, off, S(s)); CHK("dropout_fwd");
+  m.def("dropout_fwd", [](P x, P y, P mask, int64_t n, int dt, float pk, uint64_t seed, uint64_t off, P epoch, P s) {
+    sg_dropout_fwd(CV(x), V(y), V(mask), n, dt, pk, seed, off, CV(epoch), S(s)); CHK("dropout_fwd");
   });
   m.def("dropout_bwd", [](P dy, P mask, P dx, int64_t n, int dt, float pk, P s) {
     sg_dropout_bwd(CV(dy), CV(mask), V(dx), n, dt, pk, S(s)); CHK("dropout_bwd");

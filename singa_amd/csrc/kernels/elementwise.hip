@@ -211,8 +211,13 @@ __global__ void cast_k(const TI* __restrict__ x, TO* __restrict__ y, int64_t n) 
 // dropout applied at test time, src/worker/layer.cc:142-152).
 template <typename T>
 __global__ void dropout_fwd_k(const T* __restrict__ x, T* __restrict__ y, uint8_t* __restrict__ mask,
-                              int64_t n, float pkeep, uint64_t seed, uint64_t offset) {
+                              int64_t n, float pkeep, uint64_t seed, uint64_t offset,
+                              const int64_t* __restrict__ epoch) {
   const float scale = 1.f / pkeep;
+  // graph replays: the host-side (seed, offset) are frozen in the captured
+  // launch, so the Philox key also mixes a device-resident step counter that
+  // the captured step advances -> a fresh mask on every replay
+  if (epoch) seed += (uint64_t)(*epoch) * 0x9E3779B97F4A7C15ull;
   const int64_t nq = (n + 3) / 4;
   SG_GRID_STRIDE(i, nq) {
     uint4 r = Philox::gen(seed, offset + i, 0);
@@ -323,9 +328,9 @@ void sg_cast(const void* x, int dtx, void* y, int dty, int64_t n, hipStream_t s)
   else hipLaunchKernelGGL((cast_k<bf16, bf16>), g, b, 0, s, (const bf16*)x, (bf16*)y, n);
 }
 void sg_dropout_fwd(const void* x, void* y, void* mask, int64_t n, int dtype, float pkeep, uint64_t seed,
-                    uint64_t offset, hipStream_t s) {
+                    uint64_t offset, const void* epoch, hipStream_t s) {
   DISPATCH_FT(dtype, hipLaunchKernelGGL(dropout_fwd_k<T>, dim3(sg_grid(n / 4 + 1)), dim3(256), 0, s, (const T*)x,
-                                        (T*)y, (uint8_t*)mask, n, pkeep, seed, offset));
+                                        (T*)y, (uint8_t*)mask, n, pkeep, seed, offset, (const int64_t*)epoch));
 }
 void sg_dropout_bwd(const void* dy, const void* mask, void* dx, int64_t n, int dtype, float pkeep, hipStream_t s) {
   DISPATCH_FT(dtype, hipLaunchKernelGGL(dropout_bwd_k<T>, dim3(sg_grid(n)), dim3(256), 0, s, (const T*)dy,

@@ -52,6 +52,21 @@ class Device:
         self.rng_offset += (int(n) + 3) // 4
         return self.seed, off
 
+    def rng_epoch(self) -> Optional[torch.Tensor]:
+        """Device-resident int64 step counter for graph-safe RNG (GPU only):
+        RNG kernels mix it into their Philox key; a captured training step
+        advances it (:meth:`advance_rng_epoch`), so every replay differs."""
+        if self.torch_device.type != "cuda":
+            return None
+        if getattr(self, "_rng_epoch", None) is None:
+            self._rng_epoch = torch.zeros(1, dtype=torch.int64, device=self.torch_device)
+        return self._rng_epoch
+
+    def advance_rng_epoch(self) -> None:
+        ep = self.rng_epoch()
+        if ep is not None:
+            ep.add_(1)
+
     def EnableGraph(self, enable: bool) -> None:
         self.graph_enabled = bool(enable)
 

@@ -55,6 +55,24 @@ class Layer:
                     v.name = f"{key}.{i}"
         super().__setattr__(key, value)
 
+    def _sublayers(self) -> "OrderedDict[str, Layer]":
+        """Direct sub-layers in attribute order, re-scanned on every call so a
+        list filled AFTER its assignment (``self.blocks = []`` then
+        ``append``) is still found."""
+        out = OrderedDict()
+        for key, v in self.__dict__.items():
+            if key.startswith("_"):
+                continue
+            if isinstance(v, Layer):
+                out[key] = v
+            elif isinstance(v, (list, tuple)) and v and all(isinstance(e, Layer) or e is None for e in v):
+                for i, e in enumerate(v):
+                    if e is not None:
+                        if e.name is None:
+                            e.name = f"{key}.{i}"
+                        out[f"{key}.{i}"] = e
+        return out
+
     def _param(self, key: str, t: Tensor, lr_mult: float = 1.0, wd_mult: float = 1.0) -> Tensor:
         t.stores_grad = True
         t.requires_grad = True
@@ -94,7 +112,7 @@ class Layer:
         out = OrderedDict()
         for k, v in self._params.items():
             out[prefix + k] = v
-        for ln, l in self._layers.items():
+        for ln, l in self._sublayers().items():
             out.update(l.get_params(prefix + ln + self.sep))
         return out
 
@@ -112,7 +130,7 @@ class Layer:
             out[prefix + k] = v
         for k, v in self._states.items():
             out[prefix + k] = v
-        for ln, l in self._layers.items():
+        for ln, l in self._sublayers().items():
             out.update(l.get_states(prefix + ln + self.sep))
         return out
 

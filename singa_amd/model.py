@@ -134,7 +134,12 @@ class Model(layer.Layer):
                 getattr(opt, "opt", opt).graph_mode = True
                 opt.prepare_step()
             sc0 = opt.step_counter if opt is not None else 0
+            dev = args[0].device
             with torch.cuda.graph(g, pool=self._pool):
+                # first captured kernel: advance the device RNG epoch, so
+                # dropout masks differ on every replay (host-side Philox
+                # offsets are frozen into the captured launches)
+                dev.advance_rng_epoch()
                 out = fn(*args, **kwargs)
             if opt is not None:
                 opt.step_counter = sc0  # capture does not execute; replay below does

@@ -95,11 +95,13 @@ class Embeddings(layer.Layer):
 
     def forward(self, ids, types=None):
         B, S = ids.shape
-        pos = Tensor(data=torch.arange(S, device=ids.data.device).unsqueeze(0).expand(B, S), device=ids.device,
+        # [1, S] position / type ids broadcast over the batch (an exported
+        # ONNX graph stays batch-size independent)
+        pos = Tensor(data=torch.arange(S, device=ids.data.device).unsqueeze(0), device=ids.device,
                      requires_grad=False)
         e = autograd.add(autograd.embedding(ids, self.word), autograd.embedding(pos, self.position))
         if types is None:
-            types = Tensor(data=torch.zeros((B, S), dtype=torch.int64, device=ids.data.device), device=ids.device,
+            types = Tensor(data=torch.zeros((1, S), dtype=torch.int64, device=ids.data.device), device=ids.device,
                            requires_grad=False)
         e = autograd.add(e, autograd.embedding(types, self.token_type))
         return self.drop(self.ln(e))

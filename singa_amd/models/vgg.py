@@ -13,10 +13,11 @@ CFGS = {11: [64, "M", 128, "M", 256, 256, "M", 512, 512, "M", 512, 512, "M"],
 
 class VGG(model.Model):
     def __init__(self, depth: int = 16, num_classes: int = 1000, batch_norm: bool = True, small: bool = False,
-                 compute_dtype=torch.bfloat16):
+                 compute_dtype=torch.bfloat16, num_channels: int = 3):
         super().__init__()
         self.compute_dtype = compute_dtype
         self.convs, self.bns, self.kinds = [], [], []
+        cin = num_channels  # explicit: the GPU input is channel-padded to 8, the weights are not
         for v in CFGS[depth]:
             if v == "M":
                 self.kinds.append("M")
@@ -24,8 +25,9 @@ class VGG(model.Model):
                 self.bns.append(None)
             else:
                 self.kinds.append("C")
-                self.convs.append(layer.Conv2d(v, 3, padding=1, bias=not batch_norm,
+                self.convs.append(layer.Conv2d(cin, v, 3, padding=1, bias=not batch_norm,
                                                activation="NOTSET" if batch_norm else "RELU"))
+                cin = v
                 self.bns.append(layer.BatchNorm2d() if batch_norm else None)
         hid = 512 if small else 4096
         self.fc1, self.fc2 = layer.Linear(hid), layer.Linear(hid)

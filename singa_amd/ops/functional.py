@@ -189,14 +189,17 @@ def cast(x: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
     return x.to(dtype)
 
 
-def dropout_fwd(x: torch.Tensor, ratio: float, seed: int, offset: int) -> Tuple[torch.Tensor, torch.Tensor]:
+def dropout_fwd(x: torch.Tensor, ratio: float, seed: int, offset: int,
+                epoch: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """``epoch``: optional device int64 step counter mixed into the Philox key
+    (keeps masks fresh across HIP-graph replays)."""
     pkeep = 1.0 - ratio
     if _native_ok(x) and _flat_ok(x):
         x = _dense(x)
         y = _like(x)
         mask = _like(x, torch.uint8)
         N.lib().dropout_fwd(x.data_ptr(), y.data_ptr(), mask.data_ptr(), x.numel(), N.dt(x), pkeep, seed, offset,
-                            N.stream())
+                            N.ptr(epoch), N.stream())
         return y, mask
     g = torch.Generator(device=x.device).manual_seed(int(seed + offset) & 0x7FFFFFFFFFFFFFFF)
     mask = (torch.rand(x.shape, generator=g, device=x.device) < pkeep).to(torch.uint8)
@@ -763,9 +766,10 @@ def pool2d_bwd(x_shape, x_like: torch.Tensor, dy: torch.Tensor, arg, kernel, str
                          int(is_max), int(count_include_pad), N.dt(dy), N.stream())
         return dx
     g = dy.float()
-    if is_max:
-        dx = F.max_unpool2d(g, arg, (kh, kw), (sh, sw), (ph, pw), output_size=(H, W))
-        return dx.to(dy.dtype)
+    if is_max:  # scatter-ADD: overlapping windows (k > s) may pick the same input
+        dx = torch.zeros((Nn, C, H * W), dtype=torch.float32, device=dy.device)
+        dx.scatter_add_(2, arg.reshape(Nn, C, -1), g.reshape(Nn, C, -1))
+        return dx.view(Nn, C, H, W).to(dy.dtype)
     with torch.enable_grad():
         xx = torch.zeros(x_shape, dtype=torch.float32, device=dy.device, requires_grad=True)
         y = F.avg_pool2d(xx, (kh, kw), (sh, sw), (ph, pw), ceil_mode=ceil_mode, count_include_pad=count_include_pad)

@@ -263,18 +263,21 @@ class Optimizer:
         if not self.graph_mode:
             self.prepare_step()
 
-    def update(self, grad_scale: Optional[float] = None) -> None:
-        """One fused update of every parameter in the store."""
+    def update(self, grad_scale: Optional[float] = None, g: Optional[torch.Tensor] = None) -> None:
+        """One fused update of every parameter in the store (``g``: another
+        flat gradient buffer of the store's layout, e.g. an executor thread's)."""
         st = self.store
         gs = self.grad_scale if grad_scale is None else grad_scale
+        g = st.g if g is None else g
+        assert g.numel() == st.numel and g.dtype == torch.float32
         if st.gpu:
-            N.lib().opt_update(_KIND[self.kind], st.w.data_ptr(), st.g.data_ptr(), N.ptr(st.s1), N.ptr(st.s2),
+            N.lib().opt_update(_KIND[self.kind], st.w.data_ptr(), g.data_ptr(), N.ptr(st.s1), N.ptr(st.s2),
                                N.ptr(st.low), st.cstart.data_ptr(), st.clen.data_ptr(), st.cseg.data_ptr(),
                                st.seg_lr.data_ptr(), st.seg_wd.data_ptr(), self._hp_dev.data_ptr(), st.nchunks,
                                self.momentum, self.dampening, self.weight_decay, gs, self.beta1, self.beta2, self.eps,
                                self.rho, int(self.nesterov), int(self.adamw), N.stream())
             return
-        self._cpu_update(st.w, st.g, st.s1, st.s2, st.lr_vec * self.current_lr(), st.wd_vec * self.weight_decay,
+        self._cpu_update(st.w, g, st.s1, st.s2, st.lr_vec * self.current_lr(), st.wd_vec * self.weight_decay,
                          float(self.step_counter + 1), gs, st.mask)
         if st.low is not None:
             st.low.copy_(st.w)

@@ -497,6 +497,24 @@ class NeuralNet:
                     a.low = b.low
                 l.params = src[key]
 
+    def share_weights_private_grads(self, other: "NeuralNet", store, gbuf: torch.Tensor) -> None:
+        """Executor-thread replica (P3): share ``other``'s weight storage but
+        accumulate gradients into ``gbuf`` (same flat layout as ``store.g``),
+        so concurrent backward passes never write the same gradient memory."""
+        off = {id(p): (o, p) for p, o in zip(store.params, store.offsets)}
+        src = {l.name: l.params for l in other.layers}
+        for l in self.layers:
+            if l.name not in src or len(src[l.name]) != len(l.params):
+                continue
+            mine = []
+            for b in src[l.name]:
+                t = Tensor(device=b.device, data=b.data, requires_grad=True, stores_grad=True, name=b.name)
+                t.low, t.param_meta = b.low, b.param_meta
+                o, _ = off[id(b)]
+                t.grad_view = store._view(gbuf, o, b.data.shape)
+                mine.append(t)
+            l.params = mine
+
     def to_json(self) -> str:
         """Node-link JSON (colour by locationid), script/graph.py compatible."""
         from .. import _core

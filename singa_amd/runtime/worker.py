@@ -20,6 +20,7 @@ torch.distributed ranks (servers are replaced by collectives).
 from __future__ import annotations
 
 import os
+import threading
 import time
 from typing import Callable, Dict, Optional
 
@@ -73,6 +74,14 @@ class Performance:
     def to_string(self) -> str:
         a = self.avg()
         return f"{self.name}: loss : {a[0]:.6f}, precision : {a[1]:.6f}"
+
+
+class _Null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
 
 
 class Worker:
@@ -141,7 +150,36 @@ class Worker:
             else:
                 self.sync = ElasticSync(self.store, pc, up.moving_rate or 0.9, up.sync_frequency,
                                         up.warmup_steps, sharded=cl.sharded_centre())
+        self._setup_executors()
         self.perf = Performance("train")
+
+    def _setup_executors(self):
+        """P3 (reference param_manager.cc:15,163-202, worker.cc:33-39):
+        ``nthreads_per_procs`` executor threads, each with its own replica of
+        the train net and its own data stream, sharing the weights.  Each
+        thread drives its own HIP stream, so small nets overlap on the GPU.
+        ``hogwild`` (UpdaterProto, default true): every thread applies its own
+        update as soon as its backward is done; otherwise the k gradients are
+        summed and ONE update runs with grad_scale = 1/k."""
+        k = self.cluster.nthreads_per_procs()
+        self.replicas = [self.train_net]
+        self.rep_grads = [self.store.g]
+        self.hogwild = bool(self.model.updater.hogwild)
+        self.streams = None
+        if k <= 1:
+            return
+        if self.train_net.partitioned or self.train_net.placed or self.group_comm is not None:
+            raise ValueError("nthreads_per_procs > 1 is supported for unpartitioned nets only")
+        for i in range(1, k):
+            r = NeuralNet(self.model.neuralnet, 1, "kTrain", self.dev, self.data_override,
+                          seed=self.seed + self.cluster.groupid() + 7919 * i)
+            g = torch.zeros_like(self.store.g)
+            r.share_weights_private_grads(self.train_net, self.store, g)
+            self.replicas.append(r)
+            self.rep_grads.append(g)
+        gpu = self.dev.torch_device.type == "cuda"
+        self.streams = [torch.cuda.Stream(device=self.dev.torch_device) for _ in range(k)] if gpu else None
+        self._upd_lock = threading.Lock()
 
     # ------------------------------------------------------------- cadence
     @staticmethod
@@ -160,7 +198,58 @@ class Worker:
                                                                   self.model.validation_frequency)
 
     # ---------------------------------------------------------------- steps
+    def _thread_step(self, i: int, out: list) -> None:
+        net, g = self.replicas[i], self.rep_grads[i]
+        ctx = torch.cuda.stream(self.streams[i]) if self.streams else _Null()
+        try:
+            with ctx:
+                outs = net.forward(training=True)
+                roots, seeds = net.backward_roots(outs)
+                g.zero_()
+                if roots:
+                    for _ in autograd.backward(roots, seeds):
+                        pass
+                if self.hogwild:
+                    with self._upd_lock:
+                        self.updater.update(grad_scale=1.0, g=g)
+                out[i] = net.metrics()
+        except BaseException as e:  # surfaced in the caller
+            out[i] = e
+
+    def _train_threads(self, step: int) -> np.ndarray:
+        k = len(self.replicas)
+        if self.streams:
+            cur = torch.cuda.current_stream(self.dev.torch_device)
+            for s in self.streams:
+                s.wait_stream(cur)
+        res: list = [None] * k
+        with Timer(self.dev) as tb:
+            ths = [threading.Thread(target=self._thread_step, args=(i, res)) for i in range(1, k)]
+            for t in ths:
+                t.start()
+            self._thread_step(0, res)
+            for t in ths:
+                t.join()
+            for r in res:
+                if isinstance(r, BaseException):
+                    raise r
+            if self.streams:
+                for s in self.streams:
+                    cur.wait_stream(s)
+            if not self.hogwild:
+                for g in self.rep_grads[1:]:
+                    self.store.g.add_(g)
+                self.updater.update(grad_scale=1.0 / k)
+            self.updater.step()
+        self.timers["backward"] += tb.ms
+        autograd.training = False
+        return sum(res) / k
+
     def train_one_batch(self, step: int) -> np.ndarray:
+        if len(self.replicas) > 1:
+            m = self._train_threads(step)
+            self._maybe_sync(step)
+            return m
         net = self.train_net
         with Timer(self.dev) as tf:
             outs = net.forward(training=True)
@@ -180,6 +269,11 @@ class Worker:
             self.updater.step()
         self.timers["forward"] += tf.ms
         self.timers["backward"] += tb.ms
+        self._maybe_sync(step)
+        autograd.training = False
+        return net.metrics()
+
+    def _maybe_sync(self, step: int) -> None:
         if self.sync is not None and self.sync.sync_now(step + 1):
             with Timer(self.dev) as ts:
                 if isinstance(self.sync, RandomSync):
@@ -187,8 +281,6 @@ class Worker:
                 else:
                     self.sync.sync()
             self.timers["sync"] += ts.ms
-        autograd.training = False
-        return net.metrics()
 
     def test(self, net: NeuralNet, nsteps: int, name: str) -> np.ndarray:
         perf = Performance(name)

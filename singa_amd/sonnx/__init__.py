@@ -348,7 +348,10 @@ def _x_cast(c, op, xs, i, o):
 
 @exporter("Reshape")
 def _x_reshape(c, op, xs, i, o):
-    c.add("Reshape", [i[0], c.const(np.asarray(op.shape, np.int64))], [o[0]])
+    shape = list(op.shape)
+    if len(shape) > 1 and len(xs[0].shape) > 1 and shape[0] == xs[0].shape[0]:
+        shape[0] = 0  # keep the batch dim symbolic ("copy from input")
+    c.add("Reshape", [i[0], c.const(np.asarray(shape, np.int64))], [o[0]])
 
 
 @exporter("Flatten")
@@ -380,7 +383,7 @@ def _x_split_heads(c, op, xs, i, o):
     H = op.h
     D = E3 // (3 * H)
     r, t = c.fresh(), c.fresh()
-    c.add("Reshape", [i[0], c.const(np.asarray([B, S, 3, H, D], np.int64))], [r])
+    c.add("Reshape", [i[0], c.const(np.asarray([0, 0, 3, H, D], np.int64))], [r])
     c.add("Transpose", [r], [t], perm=[2, 0, 3, 1, 4])
     parts = [c.fresh() for _ in range(3)]
     c.add("Split", [t, c.const(np.asarray([1, 1, 1], np.int64))], parts, axis=0)
@@ -393,7 +396,7 @@ def _x_merge_heads(c, op, xs, i, o):
     B, H, S, D = xs[0].shape
     t = c.fresh()
     c.add("Transpose", [i[0]], [t], perm=[0, 2, 1, 3])
-    c.add("Reshape", [t, c.const(np.asarray([B, S, H * D], np.int64))], [o[0]])
+    c.add("Reshape", [t, c.const(np.asarray([0, 0, H * D], np.int64))], [o[0]])
 
 
 @exporter("TorchCLS")

@@ -142,3 +142,50 @@ def test_worker_trains_lenet_style():
     train_hist = [h for h in w.history if h[0] == "train"]
     assert train_hist[-1][2][0] < train_hist[0][2][0]
     assert any(l.startswith("test:") for l in logs)
+
+
+_MLP_NET = """
+    name: "mlp-threads" train_steps: 6 display_frequency: 0
+    updater { base_learning_rate: 0.05 type: kSGD momentum: 0.9 learning_rate_change_method: kFixed hogwild: %s }
+    neuralnet {
+      layer { name: "data" type: "kShardData" data_param { batchsize: 8 path: "/nonexistent" } }
+      layer { name: "mnist" type: "kMnistImage" srclayers: "data" mnist_param { norm_a: 255 norm_b: 0 } }
+      layer { name: "label" type: "kLabel" srclayers: "data" }
+      layer { name: "ip1" type: "kInnerProduct" srclayers: "mnist" inner_product_param { num_output: 16 }
+              param { init_method: kUniformSqrtFanIn low: -1 high: 1 } param { init_method: kConstant value: 0 } }
+      layer { name: "tanh1" type: "kTanh" srclayers: "ip1" }
+      layer { name: "ip2" type: "kInnerProduct" srclayers: "tanh1" inner_product_param { num_output: 10 }
+              param { init_method: kUniformSqrtFanIn low: -1 high: 1 } param { init_method: kConstant value: 0 } }
+      layer { name: "loss" type: "kSoftmaxLoss" srclayers: "ip2" srclayers: "label" }
+    }"""
+
+
+def _thread_worker(k, hogwild, fixed_seed=True, dev=None):
+    m = schema.parse_text("ModelProto", _MLP_NET % ("true" if hogwild else "false"))
+    cp = schema.new("ClusterProto")
+    cp.nworkers, cp.nthreads_per_procs, cp.workspace = 1, k, ""
+    ov = {"shape": (6, 6), "nclass": 10}
+    if fixed_seed:
+        ov["seed"] = 3
+    return Worker(m, cp, dev=dev, data_override={"*": ov}, log=lambda s: None)
+
+
+def test_executor_threads_aggregated_equals_single():
+    """P3, aggregated mode: k threads on identical data sum k identical
+    gradients and apply ONE update with grad_scale 1/k == the 1-thread run."""
+    w1 = _thread_worker(1, False)
+    w2 = _thread_worker(2, False)
+    assert len(w2.replicas) == 2 and w2.replicas[1].params()[0] is not w2.train_net.params()[0]
+    assert w2.replicas[1].params()[0].data.data_ptr() == w2.train_net.params()[0].data.data_ptr()
+    w1.run()
+    w2.run()
+    np.testing.assert_allclose(w1.store.w.numpy(), w2.store.w.numpy(), rtol=1e-6, atol=1e-7)
+
+
+def test_executor_threads_hogwild_trains():
+    w = _thread_worker(3, True, fixed_seed=False)
+    first = w.train_one_batch(0)
+    for s in range(1, 30):
+        last = w.train_one_batch(s)
+    assert np.isfinite(last).all()
+    assert w.updater.step_counter == 30

@@ -193,3 +193,21 @@ def test_native_core_graph_and_shard(tmp_path):
     assert n == 5
     r.seek_to_first()
     assert r.next()[0] == b"k0"
+
+
+@pytest.mark.parametrize("k,s,p", [(3, 2, 0), (3, 2, 1), (3, 1, 1), (2, 2, 0)])
+def test_cpu_maxpool_backward_overlapping_windows(k, s, p):
+    """Overlapping max-pool windows (AlexNet 3x3/2) route several outputs'
+    gradients to one input: they must accumulate, not overwrite."""
+    import torch.nn.functional as TF
+    from singa_amd.ops import functional as F
+
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(2, 4, 11, 13, generator=g)
+    xr = x.clone().requires_grad_(True)
+    yr = TF.max_pool2d(xr, k, s, p)
+    dy = torch.randn(yr.shape, generator=g)
+    yr.backward(dy)
+    y, arg = F.pool2d_fwd(x, (k, k), (s, s), (p, p), True)
+    dx = F.pool2d_bwd(x.shape, x, dy, arg, (k, k), (s, s), (p, p), True)
+    assert torch.allclose(y, yr.detach()) and torch.allclose(dx, xr.grad, atol=1e-6)

@@ -87,6 +87,11 @@ CONV_CASES = [
     (2, 3, 32, 32, 64, 7, 7, 2, 3),     # stem, C padded to 8
     (3, 20, 12, 12, 50, 5, 5, 1, 0),    # LeNet conv2: C and K not multiples of 8
     (2, 32, 9, 11, 40, 3, 3, 1, 2),
+    # AlexNet: 11x11/4 stem (C padded to 8), 5x5 pad 2, 3x3 at 13x13
+    (2, 3, 67, 67, 96, 11, 11, 4, 2),
+    (4, 3, 224, 224, 96, 11, 11, 4, 2),
+    (2, 96, 27, 27, 256, 5, 5, 1, 2),
+    (2, 256, 13, 13, 384, 3, 3, 1, 1),
     # ResNet-sized spatial extents: wgrad's stepping pixel decomposition
     # (output rows >= 16 / 32 pixels) and the 128-row tiles
     (2, 64, 56, 56, 64, 3, 3, 1, 1),

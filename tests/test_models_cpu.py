@@ -85,3 +85,17 @@ def test_attention_grad_fd():
             num = (fp - fm) / (2 * eps)
             assert abs(num - float(g[id(t)].view(-1)[i])) < 2e-2 * max(1.0, abs(num)), (num, g[id(t)].view(-1)[i])
     autograd.training = False
+
+
+def test_sublayers_in_lists_filled_after_assignment():
+    """``self.blocks = []`` followed by appends (VGG) must still expose every
+    parameter to get_params / the optimiser."""
+    from singa_amd.models import vgg
+
+    m = vgg.create_model(11, num_classes=10)
+    x = tensor.from_numpy(np.random.RandomState(0).randn(2, 3, 32, 32).astype(np.float32))
+    m.compile([x], is_train=False)
+    names = list(m.get_params())
+    assert sum(n.startswith("convs.") for n in names) == 8  # 8 conv weights (no bias with BN)
+    assert sum(n.startswith("bns.") for n in names) == 16  # gamma, beta
+    assert any(k.startswith("bns.") and "mean" in k for k in m.get_states())

@@ -211,3 +211,96 @@ def test_bottleneck_matches_torch_fp32(gpu, stride, down):
         errs[k] = rel_err(gk.reshape(P[k].grad.shape), P[k].grad)
     print(errs)
     assert max(errs.values()) < 3e-2, errs
+
+
+@pytest.mark.parametrize("small", [False, True])
+def test_alexnet_gpu_matches_cpu(gpu, small):
+    """AlexNet (LRN, 11x11/4 conv, 3x3/2 max-pool, 4096-wide FCs) on the
+    MI355X (bf16 MFMA) vs the CPU fp32 model from the same weights: first
+    loss, every parameter gradient (cosine / relative norm), and a short
+    loss trajectory (bf16 vs fp32 drifts slowly, so that check is loose)."""
+    from singa_amd.models import alexnet
+
+    B, hw = (16, 224) if not small else (32, 32)
+    rng = np.random.RandomState(0)
+    x_np = rng.standard_normal((B, 3, hw, hw)).astype(np.float32)
+    y_np = rng.randint(0, 1000 if not small else 10, B).astype(np.int32)
+    losses, grads, init = [], [], None
+    for dev in (device.get_default_device(), device.create_rocm_gpu()):
+        dev.SetRandSeed(1)
+        m = alexnet.create_model(num_classes=1000 if not small else 10, small=small, dropout=0.0,
+                                 compute_dtype=torch.bfloat16)
+        x = tensor.from_numpy(x_np).to_device(dev)
+        y = tensor.from_numpy(y_np).to_device(dev)
+        sgd = opt.SGD(0.002)
+        m.set_optimizer(sgd)
+        m.compile([x], is_train=True)
+        if init is None:
+            init = {k: v.data.clone() for k, v in m.get_states().items()}
+        else:
+            m.set_states(init)
+        ls = []
+        for i in range(5):
+            _, l = m(x, y)
+            ls.append(float(l.data.float().cpu()))
+            if i == 0:
+                grads.append({k: p.grad_view.detach().float().cpu().clone() for k, p in m.get_params().items()})
+        losses.append(ls)
+    c, g = np.array(losses[0]), np.array(losses[1])
+    assert abs(c[0] - g[0]) < 2e-3 * abs(c[0]), losses
+    # bf16 activations flip near-tied max-pool argmaxes (3x3/2 windows), so
+    # the early layers' gradients drift more than the FCs' (measured: conv
+    # cos >= 0.966, FC cos >= 0.998); a routing/accumulation bug gives cos ~0.5
+    for k, gc in grads[0].items():
+        gg = grads[1][k]
+        cos = float((gc * gg).sum() / (gc.norm() * gg.norm() + 1e-30))
+        rel = float((gc - gg).norm() / (gc.norm() + 1e-30))
+        assert cos > 0.95 and rel < 0.35, (k, cos, rel)
+    assert np.all(np.abs(c - g) < 0.1 * np.maximum(1.0, np.abs(c))), losses
+
+
+def test_dropout_masks_change_across_graph_replays(gpu):
+    """A HIP-graph replayed training step must draw a fresh dropout mask
+    every replay (the device RNG epoch advances inside the graph)."""
+    from singa_amd.models import mlp
+
+    dev = device.create_rocm_gpu()
+    dev.SetRandSeed(0)
+    m = mlp.MLP((256,), 10, dropout=0.5)
+    rng = np.random.RandomState(0)
+    x = tensor.from_numpy(rng.rand(64, 32).astype(np.float32)).to_device(dev)
+    y = tensor.from_numpy(rng.randint(0, 10, 64).astype(np.int32)).to_device(dev)
+    m.set_optimizer(opt.SGD(0.0))  # weights frozen: outputs differ only through the masks
+    m.compile([x], is_train=True, use_graph=True)
+    m.train()
+    outs = []
+    for _ in range(m.graph_warmup + 3):
+        o, _ = m(x, y)
+        outs.append(o.data.float().cpu().clone())
+    assert m._graphs, "graph was not captured"
+    a, b, c = outs[-3:]
+    assert not torch.equal(a, b) and not torch.equal(b, c)
+
+
+def test_alexnet_graph_matches_eager(gpu):
+    """HIP-graph replay of the AlexNet training step == eager execution
+    (dropout off; the graph must not freeze buffers or reorder updates)."""
+    from singa_amd.models import alexnet
+
+    rng = np.random.RandomState(0)
+    x_np = rng.standard_normal((32, 3, 224, 224)).astype(np.float32)
+    y_np = rng.randint(0, 1000, 32).astype(np.int32)
+    curves = []
+    for use_graph in (False, True):
+        dev = device.create_rocm_gpu()
+        dev.SetRandSeed(5)
+        m = alexnet.create_model(num_classes=1000, dropout=0.0, compute_dtype=torch.bfloat16)
+        x = tensor.from_numpy(x_np).to_device(dev)
+        y = tensor.from_numpy(y_np).to_device(dev)
+        m.set_optimizer(opt.SGD(0.002, 0.9))
+        m.compile([x], is_train=True, use_graph=use_graph)
+        m.train()
+        curves.append([float(m(x, y)[1].data.float().cpu()) for _ in range(8)])
+    e, g = np.array(curves[0]), np.array(curves[1])
+    assert np.all(np.isfinite(g)), curves
+    assert np.all(np.abs(e - g) < 2e-2 * np.abs(e)), curves

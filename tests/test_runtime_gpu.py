@@ -118,3 +118,20 @@ def test_partitioned_equals_unpartitioned_gpu(gpu, ptype, g):
         outs = nn.forward(training=True)
         losses.append(float(nn.total_loss(outs).data.float().cpu()))
     assert abs(losses[0] - losses[1]) < 1e-3 * max(1.0, abs(losses[0])), losses
+
+
+def test_executor_threads_on_gpu_streams():
+    """P3 on the GPU: 2 executor threads (one HIP stream each) on identical
+    data in aggregated mode == the single-thread run."""
+    from test_config_runtime import _thread_worker
+    from singa_amd import device
+
+    dev = device.create_rocm_gpu()
+    outs = []
+    for k in (1, 2):
+        dev.SetRandSeed(0)
+        w = _thread_worker(k, False, dev=dev)
+        assert (w.streams is not None) == (k > 1)
+        w.run()
+        outs.append(w.store.w.detach().cpu().numpy())
+    np.testing.assert_allclose(outs[0], outs[1], rtol=1e-4, atol=1e-5)

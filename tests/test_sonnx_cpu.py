@@ -198,3 +198,17 @@ def test_sonnx_mixed_precision_import():
     sm.compile([ids], is_train=True)
     ls = [float(sm(ids, y)[1].data.float()) for _ in range(8)]
     assert ls[-1] < ls[0], ls
+
+
+def test_exported_bert_is_batch_independent():
+    from singa_amd.models import bert
+
+    rng = np.random.RandomState(0)
+    ids2 = tensor.from_numpy(rng.randint(0, 1000, (2, 16)).astype(np.int64))
+    ids5 = tensor.from_numpy(rng.randint(0, 1000, (5, 16)).astype(np.int64))
+    m = bert.bert_tiny(dropout=0.0)
+    m.compile([ids2], is_train=False)
+    blob = sonnx.to_onnx(m, [ids2]).SerializeToString()
+    out = sonnx.prepare(P.load_model(blob)).run([ids5])[0].data.numpy()
+    autograd.training = False
+    np.testing.assert_allclose(out, m.forward(ids5).data.numpy(), atol=1e-4)
