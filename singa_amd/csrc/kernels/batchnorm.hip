@@ -372,7 +372,7 @@ extern "C" int sg_bn_deterministic() { return g_bn_det; }
 // rows the finalize sums for a reduction launched on `grid`
 static inline int fin_rows(const dim3& grid) { return g_bn_det ? (int)grid.x : NSLOT; }
 static inline void zero_ws(void* ws, int C, hipStream_t s) {
-  if (!g_bn_det) hipMemsetAsync(ws, 0, sizeof(float) * NSLOT * 2 * C, s);
+  if (!g_bn_det) sg_zero_async(ws, sizeof(float) * NSLOT * 2 * C, s);
 }
 
 static inline dim3 fin_grid(int C) { return dim3((C + 63) / 64); }

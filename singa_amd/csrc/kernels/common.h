@@ -160,3 +160,23 @@ static inline int sg_grid(int64_t n, int block = 256, int cap = 4096) {
   if (g < 1) g = 1;
   return (int)(g > cap ? cap : g);
 }
+
+// Zero a small device workspace with a kernel (16-byte stores).  Used instead
+// of hipMemsetAsync for the atomic-accumulation slots, so the zeroing is an
+// ordinary kernel node when the launch is captured into a hipGraph.
+// SG_ZERO_MEMSET=1 switches back to hipMemsetAsync (diagnostics).
+__global__ static void sg_zero_k(float4* __restrict__ p, int64_t n4) {
+  SG_GRID_STRIDE(i, n4) { p[i] = make_float4(0.f, 0.f, 0.f, 0.f); }
+}
+static inline void sg_zero_async(void* p, size_t bytes, hipStream_t s) {
+  static const int use_memset = [] {
+    const char* e = getenv("SG_ZERO_MEMSET");
+    return e && e[0] == '1';
+  }();
+  if (use_memset || (bytes & 15) || ((uintptr_t)p & 15)) {
+    hipMemsetAsync(p, 0, bytes, s);
+    return;
+  }
+  const int64_t n4 = (int64_t)(bytes / 16);
+  hipLaunchKernelGGL(sg_zero_k, dim3(sg_grid(n4, 256, 1024)), dim3(256), 0, s, (float4*)p, n4);
+}

@@ -848,7 +848,7 @@ void sg_conv_fwd(const void* x, const void* w, void* y, const void* bias, int N,
   GemmArgs p{};
   p.stats = (out_mode == OUT_BF16 && (K & 7) == 0 && g_tune[1]) ? (float*)stats : nullptr;
   p.stats_det = sg_bn_deterministic();
-  if (p.stats && !p.stats_det) hipMemsetAsync(p.stats, 0, sizeof(float) * 32 * 2 * K, s);  // atomic slot rows
+  if (p.stats && !p.stats_det) sg_zero_async(p.stats, sizeof(float) * 32 * 2 * K, s);  // atomic slot rows
   p.g = make_geom(N, H, W, C, K, R, S, Ho, Wo, sh, sw, ph, pw, dh, dw);
   p.M = N * Ho * Wo; p.N = K; p.K = R * S * C;
   p.a = (const bf16*)x; p.lda = 0; p.b = (const bf16*)w; p.ldb = R * S * C;

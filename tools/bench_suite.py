@@ -28,20 +28,31 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 
+CURVE = []
+
+
 def _time(step, steps, warmup, sync):
+    """Times ``steps`` calls after ``warmup``; every step's loss is kept as a
+    device tensor (no host sync inside the timed loop) and reported after."""
+    CURVE.clear()
     for _ in range(warmup):
-        step()
+        out = step()
+        CURVE.append(out[1].data.detach().float().reshape(()).clone())
     sync()
     t0 = time.perf_counter()
     for _ in range(steps):
         out = step()
+        CURVE.append(out[1].data.detach().float().reshape(()).clone())
     sync()
-    return (time.perf_counter() - t0) / steps, out
+    dt = (time.perf_counter() - t0) / steps
+    return dt, out
 
 
 def _rec(name, unit, per_step_items, dt, **cfg):
+    curve = [round(float(c), 4) for c in CURVE]
     return {"bench": name, "value": round(per_step_items / dt, 2), "unit": unit, "ms_per_step": round(dt * 1e3, 3),
-            "dtype": cfg.pop("dtype", "bf16"), "data": "synthetic, random-init weights", "config": cfg}
+            "dtype": cfg.pop("dtype", "bf16"), "data": "synthetic, random-init weights", "config": cfg,
+            "loss_curve": curve}
 
 
 def bench_mlp(a, gpu):
