@@ -13,7 +13,7 @@ CFGS = {11: [64, "M", 128, "M", 256, 256, "M", 512, 512, "M", 512, 512, "M"],
 
 class VGG(model.Model):
     def __init__(self, depth: int = 16, num_classes: int = 1000, batch_norm: bool = True, small: bool = False,
-                 compute_dtype=torch.bfloat16, num_channels: int = 3):
+                 compute_dtype=torch.bfloat16, num_channels: int = 3, dropout: float = 0.5):
         super().__init__()
         self.compute_dtype = compute_dtype
         self.convs, self.bns, self.kinds = [], [], []
@@ -32,7 +32,7 @@ class VGG(model.Model):
         hid = 512 if small else 4096
         self.fc1, self.fc2 = layer.Linear(hid), layer.Linear(hid)
         self.r1, self.r2 = layer.ReLU(), layer.ReLU()
-        self.d1, self.d2 = layer.Dropout(0.5), layer.Dropout(0.5)
+        self.d1, self.d2 = layer.Dropout(dropout), layer.Dropout(dropout)
         self.fc3 = layer.Linear(num_classes)
         self.loss_fn = layer.SoftMaxCrossEntropy()
 

@@ -304,3 +304,31 @@ def test_alexnet_graph_matches_eager(gpu):
     e, g = np.array(curves[0]), np.array(curves[1])
     assert np.all(np.isfinite(g)), curves
     assert np.all(np.abs(e - g) < 2e-2 * np.abs(e)), curves
+
+
+def test_graph_replay_after_device_sync_matches_eager(gpu):
+    """Regression: a replay issued right after torch.cuda.synchronize() must
+    see zeroed reduction workspaces (captured hipMemsetAsync nodes were not
+    reliably ordered; the zeroing is a kernel now).  MLP bias gradients go
+    through the atomic column-sum path."""
+    from singa_amd.models import mlp
+
+    curves = []
+    for use_graph in (False, True):
+        dev = device.create_rocm_gpu()
+        dev.SetRandSeed(0)
+        rng = np.random.RandomState(0)
+        m = mlp.MLP((500, 300), 10)
+        x = tensor.from_numpy(rng.rand(256, 784).astype(np.float32)).to_device(dev)
+        y = tensor.from_numpy(rng.randint(0, 10, 256).astype(np.int32)).to_device(dev)
+        m.set_optimizer(opt.SGD(0.01, 0.9))
+        m.compile([x], is_train=True, use_graph=use_graph)
+        m.train()
+        ls = []
+        for i in range(9):
+            if i == 5:
+                torch.cuda.synchronize()
+            ls.append(m(x, y)[1].data.detach().float().reshape(()).clone())
+        torch.cuda.synchronize()
+        curves.append([float(v) for v in ls])
+    np.testing.assert_allclose(curves[1], curves[0], rtol=1e-5)

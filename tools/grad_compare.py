@@ -16,7 +16,7 @@ def build(name, small):
         return alexnet.create_model(num_classes=10 if small else 1000, small=small, dropout=0.0,
                                     compute_dtype=torch.bfloat16), (32 if small else 224), (10 if small else 1000)
     if name == "vgg":
-        return vgg.create_model(11, num_classes=10, compute_dtype=torch.bfloat16), 32, 10
+        return vgg.create_model(11, num_classes=10, compute_dtype=torch.bfloat16, small=True, dropout=0.0), 32, 10
     if name == "resnet":
         return resnet.create_model(18, num_classes=10, compute_dtype=torch.bfloat16), 32, 10
     return cnn.create_model(), 28, 10
