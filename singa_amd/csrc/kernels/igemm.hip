@@ -89,6 +89,7 @@ struct GemmArgs {
   unsigned a_bytes, b_bytes;  // operand extents (buffer-resource ranges; per batch slice)
   float* stats;        // optional BN statistics of the bf16 output: ws[row][2][N] (sum, sum of squares)
   int stats_det;       // 1: row = tile row, plain stores (deterministic); 0: row = tile row % 32, atomics
+  int xcd_split;       // split-K: K-slice-major XCD mapping (gridDim.z % 8 == 0, gridDim.y == 1)
   ConvGeom g;
 };
 
@@ -400,8 +401,20 @@ __global__ void __launch_bounds__(NT, 2) igemm_k(const GemmArgs p) {
   const int tiles_m = (M + BM - 1) / BM, tiles_n = (p.N + BN - 1) / BN;
   const int nwg = tiles_m * tiles_n;
   int bid = blockIdx.x;
+  int split = blockIdx.z;
   if (bid >= nwg) return;
-  if (nwg >= 8) {
+  if (OUT == OUT_F32_ATOMIC && p.xcd_split) {
+    // split-K with splits % 8 == 0 (host-checked), gridDim.y == 1: workgroups
+    // are dispatched round-robin over the 8 XCDs in linear-id order, so give
+    // each XCD whole K-slices with ALL their tiles, tile index fastest: the
+    // workgroups resident on one XCD then stream the same K window (pixels)
+    // of both operands and share it through that XCD's L2, instead of every
+    // XCD holding several K windows of a tile subset.
+    const int L = blockIdx.x + (int)gridDim.x * (int)blockIdx.z;
+    const int xcd = L & 7, loc = L >> 3;
+    split = xcd * ((int)gridDim.z >> 3) + loc / nwg;
+    bid = loc % nwg;
+  } else if (nwg >= 8) {
     const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
     bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
   }
@@ -413,7 +426,7 @@ __global__ void __launch_bounds__(NT, 2) igemm_k(const GemmArgs p) {
   const int tn = (bid % (band * tiles_n)) / gm;
   const int m0 = tm * BM, n0 = tn * BN;
 
-  const int kbeg = p.out_phase ? 0 : (int)blockIdx.z * p.k_per_split;
+  const int kbeg = p.out_phase ? 0 : split * p.k_per_split;
   const int kend = p.out_phase ? K : min(K, kbeg + p.k_per_split);
   if (OUT == OUT_F32_ATOMIC && kbeg >= kend) return;
   const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
@@ -735,12 +748,13 @@ static int make_phases(ConvGeom& g) {
   return np;
 }
 
-static int g_tune[8] = {4, 1, 0, 0, 0, 0, 0, 0};
+static int g_tune[8] = {5, 1, 1, 0, 0, 0, 0, 0};
 
 template <int BM, int BN, int AM, int BMODE, int OUT>
 static void launch_t(const GemmArgs& p_in, int tiles, int ydim, int zdim, hipStream_t s) {
   GemmArgs p = p_in;
   p.lds_epilogue = g_tune[1];
+  p.xcd_split = (OUT == OUT_F32_ATOMIC && g_tune[2] && ydim == 1 && zdim >= 8 && (zdim & 7) == 0) ? 1 : 0;
   dim3 grid(tiles, ydim, zdim), block(NT);
   constexpr int stages = 2 * (BM + BN) * BK * 2;
   constexpr int etile = (OUT == OUT_BF16 || OUT == OUT_F32_ATOMIC) ? BM * (BN + 4) * 4 : 0;  // fp32 epilogue tile
@@ -777,7 +791,8 @@ static void launch_tile(const GemmArgs& p, int M, int BM, int BN, int splits, hi
 }
 
 // Tuning knobs (sg_set_tuning): 0 = wgrad tile/split policy, 1 = LDS-staged
-// bf16 epilogue (g_tune is defined above launch_t)
+// bf16 epilogue, 2 = K-slice-major XCD mapping of split-K launches, 3 = wgrad
+// split-count scale (2^v) (g_tune is defined above launch_t)
 
 // wgrad: the reduction (output pixels) is huge and M x N small, so
 // parallelism comes from split-K; use the largest tile that fits (operand
@@ -924,7 +939,27 @@ void sg_conv_wgrad(const void* x, const void* dy, void* dw_out, int N, int H, in
   p.a_bytes = extent_bytes((int64_t)N * Ho * Wo * K);
   p.b_bytes = extent_bytes((int64_t)N * H * W * C);
   int BM, BN, sp;
-  pick_wgrad(p.M, p.N, p.K, g_tune[0], BM, BN, sp);
+  int mode = g_tune[0], extra = g_tune[3];
+  if (mode == 5) {
+    // measured per-shape policy (tools/tune_conv.py, ResNet-50 b256, after the
+    // LDS-staged atomic epilogue and the K-slice-major XCD mapping):
+    //  * filters with taps (3x3, 7x7): 2x / 4x more K-slices than the base
+    //    policy (narrow outputs need more) -- -10..-25 %;
+    //  * 1x1 with stride 2, or halving the channels (a stage's entry conv):
+    //    128x128 tiles, fewer slices (mode 1) -- -5..-30 %;
+    //  * other 1x1: base policy.
+    if (R * S > 1) {
+      mode = 4;
+      extra += K <= 128 ? 2 : 1;
+    } else {
+      mode = (sh > 1 || sw > 1 || C == 2 * K) ? 1 : 4;
+    }
+  }
+  pick_wgrad(p.M, p.N, p.K, mode, BM, BN, sp);
+  if (extra > 0) {  // scale the split count (bounded by the K-tiles)
+    const int nkt = (p.K + BK - 1) / BK;
+    for (int i = 0; i < extra && sp * 2 <= nkt; ++i) sp *= 2;
+  }
   if (splits > 0) sp = splits;
   if (sg_bn_deterministic()) sp = 1;  // one writer per gradient element: reproducible
   p.k_per_split = kps(p.K, sp);

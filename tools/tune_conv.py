@@ -21,8 +21,12 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--knob", type=int, default=0)
     ap.add_argument("--values", default="0,1")
-    ap.add_argument("--pass", dest="which", default="wgrad", choices=["fwd", "dgrad", "wgrad"])
+    ap.add_argument("--pass", dest="which", default="wgrad", choices=["fwd", "dgrad", "wgrad", "dx"])
+    ap.add_argument("--set", default="", help="fixed knobs for the whole sweep, e.g. 2=1,3=0")
     a = ap.parse_args()
+    for kv in filter(None, a.set.split(",")):
+        k, v = kv.split("=")
+        N.lib().set_tuning(int(k), int(v))
     vals = [int(v) for v in a.values.split(",")]
     B = a.batch
     dev = torch.device("cuda")
@@ -45,6 +49,15 @@ def main():
                 F.conv2d_bwd(x, w, dy, (st, st), (pad, pad), need_dx=False, dw_out=dw)
                 out = dw.clone()
                 t = timeit(lambda: F.conv2d_bwd(x, w, dy, (st, st), (pad, pad), need_dx=False, dw_out=dw))
+            elif a.which == "dx":  # data gradient only (the native kernel, no weight gradient)
+                dx = torch.empty_like(x)
+
+                def run():
+                    N.lib().conv_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), B, H, H, C, K, R, R, Ho, Ho, st,
+                                       st, pad, pad, 1, 1, 0, N.stream())
+                    return dx
+                out = run().float().clone()
+                t = timeit(run)
             elif a.which == "dgrad":
                 out = F.conv2d_bwd(x, w, dy, (st, st), (pad, pad), need_dx=True, dw_out=None)[0].float()
                 t = timeit(lambda: F.conv2d_bwd(x, w, dy, (st, st), (pad, pad), need_dx=True, dw_out=None)[0])
@@ -60,7 +73,7 @@ def main():
             tot[v] += t * cnt
         print(json.dumps(row), flush=True)
     print(json.dumps({"total_ms_weighted": {str(k): round(v, 3) for k, v in tot.items()}}))
-    N.lib().set_tuning(a.knob, 1)
+    N.lib().set_tuning(a.knob, {0: 5, 1: 1, 2: 1}.get(a.knob, 0))  # restore the default
 
 
 if __name__ == "__main__":
