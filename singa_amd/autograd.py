@@ -35,6 +35,10 @@ from .tensor import Tensor
 training = False
 
 ACCUMULATED = object()  # backward() returned: grad already added to the param's grad_view
+# backward() returned: the input gradient was added IN PLACE into the partial
+# gradient the engine offered through ``op.acc_into`` (see backward())
+ACC_INPLACE = object()
+INPLACE_ACC = True  # engine switch (tests A/B the in-place accumulation against separate adds)
 
 
 def _as_tuple(x):
@@ -219,13 +223,31 @@ def backward(y, dy=None) -> Iterator[Tuple[Tensor, Tensor]]:
         if deps[op0] == 0:
             heapq.heappush(heap, (-getattr(op0, "_seq", 0), id(op0), op0))
     pgrad: Dict[int, object] = {}
+    # ids of pending partial gradients the engine exclusively owns (fresh
+    # buffers produced by one backward, or sums it made): an operator that
+    # declares ``accepts_acc`` may add its input gradient into such a buffer
+    # in place (e.g. the conv dgrad epilogue with beta=1) instead of
+    # returning a new tensor for a separate add pass
+    owned: set = set()
     while heap:
         op = heapq.heappop(heap)[2]
         dys_ = pending.pop(op)
+        for d in dys_:
+            if d is not None:
+                owned.discard(id(d))
         if all(d is None for d in dys_) and not getattr(op, "always_run", False):
             dxs = (None,) * len(op.src)
         else:
+            if INPLACE_ACC and getattr(op, "accepts_acc", False):
+                acc = {}
+                for i, (src_op, _) in enumerate(op.src):
+                    if src_op is not None and op.params[i] is None and src_op in pending:
+                        cur = pending[src_op][op.src_idx[i]]
+                        if cur is not None and id(cur) in owned:
+                            acc[i] = cur
+                op.acc_into = acc
             dxs = _as_tuple(op.backward(*dys_))
+            op.acc_into = None
         if len(dxs) != len(op.src):
             raise RuntimeError(f"{op.name}: backward returned {len(dxs)} grads for {len(op.src)} inputs")
         for i, ((src_op, stores), dx) in enumerate(zip(op.src, dxs)):
@@ -251,14 +273,23 @@ def backward(y, dy=None) -> Iterator[Tuple[Tensor, Tensor]]:
                 continue
             if src_op is None:
                 continue
-            if dx is ACCUMULATED:
-                dx = None
+            if dx is ACCUMULATED or dx is ACC_INPLACE:
+                dx = None  # (ACC_INPLACE: already summed into pending[src_op])
             elif dx is not None and dx.dtype != op.src_dt[i] and dx.is_floating_point():
                 dx = dx.to(op.src_dt[i])  # mixed-precision edge: grads take the producer's dtype
             if src_op not in pending:
                 pending[src_op] = [None] * src_op.n_out
             j = op.src_idx[i]
-            pending[src_op][j] = _accum(pending[src_op][j], dx)
+            prev = pending[src_op][j]
+            new = _accum(prev, dx)
+            if new is not prev:
+                if prev is not None:
+                    owned.discard(id(prev))
+                    if dx is not None:  # a sum the engine just allocated
+                        owned.add(id(new))
+                elif getattr(new, "_sg_fresh", False) and len([d for d in dxs if d is new]) == 1:
+                    owned.add(id(new))
+            pending[src_op][j] = new
             deps[src_op] -= 1
             if deps[src_op] == 0:
                 heapq.heappush(heap, (-getattr(src_op, "_seq", 0), id(src_op), src_op))
@@ -596,6 +627,8 @@ class Conv2d(Operator):
             self.y = y if self.fuse_relu else None
         return y
 
+    accepts_acc = True
+
     def backward(self, dy):
         x, w = self.x, self.w
         self.x = self.w = None
@@ -603,8 +636,11 @@ class Conv2d(Operator):
             dy = F.relu_bwd_from_y(self.y, dy)
             self.y = None
         tgt = self.grad_target(1)
+        acc = (getattr(self, "acc_into", None) or {}).get(0)
         dx, dw, db = F.conv2d_bwd(x, w, dy, self.stride, self.padding, self.dilation, self.group,
-                                  need_dx=self.needs_grad(0), dw_out=tgt, need_db=self.has_bias)
+                                  need_dx=self.needs_grad(0), dw_out=tgt, need_db=self.has_bias, dx_acc=acc)
+        if acc is not None and dx is acc:
+            dx = ACC_INPLACE
         res = [dx, ACCUMULATED if tgt is not None else dw]
         if self.has_bias:
             tb = self.grad_target(2)

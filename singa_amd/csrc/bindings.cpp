@@ -72,7 +72,7 @@ void sg_conv_fwd(const void*, const void*, void*, const void*, int, int, int, in
 void sg_bn_fwd_from_ws(const void*, int, const void*, const void*, void*, void*, void*, void*, void*, void*, int64_t,
                        int, float, float, hipStream_t);
 void sg_conv_dgrad(const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int, int,
-                   int, int, int, hipStream_t);
+                   int, int, int, float, hipStream_t);
 void sg_conv_wgrad(const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int, int,
                    int, int, int, hipStream_t);
 void sg_set_tuning(int key, int value);
@@ -243,8 +243,14 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("conv_dgrad", [](P dy, P wt, P dx, int N, int H, int W, int C, int K, int R, int Sd, int Ho, int Wo, int sh,
                          int sw, int ph, int pw, int dh, int dw, int out_mode, P s) {
-    sg_conv_dgrad(CV(dy), CV(wt), V(dx), N, H, W, C, K, R, Sd, Ho, Wo, sh, sw, ph, pw, dh, dw, out_mode, S(s));
+    sg_conv_dgrad(CV(dy), CV(wt), V(dx), N, H, W, C, K, R, Sd, Ho, Wo, sh, sw, ph, pw, dh, dw, out_mode, 0.f, S(s));
     CHK("conv_dgrad");
+  });
+  // dx = dgrad + beta * dx (accumulate into an existing gradient, bf16 out)
+  m.def("conv_dgrad_acc", [](P dy, P wt, P dx, int N, int H, int W, int C, int K, int R, int Sd, int Ho, int Wo,
+                             int sh, int sw, int ph, int pw, int dh, int dw, int out_mode, float beta, P s) {
+    sg_conv_dgrad(CV(dy), CV(wt), V(dx), N, H, W, C, K, R, Sd, Ho, Wo, sh, sw, ph, pw, dh, dw, out_mode, beta, S(s));
+    CHK("conv_dgrad_acc");
   });
   m.def("conv_wgrad", [](P x, P dy, P dw_out, int N, int H, int W, int C, int K, int R, int Sd, int Ho, int Wo,
                          int sh, int sw, int ph, int pw, int dh, int dw, int splits, P s) {

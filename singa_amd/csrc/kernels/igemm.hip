@@ -907,9 +907,13 @@ void sg_conv_fwd(const void* x, const void* w, void* y, const void* bias, int N,
 }
 
 // conv data gradient: dy [N*Ho*Wo][K] bf16, w [K][R][S][C] bf16 -> dx [N*H*W][C]
-// (dilation 1; stride phases on blockIdx.z)
+// (dilation 1; stride phases on blockIdx.z).  beta != 0 accumulates into dx
+// (dx = dgrad + beta*dx: the gradient of a tensor with several consumers is
+// summed in the epilogue instead of by a separate add pass; phases without
+// taps then leave beta*dx)
 void sg_conv_dgrad(const void* dy, const void* w, void* dx, int N, int H, int W, int C, int K, int R, int S, int Ho,
-                   int Wo, int sh, int sw, int ph, int pw, int dh, int dw, int out_mode, hipStream_t s) {
+                   int Wo, int sh, int sw, int ph, int pw, int dh, int dw, int out_mode, float beta,
+                   hipStream_t s) {
   GemmArgs p{};
   p.g = make_geom(N, H, W, C, K, R, S, Ho, Wo, sh, sw, ph, pw, dh, dw);
   const int np = make_phases(p.g);
@@ -917,7 +921,7 @@ void sg_conv_dgrad(const void* dy, const void* w, void* dx, int N, int H, int W,
   for (int i = 0; i < np; ++i) Mmax = Mmax > N * p.g.phs[i].Hp * p.g.phs[i].Wp ? Mmax : N * p.g.phs[i].Hp * p.g.phs[i].Wp;
   p.M = Mmax; p.N = C; p.K = R * S * K;
   p.a = (const bf16*)dy; p.lda = 0; p.b = (const bf16*)w; p.ldb = 0;
-  p.c = dx; p.ldc = C; p.alpha = 1.f; p.beta = 0.f; p.bias = nullptr; p.relu = 0;
+  p.c = dx; p.ldc = C; p.alpha = 1.f; p.beta = beta; p.bias = nullptr; p.relu = 0;
   p.out_phase = 1;
   p.k_per_split = kps(p.K, 1);
   p.a_bytes = extent_bytes((int64_t)N * Ho * Wo * K);

@@ -492,9 +492,13 @@ def conv2d_fwd(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], stri
 
 
 def conv2d_bwd(x: torch.Tensor, w: torch.Tensor, dy: torch.Tensor, stride, padding, dilation=(1, 1), groups=1,
-               need_dx=True, dw_out: Optional[torch.Tensor] = None, need_db=False):
+               need_dx=True, dw_out: Optional[torch.Tensor] = None, need_db=False,
+               dx_acc: Optional[torch.Tensor] = None):
     """Returns (dx, dw, db).  If dw_out (fp32, same logical shape as w) is given
-    the weight gradient is ACCUMULATED into it (flat grad buffer views)."""
+    the weight gradient is ACCUMULATED into it (flat grad buffer views).
+    ``dx_acc``: an existing gradient of x (another consumer's contribution);
+    when its layout allows, the data gradient is added into it in the dgrad
+    epilogue and ``dx_acc`` itself is returned as dx."""
     sh, sw = stride
     ph, pw = padding
     dh, dw_ = dilation
@@ -519,12 +523,20 @@ def conv2d_bwd(x: torch.Tensor, w: torch.Tensor, dy: torch.Tensor, stride, paddi
                 wb = w if (w.dtype == torch.bfloat16 and N.is_cl(w)) else w.to(dtype=torch.bfloat16,
                                                                                 memory_format=torch.channels_last)
             od = torch.bfloat16 if x.dtype == torch.bfloat16 else torch.float32
-            dxp = torch.empty((Nn, Cp, H, W), dtype=od, device=x.device, memory_format=torch.channels_last)
-            N.lib().conv_dgrad(dyb.data_ptr(), wb.data_ptr(), dxp.data_ptr(), Nn, H, W, Cp, Kp, R, S, Ho, Wo, sh, sw,
-                               ph, pw, dh, dw_, 0 if od == torch.bfloat16 else 1, N.stream())
-            dx = dxp[:, :C].contiguous(memory_format=torch.channels_last) if Cx != Cp else dxp
-            if dx.dtype != x.dtype:
-                dx = dx.to(x.dtype)
+            if (dx_acc is not None and Cx == Cp and dx_acc.dtype == od and od == x.dtype
+                    and tuple(dx_acc.shape) == tuple(x.shape) and N.is_cl(dx_acc) and dx_acc.is_contiguous(
+                        memory_format=torch.channels_last)):
+                N.lib().conv_dgrad_acc(dyb.data_ptr(), wb.data_ptr(), dx_acc.data_ptr(), Nn, H, W, Cp, Kp, R, S, Ho,
+                                       Wo, sh, sw, ph, pw, dh, dw_, 0 if od == torch.bfloat16 else 1, 1.0, N.stream())
+                dx = dx_acc
+            else:
+                dxp = torch.empty((Nn, Cp, H, W), dtype=od, device=x.device, memory_format=torch.channels_last)
+                N.lib().conv_dgrad(dyb.data_ptr(), wb.data_ptr(), dxp.data_ptr(), Nn, H, W, Cp, Kp, R, S, Ho, Wo, sh,
+                                   sw, ph, pw, dh, dw_, 0 if od == torch.bfloat16 else 1, N.stream())
+                dx = dxp[:, :C].contiguous(memory_format=torch.channels_last) if Cx != Cp else dxp
+                if dx.dtype != x.dtype:
+                    dx = dx.to(x.dtype)
+                dx._sg_fresh = True
         # weight gradient, fp32 [Kp][R][S][Cp]
         direct = (dw_out is not None and not padded and dw_out.dtype == torch.float32 and N.is_cl(dw_out))
         target = dw_out if direct else _zeros_cl((Kp, Cp, R, S), torch.float32, x.device)
@@ -702,6 +714,9 @@ def batchnorm_bwd(x: torch.Tensor, dy: torch.Tensor, gamma: torch.Tensor, st: BN
                  st.mean.data_ptr(), st.invstd.data_ptr(), gamma.data_ptr(), _ws(R, C, x.device).data_ptr(),
                  coef.data_ptr(), dg.data_ptr(), db.data_ptr(), dx.data_ptr(), N.ptr(dres), R, C, mode, N.dt(x),
                  N.stream())
+        dx._sg_fresh = True
+        if dres is not None:
+            dres._sg_fresh = True
         return dx, dg, db, dres
     dims = (0,) if x.dim() == 2 else (0, 2, 3)
     shp = (1, C) if x.dim() == 2 else (1, C, 1, 1)

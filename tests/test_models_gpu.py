@@ -213,6 +213,84 @@ def test_bottleneck_matches_torch_fp32(gpu, stride, down):
     assert max(errs.values()) < 3e-2, errs
 
 
+def test_stacked_bottlenecks_inplace_grad_accumulation(gpu):
+    """Three stacked bottlenecks (down-sampling, strided down-sampling,
+    identity): the gradient at each block input is the sum of the residual
+    path and the conv1 data gradient, which the engine adds IN PLACE in the
+    conv dgrad epilogue (autograd.ACC_INPLACE).  A/B against the same step
+    with separate add passes (autograd.INPLACE_ACC = False): every parameter
+    gradient must agree to bf16 rounding; plus a loose sanity check against a
+    PyTorch fp32 reference (three stacked bf16 blocks flip some ReLU masks)."""
+    import torch.nn.functional as TF
+
+    from singa_amd import autograd as AG
+    from singa_amd.models.resnet import Bottleneck
+
+    dev = device.create_rocm_gpu()
+    dev.SetRandSeed(3)
+    cfg = [(16, 1, True), (16, 2, True), (16, 1, False)]
+    blks = [Bottleneck(pl, st, dn) for pl, st, dn in cfg]
+    g = torch.Generator(device=gpu).manual_seed(5)
+    xf = torch.randn(8, 32, 16, 16, device=gpu, generator=g)
+    x = Tensor(data=xf.bfloat16().contiguous(memory_format=torch.channels_last), device=dev, requires_grad=True,
+               stores_grad=False)
+    dyt = None
+
+    def run(inplace):
+        nonlocal dyt
+        AG.INPLACE_ACC = inplace
+        AG.training = True
+        try:
+            h = x
+            for b in blks:
+                h = b(h)
+            if dyt is None:
+                dyt = torch.randn(h.shape, device=gpu, generator=g)
+            loss_t = AG.reduce_sum(AG.mul(h, Tensor(data=dyt.bfloat16().contiguous(
+                memory_format=torch.channels_last), device=dev, requires_grad=False)), None)
+            gr = {id(p): gg.data.float().clone() for p, gg in AG.backward(loss_t)}
+        finally:
+            AG.training = False
+            AG.INPLACE_ACC = True
+        return h, gr
+
+    h, grads = run(True)
+    _, grads_sep = run(False)
+    ab = {}
+    for i, b in enumerate(blks):
+        for k, p in b.get_params().items():
+            ab[f"{i}.{k}"] = rel_err(grads[id(p)], grads_sep[id(p)])
+    assert max(ab.values()) < 3e-2, ab  # one bf16 rounding of the sum fewer, amplified by 2 BN backward passes
+
+    def q(t):
+        return t + (t.to(torch.bfloat16).float() - t).detach()
+
+    refs, hr = [], x.data.float().clone()
+    for b, (pl, st, dn) in zip(blks, cfg):
+        P = {k: v.data.float().clone().requires_grad_(True) for k, v in b.get_params().items()}
+        refs.append((b, P))
+
+        def bn(t, s_, b_, P=P):
+            return TF.batch_norm(t, None, None, P[s_], P[b_], training=True, eps=1e-5)
+
+        def w(k, P=P):
+            return P[k].to(torch.bfloat16).float()
+
+        o = q(TF.relu(bn(q(TF.conv2d(hr, w("conv1.W"))), "bn1.scale", "bn1.bias")))
+        o = q(TF.relu(bn(q(TF.conv2d(o, w("conv2.W"), stride=st, padding=1)), "bn2.scale", "bn2.bias")))
+        o = bn(q(TF.conv2d(o, w("conv3.W"))), "bn3.scale", "bn3.bias")
+        r = bn(q(TF.conv2d(hr, w("down_conv.W"), stride=st)), "down_bn.scale", "down_bn.bias") if dn else hr
+        hr = q(TF.relu(o + r))
+    (hr * dyt.to(torch.bfloat16).float()).sum().backward()
+    assert rel_err(h.data.float(), hr.detach()) < 3e-2
+    errs = {}
+    for i, (b, P) in enumerate(refs):
+        for k, p in b.get_params().items():
+            errs[f"{i}.{k}"] = rel_err(grads[id(p)].reshape(P[k].grad.shape), P[k].grad)
+    print(errs)
+    assert max(errs.values()) < 0.2, errs
+
+
 @pytest.mark.parametrize("small", [False, True])
 def test_alexnet_gpu_matches_cpu(gpu, small):
     """AlexNet (LRN, 11x11/4 conv, 3x3/2 max-pool, 4096-wide FCs) on the
