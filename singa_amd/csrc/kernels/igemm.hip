@@ -824,6 +824,10 @@ template <int AM, int BMODE, int OUT>
 static void launch(const GemmArgs& p, int M, int splits, hipStream_t s, int batch, int zdim) {
   int BM, BN;
   pick_tile(M, p.N, BM, BN);
+  if (g_tune[4] > 0) {  // tuning: force a tile shape (1: 128x64, 2: 64x128, 3: 64x64, 4: 128x128)
+    BM = (g_tune[4] == 2 || g_tune[4] == 3) ? 64 : 128;
+    BN = (g_tune[4] == 1 || g_tune[4] == 3) ? 64 : 128;
+  }
   const int tiles = ((M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
   const int z = zdim > 0 ? zdim : splits;
   if (BM == 128 && BN == 128) launch_t<128, 128, AM, BMODE, OUT>(p, tiles, batch, z, s);
