@@ -665,12 +665,15 @@ class BatchNorm2d(Operator):
         self.relu, self.has_residual = relu, has_residual
 
     def forward(self, x, gamma, beta, res=None):
+        # ReLU after a residual add: the mask cannot be recomputed from x, so
+        # the forward writes it as bits (1/16 of re-reading the bf16 output)
+        want = self.requires_grad and self.relu and self.has_residual
         y, st = F.batchnorm_fwd(x, gamma, beta, self.rm, self.rv, training, self.momentum, self.eps, self.relu,
-                                res)
+                                res, want_mask=want)
         if self.requires_grad:
             self.x, self.gamma, self.st = x, gamma, st
-            # the fused output is needed as the ReLU mask only when a residual was added
-            self.y = y if (self.relu and self.has_residual) else None
+            # the fused output is the ReLU mask only when a residual was added and no bit mask exists
+            self.y = y if (want and st.mask is None) else None
         return y
 
     def backward(self, dy):

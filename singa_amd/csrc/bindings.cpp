@@ -46,7 +46,7 @@ void sg_bn_fwd_stats(const void*, void*, const void*, const void*, void*, void*,
                      int, float, float, int, hipStream_t);
 void sg_bn_infer_params(const void*, const void*, const void*, const void*, void*, void*, void*, void*, int, float,
                         hipStream_t);
-void sg_bn_apply(const void*, const void*, const void*, const void*, void*, int64_t, int, int, int, hipStream_t);
+void sg_bn_apply(const void*, const void*, const void*, const void*, void*, void*, int64_t, int, int, int, hipStream_t);
 void sg_bn_bwd(const void*, const void*, const void*, const void*, const void*, const void*, const void*, const void*,
                void*, void*, void*, void*, void*, void*, int64_t, int, int, int, hipStream_t);
 void sg_pool_fwd(const void*, void*, void*, int, int, int, int, int, int, int, int, int, int, int, int, int, int, int,
@@ -170,8 +170,8 @@ PYBIND11_MODULE(_C, m) {
     sg_bn_infer_params(CV(g), CV(b), CV(rm), CV(rv), V(scale), V(shift), V(mean), V(invstd), C, eps, S(s));
     CHK("bn_infer_params");
   });
-  m.def("bn_apply", [](P x, P scale, P shift, P res, P y, int64_t R, int C, int relu, int dt, P s) {
-    sg_bn_apply(CV(x), CV(scale), CV(shift), CV(res), V(y), R, C, relu, dt, S(s)); CHK("bn_apply");
+  m.def("bn_apply", [](P x, P scale, P shift, P res, P y, int64_t R, int C, int relu, int dt, P s, P mask) {
+    sg_bn_apply(CV(x), CV(scale), CV(shift), CV(res), V(y), V(mask), R, C, relu, dt, S(s)); CHK("bn_apply");
   });
   m.def("bn_bwd", [](P x, P dy, P y, P scale, P shift, P mean, P invstd, P gamma, P ws, P coef, P dg, P db, P dx,
                      P dres, int64_t R, int C, int mask_mode, int dt, P s) {

@@ -31,7 +31,11 @@
 
 namespace sg {
 
-enum MaskMode : int { MASK_NONE = 0, MASK_Y = 1, MASK_AFFINE = 2 };
+// MASK_BITS: the ReLU mask of a fused BN(+residual)+ReLU output, one bit per
+// element (8 channels per byte, row-major [R][C/8]) written by the forward
+// apply: the backward reads 1/16 of the bytes it would read from the bf16
+// output (which stays materialised only as the next layer's input).
+enum MaskMode : int { MASK_NONE = 0, MASK_Y = 1, MASK_AFFINE = 2, MASK_BITS = 3 };
 constexpr int NSLOT = 32;      // atomic partial-sum slot rows of the fast mode
 constexpr int FIN_GROUPS = 4;  // band groups per finalize workgroup (256 threads = 64 channels x 4)
 static int g_bn_det = 0;       // deterministic reductions (set by sg_set_deterministic)
@@ -107,6 +111,14 @@ __global__ void __launch_bounds__(256) colpart_k(const T* __restrict__ x, const 
             g0[i] = y0[i] > 0.f ? g0[i] : 0.f;
             g1[i] = y1[i] > 0.f ? g1[i] : 0.f;
           }
+        } else if (V == 8 && mask_mode == MASK_BITS) {
+          const uint8_t* mb = (const uint8_t*)y;
+          const unsigned m0 = mb[(r * C + t.c0) >> 3], m1 = mb[((r + t.RT) * C + t.c0) >> 3];
+#pragma unroll
+          for (int i = 0; i < V; ++i) {
+            g0[i] = (m0 >> i) & 1u ? g0[i] : 0.f;
+            g1[i] = (m1 >> i) & 1u ? g1[i] : 0.f;
+          }
         } else if (mask_mode == MASK_AFFINE) {
 #pragma unroll
           for (int i = 0; i < V; ++i) {
@@ -135,6 +147,10 @@ __global__ void __launch_bounds__(256) colpart_k(const T* __restrict__ x, const 
           ldv<T, V>(y + r * C + t.c0, y0);
 #pragma unroll
           for (int i = 0; i < V; ++i) g0[i] = y0[i] > 0.f ? g0[i] : 0.f;
+        } else if (V == 8 && mask_mode == MASK_BITS) {
+          const unsigned m0 = ((const uint8_t*)y)[(r * C + t.c0) >> 3];
+#pragma unroll
+          for (int i = 0; i < V; ++i) g0[i] = (m0 >> i) & 1u ? g0[i] : 0.f;
         } else if (mask_mode == MASK_AFFINE) {
 #pragma unroll
           for (int i = 0; i < V; ++i) g0[i] = v0[i] * sc[i] + sf[i] > 0.f ? g0[i] : 0.f;
@@ -276,7 +292,8 @@ __global__ void bn_infer_params_k(const float* __restrict__ gamma, const float* 
 template <typename T, int V>
 __global__ void __launch_bounds__(256) bn_apply_k(const T* __restrict__ x, const float* __restrict__ scale,
                                                   const float* __restrict__ shift, const T* __restrict__ res,
-                                                  T* __restrict__ y, int64_t R, int C, int relu) {
+                                                  T* __restrict__ y, uint8_t* __restrict__ mask, int64_t R, int C,
+                                                  int relu) {
   const Tile2D t = tile2d<V>(C);
   if (!t.cok) return;
   float sc[V], sf[V];
@@ -300,6 +317,12 @@ __global__ void __launch_bounds__(256) bn_apply_k(const T* __restrict__ x, const
       for (int k = 0; k < V; ++k) v[k] = fmaxf(v[k], 0.f);
     }
     stv<T, V>(y + o, v);
+    if (V == 8 && mask) {  // bit k = (stored output of channel c0+k) > 0
+      unsigned b = 0;
+#pragma unroll
+      for (int k = 0; k < V; ++k) b |= ((float)(T)v[k] > 0.f ? 1u : 0u) << k;
+      mask[o >> 3] = (uint8_t)b;
+    }
   }
 }
 
@@ -331,6 +354,10 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_k(const T* __restrict__ x, c
       ldv<T, V>(y + o, yy);
 #pragma unroll
       for (int k = 0; k < V; ++k) g[k] = yy[k] > 0.f ? g[k] : 0.f;
+    } else if (V == 8 && mask_mode == MASK_BITS) {
+      const unsigned mb = ((const uint8_t*)y)[o >> 3];
+#pragma unroll
+      for (int k = 0; k < V; ++k) g[k] = (mb >> k) & 1u ? g[k] : 0.f;
     } else if (mask_mode == MASK_AFFINE) {
 #pragma unroll
       for (int k = 0; k < V; ++k) g[k] = v[k] * sc[k] + sf[k] > 0.f ? g[k] : 0.f;
@@ -465,17 +492,19 @@ void sg_bn_infer_params(const void* gamma, const void* beta, const void* run_mea
                      (float*)shift, (float*)mean, (float*)invstd, C, eps);
 }
 
-void sg_bn_apply(const void* x, const void* scale, const void* shift, const void* res, void* y, int64_t R, int C,
-                 int relu, int dtype, hipStream_t s) {
+// mask (optional, C % 8 == 0 only): 1-bit ReLU mask [R][C/8] of the output
+void sg_bn_apply(const void* x, const void* scale, const void* shift, const void* res, void* y, void* mask, int64_t R,
+                 int C, int relu, int dtype, hipStream_t s) {
   const int V = (C % 8 == 0) ? 8 : 1;
   dim3 grid = apply_grid(R, C, V);
   DISPATCH_FT(dtype, DISPATCH_V(V, hipLaunchKernelGGL((bn_apply_k<T, VV>), grid, dim3(256), 0, s, (const T*)x,
                                                       (const float*)scale, (const float*)shift, (const T*)res, (T*)y,
-                                                      R, C, relu)));
+                                                      (uint8_t*)mask, R, C, relu)));
 }
 
 // Full BN backward: reduce + finalize (coef, dgamma/dbeta accumulation) + apply.
-// mask_mode: 0 none, 1 mask from y (y>0), 2 mask from x*scale+shift>0.
+// mask_mode: 0 none, 1 mask from y (y>0), 2 mask from x*scale+shift>0,
+// 3 mask bits (y points at the [R][C/8] bitmask; C % 8 == 0).
 void sg_bn_bwd(const void* x, const void* dy, const void* y, const void* scale, const void* shift, const void* mean,
                const void* invstd, const void* gamma, void* ws, void* coef, void* dg, void* db, void* dx, void* dres,
                int64_t R, int C, int mask_mode, int dtype, hipStream_t s) {

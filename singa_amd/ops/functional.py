@@ -614,11 +614,14 @@ def colsum(x2: torch.Tensor, with_sq: bool = False, out: Optional[torch.Tensor] 
 
 
 class BNState:
-    """Saved tensors of a batch-norm forward needed by the backward."""
-    __slots__ = ("mean", "invstd", "scale", "shift")
+    """Saved tensors of a batch-norm forward needed by the backward.
+    ``mask``: 1-bit ReLU mask [R][C/8] of a fused BN(+residual)+ReLU output
+    (written by the forward apply when requested; the backward then reads it
+    instead of the bf16 output)."""
+    __slots__ = ("mean", "invstd", "scale", "shift", "mask")
 
-    def __init__(self, mean, invstd, scale, shift):
-        self.mean, self.invstd, self.scale, self.shift = mean, invstd, scale, shift
+    def __init__(self, mean, invstd, scale, shift, mask=None):
+        self.mean, self.invstd, self.scale, self.shift, self.mask = mean, invstd, scale, shift, mask
 
 
 def _bn_native(x: torch.Tensor) -> bool:
@@ -627,9 +630,11 @@ def _bn_native(x: torch.Tensor) -> bool:
 
 def batchnorm_fwd(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, run_mean: torch.Tensor,
                   run_var: torch.Tensor, training: bool, momentum: float = 0.1, eps: float = 1e-5,
-                  relu: bool = False, residual: Optional[torch.Tensor] = None):
+                  relu: bool = False, residual: Optional[torch.Tensor] = None, want_mask: bool = False):
     """y = act(BN(x) + residual).  4-D x (channels_last on GPU) or 2-D [B, C].
-    momentum follows the PyTorch convention (weight of the new statistic)."""
+    momentum follows the PyTorch convention (weight of the new statistic).
+    ``want_mask`` (with relu, native path, C % 8 == 0): also write the 1-bit
+    ReLU mask into the returned state (``st.mask``) for the backward."""
     C = x.shape[1]
     if _bn_native(x):
         L = N.lib()
@@ -657,9 +662,12 @@ def batchnorm_fwd(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, run_
                 res = _dense(res).to(x.dtype).contiguous(
                     memory_format=torch.channels_last if x.dim() == 4 else torch.contiguous_format)
         y = _like(x)
+        mask = None
+        if want_mask and relu and C % 8 == 0:
+            mask = torch.empty(R * C // 8, dtype=torch.uint8, device=dev)
         L.bn_apply(x.data_ptr(), scale.data_ptr(), shift.data_ptr(), N.ptr(res), y.data_ptr(), R, C, int(relu),
-                   N.dt(x), N.stream())
-        return y, BNState(mean, invstd, scale, shift)
+                   N.dt(x), N.stream(), N.ptr(mask))
+        return y, BNState(mean, invstd, scale, shift, mask)
     # CPU reference
     dims = (0,) if x.dim() == 2 else (0, 2, 3)
     shp = (1, C) if x.dim() == 2 else (1, C, 1, 1)
@@ -699,7 +707,9 @@ def batchnorm_bwd(x: torch.Tensor, dy: torch.Tensor, gamma: torch.Tensor, st: BN
             dy = dy.to(x.dtype).contiguous(memory_format=torch.channels_last if x.dim() == 4 else
                                            torch.contiguous_format)
         ym = y_for_mask
-        if ym is not None:
+        if st.mask is not None and relu:
+            ym, mode = st.mask, 3  # 1-bit mask written by the forward apply
+        elif ym is not None:
             if ym.dtype != x.dtype or not _same_layout(ym, x):
                 raise ValueError("batchnorm_bwd: mask tensor layout mismatch")
             mode = 1

@@ -508,7 +508,7 @@ def test_bn_kernels_stay_in_bounds(gpu, R, C):
                    *[t.data_ptr() for t in p], R, C, 0.1, 1e-5, NN.BF16, s)
     wchk("bn_fwd_stats ws")
     y, chk = _guarded(R * C, torch.bfloat16, gpu)
-    L.bn_apply(x.data_ptr(), p[2].data_ptr(), p[3].data_ptr(), 0, y.data_ptr(), R, C, 1, NN.BF16, s)
+    L.bn_apply(x.data_ptr(), p[2].data_ptr(), p[3].data_ptr(), 0, y.data_ptr(), R, C, 1, NN.BF16, s, 0)
     chk("bn_apply")
     coef = torch.empty(3 * C, device=gpu)
     dg, db = torch.zeros(C, device=gpu), torch.zeros(C, device=gpu)
