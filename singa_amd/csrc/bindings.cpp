@@ -71,8 +71,10 @@ void sg_conv_fwd(const void*, const void*, void*, const void*, int, int, int, in
                  int, int, int, int, int, int, void*, hipStream_t);
 void sg_bn_fwd_from_ws(const void*, int, const void*, const void*, void*, void*, void*, void*, void*, void*, int64_t,
                        int, float, float, hipStream_t);
+void sg_set_ws_prezeroed(int);
+void sg_zero(void*, int64_t, hipStream_t);
 void sg_conv_dgrad(const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int, int,
-                   int, int, int, float, hipStream_t);
+                   int, int, int, float, void*, hipStream_t);
 void sg_conv_wgrad(const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int, int,
                    int, int, int, hipStream_t);
 void sg_set_tuning(int key, int value);
@@ -243,13 +245,16 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("conv_dgrad", [](P dy, P wt, P dx, int N, int H, int W, int C, int K, int R, int Sd, int Ho, int Wo, int sh,
                          int sw, int ph, int pw, int dh, int dw, int out_mode, P s) {
-    sg_conv_dgrad(CV(dy), CV(wt), V(dx), N, H, W, C, K, R, Sd, Ho, Wo, sh, sw, ph, pw, dh, dw, out_mode, 0.f, S(s));
+    sg_conv_dgrad(CV(dy), CV(wt), V(dx), N, H, W, C, K, R, Sd, Ho, Wo, sh, sw, ph, pw, dh, dw, out_mode, 0.f, nullptr,
+                  S(s));
     CHK("conv_dgrad");
   });
   // dx = dgrad + beta * dx (accumulate into an existing gradient, bf16 out)
+  // dx = dgrad + beta * dx; wtbuf (0 or K*R*S*C bf16 scratch): K-major transposed-weight path
   m.def("conv_dgrad_acc", [](P dy, P wt, P dx, int N, int H, int W, int C, int K, int R, int Sd, int Ho, int Wo,
-                             int sh, int sw, int ph, int pw, int dh, int dw, int out_mode, float beta, P s) {
-    sg_conv_dgrad(CV(dy), CV(wt), V(dx), N, H, W, C, K, R, Sd, Ho, Wo, sh, sw, ph, pw, dh, dw, out_mode, beta, S(s));
+                             int sh, int sw, int ph, int pw, int dh, int dw, int out_mode, float beta, P s, P wtbuf) {
+    sg_conv_dgrad(CV(dy), CV(wt), V(dx), N, H, W, C, K, R, Sd, Ho, Wo, sh, sw, ph, pw, dh, dw, out_mode, beta,
+                  V(wtbuf), S(s));
     CHK("conv_dgrad_acc");
   });
   m.def("conv_wgrad", [](P x, P dy, P dw_out, int N, int H, int W, int C, int K, int R, int Sd, int Ho, int Wo,
@@ -257,5 +262,7 @@ PYBIND11_MODULE(_C, m) {
     sg_conv_wgrad(CV(x), CV(dy), V(dw_out), N, H, W, C, K, R, Sd, Ho, Wo, sh, sw, ph, pw, dh, dw, splits, S(s));
     CHK("conv_wgrad");
   });
+  m.def("set_ws_prezeroed", [](int on) { sg_set_ws_prezeroed(on); });
+  m.def("zero", [](P p, int64_t bytes, P s) { sg_zero(V(p), bytes, S(s)); CHK("zero"); });
   m.def("set_tuning", [](int key, int value) { sg_set_tuning(key, value); });
 }

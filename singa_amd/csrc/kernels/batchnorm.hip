@@ -39,6 +39,7 @@ enum MaskMode : int { MASK_NONE = 0, MASK_Y = 1, MASK_AFFINE = 2, MASK_BITS = 3 
 constexpr int NSLOT = 32;      // atomic partial-sum slot rows of the fast mode
 constexpr int FIN_GROUPS = 4;  // band groups per finalize workgroup (256 threads = 64 channels x 4)
 static int g_bn_det = 0;       // deterministic reductions (set by sg_set_deterministic)
+static int g_ws_prezeroed = 0; // next launch's workspace is already zeroed (per-step arena): skip its zeroing
 
 struct Tile2D {
   int CT, RT, tx, ty, c0;
@@ -394,12 +395,23 @@ extern "C" int64_t sg_colreduce_ws(int64_t R, int C) {
   return (int64_t)(g_bn_det ? sg_colreduce_bands(R, C) : NSLOT) * 2 * C;
 }
 extern "C" void sg_bn_set_deterministic(int on) { g_bn_det = on; }
+// The next launch that owns a slot-atomic workspace finds it pre-zeroed
+// (one-shot flag: consumed by that launch)
+extern "C" void sg_set_ws_prezeroed(int on) { g_ws_prezeroed = on; }
+extern "C" int sg_ws_prezeroed() {
+  const int pz = g_ws_prezeroed;
+  g_ws_prezeroed = 0;
+  return pz;
+}
+extern "C" void sg_zero(void* p, int64_t bytes, hipStream_t s) { sg_zero_async(p, (size_t)bytes, s); }
 extern "C" int sg_bn_deterministic() { return g_bn_det; }
 
 // rows the finalize sums for a reduction launched on `grid`
 static inline int fin_rows(const dim3& grid) { return g_bn_det ? (int)grid.x : NSLOT; }
 static inline void zero_ws(void* ws, int C, hipStream_t s) {
-  if (!g_bn_det) sg_zero_async(ws, sizeof(float) * NSLOT * 2 * C, s);
+  const int pz = g_ws_prezeroed;  // one-shot: set by the caller for this launch only
+  g_ws_prezeroed = 0;
+  if (!g_bn_det && !pz) sg_zero_async(ws, sizeof(float) * NSLOT * 2 * C, s);
 }
 
 static inline dim3 fin_grid(int C) { return dim3((C + 63) / 64); }

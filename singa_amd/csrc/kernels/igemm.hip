@@ -51,6 +51,7 @@ enum LoadMode : int {
   LM_DGRAD_A = 3,  // A of dgrad: gather of dy NHWC over the phase taps, K = (tap, k)
   LM_WGRAD_B = 4,  // B of wgrad: x gathered, rows = (r, s, c), K = output pixels
   LM_DGRAD_B = 5,  // B of dgrad: W [K][R][S][C] as K-outer, rows = c, K = (tap, k)
+  LM_DGRAD_BT = 6, // B of dgrad from the transposed copy WT [R][S][C][K]: K-major rows c, K = (tap, k)
 };
 enum OutMode : int { OUT_BF16 = 0, OUT_F32 = 1, OUT_F32_ATOMIC = 2 };
 
@@ -171,6 +172,8 @@ struct Loader {
           base[v] = n * g.H * g.W * g.C;
           i0[v] = oh * g.sh - g.ph;
           j0[v] = ow * g.sw - g.pw;
+        } else if constexpr (MODE == LM_DGRAD_BT) {
+          base[v] = rr * p.g.K;  // row c of a tap slab [C][K]
         } else {  // LM_DGRAD_A: row = (n, hh, ww) of the phase grid
           const ConvGeom& g = p.g;
           const int n = P.dHpWp.div(rr);
@@ -207,6 +210,22 @@ struct Loader {
       for (int v = 0; v < VPT; ++v) {
         const bool o = ok[v] && kin;
         bld16(rsrc, o ? (unsigned)(base[v] + kk) * 2u : OOB, lds + (8 * w + 32 * v) * 128);
+      }
+    } else if constexpr (MODE == LM_DGRAD_BT) {
+      // K-tile = one tap (g.K % 64 == 0, host-checked): scalar tap math, then
+      // a plain K-major row fetch from that tap's [C][K] slab
+      const ConvGeom& g = p.g;
+      const int tap = g.dK.div(k0);
+      const int j = P.dns.div(tap), i = tap - j * P.ns;
+      const int r = P.r0 + g.sh * j, sc = P.s0 + g.sw * i;
+      const int tapoff = (r * g.S + sc) * g.C * g.K;
+      const int kk = k0 + lchunk * 8;
+      const bool kin = kk < kend;
+      const int k = kk - tap * g.K;
+#pragma unroll
+      for (int v = 0; v < VPT; ++v) {
+        const bool o = ok[v] && kin;
+        bld16(rsrc, o ? (unsigned)(tapoff + base[v] + k) * 2u : OOB, lds + (8 * w + 32 * v) * 128);
       }
     } else if constexpr (MODE == LM_CONV_FWD || MODE == LM_DGRAD_A) {
       const ConvGeom& g = p.g;
@@ -704,6 +723,24 @@ __global__ void __launch_bounds__(NT, 2) igemm_k(const GemmArgs p) {
   }
 }
 
+// WT[t][c][k] = W[k][t][c] (bf16): per-tap [K][C] -> [C][K] through a 64x64
+// LDS tile (+1 column pad against bank conflicts), 256 threads.
+__global__ void __launch_bounds__(256) wt_transpose_k(const bf16* __restrict__ w, bf16* __restrict__ wt, int K,
+                                                      int T, int C) {
+  __shared__ bf16 tile[64][65];
+  const int c0 = blockIdx.x * 64, k0 = blockIdx.y * 64, t = blockIdx.z;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int r = ty; r < 64; r += 4) {
+    const int k = k0 + r, c = c0 + tx;
+    tile[r][tx] = (k < K && c < C) ? w[((int64_t)k * T + t) * C + c] : (bf16)0.f;
+  }
+  __syncthreads();
+  for (int r = ty; r < 64; r += 4) {
+    const int c = c0 + r, k = k0 + tx;
+    if (c < C && k < K) wt[((int64_t)t * C + c) * K + k] = tile[tx][r];
+  }
+}
+
 }  // namespace sg
 
 using namespace sg;
@@ -861,6 +898,7 @@ static unsigned extent_bytes(int64_t elems) {
 extern "C" {
 
 int sg_bn_deterministic();  // batchnorm.hip: deterministic-reduction mode
+int sg_ws_prezeroed();      // batchnorm.hip: one-shot 'workspace pre-zeroed' flag (per-step arena)
 
 // Plain GEMM: C[M][N] = alpha * sum_k A(m,k) B(n,k) (+ beta*C) ... with
 //   a_kouter = 0: A stored [M][K] (lda), 1: A stored [K][M]
@@ -898,7 +936,8 @@ void sg_conv_fwd(const void* x, const void* w, void* y, const void* bias, int N,
   GemmArgs p{};
   p.stats = (out_mode == OUT_BF16 && (K & 7) == 0 && g_tune[1]) ? (float*)stats : nullptr;
   p.stats_det = sg_bn_deterministic();
-  if (p.stats && !p.stats_det) sg_zero_async(p.stats, sizeof(float) * 32 * 2 * K, s);  // atomic slot rows
+  if (p.stats && !p.stats_det && !sg_ws_prezeroed())  // (consumes the one-shot pre-zeroed flag)
+    sg_zero_async(p.stats, sizeof(float) * 32 * 2 * K, s);  // atomic slot rows
   p.g = make_geom(N, H, W, C, K, R, S, Ho, Wo, sh, sw, ph, pw, dh, dw);
   p.M = N * Ho * Wo; p.N = K; p.K = R * S * C;
   p.a = (const bf16*)x; p.lda = 0; p.b = (const bf16*)w; p.ldb = R * S * C;
@@ -914,9 +953,10 @@ void sg_conv_fwd(const void* x, const void* w, void* y, const void* bias, int N,
 // (dilation 1; stride phases on blockIdx.z).  beta != 0 accumulates into dx
 // (dx = dgrad + beta*dx: the gradient of a tensor with several consumers is
 // summed in the epilogue instead of by a separate add pass; phases without
-// taps then leave beta*dx)
+// taps then leave beta*dx).  wt (optional, K*R*S*C bf16 scratch, used when
+// K % 64 == 0): the weights are transposed into it and read K-major.
 void sg_conv_dgrad(const void* dy, const void* w, void* dx, int N, int H, int W, int C, int K, int R, int S, int Ho,
-                   int Wo, int sh, int sw, int ph, int pw, int dh, int dw, int out_mode, float beta,
+                   int Wo, int sh, int sw, int ph, int pw, int dh, int dw, int out_mode, float beta, void* wt,
                    hipStream_t s) {
   GemmArgs p{};
   p.g = make_geom(N, H, W, C, K, R, S, Ho, Wo, sh, sw, ph, pw, dh, dw);
@@ -931,6 +971,17 @@ void sg_conv_dgrad(const void* dy, const void* w, void* dx, int N, int H, int W,
   p.a_bytes = extent_bytes((int64_t)N * Ho * Wo * K);
   p.b_bytes = extent_bytes((int64_t)K * R * S * C);
   extent_bytes((int64_t)N * H * W * C);
+  if (wt && (K & 63) == 0) {
+    // K-major weights: transpose once per call (weights are small), then the
+    // B operand is read with ds_read_b128 like the forward's, not transposed
+    // through LDS
+    hipLaunchKernelGGL(wt_transpose_k, dim3((C + 63) / 64, (K + 63) / 64, R * S), dim3(256), 0, s, (const bf16*)w,
+                       (bf16*)wt, K, R * S, C);
+    p.b = (const bf16*)wt;
+    if (out_mode == OUT_F32) launch<LM_DGRAD_A, LM_DGRAD_BT, OUT_F32>(p, Mmax, 1, s, 1, np);
+    else launch<LM_DGRAD_A, LM_DGRAD_BT, OUT_BF16>(p, Mmax, 1, s, 1, np);
+    return;
+  }
   if (out_mode == OUT_F32) launch<LM_DGRAD_A, LM_DGRAD_B, OUT_F32>(p, Mmax, 1, s, 1, np);
   else launch<LM_DGRAD_A, LM_DGRAD_B, OUT_BF16>(p, Mmax, 1, s, 1, np);
 }

@@ -28,6 +28,7 @@ import torch
 
 from . import autograd
 from . import layer
+from .ops import functional as _F
 from .tensor import Tensor
 
 
@@ -104,7 +105,14 @@ class Model(layer.Layer):
         use_graph = self.graph_mode and args and isinstance(args[0], Tensor) and args[0].data.is_cuda
         if not use_graph:
             autograd.training = self.training
-            return fn(*args, **kwargs)
+            arena = self.training and args and isinstance(args[0], Tensor) and args[0].data.is_cuda
+            if arena:  # one zeroing launch for every reduction workspace of the step
+                _F.ARENA.begin(args[0].data.device)
+            try:
+                return fn(*args, **kwargs)
+            finally:
+                if arena:
+                    _F.ARENA.end()
         return self._run_graph(fn, args, kwargs)
 
     def _n_forward_args(self, args) -> int:
@@ -125,7 +133,12 @@ class Model(layer.Layer):
             n = self._warm.get(key, 0)
             if n < self.graph_warmup:
                 self._warm[key] = n + 1
-                return fn(*args, **kwargs)
+                if self.training:
+                    _F.ARENA.begin(args[0].data.device)
+                try:
+                    return fn(*args, **kwargs)
+                finally:
+                    _F.ARENA.end()
             torch.cuda.synchronize()
             g = torch.cuda.CUDAGraph()
             if self._pool is None:
@@ -140,7 +153,12 @@ class Model(layer.Layer):
                 # dropout masks differ on every replay (host-side Philox
                 # offsets are frozen into the captured launches)
                 dev.advance_rng_epoch()
-                out = fn(*args, **kwargs)
+                if self.training:
+                    _F.ARENA.begin(args[0].data.device)  # the arena's zeroing kernel is captured too
+                try:
+                    out = fn(*args, **kwargs)
+                finally:
+                    _F.ARENA.end()
             if opt is not None:
                 opt.step_counter = sc0  # capture does not execute; replay below does
             self._graphs[key] = (g, tuple(args), out)

@@ -475,8 +475,8 @@ def conv2d_fwd(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], stri
                 and not _NO_BN_STATS):
             L = N.lib()
             rows = L.conv_stats_rows(Nn * Ho * Wo, K)
-            if rows > 0:  # deterministic: every row written (plain stores); else 32 atomic slot rows zeroed by conv_fwd
-                ws = torch.empty(rows * 2 * K, dtype=torch.float32, device=x.device)
+            if rows > 0:  # deterministic: every row written (plain stores); else 32 atomic slot rows (zeroed)
+                ws = zeroed_ws(rows * 2 * K, x.device)
         N.lib().conv_fwd(xb.data_ptr(), wb.data_ptr(), y.data_ptr(), N.ptr(bias), Nn, H, W, Cp, Kp, R, S, Ho, Wo, sh,
                          sw, ph, pw, dh, dw, int(relu), 0 if od == torch.bfloat16 else 1, N.stream(), N.ptr(ws))
         if ws is not None:
@@ -489,6 +489,12 @@ def conv2d_fwd(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], stri
     if relu:
         y = torch.relu(y)
     return y.to(out_dtype)
+
+
+# conv data gradient reads the weights K-major from a per-call transposed copy
+# (ds_read_b128 fragments like the forward) instead of transposing them
+# through LDS (ds_read_b64_tr_b16); switchable for A/B measurements
+DGRAD_KMAJOR = os.environ.get("SINGA_AMD_DGRAD_KMAJOR", "1") != "0"
 
 
 def conv2d_bwd(x: torch.Tensor, w: torch.Tensor, dy: torch.Tensor, stride, padding, dilation=(1, 1), groups=1,
@@ -523,16 +529,20 @@ def conv2d_bwd(x: torch.Tensor, w: torch.Tensor, dy: torch.Tensor, stride, paddi
                 wb = w if (w.dtype == torch.bfloat16 and N.is_cl(w)) else w.to(dtype=torch.bfloat16,
                                                                                 memory_format=torch.channels_last)
             od = torch.bfloat16 if x.dtype == torch.bfloat16 else torch.float32
+            om = 0 if od == torch.bfloat16 else 1
+            # K-major transposed weights for the B operand (scratch from the caching allocator)
+            wt = (torch.empty(Kp * Cp * R * S, dtype=torch.bfloat16, device=x.device)
+                  if DGRAD_KMAJOR and Kp % 64 == 0 else None)
             if (dx_acc is not None and Cx == Cp and dx_acc.dtype == od and od == x.dtype
                     and tuple(dx_acc.shape) == tuple(x.shape) and N.is_cl(dx_acc) and dx_acc.is_contiguous(
                         memory_format=torch.channels_last)):
                 N.lib().conv_dgrad_acc(dyb.data_ptr(), wb.data_ptr(), dx_acc.data_ptr(), Nn, H, W, Cp, Kp, R, S, Ho,
-                                       Wo, sh, sw, ph, pw, dh, dw_, 0 if od == torch.bfloat16 else 1, 1.0, N.stream())
+                                       Wo, sh, sw, ph, pw, dh, dw_, om, 1.0, N.stream(), N.ptr(wt))
                 dx = dx_acc
             else:
                 dxp = torch.empty((Nn, Cp, H, W), dtype=od, device=x.device, memory_format=torch.channels_last)
-                N.lib().conv_dgrad(dyb.data_ptr(), wb.data_ptr(), dxp.data_ptr(), Nn, H, W, Cp, Kp, R, S, Ho, Wo, sh,
-                                   sw, ph, pw, dh, dw_, 0 if od == torch.bfloat16 else 1, N.stream())
+                N.lib().conv_dgrad_acc(dyb.data_ptr(), wb.data_ptr(), dxp.data_ptr(), Nn, H, W, Cp, Kp, R, S, Ho, Wo,
+                                       sh, sw, ph, pw, dh, dw_, om, 0.0, N.stream(), N.ptr(wt))
                 dx = dxp[:, :C].contiguous(memory_format=torch.channels_last) if Cx != Cp else dxp
                 if dx.dtype != x.dtype:
                     dx = dx.to(x.dtype)
@@ -585,14 +595,72 @@ def _rows_c(x: torch.Tensor) -> Tuple[torch.Tensor, int, int]:
 _BANDS: dict = {}
 
 
+class _ZeroArena:
+    """Per-training-step arena of ZEROED fp32 scratch for the slot-atomic
+    reduction workspaces (BatchNorm statistics / backward partial sums and
+    the conv-epilogue BN statistics).  ``begin()`` zeroes the whole arena with
+    ONE kernel at the start of a step; a launch whose workspace comes from the
+    arena tells the kernel library it is pre-zeroed (a host flag read at
+    launch time), which replaces ~2 zeroing launches per BatchNorm layer
+    (~100 per ResNet-50 step).  Sizes settle after the first step (high-water
+    mark), so a HIP-graph capture never reallocates."""
+
+    def __init__(self):
+        self.buf: Optional[torch.Tensor] = None
+        self.retired: list = []
+        self.off = 0
+        self.hwm = 0
+        self.active = False
+
+    def begin(self, device) -> None:
+        if not N.available() or device.type != "cuda" or N.lib().deterministic():
+            return
+        if self.hwm > 0 and (self.buf is None or self.buf.numel() < self.hwm or self.buf.device != device):
+            if self.buf is not None:  # a captured HIP graph may still address it: never free
+                self.retired.append(self.buf)
+            self.buf = torch.empty(self.hwm + self.hwm // 8 + 1024, dtype=torch.float32, device=device)
+        self.off = 0
+        self.active = True
+        if self.buf is not None:
+            N.lib().zero(self.buf.data_ptr(), self.buf.numel() * 4, N.stream())
+
+    def take(self, n: int, device) -> Optional[torch.Tensor]:
+        """A zeroed slice of n floats, or None (arena inactive / too small)."""
+        if not self.active:
+            return None
+        n = (n + 63) // 64 * 64
+        end = self.off + n
+        self.hwm = max(self.hwm, end)
+        if self.buf is None or end > self.buf.numel() or self.buf.device != device:
+            return None
+        t = self.buf[self.off:end]
+        self.off = end
+        return t
+
+    def end(self) -> None:
+        self.active = False
+
+
+ARENA = _ZeroArena()
+
+
+def zeroed_ws(n: int, device) -> torch.Tensor:
+    """fp32 slot-atomic workspace of n floats for the NEXT native launch:
+    an arena slice (pre-zeroed: the kernel skips its zeroing) or a fresh
+    buffer (the kernel zeroes it)."""
+    t = ARENA.take(n, device)
+    if N.available():
+        N.lib().set_ws_prezeroed(1 if t is not None else 0)
+    return t if t is not None else torch.empty(n, dtype=torch.float32, device=device)
+
+
 def _ws(R: int, C: int, device) -> torch.Tensor:
-    """Partial-sum workspace of a [R][C] column reduction (no zeroing needed:
-    every [band][2][C] slot is written)."""
+    """Partial-sum workspace of a [R][C] column reduction."""
     key = (R, C, N.lib().deterministic())
     n = _BANDS.get(key)
     if n is None:
         n = _BANDS[key] = N.lib().colreduce_ws(R, C)
-    return torch.empty(n, dtype=torch.float32, device=device)
+    return zeroed_ws(n, device)
 
 
 def colsum(x2: torch.Tensor, with_sq: bool = False, out: Optional[torch.Tensor] = None):

@@ -102,12 +102,14 @@ CONV_CASES = [
 ]
 
 
-@pytest.mark.parametrize("wmode", [0, 1])
+@pytest.mark.parametrize("kmajor", [True, False])
+@pytest.mark.parametrize("wmode", [0, 1, 5])
 @pytest.mark.parametrize("case", CONV_CASES)
-def test_conv_fwd_bwd(gpu, case, wmode):
+def test_conv_fwd_bwd(gpu, case, wmode, kmajor, monkeypatch):
     from singa_amd.ops import functional as F
     from singa_amd.ops import native as NN
-    NN.lib().set_tuning(0, wmode)  # wgrad tile policy: 64-tiles + splits / largest tiles
+    monkeypatch.setattr(F, "DGRAD_KMAJOR", kmajor)  # dgrad B operand: transposed K-major copy / LDS transpose
+    NN.lib().set_tuning(0, wmode)  # wgrad tile policy: 64-tiles + splits / largest tiles / measured default
     N_, C, H, W, K, R, S, st, pd = case
     g = torch.Generator().manual_seed(3)
     x = bf(torch.randn(N_, C, H, W, generator=g)).float()
@@ -126,7 +128,7 @@ def test_conv_fwd_bwd(gpu, case, wmode):
     dw_acc = torch.zeros(K, C, R, S, device=gpu)
     dx, dw, db = F.conv2d_bwd(xg.float().contiguous(memory_format=torch.channels_last), wg, dyg, (st, st),
                               (pd, pd), need_dx=True, dw_out=dw_acc, need_db=True)
-    NN.lib().set_tuning(0, 4)
+    NN.lib().set_tuning(0, 5)
     # bf16 outputs (the LDS-staged epilogue): fwd and dgrad
     yb = F.conv2d_fwd(xg, wg, None, (st, st), (pd, pd), out_dtype=torch.bfloat16)
     assert yb.dtype == torch.bfloat16 and rel_err(yb.float(), yr.detach()) < 1e-2

@@ -52,9 +52,12 @@ def main():
             elif a.which == "dx":  # data gradient only (the native kernel, no weight gradient)
                 dx = torch.empty_like(x)
 
-                def run():
-                    N.lib().conv_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), B, H, H, C, K, R, R, Ho, Ho, st,
-                                       st, pad, pad, 1, 1, 0, N.stream())
+                wt = torch.empty(K * C * R * R, dtype=torch.bfloat16, device=dev)
+
+                def run():  # knob 5 (tools-only): 1 = K-major transposed-weight path
+                    N.lib().conv_dgrad_acc(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), B, H, H, C, K, R, R, Ho, Ho,
+                                           st, st, pad, pad, 1, 1, 0, 0.0, N.stream(),
+                                           wt.data_ptr() if (a.knob == 5 and v == 1) else 0)
                     return dx
                 out = run().float().clone()
                 t = timeit(run)
