@@ -92,6 +92,15 @@ def main() -> int:
         if args.sync_warmup:
             torch.cuda.synchronize()
     torch.cuda.synchronize()
+    if args.warmup > 0:
+        # guard against a silently truncated backward (it would inflate the
+        # number): after a step every parameter must hold a non-zero gradient
+        st = optimizer.store
+        dead = [i for i, (p, off) in enumerate(zip(st.params, st.offsets))
+                if float(st.g[off:off + p.data.numel()].abs().sum()) == 0.0]
+        if dead:
+            print(f"bench.py: {len(dead)} of {len(st.params)} parameters got no gradient", file=sys.stderr)
+            return 3
     if world > 1:
         comm.barrier()
     torch.cuda.synchronize()

@@ -637,8 +637,16 @@ class Conv2d(Operator):
             self.y = None
         tgt = self.grad_target(1)
         acc = (getattr(self, "acc_into", None) or {}).get(0)
+        # input produced by a training BN+ReLU (no residual): its backward
+        # reduction is fused into this dgrad's epilogue
+        prod = self.src[0][0] if self.src else None
+        bnp = None
+        if (acc is None and isinstance(prod, BatchNorm2d) and prod.relu and not prod.has_residual
+                and getattr(prod, "st", None) is not None and getattr(prod, "x", None) is not None):
+            bnp = (prod.x, prod.st)
         dx, dw, db = F.conv2d_bwd(x, w, dy, self.stride, self.padding, self.dilation, self.group,
-                                  need_dx=self.needs_grad(0), dw_out=tgt, need_db=self.has_bias, dx_acc=acc)
+                                  need_dx=self.needs_grad(0), dw_out=tgt, need_db=self.has_bias, dx_acc=acc,
+                                  bn_producer=bnp)
         if acc is not None and dx is acc:
             dx = ACC_INPLACE
         res = [dx, ACCUMULATED if tgt is not None else dw]

@@ -73,6 +73,12 @@ void sg_bn_fwd_from_ws(const void*, int, const void*, const void*, void*, void*,
                        int, float, float, hipStream_t);
 void sg_set_ws_prezeroed(int);
 void sg_zero(void*, int64_t, hipStream_t);
+void sg_conv_dgrad_bn(const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int,
+                      int, int, int, int, float, void*, void*, const void*, const void*, const void*, const void*,
+                      const void*, hipStream_t);
+void sg_bn_bwd_from_ws(const void*, const void*, const void*, const void*, const void*, const void*, const void*,
+                       const void*, const void*, int, void*, void*, void*, void*, void*, int64_t, int, int, int,
+                       hipStream_t);
 void sg_conv_dgrad(const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int, int,
                    int, int, int, float, void*, hipStream_t);
 void sg_conv_wgrad(const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int, int,
@@ -261,6 +267,20 @@ PYBIND11_MODULE(_C, m) {
                          int sh, int sw, int ph, int pw, int dh, int dw, int splits, P s) {
     sg_conv_wgrad(CV(x), CV(dy), V(dw_out), N, H, W, C, K, R, Sd, Ho, Wo, sh, sw, ph, pw, dh, dw, splits, S(s));
     CHK("conv_wgrad");
+  });
+  // dgrad whose epilogue also sums the producer BN(+ReLU)'s backward partials into bn_ws [32][2][C]
+  m.def("conv_dgrad_bn", [](P dy, P wt, P dx, int N, int H, int W, int C, int K, int R, int Sd, int Ho, int Wo,
+                            int sh, int sw, int ph, int pw, int dh, int dw, P wtbuf, P bn_ws, P bn_x, P mean,
+                            P invstd, P scale, P shift, P s) {
+    sg_conv_dgrad_bn(CV(dy), CV(wt), V(dx), N, H, W, C, K, R, Sd, Ho, Wo, sh, sw, ph, pw, dh, dw, 0, 0.f, V(wtbuf),
+                     V(bn_ws), CV(bn_x), CV(mean), CV(invstd), CV(scale), CV(shift), S(s));
+    CHK("conv_dgrad_bn");
+  });
+  m.def("bn_bwd_from_ws", [](P x, P dy, P y, P scale, P shift, P mean, P invstd, P gamma, P ws, int nb, P coef, P dg,
+                             P db, P dx, P dres, int64_t R, int C, int mask_mode, int dt, P s) {
+    sg_bn_bwd_from_ws(CV(x), CV(dy), CV(y), CV(scale), CV(shift), CV(mean), CV(invstd), CV(gamma), CV(ws), nb, V(coef),
+                      V(dg), V(db), V(dx), V(dres), R, C, mask_mode, dt, S(s));
+    CHK("bn_bwd_from_ws");
   });
   m.def("set_ws_prezeroed", [](int on) { sg_set_ws_prezeroed(on); });
   m.def("zero", [](P p, int64_t bytes, P s) { sg_zero(V(p), bytes, S(s)); CHK("zero"); });

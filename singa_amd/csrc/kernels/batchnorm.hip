@@ -538,4 +538,20 @@ void sg_bn_bwd(const void* x, const void* dy, const void* y, const void* scale, 
                                                       C, mask_mode)));
 }
 
+// BN backward whose reduction was fused into the producing conv dgrad's
+// epilogue (sums in ws [nb][2][C]): finalize + apply only.
+void sg_bn_bwd_from_ws(const void* x, const void* dy, const void* y, const void* scale, const void* shift,
+                       const void* mean, const void* invstd, const void* gamma, const void* ws, int nb, void* coef,
+                       void* dg, void* db, void* dx, void* dres, int64_t R, int C, int mask_mode, int dtype,
+                       hipStream_t s) {
+  hipLaunchKernelGGL(bn_bwd_finalize_k, fin_grid(C), dim3(256), 0, s, (const float*)ws, nb, C, (const float*)gamma,
+                     (const float*)mean, (const float*)invstd, (float*)coef, (float*)dg, (float*)db, (float)R);
+  const int V = (C % 8 == 0) ? 8 : 1;
+  dim3 ag = apply_grid(R, C, V);
+  DISPATCH_FT(dtype, DISPATCH_V(V, hipLaunchKernelGGL((bn_bwd_apply_k<T, VV>), ag, dim3(256), 0, s, (const T*)x,
+                                                      (const T*)dy, (const T*)y, (const float*)scale,
+                                                      (const float*)shift, (const float*)coef, (T*)dx, (T*)dres, R,
+                                                      C, mask_mode)));
+}
+
 }  // extern "C"

@@ -91,6 +91,12 @@ struct GemmArgs {
   float* stats;        // optional BN statistics of the bf16 output: ws[row][2][N] (sum, sum of squares)
   int stats_det;       // 1: row = tile row, plain stores (deterministic); 0: row = tile row % 32, atomics
   int xcd_split;       // split-K: K-slice-major XCD mapping (gridDim.z % 8 == 0, gridDim.y == 1)
+  // stats_mode 1 (dgrad feeding a BN(+ReLU) backward): with g = out * [x*scale+shift > 0]
+  // and xhat = (x - mean) * invstd, the epilogue sums (g, g*xhat) per channel
+  // into `stats` -- the BN backward's reduction pass, fused
+  int stats_mode;
+  const bf16* bnb_x;
+  const float *bnb_mean, *bnb_invstd, *bnb_scale, *bnb_shift;
   ConvGeom g;
 };
 
@@ -569,29 +575,62 @@ __global__ void __launch_bounds__(NT, 2) igemm_k(const GemmArgs p) {
       float st_s[8], st_q[8];
 #pragma unroll
       for (int r = 0; r < 8; ++r) { st_s[r] = 0.f; st_q[r] = 0.f; }
-      if (n < p.N) {
+      float bmu[8], bis[8], bsc[8], bsf[8];
+      if (p.stats && p.stats_mode == 1 && n < p.N) {
 #pragma unroll
-        for (int pass = 0; pass < BM / RPP; ++pass) {
-          const int ml = r0 + pass * RPP;
-          const int m = m0 + ml;
-          if (m >= M) continue;
-          int64_t rowoff;
+        for (int r = 0; r < 8; ++r) {
+          bmu[r] = p.bnb_mean[n + r]; bis[r] = p.bnb_invstd[n + r];
+          bsc[r] = p.bnb_scale[n + r]; bsf[r] = p.bnb_shift[n + r];
+        }
+      }
+      if (n < p.N) {
+        // Row offsets, then every global READ of the epilogue (the beta*C
+        // accumulate source, the fused BN-backward input x) issued up front:
+        // inside the store loop the compiler cannot hoist them above the
+        // previous rows' stores (possible aliasing), which serialised one
+        // full memory latency per row.
+        constexpr int NPS = BM / RPP;
+        int64_t rofs[NPS];
+        bool rok[NPS];
+#pragma unroll
+        for (int pass = 0; pass < NPS; ++pass) {
+          const int m = m0 + r0 + pass * RPP;
+          rok[pass] = m < M;
+          const int mm = rok[pass] ? m : 0;
           if (p.out_phase) {
             const ConvGeom& g = p.g;
-            const int nn = P.dHpWp.div(m);
-            const int rem = m - nn * P.Hp * P.Wp;
+            const int nn = P.dHpWp.div(mm);
+            const int rem = mm - nn * P.Hp * P.Wp;
             const int hh = P.dWp.div(rem);
             const int ww = rem - hh * P.Wp;
-            rowoff = (((int64_t)nn * g.H + P.a + g.sh * hh) * g.W + P.b + g.sw * ww) * p.ldc;
+            rofs[pass] = (((int64_t)nn * g.H + P.a + g.sh * hh) * g.W + P.b + g.sw * ww) * p.ldc;
           } else {
-            rowoff = (int64_t)m * p.ldc;
+            rofs[pass] = (int64_t)mm * p.ldc;
           }
+        }
+        const bool bnb = p.stats && p.stats_mode == 1;
+        bf16x8 pre[NPS];
+        if (bnb || p.beta != 0.f) {
+          const bf16* src = bnb ? p.bnb_x : (const bf16*)pc;
+#pragma unroll
+          for (int pass = 0; pass < NPS; ++pass) pre[pass] = *(const bf16x8*)(src + rofs[pass] + n);
+        }
+        bf16x8 pold[NPS];
+        if (bnb && p.beta != 0.f) {
+#pragma unroll
+          for (int pass = 0; pass < NPS; ++pass) pold[pass] = *(const bf16x8*)((const bf16*)pc + rofs[pass] + n);
+        }
+#pragma unroll
+        for (int pass = 0; pass < NPS; ++pass) {
+          const int ml = r0 + pass * RPP;
+          if (!rok[pass]) continue;
+          const int64_t rowoff = rofs[pass];
           const float4 a = *(const float4*)(tile + ml * LDT + ch * 8);
           const float4 b = *(const float4*)(tile + ml * LDT + ch * 8 + 4);
           float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
           bf16* c = (bf16*)pc + rowoff + n;
           if (p.beta != 0.f) {
-            const bf16x8 old = *(const bf16x8*)c;
+            const bf16x8 old = bnb ? pold[pass] : pre[pass];
 #pragma unroll
             for (int r = 0; r < 8; ++r) v[r] += p.beta * (float)old[r];
           }
@@ -599,7 +638,16 @@ __global__ void __launch_bounds__(NT, 2) igemm_k(const GemmArgs p) {
 #pragma unroll
           for (int r = 0; r < 8; ++r) o[r] = (bf16)(p.relu ? fmaxf(v[r], 0.f) : v[r]);
           *(bf16x8*)c = o;
-          if (p.stats) {
+          if (bnb) {
+            const bf16x8 xb = pre[pass];
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+              const float xf = (float)xb[r];
+              const float gr = xf * bsc[r] + bsf[r] > 0.f ? (float)o[r] : 0.f;
+              st_s[r] += gr;
+              st_q[r] += gr * (xf - bmu[r]) * bis[r];
+            }
+          } else if (p.stats) {
 #pragma unroll
             for (int r = 0; r < 8; ++r) {
               const float f = (float)o[r];
@@ -955,10 +1003,35 @@ void sg_conv_fwd(const void* x, const void* w, void* y, const void* bias, int N,
 // summed in the epilogue instead of by a separate add pass; phases without
 // taps then leave beta*dx).  wt (optional, K*R*S*C bf16 scratch, used when
 // K % 64 == 0): the weights are transposed into it and read K-major.
+void sg_conv_dgrad_bn(const void* dy, const void* w, void* dx, int N, int H, int W, int C, int K, int R, int S,
+                      int Ho, int Wo, int sh, int sw, int ph, int pw, int dh, int dw, int out_mode, float beta,
+                      void* wt, void* bn_ws, const void* bn_x, const void* bn_mean, const void* bn_invstd,
+                      const void* bn_scale, const void* bn_shift, hipStream_t s);
+
 void sg_conv_dgrad(const void* dy, const void* w, void* dx, int N, int H, int W, int C, int K, int R, int S, int Ho,
                    int Wo, int sh, int sw, int ph, int pw, int dh, int dw, int out_mode, float beta, void* wt,
                    hipStream_t s) {
+  sg_conv_dgrad_bn(dy, w, dx, N, H, W, C, K, R, S, Ho, Wo, sh, sw, ph, pw, dh, dw, out_mode, beta, wt, nullptr,
+                   nullptr, nullptr, nullptr, nullptr, nullptr, s);
+}
+
+// As sg_conv_dgrad; with bn_ws != nullptr (bf16 out, beta == 0, C % 8 == 0,
+// non-deterministic mode) the epilogue also writes the BatchNorm(+ReLU)
+// backward partial sums of the producer BN into 32 atomic slot rows
+// bn_ws[32][2][C] (zeroed here unless the one-shot pre-zeroed flag is set).
+void sg_conv_dgrad_bn(const void* dy, const void* w, void* dx, int N, int H, int W, int C, int K, int R, int S,
+                      int Ho, int Wo, int sh, int sw, int ph, int pw, int dh, int dw, int out_mode, float beta,
+                      void* wt, void* bn_ws, const void* bn_x, const void* bn_mean, const void* bn_invstd,
+                      const void* bn_scale, const void* bn_shift, hipStream_t s) {
   GemmArgs p{};
+  if (bn_ws && out_mode == OUT_BF16 && beta == 0.f && (C & 7) == 0 && g_tune[1] && !sg_bn_deterministic()) {
+    p.stats = (float*)bn_ws;
+    p.stats_mode = 1;
+    p.bnb_x = (const bf16*)bn_x;
+    p.bnb_mean = (const float*)bn_mean; p.bnb_invstd = (const float*)bn_invstd;
+    p.bnb_scale = (const float*)bn_scale; p.bnb_shift = (const float*)bn_shift;
+    if (!sg_ws_prezeroed()) sg_zero_async(bn_ws, sizeof(float) * 32 * 2 * C, s);
+  }
   p.g = make_geom(N, H, W, C, K, R, S, Ho, Wo, sh, sw, ph, pw, dh, dw);
   const int np = make_phases(p.g);
   int Mmax = 0;

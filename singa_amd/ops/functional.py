@@ -495,16 +495,23 @@ def conv2d_fwd(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], stri
 # (ds_read_b128 fragments like the forward) instead of transposing them
 # through LDS (ds_read_b64_tr_b16); switchable for A/B measurements
 DGRAD_KMAJOR = os.environ.get("SINGA_AMD_DGRAD_KMAJOR", "1") != "0"
+# a conv dgrad whose input came from a BN+ReLU sums that BN backward's
+# partials in its epilogue (switchable for A/B tests)
+FUSE_BN_BWD_STATS = os.environ.get("SINGA_AMD_FUSE_BN_BWD", "1") != "0"
 
 
 def conv2d_bwd(x: torch.Tensor, w: torch.Tensor, dy: torch.Tensor, stride, padding, dilation=(1, 1), groups=1,
                need_dx=True, dw_out: Optional[torch.Tensor] = None, need_db=False,
-               dx_acc: Optional[torch.Tensor] = None):
+               dx_acc: Optional[torch.Tensor] = None, bn_producer=None):
     """Returns (dx, dw, db).  If dw_out (fp32, same logical shape as w) is given
     the weight gradient is ACCUMULATED into it (flat grad buffer views).
     ``dx_acc``: an existing gradient of x (another consumer's contribution);
     when its layout allows, the data gradient is added into it in the dgrad
-    epilogue and ``dx_acc`` itself is returned as dx."""
+    epilogue and ``dx_acc`` itself is returned as dx.
+    ``bn_producer`` = (x_bn, BNState): x is the output of a training-mode
+    BatchNorm+ReLU (no residual) whose pre-BN input is x_bn; the dgrad
+    epilogue then also sums that BN backward's per-channel partials and
+    attaches them to dx (``dx._sg_bnbwd_ws``) so its reduction pass is skipped."""
     sh, sw = stride
     ph, pw = padding
     dh, dw_ = dilation
@@ -539,6 +546,20 @@ def conv2d_bwd(x: torch.Tensor, w: torch.Tensor, dy: torch.Tensor, stride, paddi
                 N.lib().conv_dgrad_acc(dyb.data_ptr(), wb.data_ptr(), dx_acc.data_ptr(), Nn, H, W, Cp, Kp, R, S, Ho,
                                        Wo, sh, sw, ph, pw, dh, dw_, om, 1.0, N.stream(), N.ptr(wt))
                 dx = dx_acc
+            elif (bn_producer is not None and FUSE_BN_BWD_STATS and od == torch.bfloat16 and Cx == Cp and C % 8 == 0
+                  and not N.lib().deterministic() and bn_producer[0].dtype == torch.bfloat16
+                  and tuple(bn_producer[0].shape) == tuple(x.shape) and N.is_cl(bn_producer[0])
+                  and bn_producer[0].is_contiguous(memory_format=torch.channels_last)):
+                xbn, bst = bn_producer
+                dxp = torch.empty((Nn, Cp, H, W), dtype=od, device=x.device, memory_format=torch.channels_last)
+                bws = zeroed_ws(32 * 2 * C, x.device)
+                N.lib().conv_dgrad_bn(dyb.data_ptr(), wb.data_ptr(), dxp.data_ptr(), Nn, H, W, Cp, Kp, R, S, Ho, Wo,
+                                      sh, sw, ph, pw, dh, dw_, N.ptr(wt), bws.data_ptr(), xbn.data_ptr(),
+                                      bst.mean.data_ptr(), bst.invstd.data_ptr(), bst.scale.data_ptr(),
+                                      bst.shift.data_ptr(), N.stream())
+                dxp._sg_bnbwd_ws = (bws, 32)
+                dxp._sg_fresh = True
+                dx = dxp
             else:
                 dxp = torch.empty((Nn, Cp, H, W), dtype=od, device=x.device, memory_format=torch.channels_last)
                 N.lib().conv_dgrad_acc(dyb.data_ptr(), wb.data_ptr(), dxp.data_ptr(), Nn, H, W, Cp, Kp, R, S, Ho, Wo,
@@ -611,6 +632,7 @@ class _ZeroArena:
         self.off = 0
         self.hwm = 0
         self.active = False
+        self.hits = self.misses = 0  # of the current / last step
 
     def begin(self, device) -> None:
         if not N.available() or device.type != "cuda" or N.lib().deterministic():
@@ -621,6 +643,7 @@ class _ZeroArena:
             self.buf = torch.empty(self.hwm + self.hwm // 8 + 1024, dtype=torch.float32, device=device)
         self.off = 0
         self.active = True
+        self.hits = self.misses = 0
         if self.buf is not None:
             N.lib().zero(self.buf.data_ptr(), self.buf.numel() * 4, N.stream())
 
@@ -630,11 +653,13 @@ class _ZeroArena:
             return None
         n = (n + 63) // 64 * 64
         end = self.off + n
+        self.off = end  # advances on a miss too: the next begin() sizes for the whole step
         self.hwm = max(self.hwm, end)
         if self.buf is None or end > self.buf.numel() or self.buf.device != device:
+            self.misses += 1
             return None
-        t = self.buf[self.off:end]
-        self.off = end
+        t = self.buf[end - n:end]
+        self.hits += 1
         return t
 
     def end(self) -> None:
@@ -788,6 +813,14 @@ def batchnorm_bwd(x: torch.Tensor, dy: torch.Tensor, gamma: torch.Tensor, st: BN
         coef = torch.empty(3 * C, dtype=torch.float32, device=x.device)
         dx = _like(x)
         dres = _like(x) if need_dres else None
+        pre = getattr(dy, "_sg_bnbwd_ws", None)  # partial sums from the consuming conv's dgrad epilogue
+        if pre is not None and mode == 2 and not need_dres:
+            L.bn_bwd_from_ws(x.data_ptr(), dy.data_ptr(), 0, st.scale.data_ptr(), st.shift.data_ptr(),
+                             st.mean.data_ptr(), st.invstd.data_ptr(), gamma.data_ptr(), pre[0].data_ptr(), pre[1],
+                             coef.data_ptr(), dg.data_ptr(), db.data_ptr(), dx.data_ptr(), 0, R, C, mode, N.dt(x),
+                             N.stream())
+            dx._sg_fresh = True
+            return dx, dg, db, None
         L.bn_bwd(x.data_ptr(), dy.data_ptr(), N.ptr(ym), st.scale.data_ptr(), st.shift.data_ptr(),
                  st.mean.data_ptr(), st.invstd.data_ptr(), gamma.data_ptr(), _ws(R, C, x.device).data_ptr(),
                  coef.data_ptr(), dg.data_ptr(), db.data_ptr(), dx.data_ptr(), N.ptr(dres), R, C, mode, N.dt(x),

@@ -217,8 +217,9 @@ def test_stacked_bottlenecks_inplace_grad_accumulation(gpu):
     """Three stacked bottlenecks (down-sampling, strided down-sampling,
     identity): the gradient at each block input is the sum of the residual
     path and the conv1 data gradient, which the engine adds IN PLACE in the
-    conv dgrad epilogue (autograd.ACC_INPLACE).  A/B against the same step
-    with separate add passes (autograd.INPLACE_ACC = False): every parameter
+    conv dgrad epilogue (autograd.ACC_INPLACE); bn1/bn2's backward reductions
+    are summed in the epilogues of conv2/conv3's dgrad.  A/B against the same
+    step with separate add and reduction passes: every parameter
     gradient must agree to bf16 rounding; plus a loose sanity check against a
     PyTorch fp32 reference (three stacked bf16 blocks flip some ReLU masks)."""
     import torch.nn.functional as TF
@@ -236,9 +237,12 @@ def test_stacked_bottlenecks_inplace_grad_accumulation(gpu):
                stores_grad=False)
     dyt = None
 
+    from singa_amd.ops import functional as FF
+
     def run(inplace):
         nonlocal dyt
         AG.INPLACE_ACC = inplace
+        FF.FUSE_BN_BWD_STATS = inplace  # the BN-backward reduction fused into the conv dgrad epilogue
         AG.training = True
         try:
             h = x
@@ -252,6 +256,7 @@ def test_stacked_bottlenecks_inplace_grad_accumulation(gpu):
         finally:
             AG.training = False
             AG.INPLACE_ACC = True
+            FF.FUSE_BN_BWD_STATS = True
         return h, gr
 
     h, grads = run(True)

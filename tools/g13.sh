@@ -1,0 +1,3 @@
+tools/gpu_step.sh \
+ "400 kt13.log python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider" \
+ "300 bench13.log python bench.py --steps 20 --warmup 5"
