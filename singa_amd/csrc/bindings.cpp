@@ -84,6 +84,7 @@ void sg_conv_dgrad(const void*, const void*, void*, int, int, int, int, int, int
 void sg_conv_wgrad(const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int, int,
                    int, int, int, hipStream_t);
 void sg_set_tuning(int key, int value);
+void sg_bn_set_unroll(int);
 }
 
 static void check_launch(const char* what) {
@@ -285,4 +286,5 @@ PYBIND11_MODULE(_C, m) {
   m.def("set_ws_prezeroed", [](int on) { sg_set_ws_prezeroed(on); });
   m.def("zero", [](P p, int64_t bytes, P s) { sg_zero(V(p), bytes, S(s)); CHK("zero"); });
   m.def("set_tuning", [](int key, int value) { sg_set_tuning(key, value); });
+  m.def("bn_set_unroll", [](int ur) { sg_bn_set_unroll(ur); });
 }

@@ -289,8 +289,30 @@ __global__ void bn_infer_params_k(const float* __restrict__ gamma, const float* 
   if (invstd) invstd[c] = is;
 }
 
-// y = act(x*scale + shift + res)
+// y = act(x*scale + shift + res).  UR rows (stride = grid row step) are
+// loaded before any is stored, so each thread keeps UR (x2 with a residual)
+// 16-byte loads in flight: the kernel is HBM-bound and one load per thread
+// per iteration leaves the memory pipeline half idle.
 template <typename T, int V>
+__device__ __forceinline__ void bn_apply_row(const float* v0, const float* rv, const float* sc, const float* sf,
+                                             T* y, uint8_t* mask, int64_t o, int relu) {
+  float v[V];
+#pragma unroll
+  for (int k = 0; k < V; ++k) v[k] = v0[k] * sc[k] + sf[k] + (rv ? rv[k] : 0.f);
+  if (relu) {
+#pragma unroll
+    for (int k = 0; k < V; ++k) v[k] = fmaxf(v[k], 0.f);
+  }
+  stv<T, V>(y + o, v);
+  if (V == 8 && mask) {  // bit k = (stored output of channel c0+k) > 0
+    unsigned b = 0;
+#pragma unroll
+    for (int k = 0; k < V; ++k) b |= ((float)(T)v[k] > 0.f ? 1u : 0u) << k;
+    mask[o >> 3] = (uint8_t)b;
+  }
+}
+
+template <typename T, int V, int UR>
 __global__ void __launch_bounds__(256) bn_apply_k(const T* __restrict__ x, const float* __restrict__ scale,
                                                   const float* __restrict__ shift, const T* __restrict__ res,
                                                   T* __restrict__ y, uint8_t* __restrict__ mask, int64_t R, int C,
@@ -301,34 +323,61 @@ __global__ void __launch_bounds__(256) bn_apply_k(const T* __restrict__ x, const
   ldc<V>(scale + t.c0, sc);
   ldc<V>(shift + t.c0, sf);
   const int64_t step = (int64_t)t.RT * gridDim.x;
-  for (int64_t r = (int64_t)blockIdx.x * t.RT + t.ty; r < R; r += step) {
-    float v[V];
+  int64_t r = (int64_t)blockIdx.x * t.RT + t.ty;
+  for (; r + (UR - 1) * step < R; r += UR * step) {
+    float v[UR][V], rv[UR][V];
+#pragma unroll
+    for (int u = 0; u < UR; ++u) ldv<T, V>(x + (r + u * step) * C + t.c0, v[u]);
+    if (res) {
+#pragma unroll
+      for (int u = 0; u < UR; ++u) ldv<T, V>(res + (r + u * step) * C + t.c0, rv[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < UR; ++u)
+      bn_apply_row<T, V>(v[u], res ? rv[u] : nullptr, sc, sf, y, mask, (r + u * step) * C + t.c0, relu);
+  }
+  for (; r < R; r += step) {
+    float v[V], rv[V];
     const int64_t o = r * C + t.c0;
     ldv<T, V>(x + o, v);
-#pragma unroll
-    for (int k = 0; k < V; ++k) v[k] = v[k] * sc[k] + sf[k];
-    if (res) {
-      float rv[V];
-      ldv<T, V>(res + o, rv);
-#pragma unroll
-      for (int k = 0; k < V; ++k) v[k] += rv[k];
-    }
-    if (relu) {
-#pragma unroll
-      for (int k = 0; k < V; ++k) v[k] = fmaxf(v[k], 0.f);
-    }
-    stv<T, V>(y + o, v);
-    if (V == 8 && mask) {  // bit k = (stored output of channel c0+k) > 0
-      unsigned b = 0;
-#pragma unroll
-      for (int k = 0; k < V; ++k) b |= ((float)(T)v[k] > 0.f ? 1u : 0u) << k;
-      mask[o >> 3] = (uint8_t)b;
-    }
+    if (res) ldv<T, V>(res + o, rv);
+    bn_apply_row<T, V>(v, res ? rv : nullptr, sc, sf, y, mask, o, relu);
   }
 }
 
-// g = mask(dy); dx = k*g + b*x + a; dres = g (residual branch)
+// g = mask(dy); dx = k*g + b*x + a; dres = g (residual branch).  UR rows
+// are loaded before any is stored (see bn_apply_k).
 template <typename T, int V>
+__device__ __forceinline__ void bn_bwd_load(const T* x, const T* dy, const T* y, int64_t o, int mask_mode, float* v,
+                                            float* g, float* yy, unsigned& mb) {
+  ldv<T, V>(x + o, v);
+  ldv<T, V>(dy + o, g);
+  if (mask_mode == MASK_Y) ldv<T, V>(y + o, yy);
+  else if (V == 8 && mask_mode == MASK_BITS) mb = ((const uint8_t*)y)[o >> 3];
+}
+
+template <typename T, int V>
+__device__ __forceinline__ void bn_bwd_row(const float* v, float* g, const float* yy, unsigned mb, const float* kk,
+                                           const float* bb, const float* aa, const float* sc, const float* sf,
+                                           T* dx, T* dres, int64_t o, int mask_mode) {
+  if (mask_mode == MASK_Y) {
+#pragma unroll
+    for (int k = 0; k < V; ++k) g[k] = yy[k] > 0.f ? g[k] : 0.f;
+  } else if (V == 8 && mask_mode == MASK_BITS) {
+#pragma unroll
+    for (int k = 0; k < V; ++k) g[k] = (mb >> k) & 1u ? g[k] : 0.f;
+  } else if (mask_mode == MASK_AFFINE) {
+#pragma unroll
+    for (int k = 0; k < V; ++k) g[k] = v[k] * sc[k] + sf[k] > 0.f ? g[k] : 0.f;
+  }
+  if (dres) stv<T, V>(dres + o, g);
+  float o8[V];
+#pragma unroll
+  for (int k = 0; k < V; ++k) o8[k] = kk[k] * g[k] + bb[k] * v[k] + aa[k];
+  stv<T, V>(dx + o, o8);
+}
+
+template <typename T, int V, int UR>
 __global__ void __launch_bounds__(256) bn_bwd_apply_k(const T* __restrict__ x, const T* __restrict__ dy,
                                                       const T* __restrict__ y, const float* __restrict__ scale,
                                                       const float* __restrict__ shift,
@@ -345,29 +394,22 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_k(const T* __restrict__ x, c
     ldc<V>(shift + t.c0, sf);
   }
   const int64_t step = (int64_t)t.RT * gridDim.x;
-  for (int64_t r = (int64_t)blockIdx.x * t.RT + t.ty; r < R; r += step) {
+  int64_t r = (int64_t)blockIdx.x * t.RT + t.ty;
+  for (; r + (UR - 1) * step < R; r += UR * step) {
+    float v[UR][V], g[UR][V], yy[UR][V];
+    unsigned mb[UR] = {};
+#pragma unroll
+    for (int u = 0; u < UR; ++u) bn_bwd_load<T, V>(x, dy, y, (r + u * step) * C + t.c0, mask_mode, v[u], g[u], yy[u], mb[u]);
+#pragma unroll
+    for (int u = 0; u < UR; ++u)
+      bn_bwd_row<T, V>(v[u], g[u], yy[u], mb[u], kk, bb, aa, sc, sf, dx, dres, (r + u * step) * C + t.c0, mask_mode);
+  }
+  for (; r < R; r += step) {
+    float v[V], g[V], yy[V];
+    unsigned mb = 0;
     const int64_t o = r * C + t.c0;
-    float v[V], g[V];
-    ldv<T, V>(x + o, v);
-    ldv<T, V>(dy + o, g);
-    if (mask_mode == MASK_Y) {
-      float yy[V];
-      ldv<T, V>(y + o, yy);
-#pragma unroll
-      for (int k = 0; k < V; ++k) g[k] = yy[k] > 0.f ? g[k] : 0.f;
-    } else if (V == 8 && mask_mode == MASK_BITS) {
-      const unsigned mb = ((const uint8_t*)y)[o >> 3];
-#pragma unroll
-      for (int k = 0; k < V; ++k) g[k] = (mb >> k) & 1u ? g[k] : 0.f;
-    } else if (mask_mode == MASK_AFFINE) {
-#pragma unroll
-      for (int k = 0; k < V; ++k) g[k] = v[k] * sc[k] + sf[k] > 0.f ? g[k] : 0.f;
-    }
-    if (dres) stv<T, V>(dres + o, g);
-    float o8[V];
-#pragma unroll
-    for (int k = 0; k < V; ++k) o8[k] = kk[k] * g[k] + bb[k] * v[k] + aa[k];
-    stv<T, V>(dx + o, o8);
+    bn_bwd_load<T, V>(x, dy, y, o, mask_mode, v, g, yy, mb);
+    bn_bwd_row<T, V>(v, g, yy, mb, kk, bb, aa, sc, sf, dx, dres, o, mask_mode);
   }
 }
 
@@ -395,6 +437,20 @@ extern "C" int64_t sg_colreduce_ws(int64_t R, int C) {
   return (int64_t)(g_bn_det ? sg_colreduce_bands(R, C) : NSLOT) * 2 * C;
 }
 extern "C" void sg_bn_set_deterministic(int on) { g_bn_det = on; }
+// Rows per iteration of the HBM-bound apply kernels (1, 2 or 4; 0 = the
+// measured default: 1 for the forward, 2 for the backward apply).
+// tools/bench_bn.py on MI355X (profiles/bn_apply_bandwidth_b512.jsonl): both
+// run at 90-100% of a torch copy's bandwidth (4.5-6.3 TB/s) already with one
+// row in flight; deeper unrolls only add VGPR pressure.
+static int g_bn_ur = 0;
+extern "C" void sg_bn_set_unroll(int ur) { g_bn_ur = (ur == 1 || ur == 2 || ur == 4) ? ur : 0; }
+#define BN_UR_LAUNCH(K, UR0, T_, V_, ...)                                                   \
+  do {                                                                                     \
+    const int ur_ = g_bn_ur ? g_bn_ur : (UR0);                                              \
+    if (ur_ == 4) hipLaunchKernelGGL((K<T_, V_, 4>), __VA_ARGS__);                         \
+    else if (ur_ == 1) hipLaunchKernelGGL((K<T_, V_, 1>), __VA_ARGS__);                    \
+    else hipLaunchKernelGGL((K<T_, V_, 2>), __VA_ARGS__);                                  \
+  } while (0)
 // The next launch that owns a slot-atomic workspace finds it pre-zeroed
 // (one-shot flag: consumed by that launch)
 extern "C" void sg_set_ws_prezeroed(int on) { g_ws_prezeroed = on; }
@@ -509,7 +565,7 @@ void sg_bn_apply(const void* x, const void* scale, const void* shift, const void
                  int C, int relu, int dtype, hipStream_t s) {
   const int V = (C % 8 == 0) ? 8 : 1;
   dim3 grid = apply_grid(R, C, V);
-  DISPATCH_FT(dtype, DISPATCH_V(V, hipLaunchKernelGGL((bn_apply_k<T, VV>), grid, dim3(256), 0, s, (const T*)x,
+  DISPATCH_FT(dtype, DISPATCH_V(V, BN_UR_LAUNCH(bn_apply_k, 1, T, VV, grid, dim3(256), 0, s, (const T*)x,
                                                       (const float*)scale, (const float*)shift, (const T*)res, (T*)y,
                                                       (uint8_t*)mask, R, C, relu)));
 }
@@ -532,7 +588,7 @@ void sg_bn_bwd(const void* x, const void* dy, const void* y, const void* scale, 
                      (const float*)gamma, (const float*)mean, (const float*)invstd, (float*)coef, (float*)dg,
                      (float*)db, (float)R);
   dim3 ag = apply_grid(R, C, V);
-  DISPATCH_FT(dtype, DISPATCH_V(V, hipLaunchKernelGGL((bn_bwd_apply_k<T, VV>), ag, dim3(256), 0, s, (const T*)x,
+  DISPATCH_FT(dtype, DISPATCH_V(V, BN_UR_LAUNCH(bn_bwd_apply_k, 2, T, VV, ag, dim3(256), 0, s, (const T*)x,
                                                       (const T*)dy, (const T*)y, (const float*)scale,
                                                       (const float*)shift, (const float*)coef, (T*)dx, (T*)dres, R,
                                                       C, mask_mode)));
@@ -548,7 +604,7 @@ void sg_bn_bwd_from_ws(const void* x, const void* dy, const void* y, const void*
                      (const float*)mean, (const float*)invstd, (float*)coef, (float*)dg, (float*)db, (float)R);
   const int V = (C % 8 == 0) ? 8 : 1;
   dim3 ag = apply_grid(R, C, V);
-  DISPATCH_FT(dtype, DISPATCH_V(V, hipLaunchKernelGGL((bn_bwd_apply_k<T, VV>), ag, dim3(256), 0, s, (const T*)x,
+  DISPATCH_FT(dtype, DISPATCH_V(V, BN_UR_LAUNCH(bn_bwd_apply_k, 2, T, VV, ag, dim3(256), 0, s, (const T*)x,
                                                       (const T*)dy, (const T*)y, (const float*)scale,
                                                       (const float*)shift, (const float*)coef, (T*)dx, (T*)dres, R,
                                                       C, mask_mode)));
