@@ -213,6 +213,22 @@ class SyntheticDataLayer(_DataLayerBase):
 
 @register("kMnistImage")
 class MnistImageLayer(RefLayer):
+    """MNIST parser: ``x / norm_a - norm_b`` (optionally resized), plus the
+    training-time deformations that ``MnistProto`` describes.  The reference
+    parses the fields but leaves the transform commented out
+    (``src/worker/layer.cc:405-436``); this implements the intent, batched on
+    the layer's device with one ``grid_sample``:
+
+    * ``gamma`` — per-axis scaling by ``1 + r*gamma/100``, ``r ~ U(-1, 1)``;
+    * ``beta``  — per image, either a rotation by ``r*beta`` degrees or a
+      horizontal shear ``r*beta/90`` (halved for the digits 1 and 7);
+    * ``kernel``/``sigma``/``alpha`` — elastic distortion (Simard et al.):
+      uniform random displacement fields smoothed by a ``kernel``-wide
+      Gaussian of std ``sigma`` and scaled to ``alpha`` pixels, applied to
+      every ``elastic_freq``-th batch (every batch when 0).
+
+    All fields default to 0, i.e. no augmentation, as in the reference.
+    """
     is_parser = True
 
     def setup(self, src_shapes, dev, gen=None):
@@ -220,10 +236,63 @@ class MnistImageLayer(RefLayer):
         mp = self.proto.mnist_param
         self.norm_a, self.norm_b = mp.norm_a or 1.0, mp.norm_b
         self.resize = mp.resize
+        self.gamma, self.beta = float(mp.gamma), float(mp.beta)
+        self.kernel, self.sigma, self.alpha = int(mp.kernel), float(mp.sigma), float(mp.alpha)
+        self.elastic_freq = int(mp.elastic_freq)
+        self.nbatch = 0
+        self.gen = torch.Generator().manual_seed(0)
         B = src_shapes[0][0]
         s = src_shapes[0][1:]
         self.shape = (B, self.resize, self.resize) if self.resize else (B,) + tuple(s)
         return self.shape
+
+    def _rand(self, *shape):
+        return (torch.rand(*shape, generator=self.gen) * 2 - 1)
+
+    def _deform(self, img, label):
+        """img [B, H, W] float -> deformed [B, H, W] (bilinear, zero fill)."""
+        B, H, W = img.shape
+        use_affine = self.gamma > 0 or self.beta > 0
+        use_elastic = self.alpha > 0 and self.kernel > 0 and self.sigma > 0 and \
+            (self.elastic_freq <= 0 or self.nbatch % self.elastic_freq == 0)
+        if not (use_affine or use_elastic):
+            return img
+        theta = torch.zeros(B, 2, 3)
+        theta[:, 0, 0] = theta[:, 1, 1] = 1.0
+        if self.gamma > 0:  # scaling the image by s = sampling coordinates by 1/s
+            theta[:, 0, 0] = 1.0 / (1.0 + self._rand(B) * self.gamma / 100.0)
+            theta[:, 1, 1] = 1.0 / (1.0 + self._rand(B) * self.gamma / 100.0)
+        if self.beta > 0:
+            r = self._rand(B)
+            rot = torch.rand(B, generator=self.gen) < 0.5
+            ang = torch.deg2rad(r * self.beta)
+            c, sn = torch.cos(ang), torch.sin(ang)
+            R = torch.zeros(B, 2, 2)
+            R[:, 0, 0], R[:, 0, 1], R[:, 1, 0], R[:, 1, 1] = c, -sn, sn, c
+            sh = r * self.beta / 90.0
+            if label is not None:
+                lab = label.reshape(-1).cpu()
+                sh = torch.where((lab == 1) | (lab == 7), sh / 2, sh)
+            S = torch.eye(2).repeat(B, 1, 1)
+            S[:, 0, 1] = sh
+            A = torch.where(rot[:, None, None], R, S)
+            theta[:, :, :2] = A @ theta[:, :, :2]
+        theta = theta.to(img.device)
+        grid = torch.nn.functional.affine_grid(theta, (B, 1, H, W), align_corners=False)
+        if use_elastic:
+            k = self.kernel | 1
+            ax = torch.arange(k, dtype=torch.float32) - k // 2
+            g1 = torch.exp(-ax ** 2 / (2 * self.sigma ** 2))
+            g1 = (g1 / g1.sum()).to(img.device)
+            d = self._rand(B * 2, 1, H, W).to(img.device)
+            d = torch.nn.functional.conv2d(d, g1.view(1, 1, 1, k), padding=(0, k // 2))
+            d = torch.nn.functional.conv2d(d, g1.view(1, 1, k, 1), padding=(k // 2, 0))
+            d = d.view(B, 2, H, W).permute(0, 2, 3, 1)
+            # alpha pixels -> normalised [-1, 1] grid units
+            grid = grid + d * self.alpha * torch.tensor([2.0 / W, 2.0 / H], device=img.device)
+        out = torch.nn.functional.grid_sample(img[:, None], grid, mode="bilinear", padding_mode="zeros",
+                                              align_corners=False)
+        return out[:, 0]
 
     def forward(self, xs, training):
         img = xs[0]["image"].data.float()
@@ -232,6 +301,10 @@ class MnistImageLayer(RefLayer):
                                                   size=(self.resize, self.resize), mode="bilinear",
                                                   align_corners=False).reshape(img.shape[0], self.resize,
                                                                                self.resize)
+        if training:
+            lab = xs[0].get("label") if isinstance(xs[0], dict) else None
+            img = self._deform(img, lab.data if lab is not None else None)
+            self.nbatch += 1
         return Tensor(device=self.dev, data=img / self.norm_a - self.norm_b, requires_grad=False)
 
 

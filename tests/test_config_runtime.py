@@ -189,3 +189,52 @@ def test_executor_threads_hogwild_trains():
         last = w.train_one_batch(s)
     assert np.isfinite(last).all()
     assert w.updater.step_counter == 30
+
+
+def _mnist_layer(params: str):
+    from singa_amd import device
+    from singa_amd.runtime.layers import create_layer
+    from singa_amd.tensor import Tensor
+    lp = schema.parse_text("LayerProto", 'name: "mnist" type: "kMnistImage" srclayers: "data" '
+                                         'mnist_param { %s }' % params)
+    layer = create_layer(lp)
+    dev = device.get_default_device()
+    layer.setup([(4, 28, 28)], dev)
+    img = torch.zeros(4, 28, 28)
+    img[:, 10:18, 12:16] = 255.0  # a bar ("1")
+    x = {"image": Tensor(device=dev, data=img, requires_grad=False),
+         "label": Tensor(device=dev, data=torch.tensor([1, 7, 3, 4]), requires_grad=False)}
+    return layer, x, img
+
+
+def test_mnist_layer_no_augmentation_is_exact():
+    """All MnistProto deformation fields default to 0: plain x/norm_a - norm_b
+    (reference src/worker/layer.cc:438-444), identical in train and test."""
+    layer, x, img = _mnist_layer("norm_a: 255 norm_b: 0.5")
+    for training in (True, False):
+        out = layer.forward([x], training).data
+        assert torch.allclose(out, img / 255 - 0.5)
+
+
+@pytest.mark.parametrize("params", ["gamma: 15", "beta: 15", "kernel: 5 sigma: 2 alpha: 3",
+                                    "gamma: 10 beta: 10 kernel: 5 sigma: 2 alpha: 3 elastic_freq: 2"])
+def test_mnist_layer_deformations(params):
+    """Scaling / rotation-or-shear / elastic distortion (the intent of the
+    commented-out code at src/worker/layer.cc:405-436): the training output
+    moves pixels but keeps the value range and roughly the ink mass; the
+    test-phase output stays undeformed."""
+    layer, x, img = _mnist_layer("norm_a: 255 " + params)
+    out = layer.forward([x], True).data
+    assert out.shape == img.shape
+    assert not torch.allclose(out, img / 255)
+    assert out.min() >= -1e-5 and out.max() <= 1 + 1e-5
+    mass_in, mass_out = (img / 255).sum((1, 2)), out.sum((1, 2))
+    assert torch.all((mass_out / mass_in - 1).abs() < 0.45)
+    assert torch.allclose(layer.forward([x], False).data, img / 255)
+
+
+def test_mnist_layer_elastic_freq():
+    layer, x, img = _mnist_layer("norm_a: 255 kernel: 5 sigma: 2 alpha: 3 elastic_freq: 2")
+    outs = [layer.forward([x], True).data for _ in range(2)]
+    assert not torch.allclose(outs[0], img / 255)  # batch 0: distorted
+    assert torch.allclose(outs[1], img / 255)      # batch 1: skipped
