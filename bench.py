@@ -32,7 +32,9 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=512, help="per-GPU batch")
+    ap.add_argument("--batch", type=int, default=1024,
+                    help="per-GPU batch (measured on MI355X: 512 -> 10.2k, 768 -> 10.57k, 1024 -> 10.67k img/s; "
+                         "fits easily in 288 GB HBM3E)")
     ap.add_argument("--depth", type=int, default=50)
     ap.add_argument("--image", type=int, default=224)
     ap.add_argument("--graph", dest="graph", action="store_true", default=None,
