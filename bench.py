@@ -11,9 +11,10 @@ update of every parameter.
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
         --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
 
-Weak scaling: per-GPU batch is fixed (default 512: sized for the 288 GB of
-HBM3E per MI355X -- activations take ~60 GB -- and it fills the 256 CUs
-better than 256: measured 9.4k vs 8.75k img/s), global batch = N * 512.
+Weak scaling: per-GPU batch is fixed (default 1024: sized for the 288 GB of
+HBM3E per MI355X -- activations take ~120 GB -- and the larger grids fill the
+256 CUs better: measured 10.2k / 10.57k / 10.67k img/s at 512 / 768 / 1024),
+global batch = N * 1024.
 Rank 0 prints ONE JSON line; value = N * batch * K / max-over-ranks(elapsed).
 """
 from __future__ import annotations

@@ -141,14 +141,20 @@ class Model(layer.Layer):
                     _F.ARENA.end()
             torch.cuda.synchronize()
             g = torch.cuda.CUDAGraph()
+            # one memory pool PER graph: a shared pool would let the eval
+            # graph's static outputs live in blocks the train graph uses for
+            # intermediates, so a train replay would overwrite an eval result
+            # the caller still holds.  (A graph's own outputs stay valid only
+            # until that same graph is replayed again.)
             if self._pool is None:
-                self._pool = torch.cuda.graph_pool_handle()
+                self._pool = {}
+            pool = self._pool.setdefault(key, torch.cuda.graph_pool_handle())
             if opt is not None:
                 getattr(opt, "opt", opt).graph_mode = True
                 opt.prepare_step()
             sc0 = opt.step_counter if opt is not None else 0
             dev = args[0].device
-            with torch.cuda.graph(g, pool=self._pool):
+            with torch.cuda.graph(g, pool=pool):
                 # first captured kernel: advance the device RNG epoch, so
                 # dropout masks differ on every replay (host-side Philox
                 # offsets are frozen into the captured launches)

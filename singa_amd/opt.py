@@ -98,7 +98,7 @@ def _sched(lr) -> DecayScheduler:
 # ---------------------------------------------------------------------------
 class ParamStore:
     def __init__(self, params: Sequence[Tensor], mixed_bf16: bool = False, reverse: bool = True,
-                 state_slots: int = 2):
+                 state_slots: int = 2, channels_last: Optional[bool] = None):
         seen, ps = set(), []
         for p in params:
             if id(p) not in seen:
@@ -109,6 +109,8 @@ class ParamStore:
         dev = self.params[0].data.device
         self.device = dev
         self.gpu = dev.type == "cuda"
+        # flat memory of 4-D weights: [K][R][S][C] for the GPU kernels, [K][C][R][S] on the CPU
+        self.channels_last = self.gpu if channels_last is None else bool(channels_last)
         self.offsets, off = [], 0
         for p in self.params:
             self.offsets.append(off)
@@ -135,7 +137,7 @@ class ParamStore:
     def _view(self, flat: torch.Tensor, off: int, shape) -> torch.Tensor:
         n = int(np.prod(shape)) if len(shape) else 1
         v = flat[off:off + n]
-        if len(shape) == 4 and self.gpu:
+        if len(shape) == 4 and self.channels_last:
             K, C, R, S = shape
             return v.view(K, R, S, C).permute(0, 3, 1, 2)  # logical KCRS, memory KRSC
         return v.view(*shape) if len(shape) else v.view(())
@@ -188,6 +190,29 @@ class ParamStore:
             d["s2"] = self.s2
         return d
 
+    def slot_views(self, flat: torch.Tensor) -> List[torch.Tensor]:
+        """Per-parameter views of a flat buffer of this store's layout, in
+        each parameter's LOGICAL shape (conv weights KCRS whatever the flat
+        memory order is)."""
+        return [self._view(flat, o, p.data.shape) for p, o in zip(self.params, self.offsets)]
+
+    def export_slot(self, flat: torch.Tensor) -> Dict[str, torch.Tensor]:
+        """Device-independent form of an optimiser slot: one logical-layout
+        tensor per parameter (``"<index>"`` in store order).  A flat dump is
+        NOT portable: the GPU store keeps conv weights KRSC, the CPU store
+        KCRS, with the same numel -- a raw copy would scramble them."""
+        return {str(i): v.detach().contiguous().cpu() for i, v in enumerate(self.slot_views(flat))}
+
+    def import_slot(self, flat: torch.Tensor, parts: Dict[str, torch.Tensor]) -> None:
+        views = self.slot_views(flat)
+        if len(parts) != len(views):
+            raise ValueError(f"optimizer slot has {len(parts)} tensors, store has {len(views)} parameters")
+        for i, v in enumerate(views):
+            t = torch.as_tensor(parts[str(i)])
+            if tuple(t.shape) != tuple(v.shape):
+                raise ValueError(f"optimizer slot tensor {i}: shape {tuple(t.shape)} != parameter {tuple(v.shape)}")
+            v.copy_(t.to(device=v.device, dtype=v.dtype))
+
 
 # ---------------------------------------------------------------------------
 _KIND = {"sgd": 0, "nesterov_ref": 1, "adagrad": 2, "rmsprop": 3, "adadelta": 4, "adam": 5, "sgd_ref": 6}
@@ -214,10 +239,11 @@ class Optimizer:
         self._per_param: Dict[int, Dict[str, torch.Tensor]] = {}
 
     # -- configuration -----------------------------------------------------
-    def attach(self, params: Sequence[Tensor], mixed_bf16: bool = False) -> ParamStore:
+    def attach(self, params: Sequence[Tensor], mixed_bf16: bool = False,
+               channels_last: Optional[bool] = None) -> ParamStore:
         self.mixed_bf16 = mixed_bf16
         self.store = ParamStore(params, mixed_bf16=mixed_bf16, state_slots=2 if self.kind in (
-            "adam", "adadelta") else 1)
+            "adam", "adadelta") else 1, channels_last=channels_last)
         dev = self.store.device
         self._hp_dev = torch.zeros(4, dtype=torch.float32, device=dev)
         self._hp_host = torch.zeros(4, dtype=torch.float32, pin_memory=dev.type == "cuda")
@@ -346,20 +372,33 @@ class Optimizer:
 
     # -- checkpoint ----------------------------------------------------------
     def get_states(self) -> Dict[str, object]:
-        d: Dict[str, object] = {"step_counter": self.step_counter, "kind": self.kind}
+        d: Dict[str, object] = {"step_counter": self.step_counter, "kind": self.kind, "slot_layout": "logical"}
         if self.store is not None:
-            if self.store.s1 is not None:
-                d["s1"] = self.store.s1.detach().cpu()
-            if self.store.s2 is not None:
-                d["s2"] = self.store.s2.detach().cpu()
+            for k in ("s1", "s2"):
+                flat = getattr(self.store, k)
+                if flat is not None:
+                    for i, t in self.store.export_slot(flat).items():
+                        d[f"{k}/{i}"] = t
         return d
 
     def set_states(self, states: Dict[str, object]) -> None:
         self.step_counter = int(states.get("step_counter", 0))
         if self.store is not None:
             for k in ("s1", "s2"):
-                if k in states and getattr(self.store, k) is not None:
-                    getattr(self.store, k).copy_(torch.as_tensor(states[k]))
+                flat = getattr(self.store, k)
+                if flat is None:
+                    continue
+                parts = {key[len(k) + 1:]: v for key, v in states.items() if key.startswith(k + "/")}
+                if parts:
+                    self.store.import_slot(flat, parts)
+                elif k in states:
+                    # legacy flat dump (layout of the saving device unknown):
+                    # only safe when saved and loaded on the same kind of device
+                    import warnings
+
+                    warnings.warn(f"optimizer state '{k}' is a legacy flat buffer; restoring it assumes the "
+                                  "checkpoint was written on the same device type")
+                    flat.copy_(torch.as_tensor(states[k]))
         self.prepare_step()
 
 

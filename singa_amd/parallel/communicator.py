@@ -60,6 +60,14 @@ class Communicator:
             return None
         rop = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN,
                "avg": dist.ReduceOp.SUM}[op]
+        if op == "avg" and async_op:
+            # the host-side divide cannot follow an async handle: RCCL has a
+            # native average; gloo does not, so refuse instead of silently
+            # returning the sum
+            if self.backend != "nccl":
+                raise ValueError("all_reduce(op='avg', async_op=True) needs the nccl (RCCL) backend; "
+                                 "use op='sum' and scale, or async_op=False")
+            rop = dist.ReduceOp.AVG
         w = dist.all_reduce(t, op=rop, group=self.group, async_op=async_op)
         if op == "avg" and not async_op:
             t.div_(self.world_size)
@@ -169,6 +177,10 @@ class Communicator:
 
     def stop_heartbeat(self):
         self._hb_stop.set()
+        if self._hb_thread is not None:
+            self._hb_thread.join(timeout=2.0)
+            self._hb_thread = None
+        self._hb_stop = threading.Event()
 
 
 _STORE: dict = {}
@@ -196,9 +208,33 @@ def init_distributed(rank: Optional[int] = None, world_size: Optional[int] = Non
     elif dist.is_initialized():
         ws, rk = dist.get_world_size(), dist.get_rank()
         backend = dist.get_backend()
+    if ws > 1 and "store" not in _STORE:
+        # the rendezvous TCP store of the default group carries the
+        # heartbeats (the reference's Router PING/PONG liveness, X1)
+        st = default_store()
+        if st is not None:
+            _STORE["store"] = st
     c = Communicator(ws, rk, lr, backend)
     _COMM["comm"] = c
     return c
+
+
+def default_store():
+    """The default process group's rendezvous store (None if unavailable).
+    A PrefixStore keeps heartbeat keys out of the group's own namespace."""
+    if not dist.is_initialized():
+        return None
+    try:
+        from torch.distributed import distributed_c10d as c10d
+
+        return dist.PrefixStore("singa_amd", c10d._get_default_store())
+    except Exception:
+        return None
+
+
+def register_store(store) -> None:
+    """Use ``store`` (any torch.distributed Store) for heartbeats."""
+    _STORE["store"] = store
 
 
 def get_communicator() -> Communicator:
@@ -206,4 +242,7 @@ def get_communicator() -> Communicator:
 
 
 def reset():
-    _COMM.clear()
+    c = _COMM.pop("comm", None)
+    if c is not None:
+        c.stop_heartbeat()
+    _STORE.clear()

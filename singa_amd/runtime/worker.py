@@ -105,6 +105,9 @@ class Worker:
         self.history = []
         self.checkpoint_path = ""
         self.checkpoint_every = 0
+        if self.comm.world_size > 1:
+            # liveness through the rendezvous store (no-op if none is registered)
+            self.comm.start_heartbeat()
         self._setup()
 
     # ------------------------------------------------------------------ setup
@@ -179,6 +182,11 @@ class Worker:
             self.rep_grads.append(g)
         gpu = self.dev.torch_device.type == "cuda"
         self.streams = [torch.cuda.Stream(device=self.dev.torch_device) for _ in range(k)] if gpu else None
+        # hogwild updates of the SHARED weights/momentum all run on one
+        # stream: the lock orders the launches, the single stream serialises
+        # the kernels (on per-thread streams they would overlap on the GPU
+        # and race their read-modify-write of w and s1)
+        self.upd_stream = torch.cuda.Stream(device=self.dev.torch_device) if gpu else None
         self._upd_lock = threading.Lock()
 
     # ------------------------------------------------------------- cadence
@@ -211,7 +219,14 @@ class Worker:
                         pass
                 if self.hogwild:
                     with self._upd_lock:
-                        self.updater.update(grad_scale=1.0, g=g)
+                        if self.upd_stream is not None:
+                            mine = self.streams[i]
+                            self.upd_stream.wait_stream(mine)  # this thread's gradient is complete
+                            with torch.cuda.stream(self.upd_stream):
+                                self.updater.update(grad_scale=1.0, g=g)
+                            mine.wait_stream(self.upd_stream)  # g is free to be zeroed again
+                        else:
+                            self.updater.update(grad_scale=1.0, g=g)
                 out[i] = net.metrics()
         except BaseException as e:  # surfaced in the caller
             out[i] = e

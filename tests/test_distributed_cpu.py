@@ -259,6 +259,35 @@ def test_heartbeat_all_alive():
     assert run_ranks(_hb_rank, 2) == [[], []]
 
 
+def _hb_default_store(rank, world, comm):
+    """init_distributed registers the rendezvous store: the heartbeat needs
+    no explicit store argument (it used to silently do nothing)."""
+    import time
+
+    from singa_amd.parallel import communicator
+
+    assert communicator._STORE.get("store") is not None
+    comm.start_heartbeat(period_s=0.1)
+    time.sleep(0.3)
+    comm.barrier()
+    alive = comm.dead_ranks(timeout_s=5.0)
+    comm.stop_heartbeat()
+    # async average is refused on gloo instead of returning a plain sum
+    t = torch.ones(3)
+    try:
+        comm.all_reduce(t, op="avg", async_op=True)
+        refused = False
+    except ValueError:
+        refused = True
+    comm.all_reduce(t, op="avg")
+    return alive, refused, t.tolist()
+
+
+def test_heartbeat_default_store_and_avg():
+    for alive, refused, t in run_ranks(_hb_default_store, 2):
+        assert alive == [] and refused and t == [1.0, 1.0, 1.0]
+
+
 # ------------------------------- a partitioned / placed net across processes
 PART_CONF = """
 train_steps: 6
