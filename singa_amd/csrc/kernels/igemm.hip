@@ -91,6 +91,7 @@ struct GemmArgs {
   float* stats;        // optional BN statistics of the bf16 output: ws[row][2][N] (sum, sum of squares)
   int stats_det;       // 1: row = tile row, plain stores (deterministic); 0: row = tile row % 32, atomics
   int xcd_split;       // split-K: K-slice-major XCD mapping (gridDim.z % 8 == 0, gridDim.y == 1)
+  int early_issue;     // 2-stage loop: issue tile kt+1 before waiting for tile kt (two barriers per tile)
   // stats_mode 1 (dgrad feeding a BN(+ReLU) backward): with g = out * [x*scale+shift > 0]
   // and xhat = (x - mean) * invstd, the epilogue sums (g, g*xhat) per channel
   // into `stats` -- the BN backward's reduction pass, fused
@@ -103,7 +104,7 @@ struct GemmArgs {
 __device__ __forceinline__ int kmajor_swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 template <int ROWS>
 __device__ __forceinline__ int kouter_swz(int krow, int chunk) {
-  if constexpr (ROWS == 128) return chunk ^ (((krow & 3) << 2) | ((krow >> 2) & 3));
+  if constexpr (ROWS >= 128) return chunk ^ (((krow & 3) << 2) | ((krow >> 2) & 3));
   else return chunk ^ ((((krow >> 1) & 1) << 1) | (((krow >> 3) & 1) << 2));
 }
 
@@ -128,7 +129,13 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 // 16-byte buffer load straight into LDS (buffer_load_dwordx4 ... offen lds):
 // 32-bit byte offsets against a buffer resource; an offset past num_records
 // returns zeros, which implements padding / out-of-range rows for free.
+// Operands are < 2 GiB (host-checked), so a masked-off vector keeps its
+// per-lane offset biased by BIAS: any non-negative scalar advance (< 2 GiB)
+// added later still lands past num_records.  The K loop therefore costs one
+// v_add per 16-byte vector (per-lane part + scalar K advance) plus the SALU
+// write of the wave-uniform LDS destination into M0.
 constexpr unsigned OOB = 0xFFFFFFF0u;
+constexpr unsigned BIAS = 0x80000000u;
 __device__ __forceinline__ void bld16(__amdgpu_buffer_rsrc_t rsrc, unsigned off, char* lds_wave_base) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)lds_wave_base, 16, off, 0, 0, 0);
 }
@@ -136,39 +143,47 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, un
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
 }
 
-template <int ROWS, int MODE>
+template <int ROWS, int MODE, int NTH = NT>
 struct Loader {
-  static constexpr int VPT = ROWS / 32;
+  static constexpr int VPT = ROWS * 8 / NTH;  // 16-byte vectors (= LDS-DMA wave-instructions) per thread per K-tile
   static constexpr bool KOUT = (MODE == LM_KOUTER || MODE == LM_WGRAD_B || MODE == LM_DGRAD_B);
-  static constexpr int CPR = ROWS / 8;  // KOUTER: chunks per k-row
-  static constexpr int KRP = NT / CPR;  // KOUTER: k-rows per pass
-  int base[VPT];  // element offsets (operands are < 2 GiB: checked by the host)
-  int i0[VPT], j0[VPT];
+  static constexpr int CPR = ROWS / 8;   // KOUTER: chunks per k-row
+  static constexpr int KRP = NTH / CPR;  // KOUTER: k-rows per pass
+  static constexpr int RPV = NTH / 8;    // KMAJOR: rows per pass
+  static_assert(VPT >= 1 && CPR <= 64, "tile too small for the thread count");
   __amdgpu_buffer_rsrc_t rsrc;
+  unsigned voff[VPT];  // per-lane byte offsets (BIAS-ed when masked); see issue()
+  int base[VPT];       // conv gathers: image base (elements)
+  int i0[VPT], j0[VPT];
   bool ok[VPT];
   int64_t ld;
+  int wv;                     // wave id (wave-uniform, SGPR)
   int lchunk;                 // KMAJOR: the k-chunk this lane fetches (swizzled)
+  int kr0;                    // KOUTER: this lane's k-row within a pass
   int cr, cs, cc;             // WGRAD_B: fixed column decomposition
   bool cok;
   int tap_cached;             // conv gathers: tap of the cached row offsets
-  int ro[VPT];                // conv gathers: row element offset at the cached tap (-1 = zero)
+  bool uni;                   // conv gathers: channels per tap % 64 == 0 (whole K-tile in one tap)
 
   __device__ __forceinline__ void init(const GemmArgs& p, int row0, int nrows, const Phase& P, int64_t ld_,
                                        const bf16* src, unsigned bytes) {
     const int t = threadIdx.x;
+    wv = __builtin_amdgcn_readfirstlane(t >> 6);
     ld = ld_;
     tap_cached = -1;
     rsrc = make_rsrc(src, bytes);
     if constexpr (!KOUT) {
-      const int row_l = t >> 3;  // (row >> 1) & 7 is the same for every v (32v keeps bits 1-3)
+      const int row_l = t >> 3;  // (row >> 1) & 7 is the same for every v (RPV*v keeps bits 1-3)
       lchunk = (t & 7) ^ ((row_l >> 1) & 7);
+      if constexpr (MODE == LM_CONV_FWD) uni = (p.g.C & 63) == 0;
+      if constexpr (MODE == LM_DGRAD_A) uni = (p.g.K & 63) == 0;
 #pragma unroll
       for (int v = 0; v < VPT; ++v) {
-        const int row = row0 + row_l + 32 * v;
+        const int row = row0 + row_l + RPV * v;
         ok[v] = row < nrows;
         const int rr = ok[v] ? row : 0;
         if constexpr (MODE == LM_KMAJOR) {
-          base[v] = rr * (int)ld;
+          voff[v] = ok[v] ? (unsigned)(rr * (int)ld + lchunk * 8) * 2u : BIAS;
         } else if constexpr (MODE == LM_CONV_FWD) {
           const ConvGeom& g = p.g;
           const int n = g.dHoWo.div(rr);
@@ -179,7 +194,7 @@ struct Loader {
           i0[v] = oh * g.sh - g.ph;
           j0[v] = ow * g.sw - g.pw;
         } else if constexpr (MODE == LM_DGRAD_BT) {
-          base[v] = rr * p.g.K;  // row c of a tap slab [C][K]
+          voff[v] = ok[v] ? (unsigned)(rr * p.g.K + lchunk * 8) * 2u : BIAS;  // row c of a tap slab [C][K]
         } else {  // LM_DGRAD_A: row = (n, hh, ww) of the phase grid
           const ConvGeom& g = p.g;
           const int n = P.dHpWp.div(rr);
@@ -191,32 +206,41 @@ struct Loader {
           j0[v] = ww + P.offw;
         }
       }
-    } else if constexpr (MODE == LM_WGRAD_B) {
-      const ConvGeom& g = p.g;
-      const int kr = t / CPR;
-      const int col = row0 + (((t % CPR) ^ kouter_swz<ROWS>(kr, 0)) * 8);  // swz(kr) same for every v
+    } else {
+      kr0 = t / CPR;
+      const int col = row0 + (((t % CPR) ^ kouter_swz<ROWS>(kr0, 0)) * 8);  // swz(kr) same for every v
       cok = col < nrows;
-      const int c2 = cok ? col : 0;
-      const int rs = g.dC.div(c2);
-      cc = c2 - rs * g.C;
-      cr = g.dS.div(rs);
-      cs = rs - cr * g.S;
+      if constexpr (MODE == LM_KOUTER) {
+#pragma unroll
+        for (int v = 0; v < VPT; ++v) voff[v] = cok ? (unsigned)((kr0 + KRP * v) * (int)ld + col) * 2u : BIAS;
+      } else if constexpr (MODE == LM_WGRAD_B) {
+        const ConvGeom& g = p.g;
+        const int c2 = cok ? col : 0;
+        const int rs = g.dC.div(c2);
+        cc = c2 - rs * g.C;
+        cr = g.dS.div(rs);
+        cs = rs - cr * g.S;
+#pragma unroll
+        for (int v = 0; v < VPT; ++v) voff[v] = cok ? (unsigned)((kr0 + KRP * v) * g.C + cc) * 2u : BIAS;
+      } else {  // LM_DGRAD_B
+        cc = col;
+      }
     }
   }
 
   // Issue the K-tile starting at k0 (absolute) into the LDS stage `lds`.
-  __device__ __forceinline__ void issue(const GemmArgs& p, const bf16* __restrict__ src, int row0, int nrows, int k0,
-                                        int kend, const Phase& P, char* lds) {
-    const int t = threadIdx.x;
-    const int w = t >> 6;
+  // live == false: a dummy tile (past the end of K) that only keeps the
+  // per-tile DMA count uniform -- every vector goes through a null resource
+  // (num_records 0: no memory traffic, zeros into a stage nobody reads).
+  __device__ __forceinline__ void issue(const GemmArgs& p, int row0, int nrows, int k0, int kend, const Phase& P,
+                                        char* lds, bool live = true) {
+    const __amdgpu_buffer_rsrc_t rs = live ? rsrc : make_rsrc(nullptr, 0);
+    const bool full = kend - k0 >= BK;  // wave-uniform: no per-lane K bound inside this tile
     if constexpr (MODE == LM_KMAJOR) {
-      const int kk = k0 + lchunk * 8;
-      const bool kin = kk < kend;
+      const bool kin = full || (k0 + lchunk * 8 < kend);
 #pragma unroll
-      for (int v = 0; v < VPT; ++v) {
-        const bool o = ok[v] && kin;
-        bld16(rsrc, o ? (unsigned)(base[v] + kk) * 2u : OOB, lds + (8 * w + 32 * v) * 128);
-      }
+      for (int v = 0; v < VPT; ++v)
+        bld16(rs, kin ? voff[v] + (unsigned)k0 * 2u : OOB, lds + (8 * wv + RPV * v) * 128);
     } else if constexpr (MODE == LM_DGRAD_BT) {
       // K-tile = one tap (g.K % 64 == 0, host-checked): scalar tap math, then
       // a plain K-major row fetch from that tap's [C][K] slab
@@ -224,25 +248,16 @@ struct Loader {
       const int tap = g.dK.div(k0);
       const int j = P.dns.div(tap), i = tap - j * P.ns;
       const int r = P.r0 + g.sh * j, sc = P.s0 + g.sw * i;
-      const int tapoff = (r * g.S + sc) * g.C * g.K;
-      const int kk = k0 + lchunk * 8;
-      const bool kin = kk < kend;
-      const int k = kk - tap * g.K;
+      const unsigned adv = (unsigned)((r * g.S + sc) * g.C * g.K + k0 - tap * g.K) * 2u;
 #pragma unroll
-      for (int v = 0; v < VPT; ++v) {
-        const bool o = ok[v] && kin;
-        bld16(rsrc, o ? (unsigned)(tapoff + base[v] + k) * 2u : OOB, lds + (8 * w + 32 * v) * 128);
-      }
+      for (int v = 0; v < VPT; ++v) bld16(rs, voff[v] + adv, lds + (8 * wv + RPV * v) * 128);
     } else if constexpr (MODE == LM_CONV_FWD || MODE == LM_DGRAD_A) {
       const ConvGeom& g = p.g;
       const int CH = MODE == LM_CONV_FWD ? g.C : g.K;
       const FastDiv& dch = MODE == LM_CONV_FWD ? g.dC : g.dK;
-      int kk = k0 + lchunk * 8;
-      const bool kin = kk < kend;
-      kk = kin ? kk : 0;
-      if ((CH & 63) == 0) {  // the whole K-tile is one tap: cache row pointers per tap
+      const int HH = MODE == LM_CONV_FWD ? g.H : g.Ho, WW = MODE == LM_CONV_FWD ? g.W : g.Wo;
+      if (uni) {  // the whole K-tile is one tap (K % 64 == 0 too): row offsets cached per tap
         const int tap = dch.div(k0);
-        const int c0 = kk - tap * CH;
         if (tap != tap_cached) {
           tap_cached = tap;
           int dr, ds;
@@ -255,20 +270,20 @@ struct Loader {
             dr = -j;
             ds = -i;
           }
-          const int HH = MODE == LM_CONV_FWD ? g.H : g.Ho, WW = MODE == LM_CONV_FWD ? g.W : g.Wo;
 #pragma unroll
           for (int v = 0; v < VPT; ++v) {
             const int ih = i0[v] + dr, iw = j0[v] + ds;
             const bool o = ok[v] && (unsigned)ih < (unsigned)HH && (unsigned)iw < (unsigned)WW;
-            ro[v] = o ? base[v] + (ih * WW + iw) * CH : -1;
+            voff[v] = o ? (unsigned)(base[v] + (ih * WW + iw) * CH + lchunk * 8) * 2u : BIAS;
           }
         }
+        const unsigned adv = (unsigned)(k0 - tap * CH) * 2u;
 #pragma unroll
-        for (int v = 0; v < VPT; ++v) {
-          const bool o = ro[v] >= 0 && kin;
-          bld16(rsrc, o ? (unsigned)(ro[v] + c0) * 2u : OOB, lds + (8 * w + 32 * v) * 128);
-        }
+        for (int v = 0; v < VPT; ++v) bld16(rs, voff[v] + adv, lds + (8 * wv + RPV * v) * 128);
       } else {  // per-lane tap (channel counts not a multiple of 64, e.g. the padded stem)
+        int kk = k0 + lchunk * 8;
+        const bool kin = kk < kend;
+        kk = kin ? kk : 0;
         const int tap = dch.div(kk);
         const int c0 = kk - tap * CH;
         int dr, ds;
@@ -281,57 +296,51 @@ struct Loader {
           dr = -j;
           ds = -i;
         }
-        const int HH = MODE == LM_CONV_FWD ? g.H : g.Ho, WW = MODE == LM_CONV_FWD ? g.W : g.Wo;
 #pragma unroll
         for (int v = 0; v < VPT; ++v) {
           const int ih = i0[v] + dr, iw = j0[v] + ds;
           const bool o = ok[v] && kin && (unsigned)ih < (unsigned)HH && (unsigned)iw < (unsigned)WW;
           const int off = base[v] + (ih * WW + iw) * CH + c0;
-          bld16(rsrc, o ? (unsigned)off * 2u : OOB, lds + (8 * w + 32 * v) * 128);
+          bld16(rs, o ? (unsigned)off * 2u : OOB, lds + (8 * wv + RPV * v) * 128);
         }
       }
     } else if constexpr (MODE == LM_KOUTER) {
-      const int kr0 = t / CPR;
-      const int col = row0 + (((t % CPR) ^ kouter_swz<ROWS>(kr0, 0)) * 8);
-      const bool cin = col < nrows;
+      const unsigned adv = (unsigned)k0 * (unsigned)ld * 2u;
 #pragma unroll
       for (int v = 0; v < VPT; ++v) {
-        const int kr = k0 + kr0 + KRP * v;
-        const bool o = cin && kr < kend;
-        bld16(rsrc, o ? (unsigned)(kr * (int)ld + col) * 2u : OOB, lds + (w * (64 / CPR) + KRP * v) * (ROWS * 2));
+        const bool o = full || (k0 + kr0 + KRP * v < kend);
+        bld16(rs, o ? voff[v] + adv : OOB, lds + (wv * (64 / CPR) + KRP * v) * (ROWS * 2));
       }
     } else if constexpr (MODE == LM_DGRAD_B) {
       // B(n = c, kk = (tap, k)) = W[k][r][s][c]; rows c contiguous per (k, tap)
       const ConvGeom& g = p.g;
-      const int kr0 = t / CPR;
-      const int col = row0 + (((t % CPR) ^ kouter_swz<ROWS>(kr0, 0)) * 8);
-      const bool cin = col < nrows;
+      const int col = cc;
+      const bool cin = cok;
       const int RSC = g.R * g.S * g.C;
-      const bool uni = (g.K & 63) == 0;
+      const bool uk = (g.K & 63) == 0;
       const int tapu = g.dK.div(k0);
 #pragma unroll
       for (int v = 0; v < VPT; ++v) {
         int kk = k0 + kr0 + KRP * v;
         const bool kin = kk < kend;
         kk = kin ? kk : 0;
-        const int tap = uni ? tapu : (int)g.dK.div(kk);
+        const int tap = uk ? tapu : (int)g.dK.div(kk);
         const int k = kk - tap * g.K;
         const int j = P.dns.div(tap), i = tap - j * P.ns;
         const int r = P.r0 + g.sh * j, s = P.s0 + g.sw * i;
         const bool o = cin && kin;
         const int off = k * RSC + (r * g.S + s) * g.C + col;
-        bld16(rsrc, o ? (unsigned)off * 2u : OOB, lds + (w * (64 / CPR) + KRP * v) * (ROWS * 2));
+        bld16(rs, o ? (unsigned)off * 2u : OOB, lds + (wv * (64 / CPR) + KRP * v) * (ROWS * 2));
       }
     } else if constexpr (MODE == LM_WGRAD_B) {
       const ConvGeom& g = p.g;
-      const int kr0 = t / CPR;
       if (g.R == 1 && g.S == 1 && g.sh == 1 && g.sw == 1 && g.ph == 0 && g.pw == 0) {
         // 1x1 stride-1 conv: input pixel == output pixel, no bounds
+        const unsigned adv = (unsigned)k0 * (unsigned)g.C * 2u;
 #pragma unroll
         for (int v = 0; v < VPT; ++v) {
-          const int pix = k0 + kr0 + KRP * v;
-          const bool o = cok && pix < kend;
-          bld16(rsrc, o ? (unsigned)(pix * g.C + cc) * 2u : OOB, lds + (w * (64 / CPR) + KRP * v) * (ROWS * 2));
+          const bool o = full || (k0 + kr0 + KRP * v < kend);
+          bld16(rs, o ? voff[v] + adv : OOB, lds + (wv * (64 / CPR) + KRP * v) * (ROWS * 2));
         }
       } else {
         // decompose the first pixel once; later vectors step by KRP with
@@ -363,7 +372,7 @@ struct Loader {
           const int iw = ow * g.sw - g.pw + cs * g.dw;
           const bool o = cok && pix < kend && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
           const int off = ((n * g.H + ih) * g.W + iw) * g.C + cc;
-          bld16(rsrc, o ? (unsigned)off * 2u : OOB, lds + (w * (64 / CPR) + KRP * v) * (ROWS * 2));
+          bld16(rs, o ? (unsigned)off * 2u : OOB, lds + (wv * (64 / CPR) + KRP * v) * (ROWS * 2));
         }
       }
     }
@@ -406,12 +415,40 @@ struct Loader {
   }
 };
 
-template <int BM, int BN, int AM, int BMODE, int OUT>
-__global__ void __launch_bounds__(NT, 2) igemm_k(const GemmArgs p) {
+// s_waitcnt vmcnt(N) with the other counters left alone (gfx9 encoding:
+// vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt[5:4] at [15:14]).  The
+// builtin (not inline asm) keeps the compiler's own waitcnt bookkeeping exact.
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+// Raw workgroup barrier: unlike __syncthreads() it does not drain the LDS-DMA
+// still in flight (the fence of __syncthreads() makes the compiler emit
+// vmcnt(0)); the empty asm statements keep the compiler from moving memory
+// operations across it.
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// NTH threads = WM x WN waves, each owning a (BM/WM) x (BN/WN) block of 16x16
+// MFMA tiles.  STAGES == 2: the v2 loop (one __syncthreads per K-tile, the
+// next tile's DMA overlapping this tile's MFMAs, two workgroups per CU hide
+// the rest).  STAGES >= 3 (the 8-wave big-tile variant, one workgroup per
+// CU): a ring of STAGES LDS stages with STAGES-1 K-tiles in flight; each
+// K-tile starts with a COUNTED vmcnt (this wave's DMA for the tile retired,
+// the younger tiles still in flight) and a raw barrier (every wave's DMA
+// retired, every wave done reading the stage about to be refilled).
+template <int BM, int BN, int AM, int BMODE, int OUT, int NTH = NT, int WM = 2, int WN = 2, int STAGES = 2>
+__global__ void __launch_bounds__(NTH, 2) igemm_k(const GemmArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
   constexpr int STAGE = A_BYTES + B_BYTES;
-  constexpr int TM = BM / 32, TN = BN / 32;  // 16x16 MFMA tiles per wave
+  constexpr int WTM = BM / WM, WTN = BN / WN;  // wave tile
+  constexpr int TM = WTM / 16, TN = WTN / 16;  // 16x16 MFMA tiles per wave
+  static_assert(WM * WN * 64 == NTH, "wave grid");
 
   const bf16* __restrict__ pa = p.a + (int64_t)blockIdx.y * p.sa;
   const bf16* __restrict__ pb = p.b + (int64_t)blockIdx.y * p.sb;
@@ -456,13 +493,13 @@ __global__ void __launch_bounds__(NT, 2) igemm_k(const GemmArgs p) {
   if (OUT == OUT_F32_ATOMIC && kbeg >= kend) return;
   const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
 
-  Loader<BM, AM> la;
-  Loader<BN, BMODE> lb;
+  Loader<BM, AM, NTH> la;
+  Loader<BN, BMODE, NTH> lb;
   la.init(p, m0, M, P, p.lda, pa, p.a_bytes);
   lb.init(p, n0, p.N, P, p.ldb, pb, p.b_bytes);
 
   const int wid = threadIdx.x >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = wid / WN, wn = wid % WN;
   f32x4 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -474,41 +511,94 @@ __global__ void __launch_bounds__(NT, 2) igemm_k(const GemmArgs p) {
 #pragma unroll
   for (int kk = 0; kk < BK / 32; ++kk) {
 #pragma unroll
-    for (int i = 0; i < TM; ++i) la.frag_offsets(wm * (BM / 2) + i * 16, kk, oa0[i][kk], oa1[i][kk]);
+    for (int i = 0; i < TM; ++i) la.frag_offsets(wm * WTM + i * 16, kk, oa0[i][kk], oa1[i][kk]);
 #pragma unroll
-    for (int j = 0; j < TN; ++j) lb.frag_offsets(wn * (BN / 2) + j * 16, kk, ob0[j][kk], ob1[j][kk]);
+    for (int j = 0; j < TN; ++j) lb.frag_offsets(wn * WTN + j * 16, kk, ob0[j][kk], ob1[j][kk]);
   }
 
-  if (nk > 0) {
-    la.issue(p, pa, m0, M, kbeg, kend, P, smem);
-    lb.issue(p, pb, n0, p.N, kbeg, kend, P, smem + A_BYTES);
-    for (int kt = 0; kt < nk; ++kt) {
-      const int cur = kt & 1;
-      // this wave's DMA for tile kt retired (vmcnt(0)), then every wave's has,
-      // and every wave finished reading the other stage (tile kt-1)
-      __syncthreads();
-      if (kt + 1 < nk) {
+  auto compute = [&](const char* sa) {
+    const char* sb = sa + A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      bf16x8 fa[TM], fb[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) fa[i] = la.frag_at(sa, oa0[i][kk], oa1[i][kk]);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) fb[j] = lb.frag_at(sb, ob0[j][kk], ob1[j][kk]);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  if (STAGES == 2 && p.early_issue) {
+    // two barriers per K-tile: the DMA of tile kt+1 is issued as soon as
+    // every wave has finished reading its stage (tile kt-1), BEFORE waiting
+    // for tile kt -- two tiles in flight across that wait
+    constexpr int LPT = Loader<BM, AM, NTH>::VPT + Loader<BN, BMODE, NTH>::VPT;
+    if (nk > 0) {
+      la.issue(p, m0, M, kbeg, kend, P, smem);
+      lb.issue(p, n0, p.N, kbeg, kend, P, smem + A_BYTES);
+      for (int kt = 0; kt < nk; ++kt) {
+        const int cur = kt & 1;
+        if (kt > 0) raw_barrier();  // every wave done reading stage cur^1 (tile kt-1)
         char* nxt = smem + (cur ^ 1) * STAGE;
-        la.issue(p, pa, m0, M, kbeg + (kt + 1) * BK, kend, P, nxt);
-        lb.issue(p, pb, n0, p.N, kbeg + (kt + 1) * BK, kend, P, nxt + A_BYTES);
-      }
-      const char* sa = smem + cur * STAGE;
-      const char* sb = sa + A_BYTES;
-#pragma unroll
-      for (int kk = 0; kk < BK / 32; ++kk) {
-        bf16x8 fa[TM], fb[TN];
-#pragma unroll
-        for (int i = 0; i < TM; ++i) fa[i] = la.frag_at(sa, oa0[i][kk], oa1[i][kk]);
-#pragma unroll
-        for (int j = 0; j < TN; ++j) fb[j] = lb.frag_at(sb, ob0[j][kk], ob1[j][kk]);
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+        const bool live = kt + 1 < nk;
+        la.issue(p, m0, M, kbeg + (kt + 1) * BK, kend, P, nxt, live);
+        lb.issue(p, n0, p.N, kbeg + (kt + 1) * BK, kend, P, nxt + A_BYTES, live);
+        wait_vmcnt<LPT>();  // this wave's DMA for tile kt landed
+        raw_barrier();      // ... every wave's
+        compute(smem + cur * STAGE);
       }
     }
+  } else if constexpr (STAGES == 2) {
+    if (nk > 0) {
+      la.issue(p, m0, M, kbeg, kend, P, smem);
+      lb.issue(p, n0, p.N, kbeg, kend, P, smem + A_BYTES);
+      for (int kt = 0; kt < nk; ++kt) {
+        const int cur = kt & 1;
+        // this wave's DMA for tile kt retired (vmcnt(0)), then every wave's has,
+        // and every wave finished reading the other stage (tile kt-1)
+        __syncthreads();
+        // next tile (a null-resource dummy after the last one: the loop body
+        // stays one basic block, so the DMA issue interleaves with the MFMAs)
+        char* nxt = smem + (cur ^ 1) * STAGE;
+        const bool live = kt + 1 < nk;
+        la.issue(p, m0, M, kbeg + (kt + 1) * BK, kend, P, nxt, live);
+        lb.issue(p, n0, p.N, kbeg + (kt + 1) * BK, kend, P, nxt + A_BYTES, live);
+        compute(smem + cur * STAGE);
+      }
+    }
+  } else {
+    // LDS-DMA wave-instructions per K-tile (every thread issues all of them
+    // unconditionally: out-of-range vectors read the zero-returning OOB
+    // offset, tiles past the end go through a null resource), so the count
+    // of in-flight tiles -- and the vmcnt -- is the same every iteration
+    constexpr int LPT = Loader<BM, AM, NTH>::VPT + Loader<BN, BMODE, NTH>::VPT;
+    constexpr int D = STAGES - 1;  // K-tiles in flight ahead of the one computed
+    static_assert(D * LPT < 64, "vmcnt range");
+#pragma unroll
+    for (int s = 0; s < D; ++s) {
+      la.issue(p, m0, M, kbeg + s * BK, kend, P, smem + s * STAGE, s < nk);
+      lb.issue(p, n0, p.N, kbeg + s * BK, kend, P, smem + s * STAGE + A_BYTES, s < nk);
+    }
+    int cur = 0;   // stage of tile kt
+    int fill = D;  // stage that tile kt + D goes to
+    for (int kt = 0; kt < nk; ++kt) {
+      wait_vmcnt<(D - 1) * LPT>();  // this wave's DMA for tile kt landed
+      raw_barrier();                // ... every wave's; stage `fill` is no longer read
+      char* st = smem + fill * STAGE;
+      const bool live = kt + D < nk;
+      la.issue(p, m0, M, kbeg + (kt + D) * BK, kend, P, st, live);
+      lb.issue(p, n0, p.N, kbeg + (kt + D) * BK, kend, P, st + A_BYTES, live);
+      compute(smem + cur * STAGE);
+      cur = cur + 1 == STAGES ? 0 : cur + 1;
+      fill = fill + 1 == STAGES ? 0 : fill + 1;
+    }
   }
+  wait_vmcnt<0>();  // the dummy DMA too, before the epilogue reuses the LDS
 
   // Epilogue.  acc[i][j] = D[n][m]: lane col m = l&15, rows n = (l>>4)*4+r.
   const int l = threadIdx.x & 63;
@@ -525,10 +615,10 @@ __global__ void __launch_bounds__(NT, 2) igemm_k(const GemmArgs p) {
     __syncthreads();  // all waves are done reading the last operand stage
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
-      const int ml = wm * (BM / 2) + i * 16 + (l & 15);
+      const int ml = wm * WTM + i * 16 + (l & 15);
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        const int nl = wn * (BN / 2) + j * 16 + (l >> 4) * 4;
+        const int nl = wn * WTN + j * 16 + (l >> 4) * 4;
         *(float4*)(tile + ml * LDT + nl) = make_float4(acc[i][j][0] * p.alpha, acc[i][j][1] * p.alpha,
                                                        acc[i][j][2] * p.alpha, acc[i][j][3] * p.alpha);
       }
@@ -536,7 +626,7 @@ __global__ void __launch_bounds__(NT, 2) igemm_k(const GemmArgs p) {
     __syncthreads();
     float* cbase = (float*)pc;
 #pragma unroll 4
-    for (int e = threadIdx.x; e < BM * BN; e += NT) {
+    for (int e = threadIdx.x; e < BM * BN; e += NTH) {
       const int ml = e / BN, nl = e % BN;
       const int m = m0 + ml, n = n0 + nl;
       if (m < M && n < p.N) atomicAdd(cbase + (int64_t)m * p.ldc + n, tile[ml * LDT + nl]);
@@ -554,10 +644,10 @@ __global__ void __launch_bounds__(NT, 2) igemm_k(const GemmArgs p) {
       __syncthreads();  // all waves are done reading the last operand stage
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
-        const int ml = wm * (BM / 2) + i * 16 + (l & 15);
+        const int ml = wm * WTM + i * 16 + (l & 15);
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
-          const int nl = wn * (BN / 2) + j * 16 + (l >> 4) * 4;
+          const int nl = wn * WTN + j * 16 + (l >> 4) * 4;
           const int n = n0 + nl;
           float4 v = make_float4(acc[i][j][0] * p.alpha, acc[i][j][1] * p.alpha, acc[i][j][2] * p.alpha,
                                  acc[i][j][3] * p.alpha);
@@ -569,7 +659,7 @@ __global__ void __launch_bounds__(NT, 2) igemm_k(const GemmArgs p) {
       }
       __syncthreads();
       constexpr int CPRW = BN / 8;            // 16-byte output chunks per row
-      constexpr int RPP = NT / CPRW;           // rows per pass
+      constexpr int RPP = NTH / CPRW;           // rows per pass
       const int ch = threadIdx.x % CPRW, r0 = threadIdx.x / CPRW;
       const int n = n0 + ch * 8;
       float st_s[8], st_q[8];
@@ -663,7 +753,7 @@ __global__ void __launch_bounds__(NT, 2) igemm_k(const GemmArgs p) {
         // row tm of the [tiles_m][2][N] workspace (bn_fwd_finalize sums the
         // rows in a fixed order: deterministic)
         __syncthreads();
-        float* red = (float*)smem;  // [NT][16]
+        float* red = (float*)smem;  // [NTH][16]
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
           red[threadIdx.x * 16 + r] = st_s[r];
@@ -698,7 +788,7 @@ __global__ void __launch_bounds__(NT, 2) igemm_k(const GemmArgs p) {
   }
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
-    const int m = m0 + wm * (BM / 2) + i * 16 + (l & 15);
+    const int m = m0 + wm * WTM + i * 16 + (l & 15);
     if (m >= M) continue;
     int64_t rowoff;
     if (p.out_phase) {
@@ -713,7 +803,7 @@ __global__ void __launch_bounds__(NT, 2) igemm_k(const GemmArgs p) {
     }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      const int n = n0 + wn * (BN / 2) + j * 16 + (l >> 4) * 4;
+      const int n = n0 + wn * WTN + j * 16 + (l >> 4) * 4;
       if (n >= p.N) continue;
       float v[4] = {acc[i][j][0] * p.alpha, acc[i][j][1] * p.alpha, acc[i][j][2] * p.alpha,
                     acc[i][j][3] * p.alpha};
@@ -833,25 +923,48 @@ static int make_phases(ConvGeom& g) {
   return np;
 }
 
-static int g_tune[8] = {5, 1, 1, 0, 0, 0, 0, 0};
+// Tuning knobs (sg_set_tuning): 0 = wgrad tile/split policy, 1 = LDS-staged
+// bf16 epilogue, 2 = K-slice-major XCD mapping of split-K launches, 3 = wgrad
+// split-count scale (2^v), 4 = forced tile shape (5/6: the 8-wave tiles at any
+// size), 5 = 8-wave big-tile kernel for non-split launches (measured slower
+// than two 4-wave workgroups per CU on every ResNet-50 conv: off), 6 = big-tile
+// variant, 7 = early DMA issue in the 2-stage loop (measured -3.5 % conv time)
+static int g_tune[8] = {5, 1, 1, 0, 0, 0, 0, 1};
 
-template <int BM, int BN, int AM, int BMODE, int OUT>
+template <int BM, int BN, int AM, int BMODE, int OUT, int NTH = NT, int WM = 2, int WN = 2, int STAGES = 2>
 static void launch_t(const GemmArgs& p_in, int tiles, int ydim, int zdim, hipStream_t s) {
   GemmArgs p = p_in;
   p.lds_epilogue = g_tune[1];
+  p.early_issue = g_tune[7];
   p.xcd_split = (OUT == OUT_F32_ATOMIC && g_tune[2] && ydim == 1 && zdim >= 8 && (zdim & 7) == 0) ? 1 : 0;
-  dim3 grid(tiles, ydim, zdim), block(NT);
-  constexpr int stages = 2 * (BM + BN) * BK * 2;
+  dim3 grid(tiles, ydim, zdim), block(NTH);
+  constexpr int stages = STAGES * (BM + BN) * BK * 2;
   constexpr int etile = (OUT == OUT_BF16 || OUT == OUT_F32_ATOMIC) ? BM * (BN + 4) * 4 : 0;  // fp32 epilogue tile
   constexpr int lds = stages > etile ? stages : etile;
+  static_assert(lds <= 160 * 1024, "LDS budget");
+  auto* kern = igemm_k<BM, BN, AM, BMODE, OUT, NTH, WM, WN, STAGES>;
   if constexpr (lds > 65536) {
-    static bool attr = [] {
-      return hipFuncSetAttribute((const void*)igemm_k<BM, BN, AM, BMODE, OUT>,
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
+    static bool attr = [kern] {
+      return hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
     }();
     (void)attr;
   }
-  hipLaunchKernelGGL((igemm_k<BM, BN, AM, BMODE, OUT>), grid, block, lds, s, p);
+  hipLaunchKernelGGL(kern, grid, block, lds, s, p);
+}
+
+// 8-wave big tiles (one workgroup per CU, 3-4 stage LDS-DMA ring): 256 x 128
+// (waves 4 x 2 of 64 x 64) when N fills 128-wide tiles, 256 x 64 (waves 4 x 2
+// of 64 x 32, 4 stages = the whole 160 KB) for 64-wide problems.  Used only
+// when the grid still has >= 2 workgroups per CU.  Returns 0 (use the v2
+// 4-wave tiles), 1 (256x128) or 2 (256x64).
+static int pick_big(int M, int N) {
+  if (g_tune[4] == 5) return 1;  // tests: force the big tiles at any size
+  if (g_tune[4] == 6) return 2;
+  if (!g_tune[5] || g_tune[4] != 0) return 0;
+  auto wg = [&](int bm, int bn) { return (long)((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
+  if (N >= 128 && !((N % 128) != 0 && (N % 128) <= 64) && wg(256, 128) >= 512) return 1;
+  if (N <= 64 && wg(256, 64) >= 512) return 2;
+  return 0;
 }
 
 // pick the tile: avoid wasting half a 128-tile on 64-wide problems; prefer
@@ -874,10 +987,6 @@ static void launch_tile(const GemmArgs& p, int M, int BM, int BN, int splits, hi
   else if (BM == 64 && BN == 128) launch_t<64, 128, AM, BMODE, OUT>(p, tiles, batch, z, s);
   else launch_t<64, 64, AM, BMODE, OUT>(p, tiles, batch, z, s);
 }
-
-// Tuning knobs (sg_set_tuning): 0 = wgrad tile/split policy, 1 = LDS-staged
-// bf16 epilogue, 2 = K-slice-major XCD mapping of split-K launches, 3 = wgrad
-// split-count scale (2^v) (g_tune is defined above launch_t)
 
 // wgrad: the reduction (output pixels) is huge and M x N small, so
 // parallelism comes from split-K; use the largest tile that fits (operand
@@ -908,8 +1017,34 @@ static void pick_wgrad(int M, int N, int K, int mode, int& BM, int& BN, int& spl
 template <int AM, int BMODE, int OUT>
 static void launch(const GemmArgs& p, int M, int splits, hipStream_t s, int batch, int zdim) {
   int BM, BN;
+  if constexpr (OUT != OUT_F32_ATOMIC) {
+    {
+      const int big = pick_big(M, p.N);
+      const int z = zdim > 0 ? zdim : 1;
+      if (big == 1) {
+        if (g_tune[6] == 1) {  // experiment: 128x128, 8 waves of 64x32, 4 stages
+          const int tiles = ((M + 127) / 128) * ((p.N + 127) / 128);
+          launch_t<128, 128, AM, BMODE, OUT, 512, 2, 4, 4>(p, tiles, batch, z, s);
+          return;
+        }
+        if (g_tune[6] == 2) {  // experiment: 128x128, 8 waves of 64x32, 3 stages
+          const int tiles = ((M + 127) / 128) * ((p.N + 127) / 128);
+          launch_t<128, 128, AM, BMODE, OUT, 512, 2, 4, 3>(p, tiles, batch, z, s);
+          return;
+        }
+        const int tiles = ((M + 255) / 256) * ((p.N + 127) / 128);
+        launch_t<256, 128, AM, BMODE, OUT, 512, 4, 2, 3>(p, tiles, batch, z, s);
+        return;
+      }
+      if (big == 2) {
+        const int tiles = ((M + 255) / 256) * ((p.N + 63) / 64);
+        launch_t<256, 64, AM, BMODE, OUT, 512, 4, 2, 4>(p, tiles, batch, z, s);
+        return;
+      }
+    }
+  }
   pick_tile(M, p.N, BM, BN);
-  if (g_tune[4] > 0) {  // tuning: force a tile shape (1: 128x64, 2: 64x128, 3: 64x64, 4: 128x128)
+  if (g_tune[4] > 0 && g_tune[4] < 5) {  // tuning: force a tile shape (1: 128x64, 2: 64x128, 3: 64x64, 4: 128x128)
     BM = (g_tune[4] == 2 || g_tune[4] == 3) ? 64 : 128;
     BN = (g_tune[4] == 1 || g_tune[4] == 3) ? 64 : 128;
   }
@@ -1104,6 +1239,7 @@ void sg_conv_wgrad(const void* x, const void* dy, void* dw_out, int N, int H, in
 int sg_conv_stats_rows(int M, int N) {
   if ((N & 7) != 0 || !g_tune[1]) return 0;
   if (!sg_bn_deterministic()) return 32;
+  if (pick_big(M, N)) return (M + 255) / 256;
   int BM, BN;
   pick_tile(M, N, BM, BN);
   return (M + BM - 1) / BM;

@@ -139,6 +139,128 @@ def test_conv_fwd_bwd(gpu, case, wmode, kmajor, monkeypatch):
     assert rel_err(db, dy.sum((0, 2, 3))) < 1e-5
 
 
+@pytest.fixture
+def big_tiles():
+    """Force the 8-wave big-tile conv kernels (256x128 / 256x64, multi-stage
+    LDS-DMA ring) for every problem size, restore the size policy after."""
+    from singa_amd.ops import native as NN
+    yield lambda mode: NN.lib().set_tuning(4, mode)
+    NN.lib().set_tuning(4, 0)
+
+
+@pytest.mark.parametrize("tile", [5, 6])
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_big_tiles(gpu, case, tile, big_tiles, monkeypatch):
+    """fwd (fp32 and bf16 epilogue) and dgrad (both B-operand paths) of the
+    8-wave kernels vs a PyTorch fp32 reference, including partial tiles,
+    per-lane taps (C % 64 != 0) and stride phases."""
+    from singa_amd.ops import functional as F
+    N_, C, H, W, K, R, S, st, pd = case
+    g = torch.Generator().manual_seed(5)
+    x = bf(torch.randn(N_, C, H, W, generator=g)).float()
+    w = bf(torch.randn(K, C, R, S, generator=g) * (1.0 / math.sqrt(C * R * S))).float()
+    xr = x.clone().requires_grad_(True)
+    yr = TF.conv2d(xr, w, None, st, pd)
+    dy = bf(torch.randn(yr.shape, generator=g)).float()
+    yr.backward(dy)
+    xg = x.to(gpu).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    wg = w.to(gpu)
+    dyg = dy.to(gpu).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    big_tiles(tile)
+    y = F.conv2d_fwd(xg, wg, None, (st, st), (pd, pd), out_dtype=torch.float32)
+    assert rel_err(y, yr.detach()) < 1e-5
+    yb = F.conv2d_fwd(xg, wg, None, (st, st), (pd, pd), out_dtype=torch.bfloat16)
+    assert rel_err(yb.float(), yr.detach()) < 1e-2
+    for kmajor in (True, False):
+        monkeypatch.setattr(F, "DGRAD_KMAJOR", kmajor)
+        dx = F.conv2d_bwd(xg.float().contiguous(memory_format=torch.channels_last), wg, dyg, (st, st), (pd, pd),
+                          need_dx=True)[0]
+        assert rel_err(dx, xr.grad) < 1e-5
+        dxb = F.conv2d_bwd(xg, wg, dyg, (st, st), (pd, pd), need_dx=True)[0]
+        assert rel_err(dxb.float(), xr.grad) < 1e-2
+
+
+@pytest.mark.parametrize("tile", [5, 6])
+@pytest.mark.parametrize("det", [False, True])
+def test_conv_big_tiles_bn_stats(gpu, tile, det, big_tiles):
+    import singa_amd
+    from singa_amd.ops import functional as F
+    singa_amd.set_deterministic(det)
+    try:
+        g = torch.Generator(device=gpu).manual_seed(2)
+        x = torch.randn(8, 64, 28, 28, device=gpu, generator=g).bfloat16().contiguous(
+            memory_format=torch.channels_last)
+        w = (torch.randn(192, 64, 3, 3, device=gpu, generator=g) * 0.05).bfloat16().contiguous(
+            memory_format=torch.channels_last)
+        big_tiles(tile)
+        y1 = F.conv2d_fwd(x, w, None, (1, 1), (1, 1), out_dtype=torch.bfloat16, bn_stats=True)
+        big_tiles(0)
+        y2 = F.conv2d_fwd(x, w, None, (1, 1), (1, 1), out_dtype=torch.bfloat16)
+        assert rel_err(y1.float(), y2.float()) < 1e-2
+        gam, bet = torch.rand(192, device=gpu) + 0.5, torch.randn(192, device=gpu)
+        outs = []
+        for y in (y1, y2):
+            rm, rv = torch.zeros(192, device=gpu), torch.ones(192, device=gpu)
+            out, st = F.batchnorm_fwd(y, gam, bet, rm, rv, True, 0.1, 1e-5, relu=True)
+            outs.append((st.mean.clone(), st.invstd.clone(), rm, rv))
+    finally:
+        singa_amd.set_deterministic(False)
+    for a, b in zip(outs[0], outs[1]):
+        assert rel_err(a, b) < 1e-3
+
+
+@pytest.mark.parametrize("tile", [5, 6])
+@pytest.mark.parametrize("Nb,C,K,H,R,st", [(3, 64, 256, 14, 1, 1), (2, 128, 128, 15, 3, 2), (2, 96, 40, 9, 3, 1),
+                                           (4, 256, 64, 7, 1, 2), (2, 8, 64, 33, 7, 2)])
+def test_conv_big_tiles_stay_in_bounds(gpu, Nb, C, K, H, R, st, tile, big_tiles):
+    from singa_amd.ops import native as NN
+    L = NN.lib()
+    big_tiles(tile)
+    pad = R // 2
+    Ho = (H + 2 * pad - R) // st + 1
+    g = torch.Generator(device=gpu).manual_seed(9)
+    x = torch.randn(Nb * H * H * C, device=gpu, generator=g).bfloat16()
+    w = (torch.randn(K * R * R * C, device=gpu, generator=g) * 0.05).bfloat16()
+    dy = torch.randn(Nb * Ho * Ho * K, device=gpu, generator=g).bfloat16()
+    s = NN.stream()
+    for stats in (False, True):
+        y, chk = _guarded(Nb * Ho * Ho * K, torch.bfloat16, gpu)
+        ws = None
+        if stats:
+            rows = L.conv_stats_rows(Nb * Ho * Ho, K)
+            ws, wchk = _guarded(max(rows, 1) * 2 * K, torch.float32, gpu)
+            ws.zero_()
+        L.conv_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), 0, Nb, H, H, C, K, R, R, Ho, Ho, st, st, pad, pad, 1, 1,
+                   0, 0, s, ws.data_ptr() if ws is not None else 0)
+        chk("conv_fwd")
+        if ws is not None:
+            wchk("conv_fwd stats")
+    if st * st <= 16:
+        dx, chk = _guarded(Nb * H * H * C, torch.bfloat16, gpu)
+        L.conv_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), Nb, H, H, C, K, R, R, Ho, Ho, st, st, pad, pad, 1, 1, 0,
+                     s)
+        chk("conv_dgrad")
+
+
+@pytest.mark.parametrize("tile", [5, 6])
+@pytest.mark.parametrize("M,N,K,ak,bk", [(300, 200, 136, 0, 0), (513, 64, 96, 0, 1), (264, 384, 64, 1, 0),
+                                         (1000, 136, 200, 1, 1)])
+def test_gemm_big_tiles(gpu, M, N, K, ak, bk, tile, big_tiles):
+    from singa_amd.ops import native as NN
+    g = torch.Generator(device=gpu).manual_seed(7)
+    A = torch.randn(M, K, device=gpu, generator=g).bfloat16()
+    B = torch.randn(N, K, device=gpu, generator=g).bfloat16()
+    # (native GEMM contract: leading dimensions are multiples of 8 elements)
+    a = A.t().contiguous() if ak else A
+    b = B.t().contiguous() if bk else B
+    C = torch.empty(M, N, device=gpu)
+    big_tiles(tile)
+    NN.lib().gemm(a.data_ptr(), M if ak else K, ak, b.data_ptr(), N if bk else K, bk, C.data_ptr(), N, M, N, K, 1.0,
+                  0.0, 0, 0, 1, 1, 1, 0, 0, 0, NN.stream())
+    ref = A.float() @ B.float().t()
+    assert rel_err(C, ref) < 1e-5
+
+
 def test_conv_bias_relu_fused(gpu):
     from singa_amd.ops import functional as F
     g = torch.Generator().manual_seed(4)

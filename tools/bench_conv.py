@@ -42,6 +42,7 @@ def timeit(fn, n=10):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=128)
+    ap.add_argument("--no-miopen", action="store_true", help="skip the MIOpen (torch) yardstick")
     a = ap.parse_args()
     B = a.batch
     dev = torch.device("cuda")
@@ -59,11 +60,14 @@ def main():
         t_d = timeit(lambda: F.conv2d_bwd(x, w, dy, (st, st), (pad, pad), need_dx=True, dw_out=None)[0])
         t_w = timeit(lambda: F.conv2d_bwd(x, w, dy, (st, st), (pad, pad), need_dx=False, dw_out=dw))
         t_dw_only = t_w
-        m_f = timeit(lambda: TF.conv2d(x, w, None, st, pad))
-        m_d = timeit(lambda: torch.ops.aten.convolution_backward(dy, x, w, None, (st, st), (pad, pad), (1, 1),
-                                                                 False, (0, 0), 1, (True, False, False)))
-        m_w = timeit(lambda: torch.ops.aten.convolution_backward(dy, x, w, None, (st, st), (pad, pad), (1, 1),
-                                                                 False, (0, 0), 1, (False, True, False)))
+        if a.no_miopen:
+            m_f = m_d = m_w = float("nan")
+        else:
+            m_f = timeit(lambda: TF.conv2d(x, w, None, st, pad))
+            m_d = timeit(lambda: torch.ops.aten.convolution_backward(dy, x, w, None, (st, st), (pad, pad), (1, 1),
+                                                                     False, (0, 0), 1, (True, False, False)))
+            m_w = timeit(lambda: torch.ops.aten.convolution_backward(dy, x, w, None, (st, st), (pad, pad), (1, 1),
+                                                                     False, (0, 0), 1, (False, True, False)))
         ours = t_f + (t_d - t_dw_only if t_d > t_dw_only else t_d) + t_w
         rec = {"C": C, "H": H, "K": K, "R": R, "s": st, "n": cnt,
                "fwd_ms": round(t_f, 3), "dgrad+wgrad_ms": round(t_d, 3), "wgrad_ms": round(t_w, 3),
