@@ -197,7 +197,9 @@ def init_distributed(rank: Optional[int] = None, world_size: Optional[int] = Non
     rk = int(rank if rank is not None else os.environ.get("RANK", "0"))
     lr = int(local_rank if local_rank is not None else os.environ.get("LOCAL_RANK", str(rk)))
     if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        # SINGA_DIST_BACKEND=gloo rehearses the multi-process GPU path with
+        # several ranks sharing one GPU (RCCL refuses two ranks on one device)
+        backend = os.environ.get("SINGA_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
     if ws > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29511")
