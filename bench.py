@@ -45,6 +45,8 @@ def main() -> int:
     ap.add_argument("--loss-curve", action="store_true", help="record every step's loss (syncs; diagnostics only)")
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--sync-warmup", action="store_true", help="synchronize after every warmup step (diagnostics)")
+    ap.add_argument("--no-ps-parity", action="store_true",
+                    help="skip the PS-parity microbenchmark appended after the timed region")
     ap.add_argument("--lr", type=float, default=0.01,
                     help="SGD lr (random labels + no warmup: 0.1 occasionally diverges; throughput is lr-independent)")
     args = ap.parse_args()
@@ -123,6 +125,14 @@ def main() -> int:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     final_loss = float(loss.data.float().item())
+    ps = None
+    if not args.no_ps_parity:
+        # the reference's own headline benchmark (PS update+collect of the 12
+        # MLP tensors), measured on the same ranks AFTER the
+        # timed region: it does not touch the images/s number
+        from singa_amd.parallel import ps_parity
+
+        ps = ps_parity.run(comm, dev, iters=200, warmup=10)
     if rank == 0:
         ips = world * B * args.steps / elapsed
         rec = {
@@ -145,6 +155,9 @@ def main() -> int:
         }
         if curve:
             rec["config"]["loss_curve"] = curve
+        if ps is not None:
+            rec["ps_parity"] = {k: ps[k] for k in ("ms_per_iter", "algbw_GBps", "n_ranks",
+                                                   "speedup_vs_reference_1thread_1server")}
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.barrier()

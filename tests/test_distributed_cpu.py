@@ -400,3 +400,21 @@ def test_distopt_two_ranks_on_gpu(gpu):
     res = run_ranks(_dp_gpu_rank, 2)
     for k in res[0]:
         np.testing.assert_allclose(res[0][k], res[1][k], rtol=1e-5, atol=1e-6, err_msg=k)
+
+
+def _ps_parity(rank, world, comm, mode):
+    from singa_amd import device
+    from singa_amd.parallel import ps_parity
+
+    rec = ps_parity.run(comm, device.get_default_device(), iters=3, warmup=1, mode=mode)
+    return rec["ms_per_iter"], rec["n_ranks"], rec["bytes"]
+
+
+@pytest.mark.parametrize("mode", ["allreduce", "easgd"])
+def test_ps_parity_two_ranks(mode):
+    """The reference's headline benchmark (12 MLP tensors, update + collect)
+    runs across 2 gloo ranks and reports the max-over-ranks time."""
+    res = run_ranks(_ps_parity, 2, mode)
+    assert res[0] == res[1]  # both ranks report the same (max) time
+    ms, n, nbytes = res[0]
+    assert n == 2 and ms > 0 and nbytes >= 11972510 * 4  # (flat store pads each tensor to 64 floats)

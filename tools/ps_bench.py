@@ -23,16 +23,12 @@ import argparse
 import json
 import os
 import sys
-import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import torch  # noqa: E402
 
-SHAPES = [(784, 2500), (2500,), (2500, 2000), (2000,), (2000, 1500), (1500,), (1500, 1000), (1000,), (1000, 500),
-          (500,), (500, 10), (10,)]
-BASELINE_MS = {"1 client thread, 1 server": 48.87, "4 clients x 1 thread, 1 server": 172.0,
-               "16 threads, 1 server": 700.108, "16 threads, 4 servers": 354.59}
+from singa_amd.parallel import ps_parity  # noqa: E402
 
 
 def main():
@@ -42,59 +38,15 @@ def main():
     ap.add_argument("--mode", default="allreduce", choices=["allreduce", "easgd"])
     ap.add_argument("--bucket_mb", type=float, default=32.0)
     a = ap.parse_args()
-    from singa_amd import device, opt
+    from singa_amd import device
     from singa_amd.parallel import init_distributed
-    from singa_amd.parallel.easgd import ElasticSync
-    from singa_amd.tensor import Tensor
 
     comm = init_distributed()
-    gpu = torch.cuda.is_available()
-    dev = device.create_rocm_gpu() if gpu else device.get_default_device()
-    ps = [Tensor(data=torch.randn(s, device=dev.torch_device) * 0.01, device=dev, requires_grad=True,
-                 stores_grad=True) for s in SHAPES]
-    o = opt.SGD(0.01, 0.9)
-    st = o.attach(ps)
-    nbytes = st.numel * 4
-    es = ElasticSync(st, comm, 0.9) if a.mode == "easgd" else None
-    if es is not None:
-        es.bootstrap()
-    bucket = max(1, int(a.bucket_mb * (1 << 20) // 4))
-    spans = [(s, min(s + bucket, st.numel)) for s in range(0, st.numel, bucket)]
-
-    def one():
-        if es is not None:
-            es.sync()
-            return
-        st.g.normal_()  # a fresh "gradient" per iteration (the pm client sent random updates)
-        hs = [comm.all_reduce(st.g[s:e], async_op=True) for s, e in spans]
-        for h in hs:
-            if h is not None:
-                h.wait()
-        o.update(grad_scale=1.0 / comm.world_size)
-        o.step()
-
-    def sync():
-        if gpu:
-            torch.cuda.synchronize()
-        comm.barrier()
-
-    for _ in range(a.warmup):
-        one()
-    sync()
-    t0 = time.perf_counter()
-    for _ in range(a.iters):
-        one()
-    sync()
-    ms = (time.perf_counter() - t0) * 1e3 / a.iters
-    t = torch.tensor([ms], device=dev.torch_device)
-    comm.all_reduce(t, op="max")
-    ms = float(t.item())
+    dev = device.create_rocm_gpu() if torch.cuda.is_available() else device.get_default_device()
+    rec = ps_parity.run(comm, dev, a.iters, a.warmup, a.mode, a.bucket_mb)
     if comm.rank == 0:
-        print(json.dumps({"metric": "PS-parity update+collect round trip (12 MLP tensors, 47.9 MB)",
-                          "mode": a.mode, "n_ranks": comm.world_size, "device": "gpu" if gpu else "cpu",
-                          "iters": a.iters, "ms_per_iter": round(ms, 4), "bytes": nbytes,
-                          "algbw_GBps": round(nbytes / (ms * 1e-3) / 1e9, 2),
-                          "reference_ms (CPU cluster, ZeroMQ PS)": BASELINE_MS}))
+        rec["reference_ms (CPU cluster, ZeroMQ PS)"] = ps_parity.BASELINE_MS
+        print(json.dumps(rec))
 
 
 if __name__ == "__main__":
