@@ -18,6 +18,7 @@
 #include <condition_variable>
 #include <cstdint>
 #include <fstream>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -93,6 +94,78 @@ class Prefetcher {
   std::mutex mu_;
   std::condition_variable cv_;
   std::thread th_;
+};
+
+// ---- updaters (updater.cc) ------------------------------------------------
+enum UpdKind : int { kSGD = 0, kNesterovRef = 1, kAdaGrad = 2, kRMSProp = 3, kAdaDelta = 4, kAdam = 5, kSGDRef = 6 };
+struct UpdateArgs {
+  int kind = kSGD;
+  float lr = 0.01f, wd = 0.f, grad_scale = 1.f, t = 1.f;
+  float momentum = 0.f, dampening = 0.f, beta1 = 0.9f, beta2 = 0.999f, eps = 1e-8f, rho = 0.9f;
+  bool nesterov = false, adamw = false;
+};
+int UpdaterKind(const std::string& name);
+// w -= update(g) over n fp32 elements; s1/s2 = optimiser slots (history /
+// update / Adam moments); optional per-element lr / wd multipliers and mask
+void OptUpdate(const UpdateArgs& a, float* w, const float* g, float* s1, float* s2, int64_t n,
+               const float* lr_vec = nullptr, const float* wd_vec = nullptr, const uint8_t* mask = nullptr);
+double LearningRate(const std::string& method, double base, double final_lr, int freq, double gamma, double pw,
+                    int64_t step);
+
+// ---- parameter server (ps.cc) ---------------------------------------------
+enum PSType : uint16_t { kPSPing = 0, kPSPut = 1, kPSGet = 2, kPSUpdate = 3, kPSReplace = 4, kPSElastic = 5,
+                         kPSRandom = 6, kPSStop = 7 };
+struct PSHeader {
+  uint32_t magic;
+  uint16_t type, flags;
+  int32_t id, step;
+  float f0;
+  uint32_t pad;
+  int64_t a, b;
+  uint64_t n;
+};
+static_assert(sizeof(PSHeader) == 48, "PS wire header");
+
+class PServer {
+ public:
+  // port 0 = any free port (see port()); nworkers = kStop messages to expect
+  PServer(int port, int nworkers);
+  ~PServer();
+  int port() const;
+  int64_t messages() const;
+  void SetUpdater(const UpdateArgs& a, const std::string& method, double base, double final_lr, int freq,
+                  double gamma, double pw);
+  bool WaitStop(double timeout_s);  // true once every worker sent kStop
+  std::vector<float> Value(int id);
+  void Close();
+
+ private:
+  struct Impl;
+  std::unique_ptr<Impl> d_;
+};
+
+class PSClient {
+ public:
+  PSClient(const std::vector<std::string>& endpoints, int retries = 10, double retry_s = 1.0);
+  ~PSClient();
+  int nservers() const { return (int)fds_.size(); }
+  int server_of(int id) const;
+  void Put(int id, const float* w, uint64_t n);
+  uint64_t Get(int id, float* out, uint64_t cap);
+  void Update(int id, const float* grad, float* w_out, uint64_t n, int step = -1, float grad_scale = 0.f);
+  void Elastic(int id, float* w, uint64_t n, float alpha);
+  void RandomSync(int id, const float* delta, float* old_out, uint64_t m, int64_t a, int64_t b);
+  void PushReplace(int id, const float* w, uint64_t n);
+  void PushUpdate(int id, const float* grad, uint64_t n, int step = -1, float grad_scale = 0.f);
+  int Collect(const std::vector<float*>& outs, const std::vector<uint64_t>& caps, const std::vector<int>& ids);
+  void Stop();
+
+ private:
+  void Send(const PSHeader& h, const float* data, size_t server);
+  bool Recv(size_t server, PSHeader* r, float* out, uint64_t cap);
+  uint64_t Request(const PSHeader& h, const float* data, float* out, uint64_t cap);
+  std::vector<int> fds_;
+  std::vector<std::vector<int>> pending_;
 };
 
 struct Graph {

@@ -12,6 +12,9 @@ fan-out of one ``singa`` process per hostfile line).  One process per GPU:
   ``Router::Bind`` forever, SURVEY §5.3) and, with ``--max_restarts``,
   relaunches the whole job resuming from ``--checkpoint`` if it exists
   (checkpoint-based elastic recovery);
+* ``--nservers N`` also starts N native parameter-server processes (the
+  reference's server role, csrc/runtime/ps.cc) and switches the workers'
+  inter-group exchange to them (``SINGA_AMD_PS=native``);
 * the launcher itself never touches the GPU.
 """
 from __future__ import annotations
@@ -57,14 +60,28 @@ def _default_nproc(args_after: List[str]) -> int:
 
 
 def run_job(nproc: int, child_args: List[str], module: str = "singa_amd", poll_s: float = 0.2,
-            timeout_s: float = 0.0, env_extra=None) -> int:
+            timeout_s: float = 0.0, env_extra=None, nservers: int = 0) -> int:
     port = _free_port()
     procs = []
+    # native parameter-server processes (reference roles procsID >= nworkers):
+    # they do not join the workers' process group
+    for i in range(nservers):
+        env = dict(os.environ)
+        env.update(SINGA_AMD_ROLE="server", SINGA_AMD_SERVER_ID=str(i), SINGA_AMD_PS="native",
+                   SINGA_AMD_NWORKERS=str(nproc))
+        for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE"):
+            env.pop(k, None)
+        if env_extra:
+            env.update(env_extra)
+        procs.append(subprocess.Popen([sys.executable, "-m", module] + child_args, env=env,
+                                      start_new_session=True))
     for r in range(nproc):
         env = dict(os.environ)
         env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nproc), MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=str(port), LOCAL_WORLD_SIZE=str(nproc))
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        if nservers:
+            env["SINGA_AMD_PS"] = "native"
         if env_extra:
             env.update(env_extra)
         procs.append(subprocess.Popen([sys.executable, "-m", module] + child_args, env=env,
@@ -117,10 +134,12 @@ def main(argv=None) -> int:
     ap.add_argument("--module", default="singa_amd")
     ap.add_argument("--max_restarts", type=int, default=0)
     ap.add_argument("--timeout", type=float, default=0.0)
+    ap.add_argument("--nservers", type=int, default=0,
+                    help="also start N native parameter-server processes (SINGA_AMD_PS=native)")
     a = ap.parse_args(mine)
     n = a.nproc or _default_nproc(child)
     ckpt = child[child.index("--checkpoint") + 1] if "--checkpoint" in child else ""
-    rc = run_job(n, child, a.module, timeout_s=a.timeout)
+    rc = run_job(n, child, a.module, timeout_s=a.timeout, nservers=a.nservers)
     attempt = 0
     while rc != 0 and attempt < a.max_restarts:
         attempt += 1
@@ -130,7 +149,7 @@ def main(argv=None) -> int:
             args += ["--resume", ckpt]
         print(f"[launch] restart {attempt}/{a.max_restarts}" + (f" resuming from {ckpt}" if "--resume" in args
                                                                  else ""), file=sys.stderr)
-        rc = run_job(n, args, a.module, timeout_s=a.timeout)
+        rc = run_job(n, args, a.module, timeout_s=a.timeout, nservers=a.nservers)
     return rc
 
 

@@ -1,6 +1,9 @@
 """``singa`` entry point (reference C27, src/main.cc:13-62): read the cluster
-and model confs, set up the cluster, and run a Worker (servers are dissolved
-into collectives, so every process is a worker: SURVEY §5.8).
+and model confs, set up the cluster, and run a Worker.  By default servers are
+dissolved into collectives, so every process is a worker; with
+``launch --nservers N`` (``SINGA_AMD_PS=native``) the extra processes take
+the reference's server role (:func:`run_server`: a native C++ parameter
+server, csrc/runtime/ps.cc) and the workers exchange through them.
 
     python -m singa_amd --model_conf examples/mnist/mlp.conf --cluster_conf examples/mnist/cluster.conf
 
@@ -40,6 +43,23 @@ def build_parser() -> argparse.ArgumentParser:
     return ap
 
 
+def run_server(model, cluster) -> int:
+    """Server role (reference src/main.cc:53-55 -> Server::Run): a native
+    parameter-server shard on ``start_port + 1 + server_id`` that serves until
+    every worker has sent kStop."""
+    from .parallel.ps import ParamServer
+
+    sid = int(os.environ.get("SINGA_AMD_SERVER_ID", "0"))
+    nworkers = int(os.environ.get("SINGA_AMD_NWORKERS", "1"))
+    start = cluster.start_port if cluster is not None and cluster.HasField("start_port") else 6723
+    srv = ParamServer(start + 1 + sid, nworkers)
+    srv.set_updater_from_proto(model.updater)
+    logging.info("[server %d] listening on port %d for %d workers", sid, srv.port, nworkers)
+    srv.serve()
+    logging.info("[server %d] has shut down (%d messages)", sid, srv.messages)
+    return 0
+
+
 def main(argv=None) -> int:
     a = build_parser().parse_args(argv)
     logging.basicConfig(level=logging.DEBUG if a.v >= 3 else logging.INFO, format="%(asctime)s %(message)s")
@@ -52,6 +72,8 @@ def main(argv=None) -> int:
     cluster = schema.read_text_file("ClusterProto", a.cluster_conf) if a.cluster_conf else None
     if a.train_steps is not None:
         model.train_steps = a.train_steps
+    if os.environ.get("SINGA_AMD_ROLE") == "server":
+        return run_server(model, cluster)
     comm = init_distributed()
     use_gpu = a.device == "gpu" or (a.device == "auto" and device.get_num_gpus() > 0)
     dev = device.create_rocm_gpu() if use_gpu else device.get_default_device()

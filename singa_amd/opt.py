@@ -96,6 +96,24 @@ def _sched(lr) -> DecayScheduler:
 
 
 # ---------------------------------------------------------------------------
+def _native_cpu():
+    """The host runtime module (_core) if built: its C++ updaters run the
+    CppCPU optimiser step (the torch expression in Optimizer._cpu_update is
+    the reference oracle of the tests)."""
+    global _CORE
+    if _CORE is None:
+        try:
+            from . import _core as C  # noqa: N812
+
+            _CORE = C if hasattr(C, "opt_update") else False
+        except Exception:
+            _CORE = False
+    return _CORE or None
+
+
+_CORE = None
+
+
 class ParamStore:
     def __init__(self, params: Sequence[Tensor], mixed_bf16: bool = False, reverse: bool = True,
                  state_slots: int = 2, channels_last: Optional[bool] = None):
@@ -303,8 +321,19 @@ class Optimizer:
                                self.momentum, self.dampening, self.weight_decay, gs, self.beta1, self.beta2, self.eps,
                                self.rho, int(self.nesterov), int(self.adamw), N.stream())
             return
-        self._cpu_update(st.w, g, st.s1, st.s2, st.lr_vec * self.current_lr(), st.wd_vec * self.weight_decay,
-                         float(self.step_counter + 1), gs, st.mask)
+        if _native_cpu() is not None and st.w.is_contiguous() and g.is_contiguous():
+            # CppCPU: the C++ updater of the host runtime (csrc/runtime/updater.cc)
+            C = _native_cpu()
+            C.opt_update(C.updater_kind(self.kind), st.w.numpy(), g.numpy(),
+                         st.s1.numpy() if st.s1 is not None else None,
+                         st.s2.numpy() if st.s2 is not None else None,
+                         self.current_lr(), self.weight_decay, gs, float(self.step_counter + 1),
+                         momentum=self.momentum, dampening=self.dampening, beta1=self.beta1, beta2=self.beta2,
+                         eps=self.eps, rho=self.rho, nesterov=bool(self.nesterov), adamw=bool(self.adamw),
+                         lr_vec=st.lr_vec.numpy(), wd_vec=st.wd_vec.numpy(), mask=st.mask.numpy().view(np.uint8))
+        else:
+            self._cpu_update(st.w, g, st.s1, st.s2, st.lr_vec * self.current_lr(), st.wd_vec * self.weight_decay,
+                             float(self.step_counter + 1), gs, st.mask)
         if st.low is not None:
             st.low.copy_(st.w)
 

@@ -32,6 +32,7 @@ from ..config import schema
 from ..device import Timer, get_default_device
 from ..parallel.communicator import Communicator, init_distributed
 from ..parallel.easgd import ElasticSync, RandomSync
+from ..parallel.ps import PSClient, PSSync, server_endpoints
 from .neuralnet import NeuralNet
 
 
@@ -53,6 +54,12 @@ def make_updater(up) -> opt.Optimizer:
     if kind == "kAdaDelta":
         return opt.AdaDelta(1.0, up.rho, up.delta, up.weight_decay)
     raise ValueError(kind)
+
+
+def native_ps_enabled() -> bool:
+    """SINGA_AMD_PS=native: exchange through native parameter-server
+    processes (``launch --nservers``) instead of RCCL collectives."""
+    return os.environ.get("SINGA_AMD_PS", "") == "native"
 
 
 class Performance:
@@ -143,7 +150,16 @@ class Worker:
         self.sync = None
         self.sync_dp = False
         pc = self.peer_comm
-        if pc is not None and pc.world_size > 1:
+        if native_ps_enabled() and cl.nservers() > 0:
+            # the reference's own architecture on the native C++ PS (ps.cc):
+            # key-sharded servers, Put/Get bootstrap, EASGD / RandomSync
+            cp = self.cluster_proto
+            port = cp.start_port if cp is not None and cp.HasField("start_port") else 6723
+            client = PSClient(server_endpoints(cl.nservers(), port))
+            self.sync = PSSync(self.store, client, cl.groupid(), cl.ngroups(), up.param_type or "Elastic",
+                               up.moving_rate or 0.9, up.sync_frequency, up.warmup_steps,
+                               key_base=65536 * cl.group_procsid())
+        elif pc is not None and pc.world_size > 1:
             if cl.synchronous():  # P10: gradient all-reduce across groups every step
                 self.sync_dp = True
                 pc.broadcast(self.store.w, 0)
@@ -291,7 +307,7 @@ class Worker:
     def _maybe_sync(self, step: int) -> None:
         if self.sync is not None and self.sync.sync_now(step + 1):
             with Timer(self.dev) as ts:
-                if isinstance(self.sync, RandomSync):
+                if isinstance(self.sync, (RandomSync, PSSync)):
                     self.sync.sync(step)
                 else:
                     self.sync.sync()
@@ -360,4 +376,6 @@ class Worker:
                     self.timers[k] = 0.0
                 last = step + 1
         self.step = steps
+        if isinstance(self.sync, PSSync):
+            self.sync.client.stop()  # kStop to every server (param_manager.cc:78-86)
         return {"history": self.history}
