@@ -28,6 +28,7 @@
 #include <unistd.h>
 
 #include <atomic>
+#include <cerrno>
 #include <chrono>
 #include <condition_variable>
 #include <cstring>
@@ -48,10 +49,12 @@ namespace {
 
 constexpr uint32_t kMagic = 0x31414753u;  // "SGA1"
 
+// (a signal landing in a blocking call returns EINTR: retry, do not fail)
 bool send_all(int fd, const void* p, size_t n) {
   const char* c = (const char*)p;
   while (n > 0) {
     const ssize_t k = ::send(fd, c, n, MSG_NOSIGNAL);
+    if (k < 0 && errno == EINTR) continue;
     if (k <= 0) return false;
     c += k;
     n -= (size_t)k;
@@ -62,6 +65,7 @@ bool recv_all(int fd, void* p, size_t n) {
   char* c = (char*)p;
   while (n > 0) {
     const ssize_t k = ::recv(fd, c, n, 0);
+    if (k < 0 && errno == EINTR) continue;
     if (k <= 0) return false;
     c += k;
     n -= (size_t)k;
@@ -266,6 +270,13 @@ struct PServer::Impl {
     }
     qcv.notify_one();
     writer.join();
+    {
+      // forget the fd BEFORE closing it: Close() must never shut down a
+      // number the kernel has already handed to another socket
+      std::lock_guard<std::mutex> lk(mu);
+      for (auto& c : conn_fds)
+        if (c == fd) c = -1;
+    }
     ::close(fd);
   }
 };
@@ -345,7 +356,8 @@ void PServer::Close() {
   std::vector<std::thread> hs;
   {
     std::lock_guard<std::mutex> lk(d_->mu);
-    for (int fd : d_->conn_fds) ::shutdown(fd, SHUT_RDWR);  // unblock handlers stuck in recv
+    for (int fd : d_->conn_fds)
+      if (fd >= 0) ::shutdown(fd, SHUT_RDWR);  // unblock handlers stuck in recv / send
     hs.swap(d_->handlers);
   }
   d_->cv.notify_all();
@@ -400,7 +412,7 @@ int PSClient::server_of(int id) const { return id % (int)fds_.size(); }  // key 
 
 void PSClient::Send(const PSHeader& h, const float* data, size_t server) {
   if (!send_all(fds_[server], &h, sizeof(h)) || (h.n && !send_all(fds_[server], data, h.n * sizeof(float))))
-    throw std::runtime_error("PSClient: send failed");
+    throw std::runtime_error(std::string("PSClient: send failed: ") + std::strerror(errno));
 }
 
 bool PSClient::Recv(size_t server, PSHeader* r, float* out, uint64_t cap) {
