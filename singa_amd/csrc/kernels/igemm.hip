@@ -442,7 +442,7 @@ __device__ __forceinline__ void raw_barrier() {
 // the younger tiles still in flight) and a raw barrier (every wave's DMA
 // retired, every wave done reading the stage about to be refilled).
 template <int BM, int BN, int AM, int BMODE, int OUT, int NTH = NT, int WM = 2, int WN = 2, int STAGES = 2>
-__global__ void __launch_bounds__(NTH, 2) igemm_k(const GemmArgs p) {
+__global__ void __launch_bounds__(NTH, (NTH == 512 && STAGES == 2) ? 4 : 2) igemm_k(const GemmArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
   constexpr int STAGE = A_BYTES + B_BYTES;
@@ -925,11 +925,10 @@ static int make_phases(ConvGeom& g) {
 
 // Tuning knobs (sg_set_tuning): 0 = wgrad tile/split policy, 1 = LDS-staged
 // bf16 epilogue, 2 = K-slice-major XCD mapping of split-K launches, 3 = wgrad
-// split-count scale (2^v), 4 = forced tile shape (5/6: the 8-wave tiles at any
-// size), 5 = 8-wave big-tile kernel for non-split launches (measured slower
-// than two 4-wave workgroups per CU on every ResNet-50 conv: off), 6 = big-tile
-// variant, 7 = early DMA issue in the 2-stage loop (measured -3.5 % conv time)
-static int g_tune[8] = {5, 1, 1, 0, 0, 0, 0, 1};
+// split-count scale (2^v), 4 = forced tile shape (5/6/7: the 8-wave variants
+// of pick_big at any size), 5 = 8-wave tiles for non-split launches (pick_big),
+// 6 = unused, 7 = early DMA issue in the 2-stage loop (measured -3.5 % conv time)
+static int g_tune[8] = {5, 1, 1, 0, 0, 1, 0, 1};
 
 template <int BM, int BN, int AM, int BMODE, int OUT, int NTH = NT, int WM = 2, int WN = 2, int STAGES = 2>
 static void launch_t(const GemmArgs& p_in, int tiles, int ydim, int zdim, hipStream_t s) {
@@ -952,20 +951,26 @@ static void launch_t(const GemmArgs& p_in, int tiles, int ydim, int zdim, hipStr
   hipLaunchKernelGGL(kern, grid, block, lds, s, p);
 }
 
-// 8-wave big tiles (one workgroup per CU, 3-4 stage LDS-DMA ring): 256 x 128
-// (waves 4 x 2 of 64 x 64) when N fills 128-wide tiles, 256 x 64 (waves 4 x 2
-// of 64 x 32, 4 stages = the whole 160 KB) for 64-wide problems.  Used only
-// when the grid still has >= 2 workgroups per CU.  Returns 0 (use the v2
-// 4-wave tiles), 1 (256x128) or 2 (256x64).
+// 8-wave (512-thread) tiles.  Returns 0 (the 4-wave v2 tiles) or
+//   1: 128 x 128, waves 2 x 4 of 64 x 32, 2 stages, two workgroups per CU
+//      (measured on ResNet-50 b1024: equal or up to 10 % faster than the
+//      4-wave 128 x 128 tile when N >= 128);
+//   2: 256 x 64, waves 4 x 2 of 64 x 32, 4-stage ring (the whole 160 KB),
+//      one workgroup per CU;
+//   3: 256 x 128, waves 4 x 2 of 64 x 64, 3-stage ring, one workgroup per CU.
+// 2 and 3 keep two K-tiles in flight but lose to two independent workgroups
+// per CU on every ResNet-50 conv (the waves of one workgroup reach each
+// barrier together, nothing else covers the MFMA pipe): tests only.
 static int pick_big(int M, int N) {
-  if (g_tune[4] == 5) return 1;  // tests: force the big tiles at any size
+  if (g_tune[4] == 5) return 1;  // tests: force a variant at any size
   if (g_tune[4] == 6) return 2;
+  if (g_tune[4] == 7) return 3;
   if (!g_tune[5] || g_tune[4] != 0) return 0;
   auto wg = [&](int bm, int bn) { return (long)((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
-  if (N >= 128 && !((N % 128) != 0 && (N % 128) <= 64) && wg(256, 128) >= 512) return 1;
-  if (N <= 64 && wg(256, 64) >= 512) return 2;
+  if (N >= 128 && !((N % 128) != 0 && (N % 128) <= 64) && wg(128, 128) >= 512) return 1;
   return 0;
 }
+static int big_bm(int big) { return big == 1 ? 128 : 256; }
 
 // pick the tile: avoid wasting half a 128-tile on 64-wide problems; prefer
 // 64-row tiles when 128-row ones leave the 256 CUs under-filled
@@ -1022,23 +1027,18 @@ static void launch(const GemmArgs& p, int M, int splits, hipStream_t s, int batc
       const int big = pick_big(M, p.N);
       const int z = zdim > 0 ? zdim : 1;
       if (big == 1) {
-        if (g_tune[6] == 1) {  // experiment: 128x128, 8 waves of 64x32, 4 stages
-          const int tiles = ((M + 127) / 128) * ((p.N + 127) / 128);
-          launch_t<128, 128, AM, BMODE, OUT, 512, 2, 4, 4>(p, tiles, batch, z, s);
-          return;
-        }
-        if (g_tune[6] == 2) {  // experiment: 128x128, 8 waves of 64x32, 3 stages
-          const int tiles = ((M + 127) / 128) * ((p.N + 127) / 128);
-          launch_t<128, 128, AM, BMODE, OUT, 512, 2, 4, 3>(p, tiles, batch, z, s);
-          return;
-        }
-        const int tiles = ((M + 255) / 256) * ((p.N + 127) / 128);
-        launch_t<256, 128, AM, BMODE, OUT, 512, 4, 2, 3>(p, tiles, batch, z, s);
+        const int tiles = ((M + 127) / 128) * ((p.N + 127) / 128);
+        launch_t<128, 128, AM, BMODE, OUT, 512, 2, 4, 2>(p, tiles, batch, z, s);
         return;
       }
       if (big == 2) {
         const int tiles = ((M + 255) / 256) * ((p.N + 63) / 64);
         launch_t<256, 64, AM, BMODE, OUT, 512, 4, 2, 4>(p, tiles, batch, z, s);
+        return;
+      }
+      if (big == 3) {
+        const int tiles = ((M + 255) / 256) * ((p.N + 127) / 128);
+        launch_t<256, 128, AM, BMODE, OUT, 512, 4, 2, 3>(p, tiles, batch, z, s);
         return;
       }
     }
@@ -1239,7 +1239,7 @@ void sg_conv_wgrad(const void* x, const void* dy, void* dw_out, int N, int H, in
 int sg_conv_stats_rows(int M, int N) {
   if ((N & 7) != 0 || !g_tune[1]) return 0;
   if (!sg_bn_deterministic()) return 32;
-  if (pick_big(M, N)) return (M + 255) / 256;
+  if (const int big = pick_big(M, N)) return (M + big_bm(big) - 1) / big_bm(big);
   int BM, BN;
   pick_tile(M, N, BM, BN);
   return (M + BM - 1) / BM;

@@ -141,14 +141,15 @@ def test_conv_fwd_bwd(gpu, case, wmode, kmajor, monkeypatch):
 
 @pytest.fixture
 def big_tiles():
-    """Force the 8-wave big-tile conv kernels (256x128 / 256x64, multi-stage
-    LDS-DMA ring) for every problem size, restore the size policy after."""
+    """Force an 8-wave conv/GEMM variant (5: 128x128 two workgroups per CU,
+    6: 256x64 4-stage ring, 7: 256x128 3-stage ring) for every problem size,
+    restore the size policy after."""
     from singa_amd.ops import native as NN
     yield lambda mode: NN.lib().set_tuning(4, mode)
     NN.lib().set_tuning(4, 0)
 
 
-@pytest.mark.parametrize("tile", [5, 6])
+@pytest.mark.parametrize("tile", [5, 6, 7])
 @pytest.mark.parametrize("case", CONV_CASES)
 def test_conv_big_tiles(gpu, case, tile, big_tiles, monkeypatch):
     """fwd (fp32 and bf16 epilogue) and dgrad (both B-operand paths) of the
@@ -180,7 +181,7 @@ def test_conv_big_tiles(gpu, case, tile, big_tiles, monkeypatch):
         assert rel_err(dxb.float(), xr.grad) < 1e-2
 
 
-@pytest.mark.parametrize("tile", [5, 6])
+@pytest.mark.parametrize("tile", [5, 6, 7])
 @pytest.mark.parametrize("det", [False, True])
 def test_conv_big_tiles_bn_stats(gpu, tile, det, big_tiles):
     import singa_amd
@@ -209,7 +210,7 @@ def test_conv_big_tiles_bn_stats(gpu, tile, det, big_tiles):
         assert rel_err(a, b) < 1e-3
 
 
-@pytest.mark.parametrize("tile", [5, 6])
+@pytest.mark.parametrize("tile", [5, 6, 7])
 @pytest.mark.parametrize("Nb,C,K,H,R,st", [(3, 64, 256, 14, 1, 1), (2, 128, 128, 15, 3, 2), (2, 96, 40, 9, 3, 1),
                                            (4, 256, 64, 7, 1, 2), (2, 8, 64, 33, 7, 2)])
 def test_conv_big_tiles_stay_in_bounds(gpu, Nb, C, K, H, R, st, tile, big_tiles):
@@ -242,7 +243,7 @@ def test_conv_big_tiles_stay_in_bounds(gpu, Nb, C, K, H, R, st, tile, big_tiles)
         chk("conv_dgrad")
 
 
-@pytest.mark.parametrize("tile", [5, 6])
+@pytest.mark.parametrize("tile", [5, 6, 7])
 @pytest.mark.parametrize("M,N,K,ak,bk", [(300, 200, 136, 0, 0), (513, 64, 96, 0, 1), (264, 384, 64, 1, 0),
                                          (1000, 136, 200, 1, 1)])
 def test_gemm_big_tiles(gpu, M, N, K, ak, bk, tile, big_tiles):
