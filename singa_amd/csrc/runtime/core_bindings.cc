@@ -201,4 +201,27 @@ PYBIND11_MODULE(_core, m) {
         return c.Collect(ps, caps, ids);
       })
       .def("stop", &PSClient::Stop, py::call_guard<py::gil_scoped_release>());
+
+  // ---- LMDB (kLMDBData without liblmdb / the lmdb module) -----------------
+  py::class_<LmdbReader>(m, "LmdbReader")
+      .def(py::init<const std::string&>())
+      .def("count", &LmdbReader::Count)
+      .def("seek_to_first", &LmdbReader::SeekToFirst)
+      .def("next", [](LmdbReader& r) -> py::object {
+        std::string k, v;
+        if (!r.Next(&k, &v)) return py::none();
+        return py::make_tuple(py::bytes(k), py::bytes(v));
+      });
+  m.def("decode_datum", [](py::bytes b) -> py::object {
+    ImageRecord r;
+    bool enc = false;
+    if (!DecodeDatum(std::string(b), &r, &enc)) return py::none();
+    py::dict d;
+    d["shape"] = r.shape;
+    d["label"] = r.label;
+    d["pixel"] = py::bytes(r.pixel);
+    d["data"] = r.data;
+    d["encoded"] = enc;
+    return d;
+  });
 }

@@ -96,6 +96,22 @@ class Prefetcher {
   std::thread th_;
 };
 
+// ---- LMDB (lmdb_reader.cc): read-only cursor over data.mdb, Caffe Datum ---
+class LmdbReader {
+ public:
+  explicit LmdbReader(const std::string& path);  // an LMDB directory or its data.mdb
+  ~LmdbReader();
+  int64_t Count() const;
+  void SeekToFirst();
+  bool Next(std::string* key, std::string* val);  // false at the end (in key order)
+
+ private:
+  struct Impl;
+  std::unique_ptr<Impl> d_;
+};
+// Caffe Datum bytes -> ImageRecord (shape [c, h, w]); *encoded = Datum.encoded
+bool DecodeDatum(const std::string& bytes, ImageRecord* r, bool* encoded);
+
 // ---- updaters (updater.cc) ------------------------------------------------
 enum UpdKind : int { kSGD = 0, kNesterovRef = 1, kAdaGrad = 2, kRMSProp = 3, kAdaDelta = 4, kAdam = 5, kSGDRef = 6 };
 struct UpdateArgs {

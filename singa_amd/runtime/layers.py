@@ -97,8 +97,8 @@ class RefLayer:
 # --------------------------------------------------------------------- data
 class DataSource:
     """Batches of (images float32 [B, ...], labels int32 [B]) from a Shard
-    folder (native Prefetcher thread), an LMDB (if the lmdb module exists) or
-    a synthetic generator when the path does not exist."""
+    folder (native Prefetcher thread), an LMDB of Caffe Datums (native
+    reader) or a synthetic generator when the path does not exist."""
 
     def __init__(self, path: str, batch: int, random_skip: int = 0, synthetic_shape=(28, 28), nclass: int = 10,
                  seed: int = 0, loop: bool = True, prefetch: bool = True):
@@ -127,25 +127,40 @@ class DataSource:
                 for _ in range(skip):
                     self.prefetcher.next(buf_i, buf_l)
         elif path and os.path.isdir(path) and os.path.exists(os.path.join(path, "data.mdb")):
-            try:
-                import lmdb  # noqa: F401
-                self.kind = "lmdb"
-                self._lmdb_open(path)
-            except ImportError:
-                self.kind = "synthetic"
+            self._lmdb_open(path, random_skip)
         self.dim = int(np.prod(self.shape))
 
-    def _lmdb_open(self, path):  # pragma: no cover - needs the lmdb module
-        import lmdb
+    def _lmdb_open(self, path, random_skip=0):
+        """Native read-only LMDB cursor (csrc/runtime/lmdb_reader.cc): no
+        liblmdb / lmdb module needed.  Values are Caffe Datums
+        (reference LMDBDataLayer, src/worker/layer.cc:237-295)."""
+        from .. import _core
 
-        self.env = lmdb.open(path, readonly=True, lock=False)
-        self.txn = self.env.begin()
-        self.cur = self.txn.cursor()
-        self.cur.first()
-        datum = schema.new("Datum")
-        datum.ParseFromString(self.cur.value())
-        self.shape = (datum.channels, datum.height, datum.width) if datum.channels > 1 else (datum.height,
-                                                                                            datum.width)
+        self.kind = "lmdb"
+        self.cur = _core.LmdbReader(path)
+        if self.cur.count() == 0:
+            raise ValueError(f"empty LMDB {path}")
+        d = _core.decode_datum(self.cur.next()[1])
+        if d is None or d["encoded"]:
+            raise ValueError(f"{path}: undecodable or encoded (compressed) Datum records are not supported")
+        c, h, w = d["shape"]
+        self.shape = (c, h, w) if c > 1 else (h, w)
+        self.cur.seek_to_first()
+        for _ in range(self.rng.randint(0, random_skip + 1) if random_skip else 0):
+            if self.cur.next() is None:
+                self.cur.seek_to_first()
+
+    def _lmdb_record(self):
+        from .. import _core
+
+        kv = self.cur.next()
+        if kv is None:  # wrap around (layer.cc:268-274)
+            self.cur.seek_to_first()
+            kv = self.cur.next()
+        d = _core.decode_datum(kv[1])
+        px = (np.frombuffer(d["pixel"], np.uint8).astype(np.float32) if d["pixel"]
+              else np.asarray(d["data"], np.float32))
+        return px.reshape(self.shape), d["label"]
 
     def next(self):
         B = self.batch
@@ -154,18 +169,9 @@ class DataSource:
             lab = np.empty((B,), np.int32)
             n = self.prefetcher.next(img, lab)
             return img[:n].reshape((n,) + self.shape), lab[:n]
-        if self.kind == "lmdb":  # pragma: no cover
-            imgs, labs = [], []
-            datum = schema.new("Datum")
-            for _ in range(B):
-                datum.ParseFromString(self.cur.value())
-                px = np.frombuffer(datum.data, np.uint8).astype(np.float32) if datum.data else \
-                    np.asarray(datum.float_data, np.float32)
-                imgs.append(px.reshape(self.shape))
-                labs.append(datum.label)
-                if not self.cur.next():
-                    self.cur.first()
-            return np.stack(imgs), np.asarray(labs, np.int32)
+        if self.kind == "lmdb":
+            recs = [self._lmdb_record() for _ in range(B)]
+            return np.stack([r[0] for r in recs]), np.asarray([r[1] for r in recs], np.int32)
         img = self.rng.randint(0, 256, size=(B,) + self.shape).astype(np.float32)
         lab = self.rng.randint(0, self.nclass, size=(B,)).astype(np.int32)
         return img, lab

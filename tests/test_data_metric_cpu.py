@@ -76,3 +76,42 @@ def test_metrics():
     assert metric.Accuracy().evaluate(torch.from_numpy(x), torch.from_numpy(y)) == pytest.approx(0.5)
     from singa_amd import module, model
     assert module.Module is model.Model
+
+
+def test_native_lmdb_reader_and_datum_layer(tmp_path):
+    """kLMDBData without liblmdb: the native reader walks a multi-level
+    B+tree (branch + leaf pages, an overflow value), picks the newer meta
+    page, decodes Caffe Datums, and the data source wraps at the end."""
+    from lmdb_writer import datum, write_lmdb
+
+    from singa_amd import _core
+    from singa_amd.runtime.layers import DataSource
+
+    rng = np.random.RandomState(0)
+    items = []
+    for i in range(300):
+        px = rng.randint(0, 256, size=3 * 8 * 8).astype(np.uint8).tobytes()
+        items.append((b"%08d" % i, datum(3, 8, 8, px, i % 7)))
+    big = (b"zz_big", datum(3, 40, 40, rng.randint(0, 256, size=3 * 40 * 40).astype(np.uint8).tobytes(), 3))
+    write_lmdb(str(tmp_path / "db"), items + [big], leaf_limit=16)
+    r = _core.LmdbReader(str(tmp_path / "db"))
+    assert r.count() == 301
+    got = []
+    while True:
+        kv = r.next()
+        if kv is None:
+            break
+        got.append(kv)
+    assert [k for k, _ in got] == sorted(k for k, _ in items + [big])
+    assert dict(got)[b"00000042"] == dict(items)[b"00000042"] and dict(got)[b"zz_big"] == big[1]
+    d = _core.decode_datum(dict(items)[b"00000042"])
+    assert d["shape"] == [3, 8, 8] and d["label"] == 42 % 7 and not d["encoded"]
+    # data source over the 300 uniform records (wraps around after the last)
+    write_lmdb(str(tmp_path / "db2"), items, leaf_limit=16)
+    src = DataSource(str(tmp_path / "db2"), batch=128)
+    assert src.kind == "lmdb" and src.shape == (3, 8, 8)
+    labs = np.concatenate([src.next()[1] for _ in range(3)])
+    assert np.array_equal(labs, np.array([i % 7 for i in range(300)] + [i % 7 for i in range(84)]))
+    img, _ = DataSource(str(tmp_path / "db2"), batch=2).next()
+    px1 = np.frombuffer(_core.decode_datum(items[1][1])["pixel"], np.uint8).astype(np.float32)
+    assert np.array_equal(img[1].ravel(), px1)
