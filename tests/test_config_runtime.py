@@ -238,3 +238,72 @@ def test_mnist_layer_elastic_freq():
     outs = [layer.forward([x], True).data for _ in range(2)]
     assert not torch.allclose(outs[0], img / 255)  # batch 0: distorted
     assert torch.allclose(outs[1], img / 255)      # batch 1: skipped
+
+
+@pytest.mark.parametrize("method,kw,check", [
+    ("kConstant", dict(value=0.5), lambda d: bool(np.all(d == 0.5))),
+    ("kUniform", dict(low=-0.2, high=0.3), lambda d: d.min() >= -0.2 and d.max() <= 0.3 and abs(d.mean() - 0.05) < 0.1),
+    ("kUniform", dict(low=-1, high=1, value=2), lambda d: d.min() >= -2 and d.max() <= 2 and abs(d.std() - 2 / 3 ** .5) < 0.1),
+    ("kUniformSqrtFanIn", dict(low=-1, high=1, value=1),  # U * value / sqrt(fan_in / 3), fan_in = 75
+     lambda d: np.abs(d).max() <= 1 / (75 / 3) ** .5 + 1e-6 and abs(d.std() - (1 / 3 ** .5) / (25 ** .5)) < 0.1),
+    ("kUniformSqrtFanInOut", dict(low=-1, high=1, value=1),  # U * value / sqrt(s0 + s1)
+     lambda d: np.abs(d).max() <= 1 / (50 + 100) ** .5 + 1e-6),
+    ("kGaussain", dict(mean=0.3, std=0.5), lambda d: abs(d.mean() - 0.3) < 0.1 and abs(d.std() - 0.5) < 0.1),
+    ("kGaussainSqrtFanIn", dict(mean=0.0, std=1.0, value=1),  # N * value / sqrt(s0)
+     lambda d: abs(d.mean()) < 0.1 and abs(d.std() - 1 / 50 ** .5) < 0.1),
+])
+def test_param_init_distributions(method, kw, check):
+    """Port of the reference's Param init tests (src/test/model/test_param.cc:
+    25-140): every init method over 5000 samples, mean / std within 0.1."""
+    from singa_amd import device
+    from singa_amd.config import schema
+    from singa_amd.runtime.param import make_param
+
+    p = schema.new("ParamProto")
+    p.name = "w"
+    p.init_method = getattr(p, method)
+    for k, v in kw.items():
+        setattr(p, k, v)
+    t = make_param((50, 100), p, device.get_default_device(), fan_in=75,
+                   generator=torch.Generator().manual_seed(1))
+    d = t.data.numpy().ravel()
+    assert d.size == 5000 and check(d)
+
+
+def test_rgb_image_layer_crop_mirror_unsigned():
+    """kRGBImage (reference RGBImageLayer, src/worker/layer.cc:573-643) with
+    its quirks fixed (Appendix A #12): the crop is written also without
+    mirroring, the mirror decision is one draw, centre crop at test time,
+    random crop + mirror in training, then * scale.  (Unsigned pixel decoding
+    is the record decoder's job: shard.cc DecodeRecordToFloat.)"""
+    from singa_amd import device, tensor
+    from singa_amd.runtime.layers import create_layer
+
+    p = schema.new("LayerProto")
+    p.name, p.type = "rgb", "kRGBImage"
+    p.rgbimage_param.cropsize = 4
+    p.rgbimage_param.mirror = True
+    p.rgbimage_param.scale = 0.5
+    lay = create_layer(p)
+    dev = device.get_default_device()
+    lay.setup([(2, 3, 6, 6)], dev)
+    img = torch.arange(2 * 3 * 6 * 6, dtype=torch.float32).reshape(2, 3, 6, 6) % 256  # includes values > 127
+    src = {"image": tensor.Tensor(data=img)}
+    y = lay.forward([src], training=False).data
+    assert y.shape == (2, 3, 4, 4)
+    assert torch.equal(y, img[..., 1:5, 1:5] * 0.5)  # centre crop
+    seen = set()
+    for _ in range(40):
+        y = lay.forward([src], training=True).data
+        assert y.shape == (2, 3, 4, 4) and float(y.min()) >= 0
+        found = None
+        for h0 in range(3):
+            for w0 in range(3):
+                c = img[..., h0:h0 + 4, w0:w0 + 4] * 0.5
+                if torch.equal(y, c):
+                    found = (h0, w0, False)
+                elif torch.equal(y, torch.flip(c, dims=[-1])):
+                    found = (h0, w0, True)
+        assert found is not None
+        seen.add(found)
+    assert len({s[:2] for s in seen}) > 3 and {s[2] for s in seen} == {False, True}

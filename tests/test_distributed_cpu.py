@@ -418,3 +418,26 @@ def test_ps_parity_two_ranks(mode):
     assert res[0] == res[1]  # both ranks report the same (max) time
     ms, n, nbytes = res[0]
     assert n == 2 and ms > 0 and nbytes >= 11972510 * 4  # (flat store pads each tensor to 64 floats)
+
+
+def _sync_flag_rank(rank, world, comm):
+    from singa_amd.config import schema
+    from singa_amd.runtime import Worker
+
+    mp_ = schema.parse_text("ModelProto", MLP_CONF % "Elastic")
+    cl = schema.parse_text("ClusterProto", "nworkers: 2 synchronous: true")
+    w = Worker(mp_, cl, comm=comm, log=lambda s: None, seed=rank,
+               data_override={"*": {"shape": (8, 8), "nclass": 10, "seed": 3}})
+    w.run()
+    return w.sync_dp, w.sync is None, w.store.w.clone().numpy()
+
+
+def test_cluster_synchronous_flag_all_reduces_every_step():
+    """P10: ``synchronous: true`` (declared but never read by the reference)
+    selects gradient all-reduce every step: rank 0's initial weights are
+    broadcast and both replicas stay bit-identical while training on
+    different data."""
+    res = run_ranks(_sync_flag_rank, 2)
+    for sync_dp, no_easgd, _ in res:
+        assert sync_dp and no_easgd
+    np.testing.assert_array_equal(res[0][2], res[1][2])
