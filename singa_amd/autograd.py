@@ -239,15 +239,18 @@ def backward(y, dy=None) -> Iterator[Tuple[Tensor, Tensor]]:
             dxs = (None,) * len(op.src)
         else:
             if INPLACE_ACC and getattr(op, "accepts_acc", False):
-                acc = {}
+                acc, last = {}, {}
                 for i, (src_op, _) in enumerate(op.src):
                     if src_op is not None and op.params[i] is None and src_op in pending:
                         cur = pending[src_op][op.src_idx[i]]
                         if cur is not None and id(cur) in owned:
                             acc[i] = cur
+                            # this op's contribution completes src_op's gradient
+                            last[i] = deps[src_op] == 1 and src_op.n_out == 1
                 op.acc_into = acc
+                op.acc_last = last
             dxs = _as_tuple(op.backward(*dys_))
-            op.acc_into = None
+            op.acc_into = op.acc_last = None
         if len(dxs) != len(op.src):
             raise RuntimeError(f"{op.name}: backward returned {len(dxs)} grads for {len(op.src)} inputs")
         for i, ((src_op, stores), dx) in enumerate(zip(op.src, dxs)):
@@ -641,9 +644,14 @@ class Conv2d(Operator):
         # reduction is fused into this dgrad's epilogue
         prod = self.src[0][0] if self.src else None
         bnp = None
-        if (acc is None and isinstance(prod, BatchNorm2d) and prod.relu and not prod.has_residual
-                and getattr(prod, "st", None) is not None and getattr(prod, "x", None) is not None):
-            bnp = (prod.x, prod.st)
+        if (isinstance(prod, BatchNorm2d) and prod.relu and getattr(prod, "st", None) is not None
+                and getattr(prod, "x", None) is not None):
+            if acc is None and not prod.has_residual:
+                bnp = (prod.x, prod.st)
+            elif (acc is not None and prod.has_residual and prod.st.mask is not None
+                  and (getattr(self, "acc_last", None) or {}).get(0, False)):
+                # residual BN: this dgrad's accumulation completes its output gradient
+                bnp = (prod.x, prod.st, prod.st.mask)
         dx, dw, db = F.conv2d_bwd(x, w, dy, self.stride, self.padding, self.dilation, self.group,
                                   need_dx=self.needs_grad(0), dw_out=tgt, need_db=self.has_bias, dx_acc=acc,
                                   bn_producer=bnp)

@@ -76,6 +76,9 @@ void sg_zero(void*, int64_t, hipStream_t);
 void sg_conv_dgrad_bn(const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int,
                       int, int, int, int, float, void*, void*, const void*, const void*, const void*, const void*,
                       const void*, hipStream_t);
+void sg_conv_dgrad_bn_ex(const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int,
+                         int, int, int, int, float, void*, void*, const void*, const void*, const void*, const void*,
+                         const void*, const void*, hipStream_t);
 void sg_bn_bwd_from_ws(const void*, const void*, const void*, const void*, const void*, const void*, const void*,
                        const void*, const void*, int, void*, void*, void*, void*, void*, int64_t, int, int, int,
                        hipStream_t);
@@ -272,11 +275,15 @@ PYBIND11_MODULE(_C, m) {
   // dgrad whose epilogue also sums the producer BN(+ReLU)'s backward partials into bn_ws [32][2][C]
   m.def("conv_dgrad_bn", [](P dy, P wt, P dx, int N, int H, int W, int C, int K, int R, int Sd, int Ho, int Wo,
                             int sh, int sw, int ph, int pw, int dh, int dw, P wtbuf, P bn_ws, P bn_x, P mean,
-                            P invstd, P scale, P shift, P s) {
-    sg_conv_dgrad_bn(CV(dy), CV(wt), V(dx), N, H, W, C, K, R, Sd, Ho, Wo, sh, sw, ph, pw, dh, dw, 0, 0.f, V(wtbuf),
-                     V(bn_ws), CV(bn_x), CV(mean), CV(invstd), CV(scale), CV(shift), S(s));
+                            P invstd, P scale, P shift, P s, float beta, P bn_mask) {
+    sg_conv_dgrad_bn_ex(CV(dy), CV(wt), V(dx), N, H, W, C, K, R, Sd, Ho, Wo, sh, sw, ph, pw, dh, dw, 0, beta,
+                        V(wtbuf), V(bn_ws), CV(bn_x), CV(mean), CV(invstd), CV(scale), CV(shift), CV(bn_mask), S(s));
     CHK("conv_dgrad_bn");
-  });
+  }, py::arg("dy"), py::arg("wt"), py::arg("dx"), py::arg("N"), py::arg("H"), py::arg("W"), py::arg("C"),
+     py::arg("K"), py::arg("R"), py::arg("S"), py::arg("Ho"), py::arg("Wo"), py::arg("sh"), py::arg("sw"),
+     py::arg("ph"), py::arg("pw"), py::arg("dh"), py::arg("dw"), py::arg("wtbuf"), py::arg("bn_ws"), py::arg("bn_x"),
+     py::arg("mean"), py::arg("invstd"), py::arg("scale"), py::arg("shift"), py::arg("s"), py::arg("beta") = 0.f,
+     py::arg("bn_mask") = 0);
   m.def("bn_bwd_from_ws", [](P x, P dy, P y, P scale, P shift, P mean, P invstd, P gamma, P ws, int nb, P coef, P dg,
                              P db, P dx, P dres, int64_t R, int C, int mask_mode, int dt, P s) {
     sg_bn_bwd_from_ws(CV(x), CV(dy), CV(y), CV(scale), CV(shift), CV(mean), CV(invstd), CV(gamma), CV(ws), nb, V(coef),

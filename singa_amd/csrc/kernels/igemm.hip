@@ -95,7 +95,10 @@ struct GemmArgs {
   // stats_mode 1 (dgrad feeding a BN(+ReLU) backward): with g = out * [x*scale+shift > 0]
   // and xhat = (x - mean) * invstd, the epilogue sums (g, g*xhat) per channel
   // into `stats` -- the BN backward's reduction pass, fused
+  // stats_mode 2: the same sums for a residual BN(+ReLU) whose ReLU mask is
+  // the 1-bit map bnb_mask [rows][C/8] written by its forward apply
   int stats_mode;
+  const uint8_t* bnb_mask;
   const bf16* bnb_x;
   const float *bnb_mean, *bnb_invstd, *bnb_scale, *bnb_shift;
   ConvGeom g;
@@ -666,11 +669,11 @@ __global__ void __launch_bounds__(NTH, (NTH == 512 && STAGES == 2) ? 4 : 2) igem
 #pragma unroll
       for (int r = 0; r < 8; ++r) { st_s[r] = 0.f; st_q[r] = 0.f; }
       float bmu[8], bis[8], bsc[8], bsf[8];
-      if (p.stats && p.stats_mode == 1 && n < p.N) {
+      if (p.stats && p.stats_mode >= 1 && n < p.N) {
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
           bmu[r] = p.bnb_mean[n + r]; bis[r] = p.bnb_invstd[n + r];
-          bsc[r] = p.bnb_scale[n + r]; bsf[r] = p.bnb_shift[n + r];
+          if (p.stats_mode == 1) { bsc[r] = p.bnb_scale[n + r]; bsf[r] = p.bnb_shift[n + r]; }
         }
       }
       if (n < p.N) {
@@ -698,7 +701,13 @@ __global__ void __launch_bounds__(NTH, (NTH == 512 && STAGES == 2) ? 4 : 2) igem
             rofs[pass] = (int64_t)mm * p.ldc;
           }
         }
-        const bool bnb = p.stats && p.stats_mode == 1;
+        const bool bnb = p.stats && p.stats_mode >= 1;
+        const bool bits = p.stats && p.stats_mode == 2;
+        unsigned mbits[NPS];
+        if (bits) {
+#pragma unroll
+          for (int pass = 0; pass < NPS; ++pass) mbits[pass] = p.bnb_mask[(rofs[pass] + n) >> 3];
+        }
         bf16x8 pre[NPS];
         if (bnb || p.beta != 0.f) {
           const bf16* src = bnb ? p.bnb_x : (const bf16*)pc;
@@ -733,7 +742,8 @@ __global__ void __launch_bounds__(NTH, (NTH == 512 && STAGES == 2) ? 4 : 2) igem
 #pragma unroll
             for (int r = 0; r < 8; ++r) {
               const float xf = (float)xb[r];
-              const float gr = xf * bsc[r] + bsf[r] > 0.f ? (float)o[r] : 0.f;
+              const bool on = bits ? ((mbits[pass] >> r) & 1u) != 0 : xf * bsc[r] + bsf[r] > 0.f;
+              const float gr = on ? (float)o[r] : 0.f;
               st_s[r] += gr;
               st_q[r] += gr * (xf - bmu[r]) * bis[r];
             }
@@ -749,9 +759,12 @@ __global__ void __launch_bounds__(NTH, (NTH == 512 && STAGES == 2) ? 4 : 2) igem
       }
       if (p.stats) {
         // fused BatchNorm statistics: reduce the RPP row-threads of each
-        // 8-channel chunk through LDS, then one plain store per channel into
-        // row tm of the [tiles_m][2][N] workspace (bn_fwd_finalize sums the
-        // rows in a fixed order: deterministic)
+        // 8-channel chunk through LDS -- one thread per (chunk, value) pair,
+        // RPP reads each (a v1 summed everything in the CPRW chunk threads:
+        // RPP x 16 serial reads per thread, microseconds per workgroup) --
+        // then one plain store per value into row tm of the [tiles_m][2][N]
+        // workspace (bn_fwd_finalize sums the rows in a fixed order:
+        // deterministic) or one atomic into the 32 slot rows
         __syncthreads();
         float* red = (float*)smem;  // [NTH][16]
 #pragma unroll
@@ -760,26 +773,16 @@ __global__ void __launch_bounds__(NTH, (NTH == 512 && STAGES == 2) ? 4 : 2) igem
           red[threadIdx.x * 16 + 8 + r] = st_q[r];
         }
         __syncthreads();
-        if (threadIdx.x < CPRW && n < p.N) {
-          float a[16];
-#pragma unroll
-          for (int r = 0; r < 16; ++r) a[r] = red[threadIdx.x * 16 + r];
-          for (int k = 1; k < RPP; ++k)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) a[r] += red[(k * CPRW + threadIdx.x) * 16 + r];
-          if (p.stats_det) {  // own row per tile-row: plain stores, ordered finalize
-            float* ws = p.stats + (int64_t)tm * 2 * p.N;
-            *(float4*)(ws + n) = make_float4(a[0], a[1], a[2], a[3]);
-            *(float4*)(ws + n + 4) = make_float4(a[4], a[5], a[6], a[7]);
-            *(float4*)(ws + p.N + n) = make_float4(a[8], a[9], a[10], a[11]);
-            *(float4*)(ws + p.N + n + 4) = make_float4(a[12], a[13], a[14], a[15]);
-          } else {  // 32 atomic slot rows (zeroed by the caller)
-            float* ws = p.stats + (int64_t)(tm & 31) * 2 * p.N;
-#pragma unroll
-            for (int r = 0; r < 8; ++r) {
-              atomicAdd(ws + n + r, a[r]);
-              atomicAdd(ws + p.N + n + r, a[8 + r]);
-            }
+        static_assert(CPRW * 16 <= NTH, "stats reduction: one thread per (chunk, value)");
+        if (threadIdx.x < CPRW * 16) {
+          const int c = threadIdx.x >> 4, r = threadIdx.x & 15;
+          const int nn = n0 + c * 8;
+          if (nn < p.N) {
+            float a = red[c * 16 + r];
+            for (int k = 1; k < RPP; ++k) a += red[(k * CPRW + c) * 16 + r];
+            const int col = r < 8 ? nn + r : p.N + nn + (r - 8);
+            if (p.stats_det) p.stats[(int64_t)tm * 2 * p.N + col] = a;  // own row per tile-row
+            else atomicAdd(p.stats + (int64_t)(tm & 31) * 2 * p.N + col, a);  // 32 slot rows (zeroed by the caller)
           }
         }
       }
@@ -1154,14 +1157,32 @@ void sg_conv_dgrad(const void* dy, const void* w, void* dx, int N, int H, int W,
 // non-deterministic mode) the epilogue also writes the BatchNorm(+ReLU)
 // backward partial sums of the producer BN into 32 atomic slot rows
 // bn_ws[32][2][C] (zeroed here unless the one-shot pre-zeroed flag is set).
+void sg_conv_dgrad_bn_ex(const void* dy, const void* w, void* dx, int N, int H, int W, int C, int K, int R, int S,
+                         int Ho, int Wo, int sh, int sw, int ph, int pw, int dh, int dw, int out_mode, float beta,
+                         void* wt, void* bn_ws, const void* bn_x, const void* bn_mean, const void* bn_invstd,
+                         const void* bn_scale, const void* bn_shift, const void* bn_mask, hipStream_t s);
+
 void sg_conv_dgrad_bn(const void* dy, const void* w, void* dx, int N, int H, int W, int C, int K, int R, int S,
                       int Ho, int Wo, int sh, int sw, int ph, int pw, int dh, int dw, int out_mode, float beta,
                       void* wt, void* bn_ws, const void* bn_x, const void* bn_mean, const void* bn_invstd,
                       const void* bn_scale, const void* bn_shift, hipStream_t s) {
+  sg_conv_dgrad_bn_ex(dy, w, dx, N, H, W, C, K, R, S, Ho, Wo, sh, sw, ph, pw, dh, dw, out_mode, beta, wt, bn_ws, bn_x,
+                      bn_mean, bn_invstd, bn_scale, bn_shift, nullptr, s);
+}
+
+// bn_mask != nullptr: the producer BN is a residual BN(+ReLU) whose ReLU mask
+// is its 1-bit map; beta may then be 1 (dx accumulates the other consumers'
+// gradient and the epilogue sums the partials of the FINAL value)
+void sg_conv_dgrad_bn_ex(const void* dy, const void* w, void* dx, int N, int H, int W, int C, int K, int R, int S,
+                         int Ho, int Wo, int sh, int sw, int ph, int pw, int dh, int dw, int out_mode, float beta,
+                         void* wt, void* bn_ws, const void* bn_x, const void* bn_mean, const void* bn_invstd,
+                         const void* bn_scale, const void* bn_shift, const void* bn_mask, hipStream_t s) {
   GemmArgs p{};
-  if (bn_ws && out_mode == OUT_BF16 && beta == 0.f && (C & 7) == 0 && g_tune[1] && !sg_bn_deterministic()) {
+  if (bn_ws && out_mode == OUT_BF16 && (beta == 0.f || bn_mask) && (C & 7) == 0 && g_tune[1] &&
+      !sg_bn_deterministic()) {
     p.stats = (float*)bn_ws;
-    p.stats_mode = 1;
+    p.stats_mode = bn_mask ? 2 : 1;
+    p.bnb_mask = (const uint8_t*)bn_mask;
     p.bnb_x = (const bf16*)bn_x;
     p.bnb_mean = (const float*)bn_mean; p.bnb_invstd = (const float*)bn_invstd;
     p.bnb_scale = (const float*)bn_scale; p.bnb_shift = (const float*)bn_shift;

@@ -498,6 +498,11 @@ DGRAD_KMAJOR = os.environ.get("SINGA_AMD_DGRAD_KMAJOR", "1") != "0"
 # a conv dgrad whose input came from a BN+ReLU sums that BN backward's
 # partials in its epilogue (switchable for A/B tests)
 FUSE_BN_BWD_STATS = os.environ.get("SINGA_AMD_FUSE_BN_BWD", "1") != "0"
+# residual BN(+ReLU) backward partials in the completing dgrad's epilogue:
+# measured break-even on MI355X (tools/bench_dgrad_bn.py: the extra BN-input
+# read in the epilogue of these one/two-K-tile GEMMs costs what the separate
+# reduction pass costs, profiles/dgrad_bn_fusion_b1024.jsonl), so off by default
+FUSE_RES_BN_BWD = os.environ.get("SINGA_AMD_FUSE_RES_BN_BWD", "0") == "1"
 
 
 def conv2d_bwd(x: torch.Tensor, w: torch.Tensor, dy: torch.Tensor, stride, padding, dilation=(1, 1), groups=1,
@@ -511,7 +516,10 @@ def conv2d_bwd(x: torch.Tensor, w: torch.Tensor, dy: torch.Tensor, stride, paddi
     ``bn_producer`` = (x_bn, BNState): x is the output of a training-mode
     BatchNorm+ReLU (no residual) whose pre-BN input is x_bn; the dgrad
     epilogue then also sums that BN backward's per-channel partials and
-    attaches them to dx (``dx._sg_bnbwd_ws``) so its reduction pass is skipped."""
+    attaches them to dx (``dx._sg_bnbwd_ws``) so its reduction pass is skipped.
+    ``bn_producer`` = (x_bn, BNState, mask) with ``dx_acc``: the producer is a
+    residual BN(+ReLU) with a 1-bit ReLU mask and this accumulation is the
+    last contribution to its output gradient: same fusion, on ``dx_acc``."""
     sh, sw = stride
     ph, pw = padding
     dh, dw_ = dilation
@@ -543,8 +551,25 @@ def conv2d_bwd(x: torch.Tensor, w: torch.Tensor, dy: torch.Tensor, stride, paddi
             if (dx_acc is not None and Cx == Cp and dx_acc.dtype == od and od == x.dtype
                     and tuple(dx_acc.shape) == tuple(x.shape) and N.is_cl(dx_acc) and dx_acc.is_contiguous(
                         memory_format=torch.channels_last)):
-                N.lib().conv_dgrad_acc(dyb.data_ptr(), wb.data_ptr(), dx_acc.data_ptr(), Nn, H, W, Cp, Kp, R, S, Ho,
-                                       Wo, sh, sw, ph, pw, dh, dw_, om, 1.0, N.stream(), N.ptr(wt))
+                bmask = bn_producer[2] if bn_producer is not None and len(bn_producer) > 2 else None
+                if (bmask is not None and FUSE_BN_BWD_STATS and FUSE_RES_BN_BWD and od == torch.bfloat16 and C % 8 == 0
+                        and not N.lib().deterministic() and bn_producer[0].dtype == torch.bfloat16
+                        and tuple(bn_producer[0].shape) == tuple(x.shape) and N.is_cl(bn_producer[0])
+                        and bn_producer[0].is_contiguous(memory_format=torch.channels_last)):
+                    # this accumulation completes the gradient of a residual
+                    # BN(+ReLU) output: the epilogue also sums that BN
+                    # backward's partials from the final values (its 1-bit
+                    # ReLU mask), so the BN skips its reduction pass
+                    xbn, bst = bn_producer[0], bn_producer[1]
+                    bws = zeroed_ws(32 * 2 * C, x.device)
+                    N.lib().conv_dgrad_bn(dyb.data_ptr(), wb.data_ptr(), dx_acc.data_ptr(), Nn, H, W, Cp, Kp, R, S, Ho,
+                                          Wo, sh, sw, ph, pw, dh, dw_, N.ptr(wt), bws.data_ptr(), xbn.data_ptr(),
+                                          bst.mean.data_ptr(), bst.invstd.data_ptr(), bst.scale.data_ptr(),
+                                          bst.shift.data_ptr(), N.stream(), 1.0, bmask.data_ptr())
+                    dx_acc._sg_bnbwd_ws = (bws, 32)
+                else:
+                    N.lib().conv_dgrad_acc(dyb.data_ptr(), wb.data_ptr(), dx_acc.data_ptr(), Nn, H, W, Cp, Kp, R, S,
+                                           Ho, Wo, sh, sw, ph, pw, dh, dw_, om, 1.0, N.stream(), N.ptr(wt))
                 dx = dx_acc
             elif (bn_producer is not None and FUSE_BN_BWD_STATS and od == torch.bfloat16 and Cx == Cp and C % 8 == 0
                   and not N.lib().deterministic() and bn_producer[0].dtype == torch.bfloat16
@@ -814,13 +839,15 @@ def batchnorm_bwd(x: torch.Tensor, dy: torch.Tensor, gamma: torch.Tensor, st: BN
         dx = _like(x)
         dres = _like(x) if need_dres else None
         pre = getattr(dy, "_sg_bnbwd_ws", None)  # partial sums from the consuming conv's dgrad epilogue
-        if pre is not None and mode == 2 and not need_dres:
-            L.bn_bwd_from_ws(x.data_ptr(), dy.data_ptr(), 0, st.scale.data_ptr(), st.shift.data_ptr(),
-                             st.mean.data_ptr(), st.invstd.data_ptr(), gamma.data_ptr(), pre[0].data_ptr(), pre[1],
-                             coef.data_ptr(), dg.data_ptr(), db.data_ptr(), dx.data_ptr(), 0, R, C, mode, N.dt(x),
-                             N.stream())
+        if pre is not None and ((mode == 2 and not need_dres) or mode == 3):
+            L.bn_bwd_from_ws(x.data_ptr(), dy.data_ptr(), N.ptr(ym) if mode == 3 else 0, st.scale.data_ptr(),
+                             st.shift.data_ptr(), st.mean.data_ptr(), st.invstd.data_ptr(), gamma.data_ptr(),
+                             pre[0].data_ptr(), pre[1], coef.data_ptr(), dg.data_ptr(), db.data_ptr(), dx.data_ptr(),
+                             N.ptr(dres), R, C, mode, N.dt(x), N.stream())
             dx._sg_fresh = True
-            return dx, dg, db, None
+            if dres is not None:
+                dres._sg_fresh = True
+            return dx, dg, db, dres
         L.bn_bwd(x.data_ptr(), dy.data_ptr(), N.ptr(ym), st.scale.data_ptr(), st.shift.data_ptr(),
                  st.mean.data_ptr(), st.invstd.data_ptr(), gamma.data_ptr(), _ws(R, C, x.device).data_ptr(),
                  coef.data_ptr(), dg.data_ptr(), db.data_ptr(), dx.data_ptr(), N.ptr(dres), R, C, mode, N.dt(x),

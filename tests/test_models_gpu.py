@@ -243,6 +243,7 @@ def test_stacked_bottlenecks_inplace_grad_accumulation(gpu):
         nonlocal dyt
         AG.INPLACE_ACC = inplace
         FF.FUSE_BN_BWD_STATS = inplace  # the BN-backward reduction fused into the conv dgrad epilogue
+        FF.FUSE_RES_BN_BWD = inplace  # ... also for the residual BNs (1-bit mask, accumulating dgrad)
         AG.training = True
         try:
             h = x
@@ -257,6 +258,7 @@ def test_stacked_bottlenecks_inplace_grad_accumulation(gpu):
             AG.training = False
             AG.INPLACE_ACC = True
             FF.FUSE_BN_BWD_STATS = True
+            FF.FUSE_RES_BN_BWD = False
         return h, gr
 
     h, grads = run(True)
