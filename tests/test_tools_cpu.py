@@ -170,3 +170,18 @@ def test_launcher_two_ranks_and_restart(tmp_path):
     steps = [json.loads(l)["step"] for l in mj.read_text().splitlines()]
     # the checkpoint taken after step 5 (the one the fault hits) resumes at step 6
     assert steps == [6, 7, 8, 9]
+
+
+def test_draw_graph_dot_from_conf_and_json(tmp_path):
+    """C31 visualisation: the partitioned LeNet conf rendered as Graphviz DOT
+    (via the node-link JSON of NeuralNet.to_json), no networkx needed."""
+    r = _run(["tools/draw_graph.py", "--model_conf", "examples/mnist/conv.conf", "--group_size", "2"], timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    dot = r.stdout
+    assert dot.startswith("digraph") and '"conv1" -> "pool1"' in dot
+    js = tmp_path / "g.json"
+    js.write_text(json.dumps({"directed": 1, "nodes": [{"id": "a", "color": 0, "shape": "box"},
+                                                       {"id": "b", "color": 1, "shape": "ellipse"}],
+                              "links": [{"source": 0, "target": 1, "color": 1}]}))
+    r = _run(["tools/draw_graph.py", "--json", str(js)], timeout=60)
+    assert r.returncode == 0 and '"a" -> "b"' in r.stdout
