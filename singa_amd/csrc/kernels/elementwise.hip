@@ -287,6 +287,33 @@ __global__ void nchw_to_nhwc_pad_k(const float* __restrict__ x, bf16* __restrict
   }
 }
 
+// Stem input in "paired-tap" layout for a stride-2 conv over C <= 3
+// channels: y[n][h][w'][0..7] = {x(h, w'-1, 0..2), x(h, w', 0..2), 0, 0} for
+// w' in [0, W] (zero outside the image).  One 16-byte vector then carries two
+// horizontally adjacent taps, so the 7x7/2 stem is a 7x4 conv with horizontal
+// dilation 2 over 8 channels: 224 reduction elements per output instead of
+// 392 with the channel-padded layout (ResNetStem, models/resnet.py).
+__global__ void nchw_to_pairs_k(const float* __restrict__ x, bf16* __restrict__ y, int N, int C, int H, int W) {
+  const int W1 = W + 1;
+  const int64_t total = (int64_t)N * H * W1;
+  SG_GRID_STRIDE(p, total) {
+    const int64_t nh = p / W1;
+    const int w = (int)(p - nh * W1);
+    const int64_t n = nh / H;
+    const int h = (int)(nh - n * H);
+    const float* xb = x + (n * C * H + h) * (int64_t)W;  // channel c at xb + c*H*W
+    bf16x8 v;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      v[j] = (bf16)((j < C && w >= 1) ? xb[(int64_t)j * H * W + w - 1] : 0.f);
+      v[3 + j] = (bf16)((j < C && w < W) ? xb[(int64_t)j * H * W + w] : 0.f);
+    }
+    v[6] = (bf16)0.f;
+    v[7] = (bf16)0.f;
+    *(bf16x8*)(y + p * 8) = v;
+  }
+}
+
 }  // namespace sg
 
 using namespace sg;
@@ -341,6 +368,11 @@ void sg_rand_fill(void* y, int64_t n, int dtype, int dist, float a, float b, uin
   DISPATCH_FT(dtype, hipLaunchKernelGGL(rand_fill_k<T>, dim3(sg_grid(n / 4 + 1)), dim3(256), 0, s, (T*)y, n, dist,
                                         a, b, seed, offset));
 }
+void sg_nchw_to_pairs(const void* x, void* y, int N, int C, int H, int W, hipStream_t s) {
+  hipLaunchKernelGGL(nchw_to_pairs_k, dim3(sg_grid((int64_t)N * H * (W + 1))), dim3(256), 0, s, (const float*)x,
+                     (bf16*)y, N, C, H, W);
+}
+
 void sg_nchw_to_nhwc_pad(const void* x, void* y, int N, int C, int H, int W, int Cp, hipStream_t s) {
   hipLaunchKernelGGL(nchw_to_nhwc_pad_k, dim3(sg_grid((int64_t)N * H * W)), dim3(256), 0, s, (const float*)x,
                      (bf16*)y, N, C, H, W, Cp);

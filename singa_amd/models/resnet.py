@@ -17,6 +17,7 @@ north-star addition.
 """
 from __future__ import annotations
 
+import os
 from typing import List, Sequence
 
 import torch
@@ -50,6 +51,113 @@ class InputPrep(autograd.Operator):
 
     def backward(self, dy):
         return None
+
+
+_PAIR_IDX: dict = {}
+
+
+def _pair_maps(K: int, C: int, device):
+    """Index maps between the stem filter W [K][7][7][C] (KRSC flat, C <= 3)
+    and its paired-tap form W' [K][7][4][8]: W'[k][r][j][c'] = W[k][r][2j][c']
+    (c' < 3), W[k][r][2j+1][c'-3] (3 <= c' < 6, 2j+1 < 7), else 0.
+    fwd: W' = cat(W_flat, 0)[fwd]; bwd: dW_flat = dW'_flat[bwd]."""
+    key = (K, C, str(device))
+    if key not in _PAIR_IDX:
+        zero = K * 49 * C
+        fwd = torch.full((K, 7, 4, 8), zero, dtype=torch.int64)
+        bwd = torch.empty((K, 7, 7, C), dtype=torch.int64)
+        k = torch.arange(K).view(K, 1)
+        r = torch.arange(7).view(1, 7)
+        for s in range(7):
+            j, half = s // 2, s % 2
+            for c in range(C):
+                src = k * 49 * C + r * 7 * C + s * C + c
+                dst = ((k * 7 + r) * 4 + j) * 8 + half * 3 + c
+                fwd.view(-1)[dst.reshape(-1)] = src.reshape(-1)
+                bwd[:, :, s, c] = dst
+        _PAIR_IDX[key] = (fwd.view(-1).to(device), bwd.view(-1).to(device))
+    return _PAIR_IDX[key]
+
+
+class PairedStemConv(autograd.Operator):
+    """The 7x7 / stride-2 / pad-3 ImageNet stem over <= 3 input channels
+    (fp32 NCHW batch in, bf16 NHWC out), run as a 7x4 conv with horizontal
+    dilation 2 over the "paired-tap" input (``nchw_to_pairs``: each 16-byte
+    pixel vector holds two horizontally adjacent pixels): 224 reduction
+    elements per output instead of 392 with 3 -> 8 channel padding, and half
+    the implicit-GEMM gather vectors -- forward and weight gradient.  The
+    input needs no gradient (it is the data)."""
+
+    def __init__(self, bn_stats: bool = False, name=None):
+        super().__init__(name)
+        self.bn_stats = bn_stats
+
+    @staticmethod
+    def applies(x, w_shape) -> bool:
+        return (x.is_cuda and x.dim() == 4 and x.dtype == torch.float32 and x.is_contiguous()
+                and x.shape[1] <= 3 and tuple(w_shape[1:]) == (x.shape[1], 7, 7) and N.available()
+                and not autograd._TRACE)
+
+    def forward(self, x, W):
+        L = N.lib()
+        Nn, C, H, Wd = x.shape
+        K = W.shape[0]
+        xp = torch.empty((Nn, H, Wd + 1, 8), dtype=torch.bfloat16, device=x.device)
+        L.nchw_to_pairs(x.data_ptr(), xp.data_ptr(), Nn, C, H, Wd, N.stream())
+        p = self.params[1] if len(self.params) > 1 else None
+        low = p.low if p is not None else None
+        wk = (low if low is not None else W.to(torch.bfloat16)).permute(0, 2, 3, 1).reshape(-1)  # KRSC flat
+        fwd, bwd = _pair_maps(K, C, x.device)
+        wp = torch.cat([wk, wk.new_zeros(1)])[fwd]
+        Ho, Wo = (H + 6 - 7) // 2 + 1, (Wd + 6 - 7) // 2 + 1
+        y = torch.empty((Nn, K, Ho, Wo), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+        ws, rows = None, 0
+        if self.bn_stats and autograd.training:
+            rows = L.conv_stats_rows(Nn * Ho * Wo, K)
+            if rows > 0:
+                ws = F.zeroed_ws(rows * 2 * K, x.device)
+        # paired geometry: width Wd+1, S = 4 taps of dilation 2, pad (3, 2)
+        L.conv_fwd(xp.data_ptr(), wp.data_ptr(), y.data_ptr(), 0, Nn, H, Wd + 1, 8, K, 7, 4, Ho, Wo, 2, 2, 3, 2, 1, 2,
+                   0, 0, N.stream(), N.ptr(ws))
+        if ws is not None:
+            y._sg_bn_ws = (ws, rows)
+        if self.requires_grad:
+            self.xp, self.shape = xp, (Nn, C, H, Wd, K, Ho, Wo)
+        return y
+
+    def backward(self, dy):
+        L = N.lib()
+        Nn, C, H, Wd, K, Ho, Wo = self.shape
+        xp, self.xp = self.xp, None
+        if not (dy.dtype == torch.bfloat16 and N.is_cl(dy)):
+            dy = dy.to(dtype=torch.bfloat16, memory_format=torch.channels_last)
+        dwp = torch.zeros(K * 7 * 4 * 8, dtype=torch.float32, device=dy.device)
+        L.conv_wgrad(xp.data_ptr(), dy.data_ptr(), dwp.data_ptr(), Nn, H, Wd + 1, 8, K, 7, 4, Ho, Wo, 2, 2, 3, 2, 1,
+                     2, 0, N.stream())
+        _, bwd = _pair_maps(K, C, dy.device)
+        dw = dwp[bwd].view(K, 7, 7, C).permute(0, 3, 1, 2)  # logical KCRS
+        tgt = self.grad_target(1)
+        if tgt is not None:
+            tgt.add_(dw)
+            return None, autograd.ACCUMULATED
+        return None, dw.contiguous()
+
+
+class StemConv2d(layer.Conv2d):
+    """ResNet stem conv (7x7/2, pad 3) fed the raw fp32 NCHW batch: the
+    paired-tap HIP path for bf16 on GPU (:class:`PairedStemConv`; disable with
+    ``SINGA_PAIRED_STEM=0``), otherwise :class:`InputPrep` + the generic conv."""
+
+    compute_dtype = torch.bfloat16
+
+    def forward(self, x):
+        dt = self.compute_dtype if x.data.is_cuda else torch.float32
+        if (dt == torch.bfloat16 and os.environ.get("SINGA_PAIRED_STEM", "1") != "0"
+                and PairedStemConv.applies(x.data, self.W.shape) and not self.bias
+                and self.kernel_size == (7, 7) and self.stride == (2, 2) and self.padding == (3, 3)
+                and self.dilation == (1, 1) and self.group == 1):
+            return PairedStemConv(bn_stats=getattr(self, "bn_stats", False))(x, self.W)
+        return super().forward(InputPrep(dt)(x))
 
 
 def _feeds_bn(*convs):
@@ -110,7 +218,7 @@ class ResNet(model.Model):
         super().__init__()
         self.compute_dtype = compute_dtype
         self.num_classes = num_classes
-        self.conv1 = layer.Conv2d(num_channels, 64, 7, stride=2, padding=3, bias=False)
+        self.conv1 = StemConv2d(num_channels, 64, 7, stride=2, padding=3, bias=False)
         self.bn1 = layer.BatchNorm2d()
         _feeds_bn(self.conv1)
         self.maxpool = layer.MaxPool2d(3, 2, 1)
@@ -129,9 +237,8 @@ class ResNet(model.Model):
         self.loss_fn = layer.SoftMaxCrossEntropy()
 
     def forward(self, x):
-        dt = self.compute_dtype if x.data.is_cuda else torch.float32
-        x = InputPrep(dt)(x)
-        x = self.bn1(self.conv1(x), relu=True)
+        self.conv1.compute_dtype = self.compute_dtype
+        x = self.bn1(self.conv1(x), relu=True)  # the stem converts the fp32 NCHW batch itself
         x = self.maxpool(x)
         for b in self.blocks:
             x = b(x)

@@ -99,3 +99,38 @@ def test_sublayers_in_lists_filled_after_assignment():
     assert sum(n.startswith("convs.") for n in names) == 8  # 8 conv weights (no bias with BN)
     assert sum(n.startswith("bns.") for n in names) == 16  # gamma, beta
     assert any(k.startswith("bns.") and "mean" in k for k in m.get_states())
+
+
+def test_paired_stem_index_maps_cpu():
+    """The paired-tap stem identity the GPU stem relies on: a 7x7/2/p3 conv
+    over C <= 3 channels equals a 7x4 conv (horizontal dilation 2, pad (3, 2))
+    over "pair" pixels {x(w-1, :3), x(w, :3), 0, 0} of width W+1, with the
+    weight re-laid by ``_pair_maps``; and its weight gradient maps back."""
+    import torch.nn.functional as TF
+
+    from singa_amd.models.resnet import _pair_maps
+
+    torch.manual_seed(0)
+    for (H, W, C) in [(16, 16, 3), (15, 13, 3), (12, 10, 1)]:
+        K = 5
+        x = torch.randn(2, C, H, W, dtype=torch.float64)
+        w = torch.randn(K, C, 7, 7, dtype=torch.float64, requires_grad=True)
+        ref = TF.conv2d(x, w, stride=2, padding=3)
+        xp = torch.zeros(2, 8, H, W + 1, dtype=torch.float64)
+        xp[:, :C, :, 1:] = x
+        xp[:, 3:3 + C, :, :W] = x
+        fwd, bwd = _pair_maps(K, C, "cpu")
+        wk = w.detach().permute(0, 2, 3, 1).reshape(-1)
+        wp = torch.cat([wk, wk.new_zeros(1)])[fwd].view(K, 7, 4, 8).permute(0, 3, 1, 2).contiguous()
+        wp.requires_grad_(True)
+        # the GPU kernel takes Ho/Wo explicitly and zero-fills every out-of-range tap:
+        # pad generously, then keep the reference's output extent
+        y = TF.conv2d(TF.pad(xp, (2, 4, 3, 3)), wp, stride=2, dilation=(1, 2))[..., :ref.shape[2], :ref.shape[3]]
+        assert y.shape == ref.shape
+        assert torch.allclose(y, ref, atol=1e-9)
+        dy = torch.randn_like(ref)
+        (ref * dy).sum().backward()
+        (y * dy).sum().backward()
+        dwp = wp.grad.permute(0, 2, 3, 1).reshape(-1)  # [K][7][4][8] flat
+        dw = dwp[bwd].view(K, 7, 7, C).permute(0, 3, 1, 2)
+        assert torch.allclose(dw, w.grad, atol=1e-9)

@@ -417,3 +417,35 @@ def test_graph_replay_after_device_sync_matches_eager(gpu):
         torch.cuda.synchronize()
         curves.append([float(v) for v in ls])
     np.testing.assert_allclose(curves[1], curves[0], rtol=1e-5)
+
+
+@pytest.mark.parametrize("hw", [(32, 32), (30, 27)])
+def test_paired_stem_matches_torch_fp32(gpu, hw):
+    """ResNet stem (7x7/2/p3 over the raw fp32 NCHW batch) through the
+    paired-tap HIP path (``nchw_to_pairs`` + a 7x4 dilation-2 implicit GEMM)
+    vs a PyTorch fp32 conv on the same bf16-rounded input and weight: output
+    and weight gradient; and the paired op really ran."""
+    import torch.nn.functional as TF
+
+    from singa_amd.models import resnet as R
+
+    dev = device.create_rocm_gpu()
+    dev.SetRandSeed(3)
+    conv = R.StemConv2d(3, 64, 7, stride=2, padding=3, bias=False)
+    g = torch.Generator(device=gpu).manual_seed(4)
+    xf = torch.randn(4, 3, *hw, device=gpu, generator=g)
+    x = Tensor(data=xf, device=dev, requires_grad=False, stores_grad=False)
+    autograd.training = True
+    y = conv(x)
+    assert isinstance(y.creator, R.PairedStemConv)
+    dy = torch.randn(y.shape, device=gpu, generator=g).bfloat16()
+    loss_t = autograd.reduce_sum(autograd.mul(y, Tensor(data=dy.contiguous(memory_format=torch.channels_last),
+                                                        device=dev, requires_grad=False)), None)
+    grads = {id(p): gg.data.float().clone() for p, gg in autograd.backward(loss_t)}
+    autograd.training = False
+    wr = conv.W.data.float().to(torch.bfloat16).float().clone().requires_grad_(True)
+    ref = TF.conv2d(xf.to(torch.bfloat16).float(), wr, stride=2, padding=3)
+    (ref * dy.float()).sum().backward()
+    assert y.shape == ref.shape
+    assert rel_err(y.data.float(), ref.detach()) < 1e-2
+    assert rel_err(grads[id(conv.W)].reshape(wr.shape), wr.grad) < 1e-2
