@@ -37,6 +37,7 @@
 //     accumulates fp32 partial tiles atomically into the [K][R][S][C]
 //     gradient (the layout of the flat gradient buffer).
 #include <stdexcept>
+#include <type_traits>
 
 #include "common.h"
 
@@ -68,6 +69,7 @@ struct ConvGeom {
   int K, R, S;     // filters [K][R][S][C]
   int Ho, Wo;      // output
   int sh, sw, ph, pw, dh, dw;
+  int bq_n, bq_h, bq_w;  // BK output pixels = bq_n images + bq_h rows + bq_w columns (mixed radix)
   FastDiv dC, dS, dK, dWo, dHoWo;
   Phase phs[16];
 };
@@ -110,6 +112,10 @@ __device__ __forceinline__ int kouter_swz(int krow, int chunk) {
   if constexpr (ROWS >= 128) return chunk ^ (((krow & 3) << 2) | ((krow >> 2) & 3));
   else return chunk ^ ((((krow >> 1) & 1) << 1) | (((krow >> 3) & 1) << 2));
 }
+
+// byte distance between k-halves of a K-outer LDS image with ROWS columns
+template <int ROWS>
+constexpr int kk_off(int kk) { return kk * 32 * ROWS * 2; }
 
 __device__ __forceinline__ uint4 sel(bool ok, uint4 v) { return ok ? v : make_uint4(0, 0, 0, 0); }
 
@@ -165,6 +171,13 @@ struct Loader {
   int kr0;                    // KOUTER: this lane's k-row within a pass
   int cr, cs, cc;             // WGRAD_B: fixed column decomposition
   bool cok;
+  // WGRAD_B pixel walk (general conv): per vector the input coordinates of
+  // this lane's tap at its current pixel and the byte offset of that element,
+  // advanced by BK pixels per K-tile with mixed-radix carries (adds and
+  // selects only: the per-tile divisions and 32-bit multiplies it replaces
+  // are quarter-rate and made the weight gradient VALU-bound)
+  int wih[VPT], wiw[VPT], wpo[VPT];
+  int ihl, iwl;               // wrap limits (ow >= Wo <=> iw >= iwl; oh >= Ho <=> ih >= ihl)
   int tap_cached;             // conv gathers: tap of the cached row offsets
   bool uni;                   // conv gathers: channels per tap % 64 == 0 (whole K-tile in one tap)
 
@@ -223,11 +236,51 @@ struct Loader {
         cc = c2 - rs * g.C;
         cr = g.dS.div(rs);
         cs = rs - cr * g.S;
+        ihl = g.Ho * g.sh + cr * g.dh - g.ph;
+        iwl = g.Wo * g.sw + cs * g.dw - g.pw;
 #pragma unroll
         for (int v = 0; v < VPT; ++v) voff[v] = cok ? (unsigned)((kr0 + KRP * v) * g.C + cc) * 2u : BIAS;
       } else {  // LM_DGRAD_B
         cc = col;
       }
+    }
+  }
+
+  // WGRAD_B: position the pixel walk at the first K-tile (k0 = kbeg)
+  __device__ __forceinline__ void start(const GemmArgs& p, int k0) {
+    if constexpr (MODE == LM_WGRAD_B) {
+      const ConvGeom& g = p.g;
+#pragma unroll
+      for (int v = 0; v < VPT; ++v) {
+        const int pix = k0 + kr0 + KRP * v;
+        const int pp = pix < p.K ? pix : 0;
+        const int n = g.dHoWo.div(pp);
+        const int rem = pp - n * g.Ho * g.Wo;
+        const int oh = g.dWo.div(rem);
+        const int ow = rem - oh * g.Wo;
+        wih[v] = oh * g.sh - g.ph + cr * g.dh;
+        wiw[v] = ow * g.sw - g.pw + cs * g.dw;
+        wpo[v] = (((n * g.H + wih[v]) * g.W + wiw[v]) * g.C + cc) * 2;
+      }
+    }
+  }
+  __device__ __forceinline__ void wadvance(const ConvGeom& g) {
+    const int C2 = g.C * 2;
+    const int dw_ = g.bq_w * g.sw, dh_ = g.bq_h * g.sh;
+    const int dP = C2 * (dw_ + g.W * dh_ + g.bq_n * g.H * g.W);
+    const int dRow = C2 * (g.sh * g.W - g.Wo * g.sw), dImg = C2 * (g.H * g.W - g.Ho * g.sh * g.W);
+    const int wrapw = g.Wo * g.sw, wraph = g.Ho * g.sh;
+#pragma unroll
+    for (int v = 0; v < VPT; ++v) {
+      int iw = wiw[v] + dw_;
+      const bool c1 = iw >= iwl;
+      iw -= c1 ? wrapw : 0;
+      int ih = wih[v] + dh_ + (c1 ? g.sh : 0);
+      const bool c2 = ih >= ihl;
+      ih -= c2 ? wraph : 0;
+      wiw[v] = iw;
+      wih[v] = ih;
+      wpo[v] += dP + (c1 ? dRow : 0) + (c2 ? dImg : 0);
     }
   }
 
@@ -346,37 +399,13 @@ struct Loader {
           bld16(rs, o ? voff[v] + adv : OOB, lds + (wv * (64 / CPR) + KRP * v) * (ROWS * 2));
         }
       } else {
-        // decompose the first pixel once; later vectors step by KRP with
-        // carries when a row is at least KRP wide (else divide again)
-        const int pix0 = k0 + kr0;
-        const int pp0 = pix0 < kend ? pix0 : 0;
-        int n = g.dHoWo.div(pp0);
-        int rem = pp0 - n * g.Ho * g.Wo;
-        int oh = g.dWo.div(rem);
-        int ow = rem - oh * g.Wo;
-        const bool step = g.Wo >= KRP;
 #pragma unroll
         for (int v = 0; v < VPT; ++v) {
-          const int pix = pix0 + KRP * v;
-          if (v > 0) {
-            if (step) {
-              ow += KRP;
-              if (ow >= g.Wo) { ow -= g.Wo; ++oh; }
-              if (oh >= g.Ho) { oh -= g.Ho; ++n; }
-            } else {
-              const int pp = pix < kend ? pix : 0;
-              n = g.dHoWo.div(pp);
-              rem = pp - n * g.Ho * g.Wo;
-              oh = g.dWo.div(rem);
-              ow = rem - oh * g.Wo;
-            }
-          }
-          const int ih = oh * g.sh - g.ph + cr * g.dh;
-          const int iw = ow * g.sw - g.pw + cs * g.dw;
-          const bool o = cok && pix < kend && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
-          const int off = ((n * g.H + ih) * g.W + iw) * g.C + cc;
-          bld16(rs, o ? (unsigned)off * 2u : OOB, lds + (wv * (64 / CPR) + KRP * v) * (ROWS * 2));
+          const bool o = cok && (full || k0 + kr0 + KRP * v < kend) && (unsigned)wih[v] < (unsigned)g.H &&
+                         (unsigned)wiw[v] < (unsigned)g.W;
+          bld16(rs, o ? (unsigned)wpo[v] : OOB, lds + (wv * (64 / CPR) + KRP * v) * (ROWS * 2));
         }
+        wadvance(g);  // the K-tiles are issued in order: position the walk at k0 + BK
       }
     }
   }
@@ -400,6 +429,34 @@ struct Loader {
       const int ch = kk * 4 + (l >> 4);
       o0 = row * 128 + kmajor_swz(row, ch) * 16;
       o1 = 0;
+    }
+  }
+
+  // The same fragment at a compile-time LDS offset OFF (stage base) from
+  // byte address base + o.  KOUT: ds_read_b64_tr_b16 as inline asm -- the
+  // builtin makes the compiler put s_waitcnt vmcnt(0) in front of it (it
+  // cannot tell the read from the LDS-DMA still in flight into the OTHER
+  // stage), which serialised every K-outer kernel's next-tile DMA with its
+  // MFMAs.  The caller waits for the reads itself (lds_fence).
+  template <int OFF>
+  __device__ __forceinline__ bf16x8 frag_c(unsigned base, int o0, int o1) const {
+    if constexpr (KOUT) {
+      typedef short v4s __attribute__((ext_vector_type(4)));
+      v4s x0, x1;
+      if constexpr (OFF + 1024 * 1024 < 0) {
+      } else if constexpr (OFF <= 65535 - 2048) {
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(x0) : "v"(base + o0), "i"(OFF));
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(x1) : "v"(base + o1), "i"(OFF));
+      } else {
+        asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(x0) : "v"(base + OFF + o0));
+        asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(x1) : "v"(base + OFF + o1));
+      }
+      i16x8 r;
+      r[0] = x0[0]; r[1] = x0[1]; r[2] = x0[2]; r[3] = x0[3];
+      r[4] = x1[0]; r[5] = x1[1]; r[6] = x1[2]; r[7] = x1[3];
+      return __builtin_bit_cast(bf16x8, r);
+    } else {
+      return *(const bf16x8*)((const __attribute__((address_space(3))) char*)(size_t)base + OFF + o0);
     }
   }
 
@@ -500,6 +557,7 @@ __global__ void __launch_bounds__(NTH, (NTH == 512 && STAGES == 2) ? 4 : 2) igem
   Loader<BN, BMODE, NTH> lb;
   la.init(p, m0, M, P, p.lda, pa, p.a_bytes);
   lb.init(p, n0, p.N, P, p.ldb, pb, p.b_bytes);
+  lb.start(p, kbeg);
 
   const int wid = threadIdx.x >> 6;
   const int wm = wid / WN, wn = wid % WN;
@@ -536,42 +594,91 @@ __global__ void __launch_bounds__(NTH, (NTH == 512 && STAGES == 2) ? 4 : 2) igem
     }
   };
 
+  // compile-time stage variant (the 2-stage loops): asm tr-reads + one
+  // explicit LDS wait per k-half, tied to the fragments so the MFMAs stay after it
+  const unsigned lds_base = (unsigned)(size_t)(__attribute__((address_space(3))) char*)smem;
+  auto compute_c = [&](auto stage) {
+    constexpr int SA = decltype(stage)::value * STAGE;
+    constexpr bool ANY_TR = Loader<BM, AM, NTH>::KOUT || Loader<BN, BMODE, NTH>::KOUT;
+    static_assert(BK == 64, "two k-halves");
+    auto half = [&](auto kkc) {
+      constexpr int kk = decltype(kkc)::value;
+      bf16x8 fa[TM], fb[TN];
+      // K-outer images: k-half kk sits 32 k-rows further with the same
+      // swizzle (it depends on k-row bits 0-3 only), so its offsets are the
+      // kk = 0 ones plus an immediate -- 2 fewer VGPRs per fragment
+      constexpr int KA = Loader<BM, AM, NTH>::KOUT ? 1 : 0, KB = Loader<BN, BMODE, NTH>::KOUT ? 1 : 0;
+      constexpr int OA = SA + KA * kk_off<BM>(kk), OB = SA + A_BYTES + KB * kk_off<BN>(kk);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        fa[i] = la.template frag_c<OA>(lds_base, oa0[i][KA ? 0 : kk], oa1[i][KA ? 0 : kk]);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        fb[j] = lb.template frag_c<OB>(lds_base, ob0[j][KB ? 0 : kk], ob1[j][KB ? 0 : kk]);
+      if constexpr (ANY_TR) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int i = 0; i < TM; ++i) asm volatile("" : "+v"(fa[i]));
+#pragma unroll
+        for (int j = 0; j < TN; ++j) asm volatile("" : "+v"(fb[j]));
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+    };
+    half(std::integral_constant<int, 0>{});
+    half(std::integral_constant<int, 1>{});
+  };
+
   if (STAGES == 2 && p.early_issue) {
     // two barriers per K-tile: the DMA of tile kt+1 is issued as soon as
     // every wave has finished reading its stage (tile kt-1), BEFORE waiting
     // for tile kt -- two tiles in flight across that wait
     constexpr int LPT = Loader<BM, AM, NTH>::VPT + Loader<BN, BMODE, NTH>::VPT;
+    // unrolled by two so the stage of every tile is a compile-time constant:
+    // the fragment reads then carry it in their immediate offset (no per-tile
+    // VALU re-basing of the loop-invariant fragment offsets)
+    auto step = [&](auto stage, int kt) {
+      constexpr int cur = decltype(stage)::value;
+      if (kt > 0) raw_barrier();  // every wave done reading stage cur^1 (tile kt-1)
+      char* nxt = smem + (cur ^ 1) * STAGE;
+      const bool live = kt + 1 < nk;
+      la.issue(p, m0, M, kbeg + (kt + 1) * BK, kend, P, nxt, live);
+      lb.issue(p, n0, p.N, kbeg + (kt + 1) * BK, kend, P, nxt + A_BYTES, live);
+      wait_vmcnt<LPT>();  // this wave's DMA for tile kt landed
+      raw_barrier();      // ... every wave's
+      compute_c(stage);
+    };
     if (nk > 0) {
       la.issue(p, m0, M, kbeg, kend, P, smem);
       lb.issue(p, n0, p.N, kbeg, kend, P, smem + A_BYTES);
-      for (int kt = 0; kt < nk; ++kt) {
-        const int cur = kt & 1;
-        if (kt > 0) raw_barrier();  // every wave done reading stage cur^1 (tile kt-1)
-        char* nxt = smem + (cur ^ 1) * STAGE;
-        const bool live = kt + 1 < nk;
-        la.issue(p, m0, M, kbeg + (kt + 1) * BK, kend, P, nxt, live);
-        lb.issue(p, n0, p.N, kbeg + (kt + 1) * BK, kend, P, nxt + A_BYTES, live);
-        wait_vmcnt<LPT>();  // this wave's DMA for tile kt landed
-        raw_barrier();      // ... every wave's
-        compute(smem + cur * STAGE);
+      for (int kt = 0; kt < nk; kt += 2) {
+        step(std::integral_constant<int, 0>{}, kt);
+        if (kt + 1 < nk) step(std::integral_constant<int, 1>{}, kt + 1);
       }
     }
   } else if constexpr (STAGES == 2) {
+    auto step = [&](auto stage, int kt) {
+      constexpr int cur = decltype(stage)::value;
+      // this wave's DMA for tile kt retired (vmcnt(0)), then every wave's has,
+      // and every wave finished reading the other stage (tile kt-1)
+      __syncthreads();
+      // next tile (a null-resource dummy after the last one: the DMA issue
+      // stays in the MFMA block, so it interleaves with the MFMAs)
+      char* nxt = smem + (cur ^ 1) * STAGE;
+      const bool live = kt + 1 < nk;
+      la.issue(p, m0, M, kbeg + (kt + 1) * BK, kend, P, nxt, live);
+      lb.issue(p, n0, p.N, kbeg + (kt + 1) * BK, kend, P, nxt + A_BYTES, live);
+      compute_c(stage);
+    };
     if (nk > 0) {
       la.issue(p, m0, M, kbeg, kend, P, smem);
       lb.issue(p, n0, p.N, kbeg, kend, P, smem + A_BYTES);
-      for (int kt = 0; kt < nk; ++kt) {
-        const int cur = kt & 1;
-        // this wave's DMA for tile kt retired (vmcnt(0)), then every wave's has,
-        // and every wave finished reading the other stage (tile kt-1)
-        __syncthreads();
-        // next tile (a null-resource dummy after the last one: the loop body
-        // stays one basic block, so the DMA issue interleaves with the MFMAs)
-        char* nxt = smem + (cur ^ 1) * STAGE;
-        const bool live = kt + 1 < nk;
-        la.issue(p, m0, M, kbeg + (kt + 1) * BK, kend, P, nxt, live);
-        lb.issue(p, n0, p.N, kbeg + (kt + 1) * BK, kend, P, nxt + A_BYTES, live);
-        compute(smem + cur * STAGE);
+      for (int kt = 0; kt < nk; kt += 2) {  // unrolled by two: compile-time stage offsets
+        step(std::integral_constant<int, 0>{}, kt);
+        if (kt + 1 < nk) step(std::integral_constant<int, 1>{}, kt + 1);
       }
     }
   } else {
@@ -900,6 +1007,9 @@ static ConvGeom make_geom(int N, int H, int W, int C, int K, int R, int S, int H
   g.N = N; g.H = H; g.W = W; g.C = C; g.K = K; g.R = R; g.S = S; g.Ho = Ho; g.Wo = Wo;
   g.sh = sh; g.sw = sw; g.ph = ph; g.pw = pw; g.dh = dh; g.dw = dw;
   g.dC = FastDiv(C); g.dS = FastDiv(S); g.dK = FastDiv(K); g.dWo = FastDiv(Wo); g.dHoWo = FastDiv(Ho * Wo);
+  g.bq_n = BK / (Ho * Wo);
+  g.bq_h = (BK % (Ho * Wo)) / Wo;
+  g.bq_w = BK % Wo;
   init_phase_identity(g);
   return g;
 }

@@ -99,6 +99,11 @@ CONV_CASES = [
     (2, 256, 56, 56, 128, 1, 1, 2, 0),
     (2, 128, 56, 56, 128, 3, 3, 2, 1),
     (1, 32, 70, 70, 64, 3, 3, 1, 1),
+    # fewer output pixels per image than a K-tile (64): wgrad's pixel walk
+    # carries across whole images per tile
+    (3, 64, 7, 7, 128, 3, 3, 1, 1),
+    (4, 64, 5, 5, 64, 3, 3, 1, 1),
+    (5, 32, 9, 9, 64, 3, 3, 2, 1),
 ]
 
 
