@@ -89,6 +89,7 @@ void sg_conv_wgrad(const void*, const void*, void*, int, int, int, int, int, int
                    int, int, int, hipStream_t);
 void sg_set_tuning(int key, int value);
 void sg_bn_set_unroll(int);
+void sg_bn_set_rows_per_thread(int);
 }
 
 static void check_launch(const char* what) {
@@ -298,4 +299,5 @@ PYBIND11_MODULE(_C, m) {
   m.def("zero", [](P p, int64_t bytes, P s) { sg_zero(V(p), bytes, S(s)); CHK("zero"); });
   m.def("set_tuning", [](int key, int value) { sg_set_tuning(key, value); });
   m.def("bn_set_unroll", [](int ur) { sg_bn_set_unroll(ur); });
+  m.def("bn_set_rows_per_thread", [](int rpt) { sg_bn_set_rows_per_thread(rpt); });
 }

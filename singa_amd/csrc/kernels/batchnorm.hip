@@ -303,7 +303,7 @@ __device__ __forceinline__ void bn_apply_row(const float* v0, const float* rv, c
 #pragma unroll
     for (int k = 0; k < V; ++k) v[k] = fmaxf(v[k], 0.f);
   }
-  stv<T, V>(y + o, v);
+  stv_nt<T, V>(y + o, v);
   if (V == 8 && mask) {  // bit k = (stored output of channel c0+k) > 0
     unsigned b = 0;
 #pragma unroll
@@ -312,35 +312,60 @@ __device__ __forceinline__ void bn_apply_row(const float* v0, const float* rv, c
   }
 }
 
+// Rows of one workgroup: rpw > 0 -- the contiguous block [bid*rpw, +rpw)
+// (every workgroup streams one contiguous span; the grid is as large as the
+// tensor needs), rpw == 0 -- the legacy grid-stride walk.  Measured on
+// MI355X (tools/probes/bw_probe.hip, profiles/bw_probe_copy.jsonl): a
+// 1.6 GB copy runs at 6.0-6.5 TB/s with contiguous per-workgroup spans and
+// non-temporal accesses vs 4.5-4.7 TB/s grid-stride over 2048 workgroups.
+struct RowSpan {
+  int64_t r, end, step;
+};
+__device__ __forceinline__ RowSpan row_span(const Tile2D& t, int64_t R, int64_t rpw) {
+  RowSpan s;
+  if (rpw > 0) {
+    const int64_t r0 = (int64_t)blockIdx.x * rpw;
+    s.r = r0 + t.ty;
+    s.end = r0 + rpw < R ? r0 + rpw : R;
+    s.step = t.RT;
+  } else {
+    s.r = (int64_t)blockIdx.x * t.RT + t.ty;
+    s.end = R;
+    s.step = (int64_t)t.RT * gridDim.x;
+  }
+  return s;
+}
+
 template <typename T, int V, int UR>
 __global__ void __launch_bounds__(256) bn_apply_k(const T* __restrict__ x, const float* __restrict__ scale,
                                                   const float* __restrict__ shift, const T* __restrict__ res,
                                                   T* __restrict__ y, uint8_t* __restrict__ mask, int64_t R, int C,
-                                                  int relu) {
+                                                  int relu, int64_t rpw) {
   const Tile2D t = tile2d<V>(C);
   if (!t.cok) return;
   float sc[V], sf[V];
   ldc<V>(scale + t.c0, sc);
   ldc<V>(shift + t.c0, sf);
-  const int64_t step = (int64_t)t.RT * gridDim.x;
-  int64_t r = (int64_t)blockIdx.x * t.RT + t.ty;
-  for (; r + (UR - 1) * step < R; r += UR * step) {
+  RowSpan sp = row_span(t, R, rpw);
+  const int64_t step = sp.step;
+  int64_t r = sp.r;
+  for (; r + (UR - 1) * step < sp.end; r += UR * step) {
     float v[UR][V], rv[UR][V];
 #pragma unroll
-    for (int u = 0; u < UR; ++u) ldv<T, V>(x + (r + u * step) * C + t.c0, v[u]);
+    for (int u = 0; u < UR; ++u) ldv_nt<T, V>(x + (r + u * step) * C + t.c0, v[u]);
     if (res) {
 #pragma unroll
-      for (int u = 0; u < UR; ++u) ldv<T, V>(res + (r + u * step) * C + t.c0, rv[u]);
+      for (int u = 0; u < UR; ++u) ldv_nt<T, V>(res + (r + u * step) * C + t.c0, rv[u]);
     }
 #pragma unroll
     for (int u = 0; u < UR; ++u)
       bn_apply_row<T, V>(v[u], res ? rv[u] : nullptr, sc, sf, y, mask, (r + u * step) * C + t.c0, relu);
   }
-  for (; r < R; r += step) {
+  for (; r < sp.end; r += step) {
     float v[V], rv[V];
     const int64_t o = r * C + t.c0;
-    ldv<T, V>(x + o, v);
-    if (res) ldv<T, V>(res + o, rv);
+    ldv_nt<T, V>(x + o, v);
+    if (res) ldv_nt<T, V>(res + o, rv);
     bn_apply_row<T, V>(v, res ? rv : nullptr, sc, sf, y, mask, o, relu);
   }
 }
@@ -350,9 +375,9 @@ __global__ void __launch_bounds__(256) bn_apply_k(const T* __restrict__ x, const
 template <typename T, int V>
 __device__ __forceinline__ void bn_bwd_load(const T* x, const T* dy, const T* y, int64_t o, int mask_mode, float* v,
                                             float* g, float* yy, unsigned& mb) {
-  ldv<T, V>(x + o, v);
-  ldv<T, V>(dy + o, g);
-  if (mask_mode == MASK_Y) ldv<T, V>(y + o, yy);
+  ldv_nt<T, V>(x + o, v);
+  ldv_nt<T, V>(dy + o, g);
+  if (mask_mode == MASK_Y) ldv_nt<T, V>(y + o, yy);
   else if (V == 8 && mask_mode == MASK_BITS) mb = ((const uint8_t*)y)[o >> 3];
 }
 
@@ -370,11 +395,11 @@ __device__ __forceinline__ void bn_bwd_row(const float* v, float* g, const float
 #pragma unroll
     for (int k = 0; k < V; ++k) g[k] = v[k] * sc[k] + sf[k] > 0.f ? g[k] : 0.f;
   }
-  if (dres) stv<T, V>(dres + o, g);
+  if (dres) stv_nt<T, V>(dres + o, g);
   float o8[V];
 #pragma unroll
   for (int k = 0; k < V; ++k) o8[k] = kk[k] * g[k] + bb[k] * v[k] + aa[k];
-  stv<T, V>(dx + o, o8);
+  stv_nt<T, V>(dx + o, o8);
 }
 
 template <typename T, int V, int UR>
@@ -382,7 +407,8 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_k(const T* __restrict__ x, c
                                                       const T* __restrict__ y, const float* __restrict__ scale,
                                                       const float* __restrict__ shift,
                                                       const float* __restrict__ coef, T* __restrict__ dx,
-                                                      T* __restrict__ dres, int64_t R, int C, int mask_mode) {
+                                                      T* __restrict__ dres, int64_t R, int C, int mask_mode,
+                                                      int64_t rpw) {
   const Tile2D t = tile2d<V>(C);
   if (!t.cok) return;
   float kk[V], bb[V], aa[V], sc[V], sf[V];
@@ -393,9 +419,10 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_k(const T* __restrict__ x, c
     ldc<V>(scale + t.c0, sc);
     ldc<V>(shift + t.c0, sf);
   }
-  const int64_t step = (int64_t)t.RT * gridDim.x;
-  int64_t r = (int64_t)blockIdx.x * t.RT + t.ty;
-  for (; r + (UR - 1) * step < R; r += UR * step) {
+  RowSpan sp = row_span(t, R, rpw);
+  const int64_t step = sp.step;
+  int64_t r = sp.r;
+  for (; r + (UR - 1) * step < sp.end; r += UR * step) {
     float v[UR][V], g[UR][V], yy[UR][V];
     unsigned mb[UR] = {};
 #pragma unroll
@@ -404,7 +431,7 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_k(const T* __restrict__ x, c
     for (int u = 0; u < UR; ++u)
       bn_bwd_row<T, V>(v[u], g[u], yy[u], mb[u], kk, bb, aa, sc, sf, dx, dres, (r + u * step) * C + t.c0, mask_mode);
   }
-  for (; r < R; r += step) {
+  for (; r < sp.end; r += step) {
     float v[V], g[V], yy[V];
     unsigned mb = 0;
     const int64_t o = r * C + t.c0;
@@ -438,7 +465,8 @@ extern "C" int64_t sg_colreduce_ws(int64_t R, int C) {
 }
 extern "C" void sg_bn_set_deterministic(int on) { g_bn_det = on; }
 // Rows per iteration of the HBM-bound apply kernels (1, 2 or 4; 0 = the
-// measured default: 1 for the forward, 2 for the backward apply).
+// measured default: 1, and 2 for the backward apply on the legacy
+// grid-stride walk).
 // tools/bench_bn.py on MI355X (profiles/bn_apply_bandwidth_b512.jsonl): both
 // run at 90-100% of a torch copy's bandwidth (4.5-6.3 TB/s) already with one
 // row in flight; deeper unrolls only add VGPR pressure.
@@ -482,11 +510,23 @@ static inline void colgrid(int64_t R, int C, dim3& grid, int& rpb, int& V) {
   grid = dim3(bands, cblocks);
 }
 
-static inline dim3 apply_grid(int64_t R, int C, int V) {
+// Rows per thread of the contiguous-span apply (0: legacy grid-stride over
+// at most 2048 workgroups).  2 measured best over ResNet-50 shapes
+// (tools/bench_bn.py, profiles/bn_apply_bandwidth_spans_b512.jsonl): +15-30 %
+// over the grid-stride walk, 5.6-6.8 TB/s.
+static int g_bn_rpt = 2;
+extern "C" void sg_bn_set_rows_per_thread(int rpt) { g_bn_rpt = rpt < 0 ? 0 : rpt; }
+static inline dim3 apply_grid(int64_t R, int C, int V, int64_t& rpw) {
   const int chunks = C / V;
   const int CT = chunks < 64 ? chunks : 64;
   const int cblocks = (chunks + CT - 1) / CT;
   const int RT = 256 / CT;
+  if (g_bn_rpt > 0) {
+    rpw = (int64_t)RT * g_bn_rpt;
+    const int64_t rb = (R + rpw - 1) / rpw;
+    return dim3((unsigned)(rb < 1 ? 1 : rb), cblocks);
+  }
+  rpw = 0;
   int64_t rb = (R + RT - 1) / RT;
   int64_t cap = 2048 / cblocks;
   if (cap < 1) cap = 1;
@@ -564,10 +604,11 @@ void sg_bn_infer_params(const void* gamma, const void* beta, const void* run_mea
 void sg_bn_apply(const void* x, const void* scale, const void* shift, const void* res, void* y, void* mask, int64_t R,
                  int C, int relu, int dtype, hipStream_t s) {
   const int V = (C % 8 == 0) ? 8 : 1;
-  dim3 grid = apply_grid(R, C, V);
+  int64_t rpw;
+  dim3 grid = apply_grid(R, C, V, rpw);
   DISPATCH_FT(dtype, DISPATCH_V(V, BN_UR_LAUNCH(bn_apply_k, 1, T, VV, grid, dim3(256), 0, s, (const T*)x,
                                                       (const float*)scale, (const float*)shift, (const T*)res, (T*)y,
-                                                      (uint8_t*)mask, R, C, relu)));
+                                                      (uint8_t*)mask, R, C, relu, rpw)));
 }
 
 // Full BN backward: reduce + finalize (coef, dgamma/dbeta accumulation) + apply.
@@ -587,11 +628,12 @@ void sg_bn_bwd(const void* x, const void* dy, const void* y, const void* scale, 
   hipLaunchKernelGGL(bn_bwd_finalize_k, fin_grid(C), dim3(256), 0, s, (const float*)ws, fin_rows(grid), C,
                      (const float*)gamma, (const float*)mean, (const float*)invstd, (float*)coef, (float*)dg,
                      (float*)db, (float)R);
-  dim3 ag = apply_grid(R, C, V);
-  DISPATCH_FT(dtype, DISPATCH_V(V, BN_UR_LAUNCH(bn_bwd_apply_k, 2, T, VV, ag, dim3(256), 0, s, (const T*)x,
+  int64_t rpw;
+  dim3 ag = apply_grid(R, C, V, rpw);
+  DISPATCH_FT(dtype, DISPATCH_V(V, BN_UR_LAUNCH(bn_bwd_apply_k, g_bn_rpt ? 1 : 2, T, VV, ag, dim3(256), 0, s, (const T*)x,
                                                       (const T*)dy, (const T*)y, (const float*)scale,
                                                       (const float*)shift, (const float*)coef, (T*)dx, (T*)dres, R,
-                                                      C, mask_mode)));
+                                                      C, mask_mode, rpw)));
 }
 
 // BN backward whose reduction was fused into the producing conv dgrad's
@@ -603,11 +645,12 @@ void sg_bn_bwd_from_ws(const void* x, const void* dy, const void* y, const void*
   hipLaunchKernelGGL(bn_bwd_finalize_k, fin_grid(C), dim3(256), 0, s, (const float*)ws, nb, C, (const float*)gamma,
                      (const float*)mean, (const float*)invstd, (float*)coef, (float*)dg, (float*)db, (float)R);
   const int V = (C % 8 == 0) ? 8 : 1;
-  dim3 ag = apply_grid(R, C, V);
-  DISPATCH_FT(dtype, DISPATCH_V(V, BN_UR_LAUNCH(bn_bwd_apply_k, 2, T, VV, ag, dim3(256), 0, s, (const T*)x,
+  int64_t rpw;
+  dim3 ag = apply_grid(R, C, V, rpw);
+  DISPATCH_FT(dtype, DISPATCH_V(V, BN_UR_LAUNCH(bn_bwd_apply_k, g_bn_rpt ? 1 : 2, T, VV, ag, dim3(256), 0, s, (const T*)x,
                                                       (const T*)dy, (const T*)y, (const float*)scale,
                                                       (const float*)shift, (const float*)coef, (T*)dx, (T*)dres, R,
-                                                      C, mask_mode)));
+                                                      C, mask_mode, rpw)));
 }
 
 }  // extern "C"

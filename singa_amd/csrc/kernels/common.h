@@ -139,6 +139,42 @@ __device__ __forceinline__ void stv(T* p, const float* v) {
     for (int i = 0; i < V; ++i) p[i] = from_f32<T>(v[i]);
   }
 }
+// Non-temporal variants for the HBM-streaming passes (BatchNorm apply):
+// tensors far larger than the caches, read or written exactly once
+template <typename T, int V>
+__device__ __forceinline__ void ldv_nt(const T* p, float* v) {
+  if constexpr (V == 8 && sizeof(T) == 2) {
+    bf16x8 t = __builtin_nontemporal_load((const bf16x8*)p);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = (float)t[i];
+  } else if constexpr (V == 8) {
+    typedef float nt4 __attribute__((ext_vector_type(4)));
+    nt4 a = __builtin_nontemporal_load((const nt4*)p), b = __builtin_nontemporal_load((const nt4*)(p + 4));
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[i] = a[i];
+      v[4 + i] = b[i];
+    }
+  } else {
+    ldv<T, V>(p, v);
+  }
+}
+template <typename T, int V>
+__device__ __forceinline__ void stv_nt(T* p, const float* v) {
+  if constexpr (V == 8 && sizeof(T) == 2) {
+    bf16x8 t;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) t[i] = (bf16)v[i];
+    __builtin_nontemporal_store(t, (bf16x8*)p);
+  } else if constexpr (V == 8) {
+    typedef float nt4 __attribute__((ext_vector_type(4)));
+    __builtin_nontemporal_store(nt4{v[0], v[1], v[2], v[3]}, (nt4*)p);
+    __builtin_nontemporal_store(nt4{v[4], v[5], v[6], v[7]}, (nt4*)(p + 4));
+  } else {
+    stv<T, V>(p, v);
+  }
+}
+
 template <int V>
 __device__ __forceinline__ void ldc(const float* p, float* v) {
   if constexpr (V == 8) {

@@ -33,6 +33,8 @@ def _load():
         return _lib
     if os.environ.get("SINGA_AMD_DETERMINISTIC", "0") == "1" and hasattr(_lib, "set_deterministic"):
         _lib.set_deterministic(1)
+    if os.environ.get("SINGA_BN_RPT") and hasattr(_lib, "bn_set_rows_per_thread"):
+        _lib.bn_set_rows_per_thread(int(os.environ["SINGA_BN_RPT"]))  # 0: legacy grid-stride BN apply
     # kernel tuning knobs from the environment: SG_TUNE="0=4,1=1" (key=value)
     for kv in os.environ.get("SG_TUNE", "").split(","):
         if "=" in kv and hasattr(_lib, "set_tuning"):

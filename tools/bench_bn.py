@@ -1,7 +1,9 @@
 """HBM-bandwidth microbenchmark of the BatchNorm apply kernels (forward
 bn_apply with ReLU + 1-bit mask, with/without residual; backward apply with
 mask bits + residual gradient) on ResNet-50 activation shapes, for each
-rows-per-iteration unroll (bn_set_unroll).  Prints achieved GB/s next to a
+(rows per thread of a workgroup's contiguous row span, rows-per-iteration
+unroll) pair: rpt 0 = the legacy grid-stride walk over <= 2048 workgroups
+(bn_set_rows_per_thread, bn_set_unroll).  Prints achieved GB/s next to a
 torch copy of the same tensor as the yardstick."""
 import argparse
 import json
@@ -31,6 +33,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=512)
     ap.add_argument("--out", default="")
+    ap.add_argument("--configs", default="0:1,0:2,2:1,4:1,4:2,8:2,16:2", help="rpt:ur pairs")
     a = ap.parse_args()
     L = N.lib()
     dev = torch.device("cuda:0")
@@ -51,7 +54,9 @@ def main():
         eb = R * C * 2
         t_copy = timeit(lambda: y.copy_(x))
         rec = {"H": H, "C": C, "R": R, "copy_GBs": round(2 * eb / t_copy / 1e9)}
-        for ur in (1, 2, 4):
+        for cfg in a.configs.split(","):
+            rpt, ur = map(int, cfg.split(":"))
+            L.bn_set_rows_per_thread(rpt)
             L.bn_set_unroll(ur)
             t1 = timeit(lambda: L.bn_apply(x.data_ptr(), scale.data_ptr(), shift.data_ptr(), 0, y.data_ptr(), R, C, 1,
                                            N.dt(x), N.stream(), mask.data_ptr()))
@@ -62,11 +67,12 @@ def main():
                                                  gamma.data_ptr(), ws.data_ptr(), 1, coef.data_ptr(), dg.data_ptr(),
                                                  db.data_ptr(), dx.data_ptr(), dres.data_ptr(), R, C, 3, N.dt(x),
                                                  N.stream()))
-            rec[f"ur{ur}"] = {"fwd_GBs": round((2 * eb + eb / 16) / t1 / 1e9),
+            rec[f"rpt{rpt}_ur{ur}"] = {"fwd_GBs": round((2 * eb + eb / 16) / t1 / 1e9),
                               "fwd_res_GBs": round((3 * eb + eb / 16) / t2 / 1e9),
                               "bwd_GBs": round((4 * eb + eb / 16) / t3 / 1e9),
                               "us": [round(t * 1e6, 1) for t in (t1, t2, t3)]}
         L.bn_set_unroll(0)
+        L.bn_set_rows_per_thread(4)
         print(json.dumps(rec), flush=True)
         rows.append(rec)
         del x, res, dy, y, dx, dres, mask
