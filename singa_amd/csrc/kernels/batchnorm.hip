@@ -91,8 +91,8 @@ __global__ void __launch_bounds__(256) colpart_k(const T* __restrict__ x, const 
     // two rows per iteration keeps two independent 16-B loads per stream in flight
     for (; r + t.RT < r1; r += 2 * t.RT) {
       float v0[V], v1[V];
-      ldv<T, V>(x + r * C + t.c0, v0);
-      ldv<T, V>(x + (r + t.RT) * C + t.c0, v1);
+      ldv_nt<T, V>(x + r * C + t.c0, v0);
+      ldv_nt<T, V>(x + (r + t.RT) * C + t.c0, v1);
       if (MODE == 0) {
 #pragma unroll
         for (int i = 0; i < V; ++i) {
@@ -101,12 +101,12 @@ __global__ void __launch_bounds__(256) colpart_k(const T* __restrict__ x, const 
         }
       } else {
         float g0[V], g1[V];
-        ldv<T, V>(dy + r * C + t.c0, g0);
-        ldv<T, V>(dy + (r + t.RT) * C + t.c0, g1);
+        ldv_nt<T, V>(dy + r * C + t.c0, g0);
+        ldv_nt<T, V>(dy + (r + t.RT) * C + t.c0, g1);
         if (mask_mode == MASK_Y) {
           float y0[V], y1[V];
-          ldv<T, V>(y + r * C + t.c0, y0);
-          ldv<T, V>(y + (r + t.RT) * C + t.c0, y1);
+          ldv_nt<T, V>(y + r * C + t.c0, y0);
+          ldv_nt<T, V>(y + (r + t.RT) * C + t.c0, y1);
 #pragma unroll
           for (int i = 0; i < V; ++i) {
             g0[i] = y0[i] > 0.f ? g0[i] : 0.f;
@@ -136,16 +136,16 @@ __global__ void __launch_bounds__(256) colpart_k(const T* __restrict__ x, const 
     }
     for (; r < r1; r += t.RT) {
       float v0[V];
-      ldv<T, V>(x + r * C + t.c0, v0);
+      ldv_nt<T, V>(x + r * C + t.c0, v0);
       if (MODE == 0) {
 #pragma unroll
         for (int i = 0; i < V; ++i) { a0[i] += v0[i]; a1[i] += v0[i] * v0[i]; }
       } else {
         float g0[V];
-        ldv<T, V>(dy + r * C + t.c0, g0);
+        ldv_nt<T, V>(dy + r * C + t.c0, g0);
         if (mask_mode == MASK_Y) {
           float y0[V];
-          ldv<T, V>(y + r * C + t.c0, y0);
+          ldv_nt<T, V>(y + r * C + t.c0, y0);
 #pragma unroll
           for (int i = 0; i < V; ++i) g0[i] = y0[i] > 0.f ? g0[i] : 0.f;
         } else if (V == 8 && mask_mode == MASK_BITS) {
@@ -162,8 +162,13 @@ __global__ void __launch_bounds__(256) colpart_k(const T* __restrict__ x, const 
     }
   }
   // reduce over ty in LDS, then one partial per channel: plain store into
-  // row `band` (deterministic) or atomic add into slot band % 32
+  // row `band` (deterministic) or atomic add into slot band % 32.  Thread j
+  // owns channel offset j of the workgroup's CT*V channels, so each
+  // wave-instruction of atomics covers 256 contiguous bytes (the full-rate
+  // shape for float atomics).
   float* out = ws + (int64_t)(det ? blockIdx.x : (blockIdx.x & (NSLOT - 1))) * 2 * C;
+  const int CW = t.CT * V;                          // channels of this workgroup
+  const int cbase = blockIdx.y * t.CT * V;          // first channel
   for (int pass = 0; pass < 2; ++pass) {
     const float* acc = pass == 0 ? a0 : a1;
     __syncthreads();
@@ -172,19 +177,12 @@ __global__ void __launch_bounds__(256) colpart_k(const T* __restrict__ x, const 
       for (int i = 0; i < V; ++i) red[threadIdx.x * V + i] = acc[i];
     }
     __syncthreads();
-    if (t.ty == 0 && t.c0 < C) {
-      float s[V];
-#pragma unroll
-      for (int i = 0; i < V; ++i) s[i] = red[t.tx * V + i];
-      for (int k = 1; k < t.RT; ++k) {
-#pragma unroll
-        for (int i = 0; i < V; ++i) s[i] += red[(k * t.CT + t.tx) * V + i];
-      }
-#pragma unroll
-      for (int i = 0; i < V; ++i) {
-        if (det) out[pass * C + t.c0 + i] = s[i];
-        else atomicAdd(out + pass * C + t.c0 + i, s[i]);
-      }
+    for (int j = threadIdx.x; j < CW; j += blockDim.x) {
+      if (cbase + j >= C) break;
+      float sum = red[j];
+      for (int k = 1; k < t.RT; ++k) sum += red[k * CW + j];
+      if (det) out[pass * C + cbase + j] = sum;
+      else atomicAdd(out + pass * C + cbase + j, sum);
     }
   }
 }
@@ -505,9 +503,17 @@ static inline void colgrid(int64_t R, int C, dim3& grid, int& rpb, int& V) {
   const int chunks = C / V;
   const int CT = chunks < 64 ? chunks : 64;
   const int cblocks = (chunks + CT - 1) / CT;
-  const int bands = sg_colreduce_bands(R, C);
+  // deterministic: the partial-row workspace is sized by sg_colreduce_bands;
+  // slot atomics: one band per 16 rows per thread (a contiguous span per
+  // workgroup, the grid sized to the tensor -- see bn_apply_k)
+  int64_t bands = sg_colreduce_bands(R, C);
+  if (!g_bn_det) {
+    const int64_t rpw = (int64_t)(256 / CT) * 16;
+    const int64_t nb = (R + rpw - 1) / rpw;
+    if (nb > bands) bands = nb < 1048576 ? nb : 1048576;
+  }
   rpb = (int)((R + bands - 1) / bands);
-  grid = dim3(bands, cblocks);
+  grid = dim3((unsigned)bands, cblocks);
 }
 
 // Rows per thread of the contiguous-span apply (0: legacy grid-stride over
