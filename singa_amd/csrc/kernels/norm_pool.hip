@@ -17,18 +17,16 @@ struct PoolGeom {
   int N, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw;
 };
 
-// thread = (output pixel, V channels); V = 8 when C % 8 == 0
+// One workgroup row of blocks per output row (n, oh): thread item
+// i = ow * CV + cv (V channels each); no 64-bit index division per thread.
 template <typename T, int V>
 __global__ void maxpool_fwd_k(const T* __restrict__ x, T* __restrict__ y, uint8_t* __restrict__ arg, PoolGeom g) {
   const int CV = g.C / V;
-  const int64_t total = (int64_t)g.N * g.Ho * g.Wo * CV;
-  SG_GRID_STRIDE(i, total) {
-    const int cv = (int)(i % CV);
-    const int p = (int)(i / CV);
-    const int ow = p % g.Wo;
-    const int t2 = p / g.Wo;
-    const int oh = t2 % g.Ho;
-    const int n = t2 / g.Ho;
+  const int row = blockIdx.x;  // n * Ho + oh
+  const int n = row / g.Ho, oh = row - n * g.Ho;
+  const int items = g.Wo * CV;
+  for (int i = blockIdx.y * blockDim.x + threadIdx.x; i < items; i += gridDim.y * blockDim.x) {
+    const int ow = i / CV, cv = i - ow * CV;
     float m[V];
     uint8_t best[V];
 #pragma unroll
@@ -36,38 +34,45 @@ __global__ void maxpool_fwd_k(const T* __restrict__ x, T* __restrict__ y, uint8_
     for (int r = 0; r < g.kh; ++r) {
       const int ih = oh * g.sh - g.ph + r;
       if (ih < 0 || ih >= g.H) continue;
+      const T* xr = x + (((int64_t)n * g.H + ih) * g.W) * g.C + cv * V;
       for (int s = 0; s < g.kw; ++s) {
         const int iw = ow * g.sw - g.pw + s;
         if (iw < 0 || iw >= g.W) continue;
         float v[V];
-        ldv<T, V>(x + (((int64_t)n * g.H + ih) * g.W + iw) * g.C + cv * V, v);
+        ldv<T, V>(xr + (int64_t)iw * g.C, v);
 #pragma unroll
         for (int k = 0; k < V; ++k)
           if (v[k] > m[k]) { m[k] = v[k]; best[k] = (uint8_t)(r * g.kw + s); }
       }
     }
-    const int64_t o = (int64_t)p * g.C + cv * V;
+    const int64_t o = ((int64_t)row * g.Wo + ow) * g.C + cv * V;
     stv<T, V>(y + o, m);
     if (arg) {
+      if constexpr (V == 8) {  // the 8 window indices of this vector: one 8-byte store
+        uint2 pk;
+        pk.x = best[0] | (best[1] << 8) | (best[2] << 16) | ((unsigned)best[3] << 24);
+        pk.y = best[4] | (best[5] << 8) | (best[6] << 16) | ((unsigned)best[7] << 24);
+        *(uint2*)(arg + o) = pk;
+      } else {
 #pragma unroll
-      for (int k = 0; k < V; ++k) arg[o + k] = best[k];
+        for (int k = 0; k < V; ++k) arg[o + k] = best[k];
+      }
     }
   }
 }
 
+// One workgroup row of blocks per input row (n, ih): gather the gradient of
+// the windows whose argmax is this pixel.
 template <typename T, int V>
 __global__ void maxpool_bwd_k(const T* __restrict__ dy, const uint8_t* __restrict__ arg, T* __restrict__ dx,
                               PoolGeom g) {
   const int CV = g.C / V;
-  const int64_t total = (int64_t)g.N * g.H * g.W * CV;
-  SG_GRID_STRIDE(i, total) {
-    const int cv = (int)(i % CV);
-    const int p = (int)(i / CV);
-    const int iw = p % g.W;
-    const int t2 = p / g.W;
-    const int ih = t2 % g.H;
-    const int n = t2 / g.H;
-    const int oh0 = max(0, (ih + g.ph - g.kh + g.sh) / g.sh), oh1 = min(g.Ho - 1, (ih + g.ph) / g.sh);
+  const int row = blockIdx.x;  // n * H + ih
+  const int n = row / g.H, ih = row - n * g.H;
+  const int oh0 = max(0, (ih + g.ph - g.kh + g.sh) / g.sh), oh1 = min(g.Ho - 1, (ih + g.ph) / g.sh);
+  const int items = g.W * CV;
+  for (int i = blockIdx.y * blockDim.x + threadIdx.x; i < items; i += gridDim.y * blockDim.x) {
+    const int iw = i / CV, cv = i - iw * CV;
     const int ow0 = max(0, (iw + g.pw - g.kw + g.sw) / g.sw), ow1 = min(g.Wo - 1, (iw + g.pw) / g.sw);
     float acc[V];
 #pragma unroll
@@ -81,12 +86,18 @@ __global__ void maxpool_bwd_k(const T* __restrict__ dy, const uint8_t* __restric
         const int64_t o = (((int64_t)n * g.Ho + oh) * g.Wo + ow) * g.C + cv * V;
         float d[V];
         ldv<T, V>(dy + o, d);
-        const uint8_t want = (uint8_t)(r * g.kw + s);
+        const unsigned want = (unsigned)(r * g.kw + s);
+        if constexpr (V == 8) {
+          const uint2 pk = *(const uint2*)(arg + o);
 #pragma unroll
-        for (int k = 0; k < V; ++k) acc[k] += arg[o + k] == want ? d[k] : 0.f;
+          for (int k = 0; k < V; ++k) acc[k] += (((k < 4 ? pk.x : pk.y) >> (8 * (k & 3))) & 0xffu) == want ? d[k] : 0.f;
+        } else {
+#pragma unroll
+          for (int k = 0; k < V; ++k) acc[k] += arg[o + k] == want ? d[k] : 0.f;
+        }
       }
     }
-    stv<T, V>(dx + (int64_t)p * g.C + cv * V, acc);
+    stv_nt<T, V>(dx + ((int64_t)row * g.W + iw) * g.C + cv * V, acc);
   }
 }
 
@@ -276,7 +287,8 @@ void sg_pool_fwd(const void* x, void* y, void* arg, int N, int H, int W, int C, 
   const int V = (C % 8 == 0) ? 8 : 1;
   const int64_t total = (int64_t)N * Ho * Wo * (C / V);
   if (is_max) {
-    DISPATCH_FT(dtype, DISPATCH_V(V, hipLaunchKernelGGL((maxpool_fwd_k<T, VV>), dim3(sg_grid(total, 256, 16384)),
+    const int ych = (int)(((int64_t)Wo * (C / V) + 255) / 256);
+    DISPATCH_FT(dtype, DISPATCH_V(V, hipLaunchKernelGGL((maxpool_fwd_k<T, VV>), dim3(N * Ho, ych),
                                                         dim3(256), 0, s, (const T*)x, (T*)y, (uint8_t*)arg, g)));
   } else {
     DISPATCH_FT(dtype, DISPATCH_V(V, hipLaunchKernelGGL((avgpool_fwd_k<T, VV>), dim3(sg_grid(total, 256, 16384)),
@@ -289,7 +301,8 @@ void sg_pool_bwd(const void* dy, const void* arg, void* dx, int N, int H, int W,
   const int V = (C % 8 == 0) ? 8 : 1;
   const int64_t total = (int64_t)N * H * W * (C / V);
   if (is_max) {
-    DISPATCH_FT(dtype, DISPATCH_V(V, hipLaunchKernelGGL((maxpool_bwd_k<T, VV>), dim3(sg_grid(total, 256, 16384)),
+    const int ych = (int)(((int64_t)W * (C / V) + 255) / 256);
+    DISPATCH_FT(dtype, DISPATCH_V(V, hipLaunchKernelGGL((maxpool_bwd_k<T, VV>), dim3(N * H, ych),
                                                         dim3(256), 0, s, (const T*)dy, (const uint8_t*)arg, (T*)dx,
                                                         g)));
   } else {
