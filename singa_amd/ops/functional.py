@@ -495,9 +495,11 @@ def conv2d_fwd(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], stri
 # (ds_read_b128 fragments like the forward) instead of transposing them
 # through LDS (ds_read_b64_tr_b16); switchable for A/B measurements
 DGRAD_KMAJOR = os.environ.get("SINGA_AMD_DGRAD_KMAJOR", "1") != "0"
-# a conv dgrad whose input came from a BN+ReLU sums that BN backward's
-# partials in its epilogue (switchable for A/B tests)
-FUSE_BN_BWD_STATS = os.environ.get("SINGA_AMD_FUSE_BN_BWD", "1") != "0"
+# a conv dgrad whose input came from a BN+ReLU can sum that BN backward's
+# partials in its epilogue.  Off by default since the separate reduction
+# streams at 6+ TB/s (contiguous spans, non-temporal loads): ResNet-50 b1024
+# 12.22k img/s unfused vs 11.81k fused (A/B in one session on MI355X)
+FUSE_BN_BWD_STATS = os.environ.get("SINGA_AMD_FUSE_BN_BWD", "0") == "1"
 # residual BN(+ReLU) backward partials in the completing dgrad's epilogue:
 # measured break-even on MI355X (tools/bench_dgrad_bn.py: the extra BN-input
 # read in the epilogue of these one/two-K-tile GEMMs costs what the separate

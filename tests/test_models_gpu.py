@@ -238,6 +238,7 @@ def test_stacked_bottlenecks_inplace_grad_accumulation(gpu):
     dyt = None
 
     from singa_amd.ops import functional as FF
+    fuse0 = FF.FUSE_BN_BWD_STATS
 
     def run(inplace):
         nonlocal dyt
@@ -257,7 +258,7 @@ def test_stacked_bottlenecks_inplace_grad_accumulation(gpu):
         finally:
             AG.training = False
             AG.INPLACE_ACC = True
-            FF.FUSE_BN_BWD_STATS = True
+            FF.FUSE_BN_BWD_STATS = fuse0
             FF.FUSE_RES_BN_BWD = False
         return h, gr
 
