@@ -94,6 +94,7 @@ struct GemmArgs {
   int stats_det;       // 1: row = tile row, plain stores (deterministic); 0: row = tile row % 32, atomics
   int xcd_split;       // split-K: K-slice-major XCD mapping (gridDim.z % 8 == 0, gridDim.y == 1)
   int early_issue;     // 2-stage loop: issue tile kt+1 before waiting for tile kt (two barriers per tile)
+  int nt_out;          // bf16 epilogue: non-temporal output stores
   // stats_mode 1 (dgrad feeding a BN(+ReLU) backward): with g = out * [x*scale+shift > 0]
   // and xhat = (x - mean) * invstd, the epilogue sums (g, g*xhat) per channel
   // into `stats` -- the BN backward's reduction pass, fused
@@ -843,7 +844,8 @@ __global__ void __launch_bounds__(NTH, (NTH == 512 && STAGES == 2) ? 4 : 2) igem
           bf16x8 o;
 #pragma unroll
           for (int r = 0; r < 8; ++r) o[r] = (bf16)(p.relu ? fmaxf(v[r], 0.f) : v[r]);
-          *(bf16x8*)c = o;
+          if (p.nt_out) __builtin_nontemporal_store(o, (bf16x8*)c);
+          else *(bf16x8*)c = o;
           if (bnb) {
             const bf16x8 xb = pre[pass];
 #pragma unroll
@@ -1048,6 +1050,7 @@ static void launch_t(const GemmArgs& p_in, int tiles, int ydim, int zdim, hipStr
   GemmArgs p = p_in;
   p.lds_epilogue = g_tune[1];
   p.early_issue = g_tune[7];
+  p.nt_out = g_tune[6];
   p.xcd_split = (OUT == OUT_F32_ATOMIC && g_tune[2] && ydim == 1 && zdim >= 8 && (zdim & 7) == 0) ? 1 : 0;
   dim3 grid(tiles, ydim, zdim), block(NTH);
   constexpr int stages = STAGES * (BM + BN) * BK * 2;
@@ -1241,6 +1244,15 @@ void sg_conv_fwd(const void* x, const void* w, void* y, const void* bias, int N,
   p.k_per_split = kps(p.K, 1);
   p.a_bytes = extent_bytes((int64_t)N * H * W * C);
   p.b_bytes = extent_bytes((int64_t)K * R * S * C);
+  if (R == 1 && S == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0 && g_tune[6] != 2) {
+    // 1x1 stride-1 conv: the NHWC input IS the [pixels][C] operand -- a plain
+    // K-major GEMM (no im2col gather state: these one/two-K-tile GEMMs are
+    // dominated by their per-tile setup and epilogue)
+    p.lda = C;
+    if (out_mode == OUT_F32) launch<LM_KMAJOR, LM_KMAJOR, OUT_F32>(p, p.M, 1, s, 1, 0);
+    else launch<LM_KMAJOR, LM_KMAJOR, OUT_BF16>(p, p.M, 1, s, 1, 0);
+    return;
+  }
   if (out_mode == OUT_F32) launch<LM_CONV_FWD, LM_KMAJOR, OUT_F32>(p, p.M, 1, s, 1, 0);
   else launch<LM_CONV_FWD, LM_KMAJOR, OUT_BF16>(p, p.M, 1, s, 1, 0);
 }
@@ -1299,6 +1311,28 @@ void sg_conv_dgrad_bn_ex(const void* dy, const void* w, void* dx, int N, int H, 
     if (!sg_ws_prezeroed()) sg_zero_async(bn_ws, sizeof(float) * 32 * 2 * C, s);
   }
   p.g = make_geom(N, H, W, C, K, R, S, Ho, Wo, sh, sw, ph, pw, dh, dw);
+  if (R == 1 && S == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0 && g_tune[6] != 2) {
+    // 1x1 stride-1: dx[M][C] = dy[M][K] W[K][C], a plain GEMM (dy K-major;
+    // W K-outer, or K-major through the transposed copy)
+    p.M = N * H * W; p.N = C; p.K = K;
+    p.a = (const bf16*)dy; p.lda = K;
+    p.c = dx; p.ldc = C; p.alpha = 1.f; p.beta = beta; p.bias = nullptr; p.relu = 0;
+    p.k_per_split = kps(p.K, 1);
+    p.a_bytes = extent_bytes((int64_t)p.M * K);
+    p.b_bytes = extent_bytes((int64_t)K * C);
+    if (wt && (K & 63) == 0) {
+      hipLaunchKernelGGL(wt_transpose_k, dim3((C + 63) / 64, (K + 63) / 64, 1), dim3(256), 0, s, (const bf16*)w,
+                         (bf16*)wt, K, 1, C);
+      p.b = (const bf16*)wt; p.ldb = K;
+      if (out_mode == OUT_F32) launch<LM_KMAJOR, LM_KMAJOR, OUT_F32>(p, p.M, 1, s, 1, 0);
+      else launch<LM_KMAJOR, LM_KMAJOR, OUT_BF16>(p, p.M, 1, s, 1, 0);
+    } else {
+      p.b = (const bf16*)w; p.ldb = C;
+      if (out_mode == OUT_F32) launch<LM_KMAJOR, LM_KOUTER, OUT_F32>(p, p.M, 1, s, 1, 0);
+      else launch<LM_KMAJOR, LM_KOUTER, OUT_BF16>(p, p.M, 1, s, 1, 0);
+    }
+    return;
+  }
   const int np = make_phases(p.g);
   int Mmax = 0;
   for (int i = 0; i < np; ++i) Mmax = Mmax > N * p.g.phs[i].Hp * p.g.phs[i].Wp ? Mmax : N * p.g.phs[i].Hp * p.g.phs[i].Wp;
