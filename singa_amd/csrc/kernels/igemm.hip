@@ -94,7 +94,6 @@ struct GemmArgs {
   int stats_det;       // 1: row = tile row, plain stores (deterministic); 0: row = tile row % 32, atomics
   int xcd_split;       // split-K: K-slice-major XCD mapping (gridDim.z % 8 == 0, gridDim.y == 1)
   int early_issue;     // 2-stage loop: issue tile kt+1 before waiting for tile kt (two barriers per tile)
-  int nt_out;          // bf16 epilogue: non-temporal output stores
   // stats_mode 1 (dgrad feeding a BN(+ReLU) backward): with g = out * [x*scale+shift > 0]
   // and xhat = (x - mean) * invstd, the epilogue sums (g, g*xhat) per channel
   // into `stats` -- the BN backward's reduction pass, fused
@@ -503,7 +502,7 @@ __device__ __forceinline__ void raw_barrier() {
 // the younger tiles still in flight) and a raw barrier (every wave's DMA
 // retired, every wave done reading the stage about to be refilled).
 template <int BM, int BN, int AM, int BMODE, int OUT, int NTH = NT, int WM = 2, int WN = 2, int STAGES = 2>
-__global__ void __launch_bounds__(NTH, (NTH == 512 && STAGES == 2) ? 4 : 2) igemm_k(const GemmArgs p) {
+__global__ void __launch_bounds__(NTH, STAGES == 1 ? 4 : (NTH == 512 && STAGES == 2) ? 4 : 2) igemm_k(const GemmArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
   constexpr int STAGE = A_BYTES + B_BYTES;
@@ -633,7 +632,17 @@ __global__ void __launch_bounds__(NTH, (NTH == 512 && STAGES == 2) ? 4 : 2) igem
     half(std::integral_constant<int, 1>{});
   };
 
-  if (STAGES == 2 && p.early_issue) {
+  if constexpr (STAGES == 1) {
+    // single stage (the short-K variant: one or two K-tiles, four workgroups
+    // per CU hide each other's load latency instead of double buffering)
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt > 0) __syncthreads();  // every wave done reading the stage
+      la.issue(p, m0, M, kbeg + kt * BK, kend, P, smem);
+      lb.issue(p, n0, p.N, kbeg + kt * BK, kend, P, smem + A_BYTES);
+      __syncthreads();  // (drains this wave's DMA: vmcnt(0)) ... and every wave's
+      compute_c(std::integral_constant<int, 0>{});
+    }
+  } else if (STAGES == 2 && p.early_issue) {
     // two barriers per K-tile: the DMA of tile kt+1 is issued as soon as
     // every wave has finished reading its stage (tile kt-1), BEFORE waiting
     // for tile kt -- two tiles in flight across that wait
@@ -751,7 +760,9 @@ __global__ void __launch_bounds__(NTH, (NTH == 512 && STAGES == 2) ? 4 : 2) igem
     // beta*C + ReLU round to bf16 once.
     if ((p.N & 7) == 0 && (p.ldc & 7) == 0 && p.lds_epilogue) {
       constexpr int LDT = BN + 4;  // fp32 row stride (+16 B against bank conflicts)
+      constexpr int LDT16 = BN + 8;  // bf16 staging (single-stage variant, beta == 0): row stride +16 B
       float* tile = (float*)smem;
+      bf16* tile16 = (bf16*)smem;
       __syncthreads();  // all waves are done reading the last operand stage
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
@@ -765,7 +776,15 @@ __global__ void __launch_bounds__(NTH, (NTH == 512 && STAGES == 2) ? 4 : 2) igem
           if (p.bias && n < p.N) {
             v.x += p.bias[n]; v.y += p.bias[n + 1]; v.z += p.bias[n + 2]; v.w += p.bias[n + 3];
           }
-          *(float4*)(tile + ml * LDT + nl) = v;
+          if constexpr (STAGES == 1) {
+            // rounded to bf16 once here: with beta == 0 (host-checked) the
+            // value is final up to the ReLU, which commutes with the rounding
+            bf16x4 o;
+            o[0] = (bf16)v.x; o[1] = (bf16)v.y; o[2] = (bf16)v.z; o[3] = (bf16)v.w;
+            *(bf16x4*)(tile16 + ml * LDT16 + nl) = o;
+          } else {
+            *(float4*)(tile + ml * LDT + nl) = v;
+          }
         }
       }
       __syncthreads();
@@ -832,9 +851,16 @@ __global__ void __launch_bounds__(NTH, (NTH == 512 && STAGES == 2) ? 4 : 2) igem
           const int ml = r0 + pass * RPP;
           if (!rok[pass]) continue;
           const int64_t rowoff = rofs[pass];
-          const float4 a = *(const float4*)(tile + ml * LDT + ch * 8);
-          const float4 b = *(const float4*)(tile + ml * LDT + ch * 8 + 4);
-          float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+          float v[8];
+          if constexpr (STAGES == 1) {
+            const bf16x8 t8 = *(const bf16x8*)(tile16 + ml * LDT16 + ch * 8);
+#pragma unroll
+            for (int r = 0; r < 8; ++r) v[r] = (float)t8[r];
+          } else {
+            const float4 a = *(const float4*)(tile + ml * LDT + ch * 8);
+            const float4 b = *(const float4*)(tile + ml * LDT + ch * 8 + 4);
+            v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+          }
           bf16* c = (bf16*)pc + rowoff + n;
           if (p.beta != 0.f) {
             const bf16x8 old = bnb ? pold[pass] : pre[pass];
@@ -844,8 +870,7 @@ __global__ void __launch_bounds__(NTH, (NTH == 512 && STAGES == 2) ? 4 : 2) igem
           bf16x8 o;
 #pragma unroll
           for (int r = 0; r < 8; ++r) o[r] = (bf16)(p.relu ? fmaxf(v[r], 0.f) : v[r]);
-          if (p.nt_out) __builtin_nontemporal_store(o, (bf16x8*)c);
-          else *(bf16x8*)c = o;
+          *(bf16x8*)c = o;
           if (bnb) {
             const bf16x8 xb = pre[pass];
 #pragma unroll
@@ -1042,19 +1067,25 @@ static int make_phases(ConvGeom& g) {
 // bf16 epilogue, 2 = K-slice-major XCD mapping of split-K launches, 3 = wgrad
 // split-count scale (2^v), 4 = forced tile shape (5/6/7: the 8-wave variants
 // of pick_big at any size), 5 = 8-wave tiles for non-split launches (pick_big),
-// 6 = unused, 7 = early DMA issue in the 2-stage loop (measured -3.5 % conv time)
-static int g_tune[8] = {5, 1, 1, 0, 0, 1, 0, 1};
+// 6 = single-stage short-K variant for GEMMs of at most this many K-tiles
+// (0 = off), 7 = early DMA issue in the 2-stage loop (measured -3.5 % conv time)
+static int g_tune[8] = {5, 1, 1, 0, 0, 1, 2, 1};
+
+constexpr int stages_c(int BM, int BN, int STAGES) { return STAGES * (BM + BN) * BK * 2; }
 
 template <int BM, int BN, int AM, int BMODE, int OUT, int NTH = NT, int WM = 2, int WN = 2, int STAGES = 2>
 static void launch_t(const GemmArgs& p_in, int tiles, int ydim, int zdim, hipStream_t s) {
   GemmArgs p = p_in;
   p.lds_epilogue = g_tune[1];
   p.early_issue = g_tune[7];
-  p.nt_out = g_tune[6];
   p.xcd_split = (OUT == OUT_F32_ATOMIC && g_tune[2] && ydim == 1 && zdim >= 8 && (zdim & 7) == 0) ? 1 : 0;
   dim3 grid(tiles, ydim, zdim), block(NTH);
   constexpr int stages = STAGES * (BM + BN) * BK * 2;
-  constexpr int etile = (OUT == OUT_BF16 || OUT == OUT_F32_ATOMIC) ? BM * (BN + 4) * 4 : 0;  // fp32 epilogue tile
+  constexpr int etile = STAGES == 1 ? (OUT == OUT_BF16 ? BM * (BN + 8) * 2 : BM * (BN + 4) * 4)  // bf16 staging
+                        : (OUT == OUT_BF16 || OUT == OUT_F32_ATOMIC) ? BM * (BN + 4) * 4 : 0;  // fp32 epilogue tile
+  constexpr int ered = (OUT == OUT_BF16) ? NTH * 16 * 4 : 0;  // BN-stats reduction scratch
+  static_assert(STAGES != 1 || (OUT == OUT_BF16 && ered <= (etile > stages_c(BM, BN, STAGES) ? etile : stages_c(BM, BN, STAGES))),
+                "single-stage variant: bf16 output only");
   constexpr int lds = stages > etile ? stages : etile;
   static_assert(lds <= 160 * 1024, "LDS budget");
   auto* kern = igemm_k<BM, BN, AM, BMODE, OUT, NTH, WM, WN, STAGES>;
@@ -1140,8 +1171,15 @@ static void launch(const GemmArgs& p, int M, int splits, hipStream_t s, int batc
   int BM, BN;
   if constexpr (OUT != OUT_F32_ATOMIC) {
     {
-      const int big = pick_big(M, p.N);
       const int z = zdim > 0 ? zdim : 1;
+      if (OUT == OUT_BF16 && g_tune[6] > 0 && g_tune[4] == 0 && p.beta == 0.f &&
+          (p.K + BK - 1) / BK <= g_tune[6] && p.N >= 128 && !((p.N % 128) != 0 && (p.N % 128) <= 64) &&
+          (long)((M + 127) / 128) * ((p.N + 127) / 128) >= 1024) {
+        const int tiles = ((M + 127) / 128) * ((p.N + 127) / 128);
+        launch_t<128, 128, AM, BMODE, OUT_BF16, 256, 2, 2, 1>(p, tiles, batch, z, s);
+        return;
+      }
+      const int big = pick_big(M, p.N);
       if (big == 1) {
         const int tiles = ((M + 127) / 128) * ((p.N + 127) / 128);
         launch_t<128, 128, AM, BMODE, OUT, 512, 2, 4, 2>(p, tiles, batch, z, s);
@@ -1244,7 +1282,7 @@ void sg_conv_fwd(const void* x, const void* w, void* y, const void* bias, int N,
   p.k_per_split = kps(p.K, 1);
   p.a_bytes = extent_bytes((int64_t)N * H * W * C);
   p.b_bytes = extent_bytes((int64_t)K * R * S * C);
-  if (R == 1 && S == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0 && g_tune[6] != 2) {
+  if (R == 1 && S == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0) {
     // 1x1 stride-1 conv: the NHWC input IS the [pixels][C] operand -- a plain
     // K-major GEMM (no im2col gather state: these one/two-K-tile GEMMs are
     // dominated by their per-tile setup and epilogue)
@@ -1311,7 +1349,7 @@ void sg_conv_dgrad_bn_ex(const void* dy, const void* w, void* dx, int N, int H, 
     if (!sg_ws_prezeroed()) sg_zero_async(bn_ws, sizeof(float) * 32 * 2 * C, s);
   }
   p.g = make_geom(N, H, W, C, K, R, S, Ho, Wo, sh, sw, ph, pw, dh, dw);
-  if (R == 1 && S == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0 && g_tune[6] != 2) {
+  if (R == 1 && S == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0) {
     // 1x1 stride-1: dx[M][C] = dy[M][K] W[K][C], a plain GEMM (dy K-major;
     // W K-outer, or K-major through the transposed copy)
     p.M = N * H * W; p.N = C; p.K = K;
