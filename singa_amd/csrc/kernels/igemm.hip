@@ -502,7 +502,7 @@ __device__ __forceinline__ void raw_barrier() {
 // the younger tiles still in flight) and a raw barrier (every wave's DMA
 // retired, every wave done reading the stage about to be refilled).
 template <int BM, int BN, int AM, int BMODE, int OUT, int NTH = NT, int WM = 2, int WN = 2, int STAGES = 2>
-__global__ void __launch_bounds__(NTH, STAGES == 1 ? 4 : (NTH == 512 && STAGES == 2) ? 4 : 2) igemm_k(const GemmArgs p) {
+__global__ void __launch_bounds__(NTH, STAGES == 1 ? 3 : (NTH == 512 && STAGES == 2) ? 4 : 2) igemm_k(const GemmArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
   constexpr int STAGE = A_BYTES + B_BYTES;
