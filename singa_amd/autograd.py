@@ -703,6 +703,35 @@ class BatchNorm2d(Operator):
         return tuple(out)
 
 
+class BnReluMaxPool(Operator):
+    """max_pool(relu(BatchNorm(x))) as one forward pass (a ResNet stem): the
+    full-resolution BN output is never written.  Inputs x, gamma, beta; the
+    backward gathers the pooled gradient through the argmax, then runs the BN
+    backward with the ReLU mask recomputed from x."""
+
+    def __init__(self, running_mean: torch.Tensor, running_var: torch.Tensor, momentum: float, eps: float,
+                 kernel, stride, padding, name=None):
+        super().__init__(name)
+        self.rm, self.rv = running_mean, running_var
+        self.momentum, self.eps = momentum, eps
+        self.kernel, self.stride, self.padding = tuple(kernel), tuple(stride), tuple(padding)
+
+    def forward(self, x, gamma, beta):
+        y, arg, st = F.bn_relu_maxpool_fwd(x, gamma, beta, self.rm, self.rv, training, self.momentum, self.eps,
+                                           self.kernel, self.stride, self.padding)
+        if self.requires_grad:
+            self.x, self.gamma, self.st, self.arg = x, gamma, st, arg
+        return y
+
+    def backward(self, dy):
+        dpre = F.pool2d_bwd(self.x.shape, self.x, dy, self.arg, self.kernel, self.stride, self.padding, True)
+        tg, tb = self.grad_target(1), self.grad_target(2)
+        dx, dg, db, _ = F.batchnorm_bwd(self.x, dpre, self.gamma, self.st, None, need_dres=False, relu=True,
+                                        dg_out=tg, db_out=tb)
+        self.x = self.st = self.arg = None
+        return dx, ACCUMULATED if tg is not None else dg, ACCUMULATED if tb is not None else db
+
+
 class Pooling2d(Operator):
     def __init__(self, kernel, stride, padding=(0, 0), is_max=True, count_include_pad=True, ceil_mode=False,
                  name=None):

@@ -28,6 +28,8 @@ void sg_dropout_fwd(const void*, void*, void*, int64_t, int, float, uint64_t, ui
 void sg_dropout_bwd(const void*, const void*, void*, int64_t, int, float, hipStream_t);
 void sg_rand_fill(void*, int64_t, int, int, float, float, uint64_t, uint64_t, hipStream_t);
 void sg_nchw_to_nhwc_pad(const void*, void*, int, int, int, int, int, hipStream_t);
+void sg_bn_relu_maxpool(const void*, const void*, const void*, void*, void*, int, int, int, int, int, int, int, int, int,
+                        int, int, int, hipStream_t);
 void sg_nchw_to_pairs(const void*, void*, int, int, int, int, hipStream_t);
 void sg_softmax_fwd(const void*, void*, int64_t, int, int, int, hipStream_t);
 void sg_softmax_bwd(const void*, const void*, void*, int64_t, int, int, hipStream_t);
@@ -144,6 +146,11 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("rand_fill", [](P y, int64_t n, int dt, int dist, float a, float b, uint64_t seed, uint64_t off, P s) {
     sg_rand_fill(V(y), n, dt, dist, a, b, seed, off, S(s)); CHK("rand_fill");
+  });
+  m.def("bn_relu_maxpool", [](P x, P scale, P shift, P y, P arg, int N, int H, int W, int C, int Ho, int Wo, int kh,
+                              int kw, int sh, int sw, int ph, int pw, P s) {
+    sg_bn_relu_maxpool(CV(x), CV(scale), CV(shift), V(y), V(arg), N, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw, S(s));
+    CHK("bn_relu_maxpool");
   });
   m.def("nchw_to_pairs", [](P x, P y, int N, int C, int H, int W, P s) {
     sg_nchw_to_pairs(CV(x), V(y), N, C, H, W, S(s)); CHK("nchw_to_pairs");

@@ -61,6 +61,53 @@ __global__ void maxpool_fwd_k(const T* __restrict__ x, T* __restrict__ y, uint8_
   }
 }
 
+// Fused BatchNorm-apply + ReLU + max pooling (the ResNet stem): the window
+// maximum of bf16(relu(x*scale + shift)) -- the same bf16 values a separate
+// BN+ReLU pass would write -- with the argmax for the backward gather; the
+// full-resolution BN output is never written (its ReLU mask is recomputed from
+// x in the BN backward).  bf16, C % 8 == 0.
+__global__ void bn_relu_maxpool_fwd_k(const bf16* __restrict__ x, const float* __restrict__ scale,
+                                      const float* __restrict__ shift, bf16* __restrict__ y,
+                                      uint8_t* __restrict__ arg, PoolGeom g) {
+  constexpr int V = 8;
+  const int CV = g.C / V;
+  const int row = blockIdx.x;  // n * Ho + oh
+  const int n = row / g.Ho, oh = row - n * g.Ho;
+  const int items = g.Wo * CV;
+  for (int i = blockIdx.y * blockDim.x + threadIdx.x; i < items; i += gridDim.y * blockDim.x) {
+    const int ow = i / CV, cv = i - ow * CV;
+    float sc[V], sf[V];
+    ldc<V>(scale + cv * V, sc);
+    ldc<V>(shift + cv * V, sf);
+    float m[V];
+    uint8_t best[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) { m[k] = -INFINITY; best[k] = 0; }
+    for (int r = 0; r < g.kh; ++r) {
+      const int ih = oh * g.sh - g.ph + r;
+      if (ih < 0 || ih >= g.H) continue;
+      const bf16* xr = x + (((int64_t)n * g.H + ih) * g.W) * g.C + cv * V;
+      for (int s = 0; s < g.kw; ++s) {
+        const int iw = ow * g.sw - g.pw + s;
+        if (iw < 0 || iw >= g.W) continue;
+        float v[V];
+        ldv<bf16, V>(xr + (int64_t)iw * g.C, v);
+#pragma unroll
+        for (int k = 0; k < V; ++k) {
+          const float b = (float)(bf16)fmaxf(v[k] * sc[k] + sf[k], 0.f);
+          if (b > m[k]) { m[k] = b; best[k] = (uint8_t)(r * g.kw + s); }
+        }
+      }
+    }
+    const int64_t o = ((int64_t)row * g.Wo + ow) * g.C + cv * V;
+    stv<bf16, V>(y + o, m);
+    uint2 pk;
+    pk.x = best[0] | (best[1] << 8) | (best[2] << 16) | ((unsigned)best[3] << 24);
+    pk.y = best[4] | (best[5] << 8) | (best[6] << 16) | ((unsigned)best[7] << 24);
+    *(uint2*)(arg + o) = pk;
+  }
+}
+
 // One workgroup row of blocks per input row (n, ih): gather the gradient of
 // the windows whose argmax is this pixel.
 template <typename T, int V>
@@ -309,6 +356,13 @@ void sg_pool_bwd(const void* dy, const void* arg, void* dx, int N, int H, int W,
     DISPATCH_FT(dtype, DISPATCH_V(V, hipLaunchKernelGGL((avgpool_bwd_k<T, VV>), dim3(sg_grid(total, 256, 16384)),
                                                         dim3(256), 0, s, (const T*)dy, (T*)dx, g, count_pad)));
   }
+}
+void sg_bn_relu_maxpool(const void* x, const void* scale, const void* shift, void* y, void* arg, int N, int H, int W,
+                        int C, int Ho, int Wo, int kh, int kw, int sh, int sw, int ph, int pw, hipStream_t s) {
+  PoolGeom g{N, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw};
+  const int ych = (int)(((int64_t)Wo * (C / 8) + 255) / 256);
+  hipLaunchKernelGGL(bn_relu_maxpool_fwd_k, dim3(N * Ho, ych), dim3(256), 0, s, (const bf16*)x, (const float*)scale,
+                     (const float*)shift, (bf16*)y, (uint8_t*)arg, g);
 }
 void sg_gap_fwd(const void* x, void* y, int N, int HW, int C, int dtype, hipStream_t s) {
   if (C % 8 == 0) {

@@ -238,8 +238,19 @@ class ResNet(model.Model):
 
     def forward(self, x):
         self.conv1.compute_dtype = self.compute_dtype
-        x = self.bn1(self.conv1(x), relu=True)  # the stem converts the fp32 NCHW batch itself
-        x = self.maxpool(x)
+        x = self.conv1(x)  # the stem converts the fp32 NCHW batch itself
+        mp = self.maxpool
+        if (os.environ.get("SINGA_FUSED_STEM_POOL", "1") != "0" and not autograd._TRACE and mp.is_max
+                and F.bn_relu_maxpool_ok(x.data, mp.kernel_size, mp.stride, mp.padding, mp.ceil_mode)):
+            # BN + ReLU + max-pool in one pass (the 112x112x64 BN output is never written)
+            bn = self.bn1
+            if not bn._initialized:
+                bn.initialize(x)
+                bn._initialized = True
+            x = autograd.BnReluMaxPool(bn.running_mean.data, bn.running_var.data, 1.0 - bn.momentum, bn.eps,
+                                       mp.kernel_size, mp.stride, mp.padding)(x, bn.scale, bn.bias)
+        else:
+            x = self.maxpool(self.bn1(x, relu=True))
         for b in self.blocks:
             x = b(x)
         x = self.pool(x)

@@ -748,6 +748,58 @@ def _bn_native(x: torch.Tensor) -> bool:
     return _native_ok(x) and _flat_ok(x) and ((x.dim() == 2 and x.is_contiguous()) or N.is_cl(x))
 
 
+def _bn_params(x: torch.Tensor, gamma, beta, run_mean, run_var, training: bool, momentum: float, eps: float):
+    """Native path: (mean, invstd, scale, shift) of a BN over x (training:
+    batch statistics -- from the producing conv's epilogue sums when present
+    -- and a running-stat update; inference: running statistics)."""
+    L = N.lib()
+    C = x.shape[1]
+    R = x.numel() // C
+    dev = x.device
+    p = torch.empty(4 * C, dtype=torch.float32, device=dev)
+    mean, invstd, scale, shift = p[:C], p[C:2 * C], p[2 * C:3 * C], p[3 * C:]
+    pre = getattr(x, "_sg_bn_ws", None)  # statistics already summed by the producing conv's epilogue
+    if training and pre is not None and pre[0].numel() == pre[1] * 2 * C:
+        L.bn_fwd_from_ws(pre[0].data_ptr(), pre[1], gamma.data_ptr(), beta.data_ptr(), run_mean.data_ptr(),
+                         run_var.data_ptr(), mean.data_ptr(), invstd.data_ptr(), scale.data_ptr(),
+                         shift.data_ptr(), R, C, momentum, eps, N.stream())
+    elif training:
+        L.bn_fwd_stats(x.data_ptr(), _ws(R, C, dev).data_ptr(), gamma.data_ptr(), beta.data_ptr(),
+                       run_mean.data_ptr(), run_var.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
+                       scale.data_ptr(), shift.data_ptr(), R, C, momentum, eps, N.dt(x), N.stream())
+    else:
+        L.bn_infer_params(gamma.data_ptr(), beta.data_ptr(), run_mean.data_ptr(), run_var.data_ptr(),
+                          scale.data_ptr(), shift.data_ptr(), mean.data_ptr(), invstd.data_ptr(), C, eps,
+                          N.stream())
+    return mean, invstd, scale, shift
+
+
+def bn_relu_maxpool_ok(x: torch.Tensor, kernel, stride, padding, ceil_mode: bool = False) -> bool:
+    """The fused BN+ReLU+max-pool kernel applies (bf16 NHWC, C % 8 == 0, windows < 256 taps)."""
+    return (_bn_native(x) and x.dim() == 4 and x.dtype == torch.bfloat16 and N.is_cl(x) and x.shape[1] % 8 == 0
+            and not ceil_mode and kernel[0] * kernel[1] < 256)
+
+
+def bn_relu_maxpool_fwd(x: torch.Tensor, gamma, beta, run_mean, run_var, training: bool, momentum: float,
+                        eps: float, kernel, stride, padding):
+    """max_pool(relu(BN(x))) in one pass over x (native, see bn_relu_maxpool_ok).
+    Returns (y, arg, BNState): the BN output itself is never materialised;
+    the backward is pool2d_bwd (argmax gather) then batchnorm_bwd with the
+    ReLU mask recomputed from x."""
+    mean, invstd, scale, shift = _bn_params(x, gamma, beta, run_mean, run_var, training, momentum, eps)
+    kh, kw = kernel
+    sh, sw = stride
+    ph, pw = padding
+    Nn, C, H, W = x.shape
+    Ho = (H + 2 * ph - kh) // sh + 1
+    Wo = (W + 2 * pw - kw) // sw + 1
+    y = torch.empty((Nn, C, Ho, Wo), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+    arg = torch.empty((Nn, Ho, Wo, C), dtype=torch.uint8, device=x.device)
+    N.lib().bn_relu_maxpool(x.data_ptr(), scale.data_ptr(), shift.data_ptr(), y.data_ptr(), arg.data_ptr(), Nn, H, W,
+                            C, Ho, Wo, kh, kw, sh, sw, ph, pw, N.stream())
+    return y, arg, BNState(mean, invstd, scale, shift, None)
+
+
 def batchnorm_fwd(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, run_mean: torch.Tensor,
                   run_var: torch.Tensor, training: bool, momentum: float = 0.1, eps: float = 1e-5,
                   relu: bool = False, residual: Optional[torch.Tensor] = None, want_mask: bool = False):
@@ -760,21 +812,7 @@ def batchnorm_fwd(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, run_
         L = N.lib()
         R = x.numel() // C
         dev = x.device
-        p = torch.empty(4 * C, dtype=torch.float32, device=dev)
-        mean, invstd, scale, shift = p[:C], p[C:2 * C], p[2 * C:3 * C], p[3 * C:]
-        pre = getattr(x, "_sg_bn_ws", None)  # statistics already summed by the producing conv's epilogue
-        if training and pre is not None and pre[0].numel() == pre[1] * 2 * C:
-            L.bn_fwd_from_ws(pre[0].data_ptr(), pre[1], gamma.data_ptr(), beta.data_ptr(), run_mean.data_ptr(),
-                             run_var.data_ptr(), mean.data_ptr(), invstd.data_ptr(), scale.data_ptr(),
-                             shift.data_ptr(), R, C, momentum, eps, N.stream())
-        elif training:
-            L.bn_fwd_stats(x.data_ptr(), _ws(R, C, dev).data_ptr(), gamma.data_ptr(), beta.data_ptr(),
-                           run_mean.data_ptr(), run_var.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
-                           scale.data_ptr(), shift.data_ptr(), R, C, momentum, eps, N.dt(x), N.stream())
-        else:
-            L.bn_infer_params(gamma.data_ptr(), beta.data_ptr(), run_mean.data_ptr(), run_var.data_ptr(),
-                              scale.data_ptr(), shift.data_ptr(), mean.data_ptr(), invstd.data_ptr(), C, eps,
-                              N.stream())
+        mean, invstd, scale, shift = _bn_params(x, gamma, beta, run_mean, run_var, training, momentum, eps)
         res = None
         if residual is not None:
             res = residual

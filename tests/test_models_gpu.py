@@ -450,3 +450,53 @@ def test_paired_stem_matches_torch_fp32(gpu, hw):
     assert y.shape == ref.shape
     assert rel_err(y.data.float(), ref.detach()) < 1e-2
     assert rel_err(grads[id(conv.W)].reshape(wr.shape), wr.grad) < 1e-2
+
+
+def test_fused_stem_bn_relu_maxpool_matches_unfused(gpu, monkeypatch):
+    """The fused stem BN+ReLU+max-pool (BnReluMaxPool: one pass, argmax
+    gather in the backward, ReLU mask from x) trains exactly like the separate
+    BN+ReLU and max-pool ops: bitwise-equal loss trajectories in deterministic
+    mode, and the fused op really ran."""
+    import singa_amd
+    from singa_amd import autograd as AG
+    from singa_amd.models import resnet
+
+    singa_amd.set_deterministic(True)
+    rng = np.random.RandomState(1)
+    X = rng.randn(8, 3, 64, 64).astype(np.float32)
+    Y = rng.randint(0, 10, 8).astype(np.int32)
+    curves, init = [], None
+    seen = []
+    orig = AG.BnReluMaxPool.forward
+
+    def spy(self, *a):
+        seen.append(1)
+        return orig(self, *a)
+
+    monkeypatch.setattr(AG.BnReluMaxPool, "forward", spy)
+    try:
+        for fused in ("0", "1"):
+            monkeypatch.setenv("SINGA_FUSED_STEM_POOL", fused)
+            dev = device.create_rocm_gpu()
+            dev.SetRandSeed(0)
+            m = resnet.create_model(18, num_classes=10, compute_dtype=torch.bfloat16)
+            m.set_optimizer(opt.SGD(0.005, 0.9, weight_decay=1e-4))
+            x = tensor.from_numpy(X, dev)
+            y = tensor.from_numpy(Y, dev)
+            m.compile([x], is_train=True, use_graph=False)
+            if init is None:
+                init = {k: v.data.clone() for k, v in m.get_states().items()}
+            else:
+                m.set_states(init)
+            ls = []
+            for _ in range(4):
+                _, l = m(x, y)
+                ls.append(float(l.data.float().cpu()))
+            curves.append(ls)
+            if fused == "0":
+                assert not seen
+    finally:
+        singa_amd.set_deterministic(False)
+    assert seen, "fused stem op never ran"
+    assert all(np.isfinite(curves[1])), curves
+    assert curves[0] == curves[1], curves
