@@ -703,6 +703,35 @@ class BatchNorm2d(Operator):
         return tuple(out)
 
 
+class DualBNAddReLU(Operator):
+    """y = relu(BN(x) + BN2(x2)): a residual block's output BN with a
+    downsample shortcut (conv + BN), fused -- the shortcut BN's output and
+    the residual gradient are never materialised.  Inputs x, gamma, beta, x2,
+    gamma2, beta2."""
+
+    def __init__(self, bn1, bn2, name=None):
+        super().__init__(name)
+        self.p1 = (bn1.running_mean.data, bn1.running_var.data, 1.0 - bn1.momentum, bn1.eps)
+        self.p2 = (bn2.running_mean.data, bn2.running_var.data, 1.0 - bn2.momentum, bn2.eps)
+
+    def forward(self, x, gamma, beta, x2, gamma2, beta2):
+        rm, rv, mom, eps = self.p1
+        rm2, rv2, mom2, eps2 = self.p2
+        y, st, st2 = F.dual_bn_add_relu_fwd(x, gamma, beta, rm, rv, x2, gamma2, beta2, rm2, rv2, training, mom, eps,
+                                            mom2, eps2)
+        if self.requires_grad:
+            self.saved = (x, gamma, st, x2, gamma2, st2)
+        return y
+
+    def backward(self, dy):
+        x, gamma, st, x2, gamma2, st2 = self.saved
+        self.saved = None
+        t = [self.grad_target(i) for i in (1, 2, 4, 5)]
+        dx, dg, db, dx2, dg2, db2 = F.dual_bn_add_relu_bwd(x, dy, gamma, st, x2, gamma2, st2, *t)
+        acc = lambda tgt, v: ACCUMULATED if tgt is not None else v  # noqa: E731
+        return dx, acc(t[0], dg), acc(t[1], db), dx2, acc(t[2], dg2), acc(t[3], db2)
+
+
 class BnReluMaxPool(Operator):
     """max_pool(relu(BatchNorm(x))) as one forward pass (a ResNet stem): the
     full-resolution BN output is never written.  Inputs x, gamma, beta; the

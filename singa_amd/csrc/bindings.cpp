@@ -50,6 +50,11 @@ void sg_bn_fwd_stats(const void*, void*, const void*, const void*, void*, void*,
 void sg_bn_infer_params(const void*, const void*, const void*, const void*, void*, void*, void*, void*, int, float,
                         hipStream_t);
 void sg_bn_apply(const void*, const void*, const void*, const void*, void*, void*, int64_t, int, int, int, hipStream_t);
+void sg_bn_apply2(const void*, const void*, const void*, const void*, const void*, const void*, void*, void*, int64_t,
+                  int, int, int, hipStream_t);
+void sg_bn_bwd2(const void*, const void*, const void*, const void*, const void*, const void*, const void*, const void*,
+                const void*, const void*, void*, void*, void*, void*, void*, void*, void*, void*, void*, void*, int64_t,
+                int, int, hipStream_t);
 void sg_bn_bwd(const void*, const void*, const void*, const void*, const void*, const void*, const void*, const void*,
                void*, void*, void*, void*, void*, void*, int64_t, int, int, int, hipStream_t);
 void sg_pool_fwd(const void*, void*, void*, int, int, int, int, int, int, int, int, int, int, int, int, int, int, int,
@@ -202,6 +207,17 @@ PYBIND11_MODULE(_C, m) {
     sg_bn_bwd(CV(x), CV(dy), CV(y), CV(scale), CV(shift), CV(mean), CV(invstd), CV(gamma), V(ws), V(coef), V(dg),
               V(db), V(dx), V(dres), R, C, mask_mode, dt, S(s));
     CHK("bn_bwd");
+  });
+  m.def("bn_apply2", [](P x, P scale, P shift, P x2, P scale2, P shift2, P y, P mask, int64_t R, int C, int relu,
+                        int dt, P s) {
+    sg_bn_apply2(CV(x), CV(scale), CV(shift), CV(x2), CV(scale2), CV(shift2), V(y), V(mask), R, C, relu, dt, S(s));
+    CHK("bn_apply2");
+  });
+  m.def("bn_bwd2", [](P x, P dy, P mask, P mean, P invstd, P gamma, P x2, P mean2, P invstd2, P gamma2, P ws, P ws2,
+                      P coef, P coef2, P dg, P db, P dg2, P db2, P dx, P dx2, int64_t R, int C, int dt, P s) {
+    sg_bn_bwd2(CV(x), CV(dy), CV(mask), CV(mean), CV(invstd), CV(gamma), CV(x2), CV(mean2), CV(invstd2), CV(gamma2),
+               V(ws), V(ws2), V(coef), V(coef2), V(dg), V(db), V(dg2), V(db2), V(dx), V(dx2), R, C, dt, S(s));
+    CHK("bn_bwd2");
   });
   m.def("pool_fwd", [](P x, P y, P arg, int N, int H, int W, int C, int Ho, int Wo, int kh, int kw, int sh, int sw,
                        int ph, int pw, int is_max, int cp, int dt, P s) {

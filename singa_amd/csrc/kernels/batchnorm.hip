@@ -69,16 +69,27 @@ __global__ void __launch_bounds__(256) colpart_k(const T* __restrict__ x, const 
                                                  const T* __restrict__ y, const float* __restrict__ scale,
                                                  const float* __restrict__ shift, const float* __restrict__ mean,
                                                  const float* __restrict__ invstd, float* __restrict__ ws, int64_t R,
-                                                 int C, int rows_per_band, int mask_mode, int det) {
+                                                 int C, int rows_per_band, int mask_mode, int det,
+                                                 const T* __restrict__ x2 = nullptr,
+                                                 const float* __restrict__ mean2 = nullptr,
+                                                 const float* __restrict__ invstd2 = nullptr,
+                                                 float* __restrict__ ws2 = nullptr) {
+  // MODE 1 with x2: a second BN fed the same gradient (the downsample branch
+  // of a residual block): also p2 = sum g*xh2, into ws2 [band][2][C] as (p0, p2)
   __shared__ float red[256 * V];
   const Tile2D t = tile2d<V>(C);
-  float a0[V], a1[V];
+  const bool dual = MODE == 1 && x2 != nullptr;
+  float a0[V], a1[V], a2[V];
 #pragma unroll
-  for (int i = 0; i < V; ++i) { a0[i] = 0.f; a1[i] = 0.f; }
-  float mu[V], is[V], sc[V], sf[V];
+  for (int i = 0; i < V; ++i) { a0[i] = 0.f; a1[i] = 0.f; a2[i] = 0.f; }
+  float mu[V], is[V], sc[V], sf[V], mu2[V], is2[V];
   if (MODE == 1 && t.cok) {
     ldc<V>(mean + t.c0, mu);
     ldc<V>(invstd + t.c0, is);
+    if (dual) {
+      ldc<V>(mean2 + t.c0, mu2);
+      ldc<V>(invstd2 + t.c0, is2);
+    }
     if (mask_mode == MASK_AFFINE) {
       ldc<V>(scale + t.c0, sc);
       ldc<V>(shift + t.c0, sf);
@@ -132,6 +143,13 @@ __global__ void __launch_bounds__(256) colpart_k(const T* __restrict__ x, const 
           a0[i] += g0[i] + g1[i];
           a1[i] += g0[i] * (v0[i] - mu[i]) * is[i] + g1[i] * (v1[i] - mu[i]) * is[i];
         }
+        if (dual) {
+          float w0[V], w1[V];
+          ldv_nt<T, V>(x2 + r * C + t.c0, w0);
+          ldv_nt<T, V>(x2 + (r + t.RT) * C + t.c0, w1);
+#pragma unroll
+          for (int i = 0; i < V; ++i) a2[i] += g0[i] * (w0[i] - mu2[i]) * is2[i] + g1[i] * (w1[i] - mu2[i]) * is2[i];
+        }
       }
     }
     for (; r < r1; r += t.RT) {
@@ -158,6 +176,12 @@ __global__ void __launch_bounds__(256) colpart_k(const T* __restrict__ x, const 
         }
 #pragma unroll
         for (int i = 0; i < V; ++i) { a0[i] += g0[i]; a1[i] += g0[i] * (v0[i] - mu[i]) * is[i]; }
+        if (dual) {
+          float w0[V];
+          ldv_nt<T, V>(x2 + r * C + t.c0, w0);
+#pragma unroll
+          for (int i = 0; i < V; ++i) a2[i] += g0[i] * (w0[i] - mu2[i]) * is2[i];
+        }
       }
     }
   }
@@ -166,11 +190,12 @@ __global__ void __launch_bounds__(256) colpart_k(const T* __restrict__ x, const 
   // owns channel offset j of the workgroup's CT*V channels, so each
   // wave-instruction of atomics covers 256 contiguous bytes (the full-rate
   // shape for float atomics).
-  float* out = ws + (int64_t)(det ? blockIdx.x : (blockIdx.x & (NSLOT - 1))) * 2 * C;
+  const int64_t orow = (int64_t)(det ? blockIdx.x : (blockIdx.x & (NSLOT - 1))) * 2 * C;
+  float* out = ws + orow;
   const int CW = t.CT * V;                          // channels of this workgroup
   const int cbase = blockIdx.y * t.CT * V;          // first channel
-  for (int pass = 0; pass < 2; ++pass) {
-    const float* acc = pass == 0 ? a0 : a1;
+  for (int pass = 0; pass < (dual ? 3 : 2); ++pass) {
+    const float* acc = pass == 0 ? a0 : pass == 1 ? a1 : a2;
     __syncthreads();
     if (t.ty < t.RT) {
 #pragma unroll
@@ -181,8 +206,14 @@ __global__ void __launch_bounds__(256) colpart_k(const T* __restrict__ x, const 
       if (cbase + j >= C) break;
       float sum = red[j];
       for (int k = 1; k < t.RT; ++k) sum += red[k * CW + j];
-      if (det) out[pass * C + cbase + j] = sum;
-      else atomicAdd(out + pass * C + cbase + j, sum);
+      // pass 0 (sum g) goes to both workspaces, pass 2 is the second BN's row 1
+      float* dst = pass < 2 ? out + pass * C : ws2 + orow + C;
+      if (det) dst[cbase + j] = sum;
+      else atomicAdd(dst + cbase + j, sum);
+      if (pass == 0 && dual) {
+        if (det) ws2[orow + cbase + j] = sum;
+        else atomicAdd(ws2 + orow + cbase + j, sum);
+      }
     }
   }
 }
@@ -293,10 +324,18 @@ __global__ void bn_infer_params_k(const float* __restrict__ gamma, const float* 
 // per iteration leaves the memory pipeline half idle.
 template <typename T, int V>
 __device__ __forceinline__ void bn_apply_row(const float* v0, const float* rv, const float* sc, const float* sf,
-                                             T* y, uint8_t* mask, int64_t o, int relu) {
+                                             T* y, uint8_t* mask, int64_t o, int relu, const float* sc2 = nullptr,
+                                             const float* sf2 = nullptr) {
   float v[V];
+  if (rv && sc2) {
+    // the residual is itself a BN input (a downsample branch): res = x2*scale2 + shift2,
+    // rounded to T as the separate BN pass would have stored it (bitwise-equal results)
 #pragma unroll
-  for (int k = 0; k < V; ++k) v[k] = v0[k] * sc[k] + sf[k] + (rv ? rv[k] : 0.f);
+    for (int k = 0; k < V; ++k) v[k] = v0[k] * sc[k] + sf[k] + (float)(T)(rv[k] * sc2[k] + sf2[k]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < V; ++k) v[k] = v0[k] * sc[k] + sf[k] + (rv ? rv[k] : 0.f);
+  }
   if (relu) {
 #pragma unroll
     for (int k = 0; k < V; ++k) v[k] = fmaxf(v[k], 0.f);
@@ -338,12 +377,18 @@ template <typename T, int V, int UR>
 __global__ void __launch_bounds__(256) bn_apply_k(const T* __restrict__ x, const float* __restrict__ scale,
                                                   const float* __restrict__ shift, const T* __restrict__ res,
                                                   T* __restrict__ y, uint8_t* __restrict__ mask, int64_t R, int C,
-                                                  int relu, int64_t rpw) {
+                                                  int relu, int64_t rpw, const float* __restrict__ scale2,
+                                                  const float* __restrict__ shift2) {
   const Tile2D t = tile2d<V>(C);
   if (!t.cok) return;
-  float sc[V], sf[V];
+  float sc[V], sf[V], sc2[V], sf2[V];
   ldc<V>(scale + t.c0, sc);
   ldc<V>(shift + t.c0, sf);
+  const bool aff2 = scale2 != nullptr;
+  if (aff2) {
+    ldc<V>(scale2 + t.c0, sc2);
+    ldc<V>(shift2 + t.c0, sf2);
+  }
   RowSpan sp = row_span(t, R, rpw);
   const int64_t step = sp.step;
   int64_t r = sp.r;
@@ -357,14 +402,15 @@ __global__ void __launch_bounds__(256) bn_apply_k(const T* __restrict__ x, const
     }
 #pragma unroll
     for (int u = 0; u < UR; ++u)
-      bn_apply_row<T, V>(v[u], res ? rv[u] : nullptr, sc, sf, y, mask, (r + u * step) * C + t.c0, relu);
+      bn_apply_row<T, V>(v[u], res ? rv[u] : nullptr, sc, sf, y, mask, (r + u * step) * C + t.c0, relu,
+                         aff2 ? sc2 : nullptr, sf2);
   }
   for (; r < sp.end; r += step) {
     float v[V], rv[V];
     const int64_t o = r * C + t.c0;
     ldv_nt<T, V>(x + o, v);
     if (res) ldv_nt<T, V>(res + o, rv);
-    bn_apply_row<T, V>(v, res ? rv : nullptr, sc, sf, y, mask, o, relu);
+    bn_apply_row<T, V>(v, res ? rv : nullptr, sc, sf, y, mask, o, relu, aff2 ? sc2 : nullptr, sf2);
   }
 }
 
@@ -382,7 +428,9 @@ __device__ __forceinline__ void bn_bwd_load(const T* x, const T* dy, const T* y,
 template <typename T, int V>
 __device__ __forceinline__ void bn_bwd_row(const float* v, float* g, const float* yy, unsigned mb, const float* kk,
                                            const float* bb, const float* aa, const float* sc, const float* sf,
-                                           T* dx, T* dres, int64_t o, int mask_mode) {
+                                           T* dx, T* dres, int64_t o, int mask_mode, const T* x2 = nullptr,
+                                           const float* k2 = nullptr, const float* b2 = nullptr,
+                                           const float* a2 = nullptr, T* dx2 = nullptr) {
   if (mask_mode == MASK_Y) {
 #pragma unroll
     for (int k = 0; k < V; ++k) g[k] = yy[k] > 0.f ? g[k] : 0.f;
@@ -398,6 +446,13 @@ __device__ __forceinline__ void bn_bwd_row(const float* v, float* g, const float
 #pragma unroll
   for (int k = 0; k < V; ++k) o8[k] = kk[k] * g[k] + bb[k] * v[k] + aa[k];
   stv_nt<T, V>(dx + o, o8);
+  if (dx2) {  // the second BN (downsample branch) fed the same g
+    float w[V];
+    ldv_nt<T, V>(x2 + o, w);
+#pragma unroll
+    for (int k = 0; k < V; ++k) o8[k] = k2[k] * g[k] + b2[k] * w[k] + a2[k];
+    stv_nt<T, V>(dx2 + o, o8);
+  }
 }
 
 template <typename T, int V, int UR>
@@ -406,13 +461,20 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_k(const T* __restrict__ x, c
                                                       const float* __restrict__ shift,
                                                       const float* __restrict__ coef, T* __restrict__ dx,
                                                       T* __restrict__ dres, int64_t R, int C, int mask_mode,
-                                                      int64_t rpw) {
+                                                      int64_t rpw, const T* __restrict__ x2 = nullptr,
+                                                      const float* __restrict__ coef2 = nullptr,
+                                                      T* __restrict__ dx2 = nullptr) {
   const Tile2D t = tile2d<V>(C);
   if (!t.cok) return;
-  float kk[V], bb[V], aa[V], sc[V], sf[V];
+  float kk[V], bb[V], aa[V], sc[V], sf[V], k2[V], b2[V], a2[V];
   ldc<V>(coef + t.c0, kk);
   ldc<V>(coef + C + t.c0, bb);
   ldc<V>(coef + 2 * C + t.c0, aa);
+  if (dx2) {
+    ldc<V>(coef2 + t.c0, k2);
+    ldc<V>(coef2 + C + t.c0, b2);
+    ldc<V>(coef2 + 2 * C + t.c0, a2);
+  }
   if (mask_mode == MASK_AFFINE) {
     ldc<V>(scale + t.c0, sc);
     ldc<V>(shift + t.c0, sf);
@@ -427,14 +489,15 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_k(const T* __restrict__ x, c
     for (int u = 0; u < UR; ++u) bn_bwd_load<T, V>(x, dy, y, (r + u * step) * C + t.c0, mask_mode, v[u], g[u], yy[u], mb[u]);
 #pragma unroll
     for (int u = 0; u < UR; ++u)
-      bn_bwd_row<T, V>(v[u], g[u], yy[u], mb[u], kk, bb, aa, sc, sf, dx, dres, (r + u * step) * C + t.c0, mask_mode);
+      bn_bwd_row<T, V>(v[u], g[u], yy[u], mb[u], kk, bb, aa, sc, sf, dx, dres, (r + u * step) * C + t.c0, mask_mode,
+                       x2, k2, b2, a2, dx2);
   }
   for (; r < sp.end; r += step) {
     float v[V], g[V], yy[V];
     unsigned mb = 0;
     const int64_t o = r * C + t.c0;
     bn_bwd_load<T, V>(x, dy, y, o, mask_mode, v, g, yy, mb);
-    bn_bwd_row<T, V>(v, g, yy, mb, kk, bb, aa, sc, sf, dx, dres, o, mask_mode);
+    bn_bwd_row<T, V>(v, g, yy, mb, kk, bb, aa, sc, sf, dx, dres, o, mask_mode, x2, k2, b2, a2, dx2);
   }
 }
 
@@ -614,7 +677,20 @@ void sg_bn_apply(const void* x, const void* scale, const void* shift, const void
   dim3 grid = apply_grid(R, C, V, rpw);
   DISPATCH_FT(dtype, DISPATCH_V(V, BN_UR_LAUNCH(bn_apply_k, 1, T, VV, grid, dim3(256), 0, s, (const T*)x,
                                                       (const float*)scale, (const float*)shift, (const T*)res, (T*)y,
-                                                      (uint8_t*)mask, R, C, relu, rpw)));
+                                                      (uint8_t*)mask, R, C, relu, rpw, nullptr, nullptr)));
+}
+
+// y = act(x*scale + shift + x2*scale2 + shift2): a BN whose residual is the
+// (not materialised) output of a second BN -- the downsample branch
+void sg_bn_apply2(const void* x, const void* scale, const void* shift, const void* x2, const void* scale2,
+                  const void* shift2, void* y, void* mask, int64_t R, int C, int relu, int dtype, hipStream_t s) {
+  const int V = (C % 8 == 0) ? 8 : 1;
+  int64_t rpw;
+  dim3 grid = apply_grid(R, C, V, rpw);
+  DISPATCH_FT(dtype, DISPATCH_V(V, BN_UR_LAUNCH(bn_apply_k, 1, T, VV, grid, dim3(256), 0, s, (const T*)x,
+                                                      (const float*)scale, (const float*)shift, (const T*)x2, (T*)y,
+                                                      (uint8_t*)mask, R, C, relu, rpw, (const float*)scale2,
+                                                      (const float*)shift2)));
 }
 
 // Full BN backward: reduce + finalize (coef, dgamma/dbeta accumulation) + apply.
@@ -640,6 +716,37 @@ void sg_bn_bwd(const void* x, const void* dy, const void* y, const void* scale, 
                                                       (const T*)dy, (const T*)y, (const float*)scale,
                                                       (const float*)shift, (const float*)coef, (T*)dx, (T*)dres, R,
                                                       C, mask_mode, rpw)));
+}
+
+// Backward of y = relu(BN1(x) + BN2(x2)) (mask bits from the forward): one
+// reduction pass for both BNs (sum g shared), two finalizes, one apply pass
+// writing dx and dx2 -- the residual gradient g is never materialised.
+void sg_bn_bwd2(const void* x, const void* dy, const void* mask, const void* mean, const void* invstd,
+                const void* gamma, const void* x2, const void* mean2, const void* invstd2, const void* gamma2,
+                void* ws, void* ws2, void* coef, void* coef2, void* dg, void* db, void* dg2, void* db2, void* dx,
+                void* dx2, int64_t R, int C, int dtype, hipStream_t s) {
+  dim3 grid;
+  int rpb, V;
+  colgrid(R, C, grid, rpb, V);
+  zero_ws(ws, C, s);
+  if (!g_bn_det) sg_zero_async(ws2, sizeof(float) * NSLOT * 2 * C, s);
+  DISPATCH_FT(dtype, DISPATCH_V(V, hipLaunchKernelGGL((colpart_k<T, 1, VV>), grid, dim3(256), 0, s, (const T*)x,
+                                                      (const T*)dy, (const T*)mask, nullptr, nullptr,
+                                                      (const float*)mean, (const float*)invstd, (float*)ws, R, C, rpb,
+                                                      (int)MASK_BITS, g_bn_det, (const T*)x2, (const float*)mean2,
+                                                      (const float*)invstd2, (float*)ws2)));
+  hipLaunchKernelGGL(bn_bwd_finalize_k, fin_grid(C), dim3(256), 0, s, (const float*)ws, fin_rows(grid), C,
+                     (const float*)gamma, (const float*)mean, (const float*)invstd, (float*)coef, (float*)dg,
+                     (float*)db, (float)R);
+  hipLaunchKernelGGL(bn_bwd_finalize_k, fin_grid(C), dim3(256), 0, s, (const float*)ws2, fin_rows(grid), C,
+                     (const float*)gamma2, (const float*)mean2, (const float*)invstd2, (float*)coef2, (float*)dg2,
+                     (float*)db2, (float)R);
+  int64_t rpw;
+  dim3 ag = apply_grid(R, C, V, rpw);
+  DISPATCH_FT(dtype, DISPATCH_V(V, BN_UR_LAUNCH(bn_bwd_apply_k, 1, T, VV, ag, dim3(256), 0, s, (const T*)x,
+                                                      (const T*)dy, (const T*)mask, nullptr, nullptr,
+                                                      (const float*)coef, (T*)dx, nullptr, R, C, (int)MASK_BITS, rpw,
+                                                      (const T*)x2, (const float*)coef2, (T*)dx2)));
 }
 
 // BN backward whose reduction was fused into the producing conv dgrad's

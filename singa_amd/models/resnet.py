@@ -160,6 +160,21 @@ class StemConv2d(layer.Conv2d):
         return super().forward(InputPrep(dt)(x))
 
 
+def _dual_bn_add_relu(bn: layer.BatchNorm2d, x, bn2: layer.BatchNorm2d, x2):
+    """relu(bn(x) + bn2(x2)) -- fused (DualBNAddReLU) on the native path,
+    else the two BN layers with the residual add.  SINGA_FUSED_DOWN_BN=0
+    disables the fusion."""
+    if (os.environ.get("SINGA_FUSED_DOWN_BN", "1") != "0" and not autograd._TRACE
+            and F.dual_bn_add_relu_ok(x.data, x2.data)):
+        for b, t in ((bn2, x2), (bn, x)):
+            if not b._initialized:
+                b.initialize(t)
+                b._initialized = True
+        return autograd.DualBNAddReLU(bn, bn2)(x, bn.scale, bn.bias, x2, bn2.scale, bn2.bias)
+    res = bn2(x2)
+    return bn(x, relu=True, residual=res)
+
+
 def _feeds_bn(*convs):
     """Mark convolutions whose output goes straight into a BatchNorm: their
     epilogue sums the BN statistics (no separate statistics pass)."""
@@ -187,8 +202,10 @@ class Bottleneck(layer.Layer):
     def forward(self, x):
         out = self.bn1(self.conv1(x), relu=True)
         out = self.bn2(self.conv2(out), relu=True)
-        res = self.down_bn(self.down_conv(x)) if self.has_down else x
-        return self.bn3(self.conv3(out), relu=True, residual=res)
+        if self.has_down:
+            xd = self.down_conv(x)  # (creation order as before the fusion: same parameter-init draws)
+            return _dual_bn_add_relu(self.bn3, self.conv3(out), self.down_bn, xd)
+        return self.bn3(self.conv3(out), relu=True, residual=x)
 
 
 class BasicBlock(layer.Layer):
@@ -208,8 +225,10 @@ class BasicBlock(layer.Layer):
 
     def forward(self, x):
         out = self.bn1(self.conv1(x), relu=True)
-        res = self.down_bn(self.down_conv(x)) if self.has_down else x
-        return self.bn2(self.conv2(out), relu=True, residual=res)
+        if self.has_down:
+            xd = self.down_conv(x)
+            return _dual_bn_add_relu(self.bn2, self.conv2(out), self.down_bn, xd)
+        return self.bn2(self.conv2(out), relu=True, residual=x)
 
 
 class ResNet(model.Model):

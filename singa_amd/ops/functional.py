@@ -850,6 +850,57 @@ def batchnorm_fwd(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, run_
     return y.to(x.dtype), BNState(mean, invstd, scale, shift)
 
 
+def dual_bn_add_relu_ok(x: torch.Tensor, x2: torch.Tensor) -> bool:
+    """relu(BN(x) + BN2(x2)) runs fused: native, C % 8 == 0, same shape/layout."""
+    return (_bn_native(x) and _bn_native(x2) and x.shape == x2.shape and x.dtype == x2.dtype
+            and _same_layout(x, x2) and x.shape[1] % 8 == 0)
+
+
+def dual_bn_add_relu_fwd(x, gamma, beta, rm, rv, x2, gamma2, beta2, rm2, rv2, training: bool, momentum: float,
+                         eps: float, momentum2: float, eps2: float):
+    """y = relu(BN(x) + BN2(x2)) in one pass (a residual block whose shortcut
+    is a downsample conv + BN): BN2's output is never materialised.  Returns
+    (y, st, st2); st.mask holds the 1-bit ReLU mask for the backward."""
+    st_p = _bn_params(x, gamma, beta, rm, rv, training, momentum, eps)
+    st2_p = _bn_params(x2, gamma2, beta2, rm2, rv2, training, momentum2, eps2)
+    C = x.shape[1]
+    R = x.numel() // C
+    y = _like(x)
+    mask = torch.empty(R * C // 8, dtype=torch.uint8, device=x.device)
+    N.lib().bn_apply2(x.data_ptr(), st_p[2].data_ptr(), st_p[3].data_ptr(), x2.data_ptr(), st2_p[2].data_ptr(),
+                      st2_p[3].data_ptr(), y.data_ptr(), mask.data_ptr(), R, C, 1, N.dt(x), N.stream())
+    return y, BNState(*st_p, mask), BNState(*st2_p, None)
+
+
+def dual_bn_add_relu_bwd(x, dy, gamma, st: BNState, x2, gamma2, st2: BNState, dg_out=None, db_out=None,
+                         dg2_out=None, db2_out=None):
+    """Backward of dual_bn_add_relu_fwd: one reduction pass for both BNs, one
+    apply pass writing dx and dx2.  Returns dx, dg, db, dx2, dg2, db2 (the
+    parameter gradients accumulated into the *_out buffers when given)."""
+    C = x.shape[1]
+    R = x.numel() // C
+    dev = x.device
+    if dy.dtype != x.dtype or not _same_layout(dy, x):
+        dy = dy.to(x.dtype).contiguous(memory_format=torch.channels_last if x.dim() == 4 else torch.contiguous_format)
+    z = lambda o: o if o is not None else torch.zeros(C, dtype=torch.float32, device=dev)  # noqa: E731
+    dg, db, dg2, db2 = z(dg_out), z(db_out), z(dg2_out), z(db2_out)
+    key = (R, C, N.lib().deterministic())
+    n = _BANDS.get(key)
+    if n is None:
+        n = _BANDS[key] = N.lib().colreduce_ws(R, C)
+    wsb = zeroed_ws(2 * n, dev)  # one pre-zeroed flag for both halves (the kernel zeroes the second itself)
+    coef = torch.empty(6 * C, dtype=torch.float32, device=dev)
+    dx, dx2 = _like(x), _like(x2)
+    N.lib().bn_bwd2(x.data_ptr(), dy.data_ptr(), st.mask.data_ptr(), st.mean.data_ptr(), st.invstd.data_ptr(),
+                    gamma.data_ptr(), x2.data_ptr(), st2.mean.data_ptr(), st2.invstd.data_ptr(), gamma2.data_ptr(),
+                    wsb.data_ptr(), wsb[n:].data_ptr(), coef.data_ptr(), coef[3 * C:].data_ptr(), dg.data_ptr(),
+                    db.data_ptr(), dg2.data_ptr(), db2.data_ptr(), dx.data_ptr(), dx2.data_ptr(), R, C, N.dt(x),
+                    N.stream())
+    dx._sg_fresh = True
+    dx2._sg_fresh = True
+    return dx, dg, db, dx2, dg2, db2
+
+
 def batchnorm_bwd(x: torch.Tensor, dy: torch.Tensor, gamma: torch.Tensor, st: BNState,
                   y_for_mask: Optional[torch.Tensor] = None, need_dres: bool = False, relu: bool = False,
                   dg_out: Optional[torch.Tensor] = None, db_out: Optional[torch.Tensor] = None):

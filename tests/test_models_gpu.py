@@ -500,3 +500,92 @@ def test_fused_stem_bn_relu_maxpool_matches_unfused(gpu, monkeypatch):
     assert seen, "fused stem op never ran"
     assert all(np.isfinite(curves[1])), curves
     assert curves[0] == curves[1], curves
+
+
+@pytest.mark.parametrize("stride", [1, 2])
+def test_fused_downsample_bn_block_bitwise(gpu, monkeypatch, stride):
+    """relu(BN(x) + BN(downsample)) fused (DualBNAddReLU: one forward pass,
+    one reduction + one apply pass backward, the shortcut BN output and the
+    residual gradient never materialised) == the separate BN layers, bitwise,
+    for one downsampling Bottleneck in deterministic mode: output and every
+    parameter gradient."""
+    import singa_amd
+    from singa_amd import autograd as AG
+    from singa_amd.models.resnet import Bottleneck
+
+    seen = []
+    orig = AG.DualBNAddReLU.forward
+
+    def spy(self, *a):
+        seen.append(1)
+        return orig(self, *a)
+
+    monkeypatch.setattr(AG.DualBNAddReLU, "forward", spy)
+    singa_amd.set_deterministic(True)
+    res = {}
+    try:
+        for fused in ("0", "1"):
+            monkeypatch.setenv("SINGA_FUSED_DOWN_BN", fused)
+            dev = device.create_rocm_gpu()
+            dev.SetRandSeed(1)
+            blk = Bottleneck(16, stride, True)
+            g = torch.Generator(device=gpu).manual_seed(2)
+            xf = torch.randn(4, 64, 16, 16, device=gpu, generator=g)
+            x = Tensor(data=xf.bfloat16().contiguous(memory_format=torch.channels_last), device=dev,
+                       requires_grad=True, stores_grad=False)
+            AG.training = True
+            y = blk(x)
+            dy = torch.randn(y.shape, device=gpu, generator=g)
+            loss = AG.reduce_sum(AG.mul(y, Tensor(data=dy.bfloat16().contiguous(memory_format=torch.channels_last),
+                                                  device=dev, requires_grad=False)), None)
+            names = {id(p): k for k, p in blk.get_params().items()}
+            grads = {names[id(p)]: gg.data.float().clone() for p, gg in AG.backward(loss)}
+            AG.training = False
+            res[fused] = (y.data.float().clone(), grads)
+            assert bool(seen) == (fused == "1")
+    finally:
+        AG.training = False
+        singa_amd.set_deterministic(False)
+    assert torch.equal(res["0"][0], res["1"][0])
+    assert set(res["0"][1]) == set(res["1"][1])
+    diff = [k for k in res["0"][1] if not torch.equal(res["0"][1][k], res["1"][1][k])]
+    assert not diff, diff
+
+
+@pytest.mark.parametrize("depth", [18, 50])
+def test_fused_downsample_bn_model_step(gpu, monkeypatch, depth):
+    """Whole-model check of the fused shortcut BN: identical first-step loss
+    (forward bitwise) and first-step parameter updates equal to within 5 % of
+    the update (the fused reduction may contract its FMAs differently; a deep
+    untrained net at batch 8 amplifies rounding-level gradient differences)."""
+    import singa_amd
+    from singa_amd.models import resnet
+
+    rng = np.random.RandomState(2)
+    X = rng.randn(8, 3, 64, 64).astype(np.float32)
+    Y = rng.randint(0, 10, 8).astype(np.int32)
+    init, out = None, {}
+    singa_amd.set_deterministic(True)
+    try:
+        for fused in ("0", "1"):
+            monkeypatch.setenv("SINGA_FUSED_DOWN_BN", fused)
+            dev = device.create_rocm_gpu()
+            dev.SetRandSeed(0)
+            m = resnet.create_model(depth, num_classes=10, compute_dtype=torch.bfloat16)
+            m.set_optimizer(opt.SGD(0.005, 0.9, weight_decay=1e-4))
+            x = tensor.from_numpy(X, dev)
+            y = tensor.from_numpy(Y, dev)
+            m.compile([x], is_train=True, use_graph=False)
+            if init is None:
+                init = {k: v.data.clone() for k, v in m.get_states().items()}
+            else:
+                m.set_states(init)
+            _, l = m(x, y)
+            out[fused] = (float(l.data.float().cpu()), {k: v.data.float().clone() for k, v in m.get_states().items()})
+    finally:
+        singa_amd.set_deterministic(False)
+    assert out["0"][0] == out["1"][0]
+    for k, a in out["0"][1].items():
+        upd = (a - init[k].float()).abs().max().item()
+        if upd > 0:
+            assert (a - out["1"][1][k]).abs().max().item() <= 0.1 * upd, (k, (a - out["1"][1][k]).abs().max().item(), upd)
