@@ -162,7 +162,7 @@ struct Loader {
   static_assert(VPT >= 1 && CPR <= 64, "tile too small for the thread count");
   __amdgpu_buffer_rsrc_t rsrc;
   unsigned voff[VPT];  // per-lane byte offsets (BIAS-ed when masked); see issue()
-  int base[VPT];       // conv gathers: image base (elements)
+  int pbase[VPT];      // conv gathers: element offset of this row's pixel at tap 0 (may lie in the padding)
   int i0[VPT], j0[VPT];
   bool ok[VPT];
   int64_t ld;
@@ -206,9 +206,9 @@ struct Loader {
           const int rem = rr - n * g.Ho * g.Wo;
           const int oh = g.dWo.div(rem);
           const int ow = rem - oh * g.Wo;
-          base[v] = n * g.H * g.W * g.C;
           i0[v] = oh * g.sh - g.ph;
           j0[v] = ow * g.sw - g.pw;
+          pbase[v] = n * g.H * g.W * g.C + (i0[v] * g.W + j0[v]) * g.C;
         } else if constexpr (MODE == LM_DGRAD_BT) {
           voff[v] = ok[v] ? (unsigned)(rr * p.g.K + lchunk * 8) * 2u : BIAS;  // row c of a tap slab [C][K]
         } else {  // LM_DGRAD_A: row = (n, hh, ww) of the phase grid
@@ -217,9 +217,9 @@ struct Loader {
           const int rem = rr - n * P.Hp * P.Wp;
           const int hh = P.dWp.div(rem);
           const int ww = rem - hh * P.Wp;
-          base[v] = n * g.Ho * g.Wo * g.K;
           i0[v] = hh + P.offh;
           j0[v] = ww + P.offw;
+          pbase[v] = n * g.Ho * g.Wo * g.K + (i0[v] * g.Wo + j0[v]) * g.K;
         }
       }
     } else {
@@ -326,11 +326,14 @@ struct Loader {
             dr = -j;
             ds = -i;
           }
+          // the tap moves every row of the tile by the same (scalar) offset:
+          // only the bounds test is per lane (no per-lane multiplies)
+          const int tdelta = (dr * WW + ds) * CH + lchunk * 8;
 #pragma unroll
           for (int v = 0; v < VPT; ++v) {
             const int ih = i0[v] + dr, iw = j0[v] + ds;
             const bool o = ok[v] && (unsigned)ih < (unsigned)HH && (unsigned)iw < (unsigned)WW;
-            voff[v] = o ? (unsigned)(base[v] + (ih * WW + iw) * CH + lchunk * 8) * 2u : BIAS;
+            voff[v] = o ? (unsigned)(pbase[v] + tdelta) * 2u : BIAS;
           }
         }
         const unsigned adv = (unsigned)(k0 - tap * CH) * 2u;
@@ -352,11 +355,12 @@ struct Loader {
           dr = -j;
           ds = -i;
         }
+        const int tdelta = (dr * WW + ds) * CH + c0;
 #pragma unroll
         for (int v = 0; v < VPT; ++v) {
           const int ih = i0[v] + dr, iw = j0[v] + ds;
           const bool o = ok[v] && kin && (unsigned)ih < (unsigned)HH && (unsigned)iw < (unsigned)WW;
-          const int off = base[v] + (ih * WW + iw) * CH + c0;
+          const int off = pbase[v] + tdelta;
           bld16(rs, o ? (unsigned)off * 2u : OOB, lds + (8 * wv + RPV * v) * 128);
         }
       }
