@@ -322,12 +322,12 @@ __global__ void bn_infer_params_k(const float* __restrict__ gamma, const float* 
 // loaded before any is stored, so each thread keeps UR (x2 with a residual)
 // 16-byte loads in flight: the kernel is HBM-bound and one load per thread
 // per iteration leaves the memory pipeline half idle.
-template <typename T, int V>
+template <typename T, int V, bool AFF2 = false>
 __device__ __forceinline__ void bn_apply_row(const float* v0, const float* rv, const float* sc, const float* sf,
                                              T* y, uint8_t* mask, int64_t o, int relu, const float* sc2 = nullptr,
                                              const float* sf2 = nullptr) {
   float v[V];
-  if (rv && sc2) {
+  if constexpr (AFF2) {
     // the residual is itself a BN input (a downsample branch): res = x2*scale2 + shift2,
     // rounded to T as the separate BN pass would have stored it (bitwise-equal results)
 #pragma unroll
@@ -373,7 +373,7 @@ __device__ __forceinline__ RowSpan row_span(const Tile2D& t, int64_t R, int64_t 
   return s;
 }
 
-template <typename T, int V, int UR>
+template <typename T, int V, int UR, bool AFF2 = false>
 __global__ void __launch_bounds__(256) bn_apply_k(const T* __restrict__ x, const float* __restrict__ scale,
                                                   const float* __restrict__ shift, const T* __restrict__ res,
                                                   T* __restrict__ y, uint8_t* __restrict__ mask, int64_t R, int C,
@@ -384,8 +384,7 @@ __global__ void __launch_bounds__(256) bn_apply_k(const T* __restrict__ x, const
   float sc[V], sf[V], sc2[V], sf2[V];
   ldc<V>(scale + t.c0, sc);
   ldc<V>(shift + t.c0, sf);
-  const bool aff2 = scale2 != nullptr;
-  if (aff2) {
+  if constexpr (AFF2) {  // a separate instantiation: the plain apply's code is untouched
     ldc<V>(scale2 + t.c0, sc2);
     ldc<V>(shift2 + t.c0, sf2);
   }
@@ -402,15 +401,15 @@ __global__ void __launch_bounds__(256) bn_apply_k(const T* __restrict__ x, const
     }
 #pragma unroll
     for (int u = 0; u < UR; ++u)
-      bn_apply_row<T, V>(v[u], res ? rv[u] : nullptr, sc, sf, y, mask, (r + u * step) * C + t.c0, relu,
-                         aff2 ? sc2 : nullptr, sf2);
+      bn_apply_row<T, V, AFF2>(v[u], res ? rv[u] : nullptr, sc, sf, y, mask, (r + u * step) * C + t.c0, relu,
+                               sc2, sf2);
   }
   for (; r < sp.end; r += step) {
     float v[V], rv[V];
     const int64_t o = r * C + t.c0;
     ldv_nt<T, V>(x + o, v);
     if (res) ldv_nt<T, V>(res + o, rv);
-    bn_apply_row<T, V>(v, res ? rv : nullptr, sc, sf, y, mask, o, relu, aff2 ? sc2 : nullptr, sf2);
+    bn_apply_row<T, V, AFF2>(v, res ? rv : nullptr, sc, sf, y, mask, o, relu, sc2, sf2);
   }
 }
 
@@ -687,10 +686,10 @@ void sg_bn_apply2(const void* x, const void* scale, const void* shift, const voi
   const int V = (C % 8 == 0) ? 8 : 1;
   int64_t rpw;
   dim3 grid = apply_grid(R, C, V, rpw);
-  DISPATCH_FT(dtype, DISPATCH_V(V, BN_UR_LAUNCH(bn_apply_k, 1, T, VV, grid, dim3(256), 0, s, (const T*)x,
-                                                      (const float*)scale, (const float*)shift, (const T*)x2, (T*)y,
-                                                      (uint8_t*)mask, R, C, relu, rpw, (const float*)scale2,
-                                                      (const float*)shift2)));
+  DISPATCH_FT(dtype, DISPATCH_V(V, hipLaunchKernelGGL((bn_apply_k<T, VV, 1, true>), grid, dim3(256), 0, s,
+                                                      (const T*)x, (const float*)scale, (const float*)shift,
+                                                      (const T*)x2, (T*)y, (uint8_t*)mask, R, C, relu, rpw,
+                                                      (const float*)scale2, (const float*)shift2)));
 }
 
 // Full BN backward: reduce + finalize (coef, dgamma/dbeta accumulation) + apply.
