@@ -74,19 +74,20 @@ __global__ void __launch_bounds__(256) colpart_k(const T* __restrict__ x, const 
                                                  const float* __restrict__ mean2 = nullptr,
                                                  const float* __restrict__ invstd2 = nullptr,
                                                  float* __restrict__ ws2 = nullptr) {
-  // MODE 1 with x2: a second BN fed the same gradient (the downsample branch
-  // of a residual block): also p2 = sum g*xh2, into ws2 [band][2][C] as (p0, p2)
+  // MODE 2 = MODE 1 plus a second BN fed the same gradient (the downsample
+  // branch of a residual block): also p2 = sum g*xh2, into ws2 [band][2][C]
+  // as (p0, p2) -- its own instantiation, the plain reduction is untouched
   __shared__ float red[256 * V];
   const Tile2D t = tile2d<V>(C);
-  const bool dual = MODE == 1 && x2 != nullptr;
+  constexpr bool dual = MODE == 2;
   float a0[V], a1[V], a2[V];
 #pragma unroll
   for (int i = 0; i < V; ++i) { a0[i] = 0.f; a1[i] = 0.f; a2[i] = 0.f; }
   float mu[V], is[V], sc[V], sf[V], mu2[V], is2[V];
-  if (MODE == 1 && t.cok) {
+  if (MODE >= 1 && t.cok) {
     ldc<V>(mean + t.c0, mu);
     ldc<V>(invstd + t.c0, is);
-    if (dual) {
+    if constexpr (dual) {
       ldc<V>(mean2 + t.c0, mu2);
       ldc<V>(invstd2 + t.c0, is2);
     }
@@ -143,7 +144,7 @@ __global__ void __launch_bounds__(256) colpart_k(const T* __restrict__ x, const 
           a0[i] += g0[i] + g1[i];
           a1[i] += g0[i] * (v0[i] - mu[i]) * is[i] + g1[i] * (v1[i] - mu[i]) * is[i];
         }
-        if (dual) {
+        if constexpr (dual) {
           float w0[V], w1[V];
           ldv_nt<T, V>(x2 + r * C + t.c0, w0);
           ldv_nt<T, V>(x2 + (r + t.RT) * C + t.c0, w1);
@@ -176,7 +177,7 @@ __global__ void __launch_bounds__(256) colpart_k(const T* __restrict__ x, const 
         }
 #pragma unroll
         for (int i = 0; i < V; ++i) { a0[i] += g0[i]; a1[i] += g0[i] * (v0[i] - mu[i]) * is[i]; }
-        if (dual) {
+        if constexpr (dual) {
           float w0[V];
           ldv_nt<T, V>(x2 + r * C + t.c0, w0);
 #pragma unroll
@@ -424,7 +425,7 @@ __device__ __forceinline__ void bn_bwd_load(const T* x, const T* dy, const T* y,
   else if (V == 8 && mask_mode == MASK_BITS) mb = ((const uint8_t*)y)[o >> 3];
 }
 
-template <typename T, int V>
+template <typename T, int V, bool DUAL = false>
 __device__ __forceinline__ void bn_bwd_row(const float* v, float* g, const float* yy, unsigned mb, const float* kk,
                                            const float* bb, const float* aa, const float* sc, const float* sf,
                                            T* dx, T* dres, int64_t o, int mask_mode, const T* x2 = nullptr,
@@ -445,7 +446,7 @@ __device__ __forceinline__ void bn_bwd_row(const float* v, float* g, const float
 #pragma unroll
   for (int k = 0; k < V; ++k) o8[k] = kk[k] * g[k] + bb[k] * v[k] + aa[k];
   stv_nt<T, V>(dx + o, o8);
-  if (dx2) {  // the second BN (downsample branch) fed the same g
+  if constexpr (DUAL) {  // the second BN (downsample branch) fed the same g
     float w[V];
     ldv_nt<T, V>(x2 + o, w);
 #pragma unroll
@@ -454,7 +455,7 @@ __device__ __forceinline__ void bn_bwd_row(const float* v, float* g, const float
   }
 }
 
-template <typename T, int V, int UR>
+template <typename T, int V, int UR, bool DUAL = false>
 __global__ void __launch_bounds__(256) bn_bwd_apply_k(const T* __restrict__ x, const T* __restrict__ dy,
                                                       const T* __restrict__ y, const float* __restrict__ scale,
                                                       const float* __restrict__ shift,
@@ -469,7 +470,7 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_k(const T* __restrict__ x, c
   ldc<V>(coef + t.c0, kk);
   ldc<V>(coef + C + t.c0, bb);
   ldc<V>(coef + 2 * C + t.c0, aa);
-  if (dx2) {
+  if constexpr (DUAL) {
     ldc<V>(coef2 + t.c0, k2);
     ldc<V>(coef2 + C + t.c0, b2);
     ldc<V>(coef2 + 2 * C + t.c0, a2);
@@ -488,15 +489,15 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_k(const T* __restrict__ x, c
     for (int u = 0; u < UR; ++u) bn_bwd_load<T, V>(x, dy, y, (r + u * step) * C + t.c0, mask_mode, v[u], g[u], yy[u], mb[u]);
 #pragma unroll
     for (int u = 0; u < UR; ++u)
-      bn_bwd_row<T, V>(v[u], g[u], yy[u], mb[u], kk, bb, aa, sc, sf, dx, dres, (r + u * step) * C + t.c0, mask_mode,
-                       x2, k2, b2, a2, dx2);
+      bn_bwd_row<T, V, DUAL>(v[u], g[u], yy[u], mb[u], kk, bb, aa, sc, sf, dx, dres, (r + u * step) * C + t.c0,
+                             mask_mode, x2, k2, b2, a2, dx2);
   }
   for (; r < sp.end; r += step) {
     float v[V], g[V], yy[V];
     unsigned mb = 0;
     const int64_t o = r * C + t.c0;
     bn_bwd_load<T, V>(x, dy, y, o, mask_mode, v, g, yy, mb);
-    bn_bwd_row<T, V>(v, g, yy, mb, kk, bb, aa, sc, sf, dx, dres, o, mask_mode, x2, k2, b2, a2, dx2);
+    bn_bwd_row<T, V, DUAL>(v, g, yy, mb, kk, bb, aa, sc, sf, dx, dres, o, mask_mode, x2, k2, b2, a2, dx2);
   }
 }
 
@@ -729,7 +730,7 @@ void sg_bn_bwd2(const void* x, const void* dy, const void* mask, const void* mea
   colgrid(R, C, grid, rpb, V);
   zero_ws(ws, C, s);
   if (!g_bn_det) sg_zero_async(ws2, sizeof(float) * NSLOT * 2 * C, s);
-  DISPATCH_FT(dtype, DISPATCH_V(V, hipLaunchKernelGGL((colpart_k<T, 1, VV>), grid, dim3(256), 0, s, (const T*)x,
+  DISPATCH_FT(dtype, DISPATCH_V(V, hipLaunchKernelGGL((colpart_k<T, 2, VV>), grid, dim3(256), 0, s, (const T*)x,
                                                       (const T*)dy, (const T*)mask, nullptr, nullptr,
                                                       (const float*)mean, (const float*)invstd, (float*)ws, R, C, rpb,
                                                       (int)MASK_BITS, g_bn_det, (const T*)x2, (const float*)mean2,
@@ -742,8 +743,8 @@ void sg_bn_bwd2(const void* x, const void* dy, const void* mask, const void* mea
                      (float*)db2, (float)R);
   int64_t rpw;
   dim3 ag = apply_grid(R, C, V, rpw);
-  DISPATCH_FT(dtype, DISPATCH_V(V, BN_UR_LAUNCH(bn_bwd_apply_k, 1, T, VV, ag, dim3(256), 0, s, (const T*)x,
-                                                      (const T*)dy, (const T*)mask, nullptr, nullptr,
+  DISPATCH_FT(dtype, DISPATCH_V(V, hipLaunchKernelGGL((bn_bwd_apply_k<T, VV, 1, true>), ag, dim3(256), 0, s,
+                                                      (const T*)x, (const T*)dy, (const T*)mask, nullptr, nullptr,
                                                       (const float*)coef, (T*)dx, nullptr, R, C, (int)MASK_BITS, rpw,
                                                       (const T*)x2, (const float*)coef2, (T*)dx2)));
 }
