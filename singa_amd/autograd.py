@@ -30,6 +30,7 @@ import torch
 
 from . import tensor as _tensor
 from .ops import functional as F
+from .ops import native as N
 from .tensor import Tensor
 
 training = False
@@ -219,6 +220,13 @@ def backward(y, dy=None) -> Iterator[Tuple[Tensor, Tensor]]:
             if src_op not in seen:
                 seen.add(src_op)
                 q.append(src_op)
+    # every conv weight this backward's data gradients need, transposed K-major in one launch
+    convs = sorted((o for o in seen if isinstance(o, Conv2d) and getattr(o, "w", None) is not None and o.group == 1
+                    and o.dilation == (1, 1) and o.needs_grad(0)), key=lambda o: getattr(o, "_seq", 0))
+    if len(convs) > 1 and N.available() and convs[0].w.is_cuda:
+        pre = F.pretranspose_conv_weights([(id(o), o.w) for o in convs])
+        for o in convs:
+            o.wt_pre = pre.get(id(o))
     for op0 in pending:
         if deps[op0] == 0:
             heapq.heappush(heap, (-getattr(op0, "_seq", 0), id(op0), op0))
@@ -652,9 +660,10 @@ class Conv2d(Operator):
                   and (getattr(self, "acc_last", None) or {}).get(0, False)):
                 # residual BN: this dgrad's accumulation completes its output gradient
                 bnp = (prod.x, prod.st, prod.st.mask)
+        wt_pre, self.wt_pre = getattr(self, "wt_pre", None), None
         dx, dw, db = F.conv2d_bwd(x, w, dy, self.stride, self.padding, self.dilation, self.group,
                                   need_dx=self.needs_grad(0), dw_out=tgt, need_db=self.has_bias, dx_acc=acc,
-                                  bn_producer=bnp)
+                                  bn_producer=bnp, wt_pre=wt_pre)
         if acc is not None and dx is acc:
             dx = ACC_INPLACE
         res = [dx, ACCUMULATED if tgt is not None else dw]

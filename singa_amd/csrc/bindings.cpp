@@ -50,6 +50,8 @@ void sg_bn_fwd_stats(const void*, void*, const void*, const void*, void*, void*,
 void sg_bn_infer_params(const void*, const void*, const void*, const void*, void*, void*, void*, void*, int, float,
                         hipStream_t);
 void sg_bn_apply(const void*, const void*, const void*, const void*, void*, void*, int64_t, int, int, int, hipStream_t);
+void sg_set_wt_ready(int);
+void sg_wt_transpose_batched(const void*, int, int, hipStream_t);
 void sg_bn_apply2(const void*, const void*, const void*, const void*, const void*, const void*, void*, void*, int64_t,
                   int, int, int, hipStream_t);
 void sg_bn_bwd2(const void*, const void*, const void*, const void*, const void*, const void*, const void*, const void*,
@@ -207,6 +209,11 @@ PYBIND11_MODULE(_C, m) {
     sg_bn_bwd(CV(x), CV(dy), CV(y), CV(scale), CV(shift), CV(mean), CV(invstd), CV(gamma), V(ws), V(coef), V(dg),
               V(db), V(dx), V(dres), R, C, mask_mode, dt, S(s));
     CHK("bn_bwd");
+  });
+  m.def("set_wt_ready", [](int on) { sg_set_wt_ready(on); });
+  m.def("wt_transpose_batched", [](P desc, int n, int total, P s) {
+    sg_wt_transpose_batched(CV(desc), n, total, S(s));
+    CHK("wt_transpose_batched");
   });
   m.def("bn_apply2", [](P x, P scale, P shift, P x2, P scale2, P shift2, P y, P mask, int64_t R, int C, int relu,
                         int dt, P s) {

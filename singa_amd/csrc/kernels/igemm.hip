@@ -1020,6 +1020,35 @@ __global__ void __launch_bounds__(256) wt_transpose_k(const bf16* __restrict__ w
   }
 }
 
+// Every conv weight of a backward pass transposed in ONE launch (instead of
+// one small launch in front of each dgrad).  desc[i] = {src, dst, K, T, C,
+// first tile}; workgroup b takes tile b of the descriptor whose range holds
+// it (tiles of a weight ordered like wt_transpose_k's grid: c-block fastest).
+struct WtDesc {
+  const bf16* src;
+  bf16* dst;
+  int K, T, C, tile0;
+};
+__global__ void __launch_bounds__(256) wt_transpose_batched_k(const WtDesc* __restrict__ desc, int n) {
+  __shared__ bf16 tile[64][65];
+  int d = 0;
+  while (d + 1 < n && desc[d + 1].tile0 <= (int)blockIdx.x) ++d;  // n is small (one entry per conv)
+  const WtDesc w = desc[d];
+  const int lt = blockIdx.x - w.tile0;
+  const int cb = (w.C + 63) / 64, kbn = (w.K + 63) / 64;
+  const int c0 = (lt % cb) * 64, k0 = ((lt / cb) % kbn) * 64, t = lt / (cb * kbn);
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int r = ty; r < 64; r += 4) {
+    const int k = k0 + r, c = c0 + tx;
+    tile[r][tx] = (k < w.K && c < w.C) ? w.src[((int64_t)k * w.T + t) * w.C + c] : (bf16)0.f;
+  }
+  __syncthreads();
+  for (int r = ty; r < 64; r += 4) {
+    const int c = c0 + r, k = k0 + tx;
+    if (c < w.C && k < w.K) w.dst[((int64_t)t * w.C + c) * w.K + k] = tile[tx][r];
+  }
+}
+
 }  // namespace sg
 
 using namespace sg;
@@ -1074,6 +1103,7 @@ static int make_phases(ConvGeom& g) {
 // 6 = single-stage short-K variant for GEMMs of at most this many K-tiles
 // (0 = off), 7 = early DMA issue in the 2-stage loop (measured -3.5 % conv time)
 static int g_tune[8] = {5, 1, 1, 0, 0, 1, 2, 1};
+static int g_wt_ready = 0;  // one-shot: the next dgrad's wt scratch is already transposed
 
 constexpr int stages_c(int BM, int BN, int STAGES) { return STAGES * (BM + BN) * BK * 2; }
 
@@ -1341,6 +1371,8 @@ void sg_conv_dgrad_bn_ex(const void* dy, const void* w, void* dx, int N, int H, 
                          int Ho, int Wo, int sh, int sw, int ph, int pw, int dh, int dw, int out_mode, float beta,
                          void* wt, void* bn_ws, const void* bn_x, const void* bn_mean, const void* bn_invstd,
                          const void* bn_scale, const void* bn_shift, const void* bn_mask, hipStream_t s) {
+  const bool wt_ready = g_wt_ready;  // one-shot: wt already holds the K-major weights (batched pre-pass)
+  g_wt_ready = 0;
   GemmArgs p{};
   if (bn_ws && out_mode == OUT_BF16 && (beta == 0.f || bn_mask) && (C & 7) == 0 && g_tune[1] &&
       !sg_bn_deterministic()) {
@@ -1363,8 +1395,9 @@ void sg_conv_dgrad_bn_ex(const void* dy, const void* w, void* dx, int N, int H, 
     p.a_bytes = extent_bytes((int64_t)p.M * K);
     p.b_bytes = extent_bytes((int64_t)K * C);
     if (wt && (K & 63) == 0) {
-      hipLaunchKernelGGL(wt_transpose_k, dim3((C + 63) / 64, (K + 63) / 64, 1), dim3(256), 0, s, (const bf16*)w,
-                         (bf16*)wt, K, 1, C);
+      if (!wt_ready)
+        hipLaunchKernelGGL(wt_transpose_k, dim3((C + 63) / 64, (K + 63) / 64, 1), dim3(256), 0, s, (const bf16*)w,
+                           (bf16*)wt, K, 1, C);
       p.b = (const bf16*)wt; p.ldb = K;
       if (out_mode == OUT_F32) launch<LM_KMAJOR, LM_KMAJOR, OUT_F32>(p, p.M, 1, s, 1, 0);
       else launch<LM_KMAJOR, LM_KMAJOR, OUT_BF16>(p, p.M, 1, s, 1, 0);
@@ -1390,8 +1423,9 @@ void sg_conv_dgrad_bn_ex(const void* dy, const void* w, void* dx, int N, int H, 
     // K-major weights: transpose once per call (weights are small), then the
     // B operand is read with ds_read_b128 like the forward's, not transposed
     // through LDS
-    hipLaunchKernelGGL(wt_transpose_k, dim3((C + 63) / 64, (K + 63) / 64, R * S), dim3(256), 0, s, (const bf16*)w,
-                       (bf16*)wt, K, R * S, C);
+    if (!wt_ready)
+      hipLaunchKernelGGL(wt_transpose_k, dim3((C + 63) / 64, (K + 63) / 64, R * S), dim3(256), 0, s, (const bf16*)w,
+                         (bf16*)wt, K, R * S, C);
     p.b = (const bf16*)wt;
     if (out_mode == OUT_F32) launch<LM_DGRAD_A, LM_DGRAD_BT, OUT_F32>(p, Mmax, 1, s, 1, np);
     else launch<LM_DGRAD_A, LM_DGRAD_BT, OUT_BF16>(p, Mmax, 1, s, 1, np);
@@ -1467,6 +1501,13 @@ int sg_conv_stats_rows(int M, int N) {
   return (M + BM - 1) / BM;
 }
 
+void sg_set_wt_ready(int on) { g_wt_ready = on; }
+// desc: n WtDesc entries in device memory (32 bytes each), total = sum of tiles
+void sg_wt_transpose_batched(const void* desc, int n, int total, hipStream_t s) {
+  static_assert(sizeof(WtDesc) == 32, "descriptor layout shared with the Python packer");
+  if (n > 0 && total > 0)
+    hipLaunchKernelGGL(wt_transpose_batched_k, dim3(total), dim3(256), 0, s, (const WtDesc*)desc, n);
+}
 void sg_set_tuning(int key, int value) {
   if (key >= 0 && key < 8) g_tune[key] = value;
 }

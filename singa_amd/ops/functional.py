@@ -21,6 +21,7 @@ import math
 import os
 from typing import Optional, Sequence, Tuple
 
+import numpy as np
 import torch
 import torch.nn.functional as F
 
@@ -507,9 +508,55 @@ FUSE_BN_BWD_STATS = os.environ.get("SINGA_AMD_FUSE_BN_BWD", "0") == "1"
 FUSE_RES_BN_BWD = os.environ.get("SINGA_AMD_FUSE_RES_BN_BWD", "0") == "1"
 
 
+_WT_CACHE: dict = {}
+
+
+def pretranspose_conv_weights(items) -> dict:
+    """K-major copies ([R*S][C][K]) of every conv weight a backward pass will
+    need for its data gradients, written by ONE batched launch instead of one
+    small transpose launch in front of each dgrad.  ``items``: (key, w) with w
+    the bf16 channels-last weight the forward used.  Returns {key: wt}.  The
+    descriptor table and scratch are cached per weight set (stable pointers
+    in the flat parameter store), so a captured step replays just the launch."""
+    sel = []
+    for key, w in items:
+        if (w is not None and w.is_cuda and w.dtype == torch.bfloat16 and w.dim() == 4 and N.is_cl(w)
+                and w.shape[0] % 64 == 0 and w.shape[1] % 8 == 0):
+            sel.append((key, w))
+    if len(sel) < 2 or not DGRAD_KMAJOR:
+        return {}
+    sig = tuple((w.data_ptr(),) + tuple(w.shape) for _, w in sel)
+    ent = _WT_CACHE.get(sig)
+    if ent is None:
+        if len(_WT_CACHE) > 8:
+            _WT_CACHE.clear()
+        dev = sel[0][1].device
+        sizes = [w.numel() for _, w in sel]
+        offs = np.cumsum([0] + [(n + 63) // 64 * 64 for n in sizes])
+        scratch = torch.empty(int(offs[-1]), dtype=torch.bfloat16, device=dev)
+        desc = np.zeros((len(sel), 4), dtype=np.int64)
+        tile0 = 0
+        for i, (_, w) in enumerate(sel):
+            K, C, R, S = w.shape
+            desc[i, 0] = w.data_ptr()
+            desc[i, 1] = scratch.data_ptr() + 2 * int(offs[i])
+            desc[i, 2] = K | ((R * S) << 32)
+            desc[i, 3] = C | (tile0 << 32)
+            tile0 += ((C + 63) // 64) * ((K + 63) // 64) * R * S
+        # pinned source: a copy issued while a step is being captured becomes a
+        # graph node (a pageable one is not permitted); kept alive in the entry
+        host = torch.from_numpy(desc).pin_memory()
+        ent = (host.to(dev, non_blocking=True), scratch, [scratch[int(o):int(o) + n] for o, n in zip(offs, sizes)],
+               tile0, host)
+        _WT_CACHE[sig] = ent
+    desc_dev, _, views, total, _ = ent
+    N.lib().wt_transpose_batched(desc_dev.data_ptr(), len(sel), total, N.stream())
+    return {key: v for (key, _), v in zip(sel, views)}
+
+
 def conv2d_bwd(x: torch.Tensor, w: torch.Tensor, dy: torch.Tensor, stride, padding, dilation=(1, 1), groups=1,
                need_dx=True, dw_out: Optional[torch.Tensor] = None, need_db=False,
-               dx_acc: Optional[torch.Tensor] = None, bn_producer=None):
+               dx_acc: Optional[torch.Tensor] = None, bn_producer=None, wt_pre: Optional[torch.Tensor] = None):
     """Returns (dx, dw, db).  If dw_out (fp32, same logical shape as w) is given
     the weight gradient is ACCUMULATED into it (flat grad buffer views).
     ``dx_acc``: an existing gradient of x (another consumer's contribution);
@@ -547,9 +594,16 @@ def conv2d_bwd(x: torch.Tensor, w: torch.Tensor, dy: torch.Tensor, stride, paddi
                                                                                 memory_format=torch.channels_last)
             od = torch.bfloat16 if x.dtype == torch.bfloat16 else torch.float32
             om = 0 if od == torch.bfloat16 else 1
-            # K-major transposed weights for the B operand (scratch from the caching allocator)
-            wt = (torch.empty(Kp * Cp * R * S, dtype=torch.bfloat16, device=x.device)
-                  if DGRAD_KMAJOR and Kp % 64 == 0 else None)
+            # K-major transposed weights for the B operand: the batched pre-pass's
+            # copy (``wt_pre``) or scratch the dgrad call transposes into
+            wt, ready = None, False
+            if DGRAD_KMAJOR and Kp % 64 == 0:
+                if wt_pre is not None and not padded and wb is w and wt_pre.numel() == Kp * Cp * R * S:
+                    wt, ready = wt_pre, True
+                else:
+                    wt = torch.empty(Kp * Cp * R * S, dtype=torch.bfloat16, device=x.device)
+            if ready:
+                N.lib().set_wt_ready(1)  # one-shot: consumed by the dgrad launch below
             if (dx_acc is not None and Cx == Cp and dx_acc.dtype == od and od == x.dtype
                     and tuple(dx_acc.shape) == tuple(x.shape) and N.is_cl(dx_acc) and dx_acc.is_contiguous(
                         memory_format=torch.channels_last)):
