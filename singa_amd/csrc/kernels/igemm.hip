@@ -768,6 +768,12 @@ __global__ void __launch_bounds__(NTH, STAGES == 1 ? 3 : (NTH == 512 && STAGES =
       float* tile = (float*)smem;
       bf16* tile16 = (bf16*)smem;
       __syncthreads();  // all waves are done reading the last operand stage
+      if (p.alpha != 1.f) {  // (uniform; alpha is 1 for every conv)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] *= p.alpha;
+      }
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int ml = wm * WTM + i * 16 + (l & 15);
@@ -775,8 +781,7 @@ __global__ void __launch_bounds__(NTH, STAGES == 1 ? 3 : (NTH == 512 && STAGES =
         for (int j = 0; j < TN; ++j) {
           const int nl = wn * WTN + j * 16 + (l >> 4) * 4;
           const int n = n0 + nl;
-          float4 v = make_float4(acc[i][j][0] * p.alpha, acc[i][j][1] * p.alpha, acc[i][j][2] * p.alpha,
-                                 acc[i][j][3] * p.alpha);
+          float4 v = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
           if (p.bias && n < p.N) {
             v.x += p.bias[n]; v.y += p.bias[n + 1]; v.z += p.bias[n + 2]; v.w += p.bias[n + 3];
           }
@@ -816,20 +821,21 @@ __global__ void __launch_bounds__(NTH, STAGES == 1 ? 3 : (NTH == 512 && STAGES =
         constexpr int NPS = BM / RPP;
         int64_t rofs[NPS];
         bool rok[NPS];
+        const int64_t rbase = (int64_t)(m0 + r0) * p.ldc, rstep = (int64_t)RPP * p.ldc;
 #pragma unroll
         for (int pass = 0; pass < NPS; ++pass) {
           const int m = m0 + r0 + pass * RPP;
           rok[pass] = m < M;
           const int mm = rok[pass] ? m : 0;
-          if (p.out_phase) {
+          if (!p.out_phase) {
+            rofs[pass] = rbase + pass * rstep;  // (rows past M are never used)
+          } else {
             const ConvGeom& g = p.g;
             const int nn = P.dHpWp.div(mm);
             const int rem = mm - nn * P.Hp * P.Wp;
             const int hh = P.dWp.div(rem);
             const int ww = rem - hh * P.Wp;
             rofs[pass] = (((int64_t)nn * g.H + P.a + g.sh * hh) * g.W + P.b + g.sw * ww) * p.ldc;
-          } else {
-            rofs[pass] = (int64_t)mm * p.ldc;
           }
         }
         const bool bnb = p.stats && p.stats_mode >= 1;
