@@ -828,7 +828,8 @@ __global__ void __launch_bounds__(NTH, STAGES == 1 ? 3 : (NTH == 512 && STAGES =
           rok[pass] = m < M;
           const int mm = rok[pass] ? m : 0;
           if (!p.out_phase) {
-            rofs[pass] = rbase + pass * rstep;  // (rows past M are never used)
+            // rows past M map to row 0: the up-front loads below read every pass
+            rofs[pass] = rok[pass] ? rbase + pass * rstep : 0;
           } else {
             const ConvGeom& g = p.g;
             const int nn = P.dHpWp.div(mm);
