@@ -18,6 +18,7 @@ through export -> serialize -> import and compare outputs.
 from __future__ import annotations
 
 import math
+import os
 from collections import OrderedDict
 from typing import Dict, List, Optional, Sequence
 
@@ -814,14 +815,185 @@ def _i_onehot(rep, n, x, a):
     return [autograd.onehot(int(a.get("axis", -1)), x[0], int(_np(x[1]).reshape(-1)[0]), x[2])]
 
 
+# ------------------------------------------------------ import-time fusion
+class _Fused:
+    """One fused group of imported nodes: runs at the position of its LAST
+    member (every external input exists by then) and defines only the
+    group's final output (the intermediates have no other consumer)."""
+
+    def __init__(self, kind: str, members, inputs, output: str, scale: Optional[float] = None):
+        self.kind, self.members, self.inputs, self.output, self.scale = kind, tuple(members), list(inputs), output, scale
+
+    def _low(self, rep, t):
+        cd = rep.compute_dtype
+        return autograd.cast(t, cd) if cd is not None and t.data.is_cuda and t.dtype == torch.float32 else t
+
+    def run(self, rep, xs):
+        if self.kind == "linear":  # MatMul + bias Add -> one GEMM with a bias epilogue (bf16 weight copy)
+            return autograd.linear(self._low(rep, xs[0]), xs[1], xs[2])
+        if self.kind == "gelu":  # x * 0.5 * (1 + erf(x / sqrt 2)) -> one elementwise kernel
+            return autograd.gelu(xs[0])
+        if self.kind == "attention":  # Transpose/MatMul/scale/[mask]/Softmax/MatMul -> batched-MFMA attention
+            q, k, v = (self._low(rep, t) for t in xs[:3])
+            return autograd.attention(q, k, v, xs[3] if len(xs) > 3 else None, self.scale)
+        raise ValueError(self.kind)
+
+    def __repr__(self):
+        return f"_Fused({self.kind}, nodes={list(self.members)}, out={self.output!r})"
+
+
+def _fusion_plan(nodes, inits: Dict[str, Tensor], consts: set, outputs: Sequence[str]) -> Dict[int, _Fused]:
+    """Pattern-match the imported node list into fused groups, keyed by the
+    index of each group's last node:
+
+    * ``linear``    MatMul(x, W) -> Add(., b), W [in, out] and b [out] parameters;
+    * ``gelu``      Div(x, sqrt 2) -> Erf -> Add(., 1) -> Mul(x, .) -> Mul(., 0.5)
+                    (the exact-erf GELU both this exporter and PyTorch's emit);
+    * ``attention`` Transpose(k, swap last two) -> MatMul(q, .) -> Mul/Div(., c)
+                    -> [Add(., mask)] -> Softmax(last axis) -> MatMul(., v).
+
+    A chain only fuses when every intermediate has exactly one consumer and
+    is not a graph output, so no other node can observe what it skips.  The
+    unfused import runs 2 / 5 / 5-6 autograd ops (and their backward kernels)
+    per group, plus an fp32->bf16 cast of every MatMul weight per step."""
+    cons: Dict[str, List[int]] = {}
+    for idx, nd in enumerate(nodes):
+        for nm in nd.input:
+            if nm:
+                cons.setdefault(nm, []).append(idx)
+    outs = set(outputs)
+    used: set = set()
+
+    def only(name: str) -> Optional[int]:
+        c = cons.get(name, [])
+        if len(c) != 1 or name in outs or c[0] in used:
+            return None
+        return c[0]
+
+    def scalar(name: str) -> Optional[float]:
+        t = inits.get(name)
+        if t is None or name not in consts or t.data.numel() != 1:
+            return None
+        return float(t.data.reshape(-1)[0])
+
+    def param(name: str, dim: int) -> bool:
+        t = inits.get(name)
+        return t is not None and t.stores_grad and t.data.dim() == dim
+
+    def attr(nd, key, default=None):
+        for a in nd.attribute:
+            if a.name == key:
+                return attr_value(a)
+        return default
+
+    def other(nd, name: str) -> Optional[str]:
+        ins = list(nd.input)
+        if len(ins) != 2 or name not in ins:
+            return None
+        return ins[1] if ins[0] == name else ins[0]
+
+    def linear(i):
+        nd = nodes[i]
+        if nd.op_type != "MatMul" or not param(nd.input[1], 2):
+            return None
+        j = only(nd.output[0])
+        if j is None or nodes[j].op_type != "Add":
+            return None
+        b = other(nodes[j], nd.output[0])
+        if b is None or not param(b, 1) or inits[b].data.shape[0] != inits[nd.input[1]].data.shape[1]:
+            return None
+        return _Fused("linear", (i, j), [nd.input[0], nd.input[1], b], nodes[j].output[0])
+
+    def gelu(i):
+        nd = nodes[i]
+        if nd.op_type != "Div" or scalar(nd.input[1]) is None or abs(scalar(nd.input[1]) - math.sqrt(2.0)) > 1e-4:
+            return None
+        x = nd.input[0]
+        j = only(nd.output[0])
+        if j is None or nodes[j].op_type != "Erf":
+            return None
+        k = only(nodes[j].output[0])
+        if k is None or nodes[k].op_type != "Add":
+            return None
+        c = other(nodes[k], nodes[j].output[0])
+        if c is None or scalar(c) != 1.0:
+            return None
+        m = only(nodes[k].output[0])
+        if m is None or nodes[m].op_type != "Mul" or other(nodes[m], nodes[k].output[0]) != x:
+            return None
+        n = only(nodes[m].output[0])
+        if n is None or nodes[n].op_type != "Mul":
+            return None
+        h = other(nodes[n], nodes[m].output[0])
+        if h is None or scalar(h) != 0.5:
+            return None
+        return _Fused("gelu", (i, j, k, m, n), [x], nodes[n].output[0])
+
+    def attention(i):
+        nd = nodes[i]
+        perm = attr(nd, "perm")
+        if nd.op_type != "Transpose" or not perm or len(perm) < 2:
+            return None
+        r = len(perm)
+        if list(perm) != list(range(r - 2)) + [r - 1, r - 2]:
+            return None
+        j = only(nd.output[0])
+        if j is None or nodes[j].op_type != "MatMul" or nodes[j].input[1] != nd.output[0]:
+            return None
+        q, k_ = nodes[j].input[0], nd.input[0]
+        m = only(nodes[j].output[0])
+        if m is None or nodes[m].op_type not in ("Mul", "Div"):
+            return None
+        c = scalar(nodes[m].input[1]) if nodes[m].input[0] == nodes[j].output[0] else None
+        if c is None and nodes[m].op_type == "Mul":
+            c = scalar(nodes[m].input[0]) if nodes[m].input[1] == nodes[j].output[0] else None
+        if c is None or c == 0.0:
+            return None
+        scale = c if nodes[m].op_type == "Mul" else 1.0 / c
+        members, cur, mask = [i, j, m], nodes[m].output[0], None
+        s = only(cur)
+        if s is not None and nodes[s].op_type == "Add":
+            mask = other(nodes[s], cur)
+            if mask is None or mask in inits and inits[mask].stores_grad:
+                return None
+            members.append(s)
+            cur = nodes[s].output[0]
+            s = only(cur)
+        if s is None or nodes[s].op_type != "Softmax" or int(attr(nodes[s], "axis", -1)) not in (-1, r - 1):
+            return None
+        members.append(s)
+        t = only(nodes[s].output[0])
+        if t is None or nodes[t].op_type != "MatMul" or nodes[t].input[0] != nodes[s].output[0]:
+            return None
+        members.append(t)
+        ins = [q, k_, nodes[t].input[1]] + ([mask] if mask is not None else [])
+        return _Fused("attention", members, ins, nodes[t].output[0], scale)
+
+    plan: Dict[int, _Fused] = {}
+    for i in range(len(nodes)):
+        if i in used:
+            continue
+        for pat in (attention, gelu, linear):
+            st = pat(i)
+            if st is not None:
+                used.update(st.members)
+                plan[max(st.members)] = st
+                break
+    return plan
+
+
 class SingaRep:
-    """An imported ONNX graph bound to a device (SINGA ``SingaRep``)."""
+    """An imported ONNX graph bound to a device (SINGA ``SingaRep``).
+
+    Import-time fusion (``fuse=True``, default; ``SINGA_AMD_SONNX_FUSE=0``
+    turns it off) maps the exported Linear / GELU / attention node chains
+    back onto the fused autograd operators (:func:`_fusion_plan`)."""
 
     # ops whose float operands run at ``compute_dtype`` (MFMA GEMM / conv);
     # everything else (softmax, norms, elementwise) sees what they produce
     _LOWP = {"MatMul": (0, 1), "Gemm": (0, 1), "Conv": (0, 1), "ConvTranspose": (0, 1)}
 
-    def __init__(self, mp, device=None, trainable: bool = True, compute_dtype=None):
+    def __init__(self, mp, device=None, trainable: bool = True, compute_dtype=None, fuse: Optional[bool] = None):
         from .. import device as _dev
 
         self.model_proto = mp
@@ -836,7 +1008,9 @@ class SingaRep:
         weight_like = self._weight_inputs(g)
         for t in g.initializer:
             a = tensorproto_to_numpy(t)
-            is_param = trainable and a.dtype == np.float32 and t.name in weight_like
+            # scalar initializers (GELU's sqrt(2) / 1 / 0.5, the attention
+            # scale) are constants even in a learnable position
+            is_param = trainable and a.dtype == np.float32 and t.name in weight_like and a.size > 1
             ten = Tensor(device=self.device, data=torch.from_numpy(np.array(a, order="C")),
                          requires_grad=is_param, stores_grad=is_param)
             ten.name = t.name
@@ -849,6 +1023,10 @@ class SingaRep:
         for nd in g.node:
             if nd.op_type not in _IMPORTERS:
                 raise NotImplementedError(f"sonnx import: unsupported ONNX op {nd.op_type}")
+        if fuse is None:
+            fuse = os.environ.get("SINGA_AMD_SONNX_FUSE", "1") != "0"
+        self.fused = _fusion_plan(list(g.node), self.inits, self._consts, self.output_names) if fuse else {}
+        self._skip = {i for st in self.fused.values() for i in st.members}
 
     @staticmethod
     def _weight_inputs(g) -> set:
@@ -878,7 +1056,13 @@ class SingaRep:
             if not isinstance(x, Tensor):
                 x = Tensor(device=self.device, data=torch.as_tensor(np.asarray(x)), requires_grad=False)
             env[name] = x
-        for nd in self.graph.node:
+        for idx, nd in enumerate(self.graph.node):
+            st = self.fused.get(idx)
+            if st is not None:
+                env[st.output] = st.run(self, [env.get(i) if i else None for i in st.inputs])
+                continue
+            if idx in self._skip:
+                continue
             attrs = {a.name: attr_value(a) for a in nd.attribute}
             xs = [env.get(i) if i else None for i in nd.input]
             if self.compute_dtype is not None and nd.op_type in self._LOWP:
@@ -919,6 +1103,8 @@ class SONNXModel(model.Model):
     def __init__(self, onnx_model, device=None, loss=None, compute_dtype=None):
         super().__init__()
         self.rep = prepare(onnx_model, device, compute_dtype=compute_dtype)
+        if compute_dtype is not None:  # fp32 master weights + the optimiser's bf16 compute copies (fused Linear)
+            self.compute_dtype = compute_dtype
         self._onnx_params = self.rep.params()
         for k, v in self._onnx_params.items():
             v.param_meta = {"lr_mult": 1.0, "wd_mult": 1.0}

@@ -212,3 +212,51 @@ def test_exported_bert_is_batch_independent():
     out = sonnx.prepare(P.load_model(blob)).run([ids5])[0].data.numpy()
     autograd.training = False
     np.testing.assert_allclose(out, m.forward(ids5).data.numpy(), atol=1e-4)
+
+
+def test_import_fusion_plan_bert_matches_unfused():
+    """Import-time fusion maps the exported Linear / GELU / attention chains
+    back onto the fused operators; fused and unfused imports give the same
+    outputs and parameter gradients (fp32, CPU)."""
+    from singa_amd.models import bert
+
+    ids = tensor.from_numpy(np.random.RandomState(0).randint(0, 1000, (3, 16)).astype(np.int64))
+    y = tensor.from_numpy(np.array([0, 1, 1], np.int32))
+    device.get_default_device().SetRandSeed(0)
+    m = bert.bert_tiny(dropout=0.0)
+    m.compile([ids], is_train=False)
+    blob = sonnx.to_onnx(m, [ids]).SerializeToString()
+    kinds = {}
+    res = []
+    for fuse in (False, True):
+        rep = sonnx.prepare(P.load_model(blob), fuse=fuse)
+        for st in rep.fused.values():
+            kinds[st.kind] = kinds.get(st.kind, 0) + 1
+        autograd.training = True
+        out = rep.run([ids])[0]
+        loss = autograd.softmax_cross_entropy(out, y)
+        grads = {p.name: g.data.clone() for p, g in autograd.backward(loss)}
+        autograd.training = False
+        res.append((out.data.clone(), grads))
+    # bert_tiny: 2 layers x (qkv, proj, fc1, fc2) + pooler + classifier
+    assert kinds == {"linear": 10, "gelu": 2, "attention": 2}, kinds
+    (o0, g0), (o1, g1) = res
+    np.testing.assert_allclose(o1.numpy(), o0.numpy(), atol=1e-5, rtol=1e-5)
+    assert set(g0) == set(g1) and len(g0) > 20
+    for k in g0:
+        np.testing.assert_allclose(g1[k].numpy(), g0[k].numpy(), atol=1e-5, rtol=1e-4, err_msg=k)
+
+
+def test_import_fusion_respects_other_consumers():
+    """A MatMul whose output is also a graph output is not fused with its Add."""
+    x = R.randn(4, 6).astype(np.float32)
+    w = R.randn(6, 5).astype(np.float32)
+    b = R.randn(5).astype(np.float32)
+    nodes = [sonnx.make_node("MatMul", ["x0", "w"], ["t"]), sonnx.make_node("Add", ["t", "b"], ["y"])]
+    for outs, n_fused in ((["y"], 1), (["y", "t"], 0)):
+        m = _graph(nodes, [("x0", x)], outs, [("w", w), ("b", b)])
+        rep = sonnx.prepare(m)
+        assert len(rep.fused) == n_fused
+        autograd.training = False
+        got = rep.run([Tensor(data=torch.from_numpy(x), requires_grad=False)])
+        np.testing.assert_allclose(got[0].data.numpy(), x @ w + b, rtol=1e-5, atol=1e-5)

@@ -115,7 +115,7 @@ def bench_bert(a):
     m = bert.bert_base(dropout=0.1, compute_dtype=torch.bfloat16)
     ids, y = _bert_inputs(dev, B, S, 30522)
     m.set_optimizer(opt.Adam(1e-4))
-    m.compile([ids], is_train=True, use_graph=False)
+    m.compile([ids], is_train=True, use_graph=not a.no_graph)
     m.train()
     dt, (_, loss) = _time(lambda: m(ids, y), a.steps, a.warmup, torch.cuda.synchronize)
     return _rec("bert", "sequences/s", B, dt, model="BERT-base (native)", batch=B, seq_len=S, optimizer="Adam",
@@ -139,7 +139,7 @@ def bench_bert_sonnx(a):
     sm = sonnx.SONNXModel(P.load_model(blob), dev, compute_dtype=torch.bfloat16)
     ids, y = _bert_inputs(dev, B, S, 30522)
     sm.set_optimizer(opt.Adam(1e-4))
-    sm.compile([ids], is_train=True)
+    sm.compile([ids], is_train=True, use_graph=not a.no_graph)
     sm.train()
     dt, (_, loss) = _time(lambda: sm(ids, y), a.steps, a.warmup, torch.cuda.synchronize)
     return _rec("bert_sonnx", "sequences/s", B, dt, model="BERT-base exported -> ONNX -> sonnx import",
