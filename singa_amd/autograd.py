@@ -21,6 +21,10 @@ from __future__ import annotations
 
 import builtins as _b
 import math
+import os
+import sys
+import threading
+import types
 import heapq
 from collections import Counter, deque
 from typing import Callable, Dict, Iterator, List, Optional, Sequence, Tuple
@@ -33,7 +37,28 @@ from .ops import functional as F
 from .ops import native as N
 from .tensor import Tensor
 
-training = False
+# ``autograd.training`` is per THREAD (a property of this module's class over
+# thread-local storage): ranks driven as threads (parallel.fake) and hogwild
+# replicas each toggle their own flag -- a module global let one thread's
+# compile() (tape-free forward) switch off another thread's tape mid-step.
+_TLS = threading.local()
+
+
+def _training() -> bool:
+    return getattr(_TLS, "training", False)
+
+
+class _AutogradModule(types.ModuleType):
+    @property
+    def training(self) -> bool:
+        return getattr(_TLS, "training", False)
+
+    @training.setter
+    def training(self, v) -> None:
+        _TLS.training = bool(v)
+
+
+sys.modules[__name__].__class__ = _AutogradModule
 
 ACCUMULATED = object()  # backward() returned: grad already added to the param's grad_view
 # backward() returned: the input gradient was added IN PLACE into the partial
@@ -75,7 +100,7 @@ class Operator:
 
     def _do_forward(self, *xs):
         xs = tuple(x if isinstance(x, Tensor) else Tensor(data=x, requires_grad=False) for x in xs)
-        self.requires_grad = training and any(x.requires_grad for x in xs)
+        self.requires_grad = _training() and any(x.requires_grad for x in xs)
         if self.requires_grad:
             self.src = [(x.creator, x.stores_grad) for x in xs]
             self.src_idx = [x.creator._yid.get(id(x), 0) if x.creator is not None else 0 for x in xs]
@@ -632,7 +657,7 @@ class Conv2d(Operator):
         p = self.params[1] if len(self.params) > 1 else None
         w = p.low if (p is not None and p.low is not None and x.dtype == torch.bfloat16) else W
         y = F.conv2d_fwd(x, w, b, self.stride, self.padding, self.dilation, self.group, out_dtype=x.dtype,
-                         relu=self.fuse_relu, bn_stats=self.bn_stats and training)
+                         relu=self.fuse_relu, bn_stats=self.bn_stats and _training())
         if self.requires_grad:
             self.x, self.w = x, w
             self.y = y if self.fuse_relu else None
@@ -693,7 +718,7 @@ class BatchNorm2d(Operator):
         # ReLU after a residual add: the mask cannot be recomputed from x, so
         # the forward writes it as bits (1/16 of re-reading the bf16 output)
         want = self.requires_grad and self.relu and self.has_residual
-        y, st = F.batchnorm_fwd(x, gamma, beta, self.rm, self.rv, training, self.momentum, self.eps, self.relu,
+        y, st = F.batchnorm_fwd(x, gamma, beta, self.rm, self.rv, _training(), self.momentum, self.eps, self.relu,
                                 res, want_mask=want)
         if self.requires_grad:
             self.x, self.gamma, self.st = x, gamma, st
@@ -726,7 +751,7 @@ class DualBNAddReLU(Operator):
     def forward(self, x, gamma, beta, x2, gamma2, beta2):
         rm, rv, mom, eps = self.p1
         rm2, rv2, mom2, eps2 = self.p2
-        y, st, st2 = F.dual_bn_add_relu_fwd(x, gamma, beta, rm, rv, x2, gamma2, beta2, rm2, rv2, training, mom, eps,
+        y, st, st2 = F.dual_bn_add_relu_fwd(x, gamma, beta, rm, rv, x2, gamma2, beta2, rm2, rv2, _training(), mom, eps,
                                             mom2, eps2)
         if self.requires_grad:
             self.saved = (x, gamma, st, x2, gamma2, st2)
@@ -755,7 +780,7 @@ class BnReluMaxPool(Operator):
         self.kernel, self.stride, self.padding = tuple(kernel), tuple(stride), tuple(padding)
 
     def forward(self, x, gamma, beta):
-        y, arg, st = F.bn_relu_maxpool_fwd(x, gamma, beta, self.rm, self.rv, training, self.momentum, self.eps,
+        y, arg, st = F.bn_relu_maxpool_fwd(x, gamma, beta, self.rm, self.rv, _training(), self.momentum, self.eps,
                                            self.kernel, self.stride, self.padding)
         if self.requires_grad:
             self.x, self.gamma, self.st, self.arg = x, gamma, st, arg
@@ -837,7 +862,7 @@ class Dropout(Operator):
         self.seed_source = seed_source
 
     def forward(self, x):
-        if not training or self.ratio <= 0.0:
+        if not _training() or self.ratio <= 0.0:
             self.mask = None
             return x
         dev = self.seed_source
@@ -1324,10 +1349,13 @@ builtins_slice = _b.slice
 
 
 def gather(x, axis, indices):
+    host = np.asarray(indices) if not isinstance(indices, torch.Tensor) else None
     idx = torch.as_tensor(indices, device=x.data.device).long()
+    spec = None
+    if _TRACE:  # sonnx export only (the host copy of a device index would sync)
+        spec = _ox("Gather", {"axis": axis}, [("in", 0), ("const", host if host is not None else idx.cpu().numpy())])
     return _fn(lambda a: torch.index_select(a, axis, idx.reshape(-1)).reshape(
-        a.shape[:axis] + tuple(idx.shape) + a.shape[axis + 1:]), x,
-        onnx=_ox("Gather", {"axis": axis}, [("in", 0), ("const", idx.cpu().numpy())]))
+        a.shape[:axis] + tuple(idx.shape) + a.shape[axis + 1:]), x, onnx=spec)
 
 
 def tile(x, repeats):
@@ -1535,9 +1563,36 @@ def space_to_depth(x, blocksize, mode="DCR"):
                onnx=_ox("SpaceToDepth", {"blocksize": blocksize}))
 
 
+class Embedding(Operator):
+    """y = W[idx] (row gather).  Backward scatter-adds the dy rows into dW with
+    ``index_add_`` (atomics): no sort / unique / host sync, so a step using it
+    can be captured into a HIP graph -- torch's embedding backward computes
+    data-dependent segment counts and faults under capture.  Deterministic
+    mode keeps the ordered (sort-based, not capturable) backward."""
+
+    def forward(self, W, idx):
+        i = idx.long()
+        if self.requires_grad:
+            self.idx, self.wshape = i, W.shape
+        return torch.nn.functional.embedding(i, W)
+
+    def backward(self, dy):
+        i = self.idx.reshape(-1)
+        self.idx = None
+        d = dy.reshape(-1, dy.shape[-1])
+        if os.environ.get("SINGA_AMD_DETERMINISTIC", "0") == "1":
+            dw = torch.ops.aten.embedding_dense_backward(d.float(), i, self.wshape[0], -1, False)
+        else:
+            tgt = self.grad_target(0)
+            if tgt is not None and tgt.dim() == 2:
+                tgt.index_add_(0, i, d.to(tgt.dtype))
+                return ACCUMULATED, None
+            dw = torch.zeros(self.wshape, dtype=torch.float32, device=dy.device).index_add_(0, i, d.float())
+        return dw, None
+
+
 def embedding(x_idx, W):
-    return TorchFn(lambda w, i: torch.nn.functional.embedding(i.long(), w), nondiff=(1,),
-                   onnx=_ox("Gather", {"axis": 0}, n_in=2))(W, x_idx)
+    return Embedding()(W, x_idx)
 
 
 def globalaveragepool(x, keepdims=True):

@@ -37,6 +37,7 @@ void sg_softmax_xent(const void*, const void*, const void*, void*, void*, void*,
                      hipStream_t);
 void sg_layernorm_fwd(const void*, const void*, const void*, void*, void*, void*, int64_t, int, int, float,
                       hipStream_t);
+void sg_softmax_rows(const void*, void*, int64_t, int, int, int, hipStream_t);
 void sg_layernorm_bwd(const void*, const void*, const void*, const void*, const void*, void*, void*, void*, int64_t,
                       int, int, hipStream_t);
 int sg_colreduce_bands(int64_t, int);
@@ -178,6 +179,10 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("layernorm_fwd", [](P x, P g, P b, P y, P mean, P rstd, int64_t R, int D, int dt, float eps, P s) {
     sg_layernorm_fwd(CV(x), CV(g), CV(b), V(y), V(mean), V(rstd), R, D, dt, eps, S(s)); CHK("layernorm_fwd");
+  });
+  m.def("softmax_rows", [](P x, P y, int64_t R, int C, int idt, int odt, P s) {
+    sg_softmax_rows(CV(x), V(y), R, C, idt, odt, S(s));
+    CHK("softmax_rows");
   });
   m.def("layernorm_bwd", [](P x, P dy, P g, P mean, P rstd, P dx, P dg, P db, int64_t R, int D, int dt, P s) {
     sg_layernorm_bwd(CV(x), CV(dy), CV(g), CV(mean), CV(rstd), V(dx), V(dg), V(db), R, D, dt, S(s));

@@ -174,6 +174,180 @@ __global__ void layernorm_bwd_k(const T* __restrict__ x, const T* __restrict__ d
   }
 }
 
+
+// ---- short rows (C <= 64*NJ): one WAVE per row, the row in registers ----
+// Attention probabilities (C = sequence length, ~50K rows of 128) ran one
+// 256-thread block per row through LDS: 3/4 of every block idle and two block
+// barriers per row.  Here lane l owns columns l, l+64, ... (coalesced), the
+// reductions are wave shuffles, and the output dtype is independent of the
+// input (fp32 scores -> bf16 probabilities in the same pass).
+template <typename TI, typename TO, int NJ>
+__global__ void __launch_bounds__(256) softmax_rows_k(const TI* __restrict__ x, TO* __restrict__ y, int64_t R, int C) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= R) return;
+  const TI* xr = x + r * C;
+  float v[NJ];
+  float m = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = lane + 64 * j;
+    v[j] = c < C ? to_f32(xr[c]) : -INFINITY;
+    m = fmaxf(m, v[j]);
+  }
+  m = wave_max(m);
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    v[j] = lane + 64 * j < C ? __expf(v[j] - m) : 0.f;
+    s += v[j];
+  }
+  const float inv = 1.f / wave_sum(s);
+  TO* yr = y + r * C;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = lane + 64 * j;
+    if (c < C) yr[c] = from_f32<TO>(v[j] * inv);
+  }
+}
+
+template <typename T, int NJ>
+__global__ void __launch_bounds__(256) softmax_bwd_rows_k(const T* __restrict__ y, const T* __restrict__ dy,
+                                                          T* __restrict__ dx, int64_t R, int C) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= R) return;
+  float yv[NJ], gv[NJ];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = lane + 64 * j;
+    yv[j] = c < C ? to_f32(y[r * C + c]) : 0.f;
+    gv[j] = c < C ? to_f32(dy[r * C + c]) : 0.f;
+    s += yv[j] * gv[j];
+  }
+  s = wave_sum(s);
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = lane + 64 * j;
+    if (c < C) dx[r * C + c] = from_f32<T>(yv[j] * (gv[j] - s));
+  }
+}
+
+// ---- LayerNorm backward, rows batched per workgroup ----
+// The per-row kernel above adds every row's dgamma/dbeta contribution with a
+// global atomic per element: 2*D atomics per row, all rows hammering the same
+// D addresses (BERT: 4096 rows x 1536 atomics, 128 us per call, 21 % of the
+// step).  Here each wave owns a row at a time, lane l owns the 4-column
+// groups 4*(l + 64*j), dgamma/dbeta partials stay in registers across the
+// workgroup's rows, the 4 waves combine through LDS, and each workgroup
+// issues ONE atomic per column.
+template <typename T> struct V4;
+template <> struct V4<float> {
+  __device__ static void ld(const float* p, float v[4]) {
+    const float4 t = *(const float4*)p;
+    v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+  }
+  __device__ static void st(float* p, const float v[4]) { *(float4*)p = make_float4(v[0], v[1], v[2], v[3]); }
+};
+template <> struct V4<bf16> {
+  __device__ static void ld(const bf16* p, float v[4]) {
+    const bf16x4 t = *(const bf16x4*)p;
+    v[0] = (float)t[0]; v[1] = (float)t[1]; v[2] = (float)t[2]; v[3] = (float)t[3];
+  }
+  __device__ static void st(bf16* p, const float v[4]) {
+    bf16x4 t;
+    t[0] = (bf16)v[0]; t[1] = (bf16)v[1]; t[2] = (bf16)v[2]; t[3] = (bf16)v[3];
+    *(bf16x4*)p = t;
+  }
+};
+
+template <typename T, int NJ>
+__global__ void __launch_bounds__(256) layernorm_bwd_rows_k(const T* __restrict__ x, const T* __restrict__ dy,
+                                                            const float* __restrict__ g, const float* __restrict__ mean,
+                                                            const float* __restrict__ rstd, T* __restrict__ dx,
+                                                            float* __restrict__ dg, float* __restrict__ db, int64_t R,
+                                                            int D, int rpb) {
+  extern __shared__ float red[];  // [4 waves][2][D]
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  float gw[NJ][4], adg[NJ][4], adb[NJ][4];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = 4 * (lane + 64 * j);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      gw[j][e] = (g && c < D) ? g[c + e] : 1.f;
+      adg[j][e] = 0.f;
+      adb[j][e] = 0.f;
+    }
+  }
+  const int64_t r0 = (int64_t)blockIdx.x * rpb;
+  const int64_t r1 = r0 + rpb < R ? r0 + rpb : R;
+  const float invD = 1.f / D;
+  for (int64_t r = r0 + wave; r < r1; r += 4) {
+    const float mu = mean[r], rs = rstd[r];
+    float xh[NJ][4], dv[NJ][4];
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int c = 4 * (lane + 64 * j);
+      if (c < D) {
+        V4<T>::ld(x + r * D + c, xh[j]);
+        V4<T>::ld(dy + r * D + c, dv[j]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { xh[j][e] = mu; dv[j][e] = 0.f; }
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        xh[j][e] = (xh[j][e] - mu) * rs;
+        const float gy = dv[j][e] * gw[j][e];
+        a += gy;
+        b += gy * xh[j][e];
+      }
+    }
+    a = wave_sum(a) * invD;
+    b = wave_sum(b) * invD;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int c = 4 * (lane + 64 * j);
+      if (c < D) {
+        float o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          o[e] = rs * (dv[j][e] * gw[j][e] - a - xh[j][e] * b);
+          adg[j][e] += dv[j][e] * xh[j][e];
+          adb[j][e] += dv[j][e];
+        }
+        V4<T>::st(dx + r * D + c, o);
+      }
+    }
+  }
+  if (!dg && !db) return;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = 4 * (lane + 64 * j);
+    if (c < D) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        red[(wave * 2) * D + c + e] = adg[j][e];
+        red[(wave * 2 + 1) * D + c + e] = adb[j][e];
+      }
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < D; c += 256) {
+    float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      s0 += red[(w * 2) * D + c];
+      s1 += red[(w * 2 + 1) * D + c];
+    }
+    if (dg) atomicAdd(dg + c, s0);
+    if (db) atomicAdd(db + c, s1);
+  }
+}
+
 }  // namespace sg
 
 using namespace sg;
@@ -194,7 +368,32 @@ void sg_softmax_fwd(const void* x, void* y, int64_t R, int C, int dtype, int out
   DISPATCH_FT(dtype, hipLaunchKernelGGL(softmax_fwd_k<T>, dim3(R), dim3(256), sm, s, (const T*)x,
                                         out_f32 ? (float*)y : nullptr, out_f32 ? nullptr : (T*)y, C));
 }
+// short rows (C <= 1024): one wave per row; in_dt / out_dt: kF32 or kBF16
+void sg_softmax_rows(const void* x, void* y, int64_t R, int C, int in_dt, int out_dt, hipStream_t s) {
+  const int nj = (C + 63) / 64;
+  const dim3 grid((unsigned)((R + 3) / 4));
+#define SMR(TI, TO, NJ) hipLaunchKernelGGL((softmax_rows_k<TI, TO, NJ>), grid, dim3(256), 0, s, (const TI*)x, (TO*)y, R, C)
+#define SMR_NJ(TI, TO)                                                 \
+  if (nj <= 1) { SMR(TI, TO, 1); } else if (nj <= 2) { SMR(TI, TO, 2); } \
+  else if (nj <= 4) { SMR(TI, TO, 4); } else if (nj <= 8) { SMR(TI, TO, 8); } else { SMR(TI, TO, 16); }
+  if (in_dt == kF32 && out_dt == kF32) { SMR_NJ(float, float); }
+  else if (in_dt == kF32) { SMR_NJ(float, bf16); }
+  else if (out_dt == kF32) { SMR_NJ(bf16, float); }
+  else { SMR_NJ(bf16, bf16); }
+#undef SMR_NJ
+#undef SMR
+}
 void sg_softmax_bwd(const void* y, const void* dy, void* dx, int64_t R, int C, int dtype, hipStream_t s) {
+  if (C <= 1024) {
+    const int nj = (C + 63) / 64;
+    const dim3 grid((unsigned)((R + 3) / 4));
+#define SMB(NJ) DISPATCH_FT(dtype, hipLaunchKernelGGL((softmax_bwd_rows_k<T, NJ>), grid, dim3(256), 0, s, (const T*)y, \
+                                                      (const T*)dy, (T*)dx, R, C))
+    if (nj <= 1) { SMB(1); } else if (nj <= 2) { SMB(2); } else if (nj <= 4) { SMB(4); }
+    else if (nj <= 8) { SMB(8); } else { SMB(16); }
+#undef SMB
+    return;
+  }
   DISPATCH_FT(dtype, hipLaunchKernelGGL(softmax_bwd_k<T>, dim3(R), dim3(256), 0, s, (const T*)y, (const T*)dy,
                                         (T*)dx, C));
 }
@@ -212,6 +411,21 @@ void sg_layernorm_fwd(const void* x, const void* g, const void* b, void* y, void
 }
 void sg_layernorm_bwd(const void* x, const void* dy, const void* g, const void* mean, const void* rstd, void* dx,
                       void* dg, void* db, int64_t R, int D, int dtype, hipStream_t s) {
+  if (D % 4 == 0 && D <= 2048) {
+    // ~512 workgroups, whole waves' worth of rows each (R = 4096 -> 8 rows / workgroup)
+    int64_t rpb = (R + 511) / 512;
+    rpb = rpb < 4 ? 4 : (rpb + 3) / 4 * 4;
+    const int64_t nb = (R + rpb - 1) / rpb;
+    const size_t lds = (size_t)8 * D * sizeof(float);
+    const int nj = (D + 255) / 256;
+#define LNB(NJ)                                                                                                  \
+  DISPATCH_FT(dtype, hipLaunchKernelGGL((layernorm_bwd_rows_k<T, NJ>), dim3(nb), dim3(256), lds, s, (const T*)x, \
+                                        (const T*)dy, (const float*)g, (const float*)mean, (const float*)rstd,    \
+                                        (T*)dx, (float*)dg, (float*)db, R, D, (int)rpb))
+    if (nj <= 1) { LNB(1); } else if (nj <= 2) { LNB(2); } else if (nj <= 4) { LNB(4); } else { LNB(8); }
+#undef LNB
+    return;
+  }
   DISPATCH_FT(dtype, hipLaunchKernelGGL(layernorm_bwd_k<T>, dim3(R), dim3(256), 0, s, (const T*)x, (const T*)dy,
                                         (const float*)g, (const float*)mean, (const float*)rstd, (T*)dx, (float*)dg,
                                         (float*)db, D));

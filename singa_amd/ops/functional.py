@@ -220,8 +220,19 @@ def dropout_bwd(dy: torch.Tensor, mask: torch.Tensor, ratio: float) -> torch.Ten
 # ----------------------------------------------------------------------------
 # softmax / losses / layernorm
 # ----------------------------------------------------------------------------
-def softmax(x: torch.Tensor, axis: int = -1) -> torch.Tensor:
+def softmax(x: torch.Tensor, axis: int = -1, out_dtype: Optional[torch.dtype] = None) -> torch.Tensor:
+    """Row softmax over ``axis``; ``out_dtype`` (fp32 / bf16, default x's)
+    lets fp32 scores come out as bf16 probabilities in the same pass."""
     axis = axis % x.dim()
+    od = out_dtype or x.dtype
+    if (_native_ok(x) and _flat_ok(x) and axis == x.dim() - 1 and x.is_contiguous() and x.shape[-1] <= 1024
+            and od in (torch.float32, torch.bfloat16)):
+        C = x.shape[-1]  # short rows: one wave per row
+        y = torch.empty(x.shape, dtype=od, device=x.device)
+        N.lib().softmax_rows(x.data_ptr(), y.data_ptr(), x.numel() // C, C, N.dt(x), N.dt(y), N.stream())
+        return y
+    if od != x.dtype:
+        return softmax(x, axis).to(od)
     if _native_ok(x) and _flat_ok(x) and axis == x.dim() - 1 and x.is_contiguous() and x.shape[-1] <= 16384:
         C = x.shape[-1]
         y = torch.empty_like(x)
@@ -1161,7 +1172,7 @@ def attention_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, mask: Optio
         s = _bgemm(q3, k3, Sq, Sk, D, B, 0, 0, D, D, Sq * D, Sk * D, alpha=scale, out_dtype=torch.float32)
         if mask is not None:
             s = (s.view(*lead, Sq, Sk) + mask.to(torch.float32)).reshape(B, Sq, Sk)
-        p = softmax(s).to(torch.bfloat16)
+        p = softmax(s, out_dtype=torch.bfloat16)
         o = _bgemm(p, v3, Sq, D, Sk, B, 0, 1, Sk, D, Sq * Sk, Sk * D)
         return o.view(*lead, Sq, D), p.view(*lead, Sq, Sk)
     s = torch.matmul(q.float(), k.float().transpose(-1, -2)) * scale

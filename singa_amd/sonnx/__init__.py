@@ -400,6 +400,11 @@ def _x_merge_heads(c, op, xs, i, o):
     c.add("Reshape", [t, c.const(np.asarray([0, 0, H * D], np.int64))], [o[0]])
 
 
+@exporter("Embedding")
+def _x_embedding(c, op, xs, i, o):
+    c.add("Gather", [i[0], i[1]], [o[0]], axis=0)
+
+
 @exporter("TorchCLS")
 def _x_cls(c, op, xs, i, o):
     c.add("Gather", [i[0], c.const(np.asarray(0, np.int64))], [o[0]], axis=1)
@@ -499,7 +504,10 @@ def importer(*names):
 
 
 def _np(t) -> np.ndarray:
-    return t.data.detach().cpu().numpy() if isinstance(t, Tensor) else np.asarray(t)
+    if isinstance(t, Tensor):
+        h = getattr(t, "_host_np", None)  # constant initializers keep their host copy: no device sync
+        return h if h is not None else t.data.detach().cpu().numpy()  # (a sync cannot be captured)
+    return np.asarray(t)
 
 
 def _ints(t) -> List[int]:
@@ -686,7 +694,12 @@ def _i_gather(rep, n, x, a):
     idx = x[1]
     if ax == 0 and isinstance(idx, Tensor) and idx.creator is None and not rep.is_const(n.input[1]):
         return [autograd.embedding(idx, x[0])]
-    return [autograd.gather(x[0], ax, _np(idx))]
+    if (ax == 0 and isinstance(idx, Tensor) and x[0].data.dim() == 2 and not idx.data.is_floating_point()
+            and (_np(idx) >= 0).all()):  # constant row ids (BERT position ids): the capture-safe embedding op
+        return [autograd.embedding(idx, x[0])]
+    # a device-resident index (constant initializer): no host->device copy, which a HIP graph cannot capture
+    return [autograd.gather(x[0], ax, idx.data if isinstance(idx, Tensor) and idx.data.device == x[0].data.device
+                            else _np(idx))]
 
 
 @importer("Squeeze")
@@ -1016,6 +1029,7 @@ class SingaRep:
             ten.name = t.name
             if not is_param:
                 self._consts.add(t.name)
+                ten._host_np = a
             self.inits[t.name] = ten
         init_names = set(self.inits)
         self.input_names = [v.name for v in g.input if v.name not in init_names]
@@ -1045,7 +1059,9 @@ class SingaRep:
         return name in self._consts
 
     def const_tensor(self, a: np.ndarray) -> Tensor:
-        return Tensor(device=self.device, data=torch.from_numpy(np.array(a, order="C")), requires_grad=False)
+        t = Tensor(device=self.device, data=torch.from_numpy(np.array(a, order="C")), requires_grad=False)
+        t._host_np = np.asarray(a)
+        return t
 
     def params(self) -> Dict[str, Tensor]:
         return OrderedDict((k, v) for k, v in self.inits.items() if v.stores_grad)

@@ -43,7 +43,7 @@ class Tensor:
     """SINGA tensor.  ``data`` is the backing ``torch.Tensor``."""
 
     __slots__ = ("data", "device", "requires_grad", "stores_grad", "creator", "name", "_grad", "__weakref__",
-                 "grad_view", "low", "param_meta")
+                 "grad_view", "low", "param_meta", "_host_np")
 
     def __init__(self, shape: Sequence[int] = (), device: Optional[_dev.Device] = None, dtype=float32,
                  data=None, requires_grad: bool = True, stores_grad: bool = False, creator=None,

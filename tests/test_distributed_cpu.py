@@ -2,6 +2,8 @@
 synchronous data parallelism (DistOpt), EASGD and RandomSync.  The oracle is
 the reference's "rank 0 recomputes with gathered data" pattern
 (src/test/test_da.cc:38-61) or a single-process run on the global batch."""
+import threading
+
 import numpy as np
 import pytest
 import torch
@@ -83,13 +85,18 @@ def _data(n=16):
     return rng.randn(n, 20).astype(np.float32), rng.randint(0, 10, n).astype(np.int32)
 
 
+_INIT_LOCK = threading.Lock()
+
+
 def _train(m, X, Y, steps, optim, seed=0):
     from singa_amd import device, tensor
 
-    device.get_default_device().SetRandSeed(seed)
-    m.set_optimizer(optim)
     tx, ty = tensor.from_numpy(X), tensor.from_numpy(Y)
-    m.compile([tx], is_train=True)
+    with _INIT_LOCK:  # ranks run as threads (parallel.fake) share the default device's RNG
+        device.get_default_device().SetRandSeed(seed)
+        m.compile([tx], is_train=False)
+    m.set_optimizer(optim)
+    m.compile([tx], is_train=True)  # attach (DistOpt: broadcast rank 0's weights) outside the lock
     losses = []
     for _ in range(steps):
         _, l = m(tx, ty)

@@ -397,19 +397,58 @@ def test_softmax_xent(gpu, C):
     assert rel_err(d, sr * (dyy - (dyy * sr).sum(1, keepdim=True))) < 1e-5
 
 
-def test_layernorm(gpu):
+@pytest.mark.parametrize("R,D", [(64, 768), (4099, 768), (37, 100), (300, 1024), (50, 2048), (40, 2050), (9, 36)])
+def test_layernorm(gpu, R, D):
+    """fp32 kernels vs PyTorch fp32: the row-batched backward (D % 4 == 0,
+    D <= 2048, partial last workgroup, padded lanes) and the per-row
+    fallback (D = 2050)."""
     from singa_amd.ops import functional as F
     g = torch.Generator().manual_seed(9)
-    x = torch.randn(64, 768, generator=g)
-    gm, bt = torch.rand(768, generator=g) + 0.5, torch.randn(768, generator=g)
-    dy = torch.randn(64, 768, generator=g)
+    x = torch.randn(R, D, generator=g)
+    gm, bt = torch.rand(D, generator=g) + 0.5, torch.randn(D, generator=g)
+    dy = torch.randn(R, D, generator=g)
     xr, gr, br = x.clone().requires_grad_(True), gm.clone().requires_grad_(True), bt.clone().requires_grad_(True)
-    yr = TF.layer_norm(xr, (768,), gr, br, 1e-5)
+    yr = TF.layer_norm(xr, (D,), gr, br, 1e-5)
     yr.backward(dy)
     y, mu, rs = F.layernorm_fwd(x.to(gpu), gm.to(gpu), bt.to(gpu))
     assert rel_err(y, yr.detach()) < 1e-5
     dx, dg, db = F.layernorm_bwd(x.to(gpu), dy.to(gpu), gm.to(gpu), mu, rs)
     assert rel_err(dx, xr.grad) < 1e-4 and rel_err(dg, gr.grad) < 1e-4 and rel_err(db, br.grad) < 1e-4
+
+
+def test_layernorm_bwd_bf16(gpu):
+    from singa_amd.ops import functional as F
+    g = torch.Generator().manual_seed(10)
+    x = torch.randn(4096, 768, generator=g).bfloat16()
+    gm = torch.rand(768, generator=g) + 0.5
+    dy = torch.randn(4096, 768, generator=g).bfloat16()
+    xr, gr = x.float().requires_grad_(True), gm.clone().requires_grad_(True)
+    TF.layer_norm(xr, (768,), gr, None, 1e-5).backward(dy.float())
+    _, mu, rs = F.layernorm_fwd(x.to(gpu), gm.to(gpu), None)
+    dx, dg, db = F.layernorm_bwd(x.to(gpu), dy.to(gpu), gm.to(gpu), mu, rs)
+    assert dx.dtype == torch.bfloat16
+    assert rel_err(dx, xr.grad) < 1e-2 and rel_err(dg, gr.grad) < 1e-4
+    assert rel_err(db, dy.float().sum(0)) < 1e-4
+
+
+@pytest.mark.parametrize("C", [5, 64, 128, 300, 1024])
+@pytest.mark.parametrize("in_dt,out_dt", [(torch.float32, torch.float32), (torch.float32, torch.bfloat16),
+                                          (torch.bfloat16, torch.bfloat16)])
+def test_softmax_short_rows(gpu, C, in_dt, out_dt):
+    """Wave-per-row softmax (C <= 1024) with an independent output dtype,
+    and its backward, vs PyTorch fp32."""
+    from singa_amd.ops import functional as F
+    g = torch.Generator().manual_seed(11)
+    x = (torch.randn(2, 3, 77, C, generator=g) * 3).to(in_dt)
+    y = F.softmax(x.to(gpu), -1, out_dtype=out_dt)
+    ref = torch.softmax(x.float(), -1)
+    assert y.dtype == out_dt and y.shape == x.shape
+    assert rel_err(y, ref) < (1e-6 if out_dt == torch.float32 else 1e-2)
+    dy = torch.randn(x.shape, generator=g).to(out_dt)
+    d = F.softmax_bwd(y, dy.to(gpu))
+    yf = y.float().cpu()
+    assert rel_err(d, yf * (dy.float() - (dy.float() * yf).sum(-1, keepdim=True))) < (1e-5 if out_dt == torch.float32
+                                                                                       else 2e-2)
 
 
 @pytest.mark.parametrize("op", ["relu", "sigmoid", "tanh", "stanh", "gelu", "softplus", "exp", "abs", "square",

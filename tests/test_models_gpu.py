@@ -589,3 +589,46 @@ def test_fused_downsample_bn_model_step(gpu, monkeypatch, depth):
         upd = (a - init[k].float()).abs().max().item()
         if upd > 0:
             assert (a - out["1"][1][k]).abs().max().item() <= 0.1 * upd, (k, (a - out["1"][1][k]).abs().max().item(), upd)
+
+
+@pytest.mark.parametrize("imported", [False, True])
+def test_bert_graph_matches_eager(gpu, imported):
+    """HIP-graph replay of a BERT training step (native model, and the same
+    model exported to ONNX and re-imported with import-time fusion) ==
+    eager execution.  The embedding backward is the capture-safe index_add
+    scatter (torch's sort/unique backward faults under capture)."""
+    from singa_amd import sonnx
+    from singa_amd.models import bert
+    from singa_amd.sonnx import onnx_proto as P
+
+    rng = np.random.RandomState(0)
+    ids_np = rng.randint(0, 1000, (8, 32)).astype(np.int64)
+    y_np = rng.randint(0, 2, 8).astype(np.int32)
+    blob = None
+    if imported:
+        cpu = device.get_default_device()
+        cpu.SetRandSeed(0)
+        src = bert.bert_tiny(dropout=0.0, compute_dtype=torch.float32)
+        ids_cpu = tensor.from_numpy(ids_np[:2])
+        src.compile([ids_cpu], is_train=False)
+        blob = sonnx.to_onnx(src, [ids_cpu]).SerializeToString()
+    curves = []
+    for use_graph in (False, True):
+        dev = device.create_rocm_gpu()
+        dev.SetRandSeed(0)
+        if imported:
+            m = sonnx.SONNXModel(P.load_model(blob), dev, compute_dtype=torch.bfloat16)
+            assert {st.kind for st in m.rep.fused.values()} == {"linear", "gelu", "attention"}
+        else:
+            m = bert.bert_tiny(dropout=0.0, compute_dtype=torch.bfloat16)
+        ids = tensor.from_numpy(ids_np).to_device(dev)
+        y = tensor.from_numpy(y_np).to_device(dev)
+        m.set_optimizer(opt.Adam(1e-3))
+        m.compile([ids], is_train=True, use_graph=use_graph)
+        m.train()
+        ls = [m(ids, y)[1].data.detach().float().reshape(()).clone() for _ in range(6)]
+        torch.cuda.synchronize()
+        curves.append([float(v) for v in ls])
+    e, g = np.array(curves[0]), np.array(curves[1])
+    assert np.all(np.isfinite(g)), curves
+    np.testing.assert_allclose(g, e, rtol=2e-2, atol=2e-3)
