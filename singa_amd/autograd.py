@@ -986,16 +986,19 @@ class LayerNorm(Operator):
         return y
 
     def backward(self, dy):
-        dx, dg, db = F.layernorm_bwd(self.x, dy.contiguous(), self.g, self.mean, self.rstd)
+        tg = self.grad_target(1) if len(self.src) > 1 else None
+        tb = self.grad_target(2) if len(self.src) > 2 else None
+        # the kernel accumulates dgamma / dbeta straight into the flat-store views
+        dx, dg, db = F.layernorm_bwd(self.x, dy.contiguous(), self.g, self.mean, self.rstd, dg_acc=tg, db_acc=tb)
         self.x = None
         out = [dx]
         if len(self.src) > 1:
-            for i, gg in ((1, dg), (2, db)):
+            for i, gg, t in ((1, dg, tg), (2, db, tb)):
                 if i >= len(self.src):
                     break
-                t = self.grad_target(i)
                 if t is not None and gg is not None:
-                    t.add_(gg)
+                    if gg is not t:
+                        t.add_(gg.reshape(t.shape))
                     out.append(ACCUMULATED)
                 else:
                     out.append(gg)

@@ -29,8 +29,9 @@ class SplitHeads(autograd.Operator):
     def forward(self, x):
         B, S, E3 = x.shape
         D = E3 // (3 * self.h)
-        t = x.view(B, S, 3, self.h, D).permute(2, 0, 3, 1, 4)
-        return t[0].contiguous(), t[1].contiguous(), t[2].contiguous()
+        # one permuting copy; q, k, v are contiguous slices of it
+        t = x.view(B, S, 3, self.h, D).permute(2, 0, 3, 1, 4).contiguous()
+        return t[0], t[1], t[2]
 
     def backward(self, dq, dk, dv):
         ref = next(d for d in (dq, dk, dv) if d is not None)

@@ -321,13 +321,22 @@ def layernorm_fwd(x: torch.Tensor, g: Optional[torch.Tensor], b: Optional[torch.
     return y.to(x.dtype).reshape(x.shape), mean, rstd
 
 
-def layernorm_bwd(x, dy, g, mean, rstd):
+def layernorm_bwd(x, dy, g, mean, rstd, dg_acc=None, db_acc=None):
+    """Returns (dx, dg, db).  ``dg_acc`` / ``db_acc``: fp32 [D] gradient
+    buffers (the parameters' flat-store views) the kernel ACCUMULATES into
+    directly -- returned as dg / db (no zeroed temporaries, no extra adds)."""
     D = x.shape[-1]
     R = x.numel() // D
+
+    def _acc_ok(t):
+        return t is not None and t.dtype == torch.float32 and t.is_contiguous() and t.numel() == D and t.is_cuda
+
     if _native_ok(x, dy) and _flat_ok(x) and x.is_contiguous() and dy.is_contiguous():
         dx = torch.empty_like(x)
-        dg = torch.zeros(D, dtype=torch.float32, device=x.device) if g is not None else None
-        db = torch.zeros(D, dtype=torch.float32, device=x.device) if g is not None else None
+        dg = db = None
+        if g is not None:
+            dg = dg_acc if _acc_ok(dg_acc) else torch.zeros(D, dtype=torch.float32, device=x.device)
+            db = db_acc if _acc_ok(db_acc) else torch.zeros(D, dtype=torch.float32, device=x.device)
         gg = g.float().contiguous() if g is not None else None
         N.lib().layernorm_bwd(x.data_ptr(), dy.data_ptr(), N.ptr(gg), mean.data_ptr(), rstd.data_ptr(),
                               dx.data_ptr(), N.ptr(dg), N.ptr(db), R, D, N.dt(x), N.stream())
@@ -341,6 +350,10 @@ def layernorm_bwd(x, dy, g, mean, rstd):
     a = gg.mean(1, keepdim=True)
     bsum = (gg * xh).mean(1, keepdim=True)
     dx = rstd[:, None] * (gg - a - xh * bsum)
+    if dg is not None and dg_acc is not None:
+        dg = dg_acc.add_(dg.reshape(dg_acc.shape))
+    if db is not None and db_acc is not None:
+        db = db_acc.add_(db.reshape(db_acc.shape))
     return dx.to(x.dtype).reshape(x.shape), dg, db
 
 
