@@ -1086,6 +1086,29 @@ class Attention(Operator):
         return (dq, dk, dv) + ((None,) if len(self.src) == 4 else ())
 
 
+class QKVAttention(Operator):
+    """Multi-head attention fed by the fused q/k/v projection: qkv [B, S,
+    3*H*D] -> [B, S, H*D].  Equivalent to split-heads -> Attention ->
+    merge-heads, but the batched MFMA GEMMs address each head in place
+    (functional.attention_qkv_*), so neither direction copies the heads."""
+
+    def __init__(self, heads: int, scale: Optional[float] = None, name=None):
+        super().__init__(name)
+        self.heads, self.scale = heads, scale
+
+    def forward(self, qkv, mask=None):
+        o, p = F.attention_qkv_fwd(qkv, self.heads, mask, self.scale)
+        if self.requires_grad:
+            self.saved = (qkv, p)
+        return o
+
+    def backward(self, do):
+        qkv, p = self.saved
+        self.saved = None
+        dqkv = F.attention_qkv_bwd(qkv, p, do, self.heads, self.scale)
+        return (dqkv, None) if len(self.src) == 2 else dqkv
+
+
 def attention(q, k, v, mask=None, scale=None):
     return Attention(scale)(q, k, v, mask) if mask is not None else Attention(scale)(q, k, v)
 

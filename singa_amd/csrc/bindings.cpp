@@ -38,6 +38,9 @@ void sg_softmax_xent(const void*, const void*, const void*, void*, void*, void*,
 void sg_layernorm_fwd(const void*, const void*, const void*, void*, void*, void*, int64_t, int, int, float,
                       hipStream_t);
 void sg_softmax_rows(const void*, void*, int64_t, int, int, int, hipStream_t);
+void sg_gemm_heads(const void*, int64_t, int, const void*, int64_t, int, void*, int64_t, int, int, int, float, float,
+                   const void*, int, int, int, int, int64_t, int64_t, int64_t, int, int64_t, int64_t, int64_t,
+                   hipStream_t);
 void sg_layernorm_bwd(const void*, const void*, const void*, const void*, const void*, void*, void*, void*, int64_t,
                       int, int, hipStream_t);
 int sg_colreduce_bands(int64_t, int);
@@ -277,6 +280,13 @@ PYBIND11_MODULE(_C, m) {
     sg_gemm(CV(a), lda, ako, CV(b), ldb, bko, V(c), ldc, M, N, K, alpha, beta, CV(bias), relu, out_mode, splits,
             batch, sa, sb, sc, S(s));
     CHK("gemm");
+  });
+  m.def("gemm_heads", [](P a, int64_t lda, int ako, P b, int64_t ldb, int bko, P c, int64_t ldc, int M, int N, int K,
+                         float alpha, float beta, int out_mode, int batch, int64_t sa, int64_t sb, int64_t sc, int bh,
+                         int64_t sa2, int64_t sb2, int64_t sc2, P s) {
+    sg_gemm_heads(CV(a), lda, ako, CV(b), ldb, bko, V(c), ldc, M, N, K, alpha, beta, nullptr, 0, out_mode, 1, batch,
+                  sa, sb, sc, bh, sa2, sb2, sc2, S(s));
+    CHK("gemm_heads");
   });
   m.def("conv_fwd", [](P x, P w, P y, P bias, int N, int H, int W, int C, int K, int R, int Sd, int Ho, int Wo,
                        int sh, int sw, int ph, int pw, int dh, int dw, int relu, int out_mode, P s, P stats) {

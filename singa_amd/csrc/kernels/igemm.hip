@@ -87,6 +87,10 @@ struct GemmArgs {
   int relu;
   int k_per_split;     // multiple of BK
   int64_t sa, sb, sc;  // batch strides (elements), blockIdx.y = batch
+  // two-level batch (attention heads read in place from a [B][S][3][H][D]
+  // projection): with bh > 0, batch y -> (y / bh) * s? + (y % bh) * s?2
+  int bh;
+  int64_t sa2, sb2, sc2;
   int out_phase;       // dgrad: output rows map through the phase grid
   int lds_epilogue;    // stage bf16 output tiles through LDS (16-byte stores)
   unsigned a_bytes, b_bytes;  // operand extents (buffer-resource ranges; per batch slice)
@@ -514,9 +518,11 @@ __global__ void __launch_bounds__(NTH, STAGES == 1 ? 3 : (NTH == 512 && STAGES =
   constexpr int TM = WTM / 16, TN = WTN / 16;  // 16x16 MFMA tiles per wave
   static_assert(WM * WN * 64 == NTH, "wave grid");
 
-  const bf16* __restrict__ pa = p.a + (int64_t)blockIdx.y * p.sa;
-  const bf16* __restrict__ pb = p.b + (int64_t)blockIdx.y * p.sb;
-  char* pc = (char*)p.c + (int64_t)blockIdx.y * p.sc * (OUT == OUT_BF16 ? 2 : 4);
+  const int64_t yb = p.bh > 0 ? (int64_t)(blockIdx.y / p.bh) : (int64_t)blockIdx.y;
+  const int64_t yh = p.bh > 0 ? (int64_t)(blockIdx.y % p.bh) : 0;
+  const bf16* __restrict__ pa = p.a + yb * p.sa + yh * p.sa2;
+  const bf16* __restrict__ pb = p.b + yb * p.sb + yh * p.sb2;
+  char* pc = (char*)p.c + (yb * p.sc + yh * p.sc2) * (OUT == OUT_BF16 ? 2 : 4);
   // dgrad: phase from blockIdx.z (the output rows are that phase's pixels)
   const int phase = p.out_phase ? (int)blockIdx.z : 0;
   const Phase& P = p.g.phs[phase];
@@ -1282,12 +1288,28 @@ int sg_ws_prezeroed();      // batchnorm.hip: one-shot 'workspace pre-zeroed' fl
 //   a_kouter = 0: A stored [M][K] (lda), 1: A stored [K][M]
 //   b_kouter = 0: B stored [N][K] (ldb), 1: B stored [K][N]
 // out_mode 0 bf16, 1 f32, 2 f32 atomic (split-K, C pre-initialised).
+void sg_gemm_heads(const void* a, int64_t lda, int a_kouter, const void* b, int64_t ldb, int b_kouter, void* c,
+                   int64_t ldc, int M, int N, int K, float alpha, float beta, const void* bias, int relu,
+                   int out_mode, int splits, int batch, int64_t sa, int64_t sb, int64_t sc, int bh, int64_t sa2,
+                   int64_t sb2, int64_t sc2, hipStream_t s);
+
 void sg_gemm(const void* a, int64_t lda, int a_kouter, const void* b, int64_t ldb, int b_kouter, void* c,
              int64_t ldc, int M, int N, int K, float alpha, float beta, const void* bias, int relu, int out_mode,
              int splits, int batch, int64_t sa, int64_t sb, int64_t sc, hipStream_t s) {
+  sg_gemm_heads(a, lda, a_kouter, b, ldb, b_kouter, c, ldc, M, N, K, alpha, beta, bias, relu, out_mode, splits,
+                batch, sa, sb, sc, 0, 0, 0, 0, s);
+}
+
+// sg_gemm with a two-level batch: batch index y -> (y / bh, y % bh) with
+// strides (sa, sa2), (sb, sb2), (sc, sc2); bh = 0 is the plain batched GEMM.
+void sg_gemm_heads(const void* a, int64_t lda, int a_kouter, const void* b, int64_t ldb, int b_kouter, void* c,
+                   int64_t ldc, int M, int N, int K, float alpha, float beta, const void* bias, int relu,
+                   int out_mode, int splits, int batch, int64_t sa, int64_t sb, int64_t sc, int bh, int64_t sa2,
+                   int64_t sb2, int64_t sc2, hipStream_t s) {
   GemmArgs p{};
   init_phase_identity(p.g);
   p.sa = sa; p.sb = sb; p.sc = sc;
+  p.bh = bh; p.sa2 = sa2; p.sb2 = sb2; p.sc2 = sc2;
   p.M = M; p.N = N; p.K = K; p.a = (const bf16*)a; p.lda = lda; p.b = (const bf16*)b; p.ldb = ldb;
   p.c = c; p.ldc = ldc; p.alpha = alpha; p.beta = beta; p.bias = (const float*)bias; p.relu = relu;
   splits = (out_mode == OUT_F32_ATOMIC) ? pick_splits(M, N, K, splits) : 1;

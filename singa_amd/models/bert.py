@@ -72,9 +72,10 @@ class EncoderLayer(layer.Layer):
         self.drop2 = layer.Dropout(dropout)
 
     def forward(self, x, mask: Optional[Tensor] = None):
-        q, k, v = SplitHeads(self.heads)(self.qkv(x))
-        a = autograd.attention(q, k, v, mask)
-        a = self.drop1(self.proj(MergeHeads()(a)))
+        qkv = self.qkv(x)
+        att = autograd.QKVAttention(self.heads)  # heads addressed in place: no split / merge copies
+        a = att(qkv, mask) if mask is not None else att(qkv)
+        a = self.drop1(self.proj(a))
         x = self.ln1(autograd.add(x, a))
         f = self.drop2(self.fc2(self.act(self.fc1(x))))
         return self.ln2(autograd.add(x, f))

@@ -1196,6 +1196,88 @@ def attention_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, mask: Optio
     return o.to(q.dtype), p.to(q.dtype)
 
 
+def _gemm_heads(a, lda, ako, b, ldb, bko, c, ldc, M, Nn, K, batch, bh, sa, sa2, sb, sb2, sc, sc2, alpha=1.0):
+    """Batched MFMA GEMM over (batch / bh, batch % bh) with two-level strides:
+    a, b, c are (tensor, element offset) pairs -- attention heads addressed in
+    place inside the [B, S, 3, H, D] projection / [B, S, H, D] output."""
+    (ta, oa), (tb, ob), (tc, oc) = a, b, c
+    mode = 0 if tc.dtype == torch.bfloat16 else 1
+    N.lib().gemm_heads(ta.data_ptr() + 2 * oa, lda, ako, tb.data_ptr() + 2 * ob, ldb, bko,
+                       tc.data_ptr() + tc.element_size() * oc, ldc, M, Nn, K, alpha, 0.0, mode, batch, sa, sb, sc,
+                       bh, sa2, sb2, sc2, N.stream())
+
+
+def _qkv_native_ok(qkv, H):
+    if not (_native_ok(qkv) and qkv.dtype == torch.bfloat16 and qkv.dim() == 3 and qkv.is_contiguous()):
+        return False
+    B, S, E = qkv.shape
+    return E % (3 * H) == 0 and (E // (3 * H)) % 8 == 0 and S % 8 == 0
+
+
+def attention_qkv_fwd(qkv: torch.Tensor, heads: int, mask: Optional[torch.Tensor] = None,
+                      scale: Optional[float] = None):
+    """Multi-head attention straight from the fused projection: qkv [B, S,
+    3*H*D] (per token: q heads, k heads, v heads) -> o [B, S, H*D] (heads
+    merged), p [B*H, S, S] (bf16 probabilities, kept for backward).  The
+    batched GEMMs address every (b, h) slice in place -- no split-heads /
+    merge-heads copies in either direction."""
+    B, S, E = qkv.shape
+    H = heads
+    D = E // (3 * H)
+    HD = H * D
+    scale = (1.0 / math.sqrt(D)) if scale is None else scale
+    if _qkv_native_ok(qkv, H):
+        BH = B * H
+        sc = torch.empty((BH, S, S), dtype=torch.float32, device=qkv.device)
+        # scores = q k^T * scale : q [S][D] rows of stride E, k [S][D] (N x K, K-major)
+        _gemm_heads((qkv, 0), E, 0, (qkv, HD), E, 0, (sc, 0), S, S, S, D, BH, H, S * E, D, S * E, D, H * S * S,
+                    S * S, alpha=scale)
+        if mask is not None:
+            sc = (sc.view(B, H, S, S) + mask.to(torch.float32)).reshape(BH, S, S)
+        p = softmax(sc, out_dtype=torch.bfloat16)
+        o = torch.empty((B, S, HD), dtype=torch.bfloat16, device=qkv.device)
+        # o = p v : v [S][D] is K-outer (ldb E); o rows of stride H*D
+        _gemm_heads((p, 0), S, 0, (qkv, 2 * HD), E, 1, (o, 0), HD, S, D, S, BH, H, H * S * S, S * S, S * E, D,
+                    S * HD, D)
+        return o, p
+    t = qkv.view(B, S, 3, H, D).permute(2, 0, 3, 1, 4)
+    o, p = attention_fwd(t[0], t[1], t[2], mask, scale)
+    return o.permute(0, 2, 1, 3).reshape(B, S, HD), p.reshape(B * H, S, S)
+
+
+def attention_qkv_bwd(qkv: torch.Tensor, p: torch.Tensor, do: torch.Tensor, heads: int,
+                      scale: Optional[float] = None) -> torch.Tensor:
+    """d(qkv) [B, S, 3*H*D] of :func:`attention_qkv_fwd` given do [B, S, H*D];
+    dq / dk / dv are written in place into their slots of d(qkv)."""
+    B, S, E = qkv.shape
+    H = heads
+    D = E // (3 * H)
+    HD = H * D
+    scale = (1.0 / math.sqrt(D)) if scale is None else scale
+    if _qkv_native_ok(qkv, H) and p.dtype == torch.bfloat16 and do.dtype == torch.bfloat16:
+        BH = B * H
+        do = do.contiguous()
+        dqkv = torch.empty_like(qkv)
+        SS = S * S
+        # dV = P^T dO
+        _gemm_heads((p, 0), S, 1, (do, 0), HD, 1, (dqkv, 2 * HD), E, S, D, S, BH, H, H * SS, SS, S * HD, D, S * E, D)
+        # dP = dO V^T
+        dp = torch.empty((BH, S, S), dtype=torch.bfloat16, device=qkv.device)
+        _gemm_heads((do, 0), HD, 0, (qkv, 2 * HD), E, 0, (dp, 0), S, S, S, D, BH, H, S * HD, D, S * E, D, H * SS,
+                    SS)
+        ds = softmax_bwd(p, dp)
+        # dQ = scale * dS K ; dK = scale * dS^T Q
+        _gemm_heads((ds, 0), S, 0, (qkv, HD), E, 1, (dqkv, 0), E, S, D, S, BH, H, H * SS, SS, S * E, D, S * E, D,
+                    alpha=scale)
+        _gemm_heads((ds, 0), S, 1, (qkv, 0), E, 1, (dqkv, HD), E, S, D, S, BH, H, H * SS, SS, S * E, D, S * E, D,
+                    alpha=scale)
+        return dqkv
+    t = qkv.view(B, S, 3, H, D).permute(2, 0, 3, 1, 4)
+    dq, dk, dv = attention_bwd(t[0], t[1], t[2], p.reshape(B, H, S, S),
+                               do.reshape(B, S, H, D).permute(0, 2, 1, 3), scale)
+    return torch.stack([dq, dk, dv], 0).permute(1, 3, 0, 2, 4).reshape(B, S, E).to(qkv.dtype)
+
+
 def attention_bwd(q, k, v, p, do, scale: Optional[float] = None):
     """Gradients (dq, dk, dv) of attention_fwd given the saved probabilities."""
     D = q.shape[-1]

@@ -405,6 +405,22 @@ def _x_embedding(c, op, xs, i, o):
     c.add("Gather", [i[0], i[1]], [o[0]], axis=0)
 
 
+@exporter("QKVAttention")
+def _x_qkv_attention(c, op, xs, i, o):
+    """Lowered as split-heads -> attention -> merge-heads (standard ONNX
+    ops); the importer's fusion plan maps the attention core back."""
+    from types import SimpleNamespace as NS
+
+    B, S, E = xs[0].shape
+    H = op.heads
+    D = E // (3 * H)
+    heads = NS(shape=(B, H, S, D))
+    q, k, v, a = c.fresh(), c.fresh(), c.fresh(), c.fresh()
+    _x_split_heads(c, NS(h=H), xs[:1], i[:1], [q, k, v])
+    _x_attention(c, NS(scale=op.scale), [heads, heads, heads] + list(xs[1:]), [q, k, v] + list(i[1:]), [a])
+    _x_merge_heads(c, None, [heads], [a], o)
+
+
 @exporter("TorchCLS")
 def _x_cls(c, op, xs, i, o):
     c.add("Gather", [i[0], c.const(np.asarray(0, np.int64))], [o[0]], axis=1)
@@ -834,8 +850,9 @@ class _Fused:
     member (every external input exists by then) and defines only the
     group's final output (the intermediates have no other consumer)."""
 
-    def __init__(self, kind: str, members, inputs, output: str, scale: Optional[float] = None):
+    def __init__(self, kind: str, members, inputs, output: str, scale: Optional[float] = None, heads: int = 0):
         self.kind, self.members, self.inputs, self.output, self.scale = kind, tuple(members), list(inputs), output, scale
+        self.heads = heads
 
     def _low(self, rep, t):
         cd = rep.compute_dtype
@@ -846,6 +863,10 @@ class _Fused:
             return autograd.linear(self._low(rep, xs[0]), xs[1], xs[2])
         if self.kind == "gelu":  # x * 0.5 * (1 + erf(x / sqrt 2)) -> one elementwise kernel
             return autograd.gelu(xs[0])
+        if self.kind == "qkv_attention":  # split-heads + attention + merge-heads -> heads addressed in place
+            att = autograd.QKVAttention(self.heads, self.scale)
+            qkv = self._low(rep, xs[0])
+            return att(qkv, xs[1]) if len(xs) > 1 else att(qkv)
         if self.kind == "attention":  # Transpose/MatMul/scale/[mask]/Softmax/MatMul -> batched-MFMA attention
             q, k, v = (self._low(rep, t) for t in xs[:3])
             return autograd.attention(q, k, v, xs[3] if len(xs) > 3 else None, self.scale)
@@ -982,6 +1003,60 @@ def _fusion_plan(nodes, inits: Dict[str, Tensor], consts: set, outputs: Sequence
         ins = [q, k_, nodes[t].input[1]] + ([mask] if mask is not None else [])
         return _Fused("attention", members, ins, nodes[t].output[0], scale)
 
+    prod = {o: idx for idx, nd in enumerate(nodes) for o in nd.output if o}
+
+    def single(name: str) -> bool:  # exactly one consumer, not a graph output
+        return len(cons.get(name, [])) == 1 and name not in outs
+
+    def host_ints(name: str):
+        t = inits.get(name)
+        h = getattr(t, "_host_np", None) if t is not None else None
+        return None if h is None else [int(v) for v in np.asarray(h).reshape(-1)]
+
+    def qkv_heads(st):
+        """Extend an attention group over the split-heads chain in front of
+        it -- Reshape([0,0,3,H,D]) -> Transpose([2,0,3,1,4]) -> Split(axis 0)
+        -> Squeeze x3 -- and the merge-heads chain behind it -- Transpose
+        ([0,2,1,3]) -> Reshape([0,0,H*D])."""
+        q, k_, v = st.inputs[:3]
+        sq = [prod.get(t) for t in (q, k_, v)]
+        if any(j is None or nodes[j].op_type != "Squeeze" or j in used or not single(t) for j, t in zip(sq, (q, k_, v))):
+            return None
+        srcs = [nodes[j].input[0] for j in sq]
+        sp = prod.get(srcs[0])
+        if sp is None or sp in used or nodes[sp].op_type != "Split" or list(nodes[sp].output) != srcs:
+            return None
+        if int(attr(nodes[sp], "axis", 0)) != 0 or not all(single(t) for t in srcs):
+            return None
+        t5 = nodes[sp].input[0]
+        tr = prod.get(t5)
+        if tr is None or tr in used or nodes[tr].op_type != "Transpose" or not single(t5):
+            return None
+        if list(attr(nodes[tr], "perm", [])) != [2, 0, 3, 1, 4]:
+            return None
+        r5 = nodes[tr].input[0]
+        rs = prod.get(r5)
+        if rs is None or rs in used or nodes[rs].op_type != "Reshape" or not single(r5):
+            return None
+        shp = host_ints(nodes[rs].input[1])
+        if shp is None or len(shp) != 5 or shp[2] != 3 or shp[0] != 0 or shp[1] != 0:
+            return None
+        H, D = shp[3], shp[4]
+        a = st.output
+        if not single(a):
+            return None
+        t2 = cons[a][0]
+        if t2 in used or nodes[t2].op_type != "Transpose" or list(attr(nodes[t2], "perm", [])) != [0, 2, 1, 3]:
+            return None
+        if not single(nodes[t2].output[0]):
+            return None
+        r2 = cons[nodes[t2].output[0]][0]
+        if r2 in used or nodes[r2].op_type != "Reshape" or host_ints(nodes[r2].input[1]) != [0, 0, H * D]:
+            return None
+        members = list(st.members) + sq + [sp, tr, rs, t2, r2]
+        return _Fused("qkv_attention", members, [nodes[rs].input[0]] + st.inputs[3:], nodes[r2].output[0], st.scale,
+                      heads=H)
+
     plan: Dict[int, _Fused] = {}
     for i in range(len(nodes)):
         if i in used:
@@ -992,6 +1067,13 @@ def _fusion_plan(nodes, inits: Dict[str, Tensor], consts: set, outputs: Sequence
                 used.update(st.members)
                 plan[max(st.members)] = st
                 break
+    for key, st in list(plan.items()):
+        if st.kind == "attention":
+            big = qkv_heads(st)
+            if big is not None:
+                del plan[key]
+                used.update(big.members)
+                plan[max(big.members)] = big
     return plan
 
 

@@ -757,3 +757,27 @@ def test_conv_short_k_single_stage(gpu, C, K, H, st, bn):
         yb = outs[0][0]
         s = torch.stack([yb.sum((0, 2, 3)), (yb * yb).sum((0, 2, 3))])
         assert rel_err(outs[2][2], s) < 1e-4 and rel_err(outs[0][2], s) < 1e-4
+
+
+@pytest.mark.parametrize("B,S,H,D,masked", [(2, 64, 4, 64, False), (3, 128, 12, 64, True), (1, 40, 2, 32, False)])
+def test_attention_qkv_in_place_heads(gpu, B, S, H, D, masked):
+    """attention_qkv_fwd / _bwd (two-level-batch MFMA GEMMs addressing the
+    heads inside the [B, S, 3, H, D] projection) vs PyTorch fp32 multi-head
+    attention on the same bf16 inputs."""
+    from singa_amd.ops import functional as F
+    g = torch.Generator().manual_seed(12)
+    qkv = (torch.randn(B, S, 3 * H * D, generator=g) * 0.5).bfloat16()
+    do = torch.randn(B, S, H * D, generator=g).bfloat16()
+    mask = ((torch.rand(B, 1, 1, S, generator=g) > 0.8).float() * -10000.0) if masked else None
+    o, p = F.attention_qkv_fwd(qkv.to(gpu), H, mask.to(gpu) if masked else None)
+    dqkv = F.attention_qkv_bwd(qkv.to(gpu), p, do.to(gpu), H)
+    x = qkv.float().requires_grad_(True)
+    t = x.view(B, S, 3, H, D).permute(2, 0, 3, 1, 4)
+    s = t[0] @ t[1].transpose(-1, -2) / math.sqrt(D)
+    if masked:
+        s = s + mask
+    ref = (torch.softmax(s, -1) @ t[2]).permute(0, 2, 1, 3).reshape(B, S, H * D)
+    ref.backward(do.float())
+    assert o.shape == (B, S, H * D) and dqkv.shape == qkv.shape
+    assert rel_err(o, ref.detach()) < 2e-2
+    assert rel_err(dqkv, x.grad) < 3e-2

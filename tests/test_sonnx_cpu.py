@@ -239,7 +239,7 @@ def test_import_fusion_plan_bert_matches_unfused():
         autograd.training = False
         res.append((out.data.clone(), grads))
     # bert_tiny: 2 layers x (qkv, proj, fc1, fc2) + pooler + classifier
-    assert kinds == {"linear": 10, "gelu": 2, "attention": 2}, kinds
+    assert kinds == {"linear": 10, "gelu": 2, "qkv_attention": 2}, kinds
     (o0, g0), (o1, g1) = res
     np.testing.assert_allclose(o1.numpy(), o0.numpy(), atol=1e-5, rtol=1e-5)
     assert set(g0) == set(g1) and len(g0) > 20
