@@ -847,7 +847,7 @@ class LRN(Operator):
         return y
 
     def backward(self, dy):
-        dx = F.lrn_bwd(self.x, dy, self.norm, self.size, self.alpha, self.beta)
+        dx = F.lrn_bwd(self.x, dy, self.norm, self.size, self.alpha, self.beta, self.k)
         self.x = self.norm = None
         return dx
 

@@ -41,6 +41,7 @@ void sg_softmax_rows(const void*, void*, int64_t, int, int, int, hipStream_t);
 void sg_gemm_heads(const void*, int64_t, int, const void*, int64_t, int, void*, int64_t, int, int, int, float, float,
                    const void*, int, int, int, int, int64_t, int64_t, int64_t, int, int64_t, int64_t, int64_t,
                    hipStream_t);
+void sg_lrn_rows(const void*, const void*, void*, int64_t, int, int, float, float, float, int, int, hipStream_t);
 void sg_layernorm_bwd(const void*, const void*, const void*, const void*, const void*, void*, void*, void*, int64_t,
                       int, int, hipStream_t);
 int sg_colreduce_bands(int64_t, int);
@@ -287,6 +288,11 @@ PYBIND11_MODULE(_C, m) {
     sg_gemm_heads(CV(a), lda, ako, CV(b), ldb, bko, V(c), ldc, M, N, K, alpha, beta, nullptr, 0, out_mode, 1, batch,
                   sa, sb, sc, bh, sa2, sb2, sc2, S(s));
     CHK("gemm_heads");
+  });
+  m.def("lrn_rows", [](P x, P dy, P out, int64_t R, int C, int size, float alpha, float beta, float k, int bwd, int dt,
+                       P s) {
+    sg_lrn_rows(CV(x), CV(dy), V(out), R, C, size, alpha, beta, k, bwd, dt, S(s));
+    CHK("lrn_rows");
   });
   m.def("conv_fwd", [](P x, P w, P y, P bias, int N, int H, int W, int C, int K, int R, int Sd, int Ho, int Wo,
                        int sh, int sw, int ph, int pw, int dh, int dw, int relu, int out_mode, P s, P stats) {

@@ -304,6 +304,99 @@ __global__ void lrn_bwd_k(const T* __restrict__ x, const T* __restrict__ dy, con
   }
 }
 
+// ---- LRN, pixel-staged (C % 8 == 0) ----
+// The per-element kernels above redo the whole channel window per output
+// element from global memory with a 64-bit modulo, and the backward raises
+// every window member's norm to a power again (5 powf per element):
+// AlexNet b512's two LRNs took 38 % + 11 % of its step.  Here each workgroup
+// stages ppb pixels' squared inputs (and, backward, dy*x*norm^(-beta-1))
+// into zero-padded LDS rows, each thread owns 8 contiguous channels of one
+// pixel (16-byte loads/stores), and window sums read LDS.  The forward
+// writes no fp32 norm tensor: the backward recomputes it from x (k passed).
+// Window sums: each thread reads its 8 channels plus SZ-1 neighbours ONCE
+// (8 + 2*half LDS words, compile-time SZ: fully unrolled) and slides.
+template <int SZ>
+__device__ __forceinline__ void window8(const float* row, int c0, float out[8]) {
+  constexpr int H = SZ / 2;
+  float w[8 + 2 * H];
+#pragma unroll
+  for (int i = 0; i < 8 + 2 * H; ++i) w[i] = row[c0 - H + i];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < SZ; ++i) s += w[i];
+  out[0] = s;
+#pragma unroll
+  for (int e = 1; e < 8; ++e) {
+    s += w[e + SZ - 1] - w[e - 1];
+    out[e] = s;
+  }
+}
+
+template <typename T, bool BWD, int SZ>
+__global__ void __launch_bounds__(256) lrn_rows_k(const T* __restrict__ x, const T* __restrict__ dy,
+                                                  T* __restrict__ out, int64_t R, int C, float alpha, float beta,
+                                                  float knorm) {
+  extern __shared__ float lds[];
+  constexpr int half = SZ / 2;
+  const int tpp = C >> 3;             // threads per pixel
+  const int ppb = blockDim.x / tpp;   // pixels per workgroup (host: blockDim.x == ppb * tpp)
+  const int Wd = C + 2 * half;        // padded LDS row
+  float* sq = lds;
+  float* tt = lds + ppb * Wd;
+  const int lp = threadIdx.x / tpp, c0 = (threadIdx.x - lp * tpp) * 8;
+  for (int i = threadIdx.x; i < ppb * 2 * half; i += blockDim.x) {
+    const int pp = i / (2 * half), j = i - pp * 2 * half;
+    const int col = j < half ? j : C + j;
+    sq[pp * Wd + col] = 0.f;
+    if (BWD) tt[pp * Wd + col] = 0.f;
+  }
+  float* srow = sq + lp * Wd + half;
+  float* trow = tt + lp * Wd + half;
+  const float an = alpha / SZ;
+  // persistent over pixel chunks: ~4 KB of work per chunk is far too little
+  // to pay a workgroup dispatch each (73K workgroups for AlexNet's conv1 LRN)
+  const int64_t nchunk = (R + ppb - 1) / ppb;
+  for (int64_t ch = blockIdx.x; ch < nchunk; ch += gridDim.x) {
+    const int64_t pix = ch * ppb + lp;
+    const bool ok = pix < R;
+    float xv[8], gv[8];
+    if (ok) {
+      ldv<T, 8>(x + pix * C + c0, xv);
+      if (BWD) ldv<T, 8>(dy + pix * C + c0, gv);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { xv[e] = 0.f; gv[e] = 0.f; }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) srow[c0 + e] = xv[e] * xv[e];
+    __syncthreads();
+    float nm[8], pb[8];
+    window8<SZ>(srow, c0, nm);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      nm[e] = knorm + an * nm[e];
+      pb[e] = __powf(nm[e], -beta);
+    }
+    if constexpr (!BWD) {
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = xv[e] * pb[e];
+      if (ok) stv<T, 8>(out + pix * C + c0, o);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) trow[c0 + e] = gv[e] * xv[e] * pb[e] / nm[e];
+      __syncthreads();
+      const float f = 2.f * beta * an;
+      float sm[8], o[8];
+      window8<SZ>(trow, c0, sm);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = gv[e] * pb[e] - f * xv[e] * sm[e];
+      if (ok) stv<T, 8>(out + pix * C + c0, o);
+    }
+    __syncthreads();  // LDS rows are rewritten by the next chunk
+  }
+}
+
 }  // namespace sg
 
 using namespace sg;
@@ -386,6 +479,32 @@ void sg_lrn_fwd(const void* x, void* y, void* norm, int64_t R, int C, int size, 
                 int dtype, hipStream_t s) {
   DISPATCH_FT(dtype, hipLaunchKernelGGL(lrn_fwd_k<T>, dim3(sg_grid(R * C, 256, 16384)), dim3(256), 0, s,
                                         (const T*)x, (T*)y, (float*)norm, R, C, size, alpha, beta, knorm));
+}
+// pixel-staged LRN (C % 8 == 0, C <= 2048): bwd = 0 -> out = y; bwd = 1 -> out = dx (norm recomputed from x)
+void sg_lrn_rows(const void* x, const void* dy, void* out, int64_t R, int C, int size, float alpha, float beta,
+                 float knorm, int bwd, int dtype, hipStream_t s) {
+  const int tpp = C / 8;
+  const int ppb = 256 / tpp;
+  const int half = size / 2;
+  const size_t lds = (size_t)(bwd ? 2 : 1) * ppb * (C + 2 * half) * sizeof(float);
+  const int64_t nchunk = (R + ppb - 1) / ppb;
+  const dim3 grid((unsigned)(nchunk < 4096 ? nchunk : 4096)), block(ppb * tpp);
+#define LRN_GO(SZ)                                                                                             \
+  if (bwd) {                                                                                                   \
+    DISPATCH_FT(dtype, hipLaunchKernelGGL((lrn_rows_k<T, true, SZ>), grid, block, lds, s, (const T*)x,          \
+                                          (const T*)dy, (T*)out, R, C, alpha, beta, knorm));                    \
+  } else {                                                                                                     \
+    DISPATCH_FT(dtype, hipLaunchKernelGGL((lrn_rows_k<T, false, SZ>), grid, block, lds, s, (const T*)x, nullptr, \
+                                          (T*)out, R, C, alpha, beta, knorm));                                  \
+  }
+  switch (size) {  // (host-checked: odd, 1..9)
+    case 1: LRN_GO(1); break;
+    case 3: LRN_GO(3); break;
+    case 5: LRN_GO(5); break;
+    case 7: LRN_GO(7); break;
+    default: LRN_GO(9); break;
+  }
+#undef LRN_GO
 }
 void sg_lrn_bwd(const void* x, const void* dy, const void* norm, void* dx, int64_t R, int C, int size, float alpha,
                 float beta, int dtype, hipStream_t s) {

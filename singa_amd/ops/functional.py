@@ -1117,7 +1117,20 @@ def global_avgpool_bwd(dy: torch.Tensor, x_shape) -> torch.Tensor:
     return (dy.float()[:, :, None, None] / (H * W)).expand(x_shape).to(dy.dtype)
 
 
+def _lrn_rows_ok(x, size):
+    C = x.shape[1]
+    return C % 8 == 0 and C <= 2048 and size % 2 == 1 and size <= 9 and size <= C
+
+
 def lrn_fwd(x: torch.Tensor, size: int, alpha: float, beta: float, k: float):
+    """Returns (y, norm); norm is None on the pixel-staged native path
+    (lrn_bwd then recomputes it from x and needs ``k``)."""
+    if _native_ok(x) and _flat_ok(x) and N.is_cl(x) and _lrn_rows_ok(x, size):
+        C = x.shape[1]
+        y = _like(x)
+        N.lib().lrn_rows(x.data_ptr(), 0, y.data_ptr(), x.numel() // C, C, size, alpha, beta, k, 0, N.dt(x),
+                         N.stream())
+        return y, None
     if _native_ok(x) and _flat_ok(x) and N.is_cl(x):
         C = x.shape[1]
         R = x.numel() // C
@@ -1135,7 +1148,22 @@ def lrn_fwd(x: torch.Tensor, size: int, alpha: float, beta: float, k: float):
     return (xf * norm.pow(-beta)).to(x.dtype), norm
 
 
-def lrn_bwd(x: torch.Tensor, dy: torch.Tensor, norm: torch.Tensor, size: int, alpha: float, beta: float):
+def lrn_bwd(x: torch.Tensor, dy: torch.Tensor, norm: Optional[torch.Tensor], size: int, alpha: float, beta: float,
+            k: float = 1.0):
+    if norm is None:  # pixel-staged forward: recompute norm from x inside the backward kernel
+        if (_native_ok(x, dy) and _flat_ok(x) and N.is_cl(x) and N.is_cl(dy) and dy.dtype == x.dtype
+                and _lrn_rows_ok(x, size)):
+            C = x.shape[1]
+            dx = _like(x)
+            dyc = dy if dy.is_contiguous(memory_format=torch.channels_last) else dy.contiguous(
+                memory_format=torch.channels_last)
+            N.lib().lrn_rows(x.data_ptr(), dyc.data_ptr(), dx.data_ptr(), x.numel() // C, C, size, alpha, beta, k, 1,
+                             N.dt(x), N.stream())
+            return dx
+        xf = x.float()
+        half = size // 2
+        s2 = sum(F.pad(xf * xf, (0, 0, 0, 0, half, half))[:, i:i + x.shape[1]] for i in range(size))
+        norm = k + alpha / size * s2
     if _native_ok(x, dy) and _flat_ok(x) and N.is_cl(x) and N.is_cl(dy) and dy.dtype == x.dtype:
         C = x.shape[1]
         R = x.numel() // C

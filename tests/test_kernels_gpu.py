@@ -358,20 +358,28 @@ def test_global_avgpool(gpu):
     assert rel_err(dx, (dy[:, :, None, None] / 49).expand_as(x)) < 1e-6
 
 
-def test_lrn(gpu):
+@pytest.mark.parametrize("C,size,dtype", [(16, 5, torch.float32), (12, 5, torch.float32), (64, 5, torch.bfloat16),
+                                           (96, 5, torch.float32), (256, 3, torch.bfloat16), (192, 5, torch.bfloat16)])
+def test_lrn(gpu, C, size, dtype):
+    """LRN forward/backward (pixel-staged kernel for C % 8 == 0, the
+    per-element kernel otherwise) vs torch.nn.functional.local_response_norm
+    in fp32 with autograd."""
     from singa_amd.ops import functional as F
-    x = torch.randn(2, 16, 5, 5)
-    y_ref, norm_ref = F.lrn_fwd(x, 5, 1e-2, 0.75, 2.0)
-    dy = torch.randn(2, 16, 5, 5)
-    dx_ref = F.lrn_bwd(x, dy, norm_ref, 5, 1e-2, 0.75)
-    # torch oracle for the forward
-    tref = TF.local_response_norm(x, 5, 1e-2, 0.75, 2.0)
-    assert rel_err(y_ref, tref) < 1e-5
+    g = torch.Generator().manual_seed(13)
+    x = torch.randn(3, C, 7, 5, generator=g).to(dtype)
+    dy = torch.randn(3, C, 7, 5, generator=g).to(dtype)
+    xr = x.float().requires_grad_(True)
+    tref = TF.local_response_norm(xr, size, 1e-2, 0.75, 2.0)
+    tref.backward(dy.float())
     cl = lambda t: t.to(gpu).contiguous(memory_format=torch.channels_last)  # noqa: E731
-    y, norm = F.lrn_fwd(cl(x), 5, 1e-2, 0.75, 2.0)
-    assert rel_err(y, y_ref) < 1e-5
-    dx = F.lrn_bwd(cl(x), cl(dy), norm, 5, 1e-2, 0.75)
-    assert rel_err(dx, dx_ref) < 1e-5
+    y, norm = F.lrn_fwd(cl(x), size, 1e-2, 0.75, 2.0)
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert rel_err(y, tref.detach()) < tol
+    dx = F.lrn_bwd(cl(x), cl(dy), norm, size, 1e-2, 0.75, 2.0)
+    assert rel_err(dx, xr.grad) < (1e-4 if dtype == torch.float32 else 2e-2)
+    # CPU reference path of the wrappers agrees too
+    y_c, norm_c = F.lrn_fwd(x.float(), size, 1e-2, 0.75, 2.0)
+    assert rel_err(F.lrn_bwd(x.float(), dy.float(), norm_c, size, 1e-2, 0.75, 2.0), xr.grad) < 1e-5
 
 
 # ------------------------------------------------------- softmax / losses
