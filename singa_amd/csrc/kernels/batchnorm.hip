@@ -501,6 +501,36 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_k(const T* __restrict__ x, c
   }
 }
 
+// Column sums of a [R][C] tensor ACCUMULATED into out[C] with one atomic per
+// column per workgroup: rl row lanes x C/8 column vectors per workgroup, a
+// contiguous span of rpb rows each, LDS combine of the row lanes.
+template <typename T>
+__global__ void __launch_bounds__(256) colsum_acc_k(const T* __restrict__ x, float* __restrict__ out, int64_t R,
+                                                    int C, int64_t rpb) {
+  extern __shared__ float red[];  // [rl][C]
+  const int cv = C >> 3, rl = blockDim.x / cv;
+  const int lane_r = threadIdx.x / cv, c0 = (threadIdx.x - lane_r * cv) * 8;
+  const int64_t r0 = (int64_t)blockIdx.x * rpb;
+  const int64_t r1 = r0 + rpb < R ? r0 + rpb : R;
+  float acc[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+  for (int64_t r = r0 + lane_r; r < r1; r += rl) {
+    float v[8];
+    ldv<T, 8>(x + r * C + c0, v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] += v[e];
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) red[lane_r * C + c0 + e] = acc[e];
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float t = 0.f;
+    for (int l = 0; l < rl; ++l) t += red[l * C + c];
+    atomicAdd(out + c, t);
+  }
+}
+
 }  // namespace sg
 
 using namespace sg;
@@ -626,6 +656,17 @@ extern "C" {
 // out0/out1 (fp32 [C]) = column sums (accumulate != 0: added to existing)
 void sg_colsum(const void* x, void* ws, void* out0, void* out1, int64_t R, int C, int dtype, int accumulate,
                hipStream_t s) {
+  if (accumulate && !out1 && !g_bn_det && C % 8 == 0 && C <= 2048 && R <= (int64_t)1 << 20) {
+    // bias gradient accumulated into a flat-store view: one launch (no
+    // workspace zeroing, no finalize pass) -- these are launch-latency bound
+    const int cv = C / 8, rl = 256 / cv;
+    int64_t chunks = (R + 31) / 32;
+    const unsigned grid = (unsigned)(chunks < 512 ? chunks : 512);
+    const int64_t rpb = (R + grid - 1) / grid;
+    DISPATCH_FT(dtype, hipLaunchKernelGGL(colsum_acc_k<T>, dim3(grid), dim3(rl * cv), (size_t)rl * C * sizeof(float), s,
+                                          (const T*)x, (float*)out0, R, C, rpb));
+    return;
+  }
   dim3 grid;
   int rpb, V;
   colgrid(R, C, grid, rpb, V);

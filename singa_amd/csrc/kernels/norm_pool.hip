@@ -313,6 +313,13 @@ __global__ void lrn_bwd_k(const T* __restrict__ x, const T* __restrict__ dy, con
 // into zero-padded LDS rows, each thread owns 8 contiguous channels of one
 // pixel (16-byte loads/stores), and window sums read LDS.  The forward
 // writes no fp32 norm tensor: the backward recomputes it from x (k passed).
+// x^y for x > 0 on the hardware log2 / exp2 (v_log_f32, v_exp_f32): HIP's
+// __powf is the accurate OCML pow (~150 VALU with its special cases), which
+// made the LRN kernels VALU-bound at 8 pows per thread (PMC: ~1400 VALU per wave)
+__device__ __forceinline__ float fast_pow_pos(float x, float y) {
+  return __builtin_amdgcn_exp2f(y * __builtin_amdgcn_logf(x));
+}
+
 // Window sums: each thread reads its 8 channels plus SZ-1 neighbours ONCE
 // (8 + 2*half LDS words, compile-time SZ: fully unrolled) and slides.
 template <int SZ>
@@ -375,7 +382,7 @@ __global__ void __launch_bounds__(256) lrn_rows_k(const T* __restrict__ x, const
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       nm[e] = knorm + an * nm[e];
-      pb[e] = __powf(nm[e], -beta);
+      pb[e] = fast_pow_pos(nm[e], -beta);
     }
     if constexpr (!BWD) {
       float o[8];
@@ -384,7 +391,7 @@ __global__ void __launch_bounds__(256) lrn_rows_k(const T* __restrict__ x, const
       if (ok) stv<T, 8>(out + pix * C + c0, o);
     } else {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) trow[c0 + e] = gv[e] * xv[e] * pb[e] / nm[e];
+      for (int e = 0; e < 8; ++e) trow[c0 + e] = gv[e] * xv[e] * pb[e] * __builtin_amdgcn_rcpf(nm[e]);
       __syncthreads();
       const float f = 2.f * beta * an;
       float sm[8], o[8];

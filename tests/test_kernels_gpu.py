@@ -789,3 +789,22 @@ def test_attention_qkv_in_place_heads(gpu, B, S, H, D, masked):
     assert o.shape == (B, S, H * D) and dqkv.shape == qkv.shape
     assert rel_err(o, ref.detach()) < 2e-2
     assert rel_err(dqkv, x.grad) < 3e-2
+
+
+@pytest.mark.parametrize("R,C,dtype", [(4096, 768, torch.bfloat16), (1000, 3072, torch.bfloat16), (37, 8, torch.float32),
+                                       (5000, 2048, torch.float32), (300, 100, torch.bfloat16)])
+def test_colsum_accumulate(gpu, R, C, dtype):
+    """Column sums accumulated into an existing fp32 buffer (the bias-gradient
+    path: one launch for C % 8 == 0, C <= 2048; the workspace + finalize
+    reduction otherwise) and the fresh-output path, vs PyTorch fp32."""
+    from singa_amd.ops import functional as F
+    g = torch.Generator().manual_seed(14)
+    x = torch.randn(R, C, generator=g).to(dtype)
+    base = torch.randn(C, generator=g)
+    out = base.clone().to(gpu)
+    r, _ = F.colsum(x.to(gpu), out=out)
+    ref = base + x.float().sum(0)
+    assert r.data_ptr() == out.data_ptr()
+    assert rel_err(out, ref) < 1e-5
+    fresh, sq = F.colsum(x.to(gpu), with_sq=True)
+    assert rel_err(fresh, x.float().sum(0)) < 1e-5 and rel_err(sq, (x.float() ** 2).sum(0)) < 1e-5
