@@ -498,6 +498,14 @@ def test_dropout(gpu):
     assert torch.equal(dx, y)
     y2, m2 = F.dropout_fwd(x, 0.3, 42, 0)
     assert torch.equal(mask, m2)  # reproducible per (seed, offset)
+    # the 8-wide kernel (n % 8 == 0) draws exactly the scalar kernel's mask
+    for dt in (torch.float32, torch.bfloat16):
+        xo = torch.randn(100001, device=gpu).to(dt)
+        ys, ms = F.dropout_fwd(xo, 0.3, 7, 5)
+        yv, mv = F.dropout_fwd(xo[:100000].clone(), 0.3, 7, 5)
+        assert torch.equal(ms[:100000], mv) and torch.equal(ys[:100000], yv)
+        g = torch.randn(100000, device=gpu).to(dt)
+        assert rel_err(F.dropout_bwd(g, mv, 0.3), g.float() * mv.float() / 0.7) < (1e-6 if dt == torch.float32 else 5e-3)
 
 
 # ----------------------------------------------------------------- optimiser
