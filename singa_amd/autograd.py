@@ -658,8 +658,15 @@ class Conv2d(Operator):
         w = p.low if (p is not None and p.low is not None and x.dtype == torch.bfloat16) else W
         y = F.conv2d_fwd(x, w, b, self.stride, self.padding, self.dilation, self.group, out_dtype=x.dtype,
                          relu=self.fuse_relu, bn_stats=self.bn_stats and _training())
+        xc = getattr(y, "_sg_xconv", None)
+        if xc is not None:
+            del y._sg_xconv
         if self.requires_grad:
-            self.x, self.w = x, w
+            # an input that needs no gradient (the images) is kept in the
+            # converted bf16 NHWC (channel-padded) form the forward built, so
+            # the backward does not convert it again
+            self.x = xc if (xc is not None and not self.needs_grad(0)) else x
+            self.w = w
             self.y = y if self.fuse_relu else None
         return y
 

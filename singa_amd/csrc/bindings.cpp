@@ -28,6 +28,7 @@ void sg_dropout_fwd(const void*, void*, void*, int64_t, int, float, uint64_t, ui
 void sg_dropout_bwd(const void*, const void*, void*, int64_t, int, float, hipStream_t);
 void sg_rand_fill(void*, int64_t, int, int, float, float, uint64_t, uint64_t, hipStream_t);
 void sg_nchw_to_nhwc_pad(const void*, void*, int, int, int, int, int, hipStream_t);
+void sg_nchw_to_nhwc_pad_bf16(const void*, void*, int, int, int, int, int, hipStream_t);
 void sg_bn_relu_maxpool(const void*, const void*, const void*, void*, void*, int, int, int, int, int, int, int, int, int,
                         int, int, int, hipStream_t);
 void sg_nchw_to_pairs(const void*, void*, int, int, int, int, hipStream_t);
@@ -166,6 +167,10 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("nchw_to_pairs", [](P x, P y, int N, int C, int H, int W, P s) {
     sg_nchw_to_pairs(CV(x), V(y), N, C, H, W, S(s)); CHK("nchw_to_pairs");
+  });
+  m.def("nchw_to_nhwc_pad_bf16", [](P x, P y, int N, int C, int H, int W, int Cp, P s) {
+    sg_nchw_to_nhwc_pad_bf16(CV(x), V(y), N, C, H, W, Cp, S(s));
+    CHK("nchw_to_nhwc_pad_bf16");
   });
   m.def("nchw_to_nhwc_pad", [](P x, P y, int N, int C, int H, int W, int Cp, P s) {
     sg_nchw_to_nhwc_pad(CV(x), V(y), N, C, H, W, Cp, S(s)); CHK("nchw_to_nhwc_pad");

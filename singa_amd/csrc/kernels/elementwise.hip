@@ -329,7 +329,8 @@ __global__ void rand_fill_k(T* __restrict__ y, int64_t n, int dist, float a, flo
 }
 
 // NCHW fp32 image batch -> NHWC bf16 with channel padding (stem input prep).
-__global__ void nchw_to_nhwc_pad_k(const float* __restrict__ x, bf16* __restrict__ y, int N, int C, int H,
+template <typename TI>
+__global__ void nchw_to_nhwc_pad_k(const TI* __restrict__ x, bf16* __restrict__ y, int N, int C, int H,
                                    int W, int Cp) {
   const int64_t total = (int64_t)N * H * W;
   SG_GRID_STRIDE(p, total) {
@@ -340,7 +341,7 @@ __global__ void nchw_to_nhwc_pad_k(const float* __restrict__ x, bf16* __restrict
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         int c = c0 + j;
-        v[j] = (bf16)(c < C ? x[(n * C + c) * H * W + hw] : 0.f);
+        v[j] = (bf16)(c < C ? to_f32(x[(n * C + c) * H * W + hw]) : 0.f);
       }
       *(bf16x8*)(y + p * Cp + c0) = v;
     }
@@ -444,7 +445,12 @@ void sg_nchw_to_pairs(const void* x, void* y, int N, int C, int H, int W, hipStr
 }
 
 void sg_nchw_to_nhwc_pad(const void* x, void* y, int N, int C, int H, int W, int Cp, hipStream_t s) {
-  hipLaunchKernelGGL(nchw_to_nhwc_pad_k, dim3(sg_grid((int64_t)N * H * W)), dim3(256), 0, s, (const float*)x,
+  hipLaunchKernelGGL(nchw_to_nhwc_pad_k<float>, dim3(sg_grid((int64_t)N * H * W)), dim3(256), 0, s, (const float*)x,
+                     (bf16*)y, N, C, H, W, Cp);
+}
+// bf16 NCHW input (a model that casts its fp32 images first, e.g. AlexNet)
+void sg_nchw_to_nhwc_pad_bf16(const void* x, void* y, int N, int C, int H, int W, int Cp, hipStream_t s) {
+  hipLaunchKernelGGL(nchw_to_nhwc_pad_k<bf16>, dim3(sg_grid((int64_t)N * H * W)), dim3(256), 0, s, (const bf16*)x,
                      (bf16*)y, N, C, H, W, Cp);
 }
 

@@ -262,6 +262,66 @@ template <> struct V4<bf16> {
   }
 };
 
+// LayerNorm forward, one WAVE per row (D % 4 == 0, D <= 2048): lane l owns
+// the 4-column groups 4*(l + 64*j), the row stays in registers, mean and
+// variance are wave shuffles (the block-per-row kernel above pays two block
+// barriers per row for 768 columns)
+template <typename T, int NJ>
+__global__ void __launch_bounds__(256) layernorm_fwd_rows_k(const T* __restrict__ x, const float* __restrict__ g,
+                                                            const float* __restrict__ b, T* __restrict__ y,
+                                                            float* __restrict__ mean, float* __restrict__ rstd,
+                                                            int64_t R, int D, float eps) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= R) return;
+  float v[NJ][4];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = 4 * (lane + 64 * j);
+    if (c < D) {
+      V4<T>::ld(x + r * D + c, v[j]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[j][e] = 0.f;
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) s += v[j][e];
+  }
+  const float mu = wave_sum(s) / D;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = 4 * (lane + 64 * j);
+    if (c < D) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float d = v[j][e] - mu;
+        q += d * d;
+      }
+    }
+  }
+  const float rs = rsqrtf(wave_sum(q) / D + eps);
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = 4 * (lane + 64 * j);
+    if (c < D) {
+      float o[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        o[e] = (v[j][e] - mu) * rs;
+        if (g) o[e] *= g[c + e];
+        if (b) o[e] += b[c + e];
+      }
+      V4<T>::st(y + r * D + c, o);
+    }
+  }
+  if (lane == 0) {
+    mean[r] = mu;
+    rstd[r] = rs;
+  }
+}
+
 template <typename T, int NJ>
 __global__ void __launch_bounds__(256) layernorm_bwd_rows_k(const T* __restrict__ x, const T* __restrict__ dy,
                                                             const float* __restrict__ g, const float* __restrict__ mean,
@@ -406,6 +466,16 @@ void sg_softmax_xent(const void* x, const void* labels, const void* soft_t, void
 }
 void sg_layernorm_fwd(const void* x, const void* g, const void* b, void* y, void* mean, void* rstd, int64_t R, int D,
                       int dtype, float eps, hipStream_t s) {
+  if (D % 4 == 0 && D <= 2048) {
+    const int nj = (D + 255) / 256;
+    const dim3 grid((unsigned)((R + 3) / 4));
+#define LNF(NJ)                                                                                                     \
+  DISPATCH_FT(dtype, hipLaunchKernelGGL((layernorm_fwd_rows_k<T, NJ>), grid, dim3(256), 0, s, (const T*)x,          \
+                                        (const float*)g, (const float*)b, (T*)y, (float*)mean, (float*)rstd, R, D, eps))
+    if (nj <= 1) { LNF(1); } else if (nj <= 2) { LNF(2); } else if (nj <= 4) { LNF(4); } else { LNF(8); }
+#undef LNF
+    return;
+  }
   DISPATCH_FT(dtype, hipLaunchKernelGGL(layernorm_fwd_k<T>, dim3(R), dim3(256), 0, s, (const T*)x,
                                         (const float*)g, (const float*)b, (T*)y, (float*)mean, (float*)rstd, D, eps));
 }

@@ -452,9 +452,10 @@ def to_nhwc_bf16(x: torch.Tensor, cpad: Optional[int] = None) -> torch.Tensor:
     Nn, C, H, W = x.shape
     cp = cpad or C
     if cp != C:
-        if x.is_cuda and x.dtype == torch.float32 and x.is_contiguous() and cp % 8 == 0:
+        if x.is_cuda and x.dtype in (torch.float32, torch.bfloat16) and x.is_contiguous() and cp % 8 == 0:
             y = torch.empty((Nn, cp, H, W), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
-            N.lib().nchw_to_nhwc_pad(x.data_ptr(), y.data_ptr(), Nn, C, H, W, cp, N.stream())
+            fn = N.lib().nchw_to_nhwc_pad if x.dtype == torch.float32 else N.lib().nchw_to_nhwc_pad_bf16
+            fn(x.data_ptr(), y.data_ptr(), Nn, C, H, W, cp, N.stream())
             return y
         y = _zeros_cl((Nn, cp, H, W), torch.bfloat16, x.device)
         y[:, :C] = x
@@ -504,6 +505,8 @@ def conv2d_fwd(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], stri
                 ws = zeroed_ws(rows * 2 * K, x.device)
         N.lib().conv_fwd(xb.data_ptr(), wb.data_ptr(), y.data_ptr(), N.ptr(bias), Nn, H, W, Cp, Kp, R, S, Ho, Wo, sh,
                          sw, ph, pw, dh, dw, int(relu), 0 if od == torch.bfloat16 else 1, N.stream(), N.ptr(ws))
+        if xb is not x:  # converted input (network entry): the backward's weight gradient can reuse it
+            y._sg_xconv = xb
         if ws is not None:
             y._sg_bn_ws = (ws, rows)
         if Kp != K:
