@@ -282,6 +282,10 @@ def backward(y, dy=None) -> Iterator[Tuple[Tensor, Tensor]]:
                             last[i] = deps[src_op] == 1 and src_op.n_out == 1
                 op.acc_into = acc
                 op.acc_last = last
+            if getattr(op, "wants_sole", False):
+                # input i's producer gets its whole gradient from this op alone
+                op.sole = {i: src_op is not None and deps[src_op] == 1 and src_op not in pending
+                           and src_op.n_out == 1 for i, (src_op, _) in enumerate(op.src)}
             dxs = _as_tuple(op.backward(*dys_))
             op.acc_into = op.acc_last = None
         if len(dxs) != len(op.src):
@@ -676,7 +680,9 @@ class Conv2d(Operator):
         x, w = self.x, self.w
         self.x = self.w = None
         if self.fuse_relu:
-            dy = F.relu_bwd_from_y(self.y, dy)
+            if not getattr(self, "dy_relu_done", False):  # (an LRN consumer may have applied the mask)
+                dy = F.relu_bwd_from_y(self.y, dy)
+            self.dy_relu_done = False
             self.y = None
         tgt = self.grad_target(1)
         acc = (getattr(self, "acc_into", None) or {}).get(0)
@@ -847,6 +853,8 @@ class LRN(Operator):
         super().__init__(name)
         self.size, self.alpha, self.beta, self.k = size, alpha, beta, k
 
+    wants_sole = True
+
     def forward(self, x):
         y, norm = F.lrn_fwd(x, self.size, self.alpha, self.beta, self.k)
         if self.requires_grad:
@@ -854,7 +862,15 @@ class LRN(Operator):
         return y
 
     def backward(self, dy):
-        dx = F.lrn_bwd(self.x, dy, self.norm, self.size, self.alpha, self.beta, self.k)
+        # input from a conv with fused ReLU whose only consumer is this LRN:
+        # apply the ReLU mask (x > 0, x being that ReLU's output) in the LRN
+        # backward kernel and tell the conv to skip its relu_bwd pass
+        prod = self.src[0][0] if self.src else None
+        fold = (isinstance(prod, Conv2d) and prod.fuse_relu and getattr(prod, "y", None) is not None
+                and prod.y is self.x and (getattr(self, "sole", None) or {}).get(0, False))
+        dx = F.lrn_bwd(self.x, dy, self.norm, self.size, self.alpha, self.beta, self.k, relu_mask=fold)
+        if fold and getattr(dx, "_sg_relu_done", False):
+            prod.dy_relu_done = True
         self.x = self.norm = None
         return dx
 

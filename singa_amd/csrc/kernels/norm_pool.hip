@@ -339,7 +339,7 @@ __device__ __forceinline__ void window8(const float* row, int c0, float out[8]) 
   }
 }
 
-template <typename T, bool BWD, int SZ>
+template <typename T, bool BWD, int SZ, bool RELU = false>
 __global__ void __launch_bounds__(256) lrn_rows_k(const T* __restrict__ x, const T* __restrict__ dy,
                                                   T* __restrict__ out, int64_t R, int C, float alpha, float beta,
                                                   float knorm) {
@@ -397,7 +397,10 @@ __global__ void __launch_bounds__(256) lrn_rows_k(const T* __restrict__ x, const
       float sm[8], o[8];
       window8<SZ>(trow, c0, sm);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = gv[e] * pb[e] - f * xv[e] * sm[e];
+      for (int e = 0; e < 8; ++e) {
+        o[e] = gv[e] * pb[e] - f * xv[e] * sm[e];
+        if (RELU && !(xv[e] > 0.f)) o[e] = 0.f;  // x is a ReLU output: its backward, folded
+      }
       if (ok) stv<T, 8>(out + pix * C + c0, o);
     }
     __syncthreads();  // LDS rows are rewritten by the next chunk
@@ -487,7 +490,8 @@ void sg_lrn_fwd(const void* x, void* y, void* norm, int64_t R, int C, int size, 
   DISPATCH_FT(dtype, hipLaunchKernelGGL(lrn_fwd_k<T>, dim3(sg_grid(R * C, 256, 16384)), dim3(256), 0, s,
                                         (const T*)x, (T*)y, (float*)norm, R, C, size, alpha, beta, knorm));
 }
-// pixel-staged LRN (C % 8 == 0, C <= 2048): bwd = 0 -> out = y; bwd = 1 -> out = dx (norm recomputed from x)
+// pixel-staged LRN (C % 8 == 0, C <= 2048): bwd = 0 -> out = y; bwd = 1 -> out = dx (norm recomputed from x);
+// bwd = 2 -> dx with the ReLU mask of x (x > 0) applied
 void sg_lrn_rows(const void* x, const void* dy, void* out, int64_t R, int C, int size, float alpha, float beta,
                  float knorm, int bwd, int dtype, hipStream_t s) {
   const int tpp = C / 8;
@@ -497,7 +501,10 @@ void sg_lrn_rows(const void* x, const void* dy, void* out, int64_t R, int C, int
   const int64_t nchunk = (R + ppb - 1) / ppb;
   const dim3 grid((unsigned)(nchunk < 4096 ? nchunk : 4096)), block(ppb * tpp);
 #define LRN_GO(SZ)                                                                                             \
-  if (bwd) {                                                                                                   \
+  if (bwd == 2) {                                                                                              \
+    DISPATCH_FT(dtype, hipLaunchKernelGGL((lrn_rows_k<T, true, SZ, true>), grid, block, lds, s, (const T*)x,    \
+                                          (const T*)dy, (T*)out, R, C, alpha, beta, knorm));                    \
+  } else if (bwd) {                                                                                            \
     DISPATCH_FT(dtype, hipLaunchKernelGGL((lrn_rows_k<T, true, SZ>), grid, block, lds, s, (const T*)x,          \
                                           (const T*)dy, (T*)out, R, C, alpha, beta, knorm));                    \
   } else {                                                                                                     \

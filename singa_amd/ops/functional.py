@@ -1152,7 +1152,9 @@ def lrn_fwd(x: torch.Tensor, size: int, alpha: float, beta: float, k: float):
 
 
 def lrn_bwd(x: torch.Tensor, dy: torch.Tensor, norm: Optional[torch.Tensor], size: int, alpha: float, beta: float,
-            k: float = 1.0):
+            k: float = 1.0, relu_mask: bool = False):
+    """``relu_mask``: x is a ReLU output; the native kernel also zeroes dx
+    where x <= 0 (the ReLU backward, folded) and marks dx ``_sg_relu_done``."""
     if norm is None:  # pixel-staged forward: recompute norm from x inside the backward kernel
         if (_native_ok(x, dy) and _flat_ok(x) and N.is_cl(x) and N.is_cl(dy) and dy.dtype == x.dtype
                 and _lrn_rows_ok(x, size)):
@@ -1160,8 +1162,10 @@ def lrn_bwd(x: torch.Tensor, dy: torch.Tensor, norm: Optional[torch.Tensor], siz
             dx = _like(x)
             dyc = dy if dy.is_contiguous(memory_format=torch.channels_last) else dy.contiguous(
                 memory_format=torch.channels_last)
-            N.lib().lrn_rows(x.data_ptr(), dyc.data_ptr(), dx.data_ptr(), x.numel() // C, C, size, alpha, beta, k, 1,
-                             N.dt(x), N.stream())
+            N.lib().lrn_rows(x.data_ptr(), dyc.data_ptr(), dx.data_ptr(), x.numel() // C, C, size, alpha, beta, k,
+                             2 if relu_mask else 1, N.dt(x), N.stream())
+            if relu_mask:
+                dx._sg_relu_done = True
             return dx
         xf = x.float()
         half = size // 2

@@ -632,3 +632,35 @@ def test_bert_graph_matches_eager(gpu, imported):
     e, g = np.array(curves[0]), np.array(curves[1])
     assert np.all(np.isfinite(g)), curves
     np.testing.assert_allclose(g, e, rtol=2e-2, atol=2e-3)
+
+
+def test_lrn_folds_conv_relu_backward(gpu, monkeypatch):
+    """conv(+fused ReLU) -> LRN: the LRN backward applies the ReLU mask and
+    the conv skips its relu_bwd pass; gradients equal the unfolded chain."""
+    from singa_amd import layer
+
+    rng = np.random.RandomState(0)
+    x_np = rng.standard_normal((4, 3, 35, 35)).astype(np.float32)
+    grads = []
+    for fold in (False, True):
+        monkeypatch.setattr(autograd.LRN, "wants_sole", fold)
+        dev = device.create_rocm_gpu()
+        dev.SetRandSeed(3)
+        conv = layer.Conv2d(3, 64, 5, stride=2, padding=2, activation="RELU")
+        lrn = layer.LRN(5, 1e-2, 0.75, 2.0)
+        x = tensor.from_numpy(x_np).to_device(dev)
+        autograd.training = False
+        xb = autograd.cast(x, torch.bfloat16)
+        lrn(conv(xb))  # materialise the conv parameters
+        autograd.training = True
+        y = lrn(conv(autograd.cast(x, torch.bfloat16)))
+        g = torch.Generator().manual_seed(1)
+        dy = torch.randn(y.shape, generator=g).to(torch.bfloat16).to(gpu).contiguous(
+            memory_format=torch.channels_last)
+        gs = sorted((tuple(p.shape), gg.data.float().clone()) for p, gg in autograd.backward(y, dy))
+        autograd.training = False
+        grads.append(gs)
+    assert len(grads[0]) == len(grads[1]) >= 1
+    for (s0, g0), (s1, g1) in zip(grads[0], grads[1]):
+        assert s0 == s1
+        torch.testing.assert_close(g1, g0, rtol=1e-2, atol=1e-3)
