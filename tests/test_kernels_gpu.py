@@ -800,7 +800,9 @@ def test_attention_qkv_in_place_heads(gpu, B, S, H, D, masked):
 
 
 @pytest.mark.parametrize("R,C,dtype", [(4096, 768, torch.bfloat16), (1000, 3072, torch.bfloat16), (37, 8, torch.float32),
-                                       (5000, 2048, torch.float32), (300, 100, torch.bfloat16)])
+                                       (5000, 2048, torch.float32), (300, 100, torch.bfloat16),
+                                       (4096, 2304, torch.bfloat16), (33, 1032, torch.float32),
+                                       (70, 8192, torch.bfloat16), (50, 9000, torch.bfloat16)])
 def test_colsum_accumulate(gpu, R, C, dtype):
     """Column sums accumulated into an existing fp32 buffer (the bias-gradient
     path: one launch for C % 8 == 0, C <= 2048; the workspace + finalize
