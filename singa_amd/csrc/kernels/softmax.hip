@@ -8,6 +8,7 @@
 // does everything in a single pass over the logits staged in LDS, for any
 // class count.
 #include "common.h"
+#include <stdlib.h>
 
 namespace sg {
 
@@ -482,8 +483,17 @@ void sg_layernorm_fwd(const void* x, const void* g, const void* b, void* y, void
 void sg_layernorm_bwd(const void* x, const void* dy, const void* g, const void* mean, const void* rstd, void* dx,
                       void* dg, void* db, int64_t R, int D, int dtype, hipStream_t s) {
   if (D % 4 == 0 && D <= 2048) {
-    // ~512 workgroups, whole waves' worth of rows each (R = 4096 -> 8 rows / workgroup)
-    int64_t rpb = (R + 511) / 512;
+    // ~128 workgroups, whole waves' worth of rows each (R = 4096 -> 32 rows
+    // per workgroup): measured 15.2 us vs 23.8 us with 512 and 33.9 us with
+    // 1024 (tools/lnb_ab.py, profiles/lnb_ab.jsonl) -- every workgroup adds
+    // into the same D addresses, so fewer, longer workgroups contend less.
+    // SINGA_AMD_LNB_WG overrides for A/B
+    static const int64_t wg = [] {
+      const char* e = getenv("SINGA_AMD_LNB_WG");
+      const int64_t v = e ? atoll(e) : 128;
+      return v > 0 ? v : 128;
+    }();
+    int64_t rpb = (R + wg - 1) / wg;
     rpb = rpb < 4 ? 4 : (rpb + 3) / 4 * 4;
     const int64_t nb = (R + rpb - 1) / rpb;
     const size_t lds = (size_t)8 * D * sizeof(float);
