@@ -34,6 +34,7 @@ import torch
 
 from . import tensor as _tensor
 from .ops import functional as F
+from .ops import glue as G
 from .ops import native as N
 from .tensor import Tensor
 
@@ -186,12 +187,12 @@ def _accum(a, b):
     if b is None:
         return a
     if a.shape != b.shape:
-        b = b.reshape(a.shape)
+        b = G.reshape(b, a.shape)
     if a.dtype != b.dtype:
-        b = b.to(a.dtype)
-    if a.stride() == b.stride() and a.is_cuda:
+        b = G.to(b, a.dtype)
+    if a.stride() == b.stride() and a.is_cuda and (a.is_contiguous() or N.is_cl(a)):
         return F.add_act(a, b)
-    return a + b
+    return G.binary("add", a, b)
 
 
 def is_unit(dy) -> bool:
@@ -221,7 +222,7 @@ def backward(y, dy=None) -> Iterator[Tuple[Tensor, Tensor]]:
         if op0 not in pending:
             pending[op0] = [None] * op0.n_out
         if d is None:
-            g0 = torch.ones_like(r.data)
+            g0 = G.full(r.data.shape, 1.0, r.data.dtype, r.data.device)
             g0._sg_unit = True
         else:
             g0 = d.data if isinstance(d, Tensor) else d
@@ -457,15 +458,7 @@ class Identity(Operator):
 
 
 def _unbroadcast(g: torch.Tensor, shape) -> torch.Tensor:
-    shape = tuple(shape)
-    if tuple(g.shape) == shape:
-        return g
-    while g.dim() > len(shape):
-        g = g.sum(0)
-    for i, s in enumerate(shape):
-        if s == 1 and g.shape[i] != 1:
-            g = g.sum(i, keepdim=True)
-    return g
+    return G.sum_to(g, shape)
 
 
 class Add(Operator):
@@ -474,12 +467,13 @@ class Add(Operator):
         self.relu = relu
 
     def forward(self, a, b):
-        if a.shape == b.shape:
+        if a.shape == b.shape and a.dtype == b.dtype and (a.stride() == b.stride()) and (
+                a.is_contiguous() or N.is_cl(a)):
             y = F.add_act(a, b, relu=self.relu)
         else:
-            y = a + b
+            y = G.binary("add", a, b)
             if self.relu:
-                y = torch.relu(y)
+                y = F.unary("relu", y)
         if self.requires_grad:
             self.sa, self.sb = a.shape, b.shape
             self.y = y if self.relu else None
@@ -496,63 +490,76 @@ class Sub(Operator):
     def forward(self, a, b):
         if self.requires_grad:
             self.sa, self.sb = a.shape, b.shape
-        return a - b
+        return G.binary("sub", a, b)
 
     def backward(self, dy):
-        return _unbroadcast(dy, self.sa), _unbroadcast(-dy, self.sb)
+        return _unbroadcast(dy, self.sa), _unbroadcast(F.unary("neg", dy), self.sb)
 
 
 class Mul(Operator):
     def forward(self, a, b):
         if self.requires_grad:
             self.a, self.b = a, b
-        return a * b
+        return G.binary("mul", a, b)
 
     def backward(self, dy):
         a, b = self.a, self.b
         self.a = self.b = None
-        return _unbroadcast(dy * b, a.shape), _unbroadcast(dy * a, b.shape)
+        da = _unbroadcast(G.binary("mul", dy, b, out_dtype=a.dtype), a.shape) if self.needs_grad(0) else None
+        db = _unbroadcast(G.binary("mul", dy, a, out_dtype=b.dtype), b.shape) if self.needs_grad(1) else None
+        return da, db
 
 
 class Div(Operator):
     def forward(self, a, b):
+        y = G.binary("div", a, b)
         if self.requires_grad:
-            self.a, self.b = a, b
-        return a / b
+            self.b, self.y = b, y
+            self.sa = a.shape
+        return y
 
     def backward(self, dy):
-        a, b = self.a, self.b
-        self.a = self.b = None
-        return _unbroadcast(dy / b, a.shape), _unbroadcast(-dy * a / (b * b), b.shape)
+        b, y = self.b, self.y
+        self.b = self.y = None
+        da = G.binary("div", dy, b)  # d/da = dy / b ; d/db = -dy * y / b
+        db = G.binary("mul", G.binary("div", dy, b), y, alpha=-1.0) if self.needs_grad(1) else None
+        return _unbroadcast(da, self.sa), (_unbroadcast(db, b.shape) if db is not None else None)
 
 
 class Pow(Operator):
     def forward(self, a, b):
-        y = torch.pow(a, b)
+        y = G.binary("pow", a, b)
         if self.requires_grad:
             self.a, self.b, self.y = a, b, y
         return y
 
     def backward(self, dy):
         a, b, y = self.a, self.b, self.y
-        da = dy * b * torch.pow(a, b - 1)
-        db = dy * y * torch.log(torch.clamp(a, min=1e-30))
-        return _unbroadcast(da, a.shape), _unbroadcast(db, b.shape)
+        self.a = self.b = self.y = None
+        # da = dy * b * a^(b-1) ; db = dy * y * log(a)
+        da = G.binary("mul", G.binary("mul", dy, b), G.binary("pow", a, F.unary("adds", b, -1.0)))
+        db = None
+        if self.needs_grad(1):
+            la = F.unary("log", G.clamp_affine(a, lo=1e-30))
+            db = G.binary("mul", G.binary("mul", dy, y), la)
+        return _unbroadcast(da, a.shape), (_unbroadcast(db, b.shape) if db is not None else None)
 
 
 class Matmul(Operator):
-    """Batched/2-D matrix product; bf16 operands use the MFMA kernel."""
+    """Batched/2-D matrix product: bf16 operands on the MFMA kernel, fp32 on
+    the exact-f32 MFMA kernel (functional.gemm); backward likewise."""
 
     def forward(self, a, b):
         if self.requires_grad:
             self.a, self.b = a, b
-        return F.matmul(a, b) if a.dtype == b.dtype else torch.matmul(a, b.to(a.dtype))
+        return F.matmul(a, b, out_dtype=a.dtype)
 
     def backward(self, dy):
         a, b = self.a, self.b
         self.a = self.b = None
+        dy = dy.contiguous()
         if a.dim() == 2 and b.dim() == 2:
-            da = F.gemm_nt(dy.contiguous(), b.contiguous(), out_dtype=a.dtype) if self.needs_grad(0) else None
+            da = F.gemm_nt(dy, b, out_dtype=a.dtype) if self.needs_grad(0) else None
             db = None
             if self.needs_grad(1):
                 tgt = self.grad_target(1)
@@ -560,14 +567,18 @@ class Matmul(Operator):
                     F.gemm_tn_acc(a, dy, tgt)
                     db = ACCUMULATED
                 else:
-                    db = torch.matmul(a.t().float(), dy.float()).to(b.dtype)
+                    db = F.gemm(a, dy, ta=True, out_dtype=b.dtype)
             return da, db
-        da = torch.matmul(dy, b.transpose(-1, -2)) if self.needs_grad(0) else None
-        db = torch.matmul(a.transpose(-1, -2), dy) if self.needs_grad(1) else None
-        if db is not None:
-            db = _unbroadcast(db, b.shape)
-        if da is not None:
-            da = _unbroadcast(da, a.shape)
+        # batched: flatten leading dims (broadcast operands are reduced by _unbroadcast)
+        lead = torch.broadcast_shapes(a.shape[:-2], b.shape[:-2])
+        a3 = a.expand(*lead, *a.shape[-2:]).reshape(-1, *a.shape[-2:])
+        b3 = b.expand(*lead, *b.shape[-2:]).reshape(-1, *b.shape[-2:])
+        d3 = dy.reshape(-1, *dy.shape[-2:])
+        da = db = None
+        if self.needs_grad(0):
+            da = _unbroadcast(F.gemm(d3, b3, tb=True, out_dtype=a.dtype).reshape(*lead, *a.shape[-2:]), a.shape)
+        if self.needs_grad(1):
+            db = _unbroadcast(F.gemm(a3, d3, ta=True, out_dtype=b.dtype).reshape(*lead, *b.shape[-2:]), b.shape)
         return da, db
 
 
@@ -606,8 +617,7 @@ class Linear(Operator):
         lead = x.shape[:-1]
         x2 = x.reshape(-1, x.shape[-1])
         bias = b.float() if b is not None else None
-        y = F.matmul(x2, w, out_dtype=x.dtype, bias=bias) if x2.dtype == torch.bfloat16 else \
-            (torch.addmm(bias.to(x2.dtype), x2, w) if bias is not None else x2 @ w)
+        y = F.matmul(x2, w, out_dtype=x.dtype, bias=bias)
         if self.requires_grad:
             self.x2, self.w = x2, w
         return y.reshape(*lead, y.shape[-1])
@@ -626,14 +636,14 @@ class Linear(Operator):
         dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
         dx = None
         if self.needs_grad(0):
-            dx = F.gemm_nt(dy2, w.contiguous(), out_dtype=x2.dtype) if dy2.dtype == torch.bfloat16 else dy2 @ w.t()
+            dx = F.gemm_nt(dy2, w, out_dtype=x2.dtype)
             dx = dx.reshape(*dy.shape[:-1], x2.shape[-1])
         tgt = self.grad_target(1)
         if tgt is not None:
             F.gemm_tn_acc(x2, dy2, tgt)
             dw = ACCUMULATED
         else:
-            dw = (x2.float().t() @ dy2.float())
+            dw = F.gemm(x2, dy2, ta=True, out_dtype=torch.float32)
         res = [dx, dw]
         if self.has_bias:
             tb = self.grad_target(2)
@@ -1332,6 +1342,31 @@ def layer_norm(x, g=None, b=None, eps=1e-5):
     return LayerNorm(eps)(x, *args)
 
 
+class Fn(Operator):
+    """A glue operator whose forward and backward are plain functions over
+    raw tensors built from native kernels (:mod:`singa_amd.ops.glue` /
+    :mod:`singa_amd.ops.functional`): ``fwd(*xs) -> (ys, ctx)`` and
+    ``bwd(ctx, *dys) -> dxs`` (one entry per input, None if none).  On the
+    GPU every data movement is a hand-written kernel; PyTorch runs only on
+    CPU tensors (the CppCPU reference).  ``onnx`` is the sonnx export spec."""
+
+    def __init__(self, fwd: Callable, bwd: Optional[Callable] = None, onnx: Optional[dict] = None, name=None):
+        super().__init__(name)
+        self.fwd, self.bwd, self.onnx = fwd, bwd, onnx
+
+    def forward(self, *xs):
+        ys, ctx = self.fwd(*xs)
+        self.ctx = ctx if self.requires_grad else None
+        return ys
+
+    def backward(self, *dys):
+        if self.bwd is None:
+            return tuple(None for _ in self.src)
+        r = _as_tuple(self.bwd(self.ctx, *dys))
+        self.ctx = None
+        return r
+
+
 def _fn(fn, *xs, nondiff=(), onnx=None):
     return TorchFn(fn, nondiff=nondiff, onnx=onnx)(*xs)
 
@@ -1344,54 +1379,82 @@ def _ox(op, attrs=None, inputs=None, n_in=1):
 
 def transpose(x, shape=None):
     perm = tuple(shape) if shape is not None else tuple(reversed(range(x.ndim())))
-    return _fn(lambda a: a.permute(*perm), x, onnx=_ox("Transpose", {"perm": list(perm)}))
+    inv = tuple(int(i) for i in np.argsort(perm))
+    return Fn(lambda a: (a.permute(*perm), None), lambda c, d: d.permute(*inv),
+              onnx=_ox("Transpose", {"perm": list(perm)}))(x)
+
+
+def _reshape_fn(x, shape, onnx):
+    ins = tuple(x.shape)
+    return Fn(lambda a: (G.reshape(a, shape), None), lambda c, d: G.reshape(d, ins), onnx=onnx)(x)
 
 
 def squeeze(x, axis=None):
     ax = None if axis is None else ([axis] if isinstance(axis, int) else list(axis))
     spec = _ox("Squeeze") if ax is None else _ox("Squeeze", inputs=[("in", 0), ("const", np.asarray(ax, np.int64))])
-    return _fn(lambda a: a.squeeze() if axis is None else a.squeeze(axis if isinstance(axis, int) else tuple(axis)),
-               x, onnx=spec)
+    nd = len(x.shape)
+    axs = [a % nd for a in ax] if ax is not None else [k for k, s in enumerate(x.shape) if s == 1]
+    shape = [s for k, s in enumerate(x.shape) if not (k in axs and s == 1)]
+    return _reshape_fn(x, shape, spec)
 
 
 def unsqueeze(x, axis):
     ax = [axis] if isinstance(axis, int) else list(axis)
-
-    def f(a):
-        for d in sorted(ax):
-            a = a.unsqueeze(d)
-        return a
-    return _fn(f, x, onnx=_ox("Unsqueeze", inputs=[("in", 0), ("const", np.asarray(ax, np.int64))]))
+    shape = list(x.shape)
+    for d in sorted(a % (len(shape) + len(ax)) for a in ax):
+        shape.insert(d, 1)
+    return _reshape_fn(x, shape, _ox("Unsqueeze", inputs=[("in", 0), ("const", np.asarray(ax, np.int64))]))
 
 
 def cat(xs, axis=0):
-    return TorchFn(lambda *a: torch.cat(a, dim=axis), onnx=_ox("Concat", {"axis": axis}, n_in=len(xs)))(*xs)
+    sizes = [x.shape[axis] for x in xs]
+
+    def bwd(c, d):
+        out, o = [], 0
+        for n in sizes:
+            out.append(d.narrow(axis, o, n))
+            o += n
+        return tuple(out)
+    return Fn(lambda *a: (G.cat(a, axis), None), bwd, onnx=_ox("Concat", {"axis": axis}, n_in=len(xs)))(*xs)
 
 
 concat = cat
 
 
 def split(x, axis, parts):
-    return TorchFn(lambda a: tuple(torch.split(a, parts, dim=axis)),
-                   onnx=_ox("Split", {"axis": axis}, [("in", 0), ("const", np.asarray(parts, np.int64))]))(x)
+    parts = list(parts)
+    return Fn(lambda a: (tuple(torch.split(a, parts, dim=axis)), a),
+              lambda a, *ds: G.scatter_slices(ds, parts, axis, a),
+              onnx=_ox("Split", {"axis": axis}, [("in", 0), ("const", np.asarray(parts, np.int64))]))(x)
 
 
 def slice(x, starts, ends, axes=None, steps=None):  # noqa: A001
     axes = axes if axes is not None else list(range(len(starts)))
     steps = steps if steps is not None else [1] * len(starts)
 
-    def f(a):
+    def index(a):
         idx = [builtins_slice(None)] * a.dim()
         for s, e, ax, st in zip(starts, ends, axes, steps):
+            if st <= 0:
+                raise NotImplementedError("slice: only positive steps")
             n = a.shape[ax]
             e = _b.min(e, n) if e >= 0 else e
             idx[ax] = builtins_slice(s, e, st)
-        return a[tuple(idx)]
+        return tuple(idx)
+
+    def fwd(a):
+        return a[index(a)], (a.shape, a.dtype, a.device)
+
+    def bwd(c, d):
+        shp, dt, dev = c
+        g = G.zeros(shp, d.dtype, dev)
+        G.copy_(g[index(g)], d)
+        return g
     big = 2 ** 62
     spec = _ox("Slice", inputs=[("in", 0), ("const", np.asarray(starts, np.int64)),
                                 ("const", np.asarray([e if e < big else big for e in ends], np.int64)),
                                 ("const", np.asarray(axes, np.int64)), ("const", np.asarray(steps, np.int64))])
-    return _fn(f, x, onnx=spec)
+    return Fn(fwd, bwd, onnx=spec)(x)
 
 
 builtins_slice = _b.slice
@@ -1403,175 +1466,265 @@ def gather(x, axis, indices):
     spec = None
     if _TRACE:  # sonnx export only (the host copy of a device index would sync)
         spec = _ox("Gather", {"axis": axis}, [("in", 0), ("const", host if host is not None else idx.cpu().numpy())])
-    return _fn(lambda a: torch.index_select(a, axis, idx.reshape(-1)).reshape(
-        a.shape[:axis] + tuple(idx.shape) + a.shape[axis + 1:]), x, onnx=spec)
+
+    def bwd(c, d):
+        shp, dt = c
+        ax = axis % len(shp)
+        g = G.zeros(shp, torch.float32, d.device)
+        G.index_add_(g, ax, idx.reshape(-1), G.reshape(d, shp[:ax] + (idx.numel(),) + shp[ax + 1:]))
+        return g if dt == torch.float32 else G.to(g, dt)
+    return Fn(lambda a: (G.index_select(a, axis, idx), (tuple(a.shape), a.dtype)), bwd, onnx=spec)(x)
 
 
 def tile(x, repeats):
-    return _fn(lambda a: a.repeat(*repeats), x,
-               onnx=_ox("Tile", inputs=[("in", 0), ("const", np.asarray(repeats, np.int64))]))
+    reps = list(repeats)
+    return Fn(lambda a: (G.tile(a, reps), tuple(a.shape)), lambda shp, d: G.tile_backward(d, reps, shp),
+              onnx=_ox("Tile", inputs=[("in", 0), ("const", np.asarray(repeats, np.int64))]))(x)
 
 
 def expand(x, shape):
-    return _fn(lambda a: a.expand(*shape), x,
-               onnx=_ox("Expand", inputs=[("in", 0), ("const", np.asarray(shape, np.int64))]))
+    shape = tuple(shape)
+    return Fn(lambda a: (a.expand(*shape), tuple(a.shape)), lambda shp, d: G.sum_to(d, shp),
+              onnx=_ox("Expand", inputs=[("in", 0), ("const", np.asarray(shape, np.int64))]))(x)
 
 
 def pad(x, mode="constant", pads=None, constant=0.0):
     n = x.ndim()
     half = len(pads) // 2
-    tp = []
-    for i in reversed(range(n)):
-        tp += [pads[i], pads[i + half]]
-    m = {"constant": "constant", "reflect": "reflect", "edge": "replicate"}[mode]
+    before, after = list(pads[:half]), list(pads[half:])
+    before += [0] * (n - len(before))
+    after += [0] * (n - len(after))
     spec = _ox("Pad", {"mode": mode}, [("in", 0), ("const", np.asarray(pads, np.int64)),
                                         ("const", np.asarray(constant, np.float32))])
-    return _fn(lambda a: torch.nn.functional.pad(a, tp, mode=m, value=constant) if m == "constant"
-               else torch.nn.functional.pad(a, tp, mode=m), x, onnx=spec)
+    return Fn(lambda a: (G.pad(a, before, after, mode, float(constant)), tuple(a.shape)),
+              lambda shp, d: G.pad_backward(d, shp, before, mode), onnx=spec)(x)
 
 
 def clip(x, min=None, max=None):  # noqa: A002
+    lo = -math.inf if min is None else float(min)
+    hi = math.inf if max is None else float(max)
     ins = [("in", 0), ("const", np.asarray(-3.4e38 if min is None else min, np.float32)),
            ("const", np.asarray(3.4e38 if max is None else max, np.float32))]
-    return _fn(lambda a: torch.clamp(a, min=min, max=max), x, onnx=_ox("Clip", inputs=ins))
+    # gradient passes where lo <= x <= hi (closed interval, as torch.clamp)
+    return Fn(lambda a: (G.clamp_affine(a, 1.0, 0.0, lo, hi), a),
+              lambda a, d: G.where(G.binary("and", G.binary("ge", a, lo), G.binary("le", a, hi)), d,
+                                   G.zeros((), d.dtype, d.device)),
+              onnx=_ox("Clip", inputs=ins))(x)
 
 
 def where(x, y, condition):
     c = condition.data if isinstance(condition, Tensor) else torch.as_tensor(condition)
-    spec = _ox("Where", inputs=[("const", c.bool().cpu().numpy()), ("in", 0), ("in", 1)])
-    return _fn(lambda a, b: torch.where(c.to(a.device).bool(), a, b), x, y, onnx=spec)
+    spec = _ox("Where", inputs=[("const", c.bool().cpu().numpy()), ("in", 0), ("in", 1)]) if _TRACE else None
+
+    def fwd(a, b):
+        cc = c.to(a.device) if c.device != a.device else c
+        return G.where(cc, a, b), (cc, tuple(a.shape), tuple(b.shape))
+
+    def bwd(ctx, d):
+        cc, sa, sb = ctx
+        z = G.zeros((), d.dtype, d.device)
+        return G.sum_to(G.where(cc, d, z), sa), G.sum_to(G.where(cc, z, d), sb)
+    return Fn(fwd, bwd, onnx=spec)(x, y)
+
+
+def _reduce_op(x, axes, keepdims, op, spec):
+    def fwd(a):
+        return G.reduce(a, axes, op, bool(keepdims), out_dtype=a.dtype if a.is_floating_point() else None), \
+            (tuple(a.shape), a.dtype)
+
+    def bwd(ctx, d):
+        shp, dt = ctx
+        nd = len(shp)
+        ax = list(range(nd)) if axes is None else [a % nd for a in axes]
+        kshape = [1 if k in ax else s for k, s in enumerate(shp)]
+        g = G.expand(G.reshape(d, kshape), shp)
+        if op == "mean":
+            g = F.unary("scale", g, 1.0 / _b.max(1, int(np.prod([shp[k] for k in ax]))))
+        return G.to(g, dt) if g.dtype != dt else g
+    return Fn(fwd, bwd, onnx=spec)(x)
 
 
 def reduce_sum(x, axes=None, keepdims=1):
     ins = [("in", 0)] + ([("const", np.asarray(axes, np.int64))] if axes is not None else [])
-    return _fn(lambda a: a.sum(dim=tuple(axes), keepdim=bool(keepdims)) if axes is not None else a.sum(), x,
-               onnx=_ox("ReduceSum", {"keepdims": int(keepdims) if axes is not None else 0}, ins))
+    return _reduce_op(x, axes, keepdims if axes is not None else 0, "sum",
+                      _ox("ReduceSum", {"keepdims": int(keepdims) if axes is not None else 0}, ins))
 
 
 def reduce_mean(x, axes=None, keepdims=1):
     at = {"keepdims": int(keepdims) if axes is not None else 0}
     if axes is not None:
         at["axes"] = list(axes)
-    return _fn(lambda a: a.mean(dim=tuple(axes), keepdim=bool(keepdims)) if axes is not None else a.mean(), x,
-               onnx=_ox("ReduceMean", at))
+    return _reduce_op(x, axes, keepdims if axes is not None else 0, "mean", _ox("ReduceMean", at))
+
+
+def _nary(xs, op, spec):
+    """sum / mean / max / min of several broadcastable tensors."""
+    def fwd(*a):
+        r = a[0]
+        for t in a[1:]:
+            r = G.binary("add" if op in ("sum", "mean") else op, r, t)
+        if op == "mean":
+            r = F.unary("scale", r, 1.0 / len(a))
+        return r, (a, r)
+
+    def bwd(ctx, d):
+        a, r = ctx
+        out = []
+        for t in a:
+            if op in ("sum", "mean"):
+                g = d if op == "sum" else F.unary("scale", d, 1.0 / len(a))
+            else:  # every input equal to the result gets the gradient (reference PartialGrad)
+                g = G.binary("mul", d, G.binary("eq", t, r, out_dtype=d.dtype))
+            out.append(G.sum_to(g, t.shape))
+        return tuple(out)
+    return Fn(fwd, bwd, onnx=spec)(*xs)
 
 
 def sum(*xs):  # noqa: A001
-    return TorchFn(lambda *a: _b.sum(a[1:], a[0]), onnx=_ox("Sum", n_in=len(xs)))(*xs)
+    return _nary(xs, "sum", _ox("Sum", n_in=len(xs)))
 
 
 def mean(*xs):
-    return TorchFn(lambda *a: _b.sum(a[1:], a[0]) / len(a), onnx=_ox("Mean", n_in=len(xs)))(*xs)
+    return _nary(xs, "mean", _ox("Mean", n_in=len(xs)))
 
 
 def max(*xs):  # noqa: A001
-    def f(*a):
-        r = a[0]
-        for t in a[1:]:
-            r = torch.maximum(r, t)
-        return r
-    return TorchFn(f, onnx=_ox("Max", n_in=len(xs)))(*xs)
+    return _nary(xs, "max", _ox("Max", n_in=len(xs)))
 
 
 def min(*xs):  # noqa: A001
-    def f(*a):
-        r = a[0]
-        for t in a[1:]:
-            r = torch.minimum(r, t)
-        return r
-    return TorchFn(f, onnx=_ox("Min", n_in=len(xs)))(*xs)
+    return _nary(xs, "min", _ox("Min", n_in=len(xs)))
+
+
+class _Math(_Unary):
+    """Native elementwise math (functional.UNARY) with an ONNX name."""
+    onnx_op = ""
+
+    @property
+    def onnx(self):
+        return _ox(self.onnx_op)
+
+
+def _math(kind_, needs_, onnx_op):
+    return type(onnx_op, (_Math,), {"kind": kind_, "needs": needs_, "onnx_op": onnx_op})
+
+
+Erf, Cos, Sin, Tan = _math("erf", "x", "Erf"), _math("cos", "x", "Cos"), _math("sin", "x", "Sin"), \
+    _math("tan", "y", "Tan")
+Cosh, Sinh, Acos, Asin = _math("cosh", "x", "Cosh"), _math("sinh", "x", "Sinh"), _math("acos", "x", "Acos"), \
+    _math("asin", "x", "Asin")
+Atan, Acosh, Asinh, Atanh = _math("atan", "x", "Atan"), _math("acosh", "x", "Acosh"), _math("asinh", "x", "Asinh"), \
+    _math("atanh", "x", "Atanh")
+Ceil, Floor, Round, Softsign = _math("ceil", "", "Ceil"), _math("floor", "", "Floor"), _math("round", "", "Round"), \
+    _math("softsign", "x", "Softsign")
 
 
 def erf(x):
-    return _fn(torch.erf, x, onnx=_ox("Erf"))
+    return Erf()(x)
 
 
 def cos(x):
-    return _fn(torch.cos, x, onnx=_ox("Cos"))
+    return Cos()(x)
 
 
 def sin(x):
-    return _fn(torch.sin, x, onnx=_ox("Sin"))
+    return Sin()(x)
 
 
 def tan(x):
-    return _fn(torch.tan, x, onnx=_ox("Tan"))
+    return Tan()(x)
 
 
 def cosh(x):
-    return _fn(torch.cosh, x, onnx=_ox("Cosh"))
+    return Cosh()(x)
 
 
 def sinh(x):
-    return _fn(torch.sinh, x, onnx=_ox("Sinh"))
+    return Sinh()(x)
 
 
 def acos(x):
-    return _fn(torch.acos, x, onnx=_ox("Acos"))
+    return Acos()(x)
 
 
 def asin(x):
-    return _fn(torch.asin, x, onnx=_ox("Asin"))
+    return Asin()(x)
 
 
 def atan(x):
-    return _fn(torch.atan, x, onnx=_ox("Atan"))
+    return Atan()(x)
 
 
 def acosh(x):
-    return _fn(torch.acosh, x, onnx=_ox("Acosh"))
+    return Acosh()(x)
 
 
 def asinh(x):
-    return _fn(torch.asinh, x, onnx=_ox("Asinh"))
+    return Asinh()(x)
 
 
 def atanh(x):
-    return _fn(torch.atanh, x, onnx=_ox("Atanh"))
+    return Atanh()(x)
 
 
 def ceil(x):
-    return _fn(torch.ceil, x, onnx=_ox("Ceil"))
+    return Ceil()(x)
 
 
 def floor(x):
-    return _fn(torch.floor, x, onnx=_ox("Floor"))
+    return Floor()(x)
 
 
 def round(x):  # noqa: A001
-    return _fn(torch.round, x, onnx=_ox("Round"))
+    return Round()(x)
 
 
 def softsign(x):
-    return _fn(lambda a: a / (1 + a.abs()), x, onnx=_ox("Softsign"))
+    return Softsign()(x)
 
 
 def hardsigmoid(x, alpha=0.2, gamma=0.5):
-    return _fn(lambda a: torch.clamp(alpha * a + gamma, 0, 1), x,
-               onnx=_ox("HardSigmoid", {"alpha": float(alpha), "beta": float(gamma)}))
+    return Fn(lambda a: (G.clamp_affine(a, alpha, gamma, 0.0, 1.0), a),
+              lambda a, d: G.clamp_affine(a, alpha, gamma, 0.0, 1.0, dy=d),
+              onnx=_ox("HardSigmoid", {"alpha": float(alpha), "beta": float(gamma)}))(x)
 
 
 def prelu(x, slope):
-    return _fn(lambda a, s: torch.where(a > 0, a, a * s), x, slope, onnx=_ox("PRelu", n_in=2))
+    def fwd(a, s):
+        pos = F.unary("relu", a)
+        neg = G.binary("sub", a, pos)  # min(a, 0)
+        return G.binary("add", pos, G.binary("mul", neg, s)), (a, s, neg)
+
+    def bwd(ctx, d):
+        a, s, neg = ctx
+        pos_mask = G.binary("gt", a, 0.0)
+        # dx = d * (a > 0 ? 1 : s) = d * (mask + (1 - mask) * s)
+        one_minus = G.binary("sub", G.full((), 1.0, pos_mask.dtype, pos_mask.device), pos_mask)
+        coef = G.binary("add", pos_mask, G.binary("mul", one_minus, s))
+        dx = G.binary("mul", d, coef)
+        ds = G.sum_to(G.binary("mul", d, neg), s.shape)
+        return dx, ds
+    return Fn(fwd, bwd, onnx=_ox("PRelu", n_in=2))(x, slope)
 
 
-def _cmp_op(fn):
+def _cmp_op(op):
     def f(x, y):
-        yy = y.data if isinstance(y, Tensor) else torch.as_tensor(y, device=x.data.device)
-        return Tensor(device=x.device, data=fn(x.data, yy).to(x.dtype), requires_grad=False)
+        yy = y.data if isinstance(y, Tensor) else y
+        return Tensor(device=x.device, data=G.binary(op, x.data, yy, out_dtype=x.dtype if x.data.is_floating_point()
+                                                     else torch.float32), requires_grad=False)
     return f
 
 
-less = _cmp_op(torch.lt)
-greater = _cmp_op(torch.gt)
-equal = _cmp_op(torch.eq)
-_and = _cmp_op(lambda a, b: a.bool() & b.bool())
-_or = _cmp_op(lambda a, b: a.bool() | b.bool())
-_xor = _cmp_op(lambda a, b: a.bool() ^ b.bool())
+less = _cmp_op("lt")
+greater = _cmp_op("gt")
+equal = _cmp_op("eq")
+_and = _cmp_op("and")
+_or = _cmp_op("or")
+_xor = _cmp_op("xor")
 
 
 def _not(x):
-    return Tensor(device=x.device, data=(~x.data.bool()).to(x.dtype), requires_grad=False)
+    return Tensor(device=x.device, data=G.binary("eq", x.data, 0.0), requires_grad=False)
 
 
 def shape(x):
@@ -1580,63 +1733,102 @@ def shape(x):
 
 def constant_of_shape(x, value=0.0):
     shp = [int(v) for v in x.data.reshape(-1).tolist()]
-    return Tensor(device=x.device, data=torch.full(shp, value, dtype=torch.float32, device=x.data.device),
-                  requires_grad=False)
+    return Tensor(device=x.device, data=G.full(shp, value, torch.float32, x.data.device), requires_grad=False)
 
 
 def onehot(axis, indices, depth, values):
-    idx = indices.data.long()
-    off, on = float(values.data.reshape(-1)[0]), float(values.data.reshape(-1)[1])
-    oh = torch.nn.functional.one_hot(idx % depth, depth).to(torch.float32) * (on - off) + off
+    idx = indices.data
+    vals = values.data.reshape(-1)
+    off, on = float(vals[0]), float(vals[1])
+    dev = idx.device
+    shp = tuple(idx.shape) + (depth,)
+    oh = G.full(shp, off, torch.float32, dev)
+    ii = G.to(idx, torch.int64)  # negative ids wrap like numpy (ONNX OneHot)
+    oh = G.scatter_elements(oh, -1, G.reshape(ii, tuple(idx.shape) + (1,)), G.full(tuple(idx.shape) + (1,), on,
+                                                                                     torch.float32, dev))
     if axis != -1:
-        oh = oh.movedim(-1, axis)
+        oh = G.contiguous(oh.movedim(-1, axis))
     return Tensor(device=indices.device, data=oh, requires_grad=False)
 
 
 def upsample(x, mode, scales):
-    sc = [float(s) for s in scales]
+    sc = [int(_b.round(float(s))) for s in scales]
+    if mode != "nearest" or any(_b.abs(float(s) - r) > 1e-6 for s, r in zip(scales, sc)):
+        raise NotImplementedError("upsample: nearest mode with integer scales")
 
-    def f(a):
-        return torch.nn.functional.interpolate(a, scale_factor=sc[2:], mode="nearest")
-    return _fn(f, x, onnx=_ox("Resize", {"mode": "nearest"}, [("in", 0), ("const", np.zeros(0, np.float32)),
-                                                              ("const", np.asarray(sc, np.float32))]))
+    def fwd(a):
+        inter = []
+        src = []
+        for s, r in zip(a.shape, sc):
+            inter += [s, r]
+            src += [s, 1]
+        out = torch.empty(inter, dtype=a.dtype, device=a.device)
+        G.copy_(out, a.reshape(src).expand(*inter))
+        return out.reshape([s * r for s, r in zip(a.shape, sc)]), tuple(a.shape)
+
+    def bwd(shp, d):
+        inter = []
+        for s, r in zip(shp, sc):
+            inter += [s, r]
+        return G.reduce(G.reshape(d, inter), [2 * k + 1 for k in range(len(shp))], "sum", out_dtype=d.dtype)
+    return Fn(fwd, bwd, onnx=_ox("Resize", {"mode": "nearest"}, [("in", 0), ("const", np.zeros(0, np.float32)),
+                                                                 ("const", np.asarray(scales, np.float32))]))(x)
+
+
+def _space_perm(x, perm, mid, out_shape, spec):
+    """reshape(mid) -> permute(perm) -> reshape(out) (one native copy) and its inverse."""
+    inv = tuple(int(i) for i in np.argsort(perm))
+    in_shape = tuple(x.shape)
+    pshape = [mid[i] for i in perm]
+
+    def fwd(a):
+        return G.reshape(G.contiguous(G.reshape(a, mid).permute(*perm)), out_shape), None
+
+    def bwd(c, d):
+        return G.reshape(G.contiguous(G.reshape(d, pshape).permute(*inv)), in_shape)
+    return Fn(fwd, bwd, onnx=spec)(x)
 
 
 def depth_to_space(x, blocksize, mode="DCR"):
-    return _fn(lambda a: torch.nn.functional.pixel_shuffle(a, blocksize), x,
-               onnx=_ox("DepthToSpace", {"blocksize": blocksize, "mode": "CRD"}))
+    Nn, C, H, W = x.shape
+    b = blocksize
+    c = C // (b * b)
+    if mode == "DCR":
+        mid, perm = (Nn, b, b, c, H, W), (0, 3, 4, 1, 5, 2)
+    else:  # CRD
+        mid, perm = (Nn, c, b, b, H, W), (0, 1, 4, 2, 5, 3)
+    return _space_perm(x, perm, mid, (Nn, c, H * b, W * b),
+                       _ox("DepthToSpace", {"blocksize": blocksize, "mode": mode}))
 
 
 def space_to_depth(x, blocksize, mode="DCR"):
-    return _fn(lambda a: torch.nn.functional.pixel_unshuffle(a, blocksize), x,
-               onnx=_ox("SpaceToDepth", {"blocksize": blocksize}))
+    Nn, C, H, W = x.shape
+    b = blocksize
+    return _space_perm(x, (0, 3, 5, 1, 2, 4), (Nn, C, H // b, b, W // b, b), (Nn, C * b * b, H // b, W // b),
+                       _ox("SpaceToDepth", {"blocksize": blocksize}))
 
 
 class Embedding(Operator):
-    """y = W[idx] (row gather).  Backward scatter-adds the dy rows into dW with
-    ``index_add_`` (atomics): no sort / unique / host sync, so a step using it
-    can be captured into a HIP graph -- torch's embedding backward computes
-    data-dependent segment counts and faults under capture.  Deterministic
-    mode keeps the ordered (sort-based, not capturable) backward."""
+    """y = W[idx] (row gather, native index_select).  Backward scatter-adds
+    the dy rows into dW (native index_add, fp32 atomics) -- no sort / unique
+    / host sync, so a step using it can be captured into a HIP graph.
+    Deterministic mode keeps an ordered backward (CPU reference order)."""
 
     def forward(self, W, idx):
-        i = idx.long()
         if self.requires_grad:
-            self.idx, self.wshape = i, W.shape
-        return torch.nn.functional.embedding(i, W)
+            self.idx, self.wshape, self.wdt = idx, W.shape, W.dtype
+        return G.index_select(W, 0, idx)
 
     def backward(self, dy):
         i = self.idx.reshape(-1)
         self.idx = None
-        d = dy.reshape(-1, dy.shape[-1])
-        if os.environ.get("SINGA_AMD_DETERMINISTIC", "0") == "1":
-            dw = torch.ops.aten.embedding_dense_backward(d.float(), i, self.wshape[0], -1, False)
-        else:
-            tgt = self.grad_target(0)
-            if tgt is not None and tgt.dim() == 2:
-                tgt.index_add_(0, i, d.to(tgt.dtype))
-                return ACCUMULATED, None
-            dw = torch.zeros(self.wshape, dtype=torch.float32, device=dy.device).index_add_(0, i, d.float())
+        d = G.reshape(dy, (-1, dy.shape[-1]))
+        tgt = self.grad_target(0)
+        if tgt is not None and tgt.dim() == 2 and tgt.dtype == torch.float32 and tgt.is_contiguous():
+            G.index_add_(tgt, 0, i, d)
+            return ACCUMULATED, None
+        dw = G.zeros(self.wshape, torch.float32, dy.device)
+        G.index_add_(dw, 0, i, d)
         return dw, None
 
 
@@ -1649,22 +1841,63 @@ def globalaveragepool(x, keepdims=True):
 
 
 def scatter_elements(x, indices, updates, axis=0):
-    idx = indices.data.long()
-    return TorchFn(lambda a, u: a.scatter(axis, idx, u),
-                   onnx=_ox("ScatterElements", {"axis": axis}, [("in", 0), ("const", idx.cpu().numpy()),
-                                                                ("in", 1)]))(x, updates)
+    idx = indices.data.long() if indices.data.dtype not in (torch.int32, torch.int64) else indices.data
+    spec = _ox("ScatterElements", {"axis": axis}, [("in", 0), ("const", idx.cpu().numpy()), ("in", 1)]) \
+        if _TRACE else None
+
+    def fwd(a, u):
+        ii = idx.to(a.device) if idx.device != a.device else idx
+        return G.scatter_elements(a, axis, ii, u), ii
+
+    def bwd(ii, d):
+        dx = G.scatter_elements(d, axis, ii, G.zeros(ii.shape, d.dtype, d.device))
+        return dx, G.gather_elements(d, axis, ii)
+    return Fn(fwd, bwd, onnx=spec)(x, updates)
+
+
+class Gemm(Operator):
+    """ONNX/SINGA Gemm: y = alpha * op(A) op(B) + beta * C (C broadcast over
+    rows); op = transpose when transA / transB.  Both products of the
+    backward run on the MFMA GEMM kernels like the forward."""
+
+    def __init__(self, alpha=1.0, beta=1.0, transA=0, transB=0, name=None):
+        super().__init__(name)
+        self.alpha, self.beta, self.ta, self.tb = float(alpha), float(beta), bool(transA), bool(transB)
+
+    def forward(self, a, b, c=None):
+        bias = None
+        ncol = b.shape[0] if self.tb else b.shape[1]
+        if c is not None and c.dim() <= 1 and c.numel() == ncol and self.beta == 1.0:
+            bias = c.reshape(-1)  # row bias in the epilogue
+        y = F.gemm(a, b, self.ta, self.tb, out_dtype=a.dtype, alpha=self.alpha, bias=bias)
+        if c is not None and bias is None:
+            y = G.binary("add", y, G.binary("mul", c, self.beta, out_dtype=y.dtype) if self.beta != 1.0 else c,
+                         out_dtype=y.dtype)
+        if self.requires_grad:
+            self.a, self.b = a, b
+            self.cshape = c.shape if c is not None else None
+        return y
+
+    def backward(self, dy):
+        a, b = self.a, self.b
+        self.a = self.b = None
+        dy = dy.contiguous()
+        da = db = None
+        if self.needs_grad(0):  # d op(A) = alpha dy op(B)^T
+            da = (F.gemm(b, dy, self.tb, True, out_dtype=a.dtype, alpha=self.alpha) if self.ta else
+                  F.gemm(dy, b, False, not self.tb, out_dtype=a.dtype, alpha=self.alpha))
+        if self.needs_grad(1):  # d op(B) = alpha op(A)^T dy
+            db = (F.gemm(dy, a, True, self.ta, out_dtype=b.dtype, alpha=self.alpha) if self.tb else
+                  F.gemm(a, dy, not self.ta, False, out_dtype=b.dtype, alpha=self.alpha))
+        if self.cshape is None:
+            return da, db
+        dc = _unbroadcast(F.unary("scale", dy, self.beta) if self.beta != 1.0 else dy, self.cshape)
+        return da, db, dc
 
 
 def gemm(A, B, C=None, alpha=1.0, beta=1.0, transA=0, transB=0):
-    def f(a, b, *c):
-        aa = a.t() if transA else a
-        bb = b.t() if transB else b
-        r = alpha * (aa @ bb)
-        if c:
-            r = r + beta * c[0]
-        return r
-    args = [A, B] + ([C] if C is not None else [])
-    return TorchFn(f)(*args)
+    op = Gemm(alpha, beta, transA, transB)
+    return op(A, B, C) if C is not None else op(A, B)
 
 
 def conv2d(x, W, b=None, stride=(1, 1), padding=(0, 0), dilation=(1, 1), group=1):

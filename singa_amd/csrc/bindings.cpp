@@ -11,6 +11,7 @@
 #include <stdint.h>
 #include <stdexcept>
 #include <string>
+#include <vector>
 
 namespace py = pybind11;
 typedef uintptr_t P;
@@ -102,6 +103,30 @@ void sg_conv_dgrad(const void*, const void*, void*, int, int, int, int, int, int
                    int, int, int, float, void*, hipStream_t);
 void sg_conv_wgrad(const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int, int,
                    int, int, int, hipStream_t);
+void sg_ggemm(int, const void*, int64_t, int, int64_t, const void*, int64_t, int, int64_t, void*, int64_t, int64_t,
+              int, int, int, float, float, const void*, int, int, int, int, hipStream_t);
+void sg_gconv_fwd(int, const void*, const void*, void*, const void*, int, int, int, int, int, int, int, int, int, int,
+                  int, int, int, int, int, int, int, int, hipStream_t);
+void sg_gconv_dgrad(int, const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int,
+                    int, int, int, int, int, float, hipStream_t);
+void sg_gconv_wgrad(int, const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int,
+                    int, int, int, int, int, hipStream_t);
+void sg_copy_nd(const void*, int, void*, int, int, const int64_t*, const int64_t*, const int64_t*, hipStream_t);
+void sg_binary_nd(int, const void*, const void*, void*, int, int, const int64_t*, const int64_t*, const int64_t*,
+                  const int64_t*, float, hipStream_t);
+void sg_where_nd(const void*, const void*, const void*, void*, int, int, const int64_t*, const int64_t*,
+                 const int64_t*, const int64_t*, const int64_t*, hipStream_t);
+void sg_reduce(const void*, int, void*, int, int64_t, int64_t, int64_t, int, hipStream_t);
+void sg_index_select(const void*, const void*, int, void*, int64_t, int64_t, int64_t, int64_t, int, hipStream_t);
+void sg_index_add(void*, const void*, int, const void*, int, int64_t, int64_t, int64_t, int64_t, float, hipStream_t);
+void sg_gather_el(const void*, const void*, int, void*, int, int64_t, int64_t, int64_t, int64_t, hipStream_t);
+void sg_scatter_el(void*, const void*, int, const void*, int, int64_t, int64_t, int64_t, int64_t, int, hipStream_t);
+void sg_pad_nd(const void*, void*, int, int, const int64_t*, const int64_t*, const int64_t*, const int64_t*, int, float,
+               hipStream_t);
+void sg_pad_bwd(const void*, void*, int, int, const int64_t*, const int64_t*, const int64_t*, const int64_t*, int,
+                hipStream_t);
+void sg_fill(void*, int64_t, int, double, hipStream_t);
+void sg_clamp_affine(const void*, const void*, void*, int64_t, int, float, float, float, float, hipStream_t);
 void sg_set_tuning(int key, int value);
 void sg_bn_set_unroll(int);
 void sg_bn_set_rows_per_thread(int);
@@ -353,6 +378,84 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("set_ws_prezeroed", [](int on) { sg_set_ws_prezeroed(on); });
   m.def("zero", [](P p, int64_t bytes, P s) { sg_zero(V(p), bytes, S(s)); CHK("zero"); });
+  // generic MFMA GEMM / conv (csrc/kernels/ggemm.hip): dt 0 = fp32 operands (exact f32 MFMA), 1 = bf16
+  m.def("ggemm", [](int dt, P a, int64_t lda, int ako, int64_t sa, P b, int64_t ldb, int bko, int64_t sb, P c,
+                    int64_t ldc, int64_t sc, int M, int N, int K, float alpha, float beta, P bias, int relu,
+                    int out_mode, int splits, int batch, P s) {
+    sg_ggemm(dt, CV(a), lda, ako, sa, CV(b), ldb, bko, sb, V(c), ldc, sc, M, N, K, alpha, beta, CV(bias), relu,
+             out_mode, splits, batch, S(s));
+    CHK("ggemm");
+  });
+  m.def("gconv_fwd", [](int dt, P x, P w, P y, P bias, int N, int H, int W, int C, int K, int R, int Sd, int Ho,
+                        int Wo, int sh, int sw, int ph, int pw, int dh, int dw, int groups, int relu, int out_mode,
+                        P s) {
+    sg_gconv_fwd(dt, CV(x), CV(w), V(y), CV(bias), N, H, W, C, K, R, Sd, Ho, Wo, sh, sw, ph, pw, dh, dw, groups, relu,
+                 out_mode, S(s));
+    CHK("gconv_fwd");
+  });
+  m.def("gconv_dgrad", [](int dt, P dy, P w, P dx, int N, int H, int W, int C, int K, int R, int Sd, int Ho, int Wo,
+                          int sh, int sw, int ph, int pw, int dh, int dw, int groups, int out_mode, float beta, P s) {
+    sg_gconv_dgrad(dt, CV(dy), CV(w), V(dx), N, H, W, C, K, R, Sd, Ho, Wo, sh, sw, ph, pw, dh, dw, groups, out_mode,
+                   beta, S(s));
+    CHK("gconv_dgrad");
+  });
+  m.def("gconv_wgrad", [](int dt, P x, P dy, P dw_out, int N, int H, int W, int C, int K, int R, int Sd, int Ho,
+                          int Wo, int sh, int sw, int ph, int pw, int dh, int dw, int groups, int splits, P s) {
+    sg_gconv_wgrad(dt, CV(x), CV(dy), V(dw_out), N, H, W, C, K, R, Sd, Ho, Wo, sh, sw, ph, pw, dh, dw, groups, splits,
+                   S(s));
+    CHK("gconv_wgrad");
+  });
+  // glue kernels (csrc/kernels/glue.hip); shapes / strides as int64 lists, already coalesced
+  typedef std::vector<int64_t> VI;
+  m.def("copy_nd", [](P src, int dti, P dst, int dto, const VI& size, const VI& dst_st, const VI& src_st, P s) {
+    sg_copy_nd(CV(src), dti, V(dst), dto, (int)size.size(), size.data(), dst_st.data(), src_st.data(), S(s));
+    CHK("copy_nd");
+  });
+  m.def("binary_nd", [](int op, P a, P b, P out, int dt, const VI& size, const VI& os, const VI& as, const VI& bs,
+                        float alpha, P s) {
+    sg_binary_nd(op, CV(a), CV(b), V(out), dt, (int)size.size(), size.data(), os.data(), as.data(), bs.data(), alpha,
+                 S(s));
+    CHK("binary_nd");
+  });
+  m.def("where_nd", [](P c, P a, P b, P out, int dt, const VI& size, const VI& os, const VI& as, const VI& bs,
+                       const VI& cs, P s) {
+    sg_where_nd(CV(c), CV(a), CV(b), V(out), dt, (int)size.size(), size.data(), os.data(), as.data(), bs.data(),
+                cs.data(), S(s));
+    CHK("where_nd");
+  });
+  m.def("reduce", [](P x, int dti, P y, int dto, int64_t outer, int64_t red, int64_t inner, int op, P s) {
+    sg_reduce(CV(x), dti, V(y), dto, outer, red, inner, op, S(s)); CHK("reduce");
+  });
+  m.def("index_select", [](P src, P idx, int idx64, P dst, int64_t outer, int64_t nsrc, int64_t inner, int64_t nidx,
+                           int esize, P s) {
+    sg_index_select(CV(src), CV(idx), idx64, V(dst), outer, nsrc, inner, nidx, esize, S(s)); CHK("index_select");
+  });
+  m.def("index_add", [](P dst, P idx, int idx64, P src, int dts, int64_t outer, int64_t ndst, int64_t inner,
+                        int64_t nidx, float alpha, P s) {
+    sg_index_add(V(dst), CV(idx), idx64, CV(src), dts, outer, ndst, inner, nidx, alpha, S(s)); CHK("index_add");
+  });
+  m.def("gather_el", [](P src, P idx, int idx64, P out, int dt, int64_t outer, int64_t nsrc, int64_t nidx,
+                        int64_t inner, P s) {
+    sg_gather_el(CV(src), CV(idx), idx64, V(out), dt, outer, nsrc, nidx, inner, S(s)); CHK("gather_el");
+  });
+  m.def("scatter_el", [](P dst, P idx, int idx64, P upd, int dt, int64_t outer, int64_t ndst, int64_t nidx,
+                         int64_t inner, int add, P s) {
+    sg_scatter_el(V(dst), CV(idx), idx64, CV(upd), dt, outer, ndst, nidx, inner, add, S(s)); CHK("scatter_el");
+  });
+  m.def("pad_nd", [](P x, P y, int dt, const VI& osz, const VI& isz, const VI& ist, const VI& before, int mode,
+                     float value, P s) {
+    sg_pad_nd(CV(x), V(y), dt, (int)osz.size(), osz.data(), isz.data(), ist.data(), before.data(), mode, value, S(s));
+    CHK("pad_nd");
+  });
+  m.def("pad_bwd", [](P dy, P dx, int dt, const VI& osz, const VI& isz, const VI& ist, const VI& before, int mode,
+                      P s) {
+    sg_pad_bwd(CV(dy), V(dx), dt, (int)osz.size(), osz.data(), isz.data(), ist.data(), before.data(), mode, S(s));
+    CHK("pad_bwd");
+  });
+  m.def("fill", [](P p, int64_t n, int dt, double v, P s) { sg_fill(V(p), n, dt, v, S(s)); CHK("fill"); });
+  m.def("clamp_affine", [](P x, P dy, P out, int64_t n, int dt, float a, float b, float lo, float hi, P s) {
+    sg_clamp_affine(CV(x), CV(dy), V(out), n, dt, a, b, lo, hi, S(s)); CHK("clamp_affine");
+  });
   m.def("set_tuning", [](int key, int value) { sg_set_tuning(key, value); });
   m.def("bn_set_unroll", [](int ur) { sg_bn_set_unroll(ur); });
   m.def("bn_set_rows_per_thread", [](int rpt) { sg_bn_set_rows_per_thread(rpt); });

@@ -12,7 +12,11 @@ enum UnaryOp : int {
   U_RELU = 0, U_SIGMOID = 1, U_TANH = 2, U_STANH = 3, U_GELU = 4,
   U_IDENTITY = 5, U_SOFTPLUS = 6, U_SQUARE = 7, U_ABS = 8, U_EXP = 9,
   U_LEAKY = 10, U_ELU = 11, U_SELU = 12, U_GELU_TANH = 13, U_SQRT = 14,
-  U_NEG = 15, U_RECIP = 16, U_LOG = 17, U_SIGN = 18
+  U_NEG = 15, U_RECIP = 16, U_LOG = 17, U_SIGN = 18,
+  // ONNX / SINGA glue math (autograd erf, trig, rounding, softsign, scalar ops)
+  U_ERF = 19, U_COS = 20, U_SIN = 21, U_TAN = 22, U_COSH = 23, U_SINH = 24, U_ACOS = 25, U_ASIN = 26,
+  U_ATAN = 27, U_ACOSH = 28, U_ASINH = 29, U_ATANH = 30, U_CEIL = 31, U_FLOOR = 32, U_ROUND = 33,
+  U_SOFTSIGN = 34, U_SCALE = 35, U_ADDS = 36, U_RSQRT = 37, U_POWS = 38
 };
 
 __device__ __forceinline__ float unary_f(int op, float x, float a) {
@@ -42,6 +46,26 @@ __device__ __forceinline__ float unary_f(int op, float x, float a) {
     case U_RECIP: return 1.f / x;
     case U_LOG: return __logf(x);
     case U_SIGN: return (float)((x > 0.f) - (x < 0.f));
+    case U_ERF: return erff(x);
+    case U_COS: return cosf(x);
+    case U_SIN: return sinf(x);
+    case U_TAN: return tanf(x);
+    case U_COSH: return coshf(x);
+    case U_SINH: return sinhf(x);
+    case U_ACOS: return acosf(x);
+    case U_ASIN: return asinf(x);
+    case U_ATAN: return atanf(x);
+    case U_ACOSH: return acoshf(x);
+    case U_ASINH: return asinhf(x);
+    case U_ATANH: return atanhf(x);
+    case U_CEIL: return ceilf(x);
+    case U_FLOOR: return floorf(x);
+    case U_ROUND: return rintf(x);  // half to even (ONNX Round)
+    case U_SOFTSIGN: return x / (1.f + fabsf(x));
+    case U_SCALE: return a * x;
+    case U_ADDS: return x + a;
+    case U_RSQRT: return rsqrtf(x);
+    case U_POWS: return powf(x, a);
   }
   return x;
 }
@@ -81,6 +105,27 @@ __device__ __forceinline__ float unary_b(int op, float x, float y, float dy, flo
     case U_RECIP: return -dy * y * y;
     case U_LOG: return dy / x;
     case U_SIGN: return 0.f;
+    case U_ERF: return dy * 1.1283791671f * __expf(-x * x);
+    case U_COS: return -dy * sinf(x);
+    case U_SIN: return dy * cosf(x);
+    case U_TAN: return dy * (1.f + y * y);
+    case U_COSH: return dy * sinhf(x);
+    case U_SINH: return dy * coshf(x);
+    case U_ACOS: return -dy * rsqrtf(1.f - x * x);
+    case U_ASIN: return dy * rsqrtf(1.f - x * x);
+    case U_ATAN: return dy / (1.f + x * x);
+    case U_ACOSH: return dy * rsqrtf(x * x - 1.f);
+    case U_ASINH: return dy * rsqrtf(x * x + 1.f);
+    case U_ATANH: return dy / (1.f - x * x);
+    case U_CEIL: case U_FLOOR: case U_ROUND: return 0.f;
+    case U_SOFTSIGN: {
+      const float d = 1.f + fabsf(x);
+      return dy / (d * d);
+    }
+    case U_SCALE: return a * dy;
+    case U_ADDS: return dy;
+    case U_RSQRT: return -0.5f * dy * y * y * y;
+    case U_POWS: return dy * a * powf(x, a - 1.f);
   }
   return dy;
 }

@@ -1,0 +1,608 @@
+// Generic MFMA GEMM / implicit-GEMM convolution for gfx950: any shape, any
+// stride, groups and dilation, fp32 OR bf16 operands.
+//
+// The reference computes every InnerProduct and convolution in fp32 sgemm
+// (DotEngine, include/mshadow/tensor_expr_engine-inl.hpp:272-298,339-383;
+// ConvolutionLayer / InnerProductLayer, src/worker/layer.cc:63-123,193-211).
+// This is that precision on the matrix cores:
+//   * fp32 operands: v_mfma_f32_16x16x4_f32 -- exact f32 (a k-ordered fmaf
+//     chain), 157 TF on MI355X (gfx950 has no xf32/TF32 form, and no
+//     downcast happens here);
+//   * bf16 operands: v_mfma_f32_16x16x32_bf16, for the shapes the tuned
+//     bf16 kernel (igemm.hip: LDS-DMA staging, K-multiple-of-8 rows) does not
+//     take -- ragged dimensions, grouped / dilated convolutions.
+//
+//   C[m][n] (=|+=) alpha * sum_k A(m, k) * B(n, k) (+ bias[n]) (ReLU)
+//
+// Structure: BM x BN x 32 tiles (64 or 128 square), 256 threads = 2 x 2 waves.
+// Operands are staged global -> registers -> LDS (two stages, one barrier per
+// K-tile; the next tile's global loads are in flight during this tile's
+// MFMAs).  Every operand element is loaded through a "unit" of 4 elements
+// that are contiguous in memory when the shapes allow (one 16-byte fp32 / 8-
+// byte bf16 vector load), or 4 bounds-checked scalar loads otherwise, so no
+// dimension needs padding.  LDS images are [rows][32 k (+pad)]: each MFMA
+// lane reads its 4 (fp32) or 8 (bf16) consecutive k of one row with a single
+// ds_read_b128 -- the k order inside an MFMA step is permuted identically for
+// A and B, which leaves the sum unchanged.  Row pads of 16 bytes make the
+// 16-lane read groups conflict-free (row strides 144 B / 80 B).
+//
+// Operand modes (the loader gathers the implicit-GEMM operands itself):
+//   KMAJ    plain [rows][K] (ld)                     k-contiguous units
+//   KOUT    plain [K][rows] (ld)                     row-contiguous units
+//   CFWD_A  conv fwd A: im2col of x NHWC, rows = output pixels, k = (r, s, c)
+//   DGRAD_A conv dgrad A: dy NHWC gathered per input pixel, k = (r, s, k_out),
+//           taps that do not land on the stride grid are zero
+//   DGRAD_B conv dgrad B: W [K][R][S][Cg], rows = c, k = (r, s, k_out)
+//   WGRAD_B conv wgrad B: x gathered, rows = (r, s, c), k = output pixels
+// A group of a grouped convolution is one batch index (blockIdx.y): every
+// operand and the output advance by their per-group batch stride.
+#include <stdexcept>
+#include <string>
+
+#include "common.h"
+
+namespace sg {
+namespace gg {
+
+constexpr int BK = 32, NT = 256;
+enum Mode : int { KMAJ = 0, KOUT = 1, CFWD_A = 2, DGRAD_A = 3, DGRAD_B = 4, WGRAD_B = 5 };
+enum Out : int { O_BF16 = 0, O_F32 = 1, O_F32_ATOMIC = 2 };
+
+struct Geom {
+  int N, H, W, C, K;    // input NHWC (C total channels), K total filters
+  int Cg, Kg, R, S;     // per-group channels / filters; filter taps
+  int Ho, Wo, sh, sw, ph, pw, dh, dw;
+  FastDiv dCg, dKg, dS, dWo, dHoWo, dW, dHW, dsh, dsw;
+};
+
+struct Args {
+  int M, N, K;
+  const void* a;
+  int64_t lda, sa;  // leading dim, batch (group) stride in elements
+  const void* b;
+  int64_t ldb, sb;
+  void* c;
+  int64_t ldc, sc;
+  float alpha, beta;
+  const float* bias;
+  int64_t sbias;
+  int relu, out_mode;
+  int k_per_split;   // multiple of BK
+  int vec_a, vec_b;  // 4-element units are contiguous + aligned (vector loads)
+  Geom g;
+};
+
+template <typename T> struct V4;
+template <> struct V4<float> { typedef f32x4 t; };
+template <> struct V4<bf16> { typedef bf16x4 t; };
+
+template <typename T> constexpr int pad_of() { return sizeof(T) == 4 ? 4 : 8; }
+template <typename T> constexpr int ld_of() { return BK + pad_of<T>(); }
+
+// One operand's loader: ROWS tile rows x BK k, U units of 4 elements / thread.
+template <typename T, int ROWS, int MODE>
+struct Ld {
+  static constexpr bool RC = (MODE == KOUT || MODE == DGRAD_B || MODE == WGRAD_B);
+  static constexpr int U = ROWS * BK / 4 / NT;
+  static constexpr int RQ = ROWS / 4;   // RC: row quads per k-row
+  static constexpr int KS = NT / RQ;    // RC: k-rows per pass
+  static_assert(U >= 1, "tile too small");
+  typedef typename V4<T>::t VT;
+  VT v[U];
+  const T* base;
+  int64_t ld;
+  int nrows;
+  bool vec;
+  // k-contiguous modes: per unit row info; RC modes: per element column info
+  int ri0[U], ri1[U], ri2[U];
+  bool rok[U];
+  int ci0[4], ci1[4], ci2[4];
+  bool cok[4];
+
+  __device__ __forceinline__ void init(const Args& p, const T* src, int64_t ld_, int row0, int nrows_, bool vec_) {
+    base = src;
+    ld = ld_;
+    nrows = nrows_;
+    vec = vec_;
+    const int t = threadIdx.x;
+    const Geom& g = p.g;
+    if constexpr (!RC) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int row = row0 + (t >> 3) + 32 * u;
+        rok[u] = row < nrows;
+        const int rr = rok[u] ? row : 0;
+        if constexpr (MODE == KMAJ) {
+          ri0[u] = rr;
+        } else if constexpr (MODE == CFWD_A) {
+          const int n = g.dHoWo.div(rr);
+          const int rem = rr - n * g.Ho * g.Wo;
+          const int oh = g.dWo.div(rem);
+          const int ow = rem - oh * g.Wo;
+          ri0[u] = n;
+          ri1[u] = oh * g.sh - g.ph;
+          ri2[u] = ow * g.sw - g.pw;
+        } else {  // DGRAD_A: rows are input pixels (n, h, w)
+          const int n = g.dHW.div(rr);
+          const int rem = rr - n * g.H * g.W;
+          const int h = g.dW.div(rem);
+          const int w = rem - h * g.W;
+          ri0[u] = n;
+          ri1[u] = h + g.ph;
+          ri2[u] = w + g.pw;
+        }
+      }
+    } else {
+      const int r4 = row0 + 4 * (t % RQ);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int col = r4 + e;
+        cok[e] = col < nrows;
+        const int cc = cok[e] ? col : 0;
+        if constexpr (MODE == KOUT || MODE == DGRAD_B) {
+          ci0[e] = cc;
+        } else {  // WGRAD_B: col = (r, s, c)
+          const int rs = g.dCg.div(cc);
+          const int c = cc - rs * g.Cg;
+          const int r = g.dS.div(rs);
+          const int s = rs - r * g.S;
+          ci0[e] = r * g.dh - g.ph;
+          ci1[e] = s * g.dw - g.pw;
+          ci2[e] = c;
+        }
+      }
+    }
+  }
+
+  // element offset + validity of (row info u / column e, absolute k)
+  __device__ __forceinline__ bool at_k(const Geom& g, int u, int k, int64_t& off) const {
+    if constexpr (MODE == KMAJ) {
+      off = (int64_t)ri0[u] * ld + k;
+      return rok[u];
+    } else if constexpr (MODE == CFWD_A) {
+      const int rs = g.dCg.div(k);
+      const int c = k - rs * g.Cg;
+      const int r = g.dS.div(rs);
+      const int s = rs - r * g.S;
+      const int ih = ri1[u] + r * g.dh, iw = ri2[u] + s * g.dw;
+      off = (((int64_t)ri0[u] * g.H + ih) * g.W + iw) * g.C + c;
+      return rok[u] && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+    } else {  // DGRAD_A: k = (r, s, ko)
+      const int rs = g.dKg.div(k);
+      const int ko = k - rs * g.Kg;
+      const int r = g.dS.div(rs);
+      const int s = rs - r * g.S;
+      const int th = ri1[u] - r * g.dh, tw = ri2[u] - s * g.dw;
+      const int oh = g.dsh.div((unsigned)(th < 0 ? 0 : th)), ow = g.dsw.div((unsigned)(tw < 0 ? 0 : tw));
+      const bool ok = th >= 0 && tw >= 0 && oh * g.sh == th && ow * g.sw == tw && oh < g.Ho && ow < g.Wo;
+      off = (((int64_t)ri0[u] * g.Ho + oh) * g.Wo + ow) * g.K + ko;
+      return rok[u] && ok;
+    }
+  }
+  __device__ __forceinline__ bool at_col(const Geom& g, int e, int k, int64_t& off) const {
+    if constexpr (MODE == KOUT) {
+      off = (int64_t)k * ld + ci0[e];
+      return cok[e];
+    } else if constexpr (MODE == DGRAD_B) {  // W [Kg][R][S][Cg] (group base in src), k = (r, s, ko)
+      const int rs = g.dKg.div(k);
+      const int ko = k - rs * g.Kg;
+      off = ((int64_t)ko * g.R * g.S + rs) * g.Cg + ci0[e];
+      return cok[e];
+    } else {  // WGRAD_B: k = output pixel
+      const int n = g.dHoWo.div(k);
+      const int rem = k - n * g.Ho * g.Wo;
+      const int oh = g.dWo.div(rem);
+      const int ow = rem - oh * g.Wo;
+      const int ih = oh * g.sh + ci0[e], iw = ow * g.sw + ci1[e];
+      off = (((int64_t)n * g.H + ih) * g.W + iw) * g.C + ci2[e];
+      return cok[e] && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+    }
+  }
+
+  // global -> registers for the K-tile at k0 (k < kend valid)
+  __device__ __forceinline__ void load(const Geom& g, int k0, int kend) {
+    const int t = threadIdx.x;
+    if constexpr (!RC) {
+      const int kb = k0 + 4 * (t & 7);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (vec) {
+          int64_t off;
+          const bool ok = kb < kend && at_k(g, u, kb, off);
+          v[u] = ok ? *(const VT*)(base + off) : VT{};
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            int64_t off;
+            const bool ok = kb + e < kend && at_k(g, u, kb + e, off);
+            v[u][e] = ok ? base[off] : (T)0.f;
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int k = k0 + t / RQ + KS * u;
+        const bool kin = k < kend;
+        const int kk = kin ? k : 0;
+        if (vec) {
+          int64_t off;
+          const bool ok = kin && at_col(g, 0, kk, off);
+          v[u] = ok ? *(const VT*)(base + off) : VT{};
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            int64_t off;
+            const bool ok = kin && at_col(g, e, kk, off);
+            v[u][e] = ok ? base[off] : (T)0.f;
+          }
+        }
+      }
+    }
+  }
+
+  // registers -> LDS image [ROWS][BK + pad]
+  __device__ __forceinline__ void store(T* lds) const {
+    constexpr int LD = ld_of<T>();
+    const int t = threadIdx.x;
+    if constexpr (!RC) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) *(VT*)(lds + ((t >> 3) + 32 * u) * LD + 4 * (t & 7)) = v[u];
+    } else {
+      const int r4 = 4 * (t % RQ);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int k = t / RQ + KS * u;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) lds[(r4 + e) * LD + k] = v[u][e];
+      }
+    }
+  }
+};
+
+template <typename T, int BM, int BN, int AM, int BMODE>
+__global__ void __launch_bounds__(NT, 2) ggemm_k(const Args p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int LD = ld_of<T>();
+  constexpr int A_EL = BM * LD, STAGE_EL = (BM + BN) * LD;
+  constexpr int WTM = BM / 2, WTN = BN / 2, TM = WTM / 16, TN = WTN / 16;
+  T* lds = (T*)smem;
+
+  const int64_t y = blockIdx.y;
+  const T* pa = (const T*)p.a + y * p.sa;
+  const T* pb = (const T*)p.b + y * p.sb;
+  const float* bias = p.bias ? p.bias + y * p.sbias : nullptr;
+
+  const int tiles_m = (p.M + BM - 1) / BM, tiles_n = (p.N + BN - 1) / BN;
+  const int nwg = tiles_m * tiles_n;
+  int bid = blockIdx.x;
+  if (bid >= nwg) return;
+  if (nwg >= 8) {  // XCD-aware bijective remap: consecutive tiles share an XCD's L2
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  }
+  const int band = 8;
+  const int group = bid / (band * tiles_n);
+  const int first_m = group * band;
+  const int gm = min(tiles_m - first_m, band);
+  const int tm = first_m + (bid % (band * tiles_n)) % gm;
+  const int tn = (bid % (band * tiles_n)) / gm;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int kbeg = blockIdx.z * p.k_per_split;
+  const int kend = min(p.K, kbeg + p.k_per_split);
+  if (p.out_mode == O_F32_ATOMIC && kbeg >= kend) return;
+  const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+
+  Ld<T, BM, AM> la;
+  Ld<T, BN, BMODE> lb;
+  la.init(p, pa, p.lda, m0, p.M, p.vec_a);
+  lb.init(p, pb, p.ldb, n0, p.N, p.vec_b);
+
+  const int l = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int g4 = l >> 4;
+  auto compute = [&](const T* sa_) {
+    const T* sb_ = sa_ + A_EL;
+    if constexpr (sizeof(T) == 4) {
+#pragma unroll
+      for (int c = 0; c < BK / 16; ++c) {
+        float4 fa[TM], fb[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) fa[i] = *(const float4*)(sa_ + (wm * WTM + 16 * i + (l & 15)) * LD + 16 * c + 4 * g4);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) fb[j] = *(const float4*)(sb_ + (wn * WTN + 16 * j + (l & 15)) * LD + 16 * c + 4 * g4);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fb[j].x, fa[i].x, acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fb[j].y, fa[i].y, acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fb[j].z, fa[i].z, acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fb[j].w, fa[i].w, acc[i][j], 0, 0, 0);
+          }
+      }
+    } else {
+      bf16x8 fa[TM], fb[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) fa[i] = *(const bf16x8*)(sa_ + (wm * WTM + 16 * i + (l & 15)) * LD + 8 * g4);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) fb[j] = *(const bf16x8*)(sb_ + (wn * WTN + 16 * j + (l & 15)) * LD + 8 * g4);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  if (nk > 0) {
+    la.load(p.g, kbeg, kend);
+    lb.load(p.g, kbeg, kend);
+    la.store(lds);
+    lb.store(lds + A_EL);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      const bool more = kt + 1 < nk;
+      if (more) {  // next tile's global loads in flight during this tile's MFMAs
+        la.load(p.g, kbeg + (kt + 1) * BK, kend);
+        lb.load(p.g, kbeg + (kt + 1) * BK, kend);
+      }
+      compute(lds + cur * STAGE_EL);
+      if (more) {
+        T* nx = lds + (cur ^ 1) * STAGE_EL;
+        la.store(nx);
+        lb.store(nx + A_EL);
+      }
+      __syncthreads();
+    }
+  }
+
+  // Epilogue: acc[i][j][r] = C[m = .. + (l & 15)][n = .. + 4 (l >> 4) + r]
+  char* pc = (char*)p.c + y * p.sc * (p.out_mode == O_BF16 ? 2 : 4);
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int m = m0 + wm * WTM + 16 * i + (l & 15);
+    if (m >= p.M) continue;
+    const int64_t rowoff = (int64_t)m * p.ldc;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + wn * WTN + 16 * j + 4 * g4;
+      if (n >= p.N) continue;
+      const bool full = n + 3 < p.N;
+      float v[4] = {acc[i][j][0] * p.alpha, acc[i][j][1] * p.alpha, acc[i][j][2] * p.alpha,
+                    acc[i][j][3] * p.alpha};
+      if (p.out_mode == O_F32_ATOMIC) {
+        float* c = (float*)pc + rowoff + n;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (full || n + r < p.N) atomicAdd(c + r, v[r]);
+        continue;
+      }
+      if (bias) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] += (full || n + r < p.N) ? bias[n + r] : 0.f;
+      }
+      if (p.out_mode == O_F32) {
+        float* c = (float*)pc + rowoff + n;
+        const bool vst = full && ((p.ldc & 3) == 0) && (((uintptr_t)c & 15) == 0);
+        if (p.beta != 0.f) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (full || n + r < p.N) v[r] += p.beta * c[r];
+        }
+        if (p.relu) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+        }
+        if (vst) *(float4*)c = make_float4(v[0], v[1], v[2], v[3]);
+        else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (n + r < p.N) c[r] = v[r];
+        }
+      } else {
+        bf16* c = (bf16*)pc + rowoff + n;
+        const bool vst = full && ((p.ldc & 3) == 0) && (((uintptr_t)c & 7) == 0);
+        if (p.beta != 0.f) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (full || n + r < p.N) v[r] += p.beta * (float)c[r];
+        }
+        if (p.relu) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+        }
+        if (vst) {
+          bf16x4 o;
+          o[0] = (bf16)v[0]; o[1] = (bf16)v[1]; o[2] = (bf16)v[2]; o[3] = (bf16)v[3];
+          *(bf16x4*)c = o;
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (n + r < p.N) c[r] = (bf16)v[r];
+        }
+      }
+    }
+  }
+}
+
+template <typename T, int BM, int BN, int AM, int BMODE>
+static void launch_t(const Args& p, int batch, int splits, hipStream_t s) {
+  const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
+  constexpr int lds = 2 * (BM + BN) * ld_of<T>() * (int)sizeof(T);
+  auto* kern = ggemm_k<T, BM, BN, AM, BMODE>;
+  if constexpr (lds > 65536) {
+    static bool attr = [kern] {
+      return hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
+    }();
+    (void)attr;
+  }
+  hipLaunchKernelGGL(kern, dim3(tiles, batch, splits), dim3(NT), lds, s, p);
+}
+
+static bool big_tile(int M, int N) {
+  const long t128 = (long)((M + 127) / 128) * ((N + 127) / 128);
+  return M >= 128 && N >= 128 && t128 >= 192;
+}
+
+template <typename T, int AM, int BMODE>
+static void launch(const Args& p, int batch, int splits, hipStream_t s) {
+  if (big_tile(p.M, p.N)) launch_t<T, 128, 128, AM, BMODE>(p, batch, splits, s);
+  else launch_t<T, 64, 64, AM, BMODE>(p, batch, splits, s);
+}
+
+// split-K count for atomic outputs: fill ~512 workgroups, >= 4 K-tiles each
+static int pick_splits(int M, int N, int K, int batch, int want) {
+  if (want > 0) return want;
+  const int bm = big_tile(M, N) ? 128 : 64;
+  const long tiles = (long)((M + bm - 1) / bm) * ((N + bm - 1) / bm) * (batch > 0 ? batch : 1);
+  const int nkt = (K + BK - 1) / BK;
+  int sp = 1;
+  while (tiles * sp < 512 && sp * 2 * 4 <= nkt && sp < 4096) sp *= 2;
+  return sp;
+}
+
+static inline int kps(int K, int splits) {
+  const int nkt = (K + BK - 1) / BK;
+  return ((nkt + splits - 1) / splits) * BK;
+}
+
+static Geom make_geom(int N, int H, int W, int C, int K, int R, int S, int Ho, int Wo, int sh, int sw, int ph, int pw,
+                      int dh, int dw, int groups) {
+  Geom g{};
+  g.N = N; g.H = H; g.W = W; g.C = C; g.K = K; g.R = R; g.S = S; g.Ho = Ho; g.Wo = Wo;
+  g.Cg = C / groups; g.Kg = K / groups;
+  g.sh = sh; g.sw = sw; g.ph = ph; g.pw = pw; g.dh = dh; g.dw = dw;
+  g.dCg = FastDiv(g.Cg > 0 ? g.Cg : 1); g.dKg = FastDiv(g.Kg > 0 ? g.Kg : 1); g.dS = FastDiv(S);
+  g.dWo = FastDiv(Wo > 0 ? Wo : 1); g.dHoWo = FastDiv(Ho * Wo > 0 ? Ho * Wo : 1);
+  g.dW = FastDiv(W > 0 ? W : 1); g.dHW = FastDiv(H * W > 0 ? H * W : 1);
+  g.dsh = FastDiv(sh); g.dsw = FastDiv(sw);
+  return g;
+}
+
+static void check_int(int64_t v, const char* what) {
+  if (v >= ((int64_t)1 << 31)) throw std::runtime_error(std::string("ggemm: ") + what + " exceeds 2^31");
+}
+
+template <typename T>
+static bool aligned(const void* p, int64_t a, int64_t b = 0, int64_t c = 0) {
+  return ((uintptr_t)p % (4 * sizeof(T))) == 0 && a % 4 == 0 && b % 4 == 0 && c % 4 == 0;
+}
+
+}  // namespace gg
+}  // namespace sg
+
+using namespace sg::gg;
+
+extern "C" {
+
+// Generic GEMM (dt 0: fp32 operands, 1: bf16 operands):
+//   C[batch][M][N] = alpha * A(m, k) B(n, k) (+ beta C) (+ bias[n]) (ReLU)
+//   a_kouter = 0: A stored [M][K] (lda), 1: [K][M]; b_kouter = 0: B stored [N][K], 1: [K][N]
+//   out_mode 0 bf16, 1 fp32, 2 fp32 atomic (split-K, C pre-initialised)
+void sg_ggemm(int dt, const void* a, int64_t lda, int a_kouter, int64_t sa, const void* b, int64_t ldb, int b_kouter,
+              int64_t sb, void* c, int64_t ldc, int64_t sc, int M, int N, int K, float alpha, float beta,
+              const void* bias, int relu, int out_mode, int splits, int batch, hipStream_t s) {
+  if (M <= 0 || N <= 0 || batch <= 0) return;
+  check_int((int64_t)M * N, "M*N");
+  Args p{};
+  p.M = M; p.N = N; p.K = K;
+  p.a = a; p.lda = lda; p.sa = sa; p.b = b; p.ldb = ldb; p.sb = sb;
+  p.c = c; p.ldc = ldc; p.sc = sc; p.alpha = alpha; p.beta = beta; p.bias = (const float*)bias; p.sbias = 0;
+  p.relu = relu; p.out_mode = out_mode;
+  splits = out_mode == O_F32_ATOMIC ? pick_splits(M, N, K, batch, splits) : 1;
+  p.k_per_split = kps(K > 0 ? K : 1, splits);
+  p.g = make_geom(1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0, 0, 1, 1, 1);
+  const bool f = dt == 0;
+  p.vec_a = f ? aligned<float>(a, lda, sa, a_kouter ? M : K) : aligned<sg::bf16>(a, lda, sa, a_kouter ? M : K);
+  p.vec_b = f ? aligned<float>(b, ldb, sb, b_kouter ? N : K) : aligned<sg::bf16>(b, ldb, sb, b_kouter ? N : K);
+#define GO(T)                                                                         \
+  {                                                                                   \
+    if (!a_kouter && !b_kouter) launch<T, KMAJ, KMAJ>(p, batch, splits, s);           \
+    else if (!a_kouter && b_kouter) launch<T, KMAJ, KOUT>(p, batch, splits, s);       \
+    else if (a_kouter && !b_kouter) launch<T, KOUT, KMAJ>(p, batch, splits, s);       \
+    else launch<T, KOUT, KOUT>(p, batch, splits, s);                                  \
+  }
+  if (f) GO(float) else GO(sg::bf16)
+#undef GO
+}
+
+// Convolution forward, NHWC activations, weights [K][R][S][C/groups]:
+//   y[N*Ho*Wo][K] = conv(x, w) (+ bias) (ReLU); out_mode 0 bf16 / 1 fp32
+void sg_gconv_fwd(int dt, const void* x, const void* w, void* y, const void* bias, int N, int H, int W, int C, int K,
+                  int R, int S, int Ho, int Wo, int sh, int sw, int ph, int pw, int dh, int dw, int groups, int relu,
+                  int out_mode, hipStream_t s) {
+  Args p{};
+  p.g = make_geom(N, H, W, C, K, R, S, Ho, Wo, sh, sw, ph, pw, dh, dw, groups);
+  const Geom& g = p.g;
+  check_int((int64_t)N * H * W * C, "input");
+  check_int((int64_t)N * Ho * Wo * K, "output");
+  p.M = N * Ho * Wo; p.N = g.Kg; p.K = R * S * g.Cg;
+  p.a = x; p.lda = 0; p.sa = g.Cg;  // group g reads channels [g*Cg, (g+1)*Cg)
+  p.b = w; p.ldb = (int64_t)R * S * g.Cg; p.sb = (int64_t)g.Kg * R * S * g.Cg;
+  p.c = y; p.ldc = K; p.sc = g.Kg;
+  p.alpha = 1.f; p.beta = 0.f; p.bias = (const float*)bias; p.sbias = g.Kg; p.relu = relu; p.out_mode = out_mode;
+  p.k_per_split = kps(p.K > 0 ? p.K : 1, 1);
+  const bool f = dt == 0;
+  p.vec_a = (f ? aligned<float>(x, C, g.Cg) : aligned<sg::bf16>(x, C, g.Cg)) ? 1 : 0;
+  p.vec_b = (f ? aligned<float>(w, p.ldb, p.sb, p.K) : aligned<sg::bf16>(w, p.ldb, p.sb, p.K)) ? 1 : 0;
+  if (f) launch<float, CFWD_A, KMAJ>(p, groups, 1, s);
+  else launch<sg::bf16, CFWD_A, KMAJ>(p, groups, 1, s);
+}
+
+// Convolution data gradient: dx[N*H*W][C] (= | += beta *) dgrad(dy[N*Ho*Wo][K], w)
+void sg_gconv_dgrad(int dt, const void* dy, const void* w, void* dx, int N, int H, int W, int C, int K, int R, int S,
+                    int Ho, int Wo, int sh, int sw, int ph, int pw, int dh, int dw, int groups, int out_mode,
+                    float beta, hipStream_t s) {
+  Args p{};
+  p.g = make_geom(N, H, W, C, K, R, S, Ho, Wo, sh, sw, ph, pw, dh, dw, groups);
+  const Geom& g = p.g;
+  check_int((int64_t)N * H * W * C, "input");
+  check_int((int64_t)N * Ho * Wo * K, "output");
+  p.M = N * H * W; p.N = g.Cg; p.K = R * S * g.Kg;
+  p.a = dy; p.lda = 0; p.sa = g.Kg;
+  p.b = w; p.ldb = 0; p.sb = (int64_t)g.Kg * R * S * g.Cg;
+  p.c = dx; p.ldc = C; p.sc = g.Cg;
+  p.alpha = 1.f; p.beta = beta; p.bias = nullptr; p.relu = 0; p.out_mode = out_mode;
+  p.k_per_split = kps(p.K > 0 ? p.K : 1, 1);
+  const bool f = dt == 0;
+  p.vec_a = (f ? aligned<float>(dy, K, g.Kg) : aligned<sg::bf16>(dy, K, g.Kg)) ? 1 : 0;
+  p.vec_b = (f ? aligned<float>(w, g.Cg, p.sb) : aligned<sg::bf16>(w, g.Cg, p.sb)) ? 1 : 0;
+  if (f) launch<float, DGRAD_A, DGRAD_B>(p, groups, 1, s);
+  else launch<sg::bf16, DGRAD_A, DGRAD_B>(p, groups, 1, s);
+}
+
+// Convolution weight gradient: dw[K][R][S][C/groups] (fp32) += dy^T im2col(x)
+// (split over the pixel reduction with fp32 atomics; the caller zeroes dw
+// unless accumulating)
+void sg_gconv_wgrad(int dt, const void* x, const void* dy, void* dw_out, int N, int H, int W, int C, int K, int R,
+                    int S, int Ho, int Wo, int sh, int sw, int ph, int pw, int dh, int dw, int groups, int splits,
+                    hipStream_t s) {
+  Args p{};
+  p.g = make_geom(N, H, W, C, K, R, S, Ho, Wo, sh, sw, ph, pw, dh, dw, groups);
+  const Geom& g = p.g;
+  check_int((int64_t)N * H * W * C, "input");
+  check_int((int64_t)N * Ho * Wo * K, "output");
+  p.M = g.Kg; p.N = R * S * g.Cg; p.K = N * Ho * Wo;
+  p.a = dy; p.lda = K; p.sa = g.Kg;  // A(row = ko, k = pixel) = dy[pixel][g*Kg + ko]: K-outer
+  p.b = x; p.ldb = 0; p.sb = g.Cg;
+  p.c = dw_out; p.ldc = (int64_t)R * S * g.Cg; p.sc = (int64_t)g.Kg * R * S * g.Cg;
+  p.alpha = 1.f; p.beta = 0.f; p.bias = nullptr; p.relu = 0; p.out_mode = O_F32_ATOMIC;
+  splits = pick_splits(p.M, p.N, p.K, groups, splits);
+  p.k_per_split = kps(p.K > 0 ? p.K : 1, splits);
+  const bool f = dt == 0;
+  p.vec_a = (f ? aligned<float>(dy, K, g.Kg, p.M) : aligned<sg::bf16>(dy, K, g.Kg, p.M)) ? 1 : 0;
+  p.vec_b = (f ? aligned<float>(x, C, g.Cg) : aligned<sg::bf16>(x, C, g.Cg)) ? 1 : 0;
+  if (f) launch<float, KOUT, WGRAD_B>(p, groups, splits, s);
+  else launch<sg::bf16, KOUT, WGRAD_B>(p, groups, splits, s);
+}
+
+}  // extern "C"

@@ -1,19 +1,18 @@
 """Device-dispatching functional ops on raw ``torch.Tensor`` storage.
 
-Every hot op has two implementations:
+Every op has two implementations:
 
 * GPU (``tensor.is_cuda``): a hand-written gfx950 HIP kernel from
   ``singa_amd/csrc/kernels`` launched on the current HIP stream.  Activation
   tensors of 4-D ops are NHWC in memory (``torch.channels_last``) while the
-  logical shape stays NCHW as in SINGA's API.  Convolutions always run the
-  bf16 MFMA implicit-GEMM kernel with fp32 accumulation (fp32 tensors are cast
-  on entry, like TF32 mode on other hardware).
+  logical shape stays NCHW as in SINGA's API.  bf16 convolutions / GEMMs of
+  aligned shapes run the tuned MFMA kernels (igemm.hip); fp32 operands run
+  the exact-f32 MFMA kernels (ggemm.hip) -- no silent downcast -- as do
+  ragged bf16 shapes, grouped and dilated convolutions.  A GPU case without a
+  native kernel RAISES (``_no_native``); nothing falls back to PyTorch /
+  hipBLAS / MIOpen on the device.
 * CPU: a plain PyTorch fp32/bf16 reference, which doubles as the numerics
   oracle for the kernel tests (the reference framework's CppCPU device).
-
-Plain GEMMs whose dimensions are not multiples of 8 go to hipBLAS through
-``torch.matmul`` (the "plain library GEMM" path); everything else uses the MFMA
-kernel.
 """
 from __future__ import annotations
 
@@ -25,12 +24,15 @@ import numpy as np
 import torch
 import torch.nn.functional as F
 
+from . import glue as G
 from . import native as N
 
 # unary op codes (csrc/kernels/elementwise.hip)
 UNARY = {"relu": 0, "sigmoid": 1, "tanh": 2, "stanh": 3, "gelu": 4, "identity": 5, "softplus": 6, "square": 7,
          "abs": 8, "exp": 9, "leakyrelu": 10, "elu": 11, "selu": 12, "gelu_tanh": 13, "sqrt": 14, "neg": 15,
-         "reciprocal": 16, "log": 17, "sign": 18}
+         "reciprocal": 16, "log": 17, "sign": 18, "erf": 19, "cos": 20, "sin": 21, "tan": 22, "cosh": 23,
+         "sinh": 24, "acos": 25, "asin": 26, "atan": 27, "acosh": 28, "asinh": 29, "atanh": 30, "ceil": 31,
+         "floor": 32, "round": 33, "softsign": 34, "scale": 35, "adds": 36, "rsqrt": 37, "pows": 38}
 
 _CPU_UNARY = {
     "relu": torch.relu, "sigmoid": torch.sigmoid, "tanh": torch.tanh,
@@ -38,7 +40,10 @@ _CPU_UNARY = {
     "gelu": lambda x: F.gelu(x), "gelu_tanh": lambda x: F.gelu(x, approximate="tanh"),
     "identity": lambda x: x.clone(), "softplus": F.softplus, "square": torch.square, "abs": torch.abs,
     "exp": torch.exp, "sqrt": torch.sqrt, "neg": torch.neg, "reciprocal": torch.reciprocal, "log": torch.log,
-    "sign": torch.sign,
+    "sign": torch.sign, "erf": torch.erf, "cos": torch.cos, "sin": torch.sin, "tan": torch.tan, "cosh": torch.cosh,
+    "sinh": torch.sinh, "acos": torch.acos, "asin": torch.asin, "atan": torch.atan, "acosh": torch.acosh,
+    "asinh": torch.asinh, "atanh": torch.atanh, "ceil": torch.ceil, "floor": torch.floor, "round": torch.round,
+    "softsign": lambda x: x / (1 + x.abs()), "rsqrt": torch.rsqrt,
 }
 
 
@@ -73,37 +78,44 @@ def _like(t: torch.Tensor, dtype=None) -> torch.Tensor:
 
 
 def _zeros_cl(shape, dtype, device) -> torch.Tensor:
-    return torch.empty(shape, dtype=dtype, device=device, memory_format=torch.channels_last).zero_()
+    return G.zeros(shape, dtype, device, torch.channels_last)
 
 
 def _dense(t: torch.Tensor) -> torch.Tensor:
-    return t if (t.is_contiguous() or N.is_cl(t)) else t.contiguous()
+    return G.dense(t)
 
 
 # ----------------------------------------------------------------------------
 # elementwise
 # ----------------------------------------------------------------------------
 def unary(op: str, x: torch.Tensor, alpha: float = 0.0) -> torch.Tensor:
-    if _native_ok(x) and _flat_ok(x) and op in UNARY:
-        x = _dense(x)
+    if _native_ok(x) and x.dtype in (torch.float32, torch.bfloat16) and op in UNARY:
+        x = G.dense(x)
         y = _like(x)
         N.lib().unary_fwd(UNARY[op], x.data_ptr(), y.data_ptr(), x.numel(), N.dt(x), alpha, N.stream())
         return y
+    _no_native(f"unary {op}", x)
     if op == "leakyrelu":
         return F.leaky_relu(x, alpha)
     if op == "elu":
         return F.elu(x, alpha)
     if op == "selu":
         return F.selu(x)
+    if op == "scale":
+        return x * alpha
+    if op == "adds":
+        return x + alpha
+    if op == "pows":
+        return torch.pow(x, alpha)
     return _CPU_UNARY[op](x)
 
 
 def unary_bwd(op: str, x: Optional[torch.Tensor], y: Optional[torch.Tensor], dy: torch.Tensor,
               alpha: float = 0.0) -> torch.Tensor:
-    if _native_ok(dy) and _flat_ok(dy) and op in UNARY:
-        dy = _dense(dy)
-        xx = _dense(x) if x is not None else None
-        yy = _dense(y) if y is not None else None
+    if _native_ok(dy) and dy.dtype in (torch.float32, torch.bfloat16) and op in UNARY:
+        dy = G.dense(dy)
+        xx = G.dense(x) if x is not None else None
+        yy = G.dense(y) if y is not None else None
         for t in (xx, yy):
             if t is not None and not _same_layout(t, dy):
                 raise ValueError("unary_bwd: layout mismatch")
@@ -111,6 +123,7 @@ def unary_bwd(op: str, x: Optional[torch.Tensor], y: Optional[torch.Tensor], dy:
         N.lib().unary_bwd(UNARY[op], N.ptr(xx), N.ptr(yy), dy.data_ptr(), dx.data_ptr(), dy.numel(), N.dt(dy),
                           alpha, N.stream())
         return dx
+    _no_native(f"unary_bwd {op}", dy)
     xf = x.float() if x is not None else None
     yf = y.float() if y is not None else None
     g = dy.float()
@@ -127,7 +140,7 @@ def unary_bwd(op: str, x: Optional[torch.Tensor], y: Optional[torch.Tensor], dy:
             xx = xf.detach().requires_grad_(True)
             out = F.gelu(xx, approximate="tanh" if op == "gelu_tanh" else "none")
             (r,) = torch.autograd.grad(out, xx, g)
-    elif op == "identity":
+    elif op in ("identity", "adds"):
         r = g
     elif op == "softplus":
         r = g * torch.sigmoid(xf)
@@ -152,8 +165,40 @@ def unary_bwd(op: str, x: Optional[torch.Tensor], y: Optional[torch.Tensor], dy:
         r = -g * yf * yf
     elif op == "log":
         r = g / xf
-    elif op == "sign":
+    elif op in ("sign", "ceil", "floor", "round"):
         r = torch.zeros_like(g)
+    elif op == "erf":
+        r = g * 1.1283791671 * torch.exp(-xf * xf)
+    elif op == "cos":
+        r = -g * torch.sin(xf)
+    elif op == "sin":
+        r = g * torch.cos(xf)
+    elif op == "tan":
+        r = g * (1 + yf * yf)
+    elif op == "cosh":
+        r = g * torch.sinh(xf)
+    elif op == "sinh":
+        r = g * torch.cosh(xf)
+    elif op == "acos":
+        r = -g * torch.rsqrt(1 - xf * xf)
+    elif op == "asin":
+        r = g * torch.rsqrt(1 - xf * xf)
+    elif op == "atan":
+        r = g / (1 + xf * xf)
+    elif op == "acosh":
+        r = g * torch.rsqrt(xf * xf - 1)
+    elif op == "asinh":
+        r = g * torch.rsqrt(xf * xf + 1)
+    elif op == "atanh":
+        r = g / (1 - xf * xf)
+    elif op == "softsign":
+        r = g / (1 + xf.abs()) ** 2
+    elif op == "scale":
+        r = g * alpha
+    elif op == "rsqrt":
+        r = -0.5 * g * yf ** 3
+    elif op == "pows":
+        r = g * alpha * torch.pow(xf, alpha - 1)
     else:
         raise KeyError(op)
     return r.to(dy.dtype)
@@ -187,7 +232,7 @@ def cast(x: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
         y = _like(x, dtype)
         N.lib().cast(x.data_ptr(), N.dt(x), y.data_ptr(), N.dt(y), x.numel(), N.stream())
         return y
-    return x.to(dtype)
+    return G.to(x, dtype)
 
 
 def dropout_fwd(x: torch.Tensor, ratio: float, seed: int, offset: int,
@@ -195,13 +240,14 @@ def dropout_fwd(x: torch.Tensor, ratio: float, seed: int, offset: int,
     """``epoch``: optional device int64 step counter mixed into the Philox key
     (keeps masks fresh across HIP-graph replays)."""
     pkeep = 1.0 - ratio
-    if _native_ok(x) and _flat_ok(x):
+    if _native_ok(x) and x.dtype in (torch.float32, torch.bfloat16):
         x = _dense(x)
         y = _like(x)
         mask = _like(x, torch.uint8)
         N.lib().dropout_fwd(x.data_ptr(), y.data_ptr(), mask.data_ptr(), x.numel(), N.dt(x), pkeep, seed, offset,
                             N.ptr(epoch), N.stream())
         return y, mask
+    _no_native("dropout_fwd", x)
     g = torch.Generator(device=x.device).manual_seed(int(seed + offset) & 0x7FFFFFFFFFFFFFFF)
     mask = (torch.rand(x.shape, generator=g, device=x.device) < pkeep).to(torch.uint8)
     return x * mask.to(x.dtype) / pkeep, mask
@@ -209,11 +255,14 @@ def dropout_fwd(x: torch.Tensor, ratio: float, seed: int, offset: int,
 
 def dropout_bwd(dy: torch.Tensor, mask: torch.Tensor, ratio: float) -> torch.Tensor:
     pkeep = 1.0 - ratio
-    if _native_ok(dy) and _flat_ok(dy) and _same_layout(_dense(dy), mask):
+    if _native_ok(dy) and dy.dtype in (torch.float32, torch.bfloat16):
         dy = _dense(dy)
+        if not _same_layout(dy, mask):
+            dy = G.contiguous(dy, torch.channels_last if N.is_cl(mask) and mask.dim() == 4 else torch.contiguous_format)
         dx = _like(dy)
         N.lib().dropout_bwd(dy.data_ptr(), mask.data_ptr(), dx.data_ptr(), dy.numel(), N.dt(dy), pkeep, N.stream())
         return dx
+    _no_native("dropout_bwd", dy)
     return dy * mask.to(dy.dtype) / pkeep
 
 
@@ -225,31 +274,39 @@ def softmax(x: torch.Tensor, axis: int = -1, out_dtype: Optional[torch.dtype] = 
     lets fp32 scores come out as bf16 probabilities in the same pass."""
     axis = axis % x.dim()
     od = out_dtype or x.dtype
-    if (_native_ok(x) and _flat_ok(x) and axis == x.dim() - 1 and x.is_contiguous() and x.shape[-1] <= 1024
-            and od in (torch.float32, torch.bfloat16)):
-        C = x.shape[-1]  # short rows: one wave per row
-        y = torch.empty(x.shape, dtype=od, device=x.device)
-        N.lib().softmax_rows(x.data_ptr(), y.data_ptr(), x.numel() // C, C, N.dt(x), N.dt(y), N.stream())
-        return y
-    if od != x.dtype:
-        return softmax(x, axis).to(od)
-    if _native_ok(x) and _flat_ok(x) and axis == x.dim() - 1 and x.is_contiguous() and x.shape[-1] <= 16384:
+    if _native_ok(x) and x.dtype in (torch.float32, torch.bfloat16) and od in (torch.float32, torch.bfloat16):
+        if axis != x.dim() - 1:  # softmax over a middle axis: move it last (native copies)
+            y = softmax(G.contiguous(x.movedim(axis, -1)), -1, od)
+            return G.contiguous(y.movedim(-1, axis))
+        x = G.contiguous(x)
         C = x.shape[-1]
+        if C <= 1024:  # short rows: one wave per row
+            y = torch.empty(x.shape, dtype=od, device=x.device)
+            N.lib().softmax_rows(x.data_ptr(), y.data_ptr(), x.numel() // C, C, N.dt(x), N.dt(y), N.stream())
+            return y
+        if C > 16384:
+            raise NotImplementedError(f"softmax: rows longer than 16384 ({C})")
         y = torch.empty_like(x)
         N.lib().softmax_fwd(x.data_ptr(), y.data_ptr(), x.numel() // C, C, N.dt(x), int(x.dtype == torch.float32),
                             N.stream())
-        return y
-    return torch.softmax(x.float(), dim=axis).to(x.dtype)
+        return y if od == x.dtype else cast(y, od)
+    _no_native("softmax", x)
+    return torch.softmax(x.float(), dim=axis).to(od)
 
 
 def softmax_bwd(y: torch.Tensor, dy: torch.Tensor, axis: int = -1) -> torch.Tensor:
     axis = axis % y.dim()
-    if (_native_ok(y, dy) and _flat_ok(y) and axis == y.dim() - 1 and y.is_contiguous() and dy.is_contiguous()
-            and y.dtype == dy.dtype):
+    if _native_ok(y, dy) and y.dtype in (torch.float32, torch.bfloat16):
+        if axis != y.dim() - 1:
+            g = softmax_bwd(G.contiguous(y.movedim(axis, -1)), G.contiguous(dy.movedim(axis, -1)), -1)
+            return G.contiguous(g.movedim(-1, axis))
+        y = G.contiguous(y)
+        dy = G.contiguous(G.to(dy, y.dtype))
         C = y.shape[-1]
         dx = torch.empty_like(dy)
         N.lib().softmax_bwd(y.data_ptr(), dy.data_ptr(), dx.data_ptr(), y.numel() // C, C, N.dt(y), N.stream())
         return dx
+    _no_native("softmax_bwd", y, dy)
     yf, gf = y.float(), dy.float()
     return (yf * (gf - (gf * yf).sum(dim=axis, keepdim=True))).to(dy.dtype)
 
@@ -263,19 +320,21 @@ def softmax_xent(x: torch.Tensor, target: torch.Tensor, topk: int = 1, grad_scal
     B, C = x2.shape
     gs = (1.0 / B) if grad_scale is None else grad_scale
     soft = target.dim() > 1 and target.shape[-1] == C and target.is_floating_point()
-    if _native_ok(x) and _flat_ok(x2) and x2.is_contiguous() and C <= 16384:
+    if _native_ok(x) and x2.dtype in (torch.float32, torch.bfloat16) and C <= 16384:
+        x2 = G.contiguous(x2)
         loss = torch.empty(B, dtype=torch.float32, device=x.device)
         correct = torch.empty(B, dtype=torch.float32, device=x.device)
         dx = torch.empty_like(x2) if need_grad else None
         if soft:
-            t = target.reshape(B, C).float().contiguous()
+            t = G.contiguous(G.to(G.reshape(target, (B, C)), torch.float32))
             lab = None
         else:
-            lab = target.reshape(B).to(torch.int32).contiguous()
+            lab = G.contiguous(G.to(G.reshape(target, (B,)), torch.int32))
             t = None
         N.lib().softmax_xent(x2.data_ptr(), N.ptr(lab), N.ptr(t), loss.data_ptr(), correct.data_ptr(), N.ptr(dx), B,
                              C, N.dt(x2), topk, gs, N.stream())
         return loss, correct, (dx.reshape(x.shape) if dx is not None else None)
+    _no_native("softmax_xent", x)
     xf = x2.float()
     lse = torch.logsumexp(xf, dim=1)
     if soft:
@@ -300,16 +359,18 @@ def softmax_xent(x: torch.Tensor, target: torch.Tensor, topk: int = 1, grad_scal
 
 def layernorm_fwd(x: torch.Tensor, g: Optional[torch.Tensor], b: Optional[torch.Tensor], eps: float = 1e-5):
     D = x.shape[-1]
-    if _native_ok(x) and _flat_ok(x) and x.is_contiguous():
+    if _native_ok(x) and x.dtype in (torch.float32, torch.bfloat16):
+        x = G.contiguous(x)
         R = x.numel() // D
         y = torch.empty_like(x)
         mean = torch.empty(R, dtype=torch.float32, device=x.device)
         rstd = torch.empty(R, dtype=torch.float32, device=x.device)
-        gg = g.float().contiguous() if g is not None else None
-        bb = b.float().contiguous() if b is not None else None
+        gg = G.contiguous(G.to(g, torch.float32)) if g is not None else None
+        bb = G.contiguous(G.to(b, torch.float32)) if b is not None else None
         N.lib().layernorm_fwd(x.data_ptr(), N.ptr(gg), N.ptr(bb), y.data_ptr(), mean.data_ptr(), rstd.data_ptr(), R,
                               D, N.dt(x), eps, N.stream())
         return y, mean, rstd
+    _no_native("layernorm_fwd", x)
     xf = x.float().reshape(-1, D)
     mean = xf.mean(1)
     rstd = torch.rsqrt(xf.var(1, unbiased=False) + eps)
@@ -331,16 +392,19 @@ def layernorm_bwd(x, dy, g, mean, rstd, dg_acc=None, db_acc=None):
     def _acc_ok(t):
         return t is not None and t.dtype == torch.float32 and t.is_contiguous() and t.numel() == D and t.is_cuda
 
-    if _native_ok(x, dy) and _flat_ok(x) and x.is_contiguous() and dy.is_contiguous():
+    if _native_ok(x, dy) and x.dtype in (torch.float32, torch.bfloat16):
+        x = G.contiguous(x)
+        dy = G.contiguous(G.to(dy, x.dtype))
         dx = torch.empty_like(x)
         dg = db = None
         if g is not None:
-            dg = dg_acc if _acc_ok(dg_acc) else torch.zeros(D, dtype=torch.float32, device=x.device)
-            db = db_acc if _acc_ok(db_acc) else torch.zeros(D, dtype=torch.float32, device=x.device)
-        gg = g.float().contiguous() if g is not None else None
+            dg = dg_acc if _acc_ok(dg_acc) else G.zeros((D,), torch.float32, x.device)
+            db = db_acc if _acc_ok(db_acc) else G.zeros((D,), torch.float32, x.device)
+        gg = G.contiguous(G.to(g, torch.float32)) if g is not None else None
         N.lib().layernorm_bwd(x.data_ptr(), dy.data_ptr(), N.ptr(gg), mean.data_ptr(), rstd.data_ptr(),
                               dx.data_ptr(), N.ptr(dg), N.ptr(db), R, D, N.dt(x), N.stream())
         return dx, dg, db
+    _no_native("layernorm_bwd", x, dy)
     xf = x.float().reshape(R, D)
     gy = dy.float().reshape(R, D)
     xh = (xf - mean[:, None]) * rstd[:, None]
@@ -360,74 +424,150 @@ def layernorm_bwd(x, dy, g, mean, rstd, dg_acc=None, db_acc=None):
 # ----------------------------------------------------------------------------
 # GEMM
 # ----------------------------------------------------------------------------
-def _gemm_native_ok(*dims) -> bool:
-    return all(d % 8 == 0 for d in dims)
+def _no_native(what: str, *ts) -> None:
+    """GPU operands must run on a hand-written kernel: raise instead of
+    silently handing a device tensor to a PyTorch/vendor kernel.
+    (SINGA_AMD_NATIVE=0 -- debug only -- re-enables the PyTorch path.)"""
+    if N.force_native() and any(t is not None and t.is_cuda for t in ts):
+        raise NotImplementedError(f"{what}: no native gfx950 kernel for this case "
+                                  f"({[(tuple(t.shape), t.dtype) for t in ts if t is not None]})")
+
+
+def _mat(t: torch.Tensor, trans: bool):
+    """View a 2-D operand (or the last two dims of a 3-D one) as (tensor, ld,
+    k_outer) where the logical op(t) is [rows][K]: dense row-major, or
+    column-major (a transposed view) taken as is; other strides are copied."""
+    r, c = t.shape[-2], t.shape[-1]
+    s0, s1 = t.stride(-2), t.stride(-1)
+    if (s1 == 1 or c == 1) and (r == 1 or s0 >= c):  # row-major: t[i][j] at i*ld + j
+        return t, (s0 if r > 1 else max(c, 1)), bool(trans)
+    if (s0 == 1 or r == 1) and (c == 1 or s1 >= r):  # column-major: t[i][j] at j*ld + i
+        return t, (s1 if c > 1 else max(r, 1)), not trans
+    t = t.contiguous()
+    return t, max(c, 1), bool(trans)
+
+
+def _igemm_ok(a, lda, ako, b, ldb, bko, M, Nn, K, sa, sb) -> bool:
+    """The tuned bf16 kernel (igemm.hip: 16-byte LDS-DMA chunks of 8
+    elements) takes the problem: K-major operands need K % 8, K-outer ones
+    rows % 8, every leading dimension / batch stride % 8, 16-byte bases."""
+    if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16:
+        return False
+    for t, ld, ko, rows, st in ((a, lda, ako, M, sa), (b, ldb, bko, Nn, sb)):
+        if ld % 8 or st % 8 or t.data_ptr() % 16:
+            return False
+        if (ko and rows % 8) or (not ko and K % 8):
+            return False
+        if t.numel() * 2 >= (1 << 31):
+            return False
+    return True
+
+
+def gemm(a: torch.Tensor, b: torch.Tensor, ta: bool = False, tb: bool = False, out: Optional[torch.Tensor] = None,
+         out_dtype: Optional[torch.dtype] = None, alpha: float = 1.0, beta: float = 0.0,
+         bias: Optional[torch.Tensor] = None, relu: bool = False, accumulate: bool = False) -> torch.Tensor:
+    """C = alpha * op(a) @ op(b) (+ beta * C) (+ bias[n]) (ReLU), op(t) = t.T if
+    the flag is set.  2-D or batched 3-D operands (equal batch, or one side
+    2-D and shared).  ``accumulate``: C (fp32 ``out``) += alpha * op(a) op(b)
+    (split-K atomics).  On the GPU: bf16 operands of aligned shapes run the
+    tuned MFMA kernel, everything else (fp32 -- exact f32 MFMA -- and ragged
+    bf16) the generic one; there is no vendor-BLAS path."""
+    if a.dim() == 2 and b.dim() == 2:
+        batch = 1
+    elif a.dim() == 3 and b.dim() == 2 and not ta and a.is_contiguous() and out is None:
+        Bt = a.shape[0]
+        c = gemm(a.reshape(-1, a.shape[-1]), b, False, tb, None, out_dtype, alpha, beta, bias, relu)
+        return c.reshape(Bt, a.shape[1], c.shape[-1])
+    elif a.dim() == 3 or b.dim() == 3:
+        batch = a.shape[0] if a.dim() == 3 else b.shape[0]
+        if (a.dim() == 3 and a.shape[0] != batch) or (b.dim() == 3 and b.shape[0] != batch):
+            raise ValueError(f"gemm: batch mismatch {tuple(a.shape)} x {tuple(b.shape)}")
+    else:
+        raise ValueError(f"gemm: expected 2-D / 3-D operands, got {tuple(a.shape)} x {tuple(b.shape)}")
+    M, K = (a.shape[-1], a.shape[-2]) if ta else (a.shape[-2], a.shape[-1])
+    Kb, Nn = (b.shape[-1], b.shape[-2]) if tb else (b.shape[-2], b.shape[-1])
+    if K != Kb:
+        raise ValueError(f"gemm: inner dims differ {tuple(a.shape)} x {tuple(b.shape)} (ta={ta}, tb={tb})")
+    lead = (batch,) if batch > 1 or a.dim() == 3 or b.dim() == 3 else ()
+    if out is None:
+        od = out_dtype or (torch.float32 if accumulate else a.dtype)
+        out = (torch.zeros if accumulate else torch.empty)(lead + (M, Nn), dtype=od, device=a.device)
+    if not (_native_ok(a, b) and a.is_cuda):
+        if a.is_cuda:
+            _no_native("gemm", a, b)
+        aa = a.float().transpose(-1, -2) if ta else a.float()
+        bb = b.float().transpose(-1, -2) if tb else b.float()
+        r = alpha * torch.matmul(aa, bb)
+        if accumulate:
+            return out.add_(r.reshape(out.shape))
+        if beta != 0.0:
+            r = r + beta * out.float()
+        if bias is not None:
+            r = r + bias.float()
+        if relu:
+            r = torch.relu(r)
+        out.copy_(r.reshape(out.shape))
+        return out
+    if a.dtype != b.dtype:  # mixed operands: the wider type
+        a, b = cast(a, torch.float32), cast(b, torch.float32)
+    if not out.is_contiguous() or out.dtype not in (torch.float32, torch.bfloat16):
+        raise ValueError("gemm: output must be a dense fp32/bf16 tensor")
+    if accumulate and out.dtype != torch.float32:
+        raise ValueError("gemm: accumulation needs an fp32 output")
+    if M == 0 or Nn == 0:
+        return out
+    a, lda, ako = _mat(a, ta)
+    b, ldb, bko = _mat(b, tb)
+    bko = not bko  # B(n, k) convention of the kernels: k_outer == B stored [K][N]
+    sa = a.stride(0) if a.dim() == 3 else 0
+    sb = b.stride(0) if b.dim() == 3 else 0
+    sc = M * Nn if out.dim() == 3 else 0
+    bb = G.contiguous(G.to(bias, torch.float32)).reshape(-1) if bias is not None else None
+    mode = 2 if accumulate else (0 if out.dtype == torch.bfloat16 else 1)
+    L = N.lib()
+    if _igemm_ok(a, lda, ako, b, ldb, bko, M, Nn, K, sa, sb) and (mode == 2 or sc % 8 == 0) and K > 0:
+        L.gemm(a.data_ptr(), lda, int(ako), b.data_ptr(), ldb, int(bko), out.data_ptr(), Nn, M, Nn, K, alpha, beta,
+               N.ptr(bb), int(relu), mode, 0 if mode == 2 else 1, batch, sa, sb, sc, N.stream())
+        return out
+    if a.dtype not in (torch.float32, torch.bfloat16):
+        _no_native(f"gemm ({a.dtype})", a)
+    L.ggemm(0 if a.dtype == torch.float32 else 1, a.data_ptr(), lda, int(ako), sa, b.data_ptr(), ldb, int(bko), sb,
+            out.data_ptr(), Nn, sc, M, Nn, K, alpha, beta, N.ptr(bb), int(relu), mode, 0, batch, N.stream())
+    return out
 
 
 def matmul(a: torch.Tensor, b: torch.Tensor, out_dtype: Optional[torch.dtype] = None,
            bias: Optional[torch.Tensor] = None, relu: bool = False) -> torch.Tensor:
     """C = a @ b for 2-D (or batched 3-D with equal batch) row-major operands.
-    bf16 operands run on the MFMA kernel with fp32 accumulation."""
-    out_dtype = out_dtype or a.dtype
-    if (_native_ok(a, b) and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and a.dim() in (2, 3)
-            and a.dim() == b.dim() and (a.dim() == 2 or a.shape[0] == b.shape[0])):
-        M, K = a.shape[-2], a.shape[-1]
-        Nn = b.shape[-1]
-        if _gemm_native_ok(K, Nn) and M > 0:
-            a = a.contiguous()
-            b = b.contiguous()
-            batch = a.shape[0] if a.dim() == 3 else 1
-            c = torch.empty(a.shape[:-1] + (Nn,), dtype=out_dtype, device=a.device)
-            bb = bias.float().contiguous() if bias is not None else None
-            # C[m][n] = sum_k A[m][k] * B(n, k) where B(n,k) = b[k][n] -> b is K-outer
-            N.lib().gemm(a.data_ptr(), K, 0, b.data_ptr(), Nn, 1, c.data_ptr(), Nn, M, Nn, K, 1.0, 0.0, N.ptr(bb),
-                         int(relu), 0 if out_dtype == torch.bfloat16 else 1, 1, batch, M * K, K * Nn, M * Nn,
-                         N.stream())
-            return c
-    r = torch.matmul(a, b)
-    if bias is not None:
-        r = r + bias.to(r.dtype)
-    if relu:
-        r = torch.relu(r)
-    return r.to(out_dtype)
+    bf16 operands run on the MFMA kernel with fp32 accumulation; fp32
+    operands on the exact-f32 MFMA kernel."""
+    if a.dim() > 3 or b.dim() > 3:  # flatten equal leading dims (torch.matmul broadcasting otherwise)
+        lead = torch.broadcast_shapes(a.shape[:-2], b.shape[:-2])
+        aa = G.reshape(a.expand(*lead, *a.shape[-2:]), (-1, *a.shape[-2:]))
+        bb = G.reshape(b.expand(*lead, *b.shape[-2:]), (-1, *b.shape[-2:]))
+        c = gemm(aa, bb, out_dtype=out_dtype or a.dtype, bias=bias, relu=relu)
+        return c.reshape(*lead, c.shape[-2], c.shape[-1])
+    if a.dim() == 3 and b.dim() == 3 and a.shape[0] != b.shape[0]:
+        lead = torch.broadcast_shapes(a.shape[:1], b.shape[:1])
+        a = a.expand(*lead, *a.shape[-2:])
+        b = b.expand(*lead, *b.shape[-2:])
+    return gemm(a, b, out_dtype=out_dtype or a.dtype, bias=bias, relu=relu)
 
 
 def gemm_nt(a: torch.Tensor, b: torch.Tensor, out_dtype=None, bias=None, relu=False) -> torch.Tensor:
     """C = a @ b.T (both operands K-major: a [M,K], b [N,K])."""
-    out_dtype = out_dtype or a.dtype
-    if (_native_ok(a, b) and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and a.dim() == 2
-            and b.dim() == 2):
-        M, K = a.shape
-        Nn = b.shape[0]
-        if _gemm_native_ok(K) and M > 0:
-            a, b = a.contiguous(), b.contiguous()
-            c = torch.empty((M, Nn), dtype=out_dtype, device=a.device)
-            bb = bias.float().contiguous() if bias is not None else None
-            N.lib().gemm(a.data_ptr(), K, 0, b.data_ptr(), K, 0, c.data_ptr(), Nn, M, Nn, K, 1.0, 0.0, N.ptr(bb),
-                         int(relu), 0 if out_dtype == torch.bfloat16 else 1, 1, 1, 0, 0, 0, N.stream())
-            return c
-    r = a @ b.t()
-    if bias is not None:
-        r = r + bias.to(r.dtype)
-    return (torch.relu(r) if relu else r).to(out_dtype)
+    return gemm(a, b, tb=True, out_dtype=out_dtype or a.dtype, bias=bias, relu=relu)
 
 
 def gemm_tn_acc(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, beta: float = 1.0) -> torch.Tensor:
     """out (fp32) = beta*out + a.T @ b with a [K,M], b [K,N] (weight-gradient
     shape: reduction over the batch dim).  Uses split-K atomics on GPU."""
-    if (_native_ok(a, b, out) and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and out.dtype ==
-            torch.float32 and out.is_contiguous()):
-        K, M = a.shape
-        Nn = b.shape[1]
-        if _gemm_native_ok(M, Nn) and K > 0:
-            a, b = a.contiguous(), b.contiguous()
-            if beta == 0.0:
-                out.zero_()
-            elif beta != 1.0:
-                out.mul_(beta)
-            N.lib().gemm(a.data_ptr(), M, 1, b.data_ptr(), Nn, 1, out.data_ptr(), Nn, M, Nn, K, 1.0, 0.0, 0, 0, 2,
-                         0, 1, 0, 0, 0, N.stream())
-            return out
+    if out.is_cuda and N.available():
+        if beta == 0.0:
+            N.lib().zero(out.data_ptr(), out.numel() * out.element_size(), N.stream())
+        elif beta != 1.0:
+            G.binary("mul", out, beta, out=out)
+        return gemm(a, b, ta=True, out=out, accumulate=True)
     r = a.float().t() @ b.float()
     if beta == 0.0:
         out.copy_(r)
@@ -458,9 +598,81 @@ def to_nhwc_bf16(x: torch.Tensor, cpad: Optional[int] = None) -> torch.Tensor:
             fn(x.data_ptr(), y.data_ptr(), Nn, C, H, W, cp, N.stream())
             return y
         y = _zeros_cl((Nn, cp, H, W), torch.bfloat16, x.device)
-        y[:, :C] = x
+        G.copy_(y[:, :C], x)
         return y
-    return x.to(dtype=torch.bfloat16, memory_format=torch.channels_last)
+    return G.to(x, torch.bfloat16, torch.channels_last)
+
+
+def _nhwc(t: torch.Tensor, dt: torch.dtype) -> torch.Tensor:
+    """Dense channels_last copy of a 4-D tensor in dtype dt (no copy if it already is)."""
+    if t.dtype == dt and N.is_cl(t):
+        return t
+    if t.dtype == dt and t.is_contiguous() and t.dim() == 4 and t.shape[2] * t.shape[3] == 1:
+        return t  # [N, C, 1, 1]: NCHW and NHWC memory are the same
+    return G.to(t, dt, torch.channels_last)
+
+
+def _gconv_dt(*ts) -> torch.dtype:
+    return torch.float32 if any(t is not None and t.dtype == torch.float32 for t in ts) else torch.bfloat16
+
+
+def _gconv_fwd(x, w, b, stride, padding, dilation, groups, out_dtype, relu):
+    """Generic-kernel convolution (ggemm.hip): fp32 operands in exact f32
+    MFMA (no downcast), or bf16 grouped / dilated / unpadded-channel convs."""
+    sh, sw = stride
+    ph, pw = padding
+    dh, dw = dilation
+    Nn, C, H, W = x.shape
+    K, Cg, R, S = w.shape
+    if C != Cg * groups or K % groups:
+        raise ValueError(f"conv2d: input {tuple(x.shape)} / weight {tuple(w.shape)} / groups {groups} mismatch")
+    Ho, Wo = conv_out_size(H, R, sh, ph, dh), conv_out_size(W, S, sw, pw, dw)
+    dt = _gconv_dt(x, w)
+    xc, wc = _nhwc(x, dt), _nhwc(w, dt)
+    od = torch.bfloat16 if out_dtype == torch.bfloat16 else torch.float32
+    y = torch.empty((Nn, K, Ho, Wo), dtype=od, device=x.device, memory_format=torch.channels_last)
+    bias = G.contiguous(G.to(b, torch.float32)) if b is not None else None
+    N.lib().gconv_fwd(0 if dt == torch.float32 else 1, xc.data_ptr(), wc.data_ptr(), y.data_ptr(), N.ptr(bias), Nn,
+                      H, W, C, K, R, S, Ho, Wo, sh, sw, ph, pw, dh, dw, groups, int(relu),
+                      0 if od == torch.bfloat16 else 1, N.stream())
+    return y if y.dtype == out_dtype else cast(y, out_dtype)
+
+
+def _gconv_bwd(x, w, dy, stride, padding, dilation, groups, need_dx, dw_out, need_db, dx_acc):
+    sh, sw = stride
+    ph, pw = padding
+    dh, dw_ = dilation
+    Nn, C, H, W = x.shape
+    K, Cg, R, S = w.shape
+    Ho, Wo = dy.shape[2], dy.shape[3]
+    dt = _gconv_dt(x, w, dy)
+    dtc = 0 if dt == torch.float32 else 1
+    L = N.lib()
+    xc, wc, dyc = _nhwc(x, dt), _nhwc(w, dt), _nhwc(dy, dt)
+    dx = None
+    if need_dx:
+        od = x.dtype if x.dtype in (torch.float32, torch.bfloat16) else dt
+        if (dx_acc is not None and dx_acc.dtype == od and tuple(dx_acc.shape) == tuple(x.shape) and N.is_cl(dx_acc)
+                and dx_acc.is_contiguous(memory_format=torch.channels_last)):
+            dx, beta = dx_acc, 1.0
+        else:
+            dx, beta = torch.empty(x.shape, dtype=od, device=x.device, memory_format=torch.channels_last), 0.0
+        L.gconv_dgrad(dtc, dyc.data_ptr(), wc.data_ptr(), dx.data_ptr(), Nn, H, W, C, K, R, S, Ho, Wo, sh, sw, ph, pw,
+                      dh, dw_, groups, 0 if od == torch.bfloat16 else 1, beta, N.stream())
+        if beta == 0.0:
+            dx._sg_fresh = True
+    direct = dw_out is not None and dw_out.dtype == torch.float32 and N.is_cl(dw_out)
+    target = dw_out if direct else _zeros_cl((K, Cg, R, S), torch.float32, x.device)
+    L.gconv_wgrad(dtc, xc.data_ptr(), dyc.data_ptr(), target.data_ptr(), Nn, H, W, C, K, R, S, Ho, Wo, sh, sw, ph, pw,
+                  dh, dw_, groups, 0, N.stream())
+    if direct:
+        dwt = dw_out
+    elif dw_out is not None:
+        dwt = G.binary("add", dw_out, target, out=dw_out)
+    else:
+        dwt = target
+    db = colsum(dyc.permute(0, 2, 3, 1).reshape(-1, K))[0] if need_db else None
+    return dx, dwt, db
 
 
 def conv2d_fwd(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], stride, padding, dilation=(1, 1),
@@ -474,6 +686,8 @@ def conv2d_fwd(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], stri
     sh, sw = stride
     ph, pw = padding
     dh, dw = dilation
+    if _native_ok(x, w) and not (groups == 1 and x.dtype == torch.bfloat16):
+        return _gconv_fwd(x, w, b, stride, padding, dilation, groups, out_dtype, relu)
     if _native_ok(x, w) and groups == 1:
         Nn, Cx, H, W = x.shape
         K, C, R, S = w.shape
@@ -485,15 +699,14 @@ def conv2d_fwd(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], stri
         wb = w
         if Cp != C or Kp != K:
             wb = _zeros_cl((Kp, Cp, R, S), torch.bfloat16, w.device)
-            wb[:K, :C] = w
+            G.copy_(wb[:K, :C], w)
         elif not (w.dtype == torch.bfloat16 and N.is_cl(w)):
-            wb = w.to(dtype=torch.bfloat16, memory_format=torch.channels_last)
+            wb = G.to(w, torch.bfloat16, torch.channels_last)
         bias = None
         if b is not None:
-            bias = b.float()
+            bias = G.contiguous(G.to(b, torch.float32))
             if Kp != K:
-                bias = torch.cat([bias, bias.new_zeros(Kp - K)])
-            bias = bias.contiguous()
+                bias = G.cat([bias, G.zeros((Kp - K,), torch.float32, bias.device)])
         od = torch.bfloat16 if out_dtype == torch.bfloat16 else torch.float32
         y = torch.empty((Nn, Kp, Ho, Wo), dtype=od, device=x.device, memory_format=torch.channels_last)
         ws, rows = None, 0
@@ -510,8 +723,9 @@ def conv2d_fwd(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], stri
         if ws is not None:
             y._sg_bn_ws = (ws, rows)
         if Kp != K:
-            y = y[:, :K].contiguous(memory_format=torch.channels_last)
-        return y if y.dtype == out_dtype else y.to(out_dtype)
+            y = G.contiguous(y[:, :K], torch.channels_last)
+        return y if y.dtype == out_dtype else cast(y, out_dtype)
+    _no_native("conv2d_fwd", x, w)
     xf = x.float() if x.dtype != torch.float32 else x
     y = F.conv2d(xf, w.float(), b.float() if b is not None else None, (sh, sw), (ph, pw), (dh, dw), groups)
     if relu:
@@ -599,6 +813,9 @@ def conv2d_bwd(x: torch.Tensor, w: torch.Tensor, dy: torch.Tensor, stride, paddi
     sh, sw = stride
     ph, pw = padding
     dh, dw_ = dilation
+    if _native_ok(x, w, dy) and not (groups == 1 and x.dtype == torch.bfloat16 and
+                                     (not need_dx or (dh == 1 and dw_ == 1 and sh * sw <= 16))):
+        return _gconv_bwd(x, w, dy, stride, padding, dilation, groups, need_dx, dw_out, need_db, dx_acc)
     if _native_ok(x, w, dy) and groups == 1:
         Nn, Cx, H, W = x.shape
         K, C, R, S = w.shape
@@ -615,10 +832,10 @@ def conv2d_bwd(x: torch.Tensor, w: torch.Tensor, dy: torch.Tensor, stride, paddi
                 raise NotImplementedError("GPU conv data-gradient with stride_h*stride_w > 16")
             if padded:
                 wb = _zeros_cl((Kp, Cp, R, S), torch.bfloat16, w.device)
-                wb[:K, :C] = w
+                G.copy_(wb[:K, :C], w)
             else:
-                wb = w if (w.dtype == torch.bfloat16 and N.is_cl(w)) else w.to(dtype=torch.bfloat16,
-                                                                                memory_format=torch.channels_last)
+                wb = w if (w.dtype == torch.bfloat16 and N.is_cl(w)) else G.to(w, torch.bfloat16,
+                                                                                 torch.channels_last)
             od = torch.bfloat16 if x.dtype == torch.bfloat16 else torch.float32
             om = 0 if od == torch.bfloat16 else 1
             # K-major transposed weights for the B operand: the batched pre-pass's
@@ -672,9 +889,9 @@ def conv2d_bwd(x: torch.Tensor, w: torch.Tensor, dy: torch.Tensor, stride, paddi
                 dxp = torch.empty((Nn, Cp, H, W), dtype=od, device=x.device, memory_format=torch.channels_last)
                 N.lib().conv_dgrad_acc(dyb.data_ptr(), wb.data_ptr(), dxp.data_ptr(), Nn, H, W, Cp, Kp, R, S, Ho, Wo,
                                        sh, sw, ph, pw, dh, dw_, om, 0.0, N.stream(), N.ptr(wt))
-                dx = dxp[:, :C].contiguous(memory_format=torch.channels_last) if Cx != Cp else dxp
+                dx = G.contiguous(dxp[:, :C], torch.channels_last) if Cx != Cp else dxp
                 if dx.dtype != x.dtype:
-                    dx = dx.to(x.dtype)
+                    dx = cast(dx, x.dtype)
                 dx._sg_fresh = True
         # weight gradient, fp32 [Kp][R][S][Cp]
         direct = (dw_out is not None and not padded and dw_out.dtype == torch.float32 and N.is_cl(dw_out))
@@ -686,14 +903,14 @@ def conv2d_bwd(x: torch.Tensor, w: torch.Tensor, dy: torch.Tensor, stride, paddi
         else:
             g = target[:K, :C]
             if dw_out is not None:
-                dw_out.add_(g)
-                dwt = dw_out
+                dwt = G.binary("add", dw_out, g, out=dw_out)
             else:
-                dwt = g.contiguous()
+                dwt = G.contiguous(g)
         if need_db:
             db = colsum(dyb.permute(0, 2, 3, 1).reshape(-1, Kp))[0][:K]
         return dx, dwt, db
     # CPU reference via autograd of the functional conv
+    _no_native("conv2d_bwd", x, w, dy)
     with torch.enable_grad():
         xx = x.detach().float().requires_grad_(need_dx)
         ww = w.detach().float().requires_grad_(True)
@@ -799,13 +1016,15 @@ def _ws(R: int, C: int, device) -> torch.Tensor:
 def colsum(x2: torch.Tensor, with_sq: bool = False, out: Optional[torch.Tensor] = None):
     """Per-column sum (and sum of squares) of a [R, C] row-major tensor -> fp32.
     If ``out`` is given the column sums are ACCUMULATED into it."""
-    if _native_ok(x2) and _flat_ok(x2) and x2.is_contiguous():
+    if _native_ok(x2) and x2.dtype in (torch.float32, torch.bfloat16):
+        x2 = G.contiguous(x2)
         R, C = x2.shape
         o0 = out if out is not None else torch.empty(C, dtype=torch.float32, device=x2.device)
         o1 = torch.empty(C, dtype=torch.float32, device=x2.device) if with_sq else None
         N.lib().colsum(x2.data_ptr(), _ws(R, C, x2.device).data_ptr(), o0.data_ptr(), N.ptr(o1), R, C, N.dt(x2),
                        int(out is not None), N.stream())
         return o0, o1
+    _no_native("colsum", x2)
     xf = x2.float()
     s0 = xf.sum(0)
     if out is not None:
@@ -898,8 +1117,7 @@ def batchnorm_fwd(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, run_
         if residual is not None:
             res = residual
             if res.dtype != x.dtype or not _same_layout(res, x):
-                res = _dense(res).to(x.dtype).contiguous(
-                    memory_format=torch.channels_last if x.dim() == 4 else torch.contiguous_format)
+                res = G.to(res, x.dtype, torch.channels_last if x.dim() == 4 else torch.contiguous_format)
         y = _like(x)
         mask = None
         if want_mask and relu and C % 8 == 0:
@@ -908,6 +1126,7 @@ def batchnorm_fwd(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, run_
                    N.dt(x), N.stream(), N.ptr(mask))
         return y, BNState(mean, invstd, scale, shift, mask)
     # CPU reference
+    _no_native("batchnorm_fwd", x)
     dims = (0,) if x.dim() == 2 else (0, 2, 3)
     shp = (1, C) if x.dim() == 2 else (1, C, 1, 1)
     xf = x.float()
@@ -962,8 +1181,8 @@ def dual_bn_add_relu_bwd(x, dy, gamma, st: BNState, x2, gamma2, st2: BNState, dg
     R = x.numel() // C
     dev = x.device
     if dy.dtype != x.dtype or not _same_layout(dy, x):
-        dy = dy.to(x.dtype).contiguous(memory_format=torch.channels_last if x.dim() == 4 else torch.contiguous_format)
-    z = lambda o: o if o is not None else torch.zeros(C, dtype=torch.float32, device=dev)  # noqa: E731
+        dy = G.to(dy, x.dtype, torch.channels_last if x.dim() == 4 else torch.contiguous_format)
+    z = lambda o: o if o is not None else G.zeros((C,), torch.float32, dev)  # noqa: E731
     dg, db, dg2, db2 = z(dg_out), z(db_out), z(dg2_out), z(db2_out)
     key = (R, C, N.lib().deterministic())
     n = _BANDS.get(key)
@@ -994,8 +1213,7 @@ def batchnorm_bwd(x: torch.Tensor, dy: torch.Tensor, gamma: torch.Tensor, st: BN
         L = N.lib()
         R = x.numel() // C
         if dy.dtype != x.dtype or not _same_layout(dy, x):
-            dy = dy.to(x.dtype).contiguous(memory_format=torch.channels_last if x.dim() == 4 else
-                                           torch.contiguous_format)
+            dy = G.to(dy, x.dtype, torch.channels_last if x.dim() == 4 else torch.contiguous_format)
         ym = y_for_mask
         if st.mask is not None and relu:
             ym, mode = st.mask, 3  # 1-bit mask written by the forward apply
@@ -1005,8 +1223,8 @@ def batchnorm_bwd(x: torch.Tensor, dy: torch.Tensor, gamma: torch.Tensor, st: BN
             mode = 1
         else:
             mode = 2 if relu else 0
-        dg = dg_out if dg_out is not None else torch.zeros(C, dtype=torch.float32, device=x.device)
-        db = db_out if db_out is not None else torch.zeros(C, dtype=torch.float32, device=x.device)
+        dg = dg_out if dg_out is not None else G.zeros((C,), torch.float32, x.device)
+        db = db_out if db_out is not None else G.zeros((C,), torch.float32, x.device)
         coef = torch.empty(3 * C, dtype=torch.float32, device=x.device)
         dx = _like(x)
         dres = _like(x) if need_dres else None
@@ -1028,6 +1246,7 @@ def batchnorm_bwd(x: torch.Tensor, dy: torch.Tensor, gamma: torch.Tensor, st: BN
         if dres is not None:
             dres._sg_fresh = True
         return dx, dg, db, dres
+    _no_native("batchnorm_bwd", x, dy)
     dims = (0,) if x.dim() == 2 else (0, 2, 3)
     shp = (1, C) if x.dim() == 2 else (1, C, 1, 1)
     g = dy.float()
@@ -1062,12 +1281,16 @@ def pool2d_fwd(x: torch.Tensor, kernel, stride, padding, is_max: bool, count_inc
     else:
         Ho = (H + 2 * ph - kh) // sh + 1
         Wo = (W + 2 * pw - kw) // sw + 1
-    if _native_ok(x) and _flat_ok(x) and N.is_cl(x):
+    if _native_ok(x) and x.dtype in (torch.float32, torch.bfloat16):
+        if kh * kw > 255 and is_max:
+            raise NotImplementedError("max pool windows of more than 255 taps (8-bit argmax)")
+        x = G.to(x, memory_format=torch.channels_last)
         y = torch.empty((Nn, C, Ho, Wo), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
         arg = torch.empty((Nn, Ho, Wo, C), dtype=torch.uint8, device=x.device) if is_max else None
         N.lib().pool_fwd(x.data_ptr(), y.data_ptr(), N.ptr(arg), Nn, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw,
                          int(is_max), int(count_include_pad), N.dt(x), N.stream())
         return y, arg
+    _no_native("pool2d_fwd", x)
     xf = x.float()
     if is_max:
         y, idx = F.max_pool2d(xf, (kh, kw), (sh, sw), (ph, pw), ceil_mode=ceil_mode, return_indices=True)
@@ -1083,13 +1306,13 @@ def pool2d_bwd(x_shape, x_like: torch.Tensor, dy: torch.Tensor, arg, kernel, str
     ph, pw = padding
     Nn, C, H, W = x_shape
     Ho, Wo = dy.shape[2], dy.shape[3]
-    if _native_ok(dy) and _flat_ok(dy) and N.is_cl(x_like):
-        if not N.is_cl(dy):
-            dy = dy.contiguous(memory_format=torch.channels_last)
+    if _native_ok(dy) and dy.dtype in (torch.float32, torch.bfloat16):
+        dy = G.to(dy, memory_format=torch.channels_last)
         dx = torch.empty(x_shape, dtype=dy.dtype, device=dy.device, memory_format=torch.channels_last)
         N.lib().pool_bwd(dy.data_ptr(), N.ptr(arg), dx.data_ptr(), Nn, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw,
                          int(is_max), int(count_include_pad), N.dt(dy), N.stream())
         return dx
+    _no_native("pool2d_bwd", dy)
     g = dy.float()
     if is_max:  # scatter-ADD: overlapping windows (k > s) may pick the same input
         dx = torch.zeros((Nn, C, H * W), dtype=torch.float32, device=dy.device)
@@ -1104,19 +1327,23 @@ def pool2d_bwd(x_shape, x_like: torch.Tensor, dy: torch.Tensor, arg, kernel, str
 
 def global_avgpool_fwd(x: torch.Tensor) -> torch.Tensor:
     Nn, C, H, W = x.shape
-    if _native_ok(x) and _flat_ok(x) and N.is_cl(x):
+    if _native_ok(x) and x.dtype in (torch.float32, torch.bfloat16):
+        x = G.to(x, memory_format=torch.channels_last)
         y = torch.empty((Nn, C), dtype=x.dtype, device=x.device)
         N.lib().gap_fwd(x.data_ptr(), y.data_ptr(), Nn, H * W, C, N.dt(x), N.stream())
         return y
+    _no_native("global_avgpool_fwd", x)
     return x.float().mean(dim=(2, 3)).to(x.dtype)
 
 
 def global_avgpool_bwd(dy: torch.Tensor, x_shape) -> torch.Tensor:
     Nn, C, H, W = x_shape
-    if _native_ok(dy) and _flat_ok(dy) and dy.is_contiguous():
+    if _native_ok(dy) and dy.dtype in (torch.float32, torch.bfloat16):
+        dy = G.contiguous(dy)
         dx = torch.empty(x_shape, dtype=dy.dtype, device=dy.device, memory_format=torch.channels_last)
         N.lib().gap_bwd(dy.data_ptr(), dx.data_ptr(), Nn, H * W, C, N.dt(dy), N.stream())
         return dx
+    _no_native("global_avgpool_bwd", dy)
     return (dy.float()[:, :, None, None] / (H * W)).expand(x_shape).to(dy.dtype)
 
 
@@ -1128,6 +1355,8 @@ def _lrn_rows_ok(x, size):
 def lrn_fwd(x: torch.Tensor, size: int, alpha: float, beta: float, k: float):
     """Returns (y, norm); norm is None on the pixel-staged native path
     (lrn_bwd then recomputes it from x and needs ``k``)."""
+    if _native_ok(x) and x.dtype in (torch.float32, torch.bfloat16) and not N.is_cl(x):
+        x = G.to(x, memory_format=torch.channels_last)
     if _native_ok(x) and _flat_ok(x) and N.is_cl(x) and _lrn_rows_ok(x, size):
         C = x.shape[1]
         y = _like(x)
@@ -1142,6 +1371,7 @@ def lrn_fwd(x: torch.Tensor, size: int, alpha: float, beta: float, k: float):
         N.lib().lrn_fwd(x.data_ptr(), y.data_ptr(), norm.data_ptr(), R, C, size, alpha, beta, k, N.dt(x),
                         N.stream())
         return y, norm
+    _no_native("lrn_fwd", x)
     xf = x.float()
     sq = xf * xf
     half = size // 2
@@ -1155,6 +1385,9 @@ def lrn_bwd(x: torch.Tensor, dy: torch.Tensor, norm: Optional[torch.Tensor], siz
             k: float = 1.0, relu_mask: bool = False):
     """``relu_mask``: x is a ReLU output; the native kernel also zeroes dx
     where x <= 0 (the ReLU backward, folded) and marks dx ``_sg_relu_done``."""
+    if _native_ok(x, dy) and x.dtype in (torch.float32, torch.bfloat16):
+        x = G.to(x, memory_format=torch.channels_last)
+        dy = G.to(dy, x.dtype, torch.channels_last)
     if norm is None:  # pixel-staged forward: recompute norm from x inside the backward kernel
         if (_native_ok(x, dy) and _flat_ok(x) and N.is_cl(x) and N.is_cl(dy) and dy.dtype == x.dtype
                 and _lrn_rows_ok(x, size)):
@@ -1167,6 +1400,7 @@ def lrn_bwd(x: torch.Tensor, dy: torch.Tensor, norm: Optional[torch.Tensor], siz
             if relu_mask:
                 dx._sg_relu_done = True
             return dx
+        _no_native("lrn_bwd (window)", x)
         xf = x.float()
         half = size // 2
         s2 = sum(F.pad(xf * xf, (0, 0, 0, 0, half, half))[:, i:i + x.shape[1]] for i in range(size))
@@ -1178,6 +1412,7 @@ def lrn_bwd(x: torch.Tensor, dy: torch.Tensor, norm: Optional[torch.Tensor], siz
         N.lib().lrn_bwd(x.data_ptr(), dy.data_ptr(), norm.data_ptr(), dx.data_ptr(), R, C, size, alpha, beta,
                         N.dt(x), N.stream())
         return dx
+    _no_native("lrn_bwd", x, dy)
     xf, g = x.float(), dy.float()
     t = g * xf * norm.pow(-beta - 1)
     half = size // 2
@@ -1188,41 +1423,28 @@ def lrn_bwd(x: torch.Tensor, dy: torch.Tensor, norm: Optional[torch.Tensor], siz
 
 
 # ---------------------------------------------------------------- attention
-def _bgemm(a, b, M, Nn, K, batch, ako, bko, lda, ldb, sa, sb, alpha=1.0, out_dtype=torch.bfloat16, out=None,
-           beta=0.0):
-    """Batched C[i] = alpha * A[i] B[i] (+ beta C) on the MFMA kernel (bf16 operands)."""
-    c = out if out is not None else torch.empty((batch, M, Nn), dtype=out_dtype, device=a.device)
-    mode = 0 if c.dtype == torch.bfloat16 else 1
-    N.lib().gemm(a.data_ptr(), lda, ako, b.data_ptr(), ldb, bko, c.data_ptr(), Nn, M, Nn, K, alpha, beta, 0, 0,
-                 mode, 1, batch, sa, sb, M * Nn, N.stream())
-    return c
-
-
-def _attn_native_ok(q, k, v):
-    return (_native_ok(q, k, v) and q.dtype == torch.bfloat16 and k.dtype == q.dtype and v.dtype == q.dtype
-            and q.shape[-1] % 8 == 0 and q.shape[-2] % 8 == 0 and k.shape[-2] % 8 == 0)
-
-
 def attention_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, mask: Optional[torch.Tensor] = None,
                   scale: Optional[float] = None):
     """softmax(q k^T * scale + mask) v for q [..., Sq, D], k/v [..., Sk, D];
     mask broadcastable to [..., Sq, Sk] (additive).  Returns (o, p) with the
-    probabilities p kept for backward."""
+    probabilities p kept for backward.  GPU: batched MFMA GEMMs (bf16 or
+    exact fp32, any head size / length) + the softmax kernels."""
     D = q.shape[-1]
     scale = (1.0 / math.sqrt(D)) if scale is None else scale
     lead = q.shape[:-2]
     Sq, Sk = q.shape[-2], k.shape[-2]
-    if _attn_native_ok(q, k, v):
-        q3 = q.reshape(-1, Sq, D).contiguous()
-        k3 = k.reshape(-1, Sk, D).contiguous()
-        v3 = v.reshape(-1, Sk, D).contiguous()
+    if _native_ok(q, k, v):
+        q3 = G.reshape(q, (-1, Sq, D))
+        k3 = G.reshape(k, (-1, Sk, D))
+        v3 = G.reshape(v, (-1, Sk, D))
         B = q3.shape[0]
-        s = _bgemm(q3, k3, Sq, Sk, D, B, 0, 0, D, D, Sq * D, Sk * D, alpha=scale, out_dtype=torch.float32)
+        s = gemm(q3, k3, tb=True, alpha=scale, out_dtype=torch.float32)
         if mask is not None:
-            s = (s.view(*lead, Sq, Sk) + mask.to(torch.float32)).reshape(B, Sq, Sk)
-        p = softmax(s, out_dtype=torch.bfloat16)
-        o = _bgemm(p, v3, Sq, D, Sk, B, 0, 1, Sk, D, Sq * Sk, Sk * D)
+            s = G.binary("add", s.view(*lead, Sq, Sk), mask, out_dtype=torch.float32).reshape(B, Sq, Sk)
+        p = softmax(s, out_dtype=q.dtype)
+        o = gemm(p, v3, out_dtype=q.dtype)
         return o.view(*lead, Sq, D), p.view(*lead, Sq, Sk)
+    _no_native("attention_fwd", q, k, v)
     s = torch.matmul(q.float(), k.float().transpose(-1, -2)) * scale
     if mask is not None:
         s = s + mask.float()
@@ -1268,7 +1490,7 @@ def attention_qkv_fwd(qkv: torch.Tensor, heads: int, mask: Optional[torch.Tensor
         _gemm_heads((qkv, 0), E, 0, (qkv, HD), E, 0, (sc, 0), S, S, S, D, BH, H, S * E, D, S * E, D, H * S * S,
                     S * S, alpha=scale)
         if mask is not None:
-            sc = (sc.view(B, H, S, S) + mask.to(torch.float32)).reshape(BH, S, S)
+            sc = G.binary("add", sc.view(B, H, S, S), mask, out_dtype=torch.float32).reshape(BH, S, S)
         p = softmax(sc, out_dtype=torch.bfloat16)
         o = torch.empty((B, S, HD), dtype=torch.bfloat16, device=qkv.device)
         # o = p v : v [S][D] is K-outer (ldb E); o rows of stride H*D
@@ -1277,7 +1499,7 @@ def attention_qkv_fwd(qkv: torch.Tensor, heads: int, mask: Optional[torch.Tensor
         return o, p
     t = qkv.view(B, S, 3, H, D).permute(2, 0, 3, 1, 4)
     o, p = attention_fwd(t[0], t[1], t[2], mask, scale)
-    return o.permute(0, 2, 1, 3).reshape(B, S, HD), p.reshape(B * H, S, S)
+    return G.reshape(G.contiguous(o.permute(0, 2, 1, 3)), (B, S, HD)), G.reshape(p, (B * H, S, S))
 
 
 def attention_qkv_bwd(qkv: torch.Tensor, p: torch.Tensor, do: torch.Tensor, heads: int,
@@ -1291,7 +1513,7 @@ def attention_qkv_bwd(qkv: torch.Tensor, p: torch.Tensor, do: torch.Tensor, head
     scale = (1.0 / math.sqrt(D)) if scale is None else scale
     if _qkv_native_ok(qkv, H) and p.dtype == torch.bfloat16 and do.dtype == torch.bfloat16:
         BH = B * H
-        do = do.contiguous()
+        do = G.contiguous(do)
         dqkv = torch.empty_like(qkv)
         SS = S * S
         # dV = P^T dO
@@ -1308,9 +1530,10 @@ def attention_qkv_bwd(qkv: torch.Tensor, p: torch.Tensor, do: torch.Tensor, head
                     alpha=scale)
         return dqkv
     t = qkv.view(B, S, 3, H, D).permute(2, 0, 3, 1, 4)
-    dq, dk, dv = attention_bwd(t[0], t[1], t[2], p.reshape(B, H, S, S),
-                               do.reshape(B, S, H, D).permute(0, 2, 1, 3), scale)
-    return torch.stack([dq, dk, dv], 0).permute(1, 3, 0, 2, 4).reshape(B, S, E).to(qkv.dtype)
+    dq, dk, dv = attention_bwd(t[0], t[1], t[2], G.reshape(p, (B, H, S, S)),
+                               G.reshape(do, (B, S, H, D)).permute(0, 2, 1, 3), scale)
+    st = G.cat([dq.unsqueeze(0), dk.unsqueeze(0), dv.unsqueeze(0)], 0)  # [3, B, H, S, D]
+    return G.to(G.reshape(G.contiguous(st.permute(1, 3, 0, 2, 4)), (B, S, E)), qkv.dtype)
 
 
 def attention_bwd(q, k, v, p, do, scale: Optional[float] = None):
@@ -1318,20 +1541,20 @@ def attention_bwd(q, k, v, p, do, scale: Optional[float] = None):
     D = q.shape[-1]
     scale = (1.0 / math.sqrt(D)) if scale is None else scale
     Sq, Sk = q.shape[-2], k.shape[-2]
-    if _attn_native_ok(q, k, v) and p.dtype == torch.bfloat16 and do.dtype == torch.bfloat16:
-        q3 = q.reshape(-1, Sq, D).contiguous()
-        k3 = k.reshape(-1, Sk, D).contiguous()
-        v3 = v.reshape(-1, Sk, D).contiguous()
-        p3 = p.reshape(-1, Sq, Sk).contiguous()
-        do3 = do.reshape(-1, Sq, D).contiguous()
-        B = q3.shape[0]
-        # dV = P^T dO ; dP = dO V^T
-        dv = _bgemm(p3, do3, Sk, D, Sq, B, 1, 1, Sk, D, Sq * Sk, Sq * D)
-        dp = _bgemm(do3, v3, Sq, Sk, D, B, 0, 0, D, D, Sq * D, Sk * D)
-        ds = softmax_bwd(p3, dp)  # P * (dP - rowsum(dP * P)), bf16
-        dq = _bgemm(ds, k3, Sq, D, Sk, B, 0, 1, Sk, D, Sq * Sk, Sk * D, alpha=scale)
-        dk = _bgemm(ds, q3, Sk, D, Sq, B, 1, 1, Sk, D, Sq * Sk, Sq * D, alpha=scale)
+    if _native_ok(q, k, v, p, do):
+        q3 = G.reshape(q, (-1, Sq, D))
+        k3 = G.reshape(k, (-1, Sk, D))
+        v3 = G.reshape(v, (-1, Sk, D))
+        p3 = G.reshape(p, (-1, Sq, Sk))
+        do3 = G.reshape(G.to(do, q.dtype), (-1, Sq, D))
+        # dV = P^T dO ; dP = dO V^T ; dS = P * (dP - rowsum(dP * P)) ; dQ = scale dS K ; dK = scale dS^T Q
+        dv = gemm(p3, do3, ta=True, out_dtype=v.dtype)
+        dp = gemm(do3, v3, tb=True, out_dtype=p.dtype)
+        ds = softmax_bwd(p3, dp)
+        dq = gemm(ds, k3, alpha=scale, out_dtype=q.dtype)
+        dk = gemm(ds, q3, ta=True, alpha=scale, out_dtype=k.dtype)
         return dq.view(q.shape), dk.view(k.shape), dv.view(v.shape)
+    _no_native("attention_bwd", q, k, v)
     pf, dof = p.float(), do.float()
     dv = torch.matmul(pf.transpose(-1, -2), dof)
     dp = torch.matmul(dof, v.float().transpose(-1, -2))

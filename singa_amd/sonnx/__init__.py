@@ -480,6 +480,8 @@ def to_onnx(m, inputs: Sequence[Tensor], outputs: Optional[Sequence[Tensor]] = N
             c.keep.append(y)
             o.append(n)
         fn = _EXPORTERS.get(type(op).__name__)
+        if fn is None and getattr(op, "onnx", None) is not None:
+            fn = _x_torchfn  # glue operators (autograd.Fn / _Math) carry their ONNX spec
         if fn is None:
             raise NotImplementedError(f"sonnx export: no ONNX lowering for operator {type(op).__name__}")
         fn(c, op, xs, i, o)
