@@ -13,7 +13,7 @@ update of every parameter.
 
 Weak scaling: per-GPU batch is fixed (default 1024: sized for the 288 GB of
 HBM3E per MI355X -- activations take ~120 GB -- and the larger grids fill the
-256 CUs better: measured 10.2k / 10.57k / 10.67k img/s at 512 / 768 / 1024),
+256 CUs better; see README "Performance" for the measured batch sweep),
 global batch = N * 1024.
 Rank 0 prints ONE JSON line; value = N * batch * K / max-over-ranks(elapsed).
 """
@@ -34,8 +34,7 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=1024,
-                    help="per-GPU batch (measured on MI355X: 512 -> 10.2k, 768 -> 10.57k, 1024 -> 10.67k img/s; "
-                         "fits easily in 288 GB HBM3E)")
+                    help="per-GPU batch (1024 fits easily in 288 GB HBM3E; larger batches fill the 256 CUs better)")
     ap.add_argument("--depth", type=int, default=50)
     ap.add_argument("--image", type=int, default=224)
     ap.add_argument("--graph", dest="graph", action="store_true", default=None,
@@ -100,9 +99,11 @@ def main() -> int:
     if args.warmup > 0:
         # guard against a silently truncated backward (it would inflate the
         # number): after a step every parameter must hold a non-zero gradient
+        from singa_amd.ops import glue as G
         st = optimizer.store
-        dead = [i for i, (p, off) in enumerate(zip(st.params, st.offsets))
-                if float(st.g[off:off + p.data.numel()].abs().sum()) == 0.0]
+        norms = G.cat([G.reduce(st.g[off:off + p.data.numel()], None, "sumsq").reshape(1)
+                       for p, off in zip(st.params, st.offsets)]).cpu()  # native reductions, one copy back
+        dead = [i for i in range(len(st.params)) if float(norms[i]) == 0.0]
         if dead:
             print(f"bench.py: {len(dead)} of {len(st.params)} parameters got no gradient", file=sys.stderr)
             return 3
@@ -157,7 +158,7 @@ def main() -> int:
             rec["config"]["loss_curve"] = curve
         if ps is not None:
             rec["ps_parity"] = {k: ps[k] for k in ("ms_per_iter", "algbw_GBps", "n_ranks",
-                                                   "speedup_vs_reference_1thread_1server")}
+                                                   "speedup_vs_reference_1thread_1server", "note") if k in ps}
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.barrier()

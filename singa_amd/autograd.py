@@ -590,15 +590,14 @@ class AddBias(Operator):
         self.axis = axis
 
     def forward(self, x, b):
-        if self.axis == 0:
-            return x + b.to(x.dtype).reshape(1, -1)
-        return x + b.to(x.dtype).reshape(-1, 1)
+        bb = G.to(b, x.dtype)
+        return G.binary("add", x, bb.reshape(1, -1) if self.axis == 0 else bb.reshape(-1, 1))
 
     def backward(self, dy):
-        db = dy.float().sum(0) if self.axis == 0 else dy.float().sum(1)
+        db = G.reduce(dy, [0] if self.axis == 0 else [1], "sum", out_dtype=torch.float32)
         tgt = self.grad_target(1)
         if tgt is not None:
-            tgt.add_(db.reshape(tgt.shape))
+            G.binary("add", tgt, db.reshape(tgt.shape), out=tgt)
             return dy, ACCUMULATED
         return dy, db
 
@@ -616,7 +615,7 @@ class Linear(Operator):
         w = self._w_compute(x, W)
         lead = x.shape[:-1]
         x2 = x.reshape(-1, x.shape[-1])
-        bias = b.float() if b is not None else None
+        bias = G.to(b, torch.float32) if b is not None else None
         y = F.matmul(x2, w, out_dtype=x.dtype, bias=bias)
         if self.requires_grad:
             self.x2, self.w = x2, w
@@ -946,13 +945,13 @@ class SoftMaxCrossEntropy(Operator):
         self.correct = correct
         self.per_row = loss
         self.nt = 2 if self.t is None and t is not None else 1
-        return loss.mean()
+        return G.reduce(loss, None, "mean", out_dtype=torch.float32)
 
     def backward(self, dy=None):
         dx = self.dx
         self.dx = None
         if not is_unit(dy):
-            dx = (dx.float() * dy.float()).to(dx.dtype)
+            dx = G.binary("mul", dx, dy, out_dtype=dx.dtype)
         return (dx, None) if len(self.src) == 2 else dx
 
 
@@ -960,50 +959,63 @@ class CrossEntropy(Operator):
     """Cross entropy over probabilities: -sum(t * log(p)) / B."""
 
     def forward(self, p, t):
-        if self.requires_grad:
-            self.p, self.t = p, t
         B = p.shape[0]
-        if t.dim() == 1 or not t.is_floating_point():
-            tt = torch.nn.functional.one_hot(t.long().reshape(-1), p.shape[-1]).to(p.dtype)
+        if t.dim() == 1 or not t.is_floating_point():  # class ids -> one-hot rows
+            ids = G.reshape(G.to(t, torch.int64), (-1, 1))
+            tt = G.scatter_elements(G.zeros(p.shape, torch.float32, p.device), 1, ids,
+                                    G.full(ids.shape, 1.0, torch.float32, p.device))
         else:
-            tt = t
-        self.tt = tt
-        return -(tt * torch.log(torch.clamp(p.float(), min=1e-30))).sum() / B
+            tt = G.to(t, torch.float32)
+        lp = F.unary("log", G.clamp_affine(G.to(p, torch.float32), lo=1e-30))
+        if self.requires_grad:
+            self.p, self.tt = p, tt
+        return F.unary("scale", G.reduce(G.binary("mul", tt, lp), None, "sum", out_dtype=torch.float32), -1.0 / B)
 
     def backward(self, dy=None):
         B = self.p.shape[0]
-        g = -self.tt / torch.clamp(self.p.float(), min=1e-30) / B
-        if dy is not None:
-            g = g * dy
-        return g.to(self.p.dtype), None
+        # d/dp = -t / clamp(p) / B
+        g = G.binary("div", self.tt, G.clamp_affine(G.to(self.p, torch.float32), lo=1e-30), alpha=-1.0 / B)
+        if dy is not None and not is_unit(dy):
+            g = G.binary("mul", g, dy)
+        return G.to(g, self.p.dtype), None
 
 
 class MeanSquareError(Operator):
+    """sum((x - t)^2) / (2B)."""
+
     def forward(self, x, t):
+        d = G.binary("sub", x, t, out_dtype=torch.float32)
         if self.requires_grad:
-            self.d = (x.float() - t.float())
-        d = x.float() - t.float()
-        return (d * d).sum() / (2.0 * x.shape[0])
+            self.d = d
+        return F.unary("scale", G.reduce(d, None, "sumsq", out_dtype=torch.float32), 1.0 / (2.0 * x.shape[0]))
 
     def backward(self, dy=None):
-        g = self.d / self.d.shape[0]
-        if dy is not None:
-            g = g * dy
+        g = F.unary("scale", self.d, 1.0 / self.d.shape[0])
+        if dy is not None and not is_unit(dy):
+            g = G.binary("mul", g, dy)
         return g, None
 
 
 class BinaryCrossEntropy(Operator):
+    """-mean(t log p + (1 - t) log(1 - p)), p clamped to [1e-7, 1 - 1e-7]."""
+
     def forward(self, x, t):
-        p = torch.clamp(x.float(), 1e-7, 1 - 1e-7)
+        p = G.clamp_affine(G.to(x, torch.float32), lo=1e-7, hi=1 - 1e-7)
+        tf = G.to(t, torch.float32)
         if self.requires_grad:
-            self.p, self.t = p, t.float()
-        return -(t.float() * torch.log(p) + (1 - t.float()) * torch.log(1 - p)).mean()
+            self.p, self.t = p, tf
+        lp = F.unary("log", p)
+        l1p = F.unary("log", G.clamp_affine(p, -1.0, 1.0))  # log(1 - p)
+        s = G.binary("add", G.binary("mul", tf, lp), G.binary("mul", F.unary("adds", F.unary("neg", tf), 1.0), l1p))
+        return F.unary("neg", G.reduce(s, None, "mean", out_dtype=torch.float32))
 
     def backward(self, dy=None):
         p, t = self.p, self.t
-        g = (p - t) / (p * (1 - p)) / p.numel()
-        if dy is not None:
-            g = g * dy
+        # (p - t) / (p (1 - p)) / n
+        den = G.binary("mul", p, G.clamp_affine(p, -1.0, 1.0))
+        g = G.binary("div", G.binary("sub", p, t), den, alpha=1.0 / p.numel())
+        if dy is not None and not is_unit(dy):
+            g = G.binary("mul", g, dy)
         return g, None
 
 

@@ -126,6 +126,7 @@ void sg_pad_nd(const void*, void*, int, int, const int64_t*, const int64_t*, con
 void sg_pad_bwd(const void*, void*, int, int, const int64_t*, const int64_t*, const int64_t*, const int64_t*, int,
                 hipStream_t);
 void sg_fill(void*, int64_t, int, double, hipStream_t);
+void sg_iadd_i64(void*, int64_t, int64_t, hipStream_t);
 void sg_clamp_affine(const void*, const void*, void*, int64_t, int, float, float, float, float, hipStream_t);
 void sg_set_tuning(int key, int value);
 void sg_bn_set_unroll(int);
@@ -453,6 +454,7 @@ PYBIND11_MODULE(_C, m) {
     CHK("pad_bwd");
   });
   m.def("fill", [](P p, int64_t n, int dt, double v, P s) { sg_fill(V(p), n, dt, v, S(s)); CHK("fill"); });
+  m.def("iadd_i64", [](P p, int64_t n, int64_t v, P s) { sg_iadd_i64(V(p), n, v, S(s)); CHK("iadd_i64"); });
   m.def("clamp_affine", [](P x, P dy, P out, int64_t n, int dt, float a, float b, float lo, float hi, P s) {
     sg_clamp_affine(CV(x), CV(dy), V(out), n, dt, a, b, lo, hi, S(s)); CHK("clamp_affine");
   });

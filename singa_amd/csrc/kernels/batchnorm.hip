@@ -39,7 +39,7 @@ enum MaskMode : int { MASK_NONE = 0, MASK_Y = 1, MASK_AFFINE = 2, MASK_BITS = 3 
 constexpr int NSLOT = 32;      // atomic partial-sum slot rows of the fast mode
 constexpr int FIN_GROUPS = 4;  // band groups per finalize workgroup (256 threads = 64 channels x 4)
 static int g_bn_det = 0;       // deterministic reductions (set by sg_set_deterministic)
-static int g_ws_prezeroed = 0; // next launch's workspace is already zeroed (per-step arena): skip its zeroing
+static thread_local int g_ws_prezeroed = 0; // (per OS thread) next launch's workspace is already zeroed (per-step arena): skip its zeroing
 
 struct Tile2D {
   int CT, RT, tx, ty, c0;

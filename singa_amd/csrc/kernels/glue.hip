@@ -307,6 +307,10 @@ __global__ void pad_bwd_k(const T* __restrict__ dy, float* __restrict__ dx, cons
   }
 }
 
+__global__ void iadd_i64_k(int64_t* __restrict__ p, int64_t n, int64_t v) {
+  SG_GRID_STRIDE(i, n) { p[i] += v; }
+}
+
 template <typename T>
 __global__ void fill_k(T* __restrict__ p, int64_t n, T v) {
   SG_GRID_STRIDE(i, n) { p[i] = v; }
@@ -548,6 +552,11 @@ void sg_fill(void* p, int64_t n, int dt, double v, hipStream_t s) {
     case kU8: hipLaunchKernelGGL(fill_k<uint8_t>, g, b, 0, s, (uint8_t*)p, n, (uint8_t)v); break;
     default: throw std::runtime_error("fill: unsupported dtype");
   }
+}
+
+// p[i] += v on int64 counters (the device RNG epoch a captured step advances)
+void sg_iadd_i64(void* p, int64_t n, int64_t v, hipStream_t s) {
+  if (n > 0) hipLaunchKernelGGL(iadd_i64_k, dim3(sg_grid(n, 64, 64)), dim3(64), 0, s, (int64_t*)p, n, v);
 }
 
 void sg_clamp_affine(const void* x, const void* dy, void* out, int64_t n, int dt, float a, float b, float lo, float hi,

@@ -1116,7 +1116,11 @@ static int make_phases(ConvGeom& g) {
 // 6 = single-stage short-K variant for GEMMs of at most this many K-tiles
 // (0 = off), 7 = early DMA issue in the 2-stage loop (measured -3.5 % conv time)
 static int g_tune[8] = {5, 1, 1, 0, 0, 1, 2, 1};
-static int g_wt_ready = 0;  // one-shot: the next dgrad's wt scratch is already transposed
+// one-shot: the next dgrad's wt scratch is already transposed.  Per OS
+// thread: the runtime's executor threads (hogwild / aggregated replicas)
+// each set and consume their own flag, so one thread's set can never be
+// taken by another thread's dgrad
+static thread_local int g_wt_ready = 0;
 
 constexpr int stages_c(int BM, int BN, int STAGES) { return STAGES * (BM + BN) * BK * 2; }
 

@@ -85,18 +85,34 @@ void tune_socket(int fd) {
 // ---------------------------------------------------------------------------
 // server
 // ---------------------------------------------------------------------------
-// The value is an immutable shared buffer: a reply shares it instead of
-// copying (the writer may still be sending an older version while a new
-// request replaces it); in-place updates copy-on-write when a reply holds it.
-using FBuf = std::shared_ptr<std::vector<float>>;
+// The value is a shared buffer: a reply shares it instead of copying (a
+// connection's writer thread may still be sending an older version while a
+// new request replaces it); an in-place update copies-on-write while any
+// queued reply still refers to it.  "Still refers" is the `inflight` count,
+// incremented under the entry mutex when a reply is queued and released by
+// the writer (release) after the send; mut() reads it with acquire, so the
+// send's reads happen-before any later in-place write.  (shared_ptr's
+// use_count() is a relaxed load and orders nothing -- ThreadSanitizer
+// flagged the update racing the send under the multi-client stress test.)
+struct Buf : std::vector<float> {
+  std::atomic<int> inflight{0};
+  Buf() = default;
+  explicit Buf(size_t n) : std::vector<float>(n) {}
+  Buf(const Buf& o) : std::vector<float>(o) {}
+};
+using FBuf = std::shared_ptr<Buf>;
 struct PSEntry {
   std::mutex mu;
   FBuf w;
   std::vector<float> s1, s2;
   int64_t nupdates = 0;
-  std::vector<float>& mut() {  // the value, unshared, for an in-place update
-    if (w.use_count() > 1) w = std::make_shared<std::vector<float>>(*w);
+  std::vector<float>& mut() {  // the value, unshared, for an in-place update (entry mutex held)
+    if (w->inflight.load(std::memory_order_acquire) > 0) w = std::make_shared<Buf>(*w);
     return *w;
+  }
+  FBuf reply() {  // the value as a queued reply (entry mutex held)
+    w->inflight.fetch_add(1, std::memory_order_relaxed);
+    return w;
   }
 };
 
@@ -123,7 +139,11 @@ struct PServer::Impl {
       auto it = params.find(id);
       if (it != params.end()) return it->second.get();
       if (!wait || closing) return nullptr;
-      cv.wait_for(lk, std::chrono::milliseconds(100));  // deferred kGet (server.cc:79-95)
+      // deferred kGet (server.cc:79-95).  A system_clock deadline: libstdc++
+      // maps a steady_clock wait_for onto pthread_cond_clockwait, which the
+      // GCC 11 ThreadSanitizer does not intercept (it then reports the
+      // re-lock inside the wait as a double lock)
+      cv.wait_until(lk, std::chrono::system_clock::now() + std::chrono::milliseconds(100));
     }
   }
 
@@ -147,17 +167,19 @@ struct PServer::Impl {
           q.pop_front();
         }
         const PSHeader& r = item.first;
-        if (!send_all(fd, &r, sizeof(r)) || (r.n && !send_all(fd, item.second->data(), r.n * sizeof(float)))) {
+        const bool ok = send_all(fd, &r, sizeof(r)) && (!r.n || send_all(fd, item.second->data(), r.n * sizeof(float)));
+        if (item.second) item.second->inflight.fetch_sub(1, std::memory_order_release);
+        if (!ok) {
           ::shutdown(fd, SHUT_RDWR);  // the reader sees the error and ends the connection
           return;
         }
       }
     });
-    FBuf in = std::make_shared<std::vector<float>>();
+    FBuf in = std::make_shared<Buf>();
     for (;;) {
       PSHeader h;
       if (!recv_all(fd, &h, sizeof(h)) || h.magic != kMagic) break;
-      if (in.use_count() > 1 || !in) in = std::make_shared<std::vector<float>>();
+      if (in.use_count() > 1 || !in) in = std::make_shared<Buf>();
       in->resize(h.n);
       if (h.n && !recv_all(fd, in->data(), h.n * sizeof(float))) break;
       nmsg++;
@@ -176,7 +198,7 @@ struct PServer::Impl {
             slot->s1.assign(in->size(), 0.f);
             slot->s2.assign(in->size(), 0.f);
             slot->w = std::move(in);
-            in = std::make_shared<std::vector<float>>();
+            in = std::make_shared<Buf>();
           }
           cv.notify_all();
           break;
@@ -185,7 +207,7 @@ struct PServer::Impl {
           PSEntry* e = find(h.id, true);
           if (!e) { r.flags = 1; break; }
           std::lock_guard<std::mutex> lk(e->mu);
-          out = e->w;  // shared, no copy
+          out = e->reply();  // shared, no copy
           break;
         }
         case kPSUpdate: {  // gradient -> server-side updater -> new value
@@ -200,17 +222,20 @@ struct PServer::Impl {
           if (h.f0 > 0.f) a.grad_scale = h.f0;
           OptUpdate(a, e->mut().data(), in->data(), e->s1.data(), e->s2.data(), (int64_t)in->size());
           e->nupdates++;
-          out = e->w;
+          out = e->reply();
           break;
         }
         case kPSReplace: {  // pm HandleUpdateMsg: replace, reply the value (param.cc:57-61)
           PSEntry* e = find(h.id, true);
           if (!e) { r.flags = 1; break; }
           std::lock_guard<std::mutex> lk(e->mu);
+          // the optimiser state (s1 / s2) is sized by the Put: a value of
+          // another size would let a later Update write past their end
+          if (e->w->size() != in->size()) { r.flags = 1; break; }
           e->w = std::move(in);  // the received buffer becomes the value and the reply: no copy
-          in = std::make_shared<std::vector<float>>();
+          in = std::make_shared<Buf>();
           e->nupdates++;
-          out = e->w;
+          out = e->reply();
           break;
         }
         case kPSElastic: {  // d = alpha (w_worker - c); c += d; reply d (param.cc:244-258)
@@ -218,7 +243,8 @@ struct PServer::Impl {
           if (!e) { r.flags = 1; break; }
           std::lock_guard<std::mutex> lk(e->mu);
           if (e->w->size() != in->size()) { r.flags = 1; break; }
-          out = std::make_shared<std::vector<float>>(in->size());
+          out = std::make_shared<Buf>(in->size());
+          out->inflight.store(1, std::memory_order_relaxed);  // a fresh reply buffer: counted like a shared one
           const float alpha = h.f0;
           float* c = e->mut().data();
           const float* wv = in->data();
@@ -236,7 +262,11 @@ struct PServer::Impl {
           if (!e) { r.flags = 1; break; }
           std::lock_guard<std::mutex> lk(e->mu);
           const int64_t n = (int64_t)e->w->size();
-          out = std::make_shared<std::vector<float>>(in->size());
+          // untrusted progression: an empty value (modulo by zero) or a / b
+          // outside [0, n) (negative indices) is rejected
+          if (n == 0 || h.a < 0 || h.a >= n || h.b < 0 || h.b >= n) { r.flags = 1; break; }
+          out = std::make_shared<Buf>(in->size());
+          out->inflight.store(1, std::memory_order_relaxed);  // a fresh reply buffer: counted like a shared one
           std::vector<float>& c = e->mut();
           // the sample is the progression idx_i = (a + i*b) mod n shared by
           // every rank (parallel/easgd.py RandomSync): no index traffic
@@ -270,6 +300,9 @@ struct PServer::Impl {
     }
     qcv.notify_one();
     writer.join();
+    for (auto& it : q)  // replies never sent (the connection failed): release their buffers
+      if (it.second) it.second->inflight.fetch_sub(1, std::memory_order_release);
+    q.clear();
     {
       // forget the fd BEFORE closing it: Close() must never shut down a
       // number the kernel has already handed to another socket
@@ -336,7 +369,7 @@ bool PServer::WaitStop(double timeout_s) {
   const auto until = std::chrono::steady_clock::now() + std::chrono::duration<double>(timeout_s);
   while (d_->nstop < d_->nworkers) {
     if (timeout_s >= 0 && std::chrono::steady_clock::now() >= until) return false;
-    d_->cv.wait_for(lk, std::chrono::milliseconds(100));
+    d_->cv.wait_until(lk, std::chrono::system_clock::now() + std::chrono::milliseconds(100));
   }
   return true;
 }
@@ -442,6 +475,9 @@ uint64_t PSClient::Request(const PSHeader& h, const float* data, float* out, uin
   if (!Recv(s, &r, out, cap)) throw std::runtime_error("PSClient: receive failed");
   if (r.flags) throw std::runtime_error("PSClient: server rejected request type " + std::to_string(h.type) +
                                         " for key " + std::to_string(h.id));
+  if (out && r.n > cap)  // the payload was drained (stream stays in sync) but not delivered
+    throw std::runtime_error("PSClient: reply of " + std::to_string(r.n) + " floats exceeds the " +
+                             std::to_string(cap) + "-float buffer for key " + std::to_string(h.id));
   return r.n;
 }
 
@@ -492,16 +528,21 @@ int PSClient::Collect(const std::vector<float*>& outs, const std::vector<uint64_
   std::map<int, size_t> where;
   for (size_t i = 0; i < ids.size(); ++i) where[ids[i]] = i;
   int got = 0;
+  std::string err;  // every pending reply is drained first, then a rejection / overflow is reported
   for (size_t s = 0; s < fds_.size(); ++s) {
     for (int id : pending_[s]) {
       auto it = where.find(id);
       PSHeader r;
       const bool ok = it != where.end() ? Recv(s, &r, outs[it->second], caps[it->second]) : Recv(s, &r, nullptr, 0);
       if (!ok) throw std::runtime_error("PSClient: collect failed");
+      if (err.empty() && r.flags) err = "PSClient: server rejected a pushed request for key " + std::to_string(id);
+      if (err.empty() && it != where.end() && r.n > caps[it->second])
+        err = "PSClient: reply for key " + std::to_string(id) + " exceeds its buffer";
       got++;
     }
     pending_[s].clear();
   }
+  if (!err.empty()) throw std::runtime_error(err);
   return got;
 }
 

@@ -59,13 +59,15 @@ class Device:
         if self.torch_device.type != "cuda":
             return None
         if getattr(self, "_rng_epoch", None) is None:
-            self._rng_epoch = torch.zeros(1, dtype=torch.int64, device=self.torch_device)
+            from .ops import glue as G
+            self._rng_epoch = G.zeros((1,), torch.int64, self.torch_device)
         return self._rng_epoch
 
     def advance_rng_epoch(self) -> None:
         ep = self.rng_epoch()
         if ep is not None:
-            ep.add_(1)
+            from .ops import glue as G
+            G.iadd_(ep, 1)
 
     def EnableGraph(self, enable: bool) -> None:
         self.graph_enabled = bool(enable)

@@ -18,6 +18,7 @@ import numpy as np
 import torch
 
 from . import autograd
+from .ops import glue as G
 from . import device as _dev
 from .tensor import Tensor
 
@@ -142,9 +143,9 @@ class Layer:
             src = v
         else:
             src = torch.as_tensor(np.asarray(v))
-        dst.data.copy_(src.reshape(dst.shape).to(device=dst.data.device, dtype=dst.dtype))
+        G.copy_(dst.data, src.reshape(dst.shape))
         if dst.low is not None:
-            dst.low.copy_(dst.data.to(dst.low.dtype))
+            G.copy_(dst.low, dst.data)
 
     def set_params(self, parameters: Dict[str, Tensor]) -> None:
         own = self.get_params()
@@ -283,12 +284,12 @@ class BatchNorm2d(Layer):
         C = x.shape[1]
         dev = x.device
         s = _new_param((C,), dev)
-        s.data.fill_(1.0)
+        G.fill_(s.data, 1.0)
         self._param("scale", s, wd_mult=0.0)
         self._param("bias", _new_param((C,), dev), wd_mult=0.0)
         self._state("running_mean", Tensor((C,), dev, requires_grad=False))
         rv = Tensor((C,), dev, requires_grad=False)
-        rv.data.fill_(1.0)
+        G.fill_(rv.data, 1.0)
         self._state("running_var", rv)
 
     def forward(self, x, relu: bool = False, residual: Optional[Tensor] = None):
@@ -307,7 +308,7 @@ class LayerNorm(Layer):
     def initialize(self, x):
         D = x.shape[-1]
         g = _new_param((D,), x.device)
-        g.data.fill_(1.0)
+        G.fill_(g.data, 1.0)
         self._param("scale", g, wd_mult=0.0)
         self._param("bias", _new_param((D,), x.device), wd_mult=0.0)
 
@@ -461,7 +462,8 @@ class SoftMaxCrossEntropy(Layer):
 
     def accuracy(self) -> Optional[torch.Tensor]:
         """fp32 device tensor: fraction of the last batch within top-k."""
-        return self.last_op.correct.mean() if self.last_op is not None else None
+        return G.reduce(self.last_op.correct, None, "mean", out_dtype=torch.float32) if self.last_op is not None \
+            else None
 
 
 class MeanSquareError(Layer):

@@ -17,6 +17,23 @@ import torch
 
 from .. import autograd, layer, model
 from ..tensor import Tensor
+from ..ops import glue as G
+
+
+_IDS: dict = {}
+
+
+def _const_ids(S: int, device, kind: str) -> torch.Tensor:
+    """[1, S] position ids (0..S-1) or zero type ids, built once per (S,
+    device) on the host and uploaded (a plain DMA copy): the step launches
+    no kernel for them."""
+    key = (S, str(device), kind)
+    t = _IDS.get(key)
+    if t is None:
+        import numpy as np
+        h = np.arange(S, dtype=np.int64)[None] if kind == "pos" else np.zeros((1, S), np.int64)
+        t = _IDS[key] = torch.from_numpy(h).to(device)
+    return t
 
 
 class SplitHeads(autograd.Operator):
@@ -30,14 +47,14 @@ class SplitHeads(autograd.Operator):
         B, S, E3 = x.shape
         D = E3 // (3 * self.h)
         # one permuting copy; q, k, v are contiguous slices of it
-        t = x.view(B, S, 3, self.h, D).permute(2, 0, 3, 1, 4).contiguous()
+        t = G.contiguous(x.view(B, S, 3, self.h, D).permute(2, 0, 3, 1, 4))
         return t[0], t[1], t[2]
 
     def backward(self, dq, dk, dv):
         ref = next(d for d in (dq, dk, dv) if d is not None)
         B, H, S, D = ref.shape
-        parts = [d if d is not None else torch.zeros_like(ref) for d in (dq, dk, dv)]
-        return torch.stack(parts, 0).permute(1, 3, 0, 2, 4).reshape(B, S, 3 * H * D)
+        parts = [(d if d is not None else G.zeros_like(ref)).unsqueeze(0) for d in (dq, dk, dv)]
+        return G.reshape(G.contiguous(G.cat(parts, 0).permute(1, 3, 0, 2, 4)), (B, S, 3 * H * D))
 
 
 class MergeHeads(autograd.Operator):
@@ -45,12 +62,12 @@ class MergeHeads(autograd.Operator):
 
     def forward(self, x):
         B, H, S, D = x.shape
-        return x.permute(0, 2, 1, 3).reshape(B, S, H * D)
+        return G.reshape(G.contiguous(x.permute(0, 2, 1, 3)), (B, S, H * D))
 
     def backward(self, dy):
         B, S, E = dy.shape
         H = self.h
-        return dy.view(B, S, H, E // H).permute(0, 2, 1, 3).contiguous()
+        return G.contiguous(G.reshape(dy, (B, S, H, E // H)).permute(0, 2, 1, 3))
 
     def __call__(self, x):
         self.h = x.shape[1]
@@ -99,12 +116,10 @@ class Embeddings(layer.Layer):
         B, S = ids.shape
         # [1, S] position / type ids broadcast over the batch (an exported
         # ONNX graph stays batch-size independent)
-        pos = Tensor(data=torch.arange(S, device=ids.data.device).unsqueeze(0), device=ids.device,
-                     requires_grad=False)
+        pos = Tensor(data=_const_ids(S, ids.data.device, "pos"), device=ids.device, requires_grad=False)
         e = autograd.add(autograd.embedding(ids, self.word), autograd.embedding(pos, self.position))
         if types is None:
-            types = Tensor(data=torch.zeros((1, S), dtype=torch.int64, device=ids.data.device), device=ids.device,
-                           requires_grad=False)
+            types = Tensor(data=_const_ids(S, ids.data.device, "zero"), device=ids.device, requires_grad=False)
         e = autograd.add(e, autograd.embedding(types, self.token_type))
         return self.drop(self.ln(e))
 
@@ -129,8 +144,9 @@ class Bert(model.Model):
         m = None
         if mask is not None:  # [B, S] of 1/0 -> additive [B, 1, 1, S]
             md = mask.data if isinstance(mask, Tensor) else mask
-            m = Tensor(data=((1.0 - md.float()) * -10000.0).view(md.shape[0], 1, 1, md.shape[1]), device=ids.device,
-                       requires_grad=False)
+            add = G.binary("mul", G.binary("sub", G.full((), 1.0, torch.float32, md.device), G.to(md, torch.float32)),
+                           -10000.0)
+            m = Tensor(data=add.view(md.shape[0], 1, 1, md.shape[1]), device=ids.device, requires_grad=False)
         for blk in self.encoder:
             x = blk(x, m)
         return x
@@ -152,11 +168,11 @@ class TorchCLS(autograd.Operator):
 
     def forward(self, x):
         self.shape = x.shape
-        return x[:, 0].contiguous()
+        return G.contiguous(x[:, 0])
 
     def backward(self, dy):
-        dx = torch.zeros(self.shape, dtype=dy.dtype, device=dy.device)
-        dx[:, 0] = dy
+        dx = G.zeros(self.shape, dy.dtype, dy.device)
+        G.copy_(dx[:, 0], dy)
         return dx
 
 

@@ -26,6 +26,7 @@ from .. import autograd, layer, model
 from ..ops import functional as F
 from ..ops import native as N
 from ..tensor import Tensor
+from ..ops import glue as G
 
 
 class InputPrep(autograd.Operator):
@@ -45,9 +46,9 @@ class InputPrep(autograd.Operator):
                 N.lib().nchw_to_nhwc_pad(x.data_ptr(), y.data_ptr(), x.shape[0], C, x.shape[2], x.shape[3], cp,
                                          N.stream())
                 return y
-            return F.to_nhwc_bf16(x, cp) if self.dtype == torch.bfloat16 else x.to(
-                memory_format=torch.channels_last)
-        return x.to(self.dtype) if x.dtype != self.dtype else x
+            return F.to_nhwc_bf16(x, cp) if self.dtype == torch.bfloat16 else G.to(
+                x, memory_format=torch.channels_last)
+        return G.to(x, self.dtype) if x.dtype != self.dtype else x
 
     def backward(self, dy):
         return None
@@ -106,9 +107,9 @@ class PairedStemConv(autograd.Operator):
         L.nchw_to_pairs(x.data_ptr(), xp.data_ptr(), Nn, C, H, Wd, N.stream())
         p = self.params[1] if len(self.params) > 1 else None
         low = p.low if p is not None else None
-        wk = (low if low is not None else W.to(torch.bfloat16)).permute(0, 2, 3, 1).reshape(-1)  # KRSC flat
+        wk = G.reshape((low if low is not None else G.to(W, torch.bfloat16)).permute(0, 2, 3, 1), (-1,))  # KRSC
         fwd, bwd = _pair_maps(K, C, x.device)
-        wp = torch.cat([wk, wk.new_zeros(1)])[fwd]
+        wp = G.index_select(G.cat([wk, G.zeros((1,), torch.bfloat16, x.device)]), 0, fwd)
         Ho, Wo = (H + 6 - 7) // 2 + 1, (Wd + 6 - 7) // 2 + 1
         y = torch.empty((Nn, K, Ho, Wo), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
         ws, rows = None, 0
@@ -130,17 +131,17 @@ class PairedStemConv(autograd.Operator):
         Nn, C, H, Wd, K, Ho, Wo = self.shape
         xp, self.xp = self.xp, None
         if not (dy.dtype == torch.bfloat16 and N.is_cl(dy)):
-            dy = dy.to(dtype=torch.bfloat16, memory_format=torch.channels_last)
-        dwp = torch.zeros(K * 7 * 4 * 8, dtype=torch.float32, device=dy.device)
+            dy = G.to(dy, torch.bfloat16, torch.channels_last)
+        dwp = G.zeros((K * 7 * 4 * 8,), torch.float32, dy.device)
         L.conv_wgrad(xp.data_ptr(), dy.data_ptr(), dwp.data_ptr(), Nn, H, Wd + 1, 8, K, 7, 4, Ho, Wo, 2, 2, 3, 2, 1,
                      2, 0, N.stream())
         _, bwd = _pair_maps(K, C, dy.device)
-        dw = dwp[bwd].view(K, 7, 7, C).permute(0, 3, 1, 2)  # logical KCRS
+        dw = G.index_select(dwp, 0, bwd).view(K, 7, 7, C).permute(0, 3, 1, 2)  # logical KCRS
         tgt = self.grad_target(1)
         if tgt is not None:
-            tgt.add_(dw)
+            G.binary("add", tgt, dw, out=tgt)
             return None, autograd.ACCUMULATED
-        return None, dw.contiguous()
+        return None, G.contiguous(dw)
 
 
 class StemConv2d(layer.Conv2d):

@@ -750,6 +750,7 @@ FUSE_RES_BN_BWD = os.environ.get("SINGA_AMD_FUSE_RES_BN_BWD", "0") == "1"
 
 
 _WT_CACHE: dict = {}
+_WT_RETIRED: list = []
 
 
 def pretranspose_conv_weights(items) -> dict:
@@ -766,10 +767,15 @@ def pretranspose_conv_weights(items) -> dict:
             sel.append((key, w))
     if len(sel) < 2 or not DGRAD_KMAJOR:
         return {}
-    sig = tuple((w.data_ptr(),) + tuple(w.shape) for _, w in sel)
+    # one scratch per (weight set, stream): replica threads sharing the
+    # weights run on their own streams and must not write each other's copy
+    sig = tuple((w.data_ptr(),) + tuple(w.shape) for _, w in sel) + (N.stream(),)
     ent = _WT_CACHE.get(sig)
     if ent is None:
         if len(_WT_CACHE) > 8:
+            # a captured HIP graph may still replay into an evicted entry's
+            # scratch / descriptor table: retire (keep alive), never free
+            _WT_RETIRED.extend(_WT_CACHE.values())
             _WT_CACHE.clear()
         dev = sel[0][1].device
         sizes = [w.numel() for _, w in sel]

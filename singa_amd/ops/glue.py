@@ -145,6 +145,38 @@ def fill_(t: torch.Tensor, value: float) -> torch.Tensor:
     return t
 
 
+def zero_(t: torch.Tensor) -> torch.Tensor:
+    return fill_(t, 0.0)
+
+
+def iadd_(t: torch.Tensor, v: int) -> torch.Tensor:
+    """In-place integer increment of a dense int64 device counter."""
+    if on_gpu(t) and t.dtype == torch.int64 and t.is_contiguous():
+        _lib().iadd_i64(t.data_ptr(), t.numel(), int(v), N.stream())
+        return t
+    return t.add_(v)
+
+
+def random_(t: torch.Tensor, dist: str, a: float, b: float, device_obj=None) -> torch.Tensor:
+    """Fill t with uniform [a, b) or gaussian (mean a, std b) samples: the
+    Philox kernel on the GPU (counters reserved from the SINGA device's
+    stream, reproducible per seed), the device's torch generator on the CPU."""
+    if on_gpu(t) and t.dtype in _FLOATS:
+        seed, off = device_obj.next_rng(t.numel()) if device_obj is not None else (0, 0)
+        d = t if t.is_contiguous() else torch.empty(t.shape, dtype=t.dtype, device=t.device)
+        if d.numel():
+            _lib().rand_fill(d.data_ptr(), d.numel(), N.dt(d), 0 if dist == "uniform" else 1, float(a), float(b),
+                             int(seed), int(off), N.stream())
+        return t if d is t else copy_(t, d)
+    gen = device_obj.generator if device_obj is not None else None
+    d = torch.empty(t.shape, dtype=torch.float32, device=t.device)
+    if dist == "uniform":
+        d.uniform_(a, b, generator=gen)
+    else:
+        d.normal_(a, b, generator=gen)
+    return t.copy_(d)
+
+
 def full(shape, value, dtype, device, memory_format=torch.contiguous_format) -> torch.Tensor:
     t = torch.empty(tuple(shape), dtype=dtype, device=device, memory_format=memory_format)
     if t.is_cuda and N.force_native():
@@ -169,10 +201,8 @@ def binary(op: str, a: torch.Tensor, b, out_dtype: Optional[torch.dtype] = None,
            out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """alpha * (a OP b) with NumPy broadcasting; comparisons / logic give 0/1
     in the float dtype.  b may be a Python scalar."""
-    if not isinstance(b, torch.Tensor):
-        b = torch.tensor(float(b), dtype=a.dtype if a.is_floating_point() else torch.float32)
-        if a.is_cuda:
-            b = b.to(a.device)  # a 4-byte H2D copy
+    if not isinstance(b, torch.Tensor):  # a scalar: a fill kernel on the GPU (graph-capturable, no H2D copy)
+        b = full((), float(b), a.dtype if a.is_floating_point() else torch.float32, a.device)
     dt = a.dtype if a.dtype == b.dtype else (torch.float32 if torch.float32 in (a.dtype, b.dtype) else a.dtype)
     if on_gpu(a, b) and dt in _FLOATS and a.is_cuda and b.is_cuda:
         a = to(a, dt) if a.dtype != dt else a

@@ -29,6 +29,7 @@ import numpy as np
 import torch
 
 from . import autograd
+from .ops import glue as G
 from .ops import native as N
 from .tensor import Tensor
 
@@ -134,22 +135,22 @@ class ParamStore:
             self.offsets.append(off)
             off += (p.data.numel() + ALIGN - 1) // ALIGN * ALIGN
         self.numel = off
-        self.w = torch.zeros(off, dtype=torch.float32, device=dev)
-        self.g = torch.zeros(off, dtype=torch.float32, device=dev)
-        self.low = torch.zeros(off, dtype=torch.bfloat16, device=dev) if mixed_bf16 else None
-        self.s1 = torch.zeros(off, dtype=torch.float32, device=dev) if state_slots >= 1 else None
-        self.s2 = torch.zeros(off, dtype=torch.float32, device=dev) if state_slots >= 2 else None
+        self.w = G.zeros((off,), torch.float32, dev)
+        self.g = G.zeros((off,), torch.float32, dev)
+        self.low = G.zeros((off,), torch.bfloat16, dev) if mixed_bf16 else None
+        self.s1 = G.zeros((off,), torch.float32, dev) if state_slots >= 1 else None
+        self.s2 = G.zeros((off,), torch.float32, dev) if state_slots >= 2 else None
         self.mixed = mixed_bf16
         for p, o in zip(self.params, self.offsets):
             n = p.data.numel()
-            src = p.data.detach().to(torch.float32)
+            src = p.data.detach()
             wv = self._view(self.w, o, p.data.shape)
-            wv.copy_(src)
+            G.copy_(wv, src)
             p.data = wv
             p.grad_view = self._view(self.g, o, p.data.shape)
             if self.low is not None:
                 p.low = self._view(self.low, o, p.data.shape)
-                p.low.copy_(wv)
+                G.copy_(p.low, wv)
         self._build_chunks()
 
     def _view(self, flat: torch.Tensor, off: int, shape) -> torch.Tensor:
@@ -191,11 +192,11 @@ class ParamStore:
                 self.mask[o:o + n] = True
 
     def zero_grad(self):
-        self.g.zero_()
+        G.zero_(self.g)
 
     def sync_low(self):
         if self.low is not None:
-            self.low.copy_(self.w)
+            G.copy_(self.low, self.w)
 
     def param_range(self, i: int):
         return self.offsets[i], self.params[i].data.numel()
@@ -263,7 +264,7 @@ class Optimizer:
         self.store = ParamStore(params, mixed_bf16=mixed_bf16, state_slots=2 if self.kind in (
             "adam", "adadelta") else 1, channels_last=channels_last)
         dev = self.store.device
-        self._hp_dev = torch.zeros(4, dtype=torch.float32, device=dev)
+        self._hp_dev = G.zeros((4,), torch.float32, dev)
         self._hp_host = torch.zeros(4, dtype=torch.float32, pin_memory=dev.type == "cuda")
         self.prepare_step()
         return self.store
@@ -279,8 +280,8 @@ class Optimizer:
         # two scalar fill kernels: the values travel as kernel arguments, so
         # the host can run ahead of the GPU without racing a pinned staging
         # buffer that an earlier, still-queued async copy would read later
-        self._hp_dev[0].fill_(self.current_lr())
-        self._hp_dev[1].fill_(float(self.step_counter + 1))
+        G.fill_(self._hp_dev[0], self.current_lr())
+        G.fill_(self._hp_dev[1], float(self.step_counter + 1))
 
     # -- SINGA API -----------------------------------------------------------
     def __call__(self, loss: Tensor) -> None:

@@ -25,6 +25,7 @@ import torch
 from .. import autograd
 from ..autograd import Operator, _next_seq
 from ..tensor import Tensor
+from ..ops import glue as G
 
 _MAXD = 8
 _DT = [torch.float32, torch.bfloat16, torch.float16, torch.int32, torch.int64, torch.uint8]
@@ -71,7 +72,7 @@ class BridgeSend(Operator):
             raise ValueError(f"bridge payloads support at most {_MAXD} dims")
         shp = list(x.shape) + [0] * (_MAXD - x.dim())
         hdr = torch.tensor([_code(x.dtype), int(self.requires_grad), x.dim()] + shp, dtype=torch.int64)
-        payload = x.contiguous()
+        payload = G.contiguous(x)
         dev_hdr = hdr.to(x.device)
         self.pending.append((self.comm.isend(dev_hdr, self.peer), dev_hdr))
         self.pending.append((self.comm.isend(payload, self.peer), payload))
@@ -124,8 +125,8 @@ class BridgeRecv(Operator):
 
     def backward(self, dy=None):
         if dy is None:
-            dy = torch.zeros(self.shape, dtype=self.dtype, device=self.dev.torch_device)
-        dy = dy.to(self.dtype).contiguous()
+            dy = G.zeros(self.shape, self.dtype, self.dev.torch_device)
+        dy = G.contiguous(G.to(dy, self.dtype))
         self.pending.append((self.comm.isend(dy, self.peer), dy))
         return ()
 

@@ -33,6 +33,7 @@ from typing import List, Optional, Sequence
 
 import numpy as np
 import torch
+from ..ops import glue as G
 
 
 def _core():
@@ -176,7 +177,7 @@ class PSSync:
 
     def _push_from_host(self, i: int) -> None:
         o, n = self.store.param_range(i)
-        self.store.w[o:o + n].copy_(torch.from_numpy(self._host[i]).to(self.store.w.device))
+        G.copy_(self.store.w[o:o + n], torch.from_numpy(self._host[i]))
 
     def bootstrap(self) -> None:
         """Group 0 Puts every parameter, the other groups Get them (blocking
@@ -185,7 +186,10 @@ class PSSync:
             if self.group_id == 0:
                 self.client.put(self.key_base + i, self._pull_to_host(i))
             else:
-                self.client.get(self.key_base + i, self._host[i])
+                got = self.client.get(self.key_base + i, self._host[i])
+                if got != self._host[i].size:
+                    raise RuntimeError(f"PSSync.bootstrap: key {self.key_base + i} holds {got} floats, "
+                                       f"parameter {i} has {self._host[i].size}")
                 self._push_from_host(i)
         self._snap = [h.copy() for h in self._host]
         self.store.sync_low()

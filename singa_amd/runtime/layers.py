@@ -22,6 +22,8 @@ import torch
 
 from .. import autograd
 from ..config import schema
+from ..ops import functional as F
+from ..ops import glue as G
 from ..tensor import Tensor
 from .param import make_param
 
@@ -301,7 +303,14 @@ class MnistImageLayer(RefLayer):
         return out[:, 0]
 
     def forward(self, xs, training):
-        img = xs[0]["image"].data.float()
+        img = G.to(xs[0]["image"].data, torch.float32)
+        aug = training and (self.gamma > 0 or self.beta > 0 or (self.alpha > 0 and self.kernel > 0 and self.sigma > 0))
+        dev = img.device
+        if img.is_cuda and (aug or (self.resize and tuple(img.shape[-2:]) != (self.resize, self.resize))):
+            # resize / affine / elastic augmentation is host-side preprocessing
+            # (the reference's CPU parser, src/worker/layer.cc:382-473); the
+            # result is uploaded with one DMA copy
+            img = img.cpu()
         if self.resize and tuple(img.shape[-2:]) != (self.resize, self.resize):
             img = torch.nn.functional.interpolate(img.reshape(img.shape[0], 1, *img.shape[-2:]),
                                                   size=(self.resize, self.resize), mode="bilinear",
@@ -309,9 +318,14 @@ class MnistImageLayer(RefLayer):
                                                                                self.resize)
         if training:
             lab = xs[0].get("label") if isinstance(xs[0], dict) else None
-            img = self._deform(img, lab.data if lab is not None else None)
+            img = self._deform(img, lab.data.cpu() if lab is not None and img.device.type == "cpu" and lab.data.is_cuda
+                               else (lab.data if lab is not None else None))
             self.nbatch += 1
-        return Tensor(device=self.dev, data=img / self.norm_a - self.norm_b, requires_grad=False)
+        if img.device != dev:
+            img = img.to(dev)
+        # x / norm_a - norm_b
+        out = F.unary("adds", F.unary("scale", img, 1.0 / self.norm_a), -float(self.norm_b))
+        return Tensor(device=self.dev, data=out, requires_grad=False)
 
 
 @register("kRGBImage")
@@ -328,7 +342,7 @@ class RGBImageLayer(RefLayer):
         return self.shape
 
     def forward(self, xs, training):
-        img = xs[0]["image"].data.float()
+        img = G.to(xs[0]["image"].data, torch.float32)
         if self.crop:
             H, W = img.shape[-2:]
             if training:
@@ -336,9 +350,16 @@ class RGBImageLayer(RefLayer):
             else:
                 h0, w0 = (H - self.crop) // 2, (W - self.crop) // 2
             img = img[..., h0:h0 + self.crop, w0:w0 + self.crop]
-        if self.mirror and training and self.rng.randint(2):
-            img = torch.flip(img, dims=[-1])
-        return Tensor(device=self.dev, data=(img * self.scale).contiguous(), requires_grad=False)
+        if self.mirror and training and self.rng.randint(2):  # horizontal mirror: a reversed-index gather
+            W = img.shape[-1]
+            key = (W, str(img.device))
+            rev = self._rev.get(key) if hasattr(self, "_rev") else None
+            if rev is None:
+                self._rev = getattr(self, "_rev", {})
+                rev = self._rev[key] = torch.arange(W - 1, -1, -1, dtype=torch.int64).to(img.device)
+            img = G.index_select(img, img.dim() - 1, rev)
+        return Tensor(device=self.dev, data=F.unary("scale", G.contiguous(img), float(self.scale)),
+                      requires_grad=False)
 
 
 @register("kLabel")
@@ -488,7 +509,8 @@ class SoftmaxLossLayer(RefLayer):
             x = autograd.reshape(x, (x.shape[0], -1))
         op = autograd.SoftMaxCrossEntropy(topk=self.topk)
         loss = op(x, lab)
-        self.metric = (loss.data.detach() * self.scale, op.correct.mean() * self.scale)
+        self.metric = (F.unary("scale", loss.data.detach(), float(self.scale)),
+                       F.unary("scale", G.reduce(op.correct, None, "mean", out_dtype=torch.float32), float(self.scale)))
         s = self.scale * self.loss_scale
         if s != 1.0:
             loss = autograd.mul(loss, s)
@@ -546,7 +568,7 @@ class ConcateLayer(RefLayer):
     def forward(self, xs, training):
         if any(x.requires_grad for x in xs):
             return autograd.cat(xs, self.dim)
-        return Tensor(device=xs[0].device, data=torch.cat([x.data for x in xs], self.dim), requires_grad=False)
+        return Tensor(device=xs[0].device, data=G.cat([x.data for x in xs], self.dim), requires_grad=False)
 
 
 @register("kBridgeSrc")

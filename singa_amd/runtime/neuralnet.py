@@ -26,6 +26,8 @@ import torch
 
 from .. import autograd
 from ..config import schema
+from ..ops import functional as F
+from ..ops import glue as G
 from ..tensor import Tensor
 from .layers import RefLayer, create_layer
 
@@ -311,12 +313,12 @@ class NeuralNet:
                     continue
                 w = base.params[0].data
                 if base.type_name == "kConvolution":
-                    layer.params[0].data.copy_(w[off:off + layer.nf])
+                    G.copy_(layer.params[0].data, w[off:off + layer.nf])
                 else:
-                    layer.params[0].data.copy_(w[:, off:off + layer.hdim])
+                    G.copy_(layer.params[0].data, w[:, off:off + layer.hdim])
                 if len(base.params) > 1:
                     nb = layer.params[1].shape[0]
-                    layer.params[1].data.copy_(base.params[1].data[off:off + nb])
+                    G.copy_(layer.params[1].data, base.params[1].data[off:off + nb])
             else:
                 shapes[layer.name] = layer.setup(src_shapes, self._dev_of(layer.locationid), self.gen)
         self.layers = new_layers
@@ -377,7 +379,7 @@ class NeuralNet:
                 if not self.is_local(src):
                     y = B.BridgeRecv(self.comm, self._rank_of(src.locationid), self._pending)(ldev)
                     if y.requires_grad:
-                        self._extra_roots.append((y, torch.zeros_like(y.data)))
+                        self._extra_roots.append((y, G.zeros_like(y.data)))
                     outs[l.name] = y
                     continue
             xs = []
@@ -448,18 +450,18 @@ class NeuralNet:
             return
         held = {id(p) for p in self.params()}
         total = sum(k[2] for k in keys)
-        buf = torch.zeros(total, dtype=torch.float32, device=self.dev.torch_device)
+        buf = G.zeros((total,), torch.float32, self.dev.torch_device)
         o = 0
         spans = []
         for base, i, n in keys:
             p = base.params[i]
             if id(p) in held and p.grad_view is not None:
-                buf[o:o + n].copy_(p.grad_view.reshape(-1))
+                G.copy_(buf[o:o + n], G.reshape(p.grad_view, (-1,)))
                 spans.append((p, o, n))
             o += n
         self.comm.all_reduce(buf)
         for p, o, n in spans:
-            p.grad_view.copy_(buf[o:o + n].reshape(p.grad_view.shape))
+            G.copy_(p.grad_view, buf[o:o + n].reshape(p.grad_view.shape))
 
     def total_loss(self, outs) -> Optional[Tensor]:
         losses = [outs[l.name] for l in self.loss_layers()]
@@ -531,14 +533,17 @@ class NeuralNet:
         """norm1 (mean |x|) of every layer output and parameter (reference
         NeuralNet::DebugInfo; Blob::asum_data is a mean, Appendix A #14)."""
         lines = []
+
+        def norm1(t):
+            return float(G.reduce(F.unary("abs", G.to(t, torch.float32)), None, "mean", out_dtype=torch.float32))
         for l in self.layers:
             o = getattr(self, "outputs", {}).get(l.name)
             if isinstance(o, Tensor):
-                lines.append(f"layer {l.name} data norm1 {o.data.float().abs().mean().item():.6f}")
+                lines.append(f"layer {l.name} data norm1 {norm1(o.data):.6f}")
             for p in l.params:
                 g = p.grad_view
-                gs = f" grad norm1 {g.float().abs().mean().item():.6f}" if g is not None else ""
-                lines.append(f"param {p.name} data norm1 {p.data.float().abs().mean().item():.6f}{gs}")
+                gs = f" grad norm1 {norm1(g):.6f}" if g is not None else ""
+                lines.append(f"param {p.name} data norm1 {norm1(p.data):.6f}{gs}")
         return "\n".join(lines)
 
     def __repr__(self):

@@ -85,7 +85,8 @@ def init_param(t: Tensor, proto, fan_in: int = 0, generator: Optional[torch.Gene
         d.copy_(src[proto.name].reshape(shape).float())
     else:
         raise ValueError(f"unknown init method {method}")
-    t.data.copy_(d.to(t.data.device).reshape(t.data.shape))
+    from ..ops import glue as G
+    G.copy_(t.data, d.reshape(t.data.shape))  # host init + one DMA upload (the native layout pass if strided)
 
 
 def make_param(shape: Sequence[int], proto, dev, fan_in: int = 0, name: Optional[str] = None,

@@ -33,6 +33,7 @@ from ..device import Timer, get_default_device
 from ..parallel.communicator import Communicator, init_distributed
 from ..parallel.easgd import ElasticSync, RandomSync
 from ..parallel.ps import PSClient, PSSync, server_endpoints
+from ..ops import glue as G
 from .neuralnet import NeuralNet
 
 
@@ -192,7 +193,7 @@ class Worker:
         for i in range(1, k):
             r = NeuralNet(self.model.neuralnet, 1, "kTrain", self.dev, self.data_override,
                           seed=self.seed + self.cluster.groupid() + 7919 * i)
-            g = torch.zeros_like(self.store.g)
+            g = G.zeros_like(self.store.g)
             r.share_weights_private_grads(self.train_net, self.store, g)
             self.replicas.append(r)
             self.rep_grads.append(g)
@@ -229,7 +230,7 @@ class Worker:
             with ctx:
                 outs = net.forward(training=True)
                 roots, seeds = net.backward_roots(outs)
-                g.zero_()
+                G.zero_(g)
                 if roots:
                     for _ in autograd.backward(roots, seeds):
                         pass
@@ -269,7 +270,7 @@ class Worker:
                     cur.wait_stream(s)
             if not self.hogwild:
                 for g in self.rep_grads[1:]:
-                    self.store.g.add_(g)
+                    G.binary("add", self.store.g, g, out=self.store.g)
                 self.updater.update(grad_scale=1.0 / k)
             self.updater.step()
         self.timers["backward"] += tb.ms

@@ -1103,11 +1103,19 @@ class SingaRep:
         self.inits: Dict[str, Tensor] = OrderedDict()
         self._consts = set()
         weight_like = self._weight_inputs(g)
+        consumers: Dict[str, set] = {}
+        for nd in g.node:
+            for nm in nd.input:
+                consumers.setdefault(nm, set()).add(nd.op_type)
+        scalar_math = {"Add", "Mul", "Sub", "Div", "Pow"}
         for t in g.initializer:
             a = tensorproto_to_numpy(t)
-            # scalar initializers (GELU's sqrt(2) / 1 / 0.5, the attention
-            # scale) are constants even in a learnable position
-            is_param = trainable and a.dtype == np.float32 and t.name in weight_like and a.size > 1
+            # scalar initializers that only feed elementwise arithmetic (GELU's
+            # sqrt(2) / 1 / 0.5, the attention scale: what the fusion patterns
+            # consume) are constants; a one-element weight of any other op
+            # (a PRelu slope, a scale of a norm or a GEMM) stays learnable
+            scalar_const = a.size == 1 and consumers.get(t.name, set()) <= scalar_math
+            is_param = trainable and a.dtype == np.float32 and t.name in weight_like and not scalar_const
             ten = Tensor(device=self.device, data=torch.from_numpy(np.array(a, order="C")),
                          requires_grad=is_param, stores_grad=is_param)
             ten.name = t.name

@@ -7,7 +7,15 @@
 // Exercises every concurrent path of the runtime: several Prefetcher threads
 // (producer thread + consumer) over one shard folder, early destruction of a
 // Prefetcher while its producer is mid-batch, crash-tolerant append, split,
-// and the graph sort / JSON export.
+// the graph sort / JSON export, the threaded C++ updaters, the mmap LMDB
+// B+tree walker (argv[2]: a database written by tests/lmdb_writer.py), and the
+// parameter server under load: several client threads doing Put / Get /
+// Update / pipelined PushUpdate + Collect / Elastic / RandomSync on SHARED
+// keys, Gets deferred until another thread's Put, and kStop counting
+// (the reference's concurrency hot-spot, src/server/server.cc:45-214).
+#include <atomic>
+#include <chrono>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <string>
@@ -104,6 +112,113 @@ int main(int argc, char** argv) {
   auto order = g.Sort();
   CHECK(order.size() == 3 && order.front() == "data" && order.back() == "loss");
   CHECK(g.ToJson({0, 1, 0}).find("\"links\"") != std::string::npos);
+  // ---- threaded updaters: the pool split must equal one serial pass
+  {
+    const int64_t nn = 1 << 20;
+    std::vector<float> w(nn), w2, gr(nn), s1(nn, 0.f), s2(nn, 0.f), t1(nn, 0.f), t2(nn, 0.f);
+    for (int64_t i = 0; i < nn; ++i) {
+      w[i] = std::sin(0.001f * i);
+      gr[i] = std::cos(0.003f * i);
+    }
+    w2 = w;
+    UpdateArgs a;
+    a.kind = kAdam;
+    a.lr = 0.01f;
+    OptUpdate(a, w.data(), gr.data(), s1.data(), s2.data(), nn);
+    for (int64_t o = 0; o < nn; o += 4096)  // chunked calls: element-wise identical
+      OptUpdate(a, w2.data() + o, gr.data() + o, t1.data() + o, t2.data() + o, 4096);
+    for (int64_t i = 0; i < nn; i += 997) CHECK(w[i] == w2[i]);
+  }
+  // ---- LMDB reader: walk, count, decode, from two threads at once
+  if (argc > 2) {
+    std::vector<std::thread> lt;
+    std::vector<int64_t> cnt(2, 0);
+    for (int t = 0; t < 2; ++t)
+      lt.emplace_back([&, t] {
+        LmdbReader rd(argv[2]);
+        std::string k, v;
+        while (rd.Next(&k, &v)) {
+          ImageRecord rec;
+          bool enc = false;
+          CHECK(DecodeDatum(v, &rec, &enc));
+          cnt[t]++;
+        }
+        CHECK(cnt[t] == rd.Count());
+      });
+    for (auto& t : lt) t.join();
+    CHECK(cnt[0] == cnt[1] && cnt[0] > 0);
+  }
+  // ---- parameter server under concurrent clients
+  {
+    const int nthreads = 4, nkeys = 6, len = 4096, iters = 40;
+    PServer srv(0, nthreads);
+    UpdateArgs ua;
+    ua.kind = kSGDRef;
+    ua.momentum = 0.9f;
+    srv.SetUpdater(ua, "kFixed", 0.01, 0.0, 1, 0.5, 0.75);
+    const std::string ep = "127.0.0.1:" + std::to_string(srv.port());
+    std::atomic<int> puts_done{0};
+    std::vector<std::thread> cl;
+    for (int t = 0; t < nthreads; ++t) {
+      cl.emplace_back([&, t] {
+        PSClient c({ep});
+        std::vector<float> buf(len), out(len);
+        if (t == 0) {
+          // the Gets of the other threads on these keys may arrive first:
+          // the server defers them until this Put
+          std::this_thread::sleep_for(std::chrono::milliseconds(50));
+          for (int k = 0; k < nkeys; ++k) {
+            for (int i = 0; i < len; ++i) buf[i] = 0.001f * (k + 1) * i;
+            c.Put(k, buf.data(), len);
+          }
+          puts_done = 1;
+        } else {
+          CHECK(c.Get(t % nkeys, out.data(), len) == (uint64_t)len);  // deferred Get
+          CHECK(std::fabs(out[7] - 0.001f * (t % nkeys + 1) * 7) < 1e-6f);
+        }
+        while (!puts_done) std::this_thread::yield();
+        std::vector<float> g(len, 1e-3f * (t + 1)), old(64);
+        for (int it = 0; it < iters; ++it) {
+          const int k = (it + t) % nkeys;  // shared keys, overlapping across threads
+          switch (it % 4) {
+            case 0: c.Update(k, g.data(), out.data(), len, it, 1.f); break;
+            case 1: {  // pipelined pushes to every key, one Collect
+              std::vector<int> ids;
+              std::vector<std::vector<float>> outs(nkeys, std::vector<float>(len));
+              std::vector<float*> ptrs;
+              std::vector<uint64_t> caps;
+              for (int j = 0; j < nkeys; ++j) {
+                c.PushUpdate(j, g.data(), len, it, 1.f);
+                ids.push_back(j);
+                ptrs.push_back(outs[j].data());
+                caps.push_back(len);
+              }
+              CHECK(c.Collect(ptrs, caps, ids) == nkeys);
+              break;
+            }
+            case 2: {
+              CHECK(c.Get(k, buf.data(), len) == (uint64_t)len);
+              c.Elastic(k, buf.data(), len, 0.25f);
+              break;
+            }
+            default: {
+              std::vector<float> delta(64, 1e-4f);
+              c.RandomSync(k, delta.data(), old.data(), 64, (it * 7 + t) % len, 17);
+            }
+          }
+        }
+        c.Stop();
+      });
+    }
+    for (auto& t : cl) t.join();
+    CHECK(srv.WaitStop(30.0));
+    for (int k = 0; k < nkeys; ++k) {
+      auto v = srv.Value(k);
+      CHECK((int)v.size() == len);
+      for (float x : v) CHECK(std::isfinite(x));
+    }
+    srv.Close();
+  }
   std::printf("runtime selftest ok\n");
   return 0;
 }

@@ -178,3 +178,37 @@ def test_launcher_two_workers_one_native_server(tmp_path, ptype):
     assert "[server 0] has shut down" in r.stderr
     losses = [json.loads(l)["loss"] for l in mj.read_text().splitlines()]
     assert len(losses) == 5 and all(np.isfinite(losses))  # steps 1-5 (step 0 is the local warm-up)
+
+
+def test_ps_rejects_untrusted_requests(servers):
+    """Server-side validation of values read off the socket: a RandomSync
+    progression outside [0, n) or against an empty value, and a Replace that
+    would change a key's size (its optimiser state keeps the Put's size), are
+    rejected instead of indexing out of bounds; an oversized reply raises on
+    the client instead of leaving the buffer silently unchanged."""
+    (s,) = servers(1)
+    cl = PSClient([f"127.0.0.1:{s.port}"])
+    cl.put(0, np.arange(8, dtype=np.float32))
+    old = np.zeros(3, np.float32)
+    for a, b in ((-1, 1), (2, -3), (8, 1), (0, 9)):
+        with pytest.raises(RuntimeError, match="rejected"):
+            cl.random_sync(0, np.ones(3, np.float32), old, a, b)
+    cl.put(1, np.zeros(0, np.float32))
+    with pytest.raises(RuntimeError, match="rejected"):
+        cl.random_sync(1, np.ones(2, np.float32), np.zeros(2, np.float32), 0, 1)
+    # a size-changing Replace is rejected; the value and its optimiser state keep their size
+    cl.push_replace(0, np.ones(16, np.float32))
+    with pytest.raises(RuntimeError, match="rejected"):
+        cl.collect([0], [np.zeros(16, np.float32)])
+    np.testing.assert_allclose(s.value(0), np.arange(8))
+    s.set_updater("sgd_ref", momentum=0.9, base_lr=0.1)
+    w = np.zeros(8, np.float32)
+    cl.update(0, np.ones(8, np.float32), w)  # still the 8-float key: no overflow of s1
+    np.testing.assert_allclose(w, np.arange(8) - 0.1, rtol=1e-6)
+    # a reply larger than the caller's buffer is an error, not a silent no-op
+    small = np.zeros(4, np.float32)
+    with pytest.raises(RuntimeError, match="exceeds"):
+        cl.get(0, small)
+    # the connection stays usable (the payload was drained)
+    full = np.zeros(8, np.float32)
+    assert cl.get(0, full) == 8
