@@ -51,7 +51,6 @@ def main() -> int:
     args = ap.parse_args()
 
     import torch
-    import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -84,9 +83,10 @@ def main() -> int:
     tx = tensor.from_numpy(x, dev)
     ty = tensor.from_numpy(y, dev)
 
-    # 1 GPU: graph replay (no launch overhead).  N>1: eager, so each gradient
-    # bucket's RCCL all-reduce starts as soon as backward has produced it and
-    # overlaps the rest of the backward (a captured graph would defer it).
+    # 1 GPU: graph replay (no launch overhead).  N>1: eager by default (each
+    # gradient bucket's RCCL all-reduce is forked onto the comm stream as soon
+    # as backward has produced it); --graph captures the whole step including
+    # the forked all-reduces (the native communicator is capture-safe).
     use_graph = args.graph if args.graph is not None else world == 1
     m.compile([tx], is_train=True, use_graph=use_graph)
     m.train()
@@ -123,7 +123,7 @@ def main() -> int:
     elapsed = time.perf_counter() - t0
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev.torch_device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        comm.all_reduce(t, op="max")
         elapsed = float(t.item())
     final_loss = float(loss.data.float().item())
     ps = None
@@ -152,6 +152,7 @@ def main() -> int:
             "config": {"model": f"ResNet-{args.depth}", "global_batch": world * B, "seq_len": None,
                        "image": args.image, "parallelism": f"dp{world}",
                        "exec": "hipgraph" if use_graph else "eager", "optimizer": "SGD momentum 0.9 wd 1e-4",
+                       "comm": type(comm).__name__ if world > 1 else None,
                        "final_loss": round(final_loss, 4)},
         }
         if curve:
@@ -161,8 +162,12 @@ def main() -> int:
                                                    "speedup_vs_reference_1thread_1server", "note") if k in ps}
         print(json.dumps(rec), flush=True)
     if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+        comm.barrier()
+        if hasattr(comm, "destroy"):
+            comm.destroy()
+        else:
+            import torch.distributed as dist
+            dist.destroy_process_group()
     return 0
 
 

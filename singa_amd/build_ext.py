@@ -29,6 +29,7 @@ CSRC = PKG / "csrc"
 OBJ = PKG.parent / "build" / "obj"
 ARCH = os.environ.get("SINGA_AMD_ARCH", "gfx950")
 EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+ROCM_LIB = os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "lib")
 
 
 def _hipcc() -> str:
@@ -76,11 +77,18 @@ def build_kernels(force: bool = False, jobs: int = 8) -> Path:
     objs.append(bo)
     if force or _newer(b, bo, []):
         tasks.append([hipcc, "-O2", "-std=c++17", "-fPIC", *_py_includes(), "-c", str(b), "-o", str(bo)])
+    # native RCCL communicator (host code against librccl)
+    for c in sorted((CSRC / "comm").glob("*.cpp")):
+        co = OBJ / ("comm_" + c.stem + ".o")
+        objs.append(co)
+        if force or _newer(c, co, []):
+            tasks.append([hipcc, "-O2", "-std=c++17", "-fPIC", *_py_includes(), "-c", str(c), "-o", str(co)])
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         list(ex.map(_run, tasks))
     out = PKG / f"_C{EXT_SUFFIX}"
     if force or tasks or not out.exists():
-        _run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-o", str(out)])
+        _run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-o", str(out),
+              f"-L{ROCM_LIB}", "-lrccl", f"-Wl,-rpath,{ROCM_LIB}"])
     return out
 
 

@@ -127,11 +127,14 @@ void sg_pad_bwd(const void*, void*, int, int, const int64_t*, const int64_t*, co
                 hipStream_t);
 void sg_fill(void*, int64_t, int, double, hipStream_t);
 void sg_iadd_i64(void*, int64_t, int64_t, hipStream_t);
+void sg_kth_largest_abs(const void*, int64_t, int64_t, void*, void*, hipStream_t);
 void sg_clamp_affine(const void*, const void*, void*, int64_t, int, float, float, float, float, hipStream_t);
 void sg_set_tuning(int key, int value);
 void sg_bn_set_unroll(int);
 void sg_bn_set_rows_per_thread(int);
 }
+
+void register_rccl(py::module& m);  // csrc/comm/rccl_comm.cpp
 
 static void check_launch(const char* what) {
   hipError_t e = hipGetLastError();
@@ -141,6 +144,7 @@ static void check_launch(const char* what) {
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "singa_amd gfx950 HIP kernel library";
+  register_rccl(m);
 
   m.def("device_info", []() {
     py::dict d;
@@ -455,6 +459,9 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("fill", [](P p, int64_t n, int dt, double v, P s) { sg_fill(V(p), n, dt, v, S(s)); CHK("fill"); });
   m.def("iadd_i64", [](P p, int64_t n, int64_t v, P s) { sg_iadd_i64(V(p), n, v, S(s)); CHK("iadd_i64"); });
+  m.def("kth_largest_abs", [](P x, int64_t n, int64_t k, P out, P ws, P s) {
+    sg_kth_largest_abs(CV(x), n, k, V(out), V(ws), S(s)); CHK("kth_largest_abs");
+  });
   m.def("clamp_affine", [](P x, P dy, P out, int64_t n, int dt, float a, float b, float lo, float hi, P s) {
     sg_clamp_affine(CV(x), CV(dy), V(out), n, dt, a, b, lo, hi, S(s)); CHK("clamp_affine");
   });

@@ -307,6 +307,61 @@ __global__ void pad_bwd_k(const T* __restrict__ dy, float* __restrict__ dx, cons
   }
 }
 
+// ---- k-th largest |x| by radix select on the float bits (exact, on device,
+// no host synchronisation: the sparse-gradient threshold of DistOpt's top-K
+// exchange, replacing a full sort / kthvalue of the gradient every step).
+// Three histogram passes over bits [31:21], [20:10], [9:0] of |x| (the sign
+// cleared, non-negative floats order as unsigned ints); after each pass one
+// thread walks the bins from the top and fixes those bits of the answer.
+struct KthState {
+  uint32_t prefix;  // bits of the answer fixed so far
+  uint32_t k;       // rank still to find inside the current prefix (1 = largest)
+};
+__global__ void kth_init_k(KthState* st, uint32_t* hist, uint32_t k) {
+  for (int i = threadIdx.x; i < 2048; i += blockDim.x) hist[i] = 0;
+  if (threadIdx.x == 0) {
+    st->prefix = 0;
+    st->k = k;
+  }
+}
+__global__ void __launch_bounds__(256) kth_hist_k(const float* __restrict__ x, int64_t n, const KthState* st,
+                                                  int pass, uint32_t* __restrict__ hist) {
+  __shared__ uint32_t h[2048];
+  for (int i = threadIdx.x; i < 2048; i += blockDim.x) h[i] = 0;
+  __syncthreads();
+  const int shift = pass == 0 ? 21 : pass == 1 ? 10 : 0;
+  const uint32_t bmask = pass == 2 ? 0x3FFu : 0x7FFu;
+  const uint32_t pmask = pass == 0 ? 0u : pass == 1 ? 0xFFE00000u : 0xFFFFFC00u;
+  const uint32_t pre = st->prefix & pmask;
+  SG_GRID_STRIDE(i, n) {
+    const uint32_t b = __float_as_uint(x[i]) & 0x7FFFFFFFu;
+    if ((b & pmask) == pre) atomicAdd(&h[(b >> shift) & bmask], 1u);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 2048; i += blockDim.x)
+    if (h[i]) atomicAdd(&hist[i], h[i]);
+}
+__global__ void kth_select_k(KthState* st, uint32_t* hist, int pass, float* out) {
+  if (threadIdx.x == 0) {
+    const int shift = pass == 0 ? 21 : pass == 1 ? 10 : 0;
+    const int nb = pass == 2 ? 1024 : 2048;
+    uint32_t k = st->k, cum = 0;
+    int sel = 0;
+    for (int b = nb - 1; b >= 0; --b) {
+      if (cum + hist[b] >= k) {
+        sel = b;
+        break;
+      }
+      cum += hist[b];
+    }
+    st->prefix |= (uint32_t)sel << shift;
+    st->k = k - cum;
+    if (pass == 2) *out = __uint_as_float(st->prefix);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 2048; i += blockDim.x) hist[i] = 0;  // ready for the next pass
+}
+
 __global__ void iadd_i64_k(int64_t* __restrict__ p, int64_t n, int64_t v) {
   SG_GRID_STRIDE(i, n) { p[i] += v; }
 }
@@ -551,6 +606,20 @@ void sg_fill(void* p, int64_t n, int dt, double v, hipStream_t s) {
     case kI64: hipLaunchKernelGGL(fill_k<int64_t>, g, b, 0, s, (int64_t*)p, n, (int64_t)v); break;
     case kU8: hipLaunchKernelGGL(fill_k<uint8_t>, g, b, 0, s, (uint8_t*)p, n, (uint8_t)v); break;
     default: throw std::runtime_error("fill: unsupported dtype");
+  }
+}
+
+// out[0] = the k-th largest |x[i]| (1 <= k <= n); ws: >= 2048 + 2 uint32 of scratch
+void sg_kth_largest_abs(const void* x, int64_t n, int64_t k, void* out, void* ws, hipStream_t s) {
+  if (n <= 0) return;
+  if (k < 1) k = 1;
+  if (k > n) k = n;
+  uint32_t* hist = (uint32_t*)ws;
+  KthState* st = (KthState*)(hist + 2048);
+  hipLaunchKernelGGL(kth_init_k, dim3(1), dim3(256), 0, s, st, hist, (uint32_t)k);
+  for (int pass = 0; pass < 3; ++pass) {
+    hipLaunchKernelGGL(kth_hist_k, dim3(sg_grid(n, 256, 2048)), dim3(256), 0, s, (const float*)x, n, st, pass, hist);
+    hipLaunchKernelGGL(kth_select_k, dim3(1), dim3(256), 0, s, st, hist, pass, (float*)out);
   }
 }
 

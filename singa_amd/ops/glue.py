@@ -544,3 +544,25 @@ def pad_backward(dy: torch.Tensor, in_shape, before: Sequence[int], mode: str = 
     _lib().pad_bwd(dyc.data_ptr(), dx.data_ptr(), N.dt(dyc), list(dy.shape), list(in_shape), list(dx.stride()),
                    list(before), PAD[mode], N.stream())
     return dx if dy.dtype == torch.float32 else to(dx, dy.dtype)
+
+
+# --------------------------------------------------------------------- selection
+_KTH_WS: dict = {}
+
+
+def kth_largest_abs(x: torch.Tensor, k: int) -> torch.Tensor:
+    """0-d fp32 tensor holding the k-th largest |x| (exact): a 3-pass radix
+    select on the device (no sort, no host sync), graph-capturable."""
+    if not on_gpu(x):
+        a = x.float().abs().reshape(-1)
+        return a.kthvalue(a.numel() - int(k) + 1).values
+    if x.dtype != torch.float32:
+        x = to(x, torch.float32)
+    x = contiguous(x)
+    key = (x.device, torch.cuda.current_stream(x.device).cuda_stream)
+    ws = _KTH_WS.get(key)
+    if ws is None:
+        ws = _KTH_WS[key] = torch.empty(2048 + 2, dtype=torch.int32, device=x.device)
+    out = torch.empty((), dtype=torch.float32, device=x.device)
+    _lib().kth_largest_abs(x.data_ptr(), x.numel(), int(k), out.data_ptr(), ws.data_ptr(), N.stream())
+    return out

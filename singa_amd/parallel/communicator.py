@@ -1,5 +1,11 @@
 """Communicator: one process per GPU, collectives over RCCL/xGMI.
 
+On GPUs :func:`init_distributed` returns the native
+:class:`~singa_amd.parallel.rccl.RcclCommunicator` (direct RCCL calls, own
+comm stream, HIP-graph capturable).  The ``torch.distributed``-based
+:class:`Communicator` below remains for CPU ranks (gloo: the multi-process
+tests) and as an explicit fallback (``SINGA_AMD_COMM=torch``).
+
 Replaces the reference's ZeroMQ Router (C15, src/utils/router.cc:16-123:
 PING/PONG handshake, addressed sends) and the parameter-server transport
 (C25/C26) with ``torch.distributed``:
@@ -200,6 +206,18 @@ def init_distributed(rank: Optional[int] = None, world_size: Optional[int] = Non
         # SINGA_DIST_BACKEND=gloo rehearses the multi-process GPU path with
         # several ranks sharing one GPU (RCCL refuses two ranks on one device)
         backend = os.environ.get("SINGA_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
+    if (ws > 1 and backend == "nccl" and not dist.is_initialized()
+            and os.environ.get("SINGA_AMD_COMM", "rccl") == "rccl"):
+        # the native RCCL communicator: the env:// store carries only the
+        # unique id and the heartbeats; no torch.distributed process group
+        from .rccl import RcclCommunicator, make_store
+
+        torch.cuda.set_device(lr % max(1, torch.cuda.device_count()))
+        store = make_store(rk, ws, timeout_s)
+        _STORE["store"] = store
+        c = RcclCommunicator(ws, rk, lr, store)
+        _COMM["comm"] = c
+        return c
     if ws > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29511")

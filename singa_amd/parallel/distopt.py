@@ -1,5 +1,5 @@
-"""Synchronous data parallelism over RCCL (``torch.distributed`` backend
-"nccl" = RCCL on ROCm) with gradient buckets overlapped with backward.
+"""Synchronous data parallelism over RCCL with gradient buckets overlapped
+with backward.
 
 Reference mapping: the reference ships parameters to a ZeroMQ
 parameter server (Put/Get/kSync, src/utils/param_manager.cc:103-234).  On one
@@ -10,25 +10,32 @@ MI355X node the PS disappears: every GPU owns a full replica in a flat
 Buckets are contiguous slices of the flat fp32 gradient buffer.  Because the
 store is laid out in reverse creation order, gradients complete front to
 back during backward; as soon as every parameter overlapping a bucket is
-done, that bucket's all-reduce is launched asynchronously on RCCL's stream,
-overlapping the remaining backward kernels.  Bucket size defaults to 32 MiB:
-a ring over 8 GPUs moves each bucket in 7 xGMI-link-sized chunks of ~4 MiB,
-large enough to run near link bandwidth (§5.8 link-aware sizing), with a
-smaller first bucket so communication starts early.
+done, that bucket's all-reduce is forked onto the communicator's comm stream
+and overlaps the remaining backward kernels; the fused optimiser update
+joins every bucket back in.  Bucket size defaults to 32 MiB: a ring over 8
+GPUs moves each bucket in 7 xGMI-link-sized chunks of ~4 MiB, large enough
+to run near link bandwidth (§5.8 link-aware sizing), with a smaller first
+bucket so communication starts early.
 
-When the step is captured into a HIP graph (``Model(use_graph=True)``), the
-collective is NOT captured: forward+backward replay from the graph, then the
-bucketed all-reduce and the fused update run eagerly (:meth:`post_replay`).
+``grad_dtype=torch.bfloat16`` exchanges bf16 buckets (half the xGMI bytes):
+each bucket is cast into a bf16 staging buffer, all-reduced, and cast back on
+the comm stream.
+
+With the native communicator (:class:`~singa_amd.parallel.rccl.RcclCommunicator`,
+the default on GPUs) the fork / join is HIP-graph capturable, so a captured
+training step (``Model(use_graph=True)``) contains the overlapped bucket
+all-reduces too.  With a communicator that cannot be captured (torch gloo /
+NCCL process groups) the collective runs after the replay (:meth:`post_replay`).
 """
 from __future__ import annotations
 
-import os
 from typing import List, Optional, Sequence
 
 import torch
-import torch.distributed as dist
 
 from .. import autograd
+from ..ops import functional as F
+from ..ops import glue as G
 from ..opt import Optimizer, ParamStore
 from ..tensor import Tensor
 from .communicator import Communicator, init_distributed
@@ -37,7 +44,8 @@ from .communicator import Communicator, init_distributed
 class DistOpt:
     def __init__(self, opt: Optimizer, nccl_id=None, local_rank: Optional[int] = None,
                  world_size: Optional[int] = None, rank: Optional[int] = None, bucket_mb: float = 32.0,
-                 first_bucket_mb: float = 4.0, overlap: bool = True, comm: Optional[Communicator] = None):
+                 first_bucket_mb: float = 4.0, overlap: bool = True, comm: Optional[Communicator] = None,
+                 grad_dtype: torch.dtype = torch.float32):
         self.opt = opt
         self.comm = comm or init_distributed(rank=rank, world_size=world_size, local_rank=local_rank)
         self.world_size = self.comm.world_size
@@ -50,6 +58,10 @@ class DistOpt:
         self.graph_mode = False
         self.defer = False
         self.comm_ms = 0.0
+        if grad_dtype not in (torch.float32, torch.bfloat16):
+            raise ValueError("DistOpt: grad_dtype must be float32 or bfloat16")
+        self.grad_dtype = grad_dtype
+        self._stage = None  # bf16 staging buffer (same layout as the flat gradient)
 
     # delegate optimiser attributes (lr, step_counter, store, ...)
     def __getattr__(self, k):
@@ -103,10 +115,11 @@ class DistOpt:
             raise RuntimeError("DistOpt: parameters not attached (call model.compile first)")
         st.zero_grad()
         capturing = torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
-        if capturing or not self.overlap or self.world_size == 1:
+        capturable = getattr(self.comm, "capturable", False)
+        if (capturing and not capturable) or not self.overlap or self.world_size == 1:
             for _ in autograd.backward(loss):
                 pass
-            if capturing:
+            if capturing and not capturable:
                 self.defer = True  # collective + update happen in post_replay()
                 return
             self._allreduce_all()
@@ -121,23 +134,46 @@ class DistOpt:
                 continue
             remaining[b] -= 1
             if remaining[b] == 0:
-                s, e, _ = self.buckets[b]
-                works.append(self.comm.all_reduce(st.g[s:e], async_op=True))
+                works.append(self._reduce_bucket(b))
         for b, r in enumerate(remaining):  # params without gradients this step
             if r > 0:
-                s, e, _ = self.buckets[b]
-                works.append(self.comm.all_reduce(st.g[s:e], async_op=True))
+                works.append(self._reduce_bucket(b))
         for w in works:
             if w is not None:
                 w.wait()
         self.opt.update(grad_scale=1.0 / self.world_size)
         self.opt.step()
 
+    def _reduce_bucket(self, b: int):
+        """Fork bucket b's all-reduce onto the comm stream (bf16 exchange:
+        cast in, all-reduce, cast back -- all on the comm stream)."""
+        s, e, _ = self.buckets[b]
+        g = self.store.g[s:e]
+        if self.grad_dtype == torch.float32 or not g.is_cuda:
+            return self.comm.all_reduce(g, async_op=True)
+        if self._stage is None or self._stage.numel() != self.store.g.numel():
+            self._stage = torch.empty(self.store.g.numel(), dtype=torch.bfloat16, device=g.device)
+        stg = self._stage[s:e]
+        cs = getattr(self.comm, "comm_stream", None)
+        if cs is None:
+            G.copy_(stg, g)
+            self.comm.all_reduce(stg)
+            G.copy_(g, stg)
+            return None
+        cs.wait_stream(torch.cuda.current_stream(g.device))
+        with torch.cuda.stream(cs):
+            G.copy_(stg, g)  # fp32 -> bf16 (native copy kernel)
+            self.comm.all_reduce(stg)  # on the comm stream (its "current" stream here)
+            G.copy_(g, stg)
+            ev = torch.cuda.Event()
+            ev.record(cs)
+        from .rccl import Work
+        return Work(ev, (g, stg))
+
     def _allreduce_all(self):
-        st = self.store
         if self.world_size == 1:
             return
-        works = [self.comm.all_reduce(st.g[s:e], async_op=True) for s, e, _ in self.buckets]
+        works = [self._reduce_bucket(b) for b in range(len(self.buckets))]
         for w in works:
             if w is not None:
                 w.wait()
@@ -154,12 +190,21 @@ class DistOpt:
         self.comm.all_reduce(tensor.data)
 
     def fused_all_reduce(self, tensors: Sequence[Tensor], send: bool = True) -> None:
-        flat = torch.cat([t.data.reshape(-1).float() for t in tensors])
+        """One all-reduce over several tensors packed into a flat fp32 buffer
+        (native copies in and out)."""
+        dev = tensors[0].data.device
+        total = sum(t.data.numel() for t in tensors)
+        flat = torch.empty(total, dtype=torch.float32, device=dev)
+        o = 0
+        for t in tensors:
+            n = t.data.numel()
+            G.copy_(flat[o:o + n], G.reshape(t.data, (-1,)))
+            o += n
         self.comm.all_reduce(flat)
         o = 0
         for t in tensors:
             n = t.data.numel()
-            t.data.copy_(flat[o:o + n].reshape(t.shape).to(t.dtype))
+            G.copy_(t.data, flat[o:o + n].reshape(t.shape))
             o += n
 
     def wait(self) -> None:
@@ -177,7 +222,7 @@ class DistOpt:
         k = self.opt.step_counter % max(nb, 1)
         s, e, _ = self.buckets[k]
         self.comm.all_reduce(st.g[s:e])
-        st.g[s:e].mul_(1.0 / self.world_size)
+        G.binary("mul", st.g[s:e], 1.0 / self.world_size, out=st.g[s:e])
         self.opt.update(grad_scale=1.0)
         self.opt.step()
 
@@ -193,18 +238,18 @@ class DistOpt:
         g = st.g
         if corr:
             if not hasattr(self, "_resid"):
-                self._resid = torch.zeros_like(g)
-            g.add_(self._resid)
-        if topK:
-            k = max(1, int(threshold * g.numel()))
-            thr = g.abs().kthvalue(g.numel() - k + 1).values
-            mask = g.abs() >= thr
+                self._resid = G.zeros_like(g)
+            G.binary("add", g, self._resid, out=g)
+        absg = F.unary("abs", g)
+        if topK:  # exact k-th largest |g| by on-device radix select (no sort, no host sync)
+            thr = G.kth_largest_abs(g, max(1, int(threshold * g.numel())))
         else:
-            mask = g.abs() >= threshold
-        sparse = torch.where(mask, g, torch.zeros_like(g))
+            thr = float(threshold)
+        mask = G.binary("ge", absg, thr)
+        sparse = G.binary("mul", g, mask)
         if corr:
-            self._resid.copy_(g - sparse)
-        g.copy_(sparse)
+            G.binary("sub", g, sparse, out=self._resid)
+        G.copy_(g, sparse)
         self.comm.all_reduce(g)
         self.opt.update(grad_scale=1.0 / self.world_size)
         self.opt.step()

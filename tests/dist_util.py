@@ -16,7 +16,7 @@ def free_port() -> int:
     return p
 
 
-def _entry(rank, world, port, fn, args, q):
+def _entry(rank, world, port, fn, args, q, backend="gloo"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     import torch
@@ -27,7 +27,11 @@ def _entry(rank, world, port, fn, args, q):
 
     communicator.reset()
     try:
-        comm = communicator.init_distributed(backend="gloo", timeout_s=120)
+        if backend == "rccl":  # the native RCCL communicator (GPU ranks)
+            os.environ["SINGA_AMD_COMM"] = "rccl"
+            comm = communicator.init_distributed(backend="nccl", timeout_s=120)
+        else:
+            comm = communicator.init_distributed(backend="gloo", timeout_s=120)
         res = fn(rank, world, comm, *args)
         q.put((rank, "ok", res))
     except Exception:  # report to the parent instead of hanging the others
@@ -35,15 +39,22 @@ def _entry(rank, world, port, fn, args, q):
     finally:
         if dist.is_initialized():
             dist.destroy_process_group()
+        c = communicator._COMM.get("comm")
+        if c is not None and hasattr(c, "destroy"):
+            try:
+                c.destroy()
+            except Exception:
+                pass
 
 
-def run_ranks(fn, world: int = 2, *args, timeout: float = 240.0):
+def run_ranks(fn, world: int = 2, *args, timeout: float = 240.0, backend: str = "gloo"):
     """Run ``fn(rank, world, comm, *args)`` on ``world`` processes; returns
-    the per-rank results (must be picklable) in rank order."""
+    the per-rank results (must be picklable) in rank order.  backend "rccl":
+    GPU ranks over the native RCCL communicator."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=_entry, args=(r, world, port, fn, args, q)) for r in range(world)]
+    procs = [ctx.Process(target=_entry, args=(r, world, port, fn, args, q, backend)) for r in range(world)]
     for p in procs:
         p.start()
     out = {}
