@@ -300,7 +300,7 @@ def backward(y, dy=None) -> Iterator[Tuple[Tensor, Tensor]]:
                 elif dx is not None:
                     prev = pgrad.get(key)
                     if p.grad_view is not None:
-                        p.grad_view.add_(dx.reshape(p.grad_view.shape).to(p.grad_view.dtype))
+                        G.binary("add", p.grad_view, G.reshape(dx, p.grad_view.shape), out=p.grad_view)
                         pgrad[key] = ACCUMULATED
                     else:
                         pgrad[key] = _accum(prev, dx)
@@ -717,7 +717,7 @@ class Conv2d(Operator):
         if self.has_bias:
             tb = self.grad_target(2)
             if tb is not None:
-                tb.add_(db)
+                G.binary("add", tb, G.reshape(db, tb.shape), out=tb)
                 db = ACCUMULATED
             res.append(db)
         return tuple(res)
@@ -1043,7 +1043,7 @@ class LayerNorm(Operator):
                     break
                 if t is not None and gg is not None:
                     if gg is not t:
-                        t.add_(gg.reshape(t.shape))
+                        G.binary("add", t, G.reshape(gg, t.shape), out=t)
                     out.append(ACCUMULATED)
                 else:
                     out.append(gg)

@@ -3,6 +3,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include "cpu_ops.h"
 #include "runtime.h"
 
 namespace py = pybind11;
@@ -224,4 +225,127 @@ PYBIND11_MODULE(_core, m) {
     d["encoded"] = enc;
     return d;
   });
+
+  // ---- CppCPU compute backend (cpu_ops.cc): raw host pointers, GIL released --
+  {
+    namespace C = sgrt::cpu;
+    typedef uintptr_t P;
+    auto fp = [](P p) { return (float*)p; };
+    auto cfp = [](P p) { return (const float*)p; };
+    auto ng = py::call_guard<py::gil_scoped_release>();
+    py::module_ c = m.def_submodule("cpu", "CppCPU compute kernels (host pointers)");
+    c.def("num_threads", &C::NumThreads);
+    c.def("gemm", [=](bool ta, bool tb, int64_t M, int64_t N, int64_t K, float alpha, P a, int64_t lda, P b,
+                      int64_t ldb, float beta, P cc, int64_t ldc, P bias, bool relu) {
+      C::Gemm(ta, tb, M, N, K, alpha, cfp(a), lda, cfp(b), ldb, beta, fp(cc), ldc, cfp(bias), relu);
+    }, ng);
+    c.def("gemm_batched", [=](bool ta, bool tb, int64_t M, int64_t N, int64_t K, float alpha, P a, int64_t lda,
+                              int64_t sa, P b, int64_t ldb, int64_t sb, float beta, P cc, int64_t ldc, int64_t sc,
+                              int64_t batch) {
+      // batch-parallel: each GEMM of the batch runs on one worker
+      C::ParallelFor(batch, 1, [&](int64_t b0, int64_t b1) {
+        for (int64_t i = b0; i < b1; ++i)
+          C::Gemm(ta, tb, M, N, K, alpha, cfp(a) + i * sa, lda, cfp(b) + i * sb, ldb, beta, fp(cc) + i * sc, ldc,
+                  nullptr, false);
+      });
+    }, ng);
+    c.def("unary_fwd", [=](int op, P x, P y, int64_t n, float a) { C::UnaryFwd(op, cfp(x), fp(y), n, a); }, ng);
+    c.def("unary_bwd", [=](int op, P x, P y, P dy, P dx, int64_t n, float a) {
+      C::UnaryBwd(op, cfp(x), cfp(y), cfp(dy), fp(dx), n, a);
+    }, ng);
+    c.def("copy_nd", [](P src, int dti, P dst, int dto, std::vector<int64_t> size, std::vector<int64_t> dst_st,
+                        std::vector<int64_t> src_st) {
+      if (size.size() > 8 || dst_st.size() != size.size() || src_st.size() != size.size())
+        throw std::invalid_argument("copy_nd: bad rank");
+      py::gil_scoped_release rel;
+      C::CopyNd((const void*)src, dti, (void*)dst, dto, (int)size.size(), size.data(), dst_st.data(), src_st.data());
+    });
+    c.def("binary_nd", [=](int op, P a, P b, P out, std::vector<int64_t> size, std::vector<int64_t> os,
+                           std::vector<int64_t> as, std::vector<int64_t> bs, float alpha) {
+      if (size.size() > 8 || os.size() != size.size() || as.size() != size.size() || bs.size() != size.size())
+        throw std::invalid_argument("binary_nd: bad rank");
+      py::gil_scoped_release rel;
+      C::BinaryNd(op, cfp(a), cfp(b), fp(out), (int)size.size(), size.data(), os.data(), as.data(), bs.data(), alpha);
+    });
+    c.def("fill", [](P p, int64_t n, int dt, double v) { C::Fill((void*)p, n, dt, v); }, ng);
+    c.def("reduce", [=](P x, P y, int64_t outer, int64_t red, int64_t inner, int op) {
+      C::Reduce(cfp(x), fp(y), outer, red, inner, op);
+    }, ng);
+    c.def("softmax", [=](P x, P y, int64_t rows, int64_t n) { C::SoftmaxRows(cfp(x), fp(y), rows, n); }, ng);
+    c.def("softmax_bwd", [=](P y, P dy, P dx, int64_t rows, int64_t n) {
+      C::SoftmaxRowsBwd(cfp(y), cfp(dy), fp(dx), rows, n);
+    }, ng);
+    c.def("softmax_xent", [=](P x, P lab, int lab64, P t, P loss, P correct, P dx, int64_t B, int64_t n, int topk,
+                              float gs) {
+      C::SoftmaxXent(cfp(x), (const void*)lab, lab64, cfp(t), fp(loss), fp(correct), fp(dx), B, n, topk, gs);
+    }, ng);
+    c.def("conv_fwd", [=](P x, P w, P bias, P y, int N, int Ci, int H, int W, int K, int R, int S, int Ho, int Wo,
+                          int sh, int sw, int ph, int pw, int dh, int dw, int groups) {
+      C::ConvFwd(cfp(x), cfp(w), cfp(bias), fp(y), N, Ci, H, W, K, R, S, Ho, Wo, sh, sw, ph, pw, dh, dw, groups);
+    }, ng);
+    c.def("conv_bwd", [=](P x, P w, P dy, P dx, P dwt, P db, int N, int Ci, int H, int W, int K, int R, int S, int Ho,
+                          int Wo, int sh, int sw, int ph, int pw, int dh, int dw, int groups) {
+      C::ConvBwd(cfp(x), cfp(w), cfp(dy), fp(dx), fp(dwt), fp(db), N, Ci, H, W, K, R, S, Ho, Wo, sh, sw, ph, pw, dh,
+                 dw, groups);
+    }, ng);
+    c.def("pool_fwd", [=](P x, P y, P arg, int N, int Ci, int H, int W, int Ho, int Wo, int kh, int kw, int sh,
+                          int sw, int ph, int pw, int is_max, int cip) {
+      C::PoolFwd(cfp(x), fp(y), (int32_t*)arg, N, Ci, H, W, Ho, Wo, kh, kw, sh, sw, ph, pw, is_max, cip);
+    }, ng);
+    c.def("pool_bwd", [=](P dy, P arg, P dx, int N, int Ci, int H, int W, int Ho, int Wo, int kh, int kw, int sh,
+                          int sw, int ph, int pw, int is_max, int cip) {
+      C::PoolBwd(cfp(dy), (const int32_t*)arg, fp(dx), N, Ci, H, W, Ho, Wo, kh, kw, sh, sw, ph, pw, is_max, cip);
+    }, ng);
+    c.def("lrn_fwd", [=](P x, P y, int N, int Ci, int HW, int size, float alpha, float beta, float k) {
+      C::LrnFwd(cfp(x), fp(y), N, Ci, HW, size, alpha, beta, k);
+    }, ng);
+    c.def("lrn_bwd", [=](P x, P dy, P dx, int N, int Ci, int HW, int size, float alpha, float beta, float k) {
+      C::LrnBwd(cfp(x), cfp(dy), fp(dx), N, Ci, HW, size, alpha, beta, k);
+    }, ng);
+    c.def("dropout_fwd", [=](P x, P y, P mask, int64_t n, float pkeep, uint64_t seed, uint64_t offset) {
+      C::DropoutFwd(cfp(x), fp(y), (uint8_t*)mask, n, pkeep, seed, offset);
+    }, ng);
+    c.def("dropout_bwd", [=](P dy, P mask, P dx, int64_t n, float pkeep) {
+      C::DropoutBwd(cfp(dy), (const uint8_t*)mask, fp(dx), n, pkeep);
+    }, ng);
+    c.def("rand_fill", [=](P y, int64_t n, int dist, float a, float b, uint64_t seed, uint64_t offset) {
+      C::RandFill(fp(y), n, dist, a, b, seed, offset);
+    }, ng);
+    c.def("bn_fwd", [=](P x, P g, P b, P rm, P rv, P y, P mean, P invstd, int N, int Ci, int64_t HW, int training,
+                        float momentum, float eps, int relu, P res) {
+      C::BatchNormFwd(cfp(x), cfp(g), cfp(b), fp(rm), fp(rv), fp(y), fp(mean), fp(invstd), N, Ci, HW, training,
+                      momentum, eps, relu, cfp(res));
+    }, ng);
+    c.def("bn_bwd", [=](P x, P dy, P g, P mean, P invstd, P ym, int relu_x, P scale, P shift, P dx, P dg, P db,
+                        P dres, int N, int Ci, int64_t HW) {
+      C::BatchNormBwd(cfp(x), cfp(dy), cfp(g), cfp(mean), cfp(invstd), cfp(ym), relu_x, cfp(scale), cfp(shift), fp(dx),
+                      fp(dg), fp(db), fp(dres), N, Ci, HW);
+    }, ng);
+    c.def("where_nd", [=](P cond, P a, P b, P out, std::vector<int64_t> size, std::vector<int64_t> os,
+                          std::vector<int64_t> as, std::vector<int64_t> bs, std::vector<int64_t> cs) {
+      if (size.size() > 8 || os.size() != size.size() || as.size() != size.size() || bs.size() != size.size() ||
+          cs.size() != size.size())
+        throw std::invalid_argument("where_nd: bad rank");
+      py::gil_scoped_release rel;
+      C::WhereNd((const uint8_t*)cond, cfp(a), cfp(b), fp(out), (int)size.size(), size.data(), os.data(), as.data(),
+                 bs.data(), cs.data());
+    });
+    c.def("clamp_affine", [=](P x, P dy, P y, int64_t n, float a, float b, float lo, float hi) {
+      C::ClampAffine(cfp(x), cfp(dy), fp(y), n, a, b, lo, hi);
+    }, ng);
+    c.def("layernorm_fwd", [=](P x, P g, P b, P y, P mean, P rstd, int64_t R, int64_t D, float eps) {
+      C::LayerNormFwd(cfp(x), cfp(g), cfp(b), fp(y), fp(mean), fp(rstd), R, D, eps);
+    }, ng);
+    c.def("layernorm_bwd", [=](P x, P dy, P g, P mean, P rstd, P dx, P dg, P db, int64_t R, int64_t D) {
+      C::LayerNormBwd(cfp(x), cfp(dy), cfp(g), cfp(mean), cfp(rstd), fp(dx), fp(dg), fp(db), R, D);
+    }, ng);
+    c.def("index_select", [](P src, P idx, int idx64, P dst, int64_t outer, int64_t nsrc, int64_t inner,
+                             int64_t nidx, int esize) {
+      C::IndexSelect((const void*)src, (const void*)idx, idx64, (void*)dst, outer, nsrc, inner, nidx, esize);
+    }, ng);
+    c.def("index_add", [=](P dst, P idx, int idx64, P src, int64_t outer, int64_t ndst, int64_t inner, int64_t nidx,
+                           float alpha) {
+      C::IndexAdd(fp(dst), (const void*)idx, idx64, cfp(src), outer, ndst, inner, nidx, alpha);
+    }, ng);
+  }
 }

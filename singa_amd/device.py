@@ -1,4 +1,4 @@
-"""Devices: ``CppCPU`` (host plumbing / numerics oracle) and ``RocmGPU``.
+"""Devices: ``CppCPU`` (native C++ host kernels, csrc/runtime/cpu_ops.cc) and ``RocmGPU``.
 
 Mirrors the SINGA python device API (``create_cuda_gpu``, ``get_default_device``,
 ``Device.SetRandSeed``, ``EnableGraph``, ``Sync``, ``PrintTimeProfiling`` ...)
@@ -114,6 +114,10 @@ class Device:
 
 
 class CppCPU(Device):
+    """Host device: its tensors' compute runs on the native C++ kernels of
+    ``_core.cpu`` (threaded packed GEMM, im2col convolution, pooling, LRN,
+    softmax-xent, normalisation, elementwise / broadcast / reduction loops;
+    see :mod:`singa_amd.ops.cpu`).  PyTorch supplies host storage only."""
     lang_name = "kCpp"
 
     def __init__(self):

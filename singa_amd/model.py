@@ -29,6 +29,7 @@ import torch
 from . import autograd
 from . import layer
 from .ops import functional as _F
+from .ops import glue as G
 from .tensor import Tensor
 
 
@@ -171,7 +172,7 @@ class Model(layer.Layer):
         g, sargs, out = self._graphs[key]
         for a, s in zip(args, sargs):
             if isinstance(a, Tensor) and a is not s and a.data.data_ptr() != s.data.data_ptr():
-                s.data.copy_(a.data.reshape(s.shape))
+                G.copy_(s.data, G.reshape(a.data, s.shape))
         if opt is not None and self.training:
             opt.prepare_step()
         g.replay()

@@ -11,19 +11,24 @@ Every op has two implementations:
   ragged bf16 shapes, grouped and dilated convolutions.  A GPU case without a
   native kernel RAISES (``_no_native``); nothing falls back to PyTorch /
   hipBLAS / MIOpen on the device.
-* CPU: a plain PyTorch fp32/bf16 reference, which doubles as the numerics
-  oracle for the kernel tests (the reference framework's CppCPU device).
+* CPU (the ``CppCPU`` device): fp32 host tensors run the native C++
+  kernels of ``_core.cpu`` (csrc/runtime/cpu_ops.cc, dispatched by
+  :mod:`singa_amd.ops.cpu`).  The plain PyTorch expressions below each native
+  branch are the numerics ORACLE of the tests (``cpu.torch_oracle()``) and
+  the path of host dtypes without a native kernel (bf16 on the CPU).
 """
 from __future__ import annotations
 
 import math
 import os
+import threading
 from typing import Optional, Sequence, Tuple
 
 import numpy as np
 import torch
 import torch.nn.functional as F
 
+from . import cpu as CP
 from . import glue as G
 from . import native as N
 
@@ -95,6 +100,11 @@ def unary(op: str, x: torch.Tensor, alpha: float = 0.0) -> torch.Tensor:
         N.lib().unary_fwd(UNARY[op], x.data_ptr(), y.data_ptr(), x.numel(), N.dt(x), alpha, N.stream())
         return y
     _no_native(f"unary {op}", x)
+    if CP.ok(x) and op in UNARY:
+        x = CP.dense32(x)
+        y = torch.empty(x.shape, dtype=torch.float32)
+        CP.lib().unary_fwd(UNARY[op], x.data_ptr(), y.data_ptr(), x.numel(), float(alpha))
+        return y
     if op == "leakyrelu":
         return F.leaky_relu(x, alpha)
     if op == "elu":
@@ -124,6 +134,13 @@ def unary_bwd(op: str, x: Optional[torch.Tensor], y: Optional[torch.Tensor], dy:
                           alpha, N.stream())
         return dx
     _no_native(f"unary_bwd {op}", dy)
+    if CP.ok(x, y, dy) and op in UNARY:
+        dy = CP.dense32(dy)
+        xx = CP.dense32(x) if x is not None else None
+        yy = CP.dense32(y) if y is not None else None
+        dx = torch.empty(dy.shape, dtype=torch.float32)
+        CP.lib().unary_bwd(UNARY[op], CP.p(xx), CP.p(yy), dy.data_ptr(), dx.data_ptr(), dy.numel(), float(alpha))
+        return dx
     xf = x.float() if x is not None else None
     yf = y.float() if y is not None else None
     g = dy.float()
@@ -212,6 +229,10 @@ def add_act(a: torch.Tensor, b: torch.Tensor, alpha=1.0, beta=1.0, relu=False) -
             N.lib().add_act(a.data_ptr(), b.data_ptr(), y.data_ptr(), a.numel(), N.dt(a), alpha, beta, int(relu),
                             N.stream())
             return y
+    if CP.ok(a, b) and a.shape == b.shape:
+        r = G.binary("add", unary("scale", a, alpha) if alpha != 1.0 else a,
+                     unary("scale", b, beta) if beta != 1.0 else b)
+        return unary("relu", r) if relu else r
     r = alpha * a + beta * b
     return torch.relu(r) if relu else r
 
@@ -221,6 +242,8 @@ def relu_bwd_from_y(y: torch.Tensor, dy: torch.Tensor) -> torch.Tensor:
         dx = _like(dy)
         N.lib().relu_bwd_from_y(y.data_ptr(), dy.data_ptr(), dx.data_ptr(), dy.numel(), N.dt(dy), N.stream())
         return dx
+    if CP.ok(y, dy) and y.shape == dy.shape:
+        return unary_bwd("relu", y, None, dy)  # relu'(y) == relu'(x) for y = relu(x)
     return dy * (y > 0)
 
 
@@ -248,6 +271,16 @@ def dropout_fwd(x: torch.Tensor, ratio: float, seed: int, offset: int,
                             N.ptr(epoch), N.stream())
         return y, mask
     _no_native("dropout_fwd", x)
+    if CP.lib() is not None and not x.is_cuda:
+        # the GPU kernels' Philox stream on the host (bit-identical masks); the
+        # oracle applies the same mask with PyTorch arithmetic
+        xc = CP.dense32(x)
+        y = torch.empty(x.shape, dtype=torch.float32)
+        mask = torch.empty(x.shape, dtype=torch.uint8)
+        CP.lib().dropout_fwd(xc.data_ptr(), y.data_ptr(), mask.data_ptr(), xc.numel(), pkeep, int(seed), int(offset))
+        if CP.ok(x):
+            return y, mask
+        return x * mask.to(x.dtype) / pkeep, mask
     g = torch.Generator(device=x.device).manual_seed(int(seed + offset) & 0x7FFFFFFFFFFFFFFF)
     mask = (torch.rand(x.shape, generator=g, device=x.device) < pkeep).to(torch.uint8)
     return x * mask.to(x.dtype) / pkeep, mask
@@ -263,6 +296,11 @@ def dropout_bwd(dy: torch.Tensor, mask: torch.Tensor, ratio: float) -> torch.Ten
         N.lib().dropout_bwd(dy.data_ptr(), mask.data_ptr(), dx.data_ptr(), dy.numel(), N.dt(dy), pkeep, N.stream())
         return dx
     _no_native("dropout_bwd", dy)
+    if CP.ok(dy) and mask.dtype == torch.uint8 and mask.shape == dy.shape:
+        dy, m = CP.dense32(dy), G.contiguous(mask)
+        dx = torch.empty(dy.shape, dtype=torch.float32)
+        CP.lib().dropout_bwd(dy.data_ptr(), m.data_ptr(), dx.data_ptr(), dy.numel(), pkeep)
+        return dx
     return dy * mask.to(dy.dtype) / pkeep
 
 
@@ -291,6 +329,15 @@ def softmax(x: torch.Tensor, axis: int = -1, out_dtype: Optional[torch.dtype] = 
                             N.stream())
         return y if od == x.dtype else cast(y, od)
     _no_native("softmax", x)
+    if CP.ok(x) and od == torch.float32:
+        if axis != x.dim() - 1:
+            return G.contiguous(softmax(G.contiguous(x.movedim(axis, -1)), -1, od).movedim(-1, axis))
+        x = CP.dense32(x)
+        y = torch.empty(x.shape, dtype=torch.float32)
+        n = x.shape[-1] if x.dim() else 1
+        if y.numel():
+            CP.lib().softmax(x.data_ptr(), y.data_ptr(), x.numel() // n, n)
+        return y
     return torch.softmax(x.float(), dim=axis).to(od)
 
 
@@ -307,6 +354,16 @@ def softmax_bwd(y: torch.Tensor, dy: torch.Tensor, axis: int = -1) -> torch.Tens
         N.lib().softmax_bwd(y.data_ptr(), dy.data_ptr(), dx.data_ptr(), y.numel() // C, C, N.dt(y), N.stream())
         return dx
     _no_native("softmax_bwd", y, dy)
+    if CP.ok(y, dy):
+        if axis != y.dim() - 1:
+            g = softmax_bwd(G.contiguous(y.movedim(axis, -1)), G.contiguous(dy.movedim(axis, -1)), -1)
+            return G.contiguous(g.movedim(-1, axis))
+        y, dy = CP.dense32(y), CP.dense32(dy)
+        dx = torch.empty(y.shape, dtype=torch.float32)
+        n = y.shape[-1] if y.dim() else 1
+        if dx.numel():
+            CP.lib().softmax_bwd(y.data_ptr(), dy.data_ptr(), dx.data_ptr(), y.numel() // n, n)
+        return dx
     yf, gf = y.float(), dy.float()
     return (yf * (gf - (gf * yf).sum(dim=axis, keepdim=True))).to(dy.dtype)
 
@@ -335,6 +392,21 @@ def softmax_xent(x: torch.Tensor, target: torch.Tensor, topk: int = 1, grad_scal
                              C, N.dt(x2), topk, gs, N.stream())
         return loss, correct, (dx.reshape(x.shape) if dx is not None else None)
     _no_native("softmax_xent", x)
+    if CP.ok(x2) and (not soft or target.dtype == torch.float32):
+        x2 = CP.dense32(x2)
+        loss = torch.empty(B, dtype=torch.float32)
+        correct = torch.empty(B, dtype=torch.float32)
+        dx = torch.empty(x2.shape, dtype=torch.float32) if need_grad else None
+        if soft:
+            t, lab, l64 = CP.dense32(G.reshape(target, (B, C))), None, 0
+        else:
+            lab = G.contiguous(G.reshape(target, (B,)))
+            if lab.dtype not in (torch.int32, torch.int64):
+                lab = G.to(lab, torch.int32)
+            t, l64 = None, int(lab.dtype == torch.int64)
+        CP.lib().softmax_xent(x2.data_ptr(), CP.p(lab), l64, CP.p(t), loss.data_ptr(), correct.data_ptr(), CP.p(dx), B, C,
+                             int(topk), float(gs))
+        return loss, correct, (dx.reshape(x.shape) if dx is not None else None)
     xf = x2.float()
     lse = torch.logsumexp(xf, dim=1)
     if soft:
@@ -371,6 +443,17 @@ def layernorm_fwd(x: torch.Tensor, g: Optional[torch.Tensor], b: Optional[torch.
                               D, N.dt(x), eps, N.stream())
         return y, mean, rstd
     _no_native("layernorm_fwd", x)
+    if CP.ok(x, g, b):
+        x = CP.dense32(x)
+        R = x.numel() // D
+        y = torch.empty(x.shape, dtype=torch.float32)
+        mean = torch.empty(R, dtype=torch.float32)
+        rstd = torch.empty(R, dtype=torch.float32)
+        gg = CP.dense32(g) if g is not None else None
+        bb = CP.dense32(b) if b is not None else None
+        CP.lib().layernorm_fwd(x.data_ptr(), CP.p(gg), CP.p(bb), y.data_ptr(), mean.data_ptr(), rstd.data_ptr(), R, D,
+                               float(eps))
+        return y, mean, rstd
     xf = x.float().reshape(-1, D)
     mean = xf.mean(1)
     rstd = torch.rsqrt(xf.var(1, unbiased=False) + eps)
@@ -405,6 +488,22 @@ def layernorm_bwd(x, dy, g, mean, rstd, dg_acc=None, db_acc=None):
                               dx.data_ptr(), N.ptr(dg), N.ptr(db), R, D, N.dt(x), N.stream())
         return dx, dg, db
     _no_native("layernorm_bwd", x, dy)
+    if CP.ok(x, dy, g):
+        x, dy = CP.dense32(x), CP.dense32(dy)
+        dx = torch.empty(x.shape, dtype=torch.float32)
+        dg = db = None
+        if g is not None:
+            dg = dg_acc if (dg_acc is not None and CP.ok(dg_acc) and dg_acc.is_contiguous() and dg_acc.numel() == D) \
+                else G.zeros((D,), torch.float32, x.device)
+            db = db_acc if (db_acc is not None and CP.ok(db_acc) and db_acc.is_contiguous() and db_acc.numel() == D) \
+                else G.zeros((D,), torch.float32, x.device)
+        gg = CP.dense32(g) if g is not None else None
+        CP.lib().layernorm_bwd(x.data_ptr(), dy.data_ptr(), CP.p(gg), CP.dense32(mean).data_ptr(),
+                               CP.dense32(rstd).data_ptr(), dx.data_ptr(), CP.p(dg), CP.p(db), R, D)
+        if dg is not None and dg_acc is not None and dg is not dg_acc:
+            dg = G.binary("add", dg_acc, G.reshape(dg, dg_acc.shape), out=dg_acc)
+            db = G.binary("add", db_acc, G.reshape(db, db_acc.shape), out=db_acc)
+        return dx, dg, db
     xf = x.float().reshape(R, D)
     gy = dy.float().reshape(R, D)
     xh = (xf - mean[:, None]) * rstd[:, None]
@@ -443,7 +542,7 @@ def _mat(t: torch.Tensor, trans: bool):
         return t, (s0 if r > 1 else max(c, 1)), bool(trans)
     if (s0 == 1 or r == 1) and (c == 1 or s1 >= r):  # column-major: t[i][j] at j*ld + i
         return t, (s1 if c > 1 else max(r, 1)), not trans
-    t = t.contiguous()
+    t = G.contiguous(t)
     return t, max(c, 1), bool(trans)
 
 
@@ -491,7 +590,26 @@ def gemm(a: torch.Tensor, b: torch.Tensor, ta: bool = False, tb: bool = False, o
     lead = (batch,) if batch > 1 or a.dim() == 3 or b.dim() == 3 else ()
     if out is None:
         od = out_dtype or (torch.float32 if accumulate else a.dtype)
-        out = (torch.zeros if accumulate else torch.empty)(lead + (M, Nn), dtype=od, device=a.device)
+        out = G.zeros(lead + (M, Nn), od, a.device) if accumulate else torch.empty(lead + (M, Nn), dtype=od,
+                                                                                      device=a.device)
+    if (not a.is_cuda and CP.ok(a, b, bias) and out.dtype == torch.float32 and out.is_contiguous()
+            and (bias is None or bias.numel() == Nn)):
+        if M == 0 or Nn == 0:
+            return out
+        a, lda, ako = _mat(a, ta)
+        b, ldb, bko = _mat(b, tb)
+        sa = a.stride(0) if a.dim() == 3 else 0
+        sb = b.stride(0) if b.dim() == 3 else 0
+        sc = M * Nn if out.dim() == 3 else 0
+        bb = CP.dense32(bias).reshape(-1) if bias is not None else None
+        if batch > 1 and (bb is not None or relu):
+            for i in range(batch):
+                gemm(a[i] if a.dim() == 3 else a, b[i] if b.dim() == 3 else b, ta, tb, out[i], None, alpha,
+                     1.0 if accumulate else beta, bias, relu)
+            return out
+        CP.gemm(a, lda, ako, b, ldb, not bko, out, M, Nn, K, alpha, 1.0 if accumulate else beta, bb, relu, batch, sa,
+                sb, sc)
+        return out
     if not (_native_ok(a, b) and a.is_cuda):
         if a.is_cuda:
             _no_native("gemm", a, b)
@@ -568,6 +686,8 @@ def gemm_tn_acc(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, beta: float
         elif beta != 1.0:
             G.binary("mul", out, beta, out=out)
         return gemm(a, b, ta=True, out=out, accumulate=True)
+    if CP.ok(a, b, out) and out.is_contiguous():
+        return gemm(a, b, ta=True, out=out, beta=beta)
     r = a.float().t() @ b.float()
     if beta == 0.0:
         out.copy_(r)
@@ -726,6 +846,17 @@ def conv2d_fwd(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], stri
             y = G.contiguous(y[:, :K], torch.channels_last)
         return y if y.dtype == out_dtype else cast(y, out_dtype)
     _no_native("conv2d_fwd", x, w)
+    if CP.ok(x, w, b) and out_dtype == torch.float32:
+        Nn, Cx, H, W = x.shape
+        K, Cg, R, S = w.shape
+        if Cx != Cg * groups or K % groups:
+            raise ValueError(f"conv2d: input {tuple(x.shape)} / weight {tuple(w.shape)} / groups {groups} mismatch")
+        Ho, Wo = conv_out_size(H, R, sh, ph, dh), conv_out_size(W, S, sw, pw, dw)
+        xc, wc = CP.dense32(x), CP.dense32(w)
+        y = torch.empty((Nn, K, Ho, Wo), dtype=torch.float32)
+        CP.lib().conv_fwd(xc.data_ptr(), wc.data_ptr(), CP.p(CP.dense32(b) if b is not None else None), y.data_ptr(),
+                          Nn, Cx, H, W, K, R, S, Ho, Wo, sh, sw, ph, pw, dh, dw, groups)
+        return unary("relu", y) if relu else y
     xf = x.float() if x.dtype != torch.float32 else x
     y = F.conv2d(xf, w.float(), b.float() if b is not None else None, (sh, sw), (ph, pw), (dh, dw), groups)
     if relu:
@@ -767,9 +898,11 @@ def pretranspose_conv_weights(items) -> dict:
             sel.append((key, w))
     if len(sel) < 2 or not DGRAD_KMAJOR:
         return {}
-    # one scratch per (weight set, stream): replica threads sharing the
-    # weights run on their own streams and must not write each other's copy
-    sig = tuple((w.data_ptr(),) + tuple(w.shape) for _, w in sel) + (N.stream(),)
+    # one scratch per (weight set, thread): replica threads sharing the
+    # weights run on their own streams and must not write each other's copy.
+    # Keyed by thread, not stream: a HIP-graph capture runs the same step on a
+    # side stream and must hit the entry its eager warm-up created
+    sig = tuple((w.data_ptr(),) + tuple(w.shape) for _, w in sel) + (threading.get_ident(),)
     ent = _WT_CACHE.get(sig)
     if ent is None:
         if len(_WT_CACHE) > 8:
@@ -915,8 +1048,22 @@ def conv2d_bwd(x: torch.Tensor, w: torch.Tensor, dy: torch.Tensor, stride, paddi
         if need_db:
             db = colsum(dyb.permute(0, 2, 3, 1).reshape(-1, Kp))[0][:K]
         return dx, dwt, db
-    # CPU reference via autograd of the functional conv
     _no_native("conv2d_bwd", x, w, dy)
+    if CP.ok(x, w, dy):
+        Nn, Cx, H, W = x.shape
+        K, Cg, R, S = w.shape
+        Ho, Wo = dy.shape[2], dy.shape[3]
+        xc, wc, dyc = CP.dense32(x), CP.dense32(w), CP.dense32(dy)
+        dx = torch.empty(x.shape, dtype=torch.float32) if need_dx else None
+        direct = dw_out is not None and CP.ok(dw_out) and dw_out.is_contiguous()
+        dwt = dw_out if direct else G.zeros(tuple(w.shape), torch.float32, x.device)
+        db = G.zeros((K,), torch.float32, x.device) if need_db else None
+        CP.lib().conv_bwd(xc.data_ptr(), wc.data_ptr(), dyc.data_ptr(), CP.p(dx), dwt.data_ptr(), CP.p(db), Nn, Cx, H,
+                          W, K, R, S, Ho, Wo, sh, sw, ph, pw, dh, dw_, groups)
+        if dw_out is not None and not direct:
+            dwt = G.binary("add", dw_out, dwt, out=dw_out)
+        return dx, dwt, db
+    # CPU reference via autograd of the functional conv
     with torch.enable_grad():
         xx = x.detach().float().requires_grad_(need_dx)
         ww = w.detach().float().requires_grad_(True)
@@ -1031,6 +1178,11 @@ def colsum(x2: torch.Tensor, with_sq: bool = False, out: Optional[torch.Tensor] 
                        int(out is not None), N.stream())
         return o0, o1
     _no_native("colsum", x2)
+    if CP.ok(x2, out):
+        s0 = G.reduce(x2, [0], "sum")
+        if out is not None:
+            s0 = G.binary("add", out, s0, out=out)
+        return s0, (G.reduce(x2, [0], "sumsq") if with_sq else None)
     xf = x2.float()
     s0 = xf.sum(0)
     if out is not None:
@@ -1133,6 +1285,21 @@ def batchnorm_fwd(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, run_
         return y, BNState(mean, invstd, scale, shift, mask)
     # CPU reference
     _no_native("batchnorm_fwd", x)
+    if (CP.ok(x, gamma, beta, run_mean, run_var, residual) and run_mean.is_contiguous() and run_var.is_contiguous()
+            and x.dim() in (2, 4)):
+        xc = CP.dense32(x)
+        Nn = x.shape[0]
+        HW = x.numel() // (Nn * C) if Nn * C else 0
+        y = torch.empty(x.shape, dtype=torch.float32)
+        mean = torch.empty(C, dtype=torch.float32)
+        invstd = torch.empty(C, dtype=torch.float32)
+        res = CP.dense32(residual) if residual is not None else None
+        CP.lib().bn_fwd(xc.data_ptr(), CP.dense32(gamma).data_ptr(), CP.dense32(beta).data_ptr(),
+                        run_mean.data_ptr(), run_var.data_ptr(), y.data_ptr(), mean.data_ptr(), invstd.data_ptr(), Nn,
+                        C, HW, int(training), float(momentum), float(eps), int(relu), CP.p(res))
+        scale = G.binary("mul", gamma, invstd)
+        shift = G.binary("sub", beta, G.binary("mul", mean, scale))
+        return y, BNState(mean, invstd, scale, shift)
     dims = (0,) if x.dim() == 2 else (0, 2, 3)
     shp = (1, C) if x.dim() == 2 else (1, C, 1, 1)
     xf = x.float()
@@ -1253,6 +1420,25 @@ def batchnorm_bwd(x: torch.Tensor, dy: torch.Tensor, gamma: torch.Tensor, st: BN
             dres._sg_fresh = True
         return dx, dg, db, dres
     _no_native("batchnorm_bwd", x, dy)
+    if CP.ok(x, dy, gamma, y_for_mask, dg_out, db_out) and x.dim() in (2, 4):
+        xc, dyc = CP.dense32(x), CP.dense32(dy)
+        Nn = x.shape[0]
+        HW = x.numel() // (Nn * C) if Nn * C else 0
+        dg = dg_out if dg_out is not None and dg_out.is_contiguous() else G.zeros((C,), torch.float32, x.device)
+        db = db_out if db_out is not None and db_out.is_contiguous() else G.zeros((C,), torch.float32, x.device)
+        dx = torch.empty(x.shape, dtype=torch.float32)
+        dres = torch.empty(x.shape, dtype=torch.float32) if need_dres else None
+        ym = CP.dense32(y_for_mask) if y_for_mask is not None else None
+        relu_x = int(relu and ym is None)
+        CP.lib().bn_bwd(xc.data_ptr(), dyc.data_ptr(), CP.dense32(gamma).data_ptr(), CP.dense32(st.mean).data_ptr(),
+                        CP.dense32(st.invstd).data_ptr(), CP.p(ym), relu_x,
+                        CP.dense32(st.scale).data_ptr() if relu_x else 0,
+                        CP.dense32(st.shift).data_ptr() if relu_x else 0, dx.data_ptr(), dg.data_ptr(), db.data_ptr(),
+                        CP.p(dres), Nn, C, HW)
+        if dg_out is not None and dg is not dg_out:
+            dg = G.binary("add", dg_out, dg, out=dg_out)
+            db = G.binary("add", db_out, db, out=db_out)
+        return dx, dg, db, dres
     dims = (0,) if x.dim() == 2 else (0, 2, 3)
     shp = (1, C) if x.dim() == 2 else (1, C, 1, 1)
     g = dy.float()
@@ -1297,6 +1483,13 @@ def pool2d_fwd(x: torch.Tensor, kernel, stride, padding, is_max: bool, count_inc
                          int(is_max), int(count_include_pad), N.dt(x), N.stream())
         return y, arg
     _no_native("pool2d_fwd", x)
+    if CP.ok(x):
+        xc = CP.dense32(x)
+        y = torch.empty((Nn, C, Ho, Wo), dtype=torch.float32)
+        arg = torch.empty((Nn, C, Ho, Wo), dtype=torch.int32) if is_max else None
+        CP.lib().pool_fwd(xc.data_ptr(), y.data_ptr(), CP.p(arg), Nn, C, H, W, Ho, Wo, kh, kw, sh, sw, ph, pw,
+                          int(is_max), int(count_include_pad))
+        return y, arg
     xf = x.float()
     if is_max:
         y, idx = F.max_pool2d(xf, (kh, kw), (sh, sw), (ph, pw), ceil_mode=ceil_mode, return_indices=True)
@@ -1319,6 +1512,15 @@ def pool2d_bwd(x_shape, x_like: torch.Tensor, dy: torch.Tensor, arg, kernel, str
                          int(is_max), int(count_include_pad), N.dt(dy), N.stream())
         return dx
     _no_native("pool2d_bwd", dy)
+    if CP.ok(dy) and (not is_max or arg.dtype == torch.int32):
+        dyc = CP.dense32(dy)
+        dx = torch.empty(tuple(x_shape), dtype=torch.float32)
+        a = G.contiguous(arg) if is_max else None
+        CP.lib().pool_bwd(dyc.data_ptr(), CP.p(a), dx.data_ptr(), Nn, C, H, W, Ho, Wo, kh, kw, sh, sw, ph, pw,
+                          int(is_max), int(count_include_pad))
+        return dx
+    if is_max and arg.dtype != torch.int64:
+        arg = arg.long()
     g = dy.float()
     if is_max:  # scatter-ADD: overlapping windows (k > s) may pick the same input
         dx = torch.zeros((Nn, C, H * W), dtype=torch.float32, device=dy.device)
@@ -1339,6 +1541,8 @@ def global_avgpool_fwd(x: torch.Tensor) -> torch.Tensor:
         N.lib().gap_fwd(x.data_ptr(), y.data_ptr(), Nn, H * W, C, N.dt(x), N.stream())
         return y
     _no_native("global_avgpool_fwd", x)
+    if CP.ok(x):
+        return G.reduce(x, [2, 3], "mean")
     return x.float().mean(dim=(2, 3)).to(x.dtype)
 
 
@@ -1350,6 +1554,8 @@ def global_avgpool_bwd(dy: torch.Tensor, x_shape) -> torch.Tensor:
         N.lib().gap_bwd(dy.data_ptr(), dx.data_ptr(), Nn, H * W, C, N.dt(dy), N.stream())
         return dx
     _no_native("global_avgpool_bwd", dy)
+    if CP.ok(dy):
+        return G.expand(unary("scale", dy, 1.0 / (H * W)).reshape(Nn, C, 1, 1), tuple(x_shape))
     return (dy.float()[:, :, None, None] / (H * W)).expand(x_shape).to(dy.dtype)
 
 
@@ -1378,6 +1584,12 @@ def lrn_fwd(x: torch.Tensor, size: int, alpha: float, beta: float, k: float):
                         N.stream())
         return y, norm
     _no_native("lrn_fwd", x)
+    if CP.ok(x) and x.dim() == 4:
+        xc = CP.dense32(x)
+        Nn, C, H, W = x.shape
+        y = torch.empty(x.shape, dtype=torch.float32)
+        CP.lib().lrn_fwd(xc.data_ptr(), y.data_ptr(), Nn, C, H * W, int(size), float(alpha), float(beta), float(k))
+        return y, None  # the backward recomputes the window sums
     xf = x.float()
     sq = xf * xf
     half = size // 2
@@ -1391,6 +1603,13 @@ def lrn_bwd(x: torch.Tensor, dy: torch.Tensor, norm: Optional[torch.Tensor], siz
             k: float = 1.0, relu_mask: bool = False):
     """``relu_mask``: x is a ReLU output; the native kernel also zeroes dx
     where x <= 0 (the ReLU backward, folded) and marks dx ``_sg_relu_done``."""
+    if CP.ok(x, dy) and x.dim() == 4:
+        xc, dyc = CP.dense32(x), CP.dense32(dy)
+        Nn, C, H, W = x.shape
+        dx = torch.empty(x.shape, dtype=torch.float32)
+        CP.lib().lrn_bwd(xc.data_ptr(), dyc.data_ptr(), dx.data_ptr(), Nn, C, H * W, int(size), float(alpha),
+                         float(beta), float(k))
+        return dx
     if _native_ok(x, dy) and x.dtype in (torch.float32, torch.bfloat16):
         x = G.to(x, memory_format=torch.channels_last)
         dy = G.to(dy, x.dtype, torch.channels_last)
@@ -1439,7 +1658,7 @@ def attention_fwd(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, mask: Optio
     scale = (1.0 / math.sqrt(D)) if scale is None else scale
     lead = q.shape[:-2]
     Sq, Sk = q.shape[-2], k.shape[-2]
-    if _native_ok(q, k, v):
+    if _native_ok(q, k, v) or CP.ok(q, k, v, mask):
         q3 = G.reshape(q, (-1, Sq, D))
         k3 = G.reshape(k, (-1, Sk, D))
         v3 = G.reshape(v, (-1, Sk, D))
@@ -1547,7 +1766,7 @@ def attention_bwd(q, k, v, p, do, scale: Optional[float] = None):
     D = q.shape[-1]
     scale = (1.0 / math.sqrt(D)) if scale is None else scale
     Sq, Sk = q.shape[-2], k.shape[-2]
-    if _native_ok(q, k, v, p, do):
+    if _native_ok(q, k, v, p, do) or CP.ok(q, k, v, p, do):
         q3 = G.reshape(q, (-1, Sq, D))
         k3 = G.reshape(k, (-1, Sk, D))
         v3 = G.reshape(v, (-1, Sk, D))

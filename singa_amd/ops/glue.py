@@ -1,7 +1,9 @@
 """Layout / indexing / broadcast / reduction ops ("glue") on raw ``torch.Tensor``
 storage, dispatching to the gfx950 kernels of ``csrc/kernels/glue.hip`` on
-the GPU and to a plain PyTorch CPU reference otherwise (the CppCPU device and
-the numerics oracle of the tests).
+the GPU and to the native C++ loops of ``_core.cpu`` (csrc/runtime/cpu_ops.cc)
+for host tensors -- the CppCPU device.  The plain PyTorch expressions kept
+below each native branch are the numerics oracle of the tests
+(``cpu.torch_oracle()``) and the path of host dtypes without a kernel.
 
 Every GPU op here runs a hand-written kernel; PyTorch supplies storage and
 free *views* only (slicing, transposes, expand, reshape of contiguous data
@@ -21,6 +23,7 @@ from typing import List, Optional, Sequence, Tuple
 
 import torch
 
+from . import cpu as CP
 from . import native as N
 
 BIN = {"add": 0, "sub": 1, "mul": 2, "div": 3, "pow": 4, "max": 5, "min": 6, "lt": 7, "le": 8, "gt": 9, "ge": 10,
@@ -74,6 +77,14 @@ def copy_(dst: torch.Tensor, src: torch.Tensor) -> torch.Tensor:
     if dst.numel() == 0:
         return dst
     if not on_gpu(dst, src):
+        if CP.copy_ok(dst, src) and not src.is_cuda and not dst.is_cuda and src.dtype != torch.bool:
+            if src.data_ptr() == dst.data_ptr() and src.dtype == dst.dtype and src.stride() == dst.stride() \
+                    and src.shape == dst.shape:
+                return dst
+            shape = tuple(dst.shape)
+            size, ds, ss = coalesce(shape, list(dst.stride()), _bstrides(src, shape))
+            CP.lib().copy_nd(src.data_ptr(), CP.dt(src), dst.data_ptr(), CP.dt(dst), size, ds, ss)
+            return dst
         return dst.copy_(src)
     if not (src.is_cuda and dst.is_cuda):
         if src.is_cuda == dst.is_cuda:
@@ -95,7 +106,7 @@ def contiguous(t: torch.Tensor, memory_format=torch.contiguous_format) -> torch.
     """Dense copy in the requested memory format (no-op if already dense)."""
     if t.is_contiguous(memory_format=memory_format):
         return t
-    if not on_gpu(t):
+    if not on_gpu(t) and not CP.copy_ok(t):
         return t.contiguous(memory_format=memory_format)
     return copy_(empty_like_fmt(t, memory_format=memory_format), t)
 
@@ -119,7 +130,7 @@ def to(t: torch.Tensor, dtype: Optional[torch.dtype] = None, memory_format=None)
         fmt = memory_format
         if t.dtype == dtype and t.is_contiguous(memory_format=fmt):
             return t
-    if not on_gpu(t):
+    if not on_gpu(t) and not (CP.copy_ok(t) and dtype in CP._DT and t.dtype != torch.bool):
         return t.to(dtype=dtype, memory_format=fmt)
     return copy_(torch.empty(t.shape, dtype=dtype, device=t.device, memory_format=fmt), t)
 
@@ -134,11 +145,14 @@ def reshape(t: torch.Tensor, shape) -> torch.Tensor:
 
 # --------------------------------------------------------------------- fills
 def fill_(t: torch.Tensor, value: float) -> torch.Tensor:
+    if CP.copy_ok(t) and t.is_contiguous():
+        if t.numel():
+            CP.lib().fill(t.data_ptr(), t.numel(), CP.dt(t), float(value))
+        return t
     if not on_gpu(t) or not t.is_contiguous() and not (t.dim() == 4 and
                                                        t.is_contiguous(memory_format=torch.channels_last)):
-        if on_gpu(t):
-            tmp = full(t.shape, value, t.dtype, t.device)
-            return copy_(t, tmp)
+        if on_gpu(t) or CP.copy_ok(t):
+            return copy_(t, full((), value, t.dtype, t.device))  # broadcast (stride-0) copy into the strided view
         return t.fill_(value)
     if t.numel():
         _lib().fill(t.data_ptr(), t.numel(), N.dt(t), float(value), N.stream())
@@ -168,6 +182,15 @@ def random_(t: torch.Tensor, dist: str, a: float, b: float, device_obj=None) -> 
             _lib().rand_fill(d.data_ptr(), d.numel(), N.dt(d), 0 if dist == "uniform" else 1, float(a), float(b),
                              int(seed), int(off), N.stream())
         return t if d is t else copy_(t, d)
+    if not t.is_cuda and CP.lib() is not None and t.dtype == torch.float32:
+        # the same Philox stream as the GPU kernel (in oracle mode too: the
+        # initial weights of a native run and its oracle run are identical)
+        seed, off = device_obj.next_rng(t.numel()) if device_obj is not None else (0, 0)
+        d = t if t.is_contiguous() else torch.empty(t.shape, dtype=torch.float32)
+        if d.numel():
+            CP.lib().rand_fill(d.data_ptr(), d.numel(), 0 if dist == "uniform" else 1, float(a), float(b), int(seed),
+                               int(off))
+        return t if d is t else copy_(t, d)
     gen = device_obj.generator if device_obj is not None else None
     d = torch.empty(t.shape, dtype=torch.float32, device=t.device)
     if dist == "uniform":
@@ -182,6 +205,10 @@ def full(shape, value, dtype, device, memory_format=torch.contiguous_format) -> 
     if t.is_cuda and N.force_native():
         if t.numel():
             _lib().fill(t.data_ptr(), t.numel(), N.dt(t), float(value), N.stream())
+        return t
+    if CP.copy_ok(t):
+        if t.numel():
+            CP.lib().fill(t.data_ptr(), t.numel(), CP.dt(t), float(value))
         return t
     return t.fill_(value)
 
@@ -218,6 +245,18 @@ def binary(op: str, a: torch.Tensor, b, out_dtype: Optional[torch.dtype] = None,
         return out
     if on_gpu(a, b):
         raise NotImplementedError(f"binary {op}: no native kernel for {a.dtype} x {b.dtype}")
+    od = out_dtype or dt
+    if CP.ok(out) and CP.copy_ok(a, b) and (out is not None or od == torch.float32) and a.dtype != torch.bool \
+            and b.dtype != torch.bool:
+        a = a if a.dtype == torch.float32 else to(a, torch.float32)
+        b = b if b.dtype == torch.float32 else to(b, torch.float32)
+        shape = tuple(torch.broadcast_shapes(a.shape, b.shape))
+        o = out if out is not None and tuple(out.shape) == shape else torch.empty(shape, dtype=torch.float32)
+        size, os_, as_, bs_ = coalesce(shape, list(o.stride()), _bstrides(a, shape), _bstrides(b, shape))
+        CP.lib().binary_nd(BIN[op], a.data_ptr(), b.data_ptr(), o.data_ptr(), size, os_, as_, bs_, float(alpha))
+        if out is not None and o is not out:
+            return copy_(out, o)
+        return o
     af, bf = a.float(), b.float()
     r = {"add": lambda: af + bf, "sub": lambda: af - bf, "mul": lambda: af * bf, "div": lambda: af / bf,
          "pow": lambda: torch.pow(af, bf), "max": lambda: torch.maximum(af, bf), "min": lambda: torch.minimum(af, bf),
@@ -252,6 +291,19 @@ def where(cond: torch.Tensor, a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
         return out
     if on_gpu(cond, a, b):
         raise NotImplementedError(f"where: no native kernel for {dt}")
+    if CP.copy_ok(cond, a, b) and dt == torch.float32:
+        c = cond if cond.dtype in (torch.uint8, torch.bool) else binary("ne", to(cond, torch.float32), 0.0)
+        if c.dtype == torch.bool:
+            c = c.view(torch.uint8)
+        elif c.dtype != torch.uint8:
+            c = to(c, torch.uint8)
+        a, b = to(a, dt), to(b, dt)
+        shape = tuple(torch.broadcast_shapes(c.shape, a.shape, b.shape))
+        out = torch.empty(shape, dtype=dt)
+        size, os_, as_, bs_, cs_ = coalesce(shape, list(out.stride()), _bstrides(a, shape), _bstrides(b, shape),
+                                            _bstrides(c, shape))
+        CP.lib().where_nd(c.data_ptr(), a.data_ptr(), b.data_ptr(), out.data_ptr(), size, os_, as_, bs_, cs_)
+        return out
     return torch.where(cond.bool(), a.to(dt), b.to(dt))
 
 
@@ -275,6 +327,13 @@ def clamp_affine(x: torch.Tensor, a: float = 1.0, b: float = 0.0, lo: float = -m
         return out
     if on_gpu(x):
         raise NotImplementedError(f"clamp_affine: no native kernel for {x.dtype}")
+    if CP.ok(x, dy):
+        xc = CP.dense32(x)
+        g = CP.dense32(dy) if dy is not None else None
+        out = torch.empty(x.shape, dtype=torch.float32)
+        CP.lib().clamp_affine(xc.data_ptr(), CP.p(g), out.data_ptr(), xc.numel(), float(a), float(b),
+                              float(max(lo, -3.4e38)), float(min(hi, 3.4e38)))
+        return out
     z = a * x.float() + b
     if dy is None:
         return torch.clamp(z, lo, hi).to(x.dtype)
@@ -294,7 +353,10 @@ def reduce(x: torch.Tensor, axes: Optional[Sequence[int]] = None, op: str = "sum
         [s for k, s in enumerate(x.shape) if k not in axes]
     if not axes:
         return to(x, od).clone() if x.dtype == od else to(x, od)
-    if on_gpu(x) and x.dtype in _FLOATS and od in _FLOATS:
+    host = CP.copy_ok(x) and x.dtype != torch.bool and od in _FLOATS
+    if (on_gpu(x) and x.dtype in _FLOATS and od in _FLOATS) or host:
+        if host and x.dtype != torch.float32:
+            x = to(x, torch.float32)
         keep = [k for k in range(nd) if k not in axes]
         lo, hi = min(axes), max(axes)
         if axes == list(range(lo, hi + 1)):  # already adjacent
@@ -312,6 +374,10 @@ def reduce(x: torch.Tensor, axes: Optional[Sequence[int]] = None, op: str = "sum
             return y
         if red == 0:
             return fill_(y, 0.0 if op in ("sum", "mean", "sumsq") else float("nan"))
+        if host:
+            y32 = y if y.dtype == torch.float32 else torch.empty(oshape, dtype=torch.float32)
+            CP.lib().reduce(xc.data_ptr(), y32.data_ptr(), outer, red, inner, RED[op])
+            return y if y32 is y else copy_(y, y32)
         _lib().reduce(xc.data_ptr(), N.dt(xc), y.data_ptr(), N.dt(y), outer, red, inner, RED[op], N.stream())
         return y
     if on_gpu(x):
@@ -337,7 +403,7 @@ def sum_to(g: torch.Tensor, shape) -> torch.Tensor:
 # --------------------------------------------------------------------- concat / slices / tiles
 def cat(ts: Sequence[torch.Tensor], axis: int = 0) -> torch.Tensor:
     ts = list(ts)
-    if not on_gpu(*ts):
+    if not on_gpu(*ts) and not (CP.copy_ok(*ts) and len({t.dtype for t in ts}) == 1):
         return torch.cat(ts, dim=axis)
     nd = ts[0].dim()
     axis %= nd
@@ -375,8 +441,8 @@ def tile(x: torch.Tensor, repeats: Sequence[int]) -> torch.Tensor:
     reps = list(repeats)
     if len(reps) < x.dim():
         reps = [1] * (x.dim() - len(reps)) + reps
-    xs = x.reshape((1,) * (len(reps) - x.dim()) + tuple(x.shape))
-    if not on_gpu(x):
+    xs = reshape(x, (1,) * (len(reps) - x.dim()) + tuple(x.shape))
+    if not on_gpu(x) and not CP.copy_ok(x):
         return xs.repeat(*reps)
     inter = []
     for r, s in zip(reps, xs.shape):
@@ -405,7 +471,7 @@ def expand(x: torch.Tensor, shape) -> torch.Tensor:
     shape = tuple(shape)
     if tuple(x.shape) == shape:
         return x
-    if not on_gpu(x):
+    if not on_gpu(x) and not CP.copy_ok(x):
         return x.expand(*shape).contiguous()
     out = torch.empty(shape, dtype=x.dtype, device=x.device)
     return copy_(out, x.expand(*shape) if x.dim() == len(shape) else x)
@@ -423,6 +489,15 @@ def _idx(idx: torch.Tensor, device) -> torch.Tensor:
 def index_select(x: torch.Tensor, axis: int, idx: torch.Tensor) -> torch.Tensor:
     """out = x.take(idx, axis) with out.shape = x.shape[:axis] + idx.shape + x.shape[axis+1:]."""
     axis %= x.dim()
+    if not on_gpu(x) and CP.copy_ok(x) and not idx.is_cuda and idx.dtype in (torch.int32, torch.int64):
+        xc, ic = contiguous(x), contiguous(idx)
+        outer = int(math.prod(x.shape[:axis]))
+        inner = int(math.prod(x.shape[axis + 1:]))
+        out = torch.empty(x.shape[:axis] + tuple(idx.shape) + x.shape[axis + 1:], dtype=x.dtype)
+        if out.numel():
+            CP.lib().index_select(xc.data_ptr(), ic.data_ptr(), int(ic.dtype == torch.int64), out.data_ptr(), outer,
+                                  x.shape[axis], inner, ic.numel(), x.element_size())
+        return out
     if not on_gpu(x):
         r = torch.index_select(x, axis, idx.reshape(-1).long().to(x.device))
         return r.reshape(x.shape[:axis] + tuple(idx.shape) + x.shape[axis + 1:])
@@ -440,6 +515,16 @@ def index_select(x: torch.Tensor, axis: int, idx: torch.Tensor) -> torch.Tensor:
 def index_add_(dst: torch.Tensor, axis: int, idx: torch.Tensor, src: torch.Tensor, alpha: float = 1.0) -> torch.Tensor:
     """dst.index_add_(axis, idx, src) into an fp32 dense dst (atomics)."""
     axis %= dst.dim()
+    if (not on_gpu(dst) and CP.ok(dst) and dst.is_contiguous() and CP.copy_ok(src) and not idx.is_cuda
+            and idx.dtype in (torch.int32, torch.int64)):
+        s = src if src.dtype == torch.float32 and src.is_contiguous() else to(contiguous(src), torch.float32)
+        ic = contiguous(idx)
+        outer = int(math.prod(dst.shape[:axis]))
+        inner = int(math.prod(dst.shape[axis + 1:]))
+        if s.numel():
+            CP.lib().index_add(dst.data_ptr(), ic.data_ptr(), int(ic.dtype == torch.int64), s.data_ptr(), outer,
+                               dst.shape[axis], inner, ic.numel(), float(alpha))
+        return dst
     if not on_gpu(dst):
         s = src.reshape(dst.shape[:axis] + (idx.numel(),) + dst.shape[axis + 1:]).to(dst.dtype)
         return dst.index_add_(axis, idx.reshape(-1).long(), s, alpha=alpha)
@@ -513,6 +598,13 @@ def pad(x: torch.Tensor, before: Sequence[int], after: Sequence[int], mode: str 
     constant / reflect / edge)."""
     nd = x.dim()
     osz = [s + b + a for s, b, a in zip(x.shape, before, after)]
+    if not on_gpu(x) and mode == "constant" and CP.copy_ok(x) and min(list(before) + list(after) + [0]) >= 0:
+        y = full(osz, value, x.dtype, x.device)
+        v = y
+        for k in range(nd):
+            v = v.narrow(k, before[k], x.shape[k])
+        copy_(v, x)
+        return y
     if not on_gpu(x):
         if mode == "constant":
             tp = []

@@ -24,3 +24,17 @@ def gpu():
 
     native.lib()  # must load: GPU tests never run on a silent fallback
     return torch.device("cuda", 0)
+
+
+@pytest.fixture(autouse=True)
+def _gpu_tests_use_the_torch_oracle(request):
+    """GPU tests compare the HIP kernels against CPU results: those come from
+    the plain PyTorch fp32 expressions (the oracle), not from the native C++
+    CppCPU kernels, which have their own parity tests (test_cppcpu_cpu.py)."""
+    if request.node.get_closest_marker("gpu") is None:
+        yield
+        return
+    from singa_amd.ops import cpu as CP
+
+    with CP.torch_oracle():
+        yield

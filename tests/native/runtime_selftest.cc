@@ -13,6 +13,9 @@
 // Update / pipelined PushUpdate + Collect / Elastic / RandomSync on SHARED
 // keys, Gets deferred until another thread's Put, and kStop counting
 // (the reference's concurrency hot-spot, src/server/server.cc:45-214).
+// The CppCPU compute backend (cpu_ops.cc) runs GEMMs and convolutions from
+// several caller threads at once: one owns the worker pool, the others run
+// inline, and every result must equal the single-threaded reference.
 #include <atomic>
 #include <chrono>
 #include <cmath>
@@ -22,6 +25,7 @@
 #include <thread>
 #include <vector>
 
+#include "../../singa_amd/csrc/runtime/cpu_ops.h"
 #include "../../singa_amd/csrc/runtime/runtime.h"
 
 #define CHECK(c)                                                     \
@@ -218,6 +222,54 @@ int main(int argc, char** argv) {
       for (float x : v) CHECK(std::isfinite(x));
     }
     srv.Close();
+  }
+  {  // CppCPU kernels: concurrent callers of the persistent pool
+    namespace C = sgrt::cpu;
+    const int M = 37, N = 45, K = 70;
+    std::vector<float> A(M * K), B(K * N), ref(M * N, 0.f);
+    for (int i = 0; i < M * K; ++i) A[i] = std::sin(0.37f * i);
+    for (int i = 0; i < K * N; ++i) B[i] = std::cos(0.11f * i);
+    for (int m = 0; m < M; ++m)
+      for (int n = 0; n < N; ++n) {
+        double acc = 0;
+        for (int k = 0; k < K; ++k) acc += (double)A[m * K + k] * B[k * N + n];
+        ref[m * N + n] = (float)acc;
+      }
+    // conv: 3 images, 4 -> 6 channels, 3x3, stride 1, pad 1, 2 groups
+    const int Nn = 3, Ci = 4, H = 7, W = 6, Ko = 6, R = 3;
+    std::vector<float> x(Nn * Ci * H * W), w(Ko * (Ci / 2) * R * R), dy(Nn * Ko * H * W);
+    for (size_t i = 0; i < x.size(); ++i) x[i] = std::sin(0.05f * i);
+    for (size_t i = 0; i < w.size(); ++i) w[i] = std::cos(0.3f * i);
+    for (size_t i = 0; i < dy.size(); ++i) dy[i] = std::sin(0.7f * i);
+    std::vector<float> dw0(w.size(), 0.f), dx0(x.size());
+    C::ConvBwd(x.data(), w.data(), dy.data(), dx0.data(), dw0.data(), nullptr, Nn, Ci, H, W, Ko, R, R, H, W, 1, 1, 1,
+               1, 1, 1, 2);
+    std::vector<std::thread> th;
+    std::atomic<int> bad{0};
+    for (int t = 0; t < 4; ++t)
+      th.emplace_back([&, t] {
+        for (int it = 0; it < 3; ++it) {
+          std::vector<float> Cm(M * N, 0.f);
+          if (t % 2)
+            C::Gemm(false, false, M, N, K, 1.f, A.data(), K, B.data(), N, 0.f, Cm.data(), N, nullptr, false);
+          else  // same product from the transposed storage of B
+          {
+            std::vector<float> Bt(N * K);
+            for (int k = 0; k < K; ++k)
+              for (int n = 0; n < N; ++n) Bt[n * K + k] = B[k * N + n];
+            C::Gemm(false, true, M, N, K, 1.f, A.data(), K, Bt.data(), K, 0.f, Cm.data(), N, nullptr, false);
+          }
+          for (int i = 0; i < M * N; ++i)
+            if (std::fabs(Cm[i] - ref[i]) > 1e-4f * (1.f + std::fabs(ref[i]))) bad++;
+          std::vector<float> dw(w.size(), 0.f), dx(x.size());
+          C::ConvBwd(x.data(), w.data(), dy.data(), dx.data(), dw.data(), nullptr, Nn, Ci, H, W, Ko, R, R, H, W, 1, 1,
+                     1, 1, 1, 1, 2);
+          for (size_t i = 0; i < dw.size(); ++i) bad += dw[i] != dw0[i];  // fixed-order reduction: bitwise
+          for (size_t i = 0; i < dx.size(); ++i) bad += dx[i] != dx0[i];
+        }
+      });
+    for (auto& t : th) t.join();
+    CHECK(bad.load() == 0);
   }
   std::printf("runtime selftest ok\n");
   return 0;
