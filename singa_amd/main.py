@@ -40,6 +40,9 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--checkpoint", default="", help="save parameters + optimiser state here at the end")
     ap.add_argument("--checkpoint_frequency", type=int, default=0, help="also checkpoint every k steps")
     ap.add_argument("--resume", default="", help="resume from a checkpoint written by --checkpoint")
+    ap.add_argument("--micro_batches", type=int, default=None,
+                    help="pipelined placed nets: micro-batches per step (singa_amd.parallel.pipeline)")
+    ap.add_argument("--pipeline", default=None, choices=["gpipe", "1f1b"], help="pipeline schedule (default 1f1b)")
     return ap
 
 
@@ -89,7 +92,8 @@ def main(argv=None) -> int:
         for l in model.neuralnet.layer:
             if l.type in ("kShardData", "kLMDBData"):
                 l.type = "kSyntheticData"
-    w = Worker(model, cluster, dev=dev, comm=comm, data_override=override, log=log)
+    w = Worker(model, cluster, dev=dev, comm=comm, data_override=override, log=log, micro_batches=a.micro_batches,
+               pipeline=a.pipeline)
     w.checkpoint_path, w.checkpoint_every = a.checkpoint, a.checkpoint_frequency
     if a.resume:
         from .runtime.checkpoint import load_worker

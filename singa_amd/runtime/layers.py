@@ -547,6 +547,10 @@ class SliceLayer(RefLayer):
 
     def forward(self, xs, training):
         x = xs[0]
+        n = x.shape[self.dim]
+        if sum(self.sizes) != n:  # a micro-batch (pipelined step): same rule on the actual size
+            base = n // self.num
+            self.sizes = [base] * (self.num - 1) + [n - base * (self.num - 1)]
         if x.requires_grad:
             parts = autograd.split(x, self.dim, self.sizes)
         else:

@@ -111,6 +111,17 @@ class _PGraph:
         return list(self.nodes.values())
 
 
+def _micro_slice(out, i: int, m: int):
+    """Micro-batch i of m of a data layer's output (views along dim 0)."""
+    if isinstance(out, dict):
+        return {k: _micro_slice(v, i, m) for k, v in out.items()}
+    B = out.data.shape[0]
+    if B % m:
+        raise ValueError(f"batch {B} does not split into {m} micro-batches")
+    k = B // m
+    return Tensor(device=out.device, data=out.data[i * k:(i + 1) * k], requires_grad=False)
+
+
 class NeuralNet:
     def __init__(self, net_proto, group_size: int = 1, phase: str = "kTrain", dev=None,
                  data_override: Optional[dict] = None, seed: int = 0, devices: Optional[List] = None,
@@ -360,15 +371,19 @@ class NeuralNet:
     def loss_layers(self) -> List[RefLayer]:
         return [l for l in self.layers if l.is_loss and self.is_local(l)]
 
-    def forward(self, training: bool = True) -> Dict[str, object]:
+    def forward(self, training: bool = True, micro: Optional[tuple] = None) -> Dict[str, object]:
         """Run every (local) layer in the global topological order; returns
         name -> output.  Cross-process bridges send/receive (see
-        :mod:`singa_amd.parallel.bridge`); cross-device inputs are moved."""
+        :mod:`singa_amd.parallel.bridge`); cross-device inputs are moved.
+        ``micro`` = (i, m): micro-batch i of m (pipelined execution,
+        :mod:`singa_amd.parallel.pipeline`): data layers draw their batch at
+        i == 0 and every pass consumes its 1/m slice of it."""
         from ..parallel import bridge as B
 
         autograd.training = training
         outs: Dict[str, object] = {}
         self._extra_roots = []
+        self._mb_batch = getattr(self, "_mb_batch", {})
         self._pending = getattr(self, "_pending", [])
         for l in self.layers:
             if not self.is_local(l):
@@ -392,6 +407,12 @@ class NeuralNet:
                 if isinstance(o, Tensor) and o.data.device != ldev.torch_device:
                     o = B.to_device(o, ldev)
                 xs.append(o)
+            if micro is not None and l.is_data:
+                i, m = micro
+                if i == 0 or l.name not in self._mb_batch:
+                    self._mb_batch[l.name] = l.forward(xs, training)
+                outs[l.name] = _micro_slice(self._mb_batch[l.name], i, m)
+                continue
             if self.dist and l.type_name == "kBridgeSrc":
                 dst = self.name2layer[l.graph_dsts[0]]
                 if not self.is_local(dst):
@@ -472,14 +493,14 @@ class NeuralNet:
             tot = autograd.add(tot, t)
         return tot
 
-    def metrics(self) -> np.ndarray:
+    def metrics(self, reduce: bool = True) -> np.ndarray:
         """[loss, precision] summed over loss layers (reference metric blob);
-        summed over the processes of a distributed group."""
+        summed over the processes of a distributed group (``reduce``)."""
         m = np.zeros(2, np.float64)
         for l in self.loss_layers():
             if hasattr(l, "metric"):
                 m += np.array([float(l.metric[0]), float(l.metric[1])]) * (l.loss_scale if l.loss_scale else 1)
-        if self.dist:
+        if self.dist and reduce:
             t = torch.tensor(m, dtype=torch.float32, device=self.dev.torch_device)
             self.comm.all_reduce(t)
             m = t.cpu().double().numpy()

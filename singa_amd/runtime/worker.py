@@ -95,7 +95,7 @@ class _Null:
 class Worker:
     def __init__(self, model_proto, cluster_proto=None, dev=None, comm: Optional[Communicator] = None,
                  data_override: Optional[dict] = None, log: Callable[[str], None] = print, group_size: int = 1,
-                 seed: int = 0):
+                 seed: int = 0, micro_batches: Optional[int] = None, pipeline: Optional[str] = None):
         from .cluster import Cluster
 
         self.model = model_proto
@@ -113,6 +113,9 @@ class Worker:
         self.history = []
         self.checkpoint_path = ""
         self.checkpoint_every = 0
+        # pipelined placed nets (P6): micro-batches per step and the schedule
+        self.micro_batches = int(micro_batches or os.environ.get("SINGA_AMD_MICROBATCHES", "1"))
+        self.pipeline = pipeline or os.environ.get("SINGA_AMD_PIPELINE", "1f1b")
         if self.comm.world_size > 1:
             # liveness through the rendezvous store (no-op if none is registered)
             self.comm.start_heartbeat()
@@ -283,6 +286,21 @@ class Worker:
             self._maybe_sync(step)
             return m
         net = self.train_net
+        if self.micro_batches > 1:
+            from ..parallel.pipeline import pipelined_step
+
+            with Timer(self.dev) as tb:
+                met = pipelined_step(net, self.store.zero_grad, self.micro_batches, self.pipeline)
+                net.sync_replica_grads()
+                scale = 1.0
+                if self.sync_dp:
+                    self.peer_comm.all_reduce(self.store.g)
+                    scale = 1.0 / self.peer_comm.world_size
+                self.updater.update(grad_scale=scale)
+                self.updater.step()
+            self.timers["backward"] += tb.ms
+            self._maybe_sync(step)
+            return met
         with Timer(self.dev) as tf:
             outs = net.forward(training=True)
             roots, seeds = net.backward_roots(outs)

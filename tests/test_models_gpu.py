@@ -548,7 +548,8 @@ def test_fused_downsample_bn_block_bitwise(gpu, monkeypatch, stride):
         singa_amd.set_deterministic(False)
     assert torch.equal(res["0"][0], res["1"][0])
     assert set(res["0"][1]) == set(res["1"][1])
-    diff = [k for k in res["0"][1] if not torch.equal(res["0"][1][k], res["1"][1][k])]
+    diff = {k: float((res["0"][1][k] - res["1"][1][k]).abs().max()) for k in res["0"][1]
+            if not torch.equal(res["0"][1][k], res["1"][1][k])}
     assert not diff, diff
 
 
