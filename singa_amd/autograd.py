@@ -317,7 +317,7 @@ def backward(y, dy=None) -> Iterator[Tuple[Tensor, Tensor]]:
             if dx is ACCUMULATED or dx is ACC_INPLACE:
                 dx = None  # (ACC_INPLACE: already summed into pending[src_op])
             elif dx is not None and dx.dtype != op.src_dt[i] and dx.is_floating_point():
-                dx = dx.to(op.src_dt[i])  # mixed-precision edge: grads take the producer's dtype
+                dx = G.to(dx, op.src_dt[i])  # mixed-precision edge: grads take the producer's dtype
             if src_op not in pending:
                 pending[src_op] = [None] * src_op.n_out
             j = op.src_idx[i]
@@ -627,7 +627,7 @@ class Linear(Operator):
         p = self.params[1] if len(self.params) > 1 else None
         if p is not None and p.low is not None and x.dtype == torch.bfloat16:
             return p.low
-        return W.to(x.dtype)
+        return G.to(W, x.dtype)
 
     def backward(self, dy):
         x2, w = self.x2, self.w
@@ -708,18 +708,15 @@ class Conv2d(Operator):
                 # residual BN: this dgrad's accumulation completes its output gradient
                 bnp = (prod.x, prod.st, prod.st.mask)
         wt_pre, self.wt_pre = getattr(self, "wt_pre", None), None
+        tb = self.grad_target(2) if self.has_bias else None
         dx, dw, db = F.conv2d_bwd(x, w, dy, self.stride, self.padding, self.dilation, self.group,
                                   need_dx=self.needs_grad(0), dw_out=tgt, need_db=self.has_bias, dx_acc=acc,
-                                  bn_producer=bnp, wt_pre=wt_pre)
+                                  bn_producer=bnp, wt_pre=wt_pre, db_out=tb)
         if acc is not None and dx is acc:
             dx = ACC_INPLACE
         res = [dx, ACCUMULATED if tgt is not None else dw]
         if self.has_bias:
-            tb = self.grad_target(2)
-            if tb is not None:
-                G.binary("add", tb, G.reshape(db, tb.shape), out=tb)
-                db = ACCUMULATED
-            res.append(db)
+            res.append(ACCUMULATED if tb is not None else db)  # accumulated into the grad view by the kernel
         return tuple(res)
 
 

@@ -758,7 +758,11 @@ def _gconv_fwd(x, w, b, stride, padding, dilation, groups, out_dtype, relu):
     return y if y.dtype == out_dtype else cast(y, out_dtype)
 
 
-def _gconv_bwd(x, w, dy, stride, padding, dilation, groups, need_dx, dw_out, need_db, dx_acc):
+def _db_ok(db_out, K):
+    return db_out is not None and db_out.dtype == torch.float32 and db_out.is_contiguous() and db_out.numel() == K
+
+
+def _gconv_bwd(x, w, dy, stride, padding, dilation, groups, need_dx, dw_out, need_db, dx_acc, db_out=None):
     sh, sw = stride
     ph, pw = padding
     dh, dw_ = dilation
@@ -791,7 +795,12 @@ def _gconv_bwd(x, w, dy, stride, padding, dilation, groups, need_dx, dw_out, nee
         dwt = G.binary("add", dw_out, target, out=dw_out)
     else:
         dwt = target
-    db = colsum(dyc.permute(0, 2, 3, 1).reshape(-1, K))[0] if need_db else None
+    db = None
+    if need_db:
+        acc = _db_ok(db_out, K)
+        db = colsum(dyc.permute(0, 2, 3, 1).reshape(-1, K), out=db_out.view(-1) if acc else None)[0]
+        if db_out is not None and not acc:
+            db = G.binary("add", db_out, G.reshape(db, db_out.shape), out=db_out)
     return dx, dwt, db
 
 
@@ -936,9 +945,11 @@ def pretranspose_conv_weights(items) -> dict:
 
 def conv2d_bwd(x: torch.Tensor, w: torch.Tensor, dy: torch.Tensor, stride, padding, dilation=(1, 1), groups=1,
                need_dx=True, dw_out: Optional[torch.Tensor] = None, need_db=False,
-               dx_acc: Optional[torch.Tensor] = None, bn_producer=None, wt_pre: Optional[torch.Tensor] = None):
+               dx_acc: Optional[torch.Tensor] = None, bn_producer=None, wt_pre: Optional[torch.Tensor] = None,
+               db_out: Optional[torch.Tensor] = None):
     """Returns (dx, dw, db).  If dw_out (fp32, same logical shape as w) is given
-    the weight gradient is ACCUMULATED into it (flat grad buffer views).
+    the weight gradient is ACCUMULATED into it (flat grad buffer views); the
+    same for the bias gradient with ``db_out`` (fp32 [K]).
     ``dx_acc``: an existing gradient of x (another consumer's contribution);
     when its layout allows, the data gradient is added into it in the dgrad
     epilogue and ``dx_acc`` itself is returned as dx.
@@ -954,7 +965,7 @@ def conv2d_bwd(x: torch.Tensor, w: torch.Tensor, dy: torch.Tensor, stride, paddi
     dh, dw_ = dilation
     if _native_ok(x, w, dy) and not (groups == 1 and x.dtype == torch.bfloat16 and
                                      (not need_dx or (dh == 1 and dw_ == 1 and sh * sw <= 16))):
-        return _gconv_bwd(x, w, dy, stride, padding, dilation, groups, need_dx, dw_out, need_db, dx_acc)
+        return _gconv_bwd(x, w, dy, stride, padding, dilation, groups, need_dx, dw_out, need_db, dx_acc, db_out)
     if _native_ok(x, w, dy) and groups == 1:
         Nn, Cx, H, W = x.shape
         K, C, R, S = w.shape
@@ -1046,7 +1057,10 @@ def conv2d_bwd(x: torch.Tensor, w: torch.Tensor, dy: torch.Tensor, stride, paddi
             else:
                 dwt = G.contiguous(g)
         if need_db:
-            db = colsum(dyb.permute(0, 2, 3, 1).reshape(-1, Kp))[0][:K]
+            acc = Kp == K and _db_ok(db_out, K)
+            db = colsum(dyb.permute(0, 2, 3, 1).reshape(-1, Kp), out=db_out.view(-1) if acc else None)[0][:K]
+            if db_out is not None and not acc:
+                db = G.binary("add", db_out, G.reshape(db, db_out.shape), out=db_out)
         return dx, dwt, db
     _no_native("conv2d_bwd", x, w, dy)
     if CP.ok(x, w, dy):
@@ -1057,11 +1071,15 @@ def conv2d_bwd(x: torch.Tensor, w: torch.Tensor, dy: torch.Tensor, stride, paddi
         dx = torch.empty(x.shape, dtype=torch.float32) if need_dx else None
         direct = dw_out is not None and CP.ok(dw_out) and dw_out.is_contiguous()
         dwt = dw_out if direct else G.zeros(tuple(w.shape), torch.float32, x.device)
-        db = G.zeros((K,), torch.float32, x.device) if need_db else None
+        db = None
+        if need_db:
+            db = db_out if _db_ok(db_out, K) else G.zeros((K,), torch.float32, x.device)
         CP.lib().conv_bwd(xc.data_ptr(), wc.data_ptr(), dyc.data_ptr(), CP.p(dx), dwt.data_ptr(), CP.p(db), Nn, Cx, H,
                           W, K, R, S, Ho, Wo, sh, sw, ph, pw, dh, dw_, groups)
         if dw_out is not None and not direct:
             dwt = G.binary("add", dw_out, dwt, out=dw_out)
+        if db is not None and db_out is not None and db is not db_out:
+            db = G.binary("add", db_out, G.reshape(db, db_out.shape), out=db_out)
         return dx, dwt, db
     # CPU reference via autograd of the functional conv
     with torch.enable_grad():
@@ -1075,6 +1093,8 @@ def conv2d_bwd(x: torch.Tensor, w: torch.Tensor, dy: torch.Tensor, stride, paddi
         dw_out.add_(gw)
         gw = dw_out
     db = dy.float().sum(dim=(0, 2, 3)) if need_db else None
+    if db is not None and db_out is not None:
+        db = db_out.add_(db.reshape(db_out.shape))
     return dx, gw, db
 
 

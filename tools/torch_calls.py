@@ -63,7 +63,21 @@ class Tracer(TorchFunctionMode):
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--which", default="resnet50,alexnet,bert,bert_sonnx,mlp_gpu,conv_conf")
+    ap.add_argument("--native", default="copy_nd,fill,reduce,zero,binary_nd",
+                    help="also record the call sites of these native (_C) launches")
     a = ap.parse_args()
+    from singa_amd.ops import native as NN
+    L = NN.lib()
+    nat = collections.Counter()
+    for fname in [f for f in a.native.split(",") if f and hasattr(L, f)]:
+        def wrap(orig, fname=fname):
+            def f(*args, **kw):
+                site = " <- ".join(f"{fr.filename.replace(os.getcwd() + '/', '')}:{fr.lineno}"
+                                   for fr in traceback.extract_stack()[-6:-1])
+                nat[(fname, site)] += 1
+                return orig(*args, **kw)
+            return f
+        setattr(L, fname, wrap(getattr(L, fname)))
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__))))
     import bench_suite as BS
 
@@ -79,7 +93,6 @@ def main() -> int:
         tr = Tracer()
         with tr:
             if w == "resnet50":
-                import subprocess
                 # bench.py is its own process: trace it through this tool's
                 # import of its main() instead
                 sys.argv = ["bench.py", "--steps", "2", "--warmup", "1", "--batch", "64", "--no-ps-parity"]
@@ -96,6 +109,10 @@ def main() -> int:
         print(f"== {w}: {sum(tr.calls.values())} torch calls on device data")
         for (name, site), n in tr.calls.most_common(40):
             print(f"  {n:5d}  {name:24s} {site}")
+        print(f"-- {w}: native glue launches by call site")
+        for (name, site), n in nat.most_common(25):
+            print(f"  {n:5d}  {name:24s} {site}")
+        nat.clear()
         sys.stdout.flush()
     return 0
 

@@ -66,16 +66,20 @@ def main():
         loss.backward()
         opt.step()
         return loss
-    for _ in range(a.warmup):
+    import sys
+    for i in range(a.warmup):
         step()
+        torch.cuda.synchronize()
+        print(f"warmup step {i} done", file=sys.stderr, flush=True)  # MIOpen's first-call searches are slow
     torch.cuda.synchronize()
     t = time.perf_counter()
     for _ in range(a.steps):
         step()
     torch.cuda.synchronize()
     el = time.perf_counter() - t
-    print(json.dumps({"yardstick": "pytorch-miopen resnet50 bf16 autocast", "images_per_s": a.batch * a.steps / el,
-                      "ms_per_step": 1e3 * el / a.steps, "batch": a.batch}))
+    print(json.dumps({"yardstick": "pytorch-miopen resnet50 bf16 autocast channels_last", "images_per_s":
+                      a.batch * a.steps / el, "ms_per_step": 1e3 * el / a.steps, "batch": a.batch,
+                      "torch": torch.__version__}))
 
 
 if __name__ == "__main__":
