@@ -65,6 +65,7 @@ def main() -> int:
 
     from singa_amd import device, opt, tensor
     from singa_amd.models import resnet
+    from singa_amd.ops import glue as G
     from singa_amd.parallel import DistOpt, init_distributed
 
     dev = device.create_rocm_gpu_on(local % torch.cuda.device_count(), set_default=True)
@@ -99,7 +100,6 @@ def main() -> int:
     if args.warmup > 0:
         # guard against a silently truncated backward (it would inflate the
         # number): after a step every parameter must hold a non-zero gradient
-        from singa_amd.ops import glue as G
         st = optimizer.store
         norms = G.cat([G.reduce(st.g[off:off + p.data.numel()], None, "sumsq").reshape(1)
                        for p, off in zip(st.params, st.offsets)]).cpu()  # native reductions, one copy back
@@ -115,7 +115,7 @@ def main() -> int:
     for _ in range(args.steps):
         out, loss = m(tx, ty)
         if args.loss_curve:
-            curve.append(round(float(loss.data.float().item()), 4))
+            curve.append(round(float(G.to(loss.data, torch.float32).cpu()), 4))
     torch.cuda.synchronize()
     if world > 1:
         comm.barrier()
@@ -125,7 +125,7 @@ def main() -> int:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev.torch_device)
         comm.all_reduce(t, op="max")
         elapsed = float(t.item())
-    final_loss = float(loss.data.float().item())
+    final_loss = float(G.to(loss.data, torch.float32).cpu())
     ps = None
     if not args.no_ps_parity:
         # the reference's own headline benchmark (PS update+collect of the 12

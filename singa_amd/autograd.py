@@ -571,9 +571,9 @@ class Matmul(Operator):
             return da, db
         # batched: flatten leading dims (broadcast operands are reduced by _unbroadcast)
         lead = torch.broadcast_shapes(a.shape[:-2], b.shape[:-2])
-        a3 = a.expand(*lead, *a.shape[-2:]).reshape(-1, *a.shape[-2:])
-        b3 = b.expand(*lead, *b.shape[-2:]).reshape(-1, *b.shape[-2:])
-        d3 = dy.reshape(-1, *dy.shape[-2:])
+        a3 = G.reshape(a.expand(*lead, *a.shape[-2:]), (-1, *a.shape[-2:]))
+        b3 = G.reshape(b.expand(*lead, *b.shape[-2:]), (-1, *b.shape[-2:]))
+        d3 = G.reshape(dy, (-1, *dy.shape[-2:]))
         da = db = None
         if self.needs_grad(0):
             da = _unbroadcast(F.gemm(d3, b3, tb=True, out_dtype=a.dtype).reshape(*lead, *a.shape[-2:]), a.shape)
@@ -614,12 +614,12 @@ class Linear(Operator):
     def forward(self, x, W, b=None):
         w = self._w_compute(x, W)
         lead = x.shape[:-1]
-        x2 = x.reshape(-1, x.shape[-1])
+        x2 = G.reshape(x, (-1, x.shape[-1]))
         bias = G.to(b, torch.float32) if b is not None else None
         y = F.matmul(x2, w, out_dtype=x.dtype, bias=bias)
         if self.requires_grad:
             self.x2, self.w = x2, w
-        return y.reshape(*lead, y.shape[-1])
+        return G.reshape(y, (*lead, y.shape[-1]))
 
     def _w_compute(self, x, W):
         if x.dtype == W.dtype:
@@ -632,11 +632,11 @@ class Linear(Operator):
     def backward(self, dy):
         x2, w = self.x2, self.w
         self.x2 = self.w = None
-        dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
+        dy2 = G.contiguous(G.reshape(dy, (-1, dy.shape[-1])))
         dx = None
         if self.needs_grad(0):
             dx = F.gemm_nt(dy2, w, out_dtype=x2.dtype)
-            dx = dx.reshape(*dy.shape[:-1], x2.shape[-1])
+            dx = G.reshape(dx, (*dy.shape[:-1], x2.shape[-1]))
         tgt = self.grad_target(1)
         if tgt is not None:
             F.gemm_tn_acc(x2, dy2, tgt)
@@ -848,7 +848,7 @@ class GlobalAveragePool(Operator):
         return y.reshape(y.shape[0], y.shape[1], 1, 1) if self.keepdims else y
 
     def backward(self, dy):
-        return F.global_avgpool_bwd(dy.reshape(dy.shape[0], dy.shape[1]).contiguous(), self.xs)
+        return F.global_avgpool_bwd(G.contiguous(G.reshape(dy, (dy.shape[0], dy.shape[1]))), self.xs)
 
 
 class LRN(Operator):
@@ -1085,10 +1085,10 @@ class Reshape(Operator):
     def forward(self, x):
         self.in_shape = x.shape
         shape = [x.shape[i] if s == 0 and i < x.dim() else s for i, s in enumerate(self.shape)]
-        return x.reshape(shape)
+        return G.reshape(x, shape)
 
     def backward(self, dy):
-        return dy.reshape(self.in_shape)
+        return G.reshape(dy, self.in_shape)
 
 
 class Flatten(Operator):
@@ -1100,10 +1100,10 @@ class Flatten(Operator):
         self.in_shape = x.shape
         a = self.axis % _b.max(x.dim(), 1) if x.dim() else 0
         lead = int(np.prod(x.shape[:a])) if a > 0 else 1
-        return x.reshape(lead, -1)
+        return G.reshape(x, (lead, -1))
 
     def backward(self, dy):
-        return dy.reshape(self.in_shape)
+        return G.reshape(dy, self.in_shape)
 
 
 class Attention(Operator):

@@ -31,18 +31,25 @@ import torch  # noqa: E402
 CURVE = []
 
 
+def _snap(loss):
+    """A private fp32 copy of a (graph-static) loss tensor: one native copy
+    kernel, no PyTorch kernel in the profiled step."""
+    from singa_amd.ops import glue as G
+    return G.copy_(torch.empty((), dtype=torch.float32, device=loss.device), G.reshape(loss, ()))
+
+
 def _time(step, steps, warmup, sync):
     """Times ``steps`` calls after ``warmup``; every step's loss is kept as a
     device tensor (no host sync inside the timed loop) and reported after."""
     CURVE.clear()
     for _ in range(warmup):
         out = step()
-        CURVE.append(out[1].data.detach().float().reshape(()).clone())
+        CURVE.append(_snap(out[1].data))
     sync()
     t0 = time.perf_counter()
     for _ in range(steps):
         out = step()
-        CURVE.append(out[1].data.detach().float().reshape(()).clone())
+        CURVE.append(_snap(out[1].data))
     sync()
     dt = (time.perf_counter() - t0) / steps
     return dt, out
@@ -74,7 +81,7 @@ def bench_mlp(a, gpu):
     name = "mlp_gpu" if gpu else "mlp_cpu"
     model = "MLP 784-2500-2000-1500-1000-500-10 stanh" if gpu else "MLP 784-512-10 relu"
     return _rec(name, "samples/s", B, dt, model=model, batch=B, device="RocmGPU" if gpu else "CppCPU",
-                dtype="fp32", optimizer="SGD momentum 0.9", final_loss=round(float(loss.data.float()), 4))
+                dtype="fp32", optimizer="SGD momentum 0.9", final_loss=round(float(_snap(loss.data)), 4))
 
 
 def bench_alexnet(a):
@@ -93,7 +100,7 @@ def bench_alexnet(a):
     m.train()
     dt, (_, loss) = _time(lambda: m(x, y), a.steps, a.warmup, torch.cuda.synchronize)
     return _rec("alexnet", "images/s", B, dt, model="AlexNet-224 (LRN, dropout 0.5)", batch=B,
-                optimizer="SGD momentum 0.9 wd 5e-4", final_loss=round(float(loss.data.float()), 4))
+                optimizer="SGD momentum 0.9 wd 5e-4", final_loss=round(float(_snap(loss.data)), 4))
 
 
 def _bert_inputs(dev, B, S, vocab):
@@ -119,7 +126,7 @@ def bench_bert(a):
     m.train()
     dt, (_, loss) = _time(lambda: m(ids, y), a.steps, a.warmup, torch.cuda.synchronize)
     return _rec("bert", "sequences/s", B, dt, model="BERT-base (native)", batch=B, seq_len=S, optimizer="Adam",
-                final_loss=round(float(loss.data.float()), 4))
+                final_loss=round(float(_snap(loss.data)), 4))
 
 
 def bench_bert_sonnx(a):
@@ -144,7 +151,7 @@ def bench_bert_sonnx(a):
     dt, (_, loss) = _time(lambda: sm(ids, y), a.steps, a.warmup, torch.cuda.synchronize)
     return _rec("bert_sonnx", "sequences/s", B, dt, model="BERT-base exported -> ONNX -> sonnx import",
                 onnx_bytes=len(blob), batch=B, seq_len=S, optimizer="Adam",
-                final_loss=round(float(loss.data.float()), 4))
+                final_loss=round(float(_snap(loss.data)), 4))
 
 
 def main():
