@@ -69,10 +69,18 @@ def main():
             m_w = timeit(lambda: torch.ops.aten.convolution_backward(dy, x, w, None, (st, st), (pad, pad), (1, 1),
                                                                      False, (0, 0), 1, (False, True, False)))
         ours = t_f + (t_d - t_dw_only if t_d > t_dw_only else t_d) + t_w
+        # roofline: 2.5 PF dense bf16, 6.2 TB/s measured HBM copy ceiling (bw_probe_copy.jsonl)
+        bx, by, bw_ = B * C * H * H * 2, B * K * Ho * Ho * 2, K * C * R * R * 2
+        roof = lambda byts: max(flop / 2.5e12, byts / 6.2e9)  # noqa: E731  (ms)
+        t_dg = max(t_d - t_w, 1e-6)
         rec = {"C": C, "H": H, "K": K, "R": R, "s": st, "n": cnt,
                "fwd_ms": round(t_f, 3), "dgrad+wgrad_ms": round(t_d, 3), "wgrad_ms": round(t_w, 3),
                "miopen_fwd_ms": round(m_f, 3), "miopen_dgrad_ms": round(m_d, 3), "miopen_wgrad_ms": round(m_w, 3),
-               "fwd_TF": round(flop / t_f / 1e9, 1), "miopen_fwd_TF": round(flop / m_f / 1e9, 1)}
+               "fwd_TF": round(flop / t_f / 1e9, 1), "miopen_fwd_TF": round(flop / m_f / 1e9, 1),
+               "dgrad_TF": round(flop / t_dg / 1e9, 1), "wgrad_TF": round(flop / t_w / 1e9, 1),
+               "fwd_roof": round(roof(bx + by + bw_) / t_f, 2), "dgrad_roof": round(roof(bx + by + bw_) / t_dg, 2),
+               "wgrad_roof": round(roof(bx + by + 2 * bw_) / t_w, 2),
+               "step_ms": round(cnt * (t_f + t_d), 3)}
         tot["ours"] += cnt * (t_f + t_d)
         tot["miopen"] += cnt * (m_f + m_d + m_w)
         print(json.dumps(rec), flush=True)
