@@ -20,11 +20,19 @@
 // MFMAs).  Every operand element is loaded through a "unit" of 4 elements
 // that are contiguous in memory when the shapes allow (one 16-byte fp32 / 8-
 // byte bf16 vector load), or 4 bounds-checked scalar loads otherwise, so no
-// dimension needs padding.  LDS images are [rows][32 k (+pad)]: each MFMA
-// lane reads its 4 (fp32) or 8 (bf16) consecutive k of one row with a single
+// dimension needs padding.  LDS images are [rows][32 k]: each MFMA lane reads
+// its 4 (fp32) or 8 (bf16) consecutive k of one row with a single
 // ds_read_b128 -- the k order inside an MFMA step is permuted identically for
-// A and B, which leaves the sum unchanged.  Row pads of 16 bytes make the
-// 16-lane read groups conflict-free (row strides 144 B / 80 B).
+// A and B, which leaves the sum unchanged.
+//   fp32: unpadded 128-B rows, the 16-B chunk c of row r stored at chunk
+//         c ^ swz(r), swz(r) = (r ^ r >> 2) & 7: 8 consecutive rows (one
+//         b128 read phase) hit 8 distinct chunks, and so do the 8 row-quads
+//         a K-outer loader scatters its scalar stores over (an 8-way bank
+//         conflict with a padded [rows][36] image);
+//   bf16: rows padded by 16 bytes (80-B stride), conflict-free b128 reads.
+// fp32 tiles of 128 x 128 run v_mfma_f32_32x32x2_f32 (each wave 64 x 64 as
+// 2 x 2 blocks, lane halves reading alternate k-chunks); 64 x 64 tiles run
+// v_mfma_f32_16x16x4_f32.
 //
 // Operand modes (the loader gathers the implicit-GEMM operands itself):
 //   KMAJ    plain [rows][K] (ld)                     k-contiguous units
@@ -36,8 +44,11 @@
 //   WGRAD_B conv wgrad B: x gathered, rows = (r, s, c), k = output pixels
 // A group of a grouped convolution is one batch index (blockIdx.y): every
 // operand and the output advance by their per-group batch stride.
+#include <stdlib.h>
+
 #include <stdexcept>
 #include <string>
+#include <type_traits>
 
 #include "common.h"
 
@@ -76,8 +87,11 @@ template <typename T> struct V4;
 template <> struct V4<float> { typedef f32x4 t; };
 template <> struct V4<bf16> { typedef bf16x4 t; };
 
-template <typename T> constexpr int pad_of() { return sizeof(T) == 4 ? 4 : 8; }
+template <typename T> constexpr int pad_of() { return sizeof(T) == 4 ? 0 : 8; }
 template <typename T> constexpr int ld_of() { return BK + pad_of<T>(); }
+// fp32 LDS image: element offset of (row, k) -- 16-byte chunk XOR swizzle
+__device__ __forceinline__ int swz(int r) { return (r ^ (r >> 2)) & 7; }
+__device__ __forceinline__ int f32_pos(int row, int k) { return row * BK + 4 * (((k >> 2) ^ swz(row))) + (k & 3); }
 
 // One operand's loader: ROWS tile rows x BK k, U units of 4 elements / thread.
 template <typename T, int ROWS, int MODE>
@@ -245,7 +259,23 @@ struct Ld {
   __device__ __forceinline__ void store(T* lds) const {
     constexpr int LD = ld_of<T>();
     const int t = threadIdx.x;
-    if constexpr (!RC) {
+    if constexpr (sizeof(T) == 4) {  // swizzled unpadded image
+      if constexpr (!RC) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int row = (t >> 3) + 32 * u;
+          *(VT*)(lds + f32_pos(row, 4 * (t & 7))) = v[u];
+        }
+      } else {
+        const int r4 = 4 * (t % RQ);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int k = t / RQ + KS * u;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) lds[f32_pos(r4 + e, k)] = v[u][e];
+        }
+      }
+    } else if constexpr (!RC) {
 #pragma unroll
       for (int u = 0; u < U; ++u) *(VT*)(lds + ((t >> 3) + 32 * u) * LD + 4 * (t & 7)) = v[u];
     } else {
@@ -265,7 +295,11 @@ __global__ void __launch_bounds__(NT, 2) ggemm_k(const Args p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int LD = ld_of<T>();
   constexpr int A_EL = BM * LD, STAGE_EL = (BM + BN) * LD;
-  constexpr int WTM = BM / 2, WTN = BN / 2, TM = WTM / 16, TN = WTN / 16;
+  // fp32 128x128: 32x32x2 MFMA blocks (each wave 2 x 2 of them)
+  constexpr bool M32 = sizeof(T) == 4 && BM == 128 && BN == 128;
+  constexpr int MB = M32 ? 32 : 16;
+  constexpr int WTM = BM / 2, WTN = BN / 2, TM = WTM / MB, TN = WTN / MB;
+  typedef typename std::conditional<M32, f32x16, f32x4>::type AccT;
   T* lds = (T*)smem;
 
   const int64_t y = blockIdx.y;
@@ -301,23 +335,44 @@ __global__ void __launch_bounds__(NT, 2) ggemm_k(const Args p) {
 
   const int l = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wm = wid >> 1, wn = wid & 1;
-  f32x4 acc[TM][TN];
+  AccT acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < TN; ++j) acc[i][j] = AccT{};
 
   const int g4 = l >> 4;
   auto compute = [&](const T* sa_) {
     const T* sb_ = sa_ + A_EL;
-    if constexpr (sizeof(T) == 4) {
+    if constexpr (M32) {
+      // lane half h = l >> 5 reads k-chunk 2q + h of rows (l & 31): element e
+      // of the float4 feeds the MFMA over the k pair {8q + e, 8q + 4 + e}
+      const int h = l >> 5;
+#pragma unroll
+      for (int q = 0; q < BK / 8; ++q) {
+        float4 fa[TM], fb[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) fa[i] = *(const float4*)(sa_ + f32_pos(wm * WTM + 32 * i + (l & 31), 8 * q + 4 * h));
+#pragma unroll
+        for (int j = 0; j < TN; ++j) fb[j] = *(const float4*)(sb_ + f32_pos(wn * WTN + 32 * j + (l & 31), 8 * q + 4 * h));
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fb[j].x, fa[i].x, acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fb[j].y, fa[i].y, acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fb[j].z, fa[i].z, acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fb[j].w, fa[i].w, acc[i][j], 0, 0, 0);
+          }
+      }
+    } else if constexpr (sizeof(T) == 4) {
 #pragma unroll
       for (int c = 0; c < BK / 16; ++c) {
         float4 fa[TM], fb[TN];
 #pragma unroll
-        for (int i = 0; i < TM; ++i) fa[i] = *(const float4*)(sa_ + (wm * WTM + 16 * i + (l & 15)) * LD + 16 * c + 4 * g4);
+        for (int i = 0; i < TM; ++i) fa[i] = *(const float4*)(sa_ + f32_pos(wm * WTM + 16 * i + (l & 15), 16 * c + 4 * g4));
 #pragma unroll
-        for (int j = 0; j < TN; ++j) fb[j] = *(const float4*)(sb_ + (wn * WTN + 16 * j + (l & 15)) * LD + 16 * c + 4 * g4);
+        for (int j = 0; j < TN; ++j) fb[j] = *(const float4*)(sb_ + f32_pos(wn * WTN + 16 * j + (l & 15), 16 * c + 4 * g4));
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -365,73 +420,82 @@ __global__ void __launch_bounds__(NT, 2) ggemm_k(const Args p) {
     }
   }
 
-  // Epilogue: acc[i][j][r] = C[m = .. + (l & 15)][n = .. + 4 (l >> 4) + r]
+  // Epilogue: 16x16 blocks acc[i][j][r] = C[m = .. + (l & 15)][n = .. + 4 (l >> 4) + r];
+  // 32x32 blocks acc[i][j][4 g + r] = C[m = .. + (l & 31)][n = .. + 8 g + 4 (l >> 5) + r]
   char* pc = (char*)p.c + y * p.sc * (p.out_mode == O_BF16 ? 2 : 4);
-#pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    const int m = m0 + wm * WTM + 16 * i + (l & 15);
-    if (m >= p.M) continue;
+  auto store4 = [&](int m, int n, const float* a4) {
+    if (m >= p.M || n >= p.N) return;
     const int64_t rowoff = (int64_t)m * p.ldc;
+    const bool full = n + 3 < p.N;
+    float v[4] = {a4[0] * p.alpha, a4[1] * p.alpha, a4[2] * p.alpha, a4[3] * p.alpha};
+    if (p.out_mode == O_F32_ATOMIC) {
+      float* c = (float*)pc + rowoff + n;
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int n = n0 + wn * WTN + 16 * j + 4 * g4;
-      if (n >= p.N) continue;
-      const bool full = n + 3 < p.N;
-      float v[4] = {acc[i][j][0] * p.alpha, acc[i][j][1] * p.alpha, acc[i][j][2] * p.alpha,
-                    acc[i][j][3] * p.alpha};
-      if (p.out_mode == O_F32_ATOMIC) {
-        float* c = (float*)pc + rowoff + n;
+      for (int r = 0; r < 4; ++r)
+        if (full || n + r < p.N) atomicAdd(c + r, v[r]);
+      return;
+    }
+    if (bias) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] += (full || n + r < p.N) ? bias[n + r] : 0.f;
+    }
+    if (p.out_mode == O_F32) {
+      float* c = (float*)pc + rowoff + n;
+      const bool vst = full && ((p.ldc & 3) == 0) && (((uintptr_t)c & 15) == 0);
+      if (p.beta != 0.f) {
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          if (full || n + r < p.N) atomicAdd(c + r, v[r]);
-        continue;
+          if (full || n + r < p.N) v[r] += p.beta * c[r];
       }
-      if (bias) {
+      if (p.relu) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] += (full || n + r < p.N) ? bias[n + r] : 0.f;
+        for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
       }
-      if (p.out_mode == O_F32) {
-        float* c = (float*)pc + rowoff + n;
-        const bool vst = full && ((p.ldc & 3) == 0) && (((uintptr_t)c & 15) == 0);
-        if (p.beta != 0.f) {
+      if (vst) *(float4*)c = make_float4(v[0], v[1], v[2], v[3]);
+      else {
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (full || n + r < p.N) v[r] += p.beta * c[r];
-        }
-        if (p.relu) {
+        for (int r = 0; r < 4; ++r)
+          if (n + r < p.N) c[r] = v[r];
+      }
+    } else {
+      bf16* c = (bf16*)pc + rowoff + n;
+      const bool vst = full && ((p.ldc & 3) == 0) && (((uintptr_t)c & 7) == 0);
+      if (p.beta != 0.f) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
-        }
-        if (vst) *(float4*)c = make_float4(v[0], v[1], v[2], v[3]);
-        else {
+        for (int r = 0; r < 4; ++r)
+          if (full || n + r < p.N) v[r] += p.beta * (float)c[r];
+      }
+      if (p.relu) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (n + r < p.N) c[r] = v[r];
-        }
+        for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+      }
+      if (vst) {
+        bf16x4 o;
+        o[0] = (bf16)v[0]; o[1] = (bf16)v[1]; o[2] = (bf16)v[2]; o[3] = (bf16)v[3];
+        *(bf16x4*)c = o;
       } else {
-        bf16* c = (bf16*)pc + rowoff + n;
-        const bool vst = full && ((p.ldc & 3) == 0) && (((uintptr_t)c & 7) == 0);
-        if (p.beta != 0.f) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (full || n + r < p.N) v[r] += p.beta * (float)c[r];
-        }
-        if (p.relu) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
-        }
-        if (vst) {
-          bf16x4 o;
-          o[0] = (bf16)v[0]; o[1] = (bf16)v[1]; o[2] = (bf16)v[2]; o[3] = (bf16)v[3];
-          *(bf16x4*)c = o;
-        } else {
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (n + r < p.N) c[r] = (bf16)v[r];
-        }
+        for (int r = 0; r < 4; ++r)
+          if (n + r < p.N) c[r] = (bf16)v[r];
       }
     }
-  }
+  };
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      if constexpr (M32) {
+        const int m = m0 + wm * WTM + 32 * i + (l & 31);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float a4[4] = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
+          store4(m, n0 + wn * WTN + 32 * j + 8 * g + 4 * (l >> 5), a4);
+        }
+      } else {
+        const float a4[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        store4(m0 + wm * WTM + 16 * i + (l & 15), n0 + wn * WTN + 16 * j + 4 * g4, a4);
+      }
+    }
 }
 
 template <typename T, int BM, int BN, int AM, int BMODE>
@@ -448,21 +512,37 @@ static void launch_t(const Args& p, int batch, int splits, hipStream_t s) {
   hipLaunchKernelGGL(kern, dim3(tiles, batch, splits), dim3(NT), lds, s, p);
 }
 
-static bool big_tile(int M, int N) {
+// minimum 128x128 tile count for the big tile (fp32 / bf16); SG_GG_T128_F32 /
+// SG_GG_T128 override (A/B tuning)
+static long t128_min(bool f32) {
+  static const long v32 = [] {
+    // measured (mlp_gpu, MI355X): 64x64 16x16x4 tiles everywhere 749k samples/s,
+    // 128x128 32x32x2 tiles from 96 tiles up 352k -- the big fp32 tile stays opt-in
+    const char* e = getenv("SG_GG_T128_F32");
+    return e ? atol(e) : (1L << 40);
+  }();
+  static const long v16 = [] {
+    const char* e = getenv("SG_GG_T128");
+    return e ? atol(e) : 192L;
+  }();
+  return f32 ? v32 : v16;
+}
+
+static bool big_tile(int M, int N, bool f32 = false) {
   const long t128 = (long)((M + 127) / 128) * ((N + 127) / 128);
-  return M >= 128 && N >= 128 && t128 >= 192;
+  return M >= 128 && N >= 128 && t128 >= t128_min(f32);
 }
 
 template <typename T, int AM, int BMODE>
 static void launch(const Args& p, int batch, int splits, hipStream_t s) {
-  if (big_tile(p.M, p.N)) launch_t<T, 128, 128, AM, BMODE>(p, batch, splits, s);
+  if (big_tile(p.M, p.N, sizeof(T) == 4)) launch_t<T, 128, 128, AM, BMODE>(p, batch, splits, s);
   else launch_t<T, 64, 64, AM, BMODE>(p, batch, splits, s);
 }
 
 // split-K count for atomic outputs: fill ~512 workgroups, >= 4 K-tiles each
-static int pick_splits(int M, int N, int K, int batch, int want) {
+static int pick_splits(int M, int N, int K, int batch, int want, bool f32) {
   if (want > 0) return want;
-  const int bm = big_tile(M, N) ? 128 : 64;
+  const int bm = big_tile(M, N, f32) ? 128 : 64;
   const long tiles = (long)((M + bm - 1) / bm) * ((N + bm - 1) / bm) * (batch > 0 ? batch : 1);
   const int nkt = (K + BK - 1) / BK;
   int sp = 1;
@@ -518,7 +598,7 @@ void sg_ggemm(int dt, const void* a, int64_t lda, int a_kouter, int64_t sa, cons
   p.a = a; p.lda = lda; p.sa = sa; p.b = b; p.ldb = ldb; p.sb = sb;
   p.c = c; p.ldc = ldc; p.sc = sc; p.alpha = alpha; p.beta = beta; p.bias = (const float*)bias; p.sbias = 0;
   p.relu = relu; p.out_mode = out_mode;
-  splits = out_mode == O_F32_ATOMIC ? pick_splits(M, N, K, batch, splits) : 1;
+  splits = out_mode == O_F32_ATOMIC ? pick_splits(M, N, K, batch, splits, dt == 0) : 1;
   p.k_per_split = kps(K > 0 ? K : 1, splits);
   p.g = make_geom(1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0, 0, 1, 1, 1);
   const bool f = dt == 0;
@@ -596,7 +676,7 @@ void sg_gconv_wgrad(int dt, const void* x, const void* dy, void* dw_out, int N, 
   p.b = x; p.ldb = 0; p.sb = g.Cg;
   p.c = dw_out; p.ldc = (int64_t)R * S * g.Cg; p.sc = (int64_t)g.Kg * R * S * g.Cg;
   p.alpha = 1.f; p.beta = 0.f; p.bias = nullptr; p.relu = 0; p.out_mode = O_F32_ATOMIC;
-  splits = pick_splits(p.M, p.N, p.K, groups, splits);
+  splits = pick_splits(p.M, p.N, p.K, groups, splits, dt == 0);
   p.k_per_split = kps(p.K > 0 ? p.K : 1, splits);
   const bool f = dt == 0;
   p.vec_a = (f ? aligned<float>(dy, K, g.Kg, p.M) : aligned<sg::bf16>(dy, K, g.Kg, p.M)) ? 1 : 0;
