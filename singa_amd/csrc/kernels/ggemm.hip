@@ -423,6 +423,41 @@ __global__ void __launch_bounds__(NT, 2) ggemm_k(const Args p) {
   // Epilogue: 16x16 blocks acc[i][j][r] = C[m = .. + (l & 15)][n = .. + 4 (l >> 4) + r];
   // 32x32 blocks acc[i][j][4 g + r] = C[m = .. + (l & 31)][n = .. + 8 g + 4 (l >> 5) + r]
   char* pc = (char*)p.c + y * p.sc * (p.out_mode == O_BF16 ? 2 : 4);
+  // split-K partial tiles: staged through LDS and added row-contiguously (a
+  // wave-instruction's 64 atomics cover 256 contiguous bytes) -- straight from
+  // the MFMA layout each instruction would scatter over 16 rows
+  constexpr int LDT = BN + 4;
+  constexpr bool STAGED = BM * LDT * 4 <= 2 * STAGE_EL * (int)sizeof(T);
+  if (STAGED && p.out_mode == O_F32_ATOMIC) {
+    float* tile = (float*)smem;  // the K loop ended with a barrier: the stages are free
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        if constexpr (M32) {
+          const int ml = wm * WTM + 32 * i + (l & 31);
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            tile[ml * LDT + wn * WTN + 32 * j + 8 * (r >> 2) + 4 * (l >> 5) + (r & 3)] = acc[i][j][r] * p.alpha;
+        } else {
+          const int ml = wm * WTM + 16 * i + (l & 15);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) tile[ml * LDT + wn * WTN + 16 * j + 4 * g4 + r] = acc[i][j][r] * p.alpha;
+        }
+      }
+    __syncthreads();
+    float* cbase = (float*)pc;
+    for (int row = wid; row < BM; row += NT / 64) {
+      const int m = m0 + row;
+      if (m >= p.M) break;
+#pragma unroll
+      for (int c0 = 0; c0 < BN; c0 += 64) {
+        const int n = n0 + c0 + l;
+        if (c0 + l < BN && n < p.N) atomicAdd(cbase + (int64_t)m * p.ldc + n, tile[row * LDT + c0 + l]);
+      }
+    }
+    return;
+  }
   auto store4 = [&](int m, int n, const float* a4) {
     if (m >= p.M || n >= p.N) return;
     const int64_t rowoff = (int64_t)m * p.ldc;
@@ -600,6 +635,12 @@ void sg_ggemm(int dt, const void* a, int64_t lda, int a_kouter, int64_t sa, cons
   p.relu = relu; p.out_mode = out_mode;
   splits = out_mode == O_F32_ATOMIC ? pick_splits(M, N, K, batch, splits, dt == 0) : 1;
   p.k_per_split = kps(K > 0 ? K : 1, splits);
+  if (out_mode == O_F32_ATOMIC && splits == 1) {
+    // one writer per output element: accumulate with a plain read-add-store
+    // (C = alpha AB + 1 * C) instead of scattered fp32 atomics
+    p.out_mode = O_F32;
+    p.beta = 1.f;
+  }
   p.g = make_geom(1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0, 0, 1, 1, 1);
   const bool f = dt == 0;
   p.vec_a = f ? aligned<float>(a, lda, sa, a_kouter ? M : K) : aligned<sg::bf16>(a, lda, sa, a_kouter ? M : K);
@@ -678,6 +719,10 @@ void sg_gconv_wgrad(int dt, const void* x, const void* dy, void* dw_out, int N, 
   p.alpha = 1.f; p.beta = 0.f; p.bias = nullptr; p.relu = 0; p.out_mode = O_F32_ATOMIC;
   splits = pick_splits(p.M, p.N, p.K, groups, splits, dt == 0);
   p.k_per_split = kps(p.K > 0 ? p.K : 1, splits);
+  if (splits == 1) {  // single writer: read-add-store accumulation (see sg_ggemm)
+    p.out_mode = O_F32;
+    p.beta = 1.f;
+  }
   const bool f = dt == 0;
   p.vec_a = (f ? aligned<float>(dy, K, g.Kg, p.M) : aligned<sg::bf16>(dy, K, g.Kg, p.M)) ? 1 : 0;
   p.vec_b = (f ? aligned<float>(x, C, g.Cg) : aligned<sg::bf16>(x, C, g.Cg)) ? 1 : 0;

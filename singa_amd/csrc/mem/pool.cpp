@@ -1,0 +1,349 @@
+// Native memory pools: the framework's own device (HBM) and host allocators.
+//
+// Reference counterparts: mshadow's AllocSpace / FreeSpace
+// (include/mshadow/tensor.h:206-385, tensor_gpu-inl.hpp) and the Blob /
+// SyncedMemory pair (src/utils/blob.cc:83-298) that owned every parameter
+// and activation buffer of the reference.  Here:
+//
+//   * DevicePool: a caching allocator over hipMalloc for one GPU.  Blocks are
+//     rounded to size classes (512 B granularity up to 1 MiB, 2 MiB above),
+//     kept on per-size free lists and reused without touching the driver;
+//     a block freed while a stream may still be using it is parked with an
+//     event recorded on that stream and becomes reusable once the event has
+//     completed (no host synchronisation on the free path).
+//   * HostPool: 64-byte-aligned pageable blocks (CppCPU tensors) or pinned
+//     hipHostMalloc blocks (staging buffers for host <-> device copies).
+//   * Blocks are handed to PyTorch as DLPack tensors: storage owned by the
+//     pool, returned to it by the capsule's deleter when the last tensor
+//     referencing it dies.  PyTorch then only provides views / metadata.
+//
+// Exposed to Python (module _C) by register_mem(); singa_amd/memory.py wraps it.
+#include <hip/hip_runtime.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+#include <stdint.h>
+#include <stdlib.h>
+
+#include <map>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+namespace py = pybind11;
+
+namespace {
+
+// ------------------------------------------------------------- DLPack ABI
+// (the stable v0.x structs, declared here so no header is needed)
+struct DLDevice {
+  int32_t device_type;
+  int32_t device_id;
+};
+struct DLDataType {
+  uint8_t code, bits;
+  uint16_t lanes;
+};
+struct DLTensor {
+  void* data;
+  DLDevice device;
+  int32_t ndim;
+  DLDataType dtype;
+  int64_t* shape;
+  int64_t* strides;
+  uint64_t byte_offset;
+};
+struct DLManagedTensor {
+  DLTensor dl_tensor;
+  void* manager_ctx;
+  void (*deleter)(DLManagedTensor* self);
+};
+constexpr int32_t kDLCPU = 1;
+
+void hip_check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+size_t round_size(size_t n) {
+  if (n == 0) n = 1;
+  if (n <= (1u << 20)) return (n + 511) & ~(size_t)511;
+  return (n + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1);
+}
+
+struct Stats {
+  uint64_t allocs = 0, frees = 0, hits = 0, driver_allocs = 0;
+  uint64_t in_use = 0, reserved = 0, peak_in_use = 0;
+};
+
+struct Block {
+  void* ptr;
+  size_t size;
+  hipEvent_t ev;  // pending: recorded on the freeing stream
+};
+
+class DevicePool {
+ public:
+  explicit DevicePool(int dev) : dev_(dev) {}
+
+  void* alloc(size_t n) {
+    const size_t sz = round_size(n);
+    std::lock_guard<std::mutex> g(mu_);
+    ++st_.allocs;
+    reap_locked();
+    auto it = free_.find(sz);
+    void* p = nullptr;
+    if (it != free_.end() && !it->second.empty()) {
+      p = it->second.back();
+      it->second.pop_back();
+      ++st_.hits;
+    } else {
+      int cur = 0;
+      hip_check(hipGetDevice(&cur), "hipGetDevice");
+      if (cur != dev_) hip_check(hipSetDevice(dev_), "hipSetDevice");
+      hipError_t e = hipMalloc(&p, sz);
+      if (e != hipSuccess) {  // out of memory: drop the cache once and retry
+        release_locked();
+        e = hipMalloc(&p, sz);
+      }
+      if (cur != dev_) hipSetDevice(cur);
+      hip_check(e, "hipMalloc");
+      ++st_.driver_allocs;
+      st_.reserved += sz;
+    }
+    sizes_[p] = sz;
+    st_.in_use += sz;
+    if (st_.in_use > st_.peak_in_use) st_.peak_in_use = st_.in_use;
+    return p;
+  }
+
+  // stream != 0: the block may still be read / written by work queued on that
+  // stream; it is reused only after an event recorded there has completed
+  void free(void* p, uintptr_t stream) {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = sizes_.find(p);
+    if (it == sizes_.end()) throw std::runtime_error("DevicePool::free: pointer not from this pool");
+    const size_t sz = it->second;
+    sizes_.erase(it);
+    ++st_.frees;
+    st_.in_use -= sz;
+    if (stream) {
+      hipEvent_t ev;
+      hip_check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
+      hip_check(hipEventRecord(ev, (hipStream_t)stream), "hipEventRecord");
+      pending_.push_back(Block{p, sz, ev});
+    } else {
+      free_[sz].push_back(p);
+    }
+  }
+
+  void release() {
+    std::lock_guard<std::mutex> g(mu_);
+    release_locked();
+  }
+
+  py::dict stats() {
+    std::lock_guard<std::mutex> g(mu_);
+    reap_locked();
+    py::dict d;
+    d["allocs"] = st_.allocs;
+    d["frees"] = st_.frees;
+    d["cache_hits"] = st_.hits;
+    d["driver_allocs"] = st_.driver_allocs;
+    d["in_use_bytes"] = st_.in_use;
+    d["reserved_bytes"] = st_.reserved;
+    d["peak_in_use_bytes"] = st_.peak_in_use;
+    d["pending_frees"] = (uint64_t)pending_.size();
+    return d;
+  }
+  int device() const { return dev_; }
+
+ private:
+  void reap_locked() {
+    for (size_t i = 0; i < pending_.size();) {
+      if (hipEventQuery(pending_[i].ev) == hipSuccess) {
+        hipEventDestroy(pending_[i].ev);
+        free_[pending_[i].size].push_back(pending_[i].ptr);
+        pending_[i] = pending_.back();
+        pending_.pop_back();
+      } else {
+        ++i;
+      }
+    }
+  }
+  void release_locked() {
+    reap_locked();
+    for (auto& kv : free_)
+      for (void* p : kv.second) {
+        hipFree(p);
+        st_.reserved -= kv.first;
+      }
+    free_.clear();
+  }
+
+  int dev_;
+  std::mutex mu_;
+  std::map<size_t, std::vector<void*>> free_;
+  std::map<void*, size_t> sizes_;
+  std::vector<Block> pending_;
+  Stats st_;
+};
+
+class HostPool {
+ public:
+  explicit HostPool(bool pinned) : pinned_(pinned) {}
+  void* alloc(size_t n) {
+    const size_t sz = round_size(n);
+    std::lock_guard<std::mutex> g(mu_);
+    ++st_.allocs;
+    void* p = nullptr;
+    auto it = free_.find(sz);
+    if (it != free_.end() && !it->second.empty()) {
+      p = it->second.back();
+      it->second.pop_back();
+      ++st_.hits;
+    } else {
+      if (pinned_) {
+        hip_check(hipHostMalloc(&p, sz, hipHostMallocDefault), "hipHostMalloc");
+      } else if (posix_memalign(&p, 64, sz) != 0) {
+        throw std::bad_alloc();
+      }
+      ++st_.driver_allocs;
+      st_.reserved += sz;
+    }
+    sizes_[p] = sz;
+    st_.in_use += sz;
+    if (st_.in_use > st_.peak_in_use) st_.peak_in_use = st_.in_use;
+    return p;
+  }
+  void free(void* p) {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = sizes_.find(p);
+    if (it == sizes_.end()) throw std::runtime_error("HostPool::free: pointer not from this pool");
+    ++st_.frees;
+    st_.in_use -= it->second;
+    free_[it->second].push_back(p);
+    sizes_.erase(it);
+  }
+  void release() {
+    std::lock_guard<std::mutex> g(mu_);
+    for (auto& kv : free_)
+      for (void* p : kv.second) {
+        if (pinned_) hipHostFree(p);
+        else ::free(p);
+        st_.reserved -= kv.first;
+      }
+    free_.clear();
+  }
+  py::dict stats() {
+    std::lock_guard<std::mutex> g(mu_);
+    py::dict d;
+    d["allocs"] = st_.allocs;
+    d["frees"] = st_.frees;
+    d["cache_hits"] = st_.hits;
+    d["driver_allocs"] = st_.driver_allocs;
+    d["in_use_bytes"] = st_.in_use;
+    d["reserved_bytes"] = st_.reserved;
+    d["peak_in_use_bytes"] = st_.peak_in_use;
+    return d;
+  }
+
+ private:
+  bool pinned_;
+  std::mutex mu_;
+  std::map<size_t, std::vector<void*>> free_;
+  std::map<void*, size_t> sizes_;
+  Stats st_;
+};
+
+// pools live for the whole process (freed blocks of tensors that outlive
+// interpreter teardown must still find their pool)
+std::mutex g_mu;
+std::map<int, DevicePool*> g_dev;
+HostPool* g_host[2] = {nullptr, nullptr};
+
+DevicePool& dev_pool(int d) {
+  std::lock_guard<std::mutex> g(g_mu);
+  auto it = g_dev.find(d);
+  if (it == g_dev.end()) it = g_dev.emplace(d, new DevicePool(d)).first;
+  return *it->second;
+}
+HostPool& host_pool(bool pinned) {
+  std::lock_guard<std::mutex> g(g_mu);
+  HostPool*& h = g_host[pinned ? 1 : 0];
+  if (!h) h = new HostPool(pinned);
+  return *h;
+}
+
+struct Ctx {
+  std::vector<int64_t> shape, strides;
+  void* ptr;
+  int kind;  // 0 device, 1 host pageable, 2 host pinned
+  int dev;
+  uintptr_t stream;
+};
+
+void dl_deleter(DLManagedTensor* self) {
+  Ctx* c = (Ctx*)self->manager_ctx;
+  try {
+    if (c->kind == 0) dev_pool(c->dev).free(c->ptr, c->stream);
+    else host_pool(c->kind == 2).free(c->ptr);
+  } catch (...) {
+  }
+  delete c;
+  delete self;
+}
+
+void capsule_dtor(PyObject* cap) {
+  // an unconsumed capsule (never handed to a framework) still owns the block
+  if (PyCapsule_IsValid(cap, "dltensor")) {
+    auto* m = (DLManagedTensor*)PyCapsule_GetPointer(cap, "dltensor");
+    if (m && m->deleter) m->deleter(m);
+  }
+}
+
+// dtype: (code, bits) -- code 0 int, 1 uint, 2 float, 4 bfloat
+py::object make_capsule(std::vector<int64_t> shape, int code, int bits, int kind, int dev, int32_t dl_device_type,
+                        uintptr_t stream) {
+  int64_t n = 1;
+  for (int64_t s : shape) {
+    if (s < 0) throw std::invalid_argument("negative dimension");
+    n *= s;
+  }
+  const size_t bytes = (size_t)n * (bits / 8);
+  void* p = kind == 0 ? dev_pool(dev).alloc(bytes) : host_pool(kind == 2).alloc(bytes);
+  auto* c = new Ctx{shape, std::vector<int64_t>(shape.size()), p, kind, dev, stream};
+  int64_t st = 1;
+  for (int i = (int)shape.size() - 1; i >= 0; --i) {
+    c->strides[i] = st;
+    st *= shape[i];
+  }
+  auto* m = new DLManagedTensor{};
+  m->dl_tensor.data = p;
+  m->dl_tensor.device = DLDevice{kind == 0 ? dl_device_type : kDLCPU, kind == 0 ? dev : 0};
+  m->dl_tensor.ndim = (int32_t)shape.size();
+  m->dl_tensor.dtype = DLDataType{(uint8_t)code, (uint8_t)bits, 1};
+  m->dl_tensor.shape = c->shape.data();
+  m->dl_tensor.strides = c->strides.data();
+  m->dl_tensor.byte_offset = 0;
+  m->manager_ctx = c;
+  m->deleter = dl_deleter;
+  return py::reinterpret_steal<py::object>(PyCapsule_New(m, "dltensor", capsule_dtor));
+}
+
+}  // namespace
+
+void register_mem(py::module& m) {
+  py::module_ mm = m.def_submodule("mem", "native device / host memory pools (DLPack-exported blocks)");
+  mm.def("empty", &make_capsule, py::arg("shape"), py::arg("code"), py::arg("bits"), py::arg("kind"),
+         py::arg("device") = 0, py::arg("dl_device_type") = 10, py::arg("stream") = 0,
+         "allocate a contiguous block from a pool and return a DLPack capsule owning it");
+  mm.def("device_stats", [](int d) { return dev_pool(d).stats(); });
+  mm.def("host_stats", [](bool pinned) { return host_pool(pinned).stats(); }, py::arg("pinned") = false);
+  mm.def("empty_cache", [](int d) { dev_pool(d).release(); });
+  mm.def("empty_host_cache", [](bool pinned) { host_pool(pinned).release(); }, py::arg("pinned") = false);
+  mm.def("dl_device_type", [](py::capsule cap) {
+    auto* t = (DLManagedTensor*)PyCapsule_GetPointer(cap.ptr(), PyCapsule_GetName(cap.ptr()));
+    if (!t) throw std::runtime_error("not a DLPack capsule");
+    return t->dl_tensor.device.device_type;
+  });
+}
