@@ -77,9 +77,9 @@ def build_kernels(force: bool = False, jobs: int = 8) -> Path:
     objs.append(bo)
     if force or _newer(b, bo, []):
         tasks.append([hipcc, "-O2", "-std=c++17", "-fPIC", *_py_includes(), "-c", str(b), "-o", str(bo)])
-    # native RCCL communicator (host code against librccl)
-    for c in sorted((CSRC / "comm").glob("*.cpp")):
-        co = OBJ / ("comm_" + c.stem + ".o")
+    # native RCCL communicator (host code against librccl) and memory pools
+    for c in sorted((CSRC / "comm").glob("*.cpp")) + sorted((CSRC / "mem").glob("*.cpp")):
+        co = OBJ / (c.parent.name + "_" + c.stem + ".o")
         objs.append(co)
         if force or _newer(c, co, []):
             tasks.append([hipcc, "-O2", "-std=c++17", "-fPIC", *_py_includes(), "-c", str(c), "-o", str(co)])

@@ -126,7 +126,13 @@ class DevicePool {
     sizes_.erase(it);
     ++st_.frees;
     st_.in_use -= sz;
-    if (stream) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (stream && hipStreamIsCapturing((hipStream_t)stream, &cs) == hipSuccess &&
+        cs != hipStreamCaptureStatusNone) {
+      // freed while its stream is being captured into a HIP graph: a replay
+      // may still address it, so it is never reused (returned by release())
+      captured_.push_back(Block{p, sz, nullptr});
+    } else if (stream) {
       hipEvent_t ev;
       hip_check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
       hip_check(hipEventRecord(ev, (hipStream_t)stream), "hipEventRecord");
@@ -172,6 +178,11 @@ class DevicePool {
   }
   void release_locked() {
     reap_locked();
+    for (auto& b : captured_) {
+      hipFree(b.ptr);
+      st_.reserved -= b.size;
+    }
+    captured_.clear();
     for (auto& kv : free_)
       for (void* p : kv.second) {
         hipFree(p);
@@ -184,7 +195,7 @@ class DevicePool {
   std::mutex mu_;
   std::map<size_t, std::vector<void*>> free_;
   std::map<void*, size_t> sizes_;
-  std::vector<Block> pending_;
+  std::vector<Block> pending_, captured_;
   Stats st_;
 };
 

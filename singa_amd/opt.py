@@ -28,7 +28,7 @@ from typing import Dict, Iterable, List, Optional, Sequence
 import numpy as np
 import torch
 
-from . import autograd
+from . import autograd, memory
 from .ops import glue as G
 from .ops import native as N
 from .tensor import Tensor
@@ -135,11 +135,13 @@ class ParamStore:
             self.offsets.append(off)
             off += (p.data.numel() + ALIGN - 1) // ALIGN * ALIGN
         self.numel = off
-        self.w = G.zeros((off,), torch.float32, dev)
-        self.g = G.zeros((off,), torch.float32, dev)
-        self.low = G.zeros((off,), torch.bfloat16, dev) if mixed_bf16 else None
-        self.s1 = G.zeros((off,), torch.float32, dev) if state_slots >= 1 else None
-        self.s2 = G.zeros((off,), torch.float32, dev) if state_slots >= 2 else None
+        # the flat buffers live in the framework's own memory pools (HBM caching
+        # pool / aligned host pool, singa_amd/memory.py), not PyTorch's allocator
+        self.w = memory.zeros((off,), torch.float32, dev)
+        self.g = memory.zeros((off,), torch.float32, dev)
+        self.low = memory.zeros((off,), torch.bfloat16, dev) if mixed_bf16 else None
+        self.s1 = memory.zeros((off,), torch.float32, dev) if state_slots >= 1 else None
+        self.s2 = memory.zeros((off,), torch.float32, dev) if state_slots >= 2 else None
         self.mixed = mixed_bf16
         for p, o in zip(self.params, self.offsets):
             n = p.data.numel()
