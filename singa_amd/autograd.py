@@ -806,10 +806,9 @@ class BnReluMaxPool(Operator):
         return y
 
     def backward(self, dy):
-        dpre = F.pool2d_bwd(self.x.shape, self.x, dy, self.arg, self.kernel, self.stride, self.padding, True)
         tg, tb = self.grad_target(1), self.grad_target(2)
-        dx, dg, db, _ = F.batchnorm_bwd(self.x, dpre, self.gamma, self.st, None, need_dres=False, relu=True,
-                                        dg_out=tg, db_out=tb)
+        dx, dg, db = F.bn_relu_maxpool_bwd(self.x, dy, self.arg, self.gamma, self.st, self.kernel, self.stride,
+                                           self.padding, dg_out=tg, db_out=tb)
         self.x = self.st = self.arg = None
         return dx, ACCUMULATED if tg is not None else dg, ACCUMULATED if tb is not None else db
 

@@ -66,6 +66,9 @@ void sg_bn_bwd2(const void*, const void*, const void*, const void*, const void*,
                 int, int, hipStream_t);
 void sg_bn_bwd(const void*, const void*, const void*, const void*, const void*, const void*, const void*, const void*,
                void*, void*, void*, void*, void*, void*, int64_t, int, int, int, hipStream_t);
+void sg_bn_bwd_pool(const void*, const void*, const void*, const void*, const void*, const void*, const void*,
+                    const void*, void*, void*, void*, void*, void*, int, int, int, int, int, int, int, int, int, int,
+                    int, int, hipStream_t);
 void sg_pool_fwd(const void*, void*, void*, int, int, int, int, int, int, int, int, int, int, int, int, int, int, int,
                  hipStream_t);
 void sg_pool_bwd(const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int, int, int,
@@ -255,6 +258,13 @@ PYBIND11_MODULE(_C, m) {
     sg_bn_bwd(CV(x), CV(dy), CV(y), CV(scale), CV(shift), CV(mean), CV(invstd), CV(gamma), V(ws), V(coef), V(dg),
               V(db), V(dx), V(dres), R, C, mask_mode, dt, S(s));
     CHK("bn_bwd");
+  });
+  m.def("bn_bwd_pool", [](P x, P dyp, P arg, P scale, P shift, P mean, P invstd, P gamma, P ws, P coef, P dg, P db,
+                          P dx, int N, int H, int W, int C, int Ho, int Wo, int kh, int kw, int sh, int sw, int ph,
+                          int pw, P s) {
+    sg_bn_bwd_pool(CV(x), CV(dyp), CV(arg), CV(scale), CV(shift), CV(mean), CV(invstd), CV(gamma), V(ws), V(coef),
+                   V(dg), V(db), V(dx), N, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw, S(s));
+    CHK("bn_bwd_pool");
   });
   m.def("set_wt_ready", [](int on) { sg_set_wt_ready(on); });
   m.def("wt_transpose_batched", [](P desc, int n, int total, P s) {

@@ -27,6 +27,8 @@
 // Reference: per-channel bias-gradient reduction K4 (include/mshadow/cuda/
 // tensor_gpu-inl.cuh:135-168) and F2 (src/worker/layer.cc:107); BatchNorm
 // itself is a north-star addition (not in the reference).
+#include <stdexcept>
+
 #include "common.h"
 
 namespace sg {
@@ -58,13 +60,50 @@ __device__ __forceinline__ Tile2D tile2d(int C) {
   return t;
 }
 
+// Gradient of a max-pool's INPUT gathered straight from the pooled gradient
+// dyp [N][Ho][Wo][C] and the 8-bit window argmax (the fused stem BN+ReLU+
+// max-pool: its BN backward reads this instead of a materialised max-pool
+// backward output).  Row r = (n, ih, iw) of the BN input, channels c0..c0+7.
+struct PoolG {
+  const bf16* dy;
+  const uint8_t* arg;
+  int H, W, Ho, Wo, kh, kw, sh, sw, ph, pw;
+  FastDiv dW, dH;
+};
+__device__ __forceinline__ void pool_grad8(const PoolG& q, int64_t r, int C, int c0, float* g) {
+  const unsigned rr = (unsigned)r;
+  const unsigned t = q.dW.div(rr);
+  const int iw = (int)(rr - t * (unsigned)q.W);
+  const unsigned n = q.dH.div(t);
+  const int ih = (int)(t - n * (unsigned)q.H);
+  const int oh0 = max(0, (ih + q.ph - q.kh + q.sh) / q.sh), oh1 = min(q.Ho - 1, (ih + q.ph) / q.sh);
+  const int ow0 = max(0, (iw + q.pw - q.kw + q.sw) / q.sw), ow1 = min(q.Wo - 1, (iw + q.pw) / q.sw);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) g[k] = 0.f;
+  for (int oh = oh0; oh <= oh1; ++oh) {
+    const int a = ih + q.ph - oh * q.sh;
+    if (a < 0 || a >= q.kh) continue;
+    for (int ow = ow0; ow <= ow1; ++ow) {
+      const int b = iw + q.pw - ow * q.sw;
+      if (b < 0 || b >= q.kw) continue;
+      const int64_t o = (((int64_t)n * q.Ho + oh) * q.Wo + ow) * C + c0;
+      const uint2 pk = *(const uint2*)(q.arg + o);
+      const bf16x8 d = *(const bf16x8*)(q.dy + o);
+      const unsigned want = (unsigned)(a * q.kw + b);
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        g[k] += (((k < 4 ? pk.x : pk.y) >> (8 * (k & 3))) & 0xffu) == want ? (float)d[k] : 0.f;
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Stage 1: per-band partial column sums.
 //   MODE 0: p0 = sum x, p1 = sum x^2
 //   MODE 1: g = dy (masked), xh = (x-mean)*invstd: p0 = sum g, p1 = sum g*xh
 // ws layout: [band][2][C] fp32
 // ---------------------------------------------------------------------------
-template <typename T, int MODE, int V>
+template <typename T, int MODE, int V, bool PG = false>
 __global__ void __launch_bounds__(256) colpart_k(const T* __restrict__ x, const T* __restrict__ dy,
                                                  const T* __restrict__ y, const float* __restrict__ scale,
                                                  const float* __restrict__ shift, const float* __restrict__ mean,
@@ -73,7 +112,7 @@ __global__ void __launch_bounds__(256) colpart_k(const T* __restrict__ x, const 
                                                  const T* __restrict__ x2 = nullptr,
                                                  const float* __restrict__ mean2 = nullptr,
                                                  const float* __restrict__ invstd2 = nullptr,
-                                                 float* __restrict__ ws2 = nullptr) {
+                                                 float* __restrict__ ws2 = nullptr, const PoolG pg = PoolG{}) {
   // MODE 2 = MODE 1 plus a second BN fed the same gradient (the downsample
   // branch of a residual block): also p2 = sum g*xh2, into ws2 [band][2][C]
   // as (p0, p2) -- its own instantiation, the plain reduction is untouched
@@ -113,8 +152,13 @@ __global__ void __launch_bounds__(256) colpart_k(const T* __restrict__ x, const 
         }
       } else {
         float g0[V], g1[V];
-        ldv_nt<T, V>(dy + r * C + t.c0, g0);
-        ldv_nt<T, V>(dy + (r + t.RT) * C + t.c0, g1);
+        if constexpr (PG) {
+          pool_grad8(pg, r, C, t.c0, g0);
+          pool_grad8(pg, r + t.RT, C, t.c0, g1);
+        } else {
+          ldv_nt<T, V>(dy + r * C + t.c0, g0);
+          ldv_nt<T, V>(dy + (r + t.RT) * C + t.c0, g1);
+        }
         if (mask_mode == MASK_Y) {
           float y0[V], y1[V];
           ldv_nt<T, V>(y + r * C + t.c0, y0);
@@ -161,7 +205,8 @@ __global__ void __launch_bounds__(256) colpart_k(const T* __restrict__ x, const 
         for (int i = 0; i < V; ++i) { a0[i] += v0[i]; a1[i] += v0[i] * v0[i]; }
       } else {
         float g0[V];
-        ldv_nt<T, V>(dy + r * C + t.c0, g0);
+        if constexpr (PG) pool_grad8(pg, r, C, t.c0, g0);
+        else ldv_nt<T, V>(dy + r * C + t.c0, g0);
         if (mask_mode == MASK_Y) {
           float y0[V];
           ldv_nt<T, V>(y + r * C + t.c0, y0);
@@ -416,11 +461,13 @@ __global__ void __launch_bounds__(256) bn_apply_k(const T* __restrict__ x, const
 
 // g = mask(dy); dx = k*g + b*x + a; dres = g (residual branch).  UR rows
 // are loaded before any is stored (see bn_apply_k).
-template <typename T, int V>
+template <typename T, int V, bool PG = false>
 __device__ __forceinline__ void bn_bwd_load(const T* x, const T* dy, const T* y, int64_t o, int mask_mode, float* v,
-                                            float* g, float* yy, unsigned& mb) {
+                                            float* g, float* yy, unsigned& mb, const PoolG* pg = nullptr,
+                                            int64_t row = 0, int C = 0, int c0 = 0) {
   ldv_nt<T, V>(x + o, v);
-  ldv_nt<T, V>(dy + o, g);
+  if constexpr (PG) pool_grad8(*pg, row, C, c0, g);
+  else ldv_nt<T, V>(dy + o, g);
   if (mask_mode == MASK_Y) ldv_nt<T, V>(y + o, yy);
   else if (V == 8 && mask_mode == MASK_BITS) mb = ((const uint8_t*)y)[o >> 3];
 }
@@ -455,7 +502,7 @@ __device__ __forceinline__ void bn_bwd_row(const float* v, float* g, const float
   }
 }
 
-template <typename T, int V, int UR, bool DUAL = false>
+template <typename T, int V, int UR, bool DUAL = false, bool PG = false>
 __global__ void __launch_bounds__(256) bn_bwd_apply_k(const T* __restrict__ x, const T* __restrict__ dy,
                                                       const T* __restrict__ y, const float* __restrict__ scale,
                                                       const float* __restrict__ shift,
@@ -463,7 +510,7 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_k(const T* __restrict__ x, c
                                                       T* __restrict__ dres, int64_t R, int C, int mask_mode,
                                                       int64_t rpw, const T* __restrict__ x2 = nullptr,
                                                       const float* __restrict__ coef2 = nullptr,
-                                                      T* __restrict__ dx2 = nullptr) {
+                                                      T* __restrict__ dx2 = nullptr, const PoolG pg = PoolG{}) {
   const Tile2D t = tile2d<V>(C);
   if (!t.cok) return;
   float kk[V], bb[V], aa[V], sc[V], sf[V], k2[V], b2[V], a2[V];
@@ -486,7 +533,9 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_k(const T* __restrict__ x, c
     float v[UR][V], g[UR][V], yy[UR][V];
     unsigned mb[UR] = {};
 #pragma unroll
-    for (int u = 0; u < UR; ++u) bn_bwd_load<T, V>(x, dy, y, (r + u * step) * C + t.c0, mask_mode, v[u], g[u], yy[u], mb[u]);
+    for (int u = 0; u < UR; ++u)
+      bn_bwd_load<T, V, PG>(x, dy, y, (r + u * step) * C + t.c0, mask_mode, v[u], g[u], yy[u], mb[u], &pg,
+                            r + u * step, C, t.c0);
 #pragma unroll
     for (int u = 0; u < UR; ++u)
       bn_bwd_row<T, V, DUAL>(v[u], g[u], yy[u], mb[u], kk, bb, aa, sc, sf, dx, dres, (r + u * step) * C + t.c0,
@@ -496,7 +545,7 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_k(const T* __restrict__ x, c
     float v[V], g[V], yy[V];
     unsigned mb = 0;
     const int64_t o = r * C + t.c0;
-    bn_bwd_load<T, V>(x, dy, y, o, mask_mode, v, g, yy, mb);
+    bn_bwd_load<T, V, PG>(x, dy, y, o, mask_mode, v, g, yy, mb, &pg, r, C, t.c0);
     bn_bwd_row<T, V, DUAL>(v, g, yy, mb, kk, bb, aa, sc, sf, dx, dres, o, mask_mode, x2, k2, b2, a2, dx2);
   }
 }
@@ -757,6 +806,35 @@ void sg_bn_bwd(const void* x, const void* dy, const void* y, const void* scale, 
                                                       (const T*)dy, (const T*)y, (const float*)scale,
                                                       (const float*)shift, (const float*)coef, (T*)dx, (T*)dres, R,
                                                       C, mask_mode, rpw)));
+}
+
+// BN(+ReLU) backward of the fused stem BN+ReLU+max-pool: the gradient at
+// the BN output is gathered from the pooled gradient dyp and the window
+// argmax inside the reduction and apply passes -- the full-resolution
+// max-pool backward output is never written (bf16, C % 8 == 0, ReLU mask
+// recomputed from x).
+void sg_bn_bwd_pool(const void* x, const void* dyp, const void* arg, const void* scale, const void* shift,
+                    const void* mean, const void* invstd, const void* gamma, void* ws, void* coef, void* dg, void* db,
+                    void* dx, int N, int H, int W, int C, int Ho, int Wo, int kh, int kw, int sh, int sw, int ph,
+                    int pw, hipStream_t s) {
+  const int64_t R = (int64_t)N * H * W;
+  PoolG pg{(const bf16*)dyp, (const uint8_t*)arg, H, W, Ho, Wo, kh, kw, sh, sw, ph, pw, FastDiv(W), FastDiv(H)};
+  dim3 grid;
+  int rpb, V;
+  colgrid(R, C, grid, rpb, V);
+  if (V != 8) throw std::runtime_error("sg_bn_bwd_pool: needs C % 8 == 0");
+  zero_ws(ws, C, s);
+  hipLaunchKernelGGL((colpart_k<bf16, 1, 8, true>), grid, dim3(256), 0, s, (const bf16*)x, nullptr, nullptr,
+                     (const float*)scale, (const float*)shift, (const float*)mean, (const float*)invstd, (float*)ws,
+                     R, C, rpb, (int)MASK_AFFINE, g_bn_det, nullptr, nullptr, nullptr, nullptr, pg);
+  hipLaunchKernelGGL(bn_bwd_finalize_k, fin_grid(C), dim3(256), 0, s, (const float*)ws, fin_rows(grid), C,
+                     (const float*)gamma, (const float*)mean, (const float*)invstd, (float*)coef, (float*)dg,
+                     (float*)db, (float)R);
+  int64_t rpw;
+  dim3 ag = apply_grid(R, C, 8, rpw);
+  hipLaunchKernelGGL((bn_bwd_apply_k<bf16, 8, 2, false, true>), ag, dim3(256), 0, s, (const bf16*)x, nullptr,
+                     nullptr, (const float*)scale, (const float*)shift, (const float*)coef, (bf16*)dx, nullptr, R, C,
+                     (int)MASK_AFFINE, rpw, nullptr, nullptr, nullptr, pg);
 }
 
 // Backward of y = relu(BN1(x) + BN2(x2)) (mask bits from the forward): one

@@ -1278,6 +1278,41 @@ def bn_relu_maxpool_fwd(x: torch.Tensor, gamma, beta, run_mean, run_var, trainin
     return y, arg, BNState(mean, invstd, scale, shift, None)
 
 
+def _fuse_pool_bwd() -> bool:
+    # opt-in: measured 12.98k vs 13.09k img/s (ResNet-50 b1024, A/B/A in one
+    # session) -- the per-row argmax gather in BOTH BN passes costs more VALU
+    # than the 1.6 GB write + two reads of the max-pool backward output save
+    return os.environ.get("SINGA_AMD_FUSE_POOL_BWD", "0") == "1"
+
+
+def bn_relu_maxpool_bwd(x: torch.Tensor, dy: torch.Tensor, arg: torch.Tensor, gamma: torch.Tensor, st: "BNState",
+                        kernel, stride, padding, dg_out=None, db_out=None):
+    """Backward of :func:`bn_relu_maxpool_fwd`: (dx, dgamma, dbeta).  Native:
+    the BN backward gathers its input gradient from the pooled gradient and
+    the 8-bit argmax inside its reduction and apply passes (the full-size
+    max-pool backward output is never written).  dgamma / dbeta accumulate
+    into dg_out / db_out when given."""
+    Nn, C, H, W = x.shape
+    Ho, Wo = dy.shape[2], dy.shape[3]
+    if (_fuse_pool_bwd() and _bn_native(x) and x.dtype == torch.bfloat16 and N.is_cl(x) and C % 8 == 0
+            and dy.dtype == torch.bfloat16 and arg is not None and arg.dtype == torch.uint8):
+        dyc = G.contiguous(dy, torch.channels_last)
+        R = x.numel() // C
+        dg = dg_out if dg_out is not None else G.zeros((C,), torch.float32, x.device)
+        db = db_out if db_out is not None else G.zeros((C,), torch.float32, x.device)
+        coef = torch.empty(3 * C, dtype=torch.float32, device=x.device)
+        dx = _like(x)
+        N.lib().bn_bwd_pool(x.data_ptr(), dyc.data_ptr(), arg.data_ptr(), st.scale.data_ptr(), st.shift.data_ptr(),
+                            st.mean.data_ptr(), st.invstd.data_ptr(), gamma.data_ptr(), _ws(R, C, x.device).data_ptr(),
+                            coef.data_ptr(), dg.data_ptr(), db.data_ptr(), dx.data_ptr(), Nn, H, W, C, Ho, Wo,
+                            kernel[0], kernel[1], stride[0], stride[1], padding[0], padding[1], N.stream())
+        dx._sg_fresh = True
+        return dx, dg, db
+    dpre = pool2d_bwd(x.shape, x, dy, arg, kernel, stride, padding, True)
+    dx, dg, db, _ = batchnorm_bwd(x, dpre, gamma, st, None, need_dres=False, relu=True, dg_out=dg_out, db_out=db_out)
+    return dx, dg, db
+
+
 def batchnorm_fwd(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, run_mean: torch.Tensor,
                   run_var: torch.Tensor, training: bool, momentum: float = 0.1, eps: float = 1e-5,
                   relu: bool = False, residual: Optional[torch.Tensor] = None, want_mask: bool = False):
