@@ -148,6 +148,56 @@ __global__ void maxpool_bwd_k(const T* __restrict__ dy, const uint8_t* __restric
   }
 }
 
+// 3x3 / stride 2 / pad 1 max-pool backward (the ResNet stem), bf16 NHWC,
+// 8 channels per thread over a flat (n, ih, iw, c/8) index: the covering
+// windows in closed form -- input row ih is covered by output row (ih+1)/2
+// (tap (ih+1)&1) and, for odd ih, also by (ih+1)/2-1 (tap 2) -- with
+// constant-divisor index splits, no window loops, non-temporal stores.
+__global__ void __launch_bounds__(256) maxpool_bwd_332_k(const bf16* __restrict__ dy, const uint8_t* __restrict__ arg,
+                                                       bf16* __restrict__ dx, int H, int W, int C, int Ho, int Wo,
+                                                       uint32_t total, FastDiv dCV, FastDiv dW, FastDiv dH) {
+  const int CV = C >> 3;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const uint32_t p = dCV.div(i);
+    const int cv = (int)(i - p * (uint32_t)CV);
+    const uint32_t q = dW.div(p);
+    const int iw = (int)(p - q * (uint32_t)W);
+    const uint32_t n = dH.div(q);
+    const int ih = (int)(q - n * (uint32_t)H);
+    int ohs[2], rs[2], ows[2], ss[2];
+    int nh = 0, nw = 0;
+    {
+      const int o = (ih + 1) >> 1, r = (ih + 1) & 1;
+      if (o < Ho) { ohs[nh] = o; rs[nh] = r; ++nh; }
+      if (r == 0 && o >= 1) { ohs[nh] = o - 1; rs[nh] = 2; ++nh; }
+    }
+    {
+      const int o = (iw + 1) >> 1, t = (iw + 1) & 1;
+      if (o < Wo) { ows[nw] = o; ss[nw] = t; ++nw; }
+      if (t == 0 && o >= 1) { ows[nw] = o - 1; ss[nw] = 2; ++nw; }
+    }
+    float acc[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      if (a >= nh) break;
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        if (b >= nw) break;
+        const int64_t o = (((int64_t)n * Ho + ohs[a]) * Wo + ows[b]) * C + cv * 8;
+        const uint2 pk = *(const uint2*)(arg + o);
+        const bf16x8 d = *(const bf16x8*)(dy + o);
+        const unsigned want = (unsigned)(rs[a] * 3 + ss[b]);
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          acc[k] += (((k < 4 ? pk.x : pk.y) >> (8 * (k & 3))) & 0xffu) == want ? (float)d[k] : 0.f;
+      }
+    }
+    stv_nt<bf16, 8>(dx + (int64_t)i * 8, acc);
+  }
+}
+
 template <typename T, int V>
 __global__ void avgpool_fwd_k(const T* __restrict__ x, T* __restrict__ y, PoolGeom g, int count_pad) {
   const int CV = g.C / V;
@@ -450,7 +500,12 @@ void sg_pool_bwd(const void* dy, const void* arg, void* dx, int N, int H, int W,
   PoolGeom g{N, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw};
   const int V = (C % 8 == 0) ? 8 : 1;
   const int64_t total = (int64_t)N * H * W * (C / V);
-  if (is_max) {
+  if (is_max && dtype == 1 && V == 8 && kh == 3 && kw == 3 && sh == 2 && sw == 2 && ph == 1 && pw == 1 &&
+      total < (int64_t)UINT32_MAX && Ho == (H + 1) / 2 && Wo == (W + 1) / 2) {
+    hipLaunchKernelGGL(maxpool_bwd_332_k, dim3(sg_grid(total, 256, 16384)), dim3(256), 0, s, (const bf16*)dy,
+                       (const uint8_t*)arg, (bf16*)dx, H, W, C, Ho, Wo, (uint32_t)total, FastDiv(C / 8), FastDiv(W),
+                       FastDiv(H));
+  } else if (is_max) {
     const int ych = (int)(((int64_t)W * (C / V) + 255) / 256);
     DISPATCH_FT(dtype, DISPATCH_V(V, hipLaunchKernelGGL((maxpool_bwd_k<T, VV>), dim3(N * H, ych),
                                                         dim3(256), 0, s, (const T*)dy, (const uint8_t*)arg, (T*)dx,

@@ -330,6 +330,28 @@ def test_batchnorm_bf16(gpu):
 
 
 # ------------------------------------------------------------------ pooling
+@pytest.mark.parametrize("H,W", [(13, 11), (16, 16), (8, 9)])
+def test_maxpool_bwd_bf16_stem_shape(gpu, H, W):
+    """bf16 3x3/s2/p1 max-pool (the ResNet stem's; closed-form backward
+    kernel) vs PyTorch fp32 on the same values: a permutation of distinct
+    integers per plane (exact in bf16, so no ties)."""
+    from singa_amd.ops import functional as F
+    g = torch.Generator().manual_seed(3)
+    N_, C = 2, 16
+    x = torch.stack([torch.randperm(H * W, generator=g).float().reshape(H, W) for _ in range(N_ * C)])
+    x = x.reshape(N_, C, H, W)
+    xr = x.clone().requires_grad_(True)
+    yr = TF.max_pool2d(xr, 3, 2, 1)
+    dy = torch.randn(yr.shape, generator=g).bfloat16().float()
+    yr.backward(dy)
+    xg = x.to(gpu).bfloat16().contiguous(memory_format=torch.channels_last)
+    y, arg = F.pool2d_fwd(xg, (3, 3), (2, 2), (1, 1), True)
+    assert torch.equal(y.float().cpu(), yr.detach())
+    dx = F.pool2d_bwd(xg.shape, xg, dy.to(gpu).bfloat16().contiguous(memory_format=torch.channels_last), arg,
+                      (3, 3), (2, 2), (1, 1), True)
+    assert rel_err(dx, xr.grad) < 5e-3
+
+
 @pytest.mark.parametrize("is_max", [True, False])
 @pytest.mark.parametrize("k,s,p", [(3, 2, 1), (2, 2, 0), (3, 1, 1)])
 def test_pool(gpu, is_max, k, s, p):
