@@ -459,6 +459,9 @@ def test_stem_pool_bn_backward_gather_matches_materialised(gpu, monkeypatch):
     same bf16 tensors); and it really ran without the separate pool kernel."""
     from singa_amd.ops import functional as F
     g = torch.Generator(device=gpu).manual_seed(4)
+    orig = F.pool2d_bwd
+    calls = []
+    monkeypatch.setattr(F, "pool2d_bwd", lambda *a, **k: calls.append(1) or orig(*a, **k))
     for (N_, C, H) in ((2, 64, 32), (3, 16, 17)):
         x = torch.randn(N_, C, H, H, device=gpu, generator=g).bfloat16().contiguous(memory_format=torch.channels_last)
         gamma = torch.rand(C, device=gpu, generator=g) + 0.5
@@ -466,9 +469,7 @@ def test_stem_pool_bn_backward_gather_matches_materialised(gpu, monkeypatch):
         rm, rv = torch.zeros(C, device=gpu), torch.ones(C, device=gpu)
         y, arg, st = F.bn_relu_maxpool_fwd(x, gamma, beta, rm, rv, True, 0.1, 1e-5, (3, 3), (2, 2), (1, 1))
         dy = torch.randn(y.shape, device=gpu, generator=g).bfloat16().contiguous(memory_format=torch.channels_last)
-        calls = []
-        orig = F.pool2d_bwd
-        monkeypatch.setattr(F, "pool2d_bwd", lambda *a, **k: calls.append(1) or orig(*a, **k))
+        calls.clear()
         monkeypatch.setenv("SINGA_AMD_FUSE_POOL_BWD", "1")
         dx, dg, db = F.bn_relu_maxpool_bwd(x, dy, arg, gamma, st, (3, 3), (2, 2), (1, 1))
         assert not calls
