@@ -24,7 +24,9 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <cstring>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -288,16 +290,17 @@ HostPool& host_pool(bool pinned) {
 struct Ctx {
   std::vector<int64_t> shape, strides;
   void* ptr;
-  int kind;  // 0 device, 1 host pageable, 2 host pinned
+  int kind;  // 0 device, 1 host pageable, 2 host pinned, 3 view (owned by `keep`)
   int dev;
   uintptr_t stream;
+  std::shared_ptr<void> keep;
 };
 
 void dl_deleter(DLManagedTensor* self) {
   Ctx* c = (Ctx*)self->manager_ctx;
   try {
     if (c->kind == 0) dev_pool(c->dev).free(c->ptr, c->stream);
-    else host_pool(c->kind == 2).free(c->ptr);
+    else if (c->kind == 1 || c->kind == 2) host_pool(c->kind == 2).free(c->ptr);
   } catch (...) {
   }
   delete c;
@@ -322,7 +325,7 @@ py::object make_capsule(std::vector<int64_t> shape, int code, int bits, int kind
   }
   const size_t bytes = (size_t)n * (bits / 8);
   void* p = kind == 0 ? dev_pool(dev).alloc(bytes) : host_pool(kind == 2).alloc(bytes);
-  auto* c = new Ctx{shape, std::vector<int64_t>(shape.size()), p, kind, dev, stream};
+  auto* c = new Ctx{shape, std::vector<int64_t>(shape.size()), p, kind, dev, stream, nullptr};
   int64_t st = 1;
   for (int i = (int)shape.size() - 1; i >= 0; --i) {
     c->strides[i] = st;
@@ -341,6 +344,109 @@ py::object make_capsule(std::vector<int64_t> shape, int code, int bits, int kind
   return py::reinterpret_steal<py::object>(PyCapsule_New(m, "dltensor", capsule_dtor));
 }
 
+// --------------------------------------------------------------- SyncedBlob
+// The reference's SyncedMemory (src/utils/blob.cc:83-143): one logical buffer
+// with a host and a device copy allocated lazily from the pools and a head
+// state saying which copy is current.  Reading a side syncs it from the other
+// if needed (stream-ordered copies; the host read waits for its copy);
+// taking a side for writing makes it the only valid one.  The device side
+// may instead be an EXTERNAL region (e.g. a parameter's slice of the flat
+// parameter store), which the blob mirrors but never frees.
+class SyncedBlob : public std::enable_shared_from_this<SyncedBlob> {
+ public:
+  enum Head { UNINIT = 0, AT_CPU = 1, AT_GPU = 2, SYNCED = 3 };
+  SyncedBlob(size_t bytes, int dev, uintptr_t ext, bool pinned)
+      : bytes_(bytes), dev_(dev), d_((void*)ext), ext_(ext != 0), pinned_(pinned) {
+    if (ext_) head_ = AT_GPU;  // the external region holds the data
+  }
+  ~SyncedBlob() {
+    if (h_) host_pool(pinned_).free(h_);
+    if (d_ && !ext_) dev_pool(dev_).free(d_, 0);
+  }
+  uintptr_t cpu_ptr(uintptr_t stream) {
+    to_cpu(stream);
+    return (uintptr_t)h_;
+  }
+  uintptr_t gpu_ptr(uintptr_t stream) {
+    to_gpu(stream);
+    return (uintptr_t)d_;
+  }
+  uintptr_t mutable_cpu_ptr(uintptr_t stream) {
+    to_cpu(stream);
+    head_ = AT_CPU;
+    return (uintptr_t)h_;
+  }
+  uintptr_t mutable_gpu_ptr(uintptr_t stream) {
+    to_gpu(stream);
+    head_ = AT_GPU;
+    return (uintptr_t)d_;
+  }
+  int head() const { return head_; }
+  size_t bytes() const { return bytes_; }
+
+ private:
+  void alloc_h() {
+    if (!h_) h_ = host_pool(pinned_).alloc(bytes_);
+  }
+  void alloc_d() {
+    if (!d_) d_ = dev_pool(dev_).alloc(bytes_);
+  }
+  void to_cpu(uintptr_t stream) {
+    if (head_ == UNINIT) {
+      alloc_h();
+      memset(h_, 0, bytes_);
+      head_ = AT_CPU;
+    } else if (head_ == AT_GPU) {
+      alloc_h();
+      hip_check(hipMemcpyAsync(h_, d_, bytes_, hipMemcpyDeviceToHost, (hipStream_t)stream), "hipMemcpyAsync D2H");
+      hip_check(hipStreamSynchronize((hipStream_t)stream), "hipStreamSynchronize");
+      head_ = SYNCED;
+    }
+  }
+  void to_gpu(uintptr_t stream) {
+    if (head_ == UNINIT) {
+      alloc_d();
+      hip_check(hipMemsetAsync(d_, 0, bytes_, (hipStream_t)stream), "hipMemsetAsync");
+      head_ = AT_GPU;
+    } else if (head_ == AT_CPU) {
+      alloc_d();
+      hip_check(hipMemcpyAsync(d_, h_, bytes_, hipMemcpyHostToDevice, (hipStream_t)stream), "hipMemcpyAsync H2D");
+      head_ = SYNCED;
+    }
+  }
+  size_t bytes_;
+  int dev_;
+  void* h_ = nullptr;
+  void* d_ = nullptr;
+  bool ext_, pinned_;
+  int head_ = UNINIT;
+};
+
+// DLPack view of a blob side (the capsule keeps the blob alive)
+py::object blob_view(std::shared_ptr<SyncedBlob> b, uintptr_t ptr, bool on_device, int dev, int32_t dl_type,
+                     std::vector<int64_t> shape, int code, int bits) {
+  auto* c = new Ctx{shape, std::vector<int64_t>(shape.size()), (void*)ptr, 3, dev, 0, b};
+  int64_t st = 1;
+  for (int i = (int)shape.size() - 1; i >= 0; --i) {
+    c->strides[i] = st;
+    st *= shape[i];
+  }
+  if ((size_t)st * (bits / 8) > b->bytes()) {
+    delete c;
+    throw std::invalid_argument("blob view larger than the blob");
+  }
+  auto* m = new DLManagedTensor{};
+  m->dl_tensor.data = (void*)ptr;
+  m->dl_tensor.device = DLDevice{on_device ? dl_type : kDLCPU, on_device ? dev : 0};
+  m->dl_tensor.ndim = (int32_t)shape.size();
+  m->dl_tensor.dtype = DLDataType{(uint8_t)code, (uint8_t)bits, 1};
+  m->dl_tensor.shape = c->shape.data();
+  m->dl_tensor.strides = c->strides.data();
+  m->manager_ctx = c;
+  m->deleter = dl_deleter;
+  return py::reinterpret_steal<py::object>(PyCapsule_New(m, "dltensor", capsule_dtor));
+}
+
 }  // namespace
 
 void register_mem(py::module& m) {
@@ -352,6 +458,18 @@ void register_mem(py::module& m) {
   mm.def("host_stats", [](bool pinned) { return host_pool(pinned).stats(); }, py::arg("pinned") = false);
   mm.def("empty_cache", [](int d) { dev_pool(d).release(); });
   mm.def("empty_host_cache", [](bool pinned) { host_pool(pinned).release(); }, py::arg("pinned") = false);
+  py::class_<SyncedBlob, std::shared_ptr<SyncedBlob>>(mm, "SyncedBlob")
+      .def(py::init<size_t, int, uintptr_t, bool>(), py::arg("bytes"), py::arg("device") = 0, py::arg("ext") = 0,
+           py::arg("pinned") = true)
+      .def("cpu_ptr", &SyncedBlob::cpu_ptr, py::arg("stream") = 0, py::call_guard<py::gil_scoped_release>())
+      .def("gpu_ptr", &SyncedBlob::gpu_ptr, py::arg("stream") = 0)
+      .def("mutable_cpu_ptr", &SyncedBlob::mutable_cpu_ptr, py::arg("stream") = 0,
+           py::call_guard<py::gil_scoped_release>())
+      .def("mutable_gpu_ptr", &SyncedBlob::mutable_gpu_ptr, py::arg("stream") = 0)
+      .def_property_readonly("head", &SyncedBlob::head)
+      .def_property_readonly("bytes", &SyncedBlob::bytes);
+  mm.def("blob_view", &blob_view, py::arg("blob"), py::arg("ptr"), py::arg("on_device"), py::arg("device"),
+         py::arg("dl_device_type"), py::arg("shape"), py::arg("code"), py::arg("bits"));
   mm.def("dl_device_type", [](py::capsule cap) {
     auto* t = (DLManagedTensor*)PyCapsule_GetPointer(cap.ptr(), PyCapsule_GetName(cap.ptr()));
     if (!t) throw std::runtime_error("not a DLPack capsule");

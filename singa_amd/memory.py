@@ -94,3 +94,68 @@ def empty_cache(device=None) -> None:
     else:
         M.empty_host_cache(False)
         M.empty_host_cache(True)
+
+
+class SyncedBlob:
+    """Host/device buffer pair with a head state (the reference's
+    SyncedMemory, src/utils/blob.cc:83-143): each side is allocated lazily
+    from the native pools; reading a side syncs it from the other when the
+    other holds newer data; taking a side ``mutable_*`` makes it the only
+    valid copy.  ``like=`` mirrors an existing device region (e.g. a
+    parameter's slice of the flat store) instead of allocating one.
+
+    Head states: 0 UNINITIALIZED, 1 HEAD_AT_CPU, 2 HEAD_AT_GPU, 3 SYNCED."""
+
+    UNINITIALIZED, HEAD_AT_CPU, HEAD_AT_GPU, SYNCED = 0, 1, 2, 3
+
+    def __init__(self, shape: Sequence[int], dtype=torch.float32, device=None, like: torch.Tensor = None,
+                 pinned: bool = True):
+        M = _mod()
+        if M is None:
+            raise RuntimeError("SyncedBlob needs the native library (_C)")
+        self.shape = [int(s) for s in (like.shape if like is not None else shape)]
+        self.dtype = like.dtype if like is not None else dtype
+        code, bits = _CODES[self.dtype]
+        self._cb = (code, bits)
+        n = 1
+        for s in self.shape:
+            n *= s
+        nbytes = n * bits // 8
+        if like is not None:
+            if not (like.is_cuda and like.is_contiguous()):
+                raise ValueError("SyncedBlob(like=...) mirrors a dense device tensor")
+            self.dev = like.device.index
+            ext = like.data_ptr()
+            self._keep = like
+        else:
+            d = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+            self.dev = d.index if d.index is not None else 0
+            ext = 0
+            self._keep = None
+        self._b = M.SyncedBlob(max(nbytes, 1), self.dev, ext, pinned)
+        self._M = M
+
+    @property
+    def head(self) -> int:
+        return self._b.head
+
+    def _stream(self) -> int:
+        return torch.cuda.current_stream(self.dev).cuda_stream
+
+    def _view(self, ptr: int, on_device: bool) -> torch.Tensor:
+        code, bits = self._cb
+        cap = self._M.blob_view(self._b, ptr, on_device, self.dev, _dl_device_type() if on_device else 1,
+                                self.shape, code, bits)
+        return torch.utils.dlpack.from_dlpack(cap)
+
+    def cpu_data(self) -> torch.Tensor:
+        return self._view(self._b.cpu_ptr(self._stream()), False)
+
+    def gpu_data(self) -> torch.Tensor:
+        return self._view(self._b.gpu_ptr(self._stream()), True)
+
+    def mutable_cpu_data(self) -> torch.Tensor:
+        return self._view(self._b.mutable_cpu_ptr(self._stream()), False)
+
+    def mutable_gpu_data(self) -> torch.Tensor:
+        return self._view(self._b.mutable_gpu_ptr(self._stream()), True)

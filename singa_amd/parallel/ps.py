@@ -146,7 +146,10 @@ class PSSync:
     """Worker-side EASGD / RandomSync through native servers (same interface
     as :class:`.easgd.ElasticSync` / :class:`.easgd.RandomSync`).  Parameter
     ``i`` of the flat store is key ``i`` (sharded over servers by
-    ``i % nservers``).  Device parameters are staged through host memory."""
+    ``i % nservers``).  Device parameters are mirrored in host memory by a
+    native :class:`singa_amd.memory.SyncedBlob` per parameter (the reference
+    Param's data blob, src/utils/blob.cc:83-143): a pinned host side synced
+    from the store slice before the exchange, written back after it."""
 
     def __init__(self, store, client: PSClient, group_id: int, ngroups: int, mode: str = "Elastic",
                  moving_rate: float = 0.9, sync_frequency: int = 1, warmup_steps: int = 0, sample_ratio: float = 1.0,
@@ -163,21 +166,35 @@ class PSSync:
         self.nsync = 0
         self._host: List[np.ndarray] = []
         self._snap: List[np.ndarray] = []
-        for p in store.params:
-            self._host.append(np.empty(p.data.numel(), dtype=np.float32))
+        self._blobs = []
+        for i, p in enumerate(store.params):
+            o, n = store.param_range(i)
+            if store.w.is_cuda:
+                from ..memory import SyncedBlob
+                self._blobs.append(SyncedBlob(None, like=store.w[o:o + n]))
+                self._host.append(None)
+            else:  # CppCPU: the store slice itself is the host buffer
+                self._blobs.append(None)
+                self._host.append(store.w[o:o + n].numpy())
 
     def sync_now(self, step: int) -> bool:
         return step >= self.warmup_steps and (step - self.warmup_steps) % self.sync_frequency == 0
 
     def _pull_to_host(self, i: int) -> np.ndarray:
-        o, n = self.store.param_range(i)
-        h = self._host[i]
-        h[:] = self.store.w[o:o + n].detach().cpu().numpy()
-        return h
+        """Host view of parameter i, current with the store (D2H if needed)
+        and writable: the exchange updates it in place."""
+        b = self._blobs[i]
+        if b is None:
+            return self._host[i]
+        b.cpu_data()  # device -> pinned host when the store holds newer data
+        self._host[i] = b.mutable_cpu_data().numpy()
+        return self._host[i]
 
     def _push_from_host(self, i: int) -> None:
-        o, n = self.store.param_range(i)
-        G.copy_(self.store.w[o:o + n], torch.from_numpy(self._host[i]))
+        b = self._blobs[i]
+        if b is not None:
+            b.gpu_data()  # host -> the store slice (stream-ordered)
+            b.mutable_gpu_data()  # the device copy is authoritative again (training writes it)
 
     def bootstrap(self) -> None:
         """Group 0 Puts every parameter, the other groups Get them (blocking
@@ -186,10 +203,11 @@ class PSSync:
             if self.group_id == 0:
                 self.client.put(self.key_base + i, self._pull_to_host(i))
             else:
-                got = self.client.get(self.key_base + i, self._host[i])
-                if got != self._host[i].size:
+                h = self._pull_to_host(i)
+                got = self.client.get(self.key_base + i, h)
+                if got != h.size:
                     raise RuntimeError(f"PSSync.bootstrap: key {self.key_base + i} holds {got} floats, "
-                                       f"parameter {i} has {self._host[i].size}")
+                                       f"parameter {i} has {h.size}")
                 self._push_from_host(i)
         self._snap = [h.copy() for h in self._host]
         self.store.sync_low()

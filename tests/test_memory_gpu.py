@@ -106,3 +106,73 @@ def test_graph_step_with_param_store_in_native_pool(gpu):
     ref = _step(False)
     for k in ref:
         assert torch.equal(nat[k], ref[k]), k
+
+
+def test_synced_blob_head_states(gpu):
+    """The reference SyncedMemory state machine on native buffers: lazy
+    sides, sync on read, mutable_* makes one side authoritative, and a
+    mirror of an external device region (a parameter's store slice)."""
+    from singa_amd.memory import SyncedBlob as B
+    b = B((4, 5), torch.float32, gpu)
+    assert b.head == B.UNINITIALIZED
+    h = b.mutable_cpu_data()
+    assert b.head == B.HEAD_AT_CPU and float(h.abs().sum()) == 0.0
+    h.copy_(torch.arange(20, dtype=torch.float32).reshape(4, 5))
+    d = b.gpu_data()
+    assert b.head == B.SYNCED and d.is_cuda
+    torch.testing.assert_close(d.cpu(), h)
+    d2 = b.mutable_gpu_data()
+    d2.mul_(2.0)
+    assert b.head == B.HEAD_AT_GPU
+    torch.testing.assert_close(b.cpu_data(), h * 0 + torch.arange(20.).reshape(4, 5) * 2)
+    assert b.head == B.SYNCED
+    # mirror of an existing device slice: host edits land in the slice
+    flat = torch.arange(30, dtype=torch.float32, device=gpu)
+    m = B(None, like=flat[10:20])
+    assert m.head == B.HEAD_AT_GPU
+    hv = m.mutable_cpu_data()
+    torch.testing.assert_close(hv, torch.arange(10, 20, dtype=torch.float32))
+    hv.fill_(-1.0)
+    m.gpu_data()
+    torch.cuda.synchronize()
+    assert float(flat[10:20].sum()) == -10.0 and float(flat[:10].sum()) == 45.0
+
+
+def test_ps_sync_on_gpu_stores_through_synced_blobs(gpu):
+    """EASGD through the native PS with device parameter stores: each
+    parameter's host mirror is a SyncedBlob over its store slice."""
+    from singa_amd import device, opt
+    from singa_amd.parallel.ps import ParamServer, PSClient, PSSync
+    from singa_amd.tensor import Tensor
+
+    dev = device.create_rocm_gpu_on(0)
+    s = ParamServer(0, 2)
+    try:
+        ep = [f"127.0.0.1:{s.port}"]
+
+        def store_for(v):
+            ps = [Tensor(device=dev, data=torch.full((4, 3), v, device=gpu)),
+                  Tensor(device=dev, data=torch.full((7,), v, device=gpu))]
+            for p in ps:
+                p.requires_grad = p.stores_grad = True
+            return opt.SGD(0.1).attach(ps)
+
+        st0, st1 = store_for(1.0), store_for(5.0)
+        sy0 = PSSync(st0, PSClient(ep), 0, 2, moving_rate=0.5)
+        sy1 = PSSync(st1, PSClient(ep), 1, 2, moving_rate=0.5)
+        assert all(b is not None for b in sy1._blobs)
+        sy0.bootstrap()
+        sy1.bootstrap()
+        torch.cuda.synchronize()
+        assert all(bool(torch.all(p.data == 1.0)) for p in st1.params)
+        for p in st1.params:
+            p.data.fill_(3.0)
+        sy1.sync()
+        torch.cuda.synchronize()
+        assert all(torch.allclose(p.data, torch.full_like(p.data, 2.5)) for p in st1.params)
+        assert np.allclose(s.value(0), 1.5) and np.allclose(s.value(1), 1.5)
+        sy0.client.stop()
+        sy1.client.stop()
+        assert s.wait_stop(5.0)
+    finally:
+        s.close()
