@@ -101,7 +101,7 @@ def build_core(force: bool = False, jobs: int = 8) -> Path:
         o = OBJ / ("core_" + s.stem + ".o")
         objs.append(o)
         if force or _newer(s, o, headers):
-            opt = "-O3" if s.stem == "cpu_ops" else "-O2"  # the CppCPU compute kernels
+            opt = "-O3" if s.stem in ("cpu_ops", "updater") else "-O2"  # the CppCPU compute kernels
             tasks.append(["g++", opt, "-std=c++17", "-fPIC", "-Wall", *_py_includes(), "-c", str(s), "-o", str(o)])
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         list(ex.map(_run, tasks))

@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdlib>
 #include <mutex>
@@ -40,13 +41,17 @@ class Pool {
   ~Pool() {
     {
       std::lock_guard<std::mutex> g(m_);
-      stop_ = true;
+      stop_.store(true, std::memory_order_release);
     }
     cv_.notify_all();
     for (auto& t : th_) t.join();
   }
   int size() const { return nworkers_ + 1; }
 
+  // Back-to-back parallel regions (a training step issues dozens) must not
+  // pay a futex wake / sleep per worker each: workers spin on the job
+  // generation for a short while after finishing a job and only then sleep
+  // on the condition variable; the caller spins on the active count likewise.
   void Run(int64_t n, int64_t grain, const std::function<void(int64_t, int64_t)>& f) {
     if (n <= 0) return;
     grain = std::max<int64_t>(1, grain);
@@ -56,28 +61,39 @@ class Pool {
     }
     int64_t nchunks = std::min<int64_t>((n + grain - 1) / grain, (int64_t)size() * 4);
     int64_t chunk = (n + nchunks - 1) / nchunks;
+    job_ = &f;
+    n_ = n;
+    chunk_ = chunk;
+    next_.store(0, std::memory_order_relaxed);
+    active_.store(nworkers_, std::memory_order_relaxed);
     {
-      std::lock_guard<std::mutex> g(m_);
-      job_ = &f;
-      n_ = n;
-      chunk_ = chunk;
-      next_.store(0, std::memory_order_relaxed);
-      active_ = nworkers_;
-      ++gen_;
+      std::lock_guard<std::mutex> g(m_);  // a sleeper checks gen_ under m_: no lost wake-up
+      gen_.fetch_add(1, std::memory_order_release);
     }
-    cv_.notify_all();
+    if (sleepers_.load(std::memory_order_acquire) > 0) cv_.notify_all();
     t_in_task = true;
     Work(f, n, chunk);
     t_in_task = false;
-    {
+    if (!SpinUntil([this] { return active_.load(std::memory_order_acquire) == 0; })) {
       std::unique_lock<std::mutex> g(m_);
-      done_.wait(g, [this] { return active_ == 0; });
-      job_ = nullptr;
+      done_.wait(g, [this] { return active_.load(std::memory_order_acquire) == 0; });
     }
+    job_ = nullptr;
     busy_.unlock();
   }
 
  private:
+  template <typename P>
+  bool SpinUntil(P&& pred) const {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int it = 0;; ++it) {
+      if (pred()) return true;
+#if defined(__x86_64__)
+      __builtin_ia32_pause();
+#endif
+      if ((it & 63) == 63 && std::chrono::steady_clock::now() - t0 > spin_) return false;
+    }
+  }
   void Work(const std::function<void(int64_t, int64_t)>& f, int64_t n, int64_t chunk) {
     for (;;) {
       int64_t b = next_.fetch_add(chunk, std::memory_order_relaxed);
@@ -88,25 +104,29 @@ class Pool {
   void Worker() {
     uint64_t seen = 0;
     for (;;) {
-      const std::function<void(int64_t, int64_t)>* job;
-      int64_t n, chunk;
-      {
+      if (!SpinUntil([&] { return stop_.load(std::memory_order_acquire) ||
+                                  gen_.load(std::memory_order_acquire) != seen; })) {
         std::unique_lock<std::mutex> g(m_);
-        cv_.wait(g, [&] { return stop_ || gen_ != seen; });
-        if (stop_) return;
-        seen = gen_;
-        job = job_;
-        n = n_;
-        chunk = chunk_;
+        sleepers_.fetch_add(1, std::memory_order_acq_rel);
+        cv_.wait(g, [&] { return stop_.load(std::memory_order_acquire) ||
+                                 gen_.load(std::memory_order_acquire) != seen; });
+        sleepers_.fetch_sub(1, std::memory_order_acq_rel);
       }
+      if (stop_.load(std::memory_order_acquire)) return;
+      seen = gen_.load(std::memory_order_acquire);
       t_in_task = true;
-      Work(*job, n, chunk);
+      Work(*job_, n_, chunk_);
       t_in_task = false;
-      {
+      if (active_.fetch_sub(1, std::memory_order_acq_rel) == 1) {
         std::lock_guard<std::mutex> g(m_);
-        if (--active_ == 0) done_.notify_one();
+        done_.notify_one();
       }
     }
+  }
+
+  static std::chrono::microseconds SpinBudget() {
+    const char* v = getenv("SINGA_AMD_CPU_SPIN_US");
+    return std::chrono::microseconds(v ? std::max(0, atoi(v)) : 200);
   }
 
   int nworkers_;
@@ -116,9 +136,10 @@ class Pool {
   const std::function<void(int64_t, int64_t)>* job_ = nullptr;
   int64_t n_ = 0, chunk_ = 1;
   std::atomic<int64_t> next_{0};
-  int active_ = 0;
-  uint64_t gen_ = 0;
-  bool stop_ = false;
+  std::atomic<int> active_{0}, sleepers_{0};
+  std::atomic<uint64_t> gen_{0};
+  std::atomic<bool> stop_{false};
+  std::chrono::microseconds spin_ = SpinBudget();
 };
 
 int DefaultThreads() {

@@ -8,7 +8,7 @@
 // and AdaGrad/RMSProp/AdaDelta applied it inside the history term only),
 // Nesterov's momentum is initialised.  Kinds match singa_amd.opt._KIND.
 //
-// Large buffers are split over a small pool of std::threads (the reference's
+// Large buffers are split over the CppCPU worker pool (the reference's
 // mshadow CPU loops were single-threaded SSE2); every element's update is
 // independent, so the result does not depend on the split.
 #include <algorithm>
@@ -18,28 +18,18 @@
 #include <thread>
 #include <vector>
 
+#include "cpu_ops.h"
 #include "runtime.h"
 
 namespace sgrt {
 
 namespace {
 
+// the CppCPU device's persistent worker pool (cpu_ops.cc): no thread start-up
+// per step, inline when called from inside another parallel region
 template <typename F>
 void parallel_for(int64_t n, int64_t grain, F&& f) {
-  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-  const int64_t chunks = std::min<int64_t>(hw, (n + grain - 1) / grain);
-  if (chunks <= 1) {
-    f(0, n);
-    return;
-  }
-  std::vector<std::thread> th;
-  const int64_t step = (n + chunks - 1) / chunks;
-  for (int64_t c = 1; c < chunks; ++c) {
-    const int64_t b = c * step, e = std::min(n, b + step);
-    if (b < e) th.emplace_back([&f, b, e] { f(b, e); });
-  }
-  f(0, std::min(n, step));
-  for (auto& t : th) t.join();
+  cpu::ParallelFor(n, grain, [&f](int64_t b, int64_t e) { f(b, e); });
 }
 
 }  // namespace
@@ -52,6 +42,83 @@ int UpdaterKind(const std::string& name) {
   throw std::invalid_argument("unknown updater kind: " + name);
 }
 
+namespace {
+
+// One kind's update over [b, e).  The kind, the presence of the per-element
+// lr / wd / mask vectors and momentum != 0 are compile-time, so every inner
+// loop is branch-free and auto-vectorises (AVX2 at -O3); masked elements keep
+// their old weight and state through selects.
+template <int K, bool VEC, bool MOM>
+void UpdateRange(const UpdateArgs& a, float* __restrict w, const float* __restrict g, float* __restrict s1,
+                 float* __restrict s2, const float* __restrict lr_vec, const float* __restrict wd_vec,
+                 const uint8_t* __restrict mask, float bc1, float bc2, int64_t b, int64_t e) {
+  const float gs = a.grad_scale, mom = a.momentum, damp1 = 1.f - a.dampening, rho = a.rho, rho1 = 1.f - a.rho;
+  const float b1 = a.beta1, b1c = 1.f - a.beta1, b2 = a.beta2, b2c = 1.f - a.beta2, eps = a.eps;
+  const bool nest = a.nesterov, adamw = a.adamw;
+#pragma GCC ivdep
+  for (int64_t i = b; i < e; ++i) {
+    const bool on = VEC ? mask == nullptr || mask[i] != 0 : true;
+    const float lr = VEC && lr_vec ? a.lr * lr_vec[i] : a.lr;
+    const float wd = VEC && wd_vec ? a.wd * wd_vec[i] : a.wd;
+    const float wi = w[i];
+    float gv = g[i] * gs;
+    if (!(K == kAdam && adamw)) gv += wd * wi;
+    float upd = 0.f, n1 = 0.f, n2 = 0.f;
+    if constexpr (K == kSGD) {
+      if constexpr (MOM) {
+        n1 = mom * s1[i] + damp1 * gv;
+        gv = nest ? gv + mom * n1 : n1;
+      }
+      upd = lr * gv;
+    } else if constexpr (K == kSGDRef) {  // h = m*h + lr*g; w -= h  (src/utils/updater.cc:62-80)
+      if constexpr (MOM) {
+        n1 = mom * s1[i] + lr * gv;
+        upd = n1;
+      } else {
+        upd = lr * gv;
+      }
+    } else if constexpr (K == kNesterovRef) {  // h0 = h; h = m*h + lr*g; w -= (1+m)*h - m*h0  (:89-105)
+      const float h0 = s1[i];
+      n1 = mom * h0 + lr * gv;
+      upd = (1.f + mom) * n1 - mom * h0;
+    } else if constexpr (K == kAdaGrad) {  // h += g^2; w -= lr*g/sqrt(h+delta)  (:115-128)
+      n1 = s1[i] + gv * gv;
+      upd = lr * gv / std::sqrt(n1 + eps);
+    } else if constexpr (K == kRMSProp) {  // h = rho*h + (1-rho)*g^2  (:140-153)
+      n1 = rho * s1[i] + rho1 * gv * gv;
+      upd = lr * gv / std::sqrt(n1 + eps);
+    } else if constexpr (K == kAdaDelta) {  // (:163-182)
+      n1 = rho * s1[i] + rho1 * gv * gv;
+      const float d = gv * std::sqrt(s2[i] + eps) / std::sqrt(n1 + eps);
+      n2 = rho * s2[i] + rho1 * d * d;
+      upd = lr * d;
+    } else if constexpr (K == kAdam) {
+      n1 = b1 * s1[i] + b1c * gv;
+      n2 = b2 * s2[i] + b2c * gv * gv;
+      upd = lr * (n1 / bc1 / (std::sqrt(n2 / bc2) + eps) + (adamw ? wd * wi : 0.f));
+    }
+    constexpr bool S1 = K != kSGD && K != kSGDRef ? true : MOM;
+    constexpr bool S2 = K == kAdaDelta || K == kAdam;
+    if constexpr (S1) s1[i] = on ? n1 : s1[i];
+    if constexpr (S2) s2[i] = on ? n2 : s2[i];
+    w[i] = on ? wi - upd : wi;
+  }
+}
+
+template <int K, bool MOM>
+void Dispatch(const UpdateArgs& a, float* w, const float* g, float* s1, float* s2, int64_t n, const float* lr_vec,
+              const float* wd_vec, const uint8_t* mask, float bc1, float bc2) {
+  const bool vec = lr_vec || wd_vec || mask;
+  parallel_for(n, 1 << 15, [&](int64_t b, int64_t e) {
+    if (vec)
+      UpdateRange<K, true, MOM>(a, w, g, s1, s2, lr_vec, wd_vec, mask, bc1, bc2, b, e);
+    else
+      UpdateRange<K, false, MOM>(a, w, g, s1, s2, lr_vec, wd_vec, mask, bc1, bc2, b, e);
+  });
+}
+
+}  // namespace
+
 void OptUpdate(const UpdateArgs& a, float* w, const float* g, float* s1, float* s2, int64_t n, const float* lr_vec,
                const float* wd_vec, const uint8_t* mask) {
   if (n <= 0) return;
@@ -60,64 +127,21 @@ void OptUpdate(const UpdateArgs& a, float* w, const float* g, float* s1, float* 
   if ((a.kind == kAdaDelta || a.kind == kAdam) && !s2) throw std::invalid_argument("OptUpdate: slot 2 required");
   const float bc1 = a.kind == kAdam ? 1.f - std::pow(a.beta1, a.t) : 1.f;
   const float bc2 = a.kind == kAdam ? 1.f - std::pow(a.beta2, a.t) : 1.f;
-  parallel_for(n, 1 << 16, [&](int64_t b, int64_t e) {
-    for (int64_t i = b; i < e; ++i) {
-      if (mask && !mask[i]) continue;
-      const float lr = lr_vec ? a.lr * lr_vec[i] : a.lr;
-      const float wd = wd_vec ? a.wd * wd_vec[i] : a.wd;
-      float gv = g[i] * a.grad_scale;
-      if (!(a.kind == kAdam && a.adamw)) gv += wd * w[i];
-      float upd;
-      switch (a.kind) {
-        case kSGD:
-          if (a.momentum != 0.f) {
-            s1[i] = a.momentum * s1[i] + (1.f - a.dampening) * gv;
-            gv = a.nesterov ? gv + a.momentum * s1[i] : s1[i];
-          }
-          upd = lr * gv;
-          break;
-        case kSGDRef:  // h = m*h + lr*g; w -= h  (src/utils/updater.cc:62-80)
-          if (a.momentum > 0.f) {
-            s1[i] = a.momentum * s1[i] + lr * gv;
-            upd = s1[i];
-          } else {
-            upd = lr * gv;
-          }
-          break;
-        case kNesterovRef: {  // h0 = h; h = m*h + lr*g; w -= (1+m)*h - m*h0  (:89-105)
-          const float h0 = s1[i];
-          s1[i] = a.momentum * h0 + lr * gv;
-          upd = (1.f + a.momentum) * s1[i] - a.momentum * h0;
-          break;
-        }
-        case kAdaGrad:  // h += g^2; w -= lr*g/sqrt(h+delta)  (:115-128)
-          s1[i] += gv * gv;
-          upd = lr * gv / std::sqrt(s1[i] + a.eps);
-          break;
-        case kRMSProp:  // h = rho*h + (1-rho)*g^2  (:140-153)
-          s1[i] = a.rho * s1[i] + (1.f - a.rho) * gv * gv;
-          upd = lr * gv / std::sqrt(s1[i] + a.eps);
-          break;
-        case kAdaDelta: {  // (:163-182)
-          s1[i] = a.rho * s1[i] + (1.f - a.rho) * gv * gv;
-          const float d = gv * std::sqrt(s2[i] + a.eps) / std::sqrt(s1[i] + a.eps);
-          s2[i] = a.rho * s2[i] + (1.f - a.rho) * d * d;
-          upd = lr * d;
-          break;
-        }
-        case kAdam: {
-          s1[i] = a.beta1 * s1[i] + (1.f - a.beta1) * gv;
-          s2[i] = a.beta2 * s2[i] + (1.f - a.beta2) * gv * gv;
-          const float mh = s1[i] / bc1, vh = s2[i] / bc2;
-          upd = lr * (mh / (std::sqrt(vh) + a.eps) + (a.adamw ? wd * w[i] : 0.f));
-          break;
-        }
-        default:
-          upd = 0.f;
-      }
-      w[i] -= upd;
-    }
-  });
+  const bool mom = a.momentum != 0.f;
+#define SG_UPD(K)                                                              \
+  (mom ? Dispatch<K, true>(a, w, g, s1, s2, n, lr_vec, wd_vec, mask, bc1, bc2) \
+       : Dispatch<K, false>(a, w, g, s1, s2, n, lr_vec, wd_vec, mask, bc1, bc2))
+  switch (a.kind) {
+    case kSGD: SG_UPD(kSGD); break;
+    case kSGDRef: SG_UPD(kSGDRef); break;
+    case kNesterovRef: SG_UPD(kNesterovRef); break;
+    case kAdaGrad: SG_UPD(kAdaGrad); break;
+    case kRMSProp: SG_UPD(kRMSProp); break;
+    case kAdaDelta: SG_UPD(kAdaDelta); break;
+    case kAdam: SG_UPD(kAdam); break;
+    default: break;
+  }
+#undef SG_UPD
 }
 
 // reference GetLearningRate (src/utils/updater.cc:11-51); kLinear clamps at
