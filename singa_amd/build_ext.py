@@ -61,7 +61,7 @@ def _run(cmd: list[str]) -> None:
 def build_kernels(force: bool = False, jobs: int = 8) -> Path:
     OBJ.mkdir(parents=True, exist_ok=True)
     hipcc = _hipcc()
-    headers = list((CSRC / "kernels").glob("*.h"))
+    headers = list((CSRC / "kernels").glob("*.h")) + list((CSRC / "kernels").glob("*.inc"))
     srcs = sorted((CSRC / "kernels").glob("*.hip"))
     objs = []
     tasks = []

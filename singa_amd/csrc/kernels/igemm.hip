@@ -501,6 +501,7 @@ __device__ __forceinline__ void raw_barrier() {
   asm volatile("" ::: "memory");
 }
 
+
 // NTH threads = WM x WN waves, each owning a (BM/WM) x (BN/WN) block of 16x16
 // MFMA tiles.  STAGES == 2: the v2 loop (one __syncthreads per K-tile, the
 // next tile's DMA overlapping this tile's MFMAs, two workgroups per CU hide
@@ -510,7 +511,8 @@ __device__ __forceinline__ void raw_barrier() {
 // the younger tiles still in flight) and a raw barrier (every wave's DMA
 // retired, every wave done reading the stage about to be refilled).
 template <int BM, int BN, int AM, int BMODE, int OUT, int NTH = NT, int WM = 2, int WN = 2, int STAGES = 2>
-__global__ void __launch_bounds__(NTH, STAGES == 1 ? 3 : (NTH == 512 && STAGES == 2) ? 4 : 2) igemm_k(const GemmArgs p) {
+__global__ void __launch_bounds__(NTH, STAGES == 1 ? 3 : (NTH == 512 && STAGES == 2 && BM * BN <= 128 * 128) ? 4 : 2)
+    igemm_k(const GemmArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
   constexpr int STAGE = A_BYTES + B_BYTES;
@@ -729,289 +731,207 @@ __global__ void __launch_bounds__(NTH, STAGES == 1 ? 3 : (NTH == 512 && STAGES =
     }
   }
   wait_vmcnt<0>();  // the dummy DMA too, before the epilogue reuses the LDS
+  wait_vmcnt<0>();  // the dummy DMA too, before the epilogue reuses the LDS
+#include "igemm_epilogue.inc"
+}
 
-  // Epilogue.  acc[i][j] = D[n][m]: lane col m = l&15, rows n = (l>>4)*4+r.
-  const int l = threadIdx.x & 63;
-  if constexpr (OUT == OUT_F32_ATOMIC) {
-    // Split-K partial tile -> fp32 atomics.  Float atomics run at the memory
-    // side at ~1.3 TB/s only when one wave-instruction covers 256 contiguous
-    // bytes; straight from the MFMA layout a wave-instruction would touch 16
-    // rows x 4 scattered dwords (~17x slower, MI355X_MICROARCH "Global float
-    // atomics") -- that alone bounded the conv weight gradient.  So the tile
-    // goes through LDS and is re-read row-contiguously: lane i of a wave adds
-    // column i of a 64-wide row segment.
-    constexpr int LDT = BN + 4;
-    float* tile = (float*)smem;
-    __syncthreads();  // all waves are done reading the last operand stage
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int ml = wm * WTM + i * 16 + (l & 15);
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int nl = wn * WTN + j * 16 + (l >> 4) * 4;
-        *(float4*)(tile + ml * LDT + nl) = make_float4(acc[i][j][0] * p.alpha, acc[i][j][1] * p.alpha,
-                                                       acc[i][j][2] * p.alpha, acc[i][j][3] * p.alpha);
-      }
-    }
-    __syncthreads();
-    float* cbase = (float*)pc;
-#pragma unroll 4
-    for (int e = threadIdx.x; e < BM * BN; e += NTH) {
-      const int ml = e / BN, nl = e % BN;
-      const int m = m0 + ml, n = n0 + nl;
-      if (m < M && n < p.N) atomicAdd(cbase + (int64_t)m * p.ldc + n, tile[ml * LDT + nl]);
-    }
-    return;
+// ------------------------------------------------------------------------------
+// Ping-pong 256 x 256 x 64 GEMM (K-major A [M][K] and B [N][K]), 512 threads.
+//
+// igemm_k's loop -- every wave loads fragments, waits at the barrier, runs its
+// MFMAs, waits again -- leaves the MFMA pipe idle whenever all waves of a
+// workgroup sit at the same barrier; its 128 x 128 tile tops out near 0.9 PF on
+// large GEMMs (and a 256 x 256 tile in the same loop is no better).  Here the
+// eight waves form two groups (wave row wr = 0 / 1, one wave of each group per
+// SIMD) that run one barrier apart: while one group issues its LDS fragment
+// reads and the next half-tile's LDS-DMA, the other group's MFMAs (at raised
+// priority) own the SIMD, then they swap.  Each K-tile is 4 phases, one per
+// 64 x 32 quadrant (mi, ni) of the wave's 128 x 64 output: (0,0) (0,1) (1,1)
+// (1,0), 16 MFMAs each.
+//
+// LDS: 2 buffers x 4 half-tiles of 16 KB (A-h0, A-h1, B-h0, B-h1).  Half-tile
+// A-h(mi) holds the 64 rows of quadrant row mi of BOTH wave rows, B-h(ni) the
+// 32 columns of quadrant column ni of all four wave columns, so a half-tile is
+// dead after the phase that reads it into registers and can be refilled with
+// a later K-tile's while this K-tile's other quadrants still compute.  Each
+// phase issues one half-tile and waits with a COUNTED vmcnt for the one the
+// next phase reads, four half-tiles staying in flight (never vmcnt(0) in the
+// loop; schedule below).  Measured (profiles/r3/gemm_ceiling_pp.jsonl,
+// random bf16): 8192^3 1234 TF vs 1029 for igemm_k's best tile; +12..28 % on
+// K = 2304..4608, +8 % at K = 2048; slower than igemm_k on short K (<= 1024),
+// where the tile's prologue and epilogue dominate.
+// ------------------------------------------------------------------------------
+constexpr int PP_HALF = 128 * BK * 2;  // one half-tile image (16 KB)
+constexpr int PP_BUF = 4 * PP_HALF;    // one K-tile (64 KB)
+
+template <int OUT>
+__global__ void __launch_bounds__(512, 2) pp_gemm_k(const GemmArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int BM = 256, BN = 256;
+  const int64_t yb = p.bh > 0 ? (int64_t)(blockIdx.y / p.bh) : (int64_t)blockIdx.y;
+  const int64_t yh = p.bh > 0 ? (int64_t)(blockIdx.y % p.bh) : 0;
+  const bf16* __restrict__ pa = p.a + yb * p.sa + yh * p.sa2;
+  const bf16* __restrict__ pb = p.b + yb * p.sb + yh * p.sb2;
+  char* pc = (char*)p.c + (yb * p.sc + yh * p.sc2) * (OUT == OUT_BF16 ? 2 : 4);
+  const Phase& P = p.g.phs[0];
+  const int M = p.M, N = p.N, K = p.K;
+
+  const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
+  const int nwg = tiles_m * tiles_n;
+  int bid = blockIdx.x;
+  if (bid >= nwg) return;
+  if (nwg >= 8) {
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
   }
-  if constexpr (OUT == OUT_BF16) {
-    // Staged through LDS so every store is a full 16-byte vector of 8
-    // consecutive channels (the MFMA layout alone gives 8-byte pieces of 16
-    // different rows per wave-instruction).  The tile is kept in fp32 so
-    // beta*C + ReLU round to bf16 once.
-    if ((p.N & 7) == 0 && (p.ldc & 7) == 0 && p.lds_epilogue) {
-      constexpr int LDT = BN + 4;  // fp32 row stride (+16 B against bank conflicts)
-      constexpr int LDT16 = BN + 8;  // bf16 staging (single-stage variant, beta == 0): row stride +16 B
-      float* tile = (float*)smem;
-      bf16* tile16 = (bf16*)smem;
-      __syncthreads();  // all waves are done reading the last operand stage
-      if (p.alpha != 1.f) {  // (uniform; alpha is 1 for every conv)
+  const int band = 8;
+  const int group = bid / (band * tiles_n);
+  const int first_m = group * band;
+  const int gm = min(tiles_m - first_m, band);
+  const int tm = first_m + (bid % (band * tiles_n)) % gm;
+  const int tn = (bid % (band * tiles_n)) / gm;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int nk = (K + BK - 1) / BK;
+
+  const int t = threadIdx.x, l = t & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wr = wv >> 2, wc = wv & 3;
+
+  // LDS-DMA sources: thread t fetches local rows rl and rl + 64 of a half-tile
+  // image (one wave-instruction = 8 rows x 128 B), k-chunk (t & 7) ^ swz(row)
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(pa, p.a_bytes), rb = make_rsrc(pb, p.b_bytes);
+  const int rl = t >> 3;
+  const int lchunk = (t & 7) ^ ((rl >> 1) & 7);
+  unsigned va[2][2], vb[2][2];  // [half][v] byte offsets (BIAS-ed past the extent when out of range)
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
+  for (int h = 0; h < 2; ++h)
 #pragma unroll
-          for (int j = 0; j < TN; ++j) acc[i][j] *= p.alpha;
-      }
+    for (int v = 0; v < 2; ++v) {
+      const int m = m0 + v * 128 + h * 64 + rl;
+      va[h][v] = m < M ? (unsigned)(m * (int)p.lda + lchunk * 8) * 2u : BIAS;
+      const int lr = rl + 64 * v;
+      const int n = n0 + (lr >> 5) * 64 + h * 32 + (lr & 31);
+      vb[h][v] = n < N ? (unsigned)(n * (int)p.ldb + lchunk * 8) * 2u : BIAS;
+    }
+  // half-tile q (0 A-h0, 1 B-h0, 2 B-h1, 3 A-h1) of K-tile kt into buffer kt & 1
+  auto issue = [&](auto qc, int kt) {
+    constexpr int q = decltype(qc)::value;
+    constexpr bool isA = q == 0 || q == 3;
+    constexpr int h = q == 0 ? 0 : q == 1 ? 0 : q == 2 ? 1 : 1;
+    constexpr int slot = isA ? h : 2 + h;  // image position inside the buffer
+    const int k0 = kt * BK;
+    const bool live = kt < nk;
+    const __amdgpu_buffer_rsrc_t rs = live ? (isA ? ra : rb) : make_rsrc(nullptr, 0);
+    const bool kin = K - k0 >= BK || k0 + lchunk * 8 < K;
+    char* dst = smem + (kt & 1) * PP_BUF + slot * PP_HALF + (8 * wv) * 128;
 #pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int ml = wm * WTM + i * 16 + (l & 15);
+    for (int v = 0; v < 2; ++v) {
+      unsigned off = kin ? (isA ? va[h][v] : vb[h][v]) + (unsigned)k0 * 2u : OOB;
+      asm volatile("" : "+v"(off));  // materialise the select (else hipcc splits the load into two branches)
+      bld16(rs, off, dst + 64 * v * 128);
+    }
+  };
+
+  // fragment offsets inside a half-tile image (same layout for every image)
+  int oa[4][2], ob[2][2];
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const int nl = wn * WTN + j * 16 + (l >> 4) * 4;
-          const int n = n0 + nl;
-          float4 v = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
-          if (p.bias && n < p.N) {
-            v.x += p.bias[n]; v.y += p.bias[n + 1]; v.z += p.bias[n + 2]; v.w += p.bias[n + 3];
-          }
-          if constexpr (STAGES == 1) {
-            // rounded to bf16 once here: with beta == 0 (host-checked) the
-            // value is final up to the ReLU, which commutes with the rounding
-            bf16x4 o;
-            o[0] = (bf16)v.x; o[1] = (bf16)v.y; o[2] = (bf16)v.z; o[3] = (bf16)v.w;
-            *(bf16x4*)(tile16 + ml * LDT16 + nl) = o;
-          } else {
-            *(float4*)(tile + ml * LDT + nl) = v;
-          }
-        }
-      }
-      __syncthreads();
-      constexpr int CPRW = BN / 8;            // 16-byte output chunks per row
-      constexpr int RPP = NTH / CPRW;           // rows per pass
-      const int ch = threadIdx.x % CPRW, r0 = threadIdx.x / CPRW;
-      const int n = n0 + ch * 8;
-      float st_s[8], st_q[8];
+  for (int kk = 0; kk < 2; ++kk) {
+    const int ch = kk * 4 + (l >> 4);
 #pragma unroll
-      for (int r = 0; r < 8; ++r) { st_s[r] = 0.f; st_q[r] = 0.f; }
-      float bmu[8], bis[8], bsc[8], bsf[8];
-      if (p.stats && p.stats_mode >= 1 && n < p.N) {
+    for (int i = 0; i < 4; ++i) {
+      const int r = wr * 64 + i * 16 + (l & 15);
+      oa[i][kk] = r * 128 + kmajor_swz(r, ch) * 16;
+    }
 #pragma unroll
-        for (int r = 0; r < 8; ++r) {
-          bmu[r] = p.bnb_mean[n + r]; bis[r] = p.bnb_invstd[n + r];
-          if (p.stats_mode == 1) { bsc[r] = p.bnb_scale[n + r]; bsf[r] = p.bnb_shift[n + r]; }
-        }
-      }
-      if (n < p.N) {
-        // Row offsets, then every global READ of the epilogue (the beta*C
-        // accumulate source, the fused BN-backward input x) issued up front:
-        // inside the store loop the compiler cannot hoist them above the
-        // previous rows' stores (possible aliasing), which serialised one
-        // full memory latency per row.
-        constexpr int NPS = BM / RPP;
-        int64_t rofs[NPS];
-        bool rok[NPS];
-        const int64_t rbase = (int64_t)(m0 + r0) * p.ldc, rstep = (int64_t)RPP * p.ldc;
-#pragma unroll
-        for (int pass = 0; pass < NPS; ++pass) {
-          const int m = m0 + r0 + pass * RPP;
-          rok[pass] = m < M;
-          const int mm = rok[pass] ? m : 0;
-          if (!p.out_phase) {
-            // rows past M map to row 0: the up-front loads below read every pass
-            rofs[pass] = rok[pass] ? rbase + pass * rstep : 0;
-          } else {
-            const ConvGeom& g = p.g;
-            const int nn = P.dHpWp.div(mm);
-            const int rem = mm - nn * P.Hp * P.Wp;
-            const int hh = P.dWp.div(rem);
-            const int ww = rem - hh * P.Wp;
-            rofs[pass] = (((int64_t)nn * g.H + P.a + g.sh * hh) * g.W + P.b + g.sw * ww) * p.ldc;
-          }
-        }
-        const bool bnb = p.stats && p.stats_mode >= 1;
-        const bool bits = p.stats && p.stats_mode == 2;
-        unsigned mbits[NPS];
-        if (bits) {
-#pragma unroll
-          for (int pass = 0; pass < NPS; ++pass) mbits[pass] = p.bnb_mask[(rofs[pass] + n) >> 3];
-        }
-        bf16x8 pre[NPS];
-        if (bnb || p.beta != 0.f) {
-          const bf16* src = bnb ? p.bnb_x : (const bf16*)pc;
-#pragma unroll
-          for (int pass = 0; pass < NPS; ++pass) pre[pass] = *(const bf16x8*)(src + rofs[pass] + n);
-        }
-        bf16x8 pold[NPS];
-        if (bnb && p.beta != 0.f) {
-#pragma unroll
-          for (int pass = 0; pass < NPS; ++pass) pold[pass] = *(const bf16x8*)((const bf16*)pc + rofs[pass] + n);
-        }
-#pragma unroll
-        for (int pass = 0; pass < NPS; ++pass) {
-          const int ml = r0 + pass * RPP;
-          if (!rok[pass]) continue;
-          const int64_t rowoff = rofs[pass];
-          float v[8];
-          if constexpr (STAGES == 1) {
-            const bf16x8 t8 = *(const bf16x8*)(tile16 + ml * LDT16 + ch * 8);
-#pragma unroll
-            for (int r = 0; r < 8; ++r) v[r] = (float)t8[r];
-          } else {
-            const float4 a = *(const float4*)(tile + ml * LDT + ch * 8);
-            const float4 b = *(const float4*)(tile + ml * LDT + ch * 8 + 4);
-            v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-          }
-          bf16* c = (bf16*)pc + rowoff + n;
-          if (p.beta != 0.f) {
-            const bf16x8 old = bnb ? pold[pass] : pre[pass];
-#pragma unroll
-            for (int r = 0; r < 8; ++r) v[r] += p.beta * (float)old[r];
-          }
-          bf16x8 o;
-#pragma unroll
-          for (int r = 0; r < 8; ++r) o[r] = (bf16)(p.relu ? fmaxf(v[r], 0.f) : v[r]);
-          *(bf16x8*)c = o;
-          if (bnb) {
-            const bf16x8 xb = pre[pass];
-#pragma unroll
-            for (int r = 0; r < 8; ++r) {
-              const float xf = (float)xb[r];
-              const bool on = bits ? ((mbits[pass] >> r) & 1u) != 0 : xf * bsc[r] + bsf[r] > 0.f;
-              const float gr = on ? (float)o[r] : 0.f;
-              st_s[r] += gr;
-              st_q[r] += gr * (xf - bmu[r]) * bis[r];
-            }
-          } else if (p.stats) {
-#pragma unroll
-            for (int r = 0; r < 8; ++r) {
-              const float f = (float)o[r];
-              st_s[r] += f;
-              st_q[r] += f * f;
-            }
-          }
-        }
-      }
-      if (p.stats) {
-        // fused BatchNorm statistics: reduce the RPP row-threads of each
-        // 8-channel chunk through LDS -- one thread per (chunk, value) pair,
-        // RPP reads each (a v1 summed everything in the CPRW chunk threads:
-        // RPP x 16 serial reads per thread, microseconds per workgroup) --
-        // then one plain store per value into row tm of the [tiles_m][2][N]
-        // workspace (bn_fwd_finalize sums the rows in a fixed order:
-        // deterministic) or one atomic into the 32 slot rows
-        __syncthreads();
-        float* red = (float*)smem;  // [NTH][16]
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-          red[threadIdx.x * 16 + r] = st_s[r];
-          red[threadIdx.x * 16 + 8 + r] = st_q[r];
-        }
-        __syncthreads();
-        static_assert(CPRW * 16 <= NTH, "stats reduction: one thread per (chunk, value)");
-        if (threadIdx.x < CPRW * 16) {
-          const int c = threadIdx.x >> 4, r = threadIdx.x & 15;
-          const int nn = n0 + c * 8;
-          if (nn < p.N) {
-            float a = red[c * 16 + r];
-            for (int k = 1; k < RPP; ++k) a += red[(k * CPRW + c) * 16 + r];
-            const int col = r < 8 ? nn + r : p.N + nn + (r - 8);
-            if (p.stats_det) p.stats[(int64_t)tm * 2 * p.N + col] = a;  // own row per tile-row
-            else atomicAdd(p.stats + (int64_t)(tm & 31) * 2 * p.N + col, a);  // 32 slot rows (zeroed by the caller)
-          }
-        }
-      }
-      return;
+    for (int j = 0; j < 2; ++j) {
+      const int r = wc * 32 + j * 16 + (l & 15);
+      ob[j][kk] = r * 128 + kmajor_swz(r, ch) * 16;
     }
   }
+
+  f32x4 acc[8][4];
 #pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    const int m = m0 + wm * WTM + i * 16 + (l & 15);
-    if (m >= M) continue;
-    int64_t rowoff;
-    if (p.out_phase) {
-      const ConvGeom& g = p.g;
-      const int n = P.dHpWp.div(m);
-      const int rem = m - n * P.Hp * P.Wp;
-      const int hh = P.dWp.div(rem);
-      const int ww = rem - hh * P.Wp;
-      rowoff = (((int64_t)n * g.H + P.a + g.sh * hh) * g.W + P.b + g.sw * ww) * p.ldc;
-    } else {
-      rowoff = (int64_t)m * p.ldc;
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 fa[4][2], fb0[2][2], fb1[2][2];  // A of the current quadrant row; B of both quadrant columns
+  typedef const __attribute__((address_space(3))) char* lds_cp;
+  const lds_cp lbase = (lds_cp)(__attribute__((address_space(3))) char*)smem;
+
+  // one phase: [fragment reads + DMA of half-tile Q of K-tile kt + KT +
+  // counted wait] barrier [16 MFMAs of quadrant (MI, NI) at priority 1] barrier
+  auto phase = [&](auto mic, auto nic, auto rac, auto rbc, auto qc, auto ktc, int kt) {
+    constexpr int MI = decltype(mic)::value, NI = decltype(nic)::value;
+    const lds_cp buf = lbase + (kt & 1) * PP_BUF;
+    auto& fb = NI == 0 ? fb0 : fb1;
+    if constexpr (decltype(rbc)::value) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) fb[j][kk] = *(const bf16x8*)(buf + (2 + NI) * PP_HALF + ob[j][kk]);
     }
+    if constexpr (decltype(rac)::value) {
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int n = n0 + wn * WTN + j * 16 + (l >> 4) * 4;
-      if (n >= p.N) continue;
-      float v[4] = {acc[i][j][0] * p.alpha, acc[i][j][1] * p.alpha, acc[i][j][2] * p.alpha,
-                    acc[i][j][3] * p.alpha};
-      const bool full = n + 3 < p.N;
-      if (OUT == OUT_F32_ATOMIC) {
-        float* c = (float*)pc + rowoff + n;
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (full || n + r < p.N) atomicAdd(c + r, v[r]);
-        continue;
-      }
-      if (p.bias) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] += (full || n + r < p.N) ? p.bias[n + r] : 0.f;
-      }
-      if (OUT == OUT_F32) {
-        float* c = (float*)pc + rowoff + n;
-        if (p.beta != 0.f) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (full || n + r < p.N) v[r] += p.beta * c[r];
-        }
-        if (p.relu) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
-        }
-        if (full && ((p.ldc & 3) == 0)) *(float4*)c = make_float4(v[0], v[1], v[2], v[3]);
-        else {
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (n + r < p.N) c[r] = v[r];
-        }
-      } else {
-        bf16* c = (bf16*)pc + rowoff + n;
-        if (p.beta != 0.f) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (full || n + r < p.N) v[r] += p.beta * (float)c[r];
-        }
-        if (p.relu) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
-        }
-        if (full && ((p.ldc & 3) == 0)) {
-          bf16x4 o;
-          o[0] = (bf16)v[0]; o[1] = (bf16)v[1]; o[2] = (bf16)v[2]; o[3] = (bf16)v[3];
-          *(bf16x4*)c = o;
-        } else {
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (n + r < p.N) c[r] = (bf16)v[r];
-        }
-      }
+        for (int kk = 0; kk < 2; ++kk) fa[i][kk] = *(const bf16x8*)(buf + MI * PP_HALF + oa[i][kk]);
     }
+    issue(qc, kt + decltype(ktc)::value);
+    wait_vmcnt<8>();  // four half-tiles stay in flight
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[MI * 4 + i][NI * 2 + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j][kk], fa[i][kk], acc[MI * 4 + i][NI * 2 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
+  using T = std::true_type;
+  using F = std::false_type;
+
+  // Half-tile schedule (q: 0 A-h0, 1 B-h0, 2 B-h1, 3 A-h1).  Last reads of
+  // K-tile t: A-h0, B-h0 in phase 1 (B-h0's fragments stay in registers for
+  // phase 4), B-h1 in 2, A-h1 in 3.  Refills, each >= 2 phases after the read
+  // of the image it overwrites (same buffer, K-tile t+2 or t+1):
+  //   phase 1: B-h1(t+1)  2: A-h1(t+1)  3: A-h0(t+2)  4: B-h0(t+2)
+  // so every half-tile is issued 5-6 phases before the phase that reads it
+  // and every wait can leave the four youngest half-tiles in flight.
+  if (nk > 0) {
+    issue(I0{}, 0);
+    issue(I1{}, 0);
+    issue(I2{}, 0);
+    issue(I3{}, 0);
+    issue(I0{}, 1);
+    issue(I1{}, 1);
+    wait_vmcnt<8>();  // A-h0 and B-h0 of K-tile 0 (this wave's share)
+    raw_barrier();    // ... every wave's
+    if (wr == 1) __builtin_amdgcn_s_barrier();  // the second group runs one barrier behind
+    for (int kt = 0; kt < nk; ++kt) {
+      phase(I0{}, I0{}, T{}, T{}, I2{}, I1{}, kt);  // (0,0): reads A-h0, B-h0
+      phase(I0{}, I1{}, F{}, T{}, I3{}, I1{}, kt);  // (0,1): reads B-h1
+      phase(I1{}, I1{}, T{}, F{}, I0{}, I2{}, kt);  // (1,1): reads A-h1
+      phase(I1{}, I0{}, F{}, F{}, I1{}, I2{}, kt);  // (1,0): registers only
+    }
+    if (wr == 0) __builtin_amdgcn_s_barrier();  // rebalance the barrier count
+  }
+  wait_vmcnt<0>();  // the dummy DMA of K-tile nk too, before the epilogue reuses the LDS
+  {
+    constexpr int NTH = 512, STAGES = 2, WTM = 128, WTN = 64, TM = 8, TN = 4;
+    const int wm = wr, wn = wc;
+#include "igemm_epilogue.inc"
   }
 }
 
@@ -1132,8 +1052,10 @@ static void launch_t(const GemmArgs& p_in, int tiles, int ydim, int zdim, hipStr
   p.xcd_split = (OUT == OUT_F32_ATOMIC && g_tune[2] && ydim == 1 && zdim >= 8 && (zdim & 7) == 0) ? 1 : 0;
   dim3 grid(tiles, ydim, zdim), block(NTH);
   constexpr int stages = STAGES * (BM + BN) * BK * 2;
+  constexpr int rch = (STAGES == 1 || BM * (BN + 4) * 4 <= 152 * 1024) ? BM : BM / 4;  // epilogue row chunk
   constexpr int etile = STAGES == 1 ? (OUT == OUT_BF16 ? BM * (BN + 8) * 2 : BM * (BN + 4) * 4)  // bf16 staging
-                        : (OUT == OUT_BF16 || OUT == OUT_F32_ATOMIC) ? BM * (BN + 4) * 4 : 0;  // fp32 epilogue tile
+                        : OUT == OUT_BF16 ? rch * (BN + 4) * 4                                  // fp32 epilogue tile
+                        : OUT == OUT_F32_ATOMIC ? BM * (BN + 4) * 4 : 0;
   constexpr int ered = (OUT == OUT_BF16) ? NTH * 16 * 4 : 0;  // BN-stats reduction scratch
   static_assert(STAGES != 1 || (OUT == OUT_BF16 && ered <= (etile > stages_c(BM, BN, STAGES) ? etile : stages_c(BM, BN, STAGES))),
                 "single-stage variant: bf16 output only");
@@ -1149,6 +1071,19 @@ static void launch_t(const GemmArgs& p_in, int tiles, int ydim, int zdim, hipStr
   hipLaunchKernelGGL(kern, grid, block, lds, s, p);
 }
 
+template <int OUT>
+static void launch_pp(const GemmArgs& p_in, int tiles, int ydim, hipStream_t s) {
+  GemmArgs p = p_in;
+  p.lds_epilogue = g_tune[1];
+  constexpr int lds = 2 * PP_BUF;
+  auto* kern = pp_gemm_k<OUT>;
+  static bool attr = [kern] {
+    return hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
+  }();
+  (void)attr;
+  hipLaunchKernelGGL(kern, dim3(tiles, ydim, 1), dim3(512), lds, s, p);
+}
+
 // 8-wave (512-thread) tiles.  Returns 0 (the 4-wave v2 tiles) or
 //   1: 128 x 128, waves 2 x 4 of 64 x 32, 2 stages, two workgroups per CU
 //      (measured on ResNet-50 b1024: equal or up to 10 % faster than the
@@ -1159,10 +1094,16 @@ static void launch_t(const GemmArgs& p_in, int tiles, int ydim, int zdim, hipStr
 // 2 and 3 keep two K-tiles in flight but lose to two independent workgroups
 // per CU on every ResNet-50 conv (the waves of one workgroup reach each
 // barrier together, nothing else covers the MFMA pipe): tests only.
+//   4: the ping-pong 256 x 256 kernel (pp_gemm_k; plain K-major GEMMs).
+//      (256 x 256 and 256 x 128 tiles in igemm_k's own early-issue loop
+//      were measured slower than its 128 x 128 tile on every ResNet-50
+//      1x1-conv GEMM shape and only 8-12 % faster at 8192^3:
+//      profiles/r3/gemm_ceiling_256tiles.jsonl.)
 static int pick_big(int M, int N) {
   if (g_tune[4] == 5) return 1;  // tests: force a variant at any size
   if (g_tune[4] == 6) return 2;
   if (g_tune[4] == 7) return 3;
+  if (g_tune[4] == 8) return 4;
   if (!g_tune[5] || g_tune[4] != 0) return 0;
   auto wg = [&](int bm, int bn) { return (long)((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
   if (N >= 128 && !((N % 128) != 0 && (N % 128) <= 64) && wg(128, 128) >= 512) return 1;
@@ -1230,7 +1171,24 @@ static void launch(const GemmArgs& p, int M, int splits, hipStream_t s, int batc
         launch_t<128, 128, AM, BMODE, OUT_BF16, 256, 2, 2, 1>(p, tiles, batch, z, s);
         return;
       }
-      const int big = pick_big(M, p.N);
+      int big = pick_big(M, p.N);
+      // the ping-pong 256 x 256 kernel: plain K-major GEMMs (1x1 convs, dgrad
+      // of 1x1 convs) with long K and enough 256 x 256 tiles for the chip
+      // (measured: +8..28 % at K >= 2048, slower on short K --
+      // profiles/r3/gemm_ceiling_pp.jsonl); never with deterministic BN
+      // statistics (their row count assumes igemm_k's tile rows)
+      const bool pp_ok = AM == LM_KMAJOR && BMODE == LM_KMAJOR && !p.out_phase && zdim <= 1 &&
+                         !(p.stats && p.stats_det);
+      if (big == 0 && g_tune[4] == 0 && g_tune[5] && pp_ok && p.K >= 2048 &&
+          (long)((M + 255) / 256) * ((p.N + 255) / 256) >= 256)
+        big = 4;
+      if (big == 4) {
+        if (pp_ok) {
+          launch_pp<OUT>(p, ((M + 255) / 256) * ((p.N + 255) / 256), batch, s);
+          return;
+        }
+        big = 1;
+      }
       if (big == 1) {
         const int tiles = ((M + 127) / 128) * ((p.N + 127) / 128);
         launch_t<128, 128, AM, BMODE, OUT, 512, 2, 4, 2>(p, tiles, batch, z, s);
@@ -1528,7 +1486,10 @@ void sg_conv_wgrad(const void* x, const void* dy, void* dw_out, int N, int H, in
 int sg_conv_stats_rows(int M, int N) {
   if ((N & 7) != 0 || !g_tune[1]) return 0;
   if (!sg_bn_deterministic()) return 32;
-  if (const int big = pick_big(M, N)) return (M + big_bm(big) - 1) / big_bm(big);
+  if (int big = pick_big(M, N)) {
+    if (big == 4) big = 1;  // the ping-pong kernel is not used with deterministic statistics
+    return (M + big_bm(big) - 1) / big_bm(big);
+  }
   int BM, BN;
   pick_tile(M, N, BM, BN);
   return (M + BM - 1) / BM;

@@ -147,14 +147,16 @@ def test_conv_fwd_bwd(gpu, case, wmode, kmajor, monkeypatch):
 @pytest.fixture
 def big_tiles():
     """Force an 8-wave conv/GEMM variant (5: 128x128 two workgroups per CU,
-    6: 256x64 4-stage ring, 7: 256x128 3-stage ring) for every problem size,
-    restore the size policy after."""
+    6: 256x64 4-stage ring, 7: 256x128 3-stage ring, 8: the ping-pong 256x256
+    kernel where it applies -- plain K-major GEMMs, 1x1 stride-1 conv forward
+    and data gradient -- else 5) for every problem size, restore the size
+    policy after."""
     from singa_amd.ops import native as NN
     yield lambda mode: NN.lib().set_tuning(4, mode)
     NN.lib().set_tuning(4, 0)
 
 
-@pytest.mark.parametrize("tile", [5, 6, 7])
+@pytest.mark.parametrize("tile", [5, 6, 7, 8])
 @pytest.mark.parametrize("case", CONV_CASES)
 def test_conv_big_tiles(gpu, case, tile, big_tiles, monkeypatch):
     """fwd (fp32 and bf16 epilogue) and dgrad (both B-operand paths) of the
@@ -186,9 +188,10 @@ def test_conv_big_tiles(gpu, case, tile, big_tiles, monkeypatch):
         assert rel_err(dxb.float(), xr.grad) < 1e-2
 
 
-@pytest.mark.parametrize("tile", [5, 6, 7])
+@pytest.mark.parametrize("tile", [5, 6, 7, 8])
 @pytest.mark.parametrize("det", [False, True])
-def test_conv_big_tiles_bn_stats(gpu, tile, det, big_tiles):
+@pytest.mark.parametrize("R", [3, 1])
+def test_conv_big_tiles_bn_stats(gpu, tile, det, R, big_tiles):
     import singa_amd
     from singa_amd.ops import functional as F
     singa_amd.set_deterministic(det)
@@ -196,12 +199,13 @@ def test_conv_big_tiles_bn_stats(gpu, tile, det, big_tiles):
         g = torch.Generator(device=gpu).manual_seed(2)
         x = torch.randn(8, 64, 28, 28, device=gpu, generator=g).bfloat16().contiguous(
             memory_format=torch.channels_last)
-        w = (torch.randn(192, 64, 3, 3, device=gpu, generator=g) * 0.05).bfloat16().contiguous(
+        w = (torch.randn(192, 64, R, R, device=gpu, generator=g) * 0.05).bfloat16().contiguous(
             memory_format=torch.channels_last)
+        pd = (R // 2, R // 2)
         big_tiles(tile)
-        y1 = F.conv2d_fwd(x, w, None, (1, 1), (1, 1), out_dtype=torch.bfloat16, bn_stats=True)
+        y1 = F.conv2d_fwd(x, w, None, (1, 1), pd, out_dtype=torch.bfloat16, bn_stats=True)
         big_tiles(0)
-        y2 = F.conv2d_fwd(x, w, None, (1, 1), (1, 1), out_dtype=torch.bfloat16)
+        y2 = F.conv2d_fwd(x, w, None, (1, 1), pd, out_dtype=torch.bfloat16)
         assert rel_err(y1.float(), y2.float()) < 1e-2
         gam, bet = torch.rand(192, device=gpu) + 0.5, torch.randn(192, device=gpu)
         outs = []
@@ -215,7 +219,7 @@ def test_conv_big_tiles_bn_stats(gpu, tile, det, big_tiles):
         assert rel_err(a, b) < 1e-3
 
 
-@pytest.mark.parametrize("tile", [5, 6, 7])
+@pytest.mark.parametrize("tile", [5, 6, 7, 8])
 @pytest.mark.parametrize("Nb,C,K,H,R,st", [(3, 64, 256, 14, 1, 1), (2, 128, 128, 15, 3, 2), (2, 96, 40, 9, 3, 1),
                                            (4, 256, 64, 7, 1, 2), (2, 8, 64, 33, 7, 2)])
 def test_conv_big_tiles_stay_in_bounds(gpu, Nb, C, K, H, R, st, tile, big_tiles):
@@ -248,7 +252,7 @@ def test_conv_big_tiles_stay_in_bounds(gpu, Nb, C, K, H, R, st, tile, big_tiles)
         chk("conv_dgrad")
 
 
-@pytest.mark.parametrize("tile", [5, 6, 7])
+@pytest.mark.parametrize("tile", [5, 6, 7, 8])
 @pytest.mark.parametrize("M,N,K,ak,bk", [(300, 200, 136, 0, 0), (513, 64, 96, 0, 1), (264, 384, 64, 1, 0),
                                          (1000, 136, 200, 1, 1)])
 def test_gemm_big_tiles(gpu, M, N, K, ak, bk, tile, big_tiles):

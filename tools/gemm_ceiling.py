@@ -51,16 +51,22 @@ def main():
     dev = torch.device("cuda", 0)
     for (M, K, Nn) in SHAPES:
         x = torch.randn(M, K, device=dev).bfloat16()
-        w = torch.randn(K, Nn, device=dev).bfloat16()
+        w = torch.randn(Nn, K, device=dev).bfloat16()  # [N][K]: both operands K-major (the 1x1-conv forward layout)
         flops = 2.0 * M * K * Nn
         byts = 2.0 * (M * K + K * Nn + M * Nn)
         rec = {"M": M, "K": K, "N": Nn}
+        ref = None
+        if M * Nn <= 300_000_000:
+            ref = (x[:4096].float() @ w.float().t())
         for pol in [int(v) for v in a.policies.split(",")]:
             L.set_tuning(4, pol)
-            us = timeit(lambda: F.matmul(x, w, out_dtype=torch.bfloat16))
+            us = timeit(lambda: F.gemm_nt(x, w, out_dtype=torch.bfloat16))
             rec[f"TF_p{pol}"] = round(flops / us / 1e6, 1)
+            if ref is not None:
+                out = F.gemm_nt(x, w, out_dtype=torch.bfloat16)[:4096].float()
+                rec[f"err_p{pol}"] = float((out - ref).norm() / ref.norm())
         L.set_tuning(4, 0)
-        us = timeit(lambda: x @ w)
+        us = timeit(lambda: x @ w.t())
         rec["TF_torch"] = round(flops / us / 1e6, 1)
         rec["roof_us"] = round(max(flops / 2.5e15, byts / 6.5e12) * 1e6, 1)
         print(json.dumps(rec), flush=True)

@@ -18,7 +18,7 @@ def main():
         for f in files:
             for r in csv.DictReader(open(f)):
                 k = r.get("Kernel_Name", "?")
-                if "igemm" not in k and "conv" not in k:
+                if "igemm" not in k and "conv" not in k and "gemm" not in k:
                     continue
                 agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
                 disp[k].add(r.get("Dispatch_Id", r.get("Correlation_Id", "")))

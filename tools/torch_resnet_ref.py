@@ -66,7 +66,16 @@ def main():
         loss.backward()
         opt.step()
         return loss
+    import os
     import sys
+    import threading
+
+    def heartbeat():  # MIOpen's first-call kernel search prints nothing for minutes at b1024
+        t0 = time.time()
+        while True:
+            time.sleep(30)
+            print(f"[yardstick] alive {time.time() - t0:.0f} s", file=sys.stderr, flush=True)
+    threading.Thread(target=heartbeat, daemon=True).start()
     for i in range(a.warmup):
         step()
         torch.cuda.synchronize()
@@ -79,7 +88,7 @@ def main():
     el = time.perf_counter() - t
     print(json.dumps({"yardstick": "pytorch-miopen resnet50 bf16 autocast channels_last", "images_per_s":
                       a.batch * a.steps / el, "ms_per_step": 1e3 * el / a.steps, "batch": a.batch,
-                      "torch": torch.__version__}))
+                      "torch": torch.__version__, "miopen_find_mode": os.environ.get("MIOPEN_FIND_MODE", "default")}))
 
 
 if __name__ == "__main__":
