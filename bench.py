@@ -37,10 +37,12 @@ def main() -> int:
                     help="per-GPU batch (1024 fits easily in 288 GB HBM3E; larger batches fill the 256 CUs better)")
     ap.add_argument("--depth", type=int, default=50)
     ap.add_argument("--image", type=int, default=224)
-    ap.add_argument("--graph", dest="graph", action="store_true", default=None,
-                    help="HIP-graph replay of forward+backward (default for 1 GPU)")
+    ap.add_argument("--graph", dest="graph", action="store_true", default=False,
+                    help="HIP-graph replay of the whole step (at batch 1024 measured 0.9%% slower than eager "
+                         "launch: profiles/r3/ab_graph_vs_eager.txt)")
     ap.add_argument("--no-graph", dest="graph", action="store_false",
-                    help="eager execution; the default for N>1, where bucketed all-reduces overlap the backward")
+                    help="eager execution (default, every N: each gradient bucket's all-reduce is forked onto "
+                         "the comm stream as soon as backward has produced it)")
     ap.add_argument("--loss-curve", action="store_true", help="record every step's loss (syncs; diagnostics only)")
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--sync-warmup", action="store_true", help="synchronize after every warmup step (diagnostics)")
@@ -84,11 +86,14 @@ def main() -> int:
     tx = tensor.from_numpy(x, dev)
     ty = tensor.from_numpy(y, dev)
 
-    # 1 GPU: graph replay (no launch overhead).  N>1: eager by default (each
-    # gradient bucket's RCCL all-reduce is forked onto the comm stream as soon
-    # as backward has produced it); --graph captures the whole step including
-    # the forked all-reduces (the native communicator is capture-safe).
-    use_graph = args.graph if args.graph is not None else world == 1
+    # Eager by default for every N (at batch 1024 the ~1000 launches of a
+    # step hide behind the kernels: eager measured 0.9 % faster than graph
+    # replay, profiles/r3/ab_graph_vs_eager.txt), so N = 1 and N > 1 time the
+    # same path; with N > 1 each gradient bucket's RCCL all-reduce is forked
+    # onto the comm stream as soon as backward has produced it.  --graph
+    # captures the whole step including the forked all-reduces (the native
+    # communicator is capture-safe).
+    use_graph = args.graph
     m.compile([tx], is_train=True, use_graph=use_graph)
     m.train()
 

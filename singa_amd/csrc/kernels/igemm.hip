@@ -98,6 +98,7 @@ struct GemmArgs {
   int stats_det;       // 1: row = tile row, plain stores (deterministic); 0: row = tile row % 32, atomics
   int xcd_split;       // split-K: K-slice-major XCD mapping (gridDim.z % 8 == 0, gridDim.y == 1)
   int early_issue;     // 2-stage loop: issue tile kt+1 before waiting for tile kt (two barriers per tile)
+  int nt_store;        // LDS-staged bf16 epilogue: non-temporal 16-byte output stores
   // stats_mode 1 (dgrad feeding a BN(+ReLU) backward): with g = out * [x*scale+shift > 0]
   // and xhat = (x - mean) * invstd, the epilogue sums (g, g*xhat) per channel
   // into `stats` -- the BN backward's reduction pass, fused
@@ -1035,7 +1036,8 @@ static int make_phases(ConvGeom& g) {
 // of pick_big at any size), 5 = 8-wave tiles for non-split launches (pick_big),
 // 6 = single-stage short-K variant for GEMMs of at most this many K-tiles
 // (0 = off), 7 = early DMA issue in the 2-stage loop (measured -3.5 % conv time)
-static int g_tune[8] = {5, 1, 1, 0, 0, 1, 2, 1};
+// 8 = non-temporal output stores in the LDS-staged bf16 epilogue
+static int g_tune[9] = {5, 1, 1, 0, 0, 1, 2, 1, 0};
 // one-shot: the next dgrad's wt scratch is already transposed.  Per OS
 // thread: the runtime's executor threads (hogwild / aggregated replicas)
 // each set and consume their own flag, so one thread's set can never be
@@ -1049,6 +1051,7 @@ static void launch_t(const GemmArgs& p_in, int tiles, int ydim, int zdim, hipStr
   GemmArgs p = p_in;
   p.lds_epilogue = g_tune[1];
   p.early_issue = g_tune[7];
+  p.nt_store = g_tune[8];
   p.xcd_split = (OUT == OUT_F32_ATOMIC && g_tune[2] && ydim == 1 && zdim >= 8 && (zdim & 7) == 0) ? 1 : 0;
   dim3 grid(tiles, ydim, zdim), block(NTH);
   constexpr int stages = STAGES * (BM + BN) * BK * 2;
@@ -1075,6 +1078,7 @@ template <int OUT>
 static void launch_pp(const GemmArgs& p_in, int tiles, int ydim, hipStream_t s) {
   GemmArgs p = p_in;
   p.lds_epilogue = g_tune[1];
+  p.nt_store = g_tune[8];
   constexpr int lds = 2 * PP_BUF;
   auto* kern = pp_gemm_k<OUT>;
   static bool attr = [kern] {
@@ -1503,7 +1507,7 @@ void sg_wt_transpose_batched(const void* desc, int n, int total, hipStream_t s) 
     hipLaunchKernelGGL(wt_transpose_batched_k, dim3(total), dim3(256), 0, s, (const WtDesc*)desc, n);
 }
 void sg_set_tuning(int key, int value) {
-  if (key >= 0 && key < 8) g_tune[key] = value;
+  if (key >= 0 && key < 9) g_tune[key] = value;
 }
 
 }  // extern "C"
