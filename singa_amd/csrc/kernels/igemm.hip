@@ -936,6 +936,201 @@ __global__ void __launch_bounds__(512, 2) pp_gemm_k(const GemmArgs p) {
   }
 }
 
+// ------------------------------------------------------------------------------
+// Persistent short-K GEMM for the 1x1-conv shapes (K <= 128, K-major A [M][K]
+// and B [N][K], bf16 output): C[M][N] = A B^T (+ beta C), optional fused BN
+// statistics.  igemm_k spends most of such a tile in its fixed parts (address
+// setup, the first operand fetch, the epilogue and the per-tile statistics
+// reduction: 7.2 VALU per MFMA, profiles/r3/pmc_gemm_200704x256x1024.txt).
+// Here one workgroup per CU keeps its 128-column slice of B resident in LDS and
+// walks the M-tiles tm = blockIdx.x, + gridDim.x, ...: the next tile's A is
+// DMA'd into the other ring slot while this tile computes, the tile's output is
+// staged as bf16 through LDS into 16-byte row stores whose completion overlaps
+// the next tile's MFMAs, and the BN statistics stay in registers across all of
+// the workgroup's tiles (one LDS reduction and one atomic per column at the end).
+// Measured (profiles/r3/sk_check.log, ab_persistent_short_k.jsonl): -5..+4 % on
+// the ResNet-50 1x1 shapes against igemm_k and neutral on the step -- the
+// short-K GEMMs sit at ~4.2 TB/s of combined traffic either way (hipBLASLt
+// too), not at a per-tile fixed cost -- so it stays opt-in (tuning knob 9).
+// ------------------------------------------------------------------------------
+constexpr int SK_TILE = 128 * BK * 2;             // one 128-row K-tile image (16 KB)
+constexpr int SK_LDT = 128 + 8;                   // bf16 staging row stride (+16 B)
+constexpr int SK_STG = 128 * SK_LDT * 2;          // output staging image
+constexpr int sk_lds(int kt) { return 3 * kt * SK_TILE + SK_STG; }
+
+template <int KT>
+__global__ void __launch_bounds__(256, 1) sk_gemm_k(const GemmArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int BM = 128, BN = 128, NTH = 256, WN = 2, WTM = 64, WTN = 64, TM = 4, TN = 4;
+  char* sB = smem;
+  char* sA = smem + KT * SK_TILE;
+  bf16* sC = (bf16*)(smem + 3 * KT * SK_TILE);
+  const int M = p.M, N = p.N, K = p.K;
+  const int tiles_m = (M + BM - 1) / BM;
+  const int n0 = blockIdx.y * BN;
+  int tm = blockIdx.x;
+  if (tm >= tiles_m) return;
+  const Phase& P = p.g.phs[0];
+  const int l = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+
+  Loader<BM, LM_KMAJOR, NTH> la;
+  Loader<BN, LM_KMAJOR, NTH> lb;
+  lb.init(p, n0, N, P, p.ldb, p.b, p.b_bytes);
+#pragma unroll
+  for (int kt = 0; kt < KT; ++kt) lb.issue(p, n0, N, kt * BK, K, P, sB + kt * SK_TILE);
+  la.init(p, tm * BM, M, P, p.lda, p.a, p.a_bytes);
+#pragma unroll
+  for (int kt = 0; kt < KT; ++kt) la.issue(p, tm * BM, M, kt * BK, K, P, sA + kt * SK_TILE);
+
+  int oa0[TM][2], oa1[TM][2], ob0[TN][2], ob1[TN][2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) la.frag_offsets(wm * WTM + i * 16, kk, oa0[i][kk], oa1[i][kk]);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) lb.frag_offsets(wn * WTN + j * 16, kk, ob0[j][kk], ob1[j][kk]);
+  }
+
+  // epilogue geometry: thread owns 8 columns (chunk ch) of rows r0 + 16 * pass
+  constexpr int CPRW = BN / 8, RPP = NTH / CPRW, NPS = BM / RPP;
+  const int ch = threadIdx.x % CPRW, r0 = threadIdx.x / CPRW;
+  const int n = n0 + ch * 8;
+  float st_s[8], st_q[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) { st_s[r] = 0.f; st_q[r] = 0.f; }
+
+  // Pipeline (per thread, in issue order): ... DMA A(it) | stores(it-2) |
+  // DMA A(it+1) | stores(it-1) ...; vector-memory operations retire in issue
+  // order, so "A(it) landed" is a counted wait that leaves the two younger
+  // tiles' stores and the next DMA in flight.  Every per-tile count is
+  // uniform: out-of-range rows go through buffer stores / loads that the
+  // resource drops, tiles past the end are DMA'd from a null resource.
+  constexpr int D = KT * Loader<BM, LM_KMAJOR, NTH>::VPT;  // DMA instructions per tile
+  const bool has_beta = p.beta != 0.f;
+  const __amdgpu_buffer_rsrc_t rnull = make_rsrc(nullptr, 0);
+  // the ring: A(it) lives in slot it & 1; the prologue issued A(0), A(1) follows
+  {
+    const int t1 = tm + (int)gridDim.x;
+    const bool live = t1 < tiles_m;
+    la.init(p, (live ? t1 : tm) * BM, M, P, p.lda, p.a, p.a_bytes);
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt) la.issue(p, t1 * BM, M, kt * BK, K, P, sA + (KT + kt) * SK_TILE, live);
+  }
+  for (int it = 0;; ++it) {
+    const int buf = it & 1;
+    if (it == 0) wait_vmcnt<D>();
+    else if (it == 1) {
+      if (has_beta) wait_vmcnt<2 * NPS + D>(); else wait_vmcnt<NPS + D>();
+    } else {
+      if (has_beta) wait_vmcnt<4 * NPS + D>(); else wait_vmcnt<2 * NPS + D>();
+    }
+    raw_barrier();  // A(it) landed for every wave; every wave is done with tile it-1
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt) {
+      const char* a_img = sA + (buf * KT + kt) * SK_TILE;
+      const char* b_img = sB + kt * SK_TILE;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8 fa[TM], fb[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) fa[i] = la.frag_at(a_img, oa0[i][kk], oa1[i][kk]);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) fb[j] = lb.frag_at(b_img, ob0[j][kk], ob1[j][kk]);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+      }
+    }
+    // acc -> bf16 staging
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int ml = wm * WTM + i * 16 + (l & 15);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int nl = wn * WTN + j * 16 + (l >> 4) * 4;
+        bf16x4 o;
+        o[0] = (bf16)acc[i][j][0]; o[1] = (bf16)acc[i][j][1]; o[2] = (bf16)acc[i][j][2]; o[3] = (bf16)acc[i][j][3];
+        *(bf16x4*)(sC + ml * SK_LDT + nl) = o;
+      }
+    }
+    raw_barrier();  // staging complete; every wave is done reading A(it)'s slot
+    // A(it+2) into the slot A(it) just left (null resource past the end)
+    const int t2 = tm + 2 * (int)gridDim.x;
+    {
+      const bool live = t2 < tiles_m;
+      la.init(p, (live ? t2 : tm) * BM, M, P, p.lda, p.a, p.a_bytes);
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt) la.issue(p, t2 * BM, M, kt * BK, K, P, sA + (buf * KT + kt) * SK_TILE, live);
+    }
+    // staging -> global: 16-byte buffer stores against this tile's row range
+    const int m0 = tm * BM;
+    const int rows = min(BM, M - m0);
+    const __amdgpu_buffer_rsrc_t rc =
+        n < N ? make_rsrc((const bf16*)p.c + (int64_t)m0 * p.ldc, (unsigned)((int64_t)rows * p.ldc * 2)) : rnull;
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 old[NPS];
+    if (has_beta) {
+#pragma unroll
+      for (int pass = 0; pass < NPS; ++pass)
+        old[pass] = __builtin_amdgcn_raw_buffer_load_b128(rc, (unsigned)(((r0 + pass * RPP) * (int)p.ldc + n) * 2), 0, 0);
+    }
+#pragma unroll
+    for (int pass = 0; pass < NPS; ++pass) {
+      const int ml = r0 + pass * RPP;
+      bf16x8 o = *(const bf16x8*)(sC + ml * SK_LDT + ch * 8);
+      if (has_beta) {
+        const bf16x8 ob = __builtin_bit_cast(bf16x8, old[pass]);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) o[r] = (bf16)((float)o[r] + p.beta * (float)ob[r]);
+      }
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rc, (unsigned)((ml * (int)p.ldc + n) * 2),
+                                             0, 0);
+      if (p.stats && ml < rows) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const float f = (float)o[r];
+          st_s[r] += f;
+          st_q[r] += f * f;
+        }
+      }
+    }
+    tm += (int)gridDim.x;
+    if (tm >= tiles_m) break;
+  }
+  wait_vmcnt<0>();
+  if (p.stats) {
+    // once per workgroup: the RPP row-threads of each 8-column chunk through
+    // LDS, then one atomic per column value into slot row blockIdx.x & 31
+    __syncthreads();
+    float* red = (float*)smem;  // [NTH][16]
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      red[threadIdx.x * 16 + r] = st_s[r];
+      red[threadIdx.x * 16 + 8 + r] = st_q[r];
+    }
+    __syncthreads();
+    if (threadIdx.x < CPRW * 16) {
+      const int c = threadIdx.x >> 4, r = threadIdx.x & 15;
+      const int nn = n0 + c * 8;
+      if (nn < N) {
+        float a = red[c * 16 + r];
+        for (int k = 1; k < RPP; ++k) a += red[(k * CPRW + c) * 16 + r];
+        const int col = r < 8 ? nn + r : N + nn + (r - 8);
+        atomicAdd(p.stats + (int64_t)(blockIdx.x & 31) * 2 * N + col, a);
+      }
+    }
+  }
+}
+
 // WT[t][c][k] = W[k][t][c] (bf16): per-tap [K][C] -> [C][K] through a 64x64
 // LDS tile (+1 column pad against bank conflicts), 256 threads.
 __global__ void __launch_bounds__(256) wt_transpose_k(const bf16* __restrict__ w, bf16* __restrict__ wt, int K,
@@ -1036,8 +1231,9 @@ static int make_phases(ConvGeom& g) {
 // of pick_big at any size), 5 = 8-wave tiles for non-split launches (pick_big),
 // 6 = single-stage short-K variant for GEMMs of at most this many K-tiles
 // (0 = off), 7 = early DMA issue in the 2-stage loop (measured -3.5 % conv time)
-// 8 = non-temporal output stores in the LDS-staged bf16 epilogue
-static int g_tune[9] = {5, 1, 1, 0, 0, 1, 2, 1, 0};
+// 8 = non-temporal output stores in the LDS-staged bf16 epilogue, 9 = persistent
+// short-K kernel for the 1x1-conv GEMM shapes (sk_gemm_k)
+static int g_tune[10] = {5, 1, 1, 0, 0, 1, 2, 1, 0, 0};
 // one-shot: the next dgrad's wt scratch is already transposed.  Per OS
 // thread: the runtime's executor threads (hogwild / aggregated replicas)
 // each set and consume their own flag, so one thread's set can never be
@@ -1086,6 +1282,22 @@ static void launch_pp(const GemmArgs& p_in, int tiles, int ydim, hipStream_t s) 
   }();
   (void)attr;
   hipLaunchKernelGGL(kern, dim3(tiles, ydim, 1), dim3(512), lds, s, p);
+}
+
+// persistent short-K launch: one workgroup per CU, gridDim.x a multiple of 8
+// (the workgroups of every column slice that share an M-tile sit on one XCD)
+template <int KT>
+static void launch_sk(const GemmArgs& p, int tiles_m, int tiles_n, hipStream_t s) {
+  constexpr int lds = sk_lds(KT);
+  auto* kern = sk_gemm_k<KT>;
+  static bool attr = [kern] {
+    return hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
+  }();
+  (void)attr;
+  int g = (256 + tiles_n - 1) / tiles_n;
+  g = (g + 7) / 8 * 8;
+  if (g > tiles_m) g = tiles_m;
+  hipLaunchKernelGGL(kern, dim3(g, tiles_n, 1), dim3(256), lds, s, p);
 }
 
 // 8-wave (512-thread) tiles.  Returns 0 (the 4-wave v2 tiles) or
@@ -1168,6 +1380,16 @@ static void launch(const GemmArgs& p, int M, int splits, hipStream_t s, int batc
   if constexpr (OUT != OUT_F32_ATOMIC) {
     {
       const int z = zdim > 0 ? zdim : 1;
+      // persistent short-K kernel (knob 9): 1x1-conv forward / data-gradient shapes
+      if (OUT == OUT_BF16 && AM == LM_KMAJOR && BMODE == LM_KMAJOR && g_tune[9] && g_tune[4] == 0 &&
+          !p.out_phase && zdim <= 1 && batch == 1 && p.K <= 128 && (p.N & 127) == 0 && !p.bias && !p.relu &&
+          p.alpha == 1.f && p.stats_mode == 0 && !(p.stats && p.stats_det) && g_tune[1] &&
+          (p.ldc & 7) == 0 && (long)((M + 127) / 128) * (p.N / 128) >= 2048) {
+        const int tiles_m = (M + 127) / 128;
+        if (p.K <= 64) launch_sk<1>(p, tiles_m, p.N / 128, s);
+        else launch_sk<2>(p, tiles_m, p.N / 128, s);
+        return;
+      }
       if (OUT == OUT_BF16 && g_tune[6] > 0 && g_tune[4] == 0 && p.beta == 0.f &&
           (p.K + BK - 1) / BK <= g_tune[6] && p.N >= 128 && !((p.N % 128) != 0 && (p.N % 128) <= 64) &&
           (long)((M + 127) / 128) * ((p.N + 127) / 128) >= 1024) {
@@ -1507,7 +1729,7 @@ void sg_wt_transpose_batched(const void* desc, int n, int total, hipStream_t s) 
     hipLaunchKernelGGL(wt_transpose_batched_k, dim3(total), dim3(256), 0, s, (const WtDesc*)desc, n);
 }
 void sg_set_tuning(int key, int value) {
-  if (key >= 0 && key < 9) g_tune[key] = value;
+  if (key >= 0 && key < 10) g_tune[key] = value;
 }
 
 }  // extern "C"

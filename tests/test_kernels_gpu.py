@@ -844,3 +844,51 @@ def test_colsum_accumulate(gpu, R, C, dtype):
     assert rel_err(out, ref) < 1e-5
     fresh, sq = F.colsum(x.to(gpu), with_sq=True)
     assert rel_err(fresh, x.float().sum(0)) < 1e-5 and rel_err(sq, (x.float() ** 2).sum(0)) < 1e-5
+
+
+@pytest.mark.parametrize("M,K,N", [(262145, 64, 128), (131075, 72, 256), (270000, 128, 128)])
+@pytest.mark.parametrize("beta", [0.0, 1.0])
+def test_gemm_persistent_short_k(gpu, M, K, N, beta):
+    """The persistent short-K kernel (knob 9: B resident in LDS, M-tiles walked
+    with a two-slot A ring, counted waits, buffer stores for the ragged last
+    tile) against fp32 torch, plain and accumulating (beta)."""
+    from singa_amd.ops import functional as F
+    from singa_amd.ops import native as NN
+    g = torch.Generator(device=gpu).manual_seed(11)
+    x = torch.randn(M, K, device=gpu, generator=g).bfloat16()
+    w = torch.randn(N, K, device=gpu, generator=g).bfloat16()
+    c0 = torch.randn(M, N, device=gpu, generator=g).bfloat16()
+    c = c0.clone()
+    NN.lib().set_tuning(9, 1)
+    try:
+        F.gemm(x, w, tb=True, out=c, beta=beta)
+    finally:
+        NN.lib().set_tuning(9, 0)
+    ref = x.float() @ w.float().t() + beta * c0.float()
+    assert rel_err(c, ref) < 5e-3
+    assert rel_err(c[-5:], ref[-5:]) < 5e-3  # the partial last M-tile
+
+
+def test_conv1x1_persistent_short_k_bn_stats(gpu):
+    """1x1 conv forward through the persistent kernel with the fused BN
+    statistics (kept in registers across the workgroup's tiles) equals the
+    default kernel's output and batch statistics."""
+    from singa_amd.ops import functional as F
+    from singa_amd.ops import native as NN
+    g = torch.Generator(device=gpu).manual_seed(3)
+    x = torch.randn(64, 64, 56, 56, device=gpu, generator=g).bfloat16().contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(256, 64, 1, 1, device=gpu, generator=g) * 0.1).bfloat16().contiguous(
+        memory_format=torch.channels_last)
+    res = []
+    for knob in (0, 1):
+        NN.lib().set_tuning(9, knob)
+        try:
+            y = F.conv2d_fwd(x, w, None, (1, 1), (0, 0), out_dtype=torch.bfloat16, bn_stats=True)
+            gam, bet = torch.ones(256, device=gpu), torch.zeros(256, device=gpu)
+            rm, rv = torch.zeros(256, device=gpu), torch.ones(256, device=gpu)
+            _, st = F.batchnorm_fwd(y, gam, bet, rm, rv, True, 0.1, 1e-5, relu=True)
+            res.append((y.float(), st.mean.clone(), st.invstd.clone()))
+        finally:
+            NN.lib().set_tuning(9, 0)
+    for a, b in zip(res[1], res[0]):
+        assert rel_err(a, b) < 1e-4
