@@ -138,7 +138,10 @@ def main() -> int:
         # timed region: it does not touch the images/s number
         from singa_amd.parallel import ps_parity
 
-        ps = ps_parity.run(comm, dev, iters=200, warmup=10)
+        try:
+            ps = ps_parity.run(comm, dev, iters=200, warmup=10)
+        except Exception as e:  # never lose the timed result to the side benchmark
+            ps = {"error": f"{type(e).__name__}: {e}"[:200]}
     if rank == 0:
         ips = world * B * args.steps / elapsed
         rec = {
@@ -164,7 +167,8 @@ def main() -> int:
             rec["config"]["loss_curve"] = curve
         if ps is not None:
             rec["ps_parity"] = {k: ps[k] for k in ("ms_per_iter", "algbw_GBps", "n_ranks",
-                                                   "speedup_vs_reference_1thread_1server", "note") if k in ps}
+                                                   "speedup_vs_reference_1thread_1server", "note", "error")
+                                if k in ps}
         print(json.dumps(rec), flush=True)
     if world > 1:
         comm.barrier()
