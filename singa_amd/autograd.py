@@ -684,6 +684,7 @@ class Conv2d(Operator):
         return y
 
     accepts_acc = True
+    wants_sole = True  # the identity-sum BN backward needs to be the producer's only consumer
 
     def backward(self, dy):
         x, w = self.x, self.w
@@ -699,9 +700,18 @@ class Conv2d(Operator):
         # reduction is fused into this dgrad's epilogue
         prod = self.src[0][0] if self.src else None
         bnp = None
+        wdot = False
         if (isinstance(prod, BatchNorm2d) and prod.relu and getattr(prod, "st", None) is not None
                 and getattr(prod, "x", None) is not None):
-            if acc is None and not prod.has_residual:
+            if (acc is None and not prod.has_residual and F.BN_WDOT and prod.st.mask is not None
+                    and (getattr(self, "sole", None) or {}).get(0, False)
+                    and getattr(prod, "beta", None) is not None and tgt is not None and self.group == 1
+                    and self.needs_grad(0) and tuple(self.dilation) == (1, 1)):
+                # identity-sum BN backward: this conv's dgrad sums the masked
+                # gradient and its wgrad <W, dW>; the BN skips its reduction
+                bnp = (prod.x, prod.st, prod.st.mask)
+                wdot = True
+            elif acc is None and not prod.has_residual:
                 bnp = (prod.x, prod.st)
             elif (acc is not None and prod.has_residual and prod.st.mask is not None
                   and (getattr(self, "acc_last", None) or {}).get(0, False)):
@@ -711,7 +721,7 @@ class Conv2d(Operator):
         tb = self.grad_target(2) if self.has_bias else None
         dx, dw, db = F.conv2d_bwd(x, w, dy, self.stride, self.padding, self.dilation, self.group,
                                   need_dx=self.needs_grad(0), dw_out=tgt, need_db=self.has_bias, dx_acc=acc,
-                                  bn_producer=bnp, wt_pre=wt_pre, db_out=tb)
+                                  bn_producer=bnp, wt_pre=wt_pre, db_out=tb, bn_wdot=wdot)
         if acc is not None and dx is acc:
             dx = ACC_INPLACE
         res = [dx, ACCUMULATED if tgt is not None else dw]
@@ -736,11 +746,14 @@ class BatchNorm2d(Operator):
     def forward(self, x, gamma, beta, res=None):
         # ReLU after a residual add: the mask cannot be recomputed from x, so
         # the forward writes it as bits (1/16 of re-reading the bf16 output)
-        want = self.requires_grad and self.relu and self.has_residual
+        # (and for the identity-sum backward, F.BN_WDOT: a consuming conv
+        # reads these bits instead of x to sum the masked gradient)
+        want = self.requires_grad and self.relu and (self.has_residual or (F.BN_WDOT and _training()))
         y, st = F.batchnorm_fwd(x, gamma, beta, self.rm, self.rv, _training(), self.momentum, self.eps, self.relu,
                                 res, want_mask=want)
         if self.requires_grad:
             self.x, self.gamma, self.st = x, gamma, st
+            self.beta = beta if F.BN_WDOT else None
             # the fused output is the ReLU mask only when a residual was added and no bit mask exists
             self.y = y if (want and st.mask is None) else None
         return y
@@ -748,8 +761,8 @@ class BatchNorm2d(Operator):
     def backward(self, dy):
         tg, tb = self.grad_target(1), self.grad_target(2)
         dx, dg, db, dres = F.batchnorm_bwd(self.x, dy, self.gamma, self.st, self.y, need_dres=self.has_residual,
-                                           relu=self.relu, dg_out=tg, db_out=tb)
-        self.x = self.y = self.st = None
+                                           relu=self.relu, dg_out=tg, db_out=tb, beta=getattr(self, "beta", None))
+        self.x = self.y = self.st = self.beta = None
         out = [dx, ACCUMULATED if tg is not None else dg, ACCUMULATED if tb is not None else db]
         if self.has_residual:
             out.append(dres)

@@ -106,6 +106,11 @@ void sg_conv_dgrad(const void*, const void*, void*, int, int, int, int, int, int
                    int, int, int, float, void*, hipStream_t);
 void sg_conv_wgrad(const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int, int,
                    int, int, int, hipStream_t);
+void sg_conv_wgrad_wdot(const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int,
+                        int, int, int, int, const void*, void*, hipStream_t);
+void sg_bn_bwd_wdot(const void*, const void*, const void*, const void*, const void*, const void*, const void*,
+                    const void*, const void*, const void*, const void*, void*, void*, void*, void*, void*, void*,
+                    int64_t, int, float, hipStream_t);
 void sg_ggemm(int, const void*, int64_t, int, int64_t, const void*, int64_t, int, int64_t, void*, int64_t, int64_t,
               int, int, int, float, float, const void*, int, int, int, int, hipStream_t);
 void sg_gconv_fwd(int, const void*, const void*, void*, const void*, int, int, int, int, int, int, int, int, int, int,
@@ -392,6 +397,20 @@ PYBIND11_MODULE(_C, m) {
     sg_bn_bwd_from_ws(CV(x), CV(dy), CV(y), CV(scale), CV(shift), CV(mean), CV(invstd), CV(gamma), CV(ws), nb, V(coef),
                       V(dg), V(db), V(dx), V(dres), R, C, mask_mode, dt, S(s));
     CHK("bn_bwd_from_ws");
+  });
+  // weight gradient that also accumulates wdot[c] += sum_{k,tap} W[k][tap][c] * dW[k][tap][c]
+  m.def("conv_wgrad_wdot", [](P x, P dy, P dw_out, int N, int H, int W, int C, int K, int R, int Sd, int Ho, int Wo,
+                              int sh, int sw, int ph, int pw, int dh, int dw, P wdot_w, P wdot_out, P s) {
+    sg_conv_wgrad_wdot(CV(x), CV(dy), V(dw_out), N, H, W, C, K, R, Sd, Ho, Wo, sh, sw, ph, pw, dh, dw, 0, CV(wdot_w),
+                       V(wdot_out), S(s));
+    CHK("conv_wgrad_wdot");
+  });
+  // BN(+ReLU) backward from the consuming conv's masked-gradient sums and <W, dW> (bf16, mask bits)
+  m.def("bn_bwd_wdot", [](P x, P dy, P mask, P scale, P shift, P mean, P invstd, P gamma, P beta, P ws1, P wdot,
+                          P ws2, P flag, P coef, P dg, P db, P dx, int64_t R, int C, float tau, P s) {
+    sg_bn_bwd_wdot(CV(x), CV(dy), CV(mask), CV(scale), CV(shift), CV(mean), CV(invstd), CV(gamma), CV(beta), CV(ws1),
+                   CV(wdot), V(ws2), V(flag), V(coef), V(dg), V(db), V(dx), R, C, tau, S(s));
+    CHK("bn_bwd_wdot");
   });
   m.def("set_ws_prezeroed", [](int on) { sg_set_ws_prezeroed(on); });
   m.def("zero", [](P p, int64_t bytes, P s) { sg_zero(V(p), bytes, S(s)); CHK("zero"); });

@@ -112,7 +112,11 @@ __global__ void __launch_bounds__(256) colpart_k(const T* __restrict__ x, const 
                                                  const T* __restrict__ x2 = nullptr,
                                                  const float* __restrict__ mean2 = nullptr,
                                                  const float* __restrict__ invstd2 = nullptr,
-                                                 float* __restrict__ ws2 = nullptr, const PoolG pg = PoolG{}) {
+                                                 float* __restrict__ ws2 = nullptr, const PoolG pg = PoolG{},
+                                                 const int* __restrict__ gate = nullptr) {
+  // gated launch (the identity-sum BN backward's exact fallback): nothing to
+  // do unless the gate is set
+  if (gate != nullptr && *gate == 0) return;
   // MODE 2 = MODE 1 plus a second BN fed the same gradient (the downsample
   // branch of a residual block): also p2 = sum g*xh2, into ws2 [band][2][C]
   // as (p0, p2) -- its own instantiation, the plain reduction is untouched
@@ -340,6 +344,49 @@ __global__ void bn_bwd_finalize_k(const float* __restrict__ ws, int nb, int C, c
   if (!band_sum(ws, nb, C, &c, &sdy, &sdyx)) return;
   float is = invstd[c];
   float k = (gamma ? gamma[c] : 1.f) * is;
+  float bcoef = -k * is * sdyx / count;
+  float acoef = -k * sdy / count - bcoef * mean[c];
+  coef[c] = k;
+  coef[C + c] = bcoef;
+  coef[2 * C + c] = acoef;
+  if (dg) dg[c] += sdyx;
+  if (db) db[c] += sdy;
+}
+
+// BN(+ReLU) backward of a BN whose output feeds ONE convolution and nothing
+// else, without a reduction pass over (dy, x): sdy = sum of the ReLU-masked
+// gradient comes from that conv's data-gradient epilogue (ws1: NSLOT slot
+// rows, first half); for sum(g~ * xhat), with y = relu(gamma*xhat + beta) the
+// conv input, g~ = dy*[y>0] and x_hat = (y - beta)/gamma wherever y > 0,
+//   sum_p g~ xhat = (sum_p dy*y - beta*sdy) / gamma,
+// and sum_p dy[p,c]*y[p,c] = sum_{k,taps} W[k,c,tap]*dW[k,c,tap] (the adjoint
+// of the convolution, padding included), accumulated per input channel by the
+// conv's weight-gradient epilogue into `wdot`.  The recovery divides by gamma:
+// bn_gamma_gate_k raises `flag` when any |gamma_c| < tau, and then the gated
+// exact reduction (colpart_k over dy, x and the mask bits, into ws2) runs and
+// the finalize uses its sums instead.
+__global__ void bn_gamma_gate_k(const float* __restrict__ gamma, const float* __restrict__ beta, int C, float tau,
+                                int* __restrict__ flag) {
+  // the recovered xhat carries y's bf16 rounding times |y| / |gamma| <= |xhat| + |beta / gamma|
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < C) {
+    const float g = fabsf(gamma[c]);
+    if (!(g >= tau && fabsf(beta[c]) <= 16.f * g)) *flag = 1;  // (NaN raises it too)
+  }
+}
+__global__ void bn_bwd_finalize_wdot_k(const float* __restrict__ ws1, const float* __restrict__ ws2, int nb, int C,
+                                       const float* __restrict__ gamma, const float* __restrict__ beta,
+                                       const float* __restrict__ wdot, const int* __restrict__ flag,
+                                       const float* __restrict__ mean, const float* __restrict__ invstd,
+                                       float* __restrict__ coef, float* __restrict__ dg, float* __restrict__ db,
+                                       float count) {
+  int c;
+  float sdy, sdyx;
+  const bool exact = *flag != 0;
+  if (!band_sum(exact ? ws2 : ws1, nb, C, &c, &sdy, &sdyx)) return;
+  if (!exact) sdyx = (wdot[c] - beta[c] * sdy) / gamma[c];
+  float is = invstd[c];
+  float k = gamma[c] * is;
   float bcoef = -k * is * sdyx / count;
   float acoef = -k * sdy / count - bcoef * mean[c];
   coef[c] = k;
@@ -870,6 +917,35 @@ void sg_bn_bwd2(const void* x, const void* dy, const void* mask, const void* mea
 
 // BN backward whose reduction was fused into the producing conv dgrad's
 // epilogue (sums in ws [nb][2][C]): finalize + apply only.
+// The identity-sum BN(+ReLU) backward (see bn_bwd_finalize_wdot_k): bf16,
+// C % 8 == 0, ReLU mask as the forward's bits, non-deterministic mode.
+// ws1: the dgrad epilogue's NSLOT slot rows; wdot [C]; ws2: NSLOT x 2 x C
+// scratch for the gated exact reduction; flag: one int of scratch.
+void sg_bn_bwd_wdot(const void* x, const void* dy, const void* mask, const void* scale, const void* shift,
+                    const void* mean, const void* invstd, const void* gamma, const void* beta, const void* ws1,
+                    const void* wdot, void* ws2, void* flag, void* coef, void* dg, void* db, void* dx, int64_t R,
+                    int C, float tau, hipStream_t s) {
+  sg_zero_async(flag, sizeof(int), s);
+  hipLaunchKernelGGL(bn_gamma_gate_k, dim3((C + 255) / 256), dim3(256), 0, s, (const float*)gamma, (const float*)beta, C,
+                     tau, (int*)flag);
+  dim3 grid;
+  int rpb, V;
+  colgrid(R, C, grid, rpb, V);
+  zero_ws(ws2, C, s);
+  hipLaunchKernelGGL((colpart_k<bf16, 1, 8>), grid, dim3(256), 0, s, (const bf16*)x, (const bf16*)dy,
+                     (const bf16*)mask, (const float*)scale, (const float*)shift, (const float*)mean,
+                     (const float*)invstd, (float*)ws2, R, C, rpb, (int)MASK_BITS, 0, (const bf16*)nullptr,
+                     (const float*)nullptr, (const float*)nullptr, (float*)nullptr, PoolG{}, (const int*)flag);
+  hipLaunchKernelGGL(bn_bwd_finalize_wdot_k, fin_grid(C), dim3(256), 0, s, (const float*)ws1, (const float*)ws2,
+                     NSLOT, C, (const float*)gamma, (const float*)beta, (const float*)wdot, (const int*)flag,
+                     (const float*)mean, (const float*)invstd, (float*)coef, (float*)dg, (float*)db, (float)R);
+  int64_t rpw;
+  dim3 ag = apply_grid(R, C, 8, rpw);
+  BN_UR_LAUNCH(bn_bwd_apply_k, g_bn_rpt ? 1 : 2, bf16, 8, ag, dim3(256), 0, s, (const bf16*)x, (const bf16*)dy,
+               (const bf16*)mask, (const float*)scale, (const float*)shift, (const float*)coef, (bf16*)dx,
+               (bf16*)nullptr, R, C, (int)MASK_BITS, rpw);
+}
+
 void sg_bn_bwd_from_ws(const void* x, const void* dy, const void* y, const void* scale, const void* shift,
                        const void* mean, const void* invstd, const void* gamma, const void* ws, int nb, void* coef,
                        void* dg, void* db, void* dx, void* dres, int64_t R, int C, int mask_mode, int dtype,

@@ -104,10 +104,16 @@ struct GemmArgs {
   // into `stats` -- the BN backward's reduction pass, fused
   // stats_mode 2: the same sums for a residual BN(+ReLU) whose ReLU mask is
   // the 1-bit map bnb_mask [rows][C/8] written by its forward apply
+  // stats_mode 3: only sum(g) over the mask bits (the identity-sum BN backward)
   int stats_mode;
   const uint8_t* bnb_mask;
   const bf16* bnb_x;
   const float *bnb_mean, *bnb_invstd, *bnb_scale, *bnb_shift;
+  // weight gradient (split-K atomic output): also sum_k W[k][col] * dW[k][col]
+  // per input channel col % wdot_C into wdot_out (W read with ldc)
+  const bf16* wdot_w;
+  float* wdot_out;
+  int wdot_C;
   ConvGeom g;
 };
 
@@ -1581,6 +1587,8 @@ void sg_conv_dgrad_bn(const void* dy, const void* w, void* dx, int N, int H, int
                       bn_mean, bn_invstd, bn_scale, bn_shift, nullptr, s);
 }
 
+// bn_mask != nullptr and bn_x == nullptr: the epilogue sums only the
+// ReLU-masked gradient (stats_mode 3, the identity-sum BN backward).
 // bn_mask != nullptr: the producer BN is a residual BN(+ReLU) whose ReLU mask
 // is its 1-bit map; beta may then be 1 (dx accumulates the other consumers'
 // gradient and the epilogue sums the partials of the FINAL value)
@@ -1594,7 +1602,7 @@ void sg_conv_dgrad_bn_ex(const void* dy, const void* w, void* dx, int N, int H, 
   if (bn_ws && out_mode == OUT_BF16 && (beta == 0.f || bn_mask) && (C & 7) == 0 && g_tune[1] &&
       !sg_bn_deterministic()) {
     p.stats = (float*)bn_ws;
-    p.stats_mode = bn_mask ? 2 : 1;
+    p.stats_mode = bn_mask ? (bn_x ? 2 : 3) : 1;
     p.bnb_mask = (const uint8_t*)bn_mask;
     p.bnb_x = (const bf16*)bn_x;
     p.bnb_mean = (const float*)bn_mean; p.bnb_invstd = (const float*)bn_invstd;
@@ -1652,11 +1660,27 @@ void sg_conv_dgrad_bn_ex(const void* dy, const void* w, void* dx, int N, int H, 
   else launch<LM_DGRAD_A, LM_DGRAD_B, OUT_BF16>(p, Mmax, 1, s, 1, np);
 }
 
+void sg_conv_wgrad_wdot(const void* x, const void* dy, void* dw_out, int N, int H, int W, int C, int K, int R, int S,
+                        int Ho, int Wo, int sh, int sw, int ph, int pw, int dh, int dw, int splits,
+                        const void* wdot_w, void* wdot_out, hipStream_t s);
+
 // conv weight gradient: dW[K][R*S*C] (fp32, accumulated atomically: the caller
 // zeroes it unless accumulating) += dy^T * im2col(x)
 void sg_conv_wgrad(const void* x, const void* dy, void* dw_out, int N, int H, int W, int C, int K, int R, int S,
                    int Ho, int Wo, int sh, int sw, int ph, int pw, int dh, int dw, int splits, hipStream_t s) {
+  sg_conv_wgrad_wdot(x, dy, dw_out, N, H, W, C, K, R, S, Ho, Wo, sh, sw, ph, pw, dh, dw, splits, nullptr, nullptr, s);
+}
+
+// ... and with wdot_w (the forward's bf16 weights, [K][R*S*C]) != nullptr,
+// wdot_out[c] += sum_{k, taps} W[k][tap][c] * dW[k][tap][c] (the identity-sum
+// BN backward of the BN(+ReLU) producing x)
+void sg_conv_wgrad_wdot(const void* x, const void* dy, void* dw_out, int N, int H, int W, int C, int K, int R, int S,
+                        int Ho, int Wo, int sh, int sw, int ph, int pw, int dh, int dw, int splits,
+                        const void* wdot_w, void* wdot_out, hipStream_t s) {
   GemmArgs p{};
+  p.wdot_w = (const bf16*)wdot_w;
+  p.wdot_out = (float*)wdot_out;
+  p.wdot_C = C;
   p.g = make_geom(N, H, W, C, K, R, S, Ho, Wo, sh, sw, ph, pw, dh, dw);
   p.M = K; p.N = R * S * C; p.K = N * Ho * Wo;
   p.a = (const bf16*)dy; p.lda = K; p.b = (const bf16*)x; p.ldb = 0;

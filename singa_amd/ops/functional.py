@@ -887,6 +887,12 @@ FUSE_BN_BWD_STATS = os.environ.get("SINGA_AMD_FUSE_BN_BWD", "0") == "1"
 # read in the epilogue of these one/two-K-tile GEMMs costs what the separate
 # reduction pass costs, profiles/dgrad_bn_fusion_b1024.jsonl), so off by default
 FUSE_RES_BN_BWD = os.environ.get("SINGA_AMD_FUSE_RES_BN_BWD", "0") == "1"
+# Identity-sum BN backward (bn_bwd_finalize_wdot_k, batchnorm.hip): a
+# BN(+ReLU) whose output feeds exactly one conv skips its reduction pass;
+# sum(g~) comes from that conv's dgrad epilogue (mask bits) and sum(g~ xhat)
+# from <W, dW> of its weight gradient
+BN_WDOT = os.environ.get("SINGA_AMD_BN_WDOT", "0") == "1"
+BN_WDOT_TAU = 0.05  # |gamma| below this (or |beta| > 16 |gamma|): the exact reduction runs instead
 
 
 _WT_CACHE: dict = {}
@@ -946,7 +952,7 @@ def pretranspose_conv_weights(items) -> dict:
 def conv2d_bwd(x: torch.Tensor, w: torch.Tensor, dy: torch.Tensor, stride, padding, dilation=(1, 1), groups=1,
                need_dx=True, dw_out: Optional[torch.Tensor] = None, need_db=False,
                dx_acc: Optional[torch.Tensor] = None, bn_producer=None, wt_pre: Optional[torch.Tensor] = None,
-               db_out: Optional[torch.Tensor] = None):
+               db_out: Optional[torch.Tensor] = None, bn_wdot: bool = False):
     """Returns (dx, dw, db).  If dw_out (fp32, same logical shape as w) is given
     the weight gradient is ACCUMULATED into it (flat grad buffer views); the
     same for the bias gradient with ``db_out`` (fp32 [K]).
@@ -1021,6 +1027,20 @@ def conv2d_bwd(x: torch.Tensor, w: torch.Tensor, dy: torch.Tensor, stride, paddi
                     N.lib().conv_dgrad_acc(dyb.data_ptr(), wb.data_ptr(), dx_acc.data_ptr(), Nn, H, W, Cp, Kp, R, S,
                                            Ho, Wo, sh, sw, ph, pw, dh, dw_, om, 1.0, N.stream(), N.ptr(wt))
                 dx = dx_acc
+            elif (bn_wdot and bn_producer is not None and od == torch.bfloat16 and Cx == Cp and C % 8 == 0
+                  and not padded and not N.lib().deterministic() and x.dtype == torch.bfloat16):
+                # identity-sum BN backward of the producer BN(+ReLU): this
+                # dgrad's epilogue sums the masked gradient (mask bits only)
+                bmask = bn_producer[2]
+                dxp = torch.empty((Nn, Cp, H, W), dtype=od, device=x.device, memory_format=torch.channels_last)
+                bws = zeroed_ws(32 * 2 * C, x.device)
+                N.lib().conv_dgrad_bn(dyb.data_ptr(), wb.data_ptr(), dxp.data_ptr(), Nn, H, W, Cp, Kp, R, S, Ho, Wo,
+                                      sh, sw, ph, pw, dh, dw_, N.ptr(wt), bws.data_ptr(), 0, 0, 0, 0, 0, N.stream(),
+                                      0.0, bmask.data_ptr())
+                wdot = G.zeros((C,), torch.float32, x.device)
+                dxp._sg_bnbwd_wdot = (bws, wdot, wb)
+                dxp._sg_fresh = True
+                dx = dxp
             elif (bn_producer is not None and FUSE_BN_BWD_STATS and od == torch.bfloat16 and Cx == Cp and C % 8 == 0
                   and not N.lib().deterministic() and bn_producer[0].dtype == torch.bfloat16
                   and tuple(bn_producer[0].shape) == tuple(x.shape) and N.is_cl(bn_producer[0])
@@ -1046,8 +1066,13 @@ def conv2d_bwd(x: torch.Tensor, w: torch.Tensor, dy: torch.Tensor, stride, paddi
         # weight gradient, fp32 [Kp][R][S][Cp]
         direct = (dw_out is not None and not padded and dw_out.dtype == torch.float32 and N.is_cl(dw_out))
         target = dw_out if direct else _zeros_cl((Kp, Cp, R, S), torch.float32, x.device)
-        N.lib().conv_wgrad(xb.data_ptr(), dyb.data_ptr(), target.data_ptr(), Nn, H, W, Cp, Kp, R, S, Ho, Wo, sh, sw,
-                           ph, pw, dh, dw_, 0, N.stream())
+        wd = getattr(dx, "_sg_bnbwd_wdot", None) if dx is not None else None
+        if wd is not None:  # ... and its weight gradient accumulates <W, dW> per input channel
+            N.lib().conv_wgrad_wdot(xb.data_ptr(), dyb.data_ptr(), target.data_ptr(), Nn, H, W, Cp, Kp, R, S, Ho, Wo,
+                                    sh, sw, ph, pw, dh, dw_, wd[2].data_ptr(), wd[1].data_ptr(), N.stream())
+        else:
+            N.lib().conv_wgrad(xb.data_ptr(), dyb.data_ptr(), target.data_ptr(), Nn, H, W, Cp, Kp, R, S, Ho, Wo, sh,
+                               sw, ph, pw, dh, dw_, 0, N.stream())
         if direct:
             dwt = dw_out
         else:
@@ -1431,7 +1456,8 @@ def dual_bn_add_relu_bwd(x, dy, gamma, st: BNState, x2, gamma2, st2: BNState, dg
 
 def batchnorm_bwd(x: torch.Tensor, dy: torch.Tensor, gamma: torch.Tensor, st: BNState,
                   y_for_mask: Optional[torch.Tensor] = None, need_dres: bool = False, relu: bool = False,
-                  dg_out: Optional[torch.Tensor] = None, db_out: Optional[torch.Tensor] = None):
+                  dg_out: Optional[torch.Tensor] = None, db_out: Optional[torch.Tensor] = None,
+                  beta: Optional[torch.Tensor] = None):
     """Returns dx, dgamma, dbeta, dres.  ReLU mask: from ``y_for_mask`` (the
     fused output, required when a residual was added) or, with ``relu`` and no
     residual, recomputed from x*scale+shift.  dgamma/dbeta are accumulated
@@ -1456,6 +1482,17 @@ def batchnorm_bwd(x: torch.Tensor, dy: torch.Tensor, gamma: torch.Tensor, st: BN
         coef = torch.empty(3 * C, dtype=torch.float32, device=x.device)
         dx = _like(x)
         dres = _like(x) if need_dres else None
+        wdot = getattr(dy, "_sg_bnbwd_wdot", None)  # identity-sum inputs from the consuming conv
+        if (wdot is not None and mode == 3 and not need_dres and beta is not None and x.dtype == torch.bfloat16
+                and C % 8 == 0 and dy.dtype == torch.bfloat16):
+            ws2 = zeroed_ws(32 * 2 * C, x.device)
+            flag = torch.empty(1, dtype=torch.int32, device=x.device)
+            L.bn_bwd_wdot(x.data_ptr(), dy.data_ptr(), ym.data_ptr(), st.scale.data_ptr(), st.shift.data_ptr(),
+                          st.mean.data_ptr(), st.invstd.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
+                          wdot[0].data_ptr(), wdot[1].data_ptr(), ws2.data_ptr(), flag.data_ptr(), coef.data_ptr(),
+                          dg.data_ptr(), db.data_ptr(), dx.data_ptr(), R, C, BN_WDOT_TAU, N.stream())
+            dx._sg_fresh = True
+            return dx, dg, db, None
         pre = getattr(dy, "_sg_bnbwd_ws", None)  # partial sums from the consuming conv's dgrad epilogue
         if pre is not None and ((mode == 2 and not need_dres) or mode == 3):
             L.bn_bwd_from_ws(x.data_ptr(), dy.data_ptr(), N.ptr(ym) if mode == 3 else 0, st.scale.data_ptr(),

@@ -709,3 +709,65 @@ def test_lrn_folds_conv_relu_backward(gpu, monkeypatch):
         assert s0 == s1
         # bf16 operands, split-K fp32 atomics: an element near zero may differ by a bf16 ulp of its terms
         torch.testing.assert_close(g1, g0, rtol=1e-2, atol=5e-3)
+
+
+@pytest.mark.parametrize("small_gamma", [False, True])
+def test_bn_identity_sum_backward_matches_reduction(gpu, small_gamma):
+    """Identity-sum BN backward (F.BN_WDOT): a BN(+ReLU) whose output feeds one
+    conv takes sum(g~) from that conv's dgrad epilogue and sum(g~ xhat) from
+    <W, dW> of its weight gradient instead of a reduction pass.  Three stacked
+    bottlenecks (stride 1 and 2, 1x1 and 3x3 consumers) A/B against the
+    reduction path: every parameter gradient and the input gradient agree to
+    bf16 rounding.  small_gamma: some bn1/bn2 channels get |gamma| < tau, which
+    must switch those layers to the gated exact reduction."""
+    from singa_amd import autograd as AG
+    from singa_amd.models.resnet import Bottleneck
+    from singa_amd.ops import functional as FF
+
+    dev = device.create_rocm_gpu()
+    dev.SetRandSeed(4)
+    cfg = [(16, 1, True), (16, 2, True), (16, 1, False)]
+    blks = [Bottleneck(pl, st, dn) for pl, st, dn in cfg]
+    g = torch.Generator(device=gpu).manual_seed(6)
+    xf = torch.randn(8, 32, 16, 16, device=gpu, generator=g)
+    dyt = None
+    wdot0 = FF.BN_WDOT
+
+    def run(on):
+        nonlocal dyt
+        FF.BN_WDOT = on
+        AG.training = True
+        x = Tensor(data=xf.bfloat16().contiguous(memory_format=torch.channels_last), device=dev, requires_grad=True,
+                   stores_grad=False)
+        try:
+            h = x
+            for b in blks:
+                h = b(h)
+            if dyt is None:
+                dyt = torch.randn(h.shape, device=gpu, generator=g)
+            loss_t = AG.reduce_sum(AG.mul(h, Tensor(data=dyt.bfloat16().contiguous(
+                memory_format=torch.channels_last), device=dev, requires_grad=False)), None)
+            gr = {id(p): gg.data.float().clone() for p, gg in AG.backward(loss_t)}
+        finally:
+            AG.training = False
+            FF.BN_WDOT = wdot0
+        return h, gr
+
+    if small_gamma:
+        for b in blks:
+            for k, p in b.get_params().items():
+                if k in ("bn1.scale", "bn2.scale"):
+                    p.data[::3] = 1e-3
+    saved = {id(p): p.data.clone() for b in blks for p in b.get_params().values()}
+    h1, g_on = run(True)
+    for b in blks:
+        for p in b.get_params().values():
+            p.data.copy_(saved[id(p)])
+    h0, g_off = run(False)
+    assert torch.equal(h1.data, h0.data)
+    ab = {}
+    for i, b in enumerate(blks):
+        for k, p in b.get_params().items():
+            ab[f"{i}.{k}"] = rel_err(g_on[id(p)], g_off[id(p)])
+    print(ab)
+    assert max(ab.values()) < (1e-3 if small_gamma else 3e-2), ab
