@@ -62,6 +62,11 @@ class _AutogradModule(types.ModuleType):
 sys.modules[__name__].__class__ = _AutogradModule
 
 ACCUMULATED = object()  # backward() returned: grad already added to the param's grad_view
+# ParamStore.zero_grad() bumps GRAD_EPOCH; a conv records the epoch in which it
+# last added to its weight gradient (the identity-sum BN backward needs that
+# gradient to hold this backward's contribution only)
+GRAD_EPOCH = [0]
+_WGRAD_EPOCH: dict = {}
 # backward() returned: the input gradient was added IN PLACE into the partial
 # gradient the engine offered through ``op.acc_into`` (see backward())
 ACC_INPLACE = object()
@@ -705,7 +710,8 @@ class Conv2d(Operator):
                 and getattr(prod, "x", None) is not None):
             if (acc is None and not prod.has_residual and F.BN_WDOT and prod.st.mask is not None
                     and (getattr(self, "sole", None) or {}).get(0, False)
-                    and getattr(prod, "beta", None) is not None and tgt is not None and self.group == 1
+                    and (tgt is None or _WGRAD_EPOCH.get(id(self.params[1])) != GRAD_EPOCH[0])
+                    and getattr(prod, "beta", None) is not None and self.group == 1
                     and self.needs_grad(0) and tuple(self.dilation) == (1, 1)):
                 # identity-sum BN backward: this conv's dgrad sums the masked
                 # gradient and its wgrad <W, dW>; the BN skips its reduction
@@ -722,6 +728,8 @@ class Conv2d(Operator):
         dx, dw, db = F.conv2d_bwd(x, w, dy, self.stride, self.padding, self.dilation, self.group,
                                   need_dx=self.needs_grad(0), dw_out=tgt, need_db=self.has_bias, dx_acc=acc,
                                   bn_producer=bnp, wt_pre=wt_pre, db_out=tb, bn_wdot=wdot)
+        if tgt is not None:
+            _WGRAD_EPOCH[id(self.params[1])] = GRAD_EPOCH[0]  # this step's weight gradient is no longer empty
         if acc is not None and dx is acc:
             dx = ACC_INPLACE
         res = [dx, ACCUMULATED if tgt is not None else dw]

@@ -106,8 +106,7 @@ void sg_conv_dgrad(const void*, const void*, void*, int, int, int, int, int, int
                    int, int, int, float, void*, hipStream_t);
 void sg_conv_wgrad(const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int, int,
                    int, int, int, hipStream_t);
-void sg_conv_wgrad_wdot(const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int,
-                        int, int, int, int, const void*, void*, hipStream_t);
+void sg_wdot_colsum(const void*, const void*, int, int, float, void*, int, hipStream_t);
 void sg_bn_bwd_wdot(const void*, const void*, const void*, const void*, const void*, const void*, const void*,
                     const void*, const void*, const void*, const void*, void*, void*, void*, void*, void*, void*,
                     int64_t, int, float, hipStream_t);
@@ -398,12 +397,10 @@ PYBIND11_MODULE(_C, m) {
                       V(dg), V(db), V(dx), V(dres), R, C, mask_mode, dt, S(s));
     CHK("bn_bwd_from_ws");
   });
-  // weight gradient that also accumulates wdot[c] += sum_{k,tap} W[k][tap][c] * dW[k][tap][c]
-  m.def("conv_wgrad_wdot", [](P x, P dy, P dw_out, int N, int H, int W, int C, int K, int R, int Sd, int Ho, int Wo,
-                              int sh, int sw, int ph, int pw, int dh, int dw, P wdot_w, P wdot_out, P s) {
-    sg_conv_wgrad_wdot(CV(x), CV(dy), V(dw_out), N, H, W, C, K, R, Sd, Ho, Wo, sh, sw, ph, pw, dh, dw, 0, CV(wdot_w),
-                       V(wdot_out), S(s));
-    CHK("conv_wgrad_wdot");
+  // wdot[c] += sign * sum_rows W[row][c] * dW[row][c] (KRSC filter as [rows][C])
+  m.def("wdot_colsum", [](P w, P dw, int rows, int C, float sign, P wdot, int zero_first, P s) {
+    sg_wdot_colsum(CV(w), CV(dw), rows, C, sign, V(wdot), zero_first, S(s));
+    CHK("wdot_colsum");
   });
   // BN(+ReLU) backward from the consuming conv's masked-gradient sums and <W, dW> (bf16, mask bits)
   m.def("bn_bwd_wdot", [](P x, P dy, P mask, P scale, P shift, P mean, P invstd, P gamma, P beta, P ws1, P wdot,

@@ -109,11 +109,6 @@ struct GemmArgs {
   const uint8_t* bnb_mask;
   const bf16* bnb_x;
   const float *bnb_mean, *bnb_invstd, *bnb_scale, *bnb_shift;
-  // weight gradient (split-K atomic output): also sum_k W[k][col] * dW[k][col]
-  // per input channel col % wdot_C into wdot_out (W read with ldc)
-  const bf16* wdot_w;
-  float* wdot_out;
-  int wdot_C;
   ConvGeom g;
 };
 
@@ -1137,6 +1132,27 @@ __global__ void __launch_bounds__(256, 1) sk_gemm_k(const GemmArgs p) {
   }
 }
 
+// wdot[c] += sign * sum_rows W[row][c] * dW[row][c] over a [rows][C] weight
+// (rows = K*R*S of a KRSC filter): the <W, dW> input-channel sums of the
+// identity-sum BN backward (batchnorm.hip, bn_bwd_finalize_wdot_k).  Block =
+// 64 channels x 4 row lanes, WDOT_RB rows per block, one atomic per channel.
+constexpr int WDOT_RB = 64;
+__global__ void __launch_bounds__(256) wdot_colsum_k(const bf16* __restrict__ w, const float* __restrict__ dw,
+                                                     int rows, int C, float sign, float* __restrict__ wdot) {
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, lane = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  const int r0 = blockIdx.y * WDOT_RB;
+  float a = 0.f;
+  if (c < C) {
+    const int r1 = min(rows, r0 + WDOT_RB);
+    for (int r = r0 + lane; r < r1; r += 4) a += (float)w[(int64_t)r * C + c] * dw[(int64_t)r * C + c];
+  }
+  red[lane][cl] = a;
+  __syncthreads();
+  if (lane == 0 && c < C) atomicAdd(wdot + c, sign * (red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl]));
+}
+
 // WT[t][c][k] = W[k][t][c] (bf16): per-tap [K][C] -> [C][K] through a 64x64
 // LDS tile (+1 column pad against bank conflicts), 256 threads.
 __global__ void __launch_bounds__(256) wt_transpose_k(const bf16* __restrict__ w, bf16* __restrict__ wt, int K,
@@ -1660,27 +1676,11 @@ void sg_conv_dgrad_bn_ex(const void* dy, const void* w, void* dx, int N, int H, 
   else launch<LM_DGRAD_A, LM_DGRAD_B, OUT_BF16>(p, Mmax, 1, s, 1, np);
 }
 
-void sg_conv_wgrad_wdot(const void* x, const void* dy, void* dw_out, int N, int H, int W, int C, int K, int R, int S,
-                        int Ho, int Wo, int sh, int sw, int ph, int pw, int dh, int dw, int splits,
-                        const void* wdot_w, void* wdot_out, hipStream_t s);
-
 // conv weight gradient: dW[K][R*S*C] (fp32, accumulated atomically: the caller
 // zeroes it unless accumulating) += dy^T * im2col(x)
 void sg_conv_wgrad(const void* x, const void* dy, void* dw_out, int N, int H, int W, int C, int K, int R, int S,
                    int Ho, int Wo, int sh, int sw, int ph, int pw, int dh, int dw, int splits, hipStream_t s) {
-  sg_conv_wgrad_wdot(x, dy, dw_out, N, H, W, C, K, R, S, Ho, Wo, sh, sw, ph, pw, dh, dw, splits, nullptr, nullptr, s);
-}
-
-// ... and with wdot_w (the forward's bf16 weights, [K][R*S*C]) != nullptr,
-// wdot_out[c] += sum_{k, taps} W[k][tap][c] * dW[k][tap][c] (the identity-sum
-// BN backward of the BN(+ReLU) producing x)
-void sg_conv_wgrad_wdot(const void* x, const void* dy, void* dw_out, int N, int H, int W, int C, int K, int R, int S,
-                        int Ho, int Wo, int sh, int sw, int ph, int pw, int dh, int dw, int splits,
-                        const void* wdot_w, void* wdot_out, hipStream_t s) {
   GemmArgs p{};
-  p.wdot_w = (const bf16*)wdot_w;
-  p.wdot_out = (float*)wdot_out;
-  p.wdot_C = C;
   p.g = make_geom(N, H, W, C, K, R, S, Ho, Wo, sh, sw, ph, pw, dh, dw);
   p.M = K; p.N = R * S * C; p.K = N * Ho * Wo;
   p.a = (const bf16*)dy; p.lda = K; p.b = (const bf16*)x; p.ldb = 0;
@@ -1746,6 +1746,14 @@ int sg_conv_stats_rows(int M, int N) {
 }
 
 void sg_set_wt_ready(int on) { g_wt_ready = on; }
+// wdot[c] += sign * sum_rows W[row][c] dW[row][c] (zeroes wdot first unless the
+// one-shot pre-zeroed flag is set and sign > 0 ... callers pass zero_first)
+void sg_wdot_colsum(const void* w, const void* dw, int rows, int C, float sign, void* wdot, int zero_first,
+                    hipStream_t s) {
+  if (zero_first && !sg_ws_prezeroed()) sg_zero_async(wdot, sizeof(float) * C, s);
+  hipLaunchKernelGGL(wdot_colsum_k, dim3((C + 63) / 64, (rows + WDOT_RB - 1) / WDOT_RB), dim3(256), 0, s,
+                     (const bf16*)w, (const float*)dw, rows, C, sign, (float*)wdot);
+}
 // desc: n WtDesc entries in device memory (32 bytes each), total = sum of tiles
 void sg_wt_transpose_batched(const void* desc, int n, int total, hipStream_t s) {
   static_assert(sizeof(WtDesc) == 32, "descriptor layout shared with the Python packer");

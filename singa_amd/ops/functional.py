@@ -891,7 +891,7 @@ FUSE_RES_BN_BWD = os.environ.get("SINGA_AMD_FUSE_RES_BN_BWD", "0") == "1"
 # BN(+ReLU) whose output feeds exactly one conv skips its reduction pass;
 # sum(g~) comes from that conv's dgrad epilogue (mask bits) and sum(g~ xhat)
 # from <W, dW> of its weight gradient
-BN_WDOT = os.environ.get("SINGA_AMD_BN_WDOT", "0") == "1"
+BN_WDOT = os.environ.get("SINGA_AMD_BN_WDOT", "1") == "1"
 BN_WDOT_TAU = 0.05  # |gamma| below this (or |beta| > 16 |gamma|): the exact reduction runs instead
 
 
@@ -1037,8 +1037,7 @@ def conv2d_bwd(x: torch.Tensor, w: torch.Tensor, dy: torch.Tensor, stride, paddi
                 N.lib().conv_dgrad_bn(dyb.data_ptr(), wb.data_ptr(), dxp.data_ptr(), Nn, H, W, Cp, Kp, R, S, Ho, Wo,
                                       sh, sw, ph, pw, dh, dw_, N.ptr(wt), bws.data_ptr(), 0, 0, 0, 0, 0, N.stream(),
                                       0.0, bmask.data_ptr())
-                wdot = G.zeros((C,), torch.float32, x.device)
-                dxp._sg_bnbwd_wdot = (bws, wdot, wb)
+                dxp._sg_bnbwd_wdot = (bws, None, wb)
                 dxp._sg_fresh = True
                 dx = dxp
             elif (bn_producer is not None and FUSE_BN_BWD_STATS and od == torch.bfloat16 and Cx == Cp and C % 8 == 0
@@ -1066,13 +1065,16 @@ def conv2d_bwd(x: torch.Tensor, w: torch.Tensor, dy: torch.Tensor, stride, paddi
         # weight gradient, fp32 [Kp][R][S][Cp]
         direct = (dw_out is not None and not padded and dw_out.dtype == torch.float32 and N.is_cl(dw_out))
         target = dw_out if direct else _zeros_cl((Kp, Cp, R, S), torch.float32, x.device)
+        N.lib().conv_wgrad(xb.data_ptr(), dyb.data_ptr(), target.data_ptr(), Nn, H, W, Cp, Kp, R, S, Ho, Wo, sh, sw,
+                           ph, pw, dh, dw_, 0, N.stream())
         wd = getattr(dx, "_sg_bnbwd_wdot", None) if dx is not None else None
-        if wd is not None:  # ... and its weight gradient accumulates <W, dW> per input channel
-            N.lib().conv_wgrad_wdot(xb.data_ptr(), dyb.data_ptr(), target.data_ptr(), Nn, H, W, Cp, Kp, R, S, Ho, Wo,
-                                    sh, sw, ph, pw, dh, dw_, wd[2].data_ptr(), wd[1].data_ptr(), N.stream())
-        else:
-            N.lib().conv_wgrad(xb.data_ptr(), dyb.data_ptr(), target.data_ptr(), Nn, H, W, Cp, Kp, R, S, Ho, Wo, sh,
-                               sw, ph, pw, dh, dw_, 0, N.stream())
+        if wd is not None:
+            # <W, dW> per input channel over the finished weight gradient (the
+            # caller guarantees it held nothing else before this backward)
+            wdot = zeroed_ws(C, x.device)
+            N.lib().wdot_colsum(wd[2].data_ptr(), target.data_ptr(), Kp * R * S, C, 1.0, wdot.data_ptr(), 1,
+                                N.stream())
+            dx._sg_bnbwd_wdot = (wd[0], wdot)
         if direct:
             dwt = dw_out
         else:

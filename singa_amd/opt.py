@@ -195,6 +195,7 @@ class ParamStore:
 
     def zero_grad(self):
         G.zero_(self.g)
+        autograd.GRAD_EPOCH[0] += 1
 
     def sync_low(self):
         if self.low is not None:
