@@ -715,7 +715,7 @@ class Conv2d(Operator):
                     and self.needs_grad(0) and tuple(self.dilation) == (1, 1)):
                 # identity-sum BN backward: this conv's dgrad sums the masked
                 # gradient and its wgrad <W, dW>; the BN skips its reduction
-                bnp = (prod.x, prod.st, prod.st.mask)
+                bnp = (prod.x, prod.st, prod.st.mask, prod.gamma, prod.beta)
                 wdot = True
             elif acc is None and not prod.has_residual:
                 bnp = (prod.x, prod.st)

@@ -106,7 +106,8 @@ void sg_conv_dgrad(const void*, const void*, void*, int, int, int, int, int, int
                    int, int, int, float, void*, hipStream_t);
 void sg_conv_wgrad(const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int, int,
                    int, int, int, hipStream_t);
-void sg_wdot_colsum(const void*, const void*, int, int, float, void*, int, hipStream_t);
+void sg_wdot_colsum(const void*, const void*, int, int, float, void*, int, const void*, const void*, float,
+                    hipStream_t);
 void sg_bn_bwd_wdot(const void*, const void*, const void*, const void*, const void*, const void*, const void*,
                     const void*, const void*, const void*, const void*, void*, void*, void*, void*, void*, void*,
                     int64_t, int, float, hipStream_t);
@@ -398,8 +399,9 @@ PYBIND11_MODULE(_C, m) {
     CHK("bn_bwd_from_ws");
   });
   // wdot[c] += sign * sum_rows W[row][c] * dW[row][c] (KRSC filter as [rows][C])
-  m.def("wdot_colsum", [](P w, P dw, int rows, int C, float sign, P wdot, int zero_first, P s) {
-    sg_wdot_colsum(CV(w), CV(dw), rows, C, sign, V(wdot), zero_first, S(s));
+  m.def("wdot_colsum", [](P w, P dw, int rows, int C, float sign, P wdot, int zero_first, P gamma, P beta,
+                          float tau, P s) {
+    sg_wdot_colsum(CV(w), CV(dw), rows, C, sign, V(wdot), zero_first, CV(gamma), CV(beta), tau, S(s));
     CHK("wdot_colsum");
   });
   // BN(+ReLU) backward from the consuming conv's masked-gradient sums and <W, dW> (bf16, mask bits)

@@ -362,18 +362,10 @@ __global__ void bn_bwd_finalize_k(const float* __restrict__ ws, int nb, int C, c
 // and sum_p dy[p,c]*y[p,c] = sum_{k,taps} W[k,c,tap]*dW[k,c,tap] (the adjoint
 // of the convolution, padding included), accumulated per input channel by the
 // conv's weight-gradient epilogue into `wdot`.  The recovery divides by gamma:
-// bn_gamma_gate_k raises `flag` when any |gamma_c| < tau, and then the gated
+// `flag` is raised when any |gamma_c| < tau (or |beta_c| > 16 |gamma_c|), and then the gated
 // exact reduction (colpart_k over dy, x and the mask bits, into ws2) runs and
-// the finalize uses its sums instead.
-__global__ void bn_gamma_gate_k(const float* __restrict__ gamma, const float* __restrict__ beta, int C, float tau,
-                                int* __restrict__ flag) {
-  // the recovered xhat carries y's bf16 rounding times |y| / |gamma| <= |xhat| + |beta / gamma|
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c < C) {
-    const float g = fabsf(gamma[c]);
-    if (!(g >= tau && fabsf(beta[c]) <= 16.f * g)) *flag = 1;  // (NaN raises it too)
-  }
-}
+// the finalize uses its sums instead.  (The gate itself is evaluated by the
+// conv's <W, dW> pass, wdot_colsum_k in igemm.hip, into the flag.)
 __global__ void bn_bwd_finalize_wdot_k(const float* __restrict__ ws1, const float* __restrict__ ws2, int nb, int C,
                                        const float* __restrict__ gamma, const float* __restrict__ beta,
                                        const float* __restrict__ wdot, const int* __restrict__ flag,
@@ -925,9 +917,8 @@ void sg_bn_bwd_wdot(const void* x, const void* dy, const void* mask, const void*
                     const void* mean, const void* invstd, const void* gamma, const void* beta, const void* ws1,
                     const void* wdot, void* ws2, void* flag, void* coef, void* dg, void* db, void* dx, int64_t R,
                     int C, float tau, hipStream_t s) {
-  sg_zero_async(flag, sizeof(int), s);
-  hipLaunchKernelGGL(bn_gamma_gate_k, dim3((C + 255) / 256), dim3(256), 0, s, (const float*)gamma, (const float*)beta, C,
-                     tau, (int*)flag);
+  // flag: raised (or not) by the consuming conv's wdot pass (wdot_colsum_k)
+  (void)tau;
   dim3 grid;
   int rpb, V;
   colgrid(R, C, grid, rpb, V);

@@ -1138,10 +1138,18 @@ __global__ void __launch_bounds__(256, 1) sk_gemm_k(const GemmArgs p) {
 // 64 channels x 4 row lanes, WDOT_RB rows per block, one atomic per channel.
 constexpr int WDOT_RB = 64;
 __global__ void __launch_bounds__(256) wdot_colsum_k(const bf16* __restrict__ w, const float* __restrict__ dw,
-                                                     int rows, int C, float sign, float* __restrict__ wdot) {
+                                                     int rows, int C, float sign, float* __restrict__ wdot,
+                                                     const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                     float tau, int* __restrict__ flag) {
   __shared__ float red[4][64];
   const int cl = threadIdx.x & 63, lane = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
+  if (gamma != nullptr && blockIdx.y == 0 && lane == 0 && c < C) {
+    // the producer BN's gate (bn_bwd_finalize_wdot_k): the recovered xhat
+    // carries y's bf16 rounding times |xhat| + |beta / gamma|
+    const float g = fabsf(gamma[c]);
+    if (!(g >= tau && fabsf(beta[c]) <= 16.f * g)) *flag = 1;  // (NaN raises it too)
+  }
   const int r0 = blockIdx.y * WDOT_RB;
   float a = 0.f;
   if (c < C) {
@@ -1748,11 +1756,14 @@ int sg_conv_stats_rows(int M, int N) {
 void sg_set_wt_ready(int on) { g_wt_ready = on; }
 // wdot[c] += sign * sum_rows W[row][c] dW[row][c] (zeroes wdot first unless the
 // one-shot pre-zeroed flag is set and sign > 0 ... callers pass zero_first)
+// gamma != nullptr: also raise the int flag stored at wdot + C (zeroed with
+// wdot) when the producer BN's |gamma| / |beta| fail the recovery gate
 void sg_wdot_colsum(const void* w, const void* dw, int rows, int C, float sign, void* wdot, int zero_first,
-                    hipStream_t s) {
-  if (zero_first && !sg_ws_prezeroed()) sg_zero_async(wdot, sizeof(float) * C, s);
+                    const void* gamma, const void* beta, float tau, hipStream_t s) {
+  if (zero_first && !sg_ws_prezeroed()) sg_zero_async(wdot, sizeof(float) * (C + 1), s);
   hipLaunchKernelGGL(wdot_colsum_k, dim3((C + 63) / 64, (rows + WDOT_RB - 1) / WDOT_RB), dim3(256), 0, s,
-                     (const bf16*)w, (const float*)dw, rows, C, sign, (float*)wdot);
+                     (const bf16*)w, (const float*)dw, rows, C, sign, (float*)wdot, (const float*)gamma,
+                     (const float*)beta, tau, (int*)((float*)wdot + C));
 }
 // desc: n WtDesc entries in device memory (32 bytes each), total = sum of tiles
 void sg_wt_transpose_batched(const void* desc, int n, int total, hipStream_t s) {

@@ -1037,7 +1037,7 @@ def conv2d_bwd(x: torch.Tensor, w: torch.Tensor, dy: torch.Tensor, stride, paddi
                 N.lib().conv_dgrad_bn(dyb.data_ptr(), wb.data_ptr(), dxp.data_ptr(), Nn, H, W, Cp, Kp, R, S, Ho, Wo,
                                       sh, sw, ph, pw, dh, dw_, N.ptr(wt), bws.data_ptr(), 0, 0, 0, 0, 0, N.stream(),
                                       0.0, bmask.data_ptr())
-                dxp._sg_bnbwd_wdot = (bws, None, wb)
+                dxp._sg_bnbwd_wdot = (bws, None, wb, bn_producer[3], bn_producer[4])  # (.., gamma, beta)
                 dxp._sg_fresh = True
                 dx = dxp
             elif (bn_producer is not None and FUSE_BN_BWD_STATS and od == torch.bfloat16 and Cx == Cp and C % 8 == 0
@@ -1071,9 +1071,9 @@ def conv2d_bwd(x: torch.Tensor, w: torch.Tensor, dy: torch.Tensor, stride, paddi
         if wd is not None:
             # <W, dW> per input channel over the finished weight gradient (the
             # caller guarantees it held nothing else before this backward)
-            wdot = zeroed_ws(C, x.device)
+            wdot = zeroed_ws(C + 1, x.device)  # [C] sums + the producer BN's gate flag (int)
             N.lib().wdot_colsum(wd[2].data_ptr(), target.data_ptr(), Kp * R * S, C, 1.0, wdot.data_ptr(), 1,
-                                N.stream())
+                                wd[3].data_ptr(), wd[4].data_ptr(), BN_WDOT_TAU, N.stream())
             dx._sg_bnbwd_wdot = (wd[0], wdot)
         if direct:
             dwt = dw_out
@@ -1488,7 +1488,7 @@ def batchnorm_bwd(x: torch.Tensor, dy: torch.Tensor, gamma: torch.Tensor, st: BN
         if (wdot is not None and mode == 3 and not need_dres and beta is not None and x.dtype == torch.bfloat16
                 and C % 8 == 0 and dy.dtype == torch.bfloat16):
             ws2 = zeroed_ws(32 * 2 * C, x.device)
-            flag = torch.empty(1, dtype=torch.int32, device=x.device)
+            flag = wdot[1][C:]  # raised by the conv's <W, dW> pass when gamma fails the recovery gate
             L.bn_bwd_wdot(x.data_ptr(), dy.data_ptr(), ym.data_ptr(), st.scale.data_ptr(), st.shift.data_ptr(),
                           st.mean.data_ptr(), st.invstd.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
                           wdot[0].data_ptr(), wdot[1].data_ptr(), ws2.data_ptr(), flag.data_ptr(), coef.data_ptr(),
