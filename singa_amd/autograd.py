@@ -712,6 +712,7 @@ class Conv2d(Operator):
                     and (getattr(self, "sole", None) or {}).get(0, False)
                     and (tgt is None or _WGRAD_EPOCH.get(id(self.params[1])) != GRAD_EPOCH[0])
                     and getattr(prod, "beta", None) is not None and self.group == 1
+                    and (F.BN_WDOT_MODE != 2 or tuple(w.shape[2:]) == (1, 1))
                     and self.needs_grad(0) and tuple(self.dilation) == (1, 1)):
                 # identity-sum BN backward: this conv's dgrad sums the masked
                 # gradient and its wgrad <W, dW>; the BN skips its reduction
