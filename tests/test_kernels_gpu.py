@@ -762,7 +762,8 @@ def test_fused_bn_stats_under_graph_replay(gpu):
 
 
 @pytest.mark.parametrize("bn", [False, True])
-@pytest.mark.parametrize("C,K,H,st", [(64, 256, 64, 1), (64, 128, 96, 1), (256, 64, 64, 1), (64, 256, 96, 2)])
+@pytest.mark.parametrize("C,K,H,st", [(64, 256, 64, 1), (64, 128, 96, 1), (256, 64, 64, 1), (64, 256, 96, 2),
+                                     (512, 128, 96, 1)])
 def test_conv_short_k_single_stage(gpu, C, K, H, st, bn):
     """The single-stage short-K GEMM variant (tuning knob 6: four workgroups
     per CU, bf16-staged epilogue) on 1x1 convs big enough to take it: forward
@@ -779,26 +780,26 @@ def test_conv_short_k_single_stage(gpu, C, K, H, st, bn):
     dy = torch.randn(Nb, K, Ho, Ho, device=gpu, generator=g).bfloat16().contiguous(memory_format=torch.channels_last)
     outs = {}
     try:
-        for knob in (0, 2):
+        for knob in (0, 8):
             NN.lib().set_tuning(6, knob)
             y = F.conv2d_fwd(x, w, None, (st, st), (0, 0), out_dtype=torch.bfloat16, bn_stats=bn)
             dx = F.conv2d_bwd(x, w, dy, (st, st), (0, 0), need_dx=True)[0]
             ws = getattr(y, "_sg_bn_ws", None)
             outs[knob] = (y.float(), dx.float(), None if ws is None else ws[0][: 2 * K * ws[1]].view(ws[1], 2, K).sum(0))
     finally:
-        NN.lib().set_tuning(6, 2)  # the default
+        NN.lib().set_tuning(6, 8)  # the default
     ref = TF.conv2d(x.float(), w.float(), stride=st)
     dref = TF.conv_transpose2d(dy.float(), w.float(), stride=st, output_padding=(H - 1) % st if st > 1 else 0)
-    for knob in (0, 2):
+    for knob in (0, 8):
         yk, dxk, wsk = outs[knob]
         assert rel_err(yk, ref) < 1e-2
         assert rel_err(dxk, dref) < 1e-2
-    assert torch.equal(outs[0][0], outs[2][0])  # same bf16 rounding of the same fp32 sums
-    assert torch.equal(outs[0][1], outs[2][1])
+    assert torch.equal(outs[0][0], outs[8][0])  # same bf16 rounding of the same fp32 sums
+    assert torch.equal(outs[0][1], outs[8][1])
     if bn:
         yb = outs[0][0]
         s = torch.stack([yb.sum((0, 2, 3)), (yb * yb).sum((0, 2, 3))])
-        assert rel_err(outs[2][2], s) < 1e-4 and rel_err(outs[0][2], s) < 1e-4
+        assert rel_err(outs[8][2], s) < 1e-4 and rel_err(outs[0][2], s) < 1e-4
 
 
 @pytest.mark.parametrize("B,S,H,D,masked", [(2, 64, 4, 64, False), (3, 128, 12, 64, True), (1, 40, 2, 32, False)])
