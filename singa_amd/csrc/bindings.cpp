@@ -144,6 +144,7 @@ void sg_bn_set_rows_per_thread(int);
 
 void register_rccl(py::module& m);  // csrc/comm/rccl_comm.cpp
 void register_mem(py::module& m);   // csrc/mem/pool.cpp
+void register_loop(py::module& m);  // csrc/comm/loop_comm.cpp
 
 static void check_launch(const char* what) {
   hipError_t e = hipGetLastError();
@@ -155,6 +156,7 @@ PYBIND11_MODULE(_C, m) {
   m.doc() = "singa_amd gfx950 HIP kernel library";
   register_rccl(m);
   register_mem(m);
+  register_loop(m);
 
   m.def("device_info", []() {
     py::dict d;

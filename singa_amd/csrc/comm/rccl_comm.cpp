@@ -166,6 +166,8 @@ void register_rccl(py::module& m) {
       .def("all_to_all", &RcclComm::all_to_all)
       .def("send", &RcclComm::send)
       .def("recv", &RcclComm::recv)
+      .def_static("group_start", []() { check(ncclGroupStart(), "GroupStart"); })
+      .def_static("group_end", []() { check(ncclGroupEnd(), "GroupEnd"); })
       .def("split", &RcclComm::split, py::return_value_policy::take_ownership)
       .def("async_error", &RcclComm::async_error)
       .def("abort", &RcclComm::abort)

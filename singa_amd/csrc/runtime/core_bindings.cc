@@ -333,6 +333,14 @@ PYBIND11_MODULE(_core, m) {
     c.def("clamp_affine", [=](P x, P dy, P y, int64_t n, float a, float b, float lo, float hi) {
       C::ClampAffine(cfp(x), cfp(dy), fp(y), n, a, b, lo, hi);
     }, ng);
+    c.def("easgd_diff", [=](P w, P c_, P d, int64_t n, float alpha) { C::EasgdDiff(fp(w), cfp(c_), fp(d), n, alpha); },
+          ng);
+    c.def("rsync_gather", [=](P w, P snap, P buf, int64_t m, int64_t n, int64_t a, int64_t b) {
+      C::RsyncGather(cfp(w), cfp(snap), fp(buf), m, n, a, b);
+    }, ng);
+    c.def("rsync_scatter", [=](P w, P snap, P buf, int64_t m, int64_t n, int64_t a, int64_t b) {
+      C::RsyncScatter(fp(w), fp(snap), cfp(buf), m, n, a, b);
+    }, ng);
     c.def("layernorm_fwd", [=](P x, P g, P b, P y, P mean, P rstd, int64_t R, int64_t D, float eps) {
       C::LayerNormFwd(cfp(x), cfp(g), cfp(b), fp(y), fp(mean), fp(rstd), R, D, eps);
     }, ng);

@@ -660,6 +660,41 @@ void ClampAffine(const float* x, const float* dy, float* y, int64_t n, float a, 
   });
 }
 
+// EASGD elastic difference (reference ElasticParam, src/utils/param.cc:244-284):
+// d = alpha (w - c); w -= d.  With c_add (the centre update after the
+// exchange) : c += s instead (s = the summed differences).
+void EasgdDiff(float* w, const float* c, float* d, int64_t n, float alpha) {
+  ParallelFor(n, kEw, [&](int64_t i0, int64_t i1) {
+    for (int64_t i = i0; i < i1; ++i) {
+      const float v = alpha * (w[i] - c[i]);
+      d[i] = v;
+      w[i] -= v;
+    }
+  });
+}
+
+// RandomSync (src/utils/param.cc:130-241) over the index progression
+// idx_j = (b + j a) mod n, j < m: gather w - snapshot, and scatter
+// snapshot + summed delta back into both w and the snapshot.
+void RsyncGather(const float* w, const float* snap, float* buf, int64_t m, int64_t n, int64_t a, int64_t b) {
+  ParallelFor(m, kEw, [&](int64_t j0, int64_t j1) {
+    for (int64_t j = j0; j < j1; ++j) {
+      const int64_t i = (int64_t)(((__int128)b + (__int128)j * a) % n);
+      buf[j] = w[i] - snap[i];
+    }
+  });
+}
+void RsyncScatter(float* w, float* snap, const float* buf, int64_t m, int64_t n, int64_t a, int64_t b) {
+  ParallelFor(m, kEw, [&](int64_t j0, int64_t j1) {
+    for (int64_t j = j0; j < j1; ++j) {
+      const int64_t i = (int64_t)(((__int128)b + (__int128)j * a) % n);
+      const float v = snap[i] + buf[j];
+      w[i] = v;
+      snap[i] = v;
+    }
+  });
+}
+
 void Reduce(const float* x, float* y, int64_t outer, int64_t red, int64_t inner, int op) {
   auto init = [op]() -> double { return op == 2 ? -INFINITY : op == 3 ? INFINITY : 0.0; };
   if (inner == 1) {

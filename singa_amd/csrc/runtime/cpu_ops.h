@@ -40,6 +40,9 @@ void WhereNd(const uint8_t* c, const float* a, const float* b, float* out, int n
              const int64_t* os, const int64_t* as, const int64_t* bs, const int64_t* cs);
 // y = clamp(a x + b, lo, hi); with dy: dx = dy * a inside (lo, hi), else 0
 void ClampAffine(const float* x, const float* dy, float* y, int64_t n, float a, float b, float lo, float hi);
+void EasgdDiff(float* w, const float* c, float* d, int64_t n, float alpha);
+void RsyncGather(const float* w, const float* snap, float* buf, int64_t m, int64_t n, int64_t a, int64_t b);
+void RsyncScatter(float* w, float* snap, const float* buf, int64_t m, int64_t n, int64_t a, int64_t b);
 // y[outer][inner] = op over j of x[outer][j][inner]; ops: 0 sum 1 mean 2 max 3 min 4 sumsq
 void Reduce(const float* x, float* y, int64_t outer, int64_t red, int64_t inner, int op);
 

@@ -155,6 +155,8 @@ class Model(layer.Layer):
                 opt.prepare_step()
             sc0 = opt.step_counter if opt is not None else 0
             dev = args[0].device
+            keep: list = []
+            _F.CAPTURE_KEEP = keep
             with torch.cuda.graph(g, pool=pool):
                 # first captured kernel: advance the device RNG epoch, so
                 # dropout masks differ on every replay (host-side Philox
@@ -166,10 +168,11 @@ class Model(layer.Layer):
                     out = fn(*args, **kwargs)
                 finally:
                     _F.ARENA.end()
+                    _F.CAPTURE_KEEP = None
             if opt is not None:
                 opt.step_counter = sc0  # capture does not execute; replay below does
-            self._graphs[key] = (g, tuple(args), out)
-        g, sargs, out = self._graphs[key]
+            self._graphs[key] = (g, tuple(args), out, keep)
+        g, sargs, out = self._graphs[key][:3]
         for a, s in zip(args, sargs):
             if isinstance(a, Tensor) and a is not s and a.data.data_ptr() != s.data.data_ptr():
                 G.copy_(s.data, G.reshape(a.data, s.shape))

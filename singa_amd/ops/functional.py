@@ -897,7 +897,11 @@ BN_WDOT_TAU = 0.05  # |gamma| below this (or |beta| > 16 |gamma|): the exact red
 
 
 _WT_CACHE: dict = {}
-_WT_RETIRED: list = []
+# set to a list by Model._run_graph while it captures a HIP graph: every cached
+# scratch / descriptor entry a captured launch addresses is appended, and the
+# graph keeps the list alive (an evicted entry then lives exactly as long as
+# the graphs that replay into it)
+CAPTURE_KEEP: Optional[list] = None
 
 
 def pretranspose_conv_weights(items) -> dict:
@@ -922,9 +926,9 @@ def pretranspose_conv_weights(items) -> dict:
     ent = _WT_CACHE.get(sig)
     if ent is None:
         if len(_WT_CACHE) > 8:
-            # a captured HIP graph may still replay into an evicted entry's
-            # scratch / descriptor table: retire (keep alive), never free
-            _WT_RETIRED.extend(_WT_CACHE.values())
+            # evict: a captured HIP graph that replays into an entry holds it
+            # through its CAPTURE_KEEP list, so dropping the cache's
+            # reference here frees only entries no live graph addresses
             _WT_CACHE.clear()
         dev = sel[0][1].device
         sizes = [w.numel() for _, w in sel]
@@ -945,6 +949,8 @@ def pretranspose_conv_weights(items) -> dict:
         ent = (host.to(dev, non_blocking=True), scratch, [scratch[int(o):int(o) + n] for o, n in zip(offs, sizes)],
                tile0, host)
         _WT_CACHE[sig] = ent
+    if CAPTURE_KEEP is not None:
+        CAPTURE_KEEP.append(ent)
     desc_dev, _, views, total, _ = ent
     N.lib().wt_transpose_batched(desc_dev.data_ptr(), len(sel), total, N.stream())
     return {key: v for (key, _), v in zip(sel, views)}
@@ -1192,7 +1198,25 @@ class _ZeroArena:
         self.active = False
 
 
-ARENA = _ZeroArena()
+class _ThreadArenas(threading.local):
+    """One arena per OS thread: replica threads (hogwild / aggregated
+    executors, the loopback communicator's ranks) run their steps
+    concurrently on their own streams, and the C++ 'pre-zeroed' flag the arena
+    drives is per thread as well."""
+
+    def __init__(self):
+        self.arena = _ZeroArena()
+
+
+_ARENAS = _ThreadArenas()
+
+
+class _ArenaProxy:
+    def __getattr__(self, k):
+        return getattr(_ARENAS.arena, k)
+
+
+ARENA = _ArenaProxy()
 
 
 def zeroed_ws(n: int, device) -> torch.Tensor:

@@ -5,16 +5,17 @@ src/worker/worker.cc:216-299, include/worker/base_layer.h:264-312).
 * :class:`ToDevice` -- one process driving several devices: a copy on the
   destination's stream; the gradient is copied back in backward.
 * :class:`BridgeSend` / :class:`BridgeRecv` -- locations owned by different
-  processes (one GPU each): p2p send/recv over RCCL (xGMI) or gloo.  Every
-  payload is preceded by a small int64 header so the
-  receiver can rebuild the tensor (dtype, requires-grad flag, shape).
+  processes (one GPU each): p2p send/recv over RCCL (xGMI) or gloo through a
+  per-process :class:`P2PChannel` (deferred sends issued as one RCCL group
+  with the next receive, headers checked once per step).
 
 Deadlock freedom: every process executes its local layers in the same global
-topological order (sends are non-blocking, receives block), and the autograd
-engine runs ready operators in decreasing forward order
-(:func:`singa_amd.autograd.backward`), so a blocking gradient receive in
-``BridgeSend.backward`` only ever waits for work at strictly later positions
-of the global order -- which no process can be blocked on.
+topological order (sends are deferred and issued before -- on RCCL grouped
+with -- the next blocking receive), and the autograd engine runs ready
+operators in decreasing forward order (:func:`singa_amd.autograd.backward`),
+so a blocking gradient receive in ``BridgeSend.backward`` only ever waits for
+work at strictly later positions of the global order -- which no process can
+be blocked on.
 """
 from __future__ import annotations
 
@@ -58,35 +59,155 @@ def to_device(x: Tensor, dev) -> Tensor:
     return Tensor(device=dev, data=x.data.to(dev.torch_device), requires_grad=False)
 
 
+class P2PChannel:
+    """The point-to-point traffic of one process's bridges for one step.
+
+    * Sends are DEFERRED: a bridge posts (tensor, peer) here; the queue is
+      issued together with the next blocking receive -- as ONE RCCL group
+      (ncclGroupStart/End) on the native communicator, as non-blocking isends
+      on torch.distributed -- or at the end of the step.  All traffic of a
+      process therefore runs on one stream in one order, and the crossing
+      sends of a 1F1B schedule (stage s sends activation i+1 while its peer
+      sends gradient i) are paired with the receives that match them instead
+      of blocking each other (an ungrouped RCCL send of a large message waits
+      for its receiver).
+    * Headers: every payload is preceded by a small int64 header (dtype,
+      requires-grad flag, shape).  A receiver reads a header on the host only
+      the first time it sees a channel slot (peer, k-th receive of the step);
+      afterwards it posts header and payload receives together from the
+      cached shape and checks all the step's headers with ONE device-to-host
+      copy in :meth:`finish` -- no host synchronisation per message."""
+
+    def __init__(self, comm):
+        self.comm = comm
+        self.native = hasattr(comm, "p2p_group") and getattr(comm, "backend", "") == "rccl"
+        self.sends: List[Tuple[torch.Tensor, int]] = []
+        self.handles: List[tuple] = []
+        self.shapes: dict = {}   # (peer, k) -> header list
+        self.checks: List[tuple] = []  # (device header, expected header list, slot)
+        self.hdrs: dict = {}     # header list -> device tensor (sender side cache)
+        self.k: dict = {}        # peer -> receives this step
+        self.host_reads = 0      # headers read on the host (first use of a slot only)
+        self.checked = 0         # headers verified in bulk at step end
+
+    # compatibility with the plain pending-list protocol
+    def append(self, item) -> None:
+        self.handles.append(item)
+
+    def post(self, t: torch.Tensor, peer: int) -> None:
+        self.sends.append((t, peer))
+
+    def header(self, x: torch.Tensor, rg: bool) -> torch.Tensor:
+        shp = list(x.shape) + [0] * (_MAXD - x.dim())
+        h = (_code(x.dtype), int(rg), x.dim(), *shp)
+        t = self.hdrs.get((h, x.device))
+        if t is None:
+            t = self.hdrs[(h, x.device)] = torch.tensor(list(h), dtype=torch.int64).to(x.device)
+        return t
+
+    def _issue_sends(self) -> None:
+        for t, peer in self.sends:
+            if self.native:
+                self.comm.send(t, peer)
+            else:
+                self.handles.append((self.comm.isend(t, peer), t))
+        self.sends = []
+
+    def exchange(self, bufs: List[torch.Tensor], peer: int) -> None:
+        """Issue the deferred sends, then receive ``bufs`` (in order) from
+        ``peer`` -- one group on RCCL."""
+        if self.native:
+            with self.comm.p2p_group():
+                self._issue_sends()
+                for b in bufs:
+                    self.comm.recv(b, peer)
+        else:
+            self._issue_sends()
+            for b in bufs:
+                self.comm.recv(b, peer)
+
+    def recv_tensor(self, peer: int, dev) -> Tuple[torch.Tensor, bool]:
+        """Receive the next (header, payload) pair from ``peer``: (tensor,
+        requires-grad flag of the sender)."""
+        k = self.k.get(peer, 0)
+        self.k[peer] = k + 1
+        hdr = torch.empty(3 + _MAXD, dtype=torch.int64, device=dev.torch_device)
+        h = self.shapes.get((peer, k))
+        if h is None:  # first time on this slot: read the header on the host
+            self.exchange([hdr], peer)
+            self.host_reads += 1
+            h = self.shapes[(peer, k)] = [int(v) for v in hdr.cpu().tolist()]
+            buf = torch.empty(tuple(h[3:3 + h[2]]), dtype=_DT[h[0]], device=dev.torch_device)
+            self.exchange([buf], peer)
+        else:
+            buf = torch.empty(tuple(h[3:3 + h[2]]), dtype=_DT[h[0]], device=dev.torch_device)
+            self.exchange([hdr, buf], peer)
+            self.checks.append((hdr, h, (peer, k)))
+        return buf, bool(h[1])
+
+    def flush(self) -> None:
+        if not self.sends:
+            return
+        if self.native:
+            with self.comm.p2p_group():
+                self._issue_sends()
+        else:
+            self._issue_sends()
+
+    def finish(self) -> None:
+        """End of step: issue what is left, complete it, verify the headers
+        that were not read on the host (one copy for all of them)."""
+        self.flush()
+        for h, _ in self.handles:
+            if h is not None:
+                h.wait()
+        self.handles.clear()
+        self.k.clear()
+        if self.checks:
+            got = torch.stack([c[0] for c in self.checks]).cpu().tolist()
+            for (_, exp, slot), g in zip(self.checks, got):
+                if [int(v) for v in g] != exp:
+                    self.shapes.pop(slot, None)
+                    self.checks.clear()
+                    raise RuntimeError(f"bridge header mismatch on slot {slot}: got {g}, expected {exp} (the "
+                                       "sender's tensor shape changed between steps)")
+            self.checked += len(self.checks)
+            self.checks.clear()
+
+
+def _chan(pending) -> P2PChannel:
+    if not isinstance(pending, P2PChannel):
+        raise TypeError("bridges need a P2PChannel (parallel.bridge.P2PChannel(comm))")
+    return pending
+
+
 class BridgeSend(Operator):
-    """Forward: isend x to ``peer``.  Backward: blocking recv of dL/dx."""
+    """Forward: post x (header + payload) to ``peer``.  Backward: receive
+    dL/dx (grouped with the deferred sends)."""
 
     always_run = True
 
-    def __init__(self, comm, peer: int, pending: List, name=None):
+    def __init__(self, comm, peer: int, pending: "P2PChannel", name=None):
         super().__init__(name)
-        self.comm, self.peer, self.pending = comm, peer, pending
+        self.comm, self.peer, self.chan = comm, peer, _chan(pending)
 
     def forward(self, x):
         if x.dim() > _MAXD:
             raise ValueError(f"bridge payloads support at most {_MAXD} dims")
-        shp = list(x.shape) + [0] * (_MAXD - x.dim())
-        hdr = torch.tensor([_code(x.dtype), int(self.requires_grad), x.dim()] + shp, dtype=torch.int64)
         payload = G.contiguous(x)
-        dev_hdr = hdr.to(x.device)
-        self.pending.append((self.comm.isend(dev_hdr, self.peer), dev_hdr))
-        self.pending.append((self.comm.isend(payload, self.peer), payload))
+        self.chan.post(self.chan.header(payload, self.requires_grad), self.peer)
+        self.chan.post(payload, self.peer)
         if self.requires_grad:
             self.shape, self.dtype, self.device = x.shape, x.dtype, x.device
         return x
 
     def backward(self, dy=None):
         g = torch.empty(self.shape, dtype=self.dtype, device=self.device)
-        self.comm.recv(g, self.peer)
+        self.chan.exchange([g], self.peer)
         return g
 
 
-def bridge_send(x: Tensor, comm, peer: int, pending: List) -> Optional[Tensor]:
+def bridge_send(x: Tensor, comm, peer: int, pending: "P2PChannel") -> Optional[Tensor]:
     """Returns the root tensor to include in backward (None if no grad)."""
     op = BridgeSend(comm, peer, pending)
     y = op(x)
@@ -94,25 +215,18 @@ def bridge_send(x: Tensor, comm, peer: int, pending: List) -> Optional[Tensor]:
 
 
 class BridgeRecv(Operator):
-    """Forward: blocking recv from ``peer``.  Backward: isend dL/dy (zeros
-    if nothing downstream produced a gradient)."""
+    """Forward: receive from ``peer``.  Backward: post dL/dy (zeros if
+    nothing downstream produced a gradient)."""
 
     always_run = True
 
-    def __init__(self, comm, peer: int, pending: List, name=None):
+    def __init__(self, comm, peer: int, pending: "P2PChannel", name=None):
         super().__init__(name)
-        self.comm, self.peer, self.pending = comm, peer, pending
+        self.comm, self.peer, self.chan = comm, peer, _chan(pending)
 
     def __call__(self, dev) -> Tensor:
-        hdr = torch.empty(3 + _MAXD, dtype=torch.int64, device=dev.torch_device)
-        self.comm.recv(hdr, self.peer)
-        h = [int(v) for v in hdr.cpu().tolist()]
-        code, rg, nd = h[0], h[1], h[2]
-        shape = h[3:3 + nd]
-        dt = _DT[code]
-        buf = torch.empty(tuple(shape), dtype=dt, device=dev.torch_device)
-        self.comm.recv(buf, self.peer)
-        self.requires_grad = bool(rg) and autograd.training
+        buf, rg = self.chan.recv_tensor(self.peer, dev)
+        self.requires_grad = rg and autograd.training
         if not self.requires_grad:
             return Tensor(device=dev, data=buf, requires_grad=False)
         self.src, self.src_idx, self.params, self.input_requires = [], [], [], []
@@ -127,11 +241,14 @@ class BridgeRecv(Operator):
         if dy is None:
             dy = G.zeros(self.shape, self.dtype, self.dev.torch_device)
         dy = G.contiguous(G.to(dy, self.dtype))
-        self.pending.append((self.comm.isend(dy, self.peer), dy))
+        self.chan.post(dy, self.peer)
         return ()
 
 
-def wait_all(pending: List) -> None:
+def wait_all(pending) -> None:
+    if isinstance(pending, P2PChannel):
+        pending.finish()
+        return
     for h, _ in pending:
         if h is not None:
             h.wait()

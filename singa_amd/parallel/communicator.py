@@ -140,6 +140,14 @@ class Communicator:
     def irecv(self, t: torch.Tensor, src: int):
         return dist.irecv(t, self._g(src), group=self.group)
 
+    def p2p_group(self):
+        """Context manager grouping the point-to-point calls inside (RCCL
+        ncclGroupStart/End on the native communicator).  torch.distributed
+        sends here are posted as non-blocking isend by the bridges, so no
+        grouping is needed: a no-op context."""
+        import contextlib
+        return contextlib.nullcontext()
+
     def barrier(self):
         if self.world_size > 1:
             if self.backend == "nccl":

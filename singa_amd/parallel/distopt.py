@@ -62,6 +62,12 @@ class DistOpt:
             raise ValueError("DistOpt: grad_dtype must be float32 or bfloat16")
         self.grad_dtype = grad_dtype
         self._stage = None  # bf16 staging buffer (same layout as the flat gradient)
+        # diagnostics: with time_exposed, each step records an event pair
+        # around the join of the bucket all-reduces into the compute stream --
+        # the GPU time the compute stream waits for communication that the
+        # backward did not hide (read with exposed_comm_ms(), after a sync)
+        self.time_exposed = False
+        self._exposed: List[tuple] = []
 
     # delegate optimiser attributes (lr, step_counter, store, ...)
     def __getattr__(self, k):
@@ -138,11 +144,33 @@ class DistOpt:
         for b, r in enumerate(remaining):  # params without gradients this step
             if r > 0:
                 works.append(self._reduce_bucket(b))
+        ev = None
+        if self.time_exposed and torch.cuda.is_available() and self.store.g.is_cuda and not capturing:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
         for w in works:
             if w is not None:
                 w.wait()
+        if ev is not None:
+            ev[1].record()
+            self._exposed.append(ev)
         self.opt.update(grad_scale=1.0 / self.world_size)
         self.opt.step()
+
+    def exposed_comm_ms(self, reset: bool = True) -> Optional[float]:
+        """Mean GPU ms per step the compute stream waited at the bucket joins
+        (synchronises on the recorded events)."""
+        if not self._exposed:
+            return None
+        ms = [a.elapsed_time(b) for a, b in self._exposed]
+        if reset:
+            self._exposed = []
+        return sum(ms) / len(ms)
+
+    def exchange_bytes(self) -> int:
+        """Bytes one rank contributes to the gradient exchange per step."""
+        st = self.store
+        return 0 if st is None else st.g.numel() * (2 if self.grad_dtype == torch.bfloat16 else 4)
 
     def _reduce_bucket(self, b: int):
         """Fork bucket b's all-reduce onto the comm stream (bf16 exchange:

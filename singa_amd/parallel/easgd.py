@@ -28,10 +28,16 @@ from typing import Optional
 
 import torch
 
+from ..ops import glue as G
 from ..ops import native as N
 from .communicator import Communicator
 
 XGMI_LINK_GBPS = 153.0  # one MI355X xGMI link, GB/s per direction
+
+
+def _cpu():
+    from ..ops import cpu as CP
+    return CP.lib() if CP.enabled() else None
 
 
 class _SyncBase:
@@ -52,48 +58,93 @@ class _SyncBase:
 
 
 class ElasticSync(_SyncBase):
+    """EASGD over collectives.  Every buffer (the centre or its shard, the
+    difference, the gathered centre) is allocated once at bootstrap; the
+    worker-side update (w -= d) and the centre update (c += sum d) are native
+    kernels on both devices (``easgd_diff`` HIP / CppCPU, native add).
+
+    ``overlap=True`` (GPU, native RCCL communicator): the exchange of step t
+    -- reduce-scatter / all-reduce of d, c += sum d, and (sharded) the
+    all-gather of the new centre -- is forked onto the communicator's comm
+    stream and overlaps step t+1's forward and backward; the next sync joins
+    it before reading the centre.  This is the reference's UpdateParam (send
+    after the update) / WaitUpdate (receive before the next use) split
+    (src/utils/param_manager.cc:163-234) at whole-buffer granularity.  Since
+    d_t depends only on w_t and c_t, the overlapped schedule produces the same
+    numbers as the synchronous one."""
+
     def __init__(self, store, comm, moving_rate: float, sync_frequency: int = 1, warmup_steps: int = 0,
-                 sharded: bool = False):
+                 sharded: bool = False, overlap: bool = False):
         super().__init__(store, comm, sync_frequency, warmup_steps)
         self.ngroups = comm.world_size
         self.alpha = moving_rate / max(1, self.ngroups)
         self.sharded = sharded and comm.world_size > 1 and store.numel % comm.world_size == 0
+        self.overlap = bool(overlap)
         self.centre: Optional[torch.Tensor] = None
+        self._d = self._full = self._shard = None
+        self._pending = None  # comm-stream event of the in-flight exchange
 
     def bootstrap(self) -> None:
         super().bootstrap()
+        w = self.store.w
         if self.sharded:
             n = self.store.numel // self.comm.world_size
             r = self.comm.rank
-            self.centre = self.store.w[r * n:(r + 1) * n].clone()
+            self.centre = torch.empty(n, dtype=w.dtype, device=w.device)
+            G.copy_(self.centre, w[r * n:(r + 1) * n])
+            self._shard = torch.empty_like(self.centre)
+            self._full = torch.empty_like(w)  # the gathered centre the next difference reads
+            G.copy_(self._full, w)
         else:
-            self.centre = self.store.w.clone()
+            self.centre = torch.empty_like(w)
+            G.copy_(self.centre, w)
+        self._d = torch.empty_like(w)
+
+    def _can_overlap(self) -> bool:
+        return self.overlap and self.store.w.is_cuda and getattr(self.comm, "comm_stream", None) is not None
+
+    def wait(self) -> None:
+        """Join an in-flight overlapped exchange into the current stream."""
+        if self._pending is not None:
+            torch.cuda.current_stream(self.store.w.device).wait_event(self._pending)
+            self._pending = None
 
     def sync(self) -> None:
         w = self.store.w
         if self.centre is None:
             self.bootstrap()
-        if self.sharded:
-            full_c = torch.empty_like(w)
-            self.comm.all_gather(full_c, self.centre)
-            c = full_c
-        else:
-            c = self.centre
-        d = torch.empty_like(w)
+        self.wait()  # the previous exchange wrote the centre and read d
+        c = self._full if self.sharded else self.centre
+        d = self._d
         if w.is_cuda:
             N.lib().easgd_diff(w.data_ptr(), c.data_ptr(), d.data_ptr(), w.numel(), self.alpha, N.stream())
+        elif _cpu() is not None and w.dtype == torch.float32 and w.is_contiguous():
+            _cpu().easgd_diff(w.data_ptr(), c.data_ptr(), d.data_ptr(), w.numel(), self.alpha)
         else:
             d.copy_(self.alpha * (w - c))
             w.sub_(d)
+        self.store.sync_low()  # the worker side is complete: w -= d
+        if self._can_overlap():
+            cs = self.comm.comm_stream
+            cs.wait_stream(torch.cuda.current_stream(w.device))
+            with torch.cuda.stream(cs):
+                self._exchange(d)
+                ev = torch.cuda.Event()
+                ev.record(cs)
+            self._pending = ev
+        else:
+            self._exchange(d)
+        self.nsync += 1
+
+    def _exchange(self, d: torch.Tensor) -> None:
+        """sum_ranks d -> the centre (and its gathered copy), on the current stream."""
         if self.sharded:
-            shard = torch.empty_like(self.centre)
-            self.comm.reduce_scatter(shard, d)
-            self.centre.add_(shard)
+            self.comm.reduce_scatter(self._shard, d)
+            G.binary("add", self.centre, self._shard, out=self.centre)
+            self.comm.all_gather(self._full, self.centre)
         else:
             self.comm.all_reduce(d)
-            self.centre.add_(d)
-        self.store.sync_low()
-        self.nsync += 1
+            G.binary("add", self.centre, d, out=self.centre)
 
 
 class RandomSync(_SyncBase):
@@ -103,10 +154,12 @@ class RandomSync(_SyncBase):
         self.ratio = float(min(1.0, max(1e-6, sample_ratio)))
         self.seed = seed
         self.snapshot: Optional[torch.Tensor] = None
+        self._buf: Optional[torch.Tensor] = None
 
     def bootstrap(self) -> None:
         super().bootstrap()
-        self.snapshot = self.store.w.clone()
+        self.snapshot = torch.empty_like(self.store.w)
+        G.copy_(self.snapshot, self.store.w)
 
     def configure_bandwidth(self, step_seconds: float, bandwidth_mbps: Optional[float] = None,
                             nservers: int = 1) -> float:
@@ -132,12 +185,19 @@ class RandomSync(_SyncBase):
             self.bootstrap()
         n = w.numel()
         m, a, b = self._progression(n, step)
-        buf = torch.empty(m, dtype=torch.float32, device=w.device)
+        if self._buf is None or self._buf.numel() < m:
+            self._buf = torch.empty(m, dtype=torch.float32, device=w.device)
+        buf = self._buf[:m]
         if w.is_cuda:
             L = N.lib()
             L.rsync_gather(w.data_ptr(), self.snapshot.data_ptr(), buf.data_ptr(), m, n, a, b, N.stream())
             self.comm.all_reduce(buf)
             L.rsync_scatter(w.data_ptr(), self.snapshot.data_ptr(), buf.data_ptr(), m, n, a, b, N.stream())
+        elif _cpu() is not None and w.dtype == torch.float32 and w.is_contiguous():
+            C = _cpu()
+            C.rsync_gather(w.data_ptr(), self.snapshot.data_ptr(), buf.data_ptr(), m, n, a, b)
+            self.comm.all_reduce(buf)
+            C.rsync_scatter(w.data_ptr(), self.snapshot.data_ptr(), buf.data_ptr(), m, n, a, b)
         else:
             idx = (b + torch.arange(m, dtype=torch.int64) * a) % n
             buf.copy_(w[idx] - self.snapshot[idx])

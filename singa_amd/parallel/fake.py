@@ -255,6 +255,10 @@ class FakeCommunicator:
         if self.world_size > 1:
             self._xchg("barrier", None)
 
+    def p2p_group(self):
+        import contextlib
+        return contextlib.nullcontext()  # fake sends are buffered: nothing to pair
+
     # ------------------------------------------------------ point-to-point
     def send(self, t: torch.Tensor, dst: int):
         if self._enter("send"):

@@ -196,12 +196,26 @@ class PSSync:
             b.gpu_data()  # host -> the store slice (stream-ordered)
             b.mutable_gpu_data()  # the device copy is authoritative again (training writes it)
 
+    def _read_host(self, i: int) -> np.ndarray:
+        """Read-only host copy of parameter i that leaves the device side
+        authoritative: training keeps writing the store slice behind the
+        blob's back, so outside an exchange every blob must stay HEAD_AT_GPU
+        (else the next sync would read a stale host buffer and push it over
+        the trained weights)."""
+        b = self._blobs[i]
+        if b is None:
+            return self._host[i]
+        h = b.cpu_data().numpy().copy()  # SYNCED after the D2H copy
+        b.mutable_gpu_data()  # SYNCED -> HEAD_AT_GPU (no copy)
+        self._host[i] = h
+        return h
+
     def bootstrap(self) -> None:
         """Group 0 Puts every parameter, the other groups Get them (blocking
         until group 0's Put arrived: the server defers the Get)."""
         for i in range(len(self.store.params)):
             if self.group_id == 0:
-                self.client.put(self.key_base + i, self._pull_to_host(i))
+                self.client.put(self.key_base + i, self._read_host(i))
             else:
                 h = self._pull_to_host(i)
                 got = self.client.get(self.key_base + i, h)

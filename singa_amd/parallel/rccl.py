@@ -18,7 +18,15 @@ Sync transport (src/utils/param_manager.cc:103-234).  Here:
   fork / join is itself capturable, so a training step with bucketed
   all-reduces overlapping the backward can be ONE HIP graph;
 * ``split`` = ``ncclCommSplit`` (sub-communicators for layer-partition /
-  placement groups).
+  placement groups);
+* ``p2p_group()`` = ``ncclGroupStart/End`` around paired point-to-point calls
+  (the pipeline bridges issue a step's sends together with the next receive,
+  so crossing 1F1B exchanges cannot deadlock).
+
+``native`` may also be a ``_C.LoopComm`` (csrc/comm/loop_comm.cpp): N ranks as
+threads of one process behind the same call surface, on one GPU or on host
+memory (:mod:`.loop`), so this wrapper and everything above it run at world
+sizes 2..8 before an 8-GPU node is available.
 """
 from __future__ import annotations
 
@@ -33,6 +41,19 @@ from .communicator import Communicator
 _OPS = {"sum": 0, "prod": 1, "max": 2, "min": 3, "avg": 4}
 _DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2, torch.int32: 3, torch.int64: 4, torch.uint8: 5,
        torch.float64: 6}
+
+
+class _Done:
+    """Completed handle (host-memory loopback ranks finish work eagerly)."""
+
+    def wait(self) -> None:
+        return None
+
+    def is_completed(self) -> bool:
+        return True
+
+    def synchronize(self) -> None:
+        return None
 
 
 class Work:
@@ -65,8 +86,13 @@ class RcclCommunicator(Communicator):
     def __init__(self, world_size: int, rank: int, local_rank: int, store=None, tag: str = "world",
                  native=None, ranks: Optional[List[int]] = None, device: Optional[torch.device] = None):
         super().__init__(world_size, rank, local_rank, "rccl", None, ranks)
-        ndev = max(1, torch.cuda.device_count())
-        self.device = device or torch.device("cuda", local_rank % ndev)
+        self.loopback = bool(getattr(native, "loopback", False))
+        self.host = self.loopback and native.device < 0  # host-memory loopback ranks (CPU CI)
+        if self.host:
+            self.device = torch.device("cpu")
+        else:
+            ndev = max(1, torch.cuda.device_count())
+            self.device = device or torch.device("cuda", local_rank % ndev)
         self.store = store
         L = N.lib()
         if native is None:
@@ -83,21 +109,36 @@ class RcclCommunicator(Communicator):
         self._c = native
         # high priority: bucket all-reduces issued mid-backward get the CUs
         # they need promptly instead of queueing behind the compute stream
-        self.comm_stream = torch.cuda.Stream(device=self.device, priority=-1)
+        self.comm_stream = None if self.host else torch.cuda.Stream(device=self.device, priority=-1)
+        self.stats = {"calls": 0, "bytes": 0}  # collective calls / payload bytes issued by this rank
+        self._group_keep: Optional[list] = None
+
+    @property
+    def version(self) -> Optional[int]:
+        """librccl version (e.g. 22606 = 2.26.6), the library every rank links."""
+        try:
+            return int(N.lib().rccl_version())
+        except Exception:
+            return None
 
     # ------------------------------------------------------------ plumbing
-    @staticmethod
-    def _check(*ts):
+    def _check(self, *ts):
         for t in ts:
-            if not t.is_cuda or not t.is_contiguous():
-                raise ValueError("RCCL collectives need dense device tensors")
+            if t.is_cuda == self.host or not t.is_contiguous():
+                raise ValueError("RCCL collectives need dense device tensors" if not self.host else
+                                 "host loopback ranks need dense host tensors")
             if t.dtype not in _DT:
                 raise TypeError(f"RCCL: unsupported dtype {t.dtype}")
+        self.stats["calls"] += 1
+        self.stats["bytes"] += sum(t.numel() * t.element_size() for t in ts[:1])
+
+    def _cur(self) -> int:
+        return 0 if self.host else torch.cuda.current_stream(self.device).cuda_stream
 
     def _run(self, async_op: bool, tensors, fn):
-        if not async_op:
-            fn(torch.cuda.current_stream(self.device).cuda_stream)
-            return None
+        if not async_op or self.host:
+            fn(self._cur())
+            return _Done() if async_op else None
         cur = torch.cuda.current_stream(self.device)
         cs = self.comm_stream
         cs.wait_stream(cur)  # the inputs were produced on the current stream
@@ -167,11 +208,36 @@ class RcclCommunicator(Communicator):
 
     def send(self, t: torch.Tensor, dst: int):
         self._check(t)
-        self._c.send(t.data_ptr(), t.numel(), _DT[t.dtype], dst, torch.cuda.current_stream(self.device).cuda_stream)
+        if self._group_keep is not None:
+            self._group_keep.append(t)  # grouped calls run at group end: keep the buffer alive until then
+        self._c.send(t.data_ptr(), t.numel(), _DT[t.dtype], dst, self._cur())
 
     def recv(self, t: torch.Tensor, src: int):
         self._check(t)
-        self._c.recv(t.data_ptr(), t.numel(), _DT[t.dtype], src, torch.cuda.current_stream(self.device).cuda_stream)
+        if self._group_keep is not None:
+            self._group_keep.append(t)
+        self._c.recv(t.data_ptr(), t.numel(), _DT[t.dtype], src, self._cur())
+
+    def p2p_group(self):
+        """Context manager: the point-to-point calls inside are issued as one
+        RCCL group (ncclGroupStart/End) on the current stream."""
+        comm = self
+
+        class _G:
+            def __enter__(self_):
+                comm._group_keep = []
+                comm._c.group_start()
+
+            def __exit__(self_, *exc):
+                try:
+                    comm._c.group_end()
+                finally:
+                    keep, comm._group_keep = comm._group_keep, None
+                    if keep and not comm.host and not torch.cuda.is_current_stream_capturing():
+                        for t in keep:  # the group's kernels run on the current stream
+                            t.record_stream(torch.cuda.current_stream(comm.device))
+                return False
+        return _G()
 
     def isend(self, t: torch.Tensor, dst: int):
         self._check(t)
@@ -183,9 +249,10 @@ class RcclCommunicator(Communicator):
 
     def barrier(self):
         if self.world_size > 1:
-            t = torch.empty(1, dtype=torch.float32, device=self.device)
+            t = torch.zeros(1, dtype=torch.float32, device=self.device)
             self.all_reduce(t)
-            torch.cuda.current_stream(self.device).synchronize()
+            if not self.host:
+                torch.cuda.current_stream(self.device).synchronize()
 
     def split(self, ranks: List[int]) -> Optional["RcclCommunicator"]:
         """Collective: every rank of this communicator calls it with the same
@@ -194,13 +261,18 @@ class RcclCommunicator(Communicator):
         ranks = sorted(int(r) for r in ranks)
         mine = self.ranks[self.rank] in ranks
         if self.world_size == 1:
-            return RcclCommunicator(1, 0, self.local_rank, native=self._c, ranks=ranks,
-                                    device=self.device) if mine else None
+            if not mine:
+                return None
+            c = RcclCommunicator(1, 0, self.local_rank, native=self._c, ranks=ranks, device=self.device)
+            c.stats = self.stats
+            return c
         sub = self._c.split(0 if mine else -1, ranks.index(self.ranks[self.rank]) if mine else 0)
         if not mine or sub is None:
             return None
-        return RcclCommunicator(sub.nranks, sub.rank, self.local_rank, self.store, native=sub, ranks=ranks,
-                                device=self.device)
+        c = RcclCommunicator(sub.nranks, sub.rank, self.local_rank, self.store, native=sub, ranks=ranks,
+                             device=self.device)
+        c.stats = self.stats  # one traffic account per rank
+        return c
 
     def async_error(self) -> str:
         return self._c.async_error()

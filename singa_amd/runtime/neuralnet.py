@@ -384,7 +384,8 @@ class NeuralNet:
         outs: Dict[str, object] = {}
         self._extra_roots = []
         self._mb_batch = getattr(self, "_mb_batch", {})
-        self._pending = getattr(self, "_pending", [])
+        if getattr(self, "_pending", None) is None and self.dist:
+            self._pending = B.P2PChannel(self.comm)
         for l in self.layers:
             if not self.is_local(l):
                 continue

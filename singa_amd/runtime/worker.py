@@ -171,8 +171,11 @@ class Worker:
             elif up.param_type == "RandomSync":
                 self.sync = RandomSync(self.store, pc, 1.0, up.sync_frequency, up.warmup_steps)
             else:
+                # overlap: on the GPU (native RCCL comm stream) the centre
+                # exchange of a sync runs behind the next step's compute
                 self.sync = ElasticSync(self.store, pc, up.moving_rate or 0.9, up.sync_frequency,
-                                        up.warmup_steps, sharded=cl.sharded_centre())
+                                        up.warmup_steps, sharded=cl.sharded_centre(),
+                                        overlap=os.environ.get("SINGA_AMD_EASGD_OVERLAP", "1") != "0")
         self._setup_executors()
         self.perf = Performance("train")
 
@@ -352,6 +355,8 @@ class Worker:
         if self.checkpoint_path and self.checkpoint_every and (step + 1) % self.checkpoint_every == 0:
             from .checkpoint import save_worker
 
+            if hasattr(self.sync, "wait"):
+                self.sync.wait()  # the centre of an overlapped exchange is part of the checkpoint
             self.step = step + 1
             save_worker(self, self.checkpoint_path.replace("{rank}", str(self.comm.rank)))
         fs = os.environ.get("SINGA_AMD_FAULT_STEP")
@@ -395,6 +400,8 @@ class Worker:
                     self.timers[k] = 0.0
                 last = step + 1
         self.step = steps
+        if hasattr(self.sync, "wait"):
+            self.sync.wait()
         if isinstance(self.sync, PSSync):
             self.sync.client.stop()  # kStop to every server (param_manager.cc:78-86)
         return {"history": self.history}

@@ -156,6 +156,7 @@ class _ExportCtx:
         self.inits: "OrderedDict[str, np.ndarray]" = OrderedDict()
         self.param_names = param_names
         self.state_by_ptr: Dict[int, str] = {}
+        self.const_names: set = set()  # initializers that are constants, not parameters (tagged on export)
         self.k = 0
 
     def fresh(self, base: str = "t") -> str:
@@ -165,6 +166,7 @@ class _ExportCtx:
     def const(self, a: np.ndarray, base: str = "const") -> str:
         n = self.fresh(base)
         self.inits[n] = np.asarray(a)
+        self.const_names.add(n)
         return n
 
     def named_const(self, t: torch.Tensor, fallback: str) -> str:
@@ -174,6 +176,7 @@ class _ExportCtx:
         if n in self.inits:
             return n
         self.inits[n] = t.detach().float().cpu().numpy()
+        self.const_names.add(n)
         return n
 
     def name_of(self, t: Tensor) -> str:
@@ -185,6 +188,7 @@ class _ExportCtx:
             n = self.param_names[id(t)]
         else:
             n = self.fresh("const")
+            self.const_names.add(n)
         a = t.data.detach()
         if a.dtype == torch.bfloat16:
             a = a.float()
@@ -494,7 +498,10 @@ def to_onnx(m, inputs: Sequence[Tensor], outputs: Optional[Sequence[Tensor]] = N
         g.output.append(_value_info(out_name, y.shape, _T2ONNX.get(y.dtype, P.FLOAT), dynamic_batch))
     g.node.extend(c.nodes)
     for n, a in c.inits.items():
-        g.initializer.append(numpy_to_tensorproto(a, n))
+        tp = numpy_to_tensorproto(a, n)
+        if n in c.const_names:
+            tp.doc_string = CONST_TAG
+        g.initializer.append(tp)
     mp = P.new("ModelProto")
     mp.ir_version = 8
     mp.producer_name = "singa_amd"
@@ -878,7 +885,14 @@ class _Fused:
         return f"_Fused({self.kind}, nodes={list(self.members)}, out={self.output!r})"
 
 
-def _fusion_plan(nodes, inits: Dict[str, Tensor], consts: set, outputs: Sequence[str]) -> Dict[int, _Fused]:
+# doc_string of an exported initializer that is a constant (GELU's sqrt 2, the
+# attention scale, BN running statistics, ...) rather than a parameter: ONNX
+# itself does not say which initializers are trainable
+CONST_TAG = "singa_amd:const"
+
+
+def _fusion_plan(nodes, inits: Dict[str, Tensor], consts: set, outputs: Sequence[str],
+                 gelu_scalars: Optional[set] = None) -> Dict[int, _Fused]:
     """Pattern-match the imported node list into fused groups, keyed by the
     index of each group's last node:
 
@@ -891,8 +905,15 @@ def _fusion_plan(nodes, inits: Dict[str, Tensor], consts: set, outputs: Sequence
     A chain only fuses when every intermediate has exactly one consumer and
     is not a graph output, so no other node can observe what it skips.  The
     unfused import runs 2 / 5 / 5-6 autograd ops (and their backward kernels)
-    per group, plus an fp32->bf16 cast of every MatMul weight per step."""
+    per group, plus an fp32->bf16 cast of every MatMul weight per step.
+
+    ``gelu_scalars``: untagged one-element initializers the GELU pattern may
+    consume as its constants (sqrt 2, 1, 0.5 -- values checked exactly); the
+    importer freezes the ones a matched GELU used.  Every other pattern
+    constant must be a tagged constant, so a learnable scalar (a temperature
+    feeding the attention scores) keeps its gradient and blocks the fusion."""
     cons: Dict[str, List[int]] = {}
+    soft = gelu_scalars or set()
     for idx, nd in enumerate(nodes):
         for nm in nd.input:
             if nm:
@@ -906,9 +927,9 @@ def _fusion_plan(nodes, inits: Dict[str, Tensor], consts: set, outputs: Sequence
             return None
         return c[0]
 
-    def scalar(name: str) -> Optional[float]:
+    def scalar(name: str, allow_soft: bool = False) -> Optional[float]:
         t = inits.get(name)
-        if t is None or name not in consts or t.data.numel() != 1:
+        if t is None or t.data.numel() != 1 or not (name in consts or (allow_soft and name in soft)):
             return None
         return float(t.data.reshape(-1)[0])
 
@@ -942,7 +963,8 @@ def _fusion_plan(nodes, inits: Dict[str, Tensor], consts: set, outputs: Sequence
 
     def gelu(i):
         nd = nodes[i]
-        if nd.op_type != "Div" or scalar(nd.input[1]) is None or abs(scalar(nd.input[1]) - math.sqrt(2.0)) > 1e-4:
+        s2 = scalar(nd.input[1], True) if nd.op_type == "Div" else None
+        if s2 is None or abs(s2 - math.sqrt(2.0)) > 1e-4:
             return None
         x = nd.input[0]
         j = only(nd.output[0])
@@ -952,7 +974,7 @@ def _fusion_plan(nodes, inits: Dict[str, Tensor], consts: set, outputs: Sequence
         if k is None or nodes[k].op_type != "Add":
             return None
         c = other(nodes[k], nodes[j].output[0])
-        if c is None or scalar(c) != 1.0:
+        if c is None or scalar(c, True) != 1.0:
             return None
         m = only(nodes[k].output[0])
         if m is None or nodes[m].op_type != "Mul" or other(nodes[m], nodes[k].output[0]) != x:
@@ -961,7 +983,7 @@ def _fusion_plan(nodes, inits: Dict[str, Tensor], consts: set, outputs: Sequence
         if n is None or nodes[n].op_type != "Mul":
             return None
         h = other(nodes[n], nodes[m].output[0])
-        if h is None or scalar(h) != 0.5:
+        if h is None or scalar(h, True) != 0.5:
             return None
         return _Fused("gelu", (i, j, k, m, n), [x], nodes[n].output[0])
 
@@ -1108,14 +1130,18 @@ class SingaRep:
             for nm in nd.input:
                 consumers.setdefault(nm, set()).add(nd.op_type)
         scalar_math = {"Add", "Mul", "Sub", "Div", "Pow"}
+        soft, soft_np = set(), {}
         for t in g.initializer:
             a = tensorproto_to_numpy(t)
-            # scalar initializers that only feed elementwise arithmetic (GELU's
-            # sqrt(2) / 1 / 0.5, the attention scale: what the fusion patterns
-            # consume) are constants; a one-element weight of any other op
-            # (a PRelu slope, a scale of a norm or a GEMM) stays learnable
-            scalar_const = a.size == 1 and consumers.get(t.name, set()) <= scalar_math
-            is_param = trainable and a.dtype == np.float32 and t.name in weight_like and not scalar_const
+            # constants are what the exporter tagged as such; an untagged
+            # initializer in a learnable position is a parameter, scalars
+            # included (a learnable temperature / scale) -- except the GELU
+            # pattern's numeric constants, frozen below when the pattern matches
+            tagged = t.doc_string == CONST_TAG
+            is_param = trainable and a.dtype == np.float32 and t.name in weight_like and not tagged
+            if is_param and a.size == 1 and consumers.get(t.name, set()) <= scalar_math:
+                soft.add(t.name)
+                soft_np[t.name] = a
             ten = Tensor(device=self.device, data=torch.from_numpy(np.array(a, order="C")),
                          requires_grad=is_param, stores_grad=is_param)
             ten.name = t.name
@@ -1131,7 +1157,17 @@ class SingaRep:
                 raise NotImplementedError(f"sonnx import: unsupported ONNX op {nd.op_type}")
         if fuse is None:
             fuse = os.environ.get("SINGA_AMD_SONNX_FUSE", "1") != "0"
-        self.fused = _fusion_plan(list(g.node), self.inits, self._consts, self.output_names) if fuse else {}
+        self.fused = _fusion_plan(list(g.node), self.inits, self._consts, self.output_names, soft) if fuse else {}
+        for st in self.fused.values():
+            if st.kind != "gelu":
+                continue
+            for i in st.members:
+                for nm in g.node[i].input:
+                    if nm in soft and nm not in self._consts:  # a matched GELU's constant: freeze it
+                        ten = self.inits[nm]
+                        ten.requires_grad = ten.stores_grad = False
+                        ten._host_np = soft_np[nm]
+                        self._consts.add(nm)
         self._skip = {i for st in self.fused.values() for i in st.members}
 
     @staticmethod

@@ -130,6 +130,18 @@ def test_distopt_equals_single_process(mode, bucket_mb):
             np.testing.assert_allclose(res[r][k], v, rtol=1e-4, atol=1e-5, err_msg=f"rank {r} {k}")
 
 
+def test_distopt_eight_gloo_ranks_equals_single_process():
+    """8 processes (the scaling run's world size) x 2 samples == one process x 16."""
+    from singa_amd import opt
+
+    X, Y = _data()
+    ref, _ = _train(_mlp_model(), X, Y, 4, opt.SGD(0.1, 0.9, weight_decay=1e-4))
+    res = run_ranks(_dp_rank, 8, "overlap", 0.001)
+    for r in range(8):
+        for k, v in ref.items():
+            np.testing.assert_allclose(res[r][k], v, rtol=2e-5, atol=2e-5, err_msg=f"rank {r} {k}")
+
+
 # ---------------------------------------------------------------- EASGD / RSync
 def _easgd_rank(rank, world, comm, sharded):
     from singa_amd.opt import SGD

@@ -171,6 +171,14 @@ def test_ps_sync_on_gpu_stores_through_synced_blobs(gpu):
         torch.cuda.synchronize()
         assert all(torch.allclose(p.data, torch.full_like(p.data, 2.5)) for p in st1.params)
         assert np.allclose(s.value(0), 1.5) and np.allclose(s.value(1), 1.5)
+        # group 0 trains after its bootstrap Put: the exchange must see the
+        # trained device weights, not the host copy taken at bootstrap
+        for p in st0.params:
+            p.data.fill_(7.0)
+        sy0.sync()
+        torch.cuda.synchronize()
+        assert all(torch.allclose(p.data, torch.full_like(p.data, 5.625)) for p in st0.params)
+        assert np.allclose(s.value(0), 2.875) and np.allclose(s.value(1), 2.875)
         sy0.client.stop()
         sy1.client.stop()
         assert s.wait_stop(5.0)

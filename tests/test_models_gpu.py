@@ -711,7 +711,7 @@ def test_lrn_folds_conv_relu_backward(gpu, monkeypatch):
         torch.testing.assert_close(g1, g0, rtol=1e-2, atol=5e-3)
 
 
-@pytest.mark.parametrize("small_gamma", [False, True])
+@pytest.mark.parametrize("small_gamma", [False, True, "gate_edge"])
 def test_bn_identity_sum_backward_matches_reduction(gpu, small_gamma):
     """Identity-sum BN backward (F.BN_WDOT): a BN(+ReLU) whose output feeds one
     conv takes sum(g~) from that conv's dgrad epilogue and sum(g~ xhat) from
@@ -719,7 +719,11 @@ def test_bn_identity_sum_backward_matches_reduction(gpu, small_gamma):
     bottlenecks (stride 1 and 2, 1x1 and 3x3 consumers) A/B against the
     reduction path: every parameter gradient and the input gradient agree to
     bf16 rounding.  small_gamma: some bn1/bn2 channels get |gamma| < tau, which
-    must switch those layers to the gated exact reduction."""
+    must switch those layers to the gated exact reduction.  gate_edge: every
+    third channel sits just inside the recovery gate (|gamma| = 1.2 tau,
+    beta = 15 |gamma|), where the recovered sum(g~ xhat) =
+    (<W, dW> - beta sum(g~)) / gamma cancels the most; dgamma and the input
+    gradient must still agree with the exact reduction."""
     from singa_amd import autograd as AG
     from singa_amd.models.resnet import Bottleneck
     from singa_amd.ops import functional as FF
@@ -754,7 +758,15 @@ def test_bn_identity_sum_backward_matches_reduction(gpu, small_gamma):
         return h, gr
 
     run(False)  # creates the parameters (no optimizer: a step leaves them unchanged)
-    if small_gamma:
+    if small_gamma == "gate_edge":
+        gam = 1.2 * FF.BN_WDOT_TAU
+        for b in blks:
+            for k, p in b.get_params().items():
+                if k in ("bn1.scale", "bn2.scale"):
+                    p.data[::3] = gam
+                if k in ("bn1.bias", "bn2.bias"):
+                    p.data[::3] = 15.0 * gam
+    elif small_gamma:
         for b in blks:
             for k, p in b.get_params().items():
                 if k in ("bn1.scale", "bn2.scale"):
@@ -767,4 +779,6 @@ def test_bn_identity_sum_backward_matches_reduction(gpu, small_gamma):
         for k, p in b.get_params().items():
             ab[f"{i}.{k}"] = rel_err(g_on[id(p)], g_off[id(p)])
     print(ab)
-    assert max(ab.values()) < (1e-3 if small_gamma else 3e-2), ab
+    assert max(ab.values()) < (1e-3 if small_gamma is True else 3e-2), ab
+    if small_gamma == "gate_edge":  # the input gradient too
+        assert rel_err(g_on[id(blks[0].conv1.W)], g_off[id(blks[0].conv1.W)]) < 3e-2

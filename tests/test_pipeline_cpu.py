@@ -178,3 +178,45 @@ def test_placed_net_across_processes_pipelined_equals_unplaced(kind):
     assert seen.keys() == ref_params.keys()  # the two stages hold disjoint halves
     for k in ref_params:
         np.testing.assert_allclose(seen[k], ref_params[k], rtol=1e-5, atol=1e-6, err_msg=k)
+
+
+# ------------------------------------------- loopback RCCL ranks (threads)
+def _stage_worker_chan(rank, world, comm, m, kind):
+    from singa_amd.config import schema
+    from singa_amd.runtime import Worker
+
+    cp = schema.new("ClusterProto")
+    cp.nworkers, cp.nprocs_per_group, cp.workspace = world, world, ""
+    w = Worker(schema.parse_text("ModelProto", _conf(True)), cp, comm=comm, log=lambda s: None, seed=0,
+               data_override=_OV, micro_batches=m, pipeline=kind)
+    _fix_batch(w)
+    w.run()
+    ch = w.train_net._pending
+    return [float(h[2][0]) for h in w.history if h[0] == "train"], _params(w), comm, ch.host_reads, ch.checked
+
+
+@pytest.mark.parametrize("kind", P.SCHEDULES)
+def test_placed_net_over_loopback_rccl_grouped_p2p(kind):
+    """The same 2-stage placed net on the REAL RcclCommunicator over the
+    native loopback communicator, whose ungrouped sends are rendezvous (an
+    RCCL-style crossing 1F1B exchange deadlocks there): the bridges' grouped,
+    deferred sends complete every schedule, equal the unplaced net, and read
+    headers on the host only on the first step."""
+    from singa_amd.parallel.loop import run_ranks as loop_ranks
+
+    ref_loss, ref_params = _reference()
+    m = 4
+    res = loop_ranks(_stage_worker_chan, 2, m, kind, timeout_s=30.0)
+    seen = {}
+    for r in range(2):
+        loss, params, comm, host_reads, checked = res[r]
+        np.testing.assert_allclose(loss, ref_loss, rtol=1e-5, atol=1e-6, err_msg=f"rank {r}")
+        seen.update(params)
+        assert comm.loopback and comm.stats["calls"] > 0
+        # stage 1 receives 2 bridges x m headed tensors per step (pool1 -> fc1
+        # activations and the labels): read on the host in step 1 only,
+        # bulk-checked in the other 4 steps; stage 0 receives the gradients,
+        # whose shapes it already knows (no headers)
+        assert (host_reads, checked) == ((2 * m, 4 * 2 * m) if r == 1 else (0, 0))
+    for k in ref_params:
+        np.testing.assert_allclose(seen[k], ref_params[k], rtol=1e-5, atol=1e-6, err_msg=k)

@@ -211,3 +211,105 @@ def test_sparse_topk_threshold_is_exact(gpu):
         thr = G.kth_largest_abs(g.to(gpu), k)
         ref = g.abs().kthvalue(g.numel() - k + 1).values
         assert float(thr) == float(ref)
+
+
+# ----------------------------------------------- loopback ranks on one GPU
+# N ranks as threads of this process, each on its own HIP stream, over the
+# native loopback communicator behind the REAL RcclCommunicator: the wrapper's
+# comm-stream fork / join, DistOpt's fp32 and bf16 bucket staging and the
+# sharded EASGD centre at the world sizes of the 8-GPU run
+# (csrc/comm/loop_comm.cpp, parallel/loop.py).
+@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("bf16", [False, True])
+def test_loopback_distopt_equals_single_process_step(gpu, world, bf16):
+    from singa_amd.parallel.loop import run_ranks as loop_ranks
+
+    res = loop_ranks(_mlp_step, world, 3, bf16, device=torch.device("cuda", 0), timeout_s=120.0)
+    ref = _single_process(gpu)
+    for k in ref:
+        for r in range(world):
+            np.testing.assert_array_equal(res[r][k], res[0][k], err_msg=f"{k} rank {r}")  # replicas identical
+        if bf16:
+            np.testing.assert_allclose(res[0][k], ref[k], rtol=2e-2, atol=2e-3, err_msg=k)
+        else:
+            np.testing.assert_allclose(res[0][k], ref[k], rtol=2e-5, atol=2e-6, err_msg=k)
+
+
+def _easgd_gpu_rank(rank, world, comm, sharded):
+    from singa_amd.opt import SGD
+    from singa_amd.parallel.easgd import ElasticSync
+    from singa_amd.tensor import Tensor
+
+    g = torch.Generator().manual_seed(0)
+    p = Tensor(data=torch.randn(1000, generator=g).to(gpu_dev()), requires_grad=True, stores_grad=True)
+    q = Tensor(data=torch.randn(30, 7, generator=g).to(gpu_dev()), requires_grad=True, stores_grad=True)
+    st = SGD(0.1).attach([p, q])
+    es = ElasticSync(st, comm, moving_rate=0.5, sharded=sharded)
+    es.bootstrap()
+    c0 = st.w.clone()
+    st.w.add_(float(rank + 1))
+    wb = st.w.clone()
+    es.sync()
+    full = torch.empty_like(st.w)
+    if es.sharded:
+        comm.all_gather(full, es.centre)
+    else:
+        full.copy_(es.centre)
+    torch.cuda.current_stream().synchronize()
+    return c0.cpu().numpy(), wb.cpu().numpy(), st.w.cpu().numpy(), full.cpu().numpy(), es.alpha
+
+
+def gpu_dev():
+    return torch.device("cuda", 0)
+
+
+@pytest.mark.parametrize("sharded", [False, True])
+def test_loopback_easgd_eight_ranks(gpu, sharded):
+    """Sharded (reduce-scatter / all-gather over 8 ranks) and replicated
+    centres follow c' = c + sum_r alpha (w_r - c), w_r' = w_r - alpha (w_r - c)."""
+    from singa_amd.parallel.loop import run_ranks as loop_ranks
+
+    res = loop_ranks(_easgd_gpu_rank, 8, sharded, device=gpu_dev(), timeout_s=120.0)
+    c0, alpha = res[0][0], res[0][4]
+    ds = [alpha * (wb - c0) for _, wb, _, _, _ in res]
+    for r, (_, wb, wa, c, _) in enumerate(res):
+        np.testing.assert_allclose(wa, wb - ds[r], rtol=1e-5, atol=1e-5)
+        np.testing.assert_allclose(c, c0 + sum(ds), rtol=1e-5, atol=1e-5)
+
+
+def _easgd_rounds_rank(rank, world, comm, sharded, overlap):
+    from singa_amd.opt import SGD
+    from singa_amd.parallel.easgd import ElasticSync
+    from singa_amd.tensor import Tensor
+
+    g = torch.Generator().manual_seed(0)
+    p = Tensor(data=torch.randn(4096, generator=g).to(gpu_dev()), requires_grad=True, stores_grad=True)
+    st = SGD(0.1).attach([p])
+    es = ElasticSync(st, comm, moving_rate=0.9, sharded=sharded, overlap=overlap)
+    es.bootstrap()
+    drift = torch.randn(4096, generator=torch.Generator().manual_seed(rank + 1)).to(gpu_dev())
+    for step in range(6):
+        st.w.add_(drift)  # "training" between syncs, on the compute stream
+        es.sync()
+    es.wait()
+    full = torch.empty_like(st.w)
+    if es.sharded:
+        comm.all_gather(full, es.centre)
+    else:
+        full.copy_(es.centre)
+    torch.cuda.current_stream().synchronize()
+    return st.w.cpu().numpy(), full.cpu().numpy(), es._pending is None
+
+
+@pytest.mark.parametrize("sharded", [False, True])
+def test_loopback_easgd_overlapped_equals_synchronous(gpu, sharded):
+    """The overlapped exchange (comm stream, joined at the next sync) gives
+    the synchronous schedule's weights and centre exactly, at 4 ranks."""
+    from singa_amd.parallel.loop import run_ranks as loop_ranks
+
+    sync = loop_ranks(_easgd_rounds_rank, 4, sharded, False, device=gpu_dev(), timeout_s=120.0)
+    ovl = loop_ranks(_easgd_rounds_rank, 4, sharded, True, device=gpu_dev(), timeout_s=120.0)
+    for r in range(4):
+        np.testing.assert_array_equal(ovl[r][0], sync[r][0])
+        np.testing.assert_array_equal(ovl[r][1], sync[r][1])
+        assert ovl[r][2]

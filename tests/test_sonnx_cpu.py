@@ -2,6 +2,8 @@
 match the source model), fine-tuning an imported graph, and hand-built ONNX
 graphs through the importer (oracle: PyTorch fp32 of the same op).
 The reference has no ONNX support: parity unpinned, round-trip tested."""
+import math
+
 import numpy as np
 import pytest
 import torch
@@ -260,3 +262,36 @@ def test_import_fusion_respects_other_consumers():
         autograd.training = False
         got = rep.run([Tensor(data=torch.from_numpy(x), requires_grad=False)])
         np.testing.assert_allclose(got[0].data.numpy(), x @ w + b, rtol=1e-5, atol=1e-5)
+
+
+def test_import_scalar_params_stay_learnable():
+    """An untagged one-element initializer feeding Mul (a learnable
+    temperature) is a parameter; the GELU chain's sqrt 2 / 1 / 0.5 are frozen
+    only because the fused pattern consumed them; the exporter's tagged
+    constants are never parameters."""
+    x = R.randn(4, 6).astype(np.float32)
+    temp = np.asarray([1.7], np.float32)
+    m = _graph([sonnx.make_node("Mul", ["x0", "temp"], ["y"])], [("x0", x)], ["y"], [("temp", temp)])
+    rep = sonnx.prepare(m)
+    assert "temp" in rep.params() and not rep.is_const("temp")
+    autograd.training = True
+    out = rep.run([Tensor(data=torch.from_numpy(x), requires_grad=False)])[0]
+    grads = {p.name: g.data for p, g in autograd.backward(autograd.reduce_sum(out, keepdims=0))}
+    autograd.training = False
+    np.testing.assert_allclose(float(grads["temp"].reshape(-1)[0]), x.sum(), rtol=1e-5)
+    # untagged GELU constants: frozen by the matched pattern
+    sq, one, half = (np.asarray([v], np.float32) for v in (math.sqrt(2.0), 1.0, 0.5))
+    nodes = [sonnx.make_node("Div", ["x0", "sq"], ["a"]), sonnx.make_node("Erf", ["a"], ["b"]),
+             sonnx.make_node("Add", ["b", "one"], ["c"]), sonnx.make_node("Mul", ["x0", "c"], ["d"]),
+             sonnx.make_node("Mul", ["d", "half"], ["y"])]
+    rep = sonnx.prepare(_graph(nodes, [("x0", x)], ["y"], [("sq", sq), ("one", one), ("half", half)]))
+    assert [st.kind for st in rep.fused.values()] == ["gelu"]
+    assert all(rep.is_const(n) for n in ("sq", "one", "half")) and not rep.params()
+    # exporter-tagged initializers (bert's GELU / attention constants) are never parameters
+    from singa_amd.models import bert
+    ids = tensor.from_numpy(np.random.RandomState(0).randint(0, 1000, (2, 16)).astype(np.int64))
+    mb = bert.bert_tiny(dropout=0.0)
+    mb.compile([ids], is_train=False)
+    mp = sonnx.to_onnx(mb, [ids])
+    tagged = {t.name for t in mp.graph.initializer if t.doc_string == sonnx.CONST_TAG}
+    assert tagged and not (tagged & set(sonnx.prepare(mp, fuse=False).params()))

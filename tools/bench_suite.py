@@ -8,6 +8,16 @@ ResNet-50 headline):
 * ``bert_sonnx``  -- BERT-base exported to ONNX, re-imported with sonnx and
                      fine-tuned through autograd (MatMul/Softmax/LayerNorm) (sequences/s).
 
+Multi-GPU (BASELINE config #4, "AlexNet large-batch on 8x MI355X (bucket
+fusion)"): launched under torchrun, ``alexnet`` runs one rank per GPU with
+DistOpt over the native RCCL communicator -- per-GPU batch fixed (weak
+scaling), ~244 MB of fp32 gradients per step in link-sized buckets overlapped
+with the backward -- and rank 0 reports the whole-job images/s (slowest
+rank's clock) with the exchange diagnostics:
+
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \
+        tools/bench_suite.py --which alexnet [--grad-dtype bf16] [--bucket-mb 32]
+
 Every step is a full training step (forward, backward, optimizer update);
 inputs are synthetic and weights random-init.  One JSON line per benchmark
 on stdout (``--out`` appends them to a file too).
@@ -84,23 +94,60 @@ def bench_mlp(a, gpu):
                 dtype="fp32", optimizer="SGD momentum 0.9", final_loss=round(float(_snap(loss.data)), 4))
 
 
+def _world():
+    return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
 def bench_alexnet(a):
     from singa_amd import device, opt, tensor
     from singa_amd.models import alexnet
+    from singa_amd.parallel import DistOpt, init_distributed
 
-    dev = device.create_rocm_gpu()
-    dev.SetRandSeed(0)
+    world, rank, local = _world()
+    if world > 1:
+        torch.cuda.set_device(local % torch.cuda.device_count())
+        if a.rccl_channels > 0:
+            os.environ.setdefault("NCCL_MAX_NCHANNELS", str(a.rccl_channels))
+    dev = device.create_rocm_gpu_on(local % max(1, torch.cuda.device_count()), set_default=True)
+    dev.SetRandSeed(rank)
+    comm = init_distributed(rank=rank, world_size=world, local_rank=local) if world > 1 else None
     B = a.batch or 512
     m = alexnet.create_model(num_classes=1000, compute_dtype=torch.bfloat16)
-    rng = np.random.RandomState(0)
+    rng = np.random.RandomState(rank)
     x = tensor.from_numpy(rng.standard_normal((B, 3, 224, 224)).astype(np.float32)).to_device(dev)
     y = tensor.from_numpy(rng.randint(0, 1000, B).astype(np.int32)).to_device(dev)
-    m.set_optimizer(opt.SGD(0.01, 0.9, weight_decay=5e-4))
+    o = opt.SGD(0.01, 0.9, weight_decay=5e-4)
+    if comm is not None:
+        o = DistOpt(o, comm=comm, bucket_mb=a.bucket_mb, first_bucket_mb=a.first_bucket_mb,
+                    grad_dtype=torch.bfloat16 if a.grad_dtype == "bf16" else torch.float32)
+        o.time_exposed = a.no_graph  # event timing only in eager mode (not inside a captured graph)
+    m.set_optimizer(o)
     m.compile([x], is_train=True, use_graph=not a.no_graph)
     m.train()
-    dt, (_, loss) = _time(lambda: m(x, y), a.steps, a.warmup, torch.cuda.synchronize)
-    return _rec("alexnet", "images/s", B, dt, model="AlexNet-224 (LRN, dropout 0.5)", batch=B,
-                optimizer="SGD momentum 0.9 wd 5e-4", final_loss=round(float(_snap(loss.data)), 4))
+
+    def sync():
+        torch.cuda.synchronize()
+        if comm is not None:
+            comm.barrier()
+    dt, (_, loss) = _time(lambda: m(x, y), a.steps, a.warmup, sync)
+    extra = {}
+    if comm is not None:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev.torch_device)
+        comm.all_reduce(t, op="max")
+        dt = float(t.item())
+        ex = o.exposed_comm_ms()
+        extra = {"parallelism": f"dp{world}", "n_gpus": world, "global_batch": world * B,
+                 "comm": {"class": type(comm).__name__, "ranks": comm.world_size,
+                          "rccl_version": getattr(comm, "version", None), "grad_dtype": a.grad_dtype,
+                          "buckets": len(o.buckets), "bucket_mb": a.bucket_mb,
+                          "exchange_mb_per_step": round(o.exchange_bytes() / 2**20, 2),
+                          "exposed_comm_ms_per_step": None if ex is None else round(ex, 3),
+                          "env": {k: os.environ[k] for k in ("NCCL_MAX_NCHANNELS", "NCCL_MIN_NCHANNELS")
+                                  if k in os.environ}}}
+    rec = _rec("alexnet", "images/s", world * B, dt, model="AlexNet-224 (LRN, dropout 0.5)", batch=B,
+               optimizer="SGD momentum 0.9 wd 5e-4", final_loss=round(float(_snap(loss.data)), 4), **extra)
+    return rec if rank == 0 else None
 
 
 def _bert_inputs(dev, B, S, vocab):
@@ -163,11 +210,17 @@ def main():
     ap.add_argument("--seq", type=int, default=128)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--out", default="")
+    ap.add_argument("--grad-dtype", choices=("fp32", "bf16"), default="fp32")
+    ap.add_argument("--bucket-mb", type=float, default=32.0)
+    ap.add_argument("--first-bucket-mb", type=float, default=4.0)
+    ap.add_argument("--rccl-channels", type=int, default=16)
     a = ap.parse_args()
     fns = {"mlp_cpu": lambda: bench_mlp(a, False), "mlp_gpu": lambda: bench_mlp(a, True),
            "alexnet": lambda: bench_alexnet(a), "bert": lambda: bench_bert(a), "bert_sonnx": lambda: bench_bert_sonnx(a)}
     for w in a.which.split(","):
         rec = fns[w]()
+        if rec is None:  # non-zero rank of a torchrun job
+            continue
         line = json.dumps(rec)
         print(line, flush=True)
         if a.out:
