@@ -32,6 +32,7 @@ from typing import Callable, Dict, Iterator, List, Optional, Sequence, Tuple
 import numpy as np
 import torch
 
+from . import memory as _mem
 from . import tensor as _tensor
 from .ops import functional as F
 from .ops import glue as G
@@ -191,6 +192,10 @@ def _accum(a, b):
         return b
     if b is None:
         return a
+    if isinstance(a, F.MaskedGrad):  # a lazy residual gradient meets another contribution
+        a = a.materialize()
+    if isinstance(b, F.MaskedGrad):
+        b = b.materialize()
     if a.shape != b.shape:
         b = G.reshape(b, a.shape)
     if a.dtype != b.dtype:
@@ -274,6 +279,8 @@ def backward(y, dy=None) -> Iterator[Tuple[Tensor, Tensor]]:
         for d in dys_:
             if d is not None:
                 owned.discard(id(d))
+        # a lazy residual gradient nobody absorbed reaches its producer: make it a tensor
+        dys_ = [d.materialize() if isinstance(d, F.MaskedGrad) else d for d in dys_]
         if all(d is None for d in dys_) and not getattr(op, "always_run", False):
             dxs = (None,) * len(op.src)
         else:
@@ -770,7 +777,8 @@ class BatchNorm2d(Operator):
     def backward(self, dy):
         tg, tb = self.grad_target(1), self.grad_target(2)
         dx, dg, db, dres = F.batchnorm_bwd(self.x, dy, self.gamma, self.st, self.y, need_dres=self.has_residual,
-                                           relu=self.relu, dg_out=tg, db_out=tb, beta=getattr(self, "beta", None))
+                                           relu=self.relu, dg_out=tg, db_out=tb, beta=getattr(self, "beta", None),
+                                           lazy_dres=True)
         self.x = self.y = self.st = self.beta = None
         out = [dx, ACCUMULATED if tg is not None else dg, ACCUMULATED if tb is not None else db]
         if self.has_residual:
@@ -1792,7 +1800,7 @@ def upsample(x, mode, scales):
         for s, r in zip(a.shape, sc):
             inter += [s, r]
             src += [s, 1]
-        out = torch.empty(inter, dtype=a.dtype, device=a.device)
+        out = _mem.empty(inter, dtype=a.dtype, device=a.device)
         G.copy_(out, a.reshape(src).expand(*inter))
         return out.reshape([s * r for s, r in zip(a.shape, sc)]), tuple(a.shape)
 

@@ -24,6 +24,7 @@ void sg_unary_fwd(int, const void*, void*, int64_t, int, float, hipStream_t);
 void sg_unary_bwd(int, const void*, const void*, const void*, void*, int64_t, int, float, hipStream_t);
 void sg_add_act(const void*, const void*, void*, int64_t, int, float, float, int, hipStream_t);
 void sg_relu_bwd_from_y(const void*, const void*, void*, int64_t, int, hipStream_t);
+void sg_mask_bits_apply(const void*, const void*, void*, int64_t, hipStream_t);
 void sg_cast(const void*, int, void*, int, int64_t, hipStream_t);
 void sg_dropout_fwd(const void*, void*, void*, int64_t, int, float, uint64_t, uint64_t, const void*, hipStream_t);
 void sg_dropout_bwd(const void*, const void*, void*, int64_t, int, float, hipStream_t);
@@ -102,6 +103,8 @@ void sg_conv_dgrad_bn_ex(const void*, const void*, void*, int, int, int, int, in
 void sg_bn_bwd_from_ws(const void*, const void*, const void*, const void*, const void*, const void*, const void*,
                        const void*, const void*, int, void*, void*, void*, void*, void*, int64_t, int, int, int,
                        hipStream_t);
+int sg_conv_dgrad_res(const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int, int,
+                      int, int, void*, const void*, const void*, hipStream_t);
 void sg_conv_dgrad(const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int, int,
                    int, int, int, float, void*, hipStream_t);
 void sg_conv_wgrad(const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int, int,
@@ -186,6 +189,9 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("add_act", [](P a, P b, P y, int64_t n, int dt, float al, float be, int relu, P s) {
     sg_add_act(CV(a), CV(b), V(y), n, dt, al, be, relu, S(s)); CHK("add_act");
+  });
+  m.def("mask_bits_apply", [](P g, P mask, P out, int64_t n, P s) {
+    sg_mask_bits_apply(CV(g), CV(mask), V(out), n, S(s)); CHK("mask_bits_apply");
   });
   m.def("relu_bwd_from_y", [](P y, P dy, P dx, int64_t n, int dt, P s) {
     sg_relu_bwd_from_y(CV(y), CV(dy), V(dx), n, dt, S(s)); CHK("relu_bwd_from_y");
@@ -376,6 +382,14 @@ PYBIND11_MODULE(_C, m) {
     sg_conv_dgrad(CV(dy), CV(wt), V(dx), N, H, W, C, K, R, Sd, Ho, Wo, sh, sw, ph, pw, dh, dw, out_mode, beta,
                   V(wtbuf), S(s));
     CHK("conv_dgrad_acc");
+  });
+  // dx = dgrad + res_g * bit(res_mask) (bf16; returns 0 when the shape needs the caller to materialise)
+  m.def("conv_dgrad_res", [](P dy, P wt, P dx, int N, int H, int W, int C, int K, int R, int Sd, int Ho, int Wo,
+                             int sh, int sw, int ph, int pw, int dh, int dw, P wtbuf, P res_g, P res_mask, P s) {
+    const int r = sg_conv_dgrad_res(CV(dy), CV(wt), V(dx), N, H, W, C, K, R, Sd, Ho, Wo, sh, sw, ph, pw, dh, dw,
+                                    V(wtbuf), CV(res_g), CV(res_mask), S(s));
+    CHK("conv_dgrad_res");
+    return r;
   });
   m.def("conv_wgrad", [](P x, P dy, P dw_out, int N, int H, int W, int C, int K, int R, int Sd, int Ho, int Wo,
                          int sh, int sw, int ph, int pw, int dh, int dw, int splits, P s) {

@@ -256,6 +256,24 @@ __global__ void relu_bwd_from_y_k(const T* __restrict__ y, const T* __restrict__
   if (blockIdx.x == 0 && t < n) dx[t] = to_f32(y[t]) > 0.f ? dy[t] : from_f32<T>(0.f);
 }
 
+// out = g * bit(mask): the masked gradient of a fused BN(+residual)+ReLU
+// output, from its 1-bit ReLU mask (byte i holds elements 8i..8i+7, bit r =
+// element 8i+r); n % 8 == 0 (host-checked), 16-byte vectors
+__global__ void mask_bits_apply_k(const uint4* __restrict__ g, const uint8_t* __restrict__ mask, uint4* __restrict__ out,
+                                  int64_t nv) {
+  SG_GRID_STRIDE(i, nv) {
+    const unsigned m = mask[i];
+    const uint4 v = g[i];
+    unsigned w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const unsigned lo = (m >> (2 * j)) & 1u ? 0x0000ffffu : 0u, hi = (m >> (2 * j + 1)) & 1u ? 0xffff0000u : 0u;
+      w[j] &= lo | hi;
+    }
+    out[i] = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
 template <typename TI, typename TO>
 __global__ void cast_k(const TI* __restrict__ x, TO* __restrict__ y, int64_t n) {
   const int64_t nv = n / 4;
@@ -448,6 +466,11 @@ void sg_add_act(const void* a, const void* b, void* y, int64_t n, int dtype, flo
                 hipStream_t s) {
   DISPATCH_FT(dtype, hipLaunchKernelGGL(add_act_k<T>, dim3(sg_grid(n / Vec<T>::N + 1)), dim3(256), 0, s,
                                         (const T*)a, (const T*)b, (T*)y, n, alpha, beta, relu));
+}
+void sg_mask_bits_apply(const void* g, const void* mask, void* out, int64_t n, hipStream_t s) {
+  const int64_t nv = n / 8;
+  hipLaunchKernelGGL(mask_bits_apply_k, dim3(sg_grid(nv)), dim3(256), 0, s, (const uint4*)g, (const uint8_t*)mask,
+                     (uint4*)out, nv);
 }
 void sg_relu_bwd_from_y(const void* y, const void* dy, void* dx, int64_t n, int dtype, hipStream_t s) {
   DISPATCH_FT(dtype, hipLaunchKernelGGL(relu_bwd_from_y_k<T>, dim3(sg_grid(n / Vec<T>::N + 1)), dim3(256), 0, s,

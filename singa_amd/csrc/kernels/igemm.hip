@@ -106,6 +106,13 @@ struct GemmArgs {
   // the 1-bit map bnb_mask [rows][C/8] written by its forward apply
   // stats_mode 3: only sum(g) over the mask bits (the identity-sum BN backward)
   int stats_mode;
+  // residual-gradient accumulate (bf16 LDS-staged epilogue, beta == 0, no
+  // stats): out += res_g * bit(res_mask) -- the gradient a residual
+  // BN(+ReLU) passes to its shortcut input is its masked output gradient;
+  // the consuming conv's dgrad adds it from (dy, 1-bit mask) directly, so
+  // the BN backward never writes it as a tensor
+  const bf16* res_g;
+  const uint8_t* res_mask;
   const uint8_t* bnb_mask;
   const bf16* bnb_x;
   const float *bnb_mean, *bnb_invstd, *bnb_scale, *bnb_shift;
@@ -1270,6 +1277,9 @@ static int g_tune[10] = {5, 1, 1, 0, 0, 1, 8, 1, 0, 0};
 // each set and consume their own flag, so one thread's set can never be
 // taken by another thread's dgrad
 static thread_local int g_wt_ready = 0;
+// one-shot (per OS thread): the next dgrad adds this masked residual gradient
+static thread_local const bf16* g_res_g = nullptr;
+static thread_local const uint8_t* g_res_mask = nullptr;
 
 constexpr int stages_c(int BM, int BN, int STAGES) { return STAGES * (BM + BN) * BK * 2; }
 
@@ -1414,7 +1424,7 @@ static void launch(const GemmArgs& p, int M, int splits, hipStream_t s, int batc
       // persistent short-K kernel (knob 9): 1x1-conv forward / data-gradient shapes
       if (OUT == OUT_BF16 && AM == LM_KMAJOR && BMODE == LM_KMAJOR && g_tune[9] && g_tune[4] == 0 &&
           !p.out_phase && zdim <= 1 && batch == 1 && p.K <= 128 && (p.N & 127) == 0 && !p.bias && !p.relu &&
-          p.alpha == 1.f && p.stats_mode == 0 && !(p.stats && p.stats_det) && g_tune[1] &&
+          p.alpha == 1.f && p.stats_mode == 0 && !(p.stats && p.stats_det) && g_tune[1] && !p.res_g &&
           (p.ldc & 7) == 0 && (long)((M + 127) / 128) * (p.N / 128) >= 2048) {
         const int tiles_m = (M + 127) / 128;
         if (p.K <= 64) launch_sk<1>(p, tiles_m, p.N / 128, s);
@@ -1612,6 +1622,27 @@ void sg_conv_dgrad_bn(const void* dy, const void* w, void* dx, int N, int H, int
                       bn_mean, bn_invstd, bn_scale, bn_shift, nullptr, s);
 }
 
+// dx = dgrad(dy, w) + res_g * bit(res_mask) (bf16, fresh dx: no beta
+// read): the data gradient of a residual block's input, with the masked
+// output gradient of the block's residual BN(+ReLU) -- the shortcut path's
+// gradient -- added in the epilogue instead of being written by the BN
+// backward and read back.  Returns 0 (nothing launched) when the shape does
+// not take the LDS-staged epilogue (C % 8, stride 1 only): the caller then
+// materialises the residual gradient itself.
+int sg_conv_dgrad_res(const void* dy, const void* w, void* dx, int N, int H, int W, int C, int K, int R, int S,
+                      int Ho, int Wo, int sh, int sw, int ph, int pw, int dh, int dw, void* wt, const void* res_g,
+                      const void* res_mask, hipStream_t s) {
+  if ((C & 7) != 0 || !g_tune[1] || sh != 1 || sw != 1 || dh != 1 || dw != 1) {
+    g_wt_ready = 0;
+    return 0;
+  }
+  g_res_g = (const bf16*)res_g;
+  g_res_mask = (const uint8_t*)res_mask;
+  sg_conv_dgrad_bn_ex(dy, w, dx, N, H, W, C, K, R, S, Ho, Wo, sh, sw, ph, pw, dh, dw, OUT_BF16, 0.f, wt, nullptr,
+                      nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, s);
+  return 1;
+}
+
 // bn_mask != nullptr and bn_x == nullptr: the epilogue sums only the
 // ReLU-masked gradient (stats_mode 3, the identity-sum BN backward).
 // bn_mask != nullptr: the producer BN is a residual BN(+ReLU) whose ReLU mask
@@ -1624,6 +1655,10 @@ void sg_conv_dgrad_bn_ex(const void* dy, const void* w, void* dx, int N, int H, 
   const bool wt_ready = g_wt_ready;  // one-shot: wt already holds the K-major weights (batched pre-pass)
   g_wt_ready = 0;
   GemmArgs p{};
+  p.res_g = g_res_g;  // one-shot residual-gradient source (sg_conv_dgrad_res)
+  p.res_mask = g_res_mask;
+  g_res_g = nullptr;
+  g_res_mask = nullptr;
   if (bn_ws && out_mode == OUT_BF16 && (beta == 0.f || bn_mask) && (C & 7) == 0 && g_tune[1] &&
       !sg_bn_deterministic()) {
     p.stats = (float*)bn_ws;

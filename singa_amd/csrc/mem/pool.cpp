@@ -27,6 +27,8 @@
 #include <cstring>
 #include <map>
 #include <memory>
+#include <set>
+#include <tuple>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -77,70 +79,132 @@ struct Stats {
   uint64_t in_use = 0, reserved = 0, peak_in_use = 0;
 };
 
-struct Block {
-  void* ptr;
+// A device block: its size class, the stream it was allocated on (the stream
+// whose order makes reuse safe), the pool that owns it (0 = the default
+// pool, > 0 = a private pool of one HIP graph) and the other streams that
+// used it (record_stream): a free with foreign uses waits for events.
+struct BlockInfo {
   size_t size;
-  hipEvent_t ev;  // pending: recorded on the freeing stream
+  uintptr_t stream;
+  int pool;
+  std::vector<uintptr_t> uses;
 };
+struct Pending {
+  void* ptr;
+  BlockInfo info;
+  std::vector<hipEvent_t> evs;
+};
+
+thread_local int t_pool = 0;  // private pool of the capture this thread is running (0: default pool)
 
 class DevicePool {
  public:
   explicit DevicePool(int dev) : dev_(dev) {}
 
-  void* alloc(size_t n) {
+  // Stream-ordered caching: a block freed by its allocation stream is reused
+  // at once by the next allocation on that SAME stream (later work on the
+  // stream is ordered after every use of the old tensor) -- no event, no
+  // host sync on the hot path.  Allocations while a HIP graph is captured
+  // come from that graph's private pool and stay with it.
+  void* alloc(size_t n, uintptr_t stream) {
     const size_t sz = round_size(n);
+    const int pool = t_pool;
     std::lock_guard<std::mutex> g(mu_);
     ++st_.allocs;
-    reap_locked();
-    auto it = free_.find(sz);
+    if (!pending_.empty()) reap_locked();
     void* p = nullptr;
+    auto it = free_.find(std::make_tuple(pool, stream, sz));
     if (it != free_.end() && !it->second.empty()) {
       p = it->second.back();
       it->second.pop_back();
       ++st_.hits;
     } else {
-      int cur = 0;
-      hip_check(hipGetDevice(&cur), "hipGetDevice");
-      if (cur != dev_) hip_check(hipSetDevice(dev_), "hipSetDevice");
-      hipError_t e = hipMalloc(&p, sz);
-      if (e != hipSuccess) {  // out of memory: drop the cache once and retry
-        release_locked();
-        e = hipMalloc(&p, sz);
-      }
-      if (cur != dev_) hipSetDevice(cur);
-      hip_check(e, "hipMalloc");
-      ++st_.driver_allocs;
-      st_.reserved += sz;
+      p = driver_alloc_locked(sz);
     }
-    sizes_[p] = sz;
+    live_[p] = BlockInfo{sz, stream, pool, {}};
     st_.in_use += sz;
     if (st_.in_use > st_.peak_in_use) st_.peak_in_use = st_.in_use;
     return p;
   }
 
-  // stream != 0: the block may still be read / written by work queued on that
-  // stream; it is reused only after an event recorded there has completed
-  void free(void* p, uintptr_t stream) {
+  void free(void* p) {
     std::lock_guard<std::mutex> g(mu_);
-    auto it = sizes_.find(p);
-    if (it == sizes_.end()) throw std::runtime_error("DevicePool::free: pointer not from this pool");
-    const size_t sz = it->second;
-    sizes_.erase(it);
+    auto it = live_.find(p);
+    if (it == live_.end()) throw std::runtime_error("DevicePool::free: pointer not from this pool");
+    BlockInfo b = std::move(it->second);
+    live_.erase(it);
     ++st_.frees;
-    st_.in_use -= sz;
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (stream && hipStreamIsCapturing((hipStream_t)stream, &cs) == hipSuccess &&
-        cs != hipStreamCaptureStatusNone) {
-      // freed while its stream is being captured into a HIP graph: a replay
-      // may still address it, so it is never reused (returned by release())
-      captured_.push_back(Block{p, sz, nullptr});
-    } else if (stream) {
+    st_.in_use -= b.size;
+    if (b.pool > 0 && dead_.count(b.pool)) b.pool = 0;  // its graph is gone: back to the default pool
+    const bool capt = capturing(b.stream);
+    if (capt && b.pool == 0) {
+      // a default-pool block whose last tensor died while its stream is being
+      // captured: the graph may address it on every replay, so it is never
+      // handed out again (and never returned to the driver)
+      parked_.push_back(std::make_pair(p, b.size));
+      return;
+    }
+    if (b.uses.empty()) {
+      free_[std::make_tuple(b.pool, b.stream, b.size)].push_back(p);
+      return;
+    }
+    if (capt || anyc(b.uses)) {  // cross-stream use inside a capture: keep it out of circulation with its pool
+      held_[b.pool].push_back(std::make_pair(p, b.size));
+      return;
+    }
+    Pending pd{p, b, {}};
+    for (uintptr_t s : b.uses) {
       hipEvent_t ev;
       hip_check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
-      hip_check(hipEventRecord(ev, (hipStream_t)stream), "hipEventRecord");
-      pending_.push_back(Block{p, sz, ev});
-    } else {
-      free_[sz].push_back(p);
+      hip_check(hipEventRecord(ev, (hipStream_t)s), "hipEventRecord");
+      pd.evs.push_back(ev);
+    }
+    pending_.push_back(std::move(pd));
+  }
+
+  // the block containing ptr (a view may point inside it) is also used on stream s
+  void record_stream(void* ptr, uintptr_t s) {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = live_.upper_bound(ptr);
+    if (it == live_.begin()) return;
+    --it;
+    if ((char*)ptr >= (char*)it->first + it->second.size) return;  // not a pool block
+    if (s == it->second.stream) return;
+    for (uintptr_t u : it->second.uses)
+      if (u == s) return;
+    it->second.uses.push_back(s);
+  }
+  bool owns(void* ptr) {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = live_.upper_bound(ptr);
+    if (it == live_.begin()) return false;
+    --it;
+    return (char*)ptr < (char*)it->first + it->second.size;
+  }
+
+  int new_pool() {
+    std::lock_guard<std::mutex> g(mu_);
+    return ++last_pool_;
+  }
+  // the graph of private pool id is destroyed: its cached blocks go back to
+  // the driver, its live blocks (tensors that outlived the graph) rejoin the
+  // default pool when they are freed
+  void release_pool(int id) {
+    if (id <= 0) return;
+    std::lock_guard<std::mutex> g(mu_);
+    dead_.insert(id);
+    for (auto it = free_.begin(); it != free_.end();) {
+      if (std::get<0>(it->first) == id) {
+        for (void* q : it->second) driver_free_locked(q, std::get<2>(it->first));
+        it = free_.erase(it);
+      } else {
+        ++it;
+      }
+    }
+    auto h = held_.find(id);
+    if (h != held_.end()) {
+      for (auto& b : h->second) driver_free_locked(b.first, b.second);
+      held_.erase(h);
     }
   }
 
@@ -161,43 +225,89 @@ class DevicePool {
     d["reserved_bytes"] = st_.reserved;
     d["peak_in_use_bytes"] = st_.peak_in_use;
     d["pending_frees"] = (uint64_t)pending_.size();
+    d["parked_blocks"] = (uint64_t)parked_.size();
+    d["live_blocks"] = (uint64_t)live_.size();
     return d;
+  }
+  void reset_peak() {
+    std::lock_guard<std::mutex> g(mu_);
+    st_.peak_in_use = st_.in_use;
   }
   int device() const { return dev_; }
 
  private:
+  static bool capturing(uintptr_t s) {
+    if (!s) return false;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing((hipStream_t)s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
+  }
+  static bool anyc(const std::vector<uintptr_t>& v) {
+    for (uintptr_t s : v)
+      if (capturing(s)) return true;
+    return false;
+  }
+  void* driver_alloc_locked(size_t sz) {
+    int cur = 0;
+    hip_check(hipGetDevice(&cur), "hipGetDevice");
+    if (cur != dev_) hip_check(hipSetDevice(dev_), "hipSetDevice");
+    void* p = nullptr;
+    hipError_t e = hipMalloc(&p, sz);
+    if (e != hipSuccess) {  // out of memory: drop the default pool's cache once and retry
+      (void)hipGetLastError();
+      release_locked();
+      e = hipMalloc(&p, sz);
+    }
+    if (cur != dev_) hipSetDevice(cur);
+    hip_check(e, "hipMalloc");
+    ++st_.driver_allocs;
+    st_.reserved += sz;
+    return p;
+  }
+  void driver_free_locked(void* p, size_t sz) {
+    hipFree(p);
+    st_.reserved -= sz;
+  }
   void reap_locked() {
     for (size_t i = 0; i < pending_.size();) {
-      if (hipEventQuery(pending_[i].ev) == hipSuccess) {
-        hipEventDestroy(pending_[i].ev);
-        free_[pending_[i].size].push_back(pending_[i].ptr);
-        pending_[i] = pending_.back();
+      bool done = true;
+      for (hipEvent_t ev : pending_[i].evs)
+        if (hipEventQuery(ev) != hipSuccess) {
+          done = false;
+          break;
+        }
+      if (done) {
+        for (hipEvent_t ev : pending_[i].evs) hipEventDestroy(ev);
+        const BlockInfo& b = pending_[i].info;
+        const int pool = (b.pool > 0 && dead_.count(b.pool)) ? 0 : b.pool;
+        free_[std::make_tuple(pool, b.stream, b.size)].push_back(pending_[i].ptr);
+        pending_[i] = std::move(pending_.back());
         pending_.pop_back();
       } else {
         ++i;
       }
     }
   }
-  void release_locked() {
+  void release_locked() {  // the default pool's cached blocks (never parked / private ones)
     reap_locked();
-    for (auto& b : captured_) {
-      hipFree(b.ptr);
-      st_.reserved -= b.size;
-    }
-    captured_.clear();
-    for (auto& kv : free_)
-      for (void* p : kv.second) {
-        hipFree(p);
-        st_.reserved -= kv.first;
+    for (auto it = free_.begin(); it != free_.end();) {
+      if (std::get<0>(it->first) == 0) {
+        for (void* q : it->second) driver_free_locked(q, std::get<2>(it->first));
+        it = free_.erase(it);
+      } else {
+        ++it;
       }
-    free_.clear();
+    }
   }
 
   int dev_;
   std::mutex mu_;
-  std::map<size_t, std::vector<void*>> free_;
-  std::map<void*, size_t> sizes_;
-  std::vector<Block> pending_, captured_;
+  std::map<std::tuple<int, uintptr_t, size_t>, std::vector<void*>> free_;
+  std::map<void*, BlockInfo> live_;
+  std::vector<Pending> pending_;
+  std::vector<std::pair<void*, size_t>> parked_;
+  std::map<int, std::vector<std::pair<void*, size_t>>> held_;
+  std::set<int> dead_;
+  int last_pool_ = 0;
   Stats st_;
 };
 
@@ -299,7 +409,7 @@ struct Ctx {
 void dl_deleter(DLManagedTensor* self) {
   Ctx* c = (Ctx*)self->manager_ctx;
   try {
-    if (c->kind == 0) dev_pool(c->dev).free(c->ptr, c->stream);
+    if (c->kind == 0) dev_pool(c->dev).free(c->ptr);
     else if (c->kind == 1 || c->kind == 2) host_pool(c->kind == 2).free(c->ptr);
   } catch (...) {
   }
@@ -317,19 +427,24 @@ void capsule_dtor(PyObject* cap) {
 
 // dtype: (code, bits) -- code 0 int, 1 uint, 2 float, 4 bfloat
 py::object make_capsule(std::vector<int64_t> shape, int code, int bits, int kind, int dev, int32_t dl_device_type,
-                        uintptr_t stream) {
+                        uintptr_t stream, std::vector<int64_t> strides) {
   int64_t n = 1;
   for (int64_t s : shape) {
     if (s < 0) throw std::invalid_argument("negative dimension");
     n *= s;
   }
+  if (!strides.empty() && strides.size() != shape.size()) throw std::invalid_argument("strides rank != shape rank");
   const size_t bytes = (size_t)n * (bits / 8);
-  void* p = kind == 0 ? dev_pool(dev).alloc(bytes) : host_pool(kind == 2).alloc(bytes);
+  void* p = kind == 0 ? dev_pool(dev).alloc(bytes, stream) : host_pool(kind == 2).alloc(bytes);
   auto* c = new Ctx{shape, std::vector<int64_t>(shape.size()), p, kind, dev, stream, nullptr};
-  int64_t st = 1;
-  for (int i = (int)shape.size() - 1; i >= 0; --i) {
-    c->strides[i] = st;
-    st *= shape[i];
+  if (!strides.empty()) {
+    c->strides = strides;  // a dense permutation of the shape (e.g. NHWC memory of an NCHW view)
+  } else {
+    int64_t st = 1;
+    for (int i = (int)shape.size() - 1; i >= 0; --i) {
+      c->strides[i] = st;
+      st *= shape[i];
+    }
   }
   auto* m = new DLManagedTensor{};
   m->dl_tensor.data = p;
@@ -361,7 +476,7 @@ class SyncedBlob : public std::enable_shared_from_this<SyncedBlob> {
   }
   ~SyncedBlob() {
     if (h_) host_pool(pinned_).free(h_);
-    if (d_ && !ext_) dev_pool(dev_).free(d_, 0);
+    if (d_ && !ext_) dev_pool(dev_).free(d_);
   }
   uintptr_t cpu_ptr(uintptr_t stream) {
     to_cpu(stream);
@@ -389,7 +504,7 @@ class SyncedBlob : public std::enable_shared_from_this<SyncedBlob> {
     if (!h_) h_ = host_pool(pinned_).alloc(bytes_);
   }
   void alloc_d() {
-    if (!d_) d_ = dev_pool(dev_).alloc(bytes_);
+    if (!d_) d_ = dev_pool(dev_).alloc(bytes_, 0);
   }
   void to_cpu(uintptr_t stream) {
     if (head_ == UNINIT) {
@@ -453,8 +568,19 @@ void register_mem(py::module& m) {
   py::module_ mm = m.def_submodule("mem", "native device / host memory pools (DLPack-exported blocks)");
   mm.def("empty", &make_capsule, py::arg("shape"), py::arg("code"), py::arg("bits"), py::arg("kind"),
          py::arg("device") = 0, py::arg("dl_device_type") = 10, py::arg("stream") = 0,
-         "allocate a contiguous block from a pool and return a DLPack capsule owning it");
+         py::arg("strides") = std::vector<int64_t>(),
+         "allocate a dense block from a pool (stream-ordered on `stream`) and return a DLPack capsule owning it");
   mm.def("device_stats", [](int d) { return dev_pool(d).stats(); });
+  mm.def("reset_peak", [](int d) { dev_pool(d).reset_peak(); });
+  mm.def("record_stream", [](int d, uintptr_t ptr, uintptr_t s) { dev_pool(d).record_stream((void*)ptr, s); });
+  mm.def("owns", [](int d, uintptr_t ptr) { return dev_pool(d).owns((void*)ptr); });
+  mm.def("new_pool", [](int d) { return dev_pool(d).new_pool(); });
+  mm.def("release_pool", [](int d, int id) { dev_pool(d).release_pool(id); });
+  mm.def("set_pool", [](int id) {
+    const int prev = t_pool;
+    t_pool = id;
+    return prev;
+  }, "this thread's allocations go to private pool `id` (0: default); returns the previous id");
   mm.def("host_stats", [](bool pinned) { return host_pool(pinned).stats(); }, py::arg("pinned") = false);
   mm.def("empty_cache", [](int d) { dev_pool(d).release(); });
   mm.def("empty_host_cache", [](bool pinned) { host_pool(pinned).release(); }, py::arg("pinned") = false);

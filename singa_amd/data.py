@@ -24,6 +24,8 @@ from typing import Callable, Iterator, List, Optional, Sequence, Tuple
 import numpy as np
 import torch
 
+from . import memory as _mem
+
 
 class ArrayIterator:
     def __init__(self, x: np.ndarray, y: np.ndarray, batch_size: int, shuffle: bool = True, drop_last: bool = True,
@@ -208,6 +210,6 @@ class DevicePrefetcher:
         cur = self.next
         for t in cur:
             if self.stream is not None:
-                t.record_stream(torch.cuda.current_stream(self.device))
+                _mem.record_stream(t, torch.cuda.current_stream(self.device))
         self._preload()
         return cur

@@ -35,10 +35,6 @@ def _mod():
     return getattr(N.lib(), "mem", None)
 
 
-def enabled() -> bool:
-    return os.environ.get("SINGA_AMD_NATIVE_MEM", "1") != "0" and _mod() is not None
-
-
 def _dl_device_type() -> int:
     """The DLPack device type this PyTorch build uses for GPU tensors (kDLROCM
     on ROCm builds), read from a tensor it exports."""
@@ -49,27 +45,122 @@ def _dl_device_type() -> int:
     return _DL_DEV
 
 
-def empty(shape: Sequence[int], dtype=torch.float32, device="cpu", pinned: bool = False) -> torch.Tensor:
-    """A dense tensor whose storage is a block of the native pool."""
-    dev = torch.device(device)
-    shape = [int(s) for s in shape]
+_ON = [None]
+_DEVS: dict = {}
+
+
+def _native_on() -> bool:
+    v = _ON[0]
+    if v is None:
+        v = _ON[0] = os.environ.get("SINGA_AMD_NATIVE_MEM", "1") != "0" and _mod() is not None
+    return v
+
+
+def enabled() -> bool:
+    return _native_on()
+
+
+def _cuda_index(dev) -> int:
+    idx = dev.index
+    return idx if idx is not None else torch.cuda.current_device()
+
+
+def empty(*size, dtype=None, device=None, memory_format=None, pinned: bool = False, pin_memory: bool = False,
+          **_ignored) -> torch.Tensor:
+    """``torch.empty``'s signature; the storage is a block of a native pool:
+    the device's HBM pool (stream-ordered on the current stream) or the
+    64-byte-aligned / pinned host pool.  ``memory_format=torch.channels_last``
+    lays a 4-D block out NHWC under the logical NCHW shape (one allocation,
+    no copy).  ``SINGA_AMD_NATIVE_MEM=0`` (or no ``_C``): PyTorch's allocator."""
+    if len(size) == 1 and isinstance(size[0], (tuple, list, torch.Size)):
+        size = size[0]
+    elif len(size) >= 2 and isinstance(size[0], (tuple, list, torch.Size)):  # legacy empty(shape, dtype[, device])
+        size, dtype, device = size[0], size[1], (size[2] if len(size) > 2 else device)
+    dtype = dtype or torch.float32
+    pinned = pinned or pin_memory
+    dev = device if isinstance(device, torch.device) else _DEVS.get(device)
+    if dev is None:
+        dev = _DEVS[device] = torch.device(device if device is not None else "cpu")
+    if not _native_on() or dtype not in _CODES:
+        return torch.empty(tuple(size), dtype=dtype, device=dev, pin_memory=pinned and dev.type == "cpu",
+                           memory_format=memory_format or torch.contiguous_format)
     M = _mod()
-    if M is None or dtype not in _CODES or os.environ.get("SINGA_AMD_NATIVE_MEM", "1") == "0":
-        return torch.empty(shape, dtype=dtype, device=dev, pin_memory=pinned and dev.type == "cpu")
+    shape = [int(v) for v in size]
+    strides = []
+    if memory_format is torch.channels_last and len(shape) == 4:
+        n_, c_, h_, w_ = shape
+        strides = [h_ * w_ * c_, 1, w_ * c_, c_]
     code, bits = _CODES[dtype]
     if dev.type == "cuda":
-        idx = dev.index if dev.index is not None else torch.cuda.current_device()
-        stream = torch.cuda.current_stream(idx).cuda_stream
-        cap = M.empty(shape, code, bits, 0, idx, _dl_device_type(), stream)
+        idx = _cuda_index(dev)
+        cap = M.empty(shape, code, bits, 0, idx, _dl_device_type(), torch.cuda.current_stream(idx).cuda_stream,
+                      strides)
     else:
-        cap = M.empty(shape, code, bits, 2 if pinned else 1, 0, 1, 0)
+        cap = M.empty(shape, code, bits, 2 if pinned else 1, 0, 1, 0, strides)
     t = torch.utils.dlpack.from_dlpack(cap)
     return t.view(torch.bool) if dtype == torch.bool and t.dtype != torch.bool else t
 
 
+def empty_like(t: torch.Tensor, dtype=None, memory_format=None) -> torch.Tensor:
+    """Same shape (and, by default, the same dense layout: contiguous or
+    channels_last) as ``t``."""
+    if memory_format is None or memory_format is torch.preserve_format:
+        memory_format = (torch.channels_last if t.dim() == 4 and not t.is_contiguous()
+                         and t.is_contiguous(memory_format=torch.channels_last) else None)
+    return empty(tuple(t.shape), dtype=dtype or t.dtype, device=t.device, memory_format=memory_format)
+
+
+def record_stream(t: torch.Tensor, stream) -> None:
+    """``t`` (or a view into a pool block) is used on ``stream`` too: its
+    block is reused only after the work queued there so far completed
+    (PyTorch's record_stream for tensors it allocated)."""
+    if not t.is_cuda:
+        return
+    M = _mod()
+    s = stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream)
+    if M is not None and _native_on() and M.owns(_cuda_index(t.device), t.data_ptr()):
+        M.record_stream(_cuda_index(t.device), t.data_ptr(), s)
+    else:
+        t.record_stream(stream if hasattr(stream, "cuda_stream") else torch.cuda.ExternalStream(s))
+
+
+class graph_pool:
+    """Context manager: allocations of this thread go to a PRIVATE pool
+    (a HIP graph's memory: blocks freed inside the capture are reused within
+    it, and none of them is handed to work outside the graph).  ``release()``
+    when the graph is destroyed."""
+
+    def __init__(self, device=None):
+        M = _mod()
+        self.dev = _cuda_index(torch.device(device or "cuda"))
+        self.id = M.new_pool(self.dev) if (M is not None and _native_on()) else 0
+        self._prev = 0
+
+    def __enter__(self):
+        if self.id:
+            self._prev = _mod().set_pool(self.id)
+        return self
+
+    def __exit__(self, *exc):
+        if self.id:
+            _mod().set_pool(self._prev)
+        return False
+
+    def release(self) -> None:
+        if self.id:
+            _mod().release_pool(self.dev, self.id)
+            self.id = 0
+
+
 def zeros(shape: Sequence[int], dtype=torch.float32, device="cpu") -> torch.Tensor:
     from .ops import glue as G
-    return G.zero_(empty(shape, dtype, device))
+    return G.zero_(empty(tuple(shape), dtype=dtype, device=device))
+
+
+def reset_peak(device=None) -> None:
+    M = _mod()
+    if M is not None:
+        M.reset_peak(_cuda_index(torch.device(device or "cuda")))
 
 
 def stats(device=None) -> dict:

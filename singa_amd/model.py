@@ -28,6 +28,7 @@ import torch
 
 from . import autograd
 from . import layer
+from . import memory as _mem
 from .ops import functional as _F
 from .ops import glue as G
 from .tensor import Tensor
@@ -157,7 +158,12 @@ class Model(layer.Layer):
             dev = args[0].device
             keep: list = []
             _F.CAPTURE_KEEP = keep
-            with torch.cuda.graph(g, pool=pool):
+            # the step's activations and temporaries come from a PRIVATE native
+            # pool: blocks freed inside the capture are reused within it, and
+            # none is handed to eager work while the graph can still replay
+            gp = _mem.graph_pool(args[0].data.device)
+            keep.append(gp)
+            with torch.cuda.graph(g, pool=pool), gp:
                 # first captured kernel: advance the device RNG epoch, so
                 # dropout masks differ on every replay (host-side Philox
                 # offsets are frozen into the captured launches)
@@ -186,7 +192,11 @@ class Model(layer.Layer):
         return out
 
     def reset_graph(self) -> None:
-        self._graphs.clear()
+        gs, self._graphs = self._graphs, {}
+        pools = [k for ent in gs.values() for k in ent[3] if isinstance(k, _mem.graph_pool)]
+        del gs  # the graphs go first; then their private memory
+        for k in pools:
+            k.release()
         self._warm.clear()
 
     def forward(self, *args, **kwargs):

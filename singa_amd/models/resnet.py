@@ -22,6 +22,7 @@ from typing import List, Sequence
 
 import torch
 
+from .. import memory as _mem
 from .. import autograd, layer, model
 from ..ops import functional as F
 from ..ops import native as N
@@ -41,7 +42,7 @@ class InputPrep(autograd.Operator):
             C = x.shape[1]
             cp = (C + 7) // 8 * 8
             if x.dtype == torch.float32 and self.dtype == torch.bfloat16 and x.is_contiguous():
-                y = torch.empty((x.shape[0], cp, x.shape[2], x.shape[3]), dtype=torch.bfloat16, device=x.device,
+                y = _mem.empty((x.shape[0], cp, x.shape[2], x.shape[3]), dtype=torch.bfloat16, device=x.device,
                                 memory_format=torch.channels_last)
                 N.lib().nchw_to_nhwc_pad(x.data_ptr(), y.data_ptr(), x.shape[0], C, x.shape[2], x.shape[3], cp,
                                          N.stream())
@@ -66,7 +67,7 @@ def _pair_maps(K: int, C: int, device):
     if key not in _PAIR_IDX:
         zero = K * 49 * C
         fwd = torch.full((K, 7, 4, 8), zero, dtype=torch.int64)
-        bwd = torch.empty((K, 7, 7, C), dtype=torch.int64)
+        bwd = _mem.empty((K, 7, 7, C), dtype=torch.int64)
         k = torch.arange(K).view(K, 1)
         r = torch.arange(7).view(1, 7)
         for s in range(7):
@@ -103,7 +104,7 @@ class PairedStemConv(autograd.Operator):
         L = N.lib()
         Nn, C, H, Wd = x.shape
         K = W.shape[0]
-        xp = torch.empty((Nn, H, Wd + 1, 8), dtype=torch.bfloat16, device=x.device)
+        xp = _mem.empty((Nn, H, Wd + 1, 8), dtype=torch.bfloat16, device=x.device)
         L.nchw_to_pairs(x.data_ptr(), xp.data_ptr(), Nn, C, H, Wd, N.stream())
         p = self.params[1] if len(self.params) > 1 else None
         low = p.low if p is not None else None
@@ -111,7 +112,7 @@ class PairedStemConv(autograd.Operator):
         fwd, bwd = _pair_maps(K, C, x.device)
         wp = G.index_select(G.cat([wk, G.zeros((1,), torch.bfloat16, x.device)]), 0, fwd)
         Ho, Wo = (H + 6 - 7) // 2 + 1, (Wd + 6 - 7) // 2 + 1
-        y = torch.empty((Nn, K, Ho, Wo), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+        y = _mem.empty((Nn, K, Ho, Wo), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
         ws, rows = None, 0
         if self.bn_stats and autograd.training:
             rows = L.conv_stats_rows(Nn * Ho * Wo, K)

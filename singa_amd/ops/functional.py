@@ -28,6 +28,7 @@ import numpy as np
 import torch
 import torch.nn.functional as F
 
+from .. import memory as _mem
 from . import cpu as CP
 from . import glue as G
 from . import native as N
@@ -78,8 +79,8 @@ def _same_layout(a: torch.Tensor, b: torch.Tensor) -> bool:
 def _like(t: torch.Tensor, dtype=None) -> torch.Tensor:
     """Empty tensor with the same shape AND memory layout as t."""
     if t.dim() == 4 and N.is_cl(t) and not t.is_contiguous():
-        return torch.empty(t.shape, dtype=dtype or t.dtype, device=t.device, memory_format=torch.channels_last)
-    return torch.empty(t.shape, dtype=dtype or t.dtype, device=t.device)
+        return _mem.empty(t.shape, dtype=dtype or t.dtype, device=t.device, memory_format=torch.channels_last)
+    return _mem.empty(t.shape, dtype=dtype or t.dtype, device=t.device)
 
 
 def _zeros_cl(shape, dtype, device) -> torch.Tensor:
@@ -102,7 +103,7 @@ def unary(op: str, x: torch.Tensor, alpha: float = 0.0) -> torch.Tensor:
     _no_native(f"unary {op}", x)
     if CP.ok(x) and op in UNARY:
         x = CP.dense32(x)
-        y = torch.empty(x.shape, dtype=torch.float32)
+        y = _mem.empty(x.shape, dtype=torch.float32)
         CP.lib().unary_fwd(UNARY[op], x.data_ptr(), y.data_ptr(), x.numel(), float(alpha))
         return y
     if op == "leakyrelu":
@@ -138,7 +139,7 @@ def unary_bwd(op: str, x: Optional[torch.Tensor], y: Optional[torch.Tensor], dy:
         dy = CP.dense32(dy)
         xx = CP.dense32(x) if x is not None else None
         yy = CP.dense32(y) if y is not None else None
-        dx = torch.empty(dy.shape, dtype=torch.float32)
+        dx = _mem.empty(dy.shape, dtype=torch.float32)
         CP.lib().unary_bwd(UNARY[op], CP.p(xx), CP.p(yy), dy.data_ptr(), dx.data_ptr(), dy.numel(), float(alpha))
         return dx
     xf = x.float() if x is not None else None
@@ -275,8 +276,8 @@ def dropout_fwd(x: torch.Tensor, ratio: float, seed: int, offset: int,
         # the GPU kernels' Philox stream on the host (bit-identical masks); the
         # oracle applies the same mask with PyTorch arithmetic
         xc = CP.dense32(x)
-        y = torch.empty(x.shape, dtype=torch.float32)
-        mask = torch.empty(x.shape, dtype=torch.uint8)
+        y = _mem.empty(x.shape, dtype=torch.float32)
+        mask = _mem.empty(x.shape, dtype=torch.uint8)
         CP.lib().dropout_fwd(xc.data_ptr(), y.data_ptr(), mask.data_ptr(), xc.numel(), pkeep, int(seed), int(offset))
         if CP.ok(x):
             return y, mask
@@ -298,7 +299,7 @@ def dropout_bwd(dy: torch.Tensor, mask: torch.Tensor, ratio: float) -> torch.Ten
     _no_native("dropout_bwd", dy)
     if CP.ok(dy) and mask.dtype == torch.uint8 and mask.shape == dy.shape:
         dy, m = CP.dense32(dy), G.contiguous(mask)
-        dx = torch.empty(dy.shape, dtype=torch.float32)
+        dx = _mem.empty(dy.shape, dtype=torch.float32)
         CP.lib().dropout_bwd(dy.data_ptr(), m.data_ptr(), dx.data_ptr(), dy.numel(), pkeep)
         return dx
     return dy * mask.to(dy.dtype) / pkeep
@@ -319,12 +320,12 @@ def softmax(x: torch.Tensor, axis: int = -1, out_dtype: Optional[torch.dtype] = 
         x = G.contiguous(x)
         C = x.shape[-1]
         if C <= 1024:  # short rows: one wave per row
-            y = torch.empty(x.shape, dtype=od, device=x.device)
+            y = _mem.empty(x.shape, dtype=od, device=x.device)
             N.lib().softmax_rows(x.data_ptr(), y.data_ptr(), x.numel() // C, C, N.dt(x), N.dt(y), N.stream())
             return y
         if C > 16384:
             raise NotImplementedError(f"softmax: rows longer than 16384 ({C})")
-        y = torch.empty_like(x)
+        y = _mem.empty_like(x)
         N.lib().softmax_fwd(x.data_ptr(), y.data_ptr(), x.numel() // C, C, N.dt(x), int(x.dtype == torch.float32),
                             N.stream())
         return y if od == x.dtype else cast(y, od)
@@ -333,7 +334,7 @@ def softmax(x: torch.Tensor, axis: int = -1, out_dtype: Optional[torch.dtype] = 
         if axis != x.dim() - 1:
             return G.contiguous(softmax(G.contiguous(x.movedim(axis, -1)), -1, od).movedim(-1, axis))
         x = CP.dense32(x)
-        y = torch.empty(x.shape, dtype=torch.float32)
+        y = _mem.empty(x.shape, dtype=torch.float32)
         n = x.shape[-1] if x.dim() else 1
         if y.numel():
             CP.lib().softmax(x.data_ptr(), y.data_ptr(), x.numel() // n, n)
@@ -350,7 +351,7 @@ def softmax_bwd(y: torch.Tensor, dy: torch.Tensor, axis: int = -1) -> torch.Tens
         y = G.contiguous(y)
         dy = G.contiguous(G.to(dy, y.dtype))
         C = y.shape[-1]
-        dx = torch.empty_like(dy)
+        dx = _mem.empty_like(dy)
         N.lib().softmax_bwd(y.data_ptr(), dy.data_ptr(), dx.data_ptr(), y.numel() // C, C, N.dt(y), N.stream())
         return dx
     _no_native("softmax_bwd", y, dy)
@@ -359,7 +360,7 @@ def softmax_bwd(y: torch.Tensor, dy: torch.Tensor, axis: int = -1) -> torch.Tens
             g = softmax_bwd(G.contiguous(y.movedim(axis, -1)), G.contiguous(dy.movedim(axis, -1)), -1)
             return G.contiguous(g.movedim(-1, axis))
         y, dy = CP.dense32(y), CP.dense32(dy)
-        dx = torch.empty(y.shape, dtype=torch.float32)
+        dx = _mem.empty(y.shape, dtype=torch.float32)
         n = y.shape[-1] if y.dim() else 1
         if dx.numel():
             CP.lib().softmax_bwd(y.data_ptr(), dy.data_ptr(), dx.data_ptr(), y.numel() // n, n)
@@ -379,9 +380,9 @@ def softmax_xent(x: torch.Tensor, target: torch.Tensor, topk: int = 1, grad_scal
     soft = target.dim() > 1 and target.shape[-1] == C and target.is_floating_point()
     if _native_ok(x) and x2.dtype in (torch.float32, torch.bfloat16) and C <= 16384:
         x2 = G.contiguous(x2)
-        loss = torch.empty(B, dtype=torch.float32, device=x.device)
-        correct = torch.empty(B, dtype=torch.float32, device=x.device)
-        dx = torch.empty_like(x2) if need_grad else None
+        loss = _mem.empty(B, dtype=torch.float32, device=x.device)
+        correct = _mem.empty(B, dtype=torch.float32, device=x.device)
+        dx = _mem.empty_like(x2) if need_grad else None
         if soft:
             t = G.contiguous(G.to(G.reshape(target, (B, C)), torch.float32))
             lab = None
@@ -394,9 +395,9 @@ def softmax_xent(x: torch.Tensor, target: torch.Tensor, topk: int = 1, grad_scal
     _no_native("softmax_xent", x)
     if CP.ok(x2) and (not soft or target.dtype == torch.float32):
         x2 = CP.dense32(x2)
-        loss = torch.empty(B, dtype=torch.float32)
-        correct = torch.empty(B, dtype=torch.float32)
-        dx = torch.empty(x2.shape, dtype=torch.float32) if need_grad else None
+        loss = _mem.empty(B, dtype=torch.float32)
+        correct = _mem.empty(B, dtype=torch.float32)
+        dx = _mem.empty(x2.shape, dtype=torch.float32) if need_grad else None
         if soft:
             t, lab, l64 = CP.dense32(G.reshape(target, (B, C))), None, 0
         else:
@@ -434,9 +435,9 @@ def layernorm_fwd(x: torch.Tensor, g: Optional[torch.Tensor], b: Optional[torch.
     if _native_ok(x) and x.dtype in (torch.float32, torch.bfloat16):
         x = G.contiguous(x)
         R = x.numel() // D
-        y = torch.empty_like(x)
-        mean = torch.empty(R, dtype=torch.float32, device=x.device)
-        rstd = torch.empty(R, dtype=torch.float32, device=x.device)
+        y = _mem.empty_like(x)
+        mean = _mem.empty(R, dtype=torch.float32, device=x.device)
+        rstd = _mem.empty(R, dtype=torch.float32, device=x.device)
         gg = G.contiguous(G.to(g, torch.float32)) if g is not None else None
         bb = G.contiguous(G.to(b, torch.float32)) if b is not None else None
         N.lib().layernorm_fwd(x.data_ptr(), N.ptr(gg), N.ptr(bb), y.data_ptr(), mean.data_ptr(), rstd.data_ptr(), R,
@@ -446,9 +447,9 @@ def layernorm_fwd(x: torch.Tensor, g: Optional[torch.Tensor], b: Optional[torch.
     if CP.ok(x, g, b):
         x = CP.dense32(x)
         R = x.numel() // D
-        y = torch.empty(x.shape, dtype=torch.float32)
-        mean = torch.empty(R, dtype=torch.float32)
-        rstd = torch.empty(R, dtype=torch.float32)
+        y = _mem.empty(x.shape, dtype=torch.float32)
+        mean = _mem.empty(R, dtype=torch.float32)
+        rstd = _mem.empty(R, dtype=torch.float32)
         gg = CP.dense32(g) if g is not None else None
         bb = CP.dense32(b) if b is not None else None
         CP.lib().layernorm_fwd(x.data_ptr(), CP.p(gg), CP.p(bb), y.data_ptr(), mean.data_ptr(), rstd.data_ptr(), R, D,
@@ -478,7 +479,7 @@ def layernorm_bwd(x, dy, g, mean, rstd, dg_acc=None, db_acc=None):
     if _native_ok(x, dy) and x.dtype in (torch.float32, torch.bfloat16):
         x = G.contiguous(x)
         dy = G.contiguous(G.to(dy, x.dtype))
-        dx = torch.empty_like(x)
+        dx = _mem.empty_like(x)
         dg = db = None
         if g is not None:
             dg = dg_acc if _acc_ok(dg_acc) else G.zeros((D,), torch.float32, x.device)
@@ -490,7 +491,7 @@ def layernorm_bwd(x, dy, g, mean, rstd, dg_acc=None, db_acc=None):
     _no_native("layernorm_bwd", x, dy)
     if CP.ok(x, dy, g):
         x, dy = CP.dense32(x), CP.dense32(dy)
-        dx = torch.empty(x.shape, dtype=torch.float32)
+        dx = _mem.empty(x.shape, dtype=torch.float32)
         dg = db = None
         if g is not None:
             dg = dg_acc if (dg_acc is not None and CP.ok(dg_acc) and dg_acc.is_contiguous() and dg_acc.numel() == D) \
@@ -590,7 +591,7 @@ def gemm(a: torch.Tensor, b: torch.Tensor, ta: bool = False, tb: bool = False, o
     lead = (batch,) if batch > 1 or a.dim() == 3 or b.dim() == 3 else ()
     if out is None:
         od = out_dtype or (torch.float32 if accumulate else a.dtype)
-        out = G.zeros(lead + (M, Nn), od, a.device) if accumulate else torch.empty(lead + (M, Nn), dtype=od,
+        out = G.zeros(lead + (M, Nn), od, a.device) if accumulate else _mem.empty(lead + (M, Nn), dtype=od,
                                                                                       device=a.device)
     if (not a.is_cuda and CP.ok(a, b, bias) and out.dtype == torch.float32 and out.is_contiguous()
             and (bias is None or bias.numel() == Nn)):
@@ -713,7 +714,7 @@ def to_nhwc_bf16(x: torch.Tensor, cpad: Optional[int] = None) -> torch.Tensor:
     cp = cpad or C
     if cp != C:
         if x.is_cuda and x.dtype in (torch.float32, torch.bfloat16) and x.is_contiguous() and cp % 8 == 0:
-            y = torch.empty((Nn, cp, H, W), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+            y = _mem.empty((Nn, cp, H, W), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
             fn = N.lib().nchw_to_nhwc_pad if x.dtype == torch.float32 else N.lib().nchw_to_nhwc_pad_bf16
             fn(x.data_ptr(), y.data_ptr(), Nn, C, H, W, cp, N.stream())
             return y
@@ -750,7 +751,7 @@ def _gconv_fwd(x, w, b, stride, padding, dilation, groups, out_dtype, relu):
     dt = _gconv_dt(x, w)
     xc, wc = _nhwc(x, dt), _nhwc(w, dt)
     od = torch.bfloat16 if out_dtype == torch.bfloat16 else torch.float32
-    y = torch.empty((Nn, K, Ho, Wo), dtype=od, device=x.device, memory_format=torch.channels_last)
+    y = _mem.empty((Nn, K, Ho, Wo), dtype=od, device=x.device, memory_format=torch.channels_last)
     bias = G.contiguous(G.to(b, torch.float32)) if b is not None else None
     N.lib().gconv_fwd(0 if dt == torch.float32 else 1, xc.data_ptr(), wc.data_ptr(), y.data_ptr(), N.ptr(bias), Nn,
                       H, W, C, K, R, S, Ho, Wo, sh, sw, ph, pw, dh, dw, groups, int(relu),
@@ -780,7 +781,7 @@ def _gconv_bwd(x, w, dy, stride, padding, dilation, groups, need_dx, dw_out, nee
                 and dx_acc.is_contiguous(memory_format=torch.channels_last)):
             dx, beta = dx_acc, 1.0
         else:
-            dx, beta = torch.empty(x.shape, dtype=od, device=x.device, memory_format=torch.channels_last), 0.0
+            dx, beta = _mem.empty(x.shape, dtype=od, device=x.device, memory_format=torch.channels_last), 0.0
         L.gconv_dgrad(dtc, dyc.data_ptr(), wc.data_ptr(), dx.data_ptr(), Nn, H, W, C, K, R, S, Ho, Wo, sh, sw, ph, pw,
                       dh, dw_, groups, 0 if od == torch.bfloat16 else 1, beta, N.stream())
         if beta == 0.0:
@@ -837,7 +838,7 @@ def conv2d_fwd(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], stri
             if Kp != K:
                 bias = G.cat([bias, G.zeros((Kp - K,), torch.float32, bias.device)])
         od = torch.bfloat16 if out_dtype == torch.bfloat16 else torch.float32
-        y = torch.empty((Nn, Kp, Ho, Wo), dtype=od, device=x.device, memory_format=torch.channels_last)
+        y = _mem.empty((Nn, Kp, Ho, Wo), dtype=od, device=x.device, memory_format=torch.channels_last)
         ws, rows = None, 0
         if (bn_stats and od == torch.bfloat16 and Kp == K and out_dtype == torch.bfloat16 and not relu
                 and not _NO_BN_STATS):
@@ -862,7 +863,7 @@ def conv2d_fwd(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], stri
             raise ValueError(f"conv2d: input {tuple(x.shape)} / weight {tuple(w.shape)} / groups {groups} mismatch")
         Ho, Wo = conv_out_size(H, R, sh, ph, dh), conv_out_size(W, S, sw, pw, dw)
         xc, wc = CP.dense32(x), CP.dense32(w)
-        y = torch.empty((Nn, K, Ho, Wo), dtype=torch.float32)
+        y = _mem.empty((Nn, K, Ho, Wo), dtype=torch.float32)
         CP.lib().conv_fwd(xc.data_ptr(), wc.data_ptr(), CP.p(CP.dense32(b) if b is not None else None), y.data_ptr(),
                           Nn, Cx, H, W, K, R, S, Ho, Wo, sh, sw, ph, pw, dh, dw, groups)
         return unary("relu", y) if relu else y
@@ -933,7 +934,7 @@ def pretranspose_conv_weights(items) -> dict:
         dev = sel[0][1].device
         sizes = [w.numel() for _, w in sel]
         offs = np.cumsum([0] + [(n + 63) // 64 * 64 for n in sizes])
-        scratch = torch.empty(int(offs[-1]), dtype=torch.bfloat16, device=dev)
+        scratch = _mem.empty(int(offs[-1]), dtype=torch.bfloat16, device=dev)
         desc = np.zeros((len(sel), 4), dtype=np.int64)
         tile0 = 0
         for i, (_, w) in enumerate(sel):
@@ -956,6 +957,39 @@ def pretranspose_conv_weights(items) -> dict:
     return {key: v for (key, _), v in zip(sel, views)}
 
 
+def _conv_bwd_res(x, w, dy, stride, padding, dw_out, need_db, mg: "MaskedGrad", wt_pre, db_out):
+    """conv2d_bwd with a lazy residual gradient to absorb: dx = dgrad +
+    g * bit(mask) in the dgrad epilogue (native bf16, stride 1); the weight
+    / bias gradients as in conv2d_bwd."""
+    Nn, C, H, W = x.shape
+    K, _, R, S = w.shape
+    Ho, Wo = dy.shape[2], dy.shape[3]
+    dyb = dy if (dy.dtype == torch.bfloat16 and N.is_cl(dy)) else to_nhwc_bf16(dy, K)
+    wb = w if (w.dtype == torch.bfloat16 and N.is_cl(w)) else G.to(w, torch.bfloat16, torch.channels_last)
+    wt, ready = None, False
+    if DGRAD_KMAJOR and K % 64 == 0:
+        if wt_pre is not None and wb is w and wt_pre.numel() == K * C * R * S:
+            wt, ready = wt_pre, True
+        else:
+            wt = _mem.empty(K * C * R * S, dtype=torch.bfloat16, device=x.device)
+    if ready:
+        N.lib().set_wt_ready(1)
+    dxp = _mem.empty((Nn, C, H, W), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+    g = mg.g if N.is_cl(mg.g) else G.contiguous(mg.g, torch.channels_last)
+    ok = N.lib().conv_dgrad_res(dyb.data_ptr(), wb.data_ptr(), dxp.data_ptr(), Nn, H, W, C, K, R, S, Ho, Wo,
+                                stride[0], stride[1], padding[0], padding[1], 1, 1, N.ptr(wt), g.data_ptr(),
+                                mg.mask.data_ptr(), N.stream())
+    if not ok:  # shape the epilogue cannot take: materialise and accumulate as usual
+        return conv2d_bwd(x, w, dy, stride, padding, (1, 1), 1, True, dw_out, need_db, mg.materialize(), None,
+                          None, db_out)
+    mg.value = dxp
+    mg.g = mg.mask = None
+    dxp._sg_fresh = True
+    # weight (and bias) gradient: the plain path with no data gradient
+    _, dwt, db = conv2d_bwd(x, w, dy, stride, padding, (1, 1), 1, False, dw_out, need_db, None, None, None, db_out)
+    return mg, dwt, db
+
+
 def conv2d_bwd(x: torch.Tensor, w: torch.Tensor, dy: torch.Tensor, stride, padding, dilation=(1, 1), groups=1,
                need_dx=True, dw_out: Optional[torch.Tensor] = None, need_db=False,
                dx_acc: Optional[torch.Tensor] = None, bn_producer=None, wt_pre: Optional[torch.Tensor] = None,
@@ -976,6 +1010,14 @@ def conv2d_bwd(x: torch.Tensor, w: torch.Tensor, dy: torch.Tensor, stride, paddi
     sh, sw = stride
     ph, pw = padding
     dh, dw_ = dilation
+    if isinstance(dx_acc, MaskedGrad):
+        K_, C_ = w.shape[0], w.shape[1]
+        if (need_dx and _native_ok(x, w, dy) and groups == 1 and x.dtype == torch.bfloat16 and C_ % 8 == 0
+                and K_ % 8 == 0 and x.shape[1] == C_ and tuple(dx_acc.shape) == tuple(x.shape)
+                and dx_acc.dtype == torch.bfloat16 and dx_acc.value is None and sh == 1 and sw == 1
+                and dh == 1 and dw_ == 1 and not N.lib().deterministic()):
+            return _conv_bwd_res(x, w, dy, stride, padding, dw_out, need_db, dx_acc, wt_pre, db_out)
+        dx_acc = dx_acc.materialize()
     if _native_ok(x, w, dy) and not (groups == 1 and x.dtype == torch.bfloat16 and
                                      (not need_dx or (dh == 1 and dw_ == 1 and sh * sw <= 16))):
         return _gconv_bwd(x, w, dy, stride, padding, dilation, groups, need_dx, dw_out, need_db, dx_acc, db_out)
@@ -1008,7 +1050,7 @@ def conv2d_bwd(x: torch.Tensor, w: torch.Tensor, dy: torch.Tensor, stride, paddi
                 if wt_pre is not None and not padded and wb is w and wt_pre.numel() == Kp * Cp * R * S:
                     wt, ready = wt_pre, True
                 else:
-                    wt = torch.empty(Kp * Cp * R * S, dtype=torch.bfloat16, device=x.device)
+                    wt = _mem.empty(Kp * Cp * R * S, dtype=torch.bfloat16, device=x.device)
             if ready:
                 N.lib().set_wt_ready(1)  # one-shot: consumed by the dgrad launch below
             if (dx_acc is not None and Cx == Cp and dx_acc.dtype == od and od == x.dtype
@@ -1039,7 +1081,7 @@ def conv2d_bwd(x: torch.Tensor, w: torch.Tensor, dy: torch.Tensor, stride, paddi
                 # identity-sum BN backward of the producer BN(+ReLU): this
                 # dgrad's epilogue sums the masked gradient (mask bits only)
                 bmask = bn_producer[2]
-                dxp = torch.empty((Nn, Cp, H, W), dtype=od, device=x.device, memory_format=torch.channels_last)
+                dxp = _mem.empty((Nn, Cp, H, W), dtype=od, device=x.device, memory_format=torch.channels_last)
                 bws = zeroed_ws(32 * 2 * C, x.device)
                 N.lib().conv_dgrad_bn(dyb.data_ptr(), wb.data_ptr(), dxp.data_ptr(), Nn, H, W, Cp, Kp, R, S, Ho, Wo,
                                       sh, sw, ph, pw, dh, dw_, N.ptr(wt), bws.data_ptr(), 0, 0, 0, 0, 0, N.stream(),
@@ -1052,7 +1094,7 @@ def conv2d_bwd(x: torch.Tensor, w: torch.Tensor, dy: torch.Tensor, stride, paddi
                   and tuple(bn_producer[0].shape) == tuple(x.shape) and N.is_cl(bn_producer[0])
                   and bn_producer[0].is_contiguous(memory_format=torch.channels_last)):
                 xbn, bst = bn_producer
-                dxp = torch.empty((Nn, Cp, H, W), dtype=od, device=x.device, memory_format=torch.channels_last)
+                dxp = _mem.empty((Nn, Cp, H, W), dtype=od, device=x.device, memory_format=torch.channels_last)
                 bws = zeroed_ws(32 * 2 * C, x.device)
                 N.lib().conv_dgrad_bn(dyb.data_ptr(), wb.data_ptr(), dxp.data_ptr(), Nn, H, W, Cp, Kp, R, S, Ho, Wo,
                                       sh, sw, ph, pw, dh, dw_, N.ptr(wt), bws.data_ptr(), xbn.data_ptr(),
@@ -1062,7 +1104,7 @@ def conv2d_bwd(x: torch.Tensor, w: torch.Tensor, dy: torch.Tensor, stride, paddi
                 dxp._sg_fresh = True
                 dx = dxp
             else:
-                dxp = torch.empty((Nn, Cp, H, W), dtype=od, device=x.device, memory_format=torch.channels_last)
+                dxp = _mem.empty((Nn, Cp, H, W), dtype=od, device=x.device, memory_format=torch.channels_last)
                 N.lib().conv_dgrad_acc(dyb.data_ptr(), wb.data_ptr(), dxp.data_ptr(), Nn, H, W, Cp, Kp, R, S, Ho, Wo,
                                        sh, sw, ph, pw, dh, dw_, om, 0.0, N.stream(), N.ptr(wt))
                 dx = G.contiguous(dxp[:, :C], torch.channels_last) if Cx != Cp else dxp
@@ -1102,7 +1144,7 @@ def conv2d_bwd(x: torch.Tensor, w: torch.Tensor, dy: torch.Tensor, stride, paddi
         K, Cg, R, S = w.shape
         Ho, Wo = dy.shape[2], dy.shape[3]
         xc, wc, dyc = CP.dense32(x), CP.dense32(w), CP.dense32(dy)
-        dx = torch.empty(x.shape, dtype=torch.float32) if need_dx else None
+        dx = _mem.empty(x.shape, dtype=torch.float32) if need_dx else None
         direct = dw_out is not None and CP.ok(dw_out) and dw_out.is_contiguous()
         dwt = dw_out if direct else G.zeros(tuple(w.shape), torch.float32, x.device)
         db = None
@@ -1172,7 +1214,7 @@ class _ZeroArena:
         if self.hwm > 0 and (self.buf is None or self.buf.numel() < self.hwm or self.buf.device != device):
             if self.buf is not None:  # a captured HIP graph may still address it: never free
                 self.retired.append(self.buf)
-            self.buf = torch.empty(self.hwm + self.hwm // 8 + 1024, dtype=torch.float32, device=device)
+            self.buf = _mem.empty(self.hwm + self.hwm // 8 + 1024, dtype=torch.float32, device=device)
         self.off = 0
         self.active = True
         self.hits = self.misses = 0
@@ -1226,7 +1268,7 @@ def zeroed_ws(n: int, device) -> torch.Tensor:
     t = ARENA.take(n, device)
     if N.available():
         N.lib().set_ws_prezeroed(1 if t is not None else 0)
-    return t if t is not None else torch.empty(n, dtype=torch.float32, device=device)
+    return t if t is not None else _mem.empty(n, dtype=torch.float32, device=device)
 
 
 def _ws(R: int, C: int, device) -> torch.Tensor:
@@ -1244,8 +1286,8 @@ def colsum(x2: torch.Tensor, with_sq: bool = False, out: Optional[torch.Tensor] 
     if _native_ok(x2) and x2.dtype in (torch.float32, torch.bfloat16):
         x2 = G.contiguous(x2)
         R, C = x2.shape
-        o0 = out if out is not None else torch.empty(C, dtype=torch.float32, device=x2.device)
-        o1 = torch.empty(C, dtype=torch.float32, device=x2.device) if with_sq else None
+        o0 = out if out is not None else _mem.empty(C, dtype=torch.float32, device=x2.device)
+        o1 = _mem.empty(C, dtype=torch.float32, device=x2.device) if with_sq else None
         N.lib().colsum(x2.data_ptr(), _ws(R, C, x2.device).data_ptr(), o0.data_ptr(), N.ptr(o1), R, C, N.dt(x2),
                        int(out is not None), N.stream())
         return o0, o1
@@ -1274,6 +1316,39 @@ class BNState:
         self.mean, self.invstd, self.scale, self.shift, self.mask = mean, invstd, scale, shift, mask
 
 
+# lazy residual gradient (see MaskedGrad); SINGA_AMD_LAZY_RES=0 writes it as a tensor
+LAZY_RES = os.environ.get("SINGA_AMD_LAZY_RES", "1") != "0"
+
+
+class MaskedGrad:
+    """The gradient a residual BN(+ReLU) passes to its shortcut input, kept
+    LAZY as (g, 1-bit ReLU mask): g * bit(mask).  The autograd engine holds it
+    like a partial gradient; a conv whose data gradient completes that input
+    adds it in its dgrad epilogue straight from (g, mask) (conv_dgrad_res),
+    so the BN backward never writes it and nobody reads it back as a bf16
+    tensor.  Any other consumer gets :meth:`materialize` (one native masking
+    pass).  ``value``: set once absorbed or materialised."""
+
+    _sg_fresh = True  # the engine owns it exclusively (may be absorbed in place)
+
+    def __init__(self, g: torch.Tensor, mask: torch.Tensor):
+        self.g, self.mask, self.value = g, mask, None
+        self.shape, self.dtype, self.device = g.shape, g.dtype, g.device
+
+    def is_floating_point(self) -> bool:
+        return True
+
+    def materialize(self) -> torch.Tensor:
+        if self.value is None:
+            out = _like(self.g)
+            N.lib().mask_bits_apply(self.g.data_ptr(), self.mask.data_ptr(), out.data_ptr(), self.g.numel(),
+                                    N.stream())
+            out._sg_fresh = True
+            self.value = out
+            self.g = self.mask = None
+        return self.value
+
+
 def _bn_native(x: torch.Tensor) -> bool:
     return _native_ok(x) and _flat_ok(x) and ((x.dim() == 2 and x.is_contiguous()) or N.is_cl(x))
 
@@ -1286,7 +1361,7 @@ def _bn_params(x: torch.Tensor, gamma, beta, run_mean, run_var, training: bool, 
     C = x.shape[1]
     R = x.numel() // C
     dev = x.device
-    p = torch.empty(4 * C, dtype=torch.float32, device=dev)
+    p = _mem.empty(4 * C, dtype=torch.float32, device=dev)
     mean, invstd, scale, shift = p[:C], p[C:2 * C], p[2 * C:3 * C], p[3 * C:]
     pre = getattr(x, "_sg_bn_ws", None)  # statistics already summed by the producing conv's epilogue
     if training and pre is not None and pre[0].numel() == pre[1] * 2 * C:
@@ -1323,8 +1398,8 @@ def bn_relu_maxpool_fwd(x: torch.Tensor, gamma, beta, run_mean, run_var, trainin
     Nn, C, H, W = x.shape
     Ho = (H + 2 * ph - kh) // sh + 1
     Wo = (W + 2 * pw - kw) // sw + 1
-    y = torch.empty((Nn, C, Ho, Wo), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
-    arg = torch.empty((Nn, Ho, Wo, C), dtype=torch.uint8, device=x.device)
+    y = _mem.empty((Nn, C, Ho, Wo), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+    arg = _mem.empty((Nn, Ho, Wo, C), dtype=torch.uint8, device=x.device)
     N.lib().bn_relu_maxpool(x.data_ptr(), scale.data_ptr(), shift.data_ptr(), y.data_ptr(), arg.data_ptr(), Nn, H, W,
                             C, Ho, Wo, kh, kw, sh, sw, ph, pw, N.stream())
     return y, arg, BNState(mean, invstd, scale, shift, None)
@@ -1352,7 +1427,7 @@ def bn_relu_maxpool_bwd(x: torch.Tensor, dy: torch.Tensor, arg: torch.Tensor, ga
         R = x.numel() // C
         dg = dg_out if dg_out is not None else G.zeros((C,), torch.float32, x.device)
         db = db_out if db_out is not None else G.zeros((C,), torch.float32, x.device)
-        coef = torch.empty(3 * C, dtype=torch.float32, device=x.device)
+        coef = _mem.empty(3 * C, dtype=torch.float32, device=x.device)
         dx = _like(x)
         N.lib().bn_bwd_pool(x.data_ptr(), dyc.data_ptr(), arg.data_ptr(), st.scale.data_ptr(), st.shift.data_ptr(),
                             st.mean.data_ptr(), st.invstd.data_ptr(), gamma.data_ptr(), _ws(R, C, x.device).data_ptr(),
@@ -1386,7 +1461,7 @@ def batchnorm_fwd(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, run_
         y = _like(x)
         mask = None
         if want_mask and relu and C % 8 == 0:
-            mask = torch.empty(R * C // 8, dtype=torch.uint8, device=dev)
+            mask = _mem.empty(R * C // 8, dtype=torch.uint8, device=dev)
         L.bn_apply(x.data_ptr(), scale.data_ptr(), shift.data_ptr(), N.ptr(res), y.data_ptr(), R, C, int(relu),
                    N.dt(x), N.stream(), N.ptr(mask))
         return y, BNState(mean, invstd, scale, shift, mask)
@@ -1397,9 +1472,9 @@ def batchnorm_fwd(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, run_
         xc = CP.dense32(x)
         Nn = x.shape[0]
         HW = x.numel() // (Nn * C) if Nn * C else 0
-        y = torch.empty(x.shape, dtype=torch.float32)
-        mean = torch.empty(C, dtype=torch.float32)
-        invstd = torch.empty(C, dtype=torch.float32)
+        y = _mem.empty(x.shape, dtype=torch.float32)
+        mean = _mem.empty(C, dtype=torch.float32)
+        invstd = _mem.empty(C, dtype=torch.float32)
         res = CP.dense32(residual) if residual is not None else None
         CP.lib().bn_fwd(xc.data_ptr(), CP.dense32(gamma).data_ptr(), CP.dense32(beta).data_ptr(),
                         run_mean.data_ptr(), run_var.data_ptr(), y.data_ptr(), mean.data_ptr(), invstd.data_ptr(), Nn,
@@ -1446,7 +1521,7 @@ def dual_bn_add_relu_fwd(x, gamma, beta, rm, rv, x2, gamma2, beta2, rm2, rv2, tr
     C = x.shape[1]
     R = x.numel() // C
     y = _like(x)
-    mask = torch.empty(R * C // 8, dtype=torch.uint8, device=x.device)
+    mask = _mem.empty(R * C // 8, dtype=torch.uint8, device=x.device)
     N.lib().bn_apply2(x.data_ptr(), st_p[2].data_ptr(), st_p[3].data_ptr(), x2.data_ptr(), st2_p[2].data_ptr(),
                       st2_p[3].data_ptr(), y.data_ptr(), mask.data_ptr(), R, C, 1, N.dt(x), N.stream())
     return y, BNState(*st_p, mask), BNState(*st2_p, None)
@@ -1469,7 +1544,7 @@ def dual_bn_add_relu_bwd(x, dy, gamma, st: BNState, x2, gamma2, st2: BNState, dg
     if n is None:
         n = _BANDS[key] = N.lib().colreduce_ws(R, C)
     wsb = zeroed_ws(2 * n, dev)  # one pre-zeroed flag for both halves (the kernel zeroes the second itself)
-    coef = torch.empty(6 * C, dtype=torch.float32, device=dev)
+    coef = _mem.empty(6 * C, dtype=torch.float32, device=dev)
     dx, dx2 = _like(x), _like(x2)
     N.lib().bn_bwd2(x.data_ptr(), dy.data_ptr(), st.mask.data_ptr(), st.mean.data_ptr(), st.invstd.data_ptr(),
                     gamma.data_ptr(), x2.data_ptr(), st2.mean.data_ptr(), st2.invstd.data_ptr(), gamma2.data_ptr(),
@@ -1484,11 +1559,13 @@ def dual_bn_add_relu_bwd(x, dy, gamma, st: BNState, x2, gamma2, st2: BNState, dg
 def batchnorm_bwd(x: torch.Tensor, dy: torch.Tensor, gamma: torch.Tensor, st: BNState,
                   y_for_mask: Optional[torch.Tensor] = None, need_dres: bool = False, relu: bool = False,
                   dg_out: Optional[torch.Tensor] = None, db_out: Optional[torch.Tensor] = None,
-                  beta: Optional[torch.Tensor] = None):
+                  beta: Optional[torch.Tensor] = None, lazy_dres: bool = False):
     """Returns dx, dgamma, dbeta, dres.  ReLU mask: from ``y_for_mask`` (the
     fused output, required when a residual was added) or, with ``relu`` and no
     residual, recomputed from x*scale+shift.  dgamma/dbeta are accumulated
-    into dg_out/db_out when given (and those are returned)."""
+    into dg_out/db_out when given (and those are returned).  ``lazy_dres``
+    (native, 1-bit mask): dres is returned as a :class:`MaskedGrad` of dy
+    instead of being written."""
     C = x.shape[1]
     if _bn_native(x):
         L = N.lib()
@@ -1506,9 +1583,11 @@ def batchnorm_bwd(x: torch.Tensor, dy: torch.Tensor, gamma: torch.Tensor, st: BN
             mode = 2 if relu else 0
         dg = dg_out if dg_out is not None else G.zeros((C,), torch.float32, x.device)
         db = db_out if db_out is not None else G.zeros((C,), torch.float32, x.device)
-        coef = torch.empty(3 * C, dtype=torch.float32, device=x.device)
+        coef = _mem.empty(3 * C, dtype=torch.float32, device=x.device)
         dx = _like(x)
-        dres = _like(x) if need_dres else None
+        lazy = (need_dres and lazy_dres and LAZY_RES and mode == 3 and C % 8 == 0 and dy.dtype == torch.bfloat16
+                and x.dtype == torch.bfloat16)
+        dres = _like(x) if need_dres and not lazy else None
         wdot = getattr(dy, "_sg_bnbwd_wdot", None)  # identity-sum inputs from the consuming conv
         if (wdot is not None and mode == 3 and not need_dres and beta is not None and x.dtype == torch.bfloat16
                 and C % 8 == 0 and dy.dtype == torch.bfloat16):
@@ -1529,7 +1608,7 @@ def batchnorm_bwd(x: torch.Tensor, dy: torch.Tensor, gamma: torch.Tensor, st: BN
             dx._sg_fresh = True
             if dres is not None:
                 dres._sg_fresh = True
-            return dx, dg, db, dres
+            return dx, dg, db, (MaskedGrad(dy, ym) if lazy else dres)
         L.bn_bwd(x.data_ptr(), dy.data_ptr(), N.ptr(ym), st.scale.data_ptr(), st.shift.data_ptr(),
                  st.mean.data_ptr(), st.invstd.data_ptr(), gamma.data_ptr(), _ws(R, C, x.device).data_ptr(),
                  coef.data_ptr(), dg.data_ptr(), db.data_ptr(), dx.data_ptr(), N.ptr(dres), R, C, mode, N.dt(x),
@@ -1537,7 +1616,7 @@ def batchnorm_bwd(x: torch.Tensor, dy: torch.Tensor, gamma: torch.Tensor, st: BN
         dx._sg_fresh = True
         if dres is not None:
             dres._sg_fresh = True
-        return dx, dg, db, dres
+        return dx, dg, db, (MaskedGrad(dy, ym) if lazy else dres)
     _no_native("batchnorm_bwd", x, dy)
     if CP.ok(x, dy, gamma, y_for_mask, dg_out, db_out) and x.dim() in (2, 4):
         xc, dyc = CP.dense32(x), CP.dense32(dy)
@@ -1545,8 +1624,8 @@ def batchnorm_bwd(x: torch.Tensor, dy: torch.Tensor, gamma: torch.Tensor, st: BN
         HW = x.numel() // (Nn * C) if Nn * C else 0
         dg = dg_out if dg_out is not None and dg_out.is_contiguous() else G.zeros((C,), torch.float32, x.device)
         db = db_out if db_out is not None and db_out.is_contiguous() else G.zeros((C,), torch.float32, x.device)
-        dx = torch.empty(x.shape, dtype=torch.float32)
-        dres = torch.empty(x.shape, dtype=torch.float32) if need_dres else None
+        dx = _mem.empty(x.shape, dtype=torch.float32)
+        dres = _mem.empty(x.shape, dtype=torch.float32) if need_dres else None
         ym = CP.dense32(y_for_mask) if y_for_mask is not None else None
         relu_x = int(relu and ym is None)
         CP.lib().bn_bwd(xc.data_ptr(), dyc.data_ptr(), CP.dense32(gamma).data_ptr(), CP.dense32(st.mean).data_ptr(),
@@ -1596,16 +1675,16 @@ def pool2d_fwd(x: torch.Tensor, kernel, stride, padding, is_max: bool, count_inc
         if kh * kw > 255 and is_max:
             raise NotImplementedError("max pool windows of more than 255 taps (8-bit argmax)")
         x = G.to(x, memory_format=torch.channels_last)
-        y = torch.empty((Nn, C, Ho, Wo), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
-        arg = torch.empty((Nn, Ho, Wo, C), dtype=torch.uint8, device=x.device) if is_max else None
+        y = _mem.empty((Nn, C, Ho, Wo), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+        arg = _mem.empty((Nn, Ho, Wo, C), dtype=torch.uint8, device=x.device) if is_max else None
         N.lib().pool_fwd(x.data_ptr(), y.data_ptr(), N.ptr(arg), Nn, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw,
                          int(is_max), int(count_include_pad), N.dt(x), N.stream())
         return y, arg
     _no_native("pool2d_fwd", x)
     if CP.ok(x):
         xc = CP.dense32(x)
-        y = torch.empty((Nn, C, Ho, Wo), dtype=torch.float32)
-        arg = torch.empty((Nn, C, Ho, Wo), dtype=torch.int32) if is_max else None
+        y = _mem.empty((Nn, C, Ho, Wo), dtype=torch.float32)
+        arg = _mem.empty((Nn, C, Ho, Wo), dtype=torch.int32) if is_max else None
         CP.lib().pool_fwd(xc.data_ptr(), y.data_ptr(), CP.p(arg), Nn, C, H, W, Ho, Wo, kh, kw, sh, sw, ph, pw,
                           int(is_max), int(count_include_pad))
         return y, arg
@@ -1626,14 +1705,14 @@ def pool2d_bwd(x_shape, x_like: torch.Tensor, dy: torch.Tensor, arg, kernel, str
     Ho, Wo = dy.shape[2], dy.shape[3]
     if _native_ok(dy) and dy.dtype in (torch.float32, torch.bfloat16):
         dy = G.to(dy, memory_format=torch.channels_last)
-        dx = torch.empty(x_shape, dtype=dy.dtype, device=dy.device, memory_format=torch.channels_last)
+        dx = _mem.empty(x_shape, dtype=dy.dtype, device=dy.device, memory_format=torch.channels_last)
         N.lib().pool_bwd(dy.data_ptr(), N.ptr(arg), dx.data_ptr(), Nn, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw,
                          int(is_max), int(count_include_pad), N.dt(dy), N.stream())
         return dx
     _no_native("pool2d_bwd", dy)
     if CP.ok(dy) and (not is_max or arg.dtype == torch.int32):
         dyc = CP.dense32(dy)
-        dx = torch.empty(tuple(x_shape), dtype=torch.float32)
+        dx = _mem.empty(tuple(x_shape), dtype=torch.float32)
         a = G.contiguous(arg) if is_max else None
         CP.lib().pool_bwd(dyc.data_ptr(), CP.p(a), dx.data_ptr(), Nn, C, H, W, Ho, Wo, kh, kw, sh, sw, ph, pw,
                           int(is_max), int(count_include_pad))
@@ -1656,7 +1735,7 @@ def global_avgpool_fwd(x: torch.Tensor) -> torch.Tensor:
     Nn, C, H, W = x.shape
     if _native_ok(x) and x.dtype in (torch.float32, torch.bfloat16):
         x = G.to(x, memory_format=torch.channels_last)
-        y = torch.empty((Nn, C), dtype=x.dtype, device=x.device)
+        y = _mem.empty((Nn, C), dtype=x.dtype, device=x.device)
         N.lib().gap_fwd(x.data_ptr(), y.data_ptr(), Nn, H * W, C, N.dt(x), N.stream())
         return y
     _no_native("global_avgpool_fwd", x)
@@ -1669,7 +1748,7 @@ def global_avgpool_bwd(dy: torch.Tensor, x_shape) -> torch.Tensor:
     Nn, C, H, W = x_shape
     if _native_ok(dy) and dy.dtype in (torch.float32, torch.bfloat16):
         dy = G.contiguous(dy)
-        dx = torch.empty(x_shape, dtype=dy.dtype, device=dy.device, memory_format=torch.channels_last)
+        dx = _mem.empty(x_shape, dtype=dy.dtype, device=dy.device, memory_format=torch.channels_last)
         N.lib().gap_bwd(dy.data_ptr(), dx.data_ptr(), Nn, H * W, C, N.dt(dy), N.stream())
         return dx
     _no_native("global_avgpool_bwd", dy)
@@ -1698,7 +1777,7 @@ def lrn_fwd(x: torch.Tensor, size: int, alpha: float, beta: float, k: float):
         C = x.shape[1]
         R = x.numel() // C
         y = _like(x)
-        norm = torch.empty(x.shape, dtype=torch.float32, device=x.device, memory_format=torch.channels_last)
+        norm = _mem.empty(x.shape, dtype=torch.float32, device=x.device, memory_format=torch.channels_last)
         N.lib().lrn_fwd(x.data_ptr(), y.data_ptr(), norm.data_ptr(), R, C, size, alpha, beta, k, N.dt(x),
                         N.stream())
         return y, norm
@@ -1706,7 +1785,7 @@ def lrn_fwd(x: torch.Tensor, size: int, alpha: float, beta: float, k: float):
     if CP.ok(x) and x.dim() == 4:
         xc = CP.dense32(x)
         Nn, C, H, W = x.shape
-        y = torch.empty(x.shape, dtype=torch.float32)
+        y = _mem.empty(x.shape, dtype=torch.float32)
         CP.lib().lrn_fwd(xc.data_ptr(), y.data_ptr(), Nn, C, H * W, int(size), float(alpha), float(beta), float(k))
         return y, None  # the backward recomputes the window sums
     xf = x.float()
@@ -1725,7 +1804,7 @@ def lrn_bwd(x: torch.Tensor, dy: torch.Tensor, norm: Optional[torch.Tensor], siz
     if CP.ok(x, dy) and x.dim() == 4:
         xc, dyc = CP.dense32(x), CP.dense32(dy)
         Nn, C, H, W = x.shape
-        dx = torch.empty(x.shape, dtype=torch.float32)
+        dx = _mem.empty(x.shape, dtype=torch.float32)
         CP.lib().lrn_bwd(xc.data_ptr(), dyc.data_ptr(), dx.data_ptr(), Nn, C, H * W, int(size), float(alpha),
                          float(beta), float(k))
         return dx
@@ -1829,14 +1908,14 @@ def attention_qkv_fwd(qkv: torch.Tensor, heads: int, mask: Optional[torch.Tensor
     scale = (1.0 / math.sqrt(D)) if scale is None else scale
     if _qkv_native_ok(qkv, H):
         BH = B * H
-        sc = torch.empty((BH, S, S), dtype=torch.float32, device=qkv.device)
+        sc = _mem.empty((BH, S, S), dtype=torch.float32, device=qkv.device)
         # scores = q k^T * scale : q [S][D] rows of stride E, k [S][D] (N x K, K-major)
         _gemm_heads((qkv, 0), E, 0, (qkv, HD), E, 0, (sc, 0), S, S, S, D, BH, H, S * E, D, S * E, D, H * S * S,
                     S * S, alpha=scale)
         if mask is not None:
             sc = G.binary("add", sc.view(B, H, S, S), mask, out_dtype=torch.float32).reshape(BH, S, S)
         p = softmax(sc, out_dtype=torch.bfloat16)
-        o = torch.empty((B, S, HD), dtype=torch.bfloat16, device=qkv.device)
+        o = _mem.empty((B, S, HD), dtype=torch.bfloat16, device=qkv.device)
         # o = p v : v [S][D] is K-outer (ldb E); o rows of stride H*D
         _gemm_heads((p, 0), S, 0, (qkv, 2 * HD), E, 1, (o, 0), HD, S, D, S, BH, H, H * S * S, S * S, S * E, D,
                     S * HD, D)
@@ -1858,12 +1937,12 @@ def attention_qkv_bwd(qkv: torch.Tensor, p: torch.Tensor, do: torch.Tensor, head
     if _qkv_native_ok(qkv, H) and p.dtype == torch.bfloat16 and do.dtype == torch.bfloat16:
         BH = B * H
         do = G.contiguous(do)
-        dqkv = torch.empty_like(qkv)
+        dqkv = _mem.empty_like(qkv)
         SS = S * S
         # dV = P^T dO
         _gemm_heads((p, 0), S, 1, (do, 0), HD, 1, (dqkv, 2 * HD), E, S, D, S, BH, H, H * SS, SS, S * HD, D, S * E, D)
         # dP = dO V^T
-        dp = torch.empty((BH, S, S), dtype=torch.bfloat16, device=qkv.device)
+        dp = _mem.empty((BH, S, S), dtype=torch.bfloat16, device=qkv.device)
         _gemm_heads((do, 0), HD, 0, (qkv, 2 * HD), E, 0, (dp, 0), S, S, S, D, BH, H, S * HD, D, S * E, D, H * SS,
                     SS)
         ds = softmax_bwd(p, dp)

@@ -23,6 +23,7 @@ from typing import List, Optional, Sequence, Tuple
 
 import torch
 
+from .. import memory as _mem
 from . import cpu as CP
 from . import native as N
 
@@ -99,7 +100,7 @@ def copy_(dst: torch.Tensor, src: torch.Tensor) -> torch.Tensor:
 
 
 def empty_like_fmt(t: torch.Tensor, dtype=None, memory_format=torch.contiguous_format) -> torch.Tensor:
-    return torch.empty(t.shape, dtype=dtype or t.dtype, device=t.device, memory_format=memory_format)
+    return _mem.empty(t.shape, dtype=dtype or t.dtype, device=t.device, memory_format=memory_format)
 
 
 def contiguous(t: torch.Tensor, memory_format=torch.contiguous_format) -> torch.Tensor:
@@ -132,7 +133,7 @@ def to(t: torch.Tensor, dtype: Optional[torch.dtype] = None, memory_format=None)
             return t
     if not on_gpu(t) and not (CP.copy_ok(t) and dtype in CP._DT and t.dtype != torch.bool):
         return t.to(dtype=dtype, memory_format=fmt)
-    return copy_(torch.empty(t.shape, dtype=dtype, device=t.device, memory_format=fmt), t)
+    return copy_(_mem.empty(t.shape, dtype=dtype, device=t.device, memory_format=fmt), t)
 
 
 def reshape(t: torch.Tensor, shape) -> torch.Tensor:
@@ -177,7 +178,7 @@ def random_(t: torch.Tensor, dist: str, a: float, b: float, device_obj=None) -> 
     stream, reproducible per seed), the device's torch generator on the CPU."""
     if on_gpu(t) and t.dtype in _FLOATS:
         seed, off = device_obj.next_rng(t.numel()) if device_obj is not None else (0, 0)
-        d = t if t.is_contiguous() else torch.empty(t.shape, dtype=t.dtype, device=t.device)
+        d = t if t.is_contiguous() else _mem.empty(t.shape, dtype=t.dtype, device=t.device)
         if d.numel():
             _lib().rand_fill(d.data_ptr(), d.numel(), N.dt(d), 0 if dist == "uniform" else 1, float(a), float(b),
                              int(seed), int(off), N.stream())
@@ -186,13 +187,13 @@ def random_(t: torch.Tensor, dist: str, a: float, b: float, device_obj=None) -> 
         # the same Philox stream as the GPU kernel (in oracle mode too: the
         # initial weights of a native run and its oracle run are identical)
         seed, off = device_obj.next_rng(t.numel()) if device_obj is not None else (0, 0)
-        d = t if t.is_contiguous() else torch.empty(t.shape, dtype=torch.float32)
+        d = t if t.is_contiguous() else _mem.empty(t.shape, dtype=torch.float32)
         if d.numel():
             CP.lib().rand_fill(d.data_ptr(), d.numel(), 0 if dist == "uniform" else 1, float(a), float(b), int(seed),
                                int(off))
         return t if d is t else copy_(t, d)
     gen = device_obj.generator if device_obj is not None else None
-    d = torch.empty(t.shape, dtype=torch.float32, device=t.device)
+    d = _mem.empty(t.shape, dtype=torch.float32, device=t.device)
     if dist == "uniform":
         d.uniform_(a, b, generator=gen)
     else:
@@ -201,7 +202,7 @@ def random_(t: torch.Tensor, dist: str, a: float, b: float, device_obj=None) -> 
 
 
 def full(shape, value, dtype, device, memory_format=torch.contiguous_format) -> torch.Tensor:
-    t = torch.empty(tuple(shape), dtype=dtype, device=device, memory_format=memory_format)
+    t = _mem.empty(tuple(shape), dtype=dtype, device=device, memory_format=memory_format)
     if t.is_cuda and N.force_native():
         if t.numel():
             _lib().fill(t.data_ptr(), t.numel(), N.dt(t), float(value), N.stream())
@@ -236,7 +237,7 @@ def binary(op: str, a: torch.Tensor, b, out_dtype: Optional[torch.dtype] = None,
         b = to(b, dt) if b.dtype != dt else b
         shape = tuple(torch.broadcast_shapes(a.shape, b.shape))
         if out is None:
-            out = torch.empty(shape, dtype=dt, device=a.device)
+            out = _mem.empty(shape, dtype=dt, device=a.device)
         size, os_, as_, bs_ = coalesce(shape, list(out.stride()), _bstrides(a, shape), _bstrides(b, shape))
         _lib().binary_nd(BIN[op], a.data_ptr(), b.data_ptr(), out.data_ptr(), N.dt(out), size, os_, as_, bs_,
                          float(alpha), N.stream())
@@ -251,7 +252,7 @@ def binary(op: str, a: torch.Tensor, b, out_dtype: Optional[torch.dtype] = None,
         a = a if a.dtype == torch.float32 else to(a, torch.float32)
         b = b if b.dtype == torch.float32 else to(b, torch.float32)
         shape = tuple(torch.broadcast_shapes(a.shape, b.shape))
-        o = out if out is not None and tuple(out.shape) == shape else torch.empty(shape, dtype=torch.float32)
+        o = out if out is not None and tuple(out.shape) == shape else _mem.empty(shape, dtype=torch.float32)
         size, os_, as_, bs_ = coalesce(shape, list(o.stride()), _bstrides(a, shape), _bstrides(b, shape))
         CP.lib().binary_nd(BIN[op], a.data_ptr(), b.data_ptr(), o.data_ptr(), size, os_, as_, bs_, float(alpha))
         if out is not None and o is not out:
@@ -283,7 +284,7 @@ def where(cond: torch.Tensor, a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
             c = c.view(torch.uint8)
         a, b = to(a, dt), to(b, dt)
         shape = tuple(torch.broadcast_shapes(c.shape, a.shape, b.shape))
-        out = torch.empty(shape, dtype=dt, device=a.device)
+        out = _mem.empty(shape, dtype=dt, device=a.device)
         size, os_, as_, bs_, cs_ = coalesce(shape, list(out.stride()), _bstrides(a, shape), _bstrides(b, shape),
                                             _bstrides(c, shape))
         _lib().where_nd(c.data_ptr(), a.data_ptr(), b.data_ptr(), out.data_ptr(), N.dt(out), size, os_, as_, bs_,
@@ -299,7 +300,7 @@ def where(cond: torch.Tensor, a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
             c = to(c, torch.uint8)
         a, b = to(a, dt), to(b, dt)
         shape = tuple(torch.broadcast_shapes(c.shape, a.shape, b.shape))
-        out = torch.empty(shape, dtype=dt)
+        out = _mem.empty(shape, dtype=dt)
         size, os_, as_, bs_, cs_ = coalesce(shape, list(out.stride()), _bstrides(a, shape), _bstrides(b, shape),
                                             _bstrides(c, shape))
         CP.lib().where_nd(c.data_ptr(), a.data_ptr(), b.data_ptr(), out.data_ptr(), size, os_, as_, bs_, cs_)
@@ -320,8 +321,8 @@ def clamp_affine(x: torch.Tensor, a: float = 1.0, b: float = 0.0, lo: float = -m
         x = dense(x)
         g = None
         if dy is not None:
-            g = dy if (dy.dtype == x.dtype and dy.stride() == x.stride()) else copy_(torch.empty_like(x), dy)
-        out = torch.empty_like(x)
+            g = dy if (dy.dtype == x.dtype and dy.stride() == x.stride()) else copy_(_mem.empty_like(x), dy)
+        out = _mem.empty_like(x)
         _lib().clamp_affine(x.data_ptr(), N.ptr(g), out.data_ptr(), x.numel(), N.dt(x), float(a), float(b),
                             float(max(lo, -3.4e38)), float(min(hi, 3.4e38)), N.stream())
         return out
@@ -330,7 +331,7 @@ def clamp_affine(x: torch.Tensor, a: float = 1.0, b: float = 0.0, lo: float = -m
     if CP.ok(x, dy):
         xc = CP.dense32(x)
         g = CP.dense32(dy) if dy is not None else None
-        out = torch.empty(x.shape, dtype=torch.float32)
+        out = _mem.empty(x.shape, dtype=torch.float32)
         CP.lib().clamp_affine(xc.data_ptr(), CP.p(g), out.data_ptr(), xc.numel(), float(a), float(b),
                               float(max(lo, -3.4e38)), float(min(hi, 3.4e38)))
         return out
@@ -369,13 +370,13 @@ def reduce(x: torch.Tensor, axes: Optional[Sequence[int]] = None, op: str = "sum
             outer = int(math.prod(x.shape[k] for k in keep))
             red = int(math.prod(x.shape[k] for k in axes))
             inner = 1
-        y = torch.empty(oshape, dtype=od, device=x.device)
+        y = _mem.empty(oshape, dtype=od, device=x.device)
         if y.numel() == 0:
             return y
         if red == 0:
             return fill_(y, 0.0 if op in ("sum", "mean", "sumsq") else float("nan"))
         if host:
-            y32 = y if y.dtype == torch.float32 else torch.empty(oshape, dtype=torch.float32)
+            y32 = y if y.dtype == torch.float32 else _mem.empty(oshape, dtype=torch.float32)
             CP.lib().reduce(xc.data_ptr(), y32.data_ptr(), outer, red, inner, RED[op])
             return y if y32 is y else copy_(y, y32)
         _lib().reduce(xc.data_ptr(), N.dt(xc), y.data_ptr(), N.dt(y), outer, red, inner, RED[op], N.stream())
@@ -410,7 +411,7 @@ def cat(ts: Sequence[torch.Tensor], axis: int = 0) -> torch.Tensor:
     dt = ts[0].dtype
     shape = list(ts[0].shape)
     shape[axis] = sum(t.shape[axis] for t in ts)
-    out = torch.empty(shape, dtype=dt, device=ts[0].device)
+    out = _mem.empty(shape, dtype=dt, device=ts[0].device)
     o = 0
     for t in ts:
         n = t.shape[axis]
@@ -447,7 +448,7 @@ def tile(x: torch.Tensor, repeats: Sequence[int]) -> torch.Tensor:
     inter = []
     for r, s in zip(reps, xs.shape):
         inter += [r, s]
-    out = torch.empty(inter, dtype=x.dtype, device=x.device)
+    out = _mem.empty(inter, dtype=x.dtype, device=x.device)
     src = xs.reshape([v for s in xs.shape for v in (1, s)]).expand(*inter)
     copy_(out, src)
     return out.reshape([r * s for r, s in zip(reps, xs.shape)])
@@ -473,7 +474,7 @@ def expand(x: torch.Tensor, shape) -> torch.Tensor:
         return x
     if not on_gpu(x) and not CP.copy_ok(x):
         return x.expand(*shape).contiguous()
-    out = torch.empty(shape, dtype=x.dtype, device=x.device)
+    out = _mem.empty(shape, dtype=x.dtype, device=x.device)
     return copy_(out, x.expand(*shape) if x.dim() == len(shape) else x)
 
 
@@ -493,7 +494,7 @@ def index_select(x: torch.Tensor, axis: int, idx: torch.Tensor) -> torch.Tensor:
         xc, ic = contiguous(x), contiguous(idx)
         outer = int(math.prod(x.shape[:axis]))
         inner = int(math.prod(x.shape[axis + 1:]))
-        out = torch.empty(x.shape[:axis] + tuple(idx.shape) + x.shape[axis + 1:], dtype=x.dtype)
+        out = _mem.empty(x.shape[:axis] + tuple(idx.shape) + x.shape[axis + 1:], dtype=x.dtype)
         if out.numel():
             CP.lib().index_select(xc.data_ptr(), ic.data_ptr(), int(ic.dtype == torch.int64), out.data_ptr(), outer,
                                   x.shape[axis], inner, ic.numel(), x.element_size())
@@ -505,7 +506,7 @@ def index_select(x: torch.Tensor, axis: int, idx: torch.Tensor) -> torch.Tensor:
     xc = contiguous(x)
     outer = int(math.prod(x.shape[:axis]))
     inner = int(math.prod(x.shape[axis + 1:]))
-    out = torch.empty(x.shape[:axis] + tuple(idx.shape) + x.shape[axis + 1:], dtype=x.dtype, device=x.device)
+    out = _mem.empty(x.shape[:axis] + tuple(idx.shape) + x.shape[axis + 1:], dtype=x.dtype, device=x.device)
     if out.numel():
         _lib().index_select(xc.data_ptr(), idx.data_ptr(), int(idx.dtype == torch.int64), out.data_ptr(), outer,
                             x.shape[axis], inner, idx.numel(), x.element_size(), N.stream())
@@ -551,7 +552,7 @@ def gather_elements(x: torch.Tensor, axis: int, idx: torch.Tensor) -> torch.Tens
     inner = int(math.prod(idx.shape[axis + 1:]))
     if tuple(x.shape[:axis]) != tuple(idx.shape[:axis]) or tuple(x.shape[axis + 1:]) != tuple(idx.shape[axis + 1:]):
         raise NotImplementedError("gather_elements: index shape must match the data outside the axis")
-    out = torch.empty(idx.shape, dtype=x.dtype, device=x.device)
+    out = _mem.empty(idx.shape, dtype=x.dtype, device=x.device)
     _lib().gather_el(xc.data_ptr(), ic.data_ptr(), int(ic.dtype == torch.int64), out.data_ptr(), N.dt(x), outer,
                      x.shape[axis], idx.shape[axis], inner, N.stream())
     return out
@@ -613,7 +614,7 @@ def pad(x: torch.Tensor, before: Sequence[int], after: Sequence[int], mode: str 
             return torch.nn.functional.pad(x, tp, mode="constant", value=value)
         maps = _pad_maps(x.shape, osz, before, mode)
         return x[torch.meshgrid(*[torch.as_tensor(m) for m in maps], indexing="ij")]
-    y = torch.empty(osz, dtype=x.dtype, device=x.device)
+    y = _mem.empty(osz, dtype=x.dtype, device=x.device)
     _lib().pad_nd(x.data_ptr(), y.data_ptr(), N.dt(x), osz, list(x.shape), list(x.stride()), list(before), PAD[mode],
                   float(value), N.stream())
     return y
@@ -654,7 +655,7 @@ def kth_largest_abs(x: torch.Tensor, k: int) -> torch.Tensor:
     key = (x.device, torch.cuda.current_stream(x.device).cuda_stream)
     ws = _KTH_WS.get(key)
     if ws is None:
-        ws = _KTH_WS[key] = torch.empty(2048 + 2, dtype=torch.int32, device=x.device)
-    out = torch.empty((), dtype=torch.float32, device=x.device)
+        ws = _KTH_WS[key] = _mem.empty(2048 + 2, dtype=torch.int32, device=x.device)
+    out = _mem.empty((), dtype=torch.float32, device=x.device)
     _lib().kth_largest_abs(x.data_ptr(), x.numel(), int(k), out.data_ptr(), ws.data_ptr(), N.stream())
     return out

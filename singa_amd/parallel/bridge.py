@@ -23,6 +23,7 @@ from typing import List, Optional, Tuple
 
 import torch
 
+from .. import memory as _mem
 from .. import autograd
 from ..autograd import Operator, _next_seq
 from ..tensor import Tensor
@@ -131,16 +132,16 @@ class P2PChannel:
         requires-grad flag of the sender)."""
         k = self.k.get(peer, 0)
         self.k[peer] = k + 1
-        hdr = torch.empty(3 + _MAXD, dtype=torch.int64, device=dev.torch_device)
+        hdr = _mem.empty(3 + _MAXD, dtype=torch.int64, device=dev.torch_device)
         h = self.shapes.get((peer, k))
         if h is None:  # first time on this slot: read the header on the host
             self.exchange([hdr], peer)
             self.host_reads += 1
             h = self.shapes[(peer, k)] = [int(v) for v in hdr.cpu().tolist()]
-            buf = torch.empty(tuple(h[3:3 + h[2]]), dtype=_DT[h[0]], device=dev.torch_device)
+            buf = _mem.empty(tuple(h[3:3 + h[2]]), dtype=_DT[h[0]], device=dev.torch_device)
             self.exchange([buf], peer)
         else:
-            buf = torch.empty(tuple(h[3:3 + h[2]]), dtype=_DT[h[0]], device=dev.torch_device)
+            buf = _mem.empty(tuple(h[3:3 + h[2]]), dtype=_DT[h[0]], device=dev.torch_device)
             self.exchange([hdr, buf], peer)
             self.checks.append((hdr, h, (peer, k)))
         return buf, bool(h[1])
@@ -202,7 +203,7 @@ class BridgeSend(Operator):
         return x
 
     def backward(self, dy=None):
-        g = torch.empty(self.shape, dtype=self.dtype, device=self.device)
+        g = _mem.empty(self.shape, dtype=self.dtype, device=self.device)
         self.chan.exchange([g], self.peer)
         return g
 

@@ -33,6 +33,7 @@ from typing import List, Optional, Sequence
 
 import torch
 
+from .. import memory as _mem
 from .. import autograd
 from ..ops import functional as F
 from ..ops import glue as G
@@ -180,7 +181,7 @@ class DistOpt:
         if self.grad_dtype == torch.float32 or not g.is_cuda:
             return self.comm.all_reduce(g, async_op=True)
         if self._stage is None or self._stage.numel() != self.store.g.numel():
-            self._stage = torch.empty(self.store.g.numel(), dtype=torch.bfloat16, device=g.device)
+            self._stage = _mem.empty(self.store.g.numel(), dtype=torch.bfloat16, device=g.device)
         stg = self._stage[s:e]
         cs = getattr(self.comm, "comm_stream", None)
         if cs is None:
@@ -222,7 +223,7 @@ class DistOpt:
         (native copies in and out)."""
         dev = tensors[0].data.device
         total = sum(t.data.numel() for t in tensors)
-        flat = torch.empty(total, dtype=torch.float32, device=dev)
+        flat = _mem.empty(total, dtype=torch.float32, device=dev)
         o = 0
         for t in tensors:
             n = t.data.numel()

@@ -28,6 +28,7 @@ from typing import Optional
 
 import torch
 
+from .. import memory as _mem
 from ..ops import glue as G
 from ..ops import native as N
 from .communicator import Communicator
@@ -90,15 +91,15 @@ class ElasticSync(_SyncBase):
         if self.sharded:
             n = self.store.numel // self.comm.world_size
             r = self.comm.rank
-            self.centre = torch.empty(n, dtype=w.dtype, device=w.device)
+            self.centre = _mem.empty(n, dtype=w.dtype, device=w.device)
             G.copy_(self.centre, w[r * n:(r + 1) * n])
-            self._shard = torch.empty_like(self.centre)
-            self._full = torch.empty_like(w)  # the gathered centre the next difference reads
+            self._shard = _mem.empty_like(self.centre)
+            self._full = _mem.empty_like(w)  # the gathered centre the next difference reads
             G.copy_(self._full, w)
         else:
-            self.centre = torch.empty_like(w)
+            self.centre = _mem.empty_like(w)
             G.copy_(self.centre, w)
-        self._d = torch.empty_like(w)
+        self._d = _mem.empty_like(w)
 
     def _can_overlap(self) -> bool:
         return self.overlap and self.store.w.is_cuda and getattr(self.comm, "comm_stream", None) is not None
@@ -109,10 +110,23 @@ class ElasticSync(_SyncBase):
             torch.cuda.current_stream(self.store.w.device).wait_event(self._pending)
             self._pending = None
 
+    def _ensure_buffers(self) -> None:
+        """After a checkpoint restore only the centre is set: rebuild the
+        difference buffer and (sharded) the gathered centre -- collectively,
+        every rank resumes together."""
+        w = self.store.w
+        if self._d is None:
+            self._d = _mem.empty_like(w)
+        if self.sharded and self._full is None:
+            self._shard = _mem.empty_like(self.centre)
+            self._full = _mem.empty_like(w)
+            self.comm.all_gather(self._full, self.centre)
+
     def sync(self) -> None:
         w = self.store.w
         if self.centre is None:
             self.bootstrap()
+        self._ensure_buffers()
         self.wait()  # the previous exchange wrote the centre and read d
         c = self._full if self.sharded else self.centre
         d = self._d
@@ -158,7 +172,7 @@ class RandomSync(_SyncBase):
 
     def bootstrap(self) -> None:
         super().bootstrap()
-        self.snapshot = torch.empty_like(self.store.w)
+        self.snapshot = _mem.empty_like(self.store.w)
         G.copy_(self.snapshot, self.store.w)
 
     def configure_bandwidth(self, step_seconds: float, bandwidth_mbps: Optional[float] = None,
@@ -186,7 +200,7 @@ class RandomSync(_SyncBase):
         n = w.numel()
         m, a, b = self._progression(n, step)
         if self._buf is None or self._buf.numel() < m:
-            self._buf = torch.empty(m, dtype=torch.float32, device=w.device)
+            self._buf = _mem.empty(m, dtype=torch.float32, device=w.device)
         buf = self._buf[:m]
         if w.is_cuda:
             L = N.lib()

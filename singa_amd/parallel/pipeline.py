@@ -33,6 +33,7 @@ from typing import List, Tuple
 
 import numpy as np
 
+from .. import memory as _mem
 from .. import autograd
 
 SCHEDULES = ("gpipe", "1f1b")
@@ -102,7 +103,7 @@ def pipelined_step(net, zero_grad, m: int, kind: str = "1f1b") -> np.ndarray:
         import torch
 
         from ..ops import glue as G
-        t = G.copy_(torch.empty(2, dtype=torch.float32, device=net.dev.torch_device),
+        t = G.copy_(_mem.empty(2, dtype=torch.float32, device=net.dev.torch_device),
                     torch.tensor(met, dtype=torch.float32))
         net.comm.all_reduce(t)
         met = t.cpu().double().numpy()

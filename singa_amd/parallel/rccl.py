@@ -35,6 +35,7 @@ from typing import List, Optional
 
 import torch
 
+from .. import memory as _mem
 from ..ops import native as N
 from .communicator import Communicator
 
@@ -145,7 +146,7 @@ class RcclCommunicator(Communicator):
         fn(cs.cuda_stream)
         if not torch.cuda.is_current_stream_capturing():
             for t in tensors:  # the caching allocator must not recycle them before the comm stream is done
-                t.record_stream(cs)
+                _mem.record_stream(t, cs)
         ev = torch.cuda.Event()
         ev.record(cs)
         return Work(ev, tensors)
@@ -235,7 +236,7 @@ class RcclCommunicator(Communicator):
                     keep, comm._group_keep = comm._group_keep, None
                     if keep and not comm.host and not torch.cuda.is_current_stream_capturing():
                         for t in keep:  # the group's kernels run on the current stream
-                            t.record_stream(torch.cuda.current_stream(comm.device))
+                            _mem.record_stream(t, torch.cuda.current_stream(comm.device))
                 return False
         return _G()
 

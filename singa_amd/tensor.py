@@ -23,6 +23,7 @@ from typing import Iterable, Optional, Sequence, Tuple, Union
 import numpy as np
 import torch
 
+from . import memory as _mem
 from . import device as _dev
 from .ops import functional as _F
 from .ops import glue as _G
@@ -130,7 +131,7 @@ class Tensor:
         return self.transpose()
 
     def reset_like(self, t: "Tensor") -> None:
-        self.data = torch.empty_like(t.data)
+        self.data = _mem.empty_like(t.data)
         self.device = t.device
 
     def as_type(self, dtype) -> "Tensor":
@@ -173,7 +174,7 @@ class Tensor:
             _G.copy_(self.data.view(-1)[offset:offset + src.numel()], src.reshape(-1))
 
     def clone(self) -> "Tensor":
-        t = self._wrap(_G.copy_(torch.empty(self.data.shape, dtype=self.data.dtype, device=self.data.device),
+        t = self._wrap(_G.copy_(_mem.empty(self.data.shape, dtype=self.data.dtype, device=self.data.device),
                                 self.data))
         t.requires_grad, t.stores_grad, t.name = self.requires_grad, self.stores_grad, self.name
         return t
@@ -197,7 +198,7 @@ class Tensor:
 
     # ----------------------------------------------------------- initialisers
     def bernoulli(self, p: float, inplace: bool = True) -> "Tensor":
-        u = _G.random_(torch.empty(self.data.shape, dtype=torch.float32, device=self.data.device), "uniform", 0.0,
+        u = _G.random_(_mem.empty(self.data.shape, dtype=torch.float32, device=self.data.device), "uniform", 0.0,
                        1.0, self.device)
         d = _G.binary("lt", u, float(p))
         if inplace:
@@ -206,12 +207,12 @@ class Tensor:
         return self._wrap(_G.to(d, self.dtype))
 
     def gaussian(self, mean: float, std: float, inplace: bool = True) -> "Tensor":
-        d = self.data if inplace else torch.empty(self.data.shape, dtype=self.dtype, device=self.data.device)
+        d = self.data if inplace else _mem.empty(self.data.shape, dtype=self.dtype, device=self.data.device)
         _G.random_(d, "gaussian", mean, std, self.device)
         return self if inplace else self._wrap(d)
 
     def uniform(self, low: float, high: float, inplace: bool = True) -> "Tensor":
-        d = self.data if inplace else torch.empty(self.data.shape, dtype=self.dtype, device=self.data.device)
+        d = self.data if inplace else _mem.empty(self.data.shape, dtype=self.dtype, device=self.data.device)
         _G.random_(d, "uniform", low, high, self.device)
         return self if inplace else self._wrap(d)
 
@@ -360,7 +361,7 @@ def product(shape) -> int:
 
 
 def sizeof(dtype) -> int:
-    return torch.empty((), dtype=dtype).element_size()
+    return _mem.empty((), dtype=dtype).element_size()
 
 
 def reshape(t: Tensor, shape) -> Tensor:

@@ -782,3 +782,62 @@ def test_bn_identity_sum_backward_matches_reduction(gpu, small_gamma):
     assert max(ab.values()) < (1e-3 if small_gamma is True else 3e-2), ab
     if small_gamma == "gate_edge":  # the input gradient too
         assert rel_err(g_on[id(blks[0].conv1.W)], g_off[id(blks[0].conv1.W)]) < 3e-2
+
+
+def test_lazy_residual_gradient_matches_materialised(gpu):
+    """Residual BN(+ReLU) backward keeps the shortcut gradient lazy
+    (F.MaskedGrad: dy + 1-bit mask); the consuming 1x1 conv's dgrad adds it in
+    its epilogue (conv_dgrad_res).  Two identity-shortcut bottlenecks (plus a
+    downsample one in front) A/B against the materialised path: every
+    parameter gradient agrees to bf16 rounding, and the lazy path really ran."""
+    from singa_amd import autograd as AG
+    from singa_amd.models.resnet import Bottleneck
+    from singa_amd.ops import functional as FF
+
+    dev = device.create_rocm_gpu()
+    dev.SetRandSeed(9)
+    blks = [Bottleneck(16, 1, True), Bottleneck(16, 1, False), Bottleneck(16, 1, False)]
+    g = torch.Generator(device=gpu).manual_seed(3)
+    xf = torch.randn(8, 32, 14, 14, device=gpu, generator=g)
+    dyt = None
+    lazy0 = FF.LAZY_RES
+    calls = []
+    orig = FF._conv_bwd_res
+
+    def spy(*a, **k):
+        calls.append(1)
+        return orig(*a, **k)
+
+    def run(on):
+        nonlocal dyt
+        FF.LAZY_RES = on
+        AG.training = True
+        x = Tensor(data=xf.bfloat16().contiguous(memory_format=torch.channels_last), device=dev, requires_grad=True,
+                   stores_grad=False)
+        try:
+            h = x
+            for b in blks:
+                h = b(h)
+            if dyt is None:
+                dyt = torch.randn(h.shape, device=gpu, generator=g)
+            loss_t = AG.reduce_sum(AG.mul(h, Tensor(data=dyt.bfloat16().contiguous(
+                memory_format=torch.channels_last), device=dev, requires_grad=False)), None)
+            gr = {id(p): gg.data.float().clone() for p, gg in AG.backward(loss_t)}
+        finally:
+            AG.training = False
+            FF.LAZY_RES = lazy0
+        return gr
+
+    run(False)  # creates the parameters
+    FF._conv_bwd_res = spy
+    try:
+        g_on = run(True)
+    finally:
+        FF._conv_bwd_res = orig
+    g_off = run(False)
+    assert len(calls) == 2  # the two identity-shortcut blocks' conv1 absorbed the lazy gradient
+    errs = {}
+    for i, b in enumerate(blks):
+        for k, p in b.get_params().items():
+            errs[f"{i}.{k}"] = rel_err(g_on[id(p)], g_off[id(p)])
+    assert max(errs.values()) < 2e-2, errs
