@@ -88,6 +88,7 @@ struct BlockInfo {
   uintptr_t stream;
   int pool;
   std::vector<uintptr_t> uses;
+  bool in_capture = false;  // a default-pool block handed out while its stream was being captured
 };
 struct Pending {
   void* ptr;
@@ -96,6 +97,17 @@ struct Pending {
 };
 
 thread_local int t_pool = 0;  // private pool of the capture this thread is running (0: default pool)
+
+// hipMalloc / hipFree / event queries are "potentially unsafe" while a
+// stream is captured in the default (global) mode and would invalidate the
+// capture; the pool's own driver calls are not part of any captured work, so
+// they run with this thread's capture mode relaxed (as PyTorch's allocator
+// does around cudaMalloc)
+struct RelaxedCapture {
+  hipStreamCaptureMode m = hipStreamCaptureModeRelaxed;
+  RelaxedCapture() { (void)hipThreadExchangeStreamCaptureMode(&m); }
+  ~RelaxedCapture() { (void)hipThreadExchangeStreamCaptureMode(&m); }
+};
 
 class DevicePool {
  public:
@@ -121,7 +133,7 @@ class DevicePool {
     } else {
       p = driver_alloc_locked(sz);
     }
-    live_[p] = BlockInfo{sz, stream, pool, {}};
+    live_[p] = BlockInfo{sz, stream, pool, {}, pool == 0 && capturing(stream)};
     st_.in_use += sz;
     if (st_.in_use > st_.peak_in_use) st_.peak_in_use = st_.in_use;
     return p;
@@ -137,10 +149,11 @@ class DevicePool {
     st_.in_use -= b.size;
     if (b.pool > 0 && dead_.count(b.pool)) b.pool = 0;  // its graph is gone: back to the default pool
     const bool capt = capturing(b.stream);
-    if (capt && b.pool == 0) {
-      // a default-pool block whose last tensor died while its stream is being
-      // captured: the graph may address it on every replay, so it is never
-      // handed out again (and never returned to the driver)
+    if ((capt || b.in_capture) && b.pool == 0) {
+      // a default-pool block used by a capture outside any private pool (freed
+      // during the capture, or handed out inside it): the graph may address it
+      // on every replay, so it is never handed out again (nor returned to the
+      // driver).  Model captures use private pools instead (memory.graph_pool)
       parked_.push_back(std::make_pair(p, b.size));
       return;
     }
@@ -153,6 +166,7 @@ class DevicePool {
       return;
     }
     Pending pd{p, b, {}};
+    RelaxedCapture rc;
     for (uintptr_t s : b.uses) {
       hipEvent_t ev;
       hip_check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
@@ -247,6 +261,7 @@ class DevicePool {
     return false;
   }
   void* driver_alloc_locked(size_t sz) {
+    RelaxedCapture rc;
     int cur = 0;
     hip_check(hipGetDevice(&cur), "hipGetDevice");
     if (cur != dev_) hip_check(hipSetDevice(dev_), "hipSetDevice");
@@ -264,10 +279,13 @@ class DevicePool {
     return p;
   }
   void driver_free_locked(void* p, size_t sz) {
+    RelaxedCapture rc;
     hipFree(p);
     st_.reserved -= sz;
   }
   void reap_locked() {
+    if (pending_.empty()) return;
+    RelaxedCapture rc;
     for (size_t i = 0; i < pending_.size();) {
       bool done = true;
       for (hipEvent_t ev : pending_[i].evs)
