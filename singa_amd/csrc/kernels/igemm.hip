@@ -1155,7 +1155,7 @@ __global__ void __launch_bounds__(256) wdot_colsum_k(const bf16* __restrict__ w,
     // the producer BN's gate (bn_bwd_finalize_wdot_k): the recovered xhat
     // carries y's bf16 rounding times |xhat| + |beta / gamma|
     const float g = fabsf(gamma[c]);
-    if (!(g >= tau && fabsf(beta[c]) <= 16.f * g)) *flag = 1;  // (NaN raises it too)
+    if (!(g >= tau && fabsf(beta[c]) <= 4.f * g)) *flag = 1;  // (NaN raises it too)
   }
   const int r0 = blockIdx.y * WDOT_RB;
   float a = 0.f;

@@ -894,7 +894,7 @@ FUSE_RES_BN_BWD = os.environ.get("SINGA_AMD_FUSE_RES_BN_BWD", "0") == "1"
 # from <W, dW> of its weight gradient
 BN_WDOT_MODE = int(os.environ.get("SINGA_AMD_BN_WDOT", "1"))  # 0 off, 1 every consuming conv, 2 only 1x1 ones
 BN_WDOT = BN_WDOT_MODE > 0
-BN_WDOT_TAU = 0.05  # |gamma| below this (or |beta| > 16 |gamma|): the exact reduction runs instead
+BN_WDOT_TAU = 0.05  # |gamma| below this (or |beta| > 4 |gamma|): the exact reduction runs instead
 
 
 _WT_CACHE: dict = {}

@@ -721,7 +721,8 @@ def test_bn_identity_sum_backward_matches_reduction(gpu, small_gamma):
     bf16 rounding.  small_gamma: some bn1/bn2 channels get |gamma| < tau, which
     must switch those layers to the gated exact reduction.  gate_edge: every
     third channel sits just inside the recovery gate (|gamma| = 1.2 tau,
-    beta = 15 |gamma|), where the recovered sum(g~ xhat) =
+    beta = 3.75 |gamma|; the gate admits |beta| <= 4 |gamma|), where the
+    recovered sum(g~ xhat) =
     (<W, dW> - beta sum(g~)) / gamma cancels the most; dgamma and the input
     gradient must still agree with the exact reduction."""
     from singa_amd import autograd as AG
@@ -765,7 +766,7 @@ def test_bn_identity_sum_backward_matches_reduction(gpu, small_gamma):
                 if k in ("bn1.scale", "bn2.scale"):
                     p.data[::3] = gam
                 if k in ("bn1.bias", "bn2.bias"):
-                    p.data[::3] = 15.0 * gam
+                    p.data[::3] = 3.75 * gam
     elif small_gamma:
         for b in blks:
             for k, p in b.get_params().items():
