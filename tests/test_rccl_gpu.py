@@ -219,12 +219,45 @@ def test_sparse_topk_threshold_is_exact(gpu):
 # comm-stream fork / join, DistOpt's fp32 and bf16 bucket staging and the
 # sharded EASGD centre at the world sizes of the 8-GPU run
 # (csrc/comm/loop_comm.cpp, parallel/loop.py).
+_INIT = __import__("threading").Lock()
+
+
+def _mlp_step_locked(rank, world, comm, steps, bf16):
+    """_mlp_step for rank threads sharing one device object: the seeded
+    parameter init of each rank runs under a lock (the device RNG is shared),
+    so rank 0's initial weights -- which DistOpt broadcasts -- are exactly the
+    single-process reference's."""
+    from singa_amd import device, opt, tensor
+    from singa_amd.models import mlp
+    from singa_amd.parallel import DistOpt
+
+    dev = device.create_rocm_gpu_on(0)
+    rng = np.random.RandomState(0)
+    X = rng.randn(16, 40).astype(np.float32)
+    Y = rng.randint(0, 10, 16).astype(np.int32)
+    n = 16 // world
+    x = tensor.from_numpy(X[rank * n:(rank + 1) * n], dev)
+    y = tensor.from_numpy(Y[rank * n:(rank + 1) * n], dev)
+    m = mlp.create_model((64, 48), 10)
+    with _INIT:
+        dev.SetRandSeed(11 + rank)
+        m.compile([x], is_train=False)
+        torch.cuda.current_stream().synchronize()
+    m.set_optimizer(DistOpt(opt.SGD(0.1, 0.9), comm=comm, bucket_mb=0.004, first_bucket_mb=0.002,
+                            grad_dtype=torch.bfloat16 if bf16 else torch.float32))
+    m.compile([x], is_train=True)
+    for _ in range(steps):
+        m(x, y)
+    torch.cuda.current_stream().synchronize()
+    return {k: v.data.float().cpu().numpy() for k, v in m.get_params().items()}
+
+
 @pytest.mark.parametrize("world", [2, 4, 8])
 @pytest.mark.parametrize("bf16", [False, True])
 def test_loopback_distopt_equals_single_process_step(gpu, world, bf16):
     from singa_amd.parallel.loop import run_ranks as loop_ranks
 
-    res = loop_ranks(_mlp_step, world, 3, bf16, device=torch.device("cuda", 0), timeout_s=120.0)
+    res = loop_ranks(_mlp_step_locked, world, 3, bf16, device=torch.device("cuda", 0), timeout_s=120.0)
     ref = _single_process(gpu)
     for k in ref:
         for r in range(world):
