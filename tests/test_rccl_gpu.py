@@ -273,9 +273,11 @@ def _easgd_gpu_rank(rank, world, comm, sharded):
     from singa_amd.parallel.easgd import ElasticSync
     from singa_amd.tensor import Tensor
 
+    from singa_amd import device
+    dev = device.create_rocm_gpu_on(0)
     g = torch.Generator().manual_seed(0)
-    p = Tensor(data=torch.randn(1000, generator=g).to(gpu_dev()), requires_grad=True, stores_grad=True)
-    q = Tensor(data=torch.randn(30, 7, generator=g).to(gpu_dev()), requires_grad=True, stores_grad=True)
+    p = Tensor(device=dev, data=torch.randn(1000, generator=g).to(gpu_dev()), requires_grad=True, stores_grad=True)
+    q = Tensor(device=dev, data=torch.randn(30, 7, generator=g).to(gpu_dev()), requires_grad=True, stores_grad=True)
     st = SGD(0.1).attach([p, q])
     es = ElasticSync(st, comm, moving_rate=0.5, sharded=sharded)
     es.bootstrap()
@@ -315,8 +317,10 @@ def _easgd_rounds_rank(rank, world, comm, sharded, overlap):
     from singa_amd.parallel.easgd import ElasticSync
     from singa_amd.tensor import Tensor
 
+    from singa_amd import device
+    dev = device.create_rocm_gpu_on(0)
     g = torch.Generator().manual_seed(0)
-    p = Tensor(data=torch.randn(4096, generator=g).to(gpu_dev()), requires_grad=True, stores_grad=True)
+    p = Tensor(device=dev, data=torch.randn(4096, generator=g).to(gpu_dev()), requires_grad=True, stores_grad=True)
     st = SGD(0.1).attach([p])
     es = ElasticSync(st, comm, moving_rate=0.9, sharded=sharded, overlap=overlap)
     es.bootstrap()
