@@ -148,6 +148,7 @@ void sg_bn_set_rows_per_thread(int);
 void register_rccl(py::module& m);  // csrc/comm/rccl_comm.cpp
 void register_mem(py::module& m);   // csrc/mem/pool.cpp
 void register_loop(py::module& m);  // csrc/comm/loop_comm.cpp
+void register_stream_graph(py::module& m);  // csrc/mem/stream_graph.cpp
 
 static void check_launch(const char* what) {
   hipError_t e = hipGetLastError();
@@ -160,6 +161,7 @@ PYBIND11_MODULE(_C, m) {
   register_rccl(m);
   register_mem(m);
   register_loop(m);
+  register_stream_graph(m);
 
   m.def("device_info", []() {
     py::dict d;

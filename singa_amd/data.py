@@ -25,6 +25,7 @@ import numpy as np
 import torch
 
 from . import memory as _mem
+from . import stream as _stream
 
 
 class ArrayIterator:
@@ -181,7 +182,7 @@ class DevicePrefetcher:
     def __init__(self, it, device: Optional[torch.device] = None):
         self.it = iter(it)
         self.device = device or torch.device("cuda")
-        self.stream = torch.cuda.Stream(device=self.device) if self.device.type == "cuda" else None
+        self.stream = _stream.Stream(self.device) if self.device.type == "cuda" else None
         self.next = None
         self._preload()
 
@@ -196,7 +197,7 @@ class DevicePrefetcher:
             return
         xp, yp = torch.from_numpy(np.ascontiguousarray(x)).pin_memory(), torch.from_numpy(
             np.ascontiguousarray(y)).pin_memory()
-        with torch.cuda.stream(self.stream):
+        with self.stream:
             self.next = (xp.to(self.device, non_blocking=True), yp.to(self.device, non_blocking=True))
 
     def __iter__(self):
@@ -206,7 +207,7 @@ class DevicePrefetcher:
         if self.next is None:
             raise StopIteration
         if self.stream is not None:
-            torch.cuda.current_stream(self.device).wait_stream(self.stream)
+            _stream.Event().record(self.stream).wait()  # the consumer's stream joins the copies
         cur = self.next
         for t in cur:
             if self.stream is not None:

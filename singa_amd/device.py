@@ -221,8 +221,9 @@ class Timer:
 
     def __enter__(self):
         if self.gpu:
-            self.s = torch.cuda.Event(enable_timing=True)
-            self.e = torch.cuda.Event(enable_timing=True)
+            from . import stream as _stream
+            self.s = _stream.Event(timing=True)
+            self.e = _stream.Event(timing=True)
             self.s.record()
         else:
             self.t0 = time.perf_counter()

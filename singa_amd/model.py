@@ -29,6 +29,7 @@ import torch
 from . import autograd
 from . import layer
 from . import memory as _mem
+from . import stream as _stream
 from .ops import functional as _F
 from .ops import glue as G
 from .tensor import Tensor
@@ -142,15 +143,6 @@ class Model(layer.Layer):
                 finally:
                     _F.ARENA.end()
             torch.cuda.synchronize()
-            g = torch.cuda.CUDAGraph()
-            # one memory pool PER graph: a shared pool would let the eval
-            # graph's static outputs live in blocks the train graph uses for
-            # intermediates, so a train replay would overwrite an eval result
-            # the caller still holds.  (A graph's own outputs stay valid only
-            # until that same graph is replayed again.)
-            if self._pool is None:
-                self._pool = {}
-            pool = self._pool.setdefault(key, torch.cuda.graph_pool_handle())
             if opt is not None:
                 getattr(opt, "opt", opt).graph_mode = True
                 opt.prepare_step()
@@ -158,12 +150,8 @@ class Model(layer.Layer):
             dev = args[0].device
             keep: list = []
             _F.CAPTURE_KEEP = keep
-            # the step's activations and temporaries come from a PRIVATE native
-            # pool: blocks freed inside the capture are reused within it, and
-            # none is handed to eager work while the graph can still replay
-            gp = _mem.graph_pool(args[0].data.device)
-            keep.append(gp)
-            with torch.cuda.graph(g, pool=pool), gp:
+
+            def body():
                 # first captured kernel: advance the device RNG epoch, so
                 # dropout masks differ on every replay (host-side Philox
                 # offsets are frozen into the captured launches)
@@ -171,10 +159,29 @@ class Model(layer.Layer):
                 if self.training:
                     _F.ARENA.begin(args[0].data.device)  # the arena's zeroing kernel is captured too
                 try:
-                    out = fn(*args, **kwargs)
+                    return fn(*args, **kwargs)
                 finally:
                     _F.ARENA.end()
-                    _F.CAPTURE_KEEP = None
+
+            try:
+                if os.environ.get("SINGA_AMD_NATIVE_GRAPH", "1") != "0":
+                    # framework-owned capture (hipStreamBeginCapture on a native
+                    # stream); the step's memory is the graph's private native
+                    # pool -- one per graph, so the eval graph's static outputs
+                    # never share blocks with the train graph's temporaries
+                    g = _stream.StepGraph(args[0].data.device)
+                    out = g.capture(body)
+                else:
+                    g = torch.cuda.CUDAGraph()
+                    if self._pool is None:
+                        self._pool = {}
+                    pool = self._pool.setdefault(key, torch.cuda.graph_pool_handle())
+                    gp = _mem.graph_pool(args[0].data.device)
+                    keep.append(gp)
+                    with torch.cuda.graph(g, pool=pool), gp:
+                        out = body()
+            finally:
+                _F.CAPTURE_KEEP = None
             if opt is not None:
                 opt.step_counter = sc0  # capture does not execute; replay below does
             self._graphs[key] = (g, tuple(args), out, keep)
@@ -193,8 +200,11 @@ class Model(layer.Layer):
 
     def reset_graph(self) -> None:
         gs, self._graphs = self._graphs, {}
+        for g, _, _, keep in gs.values():
+            if isinstance(g, _stream.StepGraph):
+                g.release()  # the graph, then its private memory
         pools = [k for ent in gs.values() for k in ent[3] if isinstance(k, _mem.graph_pool)]
-        del gs  # the graphs go first; then their private memory
+        del gs
         for k in pools:
             k.release()
         self._warm.clear()

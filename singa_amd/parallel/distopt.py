@@ -33,6 +33,7 @@ from typing import List, Optional, Sequence
 
 import torch
 
+from .. import stream as _stream
 from .. import memory as _mem
 from .. import autograd
 from ..ops import functional as F
@@ -147,7 +148,7 @@ class DistOpt:
                 works.append(self._reduce_bucket(b))
         ev = None
         if self.time_exposed and torch.cuda.is_available() and self.store.g.is_cuda and not capturing:
-            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev = (_stream.Event(timing=True), _stream.Event(timing=True))
             ev[0].record()
         for w in works:
             if w is not None:
@@ -190,12 +191,11 @@ class DistOpt:
             G.copy_(g, stg)
             return None
         cs.wait_stream(torch.cuda.current_stream(g.device))
-        with torch.cuda.stream(cs):
+        with cs:
             G.copy_(stg, g)  # fp32 -> bf16 (native copy kernel)
             self.comm.all_reduce(stg)  # on the comm stream (its "current" stream here)
             G.copy_(g, stg)
-            ev = torch.cuda.Event()
-            ev.record(cs)
+            ev = _stream.Event().record(cs)
         from .rccl import Work
         return Work(ev, (g, stg))
 

@@ -28,6 +28,7 @@ from typing import Optional
 
 import torch
 
+from .. import stream as _stream
 from .. import memory as _mem
 from ..ops import glue as G
 from ..ops import native as N
@@ -107,7 +108,7 @@ class ElasticSync(_SyncBase):
     def wait(self) -> None:
         """Join an in-flight overlapped exchange into the current stream."""
         if self._pending is not None:
-            torch.cuda.current_stream(self.store.w.device).wait_event(self._pending)
+            self._pending.wait()  # the current stream joins the comm stream
             self._pending = None
 
     def _ensure_buffers(self) -> None:
@@ -141,11 +142,9 @@ class ElasticSync(_SyncBase):
         if self._can_overlap():
             cs = self.comm.comm_stream
             cs.wait_stream(torch.cuda.current_stream(w.device))
-            with torch.cuda.stream(cs):
+            with cs:
                 self._exchange(d)
-                ev = torch.cuda.Event()
-                ev.record(cs)
-            self._pending = ev
+            self._pending = _stream.Event().record(cs)
         else:
             self._exchange(d)
         self.nsync += 1

@@ -18,6 +18,7 @@ from typing import Callable, List, Optional
 
 import torch
 
+from .. import stream as _stream
 from ..ops import native as N
 from .rccl import RcclCommunicator
 
@@ -39,8 +40,8 @@ def run_ranks(fn: Callable, world: int, *args, device: Optional[torch.device] = 
         try:
             if dev >= 0:
                 torch.cuda.set_device(dev)
-                s = torch.cuda.Stream(device=dev)
-                with torch.cuda.stream(s):
+                s = _stream.Stream(torch.device("cuda", dev))
+                with s:
                     comm = RcclCommunicator(world, r, r, native=native, device=torch.device("cuda", dev))
                     res[r] = fn(r, world, comm, *args)
                 s.synchronize()

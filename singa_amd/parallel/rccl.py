@@ -35,6 +35,7 @@ from typing import List, Optional
 
 import torch
 
+from .. import stream as _stream
 from .. import memory as _mem
 from ..ops import native as N
 from .communicator import Communicator
@@ -62,14 +63,14 @@ class Work:
 
     __slots__ = ("ev", "keep")
 
-    def __init__(self, ev: torch.cuda.Event, keep):
+    def __init__(self, ev, keep):
         self.ev = ev
         self.keep = keep  # tensors referenced until the handle is dropped
 
     def wait(self) -> None:
         """Stream-ordered: the CURRENT stream waits for the collective (the
         host does not block), like a torch.distributed NCCL work."""
-        torch.cuda.current_stream().wait_event(self.ev)
+        self.ev.wait()  # (framework Event: the current stream waits on the device)
         self.keep = None
 
     def is_completed(self) -> bool:
@@ -110,7 +111,7 @@ class RcclCommunicator(Communicator):
         self._c = native
         # high priority: bucket all-reduces issued mid-backward get the CUs
         # they need promptly instead of queueing behind the compute stream
-        self.comm_stream = None if self.host else torch.cuda.Stream(device=self.device, priority=-1)
+        self.comm_stream = None if self.host else _stream.Stream(self.device, priority=-1)
         self.stats = {"calls": 0, "bytes": 0}  # collective calls / payload bytes issued by this rank
         self._group_keep: Optional[list] = None
 
@@ -147,8 +148,7 @@ class RcclCommunicator(Communicator):
         if not torch.cuda.is_current_stream_capturing():
             for t in tensors:  # the caching allocator must not recycle them before the comm stream is done
                 _mem.record_stream(t, cs)
-        ev = torch.cuda.Event()
-        ev.record(cs)
+        ev = _stream.Event().record(cs)
         return Work(ev, tensors)
 
     # ---------------------------------------------------------- collectives

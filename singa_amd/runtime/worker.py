@@ -27,6 +27,7 @@ from typing import Callable, Dict, Optional
 import numpy as np
 import torch
 
+from .. import stream as _stream
 from .. import autograd, opt
 from ..config import schema
 from ..device import Timer, get_default_device
@@ -204,12 +205,12 @@ class Worker:
             self.replicas.append(r)
             self.rep_grads.append(g)
         gpu = self.dev.torch_device.type == "cuda"
-        self.streams = [torch.cuda.Stream(device=self.dev.torch_device) for _ in range(k)] if gpu else None
+        self.streams = [_stream.Stream(self.dev.torch_device) for _ in range(k)] if gpu else None
         # hogwild updates of the SHARED weights/momentum all run on one
         # stream: the lock orders the launches, the single stream serialises
         # the kernels (on per-thread streams they would overlap on the GPU
         # and race their read-modify-write of w and s1)
-        self.upd_stream = torch.cuda.Stream(device=self.dev.torch_device) if gpu else None
+        self.upd_stream = _stream.Stream(self.dev.torch_device) if gpu else None
         self._upd_lock = threading.Lock()
 
     # ------------------------------------------------------------- cadence
@@ -231,7 +232,7 @@ class Worker:
     # ---------------------------------------------------------------- steps
     def _thread_step(self, i: int, out: list) -> None:
         net, g = self.replicas[i], self.rep_grads[i]
-        ctx = torch.cuda.stream(self.streams[i]) if self.streams else _Null()
+        ctx = self.streams[i] if self.streams else _Null()
         try:
             with ctx:
                 outs = net.forward(training=True)
@@ -245,7 +246,7 @@ class Worker:
                         if self.upd_stream is not None:
                             mine = self.streams[i]
                             self.upd_stream.wait_stream(mine)  # this thread's gradient is complete
-                            with torch.cuda.stream(self.upd_stream):
+                            with self.upd_stream:
                                 self.updater.update(grad_scale=1.0, g=g)
                             mine.wait_stream(self.upd_stream)  # g is free to be zeroed again
                         else:
@@ -273,7 +274,7 @@ class Worker:
                     raise r
             if self.streams:
                 for s in self.streams:
-                    cur.wait_stream(s)
+                    _stream.Event().record(s).wait(cur)
             if not self.hogwild:
                 for g in self.rep_grads[1:]:
                     G.binary("add", self.store.g, g, out=self.store.g)

@@ -1,0 +1,153 @@
+"""Framework-owned HIP streams, events and step graphs (``_C.rt``,
+csrc/mem/stream_graph.cpp).
+
+* :class:`Stream` -- a native non-blocking stream (priority selectable).
+  ``with s:`` makes it the current stream of this thread for every launcher
+  (PyTorch's current-stream slot is only the carrier: the handle is wrapped
+  as an ``ExternalStream``, nothing is created by PyTorch).
+* :class:`Event` -- record / wait (device-side join) / query / synchronize /
+  elapsed_ms.
+* :class:`StepGraph` -- capture of a training step on a framework stream with
+  ``hipStreamBeginCapture`` (thread-local mode), one instantiation, replay
+  with ``hipGraphLaunch``; the step's memory comes from a private native pool
+  (:class:`singa_amd.memory.graph_pool`) that lives exactly as long as the
+  graph.  This is :class:`singa_amd.model.Model`'s graph executor.
+
+Reference: the reference had no device-side execution machinery (its CUDA
+path, include/mshadow/tensor_gpu-inl.hpp:26-93, was compiled out); its
+overlap came from ZeroMQ actor threads (src/server/server.cc:53-60).
+"""
+from __future__ import annotations
+
+from typing import Callable, Optional
+
+import torch
+
+from .ops import native as N
+
+
+def _rt():
+    return N.lib().rt
+
+
+def current(device=None) -> int:
+    """Handle of this thread's current stream on ``device``."""
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+class Stream:
+    def __init__(self, device=None, priority: int = 0):
+        idx = torch.device(device).index if device is not None else None
+        self.device_index = idx if idx is not None else torch.cuda.current_device()
+        self._s = _rt().Stream(self.device_index, int(priority))
+        self.handle = self._s.handle
+        # the carrier through which ``with stream:`` sets the current stream
+        self._ext = torch.cuda.ExternalStream(self.handle, device=torch.device("cuda", self.device_index))
+        self._ctx = None
+
+    @property
+    def cuda_stream(self) -> int:  # duck-typing with torch.cuda.Stream for launch helpers
+        return self.handle
+
+    def wait_stream(self, other) -> None:
+        """This stream waits (device-side) for the work queued so far on ``other``."""
+        ev = Event()
+        ev.record(other)
+        ev.wait(self)
+
+    def synchronize(self) -> None:
+        self._s.synchronize()
+
+    def query(self) -> bool:
+        return self._s.query()
+
+    def __enter__(self):
+        self._ctx = torch.cuda.stream(self._ext)
+        self._ctx.__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        ctx, self._ctx = self._ctx, None
+        return ctx.__exit__(*exc)
+
+
+def _handle(s) -> int:
+    if s is None:
+        return current()
+    if isinstance(s, int):
+        return s
+    return s.cuda_stream
+
+
+class Event:
+    def __init__(self, timing: bool = False):
+        self._e = _rt().Event(bool(timing))
+
+    def record(self, stream=None) -> "Event":
+        self._e.record(_handle(stream))
+        return self
+
+    def wait(self, stream=None) -> None:
+        """``stream`` (default: current) waits on the device for this event."""
+        self._e.wait(_handle(stream))
+
+    def query(self) -> bool:
+        return self._e.query()
+
+    def synchronize(self) -> None:
+        self._e.synchronize()
+
+    def elapsed_time(self, end: "Event") -> float:
+        return self._e.elapsed_ms(end._e)
+
+
+_CAPTURE_STREAMS: dict = {}
+
+
+class StepGraph:
+    """One captured step: ``capture(fn, *args)`` runs fn once under capture
+    (nothing executes) on a framework stream forked from the current one and
+    returns fn's result -- the graph's static outputs; ``replay()`` launches
+    the instantiated graph on the current stream."""
+
+    def __init__(self, device=None):
+        from . import memory
+
+        idx = torch.device(device).index if device is not None else None
+        self.device_index = idx if idx is not None else torch.cuda.current_device()
+        self._g = _rt().Graph()
+        self.pool = memory.graph_pool(torch.device("cuda", self.device_index))
+        self.keep: list = []
+
+    def capture(self, fn: Callable, *args, **kwargs):
+        s = _CAPTURE_STREAMS.get(self.device_index)
+        if s is None:
+            s = _CAPTURE_STREAMS[self.device_index] = Stream(torch.device("cuda", self.device_index))
+        cur = current(self.device_index)
+        s.wait_stream(cur)
+        torch_before = torch.cuda.memory_allocated(self.device_index)
+        with s, self.pool:
+            self._g.begin(s.handle)
+            try:
+                out = fn(*args, **kwargs)
+            except BaseException:
+                self._g.abort()
+                raise
+            self._g.end()
+        if torch.cuda.memory_allocated(self.device_index) != torch_before:
+            # a PyTorch allocation inside the capture would live in PyTorch's
+            # allocator, which does not know the graph still uses it
+            raise RuntimeError("StepGraph: the captured step allocated through PyTorch's allocator")
+        Event().record(s).wait(cur)
+        return out
+
+    @property
+    def nodes(self) -> int:
+        return self._g.nodes
+
+    def replay(self) -> None:
+        self._g.replay(current(self.device_index))
+
+    def release(self) -> None:
+        self._g.reset()
+        self.pool.release()

@@ -85,14 +85,16 @@ class ChromeTrace:
         self.t0 = time.perf_counter()
         self._lock = threading.Lock()
         if self.gpu:
-            self.e0 = torch.cuda.Event(enable_timing=True)
+            from .. import stream as _stream
+            self._Ev = _stream.Event
+            self.e0 = _stream.Event(timing=True)
             self.e0.record()
 
     @contextlib.contextmanager
     def span(self, name: str, cat: str = "layer", args: Optional[dict] = None):
         push(name)
         if self.gpu:
-            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a, b = self._Ev(timing=True), self._Ev(timing=True)
             a.record()
             try:
                 yield

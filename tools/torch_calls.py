@@ -4,7 +4,13 @@ says WHICH torch kernels ran, this says WHERE they were called from).
 
 Runs the bench_suite / bench.py workloads for a couple of steps under a
 ``TorchFunctionMode`` that records every torch call touching a CUDA tensor
-other than allocation, metadata and free views, with its call site.
+other than metadata and free views, with its call site.  Allocations are
+reported in their own section: every device tensor of a step should come
+from the framework's native pool (singa_amd/memory.py), so a
+``torch.empty``-family call producing a CUDA tensor is listed as a PyTorch
+allocation, and ``torch.cuda.Stream`` / ``Event`` / ``CUDAGraph``
+constructions are counted too (the framework owns its streams, events and
+graphs: singa_amd/stream.py).
 
     python tools/torch_calls.py --which resnet50,alexnet,bert,bert_sonnx,mlp_gpu,conv_conf
 """
@@ -23,12 +29,13 @@ from torch.overrides import TorchFunctionMode  # noqa: E402
 
 ALLOW = {"__get__", "dim", "size", "stride", "numel", "data_ptr", "element_size", "is_contiguous", "view",
          "as_strided", "permute", "transpose", "t", "unsqueeze", "squeeze", "expand", "movedim", "narrow",
-         "__getitem__", "numpy", "detach", "requires_grad_", "_set_grad_enabled", "empty", "empty_like",
-         "empty_strided", "storage_offset", "untyped_storage", "__len__", "__hash__", "__eq__", "is_floating_point",
+         "__getitem__", "numpy", "detach", "requires_grad_", "_set_grad_enabled", "storage_offset", "untyped_storage", "__len__", "__hash__", "__eq__", "is_floating_point",
          "unbind", "split", "chunk", "from_numpy", "__format__", "__repr__", "tolist", "item", "__float__", "__int__",
          "__bool__", "__index__", "view_as", "get_device", "is_complex", "has_names", "__array__", "_is_view",
          "is_pinned", "__iter__", "ndimension", "nelement", "record_stream", "cuda_stream"}
 MAYBE_VIEW = {"reshape", "contiguous", "float", "to", "flatten", "long", "bfloat16"}
+ALLOC = {"empty", "empty_like", "empty_strided", "zeros", "zeros_like", "ones", "ones_like", "full", "full_like",
+         "rand", "randn", "arange", "tensor"}
 
 
 def _cuda(x) -> bool:
@@ -43,6 +50,7 @@ class Tracer(TorchFunctionMode):
     def __init__(self):
         super().__init__()
         self.calls = collections.Counter()
+        self.allocs = collections.Counter()
 
     def __torch_function__(self, func, types, args=(), kwargs=None):
         kwargs = kwargs or {}
@@ -56,8 +64,29 @@ class Tracer(TorchFunctionMode):
         site = " <- ".join(f"{f.filename.replace(os.getcwd() + '/', '')}:{f.lineno}"
                            for f in traceback.extract_stack()[-6:-1]
                            if "torch_calls.py" not in f.filename)
+        if name in ALLOC:
+            self.allocs[(name, site)] += 1
+            return r
         self.calls[(name, site)] += 1
         return r
+
+
+_CUDA_OBJS = collections.Counter()
+
+
+def _count_cuda_objects():
+    """Count torch.cuda.Stream / Event / CUDAGraph constructions."""
+    for nm in ("Stream", "Event", "CUDAGraph"):
+        orig = getattr(torch.cuda, nm)
+
+        class Sub(orig):  # noqa: D401 - counting subclass
+            def __new__(cls, *a, _nm=nm, **k):
+                site = " <- ".join(f"{f.filename.replace(os.getcwd() + '/', '')}:{f.lineno}"
+                                   for f in traceback.extract_stack()[-5:-1])
+                _CUDA_OBJS[(f"torch.cuda.{_nm}", site)] += 1
+                return orig.__new__(cls, *a, **k)
+        Sub.__name__ = nm
+        setattr(torch.cuda, nm, Sub)
 
 
 def main() -> int:
@@ -66,6 +95,7 @@ def main() -> int:
     ap.add_argument("--native", default="copy_nd,fill,reduce,zero,binary_nd",
                     help="also record the call sites of these native (_C) launches")
     a = ap.parse_args()
+    _count_cuda_objects()
     from singa_amd.ops import native as NN
     L = NN.lib()
     nat = collections.Counter()
@@ -109,6 +139,20 @@ def main() -> int:
         print(f"== {w}: {sum(tr.calls.values())} torch calls on device data")
         for (name, site), n in tr.calls.most_common(40):
             print(f"  {n:5d}  {name:24s} {site}")
+        print(f"-- {w}: {sum(tr.allocs.values())} PyTorch allocations of device tensors")
+        for (name, site), n in tr.allocs.most_common(25):
+            print(f"  {n:5d}  {name:24s} {site}")
+        print(f"-- {w}: {sum(_CUDA_OBJS.values())} torch.cuda Stream/Event/CUDAGraph objects")
+        for (name, site), n in _CUDA_OBJS.most_common(15):
+            print(f"  {n:5d}  {name:24s} {site}")
+        _CUDA_OBJS.clear()
+        from singa_amd import memory as MEM
+        if torch.cuda.is_available():
+            st = MEM.stats(torch.device("cuda", 0))
+            print(f"-- {w}: native pool: peak {st.get('peak_in_use_bytes', 0) / 2**30:.2f} GiB in use, "
+                  f"{st.get('reserved_bytes', 0) / 2**30:.2f} GiB reserved, {st.get('allocs', 0)} allocations, "
+                  f"{st.get('cache_hits', 0)} cache hits; torch allocator: "
+                  f"{torch.cuda.max_memory_allocated() / 2**30:.2f} GiB peak")
         print(f"-- {w}: native glue launches by call site")
         for (name, site), n in nat.most_common(25):
             print(f"  {n:5d}  {name:24s} {site}")
