@@ -121,7 +121,9 @@ def record_stream(t: torch.Tensor, stream) -> None:
     if M is not None and _native_on() and M.owns(_cuda_index(t.device), t.data_ptr()):
         M.record_stream(_cuda_index(t.device), t.data_ptr(), s)
     else:
-        t.record_stream(stream if hasattr(stream, "cuda_stream") else torch.cuda.ExternalStream(s))
+        ts = stream if isinstance(stream, torch.cuda.Stream) else (getattr(stream, "_ext", None) or
+                                                                   torch.cuda.ExternalStream(s, device=t.device))
+        t.record_stream(ts)  # a tensor PyTorch's allocator owns
 
 
 class graph_pool:
