@@ -39,9 +39,11 @@ class Stream {
     if (cur != device) hipSetDevice(cur);
     hchk(e, "hipStreamCreateWithPriority");
   }
-  ~Stream() {
-    if (s_) hipStreamDestroy(s_);
-  }
+  // never destroyed: a handle may live on in another runtime's bookkeeping
+  // (PyTorch's allocator keeps the streams a tensor was record_stream'ed on
+  // and records events there when the tensor dies, possibly long after this
+  // object); streams are few and created once per role
+  ~Stream() = default;
   uintptr_t handle() const { return (uintptr_t)s_; }
   int device() const { return dev_; }
   void synchronize() {
