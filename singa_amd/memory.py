@@ -28,11 +28,16 @@ _CODES = {torch.float32: (2, 32), torch.float64: (2, 64), torch.float16: (2, 16)
 _DL_DEV = None
 
 
+_MOD = [None, False]
+
+
 def _mod():
+    if _MOD[1]:
+        return _MOD[0]
     from .ops import native as N
-    if not N.available():
-        return None
-    return getattr(N.lib(), "mem", None)
+    m = getattr(N.lib(), "mem", None) if N.available() else None
+    _MOD[0], _MOD[1] = m, True
+    return m
 
 
 def _dl_device_type() -> int:
@@ -47,6 +52,16 @@ def _dl_device_type() -> int:
 
 _ON = [None]
 _DEVS: dict = {}
+_RAWQ = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+_GETD = getattr(torch._C, "_cuda_getDevice", None)
+
+
+def _raw_stream(idx: int) -> int:
+    return _RAWQ(idx) if _RAWQ is not None else torch.cuda.current_stream(idx).cuda_stream
+
+
+def _getdev() -> int:
+    return _GETD() if _GETD is not None else torch.cuda.current_device()
 
 
 def _native_on() -> bool:
@@ -92,9 +107,8 @@ def empty(*size, dtype=None, device=None, memory_format=None, pinned: bool = Fal
         strides = [h_ * w_ * c_, 1, w_ * c_, c_]
     code, bits = _CODES[dtype]
     if dev.type == "cuda":
-        idx = _cuda_index(dev)
-        cap = M.empty(shape, code, bits, 0, idx, _dl_device_type(), torch.cuda.current_stream(idx).cuda_stream,
-                      strides)
+        idx = dev.index if dev.index is not None else _getdev()
+        cap = M.empty(shape, code, bits, 0, idx, _DL_DEV or _dl_device_type(), _raw_stream(idx), strides)
     else:
         cap = M.empty(shape, code, bits, 2 if pinned else 1, 0, 1, 0, strides)
     t = torch.utils.dlpack.from_dlpack(cap)

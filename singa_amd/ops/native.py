@@ -68,8 +68,16 @@ def dt(t: torch.Tensor) -> int:
         raise TypeError(f"unsupported dtype for native kernel: {t.dtype}")
 
 
-def stream() -> int:
-    return torch.cuda.current_stream().cuda_stream
+_RAW = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+_GETDEV = getattr(torch._C, "_cuda_getDevice", None)
+
+
+def stream(device: int | None = None) -> int:
+    """Handle of this thread's current HIP stream (the raw query: ~0.1 us,
+    against ~3 us for building a torch.cuda.Stream object per launch)."""
+    if _RAW is not None and _GETDEV is not None:
+        return _RAW(_GETDEV() if device is None else device)
+    return torch.cuda.current_stream(device).cuda_stream
 
 
 def ptr(t: torch.Tensor | None) -> int:
