@@ -7,7 +7,7 @@
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 tag=${1:-r3}
 shift
-wl=${*:-"resnet50 alexnet bert bert_sonnx mlp_gpu mlp_conf conv_conf"}
+wl=${*:-"resnet50 alexnet bert bert_sonnx mlp_gpu mlp_conf conv_conf easgd rsync"}
 out=gpurun_out/purity
 mkdir -p $out
 run() {  # name, steps, command...
@@ -31,6 +31,8 @@ for w in $wl; do
     mlp_gpu) run mlp_gpu 5 python3 tools/bench_suite.py --which mlp_gpu --steps 3 --warmup 2 || exit 1 ;;
     mlp_conf) run mlp_conf 20 python3 -m singa_amd --model_conf examples/mnist/mlp.conf --device gpu --synthetic \
       --train_steps 20 || exit 1 ;;
+    easgd) run easgd 20 python3 tools/easgd_workload.py --ptype Elastic --steps 20 || exit 1 ;;
+    rsync) run rsync 20 python3 tools/easgd_workload.py --ptype RandomSync --steps 20 || exit 1 ;;
     conv_conf) run conv_conf 20 python3 -m singa_amd --model_conf examples/mnist/conv.conf --device gpu --synthetic \
       --train_steps 20 || exit 1 ;;
   esac
