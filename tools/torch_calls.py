@@ -76,17 +76,17 @@ _CUDA_OBJS = collections.Counter()
 
 def _count_cuda_objects():
     """Count torch.cuda.Stream / Event / CUDAGraph constructions."""
-    for nm in ("Stream", "Event", "CUDAGraph"):
-        orig = getattr(torch.cuda, nm)
-
-        class Sub(orig):  # noqa: D401 - counting subclass
-            def __new__(cls, *a, _nm=nm, **k):
+    def make(nm, orig):
+        class Sub(orig):  # counting subclass
+            def __new__(cls, *a, **k):
                 site = " <- ".join(f"{f.filename.replace(os.getcwd() + '/', '')}:{f.lineno}"
                                    for f in traceback.extract_stack()[-5:-1])
-                _CUDA_OBJS[(f"torch.cuda.{_nm}", site)] += 1
+                _CUDA_OBJS[(f"torch.cuda.{nm}", site)] += 1
                 return orig.__new__(cls, *a, **k)
         Sub.__name__ = nm
-        setattr(torch.cuda, nm, Sub)
+        return Sub
+    for nm in ("Stream", "Event", "CUDAGraph"):
+        setattr(torch.cuda, nm, make(nm, getattr(torch.cuda, nm)))
 
 
 def main() -> int:
