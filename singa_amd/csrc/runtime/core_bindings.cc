@@ -333,6 +333,15 @@ PYBIND11_MODULE(_core, m) {
     c.def("clamp_affine", [=](P x, P dy, P y, int64_t n, float a, float b, float lo, float hi) {
       C::ClampAffine(cfp(x), cfp(dy), fp(y), n, a, b, lo, hi);
     }, ng);
+    c.def("affine_elastic_sample", [=](P img, P theta, P disp, P out, int B, int H, int W) {
+      C::AffineElasticSample(cfp(img), cfp(theta), cfp(disp), fp(out), B, H, W);
+    }, ng);
+    c.def("gauss_blur2d", [=](P in, P out, int N, int H, int W, P g, int k) {
+      C::GaussBlur2D(cfp(in), fp(out), N, H, W, cfp(g), k);
+    }, ng);
+    c.def("resize_bilinear", [=](P in, P out, int B, int H, int W, int h, int w) {
+      C::ResizeBilinear(cfp(in), fp(out), B, H, W, h, w);
+    }, ng);
     c.def("easgd_diff", [=](P w, P c_, P d, int64_t n, float alpha) { C::EasgdDiff(fp(w), cfp(c_), fp(d), n, alpha); },
           ng);
     c.def("rsync_gather", [=](P w, P snap, P buf, int64_t m, int64_t n, int64_t a, int64_t b) {

@@ -660,6 +660,97 @@ void ClampAffine(const float* x, const float* dy, float* y, int64_t n, float a, 
   });
 }
 
+// ---- kMnistImage augmentation (the intent of the reference's commented-out
+// parser code, src/worker/layer.cc:406-438: elastic distortion, scaling,
+// rotation / shear, resize).  Coordinates follow the normalised-grid
+// convention with pixel centres at (2i+1)/n - 1 (align_corners = false).
+
+// out[b] = img[b] sampled bilinearly (zero outside) at theta[b] . (xn, yn, 1)
+// + disp[b][y][x] (normalised units; disp may be null)
+void AffineElasticSample(const float* img, const float* theta, const float* disp, float* out, int B, int H, int W) {
+  ParallelFor((int64_t)B * H, std::max<int64_t>(1, kEw / std::max(W, 1)), [&](int64_t r0, int64_t r1) {
+    for (int64_t r = r0; r < r1; ++r) {
+      const int b = (int)(r / H), y = (int)(r % H);
+      const float* t = theta + 6 * b;
+      const float* im = img + (int64_t)b * H * W;
+      const float yn = (2.f * y + 1.f) / H - 1.f;
+      for (int x = 0; x < W; ++x) {
+        const float xn = (2.f * x + 1.f) / W - 1.f;
+        float gx = t[0] * xn + t[1] * yn + t[2], gy = t[3] * xn + t[4] * yn + t[5];
+        if (disp) {
+          const float* d = disp + (((int64_t)b * H + y) * W + x) * 2;
+          gx += d[0];
+          gy += d[1];
+        }
+        const float px = ((gx + 1.f) * W - 1.f) * 0.5f, py = ((gy + 1.f) * H - 1.f) * 0.5f;
+        const float fx = std::floor(px), fy = std::floor(py);
+        const int x0 = (int)fx, y0 = (int)fy;
+        const float ax = px - fx, ay = py - fy;
+        auto at = [&](int yy, int xx) -> float {
+          return (yy >= 0 && yy < H && xx >= 0 && xx < W) ? im[(int64_t)yy * W + xx] : 0.f;
+        };
+        out[r * W + x] = (1.f - ay) * ((1.f - ax) * at(y0, x0) + ax * at(y0, x0 + 1)) +
+                         ay * ((1.f - ax) * at(y0 + 1, x0) + ax * at(y0 + 1, x0 + 1));
+      }
+    }
+  });
+}
+
+// separable 'same' Gaussian blur of N planes [N][H][W] (zero padding)
+void GaussBlur2D(const float* in, float* out, int N, int H, int W, const float* g, int k) {
+  const int hk = k / 2;
+  std::vector<float> tmp((size_t)N * H * W);
+  ParallelFor((int64_t)N * H, std::max<int64_t>(1, kEw / std::max(W * k, 1)), [&](int64_t r0, int64_t r1) {
+    for (int64_t r = r0; r < r1; ++r) {
+      const float* src = in + r * W;
+      float* dst = tmp.data() + r * W;
+      for (int x = 0; x < W; ++x) {
+        float a = 0.f;
+        for (int j = 0; j < k; ++j) {
+          const int xx = x + j - hk;
+          if (xx >= 0 && xx < W) a += g[j] * src[xx];
+        }
+        dst[x] = a;
+      }
+    }
+  });
+  ParallelFor((int64_t)N * H, std::max<int64_t>(1, kEw / std::max(W * k, 1)), [&](int64_t r0, int64_t r1) {
+    for (int64_t r = r0; r < r1; ++r) {
+      const int64_t n = r / H;
+      const int y = (int)(r % H);
+      for (int x = 0; x < W; ++x) {
+        float a = 0.f;
+        for (int j = 0; j < k; ++j) {
+          const int yy = y + j - hk;
+          if (yy >= 0 && yy < H) a += g[j] * tmp[((size_t)n * H + yy) * W + x];
+        }
+        out[r * W + x] = a;
+      }
+    }
+  });
+}
+
+// bilinear resize [B][H][W] -> [B][h][w] (half-pixel centres, edge clamp)
+void ResizeBilinear(const float* in, float* out, int B, int H, int W, int h, int w) {
+  const float sy = (float)H / h, sx = (float)W / w;
+  ParallelFor((int64_t)B * h, std::max<int64_t>(1, kEw / std::max(w, 1)), [&](int64_t r0, int64_t r1) {
+    for (int64_t r = r0; r < r1; ++r) {
+      const int b = (int)(r / h), y = (int)(r % h);
+      float fy = std::max((y + 0.5f) * sy - 0.5f, 0.f);
+      const int y0 = std::min((int)fy, H - 1), y1 = std::min(y0 + 1, H - 1);
+      const float ay = fy - y0;
+      const float* im = in + (int64_t)b * H * W;
+      for (int x = 0; x < w; ++x) {
+        float fx = std::max((x + 0.5f) * sx - 0.5f, 0.f);
+        const int x0 = std::min((int)fx, W - 1), x1 = std::min(x0 + 1, W - 1);
+        const float ax = fx - x0;
+        out[r * w + x] = (1.f - ay) * ((1.f - ax) * im[(int64_t)y0 * W + x0] + ax * im[(int64_t)y0 * W + x1]) +
+                         ay * ((1.f - ax) * im[(int64_t)y1 * W + x0] + ax * im[(int64_t)y1 * W + x1]);
+      }
+    }
+  });
+}
+
 // EASGD elastic difference (reference ElasticParam, src/utils/param.cc:244-284):
 // d = alpha (w - c); w -= d.  With c_add (the centre update after the
 // exchange) : c += s instead (s = the summed differences).

@@ -41,6 +41,9 @@ void WhereNd(const uint8_t* c, const float* a, const float* b, float* out, int n
 // y = clamp(a x + b, lo, hi); with dy: dx = dy * a inside (lo, hi), else 0
 void ClampAffine(const float* x, const float* dy, float* y, int64_t n, float a, float b, float lo, float hi);
 void EasgdDiff(float* w, const float* c, float* d, int64_t n, float alpha);
+void AffineElasticSample(const float* img, const float* theta, const float* disp, float* out, int B, int H, int W);
+void GaussBlur2D(const float* in, float* out, int N, int H, int W, const float* g, int k);
+void ResizeBilinear(const float* in, float* out, int B, int H, int W, int h, int w);
 void RsyncGather(const float* w, const float* snap, float* buf, int64_t m, int64_t n, int64_t a, int64_t b);
 void RsyncScatter(float* w, float* snap, const float* buf, int64_t m, int64_t n, int64_t a, int64_t b);
 // y[outer][inner] = op over j of x[outer][j][inner]; ops: 0 sum 1 mean 2 max 3 min 4 sumsq

@@ -51,7 +51,7 @@ def _dl_device_type() -> int:
 
 
 _ON = [None]
-_DEVS: dict = {}
+_DEVS: dict = {None: torch.device("cpu"), "cpu": torch.device("cpu")}  # (pre-built: no torch.device call per allocation)
 _RAWQ = getattr(torch._C, "_cuda_getCurrentRawStream", None)
 _GETD = getattr(torch._C, "_cuda_getDevice", None)
 

@@ -20,6 +20,7 @@ from typing import Dict, List, Optional, Sequence
 import numpy as np
 import torch
 
+from .. import memory as _mem
 from .. import autograd
 from ..config import schema
 from ..ops import functional as F
@@ -248,83 +249,103 @@ class MnistImageLayer(RefLayer):
         self.kernel, self.sigma, self.alpha = int(mp.kernel), float(mp.sigma), float(mp.alpha)
         self.elastic_freq = int(mp.elastic_freq)
         self.nbatch = 0
-        self.gen = torch.Generator().manual_seed(0)
+        self.rng = np.random.RandomState(0)
         B = src_shapes[0][0]
         s = src_shapes[0][1:]
         self.shape = (B, self.resize, self.resize) if self.resize else (B,) + tuple(s)
         return self.shape
 
-    def _rand(self, *shape):
-        return (torch.rand(*shape, generator=self.gen) * 2 - 1)
+    def _rand(self, *shape) -> np.ndarray:
+        return self.rng.uniform(-1.0, 1.0, size=shape).astype(np.float32)
 
-    def _deform(self, img, label):
-        """img [B, H, W] float -> deformed [B, H, W] (bilinear, zero fill)."""
-        B, H, W = img.shape
-        use_affine = self.gamma > 0 or self.beta > 0
-        use_elastic = self.alpha > 0 and self.kernel > 0 and self.sigma > 0 and \
-            (self.elastic_freq <= 0 or self.nbatch % self.elastic_freq == 0)
-        if not (use_affine or use_elastic):
-            return img
-        theta = torch.zeros(B, 2, 3)
+    def _theta(self, B: int, label) -> np.ndarray:
+        """Per-image affine sampling matrices [B][2][3] (host scalars)."""
+        theta = np.zeros((B, 2, 3), np.float32)
         theta[:, 0, 0] = theta[:, 1, 1] = 1.0
         if self.gamma > 0:  # scaling the image by s = sampling coordinates by 1/s
             theta[:, 0, 0] = 1.0 / (1.0 + self._rand(B) * self.gamma / 100.0)
             theta[:, 1, 1] = 1.0 / (1.0 + self._rand(B) * self.gamma / 100.0)
         if self.beta > 0:
             r = self._rand(B)
-            rot = torch.rand(B, generator=self.gen) < 0.5
-            ang = torch.deg2rad(r * self.beta)
-            c, sn = torch.cos(ang), torch.sin(ang)
-            R = torch.zeros(B, 2, 2)
+            rot = self.rng.uniform(0.0, 1.0, size=B) < 0.5
+            ang = np.deg2rad(r * self.beta)
+            c, sn = np.cos(ang), np.sin(ang)
+            R = np.zeros((B, 2, 2), np.float32)
             R[:, 0, 0], R[:, 0, 1], R[:, 1, 0], R[:, 1, 1] = c, -sn, sn, c
             sh = r * self.beta / 90.0
             if label is not None:
-                lab = label.reshape(-1).cpu()
-                sh = torch.where((lab == 1) | (lab == 7), sh / 2, sh)
-            S = torch.eye(2).repeat(B, 1, 1)
+                lab = np.asarray(label).reshape(-1)
+                sh = np.where((lab == 1) | (lab == 7), sh / 2, sh)
+            S = np.tile(np.eye(2, dtype=np.float32), (B, 1, 1))
             S[:, 0, 1] = sh
-            A = torch.where(rot[:, None, None], R, S)
+            A = np.where(rot[:, None, None], R, S)
             theta[:, :, :2] = A @ theta[:, :, :2]
-        theta = theta.to(img.device)
-        grid = torch.nn.functional.affine_grid(theta, (B, 1, H, W), align_corners=False)
+        return np.ascontiguousarray(theta, np.float32)
+
+    def _deform(self, img: np.ndarray, label) -> np.ndarray:
+        """img [B, H, W] float32 (host) -> deformed [B, H, W]: bilinear
+        sampling through the affine map plus (elastic) a Gaussian-smoothed
+        random displacement field, zero outside -- all on the native C++
+        host kernels (csrc/runtime/cpu_ops.cc AffineElasticSample /
+        GaussBlur2D)."""
+        B, H, W = img.shape
+        use_affine = self.gamma > 0 or self.beta > 0
+        use_elastic = self.alpha > 0 and self.kernel > 0 and self.sigma > 0 and \
+            (self.elastic_freq <= 0 or self.nbatch % self.elastic_freq == 0)
+        if not (use_affine or use_elastic):
+            return img
+        from ..ops import cpu as CP
+        C = CP.lib()
+        theta = self._theta(B, label)
+        disp = None
         if use_elastic:
             k = self.kernel | 1
-            ax = torch.arange(k, dtype=torch.float32) - k // 2
-            g1 = torch.exp(-ax ** 2 / (2 * self.sigma ** 2))
-            g1 = (g1 / g1.sum()).to(img.device)
-            d = self._rand(B * 2, 1, H, W).to(img.device)
-            d = torch.nn.functional.conv2d(d, g1.view(1, 1, 1, k), padding=(0, k // 2))
-            d = torch.nn.functional.conv2d(d, g1.view(1, 1, k, 1), padding=(k // 2, 0))
-            d = d.view(B, 2, H, W).permute(0, 2, 3, 1)
-            # alpha pixels -> normalised [-1, 1] grid units
-            grid = grid + d * self.alpha * torch.tensor([2.0 / W, 2.0 / H], device=img.device)
-        out = torch.nn.functional.grid_sample(img[:, None], grid, mode="bilinear", padding_mode="zeros",
-                                              align_corners=False)
-        return out[:, 0]
+            ax = np.arange(k, dtype=np.float32) - k // 2
+            g1 = np.exp(-ax ** 2 / (2 * self.sigma ** 2)).astype(np.float32)
+            g1 /= g1.sum()
+            d = self._rand(B * 2, H, W)
+            sm = np.empty_like(d)
+            C.gauss_blur2d(d.ctypes.data, sm.ctypes.data, B * 2, H, W, g1.ctypes.data, k)
+            # alpha pixels -> normalised [-1, 1] grid units, interleaved (dx, dy)
+            disp = np.ascontiguousarray(np.stack([sm.reshape(B, 2, H, W)[:, 0] * (self.alpha * 2.0 / W),
+                                                  sm.reshape(B, 2, H, W)[:, 1] * (self.alpha * 2.0 / H)], -1),
+                                        np.float32)
+        out = np.empty_like(img)
+        C.affine_elastic_sample(img.ctypes.data, theta.ctypes.data, 0 if disp is None else disp.ctypes.data,
+                                out.ctypes.data, B, H, W)
+        return out
 
     def forward(self, xs, training):
-        img = G.to(xs[0]["image"].data, torch.float32)
+        src = xs[0]["image"].data
+        dev = self.dev.torch_device  # (singa device: no tensor-attribute query on the hot path)
         aug = training and (self.gamma > 0 or self.beta > 0 or (self.alpha > 0 and self.kernel > 0 and self.sigma > 0))
-        dev = img.device
-        if img.is_cuda and (aug or (self.resize and tuple(img.shape[-2:]) != (self.resize, self.resize))):
+        need_resize = bool(self.resize) and tuple(src.shape[-2:]) != (self.resize, self.resize)
+        if aug or need_resize:
             # resize / affine / elastic augmentation is host-side preprocessing
-            # (the reference's CPU parser, src/worker/layer.cc:382-473); the
-            # result is uploaded with one DMA copy
-            img = img.cpu()
-        if self.resize and tuple(img.shape[-2:]) != (self.resize, self.resize):
-            img = torch.nn.functional.interpolate(img.reshape(img.shape[0], 1, *img.shape[-2:]),
-                                                  size=(self.resize, self.resize), mode="bilinear",
-                                                  align_corners=False).reshape(img.shape[0], self.resize,
-                                                                               self.resize)
-        if training:
-            lab = xs[0].get("label") if isinstance(xs[0], dict) else None
-            img = self._deform(img, lab.data.cpu() if lab is not None and img.device.type == "cpu" and lab.data.is_cuda
-                               else (lab.data if lab is not None else None))
-            self.nbatch += 1
-        if img.device != dev:
-            img = img.to(dev)
+            # (the reference's CPU parser, src/worker/layer.cc:382-473) on the
+            # native C++ kernels; a GPU batch comes back with one upload
+            from ..ops import cpu as CP
+            img = np.ascontiguousarray(G.to(src, torch.float32).cpu().numpy(), np.float32)
+            if img.ndim == 2:
+                img = img[None]
+            img = img.reshape(img.shape[0], img.shape[-2], img.shape[-1])
+            if need_resize:
+                r = np.empty((img.shape[0], self.resize, self.resize), np.float32)
+                CP.lib().resize_bilinear(img.ctypes.data, r.ctypes.data, img.shape[0], img.shape[1], img.shape[2],
+                                         self.resize, self.resize)
+                img = r
+            if training:
+                lab = xs[0].get("label") if isinstance(xs[0], dict) else None
+                img = self._deform(img, lab.data.cpu().numpy() if lab is not None else None)
+                self.nbatch += 1
+            t = torch.from_numpy(img)
+            imgt = t if dev.type == "cpu" else G.copy_(_mem.empty(tuple(t.shape), dtype=torch.float32, device=dev), t)
+        else:
+            imgt = G.to(src, torch.float32)
+            if training:
+                self.nbatch += 1
         # x / norm_a - norm_b
-        out = F.unary("adds", F.unary("scale", img, 1.0 / self.norm_a), -float(self.norm_b))
+        out = F.unary("adds", F.unary("scale", imgt, 1.0 / self.norm_a), -float(self.norm_b))
         return Tensor(device=self.dev, data=out, requires_grad=False)
 
 

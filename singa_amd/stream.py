@@ -32,7 +32,8 @@ def _rt():
 
 def current(device=None) -> int:
     """Handle of this thread's current stream on ``device``."""
-    return torch.cuda.current_stream(device).cuda_stream
+    idx = torch.device(device).index if isinstance(device, (str, torch.device)) else device
+    return N.stream(idx)
 
 
 class Stream:

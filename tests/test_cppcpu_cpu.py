@@ -117,13 +117,17 @@ def test_mlp_784_512_10_runs_native_and_matches_oracle():
         _close(params[k], ref_params[k], 1e-5, k)
 
 
-def _conf_run(conf, guard, steps=4):
+def _conf_run(conf, guard, steps=4, augment=""):
     from singa_amd import autograd
     from singa_amd.config import schema
     from singa_amd.runtime import Worker
 
     m = schema.read_text_file("ModelProto", os.path.join(ROOT, "examples", "mnist", conf))
     m.train_steps, m.test_frequency, m.display_frequency = steps, 0, 0
+    if augment:
+        for l in m.neuralnet.layer:
+            if l.type == "kMnistImage":
+                __import__("google.protobuf.text_format", fromlist=["Merge"]).Merge(augment, l.mnist_param)
     for l in m.neuralnet.layer:
         if l.type in ("kShardData", "kLMDBData"):
             l.type = "kSyntheticData"
@@ -154,6 +158,48 @@ def test_reference_confs_run_native_and_match_oracle(conf):
         _close(params[k], ref_params[k], 1e-5, k)
     if hist and ref_hist:
         np.testing.assert_allclose(hist, ref_hist, rtol=1e-5, atol=1e-5)
+
+
+def test_mnist_augmentation_runs_native_under_guard():
+    """conv.conf with the kMnistImage augmentation the reference intended
+    (scaling, rotation / shear, elastic distortion, resize: src/worker/
+    layer.cc:406-438) switched on: the whole training step -- augmentation
+    included -- makes no torch compute call, and it trains."""
+    g = NoTorchCompute()
+    hist, params = _conf_run("conv.conf", g, steps=6,
+                             augment="gamma: 10 beta: 10 kernel: 5 sigma: 2 alpha: 3 resize: 29")
+    g.check()
+    assert params and all(np.isfinite(v.numpy()).all() for v in params.values())
+
+
+def test_mnist_augmentation_kernels_match_torch():
+    """The native sampling / blur / resize kernels against PyTorch's
+    grid_sample (bilinear, zeros, align_corners=False), conv2d and
+    interpolate (bilinear, align_corners=False)."""
+    C = CP.lib()
+    B, H, W = 3, 28, 28
+    img = _t(B, H, W, lo=0, hi=255)
+    theta = torch.tensor([[[0.9, 0.1, 0.05], [-0.1, 1.1, -0.02]], [[1, 0, 0], [0, 1, 0]],
+                          [[1.05, -0.2, 0.0], [0.15, 0.95, 0.1]]], dtype=torch.float32)
+    disp = _t(B, H, W, 2, lo=-0.1, hi=0.1)
+    out = torch.empty_like(img)
+    C.affine_elastic_sample(img.data_ptr(), theta.data_ptr(), disp.data_ptr(), out.data_ptr(), B, H, W)
+    grid = TF.affine_grid(theta, (B, 1, H, W), align_corners=False) + disp
+    ref = TF.grid_sample(img[:, None], grid, mode="bilinear", padding_mode="zeros", align_corners=False)[:, 0]
+    _close(out, ref, 1e-3)
+    k = 5
+    g1 = torch.exp(-(torch.arange(k, dtype=torch.float32) - 2) ** 2 / 8.0)
+    g1 = (g1 / g1.sum()).contiguous()
+    d = _t(4, H, W)
+    sm = torch.empty_like(d)
+    C.gauss_blur2d(d.data_ptr(), sm.data_ptr(), 4, H, W, g1.data_ptr(), k)
+    r1 = TF.conv2d(d[:, None], g1.view(1, 1, 1, k), padding=(0, 2))
+    r1 = TF.conv2d(r1, g1.view(1, 1, k, 1), padding=(2, 0))[:, 0]
+    _close(sm, r1, 1e-5)
+    for h, w in ((29, 29), (20, 33)):
+        rs = torch.empty(B, h, w)
+        C.resize_bilinear(img.data_ptr(), rs.data_ptr(), B, H, W, h, w)
+        _close(rs, TF.interpolate(img[:, None], size=(h, w), mode="bilinear", align_corners=False)[:, 0], 1e-3)
 
 
 # ------------------------------------------------------------------ per-op parity

@@ -79,9 +79,12 @@ def _count_cuda_objects():
     def make(nm, orig):
         class Sub(orig):  # counting subclass
             def __new__(cls, *a, **k):
-                site = " <- ".join(f"{f.filename.replace(os.getcwd() + '/', '')}:{f.lineno}"
-                                   for f in traceback.extract_stack()[-5:-1])
-                _CUDA_OBJS[(f"torch.cuda.{nm}", site)] += 1
+                # (an ExternalStream is the carrier of a framework-owned stream
+                # handle -- singa_amd.stream.Stream -- not a PyTorch stream)
+                if not issubclass(cls, getattr(torch.cuda, "ExternalStream", ())):
+                    site = " <- ".join(f"{f.filename.replace(os.getcwd() + '/', '')}:{f.lineno}"
+                                       for f in traceback.extract_stack()[-5:-1])
+                    _CUDA_OBJS[(f"torch.cuda.{nm}", site)] += 1
                 return orig.__new__(cls, *a, **k)
         Sub.__name__ = nm
         return Sub
