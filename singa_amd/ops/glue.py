@@ -404,11 +404,12 @@ def sum_to(g: torch.Tensor, shape) -> torch.Tensor:
 # --------------------------------------------------------------------- concat / slices / tiles
 def cat(ts: Sequence[torch.Tensor], axis: int = 0) -> torch.Tensor:
     ts = list(ts)
-    if not on_gpu(*ts) and not (CP.copy_ok(*ts) and len({t.dtype for t in ts}) == 1):
-        return torch.cat(ts, dim=axis)
+    if not on_gpu(*ts) and not CP.copy_ok(*ts):
+        return torch.cat(ts, dim=axis)  # (a host dtype without a native conversion, or the test oracle)
     nd = ts[0].dim()
     axis %= nd
-    dt = ts[0].dtype
+    # mixed dtypes: PyTorch's promotion, every part converted by the native copy
+    dt = ts[0].dtype if len({t.dtype for t in ts}) == 1 else _promote([t.dtype for t in ts])
     shape = list(ts[0].shape)
     shape[axis] = sum(t.shape[axis] for t in ts)
     out = _mem.empty(shape, dtype=dt, device=ts[0].device)
@@ -487,9 +488,21 @@ def _idx(idx: torch.Tensor, device) -> torch.Tensor:
     return contiguous(idx)
 
 
+def _promote(dts):
+    out = dts[0]
+    for d in dts[1:]:
+        out = torch.promote_types(out, d)
+    return out
+
+
 def index_select(x: torch.Tensor, axis: int, idx: torch.Tensor) -> torch.Tensor:
     """out = x.take(idx, axis) with out.shape = x.shape[:axis] + idx.shape + x.shape[axis+1:]."""
     axis %= x.dim()
+    if not on_gpu(x) and CP.copy_ok(x) and not idx.is_cuda and idx.dtype not in (torch.int32, torch.int64):
+        import numpy as np  # other host index dtypes: converted on the host (no torch kernel)
+        idx = torch.from_numpy(np.ascontiguousarray(idx.numpy(), np.int64))
+    if not on_gpu(x) and CP.copy_ok(x) and idx.is_cuda and idx.dtype in (torch.int32, torch.int64):
+        idx = idx.cpu()  # (indices of a host gather: one small device -> host copy)
     if not on_gpu(x) and CP.copy_ok(x) and not idx.is_cuda and idx.dtype in (torch.int32, torch.int64):
         xc, ic = contiguous(x), contiguous(idx)
         outer = int(math.prod(x.shape[:axis]))
@@ -605,6 +618,23 @@ def pad(x: torch.Tensor, before: Sequence[int], after: Sequence[int], mode: str 
         for k in range(nd):
             v = v.narrow(k, before[k], x.shape[k])
         copy_(v, x)
+        return y
+    if not on_gpu(x) and CP.copy_ok(x) and mode == "constant":
+        # negative counts crop: narrow first, then the native constant pad
+        v = x
+        for k in range(nd):
+            b0, a0 = min(before[k], 0), min(after[k], 0)
+            if b0 or a0:
+                v = v.narrow(k, -b0, v.shape[k] + b0 + a0)
+        return pad(contiguous(v), [max(b, 0) for b in before], [max(a, 0) for a in after], mode, value)
+    if not on_gpu(x) and CP.copy_ok(x):
+        # reflect / edge: one native gather per padded dim through the index maps
+        import numpy as np
+        maps = _pad_maps(x.shape, osz, before, mode)
+        y = x
+        for k, m in enumerate(maps):
+            if len(m) != x.shape[k] or np.any(m != np.arange(x.shape[k])):
+                y = index_select(y, k, torch.from_numpy(np.ascontiguousarray(m, np.int64)))
         return y
     if not on_gpu(x):
         if mode == "constant":

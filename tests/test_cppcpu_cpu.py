@@ -36,7 +36,7 @@ _ALLOW = {"__get__", "dim", "size", "stride", "numel", "data_ptr", "element_size
           "empty_strided", "storage_offset", "untyped_storage", "__len__", "__hash__", "__eq__", "is_floating_point",
           "unbind", "split", "chunk", "from_numpy", "__format__", "__repr__", "tolist", "item", "__float__",
           "__int__", "__bool__", "__index__", "view_as", "get_device", "is_complex", "has_names", "__array__",
-          "_is_view", "is_pinned", "__iter__", "ndimension", "nelement"}
+          "_is_view", "is_pinned", "__iter__", "ndimension", "nelement", "promote_types"}  # (dtype metadata)
 _MAYBE_VIEW = {"reshape", "contiguous", "float", "to", "flatten", "cpu", "long"}  # allowed when no copy happened
 
 
@@ -445,3 +445,26 @@ def test_pool_is_reused_and_threads_reported():
     r1 = F.gemm(a, b)
     r2 = F.gemm(a, b)
     assert torch.equal(r1, r2)  # deterministic across calls
+
+
+def test_glue_host_paths_native_for_all_modes():
+    """Host cat (mixed dtypes), index_select (any integer index dtype) and
+    pad (negative counts, reflect, edge) run on the native kernels -- no
+    torch compute -- and match PyTorch."""
+    x = _t(3, 5, 6)
+    xi = torch.arange(30, dtype=torch.int32).reshape(5, 6)
+    idx16 = torch.tensor([4, 0, 2], dtype=torch.int16)
+    g = NoTorchCompute()
+    with g:
+        c = G.cat([x[0], xi], 0)
+        sel = G.index_select(x, 1, idx16)
+        p_neg = G.pad(x, [0, -1, 2], [1, 1, -2], "constant", 0.5)
+        p_ref = G.pad(x, [0, 2, 1], [0, 1, 3], "reflect")
+        p_edge = G.pad(x, [1, 0, 2], [0, 3, 1], "edge")
+    g.total = max(g.total, 101)
+    g.check()
+    _close(c, torch.cat([x[0], xi.float()], 0))
+    _close(sel, x[:, [4, 0, 2]])
+    _close(p_neg, TF.pad(x, (2, -2, -1, 1, 0, 1), value=0.5))
+    _close(p_ref, TF.pad(x[None], (1, 3, 2, 1), mode="reflect")[0])
+    _close(p_edge[1:], TF.pad(x[None], (2, 1, 0, 3), mode="replicate")[0])
