@@ -615,23 +615,49 @@ class AddBias(Operator):
 
 
 class Linear(Operator):
-    """y = x @ W (+ b) with W [in, out] (SINGA / reference InnerProduct layout,
-    src/worker/layer.cc:193-211).  Mixed precision: when x is bf16 the bf16
-    compute copy ``W.low`` is used and gradients accumulate in fp32."""
+    """y = act(x @ W (+ b)) with W [in, out] (SINGA / reference InnerProduct
+    layout, src/worker/layer.cc:193-211; the optional activation is the
+    reference's following kTanh / kReLU / kSigmoid layer, layer.cc:563-606,
+    fused into the GEMM epilogue).  Mixed precision: when x is bf16 the bf16
+    compute copy ``W.low`` is used and gradients accumulate in fp32.
 
-    def __init__(self, has_bias=True, name=None):
+    Backward: the activation derivative is applied to dy first -- unless the
+    consumer of this op's output was a fused Linear that is its only
+    consumer: that op's data-gradient GEMM already multiplied by act'(y) in
+    its epilogue (``preact_done``), so the separate elementwise pass
+    disappears from both directions."""
+
+    wants_sole = True
+
+    def __init__(self, has_bias=True, name=None, act: Optional[str] = None):
         super().__init__(name)
         self.has_bias = has_bias
+        self.act = act
+        self.y2 = None
+        self.preact_done = False
 
     def forward(self, x, W, b=None):
         w = self._w_compute(x, W)
         lead = x.shape[:-1]
         x2 = G.reshape(x, (-1, x.shape[-1]))
         bias = G.to(b, torch.float32) if b is not None else None
-        y = F.matmul(x2, w, out_dtype=x.dtype, bias=bias)
+        y = F.matmul(x2, w, out_dtype=x.dtype, bias=bias, act=self.act)
         if self.requires_grad:
             self.x2, self.w = x2, w
+            self.y2 = y if self.act is not None else None
         return G.reshape(y, (*lead, y.shape[-1]))
+
+    def _producer_act(self, x2):
+        """(act, y) of the fused Linear whose output is this op's input and
+        whose gradient comes from this op alone, else None."""
+        src = self.src[0][0] if self.src else None
+        if not (isinstance(src, Linear) and src.act is not None and src.y2 is not None
+                and getattr(self, "sole", {}).get(0, False)):
+            return None
+        y = src.y2
+        if y.data_ptr() != x2.data_ptr() or y.numel() != x2.numel():
+            return None
+        return src
 
     def _w_compute(self, x, W):
         if x.dtype == W.dtype:
@@ -642,23 +668,36 @@ class Linear(Operator):
         return G.to(W, x.dtype)
 
     def backward(self, dy):
-        x2, w = self.x2, self.w
-        self.x2 = self.w = None
+        x2, w, y2 = self.x2, self.w, self.y2
+        self.x2 = self.w = self.y2 = None
         dy2 = G.contiguous(G.reshape(dy, (-1, dy.shape[-1])))
+        if self.act is not None and not self.preact_done:
+            dy2 = F.relu_bwd_from_y(y2, dy2) if self.act == "relu" else F.unary_bwd(self.act, None, y2, dy2)
+        self.preact_done = False
         dx = None
         if self.needs_grad(0):
-            dx = F.gemm_nt(dy2, w, out_dtype=x2.dtype)
+            prod = self._producer_act(x2)
+            if prod is not None:
+                dx = F.gemm_nt(dy2, w, out_dtype=x2.dtype, act_grad=(prod.act, x2))
+                prod.preact_done = True
+            else:
+                dx = F.gemm_nt(dy2, w, out_dtype=x2.dtype)
             dx = G.reshape(dx, (*dy.shape[:-1], x2.shape[-1]))
         tgt = self.grad_target(1)
+        tb = self.grad_target(2) if self.has_bias else None
+        # the bias gradient (column sums of dy) rides along with the weight
+        # gradient GEMM, which stages every dy tile anyway
+        fuse_db = tb is not None and tgt is not None and tb.is_contiguous()
         if tgt is not None:
-            F.gemm_tn_acc(x2, dy2, tgt)
+            F.gemm_tn_acc(x2, dy2, tgt, colsum_b=tb if fuse_db else None)
             dw = ACCUMULATED
         else:
             dw = F.gemm(x2, dy2, ta=True, out_dtype=torch.float32)
         res = [dx, dw]
         if self.has_bias:
-            tb = self.grad_target(2)
-            if tb is not None:
+            if fuse_db:
+                db = ACCUMULATED
+            elif tb is not None:
                 F.colsum(dy2, out=tb)
                 db = ACCUMULATED
             else:
@@ -1335,8 +1374,8 @@ def add_bias(x, b, axis=0):
     return AddBias(axis)(x, b)
 
 
-def linear(x, W, b=None):
-    return Linear(b is not None)(x, W, b) if b is not None else Linear(False)(x, W)
+def linear(x, W, b=None, act=None):
+    return Linear(True, act=act)(x, W, b) if b is not None else Linear(False, act=act)(x, W)
 
 
 def softmax(x, axis=1):

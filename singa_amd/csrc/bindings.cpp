@@ -115,7 +115,8 @@ void sg_bn_bwd_wdot(const void*, const void*, const void*, const void*, const vo
                     const void*, const void*, const void*, const void*, void*, void*, void*, void*, void*, void*,
                     int64_t, int, float, hipStream_t);
 void sg_ggemm(int, const void*, int64_t, int, int64_t, const void*, int64_t, int, int64_t, void*, int64_t, int64_t,
-              int, int, int, float, float, const void*, int, int, int, int, hipStream_t);
+              int, int, int, float, float, const void*, int, int, int, int, float*, int, const void*, hipStream_t);
+void sg_ggemm_tune(int, int);
 void sg_gconv_fwd(int, const void*, const void*, void*, const void*, int, int, int, int, int, int, int, int, int, int,
                   int, int, int, int, int, int, int, int, hipStream_t);
 void sg_gconv_dgrad(int, const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int,
@@ -434,11 +435,12 @@ PYBIND11_MODULE(_C, m) {
   // generic MFMA GEMM / conv (csrc/kernels/ggemm.hip): dt 0 = fp32 operands (exact f32 MFMA), 1 = bf16
   m.def("ggemm", [](int dt, P a, int64_t lda, int ako, int64_t sa, P b, int64_t ldb, int bko, int64_t sb, P c,
                     int64_t ldc, int64_t sc, int M, int N, int K, float alpha, float beta, P bias, int relu,
-                    int out_mode, int splits, int batch, P s) {
+                    int out_mode, int splits, int batch, P csum, int act_bwd, P act_x, P s) {
     sg_ggemm(dt, CV(a), lda, ako, sa, CV(b), ldb, bko, sb, V(c), ldc, sc, M, N, K, alpha, beta, CV(bias), relu,
-             out_mode, splits, batch, S(s));
+             out_mode, splits, batch, (float*)V(csum), act_bwd, CV(act_x), S(s));
     CHK("ggemm");
   });
+  m.def("ggemm_tune", [](int key, int value) { sg_ggemm_tune(key, value); });
   m.def("gconv_fwd", [](int dt, P x, P w, P y, P bias, int N, int H, int W, int C, int K, int R, int Sd, int Ho,
                         int Wo, int sh, int sw, int ph, int pw, int dh, int dw, int groups, int relu, int out_mode,
                         P s) {

@@ -80,8 +80,34 @@ struct Args {
   int relu, out_mode;
   int k_per_split;   // multiple of BK
   int vec_a, vec_b;  // 4-element units are contiguous + aligned (vector loads)
+  float* csum;       // optional: csum[n] += sum_k B(n, k) (the bias gradient of a weight-gradient GEMM)
+  const void* act_x; // optional: C[m][n] *= act'(X[m][n]), X the activation OUTPUT laid out like C (ldc)
+  int act_bwd;       // activation of act_x (Act codes)
   Geom g;
 };
+
+// fused activations (the relu field of Args; act_bwd): codes 0 none, 1 relu,
+// 2 sigmoid, 3 tanh, 4 stanh -- the same formulas as elementwise.hip's
+// unary_f / unary_b (output-form derivatives)
+enum Act : int { A_NONE = 0, A_RELU = 1, A_SIGMOID = 2, A_TANH = 3, A_STANH = 4 };
+__device__ __forceinline__ float act_f(int a, float v) {
+  switch (a) {
+    case A_RELU: return fmaxf(v, 0.f);
+    case A_SIGMOID: return 1.f / (1.f + __expf(-v));
+    case A_TANH: return tanhf(v);
+    case A_STANH: return 1.7159047f * tanhf(0.66666667f * v);
+    default: return v;
+  }
+}
+__device__ __forceinline__ float dact_y(int a, float y) {
+  switch (a) {
+    case A_RELU: return y > 0.f ? 1.f : 0.f;
+    case A_SIGMOID: return y * (1.f - y);
+    case A_TANH: return 1.f - y * y;
+    case A_STANH: return 0.66666667f * 1.7159047f - 0.66666667f / 1.7159047f * y * y;
+    default: return 1.f;
+  }
+}
 
 template <typename T> struct V4;
 template <> struct V4<float> { typedef f32x4 t; };
@@ -290,13 +316,14 @@ struct Ld {
   }
 };
 
-template <typename T, int BM, int BN, int AM, int BMODE>
+template <typename T, int BM, int BN, int AM, int BMODE, bool M32V = true>
 __global__ void __launch_bounds__(NT, 2) ggemm_k(const Args p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int LD = ld_of<T>();
   constexpr int A_EL = BM * LD, STAGE_EL = (BM + BN) * LD;
-  // fp32 128x128: 32x32x2 MFMA blocks (each wave 2 x 2 of them)
-  constexpr bool M32 = sizeof(T) == 4 && BM == 128 && BN == 128;
+  // fp32 128x128: 32x32x2 MFMA blocks (each wave 2 x 2 of them) unless M32V
+  // is off (16x16x4 blocks, 4 x 4 per wave)
+  constexpr bool M32 = sizeof(T) == 4 && BM == 128 && BN == 128 && M32V;
   constexpr int MB = M32 ? 32 : 16;
   constexpr int WTM = BM / 2, WTN = BN / 2, TM = WTM / MB, TN = WTN / MB;
   typedef typename std::conditional<M32, f32x16, f32x4>::type AccT;
@@ -397,6 +424,20 @@ __global__ void __launch_bounds__(NT, 2) ggemm_k(const Args p) {
     }
   };
 
+  // fused column sums of B (workgroups of the first M tile): thread t sums
+  // column n = t % BN over its k slice of every K-tile image
+  const bool do_cs = p.csum != nullptr && tm == 0;
+  constexpr int CS_G = NT / BN, CS_K = BK / CS_G;
+  float cs_acc = 0.f;
+  auto colsum_tile = [&](const T* sb_) {
+    const int n = threadIdx.x % BN, k0 = (threadIdx.x / BN) * CS_K;
+#pragma unroll
+    for (int k = 0; k < CS_K; ++k) {
+      if constexpr (sizeof(T) == 4) cs_acc += (float)sb_[f32_pos(n, k0 + k)];
+      else cs_acc += (float)sb_[n * LD + k0 + k];
+    }
+  };
+
   if (nk > 0) {
     la.load(p.g, kbeg, kend);
     lb.load(p.g, kbeg, kend);
@@ -411,6 +452,7 @@ __global__ void __launch_bounds__(NT, 2) ggemm_k(const Args p) {
         lb.load(p.g, kbeg + (kt + 1) * BK, kend);
       }
       compute(lds + cur * STAGE_EL);
+      if (do_cs) colsum_tile(lds + cur * STAGE_EL + A_EL);
       if (more) {
         T* nx = lds + (cur ^ 1) * STAGE_EL;
         la.store(nx);
@@ -419,6 +461,8 @@ __global__ void __launch_bounds__(NT, 2) ggemm_k(const Args p) {
       __syncthreads();
     }
   }
+
+  if (do_cs && n0 + (int)threadIdx.x % BN < p.N) atomicAdd(p.csum + n0 + threadIdx.x % BN, cs_acc);
 
   // Epilogue: 16x16 blocks acc[i][j][r] = C[m = .. + (l & 15)][n = .. + 4 (l >> 4) + r];
   // 32x32 blocks acc[i][j][4 g + r] = C[m = .. + (l & 31)][n = .. + 8 g + 4 (l >> 5) + r]
@@ -447,13 +491,15 @@ __global__ void __launch_bounds__(NT, 2) ggemm_k(const Args p) {
       }
     __syncthreads();
     float* cbase = (float*)pc;
+    const bool addb = bias && blockIdx.z == 0;  // split-K of a biased GEMM: split 0 adds the bias
     for (int row = wid; row < BM; row += NT / 64) {
       const int m = m0 + row;
       if (m >= p.M) break;
 #pragma unroll
       for (int c0 = 0; c0 < BN; c0 += 64) {
         const int n = n0 + c0 + l;
-        if (c0 + l < BN && n < p.N) atomicAdd(cbase + (int64_t)m * p.ldc + n, tile[row * LDT + c0 + l]);
+        if (c0 + l < BN && n < p.N)
+          atomicAdd(cbase + (int64_t)m * p.ldc + n, tile[row * LDT + c0 + l] + (addb ? bias[n] : 0.f));
       }
     }
     return;
@@ -465,14 +511,20 @@ __global__ void __launch_bounds__(NT, 2) ggemm_k(const Args p) {
     float v[4] = {a4[0] * p.alpha, a4[1] * p.alpha, a4[2] * p.alpha, a4[3] * p.alpha};
     if (p.out_mode == O_F32_ATOMIC) {
       float* c = (float*)pc + rowoff + n;
+      const bool addb = bias && blockIdx.z == 0;
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        if (full || n + r < p.N) atomicAdd(c + r, v[r]);
+        if (full || n + r < p.N) atomicAdd(c + r, v[r] + (addb ? bias[n + r] : 0.f));
       return;
     }
     if (bias) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] += (full || n + r < p.N) ? bias[n + r] : 0.f;
+    }
+    if (p.act_x) {  // fused activation backward: C = (A B) * act'(X)
+      const T* xa = (const T*)p.act_x + y * p.sc + rowoff + n;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] *= (full || n + r < p.N) ? dact_y(p.act_bwd, (float)xa[r]) : 0.f;
     }
     if (p.out_mode == O_F32) {
       float* c = (float*)pc + rowoff + n;
@@ -484,7 +536,7 @@ __global__ void __launch_bounds__(NT, 2) ggemm_k(const Args p) {
       }
       if (p.relu) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+        for (int r = 0; r < 4; ++r) v[r] = act_f(p.relu, v[r]);
       }
       if (vst) *(float4*)c = make_float4(v[0], v[1], v[2], v[3]);
       else {
@@ -502,7 +554,7 @@ __global__ void __launch_bounds__(NT, 2) ggemm_k(const Args p) {
       }
       if (p.relu) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+        for (int r = 0; r < 4; ++r) v[r] = act_f(p.relu, v[r]);
       }
       if (vst) {
         bf16x4 o;
@@ -533,11 +585,11 @@ __global__ void __launch_bounds__(NT, 2) ggemm_k(const Args p) {
     }
 }
 
-template <typename T, int BM, int BN, int AM, int BMODE>
+template <typename T, int BM, int BN, int AM, int BMODE, bool M32V = true>
 static void launch_t(const Args& p, int batch, int splits, hipStream_t s) {
   const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
   constexpr int lds = 2 * (BM + BN) * ld_of<T>() * (int)sizeof(T);
-  auto* kern = ggemm_k<T, BM, BN, AM, BMODE>;
+  auto* kern = ggemm_k<T, BM, BN, AM, BMODE, M32V>;
   if constexpr (lds > 65536) {
     static bool attr = [kern] {
       return hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
@@ -575,14 +627,83 @@ static void launch(const Args& p, int batch, int splits, hipStream_t s) {
 }
 
 // split-K count for atomic outputs: fill ~512 workgroups, >= 4 K-tiles each
-static int pick_splits(int M, int N, int K, int batch, int want, bool f32) {
+static int pick_splits(int M, int N, int K, int batch, int want, int bm, int bn) {
   if (want > 0) return want;
-  const int bm = big_tile(M, N, f32) ? 128 : 64;
-  const long tiles = (long)((M + bm - 1) / bm) * ((N + bm - 1) / bm) * (batch > 0 ? batch : 1);
+  const long tiles = (long)((M + bm - 1) / bm) * ((N + bn - 1) / bn) * (batch > 0 ? batch : 1);
   const int nkt = (K + BK - 1) / BK;
   int sp = 1;
   while (tiles * sp < 512 && sp * 2 * 4 <= nkt && sp < 4096) sp *= 2;
   return sp;
+}
+
+// fp32 GEMM tuning (sg_ggemm_tune): key 0 = tile (0 auto, 1 64x64, 2 128x128
+// on 32x32x2, 3 128x64, 4 64x128, 5 128x128 on 16x16x4, 6 64x32, 7 32x64,
+// 8 32x32); key 1 = split-K (0 auto, -1 never, n > 1 forced; a plain fp32
+// output split over K is zeroed -- or kept,
+// beta = 1 -- and the splits add into it with atomics, split 0 adding the bias).
+// (Measured and dropped: a 2-deep register prefetch of the global loads --
+// no gain at any MLP shape, +36 VGPRs.)
+static int g_gg[2] = {0, 0};
+
+static void tile_dims(int t, int& bm, int& bn) {
+  bm = (t == 2 || t == 3 || t == 5) ? 128 : (t == 7 || t == 8) ? 32 : 64;
+  bn = (t == 2 || t == 4 || t == 5) ? 128 : (t == 6 || t == 8) ? 32 : 64;
+}
+
+__global__ void zero_rows_k(float* c, int64_t ldc, int64_t sc, int N) {
+  float* r = c + blockIdx.y * sc + (int64_t)blockIdx.x * ldc;
+  for (int n = threadIdx.x; n < N; n += blockDim.x) r[n] = 0.f;
+}
+
+// fp32 tile / split-K choice: the configuration with the least modelled
+// time.  A CU runs ceil(workgroups / 256) tiles concurrently, so the time is
+// that many tiles' MACs over the CU rate scaled by the tile's relative
+// efficiency (measured, tools/bench_ggemm_f32.py: 64x64 1.0; 32x64 / 128x64 /
+// 64x128 0.9; 64x32 / 32x32 0.85; one tile per CU loses another 40 %), plus
+// for split-K the extra output traffic (zeroing + one fp32 atomic per split
+// per element at ~4 TB/s).  On the mlp.conf shapes its picks are within 2.5 %
+// of the best configuration of the sweep (profiles/ggemm_r4/).
+static void pick_f32(int M, int N, int K, int batch, bool can_split, bool zero_first, int& tile, int& splits) {
+  static const int cand[] = {1, 7, 3, 4, 6, 8};
+  static const double eff[] = {0, 1.0, 0, 0.9, 0.9, 0, 0.85, 0.9, 0.85};
+  static const int sps[] = {1, 2, 3, 4, 8};
+  const int nkt = (K + BK - 1) / BK;
+  double best = 1e300;
+  tile = 1;
+  splits = 1;
+  for (int t : cand) {
+    int bm, bn;
+    tile_dims(t, bm, bn);
+    const long tiles = (long)((M + bm - 1) / bm) * ((N + bn - 1) / bn) * batch;
+    for (int sp : sps) {
+      if (sp > 1 && (!can_split || nkt < 2 * sp)) continue;
+      const long per_cu = (tiles * sp + 255) / 256;
+      const long kk = (long)((nkt + sp - 1) / sp) * BK;
+      const double e = eff[t] * (per_cu == 1 ? 0.6 : 1.0);
+      double cost = (double)per_cu * bm * bn * kk / e;  // MACs at unit efficiency
+      // split-K output traffic in MAC-equivalents: bytes / 4 TB/s * (128 MAC/clk * 2.2 GHz * 0.58)
+      if (sp > 1) cost += (double)(sp + (zero_first ? 1 : 0)) * M * N * 4.0 * batch / 4e12 * (128 * 2.2e9 * 0.58);
+      if (cost < best * 0.999) {
+        best = cost;
+        tile = t;
+        splits = sp;
+      }
+    }
+  }
+}
+
+template <int AM, int BMODE>
+static void launch_f32(const Args& p, int batch, int splits, int tile, hipStream_t s) {
+  switch (tile) {
+    case 2: launch_t<float, 128, 128, AM, BMODE, true>(p, batch, splits, s); break;
+    case 3: launch_t<float, 128, 64, AM, BMODE>(p, batch, splits, s); break;
+    case 4: launch_t<float, 64, 128, AM, BMODE>(p, batch, splits, s); break;
+    case 5: launch_t<float, 128, 128, AM, BMODE, false>(p, batch, splits, s); break;
+    case 6: launch_t<float, 64, 32, AM, BMODE>(p, batch, splits, s); break;
+    case 7: launch_t<float, 32, 64, AM, BMODE>(p, batch, splits, s); break;
+    case 8: launch_t<float, 32, 32, AM, BMODE>(p, batch, splits, s); break;
+    default: launch_t<float, 64, 64, AM, BMODE>(p, batch, splits, s); break;
+  }
 }
 
 static inline int kps(int K, int splits) {
@@ -619,21 +740,55 @@ using namespace sg::gg;
 
 extern "C" {
 
+void sg_ggemm_tune(int key, int value) {
+  if (key >= 0 && key < 2) g_gg[key] = value;
+}
+
 // Generic GEMM (dt 0: fp32 operands, 1: bf16 operands):
 //   C[batch][M][N] = alpha * A(m, k) B(n, k) (+ beta C) (+ bias[n]) (ReLU)
+//   csum (optional, batch 1): csum[n] += sum_k B(n, k) -- a weight-gradient
+//   GEMM's bias gradient from the dy tiles it already stages (no extra pass)
+//   relu: fused activation of the output (Act codes: 1 relu, 2 sigmoid, 3 tanh,
+//   4 stanh); act_x (optional): C *= act'(X), X = the activation output of
+//   code act_bwd laid out like C -- a data-gradient GEMM that also takes the
+//   producer's activation backward
 //   a_kouter = 0: A stored [M][K] (lda), 1: [K][M]; b_kouter = 0: B stored [N][K], 1: [K][N]
 //   out_mode 0 bf16, 1 fp32, 2 fp32 atomic (split-K, C pre-initialised)
 void sg_ggemm(int dt, const void* a, int64_t lda, int a_kouter, int64_t sa, const void* b, int64_t ldb, int b_kouter,
               int64_t sb, void* c, int64_t ldc, int64_t sc, int M, int N, int K, float alpha, float beta,
-              const void* bias, int relu, int out_mode, int splits, int batch, hipStream_t s) {
+              const void* bias, int relu, int out_mode, int splits, int batch, float* csum, int act_bwd,
+              const void* act_x, hipStream_t s) {
   if (M <= 0 || N <= 0 || batch <= 0) return;
+  if (csum && batch != 1) throw std::runtime_error("ggemm: fused column sums need batch 1");
   check_int((int64_t)M * N, "M*N");
   Args p{};
   p.M = M; p.N = N; p.K = K;
   p.a = a; p.lda = lda; p.sa = sa; p.b = b; p.ldb = ldb; p.sb = sb;
   p.c = c; p.ldc = ldc; p.sc = sc; p.alpha = alpha; p.beta = beta; p.bias = (const float*)bias; p.sbias = 0;
-  p.relu = relu; p.out_mode = out_mode;
-  splits = out_mode == O_F32_ATOMIC ? pick_splits(M, N, K, batch, splits, dt == 0) : 1;
+  p.relu = relu; p.out_mode = out_mode; p.csum = csum; p.act_x = act_x; p.act_bwd = act_bwd;
+  const bool f = dt == 0;
+  int tile = 0;
+  if (f) {
+    // plain fp32 output split over K: C zeroed (beta 0) or kept (beta 1) and accumulated atomically
+    const bool plain_ok = out_mode == O_F32 && !relu && !act_x && (beta == 0.f || beta == 1.f);
+    const bool can_split = out_mode == O_F32_ATOMIC || plain_ok;
+    int sp = 1;
+    pick_f32(M, N, K, batch, can_split, out_mode == O_F32 && beta == 0.f, tile, sp);
+    if (g_gg[0] > 0) tile = g_gg[0];
+    if (g_gg[1] != 0) sp = g_gg[1] > 1 && K >= 2 * BK * g_gg[1] ? g_gg[1] : 1;
+    if (out_mode == O_F32_ATOMIC && splits > 0) sp = splits;  // caller's explicit count
+    if (!can_split) sp = 1;
+    if (out_mode == O_F32 && sp > 1) {
+      if (beta == 0.f) hipLaunchKernelGGL(zero_rows_k, dim3(M, batch), dim3(256), 0, s, (float*)c, ldc, sc, N);
+      out_mode = p.out_mode = O_F32_ATOMIC;
+    }
+    splits = sp;
+  } else if (out_mode == O_F32_ATOMIC) {
+    const int bm = big_tile(M, N) ? 128 : 64;
+    splits = pick_splits(M, N, K, batch, splits, bm, bm);
+  } else {
+    splits = 1;
+  }
   p.k_per_split = kps(K > 0 ? K : 1, splits);
   if (out_mode == O_F32_ATOMIC && splits == 1) {
     // one writer per output element: accumulate with a plain read-add-store
@@ -642,18 +797,19 @@ void sg_ggemm(int dt, const void* a, int64_t lda, int a_kouter, int64_t sa, cons
     p.beta = 1.f;
   }
   p.g = make_geom(1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0, 0, 1, 1, 1);
-  const bool f = dt == 0;
   p.vec_a = f ? aligned<float>(a, lda, sa, a_kouter ? M : K) : aligned<sg::bf16>(a, lda, sa, a_kouter ? M : K);
   p.vec_b = f ? aligned<float>(b, ldb, sb, b_kouter ? N : K) : aligned<sg::bf16>(b, ldb, sb, b_kouter ? N : K);
-#define GO(T)                                                                         \
-  {                                                                                   \
-    if (!a_kouter && !b_kouter) launch<T, KMAJ, KMAJ>(p, batch, splits, s);           \
-    else if (!a_kouter && b_kouter) launch<T, KMAJ, KOUT>(p, batch, splits, s);       \
-    else if (a_kouter && !b_kouter) launch<T, KOUT, KMAJ>(p, batch, splits, s);       \
-    else launch<T, KOUT, KOUT>(p, batch, splits, s);                                  \
+  if (f) {
+    if (!a_kouter && !b_kouter) launch_f32<KMAJ, KMAJ>(p, batch, splits, tile, s);
+    else if (!a_kouter && b_kouter) launch_f32<KMAJ, KOUT>(p, batch, splits, tile, s);
+    else if (a_kouter && !b_kouter) launch_f32<KOUT, KMAJ>(p, batch, splits, tile, s);
+    else launch_f32<KOUT, KOUT>(p, batch, splits, tile, s);
+  } else {
+    if (!a_kouter && !b_kouter) launch<sg::bf16, KMAJ, KMAJ>(p, batch, splits, s);
+    else if (!a_kouter && b_kouter) launch<sg::bf16, KMAJ, KOUT>(p, batch, splits, s);
+    else if (a_kouter && !b_kouter) launch<sg::bf16, KOUT, KMAJ>(p, batch, splits, s);
+    else launch<sg::bf16, KOUT, KOUT>(p, batch, splits, s);
   }
-  if (f) GO(float) else GO(sg::bf16)
-#undef GO
 }
 
 // Convolution forward, NHWC activations, weights [K][R][S][C/groups]:
@@ -717,7 +873,10 @@ void sg_gconv_wgrad(int dt, const void* x, const void* dy, void* dw_out, int N, 
   p.b = x; p.ldb = 0; p.sb = g.Cg;
   p.c = dw_out; p.ldc = (int64_t)R * S * g.Cg; p.sc = (int64_t)g.Kg * R * S * g.Cg;
   p.alpha = 1.f; p.beta = 0.f; p.bias = nullptr; p.relu = 0; p.out_mode = O_F32_ATOMIC;
-  splits = pick_splits(p.M, p.N, p.K, groups, splits, dt == 0);
+  {
+    const int bm = big_tile(p.M, p.N, dt == 0) ? 128 : 64;
+    splits = pick_splits(p.M, p.N, p.K, groups, splits, bm, bm);
+  }
   p.k_per_split = kps(p.K > 0 ? p.K : 1, splits);
   if (splits == 1) {  // single writer: read-add-store accumulation (see sg_ggemm)
     p.out_mode = O_F32;

@@ -168,9 +168,11 @@ def _new_param(shape, dev, dtype=torch.float32) -> Tensor:
 
 
 class Linear(Layer):
-    """y = x W + b, W [in, out]."""
+    """y = act(x W + b), W [in, out].  ``activation`` (relu / sigmoid / tanh /
+    stanh, default none) is applied in the GEMM epilogue, and its backward in
+    the next fused Linear's data-gradient epilogue (see autograd.Linear)."""
 
-    def __init__(self, out_features: int, *args, bias: bool = True, **kwargs):
+    def __init__(self, out_features: int, *args, bias: bool = True, activation: Optional[str] = None, **kwargs):
         super().__init__()
         self.in_features = None
         if len(args) > 0:  # Linear(in, out[, bias])
@@ -180,6 +182,9 @@ class Linear(Layer):
                 bias = args[1]
         self.out_features = out_features
         self.bias = bias
+        if activation is not None and activation not in ("relu", "sigmoid", "tanh", "stanh"):
+            raise ValueError(f"Linear: unsupported fused activation {activation}")
+        self.activation = activation
 
     def initialize(self, x):
         self.in_features = x.shape[-1]
@@ -193,8 +198,8 @@ class Linear(Layer):
 
     def forward(self, x):
         if self.bias:
-            return autograd.Linear(True)(x, self.W, self.b)
-        return autograd.Linear(False)(x, self.W)
+            return autograd.Linear(True, act=self.activation)(x, self.W, self.b)
+        return autograd.Linear(False, act=self.activation)(x, self.W)
 
 
 class Gemm(Layer):

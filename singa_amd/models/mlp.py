@@ -15,11 +15,14 @@ from .. import layer, model
 
 class MLP(model.Model):
     def __init__(self, hidden: Sequence[int] = (512,), num_classes: int = 10, activation: str = "relu",
-                 dropout: float = 0.0):
+                 dropout: float = 0.0, fuse_activation: bool = True):
         super().__init__()
-        self.fcs = [layer.Linear(h) for h in hidden]
+        # relu / sigmoid / tanh / stanh run in the GEMM epilogues (forward, and
+        # backward inside the next layer's data-gradient GEMM)
+        fused = fuse_activation and activation in ("relu", "sigmoid", "tanh", "stanh")
+        self.fcs = [layer.Linear(h, activation=activation if fused else None) for h in hidden]
         act = {"relu": layer.ReLU, "tanh": layer.Tanh, "stanh": layer.STanh, "sigmoid": layer.Sigmoid,
-               "gelu": layer.Gelu}[activation]
+               "gelu": layer.Gelu, "identity": layer.Identity}["identity" if fused else activation]
         self.acts = [act() for _ in hidden]
         self.drops = [layer.Dropout(dropout) for _ in hidden] if dropout > 0 else []
         self.out = layer.Linear(num_classes)
@@ -31,7 +34,7 @@ class MLP(model.Model):
 
             x = autograd.flatten(x, 1)
         for i, (fc, a) in enumerate(zip(self.fcs, self.acts)):
-            x = a(fc(x))
+            x = fc(x) if fc.activation is not None else a(fc(x))
             if self.drops:
                 x = self.drops[i](x)
         return self.out(x)

@@ -563,20 +563,60 @@ def _igemm_ok(a, lda, ako, b, ldb, bko, M, Nn, K, sa, sb) -> bool:
     return True
 
 
+GEMM_ACT = {"relu": 1, "sigmoid": 2, "tanh": 3, "stanh": 4}  # ggemm.hip Act codes
+
+
 def gemm(a: torch.Tensor, b: torch.Tensor, ta: bool = False, tb: bool = False, out: Optional[torch.Tensor] = None,
          out_dtype: Optional[torch.dtype] = None, alpha: float = 1.0, beta: float = 0.0,
-         bias: Optional[torch.Tensor] = None, relu: bool = False, accumulate: bool = False) -> torch.Tensor:
+         bias: Optional[torch.Tensor] = None, relu: bool = False, accumulate: bool = False,
+         colsum_b: Optional[torch.Tensor] = None, act: Optional[str] = None,
+         act_grad: Optional[Tuple[str, torch.Tensor]] = None) -> torch.Tensor:
     """C = alpha * op(a) @ op(b) (+ beta * C) (+ bias[n]) (ReLU), op(t) = t.T if
     the flag is set.  2-D or batched 3-D operands (equal batch, or one side
     2-D and shared).  ``accumulate``: C (fp32 ``out``) += alpha * op(a) op(b)
-    (split-K atomics).  On the GPU: bf16 operands of aligned shapes run the
-    tuned MFMA kernel, everything else (fp32 -- exact f32 MFMA -- and ragged
-    bf16) the generic one; there is no vendor-BLAS path."""
+    (split-K atomics).  ``colsum_b`` (fp32 [N], 2-D operands): += the column
+    sums of op(b) -- a weight-gradient GEMM's bias gradient, summed by the
+    generic kernel from the tiles it stages anyway.  ``act`` (relu / sigmoid
+    / tanh / stanh): activation of the output; ``act_grad`` = (act, y): C *=
+    act'(y) with y that activation's output, laid out like C (a data-gradient
+    GEMM taking its producer's activation backward).  Both run in the fp32
+    kernel's epilogue; other paths apply them in a separate pass.  On the
+    GPU: bf16 operands of aligned shapes run the tuned MFMA kernel,
+    everything else (fp32 -- exact f32 MFMA -- and ragged bf16) the generic
+    one; there is no vendor-BLAS path."""
+    if colsum_b is not None and (a.dim() != 2 or b.dim() != 2):
+        raise ValueError("gemm: colsum_b needs 2-D operands")
+    if act == "relu" and act_grad is None:
+        act, relu = None, True
+    if act is not None or act_grad is not None:
+        if act is not None and act not in GEMM_ACT or act_grad is not None and act_grad[0] not in GEMM_ACT:
+            raise ValueError(f"gemm: unsupported fused activation {act or act_grad[0]}")
+        if relu or accumulate:
+            raise ValueError("gemm: act / act_grad exclude relu and accumulate")
+        fused = (a.is_cuda and N.available() and a.dtype == torch.float32 and b.dtype == torch.float32
+                 and (out is None or out.dtype == torch.float32) and (out_dtype in (None, torch.float32)))
+        if not fused:
+            c = gemm(a, b, ta, tb, out, out_dtype, alpha, beta, bias, False, False, colsum_b)
+            r = c
+            if act is not None:
+                r = unary(act, r)
+            if act_grad is not None:
+                k, yv = act_grad
+                r = relu_bwd_from_y(yv, r) if k == "relu" else unary_bwd(k, None, yv, r)
+            if r is not c:
+                G.copy_(c, r)
+            return c
+        if act_grad is not None:
+            yv = act_grad[1]
+            if yv.dtype != torch.float32 or not yv.is_contiguous():
+                raise ValueError("gemm: act_grad output must be a dense fp32 tensor")
     if a.dim() == 2 and b.dim() == 2:
         batch = 1
     elif a.dim() == 3 and b.dim() == 2 and not ta and a.is_contiguous() and out is None:
         Bt = a.shape[0]
-        c = gemm(a.reshape(-1, a.shape[-1]), b, False, tb, None, out_dtype, alpha, beta, bias, relu)
+        ag = (act_grad[0], act_grad[1].reshape(-1, act_grad[1].shape[-1])) if act_grad is not None else None
+        c = gemm(a.reshape(-1, a.shape[-1]), b, False, tb, None, out_dtype, alpha, beta, bias, relu, act=act,
+                 act_grad=ag)
         return c.reshape(Bt, a.shape[1], c.shape[-1])
     elif a.dim() == 3 or b.dim() == 3:
         batch = a.shape[0] if a.dim() == 3 else b.shape[0]
@@ -610,12 +650,16 @@ def gemm(a: torch.Tensor, b: torch.Tensor, ta: bool = False, tb: bool = False, o
             return out
         CP.gemm(a, lda, ako, b, ldb, not bko, out, M, Nn, K, alpha, 1.0 if accumulate else beta, bb, relu, batch, sa,
                 sb, sc)
+        if colsum_b is not None:
+            _colsum_opb(b, tb, colsum_b)
         return out
     if not (_native_ok(a, b) and a.is_cuda):
         if a.is_cuda:
             _no_native("gemm", a, b)
         aa = a.float().transpose(-1, -2) if ta else a.float()
         bb = b.float().transpose(-1, -2) if tb else b.float()
+        if colsum_b is not None:
+            colsum_b.add_(bb.sum(0))
         r = alpha * torch.matmul(aa, bb)
         if accumulate:
             return out.add_(r.reshape(out.shape))
@@ -647,49 +691,77 @@ def gemm(a: torch.Tensor, b: torch.Tensor, ta: bool = False, tb: bool = False, o
     if _igemm_ok(a, lda, ako, b, ldb, bko, M, Nn, K, sa, sb) and (mode == 2 or sc % 8 == 0) and K > 0:
         L.gemm(a.data_ptr(), lda, int(ako), b.data_ptr(), ldb, int(bko), out.data_ptr(), Nn, M, Nn, K, alpha, beta,
                N.ptr(bb), int(relu), mode, 0 if mode == 2 else 1, batch, sa, sb, sc, N.stream())
+        if colsum_b is not None:
+            _colsum_opb(b, not bko, colsum_b)
         return out
     if a.dtype not in (torch.float32, torch.bfloat16):
         _no_native(f"gemm ({a.dtype})", a)
+    cs = 0
+    if colsum_b is not None:
+        if colsum_b.dtype != torch.float32 or not colsum_b.is_contiguous() or colsum_b.numel() != Nn:
+            raise ValueError("gemm: colsum_b must be a dense fp32 [N] tensor")
+        cs = colsum_b.data_ptr()
+    code = GEMM_ACT[act] if act is not None else int(relu)
+    ab, ax = (GEMM_ACT[act_grad[0]], act_grad[1]) if act_grad is not None else (0, None)
+    if ax is not None and tuple(ax.shape) != tuple(out.shape):
+        raise ValueError(f"gemm: act_grad output {tuple(ax.shape)} != C {tuple(out.shape)}")
     L.ggemm(0 if a.dtype == torch.float32 else 1, a.data_ptr(), lda, int(ako), sa, b.data_ptr(), ldb, int(bko), sb,
-            out.data_ptr(), Nn, sc, M, Nn, K, alpha, beta, N.ptr(bb), int(relu), mode, 0, batch, N.stream())
+            out.data_ptr(), Nn, sc, M, Nn, K, alpha, beta, N.ptr(bb), code, mode, 0, batch, cs, ab, N.ptr(ax),
+            N.stream())
     return out
 
 
+def _colsum_opb(b: torch.Tensor, tb: bool, out: torch.Tensor) -> None:
+    """out += column sums of op(b) (op = transpose if ``tb``): the separate
+    pass for the GEMM paths that do not fuse it."""
+    if tb:
+        out_, _ = colsum(G.contiguous(b.t()))
+        G.binary("add", out, out_, out=out)
+    else:
+        colsum(G.contiguous(b), out=out)
+
+
 def matmul(a: torch.Tensor, b: torch.Tensor, out_dtype: Optional[torch.dtype] = None,
-           bias: Optional[torch.Tensor] = None, relu: bool = False) -> torch.Tensor:
+           bias: Optional[torch.Tensor] = None, relu: bool = False, act: Optional[str] = None) -> torch.Tensor:
     """C = a @ b for 2-D (or batched 3-D with equal batch) row-major operands.
     bf16 operands run on the MFMA kernel with fp32 accumulation; fp32
-    operands on the exact-f32 MFMA kernel."""
+    operands on the exact-f32 MFMA kernel (``act``: fused output activation,
+    see :func:`gemm`)."""
     if a.dim() > 3 or b.dim() > 3:  # flatten equal leading dims (torch.matmul broadcasting otherwise)
         lead = torch.broadcast_shapes(a.shape[:-2], b.shape[:-2])
         aa = G.reshape(a.expand(*lead, *a.shape[-2:]), (-1, *a.shape[-2:]))
         bb = G.reshape(b.expand(*lead, *b.shape[-2:]), (-1, *b.shape[-2:]))
-        c = gemm(aa, bb, out_dtype=out_dtype or a.dtype, bias=bias, relu=relu)
+        c = gemm(aa, bb, out_dtype=out_dtype or a.dtype, bias=bias, relu=relu, act=act)
         return c.reshape(*lead, c.shape[-2], c.shape[-1])
     if a.dim() == 3 and b.dim() == 3 and a.shape[0] != b.shape[0]:
         lead = torch.broadcast_shapes(a.shape[:1], b.shape[:1])
         a = a.expand(*lead, *a.shape[-2:])
         b = b.expand(*lead, *b.shape[-2:])
-    return gemm(a, b, out_dtype=out_dtype or a.dtype, bias=bias, relu=relu)
+    return gemm(a, b, out_dtype=out_dtype or a.dtype, bias=bias, relu=relu, act=act)
 
 
-def gemm_nt(a: torch.Tensor, b: torch.Tensor, out_dtype=None, bias=None, relu=False) -> torch.Tensor:
-    """C = a @ b.T (both operands K-major: a [M,K], b [N,K])."""
-    return gemm(a, b, tb=True, out_dtype=out_dtype or a.dtype, bias=bias, relu=relu)
+def gemm_nt(a: torch.Tensor, b: torch.Tensor, out_dtype=None, bias=None, relu=False, act_grad=None) -> torch.Tensor:
+    """C = a @ b.T (both operands K-major: a [M,K], b [N,K]); ``act_grad`` as in :func:`gemm`."""
+    return gemm(a, b, tb=True, out_dtype=out_dtype or a.dtype, bias=bias, relu=relu, act_grad=act_grad)
 
 
-def gemm_tn_acc(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, beta: float = 1.0) -> torch.Tensor:
+def gemm_tn_acc(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, beta: float = 1.0,
+                colsum_b: Optional[torch.Tensor] = None) -> torch.Tensor:
     """out (fp32) = beta*out + a.T @ b with a [K,M], b [K,N] (weight-gradient
-    shape: reduction over the batch dim).  Uses split-K atomics on GPU."""
+    shape: reduction over the batch dim).  Uses split-K atomics on GPU.
+    ``colsum_b`` (fp32 [N]) += the column sums of b (the bias gradient), fused
+    into the GEMM where the kernel supports it."""
     if out.is_cuda and N.available():
         if beta == 0.0:
             N.lib().zero(out.data_ptr(), out.numel() * out.element_size(), N.stream())
         elif beta != 1.0:
             G.binary("mul", out, beta, out=out)
-        return gemm(a, b, ta=True, out=out, accumulate=True)
+        return gemm(a, b, ta=True, out=out, accumulate=True, colsum_b=colsum_b)
     if CP.ok(a, b, out) and out.is_contiguous():
-        return gemm(a, b, ta=True, out=out, beta=beta)
+        return gemm(a, b, ta=True, out=out, beta=beta, colsum_b=colsum_b)
     r = a.float().t() @ b.float()
+    if colsum_b is not None:
+        colsum_b.add_(b.float().sum(0))
     if beta == 0.0:
         out.copy_(r)
     else:

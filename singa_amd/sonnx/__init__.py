@@ -272,12 +272,18 @@ for _n, _t in (("Sub", "Sub"), ("Mul", "Mul"), ("Div", "Div"), ("Pow", "Pow"), (
 
 @exporter("Linear")
 def _x_linear(c, op, xs, i, o):
+    act = getattr(op, "act", None)  # a fused output activation exports as its own node(s)
+    out = c.fresh() if act else o[0]
     if len(i) > 2:
         t = c.fresh()
         c.add("MatMul", i[:2], [t])
-        c.add("Add", [t, i[2]], [o[0]])
+        c.add("Add", [t, i[2]], [out])
     else:
-        c.add("MatMul", i[:2], [o[0]])
+        c.add("MatMul", i[:2], [out])
+    if act == "stanh":
+        _x_stanh(c, op, xs, [out], o)
+    elif act:
+        c.add({"relu": "Relu", "sigmoid": "Sigmoid", "tanh": "Tanh"}[act], [out], [o[0]])
 
 
 @exporter("Conv2d")

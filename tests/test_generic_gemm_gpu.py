@@ -57,6 +57,96 @@ def test_fp32_gemm_transposed_views_and_accumulate(gpu):
     assert rel_err(c, x.double().t() @ dy.double()) < 1e-5
 
 
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("splits", [0, -1, 3])
+def test_fp32_gemm_every_tile_and_split(gpu, tile, splits):
+    """Every fp32 tile variant and split-K mode (forced through ggemm_tune),
+    with a biased plain output (split-K: zeroed C, split 0 adds the bias), an
+    accumulating weight-gradient with the fused bias-gradient column sums,
+    and a dgrad-shaped call -- exact to 1e-5."""
+    from singa_amd.ops import functional as F
+    from singa_amd.ops import native as N
+    L = N.lib()
+    x, w, b = _rand(300, 203, seed=11), _rand(203, 157, seed=12), _rand(157, seed=13)
+    dy, acc, db0 = _rand(300, 157, seed=14), _rand(203, 157, seed=15), _rand(157, seed=16)
+    try:
+        L.ggemm_tune(0, tile)
+        L.ggemm_tune(1, splits)
+        y = F.matmul(x.to(gpu), w.to(gpu), bias=b.to(gpu))
+        assert rel_err(y, x.double() @ w.double() + b.double()) < 1e-5
+        g, db = acc.to(gpu), db0.to(gpu)
+        F.gemm_tn_acc(x.to(gpu), dy.to(gpu), g, colsum_b=db)
+        assert rel_err(g, acc.double() + x.double().t() @ dy.double()) < 1e-5
+        assert rel_err(db, db0.double() + dy.double().sum(0)) < 1e-5
+        dx = F.gemm_nt(dy.to(gpu), w.to(gpu))
+        assert rel_err(dx, dy.double() @ w.double().t()) < 1e-5
+    finally:
+        L.ggemm_tune(0, 0)
+        L.ggemm_tune(1, 0)
+
+
+_ACTS = {"relu": torch.relu, "sigmoid": torch.sigmoid, "tanh": torch.tanh,
+         "stanh": lambda h: 1.7159047 * torch.tanh(0.66666667 * h)}
+
+
+@pytest.mark.parametrize("act", sorted(_ACTS))
+def test_fp32_gemm_fused_activation(gpu, act):
+    """Output activation in the epilogue, and a data-gradient GEMM that also
+    multiplies by the producer activation's derivative (from its output)."""
+    from singa_amd.ops import functional as F
+    x, w, b = _rand(150, 77, seed=51), _rand(77, 93, seed=52) * 0.2, _rand(93, seed=53)
+    y = F.matmul(x.to(gpu), w.to(gpu), bias=b.to(gpu), act=act)
+    ref = _ACTS[act](x.double() @ w.double() + b.double())
+    assert rel_err(y, ref) < 1e-5
+    dy, w2 = _rand(150, 41, seed=54), _rand(93, 41, seed=55)
+    dx = F.gemm_nt(dy.to(gpu), w2.to(gpu), act_grad=(act, y))
+    h = (x.double() @ w.double() + b.double()).requires_grad_(True)
+    (gh,) = torch.autograd.grad(_ACTS[act](h), [h], dy.double() @ w2.double().t())
+    assert rel_err(dx, gh) < 1e-5
+
+
+@pytest.mark.parametrize("act", ["relu", "stanh", "sigmoid"])
+def test_fp32_mlp_step_bias_grad_fused(gpu, act):
+    """One SGD step (lr 1, no momentum) of an fp32 MLP whose Linear layers
+    fuse the activation (forward epilogue; backward in the next layer's
+    data-gradient epilogue) and take the bias gradient from the
+    weight-gradient GEMM (the optimizer's flat gradient views): every
+    parameter update equals the float64 PyTorch gradient of the same
+    network."""
+    from singa_amd import device, opt, tensor
+    from singa_amd.models import mlp
+    dev = device.create_rocm_gpu()
+    dev.SetRandSeed(3)
+    m = mlp.create_model((48, 40), 10, activation=act)
+    x = _rand(130, 33, seed=31)
+    y = torch.randint(0, 10, (130,), generator=torch.Generator().manual_seed(32)).int()
+    tx = tensor.from_numpy(x.numpy()).to_device(dev)
+    ty = tensor.from_numpy(y.numpy()).to_device(dev)
+    m.set_optimizer(opt.SGD(lr=1.0))
+    m.compile([tx], is_train=True, use_graph=False)
+    m.train()
+    before = {k: v.data.double().cpu().clone() for k, v in m.get_params().items()}
+    m(tx, ty)
+    torch.cuda.synchronize()
+    after = {k: v.data.double().cpu() for k, v in m.get_params().items()}
+    ref = {k: v.clone().requires_grad_(True) for k, v in before.items()}
+    names = sorted(ref)
+    ws = [n for n in names if ref[n].dim() == 2]
+    bs = [n for n in names if ref[n].dim() == 1]
+    assert len(ws) == 3 and len(bs) == 3
+    # layer order follows the creation order of the parameters (input width 33 first)
+    order = sorted(zip(ws, bs), key=lambda wb: [33, 48, 40].index(ref[wb[0]].shape[0]))
+    h = x.double()
+    for i, (wn, bn) in enumerate(order):
+        h = h @ ref[wn] + ref[bn]
+        if i < 2:
+            h = _ACTS[act](h)
+    loss = torch.nn.functional.cross_entropy(h, y.long())
+    loss.backward()
+    for n in names:
+        assert rel_err(before[n] - after[n], ref[n].grad) < 1e-5, n
+
+
 @pytest.mark.parametrize("M,N,K", [(37, 53, 91), (100, 10, 30), (257, 129, 67)])
 def test_bf16_ragged_gemm(gpu, M, N, K):
     from singa_amd.ops import functional as F
