@@ -68,6 +68,13 @@ ACCUMULATED = object()  # backward() returned: grad already added to the param's
 # gradient to hold this backward's contribution only)
 GRAD_EPOCH = [0]
 _WGRAD_EPOCH: dict = {}
+# params whose gradient a Linear writes (beta = 0, no zeroed buffer needed) on
+# its first contribution in an epoch; ParamStore.zero_grad(lazy=True) leaves
+# their slices alone and fix_unwritten() zeroes any that a step did not reach
+OVERWRITE_FIRST: set = set()
+# uses of each param (id) in the current backward (its producers may only
+# overwrite the gradient when they are the sole user)
+PARAM_USES: dict = {}
 # backward() returned: the input gradient was added IN PLACE into the partial
 # gradient the engine offered through ``op.acc_into`` (see backward())
 ACC_INPLACE = object()
@@ -256,6 +263,17 @@ def backward(y, dy=None) -> Iterator[Tuple[Tensor, Tensor]]:
             if src_op not in seen:
                 seen.add(src_op)
                 q.append(src_op)
+    PARAM_USES.clear()
+    PARAM_USES.update(puses)
+    if OVERWRITE_FIRST:
+        # a lazily-zeroed gradient slice with several users this time: clear
+        # it now and let zero_grad cover it again
+        for op_ in seen:
+            for p in op_.params:
+                if p is not None and id(p) in OVERWRITE_FIRST and puses[id(p)] > 1:
+                    OVERWRITE_FIRST.discard(id(p))
+                    if p.grad_view is not None and _WGRAD_EPOCH.get(id(p)) != GRAD_EPOCH[0]:
+                        G.zero_(p.grad_view)
     # every conv weight this backward's data gradients need, transposed K-major in one launch
     convs = sorted((o for o in seen if isinstance(o, Conv2d) and getattr(o, "w", None) is not None and o.group == 1
                     and o.dilation == (1, 1) and o.needs_grad(0)), key=lambda o: getattr(o, "_seq", 0))
@@ -689,7 +707,21 @@ class Linear(Operator):
         # gradient GEMM, which stages every dy tile anyway
         fuse_db = tb is not None and tgt is not None and tb.is_contiguous()
         if tgt is not None:
-            F.gemm_tn_acc(x2, dy2, tgt, colsum_b=tb if fuse_db else None)
+            wid = id(self.params[1])
+            # first (and sole) writer of this epoch's weight gradient: write
+            # it (beta 0) instead of adding into a zeroed buffer
+            empty = _WGRAD_EPOCH.get(wid) != GRAD_EPOCH[0]
+            first = (empty and PARAM_USES.get(wid) == 1 and tgt.is_cuda and tgt.is_contiguous()
+                     and x2.dtype == torch.float32 and dy2.dtype == torch.float32)
+            if first:
+                F.gemm(x2, dy2, ta=True, out=tgt, beta=0.0, colsum_b=tb if fuse_db else None)
+                OVERWRITE_FIRST.add(wid)
+            else:
+                if empty and wid in OVERWRITE_FIRST:  # its slice was not zeroed by a lazy zero_grad
+                    G.zero_(tgt)
+                    OVERWRITE_FIRST.discard(wid)
+                F.gemm_tn_acc(x2, dy2, tgt, colsum_b=tb if fuse_db else None)
+            _WGRAD_EPOCH[wid] = GRAD_EPOCH[0]
             dw = ACCUMULATED
         else:
             dw = F.gemm(x2, dy2, ta=True, out_dtype=torch.float32)

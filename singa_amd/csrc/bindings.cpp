@@ -25,6 +25,7 @@ void sg_unary_bwd(int, const void*, const void*, const void*, void*, int64_t, in
 void sg_add_act(const void*, const void*, void*, int64_t, int, float, float, int, hipStream_t);
 void sg_relu_bwd_from_y(const void*, const void*, void*, int64_t, int, hipStream_t);
 void sg_mask_bits_apply(const void*, const void*, void*, int64_t, hipStream_t);
+void sg_zero_ranges(void*, const void*, int, hipStream_t);
 void sg_cast(const void*, int, void*, int, int64_t, hipStream_t);
 void sg_dropout_fwd(const void*, void*, void*, int64_t, int, float, uint64_t, uint64_t, const void*, hipStream_t);
 void sg_dropout_bwd(const void*, const void*, void*, int64_t, int, float, hipStream_t);
@@ -192,6 +193,10 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("add_act", [](P a, P b, P y, int64_t n, int dt, float al, float be, int relu, P s) {
     sg_add_act(CV(a), CV(b), V(y), n, dt, al, be, relu, S(s)); CHK("add_act");
+  });
+  m.def("zero_ranges", [](P base, P ranges, int nr, P s) {
+    sg_zero_ranges(V(base), CV(ranges), nr, S(s));
+    CHK("zero_ranges");
   });
   m.def("mask_bits_apply", [](P g, P mask, P out, int64_t n, P s) {
     sg_mask_bits_apply(CV(g), CV(mask), V(out), n, S(s)); CHK("mask_bits_apply");

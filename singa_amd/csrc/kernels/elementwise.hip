@@ -438,6 +438,15 @@ __global__ void nchw_to_pairs_k(const float* __restrict__ x, bf16* __restrict__ 
   }
 }
 
+// zero the fp32 element ranges [off, off + len) listed as int64 pairs in a
+// device table (a lazily-zeroed gradient buffer: everything but the slices
+// whose producers overwrite them), one launch for all ranges
+__global__ void zero_ranges_k(float* __restrict__ base, const int64_t* __restrict__ r) {
+  const int64_t off = r[2 * blockIdx.y], len = r[2 * blockIdx.y + 1];
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < len; e += (int64_t)gridDim.x * blockDim.x)
+    base[off + e] = 0.f;
+}
+
 }  // namespace sg
 
 using namespace sg;
@@ -466,6 +475,10 @@ void sg_add_act(const void* a, const void* b, void* y, int64_t n, int dtype, flo
                 hipStream_t s) {
   DISPATCH_FT(dtype, hipLaunchKernelGGL(add_act_k<T>, dim3(sg_grid(n / Vec<T>::N + 1)), dim3(256), 0, s,
                                         (const T*)a, (const T*)b, (T*)y, n, alpha, beta, relu));
+}
+void sg_zero_ranges(void* base, const void* ranges, int nr, hipStream_t s) {
+  if (nr <= 0) return;
+  hipLaunchKernelGGL(sg::zero_ranges_k, dim3(512, nr), dim3(256), 0, s, (float*)base, (const int64_t*)ranges);
 }
 void sg_mask_bits_apply(const void* g, const void* mask, void* out, int64_t n, hipStream_t s) {
   const int64_t nv = n / 8;

@@ -30,6 +30,64 @@ struct OptArgs {
   int nesterov, adamw;
 };
 
+// One element of every update rule: w, optimizer state h1 / h2 (in / out).
+template <int KIND>
+__device__ __forceinline__ void opt_elem(float& wv, float gv, float& h1, float& h2, float lr, float wd, float bc1,
+                                         float bc2, const OptArgs& a) {
+  if (KIND == O_SGD) {
+    gv += wd * wv;
+    if (a.momentum != 0.f) {
+      float b = h1;
+      b = a.momentum * b + (1.f - a.dampening) * gv;
+      h1 = b;
+      gv = a.nesterov ? gv + a.momentum * b : b;
+    }
+    wv -= lr * gv;
+  } else if (KIND == O_SGD_REF) {  // reference: h = m*h + lr*g; w -= h
+    gv += wd * wv;
+    if (a.momentum > 0.f) {
+      float h = a.momentum * h1 + lr * gv;
+      h1 = h;
+      wv -= h;
+    } else {
+      wv -= lr * gv;
+    }
+  } else if (KIND == O_NESTEROV_REF) {  // h0=h; h=m*h+lr*g; w -= (1+m)h - m h0
+    gv += wd * wv;
+    float h0 = h1;
+    float h = a.momentum * h0 + lr * gv;
+    h1 = h;
+    wv -= (1.f + a.momentum) * h - a.momentum * h0;
+  } else if (KIND == O_ADAGRAD) {
+    gv += wd * wv;
+    float h = h1 + gv * gv;
+    h1 = h;
+    wv -= lr * gv / sqrtf(h + a.eps);
+  } else if (KIND == O_RMSPROP) {
+    gv += wd * wv;
+    float h = a.rho * h1 + (1.f - a.rho) * gv * gv;
+    h1 = h;
+    wv -= lr * gv / sqrtf(h + a.eps);
+  } else if (KIND == O_ADADELTA) {
+    gv += wd * wv;
+    float h = a.rho * h1 + (1.f - a.rho) * gv * gv;
+    float u = h2;
+    float d = gv * sqrtf(u + a.eps) / sqrtf(h + a.eps);
+    h1 = h;
+    h2 = a.rho * u + (1.f - a.rho) * d * d;
+    wv -= lr * d;
+  } else if (KIND == O_ADAM) {
+    if (!a.adamw) gv += wd * wv;
+    float m = a.beta1 * h1 + (1.f - a.beta1) * gv;
+    float v = a.beta2 * h2 + (1.f - a.beta2) * gv * gv;
+    h1 = m;
+    h2 = v;
+    float upd = (m / bc1) / (sqrtf(v / bc2) + a.eps);
+    if (a.adamw) upd += wd * wv;
+    wv -= lr * upd;
+  }
+}
+
 template <int KIND>
 __global__ void __launch_bounds__(256) opt_k(float* __restrict__ w, const float* __restrict__ g,
                                              float* __restrict__ s1, float* __restrict__ s2, bf16* __restrict__ wlow,
@@ -49,63 +107,34 @@ __global__ void __launch_bounds__(256) opt_k(float* __restrict__ w, const float*
     bc1 = 1.f - __powf(a.beta1, t);
     bc2 = 1.f - __powf(a.beta2, t);
   }
-  for (int i = threadIdx.x; i < len; i += blockDim.x) {
-    const int64_t e = st + i;
-    float wv = w[e];
-    float gv = g[e] * a.grad_scale;
-    if (KIND == O_SGD) {
-      gv += wd * wv;
-      if (a.momentum != 0.f) {
-        float b = s1[e];
-        b = a.momentum * b + (1.f - a.dampening) * gv;
-        s1[e] = b;
-        gv = a.nesterov ? gv + a.momentum * b : b;
-      }
-      wv -= lr * gv;
-    } else if (KIND == O_SGD_REF) {  // reference: h = m*h + lr*g; w -= h
-      gv += wd * wv;
-      if (a.momentum > 0.f) {
-        float h = a.momentum * s1[e] + lr * gv;
-        s1[e] = h;
-        wv -= h;
-      } else {
-        wv -= lr * gv;
-      }
-    } else if (KIND == O_NESTEROV_REF) {  // h0=h; h=m*h+lr*g; w -= (1+m)h - m h0
-      gv += wd * wv;
-      float h0 = s1[e];
-      float h = a.momentum * h0 + lr * gv;
-      s1[e] = h;
-      wv -= (1.f + a.momentum) * h - a.momentum * h0;
-    } else if (KIND == O_ADAGRAD) {
-      gv += wd * wv;
-      float h = s1[e] + gv * gv;
-      s1[e] = h;
-      wv -= lr * gv / sqrtf(h + a.eps);
-    } else if (KIND == O_RMSPROP) {
-      gv += wd * wv;
-      float h = a.rho * s1[e] + (1.f - a.rho) * gv * gv;
-      s1[e] = h;
-      wv -= lr * gv / sqrtf(h + a.eps);
-    } else if (KIND == O_ADADELTA) {
-      gv += wd * wv;
-      float h = a.rho * s1[e] + (1.f - a.rho) * gv * gv;
-      float u = s2[e];
-      float d = gv * sqrtf(u + a.eps) / sqrtf(h + a.eps);
-      s1[e] = h;
-      s2[e] = a.rho * u + (1.f - a.rho) * d * d;
-      wv -= lr * d;
-    } else if (KIND == O_ADAM) {
-      if (!a.adamw) gv += wd * wv;
-      float m = a.beta1 * s1[e] + (1.f - a.beta1) * gv;
-      float v = a.beta2 * s2[e] + (1.f - a.beta2) * gv * gv;
-      s1[e] = m;
-      s2[e] = v;
-      float upd = (m / bc1) / (sqrtf(v / bc2) + a.eps);
-      if (a.adamw) upd += wd * wv;
-      wv -= lr * upd;
+  // 16-byte vectors over the chunk (chunk starts are 4-element aligned: the
+  // flat store aligns every parameter), scalar tail
+  const int n4 = (st & 3) == 0 ? len >> 2 : 0;
+  for (int q = threadIdx.x; q < n4; q += blockDim.x) {
+    const int64_t e = st + 4 * (int64_t)q;
+    float4 wv = *(const float4*)(w + e), gv = *(const float4*)(g + e);
+    float4 h1 = s1 ? *(const float4*)(s1 + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 h2 = s2 ? *(const float4*)(s2 + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+    opt_elem<KIND>(wv.x, gv.x * a.grad_scale, h1.x, h2.x, lr, wd, bc1, bc2, a);
+    opt_elem<KIND>(wv.y, gv.y * a.grad_scale, h1.y, h2.y, lr, wd, bc1, bc2, a);
+    opt_elem<KIND>(wv.z, gv.z * a.grad_scale, h1.z, h2.z, lr, wd, bc1, bc2, a);
+    opt_elem<KIND>(wv.w, gv.w * a.grad_scale, h1.w, h2.w, lr, wd, bc1, bc2, a);
+    *(float4*)(w + e) = wv;
+    if (s1) *(float4*)(s1 + e) = h1;
+    if (s2) *(float4*)(s2 + e) = h2;
+    if (wlow) {
+      bf16x4 lo;
+      lo[0] = (bf16)wv.x; lo[1] = (bf16)wv.y; lo[2] = (bf16)wv.z; lo[3] = (bf16)wv.w;
+      *(bf16x4*)(wlow + e) = lo;
     }
+  }
+  for (int i = 4 * n4 + threadIdx.x; i < len; i += blockDim.x) {
+    const int64_t e = st + i;
+    float wv = w[e], h1 = s1 ? s1[e] : 0.f, h2 = s2 ? s2[e] : 0.f;
+    opt_elem<KIND>(wv, g[e] * a.grad_scale, h1, h2, lr, wd, bc1, bc2, a);
     w[e] = wv;
+    if (s1) s1[e] = h1;
+    if (s2) s2[e] = h2;
     if (wlow) wlow[e] = (bf16)wv;
   }
 }

@@ -34,6 +34,8 @@ from .ops import native as N
 from .tensor import Tensor
 
 ALIGN = 64  # elements; keeps every param view 256-B aligned
+# skip zeroing gradient slices whose producer overwrites them (ParamStore.zero_grad)
+LAZY_ZERO = True
 
 
 # ---------------------------------------------------------------------------
@@ -193,9 +195,41 @@ class ParamStore:
                 self.wd_vec[o:o + n] = w
                 self.mask[o:o + n] = True
 
-    def zero_grad(self):
-        G.zero_(self.g)
+    def zero_grad(self, lazy: bool = False):
+        """Clear the flat gradient buffer.  ``lazy``: leave the slices of
+        params whose gradient producer overwrites them on its first write
+        (autograd.OVERWRITE_FIRST) -- one launch zeroes the rest; the caller
+        then runs :meth:`fix_unwritten` after the backward."""
+        ow = [i for i, p in enumerate(self.params) if id(p) in autograd.OVERWRITE_FIRST] if lazy else []
+        key = tuple(ow)
+        if ow and self.gpu and getattr(self, "_zr_key", None) != key and N.lib().rt.is_capturing(N.stream()):
+            ow = []  # (no host->device table upload inside a graph capture: clear everything)
+        if not ow or not self.gpu:
+            G.zero_(self.g)
+        else:
+            if getattr(self, "_zr_key", None) != key:
+                skip = {self.offsets[i]: self.offsets[i] + self.params[i].data.numel() for i in ow}
+                ranges, cur = [], 0
+                for o in sorted(skip):
+                    if o > cur:
+                        ranges += [cur, o - cur]
+                    cur = skip[o]
+                if cur < self.numel:
+                    ranges += [cur, self.numel - cur]
+                self._zr = memory.empty((len(ranges),), dtype=torch.int64, device=self.g.device)
+                G.copy_(self._zr, torch.tensor(ranges, dtype=torch.int64))
+                self._zr_key = key
+            if self._zr.numel():
+                N.lib().zero_ranges(self.g.data_ptr(), self._zr.data_ptr(), self._zr.numel() // 2, N.stream())
         autograd.GRAD_EPOCH[0] += 1
+
+    def fix_unwritten(self):
+        """Zero the gradients a lazy :meth:`zero_grad` left alone that this
+        epoch's backward did not write (e.g. a branch that did not run)."""
+        for p in self.params:
+            if (id(p) in autograd.OVERWRITE_FIRST
+                    and autograd._WGRAD_EPOCH.get(id(p)) != autograd.GRAD_EPOCH[0]):
+                G.zero_(p.grad_view)
 
     def sync_low(self):
         if self.low is not None:
@@ -300,9 +334,10 @@ class Optimizer:
             self.call(loss)
             self.step()
             return
-        self.store.zero_grad()
+        self.store.zero_grad(lazy=LAZY_ZERO)
         for _ in autograd.backward(loss):
             pass
+        self.store.fix_unwritten()
         self.update()
         self.step()
 

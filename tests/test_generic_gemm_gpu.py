@@ -245,3 +245,60 @@ def test_fp32_linear_layer_step(gpu):
     ref = x.double() @ W.double() + b.double()
     assert rel_err(y.data, ref) < 1e-5
     assert rel_err(grads[id(tW)].data, x.double().t() @ torch.ones(64, 250, dtype=torch.float64)) < 1e-5
+
+
+def test_lazy_grad_zero_matches_full_zero(gpu):
+    """The optimizer leaves the weight-gradient slices of fp32 Linear layers
+    unzeroed (their GEMMs overwrite them on the first write of a step):
+    three SGD-momentum steps equal the fully-zeroed run, including a step in
+    which one layer does not run (its stale slice is cleared before the
+    update, so only momentum moves it)."""
+    from singa_amd import autograd, device, layer, model, opt, tensor
+
+    class Net(model.Model):
+        def __init__(self):
+            super().__init__()
+            self.a = layer.Linear(32, activation="relu")
+            self.b = layer.Linear(32, activation="relu")
+            self.out = layer.Linear(10)
+            self.loss_fn = layer.SoftMaxCrossEntropy()
+            self.skip_b = False
+
+        def forward(self, x):
+            h = self.a(x)
+            if not self.skip_b:
+                h = self.b(h)
+            return self.out(h)
+
+        def train_one_batch(self, x, y):
+            o = self.forward(x)
+            loss = self.loss_fn(o, y)
+            self.optimizer(loss)
+            return o, loss
+
+    def run(lazy):
+        opt.LAZY_ZERO = lazy
+        autograd.OVERWRITE_FIRST.clear()
+        dev = device.create_rocm_gpu()
+        dev.SetRandSeed(7)
+        m = Net()
+        x = tensor.from_numpy(_rand(64, 32, seed=61).numpy()).to_device(dev)
+        y = tensor.from_numpy(torch.randint(0, 10, (64,), generator=torch.Generator().manual_seed(62))
+                              .int().numpy()).to_device(dev)
+        m.set_optimizer(opt.SGD(lr=0.1, momentum=0.9))
+        m.compile([x], is_train=True, use_graph=False)
+        m.train()
+        for step in range(4):
+            m.skip_b = step == 2
+            m(x, y)
+        torch.cuda.synchronize()
+        return {k: v.data.double().cpu().clone() for k, v in m.get_params().items()}, len(autograd.OVERWRITE_FIRST)
+
+    try:
+        full, _ = run(False)
+        lazy, n_ow = run(True)
+    finally:
+        opt.LAZY_ZERO = True
+    assert n_ow >= 2  # the lazy path was taken
+    for k in full:
+        assert rel_err(lazy[k], full[k]) < 1e-6, k
