@@ -26,6 +26,7 @@ import sys
 import threading
 import types
 import heapq
+import weakref
 from collections import Counter, deque
 from typing import Callable, Dict, Iterator, List, Optional, Sequence, Tuple
 
@@ -71,7 +72,7 @@ _WGRAD_EPOCH: dict = {}
 # params whose gradient a Linear writes (beta = 0, no zeroed buffer needed) on
 # its first contribution in an epoch; ParamStore.zero_grad(lazy=True) leaves
 # their slices alone and fix_unwritten() zeroes any that a step did not reach
-OVERWRITE_FIRST: set = set()
+OVERWRITE_FIRST = weakref.WeakSet()  # the param Tensors themselves (ids get reused)
 # uses of each param (id) in the current backward (its producers may only
 # overwrite the gradient when they are the sole user)
 PARAM_USES: dict = {}
@@ -270,8 +271,8 @@ def backward(y, dy=None) -> Iterator[Tuple[Tensor, Tensor]]:
         # it now and let zero_grad cover it again
         for op_ in seen:
             for p in op_.params:
-                if p is not None and id(p) in OVERWRITE_FIRST and puses[id(p)] > 1:
-                    OVERWRITE_FIRST.discard(id(p))
+                if p is not None and p in OVERWRITE_FIRST and puses[id(p)] > 1:
+                    OVERWRITE_FIRST.discard(p)
                     if p.grad_view is not None and _WGRAD_EPOCH.get(id(p)) != GRAD_EPOCH[0]:
                         G.zero_(p.grad_view)
     # every conv weight this backward's data gradients need, transposed K-major in one launch
@@ -715,11 +716,11 @@ class Linear(Operator):
                      and x2.dtype == torch.float32 and dy2.dtype == torch.float32)
             if first:
                 F.gemm(x2, dy2, ta=True, out=tgt, beta=0.0, colsum_b=tb if fuse_db else None)
-                OVERWRITE_FIRST.add(wid)
+                OVERWRITE_FIRST.add(self.params[1])
             else:
-                if empty and wid in OVERWRITE_FIRST:  # its slice was not zeroed by a lazy zero_grad
+                if empty and self.params[1] in OVERWRITE_FIRST:  # its slice was not zeroed by a lazy zero_grad
                     G.zero_(tgt)
-                    OVERWRITE_FIRST.discard(wid)
+                    OVERWRITE_FIRST.discard(self.params[1])
                 F.gemm_tn_acc(x2, dy2, tgt, colsum_b=tb if fuse_db else None)
             _WGRAD_EPOCH[wid] = GRAD_EPOCH[0]
             dw = ACCUMULATED

@@ -200,7 +200,7 @@ class ParamStore:
         params whose gradient producer overwrites them on its first write
         (autograd.OVERWRITE_FIRST) -- one launch zeroes the rest; the caller
         then runs :meth:`fix_unwritten` after the backward."""
-        ow = [i for i, p in enumerate(self.params) if id(p) in autograd.OVERWRITE_FIRST] if lazy else []
+        ow = [i for i, p in enumerate(self.params) if p in autograd.OVERWRITE_FIRST] if lazy else []
         key = tuple(ow)
         if ow and self.gpu and getattr(self, "_zr_key", None) != key and N.lib().rt.is_capturing(N.stream()):
             ow = []  # (no host->device table upload inside a graph capture: clear everything)
@@ -227,7 +227,7 @@ class ParamStore:
         """Zero the gradients a lazy :meth:`zero_grad` left alone that this
         epoch's backward did not write (e.g. a branch that did not run)."""
         for p in self.params:
-            if (id(p) in autograd.OVERWRITE_FIRST
+            if (p in autograd.OVERWRITE_FIRST
                     and autograd._WGRAD_EPOCH.get(id(p)) != autograd.GRAD_EPOCH[0]):
                 G.zero_(p.grad_view)
 
