@@ -462,7 +462,19 @@ __global__ void __launch_bounds__(NT, 2) ggemm_k(const Args p) {
     }
   }
 
-  if (do_cs && n0 + (int)threadIdx.x % BN < p.N) atomicAdd(p.csum + n0 + threadIdx.x % BN, cs_acc);
+  if (do_cs) {  // (workgroup-uniform) the CS_G partials of a column in a fixed order, one atomic per column
+    float* red = (float*)smem;
+    __syncthreads();  // every wave done with the last stage
+    red[threadIdx.x] = cs_acc;
+    __syncthreads();
+    if ((int)threadIdx.x < BN && n0 + (int)threadIdx.x < p.N) {
+      float sum = 0.f;
+#pragma unroll
+      for (int g = 0; g < CS_G; ++g) sum += red[g * BN + threadIdx.x];
+      atomicAdd(p.csum + n0 + threadIdx.x, sum);
+    }
+    __syncthreads();  // the epilogue may reuse the LDS
+  }
 
   // Epilogue: 16x16 blocks acc[i][j][r] = C[m = .. + (l & 15)][n = .. + 4 (l >> 4) + r];
   // 32x32 blocks acc[i][j][4 g + r] = C[m = .. + (l & 31)][n = .. + 8 g + 4 (l >> 5) + r]
@@ -739,6 +751,7 @@ static bool aligned(const void* p, int64_t a, int64_t b = 0, int64_t c = 0) {
 using namespace sg::gg;
 
 extern "C" {
+int sg_bn_deterministic();
 
 void sg_ggemm_tune(int key, int value) {
   if (key >= 0 && key < 2) g_gg[key] = value;
@@ -775,6 +788,7 @@ void sg_ggemm(int dt, const void* a, int64_t lda, int a_kouter, int64_t sa, cons
     int sp = 1;
     pick_f32(M, N, K, batch, can_split, out_mode == O_F32 && beta == 0.f, tile, sp);
     if (g_gg[0] > 0) tile = g_gg[0];
+    if (sg_bn_deterministic()) sp = 1;  // split-K atomics add in arbitrary order
     if (g_gg[1] != 0) sp = g_gg[1] > 1 && K >= 2 * BK * g_gg[1] ? g_gg[1] : 1;
     if (out_mode == O_F32_ATOMIC && splits > 0) sp = splits;  // caller's explicit count
     if (!can_split) sp = 1;
