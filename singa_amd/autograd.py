@@ -652,7 +652,8 @@ class Linear(Operator):
         super().__init__(name)
         self.has_bias = has_bias
         self.act = act
-        self.y2 = None
+        self.y2 = None  # the activation output (y-form derivatives) ...
+        self.z2 = None  # ... or its input (GELU), written by the forward epilogue
         self.preact_done = False
 
     def forward(self, x, W, b=None):
@@ -660,17 +661,22 @@ class Linear(Operator):
         lead = x.shape[:-1]
         x2 = G.reshape(x, (-1, x.shape[-1]))
         bias = G.to(b, torch.float32) if b is not None else None
-        y = F.matmul(x2, w, out_dtype=x.dtype, bias=bias, act=self.act)
+        z = None
+        if self.act in F.ACT_XFORM and self.requires_grad:
+            z = _mem.empty((x2.shape[0], w.shape[-1]), dtype=x.dtype, device=x2.device)
+        y = F.matmul(x2, w, out_dtype=x.dtype, bias=bias, act=self.act, act_aux=z)
         if self.requires_grad:
             self.x2, self.w = x2, w
             self.y2 = y if self.act is not None else None
+            self.z2 = z
         return G.reshape(y, (*lead, y.shape[-1]))
 
     def _producer_act(self, x2):
-        """(act, y) of the fused Linear whose output is this op's input and
+        """The fused-activation Linear whose output is this op's input and
         whose gradient comes from this op alone, else None."""
         src = self.src[0][0] if self.src else None
         if not (isinstance(src, Linear) and src.act is not None and src.y2 is not None
+                and (src.act not in F.ACT_XFORM or src.z2 is not None)
                 and getattr(self, "sole", {}).get(0, False)):
             return None
         y = src.y2
@@ -687,17 +693,24 @@ class Linear(Operator):
         return G.to(W, x.dtype)
 
     def backward(self, dy):
-        x2, w, y2 = self.x2, self.w, self.y2
+        x2, w, y2, z2 = self.x2, self.w, self.y2, self.z2
         self.x2 = self.w = self.y2 = None
         dy2 = G.contiguous(G.reshape(dy, (-1, dy.shape[-1])))
         if self.act is not None and not self.preact_done:
-            dy2 = F.relu_bwd_from_y(y2, dy2) if self.act == "relu" else F.unary_bwd(self.act, None, y2, dy2)
+            if self.act == "relu":
+                dy2 = F.relu_bwd_from_y(y2, dy2)
+            elif self.act in F.ACT_XFORM:
+                dy2 = F.unary_bwd(self.act, z2, None, dy2)
+            else:
+                dy2 = F.unary_bwd(self.act, None, y2, dy2)
         self.preact_done = False
+        self.z2 = None
         dx = None
         if self.needs_grad(0):
             prod = self._producer_act(x2)
             if prod is not None:
-                dx = F.gemm_nt(dy2, w, out_dtype=x2.dtype, act_grad=(prod.act, x2))
+                t = prod.z2 if prod.act in F.ACT_XFORM else x2
+                dx = F.gemm_nt(dy2, w, out_dtype=x2.dtype, act_grad=(prod.act, G.reshape(t, tuple(x2.shape))))
                 prod.preact_done = True
             else:
                 dx = F.gemm_nt(dy2, w, out_dtype=x2.dtype)

@@ -116,8 +116,11 @@ void sg_bn_bwd_wdot(const void*, const void*, const void*, const void*, const vo
                     const void*, const void*, const void*, const void*, void*, void*, void*, void*, void*, void*,
                     int64_t, int, float, hipStream_t);
 void sg_ggemm(int, const void*, int64_t, int, int64_t, const void*, int64_t, int, int64_t, void*, int64_t, int64_t,
-              int, int, int, float, float, const void*, int, int, int, int, float*, int, const void*, hipStream_t);
+              int, int, int, float, float, const void*, int, int, int, int, float*, int, const void*, void*,
+              hipStream_t);
 void sg_ggemm_tune(int, int);
+int sg_gemm_act(const void*, int64_t, int, const void*, int64_t, int, void*, int64_t, int, int, int, float, const void*,
+                int, int64_t, int64_t, int64_t, int, void*, int, const void*, hipStream_t);
 void sg_gconv_fwd(int, const void*, const void*, void*, const void*, int, int, int, int, int, int, int, int, int, int,
                   int, int, int, int, int, int, int, int, hipStream_t);
 void sg_gconv_dgrad(int, const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int,
@@ -440,12 +443,20 @@ PYBIND11_MODULE(_C, m) {
   // generic MFMA GEMM / conv (csrc/kernels/ggemm.hip): dt 0 = fp32 operands (exact f32 MFMA), 1 = bf16
   m.def("ggemm", [](int dt, P a, int64_t lda, int ako, int64_t sa, P b, int64_t ldb, int bko, int64_t sb, P c,
                     int64_t ldc, int64_t sc, int M, int N, int K, float alpha, float beta, P bias, int relu,
-                    int out_mode, int splits, int batch, P csum, int act_bwd, P act_x, P s) {
+                    int out_mode, int splits, int batch, P csum, int act_bwd, P act_x, P aux, P s) {
     sg_ggemm(dt, CV(a), lda, ako, sa, CV(b), ldb, bko, sb, V(c), ldc, sc, M, N, K, alpha, beta, CV(bias), relu,
-             out_mode, splits, batch, (float*)V(csum), act_bwd, CV(act_x), S(s));
+             out_mode, splits, batch, (float*)V(csum), act_bwd, CV(act_x), V(aux), S(s));
     CHK("ggemm");
   });
   m.def("ggemm_tune", [](int key, int value) { sg_ggemm_tune(key, value); });
+  m.def("gemm_act", [](P a, int64_t lda, int ako, P b, int64_t ldb, int bko, P c, int64_t ldc, int M, int N, int K,
+                       float alpha, P bias, int batch, int64_t sa, int64_t sb, int64_t sc, int act, P aux, int act_bwd,
+                       P act_x, P s) {
+    const int r = sg_gemm_act(CV(a), lda, ako, CV(b), ldb, bko, V(c), ldc, M, N, K, alpha, CV(bias), batch, sa, sb, sc,
+                              act, V(aux), act_bwd, CV(act_x), S(s));
+    CHK("gemm_act");
+    return r;
+  });
   m.def("gconv_fwd", [](int dt, P x, P w, P y, P bias, int N, int H, int W, int C, int K, int R, int Sd, int Ho,
                         int Wo, int sh, int sw, int ph, int pw, int dh, int dw, int groups, int relu, int out_mode,
                         P s) {

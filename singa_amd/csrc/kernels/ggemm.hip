@@ -83,12 +83,15 @@ struct Args {
   float* csum;       // optional: csum[n] += sum_k B(n, k) (the bias gradient of a weight-gradient GEMM)
   const void* act_x; // optional: C[m][n] *= act'(X[m][n]), X the activation OUTPUT laid out like C (ldc)
   int act_bwd;       // activation of act_x (Act codes)
+  void* aux;         // optional: the pre-activation z of a fused activation (laid out like C)
   Geom g;
 };
 
 // fused activations (the relu field of Args; act_bwd): codes 0 none, 1 relu,
-// 2 sigmoid, 3 tanh, 4 stanh -- the same formulas as elementwise.hip's
-// unary_f / unary_b (output-form derivatives)
+// 2 sigmoid, 3 tanh, 4 stanh -- the formulas of elementwise.hip's unary_f /
+// unary_b, derivatives from the activation's output.  (The GELUs, codes 5 / 6,
+// live in the tuned bf16 kernel's epilogue only: inlined into every
+// instantiation here they doubled this file's code.)
 enum Act : int { A_NONE = 0, A_RELU = 1, A_SIGMOID = 2, A_TANH = 3, A_STANH = 4 };
 __device__ __forceinline__ float act_f(int a, float v) {
   switch (a) {
@@ -99,12 +102,12 @@ __device__ __forceinline__ float act_f(int a, float v) {
     default: return v;
   }
 }
-__device__ __forceinline__ float dact_y(int a, float y) {
+__device__ __forceinline__ float dact_y(int a, float t) {
   switch (a) {
-    case A_RELU: return y > 0.f ? 1.f : 0.f;
-    case A_SIGMOID: return y * (1.f - y);
-    case A_TANH: return 1.f - y * y;
-    case A_STANH: return 0.66666667f * 1.7159047f - 0.66666667f / 1.7159047f * y * y;
+    case A_RELU: return t > 0.f ? 1.f : 0.f;
+    case A_SIGMOID: return t * (1.f - t);
+    case A_TANH: return 1.f - t * t;
+    case A_STANH: return 0.66666667f * 1.7159047f - 0.66666667f / 1.7159047f * t * t;
     default: return 1.f;
   }
 }
@@ -546,6 +549,15 @@ __global__ void __launch_bounds__(NT, 2) ggemm_k(const Args p) {
         for (int r = 0; r < 4; ++r)
           if (full || n + r < p.N) v[r] += p.beta * c[r];
       }
+      if (p.aux) {
+        float* z = (float*)p.aux + y * p.sc + rowoff + n;
+        if (vst) *(float4*)z = make_float4(v[0], v[1], v[2], v[3]);
+        else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (n + r < p.N) z[r] = v[r];
+        }
+      }
       if (p.relu) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = act_f(p.relu, v[r]);
@@ -563,6 +575,14 @@ __global__ void __launch_bounds__(NT, 2) ggemm_k(const Args p) {
 #pragma unroll
         for (int r = 0; r < 4; ++r)
           if (full || n + r < p.N) v[r] += p.beta * (float)c[r];
+      }
+      if (p.aux) {  // z rounded as a separate pass would see it
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bf16 zb = (bf16)v[r];
+          if (n + r < p.N) ((bf16*)p.aux + y * p.sc + rowoff + n)[r] = zb;
+          v[r] = (float)zb;
+        }
       }
       if (p.relu) {
 #pragma unroll
@@ -770,7 +790,7 @@ void sg_ggemm_tune(int key, int value) {
 void sg_ggemm(int dt, const void* a, int64_t lda, int a_kouter, int64_t sa, const void* b, int64_t ldb, int b_kouter,
               int64_t sb, void* c, int64_t ldc, int64_t sc, int M, int N, int K, float alpha, float beta,
               const void* bias, int relu, int out_mode, int splits, int batch, float* csum, int act_bwd,
-              const void* act_x, hipStream_t s) {
+              const void* act_x, void* aux, hipStream_t s) {
   if (M <= 0 || N <= 0 || batch <= 0) return;
   if (csum && batch != 1) throw std::runtime_error("ggemm: fused column sums need batch 1");
   check_int((int64_t)M * N, "M*N");
@@ -778,12 +798,12 @@ void sg_ggemm(int dt, const void* a, int64_t lda, int a_kouter, int64_t sa, cons
   p.M = M; p.N = N; p.K = K;
   p.a = a; p.lda = lda; p.sa = sa; p.b = b; p.ldb = ldb; p.sb = sb;
   p.c = c; p.ldc = ldc; p.sc = sc; p.alpha = alpha; p.beta = beta; p.bias = (const float*)bias; p.sbias = 0;
-  p.relu = relu; p.out_mode = out_mode; p.csum = csum; p.act_x = act_x; p.act_bwd = act_bwd;
+  p.relu = relu; p.out_mode = out_mode; p.csum = csum; p.act_x = act_x; p.act_bwd = act_bwd; p.aux = aux;
   const bool f = dt == 0;
   int tile = 0;
   if (f) {
     // plain fp32 output split over K: C zeroed (beta 0) or kept (beta 1) and accumulated atomically
-    const bool plain_ok = out_mode == O_F32 && !relu && !act_x && (beta == 0.f || beta == 1.f);
+    const bool plain_ok = out_mode == O_F32 && !relu && !act_x && !aux && (beta == 0.f || beta == 1.f);
     const bool can_split = out_mode == O_F32_ATOMIC || plain_ok;
     int sp = 1;
     pick_f32(M, N, K, batch, can_split, out_mode == O_F32 && beta == 0.f, tile, sp);

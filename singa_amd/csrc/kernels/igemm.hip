@@ -116,8 +116,48 @@ struct GemmArgs {
   const uint8_t* bnb_mask;
   const bf16* bnb_x;
   const float *bnb_mean, *bnb_invstd, *bnb_scale, *bnb_shift;
+  // fused activation of the bf16 output (LDS-staged epilogue, host-checked):
+  // codes 1 relu, 2 sigmoid, 3 tanh, 4 stanh, 5 gelu (erf), 6 gelu (tanh);
+  // aux (optional): the pre-activation z (bf16, laid out like C)
+  int act;
+  bf16* aux;
+  // fused activation backward: out = bf16(out) * act'(act_x), act_x the
+  // activation's output (codes 1-4) or its input z (5, 6), laid out like C
+  // (beta == 0: it is read up front in place of the accumulate source)
+  const bf16* act_x;
+  int act_bwd;
   ConvGeom g;
 };
+
+// the fused activations: the formulas of elementwise.hip's unary_f / unary_b,
+// so a fused epilogue rounds exactly like the separate kernels did
+__device__ __forceinline__ float ep_act(int a, float x) {
+  switch (a) {
+    case 1: return fmaxf(x, 0.f);
+    case 2: return 1.f / (1.f + __expf(-x));
+    case 3: return tanhf(x);
+    case 4: return 1.7159047f * tanhf(0.66666667f * x);
+    case 5: return 0.5f * x * (1.f + erff(x * 0.70710678118f));
+    case 6: return 0.5f * x * (1.f + tanhf(0.7978845608f * (x + 0.044715f * x * x * x)));
+    default: return x;
+  }
+}
+// derivative from the output y (codes 1-4) or the input x (5, 6)
+__device__ __forceinline__ float ep_dact(int a, float t) {
+  switch (a) {
+    case 1: return t > 0.f ? 1.f : 0.f;
+    case 2: return t * (1.f - t);
+    case 3: return 1.f - t * t;
+    case 4: return 0.66666667f * 1.7159047f - 0.66666667f / 1.7159047f * t * t;
+    case 5: return 0.5f * (1.f + erff(t * 0.70710678118f)) + t * 0.3989422804f * __expf(-0.5f * t * t);
+    case 6: {
+      const float u = 0.7978845608f * (t + 0.044715f * t * t * t), th = tanhf(u);
+      const float du = 0.7978845608f * (1.f + 3.f * 0.044715f * t * t);
+      return 0.5f * (1.f + th) + 0.5f * t * (1.f - th * th) * du;
+    }
+    default: return 1.f;
+  }
+}
 
 __device__ __forceinline__ int kmajor_swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 template <int ROWS>
@@ -519,7 +559,10 @@ __device__ __forceinline__ void raw_barrier() {
 // K-tile starts with a COUNTED vmcnt (this wave's DMA for the tile retired,
 // the younger tiles still in flight) and a raw barrier (every wave's DMA
 // retired, every wave done reading the stage about to be refilled).
-template <int BM, int BN, int AM, int BMODE, int OUT, int NTH = NT, int WM = 2, int WN = 2, int STAGES = 2>
+// FLAGS bit 0: the fused-activation epilogue (sg_gemm_act) -- a separate
+// instantiation, so every other kernel compiles exactly as without it
+template <int BM, int BN, int AM, int BMODE, int OUT, int NTH = NT, int WM = 2, int WN = 2, int STAGES = 2,
+          int FLAGS = 0>
 __global__ void __launch_bounds__(NTH, STAGES == 1 ? 3 : (NTH == 512 && STAGES == 2 && BM * BN <= 128 * 128) ? 4 : 2)
     igemm_k(const GemmArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -773,7 +816,7 @@ __global__ void __launch_bounds__(NTH, STAGES == 1 ? 3 : (NTH == 512 && STAGES =
 constexpr int PP_HALF = 128 * BK * 2;  // one half-tile image (16 KB)
 constexpr int PP_BUF = 4 * PP_HALF;    // one K-tile (64 KB)
 
-template <int OUT>
+template <int OUT, int FLAGS = 0>
 __global__ void __launch_bounds__(512, 2) pp_gemm_k(const GemmArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int BM = 256, BN = 256;
@@ -1283,7 +1326,8 @@ static thread_local const uint8_t* g_res_mask = nullptr;
 
 constexpr int stages_c(int BM, int BN, int STAGES) { return STAGES * (BM + BN) * BK * 2; }
 
-template <int BM, int BN, int AM, int BMODE, int OUT, int NTH = NT, int WM = 2, int WN = 2, int STAGES = 2>
+template <int BM, int BN, int AM, int BMODE, int OUT, int NTH = NT, int WM = 2, int WN = 2, int STAGES = 2,
+          int FLAGS = 0>
 static void launch_t(const GemmArgs& p_in, int tiles, int ydim, int zdim, hipStream_t s) {
   GemmArgs p = p_in;
   p.lds_epilogue = g_tune[1];
@@ -1301,7 +1345,7 @@ static void launch_t(const GemmArgs& p_in, int tiles, int ydim, int zdim, hipStr
                 "single-stage variant: bf16 output only");
   constexpr int lds = stages > etile ? stages : etile;
   static_assert(lds <= 160 * 1024, "LDS budget");
-  auto* kern = igemm_k<BM, BN, AM, BMODE, OUT, NTH, WM, WN, STAGES>;
+  auto* kern = igemm_k<BM, BN, AM, BMODE, OUT, NTH, WM, WN, STAGES, FLAGS>;
   if constexpr (lds > 65536) {
     static bool attr = [kern] {
       return hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
@@ -1311,13 +1355,13 @@ static void launch_t(const GemmArgs& p_in, int tiles, int ydim, int zdim, hipStr
   hipLaunchKernelGGL(kern, grid, block, lds, s, p);
 }
 
-template <int OUT>
+template <int OUT, int FLAGS = 0>
 static void launch_pp(const GemmArgs& p_in, int tiles, int ydim, hipStream_t s) {
   GemmArgs p = p_in;
   p.lds_epilogue = g_tune[1];
   p.nt_store = g_tune[8];
   constexpr int lds = 2 * PP_BUF;
-  auto* kern = pp_gemm_k<OUT>;
+  auto* kern = pp_gemm_k<OUT, FLAGS>;
   static bool attr = [kern] {
     return hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
   }();
@@ -1415,14 +1459,14 @@ static void pick_wgrad(int M, int N, int K, int mode, int& BM, int& BN, int& spl
   while (tiles * splits < target && (splits * 2) * min_kt <= nkt) splits *= 2;
 }
 
-template <int AM, int BMODE, int OUT>
+template <int AM, int BMODE, int OUT, int FLAGS = 0>
 static void launch(const GemmArgs& p, int M, int splits, hipStream_t s, int batch, int zdim) {
   int BM, BN;
   if constexpr (OUT != OUT_F32_ATOMIC) {
     {
       const int z = zdim > 0 ? zdim : 1;
       // persistent short-K kernel (knob 9): 1x1-conv forward / data-gradient shapes
-      if (OUT == OUT_BF16 && AM == LM_KMAJOR && BMODE == LM_KMAJOR && g_tune[9] && g_tune[4] == 0 &&
+      if (FLAGS == 0 && OUT == OUT_BF16 && AM == LM_KMAJOR && BMODE == LM_KMAJOR && g_tune[9] && g_tune[4] == 0 &&
           !p.out_phase && zdim <= 1 && batch == 1 && p.K <= 128 && (p.N & 127) == 0 && !p.bias && !p.relu &&
           p.alpha == 1.f && p.stats_mode == 0 && !(p.stats && p.stats_det) && g_tune[1] && !p.res_g &&
           (p.ldc & 7) == 0 && (long)((M + 127) / 128) * (p.N / 128) >= 2048) {
@@ -1435,7 +1479,7 @@ static void launch(const GemmArgs& p, int M, int splits, hipStream_t s, int batc
           (p.K + BK - 1) / BK <= g_tune[6] && p.N >= 128 && !((p.N % 128) != 0 && (p.N % 128) <= 64) &&
           (long)((M + 127) / 128) * ((p.N + 127) / 128) >= 1024) {
         const int tiles = ((M + 127) / 128) * ((p.N + 127) / 128);
-        launch_t<128, 128, AM, BMODE, OUT_BF16, 256, 2, 2, 1>(p, tiles, batch, z, s);
+        launch_t<128, 128, AM, BMODE, OUT_BF16, 256, 2, 2, 1, FLAGS>(p, tiles, batch, z, s);
         return;
       }
       int big = pick_big(M, p.N);
@@ -1451,24 +1495,24 @@ static void launch(const GemmArgs& p, int M, int splits, hipStream_t s, int batc
         big = 4;
       if (big == 4) {
         if (pp_ok) {
-          launch_pp<OUT>(p, ((M + 255) / 256) * ((p.N + 255) / 256), batch, s);
+          launch_pp<OUT, FLAGS>(p, ((M + 255) / 256) * ((p.N + 255) / 256), batch, s);
           return;
         }
         big = 1;
       }
       if (big == 1) {
         const int tiles = ((M + 127) / 128) * ((p.N + 127) / 128);
-        launch_t<128, 128, AM, BMODE, OUT, 512, 2, 4, 2>(p, tiles, batch, z, s);
+        launch_t<128, 128, AM, BMODE, OUT, 512, 2, 4, 2, FLAGS>(p, tiles, batch, z, s);
         return;
       }
       if (big == 2) {
         const int tiles = ((M + 255) / 256) * ((p.N + 63) / 64);
-        launch_t<256, 64, AM, BMODE, OUT, 512, 4, 2, 4>(p, tiles, batch, z, s);
+        launch_t<256, 64, AM, BMODE, OUT, 512, 4, 2, 4, FLAGS>(p, tiles, batch, z, s);
         return;
       }
       if (big == 3) {
         const int tiles = ((M + 255) / 256) * ((p.N + 127) / 128);
-        launch_t<256, 128, AM, BMODE, OUT, 512, 4, 2, 3>(p, tiles, batch, z, s);
+        launch_t<256, 128, AM, BMODE, OUT, 512, 4, 2, 3, FLAGS>(p, tiles, batch, z, s);
         return;
       }
     }
@@ -1480,10 +1524,10 @@ static void launch(const GemmArgs& p, int M, int splits, hipStream_t s, int batc
   }
   const int tiles = ((M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
   const int z = zdim > 0 ? zdim : splits;
-  if (BM == 128 && BN == 128) launch_t<128, 128, AM, BMODE, OUT>(p, tiles, batch, z, s);
-  else if (BM == 128 && BN == 64) launch_t<128, 64, AM, BMODE, OUT>(p, tiles, batch, z, s);
-  else if (BM == 64 && BN == 128) launch_t<64, 128, AM, BMODE, OUT>(p, tiles, batch, z, s);
-  else launch_t<64, 64, AM, BMODE, OUT>(p, tiles, batch, z, s);
+  if (BM == 128 && BN == 128) launch_t<128, 128, AM, BMODE, OUT, NT, 2, 2, 2, FLAGS>(p, tiles, batch, z, s);
+  else if (BM == 128 && BN == 64) launch_t<128, 64, AM, BMODE, OUT, NT, 2, 2, 2, FLAGS>(p, tiles, batch, z, s);
+  else if (BM == 64 && BN == 128) launch_t<64, 128, AM, BMODE, OUT, NT, 2, 2, 2, FLAGS>(p, tiles, batch, z, s);
+  else launch_t<64, 64, AM, BMODE, OUT, NT, 2, 2, 2, FLAGS>(p, tiles, batch, z, s);
 }
 
 static int pick_splits(int M, int N, int K, int want) {
@@ -1527,6 +1571,32 @@ void sg_gemm(const void* a, int64_t lda, int a_kouter, const void* b, int64_t ld
              int splits, int batch, int64_t sa, int64_t sb, int64_t sc, hipStream_t s) {
   sg_gemm_heads(a, lda, a_kouter, b, ldb, b_kouter, c, ldc, M, N, K, alpha, beta, bias, relu, out_mode, splits,
                 batch, sa, sb, sc, 0, 0, 0, 0, s);
+}
+
+// sg_gemm with a fused activation (bf16 output through the LDS-staged
+// epilogue): act (codes in GemmArgs) with the pre-activation also written to
+// aux when given, or act_bwd: out *= act'(act_x).  Returns 0 (nothing
+// launched) when the shape cannot take the staged epilogue.
+int sg_gemm_act(const void* a, int64_t lda, int a_kouter, const void* b, int64_t ldb, int b_kouter, void* c,
+                int64_t ldc, int M, int N, int K, float alpha, const void* bias, int batch, int64_t sa, int64_t sb,
+                int64_t sc, int act, void* aux, int act_bwd, const void* act_x, hipStream_t s) {
+  if ((N & 7) != 0 || (ldc & 7) != 0 || !g_tune[1] || g_tune[4] != 0 || (act == 0) == (act_x == nullptr) ||
+      M <= 0 || K <= 0 || batch != 1)
+    return 0;
+  GemmArgs p{};
+  init_phase_identity(p.g);
+  p.sa = sa; p.sb = sb; p.sc = sc;
+  p.M = M; p.N = N; p.K = K; p.a = (const bf16*)a; p.lda = lda; p.b = (const bf16*)b; p.ldb = ldb;
+  p.c = c; p.ldc = ldc; p.alpha = alpha; p.beta = 0.f; p.bias = (const float*)bias; p.relu = 0;
+  p.act = act; p.aux = (bf16*)aux; p.act_x = (const bf16*)act_x; p.act_bwd = act_bwd;
+  p.k_per_split = kps(K, 1);
+  p.a_bytes = extent_bytes(a_kouter ? (int64_t)(K - 1) * lda + M : (int64_t)(M - 1) * lda + K);
+  p.b_bytes = extent_bytes(b_kouter ? (int64_t)(K - 1) * ldb + N : (int64_t)(N - 1) * ldb + K);
+  if (!a_kouter && !b_kouter) launch<LM_KMAJOR, LM_KMAJOR, OUT_BF16, 1>(p, M, 1, s, batch, 0);
+  else if (!a_kouter && b_kouter) launch<LM_KMAJOR, LM_KOUTER, OUT_BF16, 1>(p, M, 1, s, batch, 0);
+  else if (a_kouter && !b_kouter) launch<LM_KOUTER, LM_KMAJOR, OUT_BF16, 1>(p, M, 1, s, batch, 0);
+  else launch<LM_KOUTER, LM_KOUTER, OUT_BF16, 1>(p, M, 1, s, batch, 0);
+  return 1;
 }
 
 // sg_gemm with a two-level batch: batch index y -> (y / bh, y % bh) with

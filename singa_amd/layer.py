@@ -169,8 +169,9 @@ def _new_param(shape, dev, dtype=torch.float32) -> Tensor:
 
 class Linear(Layer):
     """y = act(x W + b), W [in, out].  ``activation`` (relu / sigmoid / tanh /
-    stanh, default none) is applied in the GEMM epilogue, and its backward in
-    the next fused Linear's data-gradient epilogue (see autograd.Linear)."""
+    stanh / gelu / gelu_tanh, default none) is applied in the GEMM epilogue,
+    and its backward in the next fused Linear's data-gradient epilogue (see
+    autograd.Linear)."""
 
     def __init__(self, out_features: int, *args, bias: bool = True, activation: Optional[str] = None, **kwargs):
         super().__init__()
@@ -182,7 +183,7 @@ class Linear(Layer):
                 bias = args[1]
         self.out_features = out_features
         self.bias = bias
-        if activation is not None and activation not in ("relu", "sigmoid", "tanh", "stanh"):
+        if activation is not None and activation not in ("relu", "sigmoid", "tanh", "stanh", "gelu", "gelu_tanh"):
             raise ValueError(f"Linear: unsupported fused activation {activation}")
         self.activation = activation
 

@@ -10,6 +10,8 @@ in the flat ParamStore.
 """
 from __future__ import annotations
 
+import os
+
 import math
 from typing import Optional
 
@@ -75,14 +77,21 @@ class MergeHeads(autograd.Operator):
 
 
 class EncoderLayer(layer.Layer):
-    def __init__(self, hidden: int, heads: int, ffn: int, dropout: float = 0.1):
+    def __init__(self, hidden: int, heads: int, ffn: int, dropout: float = 0.1, fuse_gelu: Optional[bool] = None):
         super().__init__()
+        if fuse_gelu is None:
+            fuse_gelu = os.environ.get("SINGA_AMD_FUSE_GELU", "0") != "0"
         self.heads = heads
         self.qkv = layer.Linear(3 * hidden)
         self.proj = layer.Linear(hidden)
         self.ln1 = layer.LayerNorm(1e-12)
-        self.fc1 = layer.Linear(ffn)
-        self.act = layer.Gelu()
+        # fuse_gelu (SINGA_AMD_FUSE_GELU=1): GELU in fc1's GEMM epilogue (forward)
+        # and fc2's data-gradient epilogue (backward).  Off by default: measured
+        # neutral-to-slower (3373-3381 vs 3383-3384 seq/s, sonnx 3240-3242 vs
+        # 3245-3254, profiles/r4/ab_gelu_fusion.jsonl) -- the erf in the epilogue
+        # is exposed work there, hidden behind memory in the separate kernel
+        self.fc1 = layer.Linear(ffn, activation="gelu" if fuse_gelu else None)
+        self.act = layer.Identity() if fuse_gelu else layer.Gelu()
         self.fc2 = layer.Linear(hidden)
         self.ln2 = layer.LayerNorm(1e-12)
         self.drop1 = layer.Dropout(dropout)

@@ -563,60 +563,57 @@ def _igemm_ok(a, lda, ako, b, ldb, bko, M, Nn, K, sa, sb) -> bool:
     return True
 
 
-GEMM_ACT = {"relu": 1, "sigmoid": 2, "tanh": 3, "stanh": 4}  # ggemm.hip Act codes
+GEMM_ACT = {"relu": 1, "sigmoid": 2, "tanh": 3, "stanh": 4, "gelu": 5, "gelu_tanh": 6}  # epilogue Act codes
+ACT_XFORM = {"gelu", "gelu_tanh"}  # derivative from the activation's input z (the others: from its output)
 
 
 def gemm(a: torch.Tensor, b: torch.Tensor, ta: bool = False, tb: bool = False, out: Optional[torch.Tensor] = None,
          out_dtype: Optional[torch.dtype] = None, alpha: float = 1.0, beta: float = 0.0,
          bias: Optional[torch.Tensor] = None, relu: bool = False, accumulate: bool = False,
          colsum_b: Optional[torch.Tensor] = None, act: Optional[str] = None,
-         act_grad: Optional[Tuple[str, torch.Tensor]] = None) -> torch.Tensor:
+         act_grad: Optional[Tuple[str, torch.Tensor]] = None, act_aux: Optional[torch.Tensor] = None) -> torch.Tensor:
     """C = alpha * op(a) @ op(b) (+ beta * C) (+ bias[n]) (ReLU), op(t) = t.T if
     the flag is set.  2-D or batched 3-D operands (equal batch, or one side
     2-D and shared).  ``accumulate``: C (fp32 ``out``) += alpha * op(a) op(b)
     (split-K atomics).  ``colsum_b`` (fp32 [N], 2-D operands): += the column
     sums of op(b) -- a weight-gradient GEMM's bias gradient, summed by the
     generic kernel from the tiles it stages anyway.  ``act`` (relu / sigmoid
-    / tanh / stanh): activation of the output; ``act_grad`` = (act, y): C *=
-    act'(y) with y that activation's output, laid out like C (a data-gradient
-    GEMM taking its producer's activation backward).  Both run in the fp32
-    kernel's epilogue; other paths apply them in a separate pass.  On the
+    / tanh / stanh / gelu / gelu_tanh): activation of the output, with the
+    pre-activation written to ``act_aux`` when given; ``act_grad`` = (act, t):
+    C *= act'(t), t that activation's output (or, for the gelus, its input)
+    laid out like C -- a data-gradient GEMM taking its producer's activation
+    backward.  Both run in the GEMM epilogues on the GPU (rounded exactly as
+    the separate elementwise kernels would); the host applies them in a
+    separate pass.  On the
     GPU: bf16 operands of aligned shapes run the tuned MFMA kernel,
     everything else (fp32 -- exact f32 MFMA -- and ragged bf16) the generic
     one; there is no vendor-BLAS path."""
     if colsum_b is not None and (a.dim() != 2 or b.dim() != 2):
         raise ValueError("gemm: colsum_b needs 2-D operands")
-    if act == "relu" and act_grad is None:
+    if act == "relu" and act_grad is None and act_aux is None:
         act, relu = None, True
     if act is not None or act_grad is not None:
         if act is not None and act not in GEMM_ACT or act_grad is not None and act_grad[0] not in GEMM_ACT:
             raise ValueError(f"gemm: unsupported fused activation {act or act_grad[0]}")
-        if relu or accumulate:
-            raise ValueError("gemm: act / act_grad exclude relu and accumulate")
-        fused = (a.is_cuda and N.available() and a.dtype == torch.float32 and b.dtype == torch.float32
-                 and (out is None or out.dtype == torch.float32) and (out_dtype in (None, torch.float32)))
+        if relu or accumulate or act is not None and act_grad is not None:
+            raise ValueError("gemm: act / act_grad exclude each other, relu and accumulate")
+        dt = out.dtype if out is not None else (out_dtype or a.dtype)
+        fused = (a.is_cuda and N.available() and a.dtype == b.dtype == dt and dt in (torch.float32, torch.bfloat16)
+                 and beta == 0.0)
         if not fused:
-            c = gemm(a, b, ta, tb, out, out_dtype, alpha, beta, bias, False, False, colsum_b)
-            r = c
-            if act is not None:
-                r = unary(act, r)
-            if act_grad is not None:
-                k, yv = act_grad
-                r = relu_bwd_from_y(yv, r) if k == "relu" else unary_bwd(k, None, yv, r)
-            if r is not c:
-                G.copy_(c, r)
-            return c
-        if act_grad is not None:
-            yv = act_grad[1]
-            if yv.dtype != torch.float32 or not yv.is_contiguous():
-                raise ValueError("gemm: act_grad output must be a dense fp32 tensor")
+            return _gemm_act_unfused(a, b, ta, tb, out, out_dtype, alpha, beta, bias, colsum_b, act, act_grad,
+                                     act_aux)
+        for t in ((act_grad[1] if act_grad is not None else None), act_aux):
+            if t is not None and (t.dtype != dt or not t.is_contiguous()):
+                raise ValueError("gemm: act_grad / act_aux tensors must be dense and of the output dtype")
     if a.dim() == 2 and b.dim() == 2:
         batch = 1
     elif a.dim() == 3 and b.dim() == 2 and not ta and a.is_contiguous() and out is None:
         Bt = a.shape[0]
         ag = (act_grad[0], act_grad[1].reshape(-1, act_grad[1].shape[-1])) if act_grad is not None else None
+        aux = act_aux.reshape(-1, act_aux.shape[-1]) if act_aux is not None else None
         c = gemm(a.reshape(-1, a.shape[-1]), b, False, tb, None, out_dtype, alpha, beta, bias, relu, act=act,
-                 act_grad=ag)
+                 act_grad=ag, act_aux=aux)
         return c.reshape(Bt, a.shape[1], c.shape[-1])
     elif a.dim() == 3 or b.dim() == 3:
         batch = a.shape[0] if a.dim() == 3 else b.shape[0]
@@ -688,12 +685,26 @@ def gemm(a: torch.Tensor, b: torch.Tensor, ta: bool = False, tb: bool = False, o
     bb = G.contiguous(G.to(bias, torch.float32)).reshape(-1) if bias is not None else None
     mode = 2 if accumulate else (0 if out.dtype == torch.bfloat16 else 1)
     L = N.lib()
+    code = GEMM_ACT[act] if act is not None else int(relu)
+    ab, ax = (GEMM_ACT[act_grad[0]], act_grad[1]) if act_grad is not None else (0, None)
+    for t in (ax, act_aux):
+        if t is not None and tuple(t.shape) != tuple(out.shape):
+            raise ValueError(f"gemm: act_grad / act_aux {tuple(t.shape)} != C {tuple(out.shape)}")
     if _igemm_ok(a, lda, ako, b, ldb, bko, M, Nn, K, sa, sb) and (mode == 2 or sc % 8 == 0) and K > 0:
-        L.gemm(a.data_ptr(), lda, int(ako), b.data_ptr(), ldb, int(bko), out.data_ptr(), Nn, M, Nn, K, alpha, beta,
-               N.ptr(bb), int(relu), mode, 0 if mode == 2 else 1, batch, sa, sb, sc, N.stream())
-        if colsum_b is not None:
-            _colsum_opb(b, not bko, colsum_b)
-        return out
+        if act is not None or act_grad is not None:
+            # fused activation: the tuned kernel's LDS-staged epilogue (bf16
+            # output, batch 1, N % 8), else the generic kernel below
+            if mode == 0 and batch == 1 and colsum_b is None and L.gemm_act(
+                    a.data_ptr(), lda, int(ako), b.data_ptr(), ldb, int(bko), out.data_ptr(), Nn, M, Nn, K, alpha,
+                    N.ptr(bb), batch, sa, sb, sc, code if act is not None else 0, N.ptr(act_aux), ab, N.ptr(ax),
+                    N.stream()):
+                return out
+        else:
+            L.gemm(a.data_ptr(), lda, int(ako), b.data_ptr(), ldb, int(bko), out.data_ptr(), Nn, M, Nn, K, alpha,
+                   beta, N.ptr(bb), int(relu), mode, 0 if mode == 2 else 1, batch, sa, sb, sc, N.stream())
+            if colsum_b is not None:
+                _colsum_opb(b, not bko, colsum_b)
+            return out
     if a.dtype not in (torch.float32, torch.bfloat16):
         _no_native(f"gemm ({a.dtype})", a)
     cs = 0
@@ -701,14 +712,33 @@ def gemm(a: torch.Tensor, b: torch.Tensor, ta: bool = False, tb: bool = False, o
         if colsum_b.dtype != torch.float32 or not colsum_b.is_contiguous() or colsum_b.numel() != Nn:
             raise ValueError("gemm: colsum_b must be a dense fp32 [N] tensor")
         cs = colsum_b.data_ptr()
-    code = GEMM_ACT[act] if act is not None else int(relu)
-    ab, ax = (GEMM_ACT[act_grad[0]], act_grad[1]) if act_grad is not None else (0, None)
-    if ax is not None and tuple(ax.shape) != tuple(out.shape):
-        raise ValueError(f"gemm: act_grad output {tuple(ax.shape)} != C {tuple(out.shape)}")
+    if act in ACT_XFORM or act_grad is not None and act_grad[0] in ACT_XFORM:
+        # (the generic kernel's epilogue carries only the y-form activations)
+        return _gemm_act_unfused(a, b, ta, tb, out, None, alpha, beta, bias, colsum_b, act, act_grad, act_aux)
     L.ggemm(0 if a.dtype == torch.float32 else 1, a.data_ptr(), lda, int(ako), sa, b.data_ptr(), ldb, int(bko), sb,
             out.data_ptr(), Nn, sc, M, Nn, K, alpha, beta, N.ptr(bb), code, mode, 0, batch, cs, ab, N.ptr(ax),
-            N.stream())
+            N.ptr(act_aux), N.stream())
     return out
+
+
+def _gemm_act_unfused(a, b, ta, tb, out, out_dtype, alpha, beta, bias, colsum_b, act, act_grad, act_aux):
+    """gemm() followed by the activation (or its derivative) as a separate
+    elementwise pass: the host path, and shapes no fused epilogue takes."""
+    c = gemm(a, b, ta, tb, out, out_dtype, alpha, beta, bias, False, False, colsum_b)
+    r = c
+    if act is not None:
+        if act_aux is not None:
+            G.copy_(act_aux, c)
+        r = unary(act, r)
+    if act_grad is not None:
+        k, t = act_grad
+        if k == "relu":
+            r = relu_bwd_from_y(t, r)
+        else:
+            r = unary_bwd(k, t, None, r) if k in ACT_XFORM else unary_bwd(k, None, t, r)
+    if r is not c:
+        G.copy_(c, r)
+    return c
 
 
 def _colsum_opb(b: torch.Tensor, tb: bool, out: torch.Tensor) -> None:
@@ -722,7 +752,8 @@ def _colsum_opb(b: torch.Tensor, tb: bool, out: torch.Tensor) -> None:
 
 
 def matmul(a: torch.Tensor, b: torch.Tensor, out_dtype: Optional[torch.dtype] = None,
-           bias: Optional[torch.Tensor] = None, relu: bool = False, act: Optional[str] = None) -> torch.Tensor:
+           bias: Optional[torch.Tensor] = None, relu: bool = False, act: Optional[str] = None,
+           act_aux: Optional[torch.Tensor] = None) -> torch.Tensor:
     """C = a @ b for 2-D (or batched 3-D with equal batch) row-major operands.
     bf16 operands run on the MFMA kernel with fp32 accumulation; fp32
     operands on the exact-f32 MFMA kernel (``act``: fused output activation,
@@ -731,13 +762,13 @@ def matmul(a: torch.Tensor, b: torch.Tensor, out_dtype: Optional[torch.dtype] = 
         lead = torch.broadcast_shapes(a.shape[:-2], b.shape[:-2])
         aa = G.reshape(a.expand(*lead, *a.shape[-2:]), (-1, *a.shape[-2:]))
         bb = G.reshape(b.expand(*lead, *b.shape[-2:]), (-1, *b.shape[-2:]))
-        c = gemm(aa, bb, out_dtype=out_dtype or a.dtype, bias=bias, relu=relu, act=act)
+        c = gemm(aa, bb, out_dtype=out_dtype or a.dtype, bias=bias, relu=relu, act=act, act_aux=act_aux)
         return c.reshape(*lead, c.shape[-2], c.shape[-1])
     if a.dim() == 3 and b.dim() == 3 and a.shape[0] != b.shape[0]:
         lead = torch.broadcast_shapes(a.shape[:1], b.shape[:1])
         a = a.expand(*lead, *a.shape[-2:])
         b = b.expand(*lead, *b.shape[-2:])
-    return gemm(a, b, out_dtype=out_dtype or a.dtype, bias=bias, relu=relu, act=act)
+    return gemm(a, b, out_dtype=out_dtype or a.dtype, bias=bias, relu=relu, act=act, act_aux=act_aux)
 
 
 def gemm_nt(a: torch.Tensor, b: torch.Tensor, out_dtype=None, bias=None, relu=False, act_grad=None) -> torch.Tensor:

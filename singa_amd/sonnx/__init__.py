@@ -282,7 +282,11 @@ def _x_linear(c, op, xs, i, o):
         c.add("MatMul", i[:2], [out])
     if act == "stanh":
         _x_stanh(c, op, xs, [out], o)
+    elif act == "gelu":
+        _x_gelu(c, op, xs, [out], o)
     elif act:
+        if act not in ("relu", "sigmoid", "tanh"):
+            raise NotImplementedError(f"sonnx export: Linear with fused {act}")
         c.add({"relu": "Relu", "sigmoid": "Sigmoid", "tanh": "Tanh"}[act], [out], [o[0]])
 
 
@@ -878,6 +882,8 @@ class _Fused:
             return autograd.linear(self._low(rep, xs[0]), xs[1], xs[2])
         if self.kind == "gelu":  # x * 0.5 * (1 + erf(x / sqrt 2)) -> one elementwise kernel
             return autograd.gelu(xs[0])
+        if self.kind == "linear_gelu":  # MatMul + bias Add + GELU chain -> one GEMM, GELU in its epilogue
+            return autograd.linear(self._low(rep, xs[0]), xs[1], xs[2], act="gelu")
         if self.kind == "qkv_attention":  # split-heads + attention + merge-heads -> heads addressed in place
             att = autograd.QKVAttention(self.heads, self.scale)
             qkv = self._low(rep, xs[0])
@@ -912,6 +918,9 @@ def _fusion_plan(nodes, inits: Dict[str, Tensor], consts: set, outputs: Sequence
     is not a graph output, so no other node can observe what it skips.  The
     unfused import runs 2 / 5 / 5-6 autograd ops (and their backward kernels)
     per group, plus an fp32->bf16 cast of every MatMul weight per step.
+
+    A ``linear`` whose output only feeds a ``gelu`` becomes one
+    ``linear_gelu`` (the GELU runs in the GEMM epilogue).
 
     ``gelu_scalars``: untagged one-element initializers the GELU pattern may
     consume as its constants (sqrt 2, 1, 0.5 -- values checked exactly); the
@@ -1104,6 +1113,20 @@ def _fusion_plan(nodes, inits: Dict[str, Tensor], consts: set, outputs: Sequence
                 del plan[key]
                 used.update(big.members)
                 plan[max(big.members)] = big
+    # a Linear whose output feeds only a GELU chain -> one GEMM with the GELU
+    # in its epilogue (and its derivative in the consumer's data gradient)
+    lin_by_out = ({st.output: k for k, st in plan.items() if st.kind == "linear"}
+                  if os.environ.get("SINGA_AMD_FUSE_GELU", "0") != "0" else {})
+    for key, st in list(plan.items()):
+        if st.kind != "gelu":
+            continue
+        x = st.inputs[0]
+        lk = lin_by_out.get(x)
+        if lk is None or x in outs or not set(cons.get(x, [])) <= set(st.members):
+            continue
+        lin = plan.pop(lk)
+        del plan[key]
+        plan[max(st.members)] = _Fused("linear_gelu", tuple(lin.members) + tuple(st.members), lin.inputs, st.output)
     return plan
 
 
@@ -1165,7 +1188,7 @@ class SingaRep:
             fuse = os.environ.get("SINGA_AMD_SONNX_FUSE", "1") != "0"
         self.fused = _fusion_plan(list(g.node), self.inits, self._consts, self.output_names, soft) if fuse else {}
         for st in self.fused.values():
-            if st.kind != "gelu":
+            if st.kind not in ("gelu", "linear_gelu"):
                 continue
             for i in st.members:
                 for nm in g.node[i].input:

@@ -302,3 +302,57 @@ def test_lazy_grad_zero_matches_full_zero(gpu):
     assert n_ow >= 2  # the lazy path was taken
     for k in full:
         assert rel_err(lazy[k], full[k]) < 1e-6, k
+
+
+@pytest.mark.parametrize("act", ["gelu", "gelu_tanh", "stanh"])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+def test_fused_activation_tuned_and_generic(gpu, act, dt):
+    """bf16 (tuned kernel's LDS-staged epilogue) and fp32 GEMMs with a fused
+    activation (+ the pre-activation written to act_aux) and a data-gradient
+    GEMM taking the activation's derivative: equal to the separate
+    elementwise kernels on the same rounded values."""
+    from singa_amd.ops import functional as F
+    x = _rand(256, 192, seed=71).to(gpu).to(dt)
+    w = (_rand(192, 384, seed=72) * 0.1).to(gpu).to(dt)
+    b = _rand(384, seed=73).to(gpu)
+    z = torch.empty(256, 384, device=gpu, dtype=dt)
+    y = F.matmul(x, w, out_dtype=dt, bias=b, act=act, act_aux=z)
+    z_ref = F.matmul(x, w, out_dtype=dt, bias=b)
+    assert rel_err(z, z_ref) < (1e-6 if dt == torch.float32 else 1e-3)
+    y_ref = F.unary(act, z_ref)
+    assert rel_err(y, y_ref) < (1e-6 if dt == torch.float32 else 1e-2)
+    dy, w2 = _rand(256, 128, seed=74).to(gpu).to(dt), (_rand(384, 128, seed=75) * 0.1).to(gpu).to(dt)
+    t = z if act in F.ACT_XFORM else y
+    dz = F.gemm_nt(dy, w2, out_dtype=dt, act_grad=(act, t))
+    dx = F.gemm_nt(dy, w2, out_dtype=dt)
+    dz_ref = F.unary_bwd(act, z, None, dx) if act in F.ACT_XFORM else F.unary_bwd(act, None, y, dx)
+    assert rel_err(dz, dz_ref) < (1e-6 if dt == torch.float32 else 1e-2)
+
+
+def test_bert_layer_fused_gelu_matches_unfused(gpu):
+    """A BERT encoder layer with GELU fused into fc1 / fc2's GEMM epilogues
+    gives the unfused layer's output and weight gradients (bf16 tolerance)."""
+    from singa_amd import autograd, device, tensor
+    from singa_amd.models import bert
+    dev = device.create_rocm_gpu()
+    outs = []
+    for fuse in (False, True):
+        dev.SetRandSeed(11)
+        lay = bert.EncoderLayer(64, 4, 256, dropout=0.0, fuse_gelu=fuse)
+        x = tensor.from_numpy(_rand(2, 16, 64, seed=81).numpy()).to_device(dev)
+        x = tensor.Tensor(data=x.data.bfloat16(), device=dev, requires_grad=False)
+        autograd.training = True
+        try:
+            y = lay(x)
+            dy = tensor.Tensor(data=_rand(*y.shape, seed=82).to(gpu).to(y.data.dtype), device=dev,
+                               requires_grad=False)
+            grads = {id(p): g.data.float().cpu() for p, g in autograd.backward(y, dy)}
+        finally:
+            autograd.training = False
+        ps = lay.get_params()
+        outs.append((y.data.float().cpu(), {k: grads[id(v)] for k, v in ps.items() if id(v) in grads}))
+    (y0, g0), (y1, g1) = outs
+    assert rel_err(y1, y0) < 2e-2
+    assert set(g0) == set(g1) and len(g0) > 6
+    for k in g0:
+        assert rel_err(g1[k], g0[k]) < 3e-2, k

@@ -216,11 +216,15 @@ def test_exported_bert_is_batch_independent():
     np.testing.assert_allclose(out, m.forward(ids5).data.numpy(), atol=1e-4)
 
 
-def test_import_fusion_plan_bert_matches_unfused():
+@pytest.mark.parametrize("fuse_gelu", ["0", "1"])
+def test_import_fusion_plan_bert_matches_unfused(monkeypatch, fuse_gelu):
     """Import-time fusion maps the exported Linear / GELU / attention chains
-    back onto the fused operators; fused and unfused imports give the same
-    outputs and parameter gradients (fp32, CPU)."""
+    back onto the fused operators (with SINGA_AMD_FUSE_GELU=1 a Linear
+    feeding a GELU becomes one GEMM with the GELU epilogue); fused and
+    unfused imports give the same outputs and parameter gradients (fp32,
+    CPU)."""
     from singa_amd.models import bert
+    monkeypatch.setenv("SINGA_AMD_FUSE_GELU", fuse_gelu)
 
     ids = tensor.from_numpy(np.random.RandomState(0).randint(0, 1000, (3, 16)).astype(np.int64))
     y = tensor.from_numpy(np.array([0, 1, 1], np.int32))
@@ -241,7 +245,8 @@ def test_import_fusion_plan_bert_matches_unfused():
         autograd.training = False
         res.append((out.data.clone(), grads))
     # bert_tiny: 2 layers x (qkv, proj, fc1, fc2) + pooler + classifier
-    assert kinds == {"linear": 10, "gelu": 2, "qkv_attention": 2}, kinds
+    want = {"linear": 8, "linear_gelu": 2} if fuse_gelu == "1" else {"linear": 10, "gelu": 2}
+    assert kinds == {**want, "qkv_attention": 2}, kinds
     (o0, g0), (o1, g1) = res
     np.testing.assert_allclose(o1.numpy(), o0.numpy(), atol=1e-5, rtol=1e-5)
     assert set(g0) == set(g1) and len(g0) > 20
