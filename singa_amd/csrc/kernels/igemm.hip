@@ -116,6 +116,8 @@ struct GemmArgs {
   const uint8_t* bnb_mask;
   const bf16* bnb_x;
   const float *bnb_mean, *bnb_invstd, *bnb_scale, *bnb_shift;
+  ConvGeom g;
+  // (kept after g: every other kernel's argument layout is unchanged)
   // fused activation of the bf16 output (LDS-staged epilogue, host-checked):
   // codes 1 relu, 2 sigmoid, 3 tanh, 4 stanh, 5 gelu (erf), 6 gelu (tanh);
   // aux (optional): the pre-activation z (bf16, laid out like C)
@@ -126,7 +128,6 @@ struct GemmArgs {
   // (beta == 0: it is read up front in place of the accumulate source)
   const bf16* act_x;
   int act_bwd;
-  ConvGeom g;
 };
 
 // the fused activations: the formulas of elementwise.hip's unary_f / unary_b,
