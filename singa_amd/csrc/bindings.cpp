@@ -119,6 +119,7 @@ void sg_ggemm(int, const void*, int64_t, int, int64_t, const void*, int64_t, int
               int, int, int, float, float, const void*, int, int, int, int, float*, int, const void*, void*,
               hipStream_t);
 void sg_ggemm_tune(int, int);
+int sg_stem_fwd(const void*, const void*, void*, void*, int, int, int, int, int, hipStream_t);
 int sg_gemm_act(const void*, int64_t, int, const void*, int64_t, int, void*, int64_t, int, int, int, float, const void*,
                 int, int64_t, int64_t, int64_t, int, void*, int, const void*, hipStream_t);
 void sg_gconv_fwd(int, const void*, const void*, void*, const void*, int, int, int, int, int, int, int, int, int, int,
@@ -449,6 +450,12 @@ PYBIND11_MODULE(_C, m) {
     CHK("ggemm");
   });
   m.def("ggemm_tune", [](int key, int value) { sg_ggemm_tune(key, value); });
+  // ImageNet stem forward (csrc/kernels/stem.hip): 1 if taken, 0 = use conv_fwd
+  m.def("stem_fwd", [](P x, P w, P y, P stats, int N, int H, int W, int Ho, int Wo, P s) {
+    const int r = sg_stem_fwd(CV(x), CV(w), V(y), V(stats), N, H, W, Ho, Wo, S(s));
+    CHK("stem_fwd");
+    return r;
+  });
   m.def("gemm_act", [](P a, int64_t lda, int ako, P b, int64_t ldb, int bko, P c, int64_t ldc, int M, int N, int K,
                        float alpha, P bias, int batch, int64_t sa, int64_t sb, int64_t sc, int act, P aux, int act_bwd,
                        P act_x, P s) {

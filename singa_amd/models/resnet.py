@@ -118,9 +118,14 @@ class PairedStemConv(autograd.Operator):
             rows = L.conv_stats_rows(Nn * Ho * Wo, K)
             if rows > 0:
                 ws = F.zeroed_ws(rows * 2 * K, x.device)
-        # paired geometry: width Wd+1, S = 4 taps of dilation 2, pad (3, 2)
-        L.conv_fwd(xp.data_ptr(), wp.data_ptr(), y.data_ptr(), 0, Nn, H, Wd + 1, 8, K, 7, 4, Ho, Wo, 2, 2, 3, 2, 1, 2,
-                   0, 0, N.stream(), N.ptr(ws))
+        # the persistent stem kernel (csrc/kernels/stem.hip: filters and input rows
+        # staged once in LDS), else the generic conv in the paired geometry:
+        # width Wd+1, S = 4 taps of dilation 2, pad (3, 2)
+        if not (K == 64 and (rows == 32 or ws is None) and os.environ.get("SINGA_AMD_STEM_KERNEL", "1") != "0"
+                and L.stem_fwd(xp.data_ptr(), wp.data_ptr(), y.data_ptr(), N.ptr(ws), Nn, H, Wd + 1, Ho, Wo,
+                               N.stream())):
+            L.conv_fwd(xp.data_ptr(), wp.data_ptr(), y.data_ptr(), 0, Nn, H, Wd + 1, 8, K, 7, 4, Ho, Wo, 2, 2, 3, 2, 1,
+                       2, 0, 0, N.stream(), N.ptr(ws))
         if ws is not None:
             y._sg_bn_ws = (ws, rows)
         if self.requires_grad:

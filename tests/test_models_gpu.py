@@ -842,3 +842,35 @@ def test_lazy_residual_gradient_matches_materialised(gpu):
         for k, p in b.get_params().items():
             errs[f"{i}.{k}"] = rel_err(g_on[id(p)], g_off[id(p)])
     assert max(errs.values()) < 2e-2, errs
+
+
+@pytest.mark.parametrize("hw", [(224, 224), (128, 128)])
+def test_stem_kernel_matches_generic_conv(gpu, monkeypatch, hw):
+    """The persistent stem forward kernel (csrc/kernels/stem.hip: filters and
+    input rows staged once in LDS) gives the generic implicit-GEMM conv's
+    output and fused BN statistics, and matches a PyTorch conv."""
+    from singa_amd.models import resnet
+    dev = device.create_rocm_gpu()
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(3, 3, hw[0], hw[1], generator=g).to(gpu)
+    W = (torch.randn(64, 3, 7, 7, generator=g) * 0.1).to(gpu)
+    tx = Tensor(data=x, device=dev, requires_grad=False)
+    tW = Tensor(data=W, device=dev, requires_grad=True)
+    assert tx.data.is_cuda and tW.data.is_cuda
+    outs = []
+    autograd.training = True
+    try:
+        for knob in ("0", "1"):
+            monkeypatch.setenv("SINGA_AMD_STEM_KERNEL", knob)
+            y = resnet.PairedStemConv(bn_stats=True)(tx, tW)
+            ws, rows = y.data._sg_bn_ws
+            torch.cuda.synchronize()
+            outs.append((y.data.float().cpu(), ws.reshape(-1)[: rows * 2 * 64].float().cpu().view(rows, 2, 64)))
+    finally:
+        autograd.training = False
+    (y0, s0), (y1, s1) = outs
+    assert float((y0 - y1).abs().max()) <= 1e-2 * float(y0.abs().max())
+    t0, t1 = s0.sum(0), s1.sum(0)
+    assert float((t0 - t1).abs().max()) <= 1e-3 * float(t0.abs().max())
+    ref = torch.nn.functional.conv2d(x.bfloat16().float(), W.bfloat16().float(), stride=2, padding=3)
+    assert float((y1 - ref.cpu()).abs().max()) <= 2e-2 * float(ref.abs().max())
