@@ -120,6 +120,8 @@ void sg_ggemm(int, const void*, int64_t, int, int64_t, const void*, int64_t, int
               hipStream_t);
 void sg_ggemm_tune(int, int);
 int sg_stem_fwd(const void*, const void*, void*, void*, int, int, int, int, int, hipStream_t);
+void sg_conv3x3_set(int);
+int sg_conv3x3_enabled();
 int sg_gemm_act(const void*, int64_t, int, const void*, int64_t, int, void*, int64_t, int, int, int, float, const void*,
                 int, int64_t, int64_t, int64_t, int, void*, int, const void*, hipStream_t);
 void sg_gconv_fwd(int, const void*, const void*, void*, const void*, int, int, int, int, int, int, int, int, int, int,
@@ -450,6 +452,9 @@ PYBIND11_MODULE(_C, m) {
     CHK("ggemm");
   });
   m.def("ggemm_tune", [](int key, int value) { sg_ggemm_tune(key, value); });
+  // persistent 3x3 64-channel stage-1 conv (csrc/kernels/conv3x3.hip): A/B switch
+  m.def("conv3x3_set", [](int on) { sg_conv3x3_set(on); });
+  m.def("conv3x3_enabled", []() { return sg_conv3x3_enabled(); });
   // ImageNet stem forward (csrc/kernels/stem.hip): 1 if taken, 0 = use conv_fwd
   m.def("stem_fwd", [](P x, P w, P y, P stats, int N, int H, int W, int Ho, int Wo, P s) {
     const int r = sg_stem_fwd(CV(x), CV(w), V(y), V(stats), N, H, W, Ho, Wo, S(s));

@@ -1557,6 +1557,10 @@ extern "C" {
 
 int sg_bn_deterministic();  // batchnorm.hip: deterministic-reduction mode
 int sg_ws_prezeroed();      // batchnorm.hip: one-shot 'workspace pre-zeroed' flag (per-step arena)
+// conv3x3.hip: persistent 3x3/s1/p1 64->64-channel, 56-wide convolution
+int sg_conv3x3_ok(int N, int H, int W, int C, int K);
+int sg_conv3x3_64(const void* x, const void* w, int wmode, void* y, void* stats, const void* mask, int N, int H,
+                  int W, int C, int K, hipStream_t s);
 
 // Plain GEMM: C[M][N] = alpha * sum_k A(m,k) B(n,k) (+ beta*C) ... with
 //   a_kouter = 0: A stored [M][K] (lda), 1: A stored [K][M]
@@ -1638,6 +1642,13 @@ void sg_conv_fwd(const void* x, const void* w, void* y, const void* bias, int N,
   p.stats_det = sg_bn_deterministic();
   if (p.stats && !p.stats_det && !sg_ws_prezeroed())  // (consumes the one-shot pre-zeroed flag)
     sg_zero_async(p.stats, sizeof(float) * 32 * 2 * K, s);  // atomic slot rows
+  const bool k3s1 = R == 3 && S == 3 && sh == 1 && sw == 1 && ph == 1 && pw == 1 && dh == 1 && dw == 1 &&
+                   Ho == H && Wo == W;
+  if (k3s1 && out_mode == OUT_BF16 && !bias && !relu && !(p.stats && p.stats_det) &&
+      sg_conv3x3_ok(N, H, W, C, K)) {
+    sg_conv3x3_64(x, w, 0, y, p.stats, nullptr, N, H, W, C, K, s);
+    return;
+  }
   p.g = make_geom(N, H, W, C, K, R, S, Ho, Wo, sh, sw, ph, pw, dh, dw);
   p.M = N * Ho * Wo; p.N = K; p.K = R * S * C;
   p.a = (const bf16*)x; p.lda = 0; p.b = (const bf16*)w; p.ldb = R * S * C;
@@ -1739,6 +1750,16 @@ void sg_conv_dgrad_bn_ex(const void* dy, const void* w, void* dx, int N, int H, 
     p.bnb_mean = (const float*)bn_mean; p.bnb_invstd = (const float*)bn_invstd;
     p.bnb_scale = (const float*)bn_scale; p.bnb_shift = (const float*)bn_shift;
     if (!sg_ws_prezeroed()) sg_zero_async(bn_ws, sizeof(float) * 32 * 2 * C, s);
+  }
+  if (R == 3 && S == 3 && sh == 1 && sw == 1 && ph == 1 && pw == 1 && dh == 1 && dw == 1 && Ho == H && Wo == W &&
+      out_mode == OUT_BF16 && beta == 0.f && !p.res_g && (!p.stats || p.stats_mode == 3) && wt && (K & 63) == 0 &&
+      sg_conv3x3_ok(N, H, W, C, K)) {
+    // the persistent 64-channel kernel over the flipped K-major weights
+    if (!wt_ready)
+      hipLaunchKernelGGL(wt_transpose_k, dim3((C + 63) / 64, (K + 63) / 64, R * S), dim3(256), 0, s, (const bf16*)w,
+                         (bf16*)wt, K, R * S, C);
+    sg_conv3x3_64(dy, wt, 1, dx, p.stats, p.bnb_mask, N, H, W, C, K, s);
+    return;
   }
   p.g = make_geom(N, H, W, C, K, R, S, Ho, Wo, sh, sw, ph, pw, dh, dw);
   if (R == 1 && S == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0) {

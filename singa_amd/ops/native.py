@@ -35,6 +35,8 @@ def _load():
         _lib.set_deterministic(1)
     if os.environ.get("SINGA_BN_RPT") and hasattr(_lib, "bn_set_rows_per_thread"):
         _lib.bn_set_rows_per_thread(int(os.environ["SINGA_BN_RPT"]))  # 0: legacy grid-stride BN apply
+    if os.environ.get("SINGA_AMD_CONV3X3", "1") == "0" and hasattr(_lib, "conv3x3_set"):
+        _lib.conv3x3_set(0)  # persistent stage-1 3x3 conv off (A/B against the generic implicit GEMM)
     # kernel tuning knobs from the environment: SG_TUNE="0=4,1=1" (key=value)
     for kv in os.environ.get("SG_TUNE", "").split(","):
         if "=" in kv and hasattr(_lib, "set_tuning"):
