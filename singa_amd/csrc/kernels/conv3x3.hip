@@ -31,18 +31,31 @@
 // Data gradient = the same convolution over dy with the filters flipped and
 // transposed: W'[c][r'][s'][k] = W[k][2-r'][2-s'][c], read from the K-major
 // copy WT [3][3][C][K] the dgrad path keeps (pretranspose_conv_weights).
+#include <stdlib.h>
+
+#include <type_traits>
+
 #include "common.h"
 
 namespace sg {
 namespace c3 {
+
+template <int N, int I = 0, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<N, I + 1>(f);
+  }
+}
 
 constexpr int CH = 64;                 // input channels = filters
 constexpr int WD = 56;                 // width (input = output)
 constexpr int PWD = WD + 2;            // patch row with the zero halo
 constexpr int RB = 8;                  // output rows per unit
 constexpr int PRW = RB + 2;            // patch rows
-constexpr int NPIX = PRW * PWD;        // 580 patch pixels
-constexpr int NSLOT = 584 * 8;         // fill slots: 8-pixel x 8-chunk groups (584 = NPIX rounded up to 8)
+constexpr int NPIX = PRW * PWD;        // 580 patch pixels (halo columns included)
+constexpr int NSLOT = PRW * WD * 8;    // fill slots: the 560 interior pixels x 8 chunks (the halo columns are
+                                       // zeroed once and never written)
 constexpr int PJ = 592 * 16;           // bytes of one chunk plane of the patch (592 = 16-multiple >= 584)
 constexpr int PATCH = 8 * PJ;          // 75,776 B
 constexpr int WJ = CH * 16;            // bytes of one chunk plane of the filters (64 filters x 16 B)
@@ -60,6 +73,7 @@ struct Args {
   const uint8_t* mask;   // data gradient: the producer BN's ReLU bits [N*H*56][8] (stats then = masked sum)
   int N, H;
   int units;             // N * H / 8
+  int dbg;               // timing experiments only (SG_C3_DBG): bit 0 no output stores, bit 1 no patch reloads
 };
 
 template <int WMODE>  // 0 forward, 1 data gradient
@@ -83,32 +97,38 @@ __global__ void __launch_bounds__(NT, 1) conv3x3_k(const Args a) {
     *(uint4*)(smem + jk * WJ + f * 16) = *(const uint4*)src;
   }
 
-  // fill slot e: pixel P = 8 (e >> 6) + (e & 7), chunk j = (e >> 3) & 7 -- a
-  // wave reads 8 whole pixels (1 KB) and each 8-lane store group writes 8
-  // consecutive pixels of one plane
+  // halo columns (patch columns 0 and 57 of every row): zero for good
+  for (int e = t; e < 8 * PRW * 2; e += NT) {
+    const int j = e / (PRW * 2), rr = (e >> 1) % PRW, side = e & 1;
+    *(uint4*)(smem + WBYTES + j * PJ + (rr * PWD + side * (PWD - 1)) * 16) = make_uint4(0, 0, 0, 0);
+  }
+
+  // fill slot e: interior pixel P' = 8 (e >> 6) + (e & 7) of the unit's 10
+  // input rows (contiguous in memory: row pr = P' / 56 starts at input row
+  // ih0 + pr), chunk j = (e >> 3) & 7 -- a wave reads 8 whole pixels (1 KB)
+  // and each 8-lane store group writes 8 consecutive pixels of one plane.
+  // Slot k of thread t is slot 0 plus 64 pixels: global offset + 4096 k.
+  const int P0 = (t >> 6) * 8 + (t & 7), j0 = (t >> 3) & 7;
   uint4 v[PF];
   auto load = [&](int u) {
-    const int n = u / upi;
-    const int ih0 = (u - n * upi) * RB - 1;
-    const bf16* xin = a.x + (int64_t)n * a.H * WD * CH;
+    const int n = u / upi, hg = u - n * upi;
+    const bf16* src = a.x + ((int64_t)n * a.H + hg * RB - 1) * WD * CH + P0 * CH + j0 * 8;
+    const int plo = hg == 0 ? WD : 0;                                   // row -1 is padding
+    const int phi = hg == upi - 1 ? (PRW - 1) * WD : PRW * WD;          // row H is padding
 #pragma unroll
     for (int k = 0; k < PF; ++k) {
-      const int e = t + k * NT;
-      const int P = (e >> 6) * 8 + (e & 7), j = (e >> 3) & 7;
-      const int pr = P / PWD, pc = P - pr * PWD;
-      const int ih = ih0 + pr, iw = pc - 1;
+      const int Pp = P0 + 64 * k;
       uint4 z = make_uint4(0, 0, 0, 0);
-      if (e < NSLOT && pr < PRW && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)WD)
-        z = *(const uint4*)(xin + ((int64_t)ih * WD + iw) * CH + j * 8);
+      if (Pp >= plo && Pp < phi) z = *(const uint4*)(src + k * 4096);
       v[k] = z;
     }
   };
   auto store = [&]() {
 #pragma unroll
     for (int k = 0; k < PF; ++k) {
-      const int e = t + k * NT;
-      const int P = (e >> 6) * 8 + (e & 7), j = (e >> 3) & 7;
-      if (e < NSLOT) *(uint4*)(smem + WBYTES + j * PJ + P * 16) = v[k];
+      const int Pp = P0 + 64 * k;
+      const int pr = Pp / WD;
+      if (Pp < PRW * WD) *(uint4*)(smem + WBYTES + j0 * PJ + (Pp + 2 * pr + 1) * 16) = v[k];
     }
   };
 
@@ -134,46 +154,74 @@ __global__ void __launch_bounds__(NT, 1) conv3x3_k(const Args a) {
     for (int r = 0; r < 4; ++r) s_sum[j][r] = s_sq[j][r] = 0.f;
 
   if (u_beg < u_end) load(u_beg);
+  __syncthreads();  // the filters are in
   for (int u = u_beg; u < u_end; ++u) {
-    __syncthreads();  // every wave done with the previous patch (and the filters are in)
+    if ((a.dbg & 2) && u > u_beg) goto compute;
+    // raw barriers: __syncthreads() would also drain this wave's output
+    // stores of the previous unit (its fence waits vmcnt(0)); only the
+    // prefetched patch (waited for by its use below) and the LDS writes
+    // (lgkmcnt) must complete.  Every wave's reads of the previous patch
+    // retired when its MFMAs consumed them.
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
     store();
-    __syncthreads();
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's patch stores landed
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();        // ... every wave's
+    asm volatile("" ::: "memory");
     if (u + 1 < u_end) load(u + 1);  // in flight during this unit's MFMAs
+  compute:
     f32x4 acc[TMW][2];
 #pragma unroll
     for (int i = 0; i < TMW; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // 18 k-steps (tap, channel half), software-pipelined by hand: the next
+    // step's 9 fragments are read before this step's 14 MFMAs (the compiler,
+    // left alone, reused one fragment register and waited lgkmcnt(0) in front
+    // of every MFMA pair)
+    bf16x8 fa[2][TMW], fb[2][2];
+    auto frags = [&](auto stc, auto bc) {
+      constexpr int st = decltype(stc)::value, b = decltype(bc)::value;
+      constexpr int tap = st >> 1, kh = st & 1, dr = tap / 3, ds = tap % 3;
 #pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
-      const int dr = tap / 3, ds = tap - 3 * (tap / 3);
+      for (int i = 0; i < TMW; ++i) fa[b][i] = *(const bf16x8*)(L + abase[i] + kh * 4 * PJ + (dr * PWD + ds) * 16);
 #pragma unroll
-      for (int kh = 0; kh < 2; ++kh) {
-        bf16x8 fa[TMW], fb[2];
+      for (int jb = 0; jb < 2; ++jb) fb[b][jb] = *(const bf16x8*)(L + bbase + (tap * 8 + kh * 4) * WJ + jb * 256);
+    };
+    auto mma = [&](auto bc) {
+      constexpr int b = decltype(bc)::value;
 #pragma unroll
-        for (int i = 0; i < TMW; ++i) fa[i] = *(const bf16x8*)(L + abase[i] + kh * 4 * PJ + (dr * PWD + ds) * 16);
+      for (int i = 0; i < TMW; ++i)
 #pragma unroll
-        for (int jb = 0; jb < 2; ++jb) fb[jb] = *(const bf16x8*)(L + bbase + (tap * 8 + kh * 4) * WJ + jb * 256);
-#pragma unroll
-        for (int i = 0; i < TMW; ++i)
-#pragma unroll
-          for (int jb = 0; jb < 2; ++jb)
-            acc[i][jb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[jb], fa[i], acc[i][jb], 0, 0, 0);
-      }
-    }
+        for (int jb = 0; jb < 2; ++jb)
+          acc[i][jb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[b][jb], fa[b][i], acc[i][jb], 0, 0, 0);
+    };
+    frags(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
+    static_for<18>([&](auto stc) {
+      constexpr int st = decltype(stc)::value;
+      if constexpr (st + 1 < 18) frags(std::integral_constant<int, st + 1>{}, std::integral_constant<int, (st + 1) & 1>{});
+      __builtin_amdgcn_sched_barrier(0);
+      mma(std::integral_constant<int, st & 1>{});
+      __builtin_amdgcn_sched_barrier(0);
+    });
     // acc[i][jb][r] = out[pixel (wm*7 + i)*16 + (ln & 15)][filter wn*32 + jb*16 + 4 g4 + r]
     const int64_t pix0 = (int64_t)u * RB * WD;  // the unit's first output pixel
 #pragma unroll
     for (int i = 0; i < TMW; ++i) {
       const int64_t pix = pix0 + (wm * TMW + i) * 16 + (ln & 15);
+      unsigned mw = 0;
 #pragma unroll
       for (int jb = 0; jb < 2; ++jb) {
         const int f0 = wn * 32 + jb * 16 + 4 * g4;
         bf16x4 o;
 #pragma unroll
         for (int r = 0; r < 4; ++r) o[r] = (bf16)acc[i][jb][r];
-        *(bf16x4*)(a.y + pix * CH + f0) = o;
+        if (!(a.dbg & 1)) *(bf16x4*)(a.y + pix * CH + f0) = o;
         if (a.stats) {
           if (WMODE == 1) {
-            const unsigned mb = a.mask[pix * 8 + (f0 >> 3)] >> (f0 & 7);
+            // the lane's two mask bytes (jb = 0, 1) sit in one aligned dword
+            if (jb == 0) mw = *(const unsigned*)(a.mask + pix * 8 + wn * 4);
+            const unsigned mb = (mw >> (8 * (jb * 2 + (g4 >> 1)))) >> (f0 & 7);
 #pragma unroll
             for (int r = 0; r < 4; ++r) s_sum[jb][r] += ((mb >> r) & 1u) != 0 ? (float)o[r] : 0.f;
           } else {
@@ -240,8 +288,9 @@ int sg_conv3x3_64(const void* x, const void* w, int wmode, void* y, void* stats,
                   int W, int C, int K, hipStream_t s) {
   using namespace sg::c3;
   if (!sg_conv3x3_ok(N, H, W, C, K) || (wmode == 1 && stats && !mask)) return 0;
+  static const int dbg = getenv("SG_C3_DBG") ? atoi(getenv("SG_C3_DBG")) : 0;
   Args a{(const sg::bf16*)x, (const sg::bf16*)w, (sg::bf16*)y, (float*)stats, (const uint8_t*)mask, N, H,
-         N * (H / RB)};
+         N * (H / RB), dbg};
   const int grid = a.units < 256 ? a.units : 256;
   auto go = [&](auto kern) {
     static bool attr = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -735,7 +735,9 @@ def test_bn_kernels_stay_in_bounds(gpu, R, C):
 
 def test_fused_bn_stats_under_graph_replay(gpu):
     """conv (+epilogue BN statistics) -> BN, captured once and replayed: every
-    replay must see freshly zeroed statistics (identical outputs)."""
+    replay must see freshly zeroed statistics (the same outputs: the slot-row
+    atomics may sum in another order, so a few bf16 outputs can move by one
+    ulp; statistics that were not re-zeroed would double the sums)."""
     from singa_amd.ops import functional as F
     g = torch.Generator(device=gpu).manual_seed(11)
     x = torch.randn(8, 64, 28, 28, device=gpu, generator=g).bfloat16().contiguous(memory_format=torch.channels_last)
@@ -758,7 +760,7 @@ def test_fused_bn_stats_under_graph_replay(gpu):
         gr.replay()
         torch.cuda.synchronize()
         for a, b in zip(outs, ref):
-            assert rel_err(a, b) < 1e-5
+            assert rel_err(a, b) < 1e-4
 
 
 @pytest.mark.parametrize("bn", [False, True])

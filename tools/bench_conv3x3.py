@@ -35,6 +35,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--only", default=None, help="fwd | dgrad: run that pass on the persistent kernel --iters times "
+                    "with no timing (for rocprofv3 counter passes)")
     a = ap.parse_args()
     L = N.lib()
     dev = torch.device("cuda", 0)
@@ -53,12 +55,23 @@ def main():
         L.conv_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), 0, n, h, 56, 64, 64, 3, 3, h, 56, 1, 1, 1, 1, 1, 1, 0, 0,
                    s, ws.data_ptr())
 
+    def fwd_nostats():
+        L.conv_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), 0, n, h, 56, 64, 64, 3, 3, h, 56, 1, 1, 1, 1, 1, 1, 0, 0,
+                   s, 0)
+
     def dgrad():
         L.conv_dgrad_bn(x.data_ptr(), w.data_ptr(), y.data_ptr(), n, h, 56, 64, 64, 3, 3, h, 56, 1, 1, 1, 1, 1, 1,
                         wt.data_ptr(), ws.data_ptr(), 0, 0, 0, 0, 0, s, 0.0, mask.data_ptr())
 
-    for name, fn in (("fwd+stats", fwd), ("dgrad+masksum", dgrad)):
-        for on in (1, 0):
+    if a.only:
+        fn = fwd if a.only == "fwd" else dgrad
+        for _ in range(a.iters):
+            fn()
+        torch.cuda.synchronize()
+        return
+    paths = (1,) if os.environ.get("SG_C3_DBG") else (1, 0)
+    for name, fn in (("fwd+stats", fwd), ("fwd", fwd_nostats), ("dgrad+masksum", dgrad)):
+        for on in paths:
             L.conv3x3_set(on)
             ms = timeit(fn, a.iters)
             print(json.dumps({"pass": name, "path": "persistent" if on else "generic", "batch": n, "ms": round(ms, 4),
