@@ -67,11 +67,14 @@ def build_kernels(force: bool = False, jobs: int = 8) -> Path:
     tasks = []
     common = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-ffp-contract=fast",
               "-Wno-unused-result", "-munsafe-fp-atomics"]
+    # per-file extras: the persistent conv's epilogue runs beside its MFMAs,
+    # where SLP-packed f32 adds/FMAs (v_pk_*_f32) cost ~2x two scalar ones
+    extra = {"conv3x3": ["-fno-slp-vectorize"]}
     for s in srcs:
         o = OBJ / (s.stem + ".o")
         objs.append(o)
         if force or _newer(s, o, headers):
-            tasks.append([hipcc, *common, "-c", str(s), "-o", str(o)])
+            tasks.append([hipcc, *common, *extra.get(s.stem, []), "-c", str(s), "-o", str(o)])
     b = CSRC / "bindings.cpp"
     bo = OBJ / "bindings.o"
     objs.append(bo)

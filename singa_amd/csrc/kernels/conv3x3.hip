@@ -62,7 +62,7 @@ constexpr int WJ = CH * 16;            // bytes of one chunk plane of the filter
 constexpr int WBYTES = 72 * WJ;        // 73,728 B: 9 taps x 8 chunks
 constexpr int LDS = WBYTES + PATCH;    // 149,504 B
 constexpr int NT = 512;
-constexpr int PF = (NSLOT + NT - 1) / NT;  // 10 staged 16-byte vectors per thread
+constexpr int PFH = (NSLOT / 2 + NT - 1) / NT;  // 5 staged 16-byte vectors per thread (one channel half)
 constexpr int TMW = 7;                 // pixel blocks per wave: 448 / 16 / 4
 
 struct Args {
@@ -73,7 +73,7 @@ struct Args {
   const uint8_t* mask;   // data gradient: the producer BN's ReLU bits [N*H*56][8] (stats then = masked sum)
   int N, H;
   int units;             // N * H / 8
-  int dbg;               // timing experiments only (SG_C3_DBG): bit 0 no output stores, bit 1 no patch reloads
+  int dbg;               // timing experiments only (SG_C3_DBG): bit 0 no output stores
 };
 
 template <int WMODE>  // 0 forward, 1 data gradient
@@ -103,32 +103,36 @@ __global__ void __launch_bounds__(NT, 1) conv3x3_k(const Args a) {
     *(uint4*)(smem + WBYTES + j * PJ + (rr * PWD + side * (PWD - 1)) * 16) = make_uint4(0, 0, 0, 0);
   }
 
-  // fill slot e: interior pixel P' = 8 (e >> 6) + (e & 7) of the unit's 10
-  // input rows (contiguous in memory: row pr = P' / 56 starts at input row
-  // ih0 + pr), chunk j = (e >> 3) & 7 -- a wave reads 8 whole pixels (1 KB)
-  // and each 8-lane store group writes 8 consecutive pixels of one plane.
-  // Slot k of thread t is slot 0 plus 64 pixels: global offset + 4096 k.
-  const int P0 = (t >> 6) * 8 + (t & 7), j0 = (t >> 3) & 7;
-  uint4 v[PF];
-  auto load = [&](int u) {
+  // The patch is refilled one channel HALF at a time: the k-steps run all
+  // taps of channels 0-31 (planes 0-3) first, then all taps of channels 32-63
+  // (planes 4-7), so each half's planes are dead while the other half
+  // computes and take the next data then -- no stall at a unit boundary.
+  // Fill slot e of a half: interior pixel P' = 16 (e >> 6) + (e & 15) of the
+  // unit's 10 input rows (contiguous in memory: row pr = P' / 56 starts at
+  // input row ih0 + pr), chunk j = (e >> 4) & 3 of the half -- a wave reads
+  // 16 pixels x 64 B and each 8-lane store group writes 8 consecutive pixels
+  // of one plane.  Slot k of thread t is slot 0 plus 128 pixels.
+  const int P0 = (t >> 6) * 16 + (t & 15), j0 = (t >> 4) & 3;
+  uint4 v[PFH];
+  auto load_half = [&](int u, int h) {
     const int n = u / upi, hg = u - n * upi;
-    const bf16* src = a.x + ((int64_t)n * a.H + hg * RB - 1) * WD * CH + P0 * CH + j0 * 8;
+    const bf16* src = a.x + ((int64_t)n * a.H + hg * RB - 1) * WD * CH + P0 * CH + (h * 4 + j0) * 8;
     const int plo = hg == 0 ? WD : 0;                                   // row -1 is padding
     const int phi = hg == upi - 1 ? (PRW - 1) * WD : PRW * WD;          // row H is padding
 #pragma unroll
-    for (int k = 0; k < PF; ++k) {
-      const int Pp = P0 + 64 * k;
+    for (int k = 0; k < PFH; ++k) {
+      const int Pp = P0 + 128 * k;
       uint4 z = make_uint4(0, 0, 0, 0);
-      if (Pp >= plo && Pp < phi) z = *(const uint4*)(src + k * 4096);
+      if (Pp >= plo && Pp < phi) z = *(const uint4*)(src + k * 128 * CH);
       v[k] = z;
     }
   };
-  auto store = [&]() {
+  auto store_half = [&](int h) {
 #pragma unroll
-    for (int k = 0; k < PF; ++k) {
-      const int Pp = P0 + 64 * k;
+    for (int k = 0; k < PFH; ++k) {
+      const int Pp = P0 + 128 * k;
       const int pr = Pp / WD;
-      if (Pp < PRW * WD) *(uint4*)(smem + WBYTES + j0 * PJ + (Pp + 2 * pr + 1) * 16) = v[k];
+      if (Pp < PRW * WD) *(uint4*)(smem + WBYTES + (h * 4 + j0) * PJ + (Pp + 2 * pr + 1) * 16) = v[k];
     }
   };
 
@@ -153,88 +157,119 @@ __global__ void __launch_bounds__(NT, 1) conv3x3_k(const Args a) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) s_sum[j][r] = s_sq[j][r] = 0.f;
 
-  if (u_beg < u_end) load(u_beg);
-  __syncthreads();  // the filters are in
-  for (int u = u_beg; u < u_end; ++u) {
-    if ((a.dbg & 2) && u > u_beg) goto compute;
-    // raw barriers: __syncthreads() would also drain this wave's output
-    // stores of the previous unit (its fence waits vmcnt(0)); only the
-    // prefetched patch (waited for by its use below) and the LDS writes
-    // (lgkmcnt) must complete.  Every wave's reads of the previous patch
-    // retired when its MFMAs consumed them.
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    store();
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's patch stores landed
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_s_barrier();        // ... every wave's
-    asm volatile("" ::: "memory");
-    if (u + 1 < u_end) load(u + 1);  // in flight during this unit's MFMAs
-  compute:
-    f32x4 acc[TMW][2];
+  // Epilogue of a finished unit, one pixel block i at a time: it runs inside
+  // the NEXT unit's first-half MFMAs (acc_prev), so its stores and the
+  // statistics' VALU fill the MFMA gaps instead of a phase of their own.
+  f32x4 acc[TMW][2];
+  bf16x4 accp[TMW][2];  // the finished unit, already rounded to the bf16 outputs
+  unsigned mwp[TMW];
+  auto epi = [&](int i, int64_t pix0) {
+    const int64_t pix = pix0 + (wm * TMW + i) * 16 + (ln & 15);
 #pragma unroll
-    for (int i = 0; i < TMW; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // 18 k-steps (tap, channel half), software-pipelined by hand: the next
-    // step's 9 fragments are read before this step's 14 MFMAs (the compiler,
-    // left alone, reused one fragment register and waited lgkmcnt(0) in front
-    // of every MFMA pair)
-    bf16x8 fa[2][TMW], fb[2][2];
-    auto frags = [&](auto stc, auto bc) {
-      constexpr int st = decltype(stc)::value, b = decltype(bc)::value;
-      constexpr int tap = st >> 1, kh = st & 1, dr = tap / 3, ds = tap % 3;
+    for (int jb = 0; jb < 2; ++jb) {
+      const int f0 = wn * 32 + jb * 16 + 4 * g4;
+      const bf16x4 o = accp[i][jb];
+      if (!(a.dbg & 1)) *(bf16x4*)(a.y + pix * CH + f0) = o;
+      if (a.stats) {
+        if (WMODE == 1) {
+          // the lane's two mask bytes (jb = 0, 1) sit in one aligned dword
+          const unsigned mb = (mwp[i] >> (8 * (jb * 2 + (g4 >> 1)))) >> (f0 & 7);
 #pragma unroll
-      for (int i = 0; i < TMW; ++i) fa[b][i] = *(const bf16x8*)(L + abase[i] + kh * 4 * PJ + (dr * PWD + ds) * 16);
+          for (int r = 0; r < 4; ++r) s_sum[jb][r] += ((mb >> r) & 1u) != 0 ? (float)o[r] : 0.f;
+        } else {
 #pragma unroll
-      for (int jb = 0; jb < 2; ++jb) fb[b][jb] = *(const bf16x8*)(L + bbase + (tap * 8 + kh * 4) * WJ + jb * 256);
-    };
-    auto mma = [&](auto bc) {
-      constexpr int b = decltype(bc)::value;
+          for (int r = 0; r < 4; ++r) {
+            const float f = (float)o[r];
+            s_sum[jb][r] += f;
+            s_sq[jb][r] += f * f;
+          }
+        }
+      }
+    }
+  };
+  auto mask_loads = [&](int64_t pix0) {
+    if (WMODE == 1 && a.stats) {
+#pragma unroll
+      for (int i = 0; i < TMW; ++i)
+        mwp[i] = *(const unsigned*)(a.mask + (pix0 + (wm * TMW + i) * 16 + (ln & 15)) * 8 + wn * 4);
+    }
+  };
+
+  // 9 k-steps (taps) of one channel half, software-pipelined by hand: the
+  // next step's 9 fragments are read before this step's 14 MFMAs (left alone,
+  // the compiler reused one fragment register and waited lgkmcnt(0) in front
+  // of every MFMA pair).  EPI: run epilogue block i after the MFMAs of step i.
+  bf16x8 fa[2][TMW], fb[2][2];
+  auto frags = [&](auto khc, auto tapc, auto bc) {
+    constexpr int kh = decltype(khc)::value, tap = decltype(tapc)::value, b = decltype(bc)::value;
+    constexpr int dr = tap / 3, ds = tap % 3;
+#pragma unroll
+    for (int i = 0; i < TMW; ++i) fa[b][i] = *(const bf16x8*)(L + abase[i] + kh * 4 * PJ + (dr * PWD + ds) * 16);
+#pragma unroll
+    for (int jb = 0; jb < 2; ++jb) fb[b][jb] = *(const bf16x8*)(L + bbase + (tap * 8 + kh * 4) * WJ + jb * 256);
+  };
+  auto half = [&](auto khc, bool epi_on, int64_t ppix0) {
+    constexpr int kh = decltype(khc)::value;
+    frags(khc, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
+    static_for<9>([&](auto tc) {
+      constexpr int tap = decltype(tc)::value, b = tap & 1;
+      if constexpr (tap + 1 < 9)
+        frags(khc, std::integral_constant<int, tap + 1>{}, std::integral_constant<int, (tap + 1) & 1>{});
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < TMW; ++i)
 #pragma unroll
         for (int jb = 0; jb < 2; ++jb)
           acc[i][jb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[b][jb], fa[b][i], acc[i][jb], 0, 0, 0);
-    };
-    frags(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
-    static_for<18>([&](auto stc) {
-      constexpr int st = decltype(stc)::value;
-      if constexpr (st + 1 < 18) frags(std::integral_constant<int, st + 1>{}, std::integral_constant<int, (st + 1) & 1>{});
-      __builtin_amdgcn_sched_barrier(0);
-      mma(std::integral_constant<int, st & 1>{});
+      if constexpr (kh == 0 && tap < TMW) {
+        if (epi_on) epi(tap, ppix0);
+      }
       __builtin_amdgcn_sched_barrier(0);
     });
-    // acc[i][jb][r] = out[pixel (wm*7 + i)*16 + (ln & 15)][filter wn*32 + jb*16 + 4 g4 + r]
-    const int64_t pix0 = (int64_t)u * RB * WD;  // the unit's first output pixel
+  };
+  auto wait_lds_barrier = [&]() {
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's patch stores landed
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();        // raw: no drain of the output stores (vmcnt)
+    asm volatile("" ::: "memory");
+  };
+
+  if (u_beg < u_end) {
+    load_half(u_beg, 0);
+    store_half(0);
+    load_half(u_beg, 1);
+  }
+  __syncthreads();  // the filters and the first unit's planes 0-3 are in
+  bool have_prev = false;
+  int64_t ppix0 = 0;
+  for (int u = u_beg; u < u_end; ++u) {
+    // planes 0-3 hold this unit; every wave is done with planes 4-7
+    store_half(1);
+    if (u + 1 < u_end) load_half(u + 1, 0);  // in flight during the first half
+    if (have_prev) mask_loads(ppix0);
 #pragma unroll
-    for (int i = 0; i < TMW; ++i) {
-      const int64_t pix = pix0 + (wm * TMW + i) * 16 + (ln & 15);
-      unsigned mw = 0;
-#pragma unroll
-      for (int jb = 0; jb < 2; ++jb) {
-        const int f0 = wn * 32 + jb * 16 + 4 * g4;
-        bf16x4 o;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = (bf16)acc[i][jb][r];
-        if (!(a.dbg & 1)) *(bf16x4*)(a.y + pix * CH + f0) = o;
-        if (a.stats) {
-          if (WMODE == 1) {
-            // the lane's two mask bytes (jb = 0, 1) sit in one aligned dword
-            if (jb == 0) mw = *(const unsigned*)(a.mask + pix * 8 + wn * 4);
-            const unsigned mb = (mw >> (8 * (jb * 2 + (g4 >> 1)))) >> (f0 & 7);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) s_sum[jb][r] += ((mb >> r) & 1u) != 0 ? (float)o[r] : 0.f;
-          } else {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const float f = (float)o[r];
-              s_sum[jb][r] += f;
-              s_sq[jb][r] += f * f;
-            }
-          }
-        }
-      }
+    for (int i = 0; i < TMW; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    half(std::integral_constant<int, 0>{}, have_prev, ppix0);
+    wait_lds_barrier();  // planes 4-7 hold this unit; every wave is done with planes 0-3
+    if (u + 1 < u_end) {
+      store_half(0);
+      load_half(u + 1, 1);  // in flight during the second half
     }
+    half(std::integral_constant<int, 1>{}, false, 0);
+#pragma unroll
+    for (int i = 0; i < TMW; ++i)
+#pragma unroll
+      for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) accp[i][jb][r] = (bf16)acc[i][jb][r];
+    have_prev = true;
+    ppix0 = (int64_t)u * RB * WD;  // the unit's first output pixel
+    wait_lds_barrier();
+  }
+  if (have_prev) {
+    mask_loads(ppix0);
+#pragma unroll
+    for (int i = 0; i < TMW; ++i) epi(i, ppix0);
   }
   if (!a.stats) return;
   // reduce the 16 lanes of equal g4 and the 4 waves of equal wn through LDS,
