@@ -1315,7 +1315,8 @@ static int make_phases(ConvGeom& g) {
 // (0 = off), 7 = early DMA issue in the 2-stage loop (measured -3.5 % conv time)
 // 8 = non-temporal output stores in the LDS-staged bf16 epilogue, 9 = persistent
 // short-K kernel for the 1x1-conv GEMM shapes (sk_gemm_k)
-static int g_tune[10] = {5, 1, 1, 0, 0, 1, 8, 1, 0, 0};
+// key 10: workgroup target of the 8-wave split-K weight gradient (0: 1024 with taps, 512 for 1x1)
+static int g_tune[12] = {5, 1, 1, 0, 0, 1, 8, 1, 0, 0, 0, 0};
 // one-shot: the next dgrad's wt scratch is already transposed.  Per OS
 // thread: the runtime's executor threads (hogwild / aggregated replicas)
 // each set and consume their own flag, so one thread's set can never be
@@ -1853,7 +1854,7 @@ void sg_conv_wgrad(const void* x, const void* dy, void* dw_out, int N, int H, in
   if (big) {
     const int tiles = ((p.M + 127) / 128) * ((p.N + 127) / 128);
     const int nkt = (p.K + BK - 1) / BK;
-    const int target = R * S > 1 ? 1024 : 512;
+    const int target = g_tune[10] > 0 ? g_tune[10] : R * S > 1 ? 1024 : 512;
     sp = 1;
     while (tiles * sp < target && sp * 2 * 4 <= nkt) sp *= 2;
     p.k_per_split = kps(p.K, sp);
@@ -1900,7 +1901,7 @@ void sg_wt_transpose_batched(const void* desc, int n, int total, hipStream_t s) 
     hipLaunchKernelGGL(wt_transpose_batched_k, dim3(total), dim3(256), 0, s, (const WtDesc*)desc, n);
 }
 void sg_set_tuning(int key, int value) {
-  if (key >= 0 && key < 10) g_tune[key] = value;
+  if (key >= 0 && key < 12) g_tune[key] = value;
 }
 
 }  // extern "C"
