@@ -4,6 +4,8 @@
 // Reference: Pooling/UnPooling plans (include/mshadow/tensor_expr_ext.h:
 // 787-850), channel pooling for LRN (:916-941, F8/F9 in src/worker/layer.cc:
 // 356-377).  Layout: activations are [N][H][W][C] (channels_last).
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace sg {
@@ -108,6 +110,79 @@ __global__ void bn_relu_maxpool_fwd_k(const bf16* __restrict__ x, const float* _
   }
 }
 
+// bn_relu_maxpool_fwd_k over 2x2 blocks of outputs (3x3 / stride 2 / pad 1,
+// Ho and Wo even): the 4 windows of outputs {2i, 2i+1} x {2j, 2j+1} span the
+// 5 x 5 input pixels from (4i-1, 4j-1), each loaded and BN+ReLU-transformed
+// once (25 instead of 36); taps are visited in the same row-major order, so
+// the argmax tie-breaking is unchanged.  Thread = (n, i, j, 8-channel chunk).
+__global__ void __launch_bounds__(256) bn_relu_maxpool_332_blk_k(const bf16* __restrict__ x,
+                                                               const float* __restrict__ scale,
+                                                               const float* __restrict__ shift,
+                                                               bf16* __restrict__ y, uint8_t* __restrict__ arg,
+                                                               int H, int W, int C, int Ho, int Wo, uint32_t total,
+                                                               FastDiv dCV, FastDiv dJ, FastDiv dI) {
+  constexpr int V = 8;
+  const int CV = C >> 3;
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+    const uint32_t p = dCV.div(e);
+    const int cv = (int)(e - p * (uint32_t)CV);
+    const uint32_t q = dJ.div(p);
+    const int j = (int)(p - q * (uint32_t)(Wo >> 1));
+    const uint32_t n = dI.div(q);
+    const int i = (int)(q - n * (uint32_t)(Ho >> 1));
+    float sc[V], sf[V];
+    ldc<V>(scale + cv * V, sc);
+    ldc<V>(shift + cv * V, sf);
+    float m[2][2][V];
+    unsigned best[2][2][V];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int k = 0; k < V; ++k) { m[a][b][k] = -INFINITY; best[a][b][k] = 0; }
+#pragma unroll
+    for (int lr = 0; lr < 5; ++lr) {
+      const int ih = 4 * i - 1 + lr;
+      if (ih < 0 || ih >= H) continue;
+      const bf16* xr = x + (((int64_t)n * H + ih) * W) * C + cv * V;
+#pragma unroll
+      for (int lc = 0; lc < 5; ++lc) {
+        const int iw = 4 * j - 1 + lc;
+        if (iw < 0 || iw >= W) continue;
+        float v[V];
+        ldv<bf16, V>(xr + (int64_t)iw * C, v);
+#pragma unroll
+        for (int k = 0; k < V; ++k) v[k] = (float)(bf16)fmaxf(v[k] * sc[k] + sf[k], 0.f);
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+          const int r = lr - 2 * a;
+          if (r < 0 || r > 2) continue;
+#pragma unroll
+          for (int b = 0; b < 2; ++b) {
+            const int t = lc - 2 * b;
+            if (t < 0 || t > 2) continue;
+#pragma unroll
+            for (int k = 0; k < V; ++k)
+              if (v[k] > m[a][b][k]) { m[a][b][k] = v[k]; best[a][b][k] = (unsigned)(r * 3 + t); }
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int64_t o = (((int64_t)n * Ho + 2 * i + a) * Wo + 2 * j + b) * C + cv * V;
+        stv<bf16, V>(y + o, m[a][b]);
+        uint2 pk;
+        pk.x = best[a][b][0] | (best[a][b][1] << 8) | (best[a][b][2] << 16) | (best[a][b][3] << 24);
+        pk.y = best[a][b][4] | (best[a][b][5] << 8) | (best[a][b][6] << 16) | (best[a][b][7] << 24);
+        *(uint2*)(arg + o) = pk;
+      }
+  }
+}
+
 // One workgroup row of blocks per input row (n, ih): gather the gradient of
 // the windows whose argmax is this pixel.
 template <typename T, int V>
@@ -195,6 +270,69 @@ __global__ void __launch_bounds__(256) maxpool_bwd_332_k(const bf16* __restrict_
       }
     }
     stv_nt<bf16, 8>(dx + (int64_t)i * 8, acc);
+  }
+}
+
+// Variant of maxpool_bwd_332_k over 2x2 blocks of input pixels: rows
+// {2i-1, 2i} x columns {2j-1, 2j} are covered by exactly the windows
+// {i-1, i} x {j-1, j}, so each (dy, argmax) vector is loaded once per block
+// (4 loads for 4 outputs instead of 9).  Thread = (n, i, j, 8-channel chunk),
+// i in [0, Ho], j in [0, Wo] (H = 2 Ho, W = 2 Wo: the host checks).
+__global__ void __launch_bounds__(256) maxpool_bwd_332_blk_k(const bf16* __restrict__ dy,
+                                                           const uint8_t* __restrict__ arg, bf16* __restrict__ dx,
+                                                           int H, int W, int C, int Ho, int Wo, uint32_t total,
+                                                           FastDiv dCV, FastDiv dJ, FastDiv dI) {
+  const int CV = C >> 3;
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+    const uint32_t p = dCV.div(e);
+    const int cv = (int)(e - p * (uint32_t)CV);
+    const uint32_t q = dJ.div(p);
+    const int j = (int)(p - q * (uint32_t)(Wo + 1));
+    const uint32_t n = dI.div(q);
+    const int i = (int)(q - n * (uint32_t)(Ho + 1));
+    // window (a, b) in {i-1, i} x {j-1, j}: dy / argmax vectors (zero / no match when outside)
+    bf16x8 d[2][2];
+    uint2 pk[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int oh = i - 1 + a, ow = j - 1 + b;
+        const bool ok = oh >= 0 && oh < Ho && ow >= 0 && ow < Wo;
+        const int64_t o = (((int64_t)n * Ho + (ok ? oh : 0)) * Wo + (ok ? ow : 0)) * C + cv * 8;
+        pk[a][b] = ok ? *(const uint2*)(arg + o) : make_uint2(0xffffffffu, 0xffffffffu);
+        d[a][b] = *(const bf16x8*)(dy + o);
+      }
+    // input pixel (ih, iw) = (2i-1+u, 2j-1+v): window row i-1 covers it at tap 2 (u = 0), row i at tap u
+    // (0 for the odd row, 1 for the even one); likewise for columns
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int ih = 2 * i - 1 + u;
+      if (ih < 0 || ih >= H) continue;
+#pragma unroll
+      for (int v = 0; v < 2; ++v) {
+        const int iw = 2 * j - 1 + v;
+        if (iw < 0 || iw >= W) continue;
+        float acc[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+          if (a == 0 && u == 1) continue;  // the even row lies only in window row i
+          const int r = a == 0 ? 2 : u;
+#pragma unroll
+          for (int b = 0; b < 2; ++b) {
+            if (b == 0 && v == 1) continue;
+            const unsigned want = (unsigned)(r * 3 + (b == 0 ? 2 : v));
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+              acc[k] += (((k < 4 ? pk[a][b].x : pk[a][b].y) >> (8 * (k & 3))) & 0xffu) == want ? (float)d[a][b][k]
+                                                                                                 : 0.f;
+          }
+        }
+        stv_nt<bf16, 8>(dx + (((int64_t)n * H + ih) * W + iw) * C + cv * 8, acc);
+      }
+    }
   }
 }
 
@@ -500,7 +638,14 @@ void sg_pool_bwd(const void* dy, const void* arg, void* dx, int N, int H, int W,
   PoolGeom g{N, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw};
   const int V = (C % 8 == 0) ? 8 : 1;
   const int64_t total = (int64_t)N * H * W * (C / V);
-  if (is_max && dtype == 1 && V == 8 && kh == 3 && kw == 3 && sh == 2 && sw == 2 && ph == 1 && pw == 1 &&
+  static const int blk = getenv("SG_POOL_BLK") ? atoi(getenv("SG_POOL_BLK")) : 1;
+  const int64_t tblk = (int64_t)N * (Ho + 1) * (Wo + 1) * (C / 8);
+  if (blk && is_max && dtype == 1 && V == 8 && kh == 3 && kw == 3 && sh == 2 && sw == 2 && ph == 1 && pw == 1 &&
+      H == 2 * Ho && W == 2 * Wo && tblk < (int64_t)UINT32_MAX) {
+    hipLaunchKernelGGL(maxpool_bwd_332_blk_k, dim3(sg_grid(tblk, 256, 16384)), dim3(256), 0, s, (const bf16*)dy,
+                       (const uint8_t*)arg, (bf16*)dx, H, W, C, Ho, Wo, (uint32_t)tblk, FastDiv(C / 8),
+                       FastDiv(Wo + 1), FastDiv(Ho + 1));
+  } else if (is_max && dtype == 1 && V == 8 && kh == 3 && kw == 3 && sh == 2 && sw == 2 && ph == 1 && pw == 1 &&
       total < (int64_t)UINT32_MAX && Ho == (H + 1) / 2 && Wo == (W + 1) / 2) {
     hipLaunchKernelGGL(maxpool_bwd_332_k, dim3(sg_grid(total, 256, 16384)), dim3(256), 0, s, (const bf16*)dy,
                        (const uint8_t*)arg, (bf16*)dx, H, W, C, Ho, Wo, (uint32_t)total, FastDiv(C / 8), FastDiv(W),
@@ -518,6 +663,15 @@ void sg_pool_bwd(const void* dy, const void* arg, void* dx, int N, int H, int W,
 void sg_bn_relu_maxpool(const void* x, const void* scale, const void* shift, void* y, void* arg, int N, int H, int W,
                         int C, int Ho, int Wo, int kh, int kw, int sh, int sw, int ph, int pw, hipStream_t s) {
   PoolGeom g{N, H, W, C, Ho, Wo, kh, kw, sh, sw, ph, pw};
+  static const int blk = getenv("SG_POOL_BLK") ? atoi(getenv("SG_POOL_BLK")) : 1;
+  const int64_t tblk = (int64_t)N * (Ho / 2) * (Wo / 2) * (C / 8);
+  if (blk && kh == 3 && kw == 3 && sh == 2 && sw == 2 && ph == 1 && pw == 1 && (Ho & 1) == 0 && (Wo & 1) == 0 &&
+      (C & 7) == 0 && Ho == (H + 1) / 2 && Wo == (W + 1) / 2 && tblk < (int64_t)UINT32_MAX) {
+    hipLaunchKernelGGL(bn_relu_maxpool_332_blk_k, dim3(sg_grid(tblk, 256, 16384)), dim3(256), 0, s, (const bf16*)x,
+                       (const float*)scale, (const float*)shift, (bf16*)y, (uint8_t*)arg, H, W, C, Ho, Wo,
+                       (uint32_t)tblk, FastDiv(C / 8), FastDiv(Wo / 2), FastDiv(Ho / 2));
+    return;
+  }
   const int ych = (int)(((int64_t)Wo * (C / 8) + 255) / 256);
   hipLaunchKernelGGL(bn_relu_maxpool_fwd_k, dim3(N * Ho, ych), dim3(256), 0, s, (const bf16*)x, (const float*)scale,
                      (const float*)shift, (bf16*)y, (uint8_t*)arg, g);
