@@ -4,6 +4,8 @@
 // include/mshadow/cuda/tensor_gpu-inl.cuh:56-92) and the cxxnet_op functors
 // (include/mshadow/cxxnet_op.h:14-112) with per-op wave64 kernels that move
 // 16 bytes per lane per access (8 bf16 or 4 fp32) in a grid-stride loop.
+#include <stdexcept>
+
 #include "common.h"
 
 namespace sg {
@@ -417,15 +419,17 @@ __global__ void nchw_to_nhwc_pad_k(const TI* __restrict__ x, bf16* __restrict__ 
 // horizontally adjacent taps, so the 7x7/2 stem is a 7x4 conv with horizontal
 // dilation 2 over 8 channels: 224 reduction elements per output instead of
 // 392 with the channel-padded layout (ResNetStem, models/resnet.py).
-__global__ void nchw_to_pairs_k(const float* __restrict__ x, bf16* __restrict__ y, int N, int C, int H, int W) {
+// (32-bit indices with constant-divisor splits: the int64 divisions of a
+// v1 made this pass VALU-bound at ~3 TB/s)
+__global__ void nchw_to_pairs_k(const float* __restrict__ x, bf16* __restrict__ y, int N, int C, int H, int W,
+                                uint32_t total, FastDiv dW1, FastDiv dH) {
   const int W1 = W + 1;
-  const int64_t total = (int64_t)N * H * W1;
-  SG_GRID_STRIDE(p, total) {
-    const int64_t nh = p / W1;
-    const int w = (int)(p - nh * W1);
-    const int64_t n = nh / H;
-    const int h = (int)(nh - n * H);
-    const float* xb = x + (n * C * H + h) * (int64_t)W;  // channel c at xb + c*H*W
+  for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < total; p += gridDim.x * blockDim.x) {
+    const uint32_t nh = dW1.div(p);
+    const int w = (int)(p - nh * (uint32_t)W1);
+    const uint32_t n = dH.div(nh);
+    const int h = (int)(nh - n * (uint32_t)H);
+    const float* xb = x + ((int64_t)n * C * H + h) * (int64_t)W;  // channel c at xb + c*H*W
     bf16x8 v;
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
@@ -434,7 +438,7 @@ __global__ void nchw_to_pairs_k(const float* __restrict__ x, bf16* __restrict__ 
     }
     v[6] = (bf16)0.f;
     v[7] = (bf16)0.f;
-    *(bf16x8*)(y + p * 8) = v;
+    *(bf16x8*)(y + (int64_t)p * 8) = v;
   }
 }
 
@@ -521,8 +525,10 @@ void sg_rand_fill(void* y, int64_t n, int dtype, int dist, float a, float b, uin
                                         a, b, seed, offset));
 }
 void sg_nchw_to_pairs(const void* x, void* y, int N, int C, int H, int W, hipStream_t s) {
-  hipLaunchKernelGGL(nchw_to_pairs_k, dim3(sg_grid((int64_t)N * H * (W + 1))), dim3(256), 0, s, (const float*)x,
-                     (bf16*)y, N, C, H, W);
+  const int64_t total = (int64_t)N * H * (W + 1);
+  if (total >= (int64_t)UINT32_MAX) throw std::runtime_error("nchw_to_pairs: more than 2^32 pixel pairs");
+  hipLaunchKernelGGL(nchw_to_pairs_k, dim3(sg_grid(total)), dim3(256), 0, s, (const float*)x, (bf16*)y, N, C, H, W,
+                     (uint32_t)total, FastDiv(W + 1), FastDiv(H));
 }
 
 void sg_nchw_to_nhwc_pad(const void* x, void* y, int N, int C, int H, int W, int Cp, hipStream_t s) {
