@@ -1316,6 +1316,7 @@ static int make_phases(ConvGeom& g) {
 // 8 = non-temporal output stores in the LDS-staged bf16 epilogue, 9 = persistent
 // short-K kernel for the 1x1-conv GEMM shapes (sk_gemm_k)
 // key 10: workgroup target of the 8-wave split-K weight gradient (0: 1024 with taps, 512 for 1x1)
+// key 11: 1 = strided data gradients never take the single-stage short-K kernel (A/B)
 static int g_tune[12] = {5, 1, 1, 0, 0, 1, 8, 1, 0, 0, 0, 0};
 // one-shot: the next dgrad's wt scratch is already transposed.  Per OS
 // thread: the runtime's executor threads (hogwild / aggregated replicas)
@@ -1477,9 +1478,16 @@ static void launch(const GemmArgs& p, int M, int splits, hipStream_t s, int batc
         else launch_sk<2>(p, tiles_m, p.N / 128, s);
         return;
       }
+      // (a strided dgrad's phases each reduce over their own taps only: the
+      // longest phase decides -- the stride-2 3x3 data gradients, 1-4 taps)
+      int kmax = p.K;
+      if (p.out_phase) {
+        kmax = 0;
+        for (int i = 0; i < z; ++i) kmax = max(kmax, p.g.phs[i].nr * p.g.phs[i].ns * p.g.K);
+      }
       if (OUT == OUT_BF16 && g_tune[6] > 0 && g_tune[4] == 0 && p.beta == 0.f &&
-          (p.K + BK - 1) / BK <= g_tune[6] && p.N >= 128 && !((p.N % 128) != 0 && (p.N % 128) <= 64) &&
-          (long)((M + 127) / 128) * ((p.N + 127) / 128) >= 1024) {
+          (kmax + BK - 1) / BK <= g_tune[6] && p.N >= 128 && !((p.N % 128) != 0 && (p.N % 128) <= 64) &&
+          (long)((M + 127) / 128) * ((p.N + 127) / 128) >= 1024 && (g_tune[11] == 0 || !p.out_phase)) {
         const int tiles = ((M + 127) / 128) * ((p.N + 127) / 128);
         launch_t<128, 128, AM, BMODE, OUT_BF16, 256, 2, 2, 1, FLAGS>(p, tiles, batch, z, s);
         return;
