@@ -1000,10 +1000,11 @@ __global__ void __launch_bounds__(512, 2) pp_gemm_k(const GemmArgs p) {
 // staged as bf16 through LDS into 16-byte row stores whose completion overlaps
 // the next tile's MFMAs, and the BN statistics stay in registers across all of
 // the workgroup's tiles (one LDS reduction and one atomic per column at the end).
-// Measured (profiles/r3/sk_check.log, ab_persistent_short_k.jsonl): -5..+4 % on
-// the ResNet-50 1x1 shapes against igemm_k and neutral on the step -- the
-// short-K GEMMs sit at ~4.2 TB/s of combined traffic either way (hipBLASLt
-// too), not at a per-tile fixed cost -- so it stays opt-in (tuning knob 9).
+// Measured in round 3 (profiles/r3/sk_check.log, ab_persistent_short_k.jsonl):
+// -5..+4 % per shape and neutral on the step, so it was opt-in; on the round-4
+// step (native activation pool, persistent stem / stage-1 3x3 kernels, block
+// pooling) the same switch is +2.0 % (profiles/r4/ab_sk_default.jsonl: 14.17k
+// vs 13.90k img/s, three alternating rounds), so tuning knob 9 is on by default.
 // ------------------------------------------------------------------------------
 constexpr int SK_TILE = 128 * BK * 2;             // one 128-row K-tile image (16 KB)
 constexpr int SK_LDT = 128 + 8;                   // bf16 staging row stride (+16 B)
@@ -1317,7 +1318,7 @@ static int make_phases(ConvGeom& g) {
 // short-K kernel for the 1x1-conv GEMM shapes (sk_gemm_k)
 // key 10: workgroup target of the 8-wave split-K weight gradient (0: 1024 with taps, 512 for 1x1)
 // key 11: 1 = strided data gradients never take the single-stage short-K kernel (A/B)
-static int g_tune[12] = {5, 1, 1, 0, 0, 1, 8, 1, 0, 0, 0, 0};
+static int g_tune[12] = {5, 1, 1, 0, 0, 1, 8, 1, 0, 1, 0, 0};
 // one-shot: the next dgrad's wt scratch is already transposed.  Per OS
 // thread: the runtime's executor threads (hogwild / aggregated replicas)
 // each set and consume their own flag, so one thread's set can never be
