@@ -7,7 +7,7 @@ training at 1/2/4/8 MI355X"), synthetic ImageNet-shaped data (3x224x224,
 backward, (N>1) bucketed RCCL all-reduce of every gradient, fused SGD-momentum
 update of every parameter.
 
-    python bench.py --gpus N --steps K --warmup W
+    python bench.py --gpus N --steps K --warmup W     (N > 1: spawns N ranks itself)
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
         --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
 
@@ -26,6 +26,43 @@ import sys
 import time
 
 import numpy as np
+
+
+def _load_launcher():
+    """singa_amd/launch.py loaded by path: importing the package would load
+    the kernel library, and the parent of a self-launched job must stay off
+    the GPU (a process that initialised HIP must not fork/exec workers)."""
+    import importlib.util
+
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "singa_amd", "launch.py")
+    spec = importlib.util.spec_from_file_location("_singa_amd_launch", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def self_launch(n: int, argv, timeout_s: float = 0.0, script=None) -> int:
+    """Run ``script`` (default: this file) as ``n`` ranks with
+    RANK/LOCAL_RANK/WORLD_SIZE/MASTER_ADDR=127.0.0.1/MASTER_PORT set.  The
+    children share stdout, so rank 0's JSON line is the job's output; when a
+    rank fails the launcher terminates its peers and the failing code is
+    returned.  SIGTERM/SIGINT to this parent also stop the children."""
+    import signal
+
+    launch = _load_launcher()
+
+    def _stop(signum, frame):
+        raise SystemExit(128 + signum)  # unwinds run_job's finally: the children are killed
+
+    signal.signal(signal.SIGTERM, _stop)
+    signal.signal(signal.SIGINT, _stop)
+    cmd = [sys.executable, "-u", os.path.abspath(script or __file__)]
+    rc = launch.run_job(n, list(argv), cmd=cmd, timeout_s=timeout_s)
+    if rc < 0:  # a child killed by a signal
+        rc = 128 - rc
+    if rc != 0:
+        print(f"bench.py: self-launched job of {n} ranks failed with exit code {rc}", file=sys.stderr)
+    return rc
 
 
 def main() -> int:
@@ -58,15 +95,22 @@ def main() -> int:
                     help="cap on RCCL channels (NCCL_MAX_NCHANNELS) for N > 1; 0 = RCCL's default. The ResNet-50 "
                          "exchange is ~180 MB per GPU per step (~1 ms at 16 channels over the xGMI mesh), so "
                          "fewer channels mainly means fewer CUs taken from the backward it overlaps")
+    ap.add_argument("--launch-timeout", type=float, default=0.0,
+                    help="self-launch (--gpus N > 1 without WORLD_SIZE): stop the job after this many seconds")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # self-launch (reference examples/mnist/run.sh:19-30 fans out its own
+        # processes): one child rank per GPU; nothing here touches the GPU
+        return self_launch(args.gpus, sys.argv[1:], args.launch_timeout)
 
     import torch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and world == 1 and args.gpus > 1:
-        print(f"--gpus {args.gpus} requires launching with torch.distributed.run", file=sys.stderr)
+    if world != args.gpus:
+        print(f"--gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
         return 2
     if not torch.cuda.is_available():
         print("bench.py needs a GPU", file=sys.stderr)

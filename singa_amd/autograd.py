@@ -79,7 +79,19 @@ PARAM_USES: dict = {}
 # backward() returned: the input gradient was added IN PLACE into the partial
 # gradient the engine offered through ``op.acc_into`` (see backward())
 ACC_INPLACE = object()
-INPLACE_ACC = True  # engine switch (tests A/B the in-place accumulation against separate adds)
+INPLACE_ACC = True
+
+
+class AccReplace:
+    """backward() returned: the input gradient was summed with the partial
+    gradient the engine offered through ``op.acc_into`` into the NEW tensor
+    ``t``, which replaces that partial gradient (a dgrad epilogue that adds
+    the other consumers' gradient from its own buffer)."""
+
+    __slots__ = ("t",)
+
+    def __init__(self, t):
+        self.t = t  # engine switch (tests A/B the in-place accumulation against separate adds)
 
 
 def _as_tuple(x):
@@ -271,7 +283,9 @@ def backward(y, dy=None) -> Iterator[Tuple[Tensor, Tensor]]:
         # it now and let zero_grad cover it again
         for op_ in seen:
             for p in op_.params:
-                if p is not None and p in OVERWRITE_FIRST and puses[id(p)] > 1:
+                # (only a Linear overwrites its weight gradient on its first
+                # write: any other sole user would add into the stale slice)
+                if p is not None and p in OVERWRITE_FIRST and (puses[id(p)] > 1 or not isinstance(op_, Linear)):
                     OVERWRITE_FIRST.discard(p)
                     if p.grad_view is not None and _WGRAD_EPOCH.get(id(p)) != GRAD_EPOCH[0]:
                         G.zero_(p.grad_view)
@@ -344,6 +358,17 @@ def backward(y, dy=None) -> Iterator[Tuple[Tensor, Tensor]]:
                         yield p, Tensor(device=p.device, data=g, requires_grad=False)
                 continue
             if src_op is None:
+                continue
+            if isinstance(dx, AccReplace):
+                j = op.src_idx[i]
+                prev = pending[src_op][j]
+                if prev is not None:
+                    owned.discard(id(prev))
+                pending[src_op][j] = dx.t
+                owned.add(id(dx.t))
+                deps[src_op] -= 1
+                if deps[src_op] == 0:
+                    heapq.heappush(heap, (-getattr(src_op, "_seq", 0), id(src_op), src_op))
                 continue
             if dx is ACCUMULATED or dx is ACC_INPLACE:
                 dx = None  # (ACC_INPLACE: already summed into pending[src_op])
@@ -816,6 +841,13 @@ class Conv2d(Operator):
                   and (getattr(self, "acc_last", None) or {}).get(0, False)):
                 # residual BN: this dgrad's accumulation completes its output gradient
                 bnp = (prod.x, prod.st, prod.st.mask)
+        elif (isinstance(prod, ConvBNAddReLU) and getattr(prod, "st", None) is not None and prod.st.mask is not None
+              and self.group == 1 and tuple(self.dilation) == (1, 1) and self.needs_grad(0)
+              and ((acc is not None and (getattr(self, "acc_last", None) or {}).get(0, False))
+                   or (acc is None and (getattr(self, "sole", None) or {}).get(0, False)))):
+            # the fused residual tail: this dgrad completes its output gradient,
+            # so the epilogue writes it masked (g) and sums it per channel
+            bnp = ("gmask", prod.st.mask)
         wt_pre, self.wt_pre = getattr(self, "wt_pre", None), None
         tb = self.grad_target(2) if self.has_bias else None
         dx, dw, db = F.conv2d_bwd(x, w, dy, self.stride, self.padding, self.dilation, self.group,
@@ -823,7 +855,13 @@ class Conv2d(Operator):
                                   bn_producer=bnp, wt_pre=wt_pre, db_out=tb, bn_wdot=wdot)
         if tgt is not None:
             _WGRAD_EPOCH[id(self.params[1])] = GRAD_EPOCH[0]  # this step's weight gradient is no longer empty
-        if acc is not None and dx is acc:
+        if acc is not None and getattr(dx, "_sg_absorbed", None) is acc:
+            del dx._sg_absorbed
+            dx = AccReplace(dx)  # the dgrad summed acc into its own fresh output
+        elif acc is not None and (dx is acc or (isinstance(acc, F.MaskedGrad) and acc.value is not None
+                                                and dx is acc.value)):
+            # summed in place into the pending gradient (a lazy residual
+            # gradient the dgrad materialised holds the sum as its value)
             dx = ACC_INPLACE
         res = [dx, ACCUMULATED if tgt is not None else dw]
         if self.has_bias:
@@ -838,11 +876,13 @@ class BatchNorm2d(Operator):
     gradient buffer when the params live in a ParamStore."""
 
     def __init__(self, running_mean: torch.Tensor, running_var: torch.Tensor, momentum: float = 0.1,
-                 eps: float = 1e-5, relu: bool = False, has_residual: bool = False, name=None):
+                 eps: float = 1e-5, relu: bool = False, has_residual: bool = False, name=None,
+                 colsum: bool = False):
         super().__init__(name)
         self.rm, self.rv = running_mean, running_var
         self.momentum, self.eps = momentum, eps
         self.relu, self.has_residual = relu, has_residual
+        self.colsum = colsum  # the consumer is a fused residual tail: sum the output's columns too
 
     def forward(self, x, gamma, beta, res=None):
         # ReLU after a residual add: the mask cannot be recomputed from x, so
@@ -851,7 +891,7 @@ class BatchNorm2d(Operator):
         # reads these bits instead of x to sum the masked gradient)
         want = self.requires_grad and self.relu and (self.has_residual or (F.BN_WDOT and _training()))
         y, st = F.batchnorm_fwd(x, gamma, beta, self.rm, self.rv, _training(), self.momentum, self.eps, self.relu,
-                                res, want_mask=want)
+                                res, want_mask=want, want_colsum=self.colsum and self.requires_grad)
         if self.requires_grad:
             self.x, self.gamma, self.st = x, gamma, st
             self.beta = beta if F.BN_WDOT else None
@@ -869,6 +909,65 @@ class BatchNorm2d(Operator):
         if self.has_residual:
             out.append(dres)
         return tuple(out)
+
+
+class ConvBNAddReLU(Operator):
+    """out = relu(BN(conv1x1(y, W)) + res): a bottleneck's residual tail as one
+    operator (inputs y, W, gamma, beta, res) so its backward can run
+    algebraically (F.bnres_bwd, csrc/kernels/bnres.hip): no pass over the conv
+    output c or its gradient -- the BN's two sums come from the masked output
+    gradient g (written, masked and summed, by the consuming conv's dgrad
+    epilogue) and from G = g^T y, the conv's gradients from one two-source
+    weight-gradient GEMM ([g | y]^T y) and one two-source data-gradient GEMM
+    ([g | y] against [W^T diag(s) | -W^T diag(u) W]).  The residual's gradient
+    is g itself.  The forward is the unfused conv (BN statistics in its
+    epilogue) + BN apply; c is not kept."""
+
+    wants_sole = True  # the producer BN's identity-sum backward needs this op to be y's only consumer
+
+    def __init__(self, running_mean: torch.Tensor, running_var: torch.Tensor, momentum: float, eps: float,
+                 name=None):
+        super().__init__(name)
+        self.rm, self.rv = running_mean, running_var
+        self.momentum, self.eps = momentum, eps
+
+    def forward(self, y, W, gamma, beta, res):
+        p = self.params[1] if len(self.params) > 1 else None
+        w = p.low if (p is not None and p.low is not None and y.dtype == torch.bfloat16) else W
+        c = F.conv2d_fwd(y, w, None, (1, 1), (0, 0), (1, 1), 1, out_dtype=y.dtype, relu=False,
+                         bn_stats=_training())
+        out, st = F.batchnorm_fwd(c, gamma, beta, self.rm, self.rv, _training(), self.momentum, self.eps, True, res,
+                                  want_mask=self.requires_grad)
+        if self.requires_grad:
+            self.y, self.w, self.gamma, self.st = y, w, gamma, st
+        return out
+
+    def backward(self, dout):
+        y, w, gamma, st = self.y, self.w, self.gamma, self.st
+        self.y = self.w = self.gamma = self.st = None
+        pre = getattr(dout, "_sg_gsum", None)
+        if pre is not None and pre[1] is st.mask:
+            g, gws = dout, pre[0]  # masked and summed by the consuming conv's dgrad epilogue
+            del dout._sg_gsum
+        else:
+            g, gws = F.bnres_masksum(dout, st.mask)
+        # the producer of y: a BN(+ReLU) whose identity-sum backward this op's
+        # dgrad epilogue can serve (as Conv2d.backward's wdot path)
+        prod = self.src[0][0] if self.src else None
+        prod2 = None
+        if (isinstance(prod, BatchNorm2d) and prod.relu and not prod.has_residual and F.BN_WDOT
+                and getattr(prod, "st", None) is not None and prod.st.mask is not None
+                and getattr(prod, "beta", None) is not None and (getattr(self, "sole", None) or {}).get(0, False)
+                and self.needs_grad(0)):
+            prod2 = (prod.st.mask, prod.gamma, prod.beta)
+        tw, tg, tb = self.grad_target(1), self.grad_target(2), self.grad_target(3)
+        cs = getattr(getattr(prod, "st", None), "colsum", None) if isinstance(prod, BatchNorm2d) else None
+        dy, dw, dg, db = F.bnres_bwd(g, gws, y, w, st, gamma, dw_out=tw, dg_out=tg, db_out=tb, prod2=prod2, cs=cs)
+        if tw is not None:
+            _WGRAD_EPOCH[id(self.params[1])] = GRAD_EPOCH[0]
+        g._sg_fresh = True  # the residual's gradient: the engine may accumulate into it in place
+        acc = lambda tgt, v: ACCUMULATED if tgt is not None else v  # noqa: E731
+        return dy, acc(tw, dw), acc(tg, dg), acc(tb, db), g
 
 
 class DualBNAddReLU(Operator):

@@ -69,7 +69,11 @@ def build_kernels(force: bool = False, jobs: int = 8) -> Path:
               "-Wno-unused-result", "-munsafe-fp-atomics"]
     # per-file extras: the persistent conv's epilogue runs beside its MFMAs,
     # where SLP-packed f32 adds/FMAs (v_pk_*_f32) cost ~2x two scalar ones
-    extra = {"conv3x3": ["-fno-slp-vectorize"]}
+    # the persistent kernels take a work-queue ticket one unit ahead and use it
+    # a unit later: the atomic optimizer would rewrite that one-lane atomic
+    # into a wave-aggregated one whose result is needed (vmcnt(0)) at once
+    noaopt = ["-mllvm", "-amdgpu-atomic-optimizer-strategy=None"]
+    extra = {"conv3x3": ["-fno-slp-vectorize", *noaopt], "stem": noaopt, "igemm": noaopt, "bnres": noaopt}
     for s in srcs:
         o = OBJ / (s.stem + ".o")
         objs.append(o)

@@ -122,6 +122,22 @@ void sg_ggemm_tune(int, int);
 int sg_stem_fwd(const void*, const void*, void*, void*, int, int, int, int, int, hipStream_t);
 void sg_conv3x3_set(int);
 int sg_conv3x3_enabled();
+void sg_bnres_wgrad(const void*, const void*, void*, int, int, int, hipStream_t);
+void sg_bnres_dgrad(const void*, const void*, const void*, const void*, void*, int, int, int, void*, const void*,
+                    hipStream_t);
+void sg_bnres_coef(const void*, const void*, const void*, const void*, const void*, const void*, int, int, int, void*,
+                   void*, void*, void*, void*, hipStream_t);
+void sg_bnres_combine(const void*, const void*, const void*, const void*, int, const void*, const void*, int, int,
+                      void*, void*, void*, void*, const void*, const void*, float, hipStream_t);
+void sg_bnres_masksum(const void*, const void*, void*, void*, int64_t, int, hipStream_t);
+void sg_set_dgrad_mask_out(int);
+void sg_bn_apply_cs(const void*, const void*, const void*, void*, void*, void*, int64_t, int, int, hipStream_t);
+void sg_conv_dgrad_gsum(const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int,
+                        int, int, int, void*, const void*, void*, const void*, hipStream_t);
+void sg_workq_set(int);
+int sg_workq_enabled();
+int sg_cu_count();
+void sg_cu_hog(int, double, int, int*, hipStream_t);
 int sg_gemm_act(const void*, int64_t, int, const void*, int64_t, int, void*, int64_t, int, int, int, float, const void*,
                 int, int64_t, int64_t, int64_t, int, void*, int, const void*, hipStream_t);
 void sg_gconv_fwd(int, const void*, const void*, void*, const void*, int, int, int, int, int, int, int, int, int, int,
@@ -455,6 +471,53 @@ PYBIND11_MODULE(_C, m) {
   // persistent 3x3 64-channel stage-1 conv (csrc/kernels/conv3x3.hip): A/B switch
   m.def("conv3x3_set", [](int on) { sg_conv3x3_set(on); });
   m.def("conv3x3_enabled", []() { return sg_conv3x3_enabled(); });
+  // algebraic residual-BN backward (csrc/kernels/bnres.hip)
+  m.def("bnres_wgrad", [](P g, P y, P out, int Pn, int K4, int C, P s) {
+    sg_bnres_wgrad(CV(g), CV(y), V(out), Pn, K4, C, S(s));
+    CHK("bnres_wgrad");
+  });
+  m.def("bnres_dgrad", [](P g, P y, P bd, P bias, P dx, int Pn, int K4, int C, P stats, P mask, P s) {
+    sg_bnres_dgrad(CV(g), CV(y), CV(bd), CV(bias), V(dx), Pn, K4, C, V(stats), CV(mask), S(s));
+    CHK("bnres_dgrad");
+  });
+  m.def("bnres_coef", [](P G, P w, P gws, P mean, P invstd, P gamma, int Pn, int K4, int C, P coef, P wf, P wu,
+                         P dg, P db, P s) {
+    sg_bnres_coef(CV(G), CV(w), CV(gws), CV(mean), CV(invstd), CV(gamma), Pn, K4, C, V(coef), V(wf), V(wu), V(dg),
+                  V(db), S(s));
+    CHK("bnres_coef");
+  });
+  m.def("bnres_combine", [](P G, P T, P M, P cs, int cs_rows, P coef, P w, int K4, int C, P dw, P bd, P bias,
+                            P wdot, P gamma2, P beta2, float tau, P s) {
+    sg_bnres_combine(CV(G), CV(T), CV(M), CV(cs), cs_rows, CV(coef), CV(w), K4, C, V(dw), V(bd), V(bias), V(wdot),
+                     CV(gamma2), CV(beta2), tau, S(s));
+    CHK("bnres_combine");
+  });
+  m.def("bnres_masksum", [](P dy, P mask, P g, P ws, int64_t R, int C, P s) {
+    sg_bnres_masksum(CV(dy), CV(mask), V(g), V(ws), R, C, S(s));
+    CHK("bnres_masksum");
+  });
+  // dgrad completing a fused residual tail's output gradient: (dgrad + acc) * bit, summed (stats_mode 4)
+  m.def("conv_dgrad_gsum", [](P dy, P w, P dx, int N, int H, int W, int C, int K, int R, int Sd, int Ho, int Wo,
+                              int sh, int sw, int ph, int pw, int dh, int dw, P wt, P acc, P bn_ws, P mask, P s) {
+    sg_conv_dgrad_gsum(CV(dy), CV(w), V(dx), N, H, W, C, K, R, Sd, Ho, Wo, sh, sw, ph, pw, dh, dw, V(wt), CV(acc),
+                       V(bn_ws), CV(mask), S(s));
+    CHK("conv_dgrad_gsum");
+  });
+  m.def("bn_apply_cs", [](P x, P scale, P shift, P y, P mask, P colsum, int64_t R, int C, int relu, P s) {
+    sg_bn_apply_cs(CV(x), CV(scale), CV(shift), V(y), V(mask), V(colsum), R, C, relu, S(s));
+    CHK("bn_apply_cs");
+  });
+  // one-shot: the next mask-only BN-producer dgrad writes its output masked (stats_mode 4)
+  m.def("set_dgrad_mask_out", [](int on) { sg_set_dgrad_mask_out(on); });
+  // persistent kernels' dynamic work queues (csrc/kernels/workq.hip): A/B switch
+  m.def("workq_set", [](int on) { sg_workq_set(on); });
+  m.def("workq_enabled", []() { return sg_workq_enabled(); });
+  m.def("cu_count", []() { return sg_cu_count(); });
+  // interference rehearsal: occupy ncu CUs for `us` microseconds on stream s
+  m.def("cu_hog", [](int ncu, double us, int lds_bytes, P started, P s) {
+    sg_cu_hog(ncu, us, lds_bytes, (int*)V(started), S(s));
+    CHK("cu_hog");
+  });
   // ImageNet stem forward (csrc/kernels/stem.hip): 1 if taken, 0 = use conv_fwd
   m.def("stem_fwd", [](P x, P w, P y, P stats, int N, int H, int W, int Ho, int Wo, P s) {
     const int r = sg_stem_fwd(CV(x), CV(w), V(y), V(stats), N, H, W, Ho, Wo, S(s));

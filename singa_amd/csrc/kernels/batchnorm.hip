@@ -407,10 +407,10 @@ __global__ void bn_infer_params_k(const float* __restrict__ gamma, const float* 
 // loaded before any is stored, so each thread keeps UR (x2 with a residual)
 // 16-byte loads in flight: the kernel is HBM-bound and one load per thread
 // per iteration leaves the memory pipeline half idle.
-template <typename T, int V, bool AFF2 = false>
+template <typename T, int V, bool AFF2 = false, bool CS = false>
 __device__ __forceinline__ void bn_apply_row(const float* v0, const float* rv, const float* sc, const float* sf,
                                              T* y, uint8_t* mask, int64_t o, int relu, const float* sc2 = nullptr,
-                                             const float* sf2 = nullptr) {
+                                             const float* sf2 = nullptr, float* cs = nullptr) {
   float v[V];
   if constexpr (AFF2) {
     // the residual is itself a BN input (a downsample branch): res = x2*scale2 + shift2,
@@ -426,6 +426,10 @@ __device__ __forceinline__ void bn_apply_row(const float* v0, const float* rv, c
     for (int k = 0; k < V; ++k) v[k] = fmaxf(v[k], 0.f);
   }
   stv_nt<T, V>(y + o, v);
+  if constexpr (CS) {  // column sums of the stored output
+#pragma unroll
+    for (int k = 0; k < V; ++k) cs[k] += (float)(T)v[k];
+  }
   if (V == 8 && mask) {  // bit k = (stored output of channel c0+k) > 0
     unsigned b = 0;
 #pragma unroll
@@ -458,14 +462,20 @@ __device__ __forceinline__ RowSpan row_span(const Tile2D& t, int64_t R, int64_t 
   return s;
 }
 
-template <typename T, int V, int UR, bool AFF2 = false>
+template <typename T, int V, int UR, bool AFF2 = false, bool CS = false>
 __global__ void __launch_bounds__(256) bn_apply_k(const T* __restrict__ x, const float* __restrict__ scale,
                                                   const float* __restrict__ shift, const T* __restrict__ res,
                                                   T* __restrict__ y, uint8_t* __restrict__ mask, int64_t R, int C,
                                                   int relu, int64_t rpw, const float* __restrict__ scale2,
-                                                  const float* __restrict__ shift2) {
+                                                  const float* __restrict__ shift2, float* __restrict__ colsum = nullptr) {
   const Tile2D t = tile2d<V>(C);
-  if (!t.cok) return;
+  // CS (a separate instantiation, C % 64 == 0 host-checked: every thread
+  // owns a channel chunk): also the column sums of the output, reduced over
+  // the workgroup's row lanes in LDS, one atomic per channel
+  float csum[V];
+#pragma unroll
+  for (int k = 0; k < V; ++k) csum[k] = 0.f;
+  if (!CS && !t.cok) return;
   float sc[V], sf[V], sc2[V], sf2[V];
   ldc<V>(scale + t.c0, sc);
   ldc<V>(shift + t.c0, sf);
@@ -486,15 +496,28 @@ __global__ void __launch_bounds__(256) bn_apply_k(const T* __restrict__ x, const
     }
 #pragma unroll
     for (int u = 0; u < UR; ++u)
-      bn_apply_row<T, V, AFF2>(v[u], res ? rv[u] : nullptr, sc, sf, y, mask, (r + u * step) * C + t.c0, relu,
-                               sc2, sf2);
+      bn_apply_row<T, V, AFF2, CS>(v[u], res ? rv[u] : nullptr, sc, sf, y, mask, (r + u * step) * C + t.c0, relu,
+                                   sc2, sf2, csum);
   }
   for (; r < sp.end; r += step) {
     float v[V], rv[V];
     const int64_t o = r * C + t.c0;
     ldv_nt<T, V>(x + o, v);
     if (res) ldv_nt<T, V>(res + o, rv);
-    bn_apply_row<T, V, AFF2>(v, res ? rv : nullptr, sc, sf, y, mask, o, relu, sc2, sf2);
+    bn_apply_row<T, V, AFF2, CS>(v, res ? rv : nullptr, sc, sf, y, mask, o, relu, sc2, sf2, csum);
+  }
+  if constexpr (CS) {
+    __shared__ float red[256 * V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) red[threadIdx.x * V + k] = csum[k];
+    __syncthreads();
+    const int CW = t.CT * V;
+    for (int j = threadIdx.x; j < CW; j += blockDim.x) {
+      const int cc = blockIdx.y * CW + j;
+      float a = 0.f;
+      for (int q = 0; q < t.RT; ++q) a += red[(q * t.CT + j / V) * V + (j % V)];
+      atomicAdd(colsum + (int64_t)(blockIdx.x & (NSLOT - 1)) * C + cc, a);  // 32 slot rows: no hot addresses
+    }
   }
 }
 
@@ -807,6 +830,22 @@ void sg_bn_apply(const void* x, const void* scale, const void* shift, const void
   DISPATCH_FT(dtype, DISPATCH_V(V, BN_UR_LAUNCH(bn_apply_k, 1, T, VV, grid, dim3(256), 0, s, (const T*)x,
                                                       (const float*)scale, (const float*)shift, (const T*)res, (T*)y,
                                                       (uint8_t*)mask, R, C, relu, rpw, nullptr, nullptr)));
+}
+
+// sg_bn_apply (bf16, no residual, C % 64 == 0) that also ADDS the column sums
+// of the stored output into 32 slot rows colsum[32][C] (zeroed by the caller:
+// one row per workgroup & 31 -- a single row made thousands of workgroups'
+// atomics collide on C addresses, 8x slower than the apply itself): the input
+// column sums of a consuming fused residual tail (bnres.hip), for free in
+// this HBM-bound pass instead of a separate read of its output
+void sg_bn_apply_cs(const void* x, const void* scale, const void* shift, void* y, void* mask, void* colsum, int64_t R,
+                    int C, int relu, hipStream_t s) {
+  if ((C & 63) != 0) throw std::runtime_error("bn_apply_cs: C % 64 required");
+  int64_t rpw;
+  dim3 grid = apply_grid(R, C, 8, rpw);
+  hipLaunchKernelGGL((bn_apply_k<bf16, 8, 2, false, true>), grid, dim3(256), 0, s, (const bf16*)x,
+                     (const float*)scale, (const float*)shift, (const bf16*)nullptr, (bf16*)y, (uint8_t*)mask, R, C,
+                     relu, rpw, nullptr, nullptr, (float*)colsum);
 }
 
 // y = act(x*scale + shift + x2*scale2 + shift2): a BN whose residual is the

@@ -216,3 +216,48 @@ static inline void sg_zero_async(void* p, size_t bytes, hipStream_t s) {
   const int64_t n4 = (int64_t)(bytes / 16);
   hipLaunchKernelGGL(sg_zero_k, dim3(sg_grid(n4, 256, 1024)), dim3(256), 0, s, (float4*)p, n4);
 }
+
+// ------------------------------------------------------------------------------
+// Dynamic work queue of the persistent kernels (sk_gemm_k, conv3x3_k,
+// stem_fwd_k).  A persistent grid sized to the CU count with work split
+// STATICALLY by blockIdx straggles as soon as some CUs are busy with other
+// work (RCCL's channel kernels during the overlapped gradient all-reduce): a
+// workgroup that starts late still owns its whole share.  Instead every
+// workgroup takes its next unit from a device counter, so late starters take
+// less.  A queue slot holds QMAX counters (one per independent unit sequence,
+// e.g. per column slice and XCD), each on its own 64-byte line, and a
+// done-counter; the last workgroup to finish resets the slot, so the next
+// launch (or the next replay of a captured graph) starts from zero with no
+// host work.  Slots come from a per-device ring (sg_workq_slot), so kernels
+// running concurrently on different streams never share one.
+// ------------------------------------------------------------------------------
+constexpr int QSTRIDE = 16;                  // ints between counters (64 B)
+constexpr int QMAX = 128;                    // counters per slot
+constexpr int QSLOT = (QMAX + 1) * QSTRIDE;  // ints per slot (the done-counter last)
+
+namespace sg {
+// ticket of queue q (one lane calls it; agent-scope vector atomic)
+__device__ __forceinline__ int wq_take(int* slot, int q) {
+  return __hip_atomic_fetch_add(slot + q * QSTRIDE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// one lane per workgroup, after its last ticket: the last workgroup of the
+// grid resets the slot's first nq counters and the done-counter
+__device__ __forceinline__ void wq_done(int* slot, int nq) {
+  const int total = (int)(gridDim.x * gridDim.y * gridDim.z);
+  int* done = slot + QMAX * QSTRIDE;
+  if (__hip_atomic_fetch_add(done, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == total - 1) {
+    for (int i = 0; i < nq; ++i)
+      __hip_atomic_exchange(slot + i * QSTRIDE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_exchange(done, 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+}  // namespace sg
+
+extern "C" {
+// a zeroed queue slot of the current device (nullptr: dynamic queues are
+// switched off -- SG_WORKQ=0 / sg_workq_set(0) -- and the kernels fall back
+// to the static blockIdx partition)
+int* sg_workq_slot();
+// compute units of the current device (cached)
+int sg_cu_count();
+}

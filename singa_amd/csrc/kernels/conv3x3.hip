@@ -11,7 +11,8 @@
 //
 // Here one 512-thread workgroup per CU keeps the whole filter bank (64 x 576
 // bf16, 72 KB) resident in LDS and walks a contiguous range of 8-output-row
-// units.  Per unit the 10 input rows it needs (with a zero halo: the padding)
+// units (taken from a dynamic queue, common.h, so a workgroup that starts
+// late -- its CU busy with communication kernels -- takes fewer).  Per unit the 10 input rows it needs (with a zero halo: the padding)
 // are staged once into LDS, the next unit's rows already in flight in
 // registers while this unit's 252 MFMAs per wave run.  Both LDS images are
 // PLANAR by 16-byte channel chunk ([chunk][pixel] / [chunk][filter]): the 16
@@ -74,6 +75,7 @@ struct Args {
   int N, H;
   int units;             // N * H / 8
   int dbg;               // timing experiments only (SG_C3_DBG): bit 0 no output stores
+  int* wq;               // dynamic unit queue slot (common.h) or null: static blockIdx partition
 };
 
 template <int WMODE>  // 0 forward, 1 data gradient
@@ -84,8 +86,11 @@ __global__ void __launch_bounds__(NT, 1) conv3x3_k(const Args a) {
   const int wm = wid >> 1, wn = wid & 1;  // pixel quarter, filter half
   const int g4 = ln >> 4;
 
-  const int u_beg = (int)((int64_t)blockIdx.x * a.units / gridDim.x);
-  const int u_end = (int)((int64_t)(blockIdx.x + 1) * a.units / gridDim.x);
+  // this workgroup's units: U0 = bx, U1 = bx + G, then (with a queue) U_i =
+  // 2G + ticket, each ticket taken one unit ahead; (without) U_i = bx + i G
+  const int G = (int)gridDim.x;
+  int u = (int)blockIdx.x, un = u + G;
+  int* sQ = (int*)(smem + LDS);  // ticket broadcast
   const int upi = a.H / RB;  // units per image
 
   // filter bank -> LDS plane [tap*8 + chunk][filter]; lanes take consecutive
@@ -234,26 +239,28 @@ __global__ void __launch_bounds__(NT, 1) conv3x3_k(const Args a) {
     asm volatile("" ::: "memory");
   };
 
-  if (u_beg < u_end) {
-    load_half(u_beg, 0);
+  if (u < a.units) {
+    load_half(u, 0);
     store_half(0);
-    load_half(u_beg, 1);
+    load_half(u, 1);
   }
   __syncthreads();  // the filters and the first unit's planes 0-3 are in
   bool have_prev = false;
   int64_t ppix0 = 0;
-  for (int u = u_beg; u < u_end; ++u) {
+  while (u < a.units) {
+    int ticket = 0;
+    if (t == 0 && a.wq) ticket = wq_take(a.wq, 0);  // U_{i+2}
     // planes 0-3 hold this unit; every wave is done with planes 4-7
     store_half(1);
-    if (u + 1 < u_end) load_half(u + 1, 0);  // in flight during the first half
+    if (un < a.units) load_half(un, 0);  // in flight during the first half
     if (have_prev) mask_loads(ppix0);
 #pragma unroll
     for (int i = 0; i < TMW; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
     half(std::integral_constant<int, 0>{}, have_prev, ppix0);
     wait_lds_barrier();  // planes 4-7 hold this unit; every wave is done with planes 0-3
-    if (u + 1 < u_end) {
+    if (un < a.units) {
       store_half(0);
-      load_half(u + 1, 1);  // in flight during the second half
+      load_half(un, 1);  // in flight during the second half
     }
     half(std::integral_constant<int, 1>{}, false, 0);
 #pragma unroll
@@ -264,8 +271,13 @@ __global__ void __launch_bounds__(NT, 1) conv3x3_k(const Args a) {
         for (int r = 0; r < 4; ++r) accp[i][jb][r] = (bf16)acc[i][jb][r];
     have_prev = true;
     ppix0 = (int64_t)u * RB * WD;  // the unit's first output pixel
-    wait_lds_barrier();
+    if (t == 0) *sQ = a.wq ? 2 * G + ticket : un + G;
+    wait_lds_barrier();  // (every thread read the previous ticket before the middle barrier)
+    const int unn = __builtin_amdgcn_readfirstlane(*sQ);
+    u = un;
+    un = unn;
   }
+  if (a.wq && t == 0) wq_done(a.wq, 1);
   if (have_prev) {
     mask_loads(ppix0);
 #pragma unroll
@@ -325,13 +337,14 @@ int sg_conv3x3_64(const void* x, const void* w, int wmode, void* y, void* stats,
   if (!sg_conv3x3_ok(N, H, W, C, K) || (wmode == 1 && stats && !mask)) return 0;
   static const int dbg = getenv("SG_C3_DBG") ? atoi(getenv("SG_C3_DBG")) : 0;
   Args a{(const sg::bf16*)x, (const sg::bf16*)w, (sg::bf16*)y, (float*)stats, (const uint8_t*)mask, N, H,
-         N * (H / RB), dbg};
-  const int grid = a.units < 256 ? a.units : 256;
+         N * (H / RB), dbg, sg_workq_slot()};
+  const int cus = sg_cu_count();
+  const int grid = a.units < cus ? a.units : cus;
   auto go = [&](auto kern) {
     static bool attr = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           LDS) == hipSuccess;
+                                           LDS + 16) == hipSuccess;
     (void)attr;
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), LDS, s, a);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), LDS + 16, s, a);
   };
   if (wmode == 0) go(conv3x3_k<0>);
   else go(conv3x3_k<1>);

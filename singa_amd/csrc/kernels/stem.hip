@@ -12,7 +12,8 @@
 // tile and a 128-pixel tile covers ~1.1 output rows, so input rows are
 // fetched again for every tile (~1.4 ms of the b1024 ResNet-50 step).
 //
-// Here a persistent workgroup walks a contiguous range of output ROW PAIRS:
+// Here a persistent workgroup walks output ROW PAIRS taken from a dynamic
+// queue (common.h: a workgroup that starts late takes fewer):
 // the filters (64 x 224, 29 KB) are loaded into LDS once, and per row pair
 // the 9 input rows it needs are staged in LDS with coalesced row loads (zero
 // rows / zero margins = the padding), the next pair's rows already in flight
@@ -40,6 +41,8 @@ struct Args {
   float* stats;    // [32][2][64] slot rows (zeroed by the caller) or null
   int N, H, W, Ho, Wo;
   int pairs;       // N * Ho / 2
+  int* wq;         // dynamic row-pair queue slot (common.h) or null: static blockIdx partition
+  int lds_main;    // bytes of the patch + filter images (the ticket slot follows)
 };
 
 template <int TM>  // Wo / 16 pixel blocks per output row
@@ -53,9 +56,11 @@ __global__ void __launch_bounds__(NT, 2) stem_fwd_k(const Args a) {
   const int wm = wid >> 1, wn = wid & 1;  // output row of the pair, filter half
   const int g4 = ln >> 4;
 
-  // this workgroup's contiguous range of row pairs
-  const int64_t p_beg = (int64_t)blockIdx.x * a.pairs / gridDim.x;
-  const int64_t p_end = (int64_t)(blockIdx.x + 1) * a.pairs / gridDim.x;
+  // this workgroup's row pairs: P0 = bx, P1 = bx + G, P2 = bx + 2G, then
+  // (with a queue) P_i = 3G + ticket, tickets taken two pairs ahead;
+  // (without) P_i = bx + i G
+  const int G = (int)gridDim.x;
+  int pp = (int)blockIdx.x, pn = pp + G;
   const int hp = a.Ho >> 1;  // row pairs per image
 
   for (int e = t; e < K * (KR / 8); e += NT) {
@@ -93,12 +98,22 @@ __global__ void __launch_bounds__(NT, 2) stem_fwd_k(const Args a) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) s_sum[j][r] = s_sq[j][r] = 0.f;
 
-  if (p_beg < p_end) load(p_beg);
-  for (int64_t pp = p_beg; pp < p_end; ++pp) {
+  int* sQ = (int*)(smem + a.lds_main);  // ticket broadcast
+  int ticket = 0;
+  bool first = true;
+  if (pp < a.pairs) load(pp);
+  while (pp < a.pairs) {
     __syncthreads();  // every wave done reading the previous patch (and the filters are in)
     store();
+    if (t == 0) {
+      // P_{i+2}: static for i = 0, else the ticket taken in the previous iteration
+      *sQ = first ? pp + 2 * G : (a.wq ? 3 * G + ticket : pn + G);
+      if (a.wq) ticket = wq_take(a.wq, 0);  // P_{i+3}
+    }
+    first = false;
     __syncthreads();
-    if (pp + 1 < p_end) load(pp + 1);  // in flight during this pair's MFMAs
+    const int pnn = __builtin_amdgcn_readfirstlane(*sQ);
+    if (pn < a.pairs) load(pn);  // in flight during this pair's MFMAs
     f32x4 acc[TM][2];
 #pragma unroll
     for (int i = 0; i < TM; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -137,7 +152,10 @@ __global__ void __launch_bounds__(NT, 2) stem_fwd_k(const Args a) {
         *(bf16x4*)(yrow + (int64_t)ox * K + wn * 32 + j * 16 + 4 * g4) = o;
       }
     }
+    pp = pn;
+    pn = pnn;
   }
+  if (a.wq && t == 0) wq_done(a.wq, 1);
   if (!a.stats) return;
   // reduce the 16 lanes of equal g4 (same filters, different pixels) and the
   // two waves of equal wn (the two output rows) through LDS, then one atomic
@@ -180,12 +198,14 @@ int sg_stem_fwd(const void* x, const void* w, void* y, void* stats, int N, int H
   if ((Ho & 1) != 0 || N <= 0 || (Wo != 112 && Wo != 64) || 2 * Wo + 1 > W || PR * (W + 4) > PF * NT ||
       (int64_t)N * Ho / 2 >= (1LL << 31))
     return 0;
-  Args a{(const sg::bf16*)x, (const sg::bf16*)w, (sg::bf16*)y, (float*)stats, N, H, W, Ho, Wo, N * Ho / 2};
+  const int lds_main = PR * (W + 4) * 16 + K * WROW * 2;
+  Args a{(const sg::bf16*)x, (const sg::bf16*)w, (sg::bf16*)y, (float*)stats, N, H, W, Ho, Wo, N * Ho / 2,
+         sg_workq_slot(), lds_main};
   if (stats && !sg_ws_prezeroed())  // (consumes the one-shot flag, as igemm's conv launches do)
     sg_zero_async(stats, sizeof(float) * 32 * 2 * K, s);
-  const int lds_main = PR * (W + 4) * 16 + K * WROW * 2;
-  const int lds = lds_main > 4 * 64 * 16 * 4 ? lds_main : 4 * 64 * 16 * 4;
-  const int grid = a.pairs < 512 ? a.pairs : 512;
+  const int lds = (lds_main > 4 * 64 * 16 * 4 ? lds_main : 4 * 64 * 16 * 4) + 16;
+  const int cap = 2 * sg_cu_count();  // two workgroups per CU
+  const int grid = a.pairs < cap ? a.pairs : cap;
   auto go = [&](auto kern) {
     static bool attr = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                            160 * 1024) == hipSuccess;

@@ -1,0 +1,121 @@
+// Host side of the persistent kernels' dynamic work queues (common.h) and a
+// CU-occupancy probe for the interference rehearsal.
+//
+// Queue slots live in one small device array per GPU, allocated and zeroed
+// once (outside any capture: the allocation runs with the thread's capture
+// mode relaxed and zeroes through a private non-blocking stream), handed out
+// round-robin.  A slot is reset on the device by the last workgroup of the
+// kernel that used it, so a slot is reusable as soon as that kernel ends; the
+// ring only has to be larger than the number of persistent kernels that can
+// run at the same time.
+#include <stdlib.h>
+
+#include <atomic>
+#include <mutex>
+
+#include "common.h"
+
+namespace {
+constexpr int kRing = 256;
+constexpr int kMaxDev = 16;
+int* g_ring[kMaxDev] = {};
+std::atomic<unsigned> g_next[kMaxDev];
+std::mutex g_mu;
+int g_cus[kMaxDev] = {};
+int g_on = -1;
+
+int cur_dev() {
+  int d = 0;
+  (void)hipGetDevice(&d);
+  return d < 0 || d >= kMaxDev ? 0 : d;
+}
+
+int* ring_of(int d) {
+  if (g_ring[d]) return g_ring[d];
+  std::lock_guard<std::mutex> g(g_mu);
+  if (g_ring[d]) return g_ring[d];
+  hipStreamCaptureMode m = hipStreamCaptureModeRelaxed;
+  (void)hipThreadExchangeStreamCaptureMode(&m);
+  int* p = nullptr;
+  const size_t bytes = sizeof(int) * QSLOT * kRing;
+  if (hipMalloc(&p, bytes) == hipSuccess) {
+    hipStream_t s;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess) {
+      (void)hipMemsetAsync(p, 0, bytes, s);
+      (void)hipStreamSynchronize(s);
+      (void)hipStreamDestroy(s);
+    } else {
+      (void)hipFree(p);
+      p = nullptr;
+    }
+  }
+  (void)hipThreadExchangeStreamCaptureMode(&m);
+  g_ring[d] = p;
+  return p;
+}
+
+// spin until the device's constant 100 MHz clock passes `until`
+__global__ void cu_hog_k(uint64_t ticks, int* started) {
+  extern __shared__ char lds[];  // requested at (nearly) a CU's whole LDS: one workgroup per CU
+  const uint64_t t0 = wall_clock64();
+  if (threadIdx.x == 0) {
+    lds[0] = 1;
+    atomicAdd(started, 1);
+  }
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(32);
+}
+}  // namespace
+
+extern "C" {
+
+void sg_workq_set(int on) { g_on = on ? 1 : 0; }
+
+int sg_workq_enabled() {
+  if (g_on < 0) {
+    const char* e = getenv("SG_WORKQ");
+    g_on = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_on;
+}
+
+int* sg_workq_slot() {
+  if (!sg_workq_enabled()) return nullptr;
+  const int d = cur_dev();
+  int* r = ring_of(d);
+  if (!r) return nullptr;
+  const unsigned i = g_next[d].fetch_add(1, std::memory_order_relaxed) % kRing;
+  return r + (size_t)i * QSLOT;
+}
+
+int sg_cu_count() {
+  const int d = cur_dev();
+  if (g_cus[d] <= 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess || n <= 0) n = 256;
+    g_cus[d] = n;
+  }
+  return g_cus[d];
+}
+
+// Interference rehearsal: occupy `ncu` compute units for `us` microseconds
+// with one sleeping workgroup each (each requests `lds_bytes` of LDS, by
+// default 160 KB, so no other workgroup that needs more than the rest can
+// share its CU), on stream s -- a stand-in for RCCL's channel kernels
+// holding CUs while the gradient all-reduce overlaps the backward.
+// `started` (device int, optional) counts the workgroups that got a CU.
+void sg_cu_hog(int ncu, double us, int lds_bytes, int* started, hipStream_t s) {
+  if (ncu <= 0) return;
+  const int lds = lds_bytes > 0 ? lds_bytes : 160 * 1024;
+  static bool attr = hipFuncSetAttribute((const void*)cu_hog_k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         160 * 1024) == hipSuccess;
+  (void)attr;
+  static int* dummy = nullptr;
+  if (!started) {
+    if (!dummy) (void)hipMalloc(&dummy, sizeof(int));
+    started = dummy;
+  }
+  const uint64_t ticks = (uint64_t)(us * 100.0);  // 100 MHz constant clock
+  hipLaunchKernelGGL(cu_hog_k, dim3(ncu), dim3(64), lds, s, ticks, started);
+}
+
+}  // extern "C"

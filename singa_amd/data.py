@@ -182,7 +182,7 @@ class DevicePrefetcher:
     def __init__(self, it, device: Optional[torch.device] = None):
         self.it = iter(it)
         self.device = device or torch.device("cuda")
-        self.stream = _stream.Stream(self.device) if self.device.type == "cuda" else None
+        self.stream = _stream.pooled(self.device, "prefetch") if self.device.type == "cuda" else None
         self.next = None
         self._preload()
 

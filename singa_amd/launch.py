@@ -26,7 +26,7 @@ import socket
 import subprocess
 import sys
 import time
-from typing import List
+from typing import List, Optional
 
 
 def _free_port() -> int:
@@ -60,9 +60,15 @@ def _default_nproc(args_after: List[str]) -> int:
 
 
 def run_job(nproc: int, child_args: List[str], module: str = "singa_amd", poll_s: float = 0.2,
-            timeout_s: float = 0.0, env_extra=None, nservers: int = 0) -> int:
+            timeout_s: float = 0.0, env_extra=None, nservers: int = 0, cmd: Optional[List[str]] = None) -> int:
+    """Start ``nproc`` ranks (plus ``nservers`` PS processes) and wait.  Each
+    child runs ``cmd + child_args`` (default ``python -m <module>``) with the
+    rank environment; children share this process's stdout/stderr.  Returns
+    0 when every child exits 0, otherwise the first failing child's code
+    (124 on ``timeout_s``) after terminating the rest."""
     port = _free_port()
     procs = []
+    prog = list(cmd) if cmd else [sys.executable, "-m", module]
     # native parameter-server processes (reference roles procsID >= nworkers):
     # they do not join the workers' process group
     for i in range(nservers):
@@ -73,8 +79,7 @@ def run_job(nproc: int, child_args: List[str], module: str = "singa_amd", poll_s
             env.pop(k, None)
         if env_extra:
             env.update(env_extra)
-        procs.append(subprocess.Popen([sys.executable, "-m", module] + child_args, env=env,
-                                      start_new_session=True))
+        procs.append(subprocess.Popen(prog + child_args, env=env, start_new_session=True))
     for r in range(nproc):
         env = dict(os.environ)
         env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nproc), MASTER_ADDR="127.0.0.1",
@@ -84,8 +89,7 @@ def run_job(nproc: int, child_args: List[str], module: str = "singa_amd", poll_s
             env["SINGA_AMD_PS"] = "native"
         if env_extra:
             env.update(env_extra)
-        procs.append(subprocess.Popen([sys.executable, "-m", module] + child_args, env=env,
-                                      start_new_session=True))
+        procs.append(subprocess.Popen(prog + child_args, env=env, start_new_session=True))
     t0 = time.time()
     rc = 0
     try:

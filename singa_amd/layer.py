@@ -298,9 +298,9 @@ class BatchNorm2d(Layer):
         G.fill_(rv.data, 1.0)
         self._state("running_var", rv)
 
-    def forward(self, x, relu: bool = False, residual: Optional[Tensor] = None):
+    def forward(self, x, relu: bool = False, residual: Optional[Tensor] = None, colsum: bool = False):
         op = autograd.BatchNorm2d(self.running_mean.data, self.running_var.data, 1.0 - self.momentum, self.eps,
-                                  relu=relu, has_residual=residual is not None)
+                                  relu=relu, has_residual=residual is not None, colsum=colsum)
         if residual is not None:
             return op(x, self.scale, self.bias, residual)
         return op(x, self.scale, self.bias)

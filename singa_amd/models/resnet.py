@@ -208,10 +208,25 @@ class Bottleneck(layer.Layer):
 
     def forward(self, x):
         out = self.bn1(self.conv1(x), relu=True)
-        out = self.bn2(self.conv2(out), relu=True)
+        # a fused residual tail below reads bn2's output column sums (summed in its apply pass)
+        tail = not self.has_down and autograd.training and F.BNRES and x.data.is_cuda and not autograd._TRACE
+        out = self.bn2(self.conv2(out), relu=True, colsum=tail)
         if self.has_down:
             xd = self.down_conv(x)  # (creation order as before the fusion: same parameter-init draws)
             return _dual_bn_add_relu(self.bn3, self.conv3(out), self.down_bn, xd)
+        c3 = self.conv3
+        if (autograd.training and not autograd._TRACE and c3.kernel_size == (1, 1) and c3.stride == (1, 1)
+                and tuple(c3.padding) == (0, 0) and not c3.bias and c3.group == 1
+                and F.bnres_ok(out.data, (c3.nb_kernels, out.shape[1], 1, 1), x.data)):
+            # the residual tail as one operator: its backward runs algebraically
+            # (F.bnres_bwd) -- no pass over conv3's output or its gradient
+            for lyr, t in ((c3, out), (self.bn3, x)):
+                if not lyr._initialized:
+                    lyr.initialize(t)
+                    lyr._initialized = True
+            bn = self.bn3
+            return autograd.ConvBNAddReLU(bn.running_mean.data, bn.running_var.data, 1.0 - bn.momentum,
+                                          bn.eps)(out, c3.W, bn.scale, bn.bias, x)
         return self.bn3(self.conv3(out), relu=True, residual=x)
 
 

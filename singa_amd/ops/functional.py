@@ -527,7 +527,7 @@ def layernorm_bwd(x, dy, g, mean, rstd, dg_acc=None, db_acc=None):
 def _no_native(what: str, *ts) -> None:
     """GPU operands must run on a hand-written kernel: raise instead of
     silently handing a device tensor to a PyTorch/vendor kernel.
-    (SINGA_AMD_NATIVE=0 -- debug only -- re-enables the PyTorch path.)"""
+    (native._TORCH_ORACLE_FOR_TESTS -- a test-only hook -- re-enables the PyTorch path.)"""
     if N.force_native() and any(t is not None and t.is_cuda for t in ts):
         raise NotImplementedError(f"{what}: no native gfx950 kernel for this case "
                                   f"({[(tuple(t.shape), t.dtype) for t in ts if t is not None]})")
@@ -1156,7 +1156,34 @@ def conv2d_bwd(x: torch.Tensor, w: torch.Tensor, dy: torch.Tensor, stride, paddi
                     wt = _mem.empty(Kp * Cp * R * S, dtype=torch.bfloat16, device=x.device)
             if ready:
                 N.lib().set_wt_ready(1)  # one-shot: consumed by the dgrad launch below
-            if (dx_acc is not None and Cx == Cp and dx_acc.dtype == od and od == x.dtype
+            gmask = (bn_producer[1] if bn_producer is not None and isinstance(bn_producer[0], str)
+                     and bn_producer[0] == "gmask" else None)
+            if gmask is not None:
+                bn_producer = None
+                if not (od == torch.bfloat16 and Cx == Cp and C % 8 == 0 and not padded
+                        and not N.lib().deterministic()
+                        and (dx_acc is None or (dx_acc.dtype == od and tuple(dx_acc.shape) == tuple(x.shape)
+                                                and N.is_cl(dx_acc)
+                                                and dx_acc.is_contiguous(memory_format=torch.channels_last)))):
+                    gmask = None  # (the consumer then masks and sums the gradient itself)
+            if gmask is not None:
+                # the consumer is a fused residual tail (ConvBNAddReLU): this dgrad
+                # completes its output gradient, so the epilogue writes it masked
+                # (g = d(out) * bit) and sums it per channel (stats_mode 4)
+                # (the other consumers' gradient dx_acc is added from its own
+                # buffer into a fresh dx, beta = 0: the single-stage short-K
+                # variant stays available; the caller replaces dx_acc by it)
+                dxp = _mem.empty((Nn, Cp, H, W), dtype=od, device=x.device, memory_format=torch.channels_last)
+                bws = zeroed_ws(32 * 2 * C, x.device)
+                N.lib().conv_dgrad_gsum(dyb.data_ptr(), wb.data_ptr(), dxp.data_ptr(), Nn, H, W, Cp, Kp, R, S, Ho,
+                                        Wo, sh, sw, ph, pw, dh, dw_, N.ptr(wt), N.ptr(dx_acc), bws.data_ptr(),
+                                        gmask.data_ptr(), N.stream())
+                dxp._sg_gsum = (bws, gmask)
+                dxp._sg_fresh = True
+                if dx_acc is not None:
+                    dxp._sg_absorbed = dx_acc
+                dx = dxp
+            elif (dx_acc is not None and Cx == Cp and dx_acc.dtype == od and od == x.dtype
                     and tuple(dx_acc.shape) == tuple(x.shape) and N.is_cl(dx_acc) and dx_acc.is_contiguous(
                         memory_format=torch.channels_last)):
                 bmask = bn_producer[2] if bn_producer is not None and len(bn_producer) > 2 else None
@@ -1413,10 +1440,11 @@ class BNState:
     ``mask``: 1-bit ReLU mask [R][C/8] of a fused BN(+residual)+ReLU output
     (written by the forward apply when requested; the backward then reads it
     instead of the bf16 output)."""
-    __slots__ = ("mean", "invstd", "scale", "shift", "mask")
+    __slots__ = ("mean", "invstd", "scale", "shift", "mask", "colsum")
 
     def __init__(self, mean, invstd, scale, shift, mask=None):
         self.mean, self.invstd, self.scale, self.shift, self.mask = mean, invstd, scale, shift, mask
+        self.colsum = None  # column sums of the output (want_colsum)
 
 
 # lazy residual gradient (see MaskedGrad); SINGA_AMD_LAZY_RES=0 writes it as a tensor
@@ -1545,11 +1573,15 @@ def bn_relu_maxpool_bwd(x: torch.Tensor, dy: torch.Tensor, arg: torch.Tensor, ga
 
 def batchnorm_fwd(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, run_mean: torch.Tensor,
                   run_var: torch.Tensor, training: bool, momentum: float = 0.1, eps: float = 1e-5,
-                  relu: bool = False, residual: Optional[torch.Tensor] = None, want_mask: bool = False):
+                  relu: bool = False, residual: Optional[torch.Tensor] = None, want_mask: bool = False,
+                  want_colsum: bool = False):
     """y = act(BN(x) + residual).  4-D x (channels_last on GPU) or 2-D [B, C].
     momentum follows the PyTorch convention (weight of the new statistic).
     ``want_mask`` (with relu, native path, C % 8 == 0): also write the 1-bit
-    ReLU mask into the returned state (``st.mask``) for the backward."""
+    ReLU mask into the returned state (``st.mask``) for the backward.
+    ``want_colsum`` (native bf16, no residual, C % 64 == 0): also the column
+    sums of y (``st.colsum``, fp32 [32][C] slot rows) -- for a consuming fused residual
+    tail (bnres_bwd), summed in this pass instead of re-reading y."""
     C = x.shape[1]
     if _bn_native(x):
         L = N.lib()
@@ -1565,6 +1597,13 @@ def batchnorm_fwd(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, run_
         mask = None
         if want_mask and relu and C % 8 == 0:
             mask = _mem.empty(R * C // 8, dtype=torch.uint8, device=dev)
+        if want_colsum and res is None and x.dtype == torch.bfloat16 and C % 64 == 0:
+            cs = _zeros32(32 * C, dev)  # 32 slot rows (the consumer sums them)
+            L.bn_apply_cs(x.data_ptr(), scale.data_ptr(), shift.data_ptr(), y.data_ptr(), N.ptr(mask), cs.data_ptr(),
+                          R, C, int(relu), N.stream())
+            st = BNState(mean, invstd, scale, shift, mask)
+            st.colsum = cs
+            return y, st
         L.bn_apply(x.data_ptr(), scale.data_ptr(), shift.data_ptr(), N.ptr(res), y.data_ptr(), R, C, int(relu),
                    N.dt(x), N.stream(), N.ptr(mask))
         return y, BNState(mean, invstd, scale, shift, mask)
@@ -1657,6 +1696,104 @@ def dual_bn_add_relu_bwd(x, dy, gamma, st: BNState, x2, gamma2, st2: BNState, dg
     dx._sg_fresh = True
     dx2._sg_fresh = True
     return dx, dg, db, dx2, dg2, db2
+
+
+# ---------------------------------------------------------------------------
+# Algebraic residual-tail backward (csrc/kernels/bnres.hip): out = relu(BN(W y)
+# + res) for a 1x1 conv W, with no pass over the conv output or its gradient
+# ---------------------------------------------------------------------------
+BNRES = os.environ.get("SINGA_AMD_BNRES", "1") != "0"
+
+
+def bnres_ok(y: torch.Tensor, w_shape, res: torch.Tensor) -> bool:
+    """The fused residual tail applies: native bf16 channels_last, a 1x1 /
+    stride-1 conv with C % 64 == 0 inputs and K4 % 128 == 0 outputs, a
+    residual of the output's shape, non-deterministic mode."""
+    K4, C = int(w_shape[0]), int(w_shape[1])
+    return (BNRES and _native_ok(y) and y.dtype == torch.bfloat16 and N.is_cl(y) and y.dim() == 4
+            and tuple(w_shape[2:]) == (1, 1) and y.shape[1] == C and C % 64 == 0 and K4 % 128 == 0
+            and res is not None and tuple(res.shape) == (y.shape[0], K4, y.shape[2], y.shape[3])
+            and not N.lib().deterministic() and y.numel() // C * K4 * 2 < (1 << 31))
+
+
+def _zeros32(n: int, device) -> torch.Tensor:
+    """n zeroed fp32 (an arena slice when the step arena is active)."""
+    t = ARENA.take(n, device)
+    if t is None:
+        t = _mem.empty(n, dtype=torch.float32, device=device)
+        N.lib().zero(t.data_ptr(), 4 * n, N.stream())
+    return t
+
+
+def bnres_masksum(dy: torch.Tensor, mask: torch.Tensor):
+    """g = dy * bit(mask) and the 32 slot rows of sum g (the fallback when no
+    upstream dgrad epilogue produced them)."""
+    if dy.dtype != torch.bfloat16 or not N.is_cl(dy):
+        dy = G.to(dy, torch.bfloat16, torch.channels_last)
+    C = dy.shape[1]
+    R = dy.numel() // C
+    g = _like(dy)
+    ws = _zeros32(32 * 2 * C, dy.device)
+    N.lib().bnres_masksum(dy.data_ptr(), mask.data_ptr(), g.data_ptr(), ws.data_ptr(), R, C, N.stream())
+    return g, ws
+
+
+def bnres_bwd(g: torch.Tensor, gws: torch.Tensor, y: torch.Tensor, w: torch.Tensor, st: "BNState",
+              gamma: torch.Tensor, dw_out=None, dg_out=None, db_out=None, prod2=None, cs=None):
+    """Backward of relu(BN(conv1x1(y, w)) + res) from g = d(out) * mask (bf16
+    NHWC [N, K4, H, W]) and its per-channel sums (``gws``: 32 slot rows
+    [32][2][K4]).  Returns (dy, dw, dgamma, dbeta); the parameter gradients
+    accumulate into the *_out views when given.  ``prod2`` = (mask2, gamma2,
+    beta2) of a producer BN(+ReLU) of y eligible for the identity-sum
+    backward: the data gradient's epilogue then sums its masked output and
+    the combination pass its <W, dW> sums (``dy._sg_bnbwd_wdot``), as
+    conv2d_bwd's identity-sum path does."""
+    L = N.lib()
+    s = N.stream()
+    dev = g.device
+    Nn, K4, H, W = g.shape
+    C = y.shape[1]
+    P = Nn * H * W
+    f32 = torch.float32
+    wb = w if (w.dtype == torch.bfloat16 and (N.is_cl(w) or w.is_contiguous())) else G.to(w, torch.bfloat16)
+    aug = _zeros32((K4 + C) * C, dev)  # [G ; Gram]
+    L.bnres_wgrad(g.data_ptr(), y.data_ptr(), aug.data_ptr(), P, K4, C, s)
+    Gm, Gram = aug[:K4 * C], aug[K4 * C:]
+    coef = _mem.empty(3 * K4, dtype=f32, device=dev)
+    wf = _mem.empty(K4 * C, dtype=f32, device=dev)
+    wu = _mem.empty(K4 * C, dtype=f32, device=dev)
+    dg = dg_out if dg_out is not None else _zeros32(K4, dev)
+    db = db_out if db_out is not None else _zeros32(K4, dev)
+    L.bnres_coef(Gm.data_ptr(), wb.data_ptr(), gws.data_ptr(), st.mean.data_ptr(), st.invstd.data_ptr(),
+                 gamma.data_ptr(), P, K4, C, coef.data_ptr(), wf.data_ptr(), wu.data_ptr(), dg.data_ptr(),
+                 db.data_ptr(), s)
+    T = _mem.empty(K4 * C, dtype=f32, device=dev)  # W Gram
+    L.ggemm(0, wf.data_ptr(), C, 0, 0, Gram.data_ptr(), C, 1, 0, T.data_ptr(), C, 0, K4, C, C, 1.0, 0.0, 0, 0, 1, 0,
+            1, 0, 0, 0, 0, s)
+    Mm = _mem.empty(C * C, dtype=f32, device=dev)  # W^T diag(u) W
+    L.ggemm(0, wf.data_ptr(), C, 1, 0, wu.data_ptr(), C, 1, 0, Mm.data_ptr(), C, 0, C, C, K4, 1.0, 0.0, 0, 0, 1, 0,
+            1, 0, 0, 0, 0, s)
+    if cs is None:  # (the producer BN's apply pass sums them when it knows this consumer: st.colsum)
+        cs = colsum(y.permute(0, 2, 3, 1).reshape(P, C))[0]
+    cs_rows = cs.numel() // C  # 1, or the 32 slot rows of bn_apply_cs
+    bd = _mem.empty(C * (K4 + C), dtype=torch.bfloat16, device=dev)
+    bw = _zeros32(2 * C + 64, dev)
+    wdot, bias = bw[:C + 1], bw[C + 64:]
+    dw = dw_out if dw_out is not None else _zeros32(K4 * C, dev)
+    g2, b2 = (prod2[1], prod2[2]) if prod2 is not None else (None, None)
+    L.bnres_combine(Gm.data_ptr(), T.data_ptr(), Mm.data_ptr(), cs.data_ptr(), cs_rows, coef.data_ptr(), wb.data_ptr(), K4,
+                    C, dw.data_ptr(), bd.data_ptr(), bias.data_ptr(), wdot.data_ptr(), N.ptr(g2), N.ptr(b2),
+                    BN_WDOT_TAU, s)
+    dy = _mem.empty((Nn, C, H, W), dtype=torch.bfloat16, device=dev, memory_format=torch.channels_last)
+    bws = _zeros32(32 * 2 * C, dev) if prod2 is not None else None
+    L.bnres_dgrad(g.data_ptr(), y.data_ptr(), bd.data_ptr(), bias.data_ptr(), dy.data_ptr(), P, K4, C, N.ptr(bws),
+                  N.ptr(prod2[0]) if prod2 is not None else 0, s)
+    if prod2 is not None:
+        dy._sg_bnbwd_wdot = (bws, wdot)
+    dy._sg_fresh = True
+    if dw_out is None:
+        dw = dw.view(K4, C, 1, 1)
+    return dy, dw, dg, db
 
 
 def batchnorm_bwd(x: torch.Tensor, dy: torch.Tensor, gamma: torch.Tensor, st: BNState,

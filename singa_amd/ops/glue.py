@@ -36,7 +36,7 @@ _FLOATS = (torch.float32, torch.bfloat16)
 
 def on_gpu(*ts) -> bool:
     """True when the operands live on the GPU and the native path is on
-    (SINGA_AMD_NATIVE=0 -- debug only -- routes everything to PyTorch)."""
+    (native._TORCH_ORACLE_FOR_TESTS -- a test-only hook -- routes everything to PyTorch)."""
     return any(t is not None and t.is_cuda for t in ts) and N.force_native()
 
 

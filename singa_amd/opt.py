@@ -208,16 +208,23 @@ class ParamStore:
             G.zero_(self.g)
         else:
             if getattr(self, "_zr_key", None) != key:
-                skip = {self.offsets[i]: self.offsets[i] + self.params[i].data.numel() for i in ow}
-                ranges, cur = [], 0
-                for o in sorted(skip):
-                    if o > cur:
-                        ranges += [cur, o - cur]
-                    cur = skip[o]
-                if cur < self.numel:
-                    ranges += [cur, self.numel - cur]
-                self._zr = memory.empty((len(ranges),), dtype=torch.int64, device=self.g.device)
-                G.copy_(self._zr, torch.tensor(ranges, dtype=torch.int64))
+                # every table ever built stays alive (they are a few ints): a
+                # HIP graph captured with an older key keeps zeroing from its
+                # own table, never from a block the pool has handed out again
+                tables = self.__dict__.setdefault("_zr_tables", {})
+                if key not in tables:
+                    skip = {self.offsets[i]: self.offsets[i] + self.params[i].data.numel() for i in ow}
+                    ranges, cur = [], 0
+                    for o in sorted(skip):
+                        if o > cur:
+                            ranges += [cur, o - cur]
+                        cur = skip[o]
+                    if cur < self.numel:
+                        ranges += [cur, self.numel - cur]
+                    t = memory.empty((len(ranges),), dtype=torch.int64, device=self.g.device)
+                    G.copy_(t, torch.tensor(ranges, dtype=torch.int64))
+                    tables[key] = t
+                self._zr = tables[key]
                 self._zr_key = key
             if self._zr.numel():
                 N.lib().zero_ranges(self.g.data_ptr(), self._zr.data_ptr(), self._zr.numel() // 2, N.stream())

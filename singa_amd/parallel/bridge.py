@@ -73,14 +73,27 @@ class P2PChannel:
       of blocking each other (an ungrouped RCCL send of a large message waits
       for its receiver).
     * Headers: every payload is preceded by a small int64 header (dtype,
-      requires-grad flag, shape).  A receiver reads a header on the host only
-      the first time it sees a channel slot (peer, k-th receive of the step);
-      afterwards it posts header and payload receives together from the
-      cached shape and checks all the step's headers with ONE device-to-host
-      copy in :meth:`finish` -- no host synchronisation per message."""
+      requires-grad flag, shape).  By default a receiver reads every header
+      on the host before it posts the payload receive, so a sender may change
+      a tensor's shape at any step (a partial last batch, a new sequence
+      length).  With ``static_shapes=True`` (a pipeline whose message shapes
+      are fixed: the config-driven NeuralNet, whose data layers always yield
+      full batches) a receiver reads a header on the host only the first time
+      it sees a channel slot (peer, k-th receive of the step); afterwards it
+      posts header and payload receives together from the cached shape and
+      checks all the step's headers with ONE device-to-host copy in
+      :meth:`finish` -- no host synchronisation per message.  (A shape change
+      under that promise is an error: RCCL has no way to abort a posted
+      receive of the wrong size.)
+    * :meth:`flush` issues the deferred sends as one group without a receive;
+      the pipeline schedules call it between consecutive actions of the same
+      kind, where no peer can be sending towards this process (see
+      :func:`singa_amd.parallel.pipeline.pipelined_step`)."""
 
-    def __init__(self, comm):
+    def __init__(self, comm, static_shapes: bool = False):
         self.comm = comm
+        self.static_shapes = bool(static_shapes)
+        self.log: List[tuple] = []  # ("send" | "recv", peer) in issue order (schedule-overlap tests)
         self.native = hasattr(comm, "p2p_group") and getattr(comm, "backend", "") == "rccl"
         self.sends: List[Tuple[torch.Tensor, int]] = []
         self.handles: List[tuple] = []
@@ -89,6 +102,7 @@ class P2PChannel:
         self.hdrs: dict = {}     # header list -> device tensor (sender side cache)
         self.k: dict = {}        # peer -> receives this step
         self.host_reads = 0      # headers read on the host (first use of a slot only)
+        self.flushes = 0         # send groups issued without a receive (schedule overlap)
         self.checked = 0         # headers verified in bulk at step end
 
     # compatibility with the plain pending-list protocol
@@ -108,6 +122,7 @@ class P2PChannel:
 
     def _issue_sends(self) -> None:
         for t, peer in self.sends:
+            self.log.append(("send", peer))
             if self.native:
                 self.comm.send(t, peer)
             else:
@@ -126,6 +141,7 @@ class P2PChannel:
             self._issue_sends()
             for b in bufs:
                 self.comm.recv(b, peer)
+        self.log.extend(("recv", peer) for _ in bufs)
 
     def recv_tensor(self, peer: int, dev) -> Tuple[torch.Tensor, bool]:
         """Receive the next (header, payload) pair from ``peer``: (tensor,
@@ -133,8 +149,8 @@ class P2PChannel:
         k = self.k.get(peer, 0)
         self.k[peer] = k + 1
         hdr = _mem.empty(3 + _MAXD, dtype=torch.int64, device=dev.torch_device)
-        h = self.shapes.get((peer, k))
-        if h is None:  # first time on this slot: read the header on the host
+        h = self.shapes.get((peer, k)) if self.static_shapes else None
+        if h is None:  # first time on this slot (or shapes may change): read the header on the host
             self.exchange([hdr], peer)
             self.host_reads += 1
             h = self.shapes[(peer, k)] = [int(v) for v in hdr.cpu().tolist()]
@@ -149,6 +165,7 @@ class P2PChannel:
     def flush(self) -> None:
         if not self.sends:
             return
+        self.flushes += 1
         if self.native:
             with self.comm.p2p_group():
                 self._issue_sends()

@@ -40,7 +40,7 @@ def run_ranks(fn: Callable, world: int, *args, device: Optional[torch.device] = 
         try:
             if dev >= 0:
                 torch.cuda.set_device(dev)
-                s = _stream.Stream(torch.device("cuda", dev))
+                s = _stream.pooled(torch.device("cuda", dev), f"loop-rank{r}")
                 with s:
                     comm = RcclCommunicator(world, r, r, native=native, device=torch.device("cuda", dev))
                     res[r] = fn(r, world, comm, *args)

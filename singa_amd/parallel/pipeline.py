@@ -80,8 +80,9 @@ def pipelined_step(net, zero_grad, m: int, kind: str = "1f1b") -> np.ndarray:
     roots = {}
     met = np.zeros(2, np.float64)
     zero_grad()
+    acts = schedule(kind, m, stage, stages)
     try:
-        for act, i in schedule(kind, m, stage, stages):
+        for n, (act, i) in enumerate(acts):
             if act == "F":
                 outs = net.forward(training=True, micro=(i, m))
                 roots[i] = net.backward_roots(outs)
@@ -92,6 +93,18 @@ def pipelined_step(net, zero_grad, m: int, kind: str = "1f1b") -> np.ndarray:
                 if rs:
                     for _ in autograd.backward(rs, seeds):
                         pass
+            # Sends are deferred so that a send crossing a peer's send (1F1B's
+            # steady state: activation i+1 downstream while gradient j comes
+            # up) is grouped with the receive that matches it.  Between two
+            # actions of the same kind no peer sends towards this process
+            # (forwards only receive from upstream / send downstream; a
+            # downstream stage in its drain sends gradients only after all
+            # this stage's activations have arrived), so the deferred sends
+            # leave right away: the next stage starts on micro-batch i while
+            # this one computes i+1 (GPipe's and the warm-up / drain overlap).
+            ch = getattr(net, "_pending", None)
+            if ch is not None and hasattr(ch, "flush") and n + 1 < len(acts) and acts[n + 1][0] == act:
+                ch.flush()
         net.finish_step()
     finally:
         for l, s in zip(losses, saved):

@@ -111,7 +111,8 @@ class RcclCommunicator(Communicator):
         self._c = native
         # high priority: bucket all-reduces issued mid-backward get the CUs
         # they need promptly instead of queueing behind the compute stream
-        self.comm_stream = None if self.host else _stream.Stream(self.device, priority=-1)
+        # (per rank: the loopback world runs several ranks of one process on one GPU)
+        self.comm_stream = None if self.host else _stream.pooled(self.device, f"comm-{tag}-r{rank}", priority=-1)
         self.stats = {"calls": 0, "bytes": 0}  # collective calls / payload bytes issued by this rank
         self._group_keep: Optional[list] = None
 

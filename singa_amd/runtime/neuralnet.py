@@ -385,7 +385,9 @@ class NeuralNet:
         self._extra_roots = []
         self._mb_batch = getattr(self, "_mb_batch", {})
         if getattr(self, "_pending", None) is None and self.dist:
-            self._pending = B.P2PChannel(self.comm)
+            # the config-driven data layers always yield full batches: fixed
+            # message shapes, so receives may post from the cached headers
+            self._pending = B.P2PChannel(self.comm, static_shapes=True)
         for l in self.layers:
             if not self.is_local(l):
                 continue

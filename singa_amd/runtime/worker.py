@@ -205,12 +205,12 @@ class Worker:
             self.replicas.append(r)
             self.rep_grads.append(g)
         gpu = self.dev.torch_device.type == "cuda"
-        self.streams = [_stream.Stream(self.dev.torch_device) for _ in range(k)] if gpu else None
+        self.streams = [_stream.pooled(self.dev.torch_device, f"exec{i}") for i in range(k)] if gpu else None
         # hogwild updates of the SHARED weights/momentum all run on one
         # stream: the lock orders the launches, the single stream serialises
         # the kernels (on per-thread streams they would overlap on the GPU
         # and race their read-modify-write of w and s1)
-        self.upd_stream = _stream.Stream(self.dev.torch_device) if gpu else None
+        self.upd_stream = _stream.pooled(self.dev.torch_device, "update") if gpu else None
         self._upd_lock = threading.Lock()
 
     # ------------------------------------------------------------- cadence

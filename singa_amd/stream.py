@@ -72,6 +72,23 @@ class Stream:
         return ctx.__exit__(*exc)
 
 
+_POOLED: dict = {}
+
+
+def pooled(device=None, role: str = "side", priority: int = 0) -> Stream:
+    """The framework stream of ``role`` on ``device`` (created once, reused):
+    the native pool caches freed blocks per stream, so a stream created per
+    call (and never destroyed) would strand its cached blocks; prefetchers,
+    communicators, executor threads and rank threads take theirs from here."""
+    idx = torch.device(device).index if device is not None else None
+    idx = idx if idx is not None else torch.cuda.current_device()
+    key = (idx, role, int(priority))
+    s = _POOLED.get(key)
+    if s is None:
+        s = _POOLED[key] = Stream(torch.device("cuda", idx), priority=priority)
+    return s
+
+
 def _handle(s) -> int:
     if s is None:
         return current()

@@ -192,7 +192,8 @@ def _stage_worker_chan(rank, world, comm, m, kind):
     _fix_batch(w)
     w.run()
     ch = w.train_net._pending
-    return [float(h[2][0]) for h in w.history if h[0] == "train"], _params(w), comm, ch.host_reads, ch.checked
+    return ([float(h[2][0]) for h in w.history if h[0] == "train"], _params(w), comm, ch.host_reads, ch.checked,
+            ch.flushes)
 
 
 @pytest.mark.parametrize("kind", P.SCHEDULES)
@@ -200,8 +201,9 @@ def test_placed_net_over_loopback_rccl_grouped_p2p(kind):
     """The same 2-stage placed net on the REAL RcclCommunicator over the
     native loopback communicator, whose ungrouped sends are rendezvous (an
     RCCL-style crossing 1F1B exchange deadlocks there): the bridges' grouped,
-    deferred sends complete every schedule, equal the unplaced net, and read
-    headers on the host only on the first step."""
+    deferred sends complete every schedule, equal the unplaced net, read
+    headers on the host only on the first step, and leave between actions of
+    the same kind (stage overlap, not held back to the next receive)."""
     from singa_amd.parallel.loop import run_ranks as loop_ranks
 
     ref_loss, ref_params = _reference()
@@ -209,7 +211,7 @@ def test_placed_net_over_loopback_rccl_grouped_p2p(kind):
     res = loop_ranks(_stage_worker_chan, 2, m, kind, timeout_s=30.0)
     seen = {}
     for r in range(2):
-        loss, params, comm, host_reads, checked = res[r]
+        loss, params, comm, host_reads, checked, flushes = res[r]
         np.testing.assert_allclose(loss, ref_loss, rtol=1e-5, atol=1e-6, err_msg=f"rank {r}")
         seen.update(params)
         assert comm.loopback and comm.stats["calls"] > 0
@@ -218,5 +220,12 @@ def test_placed_net_over_loopback_rccl_grouped_p2p(kind):
         # bulk-checked in the other 4 steps; stage 0 receives the gradients,
         # whose shapes it already knows (no headers)
         assert (host_reads, checked) == ((2 * m, 4 * 2 * m) if r == 1 else (0, 0))
+        # schedule overlap: between two actions of the same kind the deferred
+        # sends leave at once (GPipe: stage 0 after each of its first m-1
+        # forwards, stage 1 after each of its first m-1 backwards; 1F1B: stage
+        # 0's one warm-up forward), plus stage 1's last gradient at the step's
+        # end; 5 steps
+        want = {"gpipe": (5 * (m - 1), 5 * m), "1f1b": (5, 5)}[kind]
+        assert flushes == want[r], (kind, r, flushes)
     for k in ref_params:
         np.testing.assert_allclose(seen[k], ref_params[k], rtol=1e-5, atol=1e-6, err_msg=k)
