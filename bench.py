@@ -168,7 +168,9 @@ def main() -> int:
                        for p, off in zip(st.params, st.offsets)]).cpu()  # native reductions, one copy back
         dead = [i for i in range(len(st.params)) if float(norms[i]) == 0.0]
         if dead:
-            print(f"bench.py: {len(dead)} of {len(st.params)} parameters got no gradient", file=sys.stderr)
+            names = {id(p): k for k, p in m.get_params().items()}
+            print(f"bench.py: {len(dead)} of {len(st.params)} parameters got no gradient: "
+                  f"{[names.get(id(st.params[i]), i) for i in dead][:12]}", file=sys.stderr)
             return 3
     if world > 1:
         comm.barrier()

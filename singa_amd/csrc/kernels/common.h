@@ -245,6 +245,12 @@ __device__ __forceinline__ int wq_take(int* slot, int q) {
 __device__ __forceinline__ void wq_done(int* slot, int nq) {
   const int total = (int)(gridDim.x * gridDim.y * gridDim.z);
   int* done = slot + QMAX * QSTRIDE;
+  // every ticket this lane took has been PERFORMED before the done-count:
+  // a kernel that takes tickets ahead can exit with one whose result it never
+  // reads (stem_fwd_k), and the compiler does not wait for an unused return;
+  // landing after the last workgroup's reset, it would leave the counter at
+  // 1 for the next launch on this slot -- a skipped work unit
+  __builtin_amdgcn_s_waitcnt(0);
   if (__hip_atomic_fetch_add(done, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == total - 1) {
     for (int i = 0; i < nq; ++i)
       __hip_atomic_exchange(slot + i * QSTRIDE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

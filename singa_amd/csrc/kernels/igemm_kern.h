@@ -1160,6 +1160,12 @@ __global__ void __launch_bounds__(256, 1) sk_gemm_k(const GemmArgs p) {
       if (has_beta) wait_vmcnt<2 * NPS + D>(); else wait_vmcnt<NPS + D>();
       *sQ = p.wq ? xcd + 8 * (3 * G8 + ticket) : tm + 16 * G8;
     }
+    // this wave's LDS writes (staging, ticket) complete before the barrier: a
+    // raw s_barrier does not wait for them, and a ds_write issued just before
+    // it can still be in flight when another wave's ds_read after it runs
+    // (the ticket written last was read stale now and then: waves then
+    // disagreed on the next tile -- tests/test_workq_gpu.py stress test)
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0), vmcnt / expcnt untouched
     raw_barrier();  // staging complete; every wave is done reading A(it)'s slot; the ticket is in
     if (it > 0) t2 = __builtin_amdgcn_readfirstlane(*sQ);  // (wave-uniform: scalar tile math below)
     // A(it+2) into the slot A(it) just left (null resource past the end)

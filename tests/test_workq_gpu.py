@@ -125,3 +125,24 @@ def test_queue_graph_replay(gpu, lib):
         for name, (_, y) in cases.items():
             assert torch.equal(y, refs[name]), (name, rep)
     g.release()
+
+
+def test_queue_stress_back_to_back(gpu, lib):
+    """Many back-to-back launches of each persistent kernel, the output
+    NaN-filled before every launch and checked on the device (no host sync
+    in between, so kernel ends and the next launch's first tickets overlap as
+    in a training step): a ticket that lands after the last workgroup's reset
+    would skip a work unit of a later launch on that slot and leave NaN."""
+    L = lib
+    L.workq_set(1)
+    cases = _cases(L, gpu)
+    bad = torch.zeros(len(cases), dtype=torch.int32, device=gpu)
+    for ci, (name, (fn, y)) in enumerate(cases.items()):
+        fn()
+        ref = y.clone()
+        for _ in range(60):
+            y.fill_(float("nan"))
+            fn()
+            bad[ci] += (~torch.eq(y, ref)).any().int()
+    torch.cuda.synchronize()
+    assert bad.tolist() == [0] * len(cases), dict(zip(cases, bad.tolist()))

@@ -40,8 +40,64 @@ def copy_into_torch(m, tm):
     assert not missing.missing_keys or all("num_batches" in k for k in missing.missing_keys), missing
 
 
+def name_map(m):
+    """our parameter name -> the torch R50 parameter name (as copy_into_torch)."""
+    mp = {"conv1.W": "stem.0.weight", "bn1.scale": "stem.1.weight", "bn1.bias": "stem.1.bias",
+          "fc.W": "fc.weight", "fc.b": "fc.bias"}
+    for i in range(16):
+        pre = f"blocks.{i}."
+        for j in (1, 2, 3):
+            mp[pre + f"conv{j}.W"] = f"layers.{i}.c{j}.weight"
+            mp[pre + f"bn{j}.scale"] = f"layers.{i}.b{j}.weight"
+            mp[pre + f"bn{j}.bias"] = f"layers.{i}.b{j}.bias"
+        mp[pre + "down_conv.W"] = f"layers.{i}.down.0.weight"
+        mp[pre + "down_bn.scale"] = f"layers.{i}.down.1.weight"
+        mp[pre + "down_bn.bias"] = f"layers.{i}.down.1.bias"
+    return mp
+
+
+def step1_grads(m, x, y):
+    """One forward + backward of our model (no update): name -> fp32 gradient
+    in the logical (torch) layout."""
+    from singa_amd import autograd
+
+    autograd.training = True
+    try:
+        out = m.forward(x)
+        loss = m.loss_fn(out, y)
+        g = {id(p): gg.data.float().clone() for p, gg in autograd.backward(loss)}
+    finally:
+        autograd.training = False
+    res = {}
+    for k, p in m.get_params().items():
+        if id(p) in g:
+            t = g[id(p)]
+            res[k] = t.reshape(p.data.shape) if t.numel() == p.data.numel() else t
+    return res
+
+
+def grad_report(m, tm, x, y, xt, yt):
+    ours = step1_grads(m, x, y)
+    tm.zero_grad()
+    nn.functional.cross_entropy(tm(xt), yt).backward()
+    tp = dict(tm.named_parameters())
+    errs = {}
+    for k, tn in name_map(m).items():
+        if k not in ours or tn not in tp:
+            continue
+        a, b = ours[k].float(), tp[tn].grad.float()
+        if k == "fc.W":
+            b = b.t()
+        a = a.reshape(b.shape)
+        errs[k] = float((a - b).norm() / (b.norm() + 1e-30))
+    v = sorted(errs.values())
+    return {"n": len(v), "max": max(v), "median": v[len(v) // 2], "worst5": sorted(errs.items(), key=lambda kv: -kv[1])[:5],
+            "per_param": errs}
+
+
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--grads", action="store_true", help="also compare the step-1 gradient of every parameter")
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--lr", type=float, default=0.02)
@@ -67,6 +123,10 @@ def main():
             init = {k: v.data.clone() for k, v in m.get_states().items()}
             tm = R50().cuda()
             copy_into_torch(m, tm)
+            if a.grads:
+                xt0, yt0 = torch.from_numpy(X).cuda(), torch.from_numpy(Y).long().cuda()
+                out["grads_step1"] = grad_report(m, tm, x, y, xt0, yt0)
+                m.set_states(init)
         else:
             m.set_states(init)
         ls = []
