@@ -920,8 +920,10 @@ class ConvBNAddReLU(Operator):
     epilogue) and from G = g^T y, the conv's gradients from one two-source
     weight-gradient GEMM ([g | y]^T y) and one two-source data-gradient GEMM
     ([g | y] against [W^T diag(s) | -W^T diag(u) W]).  The residual's gradient
-    is g itself.  The forward is the unfused conv (BN statistics in its
-    epilogue) + BN apply; c is not kept."""
+    is g itself.  The forward: on short-K tails the conv runs twice and c is
+    never stored (F.bnres_fwd: statistics pass, then BN + residual + ReLU in
+    the GEMM epilogue); elsewhere the unfused conv (BN statistics in its
+    epilogue) + BN apply; c is not kept either way."""
 
     wants_sole = True  # the producer BN's identity-sum backward needs this op to be y's only consumer
 
@@ -934,10 +936,14 @@ class ConvBNAddReLU(Operator):
     def forward(self, y, W, gamma, beta, res):
         p = self.params[1] if len(self.params) > 1 else None
         w = p.low if (p is not None and p.low is not None and y.dtype == torch.bfloat16) else W
-        c = F.conv2d_fwd(y, w, None, (1, 1), (0, 0), (1, 1), 1, out_dtype=y.dtype, relu=False,
-                         bn_stats=_training())
-        out, st = F.batchnorm_fwd(c, gamma, beta, self.rm, self.rv, _training(), self.momentum, self.eps, True, res,
-                                  want_mask=self.requires_grad)
+        r = F.bnres_fwd(y, w, gamma, beta, self.rm, self.rv, _training(), self.momentum, self.eps, res)
+        if r is not None:  # c recomputed, never stored
+            out, st = r
+        else:
+            c = F.conv2d_fwd(y, w, None, (1, 1), (0, 0), (1, 1), 1, out_dtype=y.dtype, relu=False,
+                             bn_stats=_training())
+            out, st = F.batchnorm_fwd(c, gamma, beta, self.rm, self.rv, _training(), self.momentum, self.eps, True,
+                                      res, want_mask=self.requires_grad)
         if self.requires_grad:
             self.y, self.w, self.gamma, self.st = y, w, gamma, st
         return out

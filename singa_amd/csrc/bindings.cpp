@@ -134,6 +134,9 @@ void sg_set_dgrad_mask_out(int);
 void sg_bn_apply_cs(const void*, const void*, const void*, void*, void*, void*, int64_t, int, int, hipStream_t);
 void sg_conv_dgrad_gsum(const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int,
                         int, int, int, void*, const void*, void*, const void*, hipStream_t);
+int sg_sk_tail_ok(int, int, int);
+int sg_sk_tail(const void*, const void*, void*, void*, const void*, const void*, const void*, void*, int, int, int, int,
+               hipStream_t);
 void sg_workq_set(int);
 int sg_workq_enabled();
 int sg_cu_count();
@@ -502,6 +505,14 @@ PYBIND11_MODULE(_C, m) {
     sg_conv_dgrad_gsum(CV(dy), CV(w), V(dx), N, H, W, C, K, R, Sd, Ho, Wo, sh, sw, ph, pw, dh, dw, V(wt), CV(acc),
                        V(bn_ws), CV(mask), S(s));
     CHK("conv_dgrad_gsum");
+  });
+  // fused residual tail forward with the 1x1-conv output recomputed (pass 0: BN sums; pass 1: apply + mask)
+  m.def("sk_tail_ok", [](int M, int N, int K) { return sg_sk_tail_ok(M, N, K); });
+  m.def("sk_tail", [](P a, P w, P out, P stats, P scale, P shift, P res, P mask, int M, int N, int K, int pass, P s) {
+    const int r = sg_sk_tail(CV(a), CV(w), V(out), V(stats), CV(scale), CV(shift), CV(res), V(mask), M, N, K, pass,
+                             S(s));
+    CHK("sk_tail");
+    return r;
   });
   m.def("bn_apply_cs", [](P x, P scale, P shift, P y, P mask, P colsum, int64_t R, int C, int relu, P s) {
     sg_bn_apply_cs(CV(x), CV(scale), CV(shift), V(y), V(mask), V(colsum), R, C, relu, S(s));

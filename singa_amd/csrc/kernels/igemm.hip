@@ -238,10 +238,10 @@ static void launch_pp(const GemmArgs& p_in, int tiles, int ydim, hipStream_t s) 
 // persistent short-K launch: one workgroup per CU (the device's CU count),
 // gridDim.x a multiple of 8 (the workgroups of every column slice that share
 // an M-tile sit on one XCD); M-tiles from a dynamic queue per column slice
-template <int KT>
+template <int KT, int EPI = 0>
 static void launch_sk(const GemmArgs& p, int tiles_m, int tiles_n, hipStream_t s) {
   constexpr int lds = sk_lds(KT);
-  auto* kern = sk_gemm_k<KT>;
+  auto* kern = sk_gemm_k<KT, EPI>;
   static bool attr = [kern] {
     return hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
   }();
@@ -543,6 +543,47 @@ void sg_conv_fwd(const void* x, const void* w, void* y, const void* bias, int N,
   }
   if (out_mode == OUT_F32) launch<LM_CONV_FWD, LM_KMAJOR, OUT_F32>(p, p.M, 1, s, 1, 0);
   else launch<LM_CONV_FWD, LM_KMAJOR, OUT_BF16>(p, p.M, 1, s, 1, 0);
+}
+
+// The fused residual tail's forward with its 1x1-conv output recomputed
+// instead of stored (autograd.ConvBNAddReLU): pass 0 runs the persistent
+// short-K GEMM for the BN statistics only (stats: 32 atomic slot rows
+// [32][2][N]; no output written), pass 1 runs it again with the BN affine,
+// the residual add, the ReLU and the mask bits in the epilogue (out, mask
+// [M][N/8]).  On the stage-1/2 tails (K <= 128: the GEMM reads 64-128 bf16 per
+// output row of 256-512) the second GEMM pass costs far less HBM traffic than
+// writing and re-reading the conv output.  sg_sk_tail_ok: the shape takes the
+// persistent kernel (else the caller runs the unfused conv + BN apply).
+int sg_sk_tail_ok(int M, int N, int K) {
+  return g_tune[9] && g_tune[4] == 0 && g_tune[1] && !sg_bn_deterministic() && K <= 128 && (K & 7) == 0 &&
+         (N & 127) == 0 && (long)((M + 127) / 128) * (N / 128) >= 2048;
+}
+
+int sg_sk_tail(const void* a, const void* w, void* out, void* stats, const void* scale, const void* shift,
+               const void* res, void* mask, int M, int N, int K, int pass, hipStream_t s) {
+  if (!sg_sk_tail_ok(M, N, K)) return 0;
+  GemmArgs p{};
+  p.M = M; p.N = N; p.K = K;
+  p.a = (const bf16*)a; p.lda = K; p.b = (const bf16*)w; p.ldb = K;
+  p.ldc = N; p.alpha = 1.f; p.beta = 0.f;
+  p.k_per_split = kps(K, 1);
+  p.a_bytes = extent_bytes((int64_t)M * K);
+  p.b_bytes = extent_bytes((int64_t)N * K);
+  const int tiles_m = (M + 127) / 128;
+  if (pass == 0) {
+    p.stats = (float*)stats;
+    if (!sg_ws_prezeroed()) sg_zero_async(p.stats, sizeof(float) * 32 * 2 * N, s);
+    if (K <= 64) launch_sk<1, 0>(p, tiles_m, N / 128, s);
+    else launch_sk<2, 0>(p, tiles_m, N / 128, s);
+  } else {
+    extent_bytes((int64_t)M * N);  // (output and residual within 32-bit buffer offsets)
+    p.c = out;
+    p.ep_scale = (const float*)scale; p.ep_shift = (const float*)shift;
+    p.ep_res = (const bf16*)res; p.ep_mask = (uint8_t*)mask;
+    if (K <= 64) launch_sk<1, 1>(p, tiles_m, N / 128, s);
+    else launch_sk<2, 1>(p, tiles_m, N / 128, s);
+  }
+  return 1;
 }
 
 // conv data gradient: dy [N*Ho*Wo][K] bf16, w [K][R][S][C] bf16 -> dx [N*H*W][C]

@@ -107,6 +107,13 @@ struct GemmArgs {
   int64_t lda2;
   unsigned a2_bytes;
   int a2_split;
+  // sk_gemm_k<KT, 1> (a fused residual tail's recomputed forward): the output
+  // is relu(bf16(acc) * ep_scale[n] + ep_shift[n] + ep_res) and its ReLU mask
+  // bits ep_mask [M][N / 8] -- the conv output itself is never stored
+  const float* ep_scale;
+  const float* ep_shift;
+  const bf16* ep_res;
+  uint8_t* ep_mask;
 };
 
 // the fused activations: the formulas of elementwise.hip's unary_f / unary_b,
@@ -1024,7 +1031,12 @@ constexpr int SK_LDT = 128 + 8;                   // bf16 staging row stride (+1
 constexpr int SK_STG = 128 * SK_LDT * 2;          // output staging image
 constexpr int sk_lds(int kt) { return 3 * kt * SK_TILE + SK_STG; }
 
-template <int KT>
+// EPI 0: C = A B^T (+ beta C), optional BN statistics; with p.c == nullptr
+//        only the statistics (the stores go to a null resource: the first
+//        pass of a recomputed fused tail).
+// EPI 1: the fused residual tail's second pass: out = relu(bf16(A B^T) *
+//        scale + shift + res) and its ReLU mask bits (GemmArgs::ep_*).
+template <int KT, int EPI = 0>
 __global__ void __launch_bounds__(256, 1) sk_gemm_k(const GemmArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int BM = 128, BN = 128, NTH = 256, WN = 2, WTM = 64, WTN = 64, TM = 4, TN = 4;
@@ -1054,6 +1066,19 @@ __global__ void __launch_bounds__(256, 1) sk_gemm_k(const GemmArgs p) {
   if (tm >= tiles_m) {
     if (p.wq && threadIdx.x == 0) wq_done(p.wq, 8 * (int)gridDim.y);
     return;
+  }
+  // EPI 1: this thread's 8 columns of the BN affine, loaded (and waited
+  // for) before the first DMA so no wait for them lands inside the loop
+  float esc[8], esf[8];
+  if constexpr (EPI == 1) {
+    const int nn = n0 + (threadIdx.x % (BN / 8)) * 8;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      esc[r] = p.ep_scale[nn + r];
+      esf[r] = p.ep_shift[nn + r];
+    }
+#pragma unroll
+    for (int r = 0; r < 8; ++r) asm volatile("" ::"v"(esc[r]), "v"(esf[r]));
   }
 
   Loader<BM, LM_KMAJOR, NTH> la;
@@ -1109,15 +1134,36 @@ __global__ void __launch_bounds__(256, 1) sk_gemm_k(const GemmArgs p) {
 #pragma unroll
     for (int kt = 0; kt < KT; ++kt) la.issue(p, t1 * BM, M, kt * BK, K, P, sA + (KT + kt) * SK_TILE, live);
   }
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  // EPI 1: the residual rows of the NEXT tile, loaded one tile ahead (right
+  // after this tile's stores) so their latency hides behind a tile of work;
+  // ldc == N, host-checked -- residual and output share the row stride
+  u32x4 rres[NPS];
+  auto load_res = [&](int t) {
+    const int mt = t < tiles_m ? t : 0;
+    const __amdgpu_buffer_rsrc_t rr =
+        t < tiles_m ? make_rsrc(p.ep_res + (int64_t)mt * BM * p.ldc, (unsigned)((int64_t)min(BM, M - mt * BM) * p.ldc * 2))
+                    : rnull;
+#pragma unroll
+    for (int pass = 0; pass < NPS; ++pass)
+      rres[pass] = __builtin_amdgcn_raw_buffer_load_b128(rr, (unsigned)(((r0 + pass * RPP) * (int)p.ldc + n) * 2), 0, 0);
+  };
+  if constexpr (EPI == 1) load_res(tm);
   for (int it = 0;; ++it) {
     const int buf = it & 1;
     // A(it) landed (younger: [loads] stores(it-2), Q(it-1), A(it+1), [loads] stores(it-1);
     // it == 1: Q(0), A(2), [loads] stores(0))
-    if (it == 0) wait_vmcnt<D>();
-    else if (it == 1) {
-      if (has_beta) wait_vmcnt<2 * NPS + D + 1>(); else wait_vmcnt<NPS + D + 1>();
+    // (per-tile epilogue ops E: NPS stores, + NPS loads with beta; EPI 1: NPS
+    // output stores, NPS mask-byte stores and the next tile's NPS residual
+    // loads -- after the prologue's residual loads (NPS) of tile 0)
+    if (it == 0) {
+      if constexpr (EPI == 1) wait_vmcnt<NPS + D>(); else wait_vmcnt<D>();
+    } else if (it == 1) {
+      if constexpr (EPI == 1) wait_vmcnt<4 * NPS + D + 1>();
+      else if (has_beta) wait_vmcnt<2 * NPS + D + 1>(); else wait_vmcnt<NPS + D + 1>();
     } else {
-      if (has_beta) wait_vmcnt<4 * NPS + D + 1>(); else wait_vmcnt<2 * NPS + D + 1>();
+      if constexpr (EPI == 1) wait_vmcnt<6 * NPS + D + 1>();
+      else if (has_beta) wait_vmcnt<4 * NPS + D + 1>(); else wait_vmcnt<2 * NPS + D + 1>();
     }
     raw_barrier();  // A(it) landed for every wave; every wave is done with tile it-1
     f32x4 acc[TM][TN];
@@ -1157,8 +1203,9 @@ __global__ void __launch_bounds__(256, 1) sk_gemm_k(const GemmArgs p) {
     }
     if (it > 0 && wid == 0 && l == 0) {
       // Q(it-1) (the ticket of tile it+2) retired: younger are A(it+1) and [loads] stores(it-1)
-      if (has_beta) wait_vmcnt<2 * NPS + D>(); else wait_vmcnt<NPS + D>();
-      *sQ = p.wq ? xcd + 8 * (3 * G8 + ticket) : tm + 16 * G8;
+      if constexpr (EPI == 1) wait_vmcnt<3 * NPS + D>();
+      else if (has_beta) wait_vmcnt<2 * NPS + D>(); else wait_vmcnt<NPS + D>();
+      *sQ =p.wq ? xcd + 8 * (3 * G8 + ticket) : tm + 16 * G8;
     }
     // this wave's LDS writes (staging, ticket) complete before the barrier: a
     // raw s_barrier does not wait for them, and a ds_write issued just before
@@ -1182,31 +1229,51 @@ __global__ void __launch_bounds__(256, 1) sk_gemm_k(const GemmArgs p) {
     // (N % 128 == 0, host-checked: every column chunk is in range, and the
     // resource stays wave-uniform -- no waterfall loop around the stores)
     const __amdgpu_buffer_rsrc_t rc =
-        make_rsrc((const bf16*)p.c + (int64_t)m0 * p.ldc, (unsigned)((int64_t)rows * p.ldc * 2));
-    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+        p.c ? make_rsrc((const bf16*)p.c + (int64_t)m0 * p.ldc, (unsigned)((int64_t)rows * p.ldc * 2)) : rnull;
     u32x4 old[NPS];
-    if (has_beta) {
+    if constexpr (EPI == 1) {
+      const __amdgpu_buffer_rsrc_t rmk = make_rsrc(p.ep_mask + (int64_t)m0 * (N >> 3), (unsigned)(rows * (N >> 3)));
 #pragma unroll
-      for (int pass = 0; pass < NPS; ++pass)
-        old[pass] = __builtin_amdgcn_raw_buffer_load_b128(rc, (unsigned)(((r0 + pass * RPP) * (int)p.ldc + n) * 2), 0, 0);
-    }
-#pragma unroll
-    for (int pass = 0; pass < NPS; ++pass) {
-      const int ml = r0 + pass * RPP;
-      bf16x8 o = *(const bf16x8*)(sC + ml * SK_LDT + ch * 8);
-      if (has_beta) {
-        const bf16x8 ob = __builtin_bit_cast(bf16x8, old[pass]);
-#pragma unroll
-        for (int r = 0; r < 8; ++r) o[r] = (bf16)((float)o[r] + p.beta * (float)ob[r]);
-      }
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rc, (unsigned)((ml * (int)p.ldc + n) * 2),
-                                             0, 0);
-      if (p.stats && ml < rows) {
+      for (int pass = 0; pass < NPS; ++pass) {
+        const int ml = r0 + pass * RPP;
+        bf16x8 o = *(const bf16x8*)(sC + ml * SK_LDT + ch * 8);
+        const bf16x8 rb = __builtin_bit_cast(bf16x8, rres[pass]);
+        unsigned b = 0;
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
-          const float f = (float)o[r];
-          st_s[r] += f;
-          st_q[r] += f * f;
+          // the unfused path's arithmetic: the bf16 conv output, BN affine, + residual, ReLU
+          o[r] = (bf16)fmaxf((float)o[r] * esc[r] + esf[r] + (float)rb[r], 0.f);
+          b |= ((float)o[r] > 0.f ? 1u : 0u) << r;
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rc, (unsigned)((ml * (int)p.ldc + n) * 2),
+                                               0, 0);
+        __builtin_amdgcn_raw_buffer_store_b8((unsigned char)b, rmk, (unsigned)(ml * (N >> 3) + (n >> 3)), 0, 0);
+      }
+      load_res(t1);  // the next tile's residual (null resource past the end)
+    } else {
+      if (has_beta) {
+#pragma unroll
+        for (int pass = 0; pass < NPS; ++pass)
+          old[pass] = __builtin_amdgcn_raw_buffer_load_b128(rc, (unsigned)(((r0 + pass * RPP) * (int)p.ldc + n) * 2), 0, 0);
+      }
+#pragma unroll
+      for (int pass = 0; pass < NPS; ++pass) {
+        const int ml = r0 + pass * RPP;
+        bf16x8 o = *(const bf16x8*)(sC + ml * SK_LDT + ch * 8);
+        if (has_beta) {
+          const bf16x8 ob = __builtin_bit_cast(bf16x8, old[pass]);
+#pragma unroll
+          for (int r = 0; r < 8; ++r) o[r] = (bf16)((float)o[r] + p.beta * (float)ob[r]);
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rc, (unsigned)((ml * (int)p.ldc + n) * 2),
+                                               0, 0);
+        if (p.stats && ml < rows) {
+#pragma unroll
+          for (int r = 0; r < 8; ++r) {
+            const float f = (float)o[r];
+            st_s[r] += f;
+            st_q[r] += f * f;
+          }
         }
       }
     }
@@ -1216,7 +1283,7 @@ __global__ void __launch_bounds__(256, 1) sk_gemm_k(const GemmArgs p) {
   }
   wait_vmcnt<0>();
   if (p.wq && threadIdx.x == 0) wq_done(p.wq, 8 * (int)gridDim.y);  // every ticket of this workgroup is taken
-  if (p.stats) {
+  if (EPI == 0 && p.stats) {
     // once per workgroup: the RPP row-threads of each 8-column chunk through
     // LDS, then one atomic per column value into slot row blockIdx.x & 31
     __syncthreads();

@@ -1716,6 +1716,51 @@ def bnres_ok(y: torch.Tensor, w_shape, res: torch.Tensor) -> bool:
             and not N.lib().deterministic() and y.numel() // C * K4 * 2 < (1 << 31))
 
 
+# the tail's forward recomputes its 1x1 conv instead of storing the output
+# (bnres_fwd); switchable for A/B measurements
+TAIL_RECOMPUTE = os.environ.get("SINGA_AMD_TAIL_RECOMPUTE", "1") != "0"
+
+
+def bnres_fwd(y: torch.Tensor, w: torch.Tensor, gamma, beta, run_mean, run_var, training: bool, momentum: float,
+              eps: float, res: torch.Tensor):
+    """Training forward of the fused residual tail relu(BN(conv1x1(y, w)) +
+    res) without materialising the conv output c: the persistent short-K GEMM
+    runs twice -- once for the BN statistics only, once with the BN affine,
+    the residual add, the ReLU and the mask bits in its epilogue.  On the
+    short-K tails (stage 1/2: 64/128 input channels for 256/512 outputs) the
+    second GEMM reads y again (K bf16 per row) where the unfused path writes
+    and re-reads c (N bf16 per row each way): 4.2 vs 7.1 GB per stage-1 block
+    at batch 1024.  Results are bitwise those of the unfused path (same
+    statistics kernel, same bf16 rounding of c before the affine).  Returns
+    (out, BNState) or None when the shape does not take the persistent kernel
+    (the caller then runs conv + batchnorm_fwd)."""
+    if not (TAIL_RECOMPUTE and training and _native_ok(y, w) and y.dtype == torch.bfloat16 and y.dim() == 4
+            and N.is_cl(y) and tuple(w.shape[2:]) == (1, 1) and res is not None and res.dtype == torch.bfloat16
+            and N.is_cl(res)):
+        return None
+    if not (w.dtype == torch.bfloat16 and N.is_cl(w)):
+        w = G.to(w, torch.bfloat16, torch.channels_last)
+    Nn, C, H, W = y.shape
+    K = w.shape[0]
+    M = Nn * H * W
+    L = N.lib()
+    if w.shape[1] != C or tuple(res.shape) != (Nn, K, H, W) or not L.sk_tail_ok(M, K, C):
+        return None
+    dev = y.device
+    ws = zeroed_ws(32 * 2 * K, dev)
+    L.sk_tail(y.data_ptr(), w.data_ptr(), 0, ws.data_ptr(), 0, 0, 0, 0, M, K, C, 0, N.stream())
+    p = _mem.empty(4 * K, dtype=torch.float32, device=dev)
+    mean, invstd, scale, shift = p[:K], p[K:2 * K], p[2 * K:3 * K], p[3 * K:]
+    L.bn_fwd_from_ws(ws.data_ptr(), 32, gamma.data_ptr(), beta.data_ptr(), run_mean.data_ptr(), run_var.data_ptr(),
+                     mean.data_ptr(), invstd.data_ptr(), scale.data_ptr(), shift.data_ptr(), M, K, momentum, eps,
+                     N.stream())
+    out = _mem.empty((Nn, K, H, W), dtype=torch.bfloat16, device=dev, memory_format=torch.channels_last)
+    mask = _mem.empty(M * K // 8, dtype=torch.uint8, device=dev)
+    L.sk_tail(y.data_ptr(), w.data_ptr(), out.data_ptr(), 0, scale.data_ptr(), shift.data_ptr(), res.data_ptr(),
+              mask.data_ptr(), M, K, C, 1, N.stream())
+    return out, BNState(mean, invstd, scale, shift, mask)
+
+
 def _zeros32(n: int, device) -> torch.Tensor:
     """n zeroed fp32 (an arena slice when the step arena is active)."""
     t = ARENA.take(n, device)

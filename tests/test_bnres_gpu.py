@@ -158,3 +158,67 @@ def test_bnres_chain_matches_unfused(gpu):
             errs[f"{i}.{k}"] = rel_err(g_on[id(p)], g_off[id(p)])
     print(errs)
     assert max(errs.values()) < 3e-2, errs
+
+
+@pytest.mark.parametrize("C,K4", [(64, 256), (128, 512)])
+def test_bnres_recompute_forward_matches_unfused(gpu, C, K4):
+    """The recomputed tail forward (F.bnres_fwd: statistics-only GEMM pass,
+    then BN + residual + ReLU + mask in the second pass's epilogue) against
+    the unfused conv -> BN apply: same output, mask, running statistics and
+    gradients (up to the atomic-order rounding of the statistics)."""
+    from singa_amd import autograd as AG
+    from singa_amd import device
+    from singa_amd.ops import functional as FF
+    from singa_amd.ops import native as N
+    from singa_amd.tensor import Tensor
+
+    dev = device.create_rocm_gpu()
+    g0 = torch.Generator(device=gpu).manual_seed(3)
+    Nn, H = (42, 56) if C == 64 else (168, 28)  # enough 128-row tiles for the persistent kernel
+    y = _cl(torch.relu(torch.randn(Nn, C, H, H, device=gpu, generator=g0))).bfloat16()
+    W = (torch.randn(K4, C, 1, 1, device=gpu, generator=g0) * 0.08).bfloat16()
+    gamma = 1.0 + 0.2 * torch.randn(K4, device=gpu, generator=g0)
+    beta = 0.2 * torch.randn(K4, device=gpu, generator=g0)
+    res = _cl(torch.randn(Nn, K4, H, H, device=gpu, generator=g0)).bfloat16()
+    dout = _cl(torch.randn(Nn, K4, H, H, device=gpu, generator=g0)).bfloat16()
+    assert N.lib().sk_tail_ok(Nn * H * H, K4, C)
+    calls = [0]
+    orig = FF.bnres_fwd
+
+    def spy(*a, **k):
+        r = orig(*a, **k)
+        calls[0] += r is not None
+        return r
+
+    def run(on):
+        FF.TAIL_RECOMPUTE = on
+        rm, rv = torch.zeros(K4, device=gpu), torch.ones(K4, device=gpu)
+        AG.training = True
+        try:
+            ts = [Tensor(data=t.clone(), device=dev, requires_grad=True, stores_grad=True)
+                  for t in (y, W.float(), gamma, beta, res)]
+            op = AG.ConvBNAddReLU(rm, rv, 0.1, 1e-5)
+            out = op(*ts)
+            mask = op.st.mask.clone()
+            loss = AG.reduce_sum(AG.mul(out, Tensor(data=dout, device=dev, requires_grad=False)), None)
+            gr = {id(p): gg.data.float().clone() for p, gg in AG.backward(loss)}
+        finally:
+            AG.training = False
+        return out.data.float(), mask, rm, rv, [gr[id(t)] for t in ts]
+
+    on0 = FF.TAIL_RECOMPUTE
+    FF.bnres_fwd = spy
+    try:
+        o1, m1, rm1, rv1, g1 = run(True)
+        assert calls[0] == 1
+        o0, m0, rm0, rv0, g0_ = run(False)
+        assert calls[0] == 1  # (the unfused run did not take it)
+    finally:
+        FF.bnres_fwd = orig
+        FF.TAIL_RECOMPUTE = on0
+    assert rel_err(o1, o0) < 2e-3
+    assert (m1 != m0).float().mean().item() < 1e-3
+    assert rel_err(rm1, rm0) < 1e-4 and rel_err(rv1, rv0) < 1e-4
+    errs = [rel_err(a, b) for a, b in zip(g1, g0_)]
+    print(errs)
+    assert max(errs) < 1e-2, errs
