@@ -61,11 +61,21 @@ def step1_grads(m, x, y):
     in the logical (torch) layout."""
     from singa_amd import autograd
 
+    # the parameters' gradients accumulate into the optimizer's flat buffer,
+    # which a training step zeroes first (Optimizer.backward_and_update):
+    # zero it here too, or the yielded views hold stale contents plus this pass
+    st = getattr(m.optimizer, "store", None)
+    if st is not None:
+        st.zero_grad()
     autograd.training = True
     try:
         out = m.forward(x)
         loss = m.loss_fn(out, y)
-        g = {id(p): gg.data.float().clone() for p, gg in autograd.backward(loss)}
+        g = {}
+        for p, gg in autograd.backward(loss):
+            torch.cuda.synchronize()  # (side-stream work complete before the copy)
+            g[id(p)] = gg.data.float().clone()
+        torch.cuda.synchronize()
     finally:
         autograd.training = False
     res = {}
@@ -76,23 +86,49 @@ def step1_grads(m, x, y):
     return res
 
 
+def _summary(errs):
+    v = sorted(errs.values())
+    return {"n": len(v), "max": max(v), "median": v[len(v) // 2],
+            "worst5": sorted(errs.items(), key=lambda kv: -kv[1])[:5], "per_param": errs}
+
+
 def grad_report(m, tm, x, y, xt, yt):
+    """Step-1 gradient of every parameter against PyTorch fp32, and -- the
+    yardstick -- PyTorch's own bf16 autocast run against the same fp32
+    gradients: at random init a deep BN/ReLU network is chaotic (a rounding
+    perturbation grows layer by layer backwards), so the bf16-vs-fp32 distance
+    of the early layers' gradients is a property of the network, not of a
+    kernel; ours should sit at PyTorch bf16's own distance."""
+    import copy
+
     ours = step1_grads(m, x, y)
+    tb = copy.deepcopy(tm)
+    state = {k: v.clone() for k, v in tm.state_dict().items()}
     tm.zero_grad()
     nn.functional.cross_entropy(tm(xt), yt).backward()
-    tp = dict(tm.named_parameters())
-    errs = {}
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        lb = nn.functional.cross_entropy(tb(xt), yt)
+    lb.backward()
+    # the chaos yardstick proper: the SAME fp32 network, only its input
+    # rounded to bf16 (a 2^-9 relative perturbation of one tensor)
+    tr = copy.deepcopy(tm)
+    tr.load_state_dict(state)
+    tr.zero_grad()
+    nn.functional.cross_entropy(tr(xt.bfloat16().float()), yt).backward()
+    tm.load_state_dict(state)  # (the running statistics the forwards moved)
+    tp, tq, tz = dict(tm.named_parameters()), dict(tb.named_parameters()), dict(tr.named_parameters())
+    errs, errs_tb, errs_in = {}, {}, {}
+    rel = lambda u, v: float((u - v).norm() / (v.norm() + 1e-30))  # noqa: E731
     for k, tn in name_map(m).items():
         if k not in ours or tn not in tp:
             continue
-        a, b = ours[k].float(), tp[tn].grad.float()
+        a, b, c, d = ours[k].float(), tp[tn].grad.float(), tq[tn].grad.float(), tz[tn].grad.float()
         if k == "fc.W":
-            b = b.t()
+            b, c, d = b.t(), c.t(), d.t()
         a = a.reshape(b.shape)
-        errs[k] = float((a - b).norm() / (b.norm() + 1e-30))
-    v = sorted(errs.values())
-    return {"n": len(v), "max": max(v), "median": v[len(v) // 2], "worst5": sorted(errs.items(), key=lambda kv: -kv[1])[:5],
-            "per_param": errs}
+        errs[k], errs_tb[k], errs_in[k] = rel(a, b), rel(c, b), rel(d, b)
+    return {"ours_vs_torch_fp32": _summary(errs), "torch_bf16_autocast_vs_torch_fp32": _summary(errs_tb),
+            "torch_fp32_bf16_rounded_input_vs_torch_fp32": _summary(errs_in)}
 
 
 def main():
