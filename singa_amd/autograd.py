@@ -841,7 +841,8 @@ class Conv2d(Operator):
                   and (getattr(self, "acc_last", None) or {}).get(0, False)):
                 # residual BN: this dgrad's accumulation completes its output gradient
                 bnp = (prod.x, prod.st, prod.st.mask)
-        elif (isinstance(prod, ConvBNAddReLU) and getattr(prod, "st", None) is not None and prod.st.mask is not None
+        elif (isinstance(prod, (ConvBNAddReLU, ConvBNDualAddReLU)) and getattr(prod, "st", None) is not None
+              and prod.st.mask is not None
               and self.group == 1 and tuple(self.dilation) == (1, 1) and self.needs_grad(0)
               and ((acc is not None and (getattr(self, "acc_last", None) or {}).get(0, False))
                    or (acc is None and (getattr(self, "sole", None) or {}).get(0, False)))):
@@ -974,6 +975,78 @@ class ConvBNAddReLU(Operator):
         g._sg_fresh = True  # the residual's gradient: the engine may accumulate into it in place
         acc = lambda tgt, v: ACCUMULATED if tgt is not None else v  # noqa: E731
         return dy, acc(tw, dw), acc(tg, dg), acc(tb, db), g
+
+
+class ConvBNDualAddReLU(Operator):
+    """out = relu(BN3(conv1x1(y, W3)) + BNd(conv1x1_s(x, Wd))): a downsample
+    bottleneck's tail (main 1x1 conv + BN, strided 1x1 shortcut conv + BN) as
+    one operator, inputs y, W3, gamma3, beta3, x, Wd, gammad, betad.  Both
+    branches' backward runs algebraically as ConvBNAddReLU's (F.bnres_bwd,
+    twice, on the same masked output gradient g): no pass over either conv
+    output or its gradient -- the fused two-BN backward (bn_bwd2: a reduction
+    and an apply pass over g, c3 and cd, writing dc3 and dcd) disappears.  A
+    strided shortcut reads x at every s-th pixel: those pixels are gathered
+    once in the forward (F.strided_pick), so the shortcut is a plain GEMM and
+    its input gradient is placed back on the full grid (F.strided_place).
+    Reference block: src/worker/layer.cc:75-122 (conv + BN per layer)."""
+
+    wants_sole = True  # (y's producer BN: the identity-sum backward, as ConvBNAddReLU)
+
+    def __init__(self, bn3, bnd, stride: int, name=None):
+        super().__init__(name)
+        self.p3 = (bn3.running_mean.data, bn3.running_var.data, 1.0 - bn3.momentum, bn3.eps)
+        self.pd = (bnd.running_mean.data, bnd.running_var.data, 1.0 - bnd.momentum, bnd.eps)
+        self.stride = stride
+
+    def _low(self, i, W, like):
+        p = self.params[i] if len(self.params) > i else None
+        return p.low if (p is not None and p.low is not None and like.dtype == torch.bfloat16) else W
+
+    def forward(self, y, W3, g3, b3, x, Wd, gd, bd):
+        w3, wd = self._low(1, W3, y), self._low(5, Wd, x)
+        xs = x if self.stride == 1 else F.strided_pick(x, self.stride)
+        tr = _training()
+        c3 = F.conv2d_fwd(y, w3, None, (1, 1), (0, 0), (1, 1), 1, out_dtype=y.dtype, bn_stats=tr)
+        cd = F.conv2d_fwd(xs, wd, None, (1, 1), (0, 0), (1, 1), 1, out_dtype=y.dtype, bn_stats=tr)
+        rm, rv, mom, eps = self.p3
+        rm2, rv2, mom2, eps2 = self.pd
+        out, st3, std = F.dual_bn_add_relu_fwd(c3, g3, b3, rm, rv, cd, gd, bd, rm2, rv2, tr, mom, eps, mom2, eps2)
+        if self.requires_grad:
+            self.st = st3  # (the ReLU mask: the consuming conv's dgrad epilogue writes g with it)
+            self.saved = (y, w3, g3, xs, tuple(x.shape), wd, gd, std)
+        return out
+
+    def backward(self, dout):
+        y, w3, g3, xs, xshape, wd, gd, std = self.saved
+        st3 = self.st
+        self.saved = self.st = None
+        pre = getattr(dout, "_sg_gsum", None)
+        if pre is not None and pre[1] is st3.mask:
+            g, gws = dout, pre[0]  # masked and summed by the consuming conv's dgrad epilogue
+            del dout._sg_gsum
+        else:
+            g, gws = F.bnres_masksum(dout, st3.mask)
+        prod = self.src[0][0] if self.src else None
+        prod2 = None
+        if (isinstance(prod, BatchNorm2d) and prod.relu and not prod.has_residual and F.BN_WDOT
+                and getattr(prod, "st", None) is not None and prod.st.mask is not None
+                and getattr(prod, "beta", None) is not None and (getattr(self, "sole", None) or {}).get(0, False)
+                and self.needs_grad(0)):
+            prod2 = (prod.st.mask, prod.gamma, prod.beta)
+        cs = getattr(getattr(prod, "st", None), "colsum", None) if isinstance(prod, BatchNorm2d) else None
+        t = [self.grad_target(i) for i in (1, 2, 3, 5, 6, 7)]
+        dy, dw3, dg3, db3 = F.bnres_bwd(g, gws, y, w3, st3, g3, dw_out=t[0], dg_out=t[1], db_out=t[2], prod2=prod2,
+                                        cs=cs)
+        dxs, dwd, dgd, dbd = F.bnres_bwd(g, gws, xs, wd, std, gd, dw_out=t[3], dg_out=t[4], db_out=t[5])
+        for i, tg in ((1, t[0]), (5, t[3])):
+            if tg is not None:
+                _WGRAD_EPOCH[id(self.params[i])] = GRAD_EPOCH[0]
+        dx = None
+        if self.needs_grad(4):
+            dx = dxs if self.stride == 1 else F.strided_place(dxs, xshape, self.stride)
+        acc = lambda tgt, v: ACCUMULATED if tgt is not None else v  # noqa: E731
+        return (dy, acc(t[0], dw3), acc(t[1], dg3), acc(t[2], db3), dx, acc(t[3], dwd), acc(t[4], dgd),
+                acc(t[5], dbd))
 
 
 class DualBNAddReLU(Operator):

@@ -135,6 +135,7 @@ void sg_bn_apply_cs(const void*, const void*, const void*, void*, void*, void*, 
 void sg_conv_dgrad_gsum(const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int,
                         int, int, int, void*, const void*, void*, const void*, hipStream_t);
 int sg_sk_tail_ok(int, int, int);
+void sg_strided_pick(const void*, void*, int, int, int, int, int, int, int, int, hipStream_t);
 int sg_sk_tail(const void*, const void*, void*, void*, const void*, const void*, const void*, void*, int, int, int, int,
                hipStream_t);
 void sg_workq_set(int);
@@ -507,6 +508,10 @@ PYBIND11_MODULE(_C, m) {
     CHK("conv_dgrad_gsum");
   });
   // fused residual tail forward with the 1x1-conv output recomputed (pass 0: BN sums; pass 1: apply + mask)
+  m.def("strided_pick", [](P x, P y, int N, int H, int W, int C, int Ho, int Wo, int st, int place, P s) {
+    sg_strided_pick(CV(x), V(y), N, H, W, C, Ho, Wo, st, place, S(s));
+    CHK("strided_pick");
+  });
   m.def("sk_tail_ok", [](int M, int N, int K) { return sg_sk_tail_ok(M, N, K); });
   m.def("sk_tail", [](P a, P w, P out, P stats, P scale, P shift, P res, P mask, int M, int N, int K, int pass, P s) {
     const int r = sg_sk_tail(CV(a), CV(w), V(out), V(stats), CV(scale), CV(shift), CV(res), V(mask), M, N, K, pass,

@@ -27,6 +27,7 @@
 // Reference: the conv backward of src/worker/layer.cc:99-123 (F5 weight
 // gradient, col2im data gradient); BatchNorm / residual blocks are
 // north-star additions.
+#include <algorithm>
 #include <stdexcept>
 
 #include "igemm_kern.h"
@@ -183,6 +184,35 @@ __global__ void __launch_bounds__(256) masksum_k(const bf16* __restrict__ dy, co
   }
 }
 
+// A downsample tail's strided 1x1 shortcut conv reads only every s-th pixel:
+// pick_k gathers those pixels into a dense NHWC tensor (the shortcut then is
+// a plain GEMM, and its algebraic backward a dense two-source GEMM), place_k
+// writes the input gradient back to the full grid (zeros between).  16-byte
+// vectors, one per thread per iteration; 32-bit indices (host-checked).
+__global__ void __launch_bounds__(256) pick_k(const uint4* __restrict__ x, uint4* __restrict__ y, unsigned total,
+                                             unsigned CV, unsigned Wo, unsigned Ho, unsigned W, unsigned H,
+                                             unsigned st) {
+  for (unsigned i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
+    const unsigned c = i % CV, p = i / CV;
+    const unsigned j = p % Wo, t = p / Wo;
+    const unsigned r = t % Ho, n = t / Ho;
+    y[i] = x[((n * H + st * r) * W + st * j) * CV + c];
+  }
+}
+
+__global__ void __launch_bounds__(256) place_k(const uint4* __restrict__ xs, uint4* __restrict__ dx, unsigned total,
+                                              unsigned CV, unsigned W, unsigned H, unsigned Wo, unsigned Ho,
+                                              unsigned st) {
+  for (unsigned i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
+    const unsigned c = i % CV, p = i / CV;
+    const unsigned w = p % W, t = p / W;
+    const unsigned h = t % H, n = t / H;
+    uint4 v = {0u, 0u, 0u, 0u};
+    if (h % st == 0 && w % st == 0 && h / st < Ho && w / st < Wo) v = xs[((n * Ho + h / st) * Wo + w / st) * CV + c];
+    dx[i] = v;
+  }
+}
+
 template <int BM, int BN, int AM, int BMODE, int OUT, int NTH, int WM, int WN, int STAGES>
 void go(const GemmArgs& p, int tiles, int zdim, hipStream_t s) {
   constexpr int stages = STAGES * (BM + BN) * BK * 2;
@@ -316,6 +346,23 @@ void sg_bnres_masksum(const void* dy, const void* mask, void* g, void* ws, int64
   const int rpb = (int)((R + bands - 1) / bands);
   hipLaunchKernelGGL(masksum_k, dim3(bands, cb), dim3(256), 0, s, (const bf16*)dy, (const uint8_t*)mask, (bf16*)g,
                      (float*)ws, R, C, rpb);
+}
+
+// x [N][H][W][C] bf16 -> y [N][Ho][Wo][C] = x[:, ::st, ::st, :] (place: the
+// reverse, zeros at the other pixels of dx [N][H][W][C]); C % 8 == 0
+void sg_strided_pick(const void* x, void* y, int N, int H, int W, int C, int Ho, int Wo, int st, int place,
+                     hipStream_t s) {
+  if ((C & 7) != 0) throw std::runtime_error("strided_pick: C % 8 required");
+  const int64_t total = (int64_t)N * (place ? H * W : Ho * Wo) * (C / 8);
+  if (total >= ((int64_t)1 << 31) || (int64_t)N * H * W * (C / 8) >= ((int64_t)1 << 31))
+    throw std::runtime_error("strided_pick: tensor too large for 32-bit indexing");
+  const int blocks = (int)std::min<int64_t>((total + 255) / 256, 8192);
+  if (place)
+    hipLaunchKernelGGL(place_k, dim3(blocks), dim3(256), 0, s, (const uint4*)x, (uint4*)y, (unsigned)total,
+                       (unsigned)(C / 8), (unsigned)W, (unsigned)H, (unsigned)Wo, (unsigned)Ho, (unsigned)st);
+  else
+    hipLaunchKernelGGL(pick_k, dim3(blocks), dim3(256), 0, s, (const uint4*)x, (uint4*)y, (unsigned)total,
+                       (unsigned)(C / 8), (unsigned)Wo, (unsigned)Ho, (unsigned)W, (unsigned)H, (unsigned)st);
 }
 
 }  // extern "C"

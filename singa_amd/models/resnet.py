@@ -18,6 +18,7 @@ north-star addition.
 from __future__ import annotations
 
 import os
+from types import SimpleNamespace
 from typing import List, Sequence
 
 import torch
@@ -209,12 +210,28 @@ class Bottleneck(layer.Layer):
     def forward(self, x):
         out = self.bn1(self.conv1(x), relu=True)
         # a fused residual tail below reads bn2's output column sums (summed in its apply pass)
-        tail = not self.has_down and autograd.training and F.BNRES and x.data.is_cuda and not autograd._TRACE
+        tail = autograd.training and F.BNRES and x.data.is_cuda and not autograd._TRACE
         out = self.bn2(self.conv2(out), relu=True, colsum=tail)
+        c3 = self.conv3
         if self.has_down:
+            dc = self.down_conv
+            if (tail and os.environ.get("SINGA_FUSED_DOWN_TAIL", "1") != "0" and c3.kernel_size == (1, 1) and c3.stride == (1, 1) and tuple(c3.padding) == (0, 0)
+                    and not c3.bias and c3.group == 1 and dc.kernel_size == (1, 1) and tuple(dc.padding) == (0, 0)
+                    and dc.stride[0] == dc.stride[1] and not dc.bias and dc.group == 1
+                    and F.bnres_ok(out.data, (c3.nb_kernels, out.shape[1], 1, 1), None, down=(x.data, dc.stride[0]))):
+                # both branches of the tail as one operator with the algebraic
+                # backward (ConvBNDualAddReLU): no pass over either conv output
+                # (initialised in the unfused path's order: the same parameter-init draws)
+                k4 = SimpleNamespace(shape=(1, c3.nb_kernels), device=x.device)  # what a BN's initialize reads
+                for lyr, t in ((dc, x), (c3, out), (self.down_bn, k4), (self.bn3, k4)):
+                    if not lyr._initialized:
+                        lyr.initialize(t)
+                        lyr._initialized = True
+                b3, bd = self.bn3, self.down_bn
+                return autograd.ConvBNDualAddReLU(b3, bd, dc.stride[0])(out, c3.W, b3.scale, b3.bias, x, dc.W,
+                                                                        bd.scale, bd.bias)
             xd = self.down_conv(x)  # (creation order as before the fusion: same parameter-init draws)
             return _dual_bn_add_relu(self.bn3, self.conv3(out), self.down_bn, xd)
-        c3 = self.conv3
         if (autograd.training and not autograd._TRACE and c3.kernel_size == (1, 1) and c3.stride == (1, 1)
                 and tuple(c3.padding) == (0, 0) and not c3.bias and c3.group == 1
                 and F.bnres_ok(out.data, (c3.nb_kernels, out.shape[1], 1, 1), x.data)):

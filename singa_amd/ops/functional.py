@@ -1705,15 +1705,24 @@ def dual_bn_add_relu_bwd(x, dy, gamma, st: BNState, x2, gamma2, st2: BNState, dg
 BNRES = os.environ.get("SINGA_AMD_BNRES", "1") != "0"
 
 
-def bnres_ok(y: torch.Tensor, w_shape, res: torch.Tensor) -> bool:
+def bnres_ok(y: torch.Tensor, w_shape, res: Optional[torch.Tensor], down=None) -> bool:
     """The fused residual tail applies: native bf16 channels_last, a 1x1 /
     stride-1 conv with C % 64 == 0 inputs and K4 % 128 == 0 outputs, a
-    residual of the output's shape, non-deterministic mode."""
+    residual of the output's shape, non-deterministic mode.  ``down`` = (x,
+    stride): instead of a residual, a strided 1x1 shortcut conv of x (C_x %
+    64 == 0) onto the output grid (ConvBNDualAddReLU)."""
     K4, C = int(w_shape[0]), int(w_shape[1])
-    return (BNRES and _native_ok(y) and y.dtype == torch.bfloat16 and N.is_cl(y) and y.dim() == 4
-            and tuple(w_shape[2:]) == (1, 1) and y.shape[1] == C and C % 64 == 0 and K4 % 128 == 0
-            and res is not None and tuple(res.shape) == (y.shape[0], K4, y.shape[2], y.shape[3])
-            and not N.lib().deterministic() and y.numel() // C * K4 * 2 < (1 << 31))
+    ok = (BNRES and _native_ok(y) and y.dtype == torch.bfloat16 and N.is_cl(y) and y.dim() == 4
+          and tuple(w_shape[2:]) == (1, 1) and y.shape[1] == C and C % 64 == 0 and K4 % 128 == 0
+          and not N.lib().deterministic() and y.numel() // C * K4 * 2 < (1 << 31))
+    if not ok:
+        return False
+    if down is not None:
+        x, s = down
+        return (_native_ok(x) and x.dtype == torch.bfloat16 and x.dim() == 4 and N.is_cl(x) and x.shape[1] % 64 == 0
+                and x.shape[0] == y.shape[0] and (x.shape[2] - 1) // s + 1 == y.shape[2]
+                and (x.shape[3] - 1) // s + 1 == y.shape[3] and x.numel() * 2 < (1 << 31))
+    return res is not None and tuple(res.shape) == (y.shape[0], K4, y.shape[2], y.shape[3])
 
 
 # the tail's forward recomputes its 1x1 conv instead of storing the output
@@ -1759,6 +1768,28 @@ def bnres_fwd(y: torch.Tensor, w: torch.Tensor, gamma, beta, run_mean, run_var, 
     L.sk_tail(y.data_ptr(), w.data_ptr(), out.data_ptr(), 0, scale.data_ptr(), shift.data_ptr(), res.data_ptr(),
               mask.data_ptr(), M, K, C, 1, N.stream())
     return out, BNState(mean, invstd, scale, shift, mask)
+
+
+def strided_pick(x: torch.Tensor, stride: int) -> torch.Tensor:
+    """x[:, :, ::s, ::s] as a dense channels_last bf16 tensor (native; the
+    pixels a strided 1x1 conv reads)."""
+    Nn, C, H, W = x.shape
+    Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
+    y = _mem.empty((Nn, C, Ho, Wo), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+    N.lib().strided_pick(x.data_ptr(), y.data_ptr(), Nn, H, W, C, Ho, Wo, stride, 0, N.stream())
+    return y
+
+
+def strided_place(xs: torch.Tensor, shape, stride: int) -> torch.Tensor:
+    """The reverse of :func:`strided_pick`: a full-grid tensor of ``shape``
+    with xs at every s-th pixel and zeros between (a strided 1x1 conv's input
+    gradient)."""
+    Nn, C, H, W = shape
+    Ho, Wo = xs.shape[2], xs.shape[3]
+    dx = _mem.empty((Nn, C, H, W), dtype=xs.dtype, device=xs.device, memory_format=torch.channels_last)
+    N.lib().strided_pick(xs.data_ptr(), dx.data_ptr(), Nn, H, W, C, Ho, Wo, stride, 1, N.stream())
+    dx._sg_fresh = True
+    return dx
 
 
 def _zeros32(n: int, device) -> torch.Tensor:

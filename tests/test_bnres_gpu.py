@@ -98,7 +98,11 @@ def test_bnres_tail_matches_fp32(gpu):
     assert max(errs.values()) < 2e-2, errs
 
 
-def test_bnres_chain_matches_unfused(gpu):
+@pytest.mark.parametrize("stride", [1, 2])
+def test_bnres_chain_matches_unfused(gpu, stride):
+    """downsample block (ConvBNDualAddReLU: both tail branches algebraic, a
+    strided shortcut through strided_pick / strided_place) + two identity
+    blocks (ConvBNAddReLU), fused vs. the unfused conv -> BN path"""
     from singa_amd import autograd as AG
     from singa_amd import device
     from singa_amd.models.resnet import Bottleneck
@@ -107,9 +111,9 @@ def test_bnres_chain_matches_unfused(gpu):
 
     dev = device.create_rocm_gpu()
     dev.SetRandSeed(11)
-    blks = [Bottleneck(64, 1, True), Bottleneck(64, 1, False), Bottleneck(64, 1, False)]
+    blks = [Bottleneck(64, stride, True), Bottleneck(64, 1, False), Bottleneck(64, 1, False)]
     g0 = torch.Generator(device=gpu).manual_seed(4)
-    xf = torch.randn(8, 128, 14, 14, device=gpu, generator=g0)
+    xf = torch.randn(8, 128, 14 * stride, 14 * stride, device=gpu, generator=g0)
     dyt = None
     on0 = FF.BNRES
     calls = {"bwd": 0, "masksum": 0}
@@ -149,9 +153,10 @@ def test_bnres_chain_matches_unfused(gpu):
     finally:
         FF.bnres_bwd, FF.bnres_masksum = orig_bwd, orig_ms
     g_off = run(False)
-    # the two identity blocks ran fused; only the last (fed by the loss, no
-    # consuming conv) needed the fallback mask pass
-    assert calls == {"bwd": 2, "masksum": 1}, calls
+    # the two identity blocks ran fused, the downsample block's two branches
+    # too; only the last block (fed by the loss, no consuming conv) needed the
+    # fallback mask pass
+    assert calls == {"bwd": 4, "masksum": 1}, calls
     errs = {}
     for i, b in enumerate(blks):
         for k, p in b.get_params().items():
@@ -222,3 +227,17 @@ def test_bnres_recompute_forward_matches_unfused(gpu, C, K4):
     errs = [rel_err(a, b) for a, b in zip(g1, g0_)]
     print(errs)
     assert max(errs) < 1e-2, errs
+
+
+def test_strided_pick_place(gpu):
+    from singa_amd.ops import functional as FF
+
+    g0 = torch.Generator(device=gpu).manual_seed(5)
+    for (n, c, h, w, st) in ((2, 64, 7, 9, 2), (3, 256, 56, 56, 2), (1, 128, 5, 5, 3)):
+        x = _cl(torch.randn(n, c, h, w, device=gpu, generator=g0)).bfloat16()
+        xs = FF.strided_pick(x, st)
+        assert torch.equal(xs, x[:, :, ::st, ::st])
+        full = FF.strided_place(xs, x.shape, st)
+        ref = torch.zeros_like(x)
+        ref[:, :, ::st, ::st] = xs
+        assert torch.equal(full, ref)
