@@ -168,7 +168,9 @@ class ParamStore:
     def _build_chunks(self, chunk: int = 16384):
         starts, lens, segs = [], [], []
         lrm, wdm = [], []
+        self.chunk_lo = []  # first chunk of each parameter (update_range)
         for i, (p, o) in enumerate(zip(self.params, self.offsets)):
+            self.chunk_lo.append(len(starts))
             meta = p.param_meta or {}
             lrm.append(float(meta.get("lr_mult", 1.0)))
             wdm.append(float(meta.get("wd_mult", 1.0)))
@@ -382,6 +384,44 @@ class Optimizer:
                              float(self.step_counter + 1), gs, st.mask)
         if st.low is not None:
             st.low.copy_(st.w)
+
+    def update_range(self, i0: int, i1: int, grad_scale: Optional[float] = None) -> None:
+        """The fused update of store parameters [i0, i1) only (a contiguous
+        range of the flat buffers): the per-parameter schedule, where a
+        parameter is updated as soon as its gradient is final in the backward
+        (reference Worker::Update per param, src/worker/worker.cc:290-292)."""
+        st = self.store
+        if i0 >= i1:
+            return
+        gs = self.grad_scale if grad_scale is None else grad_scale
+        o0 = st.offsets[i0]
+        o1 = st.offsets[i1] if i1 < len(st.params) else st.numel
+        if st.gpu:
+            c0, c1 = st.chunk_lo[i0], st.chunk_lo[i1] if i1 < len(st.params) else st.nchunks
+            N.lib().opt_update(_KIND[self.kind], st.w.data_ptr(), st.g.data_ptr(), N.ptr(st.s1), N.ptr(st.s2),
+                               N.ptr(st.low), st.cstart[c0:].data_ptr(), st.clen[c0:].data_ptr(),
+                               st.cseg[c0:].data_ptr(), st.seg_lr.data_ptr(), st.seg_wd.data_ptr(),
+                               self._hp_dev.data_ptr(), c1 - c0, self.momentum, self.dampening, self.weight_decay, gs,
+                               self.beta1, self.beta2, self.eps, self.rho, int(self.nesterov), int(self.adamw),
+                               N.stream())
+            return
+        sl = slice(o0, o1)
+        w, g = st.w[sl], st.g[sl]
+        s1 = st.s1[sl] if st.s1 is not None else None
+        s2 = st.s2[sl] if st.s2 is not None else None
+        if _native_cpu() is not None and st.w.is_contiguous() and st.g.is_contiguous():
+            C = _native_cpu()
+            C.opt_update(C.updater_kind(self.kind), w.numpy(), g.numpy(), s1.numpy() if s1 is not None else None,
+                         s2.numpy() if s2 is not None else None, self.current_lr(), self.weight_decay, gs,
+                         float(self.step_counter + 1), momentum=self.momentum, dampening=self.dampening,
+                         beta1=self.beta1, beta2=self.beta2, eps=self.eps, rho=self.rho,
+                         nesterov=bool(self.nesterov), adamw=bool(self.adamw), lr_vec=st.lr_vec[sl].numpy(),
+                         wd_vec=st.wd_vec[sl].numpy(), mask=st.mask[sl].numpy().view(np.uint8))
+        else:
+            self._cpu_update(w, g, s1, s2, st.lr_vec[sl] * self.current_lr(), st.wd_vec[sl] * self.weight_decay,
+                             float(self.step_counter + 1), gs, st.mask[sl])
+        if st.low is not None:
+            st.low[sl].copy_(w)
 
     # reference math on flat fp32 buffers (CPU)
     def _cpu_update(self, w, g, s1, s2, lr, wd, t, gs, mask=None):

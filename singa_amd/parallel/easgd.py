@@ -76,7 +76,7 @@ class ElasticSync(_SyncBase):
     numbers as the synchronous one."""
 
     def __init__(self, store, comm, moving_rate: float, sync_frequency: int = 1, warmup_steps: int = 0,
-                 sharded: bool = False, overlap: bool = False):
+                 sharded: bool = False, overlap: bool = False, bucket_mb: float = 16.0):
         super().__init__(store, comm, sync_frequency, warmup_steps)
         self.ngroups = comm.world_size
         self.alpha = moving_rate / max(1, self.ngroups)
@@ -85,6 +85,9 @@ class ElasticSync(_SyncBase):
         self.centre: Optional[torch.Tensor] = None
         self._d = self._full = self._shard = None
         self._pending = None  # comm-stream event of the in-flight exchange
+        self.bucket_mb = float(bucket_mb)
+        self._buckets = None  # per-parameter schedule: [(i0, i1)] store-parameter ranges
+        self._bev: list = []  # per bucket: comm-stream event of its in-flight exchange
 
     def bootstrap(self) -> None:
         super().bootstrap()
@@ -106,10 +109,12 @@ class ElasticSync(_SyncBase):
         return self.overlap and self.store.w.is_cuda and getattr(self.comm, "comm_stream", None) is not None
 
     def wait(self) -> None:
-        """Join an in-flight overlapped exchange into the current stream."""
+        """Join every in-flight overlapped exchange into the current stream."""
         if self._pending is not None:
             self._pending.wait()  # the current stream joins the comm stream
             self._pending = None
+        for b in range(len(self._bev)):
+            self._wait_bucket(b)
 
     def _ensure_buffers(self) -> None:
         """After a checkpoint restore only the centre is set: rebuild the
@@ -148,6 +153,126 @@ class ElasticSync(_SyncBase):
         else:
             self._exchange(d)
         self.nsync += 1
+
+    # -- per-parameter schedule ---------------------------------------------
+    # The reference worker updates each parameter as soon as its gradient is
+    # final in the backward and sends it to the server right away
+    # (Worker::Update -> ParamManager::UpdateParam, src/worker/worker.cc:290-292,
+    # src/utils/param_manager.cc:192-201); the parameter's next forward use
+    # waits for the reply (WaitUpdate, param_manager.cc:204-234, worker.cc:
+    # 249-253).  Here at bucket granularity (contiguous ranges of the flat
+    # store, ~bucket_mb each, in backward completion order: the store keeps
+    # parameters in reverse creation order): a bucket whose gradients are all
+    # final is updated (Optimizer.update_range), its elastic difference taken
+    # (w -= d on the range) and its exchange (all-reduce of d, c += sum d)
+    # forked onto the comm stream -- overlapping the rest of the backward; the
+    # next forward joins each bucket's exchange just before its first layer
+    # reads it (NeuralNet.before_layer -> wait_params).  Numerically identical
+    # to update + sync() of the whole buffer (every step is elementwise).
+    def per_param_ok(self) -> bool:
+        return not self.sharded
+
+    def _setup_buckets(self) -> None:
+        st = self.store
+        lim = max(1, int(self.bucket_mb * (1 << 20) / 4))
+        self._buckets, self._pbucket = [], {}
+        i0, acc = 0, 0
+        for i, p in enumerate(st.params):
+            acc += p.data.numel()
+            self._pbucket[id(p)] = len(self._buckets)
+            if acc >= lim or i == len(st.params) - 1:
+                self._buckets.append((i0, i + 1))
+                i0, acc = i + 1, 0
+        self._bev = [None] * len(self._buckets)
+
+    def _range(self, b: int):
+        st = self.store
+        i0, i1 = self._buckets[b]
+        return st.offsets[i0], (st.offsets[i1] if i1 < len(st.params) else st.numel)
+
+    def begin_step(self, updater, step: int, grad_scale: float = 1.0) -> None:
+        """Start a per-parameter step: every bucket is updated (and, when
+        this step syncs, exchanged) as its gradients complete (on_grad)."""
+        if self._buckets is None:
+            self._setup_buckets()
+        self._upd, self._gs = updater, grad_scale
+        self._syncing = self.sync_now(step + 1)
+        # the first sync bootstraps the centre from the UPDATED weights (as
+        # sync() after a whole-buffer update does): that step runs whole-buffer
+        self._boot = self._syncing and self.centre is None
+        if self._boot:
+            self._syncing = False
+        if self._syncing:
+            self._ensure_buffers()
+            self.wait()  # (a whole-buffer exchange still in flight)
+        self._left = [i1 - i0 for i0, i1 in self._buckets]
+        self._done = [False] * len(self._buckets)
+
+    def on_grad(self, p) -> None:
+        """The engine yielded p: its gradient is final."""
+        b = self._pbucket.get(id(p))
+        if b is None or self._done[b]:
+            return
+        self._left[b] -= 1
+        if self._left[b] == 0:
+            self._finish(b)
+
+    def _finish(self, b: int) -> None:
+        i0, i1 = self._buckets[b]
+        self._upd.update_range(i0, i1, self._gs)
+        self._done[b] = True
+        if not self._syncing:
+            return
+        o0, o1 = self._range(b)
+        self._wait_bucket(b)  # (its previous exchange wrote the centre range read here)
+        w, c, d = self.store.w[o0:o1], self.centre[o0:o1], self._d[o0:o1]
+        if w.is_cuda:
+            N.lib().easgd_diff(w.data_ptr(), c.data_ptr(), d.data_ptr(), w.numel(), self.alpha, N.stream())
+        elif _cpu() is not None and w.dtype == torch.float32 and w.is_contiguous():
+            _cpu().easgd_diff(w.data_ptr(), c.data_ptr(), d.data_ptr(), w.numel(), self.alpha)
+        else:
+            d.copy_(self.alpha * (w - c))
+            w.sub_(d)
+        if self.store.low is not None:
+            G.copy_(self.store.low[o0:o1], w)
+        if self._can_overlap():
+            cs = self.comm.comm_stream
+            cs.wait_stream(torch.cuda.current_stream(w.device))
+            with cs:
+                self.comm.all_reduce(d)
+                G.binary("add", c, d, out=c)
+            self._bev[b] = _stream.Event().record(cs)
+        else:
+            self.comm.all_reduce(d)
+            G.binary("add", c, d, out=c)
+
+    def end_step(self) -> None:
+        """After the backward: buckets whose parameters got no gradient this
+        step are updated (and exchanged) now; the optimizer step advances."""
+        for b in range(len(self._buckets)):
+            if not self._done[b]:
+                self._finish(b)
+        if self._syncing:
+            self.nsync += 1
+        self._upd.step()
+        if self._boot:
+            self.sync()
+
+    def _wait_bucket(self, b: int) -> None:
+        ev = self._bev[b]
+        if ev is not None:
+            ev.wait()
+            self._bev[b] = None
+
+    def wait_params(self, params) -> None:
+        """A layer is about to read these parameters: join their buckets'
+        in-flight exchanges (WaitUpdate)."""
+        if not self._bev:
+            return
+        for p in params:
+            b = self._pbucket.get(id(p))
+            if b is not None and self._bev[b] is not None:
+                self._wait_bucket(b)
 
     def _exchange(self, d: torch.Tensor) -> None:
         """sum_ranks d -> the centre (and its gathered copy), on the current stream."""

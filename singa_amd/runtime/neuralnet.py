@@ -134,6 +134,7 @@ class NeuralNet:
         # (location l -> group rank l % size), bridges become p2p send/recv
         self.comm = comm if comm is not None and comm.world_size > 1 else None
         self.dist = self.comm is not None
+        self.before_layer = None  # hook(params) before a layer's forward (per-parameter EASGD waits)
         if self.dist:
             group_size = max(group_size, self.comm.world_size)
         self.group_size = group_size
@@ -424,6 +425,8 @@ class NeuralNet:
                         self._extra_roots.append((r, None))
                     outs[l.name] = xs[0]
                     continue
+            if self.before_layer is not None and l.params:
+                self.before_layer(l.params)  # (per-parameter EASGD: join this layer's exchange)
             outs[l.name] = l.forward(xs, training)
         self.outputs = outs
         return outs

@@ -176,8 +176,17 @@ class Worker:
                 # exchange of a sync runs behind the next step's compute
                 self.sync = ElasticSync(self.store, pc, up.moving_rate or 0.9, up.sync_frequency,
                                         up.warmup_steps, sharded=cl.sharded_centre(),
-                                        overlap=os.environ.get("SINGA_AMD_EASGD_OVERLAP", "1") != "0")
+                                        overlap=os.environ.get("SINGA_AMD_EASGD_OVERLAP", "1") != "0",
+                                        bucket_mb=float(os.environ.get("SINGA_AMD_EASGD_BUCKET_MB", "16")))
         self._setup_executors()
+        # per-parameter EASGD schedule (update + exchange per bucket as the
+        # backward completes it, joined per layer in the next forward):
+        # single-replica, unpartitioned nets with a replicated centre
+        self.easgd_pp = (isinstance(self.sync, ElasticSync) and self.sync.per_param_ok()
+                         and os.environ.get("SINGA_AMD_EASGD_GRANULARITY", "param") == "param"
+                         and len(self.replicas) == 1 and self.micro_batches <= 1 and not self.train_net.dist)
+        if self.easgd_pp:
+            self.train_net.before_layer = self.sync.wait_params
         self.perf = Performance("train")
 
     def _setup_executors(self):
@@ -308,6 +317,20 @@ class Worker:
         with Timer(self.dev) as tf:
             outs = net.forward(training=True)
             roots, seeds = net.backward_roots(outs)
+        if self.easgd_pp:
+            with Timer(self.dev) as tb:
+                self.store.zero_grad()
+                es = self.sync
+                es.begin_step(self.updater, step)
+                if roots:
+                    for p, _ in autograd.backward(roots, seeds):
+                        es.on_grad(p)  # final: update (and exchange) its bucket now
+                net.finish_step()
+                es.end_step()
+            self.timers["forward"] += tf.ms
+            self.timers["backward"] += tb.ms
+            autograd.training = False
+            return net.metrics()
         with Timer(self.dev) as tb:
             self.store.zero_grad()
             if roots:

@@ -259,6 +259,36 @@ def test_worker_two_groups(ptype):
         assert spread < 0.05
 
 
+def _worker_gran_rank(rank, world, comm, gran):
+    import os
+
+    os.environ["SINGA_AMD_EASGD_GRANULARITY"] = gran
+    os.environ["SINGA_AMD_EASGD_BUCKET_MB"] = "0.00001"  # one bucket per parameter
+    from singa_amd.config import schema
+    from singa_amd.runtime import Worker
+
+    mp_ = schema.parse_text("ModelProto", MLP_CONF % "Elastic")
+    w = Worker(mp_, comm=comm, log=lambda s: None, seed=rank,
+               data_override={"*": {"shape": (8, 8), "nclass": 10, "seed": 3}})
+    w.run()
+    nb = len(w.sync._buckets) if w.sync._buckets else 0
+    return w.easgd_pp, nb, w.sync.nsync, w.store.w.clone().numpy(), w.sync.centre.clone().numpy()
+
+
+def test_worker_easgd_per_param_equals_whole_buffer():
+    """The per-parameter schedule (update + elastic exchange per bucket as the
+    backward completes it; reference worker.cc:290-292, param_manager.cc:
+    192-234) reaches exactly the whole-buffer schedule's weights and centre."""
+    pp = run_ranks(_worker_gran_rank, 2, "param")
+    wb = run_ranks(_worker_gran_rank, 2, "buffer")
+    for r in range(2):
+        assert pp[r][0] and not wb[r][0]
+        assert pp[r][1] >= 4  # several buckets really exchanged separately
+        assert pp[r][2] == wb[r][2] >= 10
+        np.testing.assert_allclose(pp[r][3], wb[r][3], rtol=1e-6, atol=1e-7)
+        np.testing.assert_allclose(pp[r][4], wb[r][4], rtol=1e-6, atol=1e-7)
+
+
 # ------------------------------------------------------------- liveness
 def _hb_rank(rank, world, comm):
     import time
@@ -460,3 +490,4 @@ def test_cluster_synchronous_flag_all_reduces_every_step():
     for sync_dp, no_easgd, _ in res:
         assert sync_dp and no_easgd
     np.testing.assert_array_equal(res[0][2], res[1][2])
+

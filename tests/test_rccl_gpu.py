@@ -350,3 +350,53 @@ def test_loopback_easgd_overlapped_equals_synchronous(gpu, sharded):
         np.testing.assert_array_equal(ovl[r][0], sync[r][0])
         np.testing.assert_array_equal(ovl[r][1], sync[r][1])
         assert ovl[r][2]
+
+
+def _easgd_pp_rank(rank, world, comm, per_param):
+    from singa_amd import device
+    from singa_amd.opt import SGD
+    from singa_amd.parallel.easgd import ElasticSync
+    from singa_amd.tensor import Tensor
+
+    dev = device.create_rocm_gpu_on(0)
+    g = torch.Generator().manual_seed(0)
+    ps = [Tensor(device=dev, data=torch.randn(n, generator=g).to(gpu_dev()), requires_grad=True, stores_grad=True)
+          for n in (3000, 517, 4096, 64, 2000)]
+    o = SGD(0.05, 0.9, weight_decay=1e-4)
+    st = o.attach(ps)
+    es = ElasticSync(st, comm, moving_rate=0.9, sync_frequency=2, overlap=True, bucket_mb=0.01)
+    es.bootstrap()
+    gg = torch.Generator().manual_seed(rank + 1)
+    for step in range(7):
+        grads = torch.randn(st.numel, generator=gg).to(gpu_dev())
+        if per_param:
+            es.wait_params(st.params)  # (the forward's per-layer joins)
+            es.begin_step(o, step)
+            st.g.copy_(grads)
+            for p in st.params:  # the backward: store order = completion order
+                es.on_grad(p)
+            es.end_step()
+        else:
+            st.g.copy_(grads)
+            o.update()
+            o.step()
+            if es.sync_now(step + 1):
+                es.sync()
+    es.wait()
+    torch.cuda.current_stream().synchronize()
+    nb = len(es._buckets) if es._buckets else 0
+    return st.w.cpu().numpy(), es.centre.cpu().numpy(), es.nsync, nb
+
+
+def test_loopback_easgd_per_param_equals_whole_buffer(gpu):
+    """Per-bucket update + elastic exchange forked onto the comm stream as the
+    'backward' completes each bucket (events joined per parameter) == the
+    whole-buffer update + sync, exactly, at 4 ranks."""
+    from singa_amd.parallel.loop import run_ranks as loop_ranks
+
+    pp = loop_ranks(_easgd_pp_rank, 4, True, device=gpu_dev(), timeout_s=120.0)
+    wb = loop_ranks(_easgd_pp_rank, 4, False, device=gpu_dev(), timeout_s=120.0)
+    for r in range(4):
+        assert pp[r][3] >= 3 and pp[r][2] == wb[r][2] >= 3
+        np.testing.assert_array_equal(pp[r][0], wb[r][0])
+        np.testing.assert_array_equal(pp[r][1], wb[r][1])
