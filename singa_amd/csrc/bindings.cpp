@@ -46,6 +46,9 @@ void sg_gemm_heads(const void*, int64_t, int, const void*, int64_t, int, void*, 
                    const void*, int, int, int, int, int64_t, int64_t, int64_t, int, int64_t, int64_t, int64_t,
                    hipStream_t);
 void sg_lrn_rows(const void*, const void*, void*, int64_t, int, int, float, float, float, int, int, hipStream_t);
+int64_t sg_layernorm_bwd_ws(int64_t, int);
+void sg_layernorm_bwd_v2(const void*, const void*, const void*, const void*, const void*, void*, void*, void*, void*,
+                         int64_t, int, int, hipStream_t);
 void sg_layernorm_bwd(const void*, const void*, const void*, const void*, const void*, void*, void*, void*, int64_t,
                       int, int, hipStream_t);
 int sg_colreduce_bands(int64_t, int);
@@ -278,6 +281,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("layernorm_bwd", [](P x, P dy, P g, P mean, P rstd, P dx, P dg, P db, int64_t R, int D, int dt, P s) {
     sg_layernorm_bwd(CV(x), CV(dy), CV(g), CV(mean), CV(rstd), V(dx), V(dg), V(db), R, D, dt, S(s));
     CHK("layernorm_bwd");
+  });
+  m.def("layernorm_bwd_ws", [](int64_t R, int D) { return sg_layernorm_bwd_ws(R, D); });
+  m.def("layernorm_bwd_v2", [](P x, P dy, P g, P mean, P rstd, P dx, P dg, P db, P ws, int64_t R, int D, int dt, P s) {
+    sg_layernorm_bwd_v2(CV(x), CV(dy), CV(g), CV(mean), CV(rstd), V(dx), V(dg), V(db), V(ws), R, D, dt, S(s));
+    CHK("layernorm_bwd_v2");
   });
   m.def("colreduce_bands", [](int64_t R, int C) { return sg_colreduce_bands(R, C); });
   m.def("colreduce_ws", [](int64_t R, int C) { return sg_colreduce_ws(R, C); });

@@ -30,15 +30,31 @@ template <typename T> __device__ __forceinline__ T from_f32(float x);
 template <> __device__ __forceinline__ float from_f32<float>(float x) { return x; }
 template <> __device__ __forceinline__ bf16 from_f32<bf16>(float x) { return (bf16)x; }
 
+// Wave-wide all-reduce (every lane active): DPP within each 16-lane row
+// (quad_perm xor 1, xor 2, row_half_mirror, row_mirror), then the four row
+// results by readlane -- VALU-only, ~10x shorter than the six ds_bpermute
+// round trips of a shfl_xor butterfly (which dominated the wave-per-row
+// LayerNorm / softmax kernels).
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float lane_f(float v, int l) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+}
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v += dpp_f<0xB1>(v);   // quad_perm [1,0,3,2]: lane ^ 1
+  v += dpp_f<0x4E>(v);   // quad_perm [2,3,0,1]: lane ^ 2
+  v += dpp_f<0x141>(v);  // row_half_mirror: the other quad of each 8
+  v += dpp_f<0x140>(v);  // row_mirror: the other half of each 16
+  return (lane_f(v, 0) + lane_f(v, 16)) + (lane_f(v, 32) + lane_f(v, 48));
 }
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+  v = fmaxf(v, dpp_f<0xB1>(v));
+  v = fmaxf(v, dpp_f<0x4E>(v));
+  v = fmaxf(v, dpp_f<0x141>(v));
+  v = fmaxf(v, dpp_f<0x140>(v));
+  return fmaxf(fmaxf(lane_f(v, 0), lane_f(v, 16)), fmaxf(lane_f(v, 32), lane_f(v, 48)));
 }
 
 // Block-wide sum; `sh` must hold >= blockDim.x/64 floats. Result broadcast.

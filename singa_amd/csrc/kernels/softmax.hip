@@ -275,7 +275,7 @@ __global__ void __launch_bounds__(256) layernorm_fwd_rows_k(const T* __restrict_
   const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (r >= R) return;
-  float v[NJ][4];
+  float v[NJ][4], gv[NJ][4], bv[NJ][4];
   float s = 0.f;
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
@@ -286,9 +286,21 @@ __global__ void __launch_bounds__(256) layernorm_fwd_rows_k(const T* __restrict_
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[j][e] = 0.f;
     }
+  }
+  // gamma / beta as 16-byte loads issued with the row's (their latency hides
+  // behind the reductions instead of following them)
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = 4 * (lane + 64 * j);
+    const float4 g4 = (g && c < D) ? *(const float4*)(g + c) : make_float4(1.f, 1.f, 1.f, 1.f);
+    const float4 b4 = (b && c < D) ? *(const float4*)(b + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    gv[j][0] = g4.x; gv[j][1] = g4.y; gv[j][2] = g4.z; gv[j][3] = g4.w;
+    bv[j][0] = b4.x; bv[j][1] = b4.y; bv[j][2] = b4.z; bv[j][3] = b4.w;
+  }
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
 #pragma unroll
     for (int e = 0; e < 4; ++e) s += v[j][e];
-  }
   const float mu = wave_sum(s) / D;
   float q = 0.f;
 #pragma unroll
@@ -309,11 +321,7 @@ __global__ void __launch_bounds__(256) layernorm_fwd_rows_k(const T* __restrict_
     if (c < D) {
       float o[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        o[e] = (v[j][e] - mu) * rs;
-        if (g) o[e] *= g[c + e];
-        if (b) o[e] += b[c + e];
-      }
+      for (int e = 0; e < 4; ++e) o[e] = (v[j][e] - mu) * rs * gv[j][e] + bv[j][e];
       V4<T>::st(y + r * D + c, o);
     }
   }
@@ -409,6 +417,122 @@ __global__ void __launch_bounds__(256) layernorm_bwd_rows_k(const T* __restrict_
   }
 }
 
+// LayerNorm backward v2: RPW rows per wave, software-pipelined (the next
+// row's x / dy loads are issued before this row's reductions), and the
+// dgamma / dbeta partial sums of each workgroup go to its own workspace row
+// with plain stores; ln_fold_k folds the rows into dg / db (8 rows per
+// thread, one atomic per (row chunk, column)).  v1's single-level atomics
+// serialise every workgroup on the same 2D addresses, which is why it had to
+// run with few, long workgroups (latency-bound: 15 us isolated, 23 us in the
+// BERT step for a 6 MB row block).
+template <typename T, int NJ, int RPW>
+__global__ void __launch_bounds__(256) layernorm_bwd2_k(const T* __restrict__ x, const T* __restrict__ dy,
+                                                        const float* __restrict__ g, const float* __restrict__ mean,
+                                                        const float* __restrict__ rstd, T* __restrict__ dx,
+                                                        float* __restrict__ ws, int64_t R, int D) {
+  extern __shared__ float red[];  // [4 waves][2][D]
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  float gw[NJ][4], adg[NJ][4], adb[NJ][4];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = 4 * (lane + 64 * j);
+    const float4 g4 = (g && c < D) ? *(const float4*)(g + c) : make_float4(1.f, 1.f, 1.f, 1.f);
+    gw[j][0] = g4.x; gw[j][1] = g4.y; gw[j][2] = g4.z; gw[j][3] = g4.w;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { adg[j][e] = 0.f; adb[j][e] = 0.f; }
+  }
+  const int64_t rb = ((int64_t)blockIdx.x * 4 + wave) * RPW;
+  const float invD = 1.f / D;
+  float xn[NJ][4], dn[NJ][4];
+  auto load = [&](int64_t r) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int c = 4 * (lane + 64 * j);
+      if (c < D) {
+        V4<T>::ld(x + r * D + c, xn[j]);
+        V4<T>::ld(dy + r * D + c, dn[j]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { xn[j][e] = 0.f; dn[j][e] = 0.f; }
+      }
+    }
+  };
+  if (rb < R) load(rb);
+#pragma unroll
+  for (int i = 0; i < RPW; ++i) {
+    const int64_t r = rb + i;
+    if (r >= R) break;
+    float xh[NJ][4], dv[NJ][4];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { xh[j][e] = xn[j][e]; dv[j][e] = dn[j][e]; }
+    if (i + 1 < RPW && r + 1 < R) load(r + 1);  // the next row in flight during this one
+    const float mu = mean[r], rs = rstd[r];
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        xh[j][e] = (xh[j][e] - mu) * rs;
+        const float gy = dv[j][e] * gw[j][e];
+        a += gy;
+        b += gy * xh[j][e];
+      }
+    a = wave_sum(a) * invD;
+    b = wave_sum(b) * invD;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int c = 4 * (lane + 64 * j);
+      if (c < D) {
+        float o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          o[e] = rs * (dv[j][e] * gw[j][e] - a - xh[j][e] * b);
+          adg[j][e] += dv[j][e] * xh[j][e];
+          adb[j][e] += dv[j][e];
+        }
+        V4<T>::st(dx + r * D + c, o);
+      }
+    }
+  }
+  if (!ws) return;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = 4 * (lane + 64 * j);
+    if (c < D) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        red[(wave * 2) * D + c + e] = adg[j][e];
+        red[(wave * 2 + 1) * D + c + e] = adb[j][e];
+      }
+    }
+  }
+  __syncthreads();
+  float* wr = ws + (int64_t)blockIdx.x * 2 * D;
+  for (int c = threadIdx.x; c < 2 * D; c += 256) {
+    const int h = c >= D, cc = c - h * D;
+    float s = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) s += red[(w * 2 + h) * D + cc];
+    wr[c] = s;
+  }
+}
+
+__global__ void __launch_bounds__(256) ln_fold_k(const float* __restrict__ ws, int nb, int D, float* __restrict__ dg,
+                                                 float* __restrict__ db) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= 2 * D) return;
+  const int r0 = blockIdx.y * 8, r1 = r0 + 8 < nb ? r0 + 8 : nb;
+  float s = 0.f;
+  for (int r = r0; r < r1; ++r) s += ws[(int64_t)r * 2 * D + c];
+  if (c < D) {
+    if (dg) atomicAdd(dg + c, s);
+  } else if (db) {
+    atomicAdd(db + c - D, s);
+  }
+}
+
 }  // namespace sg
 
 using namespace sg;
@@ -473,13 +597,40 @@ void sg_layernorm_fwd(const void* x, const void* g, const void* b, void* y, void
 #define LNF(NJ)                                                                                                     \
   DISPATCH_FT(dtype, hipLaunchKernelGGL((layernorm_fwd_rows_k<T, NJ>), grid, dim3(256), 0, s, (const T*)x,          \
                                         (const float*)g, (const float*)b, (T*)y, (float*)mean, (float*)rstd, R, D, eps))
-    if (nj <= 1) { LNF(1); } else if (nj <= 2) { LNF(2); } else if (nj <= 4) { LNF(4); } else { LNF(8); }
+    if (nj <= 1) { LNF(1); } else if (nj <= 2) { LNF(2); } else if (nj <= 3) { LNF(3); } else if (nj <= 4) { LNF(4); }
+    else { LNF(8); }
 #undef LNF
     return;
   }
   DISPATCH_FT(dtype, hipLaunchKernelGGL(layernorm_fwd_k<T>, dim3(R), dim3(256), 0, s, (const T*)x,
                                         (const float*)g, (const float*)b, (T*)y, (float*)mean, (float*)rstd, D, eps));
 }
+// rows per wave of the v2 backward and its workspace (floats) for R x D
+static constexpr int kLnbRpw = 4;
+int64_t sg_layernorm_bwd_ws(int64_t R, int D) {
+  const int64_t nb = (R + 4 * kLnbRpw - 1) / (4 * kLnbRpw);
+  return (D % 4 == 0 && D <= 2048) ? nb * 2 * D : 0;
+}
+
+// ws (sg_layernorm_bwd_ws floats, any contents) selects the v2 kernel
+void sg_layernorm_bwd_v2(const void* x, const void* dy, const void* g, const void* mean, const void* rstd, void* dx,
+                         void* dg, void* db, void* ws, int64_t R, int D, int dtype, hipStream_t s) {
+  const int64_t nb = (R + 4 * kLnbRpw - 1) / (4 * kLnbRpw);
+  const size_t lds = (size_t)8 * D * sizeof(float);
+  const int nj = (D + 255) / 256;
+  float* w = (dg || db) ? (float*)ws : nullptr;
+#define LNB2(NJ)                                                                                                   \
+  DISPATCH_FT(dtype, hipLaunchKernelGGL((layernorm_bwd2_k<T, NJ, kLnbRpw>), dim3((unsigned)nb), dim3(256), lds, s, \
+                                        (const T*)x, (const T*)dy, (const float*)g, (const float*)mean,             \
+                                        (const float*)rstd, (T*)dx, w, R, D))
+  if (nj <= 1) { LNB2(1); } else if (nj <= 2) { LNB2(2); } else if (nj <= 3) { LNB2(3); } else if (nj <= 4) { LNB2(4); }
+  else { LNB2(8); }
+#undef LNB2
+  if (w)
+    hipLaunchKernelGGL(ln_fold_k, dim3((unsigned)((2 * D + 255) / 256), (unsigned)((nb + 7) / 8)), dim3(256), 0, s,
+                       (const float*)w, (int)nb, D, (float*)dg, (float*)db);
+}
+
 void sg_layernorm_bwd(const void* x, const void* dy, const void* g, const void* mean, const void* rstd, void* dx,
                       void* dg, void* db, int64_t R, int D, int dtype, hipStream_t s) {
   if (D % 4 == 0 && D <= 2048) {

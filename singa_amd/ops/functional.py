@@ -466,6 +466,9 @@ def layernorm_fwd(x: torch.Tensor, g: Optional[torch.Tensor], b: Optional[torch.
     return y.to(x.dtype).reshape(x.shape), mean, rstd
 
 
+LNB_V2 = os.environ.get("SINGA_AMD_LNB_V2", "1") != "0"  # (A/B switch: the v1 single-kernel backward)
+
+
 def layernorm_bwd(x, dy, g, mean, rstd, dg_acc=None, db_acc=None):
     """Returns (dx, dg, db).  ``dg_acc`` / ``db_acc``: fp32 [D] gradient
     buffers (the parameters' flat-store views) the kernel ACCUMULATES into
@@ -485,8 +488,15 @@ def layernorm_bwd(x, dy, g, mean, rstd, dg_acc=None, db_acc=None):
             dg = dg_acc if _acc_ok(dg_acc) else G.zeros((D,), torch.float32, x.device)
             db = db_acc if _acc_ok(db_acc) else G.zeros((D,), torch.float32, x.device)
         gg = G.contiguous(G.to(g, torch.float32)) if g is not None else None
-        N.lib().layernorm_bwd(x.data_ptr(), dy.data_ptr(), N.ptr(gg), mean.data_ptr(), rstd.data_ptr(),
-                              dx.data_ptr(), N.ptr(dg), N.ptr(db), R, D, N.dt(x), N.stream())
+        L = N.lib()
+        nws = L.layernorm_bwd_ws(R, D) if LNB_V2 else 0
+        if nws:  # pipelined rows, per-workgroup partial dgamma / dbeta rows folded by a second kernel
+            ws = _mem.empty(nws, dtype=torch.float32, device=x.device) if dg is not None else None
+            L.layernorm_bwd_v2(x.data_ptr(), dy.data_ptr(), N.ptr(gg), mean.data_ptr(), rstd.data_ptr(),
+                               dx.data_ptr(), N.ptr(dg), N.ptr(db), N.ptr(ws), R, D, N.dt(x), N.stream())
+        else:
+            L.layernorm_bwd(x.data_ptr(), dy.data_ptr(), N.ptr(gg), mean.data_ptr(), rstd.data_ptr(),
+                            dx.data_ptr(), N.ptr(dg), N.ptr(db), R, D, N.dt(x), N.stream())
         return dx, dg, db
     _no_native("layernorm_bwd", x, dy)
     if CP.ok(x, dy, g):
