@@ -742,9 +742,11 @@ class Linear(Operator):
             dx = G.reshape(dx, (*dy.shape[:-1], x2.shape[-1]))
         tgt = self.grad_target(1)
         tb = self.grad_target(2) if self.has_bias else None
+        # dy's column sums already summed by its producer (DropAddLayerNorm's backward)
+        cs_pre = getattr(dy, "_sg_colsum", None) if self.act is None else None
         # the bias gradient (column sums of dy) rides along with the weight
         # gradient GEMM, which stages every dy tile anyway
-        fuse_db = tb is not None and tgt is not None and tb.is_contiguous()
+        fuse_db = tb is not None and tgt is not None and tb.is_contiguous() and cs_pre is None
         if tgt is not None:
             wid = id(self.params[1])
             # first (and sole) writer of this epoch's weight gradient: write
@@ -766,7 +768,12 @@ class Linear(Operator):
             dw = F.gemm(x2, dy2, ta=True, out_dtype=torch.float32)
         res = [dx, dw]
         if self.has_bias:
-            if fuse_db:
+            if cs_pre is not None and tb is not None:
+                G.binary("add", tb, G.reshape(cs_pre, tb.shape), out=tb)
+                db = ACCUMULATED
+            elif cs_pre is not None:
+                db = cs_pre
+            elif fuse_db:
                 db = ACCUMULATED
             elif tb is not None:
                 F.colsum(dy2, out=tb)
@@ -1306,6 +1313,43 @@ class BinaryCrossEntropy(Operator):
         if dy is not None and not is_unit(dy):
             g = G.binary("mul", g, dy)
         return g, None
+
+
+class DropAddLayerNorm(Operator):
+    """y = LayerNorm(x + dropout(a)): a transformer block's residual tail as
+    one operator (inputs x, a, gamma, beta).  Forward: one pass writing the
+    sum s (the backward's input), the dropout byte mask and y -- instead of
+    dropout, add and LayerNorm passes; the mask comes from the dropout
+    kernel's Philox stream for the same (seed, offset) draw, so the numbers
+    are the unfused chain's.  Backward: one pass writing ds (x's gradient)
+    and da (a's, through the mask) and summing da's columns, handed to the
+    producing Linear as its bias gradient (``da._sg_colsum``: no separate
+    column-sum pass over da)."""
+
+    def __init__(self, ratio: float, seed_source, eps: float, name=None):
+        super().__init__(name)
+        self.ratio, self.seed_source, self.eps = ratio, seed_source, eps
+
+    def forward(self, x, a, g, b):
+        ratio, seed, off, ep = 0.0, 0, 0, None
+        if _training() and self.ratio > 0.0:
+            dev = self.seed_source
+            seed, off = dev.next_rng(a.numel()) if dev is not None else (0, 0)
+            ep = dev.rng_epoch() if dev is not None and a.is_cuda else None
+            ratio = self.ratio
+        y, s, mask, mean, rstd = F.drop_add_layernorm_fwd(x, a, g, b, self.eps, ratio, seed, off, ep)
+        if self.requires_grad:
+            self.saved = (s, g, mean, rstd, mask, ratio)
+        return y
+
+    def backward(self, dy):
+        s, g, mean, rstd, mask, ratio = self.saved
+        self.saved = None
+        tg, tb = self.grad_target(2), self.grad_target(3)
+        ds, da, dg, db, cs = F.drop_add_layernorm_bwd(s, dy, g, mean, rstd, mask, ratio, dg_acc=tg, db_acc=tb)
+        da._sg_colsum = cs
+        acc = lambda tgt, v: ACCUMULATED if tgt is not None else v  # noqa: E731
+        return ds, da, acc(tg, dg), acc(tb, db)
 
 
 class LayerNorm(Operator):

@@ -47,6 +47,10 @@ void sg_gemm_heads(const void*, int64_t, int, const void*, int64_t, int, void*, 
                    hipStream_t);
 void sg_lrn_rows(const void*, const void*, void*, int64_t, int, int, float, float, float, int, int, hipStream_t);
 int64_t sg_layernorm_bwd_ws(int64_t, int);
+void sg_drop_add_ln_fwd(const void*, const void*, const void*, const void*, void*, void*, void*, void*, void*, int64_t,
+                        int, int, float, float, uint64_t, uint64_t, const void*, hipStream_t);
+void sg_drop_add_ln_bwd(const void*, const void*, const void*, const void*, const void*, const void*, float, void*,
+                        void*, void*, void*, void*, void*, int64_t, int, int, hipStream_t);
 void sg_layernorm_bwd_v2(const void*, const void*, const void*, const void*, const void*, void*, void*, void*, void*,
                          int64_t, int, int, hipStream_t);
 void sg_layernorm_bwd(const void*, const void*, const void*, const void*, const void*, void*, void*, void*, int64_t,
@@ -283,6 +287,18 @@ PYBIND11_MODULE(_C, m) {
     CHK("layernorm_bwd");
   });
   m.def("layernorm_bwd_ws", [](int64_t R, int D) { return sg_layernorm_bwd_ws(R, D); });
+  m.def("drop_add_ln_fwd", [](P x, P a, P g, P b, P s_out, P mask, P y, P mean, P rstd, int64_t R, int D, int dt,
+                              float eps, float pkeep, uint64_t seed, uint64_t offset, P epoch, P s) {
+    sg_drop_add_ln_fwd(CV(x), CV(a), CV(g), CV(b), V(s_out), V(mask), V(y), V(mean), V(rstd), R, D, dt, eps, pkeep,
+                       seed, offset, CV(epoch), S(s));
+    CHK("drop_add_ln_fwd");
+  });
+  m.def("drop_add_ln_bwd", [](P x, P dy, P g, P mean, P rstd, P mask, float pkeep, P dx, P da, P dg, P db, P cs, P ws,
+                              int64_t R, int D, int dt, P s) {
+    sg_drop_add_ln_bwd(CV(x), CV(dy), CV(g), CV(mean), CV(rstd), CV(mask), pkeep, V(dx), V(da), V(dg), V(db), V(cs),
+                       V(ws), R, D, dt, S(s));
+    CHK("drop_add_ln_bwd");
+  });
   m.def("layernorm_bwd_v2", [](P x, P dy, P g, P mean, P rstd, P dx, P dg, P db, P ws, int64_t R, int D, int dt, P s) {
     sg_layernorm_bwd_v2(CV(x), CV(dy), CV(g), CV(mean), CV(rstd), V(dx), V(dg), V(db), V(ws), R, D, dt, S(s));
     CHK("layernorm_bwd_v2");

@@ -407,6 +407,12 @@ static void launch(const GemmArgs& p, int M, int splits, hipStream_t s, int batc
   else launch_t<64, 64, AM, BMODE, OUT, NT, 2, 2, 2, FLAGS>(p, tiles, batch, z, s);
 }
 
+// split-K of a plain fp32-atomic GEMM (a Linear's weight gradient): double
+// the splits only while the grid stays within two workgroups per CU and each
+// split keeps >= 32 K-tiles -- every split adds a full atomic pass over the
+// output.  Measured on BERT-base's four weight gradients (K = 4096 tokens,
+// tools/bert_gemm_sweep.py, profiles/r5/bert_gemm_sweep*.jsonl): the old
+// target of 768 workgroups (4 splits) ran 10-25 % slower than this rule.
 static int pick_splits(int M, int N, int K, int want) {
   if (want > 0) return want;
   int BM, BN;
@@ -414,7 +420,10 @@ static int pick_splits(int M, int N, int K, int want) {
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   int splits = 1;
   const int nkt = (K + BK - 1) / BK;
-  while (tiles * splits < 768 && splits * 2 <= nkt / 4) splits *= 2;
+  const int cap = 2 * sg_cu_count();
+  while (tiles * splits * 2 <= cap && nkt / (splits * 2) >= 32) splits *= 2;
+  if (tiles < cap / 8)  // (a tiny output: split-K is the only parallelism left)
+    while (tiles * splits < cap && nkt / (splits * 2) >= 4) splits *= 2;
   return splits;
 }
 

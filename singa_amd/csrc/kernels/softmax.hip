@@ -425,32 +425,42 @@ __global__ void __launch_bounds__(256) layernorm_bwd_rows_k(const T* __restrict_
 // serialise every workgroup on the same 2D addresses, which is why it had to
 // run with few, long workgroups (latency-bound: 15 us isolated, 23 us in the
 // BERT step for a 6 MB row block).
-template <typename T, int NJ, int RPW>
+// DROP: the LayerNorm of a residual sum s = x + dropout(a) (DropAddLayerNorm):
+// also writes a's gradient da = dx * keep / pkeep (keep: the forward's byte
+// mask, nullptr = keep all) and sums its columns -- the bias gradient of the
+// Linear that produced a -- as a third partial row.
+template <typename T, int NJ, int RPW, bool DROP = false>
 __global__ void __launch_bounds__(256) layernorm_bwd2_k(const T* __restrict__ x, const T* __restrict__ dy,
                                                         const float* __restrict__ g, const float* __restrict__ mean,
                                                         const float* __restrict__ rstd, T* __restrict__ dx,
-                                                        float* __restrict__ ws, int64_t R, int D) {
-  extern __shared__ float red[];  // [4 waves][2][D]
+                                                        float* __restrict__ ws, int64_t R, int D,
+                                                        const uint8_t* __restrict__ dmask = nullptr,
+                                                        float pkeep = 1.f, T* __restrict__ da = nullptr) {
+  constexpr int P = DROP ? 3 : 2;  // partial rows: dgamma, dbeta (, column sums of da)
+  extern __shared__ float red[];  // [4 waves][P][D]
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  float gw[NJ][4], adg[NJ][4], adb[NJ][4];
+  float gw[NJ][4], adg[NJ][4], adb[NJ][4], acs[NJ][4];
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int c = 4 * (lane + 64 * j);
     const float4 g4 = (g && c < D) ? *(const float4*)(g + c) : make_float4(1.f, 1.f, 1.f, 1.f);
     gw[j][0] = g4.x; gw[j][1] = g4.y; gw[j][2] = g4.z; gw[j][3] = g4.w;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) { adg[j][e] = 0.f; adb[j][e] = 0.f; }
+    for (int e = 0; e < 4; ++e) { adg[j][e] = 0.f; adb[j][e] = 0.f; acs[j][e] = 0.f; }
   }
   const int64_t rb = ((int64_t)blockIdx.x * 4 + wave) * RPW;
-  const float invD = 1.f / D;
+  const float invD = 1.f / D, dscale = 1.f / pkeep;
   float xn[NJ][4], dn[NJ][4];
+  uint32_t mn[NJ];
   auto load = [&](int64_t r) {
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const int c = 4 * (lane + 64 * j);
+      mn[j] = 0x01010101u;
       if (c < D) {
         V4<T>::ld(x + r * D + c, xn[j]);
         V4<T>::ld(dy + r * D + c, dn[j]);
+        if (DROP && dmask) mn[j] = *(const uint32_t*)(dmask + r * D + c);
       } else {
 #pragma unroll
         for (int e = 0; e < 4; ++e) { xn[j][e] = 0.f; dn[j][e] = 0.f; }
@@ -463,10 +473,13 @@ __global__ void __launch_bounds__(256) layernorm_bwd2_k(const T* __restrict__ x,
     const int64_t r = rb + i;
     if (r >= R) break;
     float xh[NJ][4], dv[NJ][4];
+    uint32_t mk[NJ];
 #pragma unroll
-    for (int j = 0; j < NJ; ++j)
+    for (int j = 0; j < NJ; ++j) {
+      mk[j] = mn[j];
 #pragma unroll
       for (int e = 0; e < 4; ++e) { xh[j][e] = xn[j][e]; dv[j][e] = dn[j][e]; }
+    }
     if (i + 1 < RPW && r + 1 < R) load(r + 1);  // the next row in flight during this one
     const float mu = mean[r], rs = rstd[r];
     float a = 0.f, b = 0.f;
@@ -493,6 +506,16 @@ __global__ void __launch_bounds__(256) layernorm_bwd2_k(const T* __restrict__ x,
           adb[j][e] += dv[j][e];
         }
         V4<T>::st(dx + r * D + c, o);
+        if constexpr (DROP) {
+          float q[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            // the unfused dropout backward's arithmetic on the stored dx
+            q[e] = ((mk[j] >> (8 * e)) & 0xffu) ? (float)(T)o[e] * dscale : 0.f;
+            acs[j][e] += (float)(T)q[e];
+          }
+          V4<T>::st(da + r * D + c, q);
+        }
       }
     }
   }
@@ -503,33 +526,131 @@ __global__ void __launch_bounds__(256) layernorm_bwd2_k(const T* __restrict__ x,
     if (c < D) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        red[(wave * 2) * D + c + e] = adg[j][e];
-        red[(wave * 2 + 1) * D + c + e] = adb[j][e];
+        red[(wave * P) * D + c + e] = adg[j][e];
+        red[(wave * P + 1) * D + c + e] = adb[j][e];
+        if (DROP) red[(wave * P + 2) * D + c + e] = acs[j][e];
       }
     }
   }
   __syncthreads();
-  float* wr = ws + (int64_t)blockIdx.x * 2 * D;
-  for (int c = threadIdx.x; c < 2 * D; c += 256) {
-    const int h = c >= D, cc = c - h * D;
+  float* wr = ws + (int64_t)blockIdx.x * P * D;
+  for (int c = threadIdx.x; c < P * D; c += 256) {
+    const int h = c / D, cc = c - h * D;
     float s = 0.f;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) s += red[(w * 2 + h) * D + cc];
+    for (int w = 0; w < 4; ++w) s += red[(w * P + h) * D + cc];
     wr[c] = s;
   }
 }
 
-__global__ void __launch_bounds__(256) ln_fold_k(const float* __restrict__ ws, int nb, int D, float* __restrict__ dg,
-                                                 float* __restrict__ db) {
+// fold the per-workgroup partial rows [nb][P][D] into out0 / out1 / out2 (+=)
+__global__ void __launch_bounds__(256) ln_fold_k(const float* __restrict__ ws, int nb, int D, int P,
+                                                 float* __restrict__ o0, float* __restrict__ o1,
+                                                 float* __restrict__ o2) {
   const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= 2 * D) return;
+  if (c >= P * D) return;
   const int r0 = blockIdx.y * 8, r1 = r0 + 8 < nb ? r0 + 8 : nb;
   float s = 0.f;
-  for (int r = r0; r < r1; ++r) s += ws[(int64_t)r * 2 * D + c];
-  if (c < D) {
-    if (dg) atomicAdd(dg + c, s);
-  } else if (db) {
-    atomicAdd(db + c - D, s);
+  for (int r = r0; r < r1; ++r) s += ws[(int64_t)r * P * D + c];
+  const int h = c / D;
+  float* o = h == 0 ? o0 : h == 1 ? o1 : o2;
+  if (o) atomicAdd(o + (c - h * D), s);
+}
+
+// y = LayerNorm(s), s = x + dropout(a) in one pass (one wave per row): the
+// dropout mask is the separate dropout kernel's Philox stream element for
+// element (dropout_fwd8_k: counter offset + 2 (e / 8) + ((e / 4) & 1)), and
+// every intermediate is rounded to T where the unfused chain stores it, so the
+// result is bitwise the dropout -> add -> LayerNorm chain's.  Writes s (the
+// backward's input), the byte mask, y and the row statistics.  pkeep >= 1:
+// no dropout (mask untouched).
+template <typename T, int NJ>
+__global__ void __launch_bounds__(256) drop_add_ln_fwd_k(const T* __restrict__ x, const T* __restrict__ a,
+                                                         const float* __restrict__ g, const float* __restrict__ b,
+                                                         T* __restrict__ s_out, uint8_t* __restrict__ dmask,
+                                                         T* __restrict__ y, float* __restrict__ mean,
+                                                         float* __restrict__ rstd, int64_t R, int D, float eps,
+                                                         float pkeep, uint64_t seed, uint64_t offset,
+                                                         const int64_t* __restrict__ epoch) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= R) return;
+  if (epoch) seed += (uint64_t)(*epoch) * 0x9E3779B97F4A7C15ull;
+  const bool drop = pkeep < 1.f;
+  const float scale = 1.f / pkeep;
+  float v[NJ][4], av[NJ][4];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = 4 * (lane + 64 * j);
+    if (c < D) {
+      V4<T>::ld(x + r * D + c, v[j]);
+      V4<T>::ld(a + r * D + c, av[j]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { v[j][e] = 0.f; av[j][e] = 0.f; }
+    }
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = 4 * (lane + 64 * j);
+    if (c < D) {
+      const int64_t e0 = r * D + c;
+      uint32_t mb = 0;
+      if (drop) {
+        const uint4 rr = Philox::gen(seed, offset + 2 * (uint64_t)(e0 >> 3) + (uint64_t)((e0 >> 2) & 1), 0);
+        const uint32_t w4[4] = {rr.x, rr.y, rr.z, rr.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const bool keep = Philox::u01(w4[e]) <= pkeep;
+          mb |= (uint32_t)keep << (8 * e);
+          av[j][e] = (float)(T)(keep ? av[j][e] * scale : 0.f);
+        }
+        *(uint32_t*)(dmask + e0) = mb;
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[j][e] = (float)(T)(v[j][e] + av[j][e]);
+      V4<T>::st(s_out + e0, v[j]);
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) s += v[j][e];
+  }
+  float gv[NJ][4], bv[NJ][4];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = 4 * (lane + 64 * j);
+    const float4 g4 = (g && c < D) ? *(const float4*)(g + c) : make_float4(1.f, 1.f, 1.f, 1.f);
+    const float4 b4 = (b && c < D) ? *(const float4*)(b + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    gv[j][0] = g4.x; gv[j][1] = g4.y; gv[j][2] = g4.z; gv[j][3] = g4.w;
+    bv[j][0] = b4.x; bv[j][1] = b4.y; bv[j][2] = b4.z; bv[j][3] = b4.w;
+  }
+  const float mu = wave_sum(s) / D;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = 4 * (lane + 64 * j);
+    if (c < D) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float d = v[j][e] - mu;
+        q += d * d;
+      }
+    }
+  }
+  const float rs = rsqrtf(wave_sum(q) / D + eps);
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = 4 * (lane + 64 * j);
+    if (c < D) {
+      float o[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = (v[j][e] - mu) * rs * gv[j][e] + bv[j][e];
+      V4<T>::st(y + r * D + c, o);
+    }
+  }
+  if (lane == 0) {
+    mean[r] = mu;
+    rstd[r] = rs;
   }
 }
 
@@ -622,13 +743,49 @@ void sg_layernorm_bwd_v2(const void* x, const void* dy, const void* g, const voi
 #define LNB2(NJ)                                                                                                   \
   DISPATCH_FT(dtype, hipLaunchKernelGGL((layernorm_bwd2_k<T, NJ, kLnbRpw>), dim3((unsigned)nb), dim3(256), lds, s, \
                                         (const T*)x, (const T*)dy, (const float*)g, (const float*)mean,             \
-                                        (const float*)rstd, (T*)dx, w, R, D))
+                                        (const float*)rstd, (T*)dx, w, R, D, nullptr, 1.f, nullptr))
   if (nj <= 1) { LNB2(1); } else if (nj <= 2) { LNB2(2); } else if (nj <= 3) { LNB2(3); } else if (nj <= 4) { LNB2(4); }
   else { LNB2(8); }
 #undef LNB2
   if (w)
     hipLaunchKernelGGL(ln_fold_k, dim3((unsigned)((2 * D + 255) / 256), (unsigned)((nb + 7) / 8)), dim3(256), 0, s,
-                       (const float*)w, (int)nb, D, (float*)dg, (float*)db);
+                       (const float*)w, (int)nb, D, 2, (float*)dg, (float*)db, (float*)nullptr);
+}
+
+// DropAddLayerNorm: forward (drop_add_ln_fwd_k; D % 8 == 0, D <= 2048) and
+// backward (layernorm_bwd2_k<DROP>: dx = ds, da, and dgamma / dbeta / colsum(da)
+// folded into dg / db / cs (+=; ws: sg_layernorm_bwd_ws * 3 / 2 floats))
+void sg_drop_add_ln_fwd(const void* x, const void* a, const void* g, const void* b, void* s_out, void* mask, void* y,
+                        void* mean, void* rstd, int64_t R, int D, int dtype, float eps, float pkeep, uint64_t seed,
+                        uint64_t offset, const void* epoch, hipStream_t s) {
+  const int nj = (D + 255) / 256;
+  const dim3 grid((unsigned)((R + 3) / 4));
+#define DALF(NJ)                                                                                                  \
+  DISPATCH_FT(dtype, hipLaunchKernelGGL((drop_add_ln_fwd_k<T, NJ>), grid, dim3(256), 0, s, (const T*)x,         \
+                                        (const T*)a, (const float*)g, (const float*)b, (T*)s_out, (uint8_t*)mask, \
+                                        (T*)y, (float*)mean, (float*)rstd, R, D, eps, pkeep, seed, offset,        \
+                                        (const int64_t*)epoch))
+  if (nj <= 1) { DALF(1); } else if (nj <= 2) { DALF(2); } else if (nj <= 3) { DALF(3); } else if (nj <= 4) { DALF(4); }
+  else { DALF(8); }
+#undef DALF
+}
+
+void sg_drop_add_ln_bwd(const void* x, const void* dy, const void* g, const void* mean, const void* rstd,
+                        const void* mask, float pkeep, void* dx, void* da, void* dg, void* db, void* cs, void* ws,
+                        int64_t R, int D, int dtype, hipStream_t s) {
+  const int64_t nb = (R + 4 * kLnbRpw - 1) / (4 * kLnbRpw);
+  const size_t lds = (size_t)12 * D * sizeof(float);
+  const int nj = (D + 255) / 256;
+#define LNBD(NJ)                                                                                                    \
+  DISPATCH_FT(dtype, hipLaunchKernelGGL((layernorm_bwd2_k<T, NJ, kLnbRpw, true>), dim3((unsigned)nb), dim3(256), lds, \
+                                        s, (const T*)x, (const T*)dy, (const float*)g, (const float*)mean,           \
+                                        (const float*)rstd, (T*)dx, (float*)ws, R, D, (const uint8_t*)mask, pkeep,   \
+                                        (T*)da))
+  if (nj <= 1) { LNBD(1); } else if (nj <= 2) { LNBD(2); } else if (nj <= 3) { LNBD(3); } else if (nj <= 4) { LNBD(4); }
+  else { LNBD(8); }
+#undef LNBD
+  hipLaunchKernelGGL(ln_fold_k, dim3((unsigned)((3 * D + 255) / 256), (unsigned)((nb + 7) / 8)), dim3(256), 0, s,
+                     (const float*)ws, (int)nb, D, 3, (float*)dg, (float*)db, (float*)cs);
 }
 
 void sg_layernorm_bwd(const void* x, const void* dy, const void* g, const void* mean, const void* rstd, void* dx,

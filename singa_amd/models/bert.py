@@ -19,6 +19,7 @@ import torch
 
 from .. import autograd, layer, model
 from ..tensor import Tensor
+from ..ops import functional as F
 from ..ops import glue as G
 
 
@@ -76,6 +77,19 @@ class MergeHeads(autograd.Operator):
         return super().__call__(x)
 
 
+def _drop_add_ln(x, a, drop: layer.Dropout, ln: layer.LayerNorm):
+    """ln(x + drop(a)): one fused operator on the GPU (autograd.DropAddLayerNorm,
+    same numbers; SINGA_AMD_FUSED_DAL=0 disables), the three layers otherwise
+    (and while tracing an ONNX export, which keeps the standard nodes)."""
+    if (os.environ.get("SINGA_AMD_FUSED_DAL", "1") != "0" and not autograd._TRACE and x.data.is_cuda
+            and F.drop_add_ln_ok(x.data, a.data)):
+        if not ln._initialized:
+            ln.initialize(x)
+            ln._initialized = True
+        return autograd.DropAddLayerNorm(drop.ratio, x.device, ln.eps)(x, a, ln.scale, ln.bias)
+    return ln(autograd.add(x, drop(a)))
+
+
 class EncoderLayer(layer.Layer):
     def __init__(self, hidden: int, heads: int, ffn: int, dropout: float = 0.1, fuse_gelu: Optional[bool] = None):
         super().__init__()
@@ -101,10 +115,8 @@ class EncoderLayer(layer.Layer):
         qkv = self.qkv(x)
         att = autograd.QKVAttention(self.heads)  # heads addressed in place: no split / merge copies
         a = att(qkv, mask) if mask is not None else att(qkv)
-        a = self.drop1(self.proj(a))
-        x = self.ln1(autograd.add(x, a))
-        f = self.drop2(self.fc2(self.act(self.fc1(x))))
-        return self.ln2(autograd.add(x, f))
+        x = _drop_add_ln(x, self.proj(a), self.drop1, self.ln1)
+        return _drop_add_ln(x, self.fc2(self.act(self.fc1(x))), self.drop2, self.ln2)
 
 
 class Embeddings(layer.Layer):

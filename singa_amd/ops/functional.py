@@ -466,6 +466,60 @@ def layernorm_fwd(x: torch.Tensor, g: Optional[torch.Tensor], b: Optional[torch.
     return y.to(x.dtype).reshape(x.shape), mean, rstd
 
 
+def drop_add_ln_ok(x: torch.Tensor, a: torch.Tensor) -> bool:
+    """The fused y = LayerNorm(x + dropout(a)) kernels apply (native, same
+    shape and dtype, last dim % 8 == 0 and <= 2048)."""
+    D = x.shape[-1] if x.dim() else 0
+    return (_native_ok(x, a) and x.is_cuda and x.dtype in (torch.float32, torch.bfloat16) and a.dtype == x.dtype
+            and tuple(a.shape) == tuple(x.shape) and D % 8 == 0 and 0 < D <= 2048)
+
+
+def drop_add_layernorm_fwd(x, a, g, b, eps: float, ratio: float, seed: int = 0, offset: int = 0, epoch=None):
+    """y = LayerNorm(s), s = x + dropout(a), in one pass (native; see
+    drop_add_ln_ok).  The mask is the dropout kernel's own Philox stream for
+    (seed, offset), so the result is bitwise the dropout -> add -> LayerNorm
+    chain's.  Returns (y, s, mask or None, mean, rstd)."""
+    D = x.shape[-1]
+    R = x.numel() // D
+    x, a = G.contiguous(x), G.contiguous(a)
+    s = _mem.empty_like(x)
+    y = _mem.empty_like(x)
+    mean = _mem.empty(R, dtype=torch.float32, device=x.device)
+    rstd = _mem.empty(R, dtype=torch.float32, device=x.device)
+    mask = _mem.empty(x.shape, dtype=torch.uint8, device=x.device) if ratio > 0 else None
+    gg = G.contiguous(G.to(g, torch.float32)) if g is not None else None
+    bb = G.contiguous(G.to(b, torch.float32)) if b is not None else None
+    N.lib().drop_add_ln_fwd(x.data_ptr(), a.data_ptr(), N.ptr(gg), N.ptr(bb), s.data_ptr(), N.ptr(mask), y.data_ptr(),
+                            mean.data_ptr(), rstd.data_ptr(), R, D, N.dt(x), eps, 1.0 - ratio if ratio > 0 else 1.0,
+                            seed, offset, N.ptr(epoch), N.stream())
+    return y, s, mask, mean, rstd
+
+
+def drop_add_layernorm_bwd(s, dy, g, mean, rstd, mask, ratio: float, dg_acc=None, db_acc=None):
+    """Backward of drop_add_layernorm_fwd in one pass: (ds, da, dg, db, cs) --
+    ds the gradient of x (and of s), da = ds * mask / (1 - ratio) that of a,
+    cs the column sums of da (fp32 [D]: the bias gradient of the Linear that
+    produced a); dg / db accumulate into the *_acc views when given."""
+    D = s.shape[-1]
+    R = s.numel() // D
+    L = N.lib()
+    dy = G.contiguous(G.to(dy, s.dtype))
+    ds, da = _mem.empty_like(s), _mem.empty_like(s)
+
+    def _acc(t):
+        ok = t is not None and t.dtype == torch.float32 and t.is_contiguous() and t.numel() == D and t.is_cuda
+        return t if ok else _zeros32(D, s.device)
+
+    dg, db = (_acc(dg_acc), _acc(db_acc)) if g is not None else (None, None)
+    cs = _zeros32(D, s.device)
+    ws = _mem.empty(L.layernorm_bwd_ws(R, D) * 3 // 2, dtype=torch.float32, device=s.device)
+    gg = G.contiguous(G.to(g, torch.float32)) if g is not None else None
+    L.drop_add_ln_bwd(s.data_ptr(), dy.data_ptr(), N.ptr(gg), mean.data_ptr(), rstd.data_ptr(), N.ptr(mask),
+                      1.0 - ratio if mask is not None else 1.0, ds.data_ptr(), da.data_ptr(), N.ptr(dg), N.ptr(db),
+                      cs.data_ptr(), ws.data_ptr(), R, D, N.dt(s), N.stream())
+    return ds, da, dg, db, cs
+
+
 LNB_V2 = os.environ.get("SINGA_AMD_LNB_V2", "1") != "0"  # (A/B switch: the v1 single-kernel backward)
 
 

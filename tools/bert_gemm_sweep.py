@@ -38,6 +38,8 @@ def main():
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) / iters * 1e3
 
+    SPLITS = tuple(int(v) for v in os.environ.get("SWEEP_SPLITS", "0,2,4,8").split(","))
+    kinds = os.environ.get("SWEEP_KINDS", "fwd,dgrad,wgrad").split(",")
     for name, (din, dout) in shapes.items():
         x = torch.randn(T, din, device="cuda", generator=g0).bfloat16()
         w = torch.randn(din, dout, device="cuda", generator=g0).bfloat16()
@@ -56,8 +58,10 @@ def main():
                                                       din, dout, T, 1.0, 1.0, 0, 0, 2, sp, 1, 0, 0, 0, s)),
         }
         for kind, (M, Nn, K, call) in cases.items():
+            if kind not in kinds:
+                continue
             for pol in (0, 1, 2, 3, 4, 5):
-                for sp in ((0, 2, 4, 8) if kind == "wgrad" else (1,)):
+                for sp in (SPLITS if kind == "wgrad" else (1,)):
                     L.set_tuning(4, pol)
                     try:
                         us = timeit(lambda: call(sp))
