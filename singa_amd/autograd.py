@@ -1393,7 +1393,13 @@ class Cast(Operator):
         return F.cast(x, self.to) if x.is_floating_point() else x.to(self.to)
 
     def backward(self, dy):
-        return F.cast(dy, self.from_dtype) if self.from_dtype.is_floating_point else None
+        if not self.from_dtype.is_floating_point:
+            return None
+        dx = F.cast(dy, self.from_dtype)
+        cs = getattr(dy, "_sg_colsum", None)  # (column sums a producer already took: still dx's)
+        if cs is not None and dx is not dy:
+            dx._sg_colsum = cs
+        return dx
 
 
 class ToChannelsLast(Operator):

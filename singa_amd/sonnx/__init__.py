@@ -26,6 +26,7 @@ import numpy as np
 import torch
 
 from .. import autograd, model
+from ..ops import functional as F
 from ..tensor import Tensor
 from . import onnx_proto as P
 
@@ -891,6 +892,16 @@ class _Fused:
         if self.kind == "attention":  # Transpose/MatMul/scale/[mask]/Softmax/MatMul -> batched-MFMA attention
             q, k, v = (self._low(rep, t) for t in xs[:3])
             return autograd.attention(q, k, v, xs[3] if len(xs) > 3 else None, self.scale)
+        if self.kind == "add_ln":  # [Identity] + Add + LayerNormalization -> one residual-tail operator
+            x, a, g, b = xs
+            if x.data.is_cuda and x.dtype != a.dtype and {x.dtype, a.dtype} == {torch.float32, torch.bfloat16}:
+                # (the mixed-precision import keeps the residual stream fp32: the
+                # add would promote the bf16 operand anyway)
+                x, a = (x, autograd.cast(a, torch.float32)) if x.dtype == torch.float32 else \
+                    (autograd.cast(x, torch.float32), a)
+            if not autograd._TRACE and x.data.is_cuda and F.drop_add_ln_ok(x.data, a.data):
+                return autograd.DropAddLayerNorm(0.0, None, self.scale)(x, a, g, b)
+            return autograd.layer_norm(autograd.add(x, a), g, b, self.scale)
         raise ValueError(self.kind)
 
     def __repr__(self):
@@ -1113,6 +1124,32 @@ def _fusion_plan(nodes, inits: Dict[str, Tensor], consts: set, outputs: Sequence
                 del plan[key]
                 used.update(big.members)
                 plan[max(big.members)] = big
+    # residual tails: [Identity (an exported dropout)] -> Add(x, a) ->
+    # LayerNormalization(last axis) -> one DropAddLayerNorm (one pass each
+    # way; the Linear producing a gets its bias gradient from the tail's
+    # backward): the operand a Linear group produces goes second
+    lin_outs = {st.output for st in plan.values() if st.kind in ("linear", "linear_gelu")}
+    for i, nd in enumerate(nodes):
+        if i in used or nd.op_type != "Add" or len(nd.input) != 2:
+            continue
+        j = only(nd.output[0])
+        if j is None or nodes[j].op_type != "LayerNormalization" or len(nodes[j].input) != 3:
+            continue
+        ax = int(attr(nodes[j], "axis", -1))
+        if ax != -1:
+            continue
+        members, ops = [i, j], []
+        for t in nd.input:
+            p = prod.get(t)
+            if p is not None and p not in used and nodes[p].op_type == "Identity" and single(t):
+                members.append(p)
+                t = nodes[p].input[0]
+            ops.append(t)
+        if ops[0] in lin_outs and ops[1] not in lin_outs:
+            ops.reverse()
+        used.update(members)
+        plan[max(members)] = _Fused("add_ln", members, ops + list(nodes[j].input[1:3]), nodes[j].output[0],
+                                    float(attr(nodes[j], "epsilon", 1e-5)))
     # a Linear whose output feeds only a GELU chain -> one GEMM with the GELU
     # in its epilogue (and its derivative in the consumer's data gradient)
     lin_by_out = ({st.output: k for k, st in plan.items() if st.kind == "linear"}

@@ -662,7 +662,7 @@ def test_bert_graph_matches_eager(gpu, imported):
         dev.SetRandSeed(0)
         if imported:
             m = sonnx.SONNXModel(P.load_model(blob), dev, compute_dtype=torch.bfloat16)
-            assert {st.kind for st in m.rep.fused.values()} == {"linear", "gelu", "qkv_attention"}
+            assert {st.kind for st in m.rep.fused.values()} == {"linear", "gelu", "qkv_attention", "add_ln"}
         else:
             m = bert.bert_tiny(dropout=0.0, compute_dtype=torch.bfloat16)
         ids = tensor.from_numpy(ids_np).to_device(dev)

@@ -244,9 +244,10 @@ def test_import_fusion_plan_bert_matches_unfused(monkeypatch, fuse_gelu):
         grads = {p.name: g.data.clone() for p, g in autograd.backward(loss)}
         autograd.training = False
         res.append((out.data.clone(), grads))
-    # bert_tiny: 2 layers x (qkv, proj, fc1, fc2) + pooler + classifier
+    # bert_tiny: 2 layers x (qkv, proj, fc1, fc2) + pooler + classifier; the
+    # residual tails Add -> LayerNormalization: 2 per layer + the embeddings'
     want = {"linear": 8, "linear_gelu": 2} if fuse_gelu == "1" else {"linear": 10, "gelu": 2}
-    assert kinds == {**want, "qkv_attention": 2}, kinds
+    assert kinds == {**want, "qkv_attention": 2, "add_ln": 5}, kinds
     (o0, g0), (o1, g1) = res
     np.testing.assert_allclose(o1.numpy(), o0.numpy(), atol=1e-5, rtol=1e-5)
     assert set(g0) == set(g1) and len(g0) > 20
