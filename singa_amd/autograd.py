@@ -212,9 +212,9 @@ def _accum(a, b):
         return b
     if b is None:
         return a
-    if isinstance(a, F.MaskedGrad):  # a lazy residual gradient meets another contribution
+    if isinstance(a, F.LAZY_GRADS):  # a lazy gradient meets another contribution
         a = a.materialize()
-    if isinstance(b, F.MaskedGrad):
+    if isinstance(b, F.LAZY_GRADS):
         b = b.materialize()
     if a.shape != b.shape:
         b = G.reshape(b, a.shape)
@@ -313,7 +313,7 @@ def backward(y, dy=None) -> Iterator[Tuple[Tensor, Tensor]]:
             if d is not None:
                 owned.discard(id(d))
         # a lazy residual gradient nobody absorbed reaches its producer: make it a tensor
-        dys_ = [d.materialize() if isinstance(d, F.MaskedGrad) else d for d in dys_]
+        dys_ = [d.materialize() if isinstance(d, F.LAZY_GRADS) else d for d in dys_]
         if all(d is None for d in dys_) and not getattr(op, "always_run", False):
             dxs = (None,) * len(op.src)
         else:
@@ -866,7 +866,7 @@ class Conv2d(Operator):
         if acc is not None and getattr(dx, "_sg_absorbed", None) is acc:
             del dx._sg_absorbed
             dx = AccReplace(dx)  # the dgrad summed acc into its own fresh output
-        elif acc is not None and (dx is acc or (isinstance(acc, F.MaskedGrad) and acc.value is not None
+        elif acc is not None and (dx is acc or (isinstance(acc, F.LAZY_GRADS) and acc.value is not None
                                                 and dx is acc.value)):
             # summed in place into the pending gradient (a lazy residual
             # gradient the dgrad materialised holds the sum as its value)
@@ -1050,7 +1050,9 @@ class ConvBNDualAddReLU(Operator):
                 _WGRAD_EPOCH[id(self.params[i])] = GRAD_EPOCH[0]
         dx = None
         if self.needs_grad(4):
-            dx = dxs if self.stride == 1 else F.strided_place(dxs, xshape, self.stride)
+            # (strided: kept compact -- the block's conv1 dgrad epilogue adds it)
+            dx = dxs if self.stride == 1 else (F.StridedGrad(dxs, self.stride, xshape) if F.STRIDED_LAZY
+                                               else F.strided_place(dxs, xshape, self.stride))
         acc = lambda tgt, v: ACCUMULATED if tgt is not None else v  # noqa: E731
         return (dy, acc(t[0], dw3), acc(t[1], dg3), acc(t[2], db3), dx, acc(t[3], dwd), acc(t[4], dgd),
                 acc(t[5], dbd))

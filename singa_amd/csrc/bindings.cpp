@@ -140,7 +140,7 @@ void sg_bnres_masksum(const void*, const void*, void*, void*, int64_t, int, hipS
 void sg_set_dgrad_mask_out(int);
 void sg_bn_apply_cs(const void*, const void*, const void*, void*, void*, void*, int64_t, int, int, hipStream_t);
 void sg_conv_dgrad_gsum(const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int,
-                        int, int, int, void*, const void*, void*, const void*, hipStream_t);
+                        int, int, int, void*, const void*, void*, const void*, int, int, int, hipStream_t);
 int sg_sk_tail_ok(int, int, int);
 void sg_strided_pick(const void*, void*, int, int, int, int, int, int, int, int, hipStream_t);
 int sg_sk_tail(const void*, const void*, void*, void*, const void*, const void*, const void*, void*, int, int, int, int,
@@ -526,9 +526,10 @@ PYBIND11_MODULE(_C, m) {
   });
   // dgrad completing a fused residual tail's output gradient: (dgrad + acc) * bit, summed (stats_mode 4)
   m.def("conv_dgrad_gsum", [](P dy, P w, P dx, int N, int H, int W, int C, int K, int R, int Sd, int Ho, int Wo,
-                              int sh, int sw, int ph, int pw, int dh, int dw, P wt, P acc, P bn_ws, P mask, P s) {
+                              int sh, int sw, int ph, int pw, int dh, int dw, P wt, P acc, P bn_ws, P mask, int acc_s,
+                              int acc_Ho, int acc_Wo, P s) {
     sg_conv_dgrad_gsum(CV(dy), CV(w), V(dx), N, H, W, C, K, R, Sd, Ho, Wo, sh, sw, ph, pw, dh, dw, V(wt), CV(acc),
-                       V(bn_ws), CV(mask), S(s));
+                       V(bn_ws), CV(mask), acc_s, acc_Ho, acc_Wo, S(s));
     CHK("conv_dgrad_gsum");
   });
   // fused residual tail forward with the 1x1-conv output recomputed (pass 0: BN sums; pass 1: apply + mask)

@@ -185,6 +185,7 @@ static int g_tune[12] = {5, 1, 1, 0, 0, 1, 8, 1, 0, 1, 0, 0};
 static thread_local int g_wt_ready = 0;
 // one-shot (per OS thread): the next dgrad adds this masked residual gradient
 static thread_local const bf16* g_res_g = nullptr;
+static thread_local int g_res_s = 1, g_res_Ho = 0, g_res_Wo = 0;  // (compact strided res_g, sg_conv_dgrad_gsum)
 static thread_local const uint8_t* g_res_mask = nullptr;
 // one-shot (per OS thread): the next dgrad with a mask-only BN producer writes
 // its output masked (stats_mode 4, the algebraic residual-BN backward's g~)
@@ -658,12 +659,19 @@ int sg_conv_dgrad_res(const void* dy, const void* w, void* dx, int N, int H, int
 // the other consumers' gradient `acc` (bf16, or nullptr) is added from its
 // own buffer like the lazy residual gradient (so the single-stage short-K
 // variant, beta == 0, still applies).
+// acc_s > 1 (1x1 stride-1 convs only): acc is compact, [N][acc_Ho][acc_Wo][C] at every
+// acc_s-th pixel (a strided shortcut's input gradient, never placed on the full grid)
 void sg_conv_dgrad_gsum(const void* dy, const void* w, void* dx, int N, int H, int W, int C, int K, int R, int S,
                         int Ho, int Wo, int sh, int sw, int ph, int pw, int dh, int dw, void* wt, const void* acc,
-                        void* bn_ws, const void* mask, hipStream_t s) {
+                        void* bn_ws, const void* mask, int acc_s, int acc_Ho, int acc_Wo, hipStream_t s) {
+  if (acc_s > 1 && (R != 1 || S != 1 || sh != 1 || sw != 1 || ph != 0 || pw != 0 || !acc))
+    throw std::runtime_error("conv_dgrad_gsum: a strided accumulator needs a 1x1 stride-1 conv");
   g_res_g = (const bf16*)acc;
   g_res_mask = nullptr;
   g_mask_out = 1;
+  g_res_s = acc_s > 1 ? acc_s : 1;
+  g_res_Ho = acc_Ho;
+  g_res_Wo = acc_Wo;
   sg_conv_dgrad_bn_ex(dy, w, dx, N, H, W, C, K, R, S, Ho, Wo, sh, sw, ph, pw, dh, dw, OUT_BF16, 0.f, wt, bn_ws,
                       nullptr, nullptr, nullptr, nullptr, nullptr, mask, s);
 }
@@ -684,8 +692,15 @@ void sg_conv_dgrad_bn_ex(const void* dy, const void* w, void* dx, int N, int H, 
   GemmArgs p{};
   p.res_g = g_res_g;  // one-shot residual-gradient source (sg_conv_dgrad_res)
   p.res_mask = g_res_mask;
+  p.res_s = g_res_s;
+  if (p.res_s > 1) {
+    p.res_H = H; p.res_W = W; p.res_Ho = g_res_Ho; p.res_Wo = g_res_Wo;
+    p.res_dW = FastDiv((uint32_t)W);
+    p.res_dH = FastDiv((uint32_t)H);
+  }
   g_res_g = nullptr;
   g_res_mask = nullptr;
+  g_res_s = 1;
   if (bn_ws && out_mode == OUT_BF16 && (beta == 0.f || bn_mask) && (C & 7) == 0 && g_tune[1] &&
       !sg_bn_deterministic()) {
     p.stats = (float*)bn_ws;

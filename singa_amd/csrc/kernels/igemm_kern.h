@@ -84,6 +84,11 @@ struct GemmArgs {
   // the BN backward never writes it as a tensor
   const bf16* res_g;
   const uint8_t* res_mask;
+  // res_s > 1: res_g is COMPACT -- the gradient of a strided 1x1 shortcut's
+  // input, [N][Ho][Wo][C] at every res_s-th pixel of this output's H x W grid
+  // (rows = pixels, 1x1 stride-1 data gradient); the other pixels add nothing
+  int res_s, res_H, res_W, res_Ho, res_Wo;
+  FastDiv res_dW, res_dH;
   const uint8_t* bnb_mask;
   const bf16* bnb_x;
   const float *bnb_mean, *bnb_invstd, *bnb_scale, *bnb_shift;

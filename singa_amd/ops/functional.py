@@ -1177,6 +1177,17 @@ def conv2d_bwd(x: torch.Tensor, w: torch.Tensor, dy: torch.Tensor, stride, paddi
     sh, sw = stride
     ph, pw = padding
     dh, dw_ = dilation
+    strided = None
+    if isinstance(dx_acc, StridedGrad):
+        # kept compact only into a gmask (fused-tail) dgrad of a 1x1 / stride-1 conv
+        if (need_dx and dx_acc.value is None and bn_producer is not None and isinstance(bn_producer[0], str)
+                and bn_producer[0] == "gmask" and _native_ok(x, w, dy) and groups == 1
+                and x.dtype == torch.bfloat16 and tuple(w.shape[2:]) == (1, 1) and sh == sw == 1 and ph == pw == 0
+                and dh == dw_ == 1 and tuple(dx_acc.shape) == tuple(x.shape) and dx_acc.dtype == torch.bfloat16
+                and x.shape[1] % 8 == 0 and not N.lib().deterministic()):
+            strided = dx_acc
+        else:
+            dx_acc = dx_acc.materialize()
     if isinstance(dx_acc, MaskedGrad):
         K_, C_ = w.shape[0], w.shape[1]
         if (need_dx and _native_ok(x, w, dy) and groups == 1 and x.dtype == torch.bfloat16 and C_ % 8 == 0
@@ -1226,10 +1237,12 @@ def conv2d_bwd(x: torch.Tensor, w: torch.Tensor, dy: torch.Tensor, stride, paddi
                 bn_producer = None
                 if not (od == torch.bfloat16 and Cx == Cp and C % 8 == 0 and not padded
                         and not N.lib().deterministic()
-                        and (dx_acc is None or (dx_acc.dtype == od and tuple(dx_acc.shape) == tuple(x.shape)
-                                                and N.is_cl(dx_acc)
-                                                and dx_acc.is_contiguous(memory_format=torch.channels_last)))):
+                        and (dx_acc is None or strided is not None
+                             or (dx_acc.dtype == od and tuple(dx_acc.shape) == tuple(x.shape) and N.is_cl(dx_acc)
+                                 and dx_acc.is_contiguous(memory_format=torch.channels_last)))):
                     gmask = None  # (the consumer then masks and sums the gradient itself)
+                    if strided is not None:
+                        dx_acc, strided = strided.materialize(), None
             if gmask is not None:
                 # the consumer is a fused residual tail (ConvBNAddReLU): this dgrad
                 # completes its output gradient, so the epilogue writes it masked
@@ -1239,9 +1252,11 @@ def conv2d_bwd(x: torch.Tensor, w: torch.Tensor, dy: torch.Tensor, stride, paddi
                 # variant stays available; the caller replaces dx_acc by it)
                 dxp = _mem.empty((Nn, Cp, H, W), dtype=od, device=x.device, memory_format=torch.channels_last)
                 bws = zeroed_ws(32 * 2 * C, x.device)
+                acc_t, acc_s = (strided.g, strided.stride) if strided is not None else (dx_acc, 1)
                 N.lib().conv_dgrad_gsum(dyb.data_ptr(), wb.data_ptr(), dxp.data_ptr(), Nn, H, W, Cp, Kp, R, S, Ho,
-                                        Wo, sh, sw, ph, pw, dh, dw_, N.ptr(wt), N.ptr(dx_acc), bws.data_ptr(),
-                                        gmask.data_ptr(), N.stream())
+                                        Wo, sh, sw, ph, pw, dh, dw_, N.ptr(wt), N.ptr(acc_t), bws.data_ptr(),
+                                        gmask.data_ptr(), acc_s, acc_t.shape[2] if acc_t is not None else 0,
+                                        acc_t.shape[3] if acc_t is not None else 0, N.stream())
                 dxp._sg_gsum = (bws, gmask)
                 dxp._sg_fresh = True
                 if dx_acc is not None:
@@ -1542,6 +1557,34 @@ class MaskedGrad:
             self.value = out
             self.g = self.mask = None
         return self.value
+
+
+class StridedGrad:
+    """The input gradient of a strided 1x1 shortcut conv kept COMPACT: g is
+    [N, C, H/s, W/s] (every s-th pixel of the input grid; zero elsewhere).  A
+    consuming 1x1 conv's data gradient adds it in its epilogue straight from
+    the compact tensor (conv_dgrad_gsum with acc_s = s), so the full-grid
+    tensor -- three quarters zeros -- is never written nor read back.  Any
+    other consumer gets :meth:`materialize` (strided_place)."""
+
+    _sg_fresh = True  # the engine owns it exclusively
+
+    def __init__(self, g: torch.Tensor, stride: int, shape):
+        self.g, self.stride, self.value = g, int(stride), None
+        self.shape, self.dtype, self.device = torch.Size(shape), g.dtype, g.device
+
+    def is_floating_point(self) -> bool:
+        return True
+
+    def materialize(self) -> torch.Tensor:
+        if self.value is None:
+            self.value = strided_place(self.g, tuple(self.shape), self.stride)
+            self.g = None
+        return self.value
+
+
+STRIDED_LAZY = os.environ.get("SINGA_AMD_STRIDED_LAZY", "1") != "0"  # (A/B: place the shortcut gradient eagerly)
+LAZY_GRADS = (MaskedGrad, StridedGrad)  # gradient placeholders the autograd engine materialises on demand
 
 
 def _bn_native(x: torch.Tensor) -> bool:
