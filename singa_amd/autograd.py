@@ -1013,11 +1013,17 @@ class ConvBNDualAddReLU(Operator):
         w3, wd = self._low(1, W3, y), self._low(5, Wd, x)
         xs = x if self.stride == 1 else F.strided_pick(x, self.stride)
         tr = _training()
-        c3 = F.conv2d_fwd(y, w3, None, (1, 1), (0, 0), (1, 1), 1, out_dtype=y.dtype, bn_stats=tr)
-        cd = F.conv2d_fwd(xs, wd, None, (1, 1), (0, 0), (1, 1), 1, out_dtype=y.dtype, bn_stats=tr)
         rm, rv, mom, eps = self.p3
         rm2, rv2, mom2, eps2 = self.pd
-        out, st3, std = F.dual_bn_add_relu_fwd(c3, g3, b3, rm, rv, cd, gd, bd, rm2, rv2, tr, mom, eps, mom2, eps2)
+        r = (F.bnres_dual_fwd(y, w3, g3, b3, rm, rv, mom, eps, xs, wd, gd, bd, rm2, rv2, mom2, eps2, tr)
+             if self.stride == 1 else None)
+        if r is not None:  # both conv outputs recomputed, never stored
+            out, st3, std = r
+        else:
+            c3 = F.conv2d_fwd(y, w3, None, (1, 1), (0, 0), (1, 1), 1, out_dtype=y.dtype, bn_stats=tr)
+            cd = F.conv2d_fwd(xs, wd, None, (1, 1), (0, 0), (1, 1), 1, out_dtype=y.dtype, bn_stats=tr)
+            out, st3, std = F.dual_bn_add_relu_fwd(c3, g3, b3, rm, rv, cd, gd, bd, rm2, rv2, tr, mom, eps, mom2,
+                                                   eps2)
         if self.requires_grad:
             self.st = st3  # (the ReLU mask: the consuming conv's dgrad epilogue writes g with it)
             self.saved = (y, w3, g3, xs, tuple(x.shape), wd, gd, std)

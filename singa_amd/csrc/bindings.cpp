@@ -142,6 +142,10 @@ void sg_bn_apply_cs(const void*, const void*, const void*, void*, void*, void*, 
 void sg_conv_dgrad_gsum(const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int,
                         int, int, int, void*, const void*, void*, const void*, int, int, int, hipStream_t);
 int sg_sk_tail_ok(int, int, int);
+int sg_sk_tail2(const void*, const void*, const void*, const void*, const void*, void*, void*, int, int, int, int,
+                hipStream_t);
+void sg_bnres_fold(const void*, const void*, const void*, const void*, const void*, const void*, int, int, int, void*,
+                   void*, void*, hipStream_t);
 void sg_strided_pick(const void*, void*, int, int, int, int, int, int, int, int, hipStream_t);
 int sg_sk_tail(const void*, const void*, void*, void*, const void*, const void*, const void*, void*, int, int, int, int,
                hipStream_t);
@@ -538,6 +542,15 @@ PYBIND11_MODULE(_C, m) {
     CHK("strided_pick");
   });
   m.def("sk_tail_ok", [](int M, int N, int K) { return sg_sk_tail_ok(M, N, K); });
+  m.def("sk_tail2", [](P y, P x, P wf, P shift, P ones, P out, P mask, int M, int N, int K1, int K2, P s) {
+    const int r = sg_sk_tail2(CV(y), CV(x), CV(wf), CV(shift), CV(ones), V(out), V(mask), M, N, K1, K2, S(s));
+    CHK("sk_tail2");
+    return r;
+  });
+  m.def("bnres_fold", [](P w3, P wd, P s3, P f3, P sd, P fd, int N, int K1, int K2, P wf, P shift, P ones, P s) {
+    sg_bnres_fold(CV(w3), CV(wd), CV(s3), CV(f3), CV(sd), CV(fd), N, K1, K2, V(wf), V(shift), V(ones), S(s));
+    CHK("bnres_fold");
+  });
   m.def("sk_tail", [](P a, P w, P out, P stats, P scale, P shift, P res, P mask, int M, int N, int K, int pass, P s) {
     const int r = sg_sk_tail(CV(a), CV(w), V(out), V(stats), CV(scale), CV(shift), CV(res), V(mask), M, N, K, pass,
                              S(s));

@@ -213,6 +213,24 @@ __global__ void __launch_bounds__(256) place_k(const uint4* __restrict__ xs, uin
   }
 }
 
+// The two-branch tail's folded weights: wf[n] = [bf16(s3[n] W3[n]) | bf16(sd[n] Wd[n])],
+// shift[n] = f3[n] + fd[n], ones[n] = 1 (the apply pass's unit scale)
+__global__ void __launch_bounds__(256) fold_k(const bf16* __restrict__ w3, const bf16* __restrict__ wd,
+                                             const float* __restrict__ s3, const float* __restrict__ f3,
+                                             const float* __restrict__ sd, const float* __restrict__ fd, int N,
+                                             int K1, int K2, bf16* __restrict__ wf, float* __restrict__ shift,
+                                             float* __restrict__ ones) {
+  const int n = blockIdx.x;
+  const int K = K1 + K2;
+  for (int k = threadIdx.x; k < K; k += 256)
+    wf[(int64_t)n * K + k] = k < K1 ? (bf16)(s3[n] * (float)w3[(int64_t)n * K1 + k])
+                                    : (bf16)(sd[n] * (float)wd[(int64_t)n * K2 + k - K1]);
+  if (threadIdx.x == 0) {
+    shift[n] = f3[n] + fd[n];
+    ones[n] = 1.f;
+  }
+}
+
 template <int BM, int BN, int AM, int BMODE, int OUT, int NTH, int WM, int WN, int STAGES>
 void go(const GemmArgs& p, int tiles, int zdim, hipStream_t s) {
   constexpr int stages = STAGES * (BM + BN) * BK * 2;
@@ -363,6 +381,13 @@ void sg_strided_pick(const void* x, void* y, int N, int H, int W, int C, int Ho,
   else
     hipLaunchKernelGGL(pick_k, dim3(blocks), dim3(256), 0, s, (const uint4*)x, (uint4*)y, (unsigned)total,
                        (unsigned)(C / 8), (unsigned)Wo, (unsigned)Ho, (unsigned)W, (unsigned)H, (unsigned)st);
+}
+
+void sg_bnres_fold(const void* w3, const void* wd, const void* s3, const void* f3, const void* sd, const void* fd, int N,
+                   int K1, int K2, void* wf, void* shift, void* ones, hipStream_t s) {
+  hipLaunchKernelGGL(fold_k, dim3(N), dim3(256), 0, s, (const bf16*)w3, (const bf16*)wd, (const float*)s3,
+                     (const float*)f3, (const float*)sd, (const float*)fd, N, K1, K2, (bf16*)wf, (float*)shift,
+                     (float*)ones);
 }
 
 }  // extern "C"

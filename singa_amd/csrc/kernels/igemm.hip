@@ -239,10 +239,10 @@ static void launch_pp(const GemmArgs& p_in, int tiles, int ydim, hipStream_t s) 
 // persistent short-K launch: one workgroup per CU (the device's CU count),
 // gridDim.x a multiple of 8 (the workgroups of every column slice that share
 // an M-tile sit on one XCD); M-tiles from a dynamic queue per column slice
-template <int KT, int EPI = 0>
+template <int KT, int EPI = 0, int AM = LM_KMAJOR>
 static void launch_sk(const GemmArgs& p, int tiles_m, int tiles_n, hipStream_t s) {
   constexpr int lds = sk_lds(KT);
-  auto* kern = sk_gemm_k<KT, EPI>;
+  auto* kern = sk_gemm_k<KT, EPI, AM>;
   static bool attr = [kern] {
     return hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
   }();
@@ -593,6 +593,32 @@ int sg_sk_tail(const void* a, const void* w, void* out, void* stats, const void*
     if (K <= 64) launch_sk<1, 1>(p, tiles_m, N / 128, s);
     else launch_sk<2, 1>(p, tiles_m, N / 128, s);
   }
+  return 1;
+}
+
+// The two-branch (downsample) tail's recomputed apply pass: out = relu(bf16([y | x] .
+// wf^T) + shift) and its mask, K = K1 + K2 <= 128 (K1 % 64 == 0): wf [N][K1 + K2]
+// holds both branches' weights with their BN scales folded in (bnres.hip
+// fold_k), shift the sum of both BN shifts.  Returns 0 when the persistent
+// kernel does not take the shape.
+int sg_sk_tail2(const void* y, const void* x, const void* wf, const void* shift, const void* ones, void* out,
+                void* mask, int M, int N, int K1, int K2, hipStream_t s) {
+  const int K = K1 + K2;
+  if (!sg_sk_tail_ok(M, N, K) || (K1 & 63) != 0 || K1 <= 0 || K2 <= 0) return 0;
+  GemmArgs p{};
+  p.M = M; p.N = N; p.K = K;
+  p.a = (const bf16*)y; p.lda = K1; p.a2 = (const bf16*)x; p.lda2 = K2; p.a2_split = K1;
+  p.b = (const bf16*)wf; p.ldb = K;
+  p.ldc = N; p.alpha = 1.f; p.beta = 0.f;
+  p.k_per_split = kps(K, 1);
+  p.a_bytes = extent_bytes((int64_t)M * K1);
+  p.a2_bytes = extent_bytes((int64_t)M * K2);
+  p.b_bytes = extent_bytes((int64_t)N * K);
+  extent_bytes((int64_t)M * N);
+  p.c = out;
+  p.ep_scale = (const float*)ones; p.ep_shift = (const float*)shift;
+  p.ep_res = nullptr; p.ep_mask = (uint8_t*)mask;
+  launch_sk<2, 1, LM_KMAJOR2>(p, (M + 127) / 128, N / 128, s);
   return 1;
 }
 

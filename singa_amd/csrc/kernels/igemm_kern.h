@@ -1041,7 +1041,9 @@ constexpr int sk_lds(int kt) { return 3 * kt * SK_TILE + SK_STG; }
 //        pass of a recomputed fused tail).
 // EPI 1: the fused residual tail's second pass: out = relu(bf16(A B^T) *
 //        scale + shift + res) and its ReLU mask bits (GemmArgs::ep_*).
-template <int KT, int EPI = 0>
+// AM: LM_KMAJOR, or LM_KMAJOR2 -- A from two sources split at p.a2_split
+// (a multiple of 64): the two-branch tail [y | x] . [W3' | Wd']^T
+template <int KT, int EPI = 0, int AM = LM_KMAJOR>
 __global__ void __launch_bounds__(256, 1) sk_gemm_k(const GemmArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int BM = 128, BN = 128, NTH = 256, WN = 2, WTM = 64, WTN = 64, TM = 4, TN = 4;
@@ -1086,7 +1088,7 @@ __global__ void __launch_bounds__(256, 1) sk_gemm_k(const GemmArgs p) {
     for (int r = 0; r < 8; ++r) asm volatile("" ::"v"(esc[r]), "v"(esf[r]));
   }
 
-  Loader<BM, LM_KMAJOR, NTH> la;
+  Loader<BM, AM, NTH> la;
   Loader<BN, LM_KMAJOR, NTH> lb;
   lb.init(p, n0, N, P, p.ldb, p.b, p.b_bytes);
 #pragma unroll
@@ -1121,7 +1123,7 @@ __global__ void __launch_bounds__(256, 1) sk_gemm_k(const GemmArgs p) {
   // resource (dropped) -- every wave's count stays uniform.  Every per-tile
   // count is uniform: out-of-range rows go through buffer stores / loads that
   // the resource drops, tiles past the end are DMA'd from a null resource.
-  constexpr int D = KT * Loader<BM, LM_KMAJOR, NTH>::VPT;  // DMA instructions per tile
+  constexpr int D = KT * Loader<BM, AM, NTH>::VPT;  // DMA instructions per tile
   const bool has_beta = p.beta != 0.f;
   const __amdgpu_buffer_rsrc_t rnull = make_rsrc(nullptr, 0);
   int ticket = 0;  // wave 0 lane 0: the last queue op's result
@@ -1146,9 +1148,10 @@ __global__ void __launch_bounds__(256, 1) sk_gemm_k(const GemmArgs p) {
   u32x4 rres[NPS];
   auto load_res = [&](int t) {
     const int mt = t < tiles_m ? t : 0;
-    const __amdgpu_buffer_rsrc_t rr =
-        t < tiles_m ? make_rsrc(p.ep_res + (int64_t)mt * BM * p.ldc, (unsigned)((int64_t)min(BM, M - mt * BM) * p.ldc * 2))
-                    : rnull;
+    const __amdgpu_buffer_rsrc_t rr =  // (no residual: loads of zeros, the count stays uniform)
+        t < tiles_m && p.ep_res
+            ? make_rsrc(p.ep_res + (int64_t)mt * BM * p.ldc, (unsigned)((int64_t)min(BM, M - mt * BM) * p.ldc * 2))
+            : rnull;
 #pragma unroll
     for (int pass = 0; pass < NPS; ++pass)
       rres[pass] = __builtin_amdgcn_raw_buffer_load_b128(rr, (unsigned)(((r0 + pass * RPP) * (int)p.ldc + n) * 2), 0, 0);

@@ -1877,6 +1877,54 @@ def bnres_fwd(y: torch.Tensor, w: torch.Tensor, gamma, beta, run_mean, run_var, 
     return out, BNState(mean, invstd, scale, shift, mask)
 
 
+def bnres_dual_fwd(y, w3, g3, b3, rm3, rv3, mom3, eps3, x, wd, gd, bd, rmd, rvd, momd, epsd, training: bool):
+    """Training forward of the two-branch (downsample, stride-1) tail
+    relu(BN3(conv1x1(y, w3)) + BNd(conv1x1(x, wd))) with neither conv output
+    stored: one statistics-only persistent-GEMM pass per branch, then ONE pass
+    over the two-source operand [y | x] against both branches' weights with
+    their BN scales folded in, BN shifts + ReLU + mask in the epilogue
+    (sk_tail2; K = C_y + C_x <= 128: ResNet-50's stage-1 downsample block).
+    Same statistics as the unfused path; the output differs only by the bf16
+    rounding of the folded weights.  Returns (out, st3, std) or None."""
+    if not (TAIL_RECOMPUTE and training and _native_ok(y, w3, x, wd) and y.dtype == torch.bfloat16
+            and x.dtype == torch.bfloat16 and y.dim() == 4 and x.dim() == 4 and N.is_cl(y) and N.is_cl(x)
+            and tuple(w3.shape[2:]) == (1, 1) and tuple(wd.shape[2:]) == (1, 1)):
+        return None
+    Nn, C1, H, W = y.shape
+    C2 = x.shape[1]
+    K4 = w3.shape[0]
+    M = Nn * H * W
+    L = N.lib()
+    if (tuple(x.shape) != (Nn, C2, H, W) or w3.shape[1] != C1 or tuple(wd.shape[:2]) != (K4, C2) or C1 % 64 != 0
+            or not L.sk_tail_ok(M, K4, C1 + C2) or not L.sk_tail_ok(M, K4, C1) or not L.sk_tail_ok(M, K4, C2)):
+        return None
+    to_b = lambda w: w if (w.dtype == torch.bfloat16 and N.is_cl(w)) else G.to(w, torch.bfloat16,  # noqa: E731
+                                                                                 torch.channels_last)
+    w3, wd = to_b(w3), to_b(wd)
+    dev = y.device
+    sts = []
+    for a, w, g, b, rm, rv, mom, eps, C in ((y, w3, g3, b3, rm3, rv3, mom3, eps3, C1),
+                                           (x, wd, gd, bd, rmd, rvd, momd, epsd, C2)):
+        ws = zeroed_ws(32 * 2 * K4, dev)
+        L.sk_tail(a.data_ptr(), w.data_ptr(), 0, ws.data_ptr(), 0, 0, 0, 0, M, K4, C, 0, N.stream())
+        p = _mem.empty(4 * K4, dtype=torch.float32, device=dev)
+        mean, invstd, scale, shift = p[:K4], p[K4:2 * K4], p[2 * K4:3 * K4], p[3 * K4:]
+        L.bn_fwd_from_ws(ws.data_ptr(), 32, g.data_ptr(), b.data_ptr(), rm.data_ptr(), rv.data_ptr(),
+                         mean.data_ptr(), invstd.data_ptr(), scale.data_ptr(), shift.data_ptr(), M, K4, mom, eps,
+                         N.stream())
+        sts.append((mean, invstd, scale, shift))
+    wf = _mem.empty(K4 * (C1 + C2), dtype=torch.bfloat16, device=dev)
+    aux = _mem.empty(2 * K4, dtype=torch.float32, device=dev)
+    L.bnres_fold(w3.data_ptr(), wd.data_ptr(), sts[0][2].data_ptr(), sts[0][3].data_ptr(), sts[1][2].data_ptr(),
+                 sts[1][3].data_ptr(), K4, C1, C2, wf.data_ptr(), aux.data_ptr(), aux[K4:].data_ptr(), N.stream())
+    out = _mem.empty((Nn, K4, H, W), dtype=torch.bfloat16, device=dev, memory_format=torch.channels_last)
+    mask = _mem.empty(M * K4 // 8, dtype=torch.uint8, device=dev)
+    if not L.sk_tail2(y.data_ptr(), x.data_ptr(), wf.data_ptr(), aux.data_ptr(), aux[K4:].data_ptr(), out.data_ptr(),
+                      mask.data_ptr(), M, K4, C1, C2, N.stream()):
+        raise RuntimeError("bnres_dual_fwd: persistent kernel refused an eligible shape")
+    return out, BNState(*sts[0], mask), BNState(*sts[1], None)
+
+
 def strided_pick(x: torch.Tensor, stride: int) -> torch.Tensor:
     """x[:, :, ::s, ::s] as a dense channels_last bf16 tensor (native; the
     pixels a strided 1x1 conv reads)."""

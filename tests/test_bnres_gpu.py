@@ -302,3 +302,89 @@ def test_strided_shortcut_grad_absorbed_by_conv1(gpu):
             for k, p in b.get_params().items()}
     print(errs)
     assert max(errs.values()) < 1e-2, errs
+
+
+def _torch_bottleneck(blk, x):
+    """fp32 PyTorch reference of a Bottleneck (training-mode BN, batch statistics)."""
+    def bn(t, layer, relu):
+        y = TF.batch_norm(t, None, None, layer.scale.data.float(), layer.bias.data.float(), True, 0.0, layer.eps)
+        return torch.relu(y) if relu else y
+    o = bn(TF.conv2d(x, blk.conv1.W.data.float()), blk.bn1, True)
+    o = bn(TF.conv2d(o, blk.conv2.W.data.float(), stride=blk.conv2.stride, padding=1), blk.bn2, True)
+    o = bn(TF.conv2d(o, blk.conv3.W.data.float()), blk.bn3, False)
+    sc = (bn(TF.conv2d(x, blk.down_conv.W.data.float(), stride=blk.down_conv.stride), blk.down_bn, False)
+          if blk.has_down else x)
+    return torch.relu(o + sc)
+
+
+def test_dual_tail_recompute_matches_unfused(gpu):
+    """ResNet-50's stage-1 downsample block (stride 1, 64 -> 256): the
+    recomputed two-branch tail forward (F.bnres_dual_fwd: statistics passes,
+    then one two-source GEMM with the BN scales folded into the weights) vs.
+    the stored-output forward.  The folded weights round differently (not
+    bitwise), so a few outputs near 0 flip their ReLU mask and, under a random
+    output gradient, every parameter gradient moves by a few percent; the
+    check is therefore that both paths are equally close to fp32 PyTorch."""
+    from singa_amd import autograd as AG
+    from singa_amd import device
+    from singa_amd.models.resnet import Bottleneck
+    from singa_amd.ops import functional as FF
+    from singa_amd.tensor import Tensor
+
+    dev = device.create_rocm_gpu()
+    dev.SetRandSeed(17)
+    blk = Bottleneck(64, 1, True)
+    g0 = torch.Generator(device=gpu).manual_seed(8)
+    xf = torch.relu(torch.randn(42, 64, 56, 56, device=gpu, generator=g0))  # 131712 pixels: the persistent kernel
+    dyt = torch.randn(42, 256, 56, 56, device=gpu, generator=g0)
+    calls = [0]
+    orig = FF.bnres_dual_fwd
+
+    def spy(*a, **k):
+        r = orig(*a, **k)
+        calls[0] += r is not None
+        return r
+
+    def run(on):
+        r0 = FF.TAIL_RECOMPUTE
+        FF.TAIL_RECOMPUTE = on
+        AG.training = True
+        try:
+            x = Tensor(data=_cl(xf).bfloat16(), device=dev, requires_grad=True, stores_grad=False)
+            h = blk(x)
+            out = h.data.float().clone()
+            loss_t = AG.reduce_sum(AG.mul(h, Tensor(data=_cl(dyt).bfloat16(), device=dev, requires_grad=False)),
+                                   None)
+            gr = {id(p): gg.data.float().clone() for p, gg in AG.backward(loss_t)}
+        finally:
+            AG.training = False
+            FF.TAIL_RECOMPUTE = r0
+        return out, gr
+
+    run(False)
+    FF.bnres_dual_fwd = spy
+    try:
+        o1, g1 = run(True)
+    finally:
+        FF.bnres_dual_fwd = orig
+    assert calls[0] == 1
+    o0, g0_ = run(False)
+    assert rel_err(o1, o0) < 1e-2
+    assert float(((o1 > 0) != (o0 > 0)).float().mean()) < 2e-3
+    params = blk.get_params()
+    leaves = {k: p.data.float().clone().requires_grad_(True) for k, p in params.items()}
+    saved = {k: p.data for k, p in params.items()}
+    for k, p in params.items():
+        p.data = leaves[k]
+    try:
+        ref = _torch_bottleneck(blk, xf.bfloat16().float())
+        (ref * dyt.bfloat16().float()).sum().backward()
+    finally:
+        for k, p in params.items():
+            p.data = saved[k]
+    assert rel_err(o1, ref.detach()) < 1e-2 and rel_err(o0, ref.detach()) < 1e-2
+    e_on = {k: rel_err(g1[id(p)], leaves[k].grad) for k, p in params.items()}
+    e_off = {k: rel_err(g0_[id(p)], leaves[k].grad) for k, p in params.items()}
+    print({k: (round(e_on[k], 4), round(e_off[k], 4)) for k in e_on})
+    for k in e_on:
+        assert e_on[k] <= 1.5 * e_off[k] + 1e-2, (k, e_on[k], e_off[k])
