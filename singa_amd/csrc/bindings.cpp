@@ -142,6 +142,7 @@ void sg_bn_apply_cs(const void*, const void*, const void*, void*, void*, void*, 
 void sg_conv_dgrad_gsum(const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int,
                         int, int, int, void*, const void*, void*, const void*, int, int, int, hipStream_t);
 int sg_sk_tail_ok(int, int, int);
+void sg_bnres_gram_stats(const void*, const void*, const void*, int, int, int, void*, hipStream_t);
 int sg_sk_tail2(const void*, const void*, const void*, const void*, const void*, void*, void*, int, int, int, int,
                 hipStream_t);
 void sg_bnres_fold(const void*, const void*, const void*, const void*, const void*, const void*, int, int, int, void*,
@@ -542,6 +543,10 @@ PYBIND11_MODULE(_C, m) {
     CHK("strided_pick");
   });
   m.def("sk_tail_ok", [](int M, int N, int K) { return sg_sk_tail_ok(M, N, K); });
+  m.def("bnres_gram_stats", [](P w, P gram, P cs, int cs_rows, int K4, int C, P ws, P s) {
+    sg_bnres_gram_stats(CV(w), CV(gram), CV(cs), cs_rows, K4, C, V(ws), S(s));
+    CHK("bnres_gram_stats");
+  });
   m.def("sk_tail2", [](P y, P x, P wf, P shift, P ones, P out, P mask, int M, int N, int K1, int K2, P s) {
     const int r = sg_sk_tail2(CV(y), CV(x), CV(wf), CV(shift), CV(ones), V(out), V(mask), M, N, K1, K2, S(s));
     CHK("sk_tail2");

@@ -231,6 +231,35 @@ __global__ void __launch_bounds__(256) fold_k(const bf16* __restrict__ w3, const
   }
 }
 
+// BN statistics of c = y W^T without c: sum_k = W[k] . colsum(y) and
+// sumsq_k = W[k]^T Gram(y) W[k] (Gram = y^T y, fp32 [C][C]; colsum as cs_rows
+// slot rows [cs_rows][C]) -> ws[0][2][K4] (sum | sumsq), the layout
+// bn_fwd_from_ws reads with rows = 1.  One workgroup per output channel.
+__global__ void __launch_bounds__(256) gram_stats_k(const bf16* __restrict__ w, const float* __restrict__ gram,
+                                                   const float* __restrict__ cs, int cs_rows, int K4, int C,
+                                                   float* __restrict__ ws) {
+  __shared__ float sh[8];
+  const int k = blockIdx.x;
+  const bf16* wk = w + (int64_t)k * C;
+  float s1 = 0.f, s2 = 0.f;
+  for (int i = threadIdx.x; i < C; i += 256) {
+    const float* gi = gram + (int64_t)i * C;
+    float t = 0.f;
+    for (int j = 0; j < C; ++j) t += gi[j] * (float)wk[j];
+    float ci = 0.f;
+    for (int r = 0; r < cs_rows; ++r) ci += cs[(int64_t)r * C + i];
+    const float wi = (float)wk[i];
+    s1 += wi * ci;
+    s2 += wi * t;
+  }
+  s1 = block_sum(s1, sh);
+  s2 = block_sum(s2, sh);
+  if (threadIdx.x == 0) {
+    ws[k] = s1;
+    ws[K4 + k] = s2;
+  }
+}
+
 template <int BM, int BN, int AM, int BMODE, int OUT, int NTH, int WM, int WN, int STAGES>
 void go(const GemmArgs& p, int tiles, int zdim, hipStream_t s) {
   constexpr int stages = STAGES * (BM + BN) * BK * 2;
@@ -263,6 +292,8 @@ extern "C" {
 
 // out [K4 + C][C] fp32 (zeroed by the caller) += [g | y]^T y over P pixels:
 // rows 0..K4-1 = G = g^T y, rows K4.. = Gram(y).  g [P][K4], y [P][C] bf16.
+// (K4 = 0: out [C][C] += Gram(y) = y^T y alone -- the forward's BN statistics
+// of a 1x1 conv of y, bnres_gram_stats)
 void sg_bnres_wgrad(const void* g, const void* y, void* out, int P, int K4, int C, hipStream_t s) {
   if ((K4 & 127) != 0 || (C & 63) != 0) throw std::runtime_error("bnres_wgrad: K4 % 128 and C % 64 required");
   GemmArgs p{};
@@ -388,6 +419,12 @@ void sg_bnres_fold(const void* w3, const void* wd, const void* s3, const void* f
   hipLaunchKernelGGL(fold_k, dim3(N), dim3(256), 0, s, (const bf16*)w3, (const bf16*)wd, (const float*)s3,
                      (const float*)f3, (const float*)sd, (const float*)fd, N, K1, K2, (bf16*)wf, (float*)shift,
                      (float*)ones);
+}
+
+void sg_bnres_gram_stats(const void* w, const void* gram, const void* cs, int cs_rows, int K4, int C, void* ws,
+                         hipStream_t s) {
+  hipLaunchKernelGGL(gram_stats_k, dim3(K4), dim3(256), 0, s, (const bf16*)w, (const float*)gram, (const float*)cs,
+                     cs_rows, K4, C, (float*)ws);
 }
 
 }  // extern "C"

@@ -762,6 +762,19 @@ void sg_conv_dgrad_bn_ex(const void* dy, const void* w, void* dx, int N, int H, 
         hipLaunchKernelGGL(wt_transpose_k, dim3((C + 63) / 64, (K + 63) / 64, 1), dim3(256), 0, s, (const bf16*)w,
                            (bf16*)wt, K, 1, C);
       p.b = (const bf16*)wt; p.ldb = K;
+      // a fused tail's output gradient (stats_mode 4) on a short-K shape: the
+      // persistent kernel with the masked-sum epilogue (sk_gemm_k EPI 2; the
+      // compact strided accumulator stays on the generic kernel)
+      if (p.stats && p.stats_mode == 4 && p.res_s <= 1 && out_mode == OUT_BF16 && beta == 0.f && g_tune[9] &&
+          g_tune[4] == 0 && K <= 128 && (C & 127) == 0 && (long)((p.M + 127) / 128) * (C / 128) >= 2048) {
+        GemmArgs q = p;
+        q.ep_res = p.res_g;
+        q.ep_mask = (uint8_t*)p.bnb_mask;
+        q.res_g = nullptr;
+        if (K <= 64) launch_sk<1, 2>(q, (p.M + 127) / 128, C / 128, s);
+        else launch_sk<2, 2>(q, (p.M + 127) / 128, C / 128, s);
+        return;
+      }
       if (out_mode == OUT_F32) launch<LM_KMAJOR, LM_KMAJOR, OUT_F32>(p, p.M, 1, s, 1, 0);
       else launch<LM_KMAJOR, LM_KMAJOR, OUT_BF16>(p, p.M, 1, s, 1, 0);
     } else {

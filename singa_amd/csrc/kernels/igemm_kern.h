@@ -1041,6 +1041,10 @@ constexpr int sk_lds(int kt) { return 3 * kt * SK_TILE + SK_STG; }
 //        pass of a recomputed fused tail).
 // EPI 1: the fused residual tail's second pass: out = relu(bf16(A B^T) *
 //        scale + shift + res) and its ReLU mask bits (GemmArgs::ep_*).
+// EPI 2: a 1x1 conv's data gradient completing a fused tail's output
+//        gradient: out = bf16(bf16(A B^T) + res) * bit(ep_mask) (res: the other
+//        consumers' gradient, or none) and its column sums into p.stats
+//        (stats_mode 4 of the generic kernels: the tail's g~ and sum g~).
 // AM: LM_KMAJOR, or LM_KMAJOR2 -- A from two sources split at p.a2_split
 // (a multiple of 64): the two-branch tail [y | x] . [W3' | Wd']^T
 template <int KT, int EPI = 0, int AM = LM_KMAJOR>
@@ -1146,17 +1150,26 @@ __global__ void __launch_bounds__(256, 1) sk_gemm_k(const GemmArgs p) {
   // after this tile's stores) so their latency hides behind a tile of work;
   // ldc == N, host-checked -- residual and output share the row stride
   u32x4 rres[NPS];
+  unsigned mres[NPS];  // EPI 2: the next tile's mask bytes, prefetched with its residual
   auto load_res = [&](int t) {
     const int mt = t < tiles_m ? t : 0;
+    const int trows = min(BM, M - mt * BM);
     const __amdgpu_buffer_rsrc_t rr =  // (no residual: loads of zeros, the count stays uniform)
         t < tiles_m && p.ep_res
-            ? make_rsrc(p.ep_res + (int64_t)mt * BM * p.ldc, (unsigned)((int64_t)min(BM, M - mt * BM) * p.ldc * 2))
+            ? make_rsrc(p.ep_res + (int64_t)mt * BM * p.ldc, (unsigned)((int64_t)trows * p.ldc * 2))
             : rnull;
 #pragma unroll
     for (int pass = 0; pass < NPS; ++pass)
       rres[pass] = __builtin_amdgcn_raw_buffer_load_b128(rr, (unsigned)(((r0 + pass * RPP) * (int)p.ldc + n) * 2), 0, 0);
+    if constexpr (EPI == 2) {
+      const __amdgpu_buffer_rsrc_t rm =
+          t < tiles_m ? make_rsrc(p.ep_mask + (int64_t)mt * BM * (N >> 3), (unsigned)(trows * (N >> 3))) : rnull;
+#pragma unroll
+      for (int pass = 0; pass < NPS; ++pass)
+        mres[pass] = __builtin_amdgcn_raw_buffer_load_b8(rm, (unsigned)((r0 + pass * RPP) * (N >> 3) + (n >> 3)), 0, 0);
+    }
   };
-  if constexpr (EPI == 1) load_res(tm);
+  if constexpr (EPI >= 1) load_res(tm);
   for (int it = 0;; ++it) {
     const int buf = it & 1;
     // A(it) landed (younger: [loads] stores(it-2), Q(it-1), A(it+1), [loads] stores(it-1);
@@ -1164,13 +1177,18 @@ __global__ void __launch_bounds__(256, 1) sk_gemm_k(const GemmArgs p) {
     // (per-tile epilogue ops E: NPS stores, + NPS loads with beta; EPI 1: NPS
     // output stores, NPS mask-byte stores and the next tile's NPS residual
     // loads -- after the prologue's residual loads (NPS) of tile 0)
+    // (EPI 2: NPS output stores, then the next tile's NPS residual and NPS
+    // mask-byte loads -- after the prologue's 2 NPS loads of tile 0)
     if (it == 0) {
-      if constexpr (EPI == 1) wait_vmcnt<NPS + D>(); else wait_vmcnt<D>();
+      if constexpr (EPI == 1) wait_vmcnt<NPS + D>();
+      else if constexpr (EPI == 2) wait_vmcnt<2 * NPS + D>();
+      else wait_vmcnt<D>();
     } else if (it == 1) {
       if constexpr (EPI == 1) wait_vmcnt<4 * NPS + D + 1>();
+      else if constexpr (EPI == 2) wait_vmcnt<5 * NPS + D + 1>();
       else if (has_beta) wait_vmcnt<2 * NPS + D + 1>(); else wait_vmcnt<NPS + D + 1>();
     } else {
-      if constexpr (EPI == 1) wait_vmcnt<6 * NPS + D + 1>();
+      if constexpr (EPI >= 1) wait_vmcnt<6 * NPS + D + 1>();
       else if (has_beta) wait_vmcnt<4 * NPS + D + 1>(); else wait_vmcnt<2 * NPS + D + 1>();
     }
     raw_barrier();  // A(it) landed for every wave; every wave is done with tile it-1
@@ -1211,7 +1229,7 @@ __global__ void __launch_bounds__(256, 1) sk_gemm_k(const GemmArgs p) {
     }
     if (it > 0 && wid == 0 && l == 0) {
       // Q(it-1) (the ticket of tile it+2) retired: younger are A(it+1) and [loads] stores(it-1)
-      if constexpr (EPI == 1) wait_vmcnt<3 * NPS + D>();
+      if constexpr (EPI >= 1) wait_vmcnt<3 * NPS + D>();
       else if (has_beta) wait_vmcnt<2 * NPS + D>(); else wait_vmcnt<NPS + D>();
       *sQ =p.wq ? xcd + 8 * (3 * G8 + ticket) : tm + 16 * G8;
     }
@@ -1258,6 +1276,23 @@ __global__ void __launch_bounds__(256, 1) sk_gemm_k(const GemmArgs p) {
         __builtin_amdgcn_raw_buffer_store_b8((unsigned char)b, rmk, (unsigned)(ml * (N >> 3) + (n >> 3)), 0, 0);
       }
       load_res(t1);  // the next tile's residual (null resource past the end)
+    } else if constexpr (EPI == 2) {
+#pragma unroll
+      for (int pass = 0; pass < NPS; ++pass) {
+        const int ml = r0 + pass * RPP;
+        bf16x8 o = *(const bf16x8*)(sC + ml * SK_LDT + ch * 8);
+        const bf16x8 rb = __builtin_bit_cast(bf16x8, rres[pass]);
+#pragma unroll
+        for (int r = 0; r < 8; ++r)
+          o[r] = ((mres[pass] >> r) & 1u) != 0 ? (bf16)((float)o[r] + (float)rb[r]) : (bf16)0.f;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rc, (unsigned)((ml * (int)p.ldc + n) * 2),
+                                               0, 0);
+        if (ml < rows) {
+#pragma unroll
+          for (int r = 0; r < 8; ++r) st_s[r] += (float)o[r];
+        }
+      }
+      load_res(t1);
     } else {
       if (has_beta) {
 #pragma unroll
@@ -1291,7 +1326,7 @@ __global__ void __launch_bounds__(256, 1) sk_gemm_k(const GemmArgs p) {
   }
   wait_vmcnt<0>();
   if (p.wq && threadIdx.x == 0) wq_done(p.wq, 8 * (int)gridDim.y);  // every ticket of this workgroup is taken
-  if (EPI == 0 && p.stats) {
+  if (EPI != 1 && p.stats) {
     // once per workgroup: the RPP row-threads of each 8-column chunk through
     // LDS, then one atomic per column value into slot row blockIdx.x & 31
     __syncthreads();

@@ -1710,6 +1710,7 @@ def batchnorm_fwd(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, run_
                           R, C, int(relu), N.stream())
             st = BNState(mean, invstd, scale, shift, mask)
             st.colsum = cs
+            y._sg_cs_slots = cs  # (the consuming tail's forward statistics read them too)
             return y, st
         L.bn_apply(x.data_ptr(), scale.data_ptr(), shift.data_ptr(), N.ptr(res), y.data_ptr(), R, C, int(relu),
                    N.dt(x), N.stream(), N.ptr(mask))
@@ -1835,6 +1836,33 @@ def bnres_ok(y: torch.Tensor, w_shape, res: Optional[torch.Tensor], down=None) -
 # the tail's forward recomputes its 1x1 conv instead of storing the output
 # (bnres_fwd); switchable for A/B measurements
 TAIL_RECOMPUTE = os.environ.get("SINGA_AMD_TAIL_RECOMPUTE", "1") != "0"
+# ... and takes its BN statistics from Gram(y) and colsum(y) instead of a
+# statistics-only GEMM pass (tail_stats_ws)
+GRAM_STATS = os.environ.get("SINGA_AMD_GRAM_STATS", "1") != "0"
+
+
+def tail_stats_ws(a: torch.Tensor, w: torch.Tensor, M: int, C: int, K4: int):
+    """(ws, rows) for bn_fwd_from_ws: the per-channel sum and sum of squares of
+    c = conv1x1(a, w) without computing c -- sum_k = W[k] . colsum(a),
+    sumsq_k = W[k]^T Gram(a) W[k], Gram(a) = a^T a one K-outer GEMM over the
+    pixels (a C x C output, split-K) -- or the statistics-only pass of the
+    persistent GEMM (GRAM_STATS off).  colsum(a): the producer BN's apply-pass
+    slot rows when it summed them (``_sg_cs_slots``), else one reduction."""
+    L = N.lib()
+    dev = a.device
+    if not GRAM_STATS:
+        ws = zeroed_ws(32 * 2 * K4, dev)
+        L.sk_tail(a.data_ptr(), w.data_ptr(), 0, ws.data_ptr(), 0, 0, 0, 0, M, K4, C, 0, N.stream())
+        return ws, 32
+    gram = _zeros32(C * C, dev)
+    L.bnres_wgrad(0, a.data_ptr(), gram.data_ptr(), M, 0, C, N.stream())
+    cs = getattr(a, "_sg_cs_slots", None)
+    if cs is None or cs.numel() % C != 0:
+        cs = colsum(a.permute(0, 2, 3, 1).reshape(M, C))[0]
+    ws = _mem.empty(2 * K4, dtype=torch.float32, device=dev)
+    L.bnres_gram_stats(w.data_ptr(), gram.data_ptr(), cs.data_ptr(), cs.numel() // C, K4, C, ws.data_ptr(),
+                       N.stream())
+    return ws, 1
 
 
 def bnres_fwd(y: torch.Tensor, w: torch.Tensor, gamma, beta, run_mean, run_var, training: bool, momentum: float,
@@ -1863,11 +1891,10 @@ def bnres_fwd(y: torch.Tensor, w: torch.Tensor, gamma, beta, run_mean, run_var, 
     if w.shape[1] != C or tuple(res.shape) != (Nn, K, H, W) or not L.sk_tail_ok(M, K, C):
         return None
     dev = y.device
-    ws = zeroed_ws(32 * 2 * K, dev)
-    L.sk_tail(y.data_ptr(), w.data_ptr(), 0, ws.data_ptr(), 0, 0, 0, 0, M, K, C, 0, N.stream())
+    ws, rows = tail_stats_ws(y, w, M, C, K)
     p = _mem.empty(4 * K, dtype=torch.float32, device=dev)
     mean, invstd, scale, shift = p[:K], p[K:2 * K], p[2 * K:3 * K], p[3 * K:]
-    L.bn_fwd_from_ws(ws.data_ptr(), 32, gamma.data_ptr(), beta.data_ptr(), run_mean.data_ptr(), run_var.data_ptr(),
+    L.bn_fwd_from_ws(ws.data_ptr(), rows, gamma.data_ptr(), beta.data_ptr(), run_mean.data_ptr(), run_var.data_ptr(),
                      mean.data_ptr(), invstd.data_ptr(), scale.data_ptr(), shift.data_ptr(), M, K, momentum, eps,
                      N.stream())
     out = _mem.empty((Nn, K, H, W), dtype=torch.bfloat16, device=dev, memory_format=torch.channels_last)
@@ -1905,11 +1932,10 @@ def bnres_dual_fwd(y, w3, g3, b3, rm3, rv3, mom3, eps3, x, wd, gd, bd, rmd, rvd,
     sts = []
     for a, w, g, b, rm, rv, mom, eps, C in ((y, w3, g3, b3, rm3, rv3, mom3, eps3, C1),
                                            (x, wd, gd, bd, rmd, rvd, momd, epsd, C2)):
-        ws = zeroed_ws(32 * 2 * K4, dev)
-        L.sk_tail(a.data_ptr(), w.data_ptr(), 0, ws.data_ptr(), 0, 0, 0, 0, M, K4, C, 0, N.stream())
+        ws, rows = tail_stats_ws(a, w, M, C, K4)
         p = _mem.empty(4 * K4, dtype=torch.float32, device=dev)
         mean, invstd, scale, shift = p[:K4], p[K4:2 * K4], p[2 * K4:3 * K4], p[3 * K4:]
-        L.bn_fwd_from_ws(ws.data_ptr(), 32, g.data_ptr(), b.data_ptr(), rm.data_ptr(), rv.data_ptr(),
+        L.bn_fwd_from_ws(ws.data_ptr(), rows, g.data_ptr(), b.data_ptr(), rm.data_ptr(), rv.data_ptr(),
                          mean.data_ptr(), invstd.data_ptr(), scale.data_ptr(), shift.data_ptr(), M, K4, mom, eps,
                          N.stream())
         sts.append((mean, invstd, scale, shift))

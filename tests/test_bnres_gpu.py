@@ -157,12 +157,28 @@ def test_bnres_chain_matches_unfused(gpu, stride):
     # too; only the last block (fed by the loss, no consuming conv) needed the
     # fallback mask pass
     assert calls == {"bwd": 4, "masksum": 1}, calls
-    errs = {}
-    for i, b in enumerate(blks):
-        for k, p in b.get_params().items():
-            errs[f"{i}.{k}"] = rel_err(g_on[id(p)], g_off[id(p)])
-    print(errs)
-    assert max(errs.values()) < 3e-2, errs
+    # both paths against fp32 PyTorch: a few ReLU bits flip between any two
+    # bf16 runs (atomic-order rounding) and, under a random output gradient,
+    # move every gradient of this small chain by a few percent -- so the fused
+    # path must be as close to fp32 as the unfused one, not equal to it
+    named = [(f"{i}.{k}", p) for i, b in enumerate(blks) for k, p in b.get_params().items()]
+    leaves = {n: p.data.float().clone().requires_grad_(True) for n, p in named}
+    saved = {n: p.data for n, p in named}
+    for n, p in named:
+        p.data = leaves[n]
+    try:
+        h = _cl(xf).bfloat16().float()
+        for b in blks:
+            h = _torch_bottleneck(b, h)
+        (h * _cl(dyt).bfloat16().float()).sum().backward()
+    finally:
+        for n, p in named:
+            p.data = saved[n]
+    e_on = {n: rel_err(g_on[id(p)], leaves[n].grad) for n, p in named}
+    e_off = {n: rel_err(g_off[id(p)], leaves[n].grad) for n, p in named}
+    print({n: (round(e_on[n], 4), round(e_off[n], 4)) for n in e_on})
+    for n in e_on:
+        assert e_on[n] <= 1.5 * e_off[n] + 2e-2, (n, e_on[n], e_off[n])
 
 
 @pytest.mark.parametrize("C,K4", [(64, 256), (128, 512)])
@@ -244,24 +260,40 @@ def test_strided_pick_place(gpu):
 
 
 def test_strided_shortcut_grad_absorbed_by_conv1(gpu):
-    """A stride-2 downsample block fed by a fused tail: its shortcut's input
-    gradient stays compact (F.StridedGrad) and the block's conv1 dgrad adds it
-    in its epilogue (no strided_place); the gradients equal those of the same
-    fused path with the shortcut gradient placed on the full grid eagerly.
-    (Against the unfused path the distance is dominated by bf16 run-to-run
-    noise amplified through three small-batch BNs: tools/dbg_chain.py.)"""
+    """The compact strided shortcut gradient (F.StridedGrad): (a) a 1x1 conv's
+    fused-tail dgrad (gmask path) adds it from the compact tensor exactly as it
+    adds the placed full-grid tensor; (b) in a chain -- a stride-2 downsample
+    block fed by a fused tail -- the engine hands it to the block's conv1 and
+    nothing is ever placed on the full grid."""
+    import numpy as np
+
     from singa_amd import autograd as AG
     from singa_amd import device
     from singa_amd.models.resnet import Bottleneck
     from singa_amd.ops import functional as FF
     from singa_amd.tensor import Tensor
 
+    g0 = torch.Generator(device=gpu).manual_seed(6)
+    Nn, C, K, H = 8, 256, 64, 28
+    x = _cl(torch.randn(Nn, C, H, H, device=gpu, generator=g0)).bfloat16()
+    w = (torch.randn(K, C, 1, 1, device=gpu, generator=g0) * 0.05).bfloat16()
+    dy = _cl(torch.randn(Nn, K, H, H, device=gpu, generator=g0)).bfloat16()
+    gc = _cl(torch.randn(Nn, C, H // 2, H // 2, device=gpu, generator=g0)).bfloat16()
+    gmask = torch.randint(0, 256, (Nn * H * H * C // 8,), device=gpu, dtype=torch.uint8, generator=g0)
+    outs = []
+    for lazy in (True, False):
+        acc = FF.StridedGrad(gc, 2, x.shape) if lazy else FF.strided_place(gc, tuple(x.shape), 2)
+        dx, _, _ = FF.conv2d_bwd(x, w, dy, (1, 1), (0, 0), (1, 1), 1, need_dx=True, dx_acc=acc,
+                                 bn_producer=("gmask", gmask))
+        assert getattr(dx, "_sg_absorbed", None) is acc
+        outs.append((dx.float(), dx._sg_gsum[0].clone()))
+    assert torch.equal(outs[0][0], outs[1][0])  # the same bf16 values, added from the compact tensor
+    assert rel_err(outs[0][1], outs[1][1]) < 1e-5  # (the masked sums: atomic order only)
+
     dev = device.create_rocm_gpu()
     dev.SetRandSeed(13)
     blks = [Bottleneck(64, 1, True), Bottleneck(64, 2, True), Bottleneck(64, 1, False)]
-    g0 = torch.Generator(device=gpu).manual_seed(6)
     xf = torch.randn(8, 128, 28, 28, device=gpu, generator=g0)
-    dyt = None
     places = [0]
     orig_place = FF.strided_place
 
@@ -269,39 +301,21 @@ def test_strided_shortcut_grad_absorbed_by_conv1(gpu):
         places[0] += 1
         return orig_place(*a, **k)
 
-    def run(lazy):
-        nonlocal dyt
-        lz0 = FF.STRIDED_LAZY
-        FF.STRIDED_LAZY = lazy
-        AG.training = True
-        try:
-            x = Tensor(data=_cl(xf).bfloat16(), device=dev, requires_grad=True, stores_grad=False)
-            h = x
-            for b in blks:
-                h = b(h)
-            if dyt is None:
-                dyt = torch.randn(h.shape, device=gpu, generator=g0)
-            loss_t = AG.reduce_sum(AG.mul(h, Tensor(data=_cl(dyt).bfloat16(), device=dev, requires_grad=False)),
-                                   None)
-            gr = {id(p): gg.data.float().clone() for p, gg in AG.backward(loss_t)}
-        finally:
-            AG.training = False
-            FF.STRIDED_LAZY = lz0
-        return gr
-
-    run(True)  # creates the parameters
-    FF.strided_place = spy_place
+    AG.training = True
     try:
-        g_lazy = run(True)
-        assert places[0] == 0, places  # absorbed, never placed on the full grid
-        g_place = run(False)
-        assert places[0] == 1, places
+        xt = Tensor(data=_cl(xf).bfloat16(), device=dev, requires_grad=True, stores_grad=False)
+        h = xt
+        for b in blks:
+            h = b(h)
+        dyt = torch.randn(h.shape, device=gpu, generator=g0)
+        FF.strided_place = spy_place
+        loss_t = AG.reduce_sum(AG.mul(h, Tensor(data=_cl(dyt).bfloat16(), device=dev, requires_grad=False)), None)
+        gr = [gg.data.float() for _, gg in AG.backward(loss_t)]
     finally:
         FF.strided_place = orig_place
-    errs = {f"{i}.{k}": rel_err(g_lazy[id(p)], g_place[id(p)]) for i, b in enumerate(blks)
-            for k, p in b.get_params().items()}
-    print(errs)
-    assert max(errs.values()) < 1e-2, errs
+        AG.training = False
+    assert places[0] == 0, places
+    assert len(gr) > 30 and all(np.isfinite(float(t.norm())) for t in gr)
 
 
 def _torch_bottleneck(blk, x):
@@ -388,3 +402,34 @@ def test_dual_tail_recompute_matches_unfused(gpu):
     print({k: (round(e_on[k], 4), round(e_off[k], 4)) for k in e_on})
     for k in e_on:
         assert e_on[k] <= 1.5 * e_off[k] + 1e-2, (k, e_on[k], e_off[k])
+
+
+@pytest.mark.parametrize("K,C,H,Nn", [(64, 256, 56, 42), (128, 512, 28, 168)])
+def test_gsum_dgrad_persistent_matches_fp32(gpu, K, C, H, Nn):
+    """The fused-tail output gradient of a 1x1 conv on the persistent kernel
+    (sk_gemm_k EPI 2: (dgrad + acc) * mask bit, column sums) against fp32 and
+    against the generic kernel's epilogue (knob 9 off)."""
+    from singa_amd.ops import functional as FF
+    from singa_amd.ops import native as N
+
+    g0 = torch.Generator(device=gpu).manual_seed(21)
+    x = _cl(torch.randn(Nn, C, H, H, device=gpu, generator=g0)).bfloat16()
+    w = (torch.randn(K, C, 1, 1, device=gpu, generator=g0) * 0.1).bfloat16()
+    dy = _cl(torch.randn(Nn, K, H, H, device=gpu, generator=g0)).bfloat16()
+    acc = _cl(torch.randn(Nn, C, H, H, device=gpu, generator=g0)).bfloat16()
+    gmask = torch.randint(0, 256, (Nn * H * H * C // 8,), device=gpu, dtype=torch.uint8, generator=g0)
+    bits = ((gmask.view(-1, 1).int() >> torch.arange(8, device=gpu).view(1, 8)) & 1).view(Nn, H, H, C)
+    ref = (TF.conv_transpose2d(dy.float(), w.float()) + acc.float()) * bits.permute(0, 3, 1, 2).float()
+    res = {}
+    for sk in (1, 0):
+        N.lib().set_tuning(9, sk)
+        try:
+            dx, _, _ = FF.conv2d_bwd(x, w, dy, (1, 1), (0, 0), (1, 1), 1, need_dx=True, dx_acc=acc.clone(),
+                                     bn_producer=("gmask", gmask))
+        finally:
+            N.lib().set_tuning(9, 1)
+        gs = dx._sg_gsum[0].view(32, 2, C)[:, 0].sum(0)
+        res[sk] = (dx.float(), gs)
+        assert rel_err(dx, ref) < 1e-2, (sk, rel_err(dx, ref))
+        assert rel_err(gs, ref.sum((0, 2, 3))) < 1e-2
+    assert rel_err(res[1][0], res[0][0]) < 1e-2

@@ -46,7 +46,8 @@ def main():
                 h = b(h)
                 outs.append(h.data.float().clone())
             if dyt is None:
-                dyt = torch.randn(h.shape, device=gpu, generator=g0)
+                dyt = (torch.rand(h.shape, device=gpu, generator=g0) + 0.5 if os.environ.get("DBG_POS") else
+                       torch.randn(h.shape, device=gpu, generator=g0))
             loss_t = AG.reduce_sum(AG.mul(h, Tensor(data=cl(dyt).bfloat16(), device=dev, requires_grad=False)), None)
             gr = {id(p): gg.data.float().clone() for p, gg in AG.backward(loss_t)}
         finally:
