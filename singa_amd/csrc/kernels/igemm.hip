@@ -177,7 +177,9 @@ static int make_phases(ConvGeom& g) {
 // short-K kernel for the 1x1-conv GEMM shapes (sk_gemm_k)
 // key 10: workgroup target of the 8-wave split-K weight gradient (0: 1024 with taps, 512 for 1x1)
 // key 11: 1 = strided data gradients never take the single-stage short-K kernel (A/B)
-static int g_tune[12] = {5, 1, 1, 0, 0, 1, 8, 1, 0, 1, 0, 0};
+// key 12: > 0 forces the split count of the 8-wave weight gradient (sweeps);
+// key 13: split policy of that kernel: 1 = quantisation-aware (default), 0 = powers of 2 to the target
+static int g_tune[16] = {5, 1, 1, 0, 0, 1, 8, 1, 0, 1, 0, 0, 0, 1, 0, 0};
 // one-shot: the next dgrad's wt scratch is already transposed.  Per OS
 // thread: the runtime's executor threads (hogwild / aggregated replicas)
 // each set and consume their own flag, so one thread's set can never be
@@ -811,6 +813,31 @@ void sg_conv_dgrad_bn_ex(const void* dy, const void* w, void* dx, int N, int H, 
   else launch<LM_DGRAD_A, LM_DGRAD_B, OUT_BF16>(p, Mmax, 1, s, 1, np);
 }
 
+// Split count of the 8-wave split-K weight gradient, quantisation-aware:
+// two of these workgroups run per CU, so the launch runs in waves of 2 x CUs
+// workgroups and a partial last wave costs a whole one -- 1152 workgroups (36
+// tiles x 32 splits) are 2.25 waves.  Among split counts with >= 16 K-tiles
+// per split and at most twice the power-of-2 choice `sp0`, take the one
+// minimising ceil(tiles * sp / slots) * (ceil(nkt / sp) + e), e the atomic
+// epilogue in K-tile units; ties go to fewer splits (fewer atomic passes over
+// the output).  Measured on the ResNet-50 b1024 shapes (tools/wgrad_sweep.py,
+// profiles/r5/wgrad_sweep.jsonl): stage-2/3/4 3x3 weight gradients 368 / 300 /
+// 293 us -> 263 / 266 / 255 us (splits 56 / 14 / 7).
+static int wgrad_splits_q(int tiles, int nkt, int sp0) {
+  const int slots = 2 * sg_cu_count();
+  constexpr int e = 6;
+  int best = sp0;
+  long best_cost = (long)((tiles * sp0 + slots - 1) / slots) * ((nkt + sp0 - 1) / sp0 + e);
+  for (int sp = 1; sp <= 2 * sp0 && nkt / sp >= 16; ++sp) {
+    const long cost = (long)((tiles * sp + slots - 1) / slots) * ((nkt + sp - 1) / sp + e);
+    if (cost < best_cost || (cost == best_cost && sp < best)) {
+      best = sp;
+      best_cost = cost;
+    }
+  }
+  return best;
+}
+
 // conv weight gradient: dW[K][R*S*C] (fp32, accumulated atomically: the caller
 // zeroes it unless accumulating) += dy^T * im2col(x)
 void sg_conv_wgrad(const void* x, const void* dy, void* dw_out, int N, int H, int W, int C, int K, int R, int S,
@@ -855,6 +882,8 @@ void sg_conv_wgrad(const void* x, const void* dy, void* dw_out, int N, int H, in
     const int target = g_tune[10] > 0 ? g_tune[10] : R * S > 1 ? 1024 : 512;
     sp = 1;
     while (tiles * sp < target && sp * 2 * 4 <= nkt) sp *= 2;
+    if (g_tune[13] && g_tune[10] <= 0) sp = wgrad_splits_q(tiles, nkt, sp);
+    if (g_tune[12] > 0) sp = g_tune[12];
     p.k_per_split = kps(p.K, sp);
     launch_t<128, 128, LM_KOUTER, LM_WGRAD_B, OUT_F32_ATOMIC, 512, 2, 4, 2>(p, tiles, 1, sp, s);
     return;
@@ -900,7 +929,7 @@ void sg_wt_transpose_batched(const void* desc, int n, int total, hipStream_t s) 
     hipLaunchKernelGGL(wt_transpose_batched_k, dim3(total), dim3(256), 0, s, (const WtDesc*)desc, n);
 }
 void sg_set_tuning(int key, int value) {
-  if (key >= 0 && key < 12) g_tune[key] = value;
+  if (key >= 0 && key < 16) g_tune[key] = value;
 }
 
 }  // extern "C"
