@@ -452,6 +452,25 @@ def test_paired_stem_matches_torch_fp32(gpu, hw):
     assert rel_err(grads[id(conv.W)].reshape(wr.shape), wr.grad) < 1e-2
 
 
+@pytest.mark.parametrize("shape", [(3, 3, 8, 32), (2, 3, 5, 27), (2, 2, 4, 16), (5, 3, 7, 224)])
+def test_nchw_to_pairs_layout(gpu, shape):
+    """Paired-tap stem layout (vector W%4==0/C==3 and scalar forms) ==
+    its definition y[n,h,w',0:3] = x[n,:,h,w'-1], y[n,h,w',3:6] =
+    x[n,:,h,w'], zeros elsewhere, bitwise."""
+    from singa_amd.ops import native as NV
+    N, C, H, W = shape
+    x = torch.randn(shape, device=gpu)
+    y = torch.full((N, H, W + 1, 8), float("nan"), device=gpu, dtype=torch.bfloat16)
+    NV.lib().nchw_to_pairs(x.data_ptr(), y.data_ptr(), N, C, H, W, NV.stream())
+    torch.cuda.synchronize()
+    xp = torch.zeros(N, H, W + 2, 3, device=gpu)
+    xp[:, :, 1:W + 1, :C] = x.permute(0, 2, 3, 1)
+    ref = torch.zeros(N, H, W + 1, 8, device=gpu)
+    ref[..., 0:3] = xp[:, :, 0:W + 1]
+    ref[..., 3:6] = xp[:, :, 1:W + 2]
+    assert torch.equal(y, ref.bfloat16())
+
+
 def test_stem_pool_bn_backward_gather_matches_materialised(gpu, monkeypatch):
     """The fused stem backward (BN reduction + apply gathering the input
     gradient from the pooled gradient and argmax, no max-pool backward
