@@ -126,6 +126,7 @@ void sg_ggemm(int, const void*, int64_t, int, int64_t, const void*, int64_t, int
               int, int, int, float, float, const void*, int, int, int, int, float*, int, const void*, void*,
               hipStream_t);
 void sg_ggemm_tune(int, int);
+int sg_ggemm_last_dma();
 int sg_stem_fwd(const void*, const void*, void*, void*, int, int, int, int, int, hipStream_t);
 void sg_conv3x3_set(int);
 int sg_conv3x3_enabled();
@@ -501,6 +502,7 @@ PYBIND11_MODULE(_C, m) {
     CHK("ggemm");
   });
   m.def("ggemm_tune", [](int key, int value) { sg_ggemm_tune(key, value); });
+  m.def("ggemm_last_dma", []() { return sg_ggemm_last_dma(); });
   // persistent 3x3 64-channel stage-1 conv (csrc/kernels/conv3x3.hip): A/B switch
   m.def("conv3x3_set", [](int on) { sg_conv3x3_set(on); });
   m.def("conv3x3_enabled", []() { return sg_conv3x3_enabled(); });

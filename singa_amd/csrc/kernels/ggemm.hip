@@ -479,142 +479,287 @@ __global__ void __launch_bounds__(NT, 2) ggemm_k(const Args p) {
     __syncthreads();  // the epilogue may reuse the LDS
   }
 
-  // Epilogue: 16x16 blocks acc[i][j][r] = C[m = .. + (l & 15)][n = .. + 4 (l >> 4) + r];
-  // 32x32 blocks acc[i][j][4 g + r] = C[m = .. + (l & 31)][n = .. + 8 g + 4 (l >> 5) + r]
-  char* pc = (char*)p.c + y * p.sc * (p.out_mode == O_BF16 ? 2 : 4);
-  // split-K partial tiles: staged through LDS and added row-contiguously (a
-  // wave-instruction's 64 atomics cover 256 contiguous bytes) -- straight from
-  // the MFMA layout each instruction would scatter over 16 rows
-  constexpr int LDT = BN + 4;
-  constexpr bool STAGED = BM * LDT * 4 <= 2 * STAGE_EL * (int)sizeof(T);
-  if (STAGED && p.out_mode == O_F32_ATOMIC) {
-    float* tile = (float*)smem;  // the K loop ended with a barrier: the stages are free
+  constexpr int EPI_LDS = 2 * STAGE_EL * (int)sizeof(T);
+#include "ggemm_epilogue.inc"
+}
+
+// ------------------------------------------------------------------------------
+// fp32 plain GEMM with LDS-DMA staging (f32d_k): the same C = alpha A B^T
+// (+ epilogue) as ggemm_k<float> for K-major / K-outer operands whose 4-float
+// units are contiguous and 16-byte aligned, but the operands go global -> LDS
+// with buffer_load_dwordx4 ... lds (no registers, no ds_write) through a ring
+// of three K-tile stages: two K-tiles stay in flight while the third is
+// multiplied, each K-tile starting with a COUNTED vmcnt and one barrier.
+// ggemm_k's register staging holds one K-tile in flight, and a 64 x 64 x 32
+// fp32 K-tile is only ~1000 MFMA cycles per wave: the load latency was exposed
+// every K-tile (MFMA pipe ~55 % busy on the mlp.conf shapes,
+// profiles/ggemm_r4/pmc_f32.txt).
+//
+// LDS images (fp32, BK = 32 k per stage):
+//   K-major operand  [rows][32 k], 16-byte chunk c of row r at c ^ swz(r)
+//                    (f32_pos, as ggemm_k's image); lane (r = t>>3, slot t&7)
+//                    fetches chunk slot ^ swz(r), so one wave-instruction
+//                    fills 8 rows = 1 KB lane-linearly;
+//   K-outer operand  [32 k][rows], chunk c of k-row kr at c ^ (4 ((kr>>2)&3))
+//                    (kout_pos): the MFMA lanes of one k-step read k-rows
+//                    kr, kr+4, kr+8, kr+12 (lane groups l>>4) of 16
+//                    consecutive rows, and the XOR puts the four groups on
+//                    disjoint 16-bank sets -- ds_read_b32 conflict-free.
+// A lane of a 16x16x4 MFMA step q of k-chunk c holds k = 16c + 4(l>>4) + q for
+// both operands (float4 reads from K-major images, four scalar reads from
+// K-outer ones), i.e. ggemm_k's k order: the sum is the same fmaf chain.
+// Reference: DotEngine's fp32 sgemm, include/mshadow/tensor_expr_engine-inl.hpp:272-298.
+// ------------------------------------------------------------------------------
+constexpr unsigned D_OOB = 0xFFFFFFF0u;  // an offset past any extent: the load returns zeros
+constexpr unsigned D_BIAS = 0x80000000u; // masked lanes keep a biased offset (see igemm_kern.h)
+// The DMA is inline asm (M0 = the wave's LDS destination): issued through the
+// builtin, the compiler puts s_waitcnt vmcnt(0) in front of every LDS read it
+// cannot prove disjoint from the DMA in flight (here: every fragment read of
+// the runtime-indexed ring), serialising the ring.  The K loop waits for the
+// DMA itself with counted vmcnts; the compiler tracks the fragment reads.
+typedef int d_i32x4 __attribute__((ext_vector_type(4)));
+// (M0 is listed as clobbered: the compiler keeps nothing in it in these
+// kernels -- it is the LDS-DMA destination register and the asm sets it first)
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ void dma16(d_i32x4 r, unsigned off, unsigned lds_wave_base) {
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" ::"s"(lds_wave_base), "v"(off), "s"(r)
+               : "memory", "m0");
+}
+#pragma clang diagnostic pop
+// buffer resource: base, stride 0, num_records = bytes (0: a null resource)
+__device__ __forceinline__ d_i32x4 rsrc_of(const void* base, unsigned bytes) {
+  const uint64_t a = (uint64_t)base;
+  return d_i32x4{(int)(unsigned)a, (int)((unsigned)(a >> 32) & 0xFFFFu), (int)bytes, 0x00020000};
+}
+template <int N>
+__device__ __forceinline__ void d_wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+template <int ROWS>
+__device__ __forceinline__ int kout_pos(int row, int k) {
+  return k * ROWS + 4 * ((row >> 2) ^ (((k >> 2) & 3) << 2)) + (row & 3);
+}
+
+template <int ROWS, int MODE>
+struct DLd {
+  static constexpr bool RC = MODE == KOUT;
+  static constexpr int VPT = ROWS * BK / 4 / NT;  // 16-byte vectors per thread per K-tile
+  static constexpr int CPR = ROWS / 4;            // K-outer: chunks per k-row
+  static constexpr int KRP = NT / CPR;            // K-outer: k-rows per pass
+  static_assert(VPT >= 1 && (!RC || ROWS >= 64), "K-outer images need >= 64 rows (16 chunks per k-row)");
+  d_i32x4 rsrc;
+  unsigned voff[VPT];
+  unsigned ldb4;  // K-outer: bytes per k-row of the source
+  int wv, lk;     // wave; K-major: this lane's k within a tile, K-outer: its k-row within a pass
+
+  __device__ __forceinline__ void init(const float* src, unsigned bytes, int64_t ld, int row0, int nrows) {
+    const int t = threadIdx.x;
+    wv = __builtin_amdgcn_readfirstlane(t >> 6);
+    rsrc = rsrc_of(src, bytes);
+    if constexpr (!RC) {
+      const int rl = t >> 3;
+      lk = 4 * ((t & 7) ^ swz(rl));  // swz(rl + 32 v) == swz(rl)
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        if constexpr (M32) {
-          const int ml = wm * WTM + 32 * i + (l & 31);
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            tile[ml * LDT + wn * WTN + 32 * j + 8 * (r >> 2) + 4 * (l >> 5) + (r & 3)] = acc[i][j][r] * p.alpha;
-        } else {
-          const int ml = wm * WTM + 16 * i + (l & 15);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) tile[ml * LDT + wn * WTN + 16 * j + 4 * g4 + r] = acc[i][j][r] * p.alpha;
-        }
-      }
-    __syncthreads();
-    float* cbase = (float*)pc;
-    const bool addb = bias && blockIdx.z == 0;  // split-K of a biased GEMM: split 0 adds the bias
-    for (int row = wid; row < BM; row += NT / 64) {
-      const int m = m0 + row;
-      if (m >= p.M) break;
-#pragma unroll
-      for (int c0 = 0; c0 < BN; c0 += 64) {
-        const int n = n0 + c0 + l;
-        if (c0 + l < BN && n < p.N)
-          atomicAdd(cbase + (int64_t)m * p.ldc + n, tile[row * LDT + c0 + l] + (addb ? bias[n] : 0.f));
-      }
-    }
-    return;
-  }
-  auto store4 = [&](int m, int n, const float* a4) {
-    if (m >= p.M || n >= p.N) return;
-    const int64_t rowoff = (int64_t)m * p.ldc;
-    const bool full = n + 3 < p.N;
-    float v[4] = {a4[0] * p.alpha, a4[1] * p.alpha, a4[2] * p.alpha, a4[3] * p.alpha};
-    if (p.out_mode == O_F32_ATOMIC) {
-      float* c = (float*)pc + rowoff + n;
-      const bool addb = bias && blockIdx.z == 0;
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        if (full || n + r < p.N) atomicAdd(c + r, v[r] + (addb ? bias[n + r] : 0.f));
-      return;
-    }
-    if (bias) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] += (full || n + r < p.N) ? bias[n + r] : 0.f;
-    }
-    if (p.act_x) {  // fused activation backward: C = (A B) * act'(X)
-      const T* xa = (const T*)p.act_x + y * p.sc + rowoff + n;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] *= (full || n + r < p.N) ? dact_y(p.act_bwd, (float)xa[r]) : 0.f;
-    }
-    if (p.out_mode == O_F32) {
-      float* c = (float*)pc + rowoff + n;
-      const bool vst = full && ((p.ldc & 3) == 0) && (((uintptr_t)c & 15) == 0);
-      if (p.beta != 0.f) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (full || n + r < p.N) v[r] += p.beta * c[r];
-      }
-      if (p.aux) {
-        float* z = (float*)p.aux + y * p.sc + rowoff + n;
-        if (vst) *(float4*)z = make_float4(v[0], v[1], v[2], v[3]);
-        else {
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (n + r < p.N) z[r] = v[r];
-        }
-      }
-      if (p.relu) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = act_f(p.relu, v[r]);
-      }
-      if (vst) *(float4*)c = make_float4(v[0], v[1], v[2], v[3]);
-      else {
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (n + r < p.N) c[r] = v[r];
+      for (int v = 0; v < VPT; ++v) {
+        const int row = row0 + rl + 32 * v;
+        voff[v] = row < nrows ? (unsigned)(row * (int)ld + lk) * 4u : D_BIAS;
       }
     } else {
-      bf16* c = (bf16*)pc + rowoff + n;
-      const bool vst = full && ((p.ldc & 3) == 0) && (((uintptr_t)c & 7) == 0);
-      if (p.beta != 0.f) {
+      ldb4 = (unsigned)ld * 4u;
+      lk = t / CPR;
+      const int slot = t % CPR;
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (full || n + r < p.N) v[r] += p.beta * (float)c[r];
-      }
-      if (p.aux) {  // z rounded as a separate pass would see it
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const bf16 zb = (bf16)v[r];
-          if (n + r < p.N) ((bf16*)p.aux + y * p.sc + rowoff + n)[r] = zb;
-          v[r] = (float)zb;
-        }
-      }
-      if (p.relu) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = act_f(p.relu, v[r]);
-      }
-      if (vst) {
-        bf16x4 o;
-        o[0] = (bf16)v[0]; o[1] = (bf16)v[1]; o[2] = (bf16)v[2]; o[3] = (bf16)v[3];
-        *(bf16x4*)c = o;
-      } else {
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (n + r < p.N) c[r] = (bf16)v[r];
+      for (int v = 0; v < VPT; ++v) {
+        const int kr = lk + KRP * v;
+        const int col = row0 + 4 * (slot ^ (((kr >> 2) & 3) << 2));
+        voff[v] = col < nrows ? (unsigned)(kr * (int)ld + col) * 4u : D_BIAS;
       }
     }
+  }
+  // the K-tile at k0 into the stage image at `img`; live == false: a dummy
+  // through a null resource (keeps the per-tile DMA count uniform)
+  __device__ __forceinline__ void issue(int k0, int kend, unsigned img, bool live) const {
+    d_i32x4 rs = rsrc;
+    if (!live) rs[2] = 0;
+    const bool full = kend - k0 >= BK;
+#pragma unroll
+    for (int v = 0; v < VPT; ++v) {
+      unsigned off;
+      if constexpr (!RC) {
+        off = (full || k0 + lk < kend) ? voff[v] + (unsigned)k0 * 4u : D_OOB;
+      } else {
+        off = (full || k0 + lk + KRP * v < kend) ? voff[v] + (unsigned)k0 * ldb4 : D_OOB;
+      }
+      dma16(rs, off, img + 1024u * wv + 4096u * v);
+    }
+  }
+};
+
+template <int BM, int BN, int AM, int BMODE>
+__global__ void __launch_bounds__(NT, 2) f32d_k(const Args p) {
+  using T = float;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int STAGES = 3, D = STAGES - 1;
+  constexpr int A_B = BM * BK * 4, STAGE = (BM + BN) * BK * 4;
+  constexpr bool M32 = false;
+  constexpr int WTM = BM / 2, WTN = BN / 2, TM = WTM / 16, TN = WTN / 16;
+  typedef f32x4 AccT;
+
+  const int64_t y = blockIdx.y;
+  const float* pa = (const float*)p.a + y * p.sa;
+  const float* pb = (const float*)p.b + y * p.sb;
+  const float* bias = p.bias ? p.bias + y * p.sbias : nullptr;
+
+  const int tiles_m = (p.M + BM - 1) / BM, tiles_n = (p.N + BN - 1) / BN;
+  const int nwg = tiles_m * tiles_n;
+  int bid = blockIdx.x;
+  if (bid >= nwg) return;
+  if (nwg >= 8) {
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  }
+  const int band = 8;
+  const int group = bid / (band * tiles_n);
+  const int first_m = group * band;
+  const int gm = min(tiles_m - first_m, band);
+  const int tm = first_m + (bid % (band * tiles_n)) % gm;
+  const int tn = (bid % (band * tiles_n)) / gm;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int kbeg = blockIdx.z * p.k_per_split;
+  const int kend = min(p.K, kbeg + p.k_per_split);
+  if (p.out_mode == O_F32_ATOMIC && kbeg >= kend) return;
+  const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+
+  // operand extents (bytes) for the buffer resources: host-checked < 2^31
+  auto extent = [&](int mode, int rows, int64_t ld) -> unsigned {
+    return mode == KOUT ? (unsigned)(((int64_t)(p.K - 1) * ld + rows) * 4) : (unsigned)(((int64_t)(rows - 1) * ld + p.K) * 4);
   };
+  DLd<BM, AM> la;
+  DLd<BN, BMODE> lb;
+  la.init(pa, extent(AM, p.M, p.lda), p.lda, m0, p.M);
+  lb.init(pb, extent(BMODE, p.N, p.ldb), p.ldb, n0, p.N);
+
+  const int l = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int g4 = l >> 4;
+  AccT acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      if constexpr (M32) {
-        const int m = m0 + wm * WTM + 32 * i + (l & 31);
+    for (int j = 0; j < TN; ++j) acc[i][j] = AccT{};
+
+  auto compute = [&](const char* st) {
+    const float* sa_ = (const float*)st;
+    const float* sb_ = (const float*)(st + A_B);
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const float a4[4] = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
-          store4(m, n0 + wn * WTN + 32 * j + 8 * g + 4 * (l >> 5), a4);
+    for (int c = 0; c < BK / 16; ++c) {
+      const int k = 16 * c + 4 * g4;
+      float fa[TM][4], fb[TN][4];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int r = wm * WTM + 16 * i + (l & 15);
+        if constexpr (AM == KOUT) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) fa[i][q] = sa_[kout_pos<BM>(r, k + q)];
+        } else {
+          const float4 v = *(const float4*)(sa_ + f32_pos(r, k));
+          fa[i][0] = v.x; fa[i][1] = v.y; fa[i][2] = v.z; fa[i][3] = v.w;
         }
-      } else {
-        const float a4[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-        store4(m0 + wm * WTM + 16 * i + (l & 15), n0 + wn * WTN + 16 * j + 4 * g4, a4);
       }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int r = wn * WTN + 16 * j + (l & 15);
+        if constexpr (BMODE == KOUT) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) fb[j][q] = sb_[kout_pos<BN>(r, k + q)];
+        } else {
+          const float4 v = *(const float4*)(sb_ + f32_pos(r, k));
+          fb[j][0] = v.x; fb[j][1] = v.y; fb[j][2] = v.z; fb[j][3] = v.w;
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fb[j][q], fa[i][q], acc[i][j], 0, 0, 0);
     }
+  };
+
+  // fused column sums of B (workgroups of the first M tile), as in ggemm_k
+  const bool do_cs = p.csum != nullptr && tm == 0;
+  constexpr int CS_G = NT / BN, CS_K = BK / CS_G;
+  float cs_acc = 0.f;
+  auto colsum_tile = [&](const char* st) {
+    const float* sb_ = (const float*)(st + A_B);
+    const int n = threadIdx.x % BN, k0 = (threadIdx.x / BN) * CS_K;
+#pragma unroll
+    for (int k = 0; k < CS_K; ++k) {
+      if constexpr (BMODE == KOUT) cs_acc += sb_[kout_pos<BN>(n, k0 + k)];
+      else cs_acc += sb_[f32_pos(n, k0 + k)];
+    }
+  };
+
+  if (nk > 0) {
+    constexpr int LPT = DLd<BM, AM>::VPT + DLd<BN, BMODE>::VPT;
+    static_assert(D * LPT < 64, "vmcnt range");
+    const unsigned lds0 = (unsigned)(size_t)(__attribute__((address_space(3))) char*)smem;
+#pragma unroll
+    for (int s = 0; s < D; ++s) {
+      la.issue(kbeg + s * BK, kend, lds0 + s * STAGE, s < nk);
+      lb.issue(kbeg + s * BK, kend, lds0 + s * STAGE + A_B, s < nk);
+    }
+    int cur = 0, fill = D;
+    for (int kt = 0; kt < nk; ++kt) {
+      d_wait_vmcnt<(D - 1) * LPT>();  // this wave's DMA of K-tile kt landed
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_s_barrier();   // ... every wave's; stage `fill` is no longer read
+      asm volatile("" ::: "memory");
+      const unsigned st = lds0 + (unsigned)(fill * STAGE);
+      const bool live = kt + D < nk;
+      la.issue(kbeg + (kt + D) * BK, kend, st, live);
+      lb.issue(kbeg + (kt + D) * BK, kend, st + A_B, live);
+      compute(smem + cur * STAGE);
+      if (do_cs) colsum_tile(smem + cur * STAGE);
+      cur = cur + 1 == STAGES ? 0 : cur + 1;
+      fill = fill + 1 == STAGES ? 0 : fill + 1;
+    }
+  }
+  d_wait_vmcnt<0>();  // the dummy DMAs too, before the LDS is reused
+  __syncthreads();
+
+  if (do_cs) {
+    float* red = (float*)smem;
+    red[threadIdx.x] = cs_acc;
+    __syncthreads();
+    if ((int)threadIdx.x < BN && n0 + (int)threadIdx.x < p.N) {
+      float sum = 0.f;
+#pragma unroll
+      for (int g = 0; g < CS_G; ++g) sum += red[g * BN + threadIdx.x];
+      atomicAdd(p.csum + n0 + threadIdx.x, sum);
+    }
+    __syncthreads();
+  }
+  constexpr int EPI_LDS = STAGES * STAGE;
+#include "ggemm_epilogue.inc"
+}
+
+template <int BM, int BN, int AM, int BMODE>
+static void launch_d(const Args& p, int batch, int splits, hipStream_t s) {
+  const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
+  constexpr int lds = 3 * (BM + BN) * BK * 4;
+  auto* kern = f32d_k<BM, BN, AM, BMODE>;
+  if constexpr (lds > 65536) {
+    static bool attr = [kern] {
+      return hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
+    }();
+    (void)attr;
+  }
+  hipLaunchKernelGGL(kern, dim3(tiles, batch, splits), dim3(NT), lds, s, p);
 }
 
 template <typename T, int BM, int BN, int AM, int BMODE, bool M32V = true>
@@ -675,7 +820,8 @@ static int pick_splits(int M, int N, int K, int batch, int want, int bm, int bn)
 // beta = 1 -- and the splits add into it with atomics, split 0 adding the bias).
 // (Measured and dropped: a 2-deep register prefetch of the global loads --
 // no gain at any MLP shape, +36 VGPRs.)
-static int g_gg[2] = {0, 0};
+// key 2 = the LDS-DMA fp32 kernel f32d_k (0 on where it applies, -1 never).
+static int g_gg[3] = {0, 0, 0};
 
 static void tile_dims(int t, int& bm, int& bn) {
   bm = (t == 2 || t == 3 || t == 5) ? 128 : (t == 7 || t == 8) ? 32 : 64;
@@ -738,6 +884,48 @@ static void launch_f32(const Args& p, int batch, int splits, int tile, hipStream
   }
 }
 
+// the LDS-DMA fp32 kernel for tile t when its constraints hold: both
+// operands in 16-byte units (vec), K-outer operands >= 64 tile rows, operand
+// extents < 2 GiB (32-bit buffer offsets)
+template <int AM, int BMODE>
+static bool launch_dma_t(const Args& p, int batch, int splits, int tile, hipStream_t s) {
+  switch (tile) {
+    case 1: launch_d<64, 64, AM, BMODE>(p, batch, splits, s); return true;
+    case 3: launch_d<128, 64, AM, BMODE>(p, batch, splits, s); return true;
+    case 4: launch_d<64, 128, AM, BMODE>(p, batch, splits, s); return true;
+    case 5: launch_d<128, 128, AM, BMODE>(p, batch, splits, s); return true;
+    default: break;
+  }
+  if constexpr (AM == KMAJ) {
+    if (tile == 7) { launch_d<32, 64, AM, BMODE>(p, batch, splits, s); return true; }
+    if constexpr (BMODE == KMAJ) {
+      if (tile == 8) { launch_d<32, 32, AM, BMODE>(p, batch, splits, s); return true; }
+    }
+  }
+  if constexpr (BMODE == KMAJ) {
+    if (tile == 6) { launch_d<64, 32, AM, BMODE>(p, batch, splits, s); return true; }
+  }
+  return false;
+}
+
+static int g_last_dma = 0;  // the last fp32 sg_ggemm ran f32d_k (tests)
+static bool try_dma(const Args& p, int a_kouter, int b_kouter, int batch, int splits, int tile, hipStream_t s) {
+  g_last_dma = 0;
+  if (g_gg[2] < 0 || !p.vec_a || !p.vec_b || p.K <= 0) return false;
+  auto ext = [&](bool kout, int rows, int64_t ld, int64_t sb) {
+    return ((kout ? (int64_t)(p.K - 1) * ld + rows : (int64_t)(rows - 1) * ld + p.K) + sb * (batch - 1)) * 4;
+  };
+  if (ext(a_kouter, p.M, p.lda, p.sa) >= ((int64_t)1 << 31) || ext(b_kouter, p.N, p.ldb, p.sb) >= ((int64_t)1 << 31))
+    return false;
+  bool ok;
+  if (!a_kouter && !b_kouter) ok = launch_dma_t<KMAJ, KMAJ>(p, batch, splits, tile, s);
+  else if (!a_kouter && b_kouter) ok = launch_dma_t<KMAJ, KOUT>(p, batch, splits, tile, s);
+  else if (a_kouter && !b_kouter) ok = launch_dma_t<KOUT, KMAJ>(p, batch, splits, tile, s);
+  else ok = launch_dma_t<KOUT, KOUT>(p, batch, splits, tile, s);
+  g_last_dma = ok ? 1 : 0;
+  return ok;
+}
+
 static inline int kps(int K, int splits) {
   const int nkt = (K + BK - 1) / BK;
   return ((nkt + splits - 1) / splits) * BK;
@@ -774,8 +962,9 @@ extern "C" {
 int sg_bn_deterministic();
 
 void sg_ggemm_tune(int key, int value) {
-  if (key >= 0 && key < 2) g_gg[key] = value;
+  if (key >= 0 && key < 3) g_gg[key] = value;
 }
+int sg_ggemm_last_dma() { return g_last_dma; }
 
 // Generic GEMM (dt 0: fp32 operands, 1: bf16 operands):
 //   C[batch][M][N] = alpha * A(m, k) B(n, k) (+ beta C) (+ bias[n]) (ReLU)
@@ -833,6 +1022,7 @@ void sg_ggemm(int dt, const void* a, int64_t lda, int a_kouter, int64_t sa, cons
   p.g = make_geom(1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0, 0, 1, 1, 1);
   p.vec_a = f ? aligned<float>(a, lda, sa, a_kouter ? M : K) : aligned<sg::bf16>(a, lda, sa, a_kouter ? M : K);
   p.vec_b = f ? aligned<float>(b, ldb, sb, b_kouter ? N : K) : aligned<sg::bf16>(b, ldb, sb, b_kouter ? N : K);
+  if (f && try_dma(p, a_kouter, b_kouter, batch, splits, tile, s)) return;
   if (f) {
     if (!a_kouter && !b_kouter) launch_f32<KMAJ, KMAJ>(p, batch, splits, tile, s);
     else if (!a_kouter && b_kouter) launch_f32<KMAJ, KOUT>(p, batch, splits, tile, s);

@@ -85,6 +85,40 @@ def test_fp32_gemm_every_tile_and_split(gpu, tile, splits):
         L.ggemm_tune(1, 0)
 
 
+@pytest.mark.parametrize("tile", [0, 1, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("splits", [0, -1, 3])
+def test_fp32_dma_gemm_every_tile_and_split(gpu, tile, splits):
+    """The LDS-DMA fp32 kernel (f32d_k: 16-byte-unit operands, ragged tile
+    edges, K not a multiple of the K-tile) on the three MLP GEMM layouts --
+    K-major x K-outer forward with bias, K-outer x K-outer weight gradient
+    with the fused bias-gradient column sums, K-major x K-major data gradient
+    -- exact to 1e-5 against fp64, and the DMA kernel really ran (32-row tiles
+    fall back to ggemm_k where a K-outer operand has 32 rows)."""
+    from singa_amd.ops import functional as F
+    from singa_amd.ops import native as N
+    L = N.lib()
+    x, w, b = _rand(300, 204, seed=21), _rand(204, 156, seed=22), _rand(156, seed=23)
+    dy, acc, db0 = _rand(300, 156, seed=24), _rand(204, 156, seed=25), _rand(156, seed=26)
+    kout_ok = tile not in (6, 7, 8)  # a K-outer operand needs >= 64 tile rows
+    try:
+        L.ggemm_tune(0, tile)
+        L.ggemm_tune(1, splits)
+        y = F.matmul(x.to(gpu), w.to(gpu), bias=b.to(gpu))
+        assert rel_err(y, x.double() @ w.double() + b.double()) < 1e-5
+        assert tile == 0 or L.ggemm_last_dma() == (1 if kout_ok or tile == 7 else 0)
+        g, db = acc.to(gpu), db0.to(gpu)
+        F.gemm_tn_acc(x.to(gpu), dy.to(gpu), g, colsum_b=db)
+        assert rel_err(g, acc.double() + x.double().t() @ dy.double()) < 1e-5
+        assert rel_err(db, db0.double() + dy.double().sum(0)) < 1e-5
+        assert tile == 0 or L.ggemm_last_dma() == (1 if kout_ok else 0)
+        dx = F.gemm_nt(dy.to(gpu), w.to(gpu))
+        assert rel_err(dx, dy.double() @ w.double().t()) < 1e-5
+        assert tile == 0 or L.ggemm_last_dma() == 1
+    finally:
+        L.ggemm_tune(0, 0)
+        L.ggemm_tune(1, 0)
+
+
 _ACTS = {"relu": torch.relu, "sigmoid": torch.sigmoid, "tanh": torch.tanh,
          "stanh": lambda h: 1.7159047 * torch.tanh(0.66666667 * h)}
 

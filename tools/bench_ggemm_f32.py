@@ -42,6 +42,7 @@ def main():
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--tiles", default="1,2,3,4,5,6,7,8")
     ap.add_argument("--splits", default="-1,2,3,4,6,8")
+    ap.add_argument("--dma", default="0,-1", help="ggemm_tune(2, v): 0 the LDS-DMA kernel where it applies, -1 never")
 
     ap.add_argument("--square", type=int, default=4096)
     ap.add_argument("--out", default=None)
@@ -52,6 +53,7 @@ def main():
     B = a.batch
     tiles = [int(v) for v in a.tiles.split(",")]
     splits = [int(v) for v in a.splits.split(",")]
+    dmas = [int(v) for v in a.dma.split(",")]
     shapes = []
     for i in range(len(DIMS) - 1):
         fin, fout = DIMS[i], DIMS[i + 1]
@@ -82,10 +84,11 @@ def main():
     for name, flops, fn, ref in shapes:
         r = ref()
         scale = r.abs().max().item() + 1e-30
-        for t, sp in [(t, sp) for t in tiles for sp in splits]:
+        for t, sp, dm in [(t, sp, dm) for t in tiles for sp in splits for dm in dmas]:
             if True:
                 L.ggemm_tune(0, t)
                 L.ggemm_tune(1, sp)
+                L.ggemm_tune(2, dm)
                 if name.startswith("square") and sp not in (-1, splits[0]):
                     continue
                 if name.startswith("wgrad"):
@@ -94,7 +97,7 @@ def main():
                 torch.cuda.synchronize()
                 err = (c.double() - r).abs().max().item() / scale
                 us = timeit(fn)
-                rec = {"shape": name, "tile": t, "splits": sp, "us": round(us, 1),
+                rec = {"shape": name, "tile": t, "splits": sp, "dma": L.ggemm_last_dma(), "us": round(us, 1),
                        "tflops": round(flops / us / 1e6, 1), "rel_err": float(f"{err:.2e}")}
                 line = json.dumps(rec)
                 print(line, flush=True)
@@ -104,8 +107,10 @@ def main():
                     best[name] = rec
         L.ggemm_tune(0, 0)
         L.ggemm_tune(1, 0)
+        L.ggemm_tune(2, 0)
         us = timeit(fn)
-        rec = {"shape": name, "tile": "auto", "us": round(us, 1), "tflops": round(flops / us / 1e6, 1)}
+        rec = {"shape": name, "tile": "auto", "dma": L.ggemm_last_dma(), "us": round(us, 1),
+               "tflops": round(flops / us / 1e6, 1)}
         print(json.dumps(rec), flush=True)
         best[name + " (auto)"] = rec
     print("# best per shape")
