@@ -820,7 +820,8 @@ static int pick_splits(int M, int N, int K, int batch, int want, int bm, int bn)
 // beta = 1 -- and the splits add into it with atomics, split 0 adding the bias).
 // (Measured and dropped: a 2-deep register prefetch of the global loads --
 // no gain at any MLP shape, +36 VGPRs.)
-// key 2 = the LDS-DMA fp32 kernel f32d_k (0 on where it applies, -1 never).
+// key 2 = the LDS-DMA fp32 kernel f32d_k (0 on where it applies, the tile
+// choice restricted to its tiles; 1 on, unrestricted choice; -1 never).
 static int g_gg[3] = {0, 0, 0};
 
 static void tile_dims(int t, int& bm, int& bn) {
@@ -841,7 +842,12 @@ __global__ void zero_rows_k(float* c, int64_t ldc, int64_t sc, int N) {
 // for split-K the extra output traffic (zeroing + one fp32 atomic per split
 // per element at ~4 TB/s).  On the mlp.conf shapes its picks are within 2.5 %
 // of the best configuration of the sweep (profiles/ggemm_r4/).
-static void pick_f32(int M, int N, int K, int batch, bool can_split, bool zero_first, int& tile, int& splits) {
+// With operands the LDS-DMA kernel takes (dma: 0 no, else 1 + 2 a_kouter +
+// 4 b_kouter), only the tiles it runs are candidates: f32d_k beat ggemm_k at
+// every such (shape, tile, splits) of the mlp.conf sweep
+// (profiles/r5/ggemm_f32_dma_sweep.jsonl); 32-row tiles need that operand K-major.
+static void pick_f32(int M, int N, int K, int batch, bool can_split, bool zero_first, int& tile, int& splits,
+                     int dma = 0) {
   static const int cand[] = {1, 7, 3, 4, 6, 8};
   static const double eff[] = {0, 1.0, 0, 0.9, 0.9, 0, 0.85, 0.9, 0.85};
   static const int sps[] = {1, 2, 3, 4, 8};
@@ -852,6 +858,7 @@ static void pick_f32(int M, int N, int K, int batch, bool can_split, bool zero_f
   for (int t : cand) {
     int bm, bn;
     tile_dims(t, bm, bn);
+    if (dma && ((bm < 64 && (dma & 2)) || (bn < 64 && (dma & 4)))) continue;
     const long tiles = (long)((M + bm - 1) / bm) * ((N + bn - 1) / bn) * batch;
     for (int sp : sps) {
       if (sp > 1 && (!can_split || nkt < 2 * sp)) continue;
@@ -995,7 +1002,10 @@ void sg_ggemm(int dt, const void* a, int64_t lda, int a_kouter, int64_t sa, cons
     const bool plain_ok = out_mode == O_F32 && !relu && !act_x && !aux && (beta == 0.f || beta == 1.f);
     const bool can_split = out_mode == O_F32_ATOMIC || plain_ok;
     int sp = 1;
-    pick_f32(M, N, K, batch, can_split, out_mode == O_F32 && beta == 0.f, tile, sp);
+    const bool dma_ops = g_gg[2] >= 0 && aligned<float>(a, lda, sa, a_kouter ? M : K) &&
+                         aligned<float>(b, ldb, sb, b_kouter ? N : K);
+    pick_f32(M, N, K, batch, can_split, out_mode == O_F32 && beta == 0.f, tile, sp,
+             dma_ops && g_gg[2] == 0 ? 1 + (a_kouter ? 2 : 0) + (b_kouter ? 4 : 0) : 0);
     if (g_gg[0] > 0) tile = g_gg[0];
     if (sg_bn_deterministic()) sp = 1;  // split-K atomics add in arbitrary order
     if (g_gg[1] != 0) sp = g_gg[1] > 1 && K >= 2 * BK * g_gg[1] ? g_gg[1] : 1;
