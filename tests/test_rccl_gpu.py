@@ -364,7 +364,7 @@ def _easgd_pp_rank(rank, world, comm, per_param):
           for n in (3000, 517, 4096, 64, 2000)]
     o = SGD(0.05, 0.9, weight_decay=1e-4)
     st = o.attach(ps)
-    es = ElasticSync(st, comm, moving_rate=0.9, sync_frequency=2, overlap=True, bucket_mb=0.01)
+    es = ElasticSync(st, comm, moving_rate=0.9, sync_frequency=2, overlap=True, bucket_mb=0.005)
     es.bootstrap()
     gg = torch.Generator().manual_seed(rank + 1)
     for step in range(7):
