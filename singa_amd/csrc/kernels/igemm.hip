@@ -179,6 +179,8 @@ static int make_phases(ConvGeom& g) {
 // key 11: 1 = strided data gradients never take the single-stage short-K kernel (A/B)
 // key 12: > 0 forces the split count of the 8-wave weight gradient (sweeps);
 // key 13: split policy of that kernel: 1 = quantisation-aware (default), 0 = powers of 2 to the target
+// key 14: the 4-wave three-stage ring for the plain (K-major / K-outer) GEMMs of the generic tile path:
+//         0 = auto (under-filled launches of 8-64 K-tiles), 3 = always, -1 = never
 static int g_tune[16] = {5, 1, 1, 0, 0, 1, 8, 1, 0, 1, 0, 0, 0, 1, 0, 0};
 // one-shot: the next dgrad's wt scratch is already transposed.  Per OS
 // thread: the runtime's executor threads (hogwild / aggregated replicas)
@@ -404,6 +406,24 @@ static void launch(const GemmArgs& p, int M, int splits, hipStream_t s, int batc
   }
   const int tiles = ((M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
   const int z = zdim > 0 ? zdim : splits;
+  // three-stage ring for plain GEMMs that leave the chip under-filled (at most
+  // four workgroups per CU) with 8-64 K-tiles each: the Linear layers of a
+  // BERT-sized batch, where each workgroup's K loop ran at the DMA latency.
+  // Measured (profiles/r5/ab_bert_three_stage_ring.jsonl, bert_tiles_r6n.jsonl):
+  // BERT-base 3 780 -> 3 905 seq/s, sonnx-BERT 3 608 -> 3 714; ResNet-50 and
+  // AlexNet within noise when forced everywhere.  Knob 14: 0 auto, 3 always, -1 never.
+  if constexpr ((AM == LM_KMAJOR || AM == LM_KOUTER) && (BMODE == LM_KMAJOR || BMODE == LM_KOUTER) && FLAGS == 0) {
+    const long wgs = (long)tiles * (batch > 0 ? batch : 1) * (z > 0 ? z : 1);
+    const int nkt = ((z > 1 ? p.k_per_split : p.K) + BK - 1) / BK;
+    const bool ring = g_tune[14] == 3 || (g_tune[14] == 0 && wgs <= 4L * sg_cu_count() && nkt >= 8 && nkt <= 64);
+    if (ring && !p.out_phase) {
+      if (BM == 128 && BN == 128) launch_t<128, 128, AM, BMODE, OUT, NT, 2, 2, 3>(p, tiles, batch, z, s);
+      else if (BM == 128 && BN == 64) launch_t<128, 64, AM, BMODE, OUT, NT, 2, 2, 3>(p, tiles, batch, z, s);
+      else if (BM == 64 && BN == 128) launch_t<64, 128, AM, BMODE, OUT, NT, 2, 2, 3>(p, tiles, batch, z, s);
+      else launch_t<64, 64, AM, BMODE, OUT, NT, 2, 2, 3>(p, tiles, batch, z, s);
+      return;
+    }
+  }
   if (BM == 128 && BN == 128) launch_t<128, 128, AM, BMODE, OUT, NT, 2, 2, 2, FLAGS>(p, tiles, batch, z, s);
   else if (BM == 128 && BN == 64) launch_t<128, 64, AM, BMODE, OUT, NT, 2, 2, 2, FLAGS>(p, tiles, batch, z, s);
   else if (BM == 64 && BN == 128) launch_t<64, 128, AM, BMODE, OUT, NT, 2, 2, 2, FLAGS>(p, tiles, batch, z, s);

@@ -759,6 +759,37 @@ __global__ void __launch_bounds__(NTH, STAGES == 1 ? 3 : (NTH == 512 && STAGES =
         if (kt + 1 < nk) step(std::integral_constant<int, 1>{}, kt + 1);
       }
     }
+  } else if constexpr (STAGES == 3 && NTH == 256) {
+    // 4-wave three-stage ring for SHORT workgroups (BERT-sized GEMMs: a few
+    // hundred tiles of 12-48 K-tiles, 1-2 workgroups per CU): two K-tiles in
+    // flight while the third multiplies.  The 2-stage loops keep one in
+    // flight, and a 64-wide K-tile is only ~250 MFMA cycles per wave, so their
+    // K loop ran at the DMA latency.  Unrolled by three: every stage offset is
+    // a compile-time constant (the fragment reads carry it as an immediate and
+    // the compiler can tell them from the DMA into the other stages).
+    constexpr int LPT = Loader<BM, AM, NTH>::VPT + Loader<BN, BMODE, NTH>::VPT;
+    static_assert(LPT < 64, "vmcnt range");
+    auto step = [&](auto stage, int kt) {
+      constexpr int cur = decltype(stage)::value;
+      constexpr int fill = (cur + 2) % 3;
+      wait_vmcnt<LPT>();  // this wave's DMA for tile kt landed (tile kt+1 may still fly)
+      raw_barrier();      // ... every wave's; every wave done reading stage `fill` (tile kt-1)
+      const bool live = kt + 2 < nk;
+      la.issue(p, m0, M, kbeg + (kt + 2) * BK, kend, P, smem + fill * STAGE, live);
+      lb.issue(p, n0, p.N, kbeg + (kt + 2) * BK, kend, P, smem + fill * STAGE + A_BYTES, live);
+      compute_c(stage);
+    };
+    if (nk > 0) {
+      la.issue(p, m0, M, kbeg, kend, P, smem);
+      lb.issue(p, n0, p.N, kbeg, kend, P, smem + A_BYTES);
+      la.issue(p, m0, M, kbeg + BK, kend, P, smem + STAGE, nk > 1);
+      lb.issue(p, n0, p.N, kbeg + BK, kend, P, smem + STAGE + A_BYTES, nk > 1);
+      for (int kt = 0; kt < nk; kt += 3) {
+        step(std::integral_constant<int, 0>{}, kt);
+        if (kt + 1 < nk) step(std::integral_constant<int, 1>{}, kt + 1);
+        if (kt + 2 < nk) step(std::integral_constant<int, 2>{}, kt + 2);
+      }
+    }
   } else if constexpr (STAGES == 2) {
     auto step = [&](auto stage, int kt) {
       constexpr int cur = decltype(stage)::value;
