@@ -181,7 +181,9 @@ static int make_phases(ConvGeom& g) {
 // key 13: split policy of that kernel: 1 = quantisation-aware (default), 0 = powers of 2 to the target
 // key 14: the 4-wave three-stage ring for the plain (K-major / K-outer) GEMMs of the generic tile path:
 //         0 = auto (under-filled launches of 8-64 K-tiles), 3 = always, -1 = never
-static int g_tune[16] = {5, 1, 1, 0, 0, 1, 8, 1, 0, 1, 0, 0, 0, 1, 0, 0};
+// key 15: 1 = the 8-wave weight gradient on 256 x 128 tiles (64 x 64 wave tiles, three-stage ring) when K >= 256
+//         (ResNet-50 b1024 step +0.33 %, three alternating pairs on one box: profiles/r5/ab_wgrad_256x128.jsonl)
+static int g_tune[16] = {5, 1, 1, 0, 0, 1, 8, 1, 0, 1, 0, 0, 0, 1, 0, 1};
 // one-shot: the next dgrad's wt scratch is already transposed.  Per OS
 // thread: the runtime's executor threads (hogwild / aggregated replicas)
 // each set and consume their own flag, so one thread's set can never be
@@ -843,8 +845,8 @@ void sg_conv_dgrad_bn_ex(const void* dy, const void* w, void* dx, int N, int H, 
 // the output).  Measured on the ResNet-50 b1024 shapes (tools/wgrad_sweep.py,
 // profiles/r5/wgrad_sweep.jsonl): stage-2/3/4 3x3 weight gradients 368 / 300 /
 // 293 us -> 263 / 266 / 255 us (splits 56 / 14 / 7).
-static int wgrad_splits_q(int tiles, int nkt, int sp0) {
-  const int slots = 2 * sg_cu_count();
+static int wgrad_splits_q(int tiles, int nkt, int sp0, int per_cu = 2) {
+  const int slots = per_cu * sg_cu_count();
   constexpr int e = 6;
   int best = sp0;
   long best_cost = (long)((tiles * sp0 + slots - 1) / slots) * ((nkt + sp0 - 1) / sp0 + e);
@@ -904,6 +906,21 @@ void sg_conv_wgrad(const void* x, const void* dy, void* dw_out, int N, int H, in
     while (tiles * sp < target && sp * 2 * 4 <= nkt) sp *= 2;
     if (g_tune[13] && g_tune[10] <= 0) sp = wgrad_splits_q(tiles, nkt, sp);
     if (g_tune[12] > 0) sp = g_tune[12];
+    if (g_tune[15] == 1 && p.M >= 256) {
+      // 256 x 128 tiles of 64 x 64 wave tiles (half the LDS fragment traffic
+      // per MFMA of the 64 x 32 wave tiles), three-stage ring, one per CU
+      const int t2 = ((p.M + 255) / 256) * ((p.N + 127) / 128);
+      int sp2 = 1;
+      while (t2 * sp2 < target && sp2 * 2 * 4 <= nkt) sp2 *= 2;
+      // (one workgroup per CU: its 144 KB ring; the model's picks match the
+      // best measured split of every eligible ResNet-50 layer,
+      // profiles/r5/wgrad_sweep_256x128_on.jsonl)
+      if (g_tune[13] && g_tune[10] <= 0) sp2 = wgrad_splits_q(t2, nkt, sp2, 1);
+      if (g_tune[12] > 0) sp2 = g_tune[12];
+      p.k_per_split = kps(p.K, sp2);
+      launch_t<256, 128, LM_KOUTER, LM_WGRAD_B, OUT_F32_ATOMIC, 512, 4, 2, 3>(p, t2, 1, sp2, s);
+      return;
+    }
     p.k_per_split = kps(p.K, sp);
     launch_t<128, 128, LM_KOUTER, LM_WGRAD_B, OUT_F32_ATOMIC, 512, 2, 4, 2>(p, tiles, 1, sp, s);
     return;

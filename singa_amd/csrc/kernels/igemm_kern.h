@@ -759,12 +759,14 @@ __global__ void __launch_bounds__(NTH, STAGES == 1 ? 3 : (NTH == 512 && STAGES =
         if (kt + 1 < nk) step(std::integral_constant<int, 1>{}, kt + 1);
       }
     }
-  } else if constexpr (STAGES == 3 && NTH == 256) {
-    // 4-wave three-stage ring for SHORT workgroups (BERT-sized GEMMs: a few
+  } else if constexpr (STAGES == 3) {
+    // Three-stage ring with compile-time stages.  4 waves: for SHORT workgroups (BERT-sized GEMMs: a few
     // hundred tiles of 12-48 K-tiles, 1-2 workgroups per CU): two K-tiles in
     // flight while the third multiplies.  The 2-stage loops keep one in
     // flight, and a 64-wide K-tile is only ~250 MFMA cycles per wave, so their
-    // K loop ran at the DMA latency.  Unrolled by three: every stage offset is
+    // K loop ran at the DMA latency.  8 waves (the 256 x 128 tile of 64 x 64
+    // wave tiles, one workgroup per CU): the weight-gradient variant of knob 15.
+    // Unrolled by three: every stage offset is
     // a compile-time constant (the fragment reads carry it as an immediate and
     // the compiler can tell them from the DMA into the other stages).
     constexpr int LPT = Loader<BM, AM, NTH>::VPT + Loader<BN, BMODE, NTH>::VPT;

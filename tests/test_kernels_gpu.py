@@ -144,6 +144,35 @@ def test_conv_fwd_bwd(gpu, case, wmode, kmajor, monkeypatch):
     assert rel_err(db, dy.sum((0, 2, 3))) < 1e-5
 
 
+@pytest.mark.parametrize("case", [(2, 64, 28, 28, 256, 3, 3, 1, 1), (2, 128, 14, 14, 512, 3, 3, 1, 1),
+                                  (2, 256, 28, 28, 256, 1, 1, 1, 0), (3, 128, 15, 15, 384, 3, 3, 2, 1)])
+def test_conv_wgrad_256x128_ring(gpu, case):
+    """The 8-wave weight gradient on 256 x 128 tiles (tuning knob 15: 64 x 64
+    wave tiles, the compile-time three-stage ring, split-K atomics) == the
+    fp32 PyTorch weight gradient of the same bf16-rounded operands."""
+    from singa_amd.ops import functional as F
+    from singa_amd.ops import native as NN
+    N_, C, H, W, K, R, S, st, pd = case
+    g = torch.Generator().manual_seed(5)
+    x = bf(torch.randn(N_, C, H, W, generator=g)).float()
+    w = bf(torch.randn(K, C, R, S, generator=g) * (1.0 / math.sqrt(C * R * S))).float()
+    wr = w.clone().requires_grad_(True)
+    yr = TF.conv2d(x, wr, None, st, pd)
+    dy = bf(torch.randn(yr.shape, generator=g)).float()
+    yr.backward(dy)
+    xg = x.to(gpu).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    dyg = dy.to(gpu).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    for knob in (1, 0):  # the 256 x 128 variant (default) and the 128 x 128 one
+        NN.lib().set_tuning(15, knob)
+        try:
+            dw_acc = torch.zeros(K, C, R, S, device=gpu)
+            F.conv2d_bwd(xg, w.to(gpu), dyg, (st, st), (pd, pd), need_dx=False, dw_out=dw_acc)
+            torch.cuda.synchronize()
+        finally:
+            NN.lib().set_tuning(15, 1)
+        assert rel_err(dw_acc, wr.grad) < 1e-5
+
+
 @pytest.fixture
 def big_tiles():
     """Force an 8-wave conv/GEMM variant (5: 128x128 two workgroups per CU,
