@@ -127,6 +127,7 @@ void sg_ggemm(int, const void*, int64_t, int, int64_t, const void*, int64_t, int
               hipStream_t);
 void sg_ggemm_tune(int, int);
 int sg_ggemm_last_dma();
+void sg_bnres_tune(int, int);
 int sg_stem_fwd(const void*, const void*, void*, void*, int, int, int, int, int, hipStream_t);
 void sg_conv3x3_set(int);
 int sg_conv3x3_enabled();
@@ -503,6 +504,7 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("ggemm_tune", [](int key, int value) { sg_ggemm_tune(key, value); });
   m.def("ggemm_last_dma", []() { return sg_ggemm_last_dma(); });
+  m.def("bnres_tune", [](int key, int v) { sg_bnres_tune(key, v); });
   // persistent 3x3 64-channel stage-1 conv (csrc/kernels/conv3x3.hip): A/B switch
   m.def("conv3x3_set", [](int on) { sg_conv3x3_set(on); });
   m.def("conv3x3_enabled", []() { return sg_conv3x3_enabled(); });

@@ -277,6 +277,8 @@ void go(const GemmArgs& p, int tiles, int zdim, hipStream_t s) {
   hipLaunchKernelGGL(kern, dim3(tiles, 1, zdim), dim3(NTH), lds, s, p);
 }
 
+int g_wide = 1;  // sg_bnres_tune(0, v): the 256 x 128 weight-gradient tiles (A/B)
+
 unsigned extent(int64_t elems) {
   if (elems * 2 >= (int64_t)1 << 31) throw std::runtime_error("bnres: operand exceeds 2 GiB (32-bit buffer offsets)");
   return (unsigned)(elems * 2);
@@ -289,6 +291,10 @@ using namespace sg;
 using namespace sg::bnres;
 
 extern "C" {
+
+void sg_bnres_tune(int key, int v) {
+  if (key == 0) g_wide = v;
+}
 
 // out [K4 + C][C] fp32 (zeroed by the caller) += [g | y]^T y over P pixels:
 // rows 0..K4-1 = G = g^T y, rows K4.. = Gram(y).  g [P][K4], y [P][C] bf16.
@@ -308,6 +314,26 @@ void sg_bnres_wgrad(const void* g, const void* y, void* out, int P, int K4, int 
   p.b = (const bf16*)y; p.ldb = C; p.b_bytes = p.a2_bytes;
   p.c = out; p.ldc = C; p.alpha = 1.f;
   const int nkt = (P + BK - 1) / BK;
+  // 256 x 128 8-wave tiles (64 x 64 wave tiles, three-stage ring, one
+  // workgroup per CU) when the G / Gram split is 256-row aligned: the split
+  // count minimising ceil(tiles * sp / CUs) * (K-tiles per split + 6) (the
+  // quantisation model of the conv weight gradient, igemm.hip wgrad_splits_q)
+  if (C >= 128 && (K4 & 255) == 0 && g_wide) {
+    const int tiles = ((p.M + 255) / 256) * ((C + 127) / 128);
+    const int slots = sg_cu_count();
+    int sp = 1;
+    long best = -1;
+    for (int s2 = 1; s2 <= 256 && nkt / s2 >= 16; ++s2) {
+      const long cost = (long)((tiles * s2 + slots - 1) / slots) * ((nkt + s2 - 1) / s2 + 6);
+      if (best < 0 || cost < best) {
+        best = cost;
+        sp = s2;
+      }
+    }
+    p.k_per_split = ((nkt + sp - 1) / sp) * BK;
+    go<256, 128, LM_KOUTER2, LM_KOUTER, OUT_F32_ATOMIC, 512, 4, 2, 3>(p, tiles, sp, s);
+    return;
+  }
   // 128 x 128 8-wave tiles when C fills them, else 64 x 64; split-K to ~512 workgroups
   if (C >= 128) {
     const int tiles = ((p.M + 127) / 128) * ((C + 127) / 128);

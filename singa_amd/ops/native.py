@@ -42,6 +42,11 @@ def _load():
         if "=" in kv and hasattr(_lib, "set_tuning"):
             k, v = kv.split("=")
             _lib.set_tuning(int(k), int(v))
+    # residual-tail GEMM knobs (bnres.hip sg_bnres_tune): SG_BNRES_TUNE="0=0"
+    for kv in os.environ.get("SG_BNRES_TUNE", "").split(","):
+        if "=" in kv and hasattr(_lib, "bnres_tune"):
+            k, v = kv.split("=")
+            _lib.bnres_tune(int(k), int(v))
     # fp32 generic-GEMM knobs (ggemm.hip sg_ggemm_tune): SG_GG_TUNE="2=1"
     for kv in os.environ.get("SG_GG_TUNE", "").split(","):
         if "=" in kv and hasattr(_lib, "ggemm_tune"):

@@ -47,6 +47,29 @@ def test_bnres_gemm_blocks(gpu):
     assert rel_err(dx, ref) < 1e-2
 
 
+@pytest.mark.parametrize("P,K4,C", [(6000, 512, 128), (3000, 1024, 256), (2500, 0, 128), (1800, 256, 384)])
+@pytest.mark.parametrize("wide", [1, 0])
+def test_bnres_wgrad_tiles(gpu, P, K4, C, wide):
+    """[g | y]^T y on the 256 x 128 three-stage tiles (wide = 1: K4 % 256 == 0,
+    C >= 128; K4 = 0 is the forward's Gram-only call) and on the 128 x 128
+    ones, exact to fp32 accumulation against the fp32 product."""
+    from singa_amd.ops import native as N
+
+    L = N.lib()
+    g0 = torch.Generator(device=gpu).manual_seed(7)
+    g = torch.randn(P, max(K4, 1), device=gpu, generator=g0).bfloat16()[:, :K4].contiguous()
+    y = torch.randn(P, C, device=gpu, generator=g0).bfloat16()
+    out = torch.zeros((K4 + C) * C, device=gpu)
+    L.bnres_tune(0, wide)
+    try:
+        L.bnres_wgrad(g.data_ptr() if K4 else y.data_ptr(), y.data_ptr(), out.data_ptr(), P, K4, C, N.stream())
+        torch.cuda.synchronize()
+    finally:
+        L.bnres_tune(0, 1)
+    ref = torch.cat([g.float(), y.float()], 1).t() @ y.float()
+    assert rel_err(out.view(K4 + C, C), ref) < 1e-5
+
+
 def test_bnres_tail_matches_fp32(gpu):
     from singa_amd import autograd as AG
     from singa_amd import device
