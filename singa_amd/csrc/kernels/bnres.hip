@@ -277,7 +277,8 @@ void go(const GemmArgs& p, int tiles, int zdim, hipStream_t s) {
   hipLaunchKernelGGL(kern, dim3(tiles, 1, zdim), dim3(NTH), lds, s, p);
 }
 
-int g_wide = 1;  // sg_bnres_tune(0, v): the 256 x 128 weight-gradient tiles (A/B)
+int g_wide = 1;   // sg_bnres_tune(0, v): the 256 x 128 weight-gradient tiles (A/B)
+int g_dwide = 0;  // sg_bnres_tune(1, v): the 256 x 128 data-gradient tiles (A/B)
 
 unsigned extent(int64_t elems) {
   if (elems * 2 >= (int64_t)1 << 31) throw std::runtime_error("bnres: operand exceeds 2 GiB (32-bit buffer offsets)");
@@ -294,6 +295,7 @@ extern "C" {
 
 void sg_bnres_tune(int key, int v) {
   if (key == 0) g_wide = v;
+  if (key == 1) g_dwide = v;
 }
 
 // out [K4 + C][C] fp32 (zeroed by the caller) += [g | y]^T y over P pixels:
@@ -382,7 +384,9 @@ void sg_bnres_dgrad(const void* g, const void* y, const void* bd, const void* bi
   // tiles as igemm's launcher picks them for these shapes: 8-wave 128 x 128
   // (two workgroups per CU) once there are enough tiles, else 4-wave 128 x 64
   const long t128 = (long)((P + 127) / 128) * ((C + 127) / 128);
-  if (C >= 128 && t128 >= 512) {
+  if (C >= 128 && t128 >= 512 && g_dwide) {  // (A/B: sg_bnres_tune(1, 1))
+    go<256, 128, LM_KMAJOR2, LM_KMAJOR, OUT_BF16, 512, 4, 2, 3>(p, (int)(((P + 255) / 256) * ((C + 127) / 128)), 1, s);
+  } else if (C >= 128 && t128 >= 512) {
     go<128, 128, LM_KMAJOR2, LM_KMAJOR, OUT_BF16, 512, 2, 4, 2>(p, (int)t128, 1, s);
   } else {
     const int tiles = ((P + 127) / 128) * ((C + 63) / 64);

@@ -183,7 +183,9 @@ static int make_phases(ConvGeom& g) {
 //         0 = auto (under-filled launches of 8-64 K-tiles), 3 = always, -1 = never
 // key 15: 1 = the 8-wave weight gradient on 256 x 128 tiles (64 x 64 wave tiles, three-stage ring) when K >= 256
 //         (ResNet-50 b1024 step +0.33 %, three alternating pairs on one box: profiles/r5/ab_wgrad_256x128.jsonl)
-static int g_tune[16] = {5, 1, 1, 0, 0, 1, 8, 1, 0, 1, 0, 0, 0, 1, 0, 1};
+// key 16: 256 x 128 three-stage tiles in place of the 8-wave 128 x 128 ones (1 conv fwd, 2 + dgrad, 3 all)
+extern "C" int sg_bn_deterministic();  // batchnorm.hip: deterministic-reduction mode
+static int g_tune[20] = {5, 1, 1, 0, 0, 1, 8, 1, 0, 1, 0, 0, 0, 1, 0, 1, 0, 0, 0, 0};
 // one-shot: the next dgrad's wt scratch is already transposed.  Per OS
 // thread: the runtime's executor threads (hogwild / aggregated replicas)
 // each set and consume their own flag, so one thread's set can never be
@@ -384,6 +386,11 @@ static void launch(const GemmArgs& p, int M, int splits, hipStream_t s, int batc
         }
         big = 1;
       }
+      // knob 16 (A/B): the 256 x 128 three-stage tiles (64 x 64 wave tiles) for
+      // 1: 3x3 / 7x7 conv forwards, 2: also data gradients, 3: every 8-wave GEMM
+      if (big == 1 && g_tune[16] > 0 && !sg_bn_deterministic() && M >= 256 &&
+          (g_tune[16] >= 3 || AM == LM_CONV_FWD || (g_tune[16] == 2 && AM == LM_DGRAD_A)))
+        big = 3;
       if (big == 1) {
         const int tiles = ((M + 127) / 128) * ((p.N + 127) / 128);
         launch_t<128, 128, AM, BMODE, OUT, 512, 2, 4, 2, FLAGS>(p, tiles, batch, z, s);
@@ -966,7 +973,7 @@ void sg_wt_transpose_batched(const void* desc, int n, int total, hipStream_t s) 
     hipLaunchKernelGGL(wt_transpose_batched_k, dim3(total), dim3(256), 0, s, (const WtDesc*)desc, n);
 }
 void sg_set_tuning(int key, int value) {
-  if (key >= 0 && key < 16) g_tune[key] = value;
+  if (key >= 0 && key < 20) g_tune[key] = value;
 }
 
 }  // extern "C"
