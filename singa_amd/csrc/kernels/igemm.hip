@@ -184,6 +184,7 @@ static int make_phases(ConvGeom& g) {
 // key 15: 1 = the 8-wave weight gradient on 256 x 128 tiles (64 x 64 wave tiles, three-stage ring) when K >= 256
 //         (ResNet-50 b1024 step +0.33 %, three alternating pairs on one box: profiles/r5/ab_wgrad_256x128.jsonl)
 // key 16: 256 x 128 three-stage tiles in place of the 8-wave 128 x 128 ones (1 conv fwd, 2 + dgrad, 3 all)
+// key 17: 1 = 128 x 256 three-stage weight-gradient tiles for K_out < 256 (with key 15)
 extern "C" int sg_bn_deterministic();  // batchnorm.hip: deterministic-reduction mode
 static int g_tune[20] = {5, 1, 1, 0, 0, 1, 8, 1, 0, 1, 0, 0, 0, 1, 0, 1, 0, 0, 0, 0};
 // one-shot: the next dgrad's wt scratch is already transposed.  Per OS
@@ -926,6 +927,17 @@ void sg_conv_wgrad(const void* x, const void* dy, void* dw_out, int N, int H, in
       if (g_tune[12] > 0) sp2 = g_tune[12];
       p.k_per_split = kps(p.K, sp2);
       launch_t<256, 128, LM_KOUTER, LM_WGRAD_B, OUT_F32_ATOMIC, 512, 4, 2, 3>(p, t2, 1, sp2, s);
+      return;
+    }
+    if (g_tune[15] == 1 && g_tune[17] == 1 && p.M < 256 && p.N >= 256) {
+      // K_out = 128 (stage 2): 128 x 256 tiles, waves 2 x 4 of 64 x 64 (A/B: knob 17)
+      const int t2 = ((p.M + 127) / 128) * ((p.N + 255) / 256);
+      int sp2 = 1;
+      while (t2 * sp2 < target && sp2 * 2 * 4 <= nkt) sp2 *= 2;
+      if (g_tune[13] && g_tune[10] <= 0) sp2 = wgrad_splits_q(t2, nkt, sp2, 1);
+      if (g_tune[12] > 0) sp2 = g_tune[12];
+      p.k_per_split = kps(p.K, sp2);
+      launch_t<128, 256, LM_KOUTER, LM_WGRAD_B, OUT_F32_ATOMIC, 512, 2, 4, 3>(p, t2, 1, sp2, s);
       return;
     }
     p.k_per_split = kps(p.K, sp);

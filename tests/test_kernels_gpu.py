@@ -145,6 +145,7 @@ def test_conv_fwd_bwd(gpu, case, wmode, kmajor, monkeypatch):
 
 
 @pytest.mark.parametrize("case", [(2, 64, 28, 28, 256, 3, 3, 1, 1), (2, 128, 14, 14, 512, 3, 3, 1, 1),
+                                  (2, 128, 28, 28, 128, 3, 3, 1, 1), (2, 512, 14, 14, 128, 1, 1, 1, 0),
                                   (2, 256, 28, 28, 256, 1, 1, 1, 0), (3, 128, 15, 15, 384, 3, 3, 2, 1)])
 def test_conv_wgrad_256x128_ring(gpu, case):
     """The 8-wave weight gradient on 256 x 128 tiles (tuning knob 15: 64 x 64
@@ -162,14 +163,16 @@ def test_conv_wgrad_256x128_ring(gpu, case):
     yr.backward(dy)
     xg = x.to(gpu).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     dyg = dy.to(gpu).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-    for knob in (1, 0):  # the 256 x 128 variant (default) and the 128 x 128 one
+    for knob, k17 in ((1, 0), (0, 0), (1, 1)):  # 256 x 128 (default), 128 x 128, 128 x 256 for K_out < 256
         NN.lib().set_tuning(15, knob)
+        NN.lib().set_tuning(17, k17)
         try:
             dw_acc = torch.zeros(K, C, R, S, device=gpu)
             F.conv2d_bwd(xg, w.to(gpu), dyg, (st, st), (pd, pd), need_dx=False, dw_out=dw_acc)
             torch.cuda.synchronize()
         finally:
             NN.lib().set_tuning(15, 1)
+            NN.lib().set_tuning(17, 0)
         assert rel_err(dw_acc, wr.grad) < 1e-5
 
 
