@@ -858,7 +858,8 @@ static void pick_f32(int M, int N, int K, int batch, bool can_split, bool zero_f
   for (int t : cand) {
     int bm, bn;
     tile_dims(t, bm, bn);
-    if (dma && ((bm < 64 && (dma & 2)) || (bn < 64 && (dma & 4)))) continue;
+    // (small outputs keep the 32-row tiles: more workgroups beat the DMA ring there)
+    if (dma && (long)M * N * batch > (1L << 18) && ((bm < 64 && (dma & 2)) || (bn < 64 && (dma & 4)))) continue;
     const long tiles = (long)((M + bm - 1) / bm) * ((N + bn - 1) / bn) * batch;
     for (int sp : sps) {
       if (sp > 1 && (!can_split || nkt < 2 * sp)) continue;

@@ -171,7 +171,10 @@ static int make_phases(ConvGeom& g) {
 // split-count scale (2^v), 4 = forced tile shape (5/6/7: the 8-wave variants
 // of pick_big at any size), 5 = 8-wave tiles for non-split launches (pick_big),
 // 6 = single-stage short-K variant for GEMMs of at most this many K-tiles
-// (8: measured +0.3..0.6 % over 4 and 2 on the ResNet-50 step, profiles/r3/ab_short_k_threshold.jsonl)
+// (round 3: 8 measured +0.3..0.6 % over 4 and 2, profiles/r3/ab_short_k_threshold.jsonl; round 5, after the
+// persistent and algebraic paths took the K <= 128 tails: 2 is +0.38 % over 8 and 0 +0.2 %, the stage-3/4
+// K = 256 / 512 forwards and gsum data gradients run faster on the 8-wave two-workgroup tile,
+// profiles/r5/ab_short_k_cap_r6w.jsonl)
 // (0 = off), 7 = early DMA issue in the 2-stage loop (measured -3.5 % conv time)
 // 8 = non-temporal output stores in the LDS-staged bf16 epilogue, 9 = persistent
 // short-K kernel for the 1x1-conv GEMM shapes (sk_gemm_k)
@@ -186,7 +189,7 @@ static int make_phases(ConvGeom& g) {
 // key 16: 256 x 128 three-stage tiles in place of the 8-wave 128 x 128 ones (1 conv fwd, 2 + dgrad, 3 all)
 // key 17: 1 = 128 x 256 three-stage weight-gradient tiles for K_out < 256 (with key 15)
 extern "C" int sg_bn_deterministic();  // batchnorm.hip: deterministic-reduction mode
-static int g_tune[20] = {5, 1, 1, 0, 0, 1, 8, 1, 0, 1, 0, 0, 0, 1, 0, 1, 0, 0, 0, 0};
+static int g_tune[20] = {5, 1, 1, 0, 0, 1, 2, 1, 0, 1, 0, 0, 0, 1, 0, 1, 0, 0, 0, 0};
 // one-shot: the next dgrad's wt scratch is already transposed.  Per OS
 // thread: the runtime's executor threads (hogwild / aggregated replicas)
 // each set and consume their own flag, so one thread's set can never be
