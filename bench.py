@@ -74,12 +74,12 @@ def main() -> int:
                     help="per-GPU batch (1024 fits easily in 288 GB HBM3E; larger batches fill the 256 CUs better)")
     ap.add_argument("--depth", type=int, default=50)
     ap.add_argument("--image", type=int, default=224)
-    ap.add_argument("--graph", dest="graph", action="store_true", default=False,
-                    help="HIP-graph replay of the whole step (at batch 1024 measured 0.9%% slower than eager "
-                         "launch: profiles/r3/ab_graph_vs_eager.txt)")
-    ap.add_argument("--no-graph", dest="graph", action="store_false",
-                    help="eager execution (default, every N: each gradient bucket's all-reduce is forked onto "
-                         "the comm stream as soon as backward has produced it)")
+    ap.add_argument("--graph", dest="graph", action="store_true", default=True,
+                    help="HIP-graph replay of the whole step (default, every N: +1.1%% over eager launch on the "
+                         "round-5 step, profiles/r5/ab_graph_vs_eager_r6z.jsonl; round 3 measured it 0.9%% slower)")
+    ap.add_argument("--no-graph", "--eager", dest="graph", action="store_false",
+                    help="eager execution (each gradient bucket's all-reduce forked onto the comm stream as soon "
+                         "as backward has produced it, as in the captured step)")
     ap.add_argument("--loss-curve", action="store_true", help="record every step's loss (syncs; diagnostics only)")
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--sync-warmup", action="store_true", help="synchronize after every warmup step (diagnostics)")
@@ -144,18 +144,32 @@ def main() -> int:
     tx = tensor.from_numpy(x, dev)
     ty = tensor.from_numpy(y, dev)
 
-    # Eager by default for every N (at batch 1024 the ~1000 launches of a
-    # step hide behind the kernels: eager measured 0.9 % faster than graph
-    # replay, profiles/r3/ab_graph_vs_eager.txt), so N = 1 and N > 1 time the
-    # same path; with N > 1 each gradient bucket's RCCL all-reduce is forked
-    # onto the comm stream as soon as backward has produced it.  --graph
-    # captures the whole step including the forked all-reduces (the native
-    # communicator is capture-safe).
+    # HIP-graph replay of the whole step by default, every N (the round-5 step
+    # has ~1 000 launches, many of them few-microsecond BN finalize / tail
+    # helpers: replay measured +1.1 % over eager, profiles/r5/ab_graph_vs_eager_r6z.jsonl),
+    # so N = 1 and N > 1 time the same path.  With N > 1 each gradient
+    # bucket's RCCL all-reduce is forked onto the comm stream inside the
+    # captured backward as soon as its gradients are final (the native
+    # communicator is capture-safe: RCCL collectives are stream-ordered).  If
+    # the capture raises (a communicator that cannot be captured), the run
+    # falls back to eager execution and says so in the record.
     use_graph = args.graph
     m.compile([tx], is_train=True, use_graph=use_graph)
     m.train()
 
-    for _ in range(args.warmup):
+    for i in range(args.warmup):
+        if use_graph and i == 0:
+            try:
+                out, loss = m(tx, ty)
+                torch.cuda.synchronize()
+            except Exception as e:  # capture failed: eager from here on
+                print(f"bench.py: HIP-graph capture failed ({type(e).__name__}: {e}); running eager",
+                      file=sys.stderr)
+                m.reset_graph()
+                m.graph(False, False)
+                use_graph = False
+                out, loss = m(tx, ty)
+            continue
         out, loss = m(tx, ty)
         if args.sync_warmup:
             torch.cuda.synchronize()
