@@ -917,7 +917,7 @@ void sg_conv_wgrad(const void* x, const void* dy, void* dw_out, int N, int H, in
     while (tiles * sp < target && sp * 2 * 4 <= nkt) sp *= 2;
     if (g_tune[13] && g_tune[10] <= 0) sp = wgrad_splits_q(tiles, nkt, sp);
     if (g_tune[12] > 0) sp = g_tune[12];
-    if (g_tune[15] == 1 && p.M >= 256) {
+    if (g_tune[15] == 1 && p.M >= 256 && (p.M & 255) == 0) {  // (M = 384: a half-empty second row of tiles, AlexNet -2 %)
       // 256 x 128 tiles of 64 x 64 wave tiles (half the LDS fragment traffic
       // per MFMA of the 64 x 32 wave tiles), three-stage ring, one per CU
       const int t2 = ((p.M + 255) / 256) * ((p.N + 127) / 128);
