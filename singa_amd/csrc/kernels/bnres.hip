@@ -78,7 +78,7 @@ __global__ void __launch_bounds__(256) coef_k(const float* __restrict__ G, const
 // 64 x 64 tile (k, c) of dW = s G - u T + v cs (T = W Gram) added into the
 // weight gradient, its <W, dW> column sums (the producer BN's identity-sum
 // input) and W^T v column sums (the data gradient's bias), and the
-// transposed Bd[c][k] = s_k W[k][c].  Blocks by >= K4 / 64: Bd[c][K4 + j] =
+// transposed Bd[c][k] = s_k W[k][c].  Blocks by >= K4 / 16: Bd[c][K4 + j] =
 // -M[c][j].  Block (cb, 0) also evaluates the producer BN's identity-sum gate
 // on gamma2 / beta2 (as wdot_colsum_k: the int flag at wdot + C).
 __global__ void __launch_bounds__(256) combine_k(const float* __restrict__ G, const float* __restrict__ T,
@@ -88,13 +88,17 @@ __global__ void __launch_bounds__(256) combine_k(const float* __restrict__ G, co
                                                  float* __restrict__ bias, float* __restrict__ wdot,
                                                  const float* __restrict__ gamma2, const float* __restrict__ beta2,
                                                  float tau, int cs_rows) {
-  __shared__ bf16 tile[64][66];
+  // main part: 16 k-rows per block (a stage-1 tail has K4 = 256, C = 64: 64-row
+  // blocks gave 5 workgroups, each thread walking 16 dependent rows -- ~18 us of
+  // latency per call; 16-row blocks quadruple the grid)
+  constexpr int KB = 16;
+  __shared__ bf16 tile[KB][66];
   __shared__ float red[2][4][64];
   const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
   const int cb = blockIdx.x, kb = blockIdx.y;
   const int c = cb * 64 + cl;
   const int ldb = K4 + C;
-  const int nkb = K4 / 64;
+  const int nkb = K4 / KB;
   if (kb >= nkb) {  // the -M part of Bd
     const int j = (kb - nkb) * 64 + cl;
 #pragma unroll 4
@@ -111,10 +115,10 @@ __global__ void __launch_bounds__(256) combine_k(const float* __restrict__ G, co
   float csv = 0.f;  // column sums of y: cs_rows slot rows [cs_rows][C]
   for (int r = 0; r < cs_rows; ++r) csv += cs[(int64_t)r * C + c];
   float wd = 0.f, bs = 0.f;
-#pragma unroll 4
-  for (int i = 0; i < 16; ++i) {
+#pragma unroll
+  for (int i = 0; i < KB / 4; ++i) {
     const int kl = rg + 4 * i;
-    const int k = kb * 64 + kl;
+    const int k = kb * KB + kl;
     const int64_t o = (int64_t)k * C + c;
     const float s = coef[k], u = coef[K4 + k], v = coef[2 * K4 + k];
     const float wv = (float)w[o];
@@ -131,11 +135,12 @@ __global__ void __launch_bounds__(256) combine_k(const float* __restrict__ G, co
     atomicAdd(wdot + c, red[0][0][cl] + red[0][1][cl] + red[0][2][cl] + red[0][3][cl]);
     atomicAdd(bias + c, red[1][0][cl] + red[1][1][cl] + red[1][2][cl] + red[1][3][cl]);
   }
-  // Bd[c][k] = tile[k][c]: rows c of this block, 64 consecutive k per row
-#pragma unroll 4
-  for (int i = 0; i < 16; ++i) {
-    const int ccl = rg + 4 * i;
-    bd[(int64_t)(cb * 64 + ccl) * ldb + kb * 64 + cl] = tile[cl][ccl];
+  // Bd[c][k] = tile[k][c]: rows c of this block, KB consecutive k per row
+  const int kk = threadIdx.x & (KB - 1), cq = threadIdx.x / KB;  // 16 rows c per pass
+#pragma unroll
+  for (int i = 0; i < 64 * KB / 256; ++i) {
+    const int ccl = cq + (256 / KB) * i;
+    bd[(int64_t)(cb * 64 + ccl) * ldb + kb * KB + kk] = tile[kk][ccl];
   }
 }
 
@@ -409,7 +414,7 @@ void sg_bnres_combine(const void* G, const void* T, const void* M, const void* c
                       const void* w, int K4, int C, void* dw, void* bd, void* bias, void* wdot, const void* gamma2,
                       const void* beta2, float tau, hipStream_t s) {
   if ((K4 & 63) != 0 || (C & 63) != 0) throw std::runtime_error("bnres_combine: K4 % 64 and C % 64 required");
-  hipLaunchKernelGGL(combine_k, dim3(C / 64, K4 / 64 + C / 64), dim3(256), 0, s, (const float*)G, (const float*)T,
+  hipLaunchKernelGGL(combine_k, dim3(C / 64, K4 / 16 + C / 64), dim3(256), 0, s, (const float*)G, (const float*)T,
                      (const float*)M, (const float*)cs, (const float*)coef, (const bf16*)w, K4, C, (float*)dw,
                      (bf16*)bd, (float*)bias, (float*)wdot, (const float*)gamma2, (const float*)beta2, tau, cs_rows);
 }
