@@ -156,6 +156,10 @@ void sg_workq_set(int);
 int sg_workq_enabled();
 int sg_cu_count();
 void sg_cu_hog(int, double, int, int*, hipStream_t);
+void* sg_workq_arena_begin();
+void sg_workq_arena_end();
+void sg_workq_arena_free(void*);
+int sg_workq_arena_slots(void*);
 int sg_gemm_act(const void*, int64_t, int, const void*, int64_t, int, void*, int64_t, int, int, int, float, const void*,
                 int, int64_t, int64_t, int64_t, int, void*, int, const void*, hipStream_t);
 void sg_gconv_fwd(int, const void*, const void*, void*, const void*, int, int, int, int, int, int, int, int, int, int,
@@ -575,6 +579,11 @@ PYBIND11_MODULE(_C, m) {
   // persistent kernels' dynamic work queues (csrc/kernels/workq.hip): A/B switch
   m.def("workq_set", [](int on) { sg_workq_set(on); });
   m.def("workq_enabled", []() { return sg_workq_enabled(); });
+  // per-capture slot arenas (a captured graph never shares a slot with other work)
+  m.def("workq_arena_begin", []() { return (P)sg_workq_arena_begin(); });
+  m.def("workq_arena_end", []() { sg_workq_arena_end(); });
+  m.def("workq_arena_free", [](P h) { sg_workq_arena_free(V(h)); });
+  m.def("workq_arena_slots", [](P h) { return sg_workq_arena_slots(V(h)); });
   m.def("cu_count", []() { return sg_cu_count(); });
   // interference rehearsal: occupy ncu CUs for `us` microseconds on stream s
   m.def("cu_hog", [](int ncu, double us, int lds_bytes, P started, P s) {

@@ -27,6 +27,18 @@
 // caller's stream followed by a stream synchronize; host mode (device < 0)
 // reads and writes host pointers directly.  Reductions run on the host in
 // rank order (deterministic), fp32 accumulation for 16/32-bit floats.
+//
+// Captured mode: when the caller's stream is being captured -- every rank
+// thread capturing its training step into ONE HIP graph (parallel/loop.py
+// WorldGraph) -- nothing can run or be waited for, so an all-reduce becomes
+// graph structure instead: each rank records an event on its stream, group
+// rank 0's stream waits on all of them and runs one device reduction over
+// every rank's buffers (kernels/loopred.hip), and every other rank's stream
+// waits on its completion event.  This is the multi-rank rehearsal of
+// DistOpt's captured step, where each bucket's all-reduce is forked onto the
+// comm stream inside the graph, as on RCCL.  Every HIP call of this path is
+// made with the Python GIL held, which serialises it with the other rank
+// threads' kernel launches into the shared capture.
 #include <hip/hip_runtime.h>
 #include <pybind11/pybind11.h>
 #include <stdint.h>
@@ -45,6 +57,9 @@
 #include <vector>
 
 namespace py = pybind11;
+
+extern "C" int sg_loop_allreduce(const void* const* sends, void* const* recvs, int n, int64_t count, int dt, int op,
+                                 hipStream_t s);
 
 namespace {
 
@@ -90,6 +105,10 @@ struct World {
   };
   std::map<std::pair<int, int>, std::deque<std::shared_ptr<Msg>>> boxes;
   std::map<std::tuple<const void*, long, int>, std::shared_ptr<Group>> splits;  // (parent, split seq, color)
+  std::vector<hipEvent_t> events;  // captured-mode fork / join events (graph edges), freed with the world
+  ~World() {
+    for (hipEvent_t e : events) (void)hipEventDestroy(e);
+  }
 
   template <class Pred>
   void wait(std::unique_lock<std::mutex>& lk, Pred pred, const char* what) {
@@ -109,6 +128,7 @@ struct Slot {
   size_t count = 0;
   int dt = 0, op = 0, root = 0, kind = 0;
   long color = 0, key = 0;
+  hipEvent_t ev = nullptr;  // captured mode: this rank's inputs are ready
 };
 
 // the ranks of one communicator (the world or a split of it)
@@ -116,6 +136,7 @@ struct Group {
   Group(std::vector<int> g) : members(std::move(g)), slots(members.size()) {}
   std::vector<int> members;  // global ranks, group order
   std::vector<Slot> slots;
+  hipEvent_t done = nullptr;  // captured mode: the current collective's completion
   int arrived = 0;
   long gen = 0;
   long splits = 0;
@@ -284,7 +305,74 @@ class LoopComm {
     if (have) write(me.recv, out.data(), out.size(), s);
   }
 
+  bool capturing(P s) const {
+    if (dev_ < 0) return false;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing((hipStream_t)s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
+  }
+  hipEvent_t new_event() {
+    hipEvent_t e = nullptr;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
+      throw std::runtime_error("LoopComm: hipEventCreateWithFlags failed");
+    std::lock_guard<std::mutex> lk(w_->mu);
+    w_->events.push_back(e);
+    return e;
+  }
+  void hchk(hipError_t e, const char* what) {
+    if (e != hipSuccess) throw std::runtime_error(std::string("LoopComm (captured) ") + what + ": " + hipGetErrorString(e));
+  }
+  // group barrier with the GIL released (the peers need it to reach theirs)
+  std::vector<Slot> gbarrier(const Slot* mine, const char* what, hipEvent_t* done_out = nullptr) {
+    py::gil_scoped_release nogil;
+    std::unique_lock<std::mutex> lk(w_->mu);
+    if (mine) g_->slots[rank_] = *mine;
+    g_->barrier(*w_, lk, what);
+    if (done_out) *done_out = g_->done;
+    return g_->slots;
+  }
+  // the captured all-reduce (see the header): called with the GIL held
+  void captured_all_reduce(P send, P recv, size_t count, int dt, int op, P s) {
+    if (nranks() > 16) throw std::runtime_error("LoopComm (captured): at most 16 ranks");
+    Slot me{send, recv, count, dt, op};
+    me.ev = new_event();
+    hchk(hipEventRecord(me.ev, (hipStream_t)s), "hipEventRecord");
+    std::vector<Slot> ps = gbarrier(&me, "all_reduce (captured)");
+    for (const Slot& p : ps)
+      if (p.count != count || p.dt != dt || p.op != op)
+        throw std::runtime_error("LoopComm all_reduce (captured): ranks disagree on count / dtype / op");
+    if (rank_ == 0) {
+      std::vector<const void*> sends(ps.size());
+      std::vector<void*> recvs(ps.size());
+      for (size_t j = 0; j < ps.size(); ++j) {
+        if (j) hchk(hipStreamWaitEvent((hipStream_t)s, ps[j].ev, 0), "hipStreamWaitEvent");
+        sends[j] = (const void*)ps[j].send;
+        recvs[j] = (void*)ps[j].recv;
+      }
+      if (sg_loop_allreduce(sends.data(), recvs.data(), (int)ps.size(), (int64_t)count, dt, op, (hipStream_t)s) != 0)
+        throw std::runtime_error("LoopComm all_reduce (captured): unsupported dtype / op or launch failure");
+      hipEvent_t d = new_event();
+      hchk(hipEventRecord(d, (hipStream_t)s), "hipEventRecord");
+      std::lock_guard<std::mutex> lk(w_->mu);
+      g_->done = d;
+    }
+    hipEvent_t d = nullptr;
+    gbarrier(nullptr, "all_reduce (captured)", &d);
+    if (rank_ != 0) hchk(hipStreamWaitEvent((hipStream_t)s, d, 0), "hipStreamWaitEvent");
+    gbarrier(nullptr, "all_reduce (captured)");  // every rank joined: g_->done may be replaced
+  }
+  void no_capture(P s, const char* what) {
+    if (capturing(s))
+      throw std::runtime_error(std::string("LoopComm ") + what + ": not supported inside a captured graph "
+                                                                 "(only all_reduce is)");
+  }
+
   void all_reduce(P send, P recv, size_t count, int dt, int op, P s) {
+    if (capturing(s)) {
+      if (op == 1 || (dt != 0 && dt != 1 && dt != 6))
+        throw std::runtime_error("LoopComm all_reduce (captured): sum / avg / max / min of f32, bf16, f64 only");
+      captured_all_reduce(send, recv, count, dt, op, s);
+      return;
+    }
     const size_t b = count * dt_size(dt);
     collective(Slot{send, recv, count, dt, op}, s, "all_reduce", [&](std::vector<Slot>& ps, std::vector<char>& out) {
       std::vector<char> x(b);
@@ -297,6 +385,7 @@ class LoopComm {
     });
   }
   void reduce_scatter(P send, P recv, size_t recvcount, int dt, int op, P s) {
+    no_capture(s, "reduce_scatter");
     const size_t e = dt_size(dt), b = recvcount * e;
     collective(Slot{send, recv, recvcount, dt, op}, s, "reduce_scatter",
                [&](std::vector<Slot>& ps, std::vector<char>& out) {
@@ -310,6 +399,7 @@ class LoopComm {
                });
   }
   void all_gather(P send, P recv, size_t sendcount, int dt, P s) {
+    no_capture(s, "all_gather");
     const size_t b = sendcount * dt_size(dt);
     collective(Slot{send, recv, sendcount, dt}, s, "all_gather", [&](std::vector<Slot>& ps, std::vector<char>& out) {
       out.resize(b * ps.size());
@@ -318,6 +408,7 @@ class LoopComm {
     });
   }
   void broadcast(P send, P recv, size_t count, int dt, int root, P s) {
+    no_capture(s, "broadcast");
     const size_t b = count * dt_size(dt);
     collective(Slot{send, recv, count, dt, 0, root}, s, "broadcast",
                [&](std::vector<Slot>& ps, std::vector<char>& out) {
@@ -329,6 +420,7 @@ class LoopComm {
                });
   }
   void reduce(P send, P recv, size_t count, int dt, int op, int root, P s) {
+    no_capture(s, "reduce");
     const size_t b = count * dt_size(dt);
     collective(Slot{send, recv, count, dt, op, root}, s, "reduce", [&](std::vector<Slot>& ps, std::vector<char>& out) {
       if (rank_ != root) return false;
@@ -342,6 +434,7 @@ class LoopComm {
     });
   }
   void all_to_all(P send, P recv, size_t count, int dt, P s) {
+    no_capture(s, "all_to_all");
     const size_t b = count * dt_size(dt);
     collective(Slot{send, recv, count, dt}, s, "all_to_all", [&](std::vector<Slot>& ps, std::vector<char>& out) {
       out.resize(b * ps.size());
@@ -352,6 +445,7 @@ class LoopComm {
 
   // ------------------------------------------------------------- p2p
   void send(P buf, size_t count, int dt, int peer, P s) {
+    no_capture(s, "send");
     if (t_group_depth > 0) {
       t_pending.push_back(PendingP2P{true, this, buf, count, dt, peer, s});
       return;
@@ -361,6 +455,7 @@ class LoopComm {
     await_consumed(m);
   }
   void recv(P buf, size_t count, int dt, int peer, P s) {
+    no_capture(s, "recv");
     if (t_group_depth > 0) {
       t_pending.push_back(PendingP2P{false, this, buf, count, dt, peer, s});
       return;

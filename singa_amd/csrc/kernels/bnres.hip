@@ -74,8 +74,8 @@ __global__ void __launch_bounds__(256) coef_k(const float* __restrict__ G, const
   for (int c = lane; c < C; c += 64) wu[(int64_t)k * C + c] = u * (float)wr[c];
 }
 
-// grid (C / 64, K4 / 64 + C / 64), 256 threads.  Blocks by < K4 / 64: the
-// 64 x 64 tile (k, c) of dW = s G - u T + v cs (T = W Gram) added into the
+// grid (C / 64, K4 / 16 + C / 64), 256 threads.  Blocks by < K4 / 16: the
+// 16 x 64 tile (k, c) of dW = s G - u T + v cs (T = W Gram) added into the
 // weight gradient, its <W, dW> column sums (the producer BN's identity-sum
 // input) and W^T v column sums (the data gradient's bias), and the
 // transposed Bd[c][k] = s_k W[k][c].  Blocks by >= K4 / 16: Bd[c][K4 + j] =

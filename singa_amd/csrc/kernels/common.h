@@ -244,8 +244,11 @@ static inline void sg_zero_async(void* p, size_t bytes, hipStream_t s) {
 // e.g. per column slice and XCD), each on its own 64-byte line, and a
 // done-counter; the last workgroup to finish resets the slot, so the next
 // launch (or the next replay of a captured graph) starts from zero with no
-// host work.  Slots come from a per-device ring (sg_workq_slot), so kernels
-// running concurrently on different streams never share one.
+// host work.  Eager launches take slots from a per-device ring
+// (sg_workq_slot), so kernels running concurrently on different streams never
+// share one; a thread that is capturing a HIP graph takes fresh slots from the
+// capture's own arena (workq.hip), so a graph's frozen slots are never handed
+// to other work while the graph can still be replayed.
 // ------------------------------------------------------------------------------
 constexpr int QSTRIDE = 16;                  // ints between counters (64 B)
 constexpr int QMAX = 128;                    // counters per slot

@@ -8,10 +8,20 @@
 // kernel that used it, so a slot is reusable as soon as that kernel ends; the
 // ring only has to be larger than the number of persistent kernels that can
 // run at the same time.
+//
+// A captured HIP graph freezes the slot each of its persistent kernels was
+// given, while later launches keep advancing the ring -- so two graphs (or a
+// graph and eager launches) replayed at the same time could share a slot.
+// Captures therefore take their slots from a private ARENA instead: while a
+// thread captures (sg_workq_arena_begin .. sg_workq_arena_end) every slot it
+// is handed is a fresh one of that arena, never handed out again, and the
+// arena is freed with its graph (sg_workq_arena_free).  Several threads
+// capturing into one graph (the loopback world's ranks) each use their own.
 #include <stdlib.h>
 
 #include <atomic>
 #include <mutex>
+#include <vector>
 
 #include "common.h"
 
@@ -24,20 +34,15 @@ std::mutex g_mu;
 int g_cus[kMaxDev] = {};
 int g_on = -1;
 
-int cur_dev() {
-  int d = 0;
-  (void)hipGetDevice(&d);
-  return d < 0 || d >= kMaxDev ? 0 : d;
-}
+constexpr int kArenaChunk = 64;  // slots per arena allocation
 
-int* ring_of(int d) {
-  if (g_ring[d]) return g_ring[d];
-  std::lock_guard<std::mutex> g(g_mu);
-  if (g_ring[d]) return g_ring[d];
+// a device allocation of `slots` zeroed queue slots, made outside any capture
+// (this thread's capture mode relaxed; zeroed through a private stream)
+int* alloc_zeroed_slots(int slots) {
   hipStreamCaptureMode m = hipStreamCaptureModeRelaxed;
   (void)hipThreadExchangeStreamCaptureMode(&m);
   int* p = nullptr;
-  const size_t bytes = sizeof(int) * QSLOT * kRing;
+  const size_t bytes = sizeof(int) * QSLOT * (size_t)slots;
   if (hipMalloc(&p, bytes) == hipSuccess) {
     hipStream_t s;
     if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess) {
@@ -50,8 +55,39 @@ int* ring_of(int d) {
     }
   }
   (void)hipThreadExchangeStreamCaptureMode(&m);
-  g_ring[d] = p;
   return p;
+}
+
+struct Arena {
+  std::vector<int*> chunks;
+  int used = kArenaChunk;  // slots taken from the last chunk
+  int* take() {
+    if (used == kArenaChunk) {
+      int* c = alloc_zeroed_slots(kArenaChunk);
+      if (!c) return nullptr;
+      chunks.push_back(c);
+      used = 0;
+    }
+    return chunks.back() + (size_t)(used++) * QSLOT;
+  }
+  ~Arena() {
+    for (int* c : chunks) (void)hipFree(c);
+  }
+};
+thread_local Arena* t_arena = nullptr;
+
+int cur_dev() {
+  int d = 0;
+  (void)hipGetDevice(&d);
+  return d < 0 || d >= kMaxDev ? 0 : d;
+}
+
+int* ring_of(int d) {
+  if (g_ring[d]) return g_ring[d];
+  std::lock_guard<std::mutex> g(g_mu);
+  if (g_ring[d]) return g_ring[d];
+  g_ring[d] = alloc_zeroed_slots(kRing);
+  return g_ring[d];
 }
 
 // spin until the device's constant 100 MHz clock passes `until`
@@ -80,11 +116,33 @@ int sg_workq_enabled() {
 
 int* sg_workq_slot() {
   if (!sg_workq_enabled()) return nullptr;
+  if (t_arena) return t_arena->take();  // a capture: a slot of its own
   const int d = cur_dev();
   int* r = ring_of(d);
   if (!r) return nullptr;
   const unsigned i = g_next[d].fetch_add(1, std::memory_order_relaxed) % kRing;
   return r + (size_t)i * QSLOT;
+}
+
+// Route this thread's slots to a new arena (call before a capture begins,
+// on the capture's device); returns its handle.
+void* sg_workq_arena_begin() {
+  Arena* a = new Arena();
+  t_arena = a;
+  return a;
+}
+// Stop routing (the capture ended or was abandoned); the arena lives on with
+// the graph that addresses it.
+void sg_workq_arena_end() { t_arena = nullptr; }
+// Free an arena once no graph that addresses it can run any more.
+void sg_workq_arena_free(void* h) {
+  Arena* a = (Arena*)h;
+  if (t_arena == a) t_arena = nullptr;
+  delete a;
+}
+int sg_workq_arena_slots(void* h) {
+  const Arena* a = (const Arena*)h;
+  return a->chunks.empty() ? 0 : (int)(a->chunks.size() - 1) * kArenaChunk + a->used;
 }
 
 int sg_cu_count() {

@@ -171,6 +171,30 @@ void register_stream_graph(py::module& m) {
     hchk(hipDeviceGetStreamPriorityRange(&lo, &hi), "hipDeviceGetStreamPriorityRange");
     return py::make_tuple(lo, hi);
   });
+  sm.def("device_synchronize", [](int device) {
+    int cur = 0;
+    hchk(hipGetDevice(&cur), "hipGetDevice");
+    if (device >= 0 && device != cur) hchk(hipSetDevice(device), "hipSetDevice");
+    hipError_t e;
+    {
+      py::gil_scoped_release nogil;
+      e = hipDeviceSynchronize();
+    }
+    if (device >= 0 && device != cur) (void)hipSetDevice(cur);
+    hchk(e, "hipDeviceSynchronize");
+  });
+  // host <-> device copies ordered on stream s; the call returns when the
+  // copy is complete (the host side may be pageable memory owned by the caller)
+  sm.def("memcpy_d2h", [](uintptr_t dst, uintptr_t src, size_t bytes, uintptr_t s) {
+    py::gil_scoped_release nogil;
+    hchk(hipMemcpyAsync((void*)dst, (const void*)src, bytes, hipMemcpyDeviceToHost, (hipStream_t)s), "hipMemcpyAsync D2H");
+    hchk(hipStreamSynchronize((hipStream_t)s), "hipStreamSynchronize");
+  });
+  sm.def("memcpy_h2d", [](uintptr_t dst, uintptr_t src, size_t bytes, uintptr_t s) {
+    py::gil_scoped_release nogil;
+    hchk(hipMemcpyAsync((void*)dst, (const void*)src, bytes, hipMemcpyHostToDevice, (hipStream_t)s), "hipMemcpyAsync H2D");
+    hchk(hipStreamSynchronize((hipStream_t)s), "hipStreamSynchronize");
+  });
   sm.def("is_capturing", [](uintptr_t s) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     hchk(hipStreamIsCapturing((hipStream_t)s, &cs), "hipStreamIsCapturing");

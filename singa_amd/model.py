@@ -47,6 +47,10 @@ class Model(layer.Layer):
         self._warm: Dict[str, int] = {}
         self._pool = None
         self.graph_warmup = 2
+        # a capture that raises: False -> re-raise; True -> log, switch this
+        # model to eager execution and run the step eagerly (bench.py)
+        self.graph_fallback = False
+        self.graph_error: Optional[str] = None
 
     # ---------------------------------------------------------------- config
     def set_optimizer(self, optimizer) -> None:
@@ -142,7 +146,7 @@ class Model(layer.Layer):
                     return fn(*args, **kwargs)
                 finally:
                     _F.ARENA.end()
-            torch.cuda.synchronize()
+            _stream.device_synchronize(args[0].data.device)
             if opt is not None:
                 getattr(opt, "opt", opt).graph_mode = True
                 opt.prepare_step()
@@ -164,12 +168,14 @@ class Model(layer.Layer):
                     _F.ARENA.end()
 
             try:
+                if os.environ.get("SINGA_AMD_GRAPH_FAIL_TEST") == "1":  # test hook: a capture that raises
+                    raise RuntimeError("SINGA_AMD_GRAPH_FAIL_TEST: capture refused")
                 if os.environ.get("SINGA_AMD_NATIVE_GRAPH", "1") != "0":
                     # framework-owned capture (hipStreamBeginCapture on a native
                     # stream); the step's memory is the graph's private native
                     # pool -- one per graph, so the eval graph's static outputs
                     # never share blocks with the train graph's temporaries
-                    g = _stream.StepGraph(args[0].data.device)
+                    g = _stream.new_step_graph(args[0].data.device)
                     out = g.capture(body)
                 else:
                     g = torch.cuda.CUDAGraph()
@@ -180,6 +186,11 @@ class Model(layer.Layer):
                     keep.append(gp)
                     with torch.cuda.graph(g, pool=pool), gp:
                         out = body()
+            except Exception as e:
+                _F.CAPTURE_KEEP = None
+                if not self.graph_fallback:
+                    raise
+                return self._eager_after_failed_capture(fn, args, kwargs, e)
             finally:
                 _F.CAPTURE_KEEP = None
             if opt is not None:
@@ -198,10 +209,32 @@ class Model(layer.Layer):
             opt.step_counter += 1
         return out
 
+    def _eager_after_failed_capture(self, fn, args, kwargs, err):
+        """The capture raised: this model runs eagerly from now on.  The
+        optimiser leaves graph mode (its eager ``step()`` writes lr / t again)
+        and gets the hyper-parameters of the step about to run."""
+        import sys
+
+        self.graph_error = f"{type(err).__name__}: {err}"[:300]
+        print(f"singa_amd.Model: HIP-graph capture failed ({self.graph_error}); running eagerly", file=sys.stderr)
+        self.reset_graph()
+        self.graph(False, self.sequential)
+        opt = self.optimizer
+        if opt is not None:
+            getattr(opt, "opt", opt).graph_mode = False
+            opt.prepare_step()
+        autograd.training = self.training
+        if self.training:
+            _F.ARENA.begin(args[0].data.device)
+        try:
+            return fn(*args, **kwargs)
+        finally:
+            _F.ARENA.end()
+
     def reset_graph(self) -> None:
         gs, self._graphs = self._graphs, {}
         for g, _, _, keep in gs.values():
-            if isinstance(g, _stream.StepGraph):
+            if hasattr(g, "release"):
                 g.release()  # the graph, then its private memory
         pools = [k for ent in gs.values() for k in ent[3] if isinstance(k, _mem.graph_pool)]
         del gs

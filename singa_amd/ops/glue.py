@@ -71,6 +71,45 @@ def _bstrides(t: torch.Tensor, shape) -> List[int]:
     return st
 
 
+# ------------------------------------------------------------- host transfer
+_NP_OF = {torch.float32: "float32", torch.float64: "float64", torch.float16: "float16", torch.int32: "int32",
+          torch.int64: "int64", torch.int16: "int16", torch.int8: "int8", torch.uint8: "uint8", torch.bool: "bool"}
+
+
+def to_numpy(t: torch.Tensor):
+    """A host numpy copy of ``t`` (bf16 widened to fp32).  Device tensors
+    are made dense by a native kernel and copied with one stream-ordered
+    hipMemcpy (csrc/mem/stream_graph.cpp), no PyTorch copy."""
+    import numpy as np
+
+    if t.dtype == torch.bfloat16:
+        t = to(t, torch.float32)
+    if not t.is_cuda:
+        return t.detach().contiguous().numpy().copy()
+    d = contiguous(t)
+    out = np.empty(tuple(d.shape), dtype=_NP_OF[d.dtype])
+    if out.nbytes:
+        _lib().rt.memcpy_d2h(out.ctypes.data, d.data_ptr(), out.nbytes, N.stream(d.device.index))
+    return out
+
+
+def from_numpy(a, device) -> torch.Tensor:
+    """A dense device (or host) tensor holding numpy array ``a``, in the
+    native pool; dtypes are kept (float64 included)."""
+    import numpy as np
+
+    a = np.ascontiguousarray(a)
+    dev = device if isinstance(device, torch.device) else torch.device(device)
+    dt = {v: k for k, v in _NP_OF.items()}[a.dtype.name]
+    out = _mem.empty(tuple(a.shape), dtype=dt, device=dev)
+    if dev.type != "cuda":
+        out.copy_(torch.from_numpy(a))
+        return out
+    if a.nbytes:
+        _lib().rt.memcpy_h2d(out.data_ptr(), a.ctypes.data, a.nbytes, N.stream(dev.index))
+    return out
+
+
 # --------------------------------------------------------------------- copies
 def copy_(dst: torch.Tensor, src: torch.Tensor) -> torch.Tensor:
     """dst[...] = src (broadcast to dst's shape, converted to dst's dtype),

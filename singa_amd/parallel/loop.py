@@ -10,6 +10,15 @@ stream) or on host memory in CPU CI (``device=None``).  The exchange itself is
 synchronous host staging, so it proves correctness of everything above the
 transport, not xGMI bandwidth.  (The reference exercised its exchange only as
 real multi-process ZeroMQ traffic: src/utils/param_manager.cc:103-234.)
+
+``run_ranks(..., captured=True)`` runs the ranks' HIP-graph steps as ONE
+graph (:class:`WorldGraph`): each rank thread's ``Model(use_graph=True)``
+capture joins a capture rooted on a world stream, the bucket all-reduces that
+DistOpt forks onto each rank's comm stream inside the captured backward
+become graph edges plus a device reduction (LoopComm's captured mode), and a
+replay launches every rank's step at once.  That is the N > 1 timed path of
+``bench.py`` -- collectives inside the captured step -- executed with N ranks
+on one GPU.
 """
 from __future__ import annotations
 
@@ -23,15 +32,145 @@ from ..ops import native as N
 from .rccl import RcclCommunicator
 
 
+class WorldGraph:
+    """One HIP graph holding the captured steps of every rank thread of a
+    loopback world on one GPU.
+
+    Each rank thread's models get a :meth:`view` (through
+    :func:`singa_amd.stream.set_step_graph_factory`) with StepGraph's
+    ``capture`` / ``replay`` / ``release``.  ``capture``: all ranks meet,
+    rank 0 begins a capture on the world's origin stream, each rank's current
+    stream joins it through an event and runs its step body (its own private
+    memory pool and work-queue arena), the origin joins every rank's stream
+    and rank 0 ends the capture.  ``replay``: all ranks meet (each one's
+    ``prepare_step`` kernels fenced in with an event), rank 0 launches the
+    graph on the origin stream, and every rank's stream waits for it.  A rank
+    that fails breaks the barrier, so its peers fail instead of waiting."""
+
+    def __init__(self, world: int, device: torch.device, timeout_s: float = 120.0):
+        self.world = world
+        self.device = torch.device(device)
+        self.dev = self.device.index or 0
+        self.timeout_s = timeout_s
+        self.bar = threading.Barrier(world)
+        self.origin = _stream.Stream(self.device)
+        self._g = N.lib().rt.Graph()
+        self.events: List[object] = [None] * world
+        self.done = None
+        self.captures = 0
+        self.replays = 0
+
+    def _meet(self) -> None:
+        self.bar.wait(self.timeout_s)
+
+    def abort(self) -> None:
+        self.bar.abort()
+
+    def view(self, rank: int):
+        return _RankGraph(self, rank)
+
+    @property
+    def nodes(self) -> int:
+        return self._g.nodes
+
+
+class _RankGraph:
+    """Rank ``rank``'s handle on a :class:`WorldGraph` (StepGraph interface)."""
+
+    def __init__(self, wg: WorldGraph, rank: int):
+        from .. import memory
+
+        self.wg, self.rank = wg, rank
+        self.pool = memory.graph_pool(wg.device)
+        self._arena = 0
+
+    def capture(self, fn: Callable, *args, **kwargs):
+        wg, L = self.wg, N.lib()
+        cur = _stream.current(wg.dev)
+        began = False
+        try:
+            wg._meet()
+            if self.rank == 0:
+                wg._g.begin(wg.origin.handle)
+                began = True
+            wg._meet()
+            _stream.Event().record(wg.origin).wait(cur)  # this rank's stream joins the capture
+            with self.pool:
+                self._arena = L.workq_arena_begin()
+                try:
+                    out = fn(*args, **kwargs)
+                finally:
+                    L.workq_arena_end()
+            wg.events[self.rank] = _stream.Event().record(cur)
+            wg._meet()
+            if self.rank == 0:
+                for ev in wg.events:
+                    ev.wait(wg.origin)  # every rank's work rejoins the origin
+                wg._g.end()
+                began = False
+                wg.captures += 1
+            wg._meet()
+            return out
+        except BaseException:
+            wg.abort()
+            if began:
+                wg._g.abort()
+            raise
+
+    @property
+    def nodes(self) -> int:
+        return self.wg.nodes
+
+    def replay(self) -> None:
+        wg = self.wg
+        cur = _stream.current(wg.dev)
+        wg.events[self.rank] = _stream.Event().record(cur)  # this rank's prepare_step work
+        wg._meet()
+        if self.rank == 0:
+            try:
+                for ev in wg.events:
+                    ev.wait(wg.origin)
+                wg._g.replay(wg.origin.handle)
+                wg.done = _stream.Event().record(wg.origin)
+                wg.replays += 1
+            except BaseException:
+                wg.abort()
+                raise
+        wg._meet()
+        wg.done.wait(cur)
+
+    def release(self) -> None:
+        wg = self.wg
+        try:
+            wg._meet()
+        except threading.BrokenBarrierError:
+            pass
+        if self.rank == 0:
+            wg._g.reset()
+        try:
+            wg._meet()
+        except threading.BrokenBarrierError:
+            pass
+        self.pool.release()
+        if self._arena:
+            N.lib().workq_arena_free(self._arena)
+            self._arena = 0
+
+
 def run_ranks(fn: Callable, world: int, *args, device: Optional[torch.device] = None, timeout_s: float = 60.0,
-              return_exceptions: bool = False) -> List[object]:
+              return_exceptions: bool = False, captured: bool = False) -> List[object]:
     """Run ``fn(rank, world, comm, *args)`` on ``world`` threads sharing one
     loopback world; returns the per-rank results in rank order (re-raising
     the first failure unless ``return_exceptions``).  A failing rank aborts
-    the world, so its peers fail fast instead of waiting for the timeout."""
+    the world, so its peers fail fast instead of waiting for the timeout.
+    ``captured=True`` (device ranks): the ranks' HIP-graph steps are captured
+    into one :class:`WorldGraph` (``fn`` may read it as ``comm.world_graph``)."""
     L = N.lib()
     lw = L.LoopWorld(world, float(timeout_s))
     dev = -1 if device is None or torch.device(device).type == "cpu" else (torch.device(device).index or 0)
+    if captured and dev < 0:
+        raise ValueError("run_ranks(captured=True) needs device ranks")
+    wg = WorldGraph(world, torch.device("cuda", dev), timeout_s) if captured else None
     res: List[object] = [None] * world
     errs: List[Optional[BaseException]] = [None] * world
 
@@ -41,16 +180,24 @@ def run_ranks(fn: Callable, world: int, *args, device: Optional[torch.device] = 
             if dev >= 0:
                 torch.cuda.set_device(dev)
                 s = _stream.pooled(torch.device("cuda", dev), f"loop-rank{r}")
-                with s:
-                    comm = RcclCommunicator(world, r, r, native=native, device=torch.device("cuda", dev))
-                    res[r] = fn(r, world, comm, *args)
-                s.synchronize()
+                if wg is not None:
+                    _stream.set_step_graph_factory(lambda device, r=r: wg.view(r))
+                try:
+                    with s:
+                        comm = RcclCommunicator(world, r, r, native=native, device=torch.device("cuda", dev))
+                        comm.world_graph = wg
+                        res[r] = fn(r, world, comm, *args)
+                    s.synchronize()
+                finally:
+                    _stream.set_step_graph_factory(None)
             else:
                 comm = RcclCommunicator(world, r, r, native=native)
                 res[r] = fn(r, world, comm, *args)
         except BaseException as e:  # noqa: BLE001 - reported to the caller
             errs[r] = e
             native.abort()
+            if wg is not None:
+                wg.abort()
 
     ts = [threading.Thread(target=body, args=(r,), daemon=True, name=f"loop-rank-{r}") for r in range(world)]
     for t in ts:

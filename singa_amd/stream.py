@@ -30,6 +30,12 @@ def _rt():
     return N.lib().rt
 
 
+def device_synchronize(device=None) -> None:
+    """Wait until every stream of ``device`` is idle (hipDeviceSynchronize)."""
+    idx = torch.device(device).index if isinstance(device, (str, torch.device)) else device
+    _rt().device_synchronize(-1 if idx is None else int(idx))
+
+
 def current(device=None) -> int:
     """Handle of this thread's current stream on ``device``."""
     idx = torch.device(device).index if isinstance(device, (str, torch.device)) else device
@@ -120,6 +126,20 @@ class Event:
 
 
 _CAPTURE_STREAMS: dict = {}
+_TLS = __import__("threading").local()
+
+
+def set_step_graph_factory(factory) -> None:
+    """This thread's models capture their steps with ``factory(device)``
+    instead of :class:`StepGraph` (None restores the default).  The loopback
+    world's rank threads install their rank's :class:`~singa_amd.parallel.loop.WorldGraph`
+    view here, so every rank's step lands in ONE graph."""
+    _TLS.factory = factory
+
+
+def new_step_graph(device=None):
+    f = getattr(_TLS, "factory", None)
+    return f(device) if f is not None else StepGraph(device)
 
 
 class StepGraph:
@@ -136,6 +156,7 @@ class StepGraph:
         self._g = _rt().Graph()
         self.pool = memory.graph_pool(torch.device("cuda", self.device_index))
         self.keep: list = []
+        self._arena = 0  # the persistent kernels' queue slots of this graph (workq.hip)
 
     def capture(self, fn: Callable, *args, **kwargs):
         s = _CAPTURE_STREAMS.get(self.device_index)
@@ -144,14 +165,19 @@ class StepGraph:
         cur = current(self.device_index)
         s.wait_stream(cur)
         torch_before = torch.cuda.memory_allocated(self.device_index)
+        L = N.lib()
         with s, self.pool:
-            self._g.begin(s.handle)
+            self._arena = L.workq_arena_begin()
             try:
-                out = fn(*args, **kwargs)
-            except BaseException:
-                self._g.abort()
-                raise
-            self._g.end()
+                self._g.begin(s.handle)
+                try:
+                    out = fn(*args, **kwargs)
+                except BaseException:
+                    self._g.abort()
+                    raise
+                self._g.end()
+            finally:
+                L.workq_arena_end()
         if torch.cuda.memory_allocated(self.device_index) != torch_before:
             # a PyTorch allocation inside the capture would live in PyTorch's
             # allocator, which does not know the graph still uses it
@@ -166,6 +192,14 @@ class StepGraph:
     def replay(self) -> None:
         self._g.replay(current(self.device_index))
 
+    @property
+    def queue_slots(self) -> int:
+        """Work-queue slots the captured persistent kernels hold."""
+        return N.lib().workq_arena_slots(self._arena) if self._arena else 0
+
     def release(self) -> None:
         self._g.reset()
         self.pool.release()
+        if self._arena:
+            N.lib().workq_arena_free(self._arena)
+            self._arena = 0

@@ -79,3 +79,80 @@ def test_bench_parent_does_not_import_torch(tmp_path):
     p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, env=env)
     assert p.returncode == 0, p.stderr
     assert out.read_text() == "clean"
+
+
+def _bench():
+    import importlib
+    import sys as _sys
+    _sys.path.insert(0, REPO)
+    return importlib.import_module("bench")
+
+
+def test_bench_model_switch_builds_each_config():
+    """--model resnet50 / alexnet / bert: the BASELINE configs' models, inputs
+    of their shapes and the record fields (built on the CppCPU device, tiny
+    batch; the GPU run is the same code)."""
+    import numpy as np
+
+    from singa_amd import device
+
+    bench = _bench()
+    cpu = device.get_default_device()
+    args = bench._parser().parse_args(["--model", "alexnet", "--batch", "2"])
+    m, (x, y), o, info = bench._build(args, cpu, 0)
+    assert x.shape == (2, 3, 224, 224) and info["unit"] == "images/s" and "AlexNet" in info["metric"]
+    assert type(o).__name__ == "SGD" and o.weight_decay == 5e-4
+    args = bench._parser().parse_args(["--model", "bert", "--batch", "2", "--seq", "16"])
+    m, (ids, y), o, info = bench._build(args, cpu, 0)
+    assert ids.shape == (2, 16) and info["unit"] == "sequences/s" and info["seq_len"] == 16
+    assert type(o).__name__ == "Adam"
+    args = bench._parser().parse_args(["--batch", "2", "--image", "32"])
+    m, (x, y), o, info = bench._build(args, cpu, 0)
+    assert info["metric"] == "images/sec (whole node) ResNet-50 bf16 training" and x.shape == (2, 3, 32, 32)
+    assert bench._parser().parse_args([]).model == "resnet50"
+    assert np.asarray(y.data).shape == (2,)
+
+
+class _StubComm:
+    """all_reduce(max/min) as if a peer held `peer` (a host numpy vector)."""
+
+    def __init__(self, peer):
+        self.peer = peer
+
+    def all_reduce(self, t, op="sum"):
+        import numpy as np
+        v = t.numpy()
+        v[:] = np.maximum(v, self.peer) if op == "max" else np.minimum(v, self.peer)
+
+
+class _StubOpt:
+    def __init__(self, w, buckets):
+        import torch
+
+        class S:
+            pass
+        self.store = S()
+        self.store.w = torch.from_numpy(w)
+        self.buckets = buckets
+
+
+def test_replica_guard_detects_drift():
+    """bench.py's cross-rank guard: identical replicas pass bit-exactly; one
+    bucket of one rank off by a single lr*g-sized step fails it."""
+    import numpy as np
+
+    from singa_amd import device
+
+    bench = _bench()
+    cpu = device.get_default_device()
+    rng = np.random.RandomState(0)
+    w = (rng.randn(10000) * 0.05).astype(np.float32)
+    opt_ = _StubOpt(w, [(0, 4000, []), (4000, 10000, [])])
+    same = bench.replica_checksums(opt_)
+    r = bench.replica_guard(_StubComm(same.copy()), opt_, cpu)
+    assert r["ok"] and r["bitwise_equal"] and r["buckets"] == 2
+    w2 = w.copy()
+    w2[4000:4100] -= np.float32(1e-2) * rng.randn(100).astype(np.float32) * 0.05  # a lost bucket update
+    other = bench.replica_checksums(_StubOpt(w2, opt_.buckets))
+    r = bench.replica_guard(_StubComm(other), opt_, cpu)
+    assert not r["ok"] and r["max_rel_spread"] > 1e-6

@@ -1,0 +1,207 @@
+"""The N > 1 timed path of bench.py -- each gradient bucket's all-reduce
+forked onto the comm stream INSIDE the captured HIP-graph step -- executed
+with several ranks on one GPU.
+
+The ranks are threads over the loopback transport; ``run_ranks(captured=True)``
+makes every rank's ``Model(use_graph=True)`` capture land in ONE world graph
+(parallel/loop.py WorldGraph) in which each all-reduce is graph edges plus a
+device reduction (loop_comm.cpp captured mode, kernels/loopred.hip).  The
+captured step is compared with the eager loopback step (same transport, no
+graph) and with one process training on the full batch.  Also here: the
+graph-capture fallback of Model (bench.py's eager fallback) and bench.py's
+loopback rehearsal entry point.
+"""
+import os
+import sys
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+pytestmark = pytest.mark.gpu
+
+_INIT = threading.Lock()
+
+
+def _dev0():
+    return torch.device("cuda", 0)
+
+
+def _mlp_rank(rank, world, comm, steps, bf16, use_graph):
+    from singa_amd import device, opt, tensor
+    from singa_amd.models import mlp
+    from singa_amd.parallel import DistOpt
+
+    dev = device.create_rocm_gpu_on(0)
+    rng = np.random.RandomState(0)
+    X = rng.randn(32, 40).astype(np.float32)
+    Y = rng.randint(0, 10, 32).astype(np.int32)
+    n = 32 // world
+    x = tensor.from_numpy(X[rank * n:(rank + 1) * n], dev)
+    y = tensor.from_numpy(Y[rank * n:(rank + 1) * n], dev)
+    m = mlp.create_model((64, 48), 10)
+    with _INIT:  # rank 0's seeded init is the single-process reference's (DistOpt broadcasts it)
+        dev.SetRandSeed(11 + rank)
+        m.compile([x], is_train=False)
+        torch.cuda.current_stream().synchronize()
+    # small buckets: several all-reduces per captured step, forked as the backward completes them
+    m.set_optimizer(DistOpt(opt.SGD(0.1, 0.9), comm=comm, bucket_mb=0.004, first_bucket_mb=0.002,
+                            grad_dtype=torch.bfloat16 if bf16 else torch.float32))
+    m.compile([x], is_train=True, use_graph=use_graph)
+    losses = []
+    for _ in range(steps):
+        _, loss = m(x, y)
+        losses.append(loss.data.float().clone())
+    torch.cuda.current_stream().synchronize()
+    params = {k: v.data.float().cpu().numpy() for k, v in m.get_params().items()}
+    wg = getattr(comm, "world_graph", None)
+    info = None if wg is None else (wg.captures, wg.replays, wg.nodes, len(m.optimizer.buckets))
+    return params, [float(v.cpu()) for v in losses], info
+
+
+def _single(steps):
+    from singa_amd import device, opt, tensor
+    from singa_amd.models import mlp
+
+    dev = device.create_rocm_gpu_on(0)
+    dev.SetRandSeed(11)
+    rng = np.random.RandomState(0)
+    X = rng.randn(32, 40).astype(np.float32)
+    Y = rng.randint(0, 10, 32).astype(np.int32)
+    m = mlp.create_model((64, 48), 10)
+    m.set_optimizer(opt.SGD(0.1, 0.9))
+    x, y = tensor.from_numpy(X, dev), tensor.from_numpy(Y, dev)
+    m.compile([x], is_train=True)
+    for _ in range(steps):
+        m(x, y)
+    torch.cuda.synchronize()
+    return {k: v.data.float().cpu().numpy() for k, v in m.get_params().items()}
+
+
+@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("bf16", [False, True])
+def test_captured_distopt_world(gpu, world, bf16):
+    """test_captured_distopt_world{2,4}: 2 eager warm-up steps, then the
+    capture, then replays -- every rank's step in one graph."""
+    from singa_amd.parallel.loop import run_ranks
+
+    steps = 6
+    cap = run_ranks(_mlp_rank, world, steps, bf16, True, device=_dev0(), timeout_s=120.0, captured=True)
+    eager = run_ranks(_mlp_rank, world, steps, bf16, False, device=_dev0(), timeout_s=120.0)
+    ref = _single(steps)
+    captures, replays, nodes, nbuckets = cap[0][2]
+    assert captures == 1 and replays == steps - 2 and nodes > 0 and nbuckets >= 3, cap[0][2]
+    for k in ref:
+        for r in range(world):
+            np.testing.assert_array_equal(cap[r][0][k], cap[0][0][k], err_msg=f"{k} rank {r}")  # replicas identical
+        if bf16:
+            # the captured reduction accumulates in fp32 and rounds once; the
+            # host path rounds every partial sum to bf16
+            np.testing.assert_allclose(cap[0][0][k], eager[0][0][k], rtol=2e-2, atol=2e-3, err_msg=k)
+            np.testing.assert_allclose(cap[0][0][k], ref[k], rtol=2e-2, atol=2e-3, err_msg=k)
+        else:
+            np.testing.assert_allclose(cap[0][0][k], eager[0][0][k], rtol=1e-6, atol=1e-7, err_msg=k)
+            np.testing.assert_allclose(cap[0][0][k], ref[k], rtol=2e-5, atol=2e-6, err_msg=k)
+    for r in range(world):  # per-rank losses of the captured replays == the eager steps'
+        np.testing.assert_allclose(cap[r][1], eager[r][1], rtol=2e-2 if bf16 else 1e-5)
+
+
+def _cnn_rank(rank, world, comm, steps, use_graph):
+    """A small bottleneck ResNet (persistent 1x1 / 3x3 conv kernels with work
+    queues, BN, residual tails) per rank: every rank's persistent kernels
+    land in the same graph and run concurrently on replay."""
+    from singa_amd import device, opt, tensor
+    from singa_amd.models import resnet
+    from singa_amd.parallel import DistOpt
+
+    dev = device.create_rocm_gpu_on(0)
+    rng = np.random.RandomState(rank)
+    x = tensor.from_numpy(rng.standard_normal((16, 3, 64, 64)).astype(np.float32), dev)
+    y = tensor.from_numpy(rng.randint(0, 10, 16).astype(np.int32), dev)
+    m = resnet.ResNet(resnet.Bottleneck, [1, 1, 1, 1], num_classes=10, compute_dtype=torch.bfloat16)
+    with _INIT:
+        dev.SetRandSeed(5 + rank)
+        m.compile([x], is_train=False)
+        torch.cuda.current_stream().synchronize()
+    m.set_optimizer(DistOpt(opt.SGD(0.05, 0.9), comm=comm, bucket_mb=1.0, first_bucket_mb=0.25))
+    m.compile([x], is_train=True, use_graph=use_graph)
+    losses = []
+    for _ in range(steps):
+        _, loss = m(x, y)
+        losses.append(loss.data.float().clone())
+    torch.cuda.current_stream().synchronize()
+    w = m.optimizer.store.w.cpu().numpy()
+    return w, [float(v.cpu()) for v in losses]
+
+
+def test_captured_resnet_world2_equals_eager(gpu):
+    from singa_amd.parallel.loop import run_ranks
+
+    steps = 5
+    cap = run_ranks(_cnn_rank, 2, steps, True, device=_dev0(), timeout_s=180.0, captured=True)
+    eager = run_ranks(_cnn_rank, 2, steps, False, device=_dev0(), timeout_s=180.0)
+    np.testing.assert_array_equal(cap[0][0], cap[1][0])  # replicas bit-identical after the captured steps
+    for r in range(2):
+        assert np.isfinite(cap[r][1]).all()
+        np.testing.assert_allclose(cap[r][1], eager[r][1], rtol=2e-2, atol=2e-2)
+    # weights after 5 steps: same trajectory as the eager world (bf16 convs; the
+    # graph and eager paths launch the same kernels)
+    rel = np.linalg.norm(cap[0][0] - eager[0][0]) / np.linalg.norm(eager[0][0])
+    assert rel < 1e-3, rel
+
+
+def test_graph_capture_failure_falls_back_to_eager(gpu, monkeypatch):
+    """Model.graph_fallback: a capture that raises switches the model to eager
+    execution; the optimiser leaves graph mode and keeps its lr / step
+    schedule, so the run equals a pure eager run (bench.py's
+    fallback only wrapped warm-up call 0)."""
+    from singa_amd import device, opt, tensor
+    from singa_amd.models import mlp
+
+    def run(use_graph, fail):
+        if fail:
+            monkeypatch.setenv("SINGA_AMD_GRAPH_FAIL_TEST", "1")
+        else:
+            monkeypatch.delenv("SINGA_AMD_GRAPH_FAIL_TEST", raising=False)
+        dev = device.create_rocm_gpu_on(0)
+        dev.SetRandSeed(3)
+        rng = np.random.RandomState(0)
+        x = tensor.from_numpy(rng.randn(16, 40).astype(np.float32), dev)
+        y = tensor.from_numpy(rng.randint(0, 10, 16).astype(np.int32), dev)
+        m = mlp.create_model((32,), 10)
+        sched = opt.ExponentialDecay(0.1, 2, 0.5)
+        m.set_optimizer(opt.SGD(sched, 0.9))
+        m.compile([x], is_train=True, use_graph=use_graph)
+        m.graph_fallback = True
+        for _ in range(6):
+            m(x, y)
+        torch.cuda.synchronize()
+        return m, {k: v.data.float().cpu().numpy() for k, v in m.get_params().items()}
+
+    m, fb = run(True, True)
+    assert not m.graph_mode and m.graph_error and "capture refused" in m.graph_error
+    assert not m.optimizer.graph_mode and m.optimizer.step_counter == 6
+    _, ref = run(False, False)
+    for k in ref:
+        np.testing.assert_allclose(fb[k], ref[k], rtol=1e-6, atol=1e-7, err_msg=k)
+
+
+def test_bench_loopback_rehearsal(gpu):
+    """bench.py --loopback: ResNet-18 ranks on one GPU through the captured
+    world graph, the replica guard run over the loopback transport."""
+    import subprocess
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--loopback", "--model", "resnet18", "--batch",
+                        "16", "--image", "64", "--steps", "3", "--warmup", "3", "--bucket-mb", "4"],
+                       cwd=repo, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    import json
+    rec = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    c = rec["config"]["comm"]
+    assert rec["loopback_ranks"] == 2 and rec["config"]["exec"] == "hipgraph"
+    assert c["replicas"]["ok"] and c["replicas"]["bitwise_equal"]
+    assert c["world_graph"]["captures"] == 1 and c["world_graph"]["replays"] == 4

@@ -127,6 +127,53 @@ def test_queue_graph_replay(gpu, lib):
     g.release()
 
 
+def test_two_graphs_replayed_concurrently_own_their_slots(gpu, lib):
+    """Two graphs capturing the same persistent kernels, replayed at the same
+    time on two streams while eager launches of those kernels run on a third:
+    each capture takes its queue slots from its own arena (never from the
+    shared ring the eager launches advance), so no two running kernels share
+    counters and every output is exact."""
+    from singa_amd import stream as S
+    from singa_amd.stream import StepGraph
+
+    L = lib
+    L.workq_set(1)
+    sets = [_cases(L, gpu) for _ in range(3)]
+    refs = []
+    for cases in sets:
+        r = {}
+        for name, (fn, y) in cases.items():
+            fn()
+            r[name] = y.clone()
+        refs.append(r)
+    torch.cuda.synchronize()
+    graphs = []
+    for cases in sets[:2]:
+        g = StepGraph()
+        g.capture(lambda cases=cases: [fn() for fn, _ in cases.values()])
+        assert g.queue_slots == len(cases), g.queue_slots  # one fresh slot per captured persistent launch
+        graphs.append(g)
+    streams = [S.pooled(gpu, f"wq-test-{i}") for i in range(3)]
+    for rep in range(4):
+        for cases in sets:
+            for _, y in cases.values():
+                y.fill_(float("nan"))
+        torch.cuda.synchronize()
+        for g, s in zip(graphs, streams[:2]):
+            with s:
+                g.replay()
+        with streams[2]:
+            for _ in range(2):
+                for fn, _ in sets[2].values():
+                    fn()
+        torch.cuda.synchronize()
+        for cases, r in zip(sets, refs):
+            for name, (_, y) in cases.items():
+                assert torch.equal(y, r[name]), (name, rep)
+    for g in graphs:
+        g.release()
+
+
 def test_queue_stress_back_to_back(gpu, lib):
     """Many back-to-back launches of each persistent kernel, the output
     NaN-filled before every launch and checked on the device (no host sync
