@@ -36,6 +36,9 @@
 //   * wgrad splits the pixel reduction across workgroups (blockIdx.z) and
 //     accumulates fp32 partial tiles atomically into the [K][R][S][C]
 //     gradient (the layout of the flat gradient buffer).
+#include <stdio.h>
+#include <stdlib.h>
+
 #include <stdexcept>
 #include <type_traits>
 
@@ -203,6 +206,16 @@ static thread_local const uint8_t* g_res_mask = nullptr;
 // its output masked (stats_mode 4, the algebraic residual-BN backward's g~)
 static thread_local int g_mask_out = 0;
 
+// SG_GEMM_LOG=1: one stderr line per GEMM launch (operand modes, shape,
+// epilogue features) -- the per-shape breakdown behind a kernel profile
+static int gemm_log() {
+  static int on = [] {
+    const char* e = getenv("SG_GEMM_LOG");
+    return e && e[0] == '1' ? 1 : 0;
+  }();
+  return on;
+}
+
 constexpr int stages_c(int BM, int BN, int STAGES) { return STAGES * (BM + BN) * BK * 2; }
 
 template <int BM, int BN, int AM, int BMODE, int OUT, int NTH = NT, int WM = 2, int WN = 2, int STAGES = 2,
@@ -225,6 +238,9 @@ static void launch_t(const GemmArgs& p_in, int tiles, int ydim, int zdim, hipStr
   constexpr int lds = stages > etile ? stages : etile;
   static_assert(lds <= 160 * 1024, "LDS budget");
   auto* kern = igemm_k<BM, BN, AM, BMODE, OUT, NTH, WM, WN, STAGES, FLAGS>;
+  if (gemm_log())
+    fprintf(stderr, "SG_GEMM_L igemm_k<%d,%d,%d,%d,%d,%d,%d,%d,%d,%d> grid %d %d %d\n", BM, BN, AM, BMODE, OUT, NTH, WM,
+            WN, STAGES, FLAGS, tiles, ydim, zdim);
   if constexpr (lds > 65536) {
     static bool attr = [kern] {
       return hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
@@ -241,6 +257,7 @@ static void launch_pp(const GemmArgs& p_in, int tiles, int ydim, hipStream_t s) 
   p.nt_store = g_tune[8];
   constexpr int lds = 2 * PP_BUF;
   auto* kern = pp_gemm_k<OUT, FLAGS>;
+  if (gemm_log()) fprintf(stderr, "SG_GEMM_L pp_gemm_k<%d,%d> grid %d %d 1\n", OUT, FLAGS, tiles, ydim);
   static bool attr = [kern] {
     return hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess;
   }();
@@ -265,6 +282,9 @@ static void launch_sk(const GemmArgs& p, int tiles_m, int tiles_n, hipStream_t s
   if (g > tiles_m) g = tiles_m >= 8 ? tiles_m / 8 * 8 : 8;  // (a multiple of 8: the per-XCD tile partition)
   GemmArgs q = p;
   q.wq = 8 * tiles_n <= QMAX ? sg_workq_slot() : nullptr;
+  if (gemm_log())
+    fprintf(stderr, "SG_GEMM_L sk_gemm_k<%d,%d,%d> grid %d %d 1 M=%d N=%d K=%d\n", KT, EPI, AM, g, tiles_n, p.M, p.N,
+            p.K);
   hipLaunchKernelGGL(kern, dim3(g, tiles_n, 1), dim3(256), lds, s, q);
 }
 
@@ -345,6 +365,12 @@ static void pick_wgrad(int M, int N, int K, int mode, int& BM, int& BN, int& spl
 template <int AM, int BMODE, int OUT, int FLAGS = 0>
 static void launch(const GemmArgs& p, int M, int splits, hipStream_t s, int batch, int zdim) {
   int BM, BN;
+  if (gemm_log())
+    fprintf(stderr, "SG_GEMM am=%d bm=%d out=%d flags=%d M=%d N=%d K=%d splits=%d batch=%d z=%d beta=%g stats=%d "
+                    "smode=%d det=%d res=%d bias=%d relu=%d act=%d phase=%d R=%d S=%d C=%d sh=%d\n",
+            AM, BMODE, OUT, FLAGS, M, p.N, p.K, splits, batch, zdim, p.beta, p.stats != nullptr, p.stats_mode,
+            p.stats_det, p.res_g != nullptr, p.bias != nullptr, p.relu, p.act, p.out_phase, p.g.R, p.g.S, p.g.C,
+            p.g.sh);
   if constexpr (OUT != OUT_F32_ATOMIC) {
     {
       const int z = zdim > 0 ? zdim : 1;
