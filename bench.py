@@ -178,7 +178,9 @@ def run_rank(args, rank: int, world: int, local: int, comm, loopback: bool = Fal
     from singa_amd.ops import glue as G
     from singa_amd.parallel import DistOpt
 
-    dev = device.create_rocm_gpu_on(local % torch.cuda.device_count(), set_default=not loopback)
+    # (loopback ranks: every rank thread is on GPU 0)
+    dev = device.create_rocm_gpu_on(0 if loopback else local % max(1, torch.cuda.device_count()),
+                                    set_default=not loopback)
     if not loopback:
         dev.SetRandSeed(args.seed + rank)
     m, (tx, ty), base_opt, info = _build(args, dev, rank)
