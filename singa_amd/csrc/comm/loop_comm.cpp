@@ -42,6 +42,8 @@
 #include <hip/hip_runtime.h>
 #include <pybind11/pybind11.h>
 #include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
 
 #include <algorithm>
 #include <chrono>
@@ -330,8 +332,16 @@ class LoopComm {
     if (done_out) *done_out = g_->done;
     return g_->slots;
   }
+  static bool dbg() {
+    static int on = [] {
+      const char* e = getenv("SG_LOOP_DEBUG");
+      return e && e[0] == '1' ? 1 : 0;
+    }();
+    return on;
+  }
   // the captured all-reduce (see the header): called with the GIL held
   void captured_all_reduce(P send, P recv, size_t count, int dt, int op, P s) {
+    if (dbg()) fprintf(stderr, "[loop r%d] captured all_reduce count=%zu dt=%d stream=%p\n", rank_, count, dt, (void*)s);
     if (nranks() > 16) throw std::runtime_error("LoopComm (captured): at most 16 ranks");
     Slot me{send, recv, count, dt, op};
     me.ev = new_event();
@@ -359,6 +369,7 @@ class LoopComm {
     gbarrier(nullptr, "all_reduce (captured)", &d);
     if (rank_ != 0) hchk(hipStreamWaitEvent((hipStream_t)s, d, 0), "hipStreamWaitEvent");
     gbarrier(nullptr, "all_reduce (captured)");  // every rank joined: g_->done may be replaced
+    if (dbg()) fprintf(stderr, "[loop r%d] captured all_reduce done\n", rank_);
   }
   void no_capture(P s, const char* what) {
     if (capturing(s))

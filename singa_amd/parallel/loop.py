@@ -22,6 +22,8 @@ on one GPU.
 """
 from __future__ import annotations
 
+import os
+import sys
 import threading
 from typing import Callable, List, Optional
 
@@ -30,6 +32,14 @@ import torch
 from .. import stream as _stream
 from ..ops import native as N
 from .rccl import RcclCommunicator
+
+
+_DBG = os.environ.get("SG_LOOP_DEBUG") == "1"
+
+
+def _dbg(*a) -> None:
+    if _DBG:
+        print(f"[{threading.current_thread().name}]", *a, file=sys.stderr, flush=True)
 
 
 class WorldGraph:
@@ -91,22 +101,28 @@ class _RankGraph:
         try:
             wg._meet()
             if self.rank == 0:
+                _dbg("begin capture")
                 wg._g.begin(wg.origin.handle)
                 began = True
             wg._meet()
+            _dbg("fork")
             _stream.Event().record(wg.origin).wait(cur)  # this rank's stream joins the capture
             with self.pool:
                 self._arena = L.workq_arena_begin()
                 try:
+                    _dbg("body")
                     out = fn(*args, **kwargs)
                 finally:
                     L.workq_arena_end()
+            _dbg("body done")
             wg.events[self.rank] = _stream.Event().record(cur)
             wg._meet()
             if self.rank == 0:
                 for ev in wg.events:
                     ev.wait(wg.origin)  # every rank's work rejoins the origin
+                _dbg("end capture")
                 wg._g.end()
+                _dbg("instantiated", wg._g.nodes)
                 began = False
                 wg.captures += 1
             wg._meet()
@@ -130,6 +146,7 @@ class _RankGraph:
             try:
                 for ev in wg.events:
                     ev.wait(wg.origin)
+                _dbg("replay")
                 wg._g.replay(wg.origin.handle)
                 wg.done = _stream.Event().record(wg.origin)
                 wg.replays += 1

@@ -1,4 +1,5 @@
 #!/bin/bash
-# round 6, call b: the crash of test_captured_distopt_world (faulthandler), then the rest of the suite
+# round 6, call b: step trace of the captured loopback world
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-tools/gpu_step.sh "240 t_cap.log python -X faulthandler -u -m pytest tests/test_captured_world_gpu.py -x -v -s -p no:cacheprovider -k 'world and False-2'"
+export SG_LOOP_DEBUG=1
+tools/gpu_step.sh "120 dbg_world.log python -X faulthandler -u tools/world_capture_dbg.py 2"
