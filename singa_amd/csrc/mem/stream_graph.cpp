@@ -90,10 +90,15 @@ class Graph {
   ~Graph() { reset(); }
   // capture everything enqueued on stream s (and on streams forked from it
   // through events) by THIS thread until end()
-  void begin(uintptr_t s) {
+  // mode: 1 thread-local (the default), 2 relaxed (a capture that several
+  // threads enqueue into -- the loopback world's rank threads), 0 global
+  void begin(uintptr_t s, int mode) {
     if (capturing_) throw std::runtime_error("Graph.begin: already capturing");
     reset();
-    hchk(hipStreamBeginCapture((hipStream_t)s, hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture");
+    const hipStreamCaptureMode m = mode == 0   ? hipStreamCaptureModeGlobal
+                                   : mode == 2 ? hipStreamCaptureModeRelaxed
+                                               : hipStreamCaptureModeThreadLocal;
+    hchk(hipStreamBeginCapture((hipStream_t)s, m), "hipStreamBeginCapture");
     s_ = (hipStream_t)s;
     capturing_ = true;
   }
@@ -159,7 +164,7 @@ void register_stream_graph(py::module& m) {
       .def("elapsed_ms", &Event::elapsed_ms);
   py::class_<Graph>(sm, "Graph")
       .def(py::init<>())
-      .def("begin", &Graph::begin)
+      .def("begin", &Graph::begin, py::arg("stream"), py::arg("mode") = 1)
       .def("end", &Graph::end)
       .def("abort", &Graph::abort)
       .def("replay", &Graph::replay)

@@ -102,7 +102,7 @@ class _RankGraph:
             wg._meet()
             if self.rank == 0:
                 _dbg("begin capture")
-                wg._g.begin(wg.origin.handle)
+                wg._g.begin(wg.origin.handle, 2)  # relaxed: every rank thread enqueues into this capture
                 began = True
             wg._meet()
             _dbg("fork")
