@@ -17,6 +17,8 @@
 #include <hip/hip_runtime.h>
 #include <pybind11/pybind11.h>
 #include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
 
 #include <stdexcept>
 #include <string>
@@ -106,9 +108,20 @@ class Graph {
     if (!capturing_) throw std::runtime_error("Graph.end: not capturing");
     capturing_ = false;
     hipGraph_t g = nullptr;
+    static const bool dbg = [] {
+      const char* e = getenv("SG_LOOP_DEBUG");
+      return e && e[0] == '1';
+    }();
+    if (dbg) fprintf(stderr, "[graph] end capture\n");
     hchk(hipStreamEndCapture(s_, &g), "hipStreamEndCapture");
     g_ = g;
+    if (dbg) {
+      size_t n = 0;
+      (void)hipGraphGetNodes(g_, nullptr, &n);
+      fprintf(stderr, "[graph] captured %zu nodes; instantiate\n", n);
+    }
     hchk(hipGraphInstantiate(&exec_, g_, nullptr, nullptr, 0), "hipGraphInstantiate");
+    if (dbg) fprintf(stderr, "[graph] instantiated\n");
     size_t n = 0;
     hchk(hipGraphGetNodes(g_, nullptr, &n), "hipGraphGetNodes");
     nodes_ = n;

@@ -1,7 +1,7 @@
 #!/bin/bash
-# round 6, call b: cross-thread capture probe
+# round 6, call b: captured loopback world, narrowed
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-tools/gpu_step.sh "60 p_single.log python -X faulthandler -u tools/capture_threads_probe.py single 2" && \
-tools/gpu_step.sh "60 p_tempev.log python -X faulthandler -u tools/capture_threads_probe.py tempev 2" && \
-tools/gpu_step.sh "60 p_launchB.log python -X faulthandler -u tools/capture_threads_probe.py launchB 2" && \
-tools/gpu_step.sh "60 p_forkB.log python -X faulthandler -u tools/capture_threads_probe.py forkB 2"
+export SG_LOOP_DEBUG=1
+tools/gpu_step.sh "60 w1.log python -X faulthandler -u tools/world_capture_dbg.py 1" && \
+tools/gpu_step.sh "60 w2n.log python -X faulthandler -u tools/world_capture_dbg.py 2 nooverlap" && \
+tools/gpu_step.sh "60 w2.log python -X faulthandler -u tools/world_capture_dbg.py 2"

@@ -50,6 +50,14 @@ def main():
         return out
     LP._RankGraph.capture = capture
     world = int(sys.argv[1]) if len(sys.argv) > 1 else 2
+    if len(sys.argv) > 2 and sys.argv[2] == "nooverlap":
+        from singa_amd.parallel import distopt
+        orig = distopt.DistOpt.__init__
+
+        def init(self, *a, **k):
+            orig(self, *a, **k)
+            self.overlap = False
+        distopt.DistOpt.__init__ = init
     res = LP.run_ranks(rank_fn, world, 4, device=torch.device("cuda", 0), timeout_s=60.0, captured=True)
     log("results", res)
 
