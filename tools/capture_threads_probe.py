@@ -9,6 +9,8 @@ work.
       launchB  thread A begins and forks; thread B launches the kernel on S1; A joins and ends
       forkB    thread A begins; thread B forks S1, launches, records the join event; A joins and ends
       tempev   one thread, the fork event destroyed right after the wait (before the capture ends)
+      xrank1   the loopback world's captured all-reduce pattern between two "ranks", one thread
+      xrank2   the same with each rank's calls on its own thread
 """
 import os
 import sys
@@ -51,6 +53,8 @@ def main():
         t.start()
         t.join()
 
+    if variant.startswith("xrank"):
+        return xrank(variant == "xrank2", mode)
     g.begin(s0.handle, mode)
     if variant == "single":
         fork(); launch(); join_ev()
@@ -71,6 +75,72 @@ def main():
     v = float(G.to_numpy(x[:1])[0])
     print(variant, "replayed, x[0] =", v, flush=True)
     assert v == 3.0
+
+
+def xrank(threaded: bool, mode: int):
+    """rank r: cur_r joins the origin, cs_r forks from cur_r, records E_r;
+    rank 0's cs waits every E_r and runs the reduction, records d; the other
+    ranks' cs wait d; each cur_r joins its cs_r; the origin joins each cur_r."""
+    from singa_amd import memory, stream
+    from singa_amd.ops import glue as G
+    from singa_amd.ops import native as N
+
+    rt = N.lib().rt
+    dev = torch.device("cuda", 0)
+    origin = stream.Stream(dev)
+    cur = [stream.Stream(dev) for _ in range(2)]
+    cs = [stream.Stream(dev, priority=-1) for _ in range(2)]
+    xs = [memory.empty((4096,), dtype=torch.float32, device=dev) for _ in range(2)]
+    torch.cuda.synchronize()
+    g = rt.Graph()
+    keep = []
+    bar = threading.Barrier(2 if threaded else 1)
+    E = [None, None]
+    box = {}
+
+    def part1(r):
+        stream.Event().record(origin).wait(cur[r])
+        with cur[r]:
+            G.fill_(xs[r], float(r + 1))
+        cs[r].wait_stream(cur[r])
+        E[r] = stream.Event().record(cs[r])
+
+    def part2(r):
+        if r == 0:
+            for j in range(2):
+                E[j].wait(cs[0])
+            with cs[0]:
+                G.binary("add", xs[0], xs[1], out=xs[0])
+                G.copy_(xs[1], xs[0])
+            box["d"] = stream.Event().record(cs[0])
+
+    def part3(r):
+        if r != 0:
+            box["d"].wait(cs[r])
+        w = stream.Event().record(cs[r])
+        w.wait(cur[r])
+        keep.append(stream.Event().record(cur[r]))
+
+    g.begin(origin.handle, mode)
+    if threaded:
+        def body(r):
+            part1(r); bar.wait(); part2(r); bar.wait(); part3(r)
+        ts = [threading.Thread(target=body, args=(r,)) for r in range(2)]
+        [t.start() for t in ts]
+        [t.join() for t in ts]
+    else:
+        for f in (part1, part2, part3):
+            for r in range(2):
+                f(r)
+    for ev in keep:
+        ev.wait(origin)
+    g.end()
+    print("xrank captured nodes", g.nodes, flush=True)
+    g.replay(origin.handle)
+    origin.synchronize()
+    v = [float(G.to_numpy(x[:1])[0]) for x in xs]
+    print("xrank replayed", v, flush=True)
+    assert v == [3.0, 3.0]
 
 
 if __name__ == "__main__":
