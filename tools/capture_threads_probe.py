@@ -11,6 +11,8 @@ work.
       tempev   one thread, the fork event destroyed right after the wait (before the capture ends)
       xrank1   the loopback world's captured all-reduce pattern between two "ranks", one thread
       xrank2   the same with each rank's calls on its own thread
+      xorig1   the reduction on the ORIGIN stream instead of rank 0's comm stream (one thread)
+      xorig2   the same, threaded
 """
 import os
 import sys
@@ -55,6 +57,8 @@ def main():
 
     if variant.startswith("xrank"):
         return xrank(variant == "xrank2", mode)
+    if variant.startswith("xorig"):
+        return xrank(variant == "xorig2", mode, on_origin=True)
     g.begin(s0.handle, mode)
     if variant == "single":
         fork(); launch(); join_ev()
@@ -77,7 +81,7 @@ def main():
     assert v == 3.0
 
 
-def xrank(threaded: bool, mode: int):
+def xrank(threaded: bool, mode: int, on_origin: bool = False):
     """rank r: cur_r joins the origin, cs_r forks from cur_r, records E_r;
     rank 0's cs waits every E_r and runs the reduction, records d; the other
     ranks' cs wait d; each cur_r joins its cs_r; the origin joins each cur_r."""
@@ -105,17 +109,20 @@ def xrank(threaded: bool, mode: int):
         cs[r].wait_stream(cur[r])
         E[r] = stream.Event().record(cs[r])
 
+    red = origin if on_origin else cs[0]
+
     def part2(r):
         if r == 0:
             for j in range(2):
-                E[j].wait(cs[0])
-            with cs[0]:
+                if on_origin or j:
+                    E[j].wait(red)
+            with red:
                 G.binary("add", xs[0], xs[1], out=xs[0])
                 G.copy_(xs[1], xs[0])
-            box["d"] = stream.Event().record(cs[0])
+            box["d"] = stream.Event().record(red)
 
     def part3(r):
-        if r != 0:
+        if r != 0 or on_origin:
             box["d"].wait(cs[r])
         w = stream.Event().record(cs[r])
         w.wait(cur[r])
