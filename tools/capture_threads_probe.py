@@ -13,6 +13,11 @@ work.
       xrank2   the same with each rank's calls on its own thread
       xorig1   the reduction on the ORIGIN stream instead of rank 0's comm stream (one thread)
       xorig2   the same, threaded
+      multifork  the DistOpt bucket pattern: origin -> comm stream forked once per bucket (3), every
+                 bucket joined back at the end
+      forkjoin   fork -> kernel -> join per bucket (3), sequentially
+      chain      two side streams forked from the origin, the second waiting on the first's event
+      nested     a side stream forked from another side stream, both joined back to the origin
 """
 import os
 import sys
@@ -57,6 +62,8 @@ def main():
 
     if variant.startswith("xrank"):
         return xrank(variant == "xrank2", mode)
+    if variant in ("multifork", "forkjoin", "chain", "nested"):
+        return patterns(variant, mode)
     if variant.startswith("xorig"):
         return xrank(variant == "xorig2", mode, on_origin=True)
     g.begin(s0.handle, mode)
@@ -79,6 +86,74 @@ def main():
     v = float(G.to_numpy(x[:1])[0])
     print(variant, "replayed, x[0] =", v, flush=True)
     assert v == 3.0
+
+
+def patterns(variant: str, mode: int):
+    from singa_amd import memory, stream
+    from singa_amd.ops import glue as G
+    from singa_amd.ops import native as N
+
+    rt = N.lib().rt
+    dev = torch.device("cuda", 0)
+    o = stream.Stream(dev)
+    cs = stream.Stream(dev, priority=-1)
+    s2 = stream.Stream(dev)
+    xs = [memory.empty((4096,), dtype=torch.float32, device=dev) for _ in range(3)]
+    torch.cuda.synchronize()
+    g = rt.Graph()
+    g.begin(o.handle, mode)
+    joins = []
+    if variant in ("multifork", "forkjoin"):
+        for b in range(3):
+            with o:
+                G.fill_(xs[b], 1.0)
+            cs.wait_stream(o)
+            with cs:
+                G.binary("mul", xs[b], 2.0, out=xs[b])
+            ev = stream.Event().record(cs)
+            if variant == "forkjoin":
+                ev.wait(o)
+            else:
+                joins.append(ev)
+        for ev in joins:
+            ev.wait(o)
+        expect = [2.0, 2.0, 2.0]
+    elif variant == "chain":
+        with o:
+            G.fill_(xs[0], 1.0)
+        cs.wait_stream(o)
+        s2.wait_stream(o)
+        with cs:
+            G.fill_(xs[1], 3.0)
+        cs_ev = stream.Event().record(cs)
+        cs_ev.wait(s2)
+        with s2:
+            G.binary("add", xs[1], xs[0], out=xs[2])
+        stream.Event().record(s2).wait(o)
+        stream.Event().record(cs).wait(o)
+        expect = [1.0, 3.0, 4.0]
+    else:  # nested
+        with o:
+            G.fill_(xs[0], 1.0)
+        cs.wait_stream(o)
+        with cs:
+            G.fill_(xs[1], 3.0)
+        s2.wait_stream(cs)
+        with s2:
+            G.binary("add", xs[1], xs[0], out=xs[2])
+        stream.Event().record(s2).wait(o)
+        stream.Event().record(cs).wait(o)
+        expect = [1.0, 3.0, 4.0]
+    g.end()
+    print(variant, "captured nodes", g.nodes, flush=True)
+    for x in xs:
+        G.fill_(x, 0.0)
+    torch.cuda.synchronize()
+    g.replay(o.handle)
+    o.synchronize()
+    v = [float(G.to_numpy(x[:1])[0]) for x in xs]
+    print(variant, "replayed", v, flush=True)
+    assert v == expect, v
 
 
 def xrank(threaded: bool, mode: int, on_origin: bool = False):
