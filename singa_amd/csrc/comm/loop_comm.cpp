@@ -30,15 +30,21 @@
 //
 // Captured mode: when the caller's stream is being captured -- every rank
 // thread capturing its training step into ONE HIP graph (parallel/loop.py
-// WorldGraph) -- nothing can run or be waited for, so an all-reduce becomes
-// graph structure instead: each rank records an event on its stream, group
-// rank 0's stream waits on all of them and runs one device reduction over
-// every rank's buffers (kernels/loopred.hip), and every other rank's stream
-// waits on its completion event.  This is the multi-rank rehearsal of
-// DistOpt's captured step, where each bucket's all-reduce is forked onto the
-// comm stream inside the graph, as on RCCL.  Every HIP call of this path is
-// made with the Python GIL held, which serialises it with the other rank
-// threads' kernel launches into the shared capture.
+// WorldGraph) -- nothing can run or be waited for, so an all-reduce becomes a
+// graph node instead.  The world's ranks all enqueue onto the capture's one
+// origin stream (a rank thread's compute AND comm stream, while it captures),
+// so stream order is the dependency: once every rank has reached the
+// collective (a barrier: all their earlier work is enqueued) group rank 0
+// enqueues one device reduction over every rank's buffers
+// (kernels/loopred.hip), and a second barrier keeps any rank's later work
+// behind it.  (Cross-stream waits between the ranks' side streams were the
+// first design; this HIP runtime's hipStreamEndCapture crashes on a capture in
+// which two non-origin streams wait on each other's events --
+// tools/capture_threads_probe.py xrank1 -- while the real N > 1 pattern, one
+// comm stream forked from and joined to the capture stream once per bucket,
+// captures and replays correctly: tests/test_captured_world_gpu.py.)  Every
+// HIP call of this path is made with the Python GIL held, which serialises it
+// with the other rank threads' launches into the shared capture.
 #include <hip/hip_runtime.h>
 #include <pybind11/pybind11.h>
 #include <stdint.h>
@@ -107,10 +113,6 @@ struct World {
   };
   std::map<std::pair<int, int>, std::deque<std::shared_ptr<Msg>>> boxes;
   std::map<std::tuple<const void*, long, int>, std::shared_ptr<Group>> splits;  // (parent, split seq, color)
-  std::vector<hipEvent_t> events;  // captured-mode fork / join events (graph edges), freed with the world
-  ~World() {
-    for (hipEvent_t e : events) (void)hipEventDestroy(e);
-  }
 
   template <class Pred>
   void wait(std::unique_lock<std::mutex>& lk, Pred pred, const char* what) {
@@ -130,7 +132,6 @@ struct Slot {
   size_t count = 0;
   int dt = 0, op = 0, root = 0, kind = 0;
   long color = 0, key = 0;
-  hipEvent_t ev = nullptr;  // captured mode: this rank's inputs are ready
 };
 
 // the ranks of one communicator (the world or a split of it)
@@ -138,7 +139,7 @@ struct Group {
   Group(std::vector<int> g) : members(std::move(g)), slots(members.size()) {}
   std::vector<int> members;  // global ranks, group order
   std::vector<Slot> slots;
-  hipEvent_t done = nullptr;  // captured mode: the current collective's completion
+
   int arrived = 0;
   long gen = 0;
   long splits = 0;
@@ -312,24 +313,15 @@ class LoopComm {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     return hipStreamIsCapturing((hipStream_t)s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
   }
-  hipEvent_t new_event() {
-    hipEvent_t e = nullptr;
-    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
-      throw std::runtime_error("LoopComm: hipEventCreateWithFlags failed");
-    std::lock_guard<std::mutex> lk(w_->mu);
-    w_->events.push_back(e);
-    return e;
-  }
   void hchk(hipError_t e, const char* what) {
     if (e != hipSuccess) throw std::runtime_error(std::string("LoopComm (captured) ") + what + ": " + hipGetErrorString(e));
   }
   // group barrier with the GIL released (the peers need it to reach theirs)
-  std::vector<Slot> gbarrier(const Slot* mine, const char* what, hipEvent_t* done_out = nullptr) {
+  std::vector<Slot> gbarrier(const Slot* mine, const char* what) {
     py::gil_scoped_release nogil;
     std::unique_lock<std::mutex> lk(w_->mu);
     if (mine) g_->slots[rank_] = *mine;
     g_->barrier(*w_, lk, what);
-    if (done_out) *done_out = g_->done;
     return g_->slots;
   }
   static bool dbg() {
@@ -344,31 +336,25 @@ class LoopComm {
     if (dbg()) fprintf(stderr, "[loop r%d] captured all_reduce count=%zu dt=%d stream=%p\n", rank_, count, dt, (void*)s);
     if (nranks() > 16) throw std::runtime_error("LoopComm (captured): at most 16 ranks");
     Slot me{send, recv, count, dt, op};
-    me.ev = new_event();
-    hchk(hipEventRecord(me.ev, (hipStream_t)s), "hipEventRecord");
-    std::vector<Slot> ps = gbarrier(&me, "all_reduce (captured)");
+    me.kind = 1;
+    me.root = 0;
+    me.key = (long)s;
+    std::vector<Slot> ps = gbarrier(&me, "all_reduce (captured)");  // every rank's earlier work is enqueued
     for (const Slot& p : ps)
-      if (p.count != count || p.dt != dt || p.op != op)
-        throw std::runtime_error("LoopComm all_reduce (captured): ranks disagree on count / dtype / op");
+      if (p.count != count || p.dt != dt || p.op != op || p.key != (long)s)
+        throw std::runtime_error("LoopComm all_reduce (captured): ranks disagree on count / dtype / op / stream "
+                                 "(every rank must capture onto the world's one stream)");
     if (rank_ == 0) {
       std::vector<const void*> sends(ps.size());
       std::vector<void*> recvs(ps.size());
       for (size_t j = 0; j < ps.size(); ++j) {
-        if (j) hchk(hipStreamWaitEvent((hipStream_t)s, ps[j].ev, 0), "hipStreamWaitEvent");
         sends[j] = (const void*)ps[j].send;
         recvs[j] = (void*)ps[j].recv;
       }
       if (sg_loop_allreduce(sends.data(), recvs.data(), (int)ps.size(), (int64_t)count, dt, op, (hipStream_t)s) != 0)
         throw std::runtime_error("LoopComm all_reduce (captured): unsupported dtype / op or launch failure");
-      hipEvent_t d = new_event();
-      hchk(hipEventRecord(d, (hipStream_t)s), "hipEventRecord");
-      std::lock_guard<std::mutex> lk(w_->mu);
-      g_->done = d;
     }
-    hipEvent_t d = nullptr;
-    gbarrier(nullptr, "all_reduce (captured)", &d);
-    if (rank_ != 0) hchk(hipStreamWaitEvent((hipStream_t)s, d, 0), "hipStreamWaitEvent");
-    gbarrier(nullptr, "all_reduce (captured)");  // every rank joined: g_->done may be replaced
+    gbarrier(nullptr, "all_reduce (captured)");  // the reduction is enqueued before any rank's later work
     if (dbg()) fprintf(stderr, "[loop r%d] captured all_reduce done\n", rank_);
   }
   void no_capture(P s, const char* what) {

@@ -197,7 +197,7 @@ class DistOpt:
             G.copy_(g, stg)
             ev = _stream.Event().record(cs)
         from .rccl import Work
-        return Work(ev, (g, stg))
+        return Work(ev, (g, stg), cs.handle)
 
     def _allreduce_all(self):
         if self.world_size == 1:

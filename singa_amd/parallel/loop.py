@@ -49,13 +49,23 @@ class WorldGraph:
     Each rank thread's models get a :meth:`view` (through
     :func:`singa_amd.stream.set_step_graph_factory`) with StepGraph's
     ``capture`` / ``replay`` / ``release``.  ``capture``: all ranks meet,
-    rank 0 begins a capture on the world's origin stream, each rank's current
-    stream joins it through an event and runs its step body (its own private
-    memory pool and work-queue arena), the origin joins every rank's stream
-    and rank 0 ends the capture.  ``replay``: all ranks meet (each one's
-    ``prepare_step`` kernels fenced in with an event), rank 0 launches the
-    graph on the origin stream, and every rank's stream waits for it.  A rank
-    that fails breaks the barrier, so its peers fail instead of waiting."""
+    rank 0 begins a capture on the world's origin stream, and every rank runs
+    its step body with the ORIGIN as its current stream and its
+    communicator's comm stream (its own private memory pool and work-queue
+    arena): stream order then carries every dependency, and a collective is
+    one device reduction enqueued once all ranks have reached it (LoopComm's
+    captured mode).  Rank 0 ends the capture.  ``replay``: all ranks meet
+    (each one's ``prepare_step`` kernels fenced in with an event), rank 0
+    launches the graph on the origin stream, and every rank's stream waits for
+    it.  A rank that fails breaks the barrier, so its peers fail instead of
+    waiting.
+
+    The ranks' work is serialised on one stream inside the graph: this checks
+    the captured step's logic at N ranks (buckets reduced inside the graph,
+    replicas in lock-step), not cross-rank concurrency.  Side streams that
+    wait on each other's events from two rank threads were the first design;
+    this HIP runtime's hipStreamEndCapture crashes on such a capture
+    (tools/capture_threads_probe.py xrank1)."""
 
     def __init__(self, world: int, device: torch.device, timeout_s: float = 120.0):
         self.world = world
@@ -65,6 +75,7 @@ class WorldGraph:
         self.bar = threading.Barrier(world)
         self.origin = _stream.Stream(self.device)
         self._g = N.lib().rt.Graph()
+        self.comms: List[object] = [None] * world  # each rank's communicator (its comm stream swapped during capture)
         self.events: List[object] = [None] * world
         self.done = None
         self.captures = 0
@@ -96,7 +107,6 @@ class _RankGraph:
 
     def capture(self, fn: Callable, *args, **kwargs):
         wg, L = self.wg, N.lib()
-        cur = _stream.current(wg.dev)
         began = False
         try:
             wg._meet()
@@ -105,21 +115,24 @@ class _RankGraph:
                 wg._g.begin(wg.origin.handle, 2)  # relaxed: every rank thread enqueues into this capture
                 began = True
             wg._meet()
-            _dbg("fork")
-            _stream.Event().record(wg.origin).wait(cur)  # this rank's stream joins the capture
-            with self.pool:
-                self._arena = L.workq_arena_begin()
-                try:
-                    _dbg("body")
-                    out = fn(*args, **kwargs)
-                finally:
-                    L.workq_arena_end()
+            comm = wg.comms[self.rank]
+            saved = getattr(comm, "comm_stream", None)
+            if comm is not None:
+                comm.comm_stream = wg.origin
+            try:
+                with wg.origin, self.pool:
+                    self._arena = L.workq_arena_begin()
+                    try:
+                        _dbg("body")
+                        out = fn(*args, **kwargs)
+                    finally:
+                        L.workq_arena_end()
+            finally:
+                if comm is not None:
+                    comm.comm_stream = saved
             _dbg("body done")
-            wg.events[self.rank] = _stream.Event().record(cur)
             wg._meet()
             if self.rank == 0:
-                for ev in wg.events:
-                    ev.wait(wg.origin)  # every rank's work rejoins the origin
                 _dbg("end capture")
                 wg._g.end()
                 _dbg("instantiated", wg._g.nodes)
@@ -203,6 +216,8 @@ def run_ranks(fn: Callable, world: int, *args, device: Optional[torch.device] = 
                     with s:
                         comm = RcclCommunicator(world, r, r, native=native, device=torch.device("cuda", dev))
                         comm.world_graph = wg
+                        if wg is not None:
+                            wg.comms[r] = comm
                         res[r] = fn(r, world, comm, *args)
                     s.synchronize()
                 finally:

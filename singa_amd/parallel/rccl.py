@@ -61,16 +61,18 @@ class _Done:
 class Work:
     """Handle of an asynchronous collective on the comm stream."""
 
-    __slots__ = ("ev", "keep")
+    __slots__ = ("ev", "keep", "stream")
 
-    def __init__(self, ev, keep):
+    def __init__(self, ev, keep, stream: int = 0):
         self.ev = ev
         self.keep = keep  # tensors referenced until the handle is dropped
+        self.stream = stream  # the stream the event was recorded on (0: unknown)
 
     def wait(self) -> None:
         """Stream-ordered: the CURRENT stream waits for the collective (the
         host does not block), like a torch.distributed NCCL work."""
-        self.ev.wait()  # (framework Event: the current stream waits on the device)
+        if not (self.stream and self.stream == _stream.current()):
+            self.ev.wait()  # (framework Event: the current stream waits on the device)
         self.keep = None
 
     def is_completed(self) -> bool:
@@ -150,7 +152,7 @@ class RcclCommunicator(Communicator):
             for t in tensors:  # the caching allocator must not recycle them before the comm stream is done
                 _mem.record_stream(t, cs)
         ev = _stream.Event().record(cs)
-        return Work(ev, tensors)
+        return Work(ev, tensors, cs.handle)
 
     # ---------------------------------------------------------- collectives
     def all_reduce(self, t: torch.Tensor, op: str = "sum", async_op: bool = False):

@@ -58,6 +58,8 @@ class Stream:
 
     def wait_stream(self, other) -> None:
         """This stream waits (device-side) for the work queued so far on ``other``."""
+        if _handle(other) == self.handle:
+            return  # stream order already
         ev = Event()
         ev.record(other)
         ev.wait(self)

@@ -205,3 +205,18 @@ def test_bench_loopback_rehearsal(gpu):
     assert rec["loopback_ranks"] == 2 and rec["config"]["exec"] == "hipgraph"
     assert c["replicas"]["ok"] and c["replicas"]["bitwise_equal"]
     assert c["world_graph"]["captures"] == 1 and c["world_graph"]["replays"] == 4
+
+
+@pytest.mark.parametrize("variant", ["single", "tempev", "launchB", "forkB", "multifork", "forkjoin", "chain",
+                                     "nested"])
+def test_capture_patterns(gpu, variant):
+    """The stream-capture patterns the framework relies on capture and replay
+    correctly on this HIP runtime (tools/capture_threads_probe.py): among them
+    "multifork" -- the N > 1 bench's pattern, one comm stream forked from the
+    capture stream once per gradient bucket and every bucket joined back at
+    the end -- and launches / forks from a second thread (the loopback
+    world's rank threads).  (Two side streams waiting on each other's events,
+    "xrank1", crashes hipStreamEndCapture here and is deliberately not used.)"""
+    from tools.capture_threads_probe import run_variant
+
+    run_variant(variant, 1)

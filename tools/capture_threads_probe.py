@@ -29,12 +29,14 @@ import torch  # noqa: E402
 
 
 def main():
+    run_variant(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 2)
+
+
+def run_variant(variant: str, mode: int = 1):
     from singa_amd import memory, stream
     from singa_amd.ops import glue as G
     from singa_amd.ops import native as N
 
-    variant = sys.argv[1]
-    mode = int(sys.argv[2]) if len(sys.argv) > 2 else 2
     rt = N.lib().rt
     dev = torch.device("cuda", 0)
     s0, s1 = stream.Stream(dev), stream.Stream(dev)
