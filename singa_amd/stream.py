@@ -50,7 +50,7 @@ class Stream:
         self.handle = self._s.handle
         # the carrier through which ``with stream:`` sets the current stream
         self._ext = torch.cuda.ExternalStream(self.handle, device=torch.device("cuda", self.device_index))
-        self._ctx = None
+        self._ctx = __import__("threading").local()  # per-thread stack: threads may enter one stream together
 
     @property
     def cuda_stream(self) -> int:  # duck-typing with torch.cuda.Stream for launch helpers
@@ -71,13 +71,16 @@ class Stream:
         return self._s.query()
 
     def __enter__(self):
-        self._ctx = torch.cuda.stream(self._ext)
-        self._ctx.__enter__()
+        ctx = torch.cuda.stream(self._ext)
+        ctx.__enter__()
+        st = getattr(self._ctx, "stack", None)
+        if st is None:
+            st = self._ctx.stack = []
+        st.append(ctx)
         return self
 
     def __exit__(self, *exc):
-        ctx, self._ctx = self._ctx, None
-        return ctx.__exit__(*exc)
+        return self._ctx.stack.pop().__exit__(*exc)
 
 
 _POOLED: dict = {}
