@@ -239,9 +239,11 @@ def run_rank(args, rank: int, world: int, local: int, comm, loopback: bool = Fal
     exposed = optimizer.exposed_comm_ms() if world > 1 else None
     replicas = None
     if world > 1:
-        t = G.from_numpy(np.array([elapsed, exposed or 0.0], dtype=np.float64), dev.torch_device)
+        t = G.from_numpy(np.array([elapsed, -1.0 if exposed is None else exposed], dtype=np.float64),
+                         dev.torch_device)
         comm.all_reduce(t, op="max")
         elapsed, exposed = (float(v) for v in G.to_numpy(t))
+        exposed = None if exposed < 0 else exposed  # (only measured eagerly: events inside a graph are not timed)
         replicas = replica_guard(comm, optimizer, dev)
         if not replicas["ok"]:
             if rank == 0:
