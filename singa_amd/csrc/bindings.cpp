@@ -156,6 +156,11 @@ void sg_workq_set(int);
 int sg_workq_enabled();
 int sg_cu_count();
 void sg_cu_hog(int, double, int, int*, hipStream_t);
+int sg_fattn_ok(int, int);
+int sg_fattn_fwd(const void*, void*, float*, const float*, int64_t, int, int, int, int, float, hipStream_t);
+int sg_fattn_bwd(const void*, const void*, const void*, const float*, const float*, int64_t, void*, int, int, int, int,
+                 float, hipStream_t);
+int sg_loop_allreduce(const void* const*, void* const*, int, int64_t, int, int, hipStream_t);
 void* sg_workq_arena_begin();
 void sg_workq_arena_end();
 void sg_workq_arena_free(void*);
@@ -417,6 +422,20 @@ PYBIND11_MODULE(_C, m) {
     sg_gemm_heads(CV(a), lda, ako, CV(b), ldb, bko, V(c), ldc, M, N, K, alpha, beta, nullptr, 0, out_mode, 1, batch,
                   sa, sb, sc, bh, sa2, sb2, sc2, S(s));
     CHK("gemm_heads");
+  });
+  // fused multi-head attention over the in-place [B][S][3][H][D] projection (fattn.hip)
+  m.def("fattn_ok", [](int S, int D) { return sg_fattn_ok(S, D); });
+  m.def("fattn_fwd", [](P qkv, P o, P lse, P mask, int64_t mstride, int B, int S, int H, int D, float scale, P s) {
+    const int rc = sg_fattn_fwd(CV(qkv), V(o), (float*)V(lse), (const float*)CV(mask), mstride, B, S, H, D, scale, S(s));
+    if (rc != 0) throw std::runtime_error("fattn_fwd: unsupported shape or launch failure (" + std::to_string(rc) + ")");
+    CHK("fattn_fwd");
+  });
+  m.def("fattn_bwd", [](P qkv, P o, P dout, P lse, P mask, int64_t mstride, P dqkv, int B, int S, int H, int D,
+                        float scale, P s) {
+    const int rc = sg_fattn_bwd(CV(qkv), CV(o), CV(dout), (const float*)CV(lse), (const float*)CV(mask), mstride,
+                                V(dqkv), B, S, H, D, scale, S(s));
+    if (rc != 0) throw std::runtime_error("fattn_bwd: unsupported shape or launch failure (" + std::to_string(rc) + ")");
+    CHK("fattn_bwd");
   });
   m.def("lrn_rows", [](P x, P dy, P out, int64_t R, int C, int size, float alpha, float beta, float k, int bwd, int dt,
                        P s) {

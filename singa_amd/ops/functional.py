@@ -2391,6 +2391,40 @@ def _qkv_native_ok(qkv, H):
     return E % (3 * H) == 0 and (E // (3 * H)) % 8 == 0 and S % 8 == 0
 
 
+class FAttnState:
+    """What the fused attention backward needs from its forward: the per-row
+    log-sum-exp, the output and the key mask (the probabilities are
+    recomputed, never stored)."""
+
+    __slots__ = ("lse", "o", "mask", "mstride")
+
+    def __init__(self, lse, o, mask, mstride):
+        self.lse, self.o, self.mask, self.mstride = lse, o, mask, mstride
+
+
+def _fattn_mask(mask: Optional[torch.Tensor], B: int, S: int):
+    """(mask tensor, batch stride) when ``mask`` is an additive key mask the
+    fused kernel takes ([B or 1, 1, 1, S] or [B or 1, S], fp32, unit key
+    stride, 16-byte aligned rows); (None, 0) for no mask; False otherwise."""
+    if mask is None:
+        return None, 0
+    m = mask
+    if m.dtype != torch.float32 or not m.is_cuda or m.shape[-1] != S or m.stride(-1) != 1:
+        return False
+    if m.dim() == 4 and (m.shape[1] != 1 or m.shape[2] != 1):
+        return False
+    if m.dim() not in (2, 4) or m.shape[0] not in (1, B):
+        return False
+    ms = m.stride(0) if m.shape[0] == B and B > 1 else 0
+    if m.data_ptr() % 16 or (ms * 4) % 16:
+        return False
+    return m, ms
+
+
+def _fattn_on() -> bool:
+    return os.environ.get("SINGA_AMD_FATTN", "1") != "0"
+
+
 def attention_qkv_fwd(qkv: torch.Tensor, heads: int, mask: Optional[torch.Tensor] = None,
                       scale: Optional[float] = None):
     """Multi-head attention straight from the fused projection: qkv [B, S,
@@ -2403,6 +2437,17 @@ def attention_qkv_fwd(qkv: torch.Tensor, heads: int, mask: Optional[torch.Tensor
     D = E // (3 * H)
     HD = H * D
     scale = (1.0 / math.sqrt(D)) if scale is None else scale
+    if _qkv_native_ok(qkv, H) and _fattn_on() and N.lib().fattn_ok(S, D):
+        mk = _fattn_mask(mask, B, S)
+        if mk is not False:
+            # fused kernel (csrc/kernels/fattn.hip): QK^T, softmax and PV per
+            # (batch, head) in registers / LDS; only the row log-sum-exp is kept
+            m, ms = mk
+            o = _mem.empty((B, S, HD), dtype=torch.bfloat16, device=qkv.device)
+            lse = _mem.empty((B * H, S), dtype=torch.float32, device=qkv.device)
+            N.lib().fattn_fwd(qkv.data_ptr(), o.data_ptr(), lse.data_ptr(), N.ptr(m), ms, B, S, H, D, scale,
+                              N.stream())
+            return o, FAttnState(lse, o, m, ms)
     if _qkv_native_ok(qkv, H):
         BH = B * H
         sc = _mem.empty((BH, S, S), dtype=torch.float32, device=qkv.device)
@@ -2431,6 +2476,12 @@ def attention_qkv_bwd(qkv: torch.Tensor, p: torch.Tensor, do: torch.Tensor, head
     D = E // (3 * H)
     HD = H * D
     scale = (1.0 / math.sqrt(D)) if scale is None else scale
+    if isinstance(p, FAttnState):
+        do = G.contiguous(G.to(do, torch.bfloat16))
+        dqkv = _mem.empty_like(qkv)
+        N.lib().fattn_bwd(qkv.data_ptr(), p.o.data_ptr(), do.data_ptr(), p.lse.data_ptr(), N.ptr(p.mask), p.mstride,
+                          dqkv.data_ptr(), B, S, H, D, scale, N.stream())
+        return dqkv
     if _qkv_native_ok(qkv, H) and p.dtype == torch.bfloat16 and do.dtype == torch.bfloat16:
         BH = B * H
         do = G.contiguous(do)

@@ -1,0 +1,10 @@
+#!/bin/bash
+# round 6, call d: fused attention tests + BERT A/B, captured-world tests
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+BB="python bench.py --model bert --steps 30 --warmup 5"
+tools/gpu_step.sh "300 t_fa.log python -u -m pytest tests/test_fattn_gpu.py tests/test_captured_world_gpu.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider" || exit $?
+grep -q "failed" gpurun_out/t_fa.log && exit 1
+tools/gpu_step.sh "200 d_bert_f1.log $BB" "200 d_bert_u1.log SINGA_AMD_FATTN=0 $BB" "200 d_bert_f2.log $BB" "200 d_bert_u2.log SINGA_AMD_FATTN=0 $BB" || exit $?
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/pb -o pb --output-format rocpd -- python3 bench.py --model bert --steps 10 --warmup 3 > gpurun_out/pb.log 2>&1 || exit $?
+python3 tools/prof_summary.py $(find gpurun_out/pb -name '*.db' | head -1) --steps 13 > gpurun_out/bert_kernel_stats_fattn.txt
+rm -rf gpurun_out/pb
