@@ -29,6 +29,7 @@ namespace fa {
 
 constexpr int D = 64;
 constexpr int SMAX = 128;
+constexpr int NW = 8;     // waves per workgroup (one 16-row block each at S = 128)
 constexpr int RS = 144;  // LDS row stride of a [S][64] bf16 image: 128 B + 16 (conflict-free 16-B and tr reads)
 
 struct Args {
@@ -82,8 +83,8 @@ __device__ __forceinline__ f32x4 mfma(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
-// grid B*H, 256 threads; LDS 3 S RS
-__global__ void __launch_bounds__(256) fwd_k(const Args a) {
+// grid B*H, 64 NW threads; LDS 3 S RS
+__global__ void __launch_bounds__(64 * NW) fwd_k(const Args a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int S = a.S, H = a.H;
   const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
@@ -98,7 +99,7 @@ __global__ void __launch_bounds__(256) fwd_k(const Args a) {
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6, g = l >> 4, li = l & 15;
   const int nkb = S / 16;
   const float* mrow = a.mask ? a.mask + (int64_t)b * a.mstride : nullptr;
-  for (int qb = w; qb < nkb; qb += 4) {
+  for (int qb = w; qb < nkb; qb += NW) {
     const int q0 = qb * 16;
     const bf16x8 fq0 = frag_rm(sQ, RS, q0, 0), fq1 = frag_rm(sQ, RS, q0, 32);
     f32x4 s[SMAX / 16];
@@ -161,8 +162,8 @@ __global__ void __launch_bounds__(256) fwd_k(const Args a) {
   }
 }
 
-// grid B*H, 256 threads; LDS 4 S RS + S (2S + 16) + 8 S
-__global__ void __launch_bounds__(256) bwd_k(const Args a) {
+// grid B*H, 64 NW threads; LDS 4 S RS + S (2S + 16) + 8 S
+__global__ void __launch_bounds__(64 * NW) bwd_k(const Args a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int S = a.S, H = a.H;
   const int SS = 2 * S + 16;  // dS image row stride (bytes)
@@ -180,16 +181,16 @@ __global__ void __launch_bounds__(256) bwd_k(const Args a) {
   stage(sV, base + 2 * H * D, a.E, S);
   stage(sO, a.dout + (int64_t)b * S * a.ldo + h * D, a.ldo, S);
   for (int q = threadIdx.x; q < S; q += blockDim.x) sL[q] = a.lse[(int64_t)bh * S + q];
-  // Delta[q] = sum_d dO[q][d] O[q][d] (two threads per row, 32 d each)
+  // Delta[q] = sum_d dO[q][d] O[q][d] (four threads per row, 16 d each)
   {
     const int t = threadIdx.x;
     float acc = 0.f;
-    const int q = t >> 1, hf = t & 1;
+    const int q = t >> 2, hf = t & 3;
     if (q < S) {
-      const bf16* orow = a.out + ((int64_t)b * S + q) * a.ldo + h * D + hf * 32;
-      const bf16* drow = a.dout + ((int64_t)b * S + q) * a.ldo + h * D + hf * 32;
+      const bf16* orow = a.out + ((int64_t)b * S + q) * a.ldo + h * D + hf * 16;
+      const bf16* drow = a.dout + ((int64_t)b * S + q) * a.ldo + h * D + hf * 16;
 #pragma unroll
-      for (int v = 0; v < 4; ++v) {
+      for (int v = 0; v < 2; ++v) {
         const bf16x8 x = *(const bf16x8*)(orow + v * 8);
         const bf16x8 y = *(const bf16x8*)(drow + v * 8);
 #pragma unroll
@@ -197,6 +198,7 @@ __global__ void __launch_bounds__(256) bwd_k(const Args a) {
       }
     }
     acc += __shfl_xor(acc, 1);
+    acc += __shfl_xor(acc, 2);
     if (q < S && hf == 0) sD[q] = acc;
   }
   __syncthreads();
@@ -204,8 +206,8 @@ __global__ void __launch_bounds__(256) bwd_k(const Args a) {
   const int nkb = S / 16;
   const float* mrow = a.mask ? a.mask + (int64_t)b * a.mstride : nullptr;
   const int64_t E = a.E;
-  // phase 1: dK, dV of key blocks kb = w, w + 4, ...; dS into LDS
-  for (int kb = w; kb < nkb; kb += 4) {
+  // phase 1: dK, dV of key blocks kb = w, w + NW, ...; dS into LDS
+  for (int kb = w; kb < nkb; kb += NW) {
     const int k0 = kb * 16;
     const float mk = mrow ? mrow[k0 + li] : 0.f;
     const bf16x8 fk0 = frag_rm(sK, RS, k0, 0), fk1 = frag_rm(sK, RS, k0, 32);
@@ -255,8 +257,8 @@ __global__ void __launch_bounds__(256) bwd_k(const Args a) {
       }
   }
   __syncthreads();  // dS complete
-  // phase 2: dQ of query blocks qb = w, w + 4, ...: dQ = scale dS K
-  for (int qb = w; qb < nkb; qb += 4) {
+  // phase 2: dQ of query blocks qb = w, w + NW, ...: dQ = scale dS K
+  for (int qb = w; qb < nkb; qb += NW) {
     const int q0 = qb * 16;
     f32x4 dq[4];
 #pragma unroll
@@ -299,7 +301,7 @@ extern "C" int sg_fattn_fwd(const void* qkv, void* o, float* lse, const float* m
   a.mstride = mstride;
   a.scale = scale;
   const int lds = 3 * S * sg::fa::RS;
-  hipLaunchKernelGGL(sg::fa::fwd_k, dim3(B * H), dim3(256), lds, s, a);
+  hipLaunchKernelGGL(sg::fa::fwd_k, dim3(B * H), dim3(64 * sg::fa::NW), lds, s, a);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
@@ -324,6 +326,6 @@ extern "C" int sg_fattn_bwd(const void* qkv, const void* o, const void* dout, co
                                          4 * sg::fa::SMAX * sg::fa::RS + sg::fa::SMAX * (2 * sg::fa::SMAX + 16) +
                                              8 * sg::fa::SMAX) == hipSuccess;
   (void)attr;
-  hipLaunchKernelGGL(sg::fa::bwd_k, dim3(B * H), dim3(256), lds, s, a);
+  hipLaunchKernelGGL(sg::fa::bwd_k, dim3(B * H), dim3(64 * sg::fa::NW), lds, s, a);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }

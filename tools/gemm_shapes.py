@@ -36,16 +36,29 @@ def main():
         elif ln.startswith("SG_GEMM_L "):
             launches.append((ln.split()[1], shape))
             shape = None
-    n = min(len(disp), len(launches))
-    mism = sum(1 for i in range(n) if launches[i][0].split("<")[0] not in disp[i][0])
-    print(f"# {len(disp)} GEMM dispatches, {len(launches)} logged launches, {mism} name mismatches in the first {n}")
+    def key_of(name):
+        m = re.search(r"(igemm_k|pp_gemm_k|sk_gemm_k)<([^>]*)>", name)
+        return (m.group(1) + "<" + m.group(2).replace(" ", "") + ">") if m else name
+
+    # greedy in-order alignment: a dispatch takes the next logged launch of the
+    # same kernel instantiation; dispatches launched by unlogged paths are
+    # counted apart
+    pairs, unlogged, j = [], defaultdict(list), 0
+    for name, dur in disp:
+        k = key_of(name)
+        if j < len(launches) and key_of(launches[j][0]) == k:
+            pairs.append((launches[j], dur))
+            j += 1
+        else:
+            unlogged[k].append(dur)
+    print(f"# {len(disp)} GEMM dispatches, {len(launches)} logged launches, {len(pairs)} aligned, "
+          f"{sum(len(v) for v in unlogged.values())} dispatches from unlogged paths")
     agg = defaultdict(list)
-    for i in range(n):
-        kname, sh = launches[i]
+    for (kname, sh), dur in pairs:
         key = (kname,) + ((sh.get("am"), sh.get("bm"), sh.get("M"), sh.get("N"), sh.get("K"), sh.get("smode"),
                             sh.get("stats"), sh.get("res"), sh.get("beta"), sh.get("R"), sh.get("sh"))
                            if sh else ("?",) * 11)
-        agg[key].append(disp[i][1])
+        agg[key].append(dur)
     tot = sum(sum(v) for v in agg.values())
     print(f"# total {tot / 1e6 / a.steps:.3f} ms/step")
     print("#  ms/step calls/st  mean_us   TB/s  TF/s  kernel am bm M N K smode stats res beta R sh")
@@ -60,6 +73,8 @@ def main():
         except (TypeError, ValueError):
             pass
         print(f"{ms:9.3f} {len(v) / a.steps:7.1f} {us:8.1f} {tb:6.2f} {tf:5.0f}  " + " ".join(str(k) for k in key))
+    for k, v in sorted(unlogged.items(), key=lambda kv: -sum(kv[1])):
+        print(f"# unlogged {sum(v) / 1e6 / a.steps:9.3f} ms/step {len(v) / a.steps:7.1f} calls/step  {k}")
 
 
 if __name__ == "__main__":
