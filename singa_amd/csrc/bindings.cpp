@@ -192,6 +192,7 @@ void sg_iadd_i64(void*, int64_t, int64_t, hipStream_t);
 void sg_kth_largest_abs(const void*, int64_t, int64_t, void*, void*, hipStream_t);
 void sg_clamp_affine(const void*, const void*, void*, int64_t, int, float, float, float, float, hipStream_t);
 void sg_set_tuning(int key, int value);
+int sg_get_tuning(int key);
 void sg_bn_set_unroll(int);
 void sg_bn_set_rows_per_thread(int);
 }
@@ -698,6 +699,7 @@ PYBIND11_MODULE(_C, m) {
     sg_clamp_affine(CV(x), CV(dy), V(out), n, dt, a, b, lo, hi, S(s)); CHK("clamp_affine");
   });
   m.def("set_tuning", [](int key, int value) { sg_set_tuning(key, value); });
+  m.def("get_tuning", [](int key) { return sg_get_tuning(key); });
   m.def("bn_set_unroll", [](int ur) { sg_bn_set_unroll(ur); });
   m.def("bn_set_rows_per_thread", [](int rpt) { sg_bn_set_rows_per_thread(rpt); });
 }

@@ -191,6 +191,8 @@ static int make_phases(ConvGeom& g) {
 //         (ResNet-50 b1024 step +0.33 %, three alternating pairs on one box: profiles/r5/ab_wgrad_256x128.jsonl)
 // key 16: 256 x 128 three-stage tiles in place of the 8-wave 128 x 128 ones (1 conv fwd, 2 + dgrad, 3 all)
 // key 17: 1 = 128 x 256 three-stage weight-gradient tiles for K_out < 256 (with key 15)
+// key 18: 1 = the persistent streaming GEMM (st_gemm_k) for the 1x1-conv shapes with K >= 256
+//         (plain bf16 output, optional BN statistics)
 extern "C" int sg_bn_deterministic();  // batchnorm.hip: deterministic-reduction mode
 static int g_tune[20] = {5, 1, 1, 0, 0, 1, 2, 1, 0, 1, 0, 0, 0, 1, 0, 1, 0, 0, 0, 0};
 // one-shot: the next dgrad's wt scratch is already transposed.  Per OS
@@ -288,6 +290,25 @@ static void launch_sk(const GemmArgs& p, int tiles_m, int tiles_n, hipStream_t s
   hipLaunchKernelGGL(kern, dim3(g, tiles_n, 1), dim3(256), lds, s, q);
 }
 
+// persistent streaming launch (st_gemm_k): one workgroup per CU as launch_sk,
+// A and B both streamed through the K-tile ring
+static void launch_st(const GemmArgs& p, int tiles_m, int tiles_n, hipStream_t s) {
+  auto* kern = st_gemm_k<0>;
+  static bool attr = [kern] {
+    return hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, ST_LDS) == hipSuccess;
+  }();
+  (void)attr;
+  const int cus = sg_cu_count();
+  int g = (cus + tiles_n - 1) / tiles_n;
+  g = (g + 7) / 8 * 8;
+  if (g > tiles_m) g = tiles_m >= 8 ? tiles_m / 8 * 8 : 8;
+  GemmArgs q = p;
+  q.wq = 8 * tiles_n <= QMAX ? sg_workq_slot() : nullptr;
+  if (gemm_log())
+    fprintf(stderr, "SG_GEMM_L st_gemm_k<0> grid %d %d 1 M=%d N=%d K=%d\n", g, tiles_n, p.M, p.N, p.K);
+  hipLaunchKernelGGL(kern, dim3(g, tiles_n, 1), dim3(256), ST_LDS, s, q);
+}
+
 // 8-wave (512-thread) tiles.  Returns 0 (the 4-wave v2 tiles) or
 //   1: 128 x 128, waves 2 x 4 of 64 x 32, 2 stages, two workgroups per CU
 //      (measured on ResNet-50 b1024: equal or up to 10 % faster than the
@@ -382,6 +403,15 @@ static void launch(const GemmArgs& p, int M, int splits, hipStream_t s, int batc
         const int tiles_m = (M + 127) / 128;
         if (p.K <= 64) launch_sk<1>(p, tiles_m, p.N / 128, s);
         else launch_sk<2>(p, tiles_m, p.N / 128, s);
+        return;
+      }
+      // persistent streaming kernel (knob 18): the 1x1-conv shapes with longer K
+      if (FLAGS == 0 && OUT == OUT_BF16 && AM == LM_KMAJOR && BMODE == LM_KMAJOR && g_tune[18] && g_tune[4] == 0 &&
+          !p.out_phase && zdim <= 1 && batch == 1 && p.K >= 256 && (p.K & 63) == 0 && (p.N & 127) == 0 &&
+          !p.bias && !p.relu && p.act == 0 && p.act_bwd == 0 && p.alpha == 1.f && p.beta == 0.f &&
+          p.stats_mode == 0 && !(p.stats && p.stats_det) && !p.res_g && g_tune[1] && (p.ldc & 7) == 0 &&
+          (p.lda & 7) == 0 && (p.ldb & 7) == 0 && (long)((M + 127) / 128) * (p.N / 128) >= 2048) {
+        launch_st(p, (M + 127) / 128, p.N / 128, s);
         return;
       }
       // (a strided dgrad's phases each reduce over their own taps only: the
@@ -1016,5 +1046,6 @@ void sg_wt_transpose_batched(const void* desc, int n, int total, hipStream_t s) 
 void sg_set_tuning(int key, int value) {
   if (key >= 0 && key < 20) g_tune[key] = value;
 }
+int sg_get_tuning(int key) { return key >= 0 && key < 20 ? g_tune[key] : 0; }
 
 }  // extern "C"

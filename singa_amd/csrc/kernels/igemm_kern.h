@@ -1383,4 +1383,214 @@ __global__ void __launch_bounds__(256, 1) sk_gemm_k(const GemmArgs p) {
   }
 }
 
+// ------------------------------------------------------------------------------
+// Persistent streaming GEMM for the memory-bound 1x1-conv shapes with longer K
+// (K = 256 .. 2048 in 64-wide K-tiles, K-major A [M][K] and B [N][K], bf16
+// output, optional fused BN statistics).  igemm_k's two workgroups per CU keep
+// ONE K-tile in flight each and stop streaming at every tile's prologue and
+// epilogue: the wide-N shapes (N = 512 .. 2048, two thirds of their bytes are
+// output) ran at 1.3-2.3 TB/s (tools/bench_1x1.py, tools/gemm_shapes.py).  The
+// sk_gemm_k design (one workgroup per CU walking the M-tiles of one 128-column
+// slice, M-tiles from per-(slice, XCD) work queues, statistics in registers,
+// the tile staged through LDS into 16-byte stores that retire behind the next
+// tile's work) cannot keep B resident at these K, so here A and B both stream
+// through a three-stage ring of K-tiles that runs CONTINUOUSLY across tiles:
+// the DMA of the next tile's first two K-tiles is in flight while this tile
+// finishes and writes its output.  Every wave issues the same vector-memory
+// ops per K-tile (DMA; past the last tile from a null resource) and per tile
+// (its stores and one queue op), so each K-tile's wait is a counted vmcnt.
+// ------------------------------------------------------------------------------
+constexpr int ST_STAGE = 2 * SK_TILE;                    // A and B K-tile images (32 KB)
+
+// wq_take without the wait: through the builtin, the atomic optimizer turns
+// the one-lane atomic into a wave scan that needs the returned value at once
+// (s_waitcnt vmcnt(0) right after it -- wave 0 would drain every DMA in flight
+// once per tile).  The result is read only after an explicit counted wait
+// that retires this op (st_gemm_k's wait before the ticket broadcast).
+__device__ __forceinline__ int wq_take_nowait(int* slot, int q) {
+  int v;
+  int* addr = slot + q * QSTRIDE;
+  asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=v"(v) : "v"(addr), "v"(1) : "memory");
+  return v;
+}
+constexpr int ST_LDS = 3 * ST_STAGE + SK_STG;             // ring + output staging (130 KB)
+
+template <int EPI = 0>
+__global__ void __launch_bounds__(256, 1) st_gemm_k(const GemmArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int BM = 128, BN = 128, NTH = 256, WN = 2, WTM = 64, WTN = 64, TM = 4, TN = 4;
+  static_assert(EPI == 0, "plain output with optional BN statistics");
+  bf16* sC = (bf16*)(smem + 3 * ST_STAGE);
+  int* sQ = (int*)(smem + ST_LDS - 16);  // ticket broadcast (the staging image leaves its last 16 B unused)
+  const int M = p.M, N = p.N, K = p.K;
+  const int KT = K / BK;  // >= 2, host-checked (K % 64 == 0)
+  const int tiles_m = (M + BM - 1) / BM;
+  const int n0 = blockIdx.y * BN;
+  // tiles as sk_gemm_k: XCD xcd = bx & 7 owns M-tiles m = xcd + 8 i; this
+  // workgroup's i = j, j + G8, j + 2 G8, then 3 G8 + ticket (queue) or j + k G8
+  const int G = (int)gridDim.x, G8 = G >> 3, xcd = blockIdx.x & 7;
+  const int qid = blockIdx.y * 8 + xcd;
+  int tm = xcd + 8 * (blockIdx.x >> 3);
+  int t1 = tm + 8 * G8, t2 = tm + 16 * G8;
+  const Phase& P = p.g.phs[0];
+  const int l = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  if (tm >= tiles_m) {
+    if (p.wq && threadIdx.x == 0) wq_done(p.wq, 8 * (int)gridDim.y);
+    return;
+  }
+  Loader<BM, LM_KMAJOR, NTH> la, la1;  // this tile's A loader and the next tile's
+  Loader<BN, LM_KMAJOR, NTH> lb;
+  lb.init(p, n0, N, P, p.ldb, p.b, p.b_bytes);
+  la.init(p, tm * BM, M, P, p.lda, p.a, p.a_bytes);
+  la1.init(p, (t1 < tiles_m ? t1 : tm) * BM, M, P, p.lda, p.a, p.a_bytes);
+  constexpr int LPT = Loader<BM, LM_KMAJOR, NTH>::VPT + Loader<BN, LM_KMAJOR, NTH>::VPT;  // DMA ops per K-tile
+  // epilogue geometry: thread owns 8 columns (chunk ch) of rows r0 + RPP * pass
+  constexpr int CPRW = BN / 8, RPP = NTH / CPRW, NPS = BM / RPP;
+  constexpr int E_OPS = NPS + 1;  // per tile: NPS output stores and one queue op
+  static_assert(2 * LPT + E_OPS < 64, "vmcnt range");
+  // DMA of K-tile kt of tile t (live: t in range) into ring stage st
+  auto issue = [&](Loader<BM, LM_KMAJOR, NTH>& a, int t, int kt, int st) {
+    char* base = smem + st * ST_STAGE;
+    const bool live = t < tiles_m;
+    a.issue(p, t * BM, M, kt * BK, K, P, base, live);
+    lb.issue(p, n0, N, kt * BK, K, P, base + SK_TILE, live);
+  };
+  issue(la, tm, 0, 0);
+  issue(la, tm, 1, 1);
+
+  int oa0[TM][2], oa1[TM][2], ob0[TN][2], ob1[TN][2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) la.frag_offsets(wm * WTM + i * 16, kk, oa0[i][kk], oa1[i][kk]);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) lb.frag_offsets(wn * WTN + j * 16, kk, ob0[j][kk], ob1[j][kk]);
+  }
+  const int ch = threadIdx.x % CPRW, r0 = threadIdx.x / CPRW;
+  const int n = n0 + ch * 8;
+  float st_s[8], st_q[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) { st_s[r] = 0.f; st_q[r] = 0.f; }
+  const __amdgpu_buffer_rsrc_t rnull = make_rsrc(nullptr, 0);
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  int ticket = 0;  // wave 0 lane 0: the last queue op's result
+  int stage = 0;   // ring stage of the K-tile being computed
+  for (int it = 0;; ++it) {
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int kt = 0; kt < KT; ++kt) {
+      // K-tile (it, kt) landed: younger are the next K-tile's DMA and, for the
+      // first two K-tiles of a tile after the first, the previous tile's
+      // epilogue ops (stores + queue op) -- issued between those DMAs
+      if (it > 0 && kt < 2) wait_vmcnt<LPT + E_OPS>();
+      else wait_vmcnt<LPT>();
+      raw_barrier();  // ... for every wave; every wave is done reading the stage refilled below
+      {
+        const int fill = stage == 0 ? 2 : stage - 1;  // (stage + 2) % 3
+        if (kt + 2 < KT) issue(la, tm, kt + 2, fill);
+        else issue(la1, t1, kt + 2 - KT, fill);
+      }
+      const char* a_img = smem + stage * ST_STAGE;
+      const char* b_img = a_img + SK_TILE;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8 fa[TM], fb[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) fa[i] = la.frag_at(a_img, oa0[i][kk], oa1[i][kk]);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) fb[j] = lb.frag_at(b_img, ob0[j][kk], ob1[j][kk]);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+      }
+      stage = stage == 2 ? 0 : stage + 1;
+    }
+    // ---- epilogue of tile tm: acc -> bf16 staging
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int ml = wm * WTM + i * 16 + (l & 15);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int nl = wn * WTN + j * 16 + (l >> 4) * 4;
+        bf16x4 o;
+        o[0] = (bf16)acc[i][j][0]; o[1] = (bf16)acc[i][j][1]; o[2] = (bf16)acc[i][j][2]; o[3] = (bf16)acc[i][j][3];
+        *(bf16x4*)(sC + ml * SK_LDT + nl) = o;
+      }
+    }
+    if (it > 0 && wid == 0 && l == 0) {
+      // Q(it-1) -- the ticket of tile it+2 -- retired: only this tile's last
+      // two DMAs (the next tile's first K-tiles) may still be younger
+      wait_vmcnt<2 * LPT>();
+      *sQ = p.wq ? xcd + 8 * (3 * G8 + ticket) : tm + 16 * G8;
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): staging / ticket writes complete before the barrier
+    raw_barrier();  // staging complete; the ticket is in
+    if (it > 0) t2 = __builtin_amdgcn_readfirstlane(*sQ);
+    // Q(it): the ticket of tile it+3 (one op per wave: the others store to a null resource)
+    if (wid == 0 && p.wq) {
+      if (l == 0) ticket = wq_take_nowait(p.wq, qid);
+    } else {
+      __builtin_amdgcn_raw_buffer_store_b32(0u, rnull, 0u, 0, 0);
+    }
+    // staging -> global: 16-byte buffer stores against this tile's row range
+    const int m0 = tm * BM;
+    const int rows = min(BM, M - m0);
+    const __amdgpu_buffer_rsrc_t rc =
+        make_rsrc((const bf16*)p.c + (int64_t)m0 * p.ldc, (unsigned)((int64_t)rows * p.ldc * 2));
+#pragma unroll
+    for (int pass = 0; pass < NPS; ++pass) {
+      const int ml = r0 + pass * RPP;
+      const bf16x8 o = *(const bf16x8*)(sC + ml * SK_LDT + ch * 8);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rc, (unsigned)((ml * (int)p.ldc + n) * 2),
+                                             0, 0);
+      if (p.stats && ml < rows) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const float f = (float)o[r];
+          st_s[r] += f;
+          st_q[r] += f * f;
+        }
+      }
+    }
+    // (the staging image is rewritten only after the next tile's K loop: its
+    // barriers order these reads before those writes)
+    tm = t1;
+    t1 = t2;
+    if (tm >= tiles_m) break;
+    la = la1;
+    la1.init(p, (t1 < tiles_m ? t1 : tm) * BM, M, P, p.lda, p.a, p.a_bytes);
+  }
+  wait_vmcnt<0>();
+  if (p.wq && threadIdx.x == 0) wq_done(p.wq, 8 * (int)gridDim.y);  // every ticket of this workgroup is taken
+  if (p.stats) {
+    // once per workgroup: the RPP row-threads of each 8-column chunk through
+    // LDS, then one atomic per column value into slot row blockIdx.x & 31
+    __syncthreads();
+    float* red = (float*)smem;  // [NTH][16]
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      red[threadIdx.x * 16 + r] = st_s[r];
+      red[threadIdx.x * 16 + 8 + r] = st_q[r];
+    }
+    __syncthreads();
+    if (threadIdx.x < CPRW * 16) {
+      const int c = threadIdx.x >> 4, r = threadIdx.x & 15;
+      const int nn = n0 + c * 8;
+      if (nn < N) {
+        float a = red[c * 16 + r];
+        for (int k = 1; k < RPP; ++k) a += red[(k * CPRW + c) * 16 + r];
+        const int col = r < 8 ? nn + r : N + nn + (r - 8);
+        atomicAdd(p.stats + (int64_t)(blockIdx.x & 31) * 2 * N + col, a);
+      }
+    }
+  }
+}
+
 }  // namespace sg

@@ -29,6 +29,7 @@ POLICIES = {
     "v2_4wave": [(5, 0)],
     "single_stage": [(6, 16)],
     "no_early_issue": [(7, 0)],
+    "stream": [(18, 1)],
 }
 
 
@@ -39,7 +40,7 @@ def main():
     ap.add_argument("--policies", default=",".join(POLICIES))
     a = ap.parse_args()
     L = N.lib()
-    base = {k: L.get_tuning(k) for k in (4, 5, 6, 7, 9, 16)} if hasattr(L, "get_tuning") else None
+    base = {k: L.get_tuning(k) for k in (4, 5, 6, 7, 9, 16, 18)} if hasattr(L, "get_tuning") else None
     recs = []
     for (M, Nn, K) in SHAPES:
         x = (torch.randn(M, K, device="cuda") * 0.1).bfloat16()
