@@ -194,7 +194,7 @@ static int make_phases(ConvGeom& g) {
 // key 18: 1 = the persistent streaming GEMM (st_gemm_k) for the 1x1-conv shapes with K >= 256
 //         (plain bf16 output, optional BN statistics)
 extern "C" int sg_bn_deterministic();  // batchnorm.hip: deterministic-reduction mode
-static int g_tune[20] = {5, 1, 1, 0, 0, 1, 2, 1, 0, 1, 0, 0, 0, 1, 0, 1, 0, 0, 0, 0};
+static int g_tune[20] = {5, 1, 1, 0, 0, 1, 2, 1, 0, 1, 0, 0, 0, 1, 0, 1, 0, 0, 1, 0};
 // one-shot: the next dgrad's wt scratch is already transposed.  Per OS
 // thread: the runtime's executor threads (hogwild / aggregated replicas)
 // each set and consume their own flag, so one thread's set can never be
@@ -405,8 +405,13 @@ static void launch(const GemmArgs& p, int M, int splits, hipStream_t s, int batc
         else launch_sk<2>(p, tiles_m, p.N / 128, s);
         return;
       }
-      // persistent streaming kernel (knob 18): the 1x1-conv shapes with longer K
+      // persistent streaming kernel (knob 18; 1: where it measured faster --
+      // K = 256, and K = 512 with one column slice -- 2: every K >= 256):
+      // tools/bench_1x1.py, profiles/r6/bench_1x1_stream.jsonl: -11..-13 % on
+      // 200704 x 1024 x 256, 802816 x 512 x 256, 3211264 x 128 x 256, -4 % on
+      // 802816 x 128 x 512, +9..+19 % on the K >= 512 wide-N shapes
       if (FLAGS == 0 && OUT == OUT_BF16 && AM == LM_KMAJOR && BMODE == LM_KMAJOR && g_tune[18] && g_tune[4] == 0 &&
+          (g_tune[18] >= 2 || p.K == 256 || (p.K == 512 && p.N == 128)) &&
           !p.out_phase && zdim <= 1 && batch == 1 && p.K >= 256 && (p.K & 63) == 0 && (p.N & 127) == 0 &&
           !p.bias && !p.relu && p.act == 0 && p.act_bwd == 0 && p.alpha == 1.f && p.beta == 0.f &&
           p.stats_mode == 0 && !(p.stats && p.stats_det) && !p.res_g && g_tune[1] && (p.ldc & 7) == 0 &&

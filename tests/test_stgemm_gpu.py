@@ -29,7 +29,7 @@ def test_streaming_gemm_matches_fp32_and_generic(gpu, knob, M, N, K):
     b = (torch.randn(N, K, device=gpu, generator=g) * 0.1).bfloat16()
     knob.set_tuning(18, 0)
     ref_gen = F.gemm_nt(a, b, out_dtype=torch.bfloat16)
-    knob.set_tuning(18, 1)
+    knob.set_tuning(18, 2)
     y = F.gemm_nt(a, b, out_dtype=torch.bfloat16)
     torch.cuda.synchronize()
     ref = a.float() @ b.float().t()
@@ -51,7 +51,7 @@ def test_streaming_conv1x1_bn_stats(gpu, knob, shape):
     w = (torch.randn(k, c, 1, 1, device=gpu, generator=g) * (1.0 / c ** 0.5)).bfloat16()
     res = {}
     for on in (0, 1):
-        knob.set_tuning(18, on)
+        knob.set_tuning(18, 2 * on)
         y = F.conv2d_fwd(x, w, None, (1, 1), (0, 0), bn_stats=True)
         ws, rows = y._sg_bn_ws
         torch.cuda.synchronize()
@@ -70,7 +70,7 @@ def test_streaming_gemm_in_graph_with_generic(gpu, knob):
     from singa_amd.ops import functional as F
     from singa_amd.stream import StepGraph
 
-    knob.set_tuning(18, 1)
+    knob.set_tuning(18, 2)
     g = torch.Generator(device=gpu).manual_seed(3)
     a = (torch.randn(65536, 256, device=gpu, generator=g) * 0.1).bfloat16()
     b = (torch.randn(1024, 256, device=gpu, generator=g) * 0.1).bfloat16()

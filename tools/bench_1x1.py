@@ -29,7 +29,8 @@ POLICIES = {
     "v2_4wave": [(5, 0)],
     "single_stage": [(6, 16)],
     "no_early_issue": [(7, 0)],
-    "stream": [(18, 1)],
+    "stream": [(18, 2)],
+    "generic": [(18, 0)],
 }
 
 
@@ -71,7 +72,7 @@ def main():
                         L.set_tuning(k, v)
                 else:
                     for k, v in POLICIES[pname]:
-                        L.set_tuning(k, {4: 0, 5: 1, 6: 2, 7: 1, 9: 1, 16: 0}[k])
+                        L.set_tuning(k, {4: 0, 5: 1, 6: 2, 7: 1, 9: 1, 16: 0, 18: 1}[k])
             recs.append(rec)
             print(json.dumps(rec), flush=True)
         del x, w, ref
