@@ -123,24 +123,33 @@ def grad_report(m, tm, x, y, xt, yt):
     tr.load_state_dict(state)
     tr.zero_grad()
     nn.functional.cross_entropy(tr(xt.bfloat16().float()), yt).backward()
+    # the fp32 floor: the same fp32 network with its input moved by ONE fp32
+    # ulp (x * (1 + 2^-23)) -- what any change of fp32 summation order does
+    tu = copy.deepcopy(tm)
+    tu.load_state_dict(state)
+    tu.zero_grad()
+    nn.functional.cross_entropy(tu(xt * (1.0 + 2.0 ** -23)), yt).backward()
     tm.load_state_dict(state)  # (the running statistics the forwards moved)
     tp, tq, tz = dict(tm.named_parameters()), dict(tb.named_parameters()), dict(tr.named_parameters())
-    errs, errs_tb, errs_in = {}, {}, {}
+    tw = dict(tu.named_parameters())
+    errs, errs_tb, errs_in, errs_ulp = {}, {}, {}, {}
     zero = []  # parameters whose reference gradient is exactly zero (zero-gamma branches): ours must be too
     rel = lambda u, v: float((u - v).norm() / (v.norm() + 1e-30))  # noqa: E731
     for k, tn in name_map(m).items():
         if k not in ours or tn not in tp:
             continue
         a, b, c, d = ours[k].float(), tp[tn].grad.float(), tq[tn].grad.float(), tz[tn].grad.float()
+        e = tw[tn].grad.float()
         if k == "fc.W":
-            b, c, d = b.t(), c.t(), d.t()
+            b, c, d, e = b.t(), c.t(), d.t(), e.t()
         a = a.reshape(b.shape)
         if float(b.norm()) == 0.0:
             zero.append((k, float(a.norm())))
             continue
-        errs[k], errs_tb[k], errs_in[k] = rel(a, b), rel(c, b), rel(d, b)
+        errs[k], errs_tb[k], errs_in[k], errs_ulp[k] = rel(a, b), rel(c, b), rel(d, b), rel(e, b)
     return {"ours_vs_torch_fp32": _summary(errs), "torch_bf16_autocast_vs_torch_fp32": _summary(errs_tb),
             "torch_fp32_bf16_rounded_input_vs_torch_fp32": _summary(errs_in),
+            "torch_fp32_one_ulp_input_vs_torch_fp32": _summary(errs_ulp),
             "zero_reference_grads": {"n": len(zero), "ours_max_norm": max([z for _, z in zero], default=0.0)}}
 
 
