@@ -89,9 +89,11 @@ def bench_mlp(a, gpu):
     sync = torch.cuda.synchronize if gpu else (lambda: None)
     dt, (_, loss) = _time(lambda: m(x, y), a.steps, a.warmup, sync)
     name = "mlp_gpu" if gpu else "mlp_cpu"
+    host = {"cpus_visible": len(os.sched_getaffinity(0)), "os_cpu_count": os.cpu_count(),
+            "omp_threads": os.environ.get("OMP_NUM_THREADS"), "hostname_is_gpu_box": bool(os.environ.get("GRAFT_REPO_ROOT"))}
     model = "MLP 784-2500-2000-1500-1000-500-10 stanh" if gpu else "MLP 784-512-10 relu"
     return _rec(name, "samples/s", B, dt, model=model, batch=B, device="RocmGPU" if gpu else "CppCPU",
-                dtype="fp32", optimizer="SGD momentum 0.9", final_loss=round(float(_snap(loss.data)), 4))
+                dtype="fp32", optimizer="SGD momentum 0.9", final_loss=round(float(_snap(loss.data)), 4), host=host)
 
 
 def _world():
