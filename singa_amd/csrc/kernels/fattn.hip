@@ -47,13 +47,33 @@ struct Args {
   bf16* dqkv;           // backward: d(qkv), laid out like qkv
 };
 
-// rows [0, S) of a [S][64] bf16 matrix (row stride ld elements) -> LDS image
-__device__ __forceinline__ void stage(char* img, const bf16* __restrict__ src, int64_t ld, int S) {
-  for (int v = threadIdx.x; v < S * 8; v += blockDim.x) {
-    const int r = v >> 3, c = v & 7;
-    const uint4 x = *(const uint4*)(src + r * ld + c * 8);
-    *(uint4*)(img + r * RS + c * 16) = x;
-  }
+// Staging: every thread first issues ALL its 16-byte global loads (vector v
+// of an image = row v >> 3, chunk v & 7; VPI per image at S = SMAX), then
+// writes them to the LDS images -- one global latency per workgroup instead
+// of one per load (a load -> store loop serialises them: the first version
+// spent most of its 15 / 40 us per call there).
+constexpr int VPI = SMAX * 8 / (64 * NW);
+
+template <int NI>
+__device__ __forceinline__ void load_imgs(uint4 (&x)[NI][VPI], const bf16* const (&src)[NI], const int64_t (&ld)[NI],
+                                          int S) {
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int v = 0; v < VPI; ++v) {
+      const int e = threadIdx.x + v * 64 * NW;
+      if (e < S * 8) x[i][v] = *(const uint4*)(src[i] + (e >> 3) * ld[i] + (e & 7) * 8);
+    }
+}
+template <int NI>
+__device__ __forceinline__ void store_imgs(const uint4 (&x)[NI][VPI], char* const (&img)[NI], int S) {
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int v = 0; v < VPI; ++v) {
+      const int e = threadIdx.x + v * 64 * NW;
+      if (e < S * 8) *(uint4*)(img[i] + (e >> 3) * RS + (e & 7) * 16) = x[i][v];
+    }
 }
 
 // row-major fragment: lane (g, i) -> row r0 + i, k = 32 kk + 8 g .. + 7 (A or B operand)
@@ -92,9 +112,14 @@ __global__ void __launch_bounds__(64 * NW) fwd_k(const Args a) {
   char* sK = smem + S * RS;
   char* sV = sK + S * RS;
   const bf16* base = a.qkv + (int64_t)b * S * a.E + h * D;
-  stage(sQ, base, a.E, S);
-  stage(sK, base + H * D, a.E, S);
-  stage(sV, base + 2 * H * D, a.E, S);
+  {
+    uint4 x[3][VPI];
+    const bf16* const src[3] = {base, base + H * D, base + 2 * H * D};
+    const int64_t ld[3] = {a.E, a.E, a.E};
+    char* const img[3] = {sQ, sK, sV};
+    load_imgs<3>(x, src, ld, S);
+    store_imgs<3>(x, img, S);
+  }
   __syncthreads();
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6, g = l >> 4, li = l & 15;
   const int nkb = S / 16;
@@ -176,30 +201,36 @@ __global__ void __launch_bounds__(64 * NW) bwd_k(const Args a) {
   float* sL = (float*)(sdS + S * SS);
   float* sD = sL + S;
   const bf16* base = a.qkv + (int64_t)b * S * a.E + h * D;
-  stage(sQ, base, a.E, S);
-  stage(sK, base + H * D, a.E, S);
-  stage(sV, base + 2 * H * D, a.E, S);
-  stage(sO, a.dout + (int64_t)b * S * a.ldo + h * D, a.ldo, S);
-  for (int q = threadIdx.x; q < S; q += blockDim.x) sL[q] = a.lse[(int64_t)bh * S + q];
-  // Delta[q] = sum_d dO[q][d] O[q][d] (four threads per row, 16 d each)
+  const bf16* dob = a.dout + (int64_t)b * S * a.ldo + h * D;
+  const bf16* ob = a.out + (int64_t)b * S * a.ldo + h * D;
   {
-    const int t = threadIdx.x;
-    float acc = 0.f;
-    const int q = t >> 2, hf = t & 3;
-    if (q < S) {
-      const bf16* orow = a.out + ((int64_t)b * S + q) * a.ldo + h * D + hf * 16;
-      const bf16* drow = a.dout + ((int64_t)b * S + q) * a.ldo + h * D + hf * 16;
+    // Q, K, V, dO and O (O only for Delta[q] = sum_d dO[q][d] O[q][d]): all
+    // loads in flight together
+    uint4 x[5][VPI];
+    const bf16* const src[5] = {base, base + H * D, base + 2 * H * D, dob, ob};
+    const int64_t ld[5] = {a.E, a.E, a.E, a.ldo, a.ldo};
+    load_imgs<5>(x, src, ld, S);
+    float lse = 0.f;
+    if ((int)threadIdx.x < S) lse = a.lse[(int64_t)bh * S + threadIdx.x];
+    char* const img[4] = {sQ, sK, sV, sO};
+    store_imgs<4>(*(const uint4(*)[4][VPI])x, img, S);
+    if ((int)threadIdx.x < S) sL[threadIdx.x] = lse;
+    // this thread's 8-value pieces of dO . O; the 8 threads of a row (chunks
+    // 0-7, consecutive lanes) reduce with xor 1, 2, 4
 #pragma unroll
-      for (int v = 0; v < 2; ++v) {
-        const bf16x8 x = *(const bf16x8*)(orow + v * 8);
-        const bf16x8 y = *(const bf16x8*)(drow + v * 8);
+    for (int v = 0; v < VPI; ++v) {
+      const int e = threadIdx.x + v * 64 * NW;
+      float acc = 0.f;
+      if (e < S * 8) {
+        const bf16x8 p = __builtin_bit_cast(bf16x8, x[3][v]), q = __builtin_bit_cast(bf16x8, x[4][v]);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc += (float)x[j] * (float)y[j];
+        for (int j = 0; j < 8; ++j) acc += (float)p[j] * (float)q[j];
       }
+      acc += __shfl_xor(acc, 1);
+      acc += __shfl_xor(acc, 2);
+      acc += __shfl_xor(acc, 4);
+      if (e < S * 8 && (e & 7) == 0) sD[e >> 3] = acc;
     }
-    acc += __shfl_xor(acc, 1);
-    acc += __shfl_xor(acc, 2);
-    if (q < S && hf == 0) sD[q] = acc;
   }
   __syncthreads();
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6, g = l >> 4, li = l & 15;

@@ -157,6 +157,13 @@ class Graph {
   bool capturing_ = false;
 };
 
+// Framework-owned current stream, per thread and device: set by
+// singa_amd.stream.Stream's context manager, read by every kernel launcher
+// (ops/native.py stream()).  -1 = not set: the launchers then follow the
+// caller's PyTorch current stream (tests that drive work on torch streams).
+constexpr int kMaxDev = 16;
+thread_local intptr_t t_cur[kMaxDev] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+
 }  // namespace
 
 void register_stream_graph(py::module& m) {
@@ -189,6 +196,25 @@ void register_stream_graph(py::module& m) {
     hchk(hipDeviceGetStreamPriorityRange(&lo, &hi), "hipDeviceGetStreamPriorityRange");
     return py::make_tuple(lo, hi);
   });
+  // current stream / device of this thread (framework state, no PyTorch query)
+  sm.def("set_current", [](int device, intptr_t handle) {
+    if (device < 0 || device >= kMaxDev) throw std::runtime_error("rt.set_current: device out of range");
+    const intptr_t old = t_cur[device];
+    t_cur[device] = handle;
+    return old;
+  });
+  // (the device is hipGetDevice's every time, ~50 ns: PyTorch's set_device
+  // and the runtime's own calls change it, so it is never cached)
+  sm.def("current", [](int device) -> intptr_t {
+    if (device < 0 && hipGetDevice(&device) != hipSuccess) return -1;
+    return device < kMaxDev ? t_cur[device] : -1;
+  });
+  sm.def("get_device", []() {
+    int d = 0;
+    hchk(hipGetDevice(&d), "hipGetDevice");
+    return d;
+  });
+  sm.def("set_device", [](int device) { hchk(hipSetDevice(device), "hipSetDevice"); });
   sm.def("device_synchronize", [](int device) {
     int cur = 0;
     hchk(hipGetDevice(&cur), "hipGetDevice");

@@ -57,11 +57,13 @@ _GETD = getattr(torch._C, "_cuda_getDevice", None)
 
 
 def _raw_stream(idx: int) -> int:
-    return _RAWQ(idx) if _RAWQ is not None else torch.cuda.current_stream(idx).cuda_stream
+    from .ops import native as N
+    return N.stream(idx)  # the framework's current stream (native state), else PyTorch's
 
 
 def _getdev() -> int:
-    return _GETD() if _GETD is not None else torch.cuda.current_device()
+    from .ops import native as N
+    return N.device()
 
 
 def _native_on() -> bool:

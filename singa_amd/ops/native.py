@@ -84,9 +84,38 @@ _RAW = getattr(torch._C, "_cuda_getCurrentRawStream", None)
 _GETDEV = getattr(torch._C, "_cuda_getDevice", None)
 
 
+_RT = [None]
+
+
+def _rt():
+    r = _RT[0]
+    if r is None:
+        lb = _load()
+        r = _RT[0] = getattr(lb, "rt", None) if lb is not None else None
+        if r is None:
+            _RT[0] = False
+    return r or None
+
+
+def device() -> int:
+    """This thread's current device (framework state: singa_amd.stream /
+    device.py set it; the first query reads hipGetDevice)."""
+    r = _rt()
+    if r is not None:
+        return r.get_device()
+    return _GETDEV() if _GETDEV is not None else torch.cuda.current_device()
+
+
 def stream(device: int | None = None) -> int:
-    """Handle of this thread's current HIP stream (the raw query: ~0.1 us,
-    against ~3 us for building a torch.cuda.Stream object per launch)."""
+    """Handle of this thread's current HIP stream: the framework stream this
+    thread entered (singa_amd.stream.Stream), read from the native runtime
+    -- no PyTorch call; when none is set, the caller's PyTorch current
+    stream (the raw query: ~0.1 us)."""
+    r = _rt()
+    if r is not None:
+        h = r.current(-1 if device is None else device)
+        if h >= 0:
+            return h
     if _RAW is not None and _GETDEV is not None:
         return _RAW(_GETDEV() if device is None else device)
     return torch.cuda.current_stream(device).cuda_stream

@@ -122,7 +122,7 @@ class DistOpt:
         if st is None:
             raise RuntimeError("DistOpt: parameters not attached (call model.compile first)")
         st.zero_grad()
-        capturing = torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+        capturing = st.g.is_cuda and _stream.is_capturing()
         capturable = getattr(self.comm, "capturable", False)
         if (capturing and not capturable) or not self.overlap or self.world_size == 1:
             for _ in autograd.backward(loss):
@@ -190,7 +190,7 @@ class DistOpt:
             self.comm.all_reduce(stg)
             G.copy_(g, stg)
             return None
-        cs.wait_stream(torch.cuda.current_stream(g.device))
+        cs.wait_stream(_stream.current(g.device.index))
         with cs:
             G.copy_(stg, g)  # fp32 -> bf16 (native copy kernel)
             self.comm.all_reduce(stg)  # on the comm stream (its "current" stream here)

@@ -138,17 +138,17 @@ class RcclCommunicator(Communicator):
         self.stats["bytes"] += sum(t.numel() * t.element_size() for t in ts[:1])
 
     def _cur(self) -> int:
-        return 0 if self.host else torch.cuda.current_stream(self.device).cuda_stream
+        return 0 if self.host else N.stream(self.device.index)
 
     def _run(self, async_op: bool, tensors, fn):
         if not async_op or self.host:
             fn(self._cur())
             return _Done() if async_op else None
-        cur = torch.cuda.current_stream(self.device)
+        cur = N.stream(self.device.index)
         cs = self.comm_stream
         cs.wait_stream(cur)  # the inputs were produced on the current stream
         fn(cs.cuda_stream)
-        if not torch.cuda.is_current_stream_capturing():
+        if not _stream.is_capturing(cur):
             for t in tensors:  # the caching allocator must not recycle them before the comm stream is done
                 _mem.record_stream(t, cs)
         ev = _stream.Event().record(cs)
@@ -237,9 +237,9 @@ class RcclCommunicator(Communicator):
                     comm._c.group_end()
                 finally:
                     keep, comm._group_keep = comm._group_keep, None
-                    if keep and not comm.host and not torch.cuda.is_current_stream_capturing():
+                    if keep and not comm.host and not _stream.is_capturing():
                         for t in keep:  # the group's kernels run on the current stream
-                            _mem.record_stream(t, torch.cuda.current_stream(comm.device))
+                            _mem.record_stream(t, N.stream(comm.device.index))
                 return False
         return _G()
 

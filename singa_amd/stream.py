@@ -42,10 +42,16 @@ def current(device=None) -> int:
     return N.stream(idx)
 
 
+def is_capturing(stream=None) -> bool:
+    """True while ``stream`` (default: this thread's current stream) is being
+    captured into a HIP graph (hipStreamIsCapturing)."""
+    return bool(_rt().is_capturing(_handle(stream)))
+
+
 class Stream:
     def __init__(self, device=None, priority: int = 0):
         idx = torch.device(device).index if device is not None else None
-        self.device_index = idx if idx is not None else torch.cuda.current_device()
+        self.device_index = idx if idx is not None else N.device()
         self._s = _rt().Stream(self.device_index, int(priority))
         self.handle = self._s.handle
         # the carrier through which ``with stream:`` sets the current stream
@@ -71,16 +77,21 @@ class Stream:
         return self._s.query()
 
     def __enter__(self):
+        # the framework's own current stream (read by every launcher, no
+        # PyTorch query), and PyTorch's slot too, for torch ops in tests
+        old = _rt().set_current(self.device_index, self.handle)
         ctx = torch.cuda.stream(self._ext)
         ctx.__enter__()
         st = getattr(self._ctx, "stack", None)
         if st is None:
             st = self._ctx.stack = []
-        st.append(ctx)
+        st.append((ctx, old))
         return self
 
     def __exit__(self, *exc):
-        return self._ctx.stack.pop().__exit__(*exc)
+        ctx, old = self._ctx.stack.pop()
+        _rt().set_current(self.device_index, old)
+        return ctx.__exit__(*exc)
 
 
 _POOLED: dict = {}
