@@ -47,26 +47,25 @@ struct Args {
   bf16* dqkv;           // backward: d(qkv), laid out like qkv
 };
 
-// Staging: every thread first issues ALL its 16-byte global loads (vector v
-// of an image = row v >> 3, chunk v & 7; VPI per image at S = SMAX), then
-// writes them to the LDS images -- one global latency per workgroup instead
-// of one per load (a load -> store loop serialises them: the first version
-// spent most of its 15 / 40 us per call there).
+// Staging of NI [S][64] bf16 matrices into LDS images: every thread issues
+// ALL its 16-byte global loads first (vector e = row e >> 3, chunk e & 7;
+// VPI per image at S = SMAX), then writes them.  The loads are unconditional
+// (rows past S re-read row 0 and are not stored): a load inside a divergent
+// branch gets an s_waitcnt vmcnt(0) at the branch join, which serialised the
+// first version's loads (one global latency each).
 constexpr int VPI = SMAX * 8 / (64 * NW);
 
 template <int NI>
-__device__ __forceinline__ void load_imgs(uint4 (&x)[NI][VPI], const bf16* const (&src)[NI], const int64_t (&ld)[NI],
-                                          int S) {
+__device__ __forceinline__ void stage(char* const (&img)[NI], const bf16* const (&src)[NI],
+                                      const int64_t (&ld)[NI], int S, uint4 (&x)[NI][VPI]) {
 #pragma unroll
   for (int i = 0; i < NI; ++i)
 #pragma unroll
     for (int v = 0; v < VPI; ++v) {
-      const int e = threadIdx.x + v * 64 * NW;
-      if (e < S * 8) x[i][v] = *(const uint4*)(src[i] + (e >> 3) * ld[i] + (e & 7) * 8);
+      int e = threadIdx.x + v * 64 * NW;
+      e = e < S * 8 ? e : 0;
+      x[i][v] = *(const uint4*)(src[i] + (e >> 3) * ld[i] + (e & 7) * 8);
     }
-}
-template <int NI>
-__device__ __forceinline__ void store_imgs(const uint4 (&x)[NI][VPI], char* const (&img)[NI], int S) {
 #pragma unroll
   for (int i = 0; i < NI; ++i)
 #pragma unroll
@@ -112,18 +111,25 @@ __global__ void __launch_bounds__(64 * NW) fwd_k(const Args a) {
   char* sK = smem + S * RS;
   char* sV = sK + S * RS;
   const bf16* base = a.qkv + (int64_t)b * S * a.E + h * D;
-  {
-    uint4 x[3][VPI];
-    const bf16* const src[3] = {base, base + H * D, base + 2 * H * D};
-    const int64_t ld[3] = {a.E, a.E, a.E};
-    char* const img[3] = {sQ, sK, sV};
-    load_imgs<3>(x, src, ld, S);
-    store_imgs<3>(x, img, S);
-  }
-  __syncthreads();
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6, g = l >> 4, li = l & 15;
   const int nkb = S / 16;
   const float* mrow = a.mask ? a.mask + (int64_t)b * a.mstride : nullptr;
+  // this lane's key-mask values (keys kb*16 + 4g + j), loaded with the staging
+  f32x4 mks[SMAX / 16];
+#pragma unroll
+  for (int kb = 0; kb < SMAX / 16; ++kb) mks[kb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (mrow) {
+#pragma unroll
+    for (int kb = 0; kb < SMAX / 16; ++kb) mks[kb] = *(const f32x4*)(mrow + (kb < nkb ? kb : 0) * 16 + 4 * g);
+  }
+  {
+    uint4 x[3][VPI];
+    char* const img[3] = {sQ, sK, sV};
+    const bf16* const src[3] = {base, base + H * D, base + 2 * H * D};
+    const int64_t ld[3] = {a.E, a.E, a.E};
+    stage<3>(img, src, ld, S, x);
+  }
+  __syncthreads();
   for (int qb = w; qb < nkb; qb += NW) {
     const int q0 = qb * 16;
     const bf16x8 fq0 = frag_rm(sQ, RS, q0, 0), fq1 = frag_rm(sQ, RS, q0, 32);
@@ -135,11 +141,9 @@ __global__ void __launch_bounds__(64 * NW) fwd_k(const Args a) {
         f32x4 t = {0.f, 0.f, 0.f, 0.f};
         t = mfma(frag_rm(sK, RS, kb * 16, 0), fq0, t);   // D[key][query]: keys kb*16 + 4g + j, query q0 + li
         t = mfma(frag_rm(sK, RS, kb * 16, 32), fq1, t);
-        f32x4 mk = {0.f, 0.f, 0.f, 0.f};
-        if (mrow) mk = *(const f32x4*)(mrow + kb * 16 + 4 * g);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          t[j] = t[j] * a.scale + mk[j];
+          t[j] = t[j] * a.scale + mks[kb][j];
           mx = fmaxf(mx, t[j]);
         }
         s[kb] = t;
@@ -201,36 +205,39 @@ __global__ void __launch_bounds__(64 * NW) bwd_k(const Args a) {
   float* sL = (float*)(sdS + S * SS);
   float* sD = sL + S;
   const bf16* base = a.qkv + (int64_t)b * S * a.E + h * D;
-  const bf16* dob = a.dout + (int64_t)b * S * a.ldo + h * D;
-  const bf16* ob = a.out + (int64_t)b * S * a.ldo + h * D;
   {
-    // Q, K, V, dO and O (O only for Delta[q] = sum_d dO[q][d] O[q][d]): all
-    // loads in flight together
-    uint4 x[5][VPI];
-    const bf16* const src[5] = {base, base + H * D, base + 2 * H * D, dob, ob};
-    const int64_t ld[5] = {a.E, a.E, a.E, a.ldo, a.ldo};
-    load_imgs<5>(x, src, ld, S);
-    float lse = 0.f;
-    if ((int)threadIdx.x < S) lse = a.lse[(int64_t)bh * S + threadIdx.x];
+    const float lse = a.lse[(int64_t)bh * S + ((int)threadIdx.x < S ? (int)threadIdx.x : 0)];
+    uint4 x[4][VPI];
     char* const img[4] = {sQ, sK, sV, sO};
-    store_imgs<4>(*(const uint4(*)[4][VPI])x, img, S);
+    const bf16* const src[4] = {base, base + H * D, base + 2 * H * D, a.dout + (int64_t)b * S * a.ldo + h * D};
+    const int64_t ld[4] = {a.E, a.E, a.E, a.ldo};
+    stage<4>(img, src, ld, S, x);
     if ((int)threadIdx.x < S) sL[threadIdx.x] = lse;
-    // this thread's 8-value pieces of dO . O; the 8 threads of a row (chunks
-    // 0-7, consecutive lanes) reduce with xor 1, 2, 4
+  }
+  // Delta[q] = sum_d dO[q][d] O[q][d] (four threads per row, 16 d each)
+  {
+    const int t = threadIdx.x;
+    float acc = 0.f;
+    const int q = t >> 2, hf = t & 3;
+    {
+      const int qq = q < S ? q : 0;  // (unconditional loads: no vmcnt(0) per branch join)
+      const bf16* orow = a.out + ((int64_t)b * S + qq) * a.ldo + h * D + hf * 16;
+      const bf16* drow = a.dout + ((int64_t)b * S + qq) * a.ldo + h * D + hf * 16;
+      bf16x8 x[2], y[2];
 #pragma unroll
-    for (int v = 0; v < VPI; ++v) {
-      const int e = threadIdx.x + v * 64 * NW;
-      float acc = 0.f;
-      if (e < S * 8) {
-        const bf16x8 p = __builtin_bit_cast(bf16x8, x[3][v]), q = __builtin_bit_cast(bf16x8, x[4][v]);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc += (float)p[j] * (float)q[j];
+      for (int v = 0; v < 2; ++v) {
+        x[v] = *(const bf16x8*)(orow + v * 8);
+        y[v] = *(const bf16x8*)(drow + v * 8);
       }
-      acc += __shfl_xor(acc, 1);
-      acc += __shfl_xor(acc, 2);
-      acc += __shfl_xor(acc, 4);
-      if (e < S * 8 && (e & 7) == 0) sD[e >> 3] = acc;
+#pragma unroll
+      for (int v = 0; v < 2; ++v)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc += (float)x[v][j] * (float)y[v][j];
+      if (q >= S) acc = 0.f;
     }
+    acc += __shfl_xor(acc, 1);
+    acc += __shfl_xor(acc, 2);
+    if (q < S && hf == 0) sD[q] = acc;
   }
   __syncthreads();
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6, g = l >> 4, li = l & 15;
