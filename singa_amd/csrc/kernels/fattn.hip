@@ -102,6 +102,29 @@ __device__ __forceinline__ f32x4 mfma(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
+// A wave's 16 x 64 output block (MFMA layout: lane (g, i) holds rows 4g + j,
+// column 16 db + i) -> global rows dst + r * ld, through the wave's own LDS
+// scratch (16 rows of OS bytes): 16-byte stores of 8 consecutive columns
+// instead of 2-byte ones.
+constexpr int OS = 64 * 2 + 16;  // scratch row stride (bytes)
+constexpr int WSCR = 16 * OS;    // per-wave scratch
+__device__ __forceinline__ void store_block(char* scr, const f32x4 (&acc)[4], float scale, bf16* dst, int64_t ld) {
+  const int l = threadIdx.x & 63, g = l >> 4, li = l & 15;
+#pragma unroll
+  for (int db = 0; db < 4; ++db)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) *(bf16*)(scr + (4 * g + j) * OS + (db * 16 + li) * 2) = (bf16)(acc[db][j] * scale);
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's scratch writes done
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int v = 0; v < 2; ++v) {
+    const int e = l + 64 * v, r = e >> 3, c = e & 7;
+    *(uint4*)(dst + r * ld + c * 8) = *(const uint4*)(scr + r * OS + c * 16);
+  }
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // reads done before the scratch is reused
+  __builtin_amdgcn_wave_barrier();
+}
+
 // grid B*H, 64 NW threads; LDS 3 S RS
 __global__ void __launch_bounds__(64 * NW) fwd_k(const Args a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -110,8 +133,9 @@ __global__ void __launch_bounds__(64 * NW) fwd_k(const Args a) {
   char* sQ = smem;
   char* sK = smem + S * RS;
   char* sV = sK + S * RS;
-  const bf16* base = a.qkv + (int64_t)b * S * a.E + h * D;
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6, g = l >> 4, li = l & 15;
+  char* scr = sV + S * RS + w * WSCR;
+  const bf16* base = a.qkv + (int64_t)b * S * a.E + h * D;
   const int nkb = S / 16;
   const float* mrow = a.mask ? a.mask + (int64_t)b * a.mstride : nullptr;
   // this lane's key-mask values (keys kb*16 + 4g + j), loaded with the staging
@@ -183,11 +207,7 @@ __global__ void __launch_bounds__(64 * NW) fwd_k(const Args a) {
           o[db] = mfma(pa, frag_tr(sV, 32 * c + 4 * g, 32 * c + 16 + 4 * g, db * 16), o[db]);  // D[query][d]
       }
     }
-    bf16* orow = a.o + ((int64_t)b * S + q0 + 4 * g) * a.ldo + h * D + li;
-#pragma unroll
-    for (int db = 0; db < 4; ++db)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) orow[j * a.ldo + db * 16] = (bf16)o[db][j];
+    store_block(scr, o, 1.f, a.o + ((int64_t)b * S + q0) * a.ldo + h * D, a.ldo);
   }
 }
 
@@ -204,6 +224,7 @@ __global__ void __launch_bounds__(64 * NW) bwd_k(const Args a) {
   char* sdS = sO + S * RS;
   float* sL = (float*)(sdS + S * SS);
   float* sD = sL + S;
+  char* scr_base = (char*)(sD + S);
   const bf16* base = a.qkv + (int64_t)b * S * a.E + h * D;
   {
     const float lse = a.lse[(int64_t)bh * S + ((int)threadIdx.x < S ? (int)threadIdx.x : 0)];
@@ -285,14 +306,9 @@ __global__ void __launch_bounds__(64 * NW) bwd_k(const Args a) {
       }
     }
     // D[key][d]: keys k0 + 4g + j, d = db*16 + li
-    bf16* krow = a.dqkv + ((int64_t)b * S + k0 + 4 * g) * E + H * D + h * D + li;
-#pragma unroll
-    for (int db = 0; db < 4; ++db)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        krow[j * E + db * 16] = (bf16)(dk[db][j] * a.scale);
-        krow[j * E + H * D + db * 16] = (bf16)dv[db][j];
-      }
+    bf16* krow = a.dqkv + ((int64_t)b * S + k0) * E + H * D + h * D;
+    store_block(scr_base + w * WSCR, dk, a.scale, krow, E);
+    store_block(scr_base + w * WSCR, dv, 1.f, krow + H * D, E);
   }
   __syncthreads();  // dS complete
   // phase 2: dQ of query blocks qb = w, w + NW, ...: dQ = scale dS K
@@ -307,11 +323,7 @@ __global__ void __launch_bounds__(64 * NW) bwd_k(const Args a) {
       for (int db = 0; db < 4; ++db)
         dq[db] = mfma(fa, frag_tr(sK, 32 * c + 8 * g, 32 * c + 8 * g + 4, db * 16), dq[db]);
     }
-    bf16* qrow = a.dqkv + ((int64_t)b * S + q0 + 4 * g) * E + h * D + li;
-#pragma unroll
-    for (int db = 0; db < 4; ++db)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) qrow[j * E + db * 16] = (bf16)(dq[db][j] * a.scale);
+    store_block(scr_base + w * WSCR, dq, a.scale, a.dqkv + ((int64_t)b * S + q0) * E + h * D, E);
   }
 }
 
@@ -338,7 +350,7 @@ extern "C" int sg_fattn_fwd(const void* qkv, void* o, float* lse, const float* m
   a.mask = mask;
   a.mstride = mstride;
   a.scale = scale;
-  const int lds = 3 * S * sg::fa::RS;
+  const int lds = 3 * S * sg::fa::RS + sg::fa::NW * sg::fa::WSCR;
   hipLaunchKernelGGL(sg::fa::fwd_k, dim3(B * H), dim3(64 * sg::fa::NW), lds, s, a);
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
@@ -359,10 +371,10 @@ extern "C" int sg_fattn_bwd(const void* qkv, const void* o, const void* dout, co
   a.dout = (const sg::bf16*)dout;
   a.out = (const sg::bf16*)o;
   a.dqkv = (sg::bf16*)dqkv;
-  const int lds = 4 * S * sg::fa::RS + S * (2 * S + 16) + 8 * S;
+  const int lds = 4 * S * sg::fa::RS + S * (2 * S + 16) + 8 * S + sg::fa::NW * sg::fa::WSCR;
   static bool attr = hipFuncSetAttribute((const void*)sg::fa::bwd_k, hipFuncAttributeMaxDynamicSharedMemorySize,
                                          4 * sg::fa::SMAX * sg::fa::RS + sg::fa::SMAX * (2 * sg::fa::SMAX + 16) +
-                                             8 * sg::fa::SMAX) == hipSuccess;
+                                             8 * sg::fa::SMAX + sg::fa::NW * sg::fa::WSCR) == hipSuccess;
   (void)attr;
   hipLaunchKernelGGL(sg::fa::bwd_k, dim3(B * H), dim3(64 * sg::fa::NW), lds, s, a);
   return hipGetLastError() == hipSuccess ? 0 : -3;
