@@ -226,17 +226,10 @@ __global__ void __launch_bounds__(64 * NW) bwd_k(const Args a) {
   float* sD = sL + S;
   char* scr_base = (char*)(sD + S);
   const bf16* base = a.qkv + (int64_t)b * S * a.E + h * D;
-  if (a.scale < 0.f) {  // (never: A/B of the staging order, see below)
-    const float lse = a.lse[(int64_t)bh * S + ((int)threadIdx.x < S ? (int)threadIdx.x : 0)];
-    uint4 x[4][VPI];
-    char* const img[4] = {sQ, sK, sV, sO};
-    const bf16* const src[4] = {base, base + H * D, base + 2 * H * D, a.dout + (int64_t)b * S * a.ldo + h * D};
-    const int64_t ld[4] = {a.E, a.E, a.E, a.ldo};
-    stage<4>(img, src, ld, S, x);
-    if ((int)threadIdx.x < S) sL[threadIdx.x] = lse;
-  } else {
-    // one image at a time (measured faster here than all four loads in flight:
-    // 25.5 vs 31-33 us per BERT-base layer)
+  {
+    // one image at a time: measured faster here than stage() with all four
+    // images' loads in flight (25.7 vs 31-33 us per BERT-base layer,
+    // profiles/r6/attention_staging_ab.txt) -- unlike the forward (9.7 vs 15 us)
     const bf16* const srcs[4] = {base, base + H * D, base + 2 * H * D, a.dout + (int64_t)b * S * a.ldo + h * D};
     char* const imgs[4] = {sQ, sK, sV, sO};
     const int64_t lds_[4] = {a.E, a.E, a.E, a.ldo};
