@@ -55,6 +55,37 @@ def _load():
     return _lib
 
 
+class _TracedLib:
+    """SG_LAUNCH_TRACE=1: counts every binding call by (name, call site) --
+    which Python lines launch the step's small kernels (tools/launch_sites.py)."""
+
+    def __init__(self, m):
+        import collections
+        self._m = m
+        self.counts = collections.Counter()
+        self.enabled = False
+
+    def __getattr__(self, k):
+        v = getattr(self._m, k)
+        if not callable(v) or not self.enabled or k in ("rt", "mem"):
+            return v
+        import sys
+
+        f = sys._getframe(1)
+        site = f"{f.f_code.co_filename.split('singa_amd/')[-1]}:{f.f_lineno}"
+        f2 = f.f_back
+        if f2 is not None:
+            site += f" <- {f2.f_code.co_filename.split('singa_amd/')[-1]}:{f2.f_lineno}"
+
+        def call(*a, **kw):
+            self.counts[(k, site)] += 1
+            return v(*a, **kw)
+        return call
+
+
+_TRACED = [None]
+
+
 def lib():
     """Return the loaded ``_C`` module or raise a descriptive error."""
     m = _load()
@@ -62,6 +93,10 @@ def lib():
         raise RuntimeError(
             "singa_amd native kernel library (_C) is not built or failed to load: "
             f"{_err!r}. Run `python -m singa_amd.build_ext`.")
+    if os.environ.get("SG_LAUNCH_TRACE") == "1":
+        if _TRACED[0] is None:
+            _TRACED[0] = _TracedLib(m)
+        return _TRACED[0]
     return m
 
 
