@@ -14,8 +14,9 @@ gfx950 kernels through :mod:`singa_amd.ops.functional`.  Parameters that live
 in a flat :class:`singa_amd.opt.ParamStore` carry an fp32 ``grad_view``; the
 conv/linear/BN backward kernels accumulate straight into it (no per-param
 gradient tensors, one fused optimiser launch afterwards).  Non-hot "glue"
-operators (shape manipulation, ONNX odds and ends) are expressed through
-:class:`TorchFn`, which differentiates a small PyTorch function locally.
+operators (shape manipulation, ONNX odds and ends) are :class:`Fn` operators
+whose forward and backward are explicit functions over native glue kernels
+(views: their inverse view) -- the tape is the only autograd engine.
 """
 from __future__ import annotations
 
@@ -1505,43 +1506,6 @@ def attention(q, k, v, mask=None, scale=None):
     return Attention(scale)(q, k, v, mask) if mask is not None else Attention(scale)(q, k, v)
 
 
-class TorchFn(Operator):
-    """Generic differentiable op defined by a PyTorch function of the raw
-    inputs (used for shape/glue ops that need no hand-written kernel)."""
-
-    def __init__(self, fn: Callable, name=None, nondiff: Sequence[int] = (), onnx: Optional[dict] = None):
-        super().__init__(name)
-        self.fn = fn
-        self.nondiff = set(nondiff)
-        # export spec for sonnx: {"op": type, "attrs": {...}, "inputs": [("in", i) | ("const", array)]}
-        self.onnx = onnx
-
-    def forward(self, *xs):
-        if not self.requires_grad:
-            with torch.no_grad():
-                return self.fn(*xs)
-        with torch.enable_grad():
-            self.inp = [x.detach().requires_grad_(True) if (x.is_floating_point() and i not in self.nondiff)
-                        else x.detach() for i, x in enumerate(xs)]
-            out = self.fn(*self.inp)
-        self.out = out
-        outs = out if isinstance(out, tuple) else (out,)
-        return tuple(o.detach() for o in outs) if isinstance(out, tuple) else out.detach()
-
-    def backward(self, *dys):
-        outs = self.out if isinstance(self.out, tuple) else (self.out,)
-        pairs = [(o, d) for o, d in zip(outs, dys) if d is not None and o.requires_grad]
-        req = [x for x in self.inp if x.requires_grad]
-        if not pairs or not req:
-            return tuple(None for _ in self.inp)
-        gs = torch.autograd.grad([o for o, _ in pairs], req, [d.to(o.dtype) for o, d in pairs],
-                                 allow_unused=True)
-        it = iter(gs)
-        res = tuple(next(it) if x.requires_grad else None for x in self.inp)
-        self.inp = self.out = None
-        return res
-
-
 # ===========================================================================
 # functional API (singa.autograd.xxx)
 # ===========================================================================
@@ -1724,10 +1688,6 @@ class Fn(Operator):
         r = _as_tuple(self.bwd(self.ctx, *dys))
         self.ctx = None
         return r
-
-
-def _fn(fn, *xs, nondiff=(), onnx=None):
-    return TorchFn(fn, nondiff=nondiff, onnx=onnx)(*xs)
 
 
 def _ox(op, attrs=None, inputs=None, n_in=1):

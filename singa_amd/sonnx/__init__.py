@@ -441,11 +441,11 @@ def _x_cls(c, op, xs, i, o):
     c.add("Gather", [i[0], c.const(np.asarray(0, np.int64))], [o[0]], axis=1)
 
 
-@exporter("TorchFn")
-def _x_torchfn(c, op, xs, i, o):
+def _x_spec(c, op, xs, i, o):
+    """Glue operators (autograd.Fn / _Math) carry their ONNX spec."""
     spec = getattr(op, "onnx", None)
     if spec is None:
-        raise NotImplementedError("sonnx: a generic TorchFn op has no ONNX lowering")
+        raise NotImplementedError(f"sonnx: operator {type(op).__name__} has no ONNX lowering")
     ins = []
     for kind, v in spec["inputs"]:
         ins.append(i[v] if kind == "in" else c.const(np.asarray(v)))
@@ -496,7 +496,7 @@ def to_onnx(m, inputs: Sequence[Tensor], outputs: Optional[Sequence[Tensor]] = N
             o.append(n)
         fn = _EXPORTERS.get(type(op).__name__)
         if fn is None and getattr(op, "onnx", None) is not None:
-            fn = _x_torchfn  # glue operators (autograd.Fn / _Math) carry their ONNX spec
+            fn = _x_spec  # glue operators (autograd.Fn / _Math) carry their ONNX spec
         if fn is None:
             raise NotImplementedError(f"sonnx export: no ONNX lowering for operator {type(op).__name__}")
         fn(c, op, xs, i, o)
