@@ -681,6 +681,7 @@ class Linear(Operator):
         self.y2 = None  # the activation output (y-form derivatives) ...
         self.z2 = None  # ... or its input (GELU), written by the forward epilogue
         self.preact_done = False
+        self.db_done = False  # a consumer (DropAddLayerNorm) already summed the bias gradient into its view
 
     def forward(self, x, W, b=None):
         w = self._w_compute(x, W)
@@ -745,9 +746,10 @@ class Linear(Operator):
         tb = self.grad_target(2) if self.has_bias else None
         # dy's column sums already summed by its producer (DropAddLayerNorm's backward)
         cs_pre = getattr(dy, "_sg_colsum", None) if self.act is None else None
+        db_done, self.db_done = self.db_done and tb is not None, False
         # the bias gradient (column sums of dy) rides along with the weight
         # gradient GEMM, which stages every dy tile anyway
-        fuse_db = tb is not None and tgt is not None and tb.is_contiguous() and cs_pre is None
+        fuse_db = tb is not None and tgt is not None and tb.is_contiguous() and cs_pre is None and not db_done
         if tgt is not None:
             wid = id(self.params[1])
             # first (and sole) writer of this epoch's weight gradient: write
@@ -769,7 +771,9 @@ class Linear(Operator):
             dw = F.gemm(x2, dy2, ta=True, out_dtype=torch.float32)
         res = [dx, dw]
         if self.has_bias:
-            if cs_pre is not None and tb is not None:
+            if db_done:
+                db = ACCUMULATED
+            elif cs_pre is not None and tb is not None:
                 G.binary("add", tb, G.reshape(cs_pre, tb.shape), out=tb)
                 db = ACCUMULATED
             elif cs_pre is not None:
@@ -1335,6 +1339,8 @@ class DropAddLayerNorm(Operator):
     producing Linear as its bias gradient (``da._sg_colsum``: no separate
     column-sum pass over da)."""
 
+    wants_sole = True  # (the producing Linear's bias gradient is summed here when this op is a's only consumer)
+
     def __init__(self, ratio: float, seed_source, eps: float, name=None):
         super().__init__(name)
         self.ratio, self.seed_source, self.eps = ratio, seed_source, eps
@@ -1351,12 +1357,22 @@ class DropAddLayerNorm(Operator):
             self.saved = (s, g, mean, rstd, mask, ratio)
         return y
 
+    def _producer_bias(self):
+        return producer_bias(self, 1)
+
     def backward(self, dy):
         s, g, mean, rstd, mask, ratio = self.saved
         self.saved = None
         tg, tb = self.grad_target(2), self.grad_target(3)
-        ds, da, dg, db, cs = F.drop_add_layernorm_bwd(s, dy, g, mean, rstd, mask, ratio, dg_acc=tg, db_acc=tb)
-        da._sg_colsum = cs
+        prod, cs_to = self._producer_bias()
+        if cs_to is not None and cs_to.numel() != s.shape[-1]:
+            prod = cs_to = None
+        ds, da, dg, db, cs = F.drop_add_layernorm_bwd(s, dy, g, mean, rstd, mask, ratio, dg_acc=tg, db_acc=tb,
+                                                      cs_acc=cs_to)
+        if prod is not None:
+            prod.db_done = True  # da's column sums went straight into the producer's bias gradient
+        else:
+            da._sg_colsum = cs
         acc = lambda tgt, v: ACCUMULATED if tgt is not None else v  # noqa: E731
         return ds, da, acc(tg, dg), acc(tb, db)
 
@@ -1479,11 +1495,31 @@ class Attention(Operator):
         return (dq, dk, dv) + ((None,) if len(self.src) == 4 else ())
 
 
+BIAS_INPLACE = os.environ.get("SINGA_AMD_BIAS_INPLACE", "1") != "0"  # (A/B switch)
+
+
+def producer_bias(op: Operator, i: int):
+    """(Linear, its fp32 bias-gradient view) when input i of ``op`` is the
+    output of a plain Linear (bias, no fused activation) whose gradient comes
+    from ``op`` alone: ``op``'s backward may then sum that gradient's columns
+    straight into the bias gradient (and set ``Linear.db_done``), else
+    (None, None)."""
+    src = op.src[i][0] if len(op.src) > i and BIAS_INPLACE else None
+    if not (isinstance(src, Linear) and src.has_bias and src.act is None
+            and (getattr(op, "sole", None) or {}).get(i, False)):
+        return None, None
+    tb = src.grad_target(2)
+    ok = tb is not None and tb.is_cuda and tb.dtype == torch.float32 and tb.is_contiguous()
+    return (src, tb) if ok else (None, None)
+
+
 class QKVAttention(Operator):
     """Multi-head attention fed by the fused q/k/v projection: qkv [B, S,
     3*H*D] -> [B, S, H*D].  Equivalent to split-heads -> Attention ->
     merge-heads, but the batched MFMA GEMMs address each head in place
     (functional.attention_qkv_*), so neither direction copies the heads."""
+
+    wants_sole = True  # (the fused backward sums the q/k/v projection's bias gradient when qkv has no other consumer)
 
     def __init__(self, heads: int, scale: Optional[float] = None, name=None):
         super().__init__(name)
@@ -1498,8 +1534,16 @@ class QKVAttention(Operator):
     def backward(self, do):
         qkv, p = self.saved
         self.saved = None
-        dqkv = F.attention_qkv_bwd(qkv, p, do, self.heads, self.scale)
+        prod, db = self._producer_bias()
+        if not F.fattn_bias_ok(p, db, qkv.shape[-1]):
+            prod = db = None
+        dqkv = F.attention_qkv_bwd(qkv, p, do, self.heads, self.scale, db_acc=db)
+        if prod is not None:
+            prod.db_done = True  # d(qkv)'s column sums went straight into the projection's bias gradient
         return (dqkv, None) if len(self.src) == 2 else dqkv
+
+    def _producer_bias(self):
+        return producer_bias(self, 0)
 
 
 def attention(q, k, v, mask=None, scale=None):

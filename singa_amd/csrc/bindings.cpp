@@ -158,8 +158,8 @@ int sg_cu_count();
 void sg_cu_hog(int, double, int, int*, hipStream_t);
 int sg_fattn_ok(int, int);
 int sg_fattn_fwd(const void*, void*, float*, const float*, int64_t, int, int, int, int, float, hipStream_t);
-int sg_fattn_bwd(const void*, const void*, const void*, const float*, const float*, int64_t, void*, int, int, int, int,
-                 float, hipStream_t);
+int sg_fattn_bwd(const void*, const void*, const void*, const float*, const float*, int64_t, void*, float*, int, int,
+                 int, int, float, hipStream_t);
 int sg_loop_allreduce(const void* const*, void* const*, int, int64_t, int, int, hipStream_t);
 void* sg_workq_arena_begin();
 void sg_workq_arena_end();
@@ -431,10 +431,10 @@ PYBIND11_MODULE(_C, m) {
     if (rc != 0) throw std::runtime_error("fattn_fwd: unsupported shape or launch failure (" + std::to_string(rc) + ")");
     CHK("fattn_fwd");
   });
-  m.def("fattn_bwd", [](P qkv, P o, P dout, P lse, P mask, int64_t mstride, P dqkv, int B, int S, int H, int D,
-                        float scale, P s) {
+  m.def("fattn_bwd", [](P qkv, P o, P dout, P lse, P mask, int64_t mstride, P dqkv, P dbias, int B, int S, int H,
+                        int D, float scale, P s) {
     const int rc = sg_fattn_bwd(CV(qkv), CV(o), CV(dout), (const float*)CV(lse), (const float*)CV(mask), mstride,
-                                V(dqkv), B, S, H, D, scale, S(s));
+                                V(dqkv), (float*)V(dbias), B, S, H, D, scale, S(s));
     if (rc != 0) throw std::runtime_error("fattn_bwd: unsupported shape or launch failure (" + std::to_string(rc) + ")");
     CHK("fattn_bwd");
   });

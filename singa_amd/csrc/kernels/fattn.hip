@@ -6,7 +6,8 @@
 // attention_qkv_fwd: two batched GEMMs + softmax) never exist.  The forward
 // keeps only the per-row log-sum-exp; the backward recomputes P from it
 // (flash-attention style) and writes dQ / dK / dV straight into their slots of
-// d(qkv).
+// d(qkv), optionally summing their columns into the q/k/v projection's bias
+// gradient on the way (no separate column-sum pass over d(qkv)).
 //
 // Shapes: D = 64, S <= 128, S % 32 == 0 (host-checked; anything else takes
 // the unfused path).  Additive key mask (BERT's [B][1][1][S] padding mask) or
@@ -45,6 +46,8 @@ struct Args {
   const bf16* dout;     // backward: dO, laid out like o
   const bf16* out;      // backward: the forward output O
   bf16* dqkv;           // backward: d(qkv), laid out like qkv
+  float* dbias;         // backward: += column sums of d(qkv) over all B S rows (the q/k/v projection's bias
+                        // gradient, fp32 [3][H][D]), or null
 };
 
 // Staging of NI [S][64] bf16 matrices into LDS images: every thread issues
@@ -123,6 +126,16 @@ __device__ __forceinline__ void store_block(char* scr, const f32x4 (&acc)[4], fl
   }
   __builtin_amdgcn_s_waitcnt(0xC07F);  // reads done before the scratch is reused
   __builtin_amdgcn_wave_barrier();
+}
+
+// column sums of a wave's stored 16 x 64 block (the bf16 values store_block
+// writes) into per-lane partials: lane (g, i) adds its rows 4g..4g+3 of
+// column 16 db + i
+__device__ __forceinline__ void colsum_block(const f32x4 (&acc)[4], float scale, float (&cs)[4]) {
+#pragma unroll
+  for (int db = 0; db < 4; ++db)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) cs[db] += (float)(bf16)(acc[db][j] * scale);
 }
 
 // grid B*H, 64 NW threads; LDS 3 S RS
@@ -211,7 +224,7 @@ __global__ void __launch_bounds__(64 * NW) fwd_k(const Args a) {
   }
 }
 
-// grid B*H, 64 NW threads; LDS 4 S RS + S (2S + 16) + 8 S
+// grid B*H, 64 NW threads; LDS 4 S RS + S (2S + 16) + 8 S + NW WSCR (+ 3 * 64 floats with dbias)
 __global__ void __launch_bounds__(64 * NW) bwd_k(const Args a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int S = a.S, H = a.H;
@@ -225,7 +238,9 @@ __global__ void __launch_bounds__(64 * NW) bwd_k(const Args a) {
   float* sL = (float*)(sdS + S * SS);
   float* sD = sL + S;
   char* scr_base = (char*)(sD + S);
+  float* sCS = (float*)(scr_base + NW * WSCR);  // [q, k, v][64] column sums of this (b, h)
   const bf16* base = a.qkv + (int64_t)b * S * a.E + h * D;
+  if (a.dbias && threadIdx.x < 3 * D) sCS[threadIdx.x] = 0.f;
   {
     // one image at a time: measured faster here than stage() with all four
     // images' loads in flight (25.7 vs 31-33 us per BERT-base layer,
@@ -270,6 +285,7 @@ __global__ void __launch_bounds__(64 * NW) bwd_k(const Args a) {
   const int nkb = S / 16;
   const float* mrow = a.mask ? a.mask + (int64_t)b * a.mstride : nullptr;
   const int64_t E = a.E;
+  float csq[4] = {0.f, 0.f, 0.f, 0.f}, csk[4] = {0.f, 0.f, 0.f, 0.f}, csv[4] = {0.f, 0.f, 0.f, 0.f};
   // phase 1: dK, dV of key blocks kb = w, w + NW, ...; dS into LDS
   for (int kb = w; kb < nkb; kb += NW) {
     const int k0 = kb * 16;
@@ -314,6 +330,10 @@ __global__ void __launch_bounds__(64 * NW) bwd_k(const Args a) {
     bf16* krow = a.dqkv + ((int64_t)b * S + k0) * E + H * D + h * D;
     store_block(scr_base + w * WSCR, dk, a.scale, krow, E);
     store_block(scr_base + w * WSCR, dv, 1.f, krow + H * D, E);
+    if (a.dbias) {
+      colsum_block(dk, a.scale, csk);
+      colsum_block(dv, 1.f, csv);
+    }
   }
   __syncthreads();  // dS complete
   // phase 2: dQ of query blocks qb = w, w + NW, ...: dQ = scale dS K
@@ -329,6 +349,33 @@ __global__ void __launch_bounds__(64 * NW) bwd_k(const Args a) {
         dq[db] = mfma(fa, frag_tr(sK, 32 * c + 8 * g, 32 * c + 8 * g + 4, db * 16), dq[db]);
     }
     store_block(scr_base + w * WSCR, dq, a.scale, a.dqkv + ((int64_t)b * S + q0) * E + h * D, E);
+    if (a.dbias) colsum_block(dq, a.scale, csq);
+  }
+  if (a.dbias) {  // (uniform branch)
+    // lane groups g = 0..3 hold different rows of the same columns: fold
+    // them, then the waves through LDS, then one global atomic per column
+#pragma unroll
+    for (int db = 0; db < 4; ++db) {
+      csq[db] += __shfl_xor(csq[db], 16);
+      csq[db] += __shfl_xor(csq[db], 32);
+      csk[db] += __shfl_xor(csk[db], 16);
+      csk[db] += __shfl_xor(csk[db], 32);
+      csv[db] += __shfl_xor(csv[db], 16);
+      csv[db] += __shfl_xor(csv[db], 32);
+    }
+    if (g == 0) {
+#pragma unroll
+      for (int db = 0; db < 4; ++db) {
+        atomicAdd(sCS + db * 16 + li, csq[db]);
+        atomicAdd(sCS + D + db * 16 + li, csk[db]);
+        atomicAdd(sCS + 2 * D + db * 16 + li, csv[db]);
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x < 3 * D) {
+      const int part = threadIdx.x / D, c = threadIdx.x - part * D;
+      atomicAdd(a.dbias + (int64_t)part * H * D + h * D + c, sCS[threadIdx.x]);
+    }
   }
 }
 
@@ -361,7 +408,8 @@ extern "C" int sg_fattn_fwd(const void* qkv, void* o, float* lse, const float* m
 }
 
 extern "C" int sg_fattn_bwd(const void* qkv, const void* o, const void* dout, const float* lse, const float* mask,
-                            int64_t mstride, void* dqkv, int B, int S, int H, int D, float scale, hipStream_t s) {
+                            int64_t mstride, void* dqkv, float* dbias, int B, int S, int H, int D, float scale,
+                            hipStream_t s) {
   if (!fattn_ok(S, D) || B <= 0 || H <= 0) return -1;
   Args a{};
   a.qkv = (const sg::bf16*)qkv;
@@ -376,10 +424,12 @@ extern "C" int sg_fattn_bwd(const void* qkv, const void* o, const void* dout, co
   a.dout = (const sg::bf16*)dout;
   a.out = (const sg::bf16*)o;
   a.dqkv = (sg::bf16*)dqkv;
-  const int lds = 4 * S * sg::fa::RS + S * (2 * S + 16) + 8 * S + sg::fa::NW * sg::fa::WSCR;
+  a.dbias = dbias;
+  const int cs = 3 * sg::fa::D * (int)sizeof(float);
+  const int lds = 4 * S * sg::fa::RS + S * (2 * S + 16) + 8 * S + sg::fa::NW * sg::fa::WSCR + (dbias ? cs : 0);
   static bool attr = hipFuncSetAttribute((const void*)sg::fa::bwd_k, hipFuncAttributeMaxDynamicSharedMemorySize,
                                          4 * sg::fa::SMAX * sg::fa::RS + sg::fa::SMAX * (2 * sg::fa::SMAX + 16) +
-                                             8 * sg::fa::SMAX + sg::fa::NW * sg::fa::WSCR) == hipSuccess;
+                                             8 * sg::fa::SMAX + sg::fa::NW * sg::fa::WSCR + cs) == hipSuccess;
   (void)attr;
   hipLaunchKernelGGL(sg::fa::bwd_k, dim3(B * H), dim3(64 * sg::fa::NW), lds, s, a);
   return hipGetLastError() == hipSuccess ? 0 : -3;

@@ -495,11 +495,12 @@ def drop_add_layernorm_fwd(x, a, g, b, eps: float, ratio: float, seed: int = 0, 
     return y, s, mask, mean, rstd
 
 
-def drop_add_layernorm_bwd(s, dy, g, mean, rstd, mask, ratio: float, dg_acc=None, db_acc=None):
+def drop_add_layernorm_bwd(s, dy, g, mean, rstd, mask, ratio: float, dg_acc=None, db_acc=None, cs_acc=None):
     """Backward of drop_add_layernorm_fwd in one pass: (ds, da, dg, db, cs) --
     ds the gradient of x (and of s), da = ds * mask / (1 - ratio) that of a,
     cs the column sums of da (fp32 [D]: the bias gradient of the Linear that
-    produced a); dg / db accumulate into the *_acc views when given."""
+    produced a); dg / db / cs accumulate into the *_acc views when given
+    (``cs_acc``: that Linear's bias-gradient view itself)."""
     D = s.shape[-1]
     R = s.numel() // D
     L = N.lib()
@@ -511,7 +512,7 @@ def drop_add_layernorm_bwd(s, dy, g, mean, rstd, mask, ratio: float, dg_acc=None
         return t if ok else _zeros32(D, s.device)
 
     dg, db = (_acc(dg_acc), _acc(db_acc)) if g is not None else (None, None)
-    cs = _zeros32(D, s.device)
+    cs = _acc(cs_acc)
     ws = _mem.empty(L.layernorm_bwd_ws(R, D) * 3 // 2, dtype=torch.float32, device=s.device)
     gg = G.contiguous(G.to(g, torch.float32)) if g is not None else None
     L.drop_add_ln_bwd(s.data_ptr(), dy.data_ptr(), N.ptr(gg), mean.data_ptr(), rstd.data_ptr(), N.ptr(mask),
@@ -2467,10 +2468,18 @@ def attention_qkv_fwd(qkv: torch.Tensor, heads: int, mask: Optional[torch.Tensor
     return G.reshape(G.contiguous(o.permute(0, 2, 1, 3)), (B, S, HD)), G.reshape(p, (B * H, S, S))
 
 
+def fattn_bias_ok(p, db: Optional[torch.Tensor], E: int) -> bool:
+    """The fused attention backward can sum d(qkv)'s columns into ``db``."""
+    return (isinstance(p, FAttnState) and db is not None and db.is_cuda and db.dtype == torch.float32
+            and db.is_contiguous() and db.numel() == E)
+
+
 def attention_qkv_bwd(qkv: torch.Tensor, p: torch.Tensor, do: torch.Tensor, heads: int,
-                      scale: Optional[float] = None) -> torch.Tensor:
+                      scale: Optional[float] = None, db_acc: Optional[torch.Tensor] = None) -> torch.Tensor:
     """d(qkv) [B, S, 3*H*D] of :func:`attention_qkv_fwd` given do [B, S, H*D];
-    dq / dk / dv are written in place into their slots of d(qkv)."""
+    dq / dk / dv are written in place into their slots of d(qkv).
+    ``db_acc`` (fp32 [3*H*D], fused path only: see :func:`fattn_bias_ok`)
+    += the column sums of d(qkv), summed by the fused backward kernel."""
     B, S, E = qkv.shape
     H = heads
     D = E // (3 * H)
@@ -2479,9 +2488,13 @@ def attention_qkv_bwd(qkv: torch.Tensor, p: torch.Tensor, do: torch.Tensor, head
     if isinstance(p, FAttnState):
         do = G.contiguous(G.to(do, torch.bfloat16))
         dqkv = _mem.empty_like(qkv)
+        if db_acc is not None and not fattn_bias_ok(p, db_acc, E):
+            raise ValueError("attention_qkv_bwd: db_acc must be a dense fp32 [3*H*D] device tensor")
         N.lib().fattn_bwd(qkv.data_ptr(), p.o.data_ptr(), do.data_ptr(), p.lse.data_ptr(), N.ptr(p.mask), p.mstride,
-                          dqkv.data_ptr(), B, S, H, D, scale, N.stream())
+                          dqkv.data_ptr(), N.ptr(db_acc), B, S, H, D, scale, N.stream())
         return dqkv
+    if db_acc is not None:
+        raise ValueError("attention_qkv_bwd: db_acc needs the fused attention state")
     if _qkv_native_ok(qkv, H) and p.dtype == torch.bfloat16 and do.dtype == torch.bfloat16:
         BH = B * H
         do = G.contiguous(do)

@@ -99,3 +99,50 @@ def test_bert_fused_tail_equals_unfused(gpu, monkeypatch):
     assert calls[0] == n_fused  # the unfused run did not take it
     print(curves)
     np.testing.assert_allclose(curves["1"], curves["0"], rtol=2e-3)
+
+
+def test_producer_bias_gradient_summed_in_place(gpu, monkeypatch):
+    """The residual tail's backward sums da's columns straight into the
+    producing Linear's bias gradient (no temporary + add): one SGD step
+    (lr 1, so w0 - w1 is the gradient) equals the path that hands the sums
+    to the Linear, and the in-place route really ran."""
+    import numpy as np
+
+    from singa_amd import autograd, device, opt, tensor
+    from singa_amd.models import bert
+
+    cfg = dict(vocab=1000, hidden=128, layers=2, heads=2, ffn=512, max_pos=128)
+    rng = np.random.RandomState(1)
+    ids_np = rng.randint(0, cfg["vocab"], (8, 64)).astype(np.int64)
+    y_np = rng.randint(0, 2, 8).astype(np.int32)
+    orig = autograd.DropAddLayerNorm._producer_bias
+    taken = [0]
+
+    def spy(self):
+        r = orig(self)
+        taken[0] += r[1] is not None
+        return r
+
+    res, init = {}, None
+    for arm in ("inplace", "handoff"):
+        monkeypatch.setattr(autograd.DropAddLayerNorm, "_producer_bias",
+                            spy if arm == "inplace" else (lambda self: (None, None)))
+        dev = device.create_rocm_gpu()
+        dev.SetRandSeed(0)
+        m = bert.Bert(dropout=0.1, compute_dtype=torch.bfloat16, **cfg)
+        ids = tensor.from_numpy(ids_np, dev)
+        y = tensor.from_numpy(y_np, dev)
+        m.set_optimizer(opt.SGD(lr=1.0))
+        m.compile([ids], is_train=True, use_graph=False)
+        if init is None:
+            init = {k: v.data.float().clone() for k, v in m.get_states().items()}
+        else:
+            m.set_states({k: v.to(m.get_states()[k].data.dtype) for k, v in init.items()})
+        dev.SetRandSeed(5)
+        m.train()
+        m(ids, y)
+        res[arm] = {k: init[k] - v.data.float() for k, v in m.get_params().items()}
+    assert taken[0] == 2 * cfg["layers"]  # proj and fc2 of every layer
+    worst = max(rel_err(res["inplace"][k], res["handoff"][k]) for k in res["handoff"]
+                if float(res["handoff"][k].norm()) > 0)
+    assert worst < 1e-4, worst

@@ -62,6 +62,13 @@ def test_fused_attention_matches_fp32(gpu, B, S, H, masked):
     if mask is not None:
         s = s + mask
     torch.testing.assert_close(st.lse.view(B, H, S), torch.logsumexp(s, -1), rtol=1e-3, atol=1e-3)
+    # the projection's bias gradient summed on the way (accumulated into an
+    # existing buffer); d(qkv) itself unchanged
+    db0 = torch.randn(3 * HD, device=gpu, generator=g)
+    db = db0.clone()
+    dq2 = F.attention_qkv_bwd(qkv, st, do, H, scale, db_acc=db)
+    assert torch.equal(dq2, dq)
+    torch.testing.assert_close(db, db0 + dq.float().sum((0, 1)), rtol=1e-4, atol=1e-3)
 
 
 def test_fused_attention_equals_unfused_path(gpu, monkeypatch):
