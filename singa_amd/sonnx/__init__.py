@@ -895,10 +895,14 @@ class _Fused:
         if self.kind == "add_ln":  # [Identity] + Add + LayerNormalization -> one residual-tail operator
             x, a, g, b = xs
             if x.data.is_cuda and x.dtype != a.dtype and {x.dtype, a.dtype} == {torch.float32, torch.bfloat16}:
-                # (the mixed-precision import keeps the residual stream fp32: the
-                # add would promote the bf16 operand anyway)
-                x, a = (x, autograd.cast(a, torch.float32)) if x.dtype == torch.float32 else \
-                    (autograd.cast(x, torch.float32), a)
+                # mixed-precision import: the residual stream joins the compute
+                # dtype here (once, after the fp32 embedding LayerNorm), as in
+                # the native bf16 model -- every later projection input is then
+                # already bf16 (no per-GEMM input casts), the tail runs on bf16
+                # bytes and its input a is the projection's own output (so the
+                # tail can sum that projection's bias gradient in place)
+                lo = rep.compute_dtype if rep.compute_dtype in (torch.float32, torch.bfloat16) else torch.float32
+                x, a = (autograd.cast(x, lo) if x.dtype != lo else x), (autograd.cast(a, lo) if a.dtype != lo else a)
             if not autograd._TRACE and x.data.is_cuda and F.drop_add_ln_ok(x.data, a.data):
                 return autograd.DropAddLayerNorm(0.0, None, self.scale)(x, a, g, b)
             return autograd.layer_norm(autograd.add(x, a), g, b, self.scale)

@@ -904,3 +904,42 @@ def test_stem_kernel_matches_generic_conv(gpu, monkeypatch, hw):
     assert float((t0 - t1).abs().max()) <= 1e-3 * float(t0.abs().max())
     ref = torch.nn.functional.conv2d(x.bfloat16().float(), W.bfloat16().float(), stride=2, padding=3)
     assert float((y1 - ref.cpu()).abs().max()) <= 2e-2 * float(ref.abs().max())
+
+
+def test_sonnx_bert_tracks_native_model(gpu):
+    """BERT-tiny exported to ONNX and re-imported (bf16 compute, the import's
+    fused operators) trains like the native model it came from, loaded with
+    the same weights: same mixed-precision policy (the residual stream in
+    bf16 from the first residual tail on), loss curves within bf16 noise."""
+    from singa_amd import sonnx
+    from singa_amd.models import bert
+    from singa_amd.sonnx import onnx_proto as P
+
+    rng = np.random.RandomState(3)
+    ids_np = rng.randint(0, 1000, (8, 32)).astype(np.int64)
+    y_np = rng.randint(0, 2, 8).astype(np.int32)
+    cpu = device.get_default_device()
+    cpu.SetRandSeed(0)
+    src = bert.bert_tiny(dropout=0.0, compute_dtype=torch.float32)
+    ids_cpu = tensor.from_numpy(ids_np[:2])
+    src.compile([ids_cpu], is_train=False)
+    blob = sonnx.to_onnx(src, [ids_cpu]).SerializeToString()
+    states = {k: v.data.clone() for k, v in src.get_states().items()}
+    curves = {}
+    for kind in ("native", "imported"):
+        dev = device.create_rocm_gpu()
+        dev.SetRandSeed(0)
+        if kind == "imported":
+            m = sonnx.SONNXModel(P.load_model(blob), dev, compute_dtype=torch.bfloat16)
+        else:
+            m = bert.bert_tiny(dropout=0.0, compute_dtype=torch.bfloat16)
+        ids = tensor.from_numpy(ids_np).to_device(dev)
+        y = tensor.from_numpy(y_np).to_device(dev)
+        m.set_optimizer(opt.SGD(0.05))
+        m.compile([ids], is_train=True, use_graph=False)
+        if kind == "native":
+            m.set_states({k: v.to(m.get_states()[k].data.dtype) for k, v in states.items()})
+        m.train()
+        curves[kind] = [float(m(ids, y)[1].data.float().cpu()) for _ in range(4)]
+    print(curves)
+    np.testing.assert_allclose(curves["imported"], curves["native"], rtol=2e-2)
