@@ -9,6 +9,7 @@ from __future__ import annotations
 import torch
 
 from .. import autograd, layer, model
+from .resnet import InputPrep
 
 
 class AlexNet(model.Model):
@@ -46,7 +47,13 @@ class AlexNet(model.Model):
         self.loss_fn = layer.SoftMaxCrossEntropy()
 
     def forward(self, x):
-        if x.data.is_cuda and x.dtype != self.compute_dtype:
+        if (x.data.is_cuda and x.dtype == torch.float32 and self.compute_dtype == torch.bfloat16
+                and x.data.dim() == 4 and x.data.is_contiguous()):
+            # fp32 NCHW images -> bf16 NHWC with the channels padded to 8 in one
+            # pass (the first conv takes the padded input as is), instead of a
+            # cast pass followed by the conv's own layout pass
+            x = InputPrep(torch.bfloat16)(x)
+        elif x.data.is_cuda and x.dtype != self.compute_dtype:
             x = autograd.cast(x, self.compute_dtype)
         if self.small:
             y = self.n1(self.p1(self.c1(x)))

@@ -2025,11 +2025,13 @@ def bnres_bwd(g: torch.Tensor, gws: torch.Tensor, y: torch.Tensor, w: torch.Tens
     L.bnres_coef(Gm.data_ptr(), wb.data_ptr(), gws.data_ptr(), st.mean.data_ptr(), st.invstd.data_ptr(),
                  gamma.data_ptr(), P, K4, C, coef.data_ptr(), wf.data_ptr(), wu.data_ptr(), dg.data_ptr(),
                  db.data_ptr(), s)
-    T = _mem.empty(K4 * C, dtype=f32, device=dev)  # W Gram
-    L.ggemm(0, wf.data_ptr(), C, 0, 0, Gram.data_ptr(), C, 1, 0, T.data_ptr(), C, 0, K4, C, C, 1.0, 0.0, 0, 0, 1, 0,
+    # the two small fp32 GEMMs accumulate (split-K atomics) into zeroed arena
+    # slices: no zeroing launch of their own
+    TM = _zeros32(K4 * C + C * C, dev)
+    T, Mm = TM[:K4 * C], TM[K4 * C:]  # W Gram ; W^T diag(u) W
+    L.ggemm(0, wf.data_ptr(), C, 0, 0, Gram.data_ptr(), C, 1, 0, T.data_ptr(), C, 0, K4, C, C, 1.0, 1.0, 0, 0, 2, 0,
             1, 0, 0, 0, 0, s)
-    Mm = _mem.empty(C * C, dtype=f32, device=dev)  # W^T diag(u) W
-    L.ggemm(0, wf.data_ptr(), C, 1, 0, wu.data_ptr(), C, 1, 0, Mm.data_ptr(), C, 0, C, C, K4, 1.0, 0.0, 0, 0, 1, 0,
+    L.ggemm(0, wf.data_ptr(), C, 1, 0, wu.data_ptr(), C, 1, 0, Mm.data_ptr(), C, 0, C, C, K4, 1.0, 1.0, 0, 0, 2, 0,
             1, 0, 0, 0, 0, s)
     if cs is None:  # (the producer BN's apply pass sums them when it knows this consumer: st.colsum)
         cs = colsum(y.permute(0, 2, 3, 1).reshape(P, C))[0]
