@@ -737,8 +737,17 @@ class Linear(Operator):
             prod = self._producer_act(x2)
             if prod is not None:
                 t = prod.z2 if prod.act in F.ACT_XFORM else x2
-                dx = F.gemm_nt(dy2, w, out_dtype=x2.dtype, act_grad=(prod.act, G.reshape(t, tuple(x2.shape))))
+                # the producer's bias gradient = column sums of this GEMM's
+                # output (its pre-activation gradient): summed in the same epilogue
+                pb = prod.grad_target(2) if (prod.has_bias and BIAS_INPLACE) else None
+                if not (pb is not None and pb.is_cuda and pb.dtype == torch.float32 and pb.is_contiguous()
+                        and pb.numel() == x2.shape[-1]):
+                    pb = None
+                dx = F.gemm_nt(dy2, w, out_dtype=x2.dtype, act_grad=(prod.act, G.reshape(t, tuple(x2.shape))),
+                               colsum_c=pb)
                 prod.preact_done = True
+                if pb is not None:
+                    prod.db_done = True
             else:
                 dx = F.gemm_nt(dy2, w, out_dtype=x2.dtype)
             dx = G.reshape(dx, (*dy.shape[:-1], x2.shape[-1]))

@@ -166,7 +166,7 @@ void sg_workq_arena_end();
 void sg_workq_arena_free(void*);
 int sg_workq_arena_slots(void*);
 int sg_gemm_act(const void*, int64_t, int, const void*, int64_t, int, void*, int64_t, int, int, int, float, const void*,
-                int, int64_t, int64_t, int64_t, int, void*, int, const void*, hipStream_t);
+                int, int64_t, int64_t, int64_t, int, void*, int, const void*, float*, hipStream_t);
 void sg_gconv_fwd(int, const void*, const void*, void*, const void*, int, int, int, int, int, int, int, int, int, int,
                   int, int, int, int, int, int, int, int, hipStream_t);
 void sg_gconv_dgrad(int, const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int,
@@ -618,9 +618,9 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("gemm_act", [](P a, int64_t lda, int ako, P b, int64_t ldb, int bko, P c, int64_t ldc, int M, int N, int K,
                        float alpha, P bias, int batch, int64_t sa, int64_t sb, int64_t sc, int act, P aux, int act_bwd,
-                       P act_x, P s) {
+                       P act_x, P colsum, P s) {
     const int r = sg_gemm_act(CV(a), lda, ako, CV(b), ldb, bko, V(c), ldc, M, N, K, alpha, CV(bias), batch, sa, sb, sc,
-                              act, V(aux), act_bwd, CV(act_x), S(s));
+                              act, V(aux), act_bwd, CV(act_x), (float*)V(colsum), S(s));
     CHK("gemm_act");
     return r;
   });

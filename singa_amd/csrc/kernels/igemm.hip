@@ -562,13 +562,14 @@ void sg_gemm(const void* a, int64_t lda, int a_kouter, const void* b, int64_t ld
 
 // sg_gemm with a fused activation (bf16 output through the LDS-staged
 // epilogue): act (codes in GemmArgs) with the pre-activation also written to
-// aux when given, or act_bwd: out *= act'(act_x).  Returns 0 (nothing
-// launched) when the shape cannot take the staged epilogue.
+// aux when given, or act_bwd: out *= act'(act_x) -- then optionally also
+// colsum[n] += sum_m out[m][n] (fp32 atomics).  Returns 0 (nothing launched)
+// when the shape cannot take the staged epilogue.
 int sg_gemm_act(const void* a, int64_t lda, int a_kouter, const void* b, int64_t ldb, int b_kouter, void* c,
                 int64_t ldc, int M, int N, int K, float alpha, const void* bias, int batch, int64_t sa, int64_t sb,
-                int64_t sc, int act, void* aux, int act_bwd, const void* act_x, hipStream_t s) {
+                int64_t sc, int act, void* aux, int act_bwd, const void* act_x, float* colsum, hipStream_t s) {
   if ((N & 7) != 0 || (ldc & 7) != 0 || !g_tune[1] || g_tune[4] != 0 || (act == 0) == (act_x == nullptr) ||
-      M <= 0 || K <= 0 || batch != 1)
+      M <= 0 || K <= 0 || batch != 1 || (colsum && (act != 0 || sg_bn_deterministic())))
     return 0;
   GemmArgs p{};
   init_phase_identity(p.g);
@@ -576,6 +577,11 @@ int sg_gemm_act(const void* a, int64_t lda, int a_kouter, const void* b, int64_t
   p.M = M; p.N = N; p.K = K; p.a = (const bf16*)a; p.lda = lda; p.b = (const bf16*)b; p.ldb = ldb;
   p.c = c; p.ldc = ldc; p.alpha = alpha; p.beta = 0.f; p.bias = (const float*)bias; p.relu = 0;
   p.act = act; p.aux = (bf16*)aux; p.act_x = (const bf16*)act_x; p.act_bwd = act_bwd;
+  if (colsum) {  // += column sums of the output (the producer's bias gradient), summed in the staged epilogue
+    p.stats = colsum;
+    p.stats_mode = 5;
+    p.stats_det = 0;
+  }
   p.k_per_split = kps(K, 1);
   p.a_bytes = extent_bytes(a_kouter ? (int64_t)(K - 1) * lda + M : (int64_t)(M - 1) * lda + K);
   p.b_bytes = extent_bytes(b_kouter ? (int64_t)(K - 1) * ldb + N : (int64_t)(N - 1) * ldb + K);

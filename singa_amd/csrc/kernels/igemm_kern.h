@@ -76,6 +76,8 @@ struct GemmArgs {
   // stats_mode 2: the same sums for a residual BN(+ReLU) whose ReLU mask is
   // the 1-bit map bnb_mask [rows][C/8] written by its forward apply
   // stats_mode 3: only sum(g) over the mask bits (the identity-sum BN backward)
+  // stats_mode 5 (gemm_act only): stats is an fp32 [N] vector += the column
+  // sums of the bf16 output (atomics; the staged epilogue of igemm_k / pp_gemm_k)
   int stats_mode;
   // residual-gradient accumulate (bf16 LDS-staged epilogue, beta == 0, no
   // stats): out += res_g * bit(res_mask) -- the gradient a residual

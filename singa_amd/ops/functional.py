@@ -636,7 +636,8 @@ def gemm(a: torch.Tensor, b: torch.Tensor, ta: bool = False, tb: bool = False, o
          out_dtype: Optional[torch.dtype] = None, alpha: float = 1.0, beta: float = 0.0,
          bias: Optional[torch.Tensor] = None, relu: bool = False, accumulate: bool = False,
          colsum_b: Optional[torch.Tensor] = None, act: Optional[str] = None,
-         act_grad: Optional[Tuple[str, torch.Tensor]] = None, act_aux: Optional[torch.Tensor] = None) -> torch.Tensor:
+         act_grad: Optional[Tuple[str, torch.Tensor]] = None, act_aux: Optional[torch.Tensor] = None,
+         colsum_c: Optional[torch.Tensor] = None) -> torch.Tensor:
     """C = alpha * op(a) @ op(b) (+ beta * C) (+ bias[n]) (ReLU), op(t) = t.T if
     the flag is set.  2-D or batched 3-D operands (equal batch, or one side
     2-D and shared).  ``accumulate``: C (fp32 ``out``) += alpha * op(a) op(b)
@@ -649,12 +650,20 @@ def gemm(a: torch.Tensor, b: torch.Tensor, ta: bool = False, tb: bool = False, o
     laid out like C -- a data-gradient GEMM taking its producer's activation
     backward.  Both run in the GEMM epilogues on the GPU (rounded exactly as
     the separate elementwise kernels would); the host applies them in a
-    separate pass.  On the
+    separate pass.  ``colsum_c`` (fp32 [N], with ``act_grad``): += the column
+    sums of the final C -- that producer's bias gradient -- summed in the
+    same epilogue where the tuned kernel takes the call, else by a separate
+    pass.  On the
     GPU: bf16 operands of aligned shapes run the tuned MFMA kernel,
     everything else (fp32 -- exact f32 MFMA -- and ragged bf16) the generic
     one; there is no vendor-BLAS path."""
     if colsum_b is not None and (a.dim() != 2 or b.dim() != 2):
         raise ValueError("gemm: colsum_b needs 2-D operands")
+    if colsum_c is not None:
+        if act_grad is None or a.dim() != 2 or b.dim() != 2:
+            raise ValueError("gemm: colsum_c needs act_grad and 2-D operands")
+        if colsum_c.dtype != torch.float32 or not colsum_c.is_contiguous():
+            raise ValueError("gemm: colsum_c must be a dense fp32 [N] tensor")
     if act == "relu" and act_grad is None and act_aux is None:
         act, relu = None, True
     if act is not None or act_grad is not None:
@@ -666,8 +675,10 @@ def gemm(a: torch.Tensor, b: torch.Tensor, ta: bool = False, tb: bool = False, o
         fused = (a.is_cuda and N.available() and a.dtype == b.dtype == dt and dt in (torch.float32, torch.bfloat16)
                  and beta == 0.0)
         if not fused:
-            return _gemm_act_unfused(a, b, ta, tb, out, out_dtype, alpha, beta, bias, colsum_b, act, act_grad,
-                                     act_aux)
+            c = _gemm_act_unfused(a, b, ta, tb, out, out_dtype, alpha, beta, bias, colsum_b, act, act_grad, act_aux)
+            if colsum_c is not None:
+                _colsum_into(c, colsum_c)
+            return c
         for t in ((act_grad[1] if act_grad is not None else None), act_aux):
             if t is not None and (t.dtype != dt or not t.is_contiguous()):
                 raise ValueError("gemm: act_grad / act_aux tensors must be dense and of the output dtype")
@@ -759,10 +770,12 @@ def gemm(a: torch.Tensor, b: torch.Tensor, ta: bool = False, tb: bool = False, o
         if act is not None or act_grad is not None:
             # fused activation: the tuned kernel's LDS-staged epilogue (bf16
             # output, batch 1, N % 8), else the generic kernel below
+            if colsum_c is not None and colsum_c.numel() != Nn:
+                raise ValueError(f"gemm: colsum_c has {colsum_c.numel()} entries, C has {Nn} columns")
             if mode == 0 and batch == 1 and colsum_b is None and L.gemm_act(
                     a.data_ptr(), lda, int(ako), b.data_ptr(), ldb, int(bko), out.data_ptr(), Nn, M, Nn, K, alpha,
                     N.ptr(bb), batch, sa, sb, sc, code if act is not None else 0, N.ptr(act_aux), ab, N.ptr(ax),
-                    N.stream()):
+                    N.ptr(colsum_c), N.stream()):
                 return out
         else:
             L.gemm(a.data_ptr(), lda, int(ako), b.data_ptr(), ldb, int(bko), out.data_ptr(), Nn, M, Nn, K, alpha,
@@ -779,11 +792,24 @@ def gemm(a: torch.Tensor, b: torch.Tensor, ta: bool = False, tb: bool = False, o
         cs = colsum_b.data_ptr()
     if act in ACT_XFORM or act_grad is not None and act_grad[0] in ACT_XFORM:
         # (the generic kernel's epilogue carries only the y-form activations)
-        return _gemm_act_unfused(a, b, ta, tb, out, None, alpha, beta, bias, colsum_b, act, act_grad, act_aux)
+        c = _gemm_act_unfused(a, b, ta, tb, out, None, alpha, beta, bias, colsum_b, act, act_grad, act_aux)
+        if colsum_c is not None:
+            _colsum_into(c, colsum_c)
+        return c
     L.ggemm(0 if a.dtype == torch.float32 else 1, a.data_ptr(), lda, int(ako), sa, b.data_ptr(), ldb, int(bko), sb,
             out.data_ptr(), Nn, sc, M, Nn, K, alpha, beta, N.ptr(bb), code, mode, 0, batch, cs, ab, N.ptr(ax),
             N.ptr(act_aux), N.stream())
+    if colsum_c is not None:
+        _colsum_into(out, colsum_c)
     return out
+
+
+def _colsum_into(c: torch.Tensor, out: torch.Tensor) -> None:
+    """out += column sums of the 2-D C (the separate pass behind gemm's colsum_c)."""
+    if c.is_cuda:
+        colsum(G.contiguous(c), out=out)
+    else:
+        out.add_(c.float().sum(0))
 
 
 def _gemm_act_unfused(a, b, ta, tb, out, out_dtype, alpha, beta, bias, colsum_b, act, act_grad, act_aux):
@@ -836,9 +862,11 @@ def matmul(a: torch.Tensor, b: torch.Tensor, out_dtype: Optional[torch.dtype] = 
     return gemm(a, b, out_dtype=out_dtype or a.dtype, bias=bias, relu=relu, act=act, act_aux=act_aux)
 
 
-def gemm_nt(a: torch.Tensor, b: torch.Tensor, out_dtype=None, bias=None, relu=False, act_grad=None) -> torch.Tensor:
-    """C = a @ b.T (both operands K-major: a [M,K], b [N,K]); ``act_grad`` as in :func:`gemm`."""
-    return gemm(a, b, tb=True, out_dtype=out_dtype or a.dtype, bias=bias, relu=relu, act_grad=act_grad)
+def gemm_nt(a: torch.Tensor, b: torch.Tensor, out_dtype=None, bias=None, relu=False, act_grad=None,
+            colsum_c=None) -> torch.Tensor:
+    """C = a @ b.T (both operands K-major: a [M,K], b [N,K]); ``act_grad`` / ``colsum_c`` as in :func:`gemm`."""
+    return gemm(a, b, tb=True, out_dtype=out_dtype or a.dtype, bias=bias, relu=relu, act_grad=act_grad,
+                colsum_c=colsum_c)
 
 
 def gemm_tn_acc(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, beta: float = 1.0,

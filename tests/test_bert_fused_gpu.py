@@ -146,3 +146,37 @@ def test_producer_bias_gradient_summed_in_place(gpu, monkeypatch):
     worst = max(rel_err(res["inplace"][k], res["handoff"][k]) for k in res["handoff"]
                 if float(res["handoff"][k].norm()) > 0)
     assert worst < 1e-4, worst
+
+
+def test_fc1_bias_gradient_from_fc2_dgrad_epilogue(gpu, monkeypatch):
+    """fc1's bias gradient summed in fc2's data-gradient epilogue (the GEMM
+    that applies fc1's GELU backward): one SGD step equals the path with the
+    separate column-sum pass (SINGA_AMD_BIAS_INPLACE=0 equivalent)."""
+    import numpy as np
+
+    from singa_amd import autograd, device, opt, tensor
+    from singa_amd.models import bert
+
+    cfg = dict(vocab=1000, hidden=128, layers=2, heads=2, ffn=512, max_pos=128)
+    rng = np.random.RandomState(2)
+    ids_np = rng.randint(0, cfg["vocab"], (8, 64)).astype(np.int64)
+    y_np = rng.randint(0, 2, 8).astype(np.int32)
+    res, init = {}, None
+    for on in (True, False):
+        monkeypatch.setattr(autograd, "BIAS_INPLACE", on)
+        dev = device.create_rocm_gpu()
+        dev.SetRandSeed(0)
+        m = bert.Bert(dropout=0.0, compute_dtype=torch.bfloat16, **cfg)
+        ids = tensor.from_numpy(ids_np, dev)
+        y = tensor.from_numpy(y_np, dev)
+        m.set_optimizer(opt.SGD(lr=1.0))
+        m.compile([ids], is_train=True, use_graph=False)
+        if init is None:
+            init = {k: v.data.float().clone() for k, v in m.get_states().items()}
+        else:
+            m.set_states({k: v.to(m.get_states()[k].data.dtype) for k, v in init.items()})
+        m.train()
+        m(ids, y)
+        res[on] = {k: init[k] - v.data.float() for k, v in m.get_params().items()}
+    worst = max(rel_err(res[True][k], res[False][k]) for k in res[False] if float(res[False][k].norm()) > 0)
+    assert worst < 1e-4, worst

@@ -390,3 +390,23 @@ def test_bert_layer_fused_gelu_matches_unfused(gpu):
     assert set(g0) == set(g1) and len(g0) > 6
     for k in g0:
         assert rel_err(g1[k], g0[k]) < 3e-2, k
+
+
+@pytest.mark.parametrize("M,N,K", [(4096, 3072, 768), (1000, 136, 64), (300, 124, 96), (777, 2048, 2304)])
+def test_act_grad_gemm_output_column_sums(gpu, M, N, K):
+    """A data-gradient GEMM taking its producer's activation backward also
+    sums its output's columns into the producer's bias gradient (colsum_c,
+    accumulated): the tuned kernel's staged epilogue where N % 8 == 0, else
+    a separate pass -- equal to fp32 column sums of the bf16 output, and the
+    output bitwise the call without it."""
+    from singa_amd.ops import functional as F
+    dy = _rand(M, K, seed=91).to(gpu).bfloat16()
+    w = (_rand(N, K, seed=92) * 0.1).to(gpu).bfloat16()
+    z = _rand(M, N, seed=93).to(gpu).bfloat16()
+    ref = F.gemm_nt(dy, w, out_dtype=torch.bfloat16, act_grad=("gelu", z))
+    cs0 = _rand(N, seed=94).to(gpu)
+    cs = cs0.clone()
+    out = F.gemm_nt(dy, w, out_dtype=torch.bfloat16, act_grad=("gelu", z), colsum_c=cs)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    torch.testing.assert_close(cs, cs0 + out.float().sum(0), rtol=1e-4, atol=1e-2)
