@@ -80,7 +80,7 @@ PARAM_USES: dict = {}
 # backward() returned: the input gradient was added IN PLACE into the partial
 # gradient the engine offered through ``op.acc_into`` (see backward())
 ACC_INPLACE = object()
-INPLACE_ACC = True
+INPLACE_ACC = os.environ.get("SINGA_AMD_INPLACE_ACC", "1") != "0"  # (A/B switch)
 
 
 class AccReplace:
@@ -683,6 +683,8 @@ class Linear(Operator):
         self.preact_done = False
         self.db_done = False  # a consumer (DropAddLayerNorm) already summed the bias gradient into its view
 
+    accepts_acc = True  # the data gradient can add into another consumer's pending gradient of x
+
     def forward(self, x, W, b=None):
         w = self._w_compute(x, W)
         lead = x.shape[:-1]
@@ -749,8 +751,18 @@ class Linear(Operator):
                 if pb is not None:
                     prod.db_done = True
             else:
-                dx = F.gemm_nt(dy2, w, out_dtype=x2.dtype)
-            dx = G.reshape(dx, (*dy.shape[:-1], x2.shape[-1]))
+                # another consumer's gradient of x already pending (a residual
+                # stream: the tail's ds): this data gradient adds into it in
+                # its epilogue (beta 1) instead of a separate add pass
+                acc = (getattr(self, "acc_into", None) or {}).get(0)
+                if (acc is not None and acc.is_cuda and acc.dtype == x2.dtype and acc.is_contiguous()
+                        and acc.numel() == x2.numel() and w.dtype == dy2.dtype == x2.dtype):
+                    F.gemm(dy2, w, tb=True, out=G.reshape(acc, tuple(x2.shape)), beta=1.0)
+                    dx = ACC_INPLACE
+                else:
+                    dx = F.gemm_nt(dy2, w, out_dtype=x2.dtype)
+            if dx is not ACC_INPLACE:
+                dx = G.reshape(dx, (*dy.shape[:-1], x2.shape[-1]))
         tgt = self.grad_target(1)
         tb = self.grad_target(2) if self.has_bias else None
         # dy's column sums already summed by its producer (DropAddLayerNorm's backward)
@@ -1378,6 +1390,7 @@ class DropAddLayerNorm(Operator):
             prod = cs_to = None
         ds, da, dg, db, cs = F.drop_add_layernorm_bwd(s, dy, g, mean, rstd, mask, ratio, dg_acc=tg, db_acc=tb,
                                                       cs_acc=cs_to)
+        ds._sg_fresh = True  # (a buffer of its own: x's other consumer may add into it in place)
         if prod is not None:
             prod.db_done = True  # da's column sums went straight into the producer's bias gradient
         else:

@@ -72,6 +72,9 @@ def test_bert_fused_tail_equals_unfused(gpu, monkeypatch):
     # the unfused attention in both arms: this compares the residual tails
     # alone (the fused attention is checked in test_fattn_gpu.py)
     monkeypatch.setenv("SINGA_AMD_FATTN", "0")
+    # and the separate gradient adds in both (the in-place accumulation into
+    # the tail's ds rounds once instead of twice: test_linear_dgrad_accumulates_...)
+    monkeypatch.setattr(autograd, "INPLACE_ACC", False)
     curves, init = {}, None
     for fused in ("1", "0"):
         monkeypatch.setenv("SINGA_AMD_FUSED_DAL", fused)
@@ -180,3 +183,51 @@ def test_fc1_bias_gradient_from_fc2_dgrad_epilogue(gpu, monkeypatch):
         res[on] = {k: init[k] - v.data.float() for k, v in m.get_params().items()}
     worst = max(rel_err(res[True][k], res[False][k]) for k in res[False] if float(res[False][k].norm()) > 0)
     assert worst < 1e-4, worst
+
+
+def test_linear_dgrad_accumulates_into_residual_gradient(gpu, monkeypatch):
+    """The q/k/v and fc1 projections' data gradients add into the residual
+    tail's pending gradient of their shared input in the GEMM epilogue (beta
+    1, one bf16 rounding instead of two): one SGD step matches the separate
+    add pass (autograd.INPLACE_ACC off) to bf16 accuracy, and the in-place
+    route really ran."""
+    import numpy as np
+
+    from singa_amd import autograd, device, opt, tensor
+    from singa_amd.models import bert
+    from singa_amd.ops import functional as F
+
+    cfg = dict(vocab=1000, hidden=128, layers=2, heads=2, ffn=512, max_pos=128)
+    rng = np.random.RandomState(4)
+    ids_np = rng.randint(0, cfg["vocab"], (8, 64)).astype(np.int64)
+    y_np = rng.randint(0, 2, 8).astype(np.int32)
+    orig = F.gemm
+    n_beta1 = [0]
+
+    def spy(*a, **kw):
+        n_beta1[0] += kw.get("beta", 0.0) == 1.0 and kw.get("out") is not None and kw.get("out").dtype == torch.bfloat16
+        return orig(*a, **kw)
+
+    monkeypatch.setattr(F, "gemm", spy)
+    res, init = {}, None
+    for on in (True, False):
+        monkeypatch.setattr(autograd, "INPLACE_ACC", on)
+        dev = device.create_rocm_gpu()
+        dev.SetRandSeed(0)
+        m = bert.Bert(dropout=0.0, compute_dtype=torch.bfloat16, **cfg)
+        ids = tensor.from_numpy(ids_np, dev)
+        y = tensor.from_numpy(y_np, dev)
+        m.set_optimizer(opt.SGD(lr=1.0))
+        m.compile([ids], is_train=True, use_graph=False)
+        if init is None:
+            init = {k: v.data.float().clone() for k, v in m.get_states().items()}
+        else:
+            m.set_states({k: v.to(m.get_states()[k].data.dtype) for k, v in init.items()})
+        m.train()
+        n0 = n_beta1[0]
+        m(ids, y)
+        if on:
+            assert n_beta1[0] - n0 >= 2 * cfg["layers"]  # q/k/v and fc1 of every layer
+        res[on] = {k: init[k] - v.data.float() for k, v in m.get_params().items()}
+    worst = max(rel_err(res[True][k], res[False][k]) for k in res[False] if float(res[False][k].norm()) > 0)
+    assert worst < 2e-2, worst
