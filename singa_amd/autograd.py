@@ -741,7 +741,9 @@ class Linear(Operator):
                 t = prod.z2 if prod.act in F.ACT_XFORM else x2
                 # the producer's bias gradient = column sums of this GEMM's
                 # output (its pre-activation gradient): summed in the same epilogue
-                pb = prod.grad_target(2) if (prod.has_bias and BIAS_INPLACE) else None
+                # (bf16: the tuned kernel's epilogue; the fp32 generic GEMM sums
+                # the bias gradient in the producer's weight-gradient GEMM for free)
+                pb = prod.grad_target(2) if (prod.has_bias and BIAS_INPLACE and x2.dtype == torch.bfloat16) else None
                 if not (pb is not None and pb.is_cuda and pb.dtype == torch.float32 and pb.is_contiguous()
                         and pb.numel() == x2.shape[-1]):
                     pb = None
