@@ -224,7 +224,7 @@ __global__ void __launch_bounds__(64 * NW) fwd_k(const Args a) {
   }
 }
 
-// grid B*H, 64 NW threads; LDS 4 S RS + S (2S + 16) + 8 S + NW WSCR (+ 3 * 64 floats with dbias)
+// grid B*H, 64 NW threads; LDS 4 S RS + S (2S + 16) + 8 S + NW WSCR (+ NW * 4 * 3 * 64 floats with dbias)
 __global__ void __launch_bounds__(64 * NW) bwd_k(const Args a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int S = a.S, H = a.H;
@@ -238,9 +238,8 @@ __global__ void __launch_bounds__(64 * NW) bwd_k(const Args a) {
   float* sL = (float*)(sdS + S * SS);
   float* sD = sL + S;
   char* scr_base = (char*)(sD + S);
-  float* sCS = (float*)(scr_base + NW * WSCR);  // [q, k, v][64] column sums of this (b, h)
+  float* sCS = (float*)(scr_base + NW * WSCR);  // [NW][4][q, k, v][64] partial column sums of this (b, h)
   const bf16* base = a.qkv + (int64_t)b * S * a.E + h * D;
-  if (a.dbias && threadIdx.x < 3 * D) sCS[threadIdx.x] = 0.f;
   {
     // one image at a time: measured faster here than stage() with all four
     // images' loads in flight (25.7 vs 31-33 us per BERT-base layer,
@@ -352,29 +351,27 @@ __global__ void __launch_bounds__(64 * NW) bwd_k(const Args a) {
     if (a.dbias) colsum_block(dq, a.scale, csq);
   }
   if (a.dbias) {  // (uniform branch)
-    // lane groups g = 0..3 hold different rows of the same columns: fold
-    // them, then the waves through LDS, then one global atomic per column
+    // every lane stores its 12 partial column sums into its own slot of an
+    // [NW][4][3 D] LDS image (plain stores, conflict-free), then 3 D threads
+    // each fold 4 NW slots and issue one global atomic.  (LDS float atomics
+    // from the lanes cost 5-16 us per launch here; shuffles + LDS atomics ~5.)
+    float* slot = sCS + (w * 4 + g) * 3 * D;
 #pragma unroll
     for (int db = 0; db < 4; ++db) {
-      csq[db] += __shfl_xor(csq[db], 16);
-      csq[db] += __shfl_xor(csq[db], 32);
-      csk[db] += __shfl_xor(csk[db], 16);
-      csk[db] += __shfl_xor(csk[db], 32);
-      csv[db] += __shfl_xor(csv[db], 16);
-      csv[db] += __shfl_xor(csv[db], 32);
+      slot[db * 16 + li] = csq[db];
+      slot[D + db * 16 + li] = csk[db];
+      slot[2 * D + db * 16 + li] = csv[db];
     }
-    if (g == 0) {
-#pragma unroll
-      for (int db = 0; db < 4; ++db) {
-        atomicAdd(sCS + db * 16 + li, csq[db]);
-        atomicAdd(sCS + D + db * 16 + li, csk[db]);
-        atomicAdd(sCS + 2 * D + db * 16 + li, csv[db]);
-      }
-    }
-    __syncthreads();
+    // raw barrier after the LDS stores only: __syncthreads' fence would first
+    // wait for this wave's dQ / dK / dV global stores
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    __builtin_amdgcn_s_barrier();
     if (threadIdx.x < 3 * D) {
       const int part = threadIdx.x / D, c = threadIdx.x - part * D;
-      atomicAdd(a.dbias + (int64_t)part * H * D + h * D + c, sCS[threadIdx.x]);
+      float v = 0.f;
+#pragma unroll 8
+      for (int k = 0; k < 4 * NW; ++k) v += sCS[k * 3 * D + threadIdx.x];
+      atomicAdd(a.dbias + (int64_t)part * H * D + h * D + c, v);
     }
   }
 }
@@ -425,7 +422,7 @@ extern "C" int sg_fattn_bwd(const void* qkv, const void* o, const void* dout, co
   a.out = (const sg::bf16*)o;
   a.dqkv = (sg::bf16*)dqkv;
   a.dbias = dbias;
-  const int cs = 3 * sg::fa::D * (int)sizeof(float);
+  const int cs = sg::fa::NW * 4 * 3 * sg::fa::D * (int)sizeof(float);  // partial column-sum slots
   const int lds = 4 * S * sg::fa::RS + S * (2 * S + 16) + 8 * S + sg::fa::NW * sg::fa::WSCR + (dbias ? cs : 0);
   static bool attr = hipFuncSetAttribute((const void*)sg::fa::bwd_k, hipFuncAttributeMaxDynamicSharedMemorySize,
                                          4 * sg::fa::SMAX * sg::fa::RS + sg::fa::SMAX * (2 * sg::fa::SMAX + 16) +
