@@ -193,6 +193,8 @@ static int make_phases(ConvGeom& g) {
 // key 17: 1 = 128 x 256 three-stage weight-gradient tiles for K_out < 256 (with key 15)
 // key 18: 1 = the persistent streaming GEMM (st_gemm_k) for the 1x1-conv shapes with K >= 256
 //         (plain bf16 output, optional BN statistics)
+// key 19: 1 = __syncthreads (vmcnt(0) drain of the output stores) at the staged epilogue's barriers
+//         after its global stores; 0 = LDS-only barriers (default)
 extern "C" int sg_bn_deterministic();  // batchnorm.hip: deterministic-reduction mode
 static int g_tune[20] = {5, 1, 1, 0, 0, 1, 2, 1, 0, 1, 0, 0, 0, 1, 0, 1, 0, 0, 1, 0};
 // one-shot: the next dgrad's wt scratch is already transposed.  Per OS
@@ -225,6 +227,7 @@ template <int BM, int BN, int AM, int BMODE, int OUT, int NTH = NT, int WM = 2, 
 static void launch_t(const GemmArgs& p_in, int tiles, int ydim, int zdim, hipStream_t s) {
   GemmArgs p = p_in;
   p.lds_epilogue = g_tune[1];
+  p.epi_fence = g_tune[19];
   p.early_issue = g_tune[7];
   p.nt_store = g_tune[8];
   p.xcd_split = (OUT == OUT_F32_ATOMIC && g_tune[2] && ydim == 1 && zdim >= 8 && (zdim & 7) == 0) ? 1 : 0;
@@ -256,6 +259,7 @@ template <int OUT, int FLAGS = 0>
 static void launch_pp(const GemmArgs& p_in, int tiles, int ydim, hipStream_t s) {
   GemmArgs p = p_in;
   p.lds_epilogue = g_tune[1];
+  p.epi_fence = g_tune[19];
   p.nt_store = g_tune[8];
   constexpr int lds = 2 * PP_BUF;
   auto* kern = pp_gemm_k<OUT, FLAGS>;

@@ -64,6 +64,7 @@ struct GemmArgs {
   int64_t sa2, sb2, sc2;
   int out_phase;       // dgrad: output rows map through the phase grid
   int lds_epilogue;    // stage bf16 output tiles through LDS (16-byte stores)
+  int epi_fence;       // 1: the staged epilogue's barriers after output stores are __syncthreads (knob 19 A/B)
   unsigned a_bytes, b_bytes;  // operand extents (buffer-resource ranges; per batch slice)
   float* stats;        // optional BN statistics of the bf16 output: ws[row][2][N] (sum, sum of squares)
   int stats_det;       // 1: row = tile row, plain stores (deterministic); 0: row = tile row % 32, atomics
@@ -576,6 +577,20 @@ __device__ __forceinline__ void raw_barrier() {
   asm volatile("" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
+}
+// Barrier ordering LDS accesses only (this wave's LDS operations complete,
+// then the raw barrier): an epilogue barrier after global stores.  With
+// __syncthreads() the compiler emits s_waitcnt vmcnt(0) first, so every wave
+// of the workgroup would wait for its output stores to land before the BN
+// statistics reduction (fence = 1: that behaviour, tuning knob 19 for A/B).
+__device__ __forceinline__ void lds_barrier(int fence) {
+  if (fence) {
+    __syncthreads();
+  } else {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    raw_barrier();
+  }
 }
 
 
