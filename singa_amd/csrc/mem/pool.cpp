@@ -24,6 +24,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <algorithm>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -580,6 +581,262 @@ py::object blob_view(std::shared_ptr<SyncedBlob> b, uintptr_t ptr, bool on_devic
   return py::reinterpret_steal<py::object>(PyCapsule_New(m, "dltensor", capsule_dtor));
 }
 
+// ------------------------------------------------------------ native Tensor
+// The framework's tensor handle: the mshadow Tensor / Shape and Blob of the
+// reference (include/mshadow/tensor.h:206-385 -- dptr, shape, stride;
+// include/utils/blob.h:94-163 -- count, shape, data) over this file's pools.
+// A Storage is one allocation (a pool block, or a foreign DLPack buffer the
+// handle keeps alive); a Tensor is (storage, byte offset, shape, strides in
+// elements, dtype, device).  Views (reshape, permute, slice, select, expand,
+// squeeze / unsqueeze, as_strided) are metadata over the same storage; DLPack
+// export hands the bytes to PyTorch / NumPy without a copy and keeps the
+// storage alive for as long as the importer holds them.
+struct Storage {
+  void* ptr = nullptr;
+  size_t bytes = 0;
+  int kind = 0;  // 0 device pool, 1 host pageable pool, 2 host pinned pool, 3 foreign (DLPack import)
+  int dev = 0;
+  DLManagedTensor* foreign = nullptr;
+  ~Storage() {
+    try {
+      if (kind == 0 && ptr) dev_pool(dev).free(ptr);
+      else if ((kind == 1 || kind == 2) && ptr) host_pool(kind == 2).free(ptr);
+      else if (kind == 3 && foreign && foreign->deleter) foreign->deleter(foreign);
+    } catch (...) {
+    }
+  }
+};
+
+struct NTensor {
+  std::shared_ptr<Storage> st;
+  int64_t offset = 0;  // bytes from st->ptr
+  std::vector<int64_t> shape, strides;
+  int code = 2, bits = 32;
+  int32_t dl_type = kDLCPU;
+  int dev = 0;
+
+  int64_t numel() const {
+    int64_t n = 1;
+    for (int64_t v : shape) n *= v;
+    return n;
+  }
+  int itemsize() const { return bits / 8; }
+  uintptr_t data_ptr() const { return (uintptr_t)st->ptr + offset; }
+  static std::vector<int64_t> dense_strides(const std::vector<int64_t>& shape) {
+    std::vector<int64_t> r(shape.size());
+    int64_t st = 1;
+    for (int i = (int)shape.size() - 1; i >= 0; --i) {
+      r[i] = st;
+      st *= shape[i];
+    }
+    return r;
+  }
+  bool is_contiguous() const {
+    int64_t exp = 1;
+    for (int i = (int)shape.size() - 1; i >= 0; --i) {
+      if (shape[i] != 1 && strides[i] != exp) return false;
+      exp *= shape[i];
+    }
+    return true;
+  }
+  bool is_channels_last() const {  // 4-D NCHW logical shape over dense NHWC memory
+    if (shape.size() != 4) return false;
+    const int64_t C = shape[1], H = shape[2], W = shape[3];
+    return (C == 1 || strides[1] == 1) && (W == 1 || strides[3] == C) && (H == 1 || strides[2] == W * C) &&
+           (shape[0] == 1 || strides[0] == H * W * C);
+  }
+  int norm_dim(int d, int rank) const {
+    if (d < 0) d += rank;
+    if (d < 0 || d >= rank) throw std::out_of_range("dimension out of range");
+    return d;
+  }
+  NTensor view_of(std::vector<int64_t> shp, std::vector<int64_t> str, int64_t off) const {
+    NTensor t = *this;
+    t.shape = std::move(shp);
+    t.strides = std::move(str);
+    t.offset = off;
+    return t;
+  }
+  // reshape: a view when the strides allow it (dense row-major layout), else an error
+  NTensor reshape(std::vector<int64_t> shp) const {
+    int64_t known = 1, infer = -1;
+    for (size_t i = 0; i < shp.size(); ++i) {
+      if (shp[i] == -1) {
+        if (infer >= 0) throw std::invalid_argument("reshape: more than one -1");
+        infer = (int64_t)i;
+      } else {
+        if (shp[i] < 0) throw std::invalid_argument("reshape: negative dimension");
+        known *= shp[i];
+      }
+    }
+    const int64_t n = numel();
+    if (infer >= 0) {
+      if (known == 0 || n % known) throw std::invalid_argument("reshape: cannot infer the -1 dimension");
+      shp[infer] = n / known;
+    } else if (known != n) {
+      throw std::invalid_argument("reshape: element count changes");
+    }
+    if (!is_contiguous()) throw std::invalid_argument("reshape of a non-contiguous tensor: copy it first");
+    return view_of(shp, dense_strides(shp), offset);
+  }
+  NTensor permute(std::vector<int> dims) const {
+    const int r = (int)shape.size();
+    if ((int)dims.size() != r) throw std::invalid_argument("permute: rank mismatch");
+    std::vector<int64_t> shp(r), str(r);
+    std::vector<bool> seen(r, false);
+    for (int i = 0; i < r; ++i) {
+      const int d = norm_dim(dims[i], r);
+      if (seen[d]) throw std::invalid_argument("permute: repeated dimension");
+      seen[d] = true;
+      shp[i] = shape[d];
+      str[i] = strides[d];
+    }
+    return view_of(shp, str, offset);
+  }
+  NTensor transpose(int a, int b) const {
+    std::vector<int> dims(shape.size());
+    for (size_t i = 0; i < dims.size(); ++i) dims[i] = (int)i;
+    std::swap(dims[norm_dim(a, (int)shape.size())], dims[norm_dim(b, (int)shape.size())]);
+    return permute(dims);
+  }
+  NTensor slice(int d, int64_t start, int64_t stop, int64_t step) const {
+    d = norm_dim(d, (int)shape.size());
+    if (step <= 0) throw std::invalid_argument("slice: step must be positive");
+    const int64_t n = shape[d];
+    if (start < 0) start += n;
+    if (stop < 0) stop += n;
+    start = std::min(std::max<int64_t>(start, 0), n);
+    stop = std::min(std::max<int64_t>(stop, start), n);
+    std::vector<int64_t> shp = shape, str = strides;
+    shp[d] = (stop - start + step - 1) / step;
+    str[d] = strides[d] * step;
+    return view_of(shp, str, offset + start * strides[d] * itemsize());
+  }
+  NTensor select(int d, int64_t i) const {
+    d = norm_dim(d, (int)shape.size());
+    if (i < 0) i += shape[d];
+    if (i < 0 || i >= shape[d]) throw std::out_of_range("select: index out of range");
+    std::vector<int64_t> shp = shape, str = strides;
+    shp.erase(shp.begin() + d);
+    str.erase(str.begin() + d);
+    return view_of(shp, str, offset + i * strides[d] * itemsize());
+  }
+  NTensor unsqueeze(int d) const {
+    const int r = (int)shape.size() + 1;
+    if (d < 0) d += r;
+    if (d < 0 || d >= r) throw std::out_of_range("unsqueeze: dimension out of range");
+    std::vector<int64_t> shp = shape, str = strides;
+    const int64_t s = d < (int)shape.size() ? strides[d] * shape[d] : 1;
+    shp.insert(shp.begin() + d, 1);
+    str.insert(str.begin() + d, s);
+    return view_of(shp, str, offset);
+  }
+  NTensor squeeze(int d) const {
+    d = norm_dim(d, (int)shape.size());
+    if (shape[d] != 1) return *this;
+    std::vector<int64_t> shp = shape, str = strides;
+    shp.erase(shp.begin() + d);
+    str.erase(str.begin() + d);
+    return view_of(shp, str, offset);
+  }
+  NTensor expand(std::vector<int64_t> shp) const {  // broadcast size-1 (or new leading) dims with stride 0
+    if (shp.size() < shape.size()) throw std::invalid_argument("expand: fewer dimensions");
+    const size_t lead = shp.size() - shape.size();
+    std::vector<int64_t> str(shp.size(), 0);
+    for (size_t i = 0; i < shp.size(); ++i) {
+      if (i < lead) {
+        if (shp[i] < 0) throw std::invalid_argument("expand: -1 for a new dimension");
+        continue;
+      }
+      const int64_t cur = shape[i - lead];
+      if (shp[i] == -1) shp[i] = cur;
+      if (cur == shp[i]) str[i] = strides[i - lead];
+      else if (cur != 1) throw std::invalid_argument("expand: only size-1 dimensions broadcast");
+    }
+    return view_of(shp, str, offset);
+  }
+  NTensor as_strided(std::vector<int64_t> shp, std::vector<int64_t> str, int64_t elem_offset) const {
+    if (shp.size() != str.size()) throw std::invalid_argument("as_strided: rank mismatch");
+    int64_t hi = elem_offset;  // the largest element reached must lie inside the storage
+    for (size_t i = 0; i < shp.size(); ++i) {
+      if (shp[i] < 0 || str[i] < 0) throw std::invalid_argument("as_strided: negative size / stride");
+      if (shp[i] > 0) hi += (shp[i] - 1) * str[i];
+    }
+    if (elem_offset < 0 || (size_t)(hi + 1) * itemsize() > st->bytes)
+      throw std::out_of_range("as_strided: view outside the storage");
+    return view_of(shp, str, elem_offset * itemsize());
+  }
+  py::object to_dlpack() const {
+    auto* c = new Ctx{shape, strides, (void*)data_ptr(), 3, dev, 0, st};
+    auto* m = new DLManagedTensor{};
+    m->dl_tensor.data = (void*)data_ptr();
+    m->dl_tensor.device = DLDevice{dl_type, dl_type == kDLCPU ? 0 : dev};
+    m->dl_tensor.ndim = (int32_t)shape.size();
+    m->dl_tensor.dtype = DLDataType{(uint8_t)code, (uint8_t)bits, 1};
+    m->dl_tensor.shape = c->shape.data();
+    m->dl_tensor.strides = c->strides.data();
+    m->dl_tensor.byte_offset = 0;
+    m->manager_ctx = c;
+    m->deleter = dl_deleter;
+    return py::reinterpret_steal<py::object>(PyCapsule_New(m, "dltensor", capsule_dtor));
+  }
+};
+
+NTensor ntensor_empty(std::vector<int64_t> shape, int code, int bits, int kind, int dev, int32_t dl_device_type,
+                      uintptr_t stream, bool channels_last) {
+  if (bits % 8 || bits <= 0) throw std::invalid_argument("dtype bits must be a positive multiple of 8");
+  NTensor t;
+  t.shape = shape;
+  for (int64_t v : shape)
+    if (v < 0) throw std::invalid_argument("negative dimension");
+  const size_t bytes = (size_t)t.numel() * (bits / 8);
+  auto st = std::make_shared<Storage>();
+  st->kind = kind;
+  st->dev = dev;
+  st->bytes = bytes;
+  st->ptr = kind == 0 ? dev_pool(dev).alloc(bytes, stream) : host_pool(kind == 2).alloc(bytes);
+  t.st = st;
+  t.code = code;
+  t.bits = bits;
+  t.dev = kind == 0 ? dev : 0;
+  t.dl_type = kind == 0 ? dl_device_type : kDLCPU;
+  if (channels_last && shape.size() == 4) {
+    const int64_t C = shape[1], H = shape[2], W = shape[3];
+    t.strides = {H * W * C, 1, W * C, C};
+  } else {
+    t.strides = NTensor::dense_strides(shape);
+  }
+  return t;
+}
+
+// import a DLPack capsule (any producer): the handle owns the managed tensor
+// and calls its deleter when the last view of the storage dies
+NTensor ntensor_from_dlpack(py::capsule cap) {
+  PyObject* o = cap.ptr();
+  if (!PyCapsule_IsValid(o, "dltensor")) throw std::invalid_argument("not an unconsumed DLPack capsule");
+  auto* m = (DLManagedTensor*)PyCapsule_GetPointer(o, "dltensor");
+  PyCapsule_SetName(o, "used_dltensor");  // consumed: the capsule destructor no longer frees it
+  const DLTensor& d = m->dl_tensor;
+  NTensor t;
+  t.shape.assign(d.shape, d.shape + d.ndim);
+  t.strides = d.strides ? std::vector<int64_t>(d.strides, d.strides + d.ndim) : NTensor::dense_strides(t.shape);
+  t.code = d.dtype.code;
+  t.bits = d.dtype.bits * (d.dtype.lanes ? d.dtype.lanes : 1);
+  t.dl_type = d.device.device_type;
+  t.dev = d.device.device_id;
+  auto st = std::make_shared<Storage>();
+  st->kind = 3;
+  st->foreign = m;
+  st->ptr = (char*)d.data + d.byte_offset;
+  int64_t hi = 0;
+  for (int i = 0; i < d.ndim; ++i)
+    if (t.shape[i] > 0) hi += (t.shape[i] - 1) * t.strides[i];
+  st->bytes = t.numel() ? (size_t)(hi + 1) * t.itemsize() : 0;
+  st->dev = t.dev;
+  t.st = st;
+  return t;
+}
+
 }  // namespace
 
 void register_mem(py::module& m) {
@@ -614,6 +871,39 @@ void register_mem(py::module& m) {
       .def_property_readonly("bytes", &SyncedBlob::bytes);
   mm.def("blob_view", &blob_view, py::arg("blob"), py::arg("ptr"), py::arg("on_device"), py::arg("device"),
          py::arg("dl_device_type"), py::arg("shape"), py::arg("code"), py::arg("bits"));
+  py::class_<NTensor>(mm, "Tensor", "framework-owned tensor handle: pool storage + offset, shape, strides, dtype, device")
+      .def_static("empty", &ntensor_empty, py::arg("shape"), py::arg("code"), py::arg("bits"), py::arg("kind"),
+                  py::arg("device") = 0, py::arg("dl_device_type") = 10, py::arg("stream") = 0,
+                  py::arg("channels_last") = false)
+      .def_static("from_dlpack", &ntensor_from_dlpack, py::arg("capsule"))
+      .def_property_readonly("shape", [](const NTensor& t) { return py::tuple(py::cast(t.shape)); })
+      .def_property_readonly("strides", [](const NTensor& t) { return py::tuple(py::cast(t.strides)); })
+      .def_property_readonly("ndim", [](const NTensor& t) { return (int)t.shape.size(); })
+      .def_property_readonly("dtype", [](const NTensor& t) { return py::make_tuple(t.code, t.bits); })
+      .def_property_readonly("device", [](const NTensor& t) { return py::make_tuple(t.dl_type, t.dev); })
+      .def_property_readonly("offset", [](const NTensor& t) { return t.offset; })
+      .def_property_readonly("itemsize", &NTensor::itemsize)
+      .def_property_readonly("storage_bytes", [](const NTensor& t) { return t.st->bytes; })
+      .def_property_readonly("storage_kind", [](const NTensor& t) { return t.st->kind; })
+      .def_property_readonly("storage_refs", [](const NTensor& t) { return (long)t.st.use_count(); })
+      .def("numel", &NTensor::numel)
+      .def("nbytes", [](const NTensor& t) { return t.numel() * t.itemsize(); })
+      .def("data_ptr", &NTensor::data_ptr)
+      .def("is_contiguous", &NTensor::is_contiguous)
+      .def("is_channels_last", &NTensor::is_channels_last)
+      .def("same_storage", [](const NTensor& a, const NTensor& b) { return a.st == b.st; })
+      .def("reshape", &NTensor::reshape)
+      .def("permute", &NTensor::permute)
+      .def("transpose", &NTensor::transpose)
+      .def("slice", &NTensor::slice, py::arg("dim"), py::arg("start"), py::arg("stop"), py::arg("step") = 1)
+      .def("select", &NTensor::select)
+      .def("unsqueeze", &NTensor::unsqueeze)
+      .def("squeeze", &NTensor::squeeze)
+      .def("expand", &NTensor::expand)
+      .def("as_strided", &NTensor::as_strided, py::arg("shape"), py::arg("strides"), py::arg("offset") = 0)
+      .def("to_dlpack", &NTensor::to_dlpack)
+      .def("__dlpack__", [](const NTensor& t, py::object) { return t.to_dlpack(); }, py::arg("stream") = py::none())
+      .def("__dlpack_device__", [](const NTensor& t) { return py::make_tuple(t.dl_type, t.dl_type == kDLCPU ? 0 : t.dev); });
   mm.def("dl_device_type", [](py::capsule cap) {
     auto* t = (DLManagedTensor*)PyCapsule_GetPointer(cap.ptr(), PyCapsule_GetName(cap.ptr()));
     if (!t) throw std::runtime_error("not a DLPack capsule");

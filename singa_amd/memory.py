@@ -117,6 +117,40 @@ def empty(*size, dtype=None, device=None, memory_format=None, pinned: bool = Fal
     return t.view(torch.bool) if dtype == torch.bool and t.dtype != torch.bool else t
 
 
+def empty_native(shape: Sequence[int], dtype=torch.float32, device=None, channels_last: bool = False,
+                 pinned: bool = False):
+    """A framework-owned tensor handle (``_C.mem.Tensor``: pool storage, byte
+    offset, shape, strides, dtype, device -- csrc/mem/pool.cpp) over a new
+    block of the device's HBM pool (stream-ordered on the current stream) or
+    the host pool.  ``to_torch(h)`` / ``numpy.from_dlpack(h)`` view its bytes."""
+    M = _mod()
+    if M is None or not hasattr(M, "Tensor"):
+        raise RuntimeError("the native tensor handle needs the _C extension")
+    dev = device if isinstance(device, torch.device) else torch.device(device if device is not None else "cpu")
+    code, bits = _CODES[dtype]
+    shape = [int(v) for v in shape]
+    if dev.type == "cuda":
+        idx = dev.index if dev.index is not None else _getdev()
+        return M.Tensor.empty(shape, code, bits, 0, idx, _DL_DEV or _dl_device_type(), _raw_stream(idx),
+                              channels_last)
+    return M.Tensor.empty(shape, code, bits, 2 if pinned else 1, 0, 1, 0, channels_last)
+
+
+def native(t: torch.Tensor):
+    """The native handle of any tensor's bytes (zero copy, DLPack: the handle
+    keeps ``t``'s storage alive); views taken on it are native metadata."""
+    M = _mod()
+    if M is None or not hasattr(M, "Tensor"):
+        raise RuntimeError("the native tensor handle needs the _C extension")
+    return M.Tensor.from_dlpack(torch.utils.dlpack.to_dlpack(t))
+
+
+def to_torch(h) -> torch.Tensor:
+    """A torch view of a native handle's bytes (the view keeps the storage alive)."""
+    t = torch.utils.dlpack.from_dlpack(h.to_dlpack())
+    return t.view(torch.bool) if h.dtype == (6, 8) and t.dtype != torch.bool else t
+
+
 def empty_like(t: torch.Tensor, dtype=None, memory_format=None) -> torch.Tensor:
     """Same shape (and, by default, the same dense layout: contiguous or
     channels_last) as ``t``."""

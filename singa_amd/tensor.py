@@ -119,6 +119,18 @@ class Tensor:
         return Tensor(device=self.device, data=d, requires_grad=kw.get("requires_grad", self.requires_grad),
                       stores_grad=False)
 
+    @property
+    def native(self):
+        """The framework-owned handle of this tensor's bytes (``_C.mem.Tensor``:
+        storage, offset, shape, strides, dtype, device; native views and
+        DLPack export -- see :func:`singa_amd.memory.native`)."""
+        return _mem.native(self.data)
+
+    @classmethod
+    def from_native(cls, h, device: Optional[_dev.Device] = None, requires_grad: bool = True) -> "Tensor":
+        """Wrap a native handle (no copy)."""
+        return cls(device=device, data=_mem.to_torch(h), requires_grad=requires_grad)
+
     def reshape(self, shape: Sequence[int]) -> "Tensor":
         return self._wrap(_G.reshape(self.data, tuple(shape)))
 
