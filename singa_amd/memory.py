@@ -145,6 +145,20 @@ def native(t: torch.Tensor):
     return M.Tensor.from_dlpack(torch.utils.dlpack.to_dlpack(t))
 
 
+def native_views() -> bool:
+    """Tensor.reshape / transpose build their views on the native handle
+    (``SINGA_AMD_NATIVE_VIEWS=0``: PyTorch's view machinery)."""
+    v = _NV[0]
+    if v is None:
+        M = _mod()
+        v = _NV[0] = (os.environ.get("SINGA_AMD_NATIVE_VIEWS", "1") != "0" and M is not None
+                      and hasattr(M, "Tensor"))
+    return v
+
+
+_NV = [None]
+
+
 def to_torch(h) -> torch.Tensor:
     """A torch view of a native handle's bytes (the view keeps the storage alive)."""
     t = torch.utils.dlpack.from_dlpack(h.to_dlpack())

@@ -131,12 +131,20 @@ class Tensor:
         """Wrap a native handle (no copy)."""
         return cls(device=device, data=_mem.to_torch(h), requires_grad=requires_grad)
 
+    def _native_ok(self) -> bool:
+        return _mem.native_views() and self.data.dtype in _mem._CODES and self.data.numel() > 0
+
     def reshape(self, shape: Sequence[int]) -> "Tensor":
+        # a native view over the same storage when the layout allows, else a copy
+        if self._native_ok() and self.data.is_contiguous():
+            return self._wrap(_mem.to_torch(_mem.native(self.data).reshape([int(v) for v in shape])))
         return self._wrap(_G.reshape(self.data, tuple(shape)))
 
     def transpose(self, axes: Optional[Sequence[int]] = None) -> "Tensor":
         if axes is None:
             axes = tuple(reversed(range(self.data.dim())))
+        if self._native_ok():
+            return self._wrap(_mem.to_torch(_mem.native(self.data).permute([int(a) for a in axes])))
         return self._wrap(self.data.permute(*axes))
 
     def T(self) -> "Tensor":
