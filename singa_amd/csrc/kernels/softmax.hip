@@ -726,27 +726,57 @@ void sg_layernorm_fwd(const void* x, const void* g, const void* b, void* y, void
   DISPATCH_FT(dtype, hipLaunchKernelGGL(layernorm_fwd_k<T>, dim3(R), dim3(256), 0, s, (const T*)x,
                                         (const float*)g, (const float*)b, (T*)y, (float*)mean, (float*)rstd, D, eps));
 }
-// rows per wave of the v2 backward and its workspace (floats) for R x D
-static constexpr int kLnbRpw = 4;
+// rows per wave of the v2 backward (SG_LNB_RPW: 1, 2, 4 or 8; read once) and
+// its workspace (floats) for R x D.  BERT-base (4096 x 768 rows, one box,
+// alternating: profiles/r6/ab_lnb_rows_per_wave.txt): 2 rows 4 477-4 484 seq/s,
+// 1 row 4 461-4 466, 4 rows 4 442-4 448, 8 rows 4 333 -- two rows per wave
+// (512 workgroups) keep more rows in flight per CU than four (256)
+static int lnb_rpw() {
+  static const int v = [] {
+    const char* e = getenv("SG_LNB_RPW");
+    const int r = e ? atoi(e) : 2;
+    return (r == 1 || r == 2 || r == 4 || r == 8) ? r : 2;
+  }();
+  return v;
+}
 int64_t sg_layernorm_bwd_ws(int64_t R, int D) {
-  const int64_t nb = (R + 4 * kLnbRpw - 1) / (4 * kLnbRpw);
+  const int rpw = lnb_rpw();
+  const int64_t nb = (R + 4 * rpw - 1) / (4 * rpw);
   return (D % 4 == 0 && D <= 2048) ? nb * 2 * D : 0;
 }
+#define LNB_RPW_DISPATCH(X)          \
+  switch (lnb_rpw()) {               \
+    case 1: { X(1); break; }         \
+    case 8: { X(8); break; }         \
+    case 4: { X(4); break; }         \
+    default: { X(2); break; }        \
+  }
 
 // ws (sg_layernorm_bwd_ws floats, any contents) selects the v2 kernel
 void sg_layernorm_bwd_v2(const void* x, const void* dy, const void* g, const void* mean, const void* rstd, void* dx,
                          void* dg, void* db, void* ws, int64_t R, int D, int dtype, hipStream_t s) {
-  const int64_t nb = (R + 4 * kLnbRpw - 1) / (4 * kLnbRpw);
+  const int64_t nb = (R + 4 * lnb_rpw() - 1) / (4 * lnb_rpw());
   const size_t lds = (size_t)8 * D * sizeof(float);
   const int nj = (D + 255) / 256;
   float* w = (dg || db) ? (float*)ws : nullptr;
-#define LNB2(NJ)                                                                                                   \
-  DISPATCH_FT(dtype, hipLaunchKernelGGL((layernorm_bwd2_k<T, NJ, kLnbRpw>), dim3((unsigned)nb), dim3(256), lds, s, \
-                                        (const T*)x, (const T*)dy, (const float*)g, (const float*)mean,             \
+#define LNB2R(NJ, RPW)                                                                                          \
+  DISPATCH_FT(dtype, hipLaunchKernelGGL((layernorm_bwd2_k<T, NJ, RPW>), dim3((unsigned)nb), dim3(256), lds, s, \
+                                        (const T*)x, (const T*)dy, (const float*)g, (const float*)mean,         \
                                         (const float*)rstd, (T*)dx, w, R, D, nullptr, 1.f, nullptr))
-  if (nj <= 1) { LNB2(1); } else if (nj <= 2) { LNB2(2); } else if (nj <= 3) { LNB2(3); } else if (nj <= 4) { LNB2(4); }
-  else { LNB2(8); }
-#undef LNB2
+#define LNB2_1(RPW) LNB2R(1, RPW)
+#define LNB2_2(RPW) LNB2R(2, RPW)
+#define LNB2_3(RPW) LNB2R(3, RPW)
+#define LNB2_4(RPW) LNB2R(4, RPW)
+#define LNB2_8(RPW) LNB2R(8, RPW)
+  if (nj <= 1) { LNB_RPW_DISPATCH(LNB2_1) } else if (nj <= 2) { LNB_RPW_DISPATCH(LNB2_2) }
+  else if (nj <= 3) { LNB_RPW_DISPATCH(LNB2_3) } else if (nj <= 4) { LNB_RPW_DISPATCH(LNB2_4) }
+  else { LNB_RPW_DISPATCH(LNB2_8) }
+#undef LNB2_1
+#undef LNB2_2
+#undef LNB2_3
+#undef LNB2_4
+#undef LNB2_8
+#undef LNB2R
   if (w)
     hipLaunchKernelGGL(ln_fold_k, dim3((unsigned)((2 * D + 255) / 256), (unsigned)((nb + 7) / 8)), dim3(256), 0, s,
                        (const float*)w, (int)nb, D, 2, (float*)dg, (float*)db, (float*)nullptr);
@@ -773,17 +803,28 @@ void sg_drop_add_ln_fwd(const void* x, const void* a, const void* g, const void*
 void sg_drop_add_ln_bwd(const void* x, const void* dy, const void* g, const void* mean, const void* rstd,
                         const void* mask, float pkeep, void* dx, void* da, void* dg, void* db, void* cs, void* ws,
                         int64_t R, int D, int dtype, hipStream_t s) {
-  const int64_t nb = (R + 4 * kLnbRpw - 1) / (4 * kLnbRpw);
+  const int64_t nb = (R + 4 * lnb_rpw() - 1) / (4 * lnb_rpw());
   const size_t lds = (size_t)12 * D * sizeof(float);
   const int nj = (D + 255) / 256;
-#define LNBD(NJ)                                                                                                    \
-  DISPATCH_FT(dtype, hipLaunchKernelGGL((layernorm_bwd2_k<T, NJ, kLnbRpw, true>), dim3((unsigned)nb), dim3(256), lds, \
-                                        s, (const T*)x, (const T*)dy, (const float*)g, (const float*)mean,           \
-                                        (const float*)rstd, (T*)dx, (float*)ws, R, D, (const uint8_t*)mask, pkeep,   \
+#define LNBDR(NJ, RPW)                                                                                          \
+  DISPATCH_FT(dtype, hipLaunchKernelGGL((layernorm_bwd2_k<T, NJ, RPW, true>), dim3((unsigned)nb), dim3(256), lds, \
+                                        s, (const T*)x, (const T*)dy, (const float*)g, (const float*)mean,       \
+                                        (const float*)rstd, (T*)dx, (float*)ws, R, D, (const uint8_t*)mask, pkeep, \
                                         (T*)da))
-  if (nj <= 1) { LNBD(1); } else if (nj <= 2) { LNBD(2); } else if (nj <= 3) { LNBD(3); } else if (nj <= 4) { LNBD(4); }
-  else { LNBD(8); }
-#undef LNBD
+#define LNBD_1(RPW) LNBDR(1, RPW)
+#define LNBD_2(RPW) LNBDR(2, RPW)
+#define LNBD_3(RPW) LNBDR(3, RPW)
+#define LNBD_4(RPW) LNBDR(4, RPW)
+#define LNBD_8(RPW) LNBDR(8, RPW)
+  if (nj <= 1) { LNB_RPW_DISPATCH(LNBD_1) } else if (nj <= 2) { LNB_RPW_DISPATCH(LNBD_2) }
+  else if (nj <= 3) { LNB_RPW_DISPATCH(LNBD_3) } else if (nj <= 4) { LNB_RPW_DISPATCH(LNBD_4) }
+  else { LNB_RPW_DISPATCH(LNBD_8) }
+#undef LNBD_1
+#undef LNBD_2
+#undef LNBD_3
+#undef LNBD_4
+#undef LNBD_8
+#undef LNBDR
   hipLaunchKernelGGL(ln_fold_k, dim3((unsigned)((3 * D + 255) / 256), (unsigned)((nb + 7) / 8)), dim3(256), 0, s,
                      (const float*)ws, (int)nb, D, 3, (float*)dg, (float*)db, (float*)cs);
 }
