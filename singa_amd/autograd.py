@@ -277,6 +277,8 @@ def backward(y, dy=None) -> Iterator[Tuple[Tensor, Tensor]]:
             if src_op not in seen:
                 seen.add(src_op)
                 q.append(src_op)
+    for op_ in seen:  # consumers of each op's output in this backward (fusion decisions look ahead with it)
+        op_._consumers = deps[op_]
     PARAM_USES.clear()
     PARAM_USES.update(puses)
     if OVERWRITE_FIRST:
@@ -416,6 +418,12 @@ class _Unary(Operator):
         return y
 
     def backward(self, dy):
+        if getattr(self, "bwd_done", False):
+            # the consuming Linear's data-gradient GEMM applied this
+            # activation's derivative in its epilogue: dy is already dx
+            self.bwd_done = False
+            self.x = self.y = None
+            return dy
         dx = F.unary_bwd(self.kind, self.x, self.y, dy, self.alpha)
         self.x = self.y = None
         return dx
@@ -426,6 +434,10 @@ class ReLU(_Unary):
     needs = "y"
 
     def backward(self, dy):
+        if getattr(self, "bwd_done", False):  # (applied by the consuming Linear's dgrad epilogue)
+            self.bwd_done = False
+            self.y = None
+            return dy
         dx = F.relu_bwd_from_y(self.y, dy)
         self.y = None
         return dx
@@ -713,6 +725,17 @@ class Linear(Operator):
             return None
         return src
 
+    def _producer_unary(self):
+        """The standalone activation op (GELU, tanh, ...) whose output is this
+        op's input and whose gradient comes from this op alone: the data
+        gradient GEMM can apply its derivative in the epilogue."""
+        src = self.src[0][0] if self.src else None
+        if not (ACT_GRAD_FUSE and isinstance(src, _Unary) and src.kind in F.GEMM_ACT and src.alpha == 0.0
+                and (getattr(self, "sole", None) or {}).get(0, False)):
+            return None
+        t = src.x if src.kind in F.ACT_XFORM else src.y
+        return src if t is not None else None
+
     def _w_compute(self, x, W):
         if x.dtype == W.dtype:
             return W
@@ -752,6 +775,24 @@ class Linear(Operator):
                 prod.preact_done = True
                 if pb is not None:
                     prod.db_done = True
+            elif self._producer_unary() is not None and x2.is_cuda:
+                un = self._producer_unary()
+                t = un.x if un.kind in F.ACT_XFORM else un.y
+                # the activation's producer: its bias gradient is the column
+                # sum of this GEMM's output when the activation is its only consumer
+                lin = un.src[0][0] if un.src else None
+                pb = None
+                if (isinstance(lin, Linear) and lin.has_bias and lin.act is None and BIAS_INPLACE
+                        and getattr(lin, "_consumers", 0) == 1 and x2.dtype == torch.bfloat16):
+                    pb = lin.grad_target(2)
+                    if not (pb is not None and pb.is_cuda and pb.dtype == torch.float32 and pb.is_contiguous()
+                            and pb.numel() == x2.shape[-1]):
+                        pb = None
+                dx = F.gemm_nt(dy2, w, out_dtype=x2.dtype, act_grad=(un.kind, G.reshape(t, tuple(x2.shape))),
+                               colsum_c=pb)
+                un.bwd_done = True
+                if pb is not None:
+                    lin.db_done = True
             else:
                 # another consumer's gradient of x already pending (a residual
                 # stream: the tail's ds): this data gradient adds into it in
@@ -1520,6 +1561,9 @@ class Attention(Operator):
 
 
 BIAS_INPLACE = os.environ.get("SINGA_AMD_BIAS_INPLACE", "1") != "0"  # (A/B switch)
+# a Linear's data-gradient GEMM applies the derivative of a standalone
+# activation op that feeds it (GELU between BERT's fc1 and fc2)
+ACT_GRAD_FUSE = os.environ.get("SINGA_AMD_ACT_GRAD_FUSE", "1") != "0"  # (A/B switch)
 
 
 def producer_bias(op: Operator, i: int):

@@ -231,3 +231,50 @@ def test_linear_dgrad_accumulates_into_residual_gradient(gpu, monkeypatch):
         res[on] = {k: init[k] - v.data.float() for k, v in m.get_params().items()}
     worst = max(rel_err(res[True][k], res[False][k]) for k in res[False] if float(res[False][k].norm()) > 0)
     assert worst < 2e-2, worst
+
+
+def test_gelu_backward_in_fc2_dgrad_epilogue(gpu, monkeypatch):
+    """fc2's data-gradient GEMM applies the standalone GELU's derivative in its
+    epilogue (and sums fc1's bias gradient there): one SGD step equals the
+    separate GELU-backward / column-sum passes, and the fused route ran."""
+    import numpy as np
+
+    from singa_amd import autograd, device, opt, tensor
+    from singa_amd.models import bert
+    from singa_amd.ops import functional as F
+
+    cfg = dict(vocab=1000, hidden=128, layers=2, heads=2, ffn=512, max_pos=128)
+    rng = np.random.RandomState(6)
+    ids_np = rng.randint(0, cfg["vocab"], (8, 64)).astype(np.int64)
+    y_np = rng.randint(0, 2, 8).astype(np.int32)
+    orig = F.unary_bwd
+    n_gelu_bwd = [0]
+
+    def spy(kind, *a, **kw):
+        n_gelu_bwd[0] += kind == "gelu"
+        return orig(kind, *a, **kw)
+
+    monkeypatch.setattr(F, "unary_bwd", spy)
+    monkeypatch.setenv("SINGA_AMD_FUSE_GELU", "0")
+    res, init, counts = {}, None, {}
+    for on in (True, False):
+        monkeypatch.setattr(autograd, "ACT_GRAD_FUSE", on)
+        dev = device.create_rocm_gpu()
+        dev.SetRandSeed(0)
+        m = bert.Bert(dropout=0.0, compute_dtype=torch.bfloat16, **cfg)
+        ids = tensor.from_numpy(ids_np, dev)
+        y = tensor.from_numpy(y_np, dev)
+        m.set_optimizer(opt.SGD(lr=1.0))
+        m.compile([ids], is_train=True, use_graph=False)
+        if init is None:
+            init = {k: v.data.float().clone() for k, v in m.get_states().items()}
+        else:
+            m.set_states({k: v.to(m.get_states()[k].data.dtype) for k, v in init.items()})
+        m.train()
+        n0 = n_gelu_bwd[0]
+        m(ids, y)
+        counts[on] = n_gelu_bwd[0] - n0
+        res[on] = {k: init[k] - v.data.float() for k, v in m.get_params().items()}
+    assert counts[True] == 0 and counts[False] >= cfg["layers"], counts
+    worst = max(rel_err(res[True][k], res[False][k]) for k in res[False] if float(res[False][k].norm()) > 0)
+    assert worst < 2e-2, worst
