@@ -23,7 +23,9 @@ def main():
     cs = torch.zeros(3072, device="cuda")
     for name, fn in [("plain", lambda: F.gemm_nt(dy, w, out_dtype=torch.bfloat16)),
                      ("act", lambda: F.gemm_nt(dy, w, out_dtype=torch.bfloat16, act_grad=("gelu", z))),
-                     ("act_cs", lambda: F.gemm_nt(dy, w, out_dtype=torch.bfloat16, act_grad=("gelu", z), colsum_c=cs))]:
+                     ("act_cs", lambda: F.gemm_nt(dy, w, out_dtype=torch.bfloat16, act_grad=("gelu", z), colsum_c=cs)),
+                     ("act_relu", lambda: F.gemm_nt(dy, w, out_dtype=torch.bfloat16, act_grad=("relu", z))),
+                     ("act_tanh", lambda: F.gemm_nt(dy, w, out_dtype=torch.bfloat16, act_grad=("tanh", z)))]:
         for _ in range(a.iters):
             fn()
         torch.cuda.synchronize()
