@@ -154,6 +154,26 @@ __device__ __forceinline__ float ep_dact(int a, float t) {
   }
 }
 
+// 8-wide forms of the fused activations, NOT inlined: the staged epilogue's
+// unrolled passes would otherwise carry 32 inlined copies of every
+// activation's math (erf, exp, tanh), and that code growth made the fused
+// kernels slow whatever the activation (tools/bench_actgrad.py: relu ~ gelu)
+struct F8 {
+  float x[8];
+};
+__device__ __attribute__((noinline)) bf16x8 ep_act8(int a, bf16x8 z) {
+  bf16x8 o;
+#pragma unroll
+  for (int r = 0; r < 8; ++r) o[r] = (bf16)ep_act(a, (float)z[r]);
+  return o;
+}
+__device__ __attribute__((noinline)) bf16x8 ep_dact8(int a, F8 v, bf16x8 t) {
+  bf16x8 o;
+#pragma unroll
+  for (int r = 0; r < 8; ++r) o[r] = (bf16)((float)(bf16)v.x[r] * ep_dact(a, (float)t[r]));
+  return o;
+}
+
 __device__ __forceinline__ int kmajor_swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 template <int ROWS>
 __device__ __forceinline__ int kouter_swz(int krow, int chunk) {

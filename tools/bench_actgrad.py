@@ -21,11 +21,13 @@ def main():
     w = (torch.randn(3072, 768, device="cuda", generator=g) * 0.05).bfloat16()
     z = torch.randn(4096, 3072, device="cuda", generator=g).bfloat16()
     cs = torch.zeros(3072, device="cuda")
+    acc = torch.zeros(4096, 3072, device="cuda").bfloat16()
     for name, fn in [("plain", lambda: F.gemm_nt(dy, w, out_dtype=torch.bfloat16)),
                      ("act", lambda: F.gemm_nt(dy, w, out_dtype=torch.bfloat16, act_grad=("gelu", z))),
                      ("act_cs", lambda: F.gemm_nt(dy, w, out_dtype=torch.bfloat16, act_grad=("gelu", z), colsum_c=cs)),
                      ("act_relu", lambda: F.gemm_nt(dy, w, out_dtype=torch.bfloat16, act_grad=("relu", z))),
-                     ("act_tanh", lambda: F.gemm_nt(dy, w, out_dtype=torch.bfloat16, act_grad=("tanh", z)))]:
+                     ("act_tanh", lambda: F.gemm_nt(dy, w, out_dtype=torch.bfloat16, act_grad=("tanh", z))),
+                     ("beta1", lambda: F.gemm(dy, w, tb=True, out=acc, beta=1.0))]:
         for _ in range(a.iters):
             fn()
         torch.cuda.synchronize()
