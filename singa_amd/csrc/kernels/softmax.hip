@@ -452,16 +452,23 @@ __global__ void __launch_bounds__(256) layernorm_bwd2_k(const T* __restrict__ x,
   const float invD = 1.f / D, dscale = 1.f / pkeep;
   float xn[NJ][4], dn[NJ][4];
   uint32_t mn[NJ];
+  // unconditional loads (columns past D re-read column 0, then zeroed): a
+  // load inside the divergent c < D branch gets an s_waitcnt vmcnt(0) at the
+  // branch join, which would also drain the next row's prefetch
+  const uint8_t* mp = dmask ? dmask : (const uint8_t*)x;  // (a valid address when there is no mask)
   auto load = [&](int64_t r) {
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const int c = 4 * (lane + 64 * j);
+      const int cc = c < D ? c : 0;
+      V4<T>::ld(x + r * D + cc, xn[j]);
+      V4<T>::ld(dy + r * D + cc, dn[j]);
       mn[j] = 0x01010101u;
-      if (c < D) {
-        V4<T>::ld(x + r * D + c, xn[j]);
-        V4<T>::ld(dy + r * D + c, dn[j]);
-        if (DROP && dmask) mn[j] = *(const uint32_t*)(dmask + r * D + c);
-      } else {
+      if constexpr (DROP) {
+        const uint32_t mw = *(const uint32_t*)(mp + r * D + cc);
+        mn[j] = dmask ? mw : 0x01010101u;
+      }
+      if (c >= D) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) { xn[j][e] = 0.f; dn[j][e] = 0.f; }
       }
@@ -579,13 +586,15 @@ __global__ void __launch_bounds__(256) drop_add_ln_fwd_k(const T* __restrict__ x
   const bool drop = pkeep < 1.f;
   const float scale = 1.f / pkeep;
   float v[NJ][4], av[NJ][4];
+  // unconditional loads (columns past D re-read column 0, then zeroed): no
+  // vmcnt(0) at a divergent branch join between them
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int c = 4 * (lane + 64 * j);
-    if (c < D) {
-      V4<T>::ld(x + r * D + c, v[j]);
-      V4<T>::ld(a + r * D + c, av[j]);
-    } else {
+    const int cc = c < D ? c : 0;
+    V4<T>::ld(x + r * D + cc, v[j]);
+    V4<T>::ld(a + r * D + cc, av[j]);
+    if (c >= D) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) { v[j][e] = 0.f; av[j][e] = 0.f; }
     }
