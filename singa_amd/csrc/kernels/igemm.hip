@@ -589,6 +589,14 @@ int sg_gemm_act(const void* a, int64_t lda, int a_kouter, const void* b, int64_t
   p.k_per_split = kps(K, 1);
   p.a_bytes = extent_bytes(a_kouter ? (int64_t)(K - 1) * lda + M : (int64_t)(M - 1) * lda + K);
   p.b_bytes = extent_bytes(b_kouter ? (int64_t)(K - 1) * ldb + N : (int64_t)(N - 1) * ldb + K);
+  // the GELU derivative alone (BERT's fc2 data gradient, K-major operands):
+  // its own instantiation with the activation fixed at compile time (FLAGS
+  // bit 1; the runtime dispatch multiplied the epilogue's SALU / VALU work,
+  // profiles/r6/pmc_actgrad_epilogue.txt)
+  if (act == 0 && act_bwd == 5 && !a_kouter && !b_kouter) {
+    launch<LM_KMAJOR, LM_KMAJOR, OUT_BF16, 3>(p, M, 1, s, batch, 0);
+    return 1;
+  }
   if (!a_kouter && !b_kouter) launch<LM_KMAJOR, LM_KMAJOR, OUT_BF16, 1>(p, M, 1, s, batch, 0);
   else if (!a_kouter && b_kouter) launch<LM_KMAJOR, LM_KOUTER, OUT_BF16, 1>(p, M, 1, s, batch, 0);
   else if (a_kouter && !b_kouter) launch<LM_KOUTER, LM_KMAJOR, OUT_BF16, 1>(p, M, 1, s, batch, 0);
