@@ -456,3 +456,46 @@ def test_gsum_dgrad_persistent_matches_fp32(gpu, K, C, H, Nn):
         assert rel_err(dx, ref) < 1e-2, (sk, rel_err(dx, ref))
         assert rel_err(gs, ref.sum((0, 2, 3))) < 1e-2
     assert rel_err(res[1][0], res[0][0]) < 1e-2
+
+
+@pytest.mark.parametrize("shift", [0.0, 4.0])
+def test_tail_gram_statistics_large_mean(gpu, shift):
+    """The residual tail's BN statistics from Gram(y) / colsum(y) (the default,
+    ops/functional.py tail_stats_ws) against the statistics-only GEMM pass and
+    an fp32 reference, for post-ReLU inputs whose channel means dwarf their
+    spread (var = W^T Gram W / P - mean^2 cancels): the variance stays within
+    the statistics pass's own distance from fp32 (plus a small absolute slack)."""
+    from singa_amd.ops import functional as FF
+    from singa_amd.ops import native as N
+
+    C, K4, Nn, H = 64, 256, 42, 56
+    g0 = torch.Generator(device=gpu).manual_seed(11)
+    y = _cl(torch.relu(shift + 0.3 * torch.randn(Nn, C, H, H, device=gpu, generator=g0))).bfloat16()
+    W = _cl((torch.randn(K4, C, 1, 1, device=gpu, generator=g0) * 0.08)).bfloat16()
+    M = Nn * H * H
+    L = N.lib()
+    assert L.sk_tail_ok(M, K4, C)
+    c = y.float().permute(0, 2, 3, 1).reshape(M, C) @ W.float().reshape(K4, C).t()
+    var_ref = c.var(0, unbiased=False)
+    out = {}
+    old = FF.GRAM_STATS
+    try:
+        for gram in (True, False):
+            FF.GRAM_STATS = gram
+            ws, rows = FF.tail_stats_ws(y, W, M, C, K4)
+            gamma, beta = torch.ones(K4, device=gpu), torch.zeros(K4, device=gpu)
+            rm, rv = torch.zeros(K4, device=gpu), torch.ones(K4, device=gpu)
+            p = torch.empty(4 * K4, device=gpu)
+            L.bn_fwd_from_ws(ws.data_ptr(), rows, gamma.data_ptr(), beta.data_ptr(), rm.data_ptr(), rv.data_ptr(),
+                             p[:K4].data_ptr(), p[K4:2 * K4].data_ptr(), p[2 * K4:3 * K4].data_ptr(),
+                             p[3 * K4:].data_ptr(), M, K4, 0.1, 1e-5, N.stream())
+            torch.cuda.synchronize()
+            var = 1.0 / p[K4:2 * K4] ** 2 - 1e-5
+            out[gram] = (p[:K4].clone(), var.clone())
+    finally:
+        FF.GRAM_STATS = old
+    torch.testing.assert_close(out[True][0], c.mean(0), rtol=1e-3, atol=1e-3)
+    e_gram = float(((out[True][1] - var_ref).abs() / var_ref).max())
+    e_pass = float(((out[False][1] - var_ref).abs() / var_ref).max())
+    print({"shift": shift, "gram": e_gram, "stats_pass": e_pass, "mean/std": float((c.mean(0).abs() / var_ref.sqrt()).max())})
+    assert e_gram <= 2 * e_pass + 1e-2, (e_gram, e_pass)
